@@ -1,0 +1,138 @@
+// Marker back-solve and linear predictor (HBM-bound GEMV streams over the locus rows).
+//   B[t, j] = (z_j · a_t) / (q s_j)  — Fit.b_hat (pattern of reference src/linear.jl:218-221)
+//   msum[t] = Σ_j m_j B[t, j]        — b0 = μ̂ − msum makes `predict` exact
+//   out[t, i] = b0_t + Σ_j X[i, j] b_t[j]   — reference src/prediction.jl:228
+#include "gbm_internal.h"
+
+namespace gbm {
+
+// One wave per locus row; each lane reads 16-byte pairs along individuals; up to 4 traits per
+// pass over the row (the row stays in L1/L2 for later passes).
+__global__ void __launch_bounds__(256) marker_effects_kernel(const double* __restrict__ Zt, int64_t ldz, int64_t p,
+                                                             int64_t n, const double* __restrict__ A, int64_t lda,
+                                                             int64_t nrhs, double inv_q,
+                                                             const double* __restrict__ sd,
+                                                             const int32_t* __restrict__ keep,
+                                                             double* __restrict__ B, int64_t ldb) {
+  const int lane = threadIdx.x & 63;
+  const int64_t wave_g = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int64_t nwaves = (int64_t)gridDim.x * 4;
+  const int64_t n2 = (n + 1) & ~(int64_t)1;  // ldz is even and the padding is zero
+  for (int64_t j = wave_g; j < p; j += nwaves) {
+    const double* z = Zt + j * ldz;
+    const bool kp = keep[j] != 0;
+    for (int64_t t0 = 0; t0 < nrhs; t0 += 4) {
+      double acc[4] = {0.0, 0.0, 0.0, 0.0};
+      if (kp) {
+        for (int64_t i = (int64_t)lane * 2; i < n2; i += 128) {
+          const double2 zv = *reinterpret_cast<const double2*>(z + i);
+#pragma unroll
+          for (int u = 0; u < 4; u++)
+            if (t0 + u < nrhs) {
+              const double2 av = *reinterpret_cast<const double2*>(A + (t0 + u) * lda + i);
+              acc[u] += zv.x * av.x + zv.y * av.y;
+            }
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < 4; u++) {
+        double v = acc[u];
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
+        if (lane == 0 && t0 + u < nrhs) B[(t0 + u) * ldb + j] = kp ? v * inv_q / sd[j] : 0.0;
+      }
+    }
+  }
+}
+
+// msum[t] = Σ_j mean_j B[t, j]: one workgroup per trait, fixed reduction order.
+__global__ void __launch_bounds__(1024) weighted_sum_kernel(const double* __restrict__ mean,
+                                                            const double* __restrict__ B, int64_t ldb, int64_t p,
+                                                            double* __restrict__ msum) {
+  __shared__ double red[16];
+  const int64_t t = blockIdx.x;
+  double s = 0.0;
+  for (int64_t j = threadIdx.x; j < p; j += 1024) s += mean[j] * B[t * ldb + j];
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) s += __shfl_xor(s, off, 64);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double tot = 0.0;
+    for (int w = 0; w < 16; w++) tot += red[w];
+    msum[t] = tot;
+  }
+}
+
+// partial[c, t, i] = Σ_{j in chunk c} Xt[j, i] b_t[j]
+__global__ void __launch_bounds__(256) predict_partial_kernel(const double* __restrict__ Xt, int64_t ldx, int64_t p,
+                                                              int64_t n, const double* __restrict__ b,
+                                                              int64_t ldb, int64_t nrhs, int64_t chunk,
+                                                              double* __restrict__ partial) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t c = blockIdx.y;
+  const int64_t j0 = c * chunk;
+  const int64_t j1 = j0 + chunk < p ? j0 + chunk : p;
+  for (int64_t t0 = 0; t0 < nrhs; t0 += 4) {
+    double acc[4] = {0.0, 0.0, 0.0, 0.0};
+    if (i < n) {
+      for (int64_t j = j0; j < j1; j++) {
+        const double x = Xt[j * ldx + i];
+#pragma unroll
+        for (int u = 0; u < 4; u++)
+          if (t0 + u < nrhs) acc[u] += x * b[(t0 + u) * ldb + 1 + j];
+      }
+#pragma unroll
+      for (int u = 0; u < 4; u++)
+        if (t0 + u < nrhs) partial[(c * nrhs + t0 + u) * n + i] = acc[u];
+    }
+  }
+}
+
+__global__ void __launch_bounds__(256) predict_reduce_kernel(const double* __restrict__ partial, int64_t nchunks,
+                                                             int64_t n, const double* __restrict__ b, int64_t ldb,
+                                                             int64_t nrhs, double* __restrict__ out, int64_t ldo) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t t = blockIdx.y;
+  if (i >= n) return;
+  double s = 0.0;
+  for (int64_t c = 0; c < nchunks; c++) s += partial[(c * nrhs + t) * n + i];
+  out[t * ldo + i] = b[t * ldb] + s;
+}
+
+int launch_predict(const double* Xt, int64_t ldx, int64_t p, int64_t n, const double* b, int64_t ldb, int64_t nrhs,
+                   double* partial, int64_t nchunks, double* out, int64_t ldo, hipStream_t s) {
+  const int64_t chunk = (p + nchunks - 1) / nchunks;
+  const unsigned gx = (unsigned)((n + 255) / 256);
+  predict_partial_kernel<<<dim3(gx, (unsigned)nchunks), 256, 0, s>>>(Xt, ldx, p, n, b, ldb, nrhs, chunk, partial);
+  GBM_LAUNCH_CHECK();
+  predict_reduce_kernel<<<dim3(gx, (unsigned)nrhs), 256, 0, s>>>(partial, nchunks, n, b, ldb, nrhs, out, ldo);
+  GBM_LAUNCH_CHECK();
+  return GBM_OK;
+}
+
+int64_t predict_chunks(int64_t n, int64_t p) {
+  const int64_t col_blocks = (n + 255) / 256;
+  int64_t c = (2048 + col_blocks - 1) / col_blocks;
+  if (c > p) c = p;
+  return c < 1 ? 1 : c;
+}
+
+}  // namespace gbm
+
+using namespace gbm;
+
+extern "C" int gbm_dev_marker_effects(const double* Zt, int64_t ldz, int64_t p, int64_t n, const double* A,
+                                      int64_t lda, int64_t nrhs, double inv_q, const double* mean, const double* sd,
+                                      const int32_t* keep, double* B, int64_t ldb, double* msum, void* stream) {
+  if (!Zt || !A || !mean || !sd || !keep || !B || !msum || p < 1 || n < 1 || ldz < n || (ldz & 1) ||
+      lda < ldz || (lda & 1) || nrhs < 1 || ldb < p || !(inv_q > 0.0))
+    return fail(GBM_E_ARG, "gbm_dev_marker_effects: bad arguments (need ldz >= n even, lda >= ldz even, ldb >= p)");
+  hipStream_t s = (hipStream_t)stream;
+  const int64_t blocks = (p + 3) / 4 < 8192 ? (p + 3) / 4 : 8192;
+  marker_effects_kernel<<<(unsigned)blocks, 256, 0, s>>>(Zt, ldz, p, n, A, lda, nrhs, inv_q, sd, keep, B, ldb);
+  GBM_LAUNCH_CHECK();
+  weighted_sum_kernel<<<(unsigned)nrhs, 1024, 0, s>>>(mean, B, ldb, p, msum);
+  GBM_LAUNCH_CHECK();
+  return GBM_OK;
+}

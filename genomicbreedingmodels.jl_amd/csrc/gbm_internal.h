@@ -1,0 +1,42 @@
+// Internal helpers shared by the libgbm translation units (not part of the ABI).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string>
+
+#include "../../include/gbm.h"
+
+namespace gbm {
+
+// Tile geometry (see DESIGN.md "Data layout in HBM").
+constexpr int64_t kNPadTile = 128;  // individuals padded to a multiple of the GRM tile
+constexpr int64_t kRhsRows = 64;    // bordered right-hand-side rows appended to V
+constexpr int kCholNB = 64;         // Cholesky panel width
+
+inline int64_t round_up(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
+inline int64_t npad_of(int64_t n) { return round_up(n < 1 ? 1 : n, kNPadTile); }
+inline int64_t gdim_of(int64_t n) { return npad_of(n) + kRhsRows; }
+
+void set_error(const std::string& msg);
+int fail(int code, const std::string& msg);
+
+#define GBM_HIP_TRY(expr)                                                                      \
+  do {                                                                                         \
+    hipError_t e_ = (expr);                                                                    \
+    if (e_ != hipSuccess)                                                                      \
+      return ::gbm::fail(GBM_E_HIP, std::string("HIP error '") + hipGetErrorString(e_) +       \
+                                        "' at " __FILE__ ":" + std::to_string(__LINE__) + " (" #expr ")"); \
+  } while (0)
+
+#define GBM_LAUNCH_CHECK() GBM_HIP_TRY(hipGetLastError())
+
+// Stage launchers (device pointers, stream-ordered); defined in the .hip files.
+int launch_grm(const double* Zt, int64_t ldz, int64_t p, int64_t n, double* G, int64_t ldg,
+               void* ws, int64_t ws_bytes, hipStream_t s);
+int64_t grm_workspace_bytes(int64_t n, int64_t p);
+int launch_grm_export(const double* G, int64_t ldg, int64_t n, double inv_q, double* out, int64_t ldo, hipStream_t s);
+int launch_predict(const double* Xt, int64_t ldx, int64_t p, int64_t n, const double* b, int64_t ldb, int64_t nrhs,
+                   double* partial, int64_t nchunks, double* out, int64_t ldo, hipStream_t s);
+int64_t predict_chunks(int64_t n, int64_t p);
+
+}  // namespace gbm

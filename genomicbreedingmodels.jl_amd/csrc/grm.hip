@@ -1,0 +1,238 @@
+// GRM build: G = Σ_j z_j z_jᵀ over the standardised locus rows of Zt — an fp64 SYRK on the
+// CDNA4 matrix cores (v_mfma_f64_16x16x4_f64), the dominant cost of the path.
+//
+// Geometry (DESIGN.md "GRM kernel"):
+//   * workgroup tile 128 x 128 of G (lower-triangular tiles only: nt(nt+1)/2 tiles),
+//     256 threads = 4 waves in 2 x 2, each wave a 64 x 64 sub-tile = 4 x 4 MFMA 16x16 tiles
+//     (16 f64x4 accumulators per lane);
+//   * K (= loci) consumed in stages of 16 rows; each stage is 2 x 16 rows x 1 KB of Zt brought
+//     straight into LDS by global_load_lds_dwordx4 (one wave-instruction = one 1-KB locus row
+//     segment), double-buffered; LDS rows padded to 1152 B so the two 16-lane halves of a
+//     ds_read_b64 fragment load land on disjoint bank halves;
+//   * split-K over loci ("slices") when the triangular tile count alone cannot fill the
+//     256 CUs x 2 resident workgroups; slices write private slabs that a second kernel sums in
+//     a fixed order (deterministic, no float atomics).
+#include "gbm_internal.h"
+
+namespace gbm {
+
+typedef double d4 __attribute__((ext_vector_type(4)));
+
+constexpr int BT = 128;            // tile edge
+constexpr int BK = 16;             // loci per stage
+constexpr int LROW = BT + 16;      // LDS row pitch in doubles (1152 B)
+constexpr int STAGE = 2 * BK * LROW;  // doubles per stage (A rows then B rows)
+
+__device__ __forceinline__ void tile_of(int64_t t, int64_t& ti, int64_t& tj) {
+  // t -> (ti, tj), tj <= ti, row-major over the lower triangle
+  int64_t r = (int64_t)((sqrt(8.0 * (double)t + 1.0) - 1.0) * 0.5);
+  while ((r + 1) * (r + 2) / 2 <= t) r++;
+  while (r * (r + 1) / 2 > t) r--;
+  ti = r;
+  tj = t - r * (r + 1) / 2;
+}
+
+__global__ void __launch_bounds__(256, 2)
+grm_syrk_kernel(const double* __restrict__ Zt, int64_t ldz, int64_t p, double* __restrict__ G, int64_t ldg,
+                double* __restrict__ slab, int64_t ntiles, int nslices, int64_t steps_per_slice) {
+  __shared__ __attribute__((aligned(16))) double lds[2 * STAGE];  // 2 stages, 72 KB
+
+  const int64_t wg = blockIdx.x;
+  const int s = (int)(wg / ntiles);
+  const int64_t t = wg - (int64_t)s * ntiles;
+  int64_t ti, tj;
+  tile_of(t, ti, tj);
+  const bool diag = (ti == tj);
+  const int64_t i0 = ti * BT, j0 = tj * BT;
+
+  const int64_t nsteps_total = (p + BK - 1) / BK;
+  const int64_t kstep0 = (int64_t)s * steps_per_slice;
+  int64_t kstep1 = kstep0 + steps_per_slice;
+  if (kstep1 > nsteps_total) kstep1 = nsteps_total;
+  const int64_t nsteps = kstep1 > kstep0 ? kstep1 - kstep0 : 0;
+
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+
+  // each wave stages rows r = wave*4 .. wave*4+3 of A (and of B off-diagonal)
+  auto stage = [&](int64_t kstep, int buf) {
+    double* base = lds + buf * STAGE;
+#pragma unroll
+    for (int rr = 0; rr < 4; rr++) {
+      const int r = wave * 4 + rr;
+      const int64_t k = kstep * BK + r;
+      double* la = base + r * LROW;
+      double* lb = base + (BK + r) * LROW;
+      if (k < p) {
+        const double* src = Zt + k * ldz;
+        __builtin_amdgcn_global_load_lds((const void*)(src + i0 + lane * 2), (void*)la, 16, 0, 0);
+        if (!diag) __builtin_amdgcn_global_load_lds((const void*)(src + j0 + lane * 2), (void*)lb, 16, 0, 0);
+      } else {
+        *reinterpret_cast<double2*>(la + lane * 2) = make_double2(0.0, 0.0);
+        if (!diag) *reinterpret_cast<double2*>(lb + lane * 2) = make_double2(0.0, 0.0);
+      }
+    }
+  };
+
+  d4 acc[4][4];
+#pragma unroll
+  for (int a = 0; a < 4; a++)
+#pragma unroll
+    for (int b = 0; b < 4; b++) acc[a][b] = (d4){0.0, 0.0, 0.0, 0.0};
+
+  if (nsteps > 0) stage(kstep0, 0);
+  __syncthreads();
+
+  const int frag_row = lane >> 4;  // k within a 4-deep MFMA step
+  const int frag_col = lane & 15;
+  for (int64_t st = 0; st < nsteps; st++) {
+    const int buf = (int)(st & 1);
+    if (st + 1 < nsteps) stage(kstep0 + st + 1, buf ^ 1);
+    const double* A = lds + buf * STAGE;
+    const double* B = diag ? A : A + BK * LROW;
+#pragma unroll
+    for (int ks = 0; ks < BK / 4; ks++) {
+      const int kr = ks * 4 + frag_row;
+      double af[4], bf[4];
+#pragma unroll
+      for (int m = 0; m < 4; m++) af[m] = A[kr * LROW + wm * 64 + m * 16 + frag_col];
+#pragma unroll
+      for (int q = 0; q < 4; q++) bf[q] = B[kr * LROW + wn * 64 + q * 16 + frag_col];
+#pragma unroll
+      for (int m = 0; m < 4; m++)
+#pragma unroll
+        for (int q = 0; q < 4; q++) acc[m][q] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[m], bf[q], acc[m][q], 0, 0, 0);
+    }
+    __syncthreads();
+  }
+
+  // epilogue: f64 MFMA C/D map: col = lane & 15, row = (lane >> 4) + 4 * reg
+  if (nslices == 1) {
+#pragma unroll
+    for (int m = 0; m < 4; m++)
+#pragma unroll
+      for (int q = 0; q < 4; q++)
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+          const int64_t row = i0 + wm * 64 + m * 16 + frag_row + 4 * r;
+          const int64_t col = j0 + wn * 64 + q * 16 + frag_col;
+          G[row * ldg + col] = acc[m][q][r];
+        }
+  } else {
+    double* out = slab + ((int64_t)s * ntiles + t) * (int64_t)(BT * BT);
+#pragma unroll
+    for (int m = 0; m < 4; m++)
+#pragma unroll
+      for (int q = 0; q < 4; q++)
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+          const int row = wm * 64 + m * 16 + frag_row + 4 * r;
+          const int col = wn * 64 + q * 16 + frag_col;
+          out[row * BT + col] = acc[m][q][r];
+        }
+  }
+}
+
+// G tile = Σ_s slab[s][tile] in slice order (deterministic).
+__global__ void __launch_bounds__(256) grm_slab_reduce_kernel(const double* __restrict__ slab, int64_t ntiles,
+                                                              int nslices, double* __restrict__ G, int64_t ldg) {
+  const int64_t t = blockIdx.x;
+  int64_t ti, tj;
+  tile_of(t, ti, tj);
+  const int64_t per = (int64_t)BT * BT;
+  for (int e = threadIdx.x * 2; e < BT * BT; e += 256 * 2) {
+    double2 acc = make_double2(0.0, 0.0);
+    for (int s = 0; s < nslices; s++) {
+      const double2 v = *reinterpret_cast<const double2*>(slab + ((int64_t)s * ntiles + t) * per + e);
+      acc.x += v.x;
+      acc.y += v.y;
+    }
+    const int row = e / BT, col = e % BT;
+    *reinterpret_cast<double2*>(G + (ti * BT + row) * ldg + tj * BT + col) = acc;
+  }
+}
+
+static int resident_wgs() {
+  int dev = 0, cus = 256;
+  if (hipGetDevice(&dev) == hipSuccess) {
+    int v = 0;
+    if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0) cus = v;
+  }
+  return cus * 2;  // 2 workgroups per CU (LDS 72 KB each, 2 waves per SIMD)
+}
+
+static void plan(int64_t n, int64_t p, int64_t& ntiles, int& nslices, int64_t& steps_per_slice) {
+  const int64_t nt = npad_of(n) / BT;
+  ntiles = nt * (nt + 1) / 2;
+  const int64_t nsteps = (p + BK - 1) / BK;
+  const int64_t R = resident_wgs();
+  int best = 1;
+  double best_eff = 0.0;
+  for (int S = 1; S <= 8; S++) {
+    if (S > 1 && nsteps / S < 16) break;  // keep >= 16 stages per workgroup
+    const int64_t w = ntiles * S;
+    const double eff = (double)w / (double)(R * ((w + R - 1) / R));
+    if (eff > best_eff + 0.05) {
+      best_eff = eff;
+      best = S;
+    }
+    if (eff >= 0.92) break;
+  }
+  nslices = best;
+  steps_per_slice = (nsteps + nslices - 1) / nslices;
+}
+
+int64_t grm_workspace_bytes(int64_t n, int64_t p) {
+  int64_t ntiles, sps;
+  int S;
+  plan(n, p, ntiles, S, sps);
+  return S > 1 ? (int64_t)S * ntiles * BT * BT * (int64_t)sizeof(double) : 0;
+}
+
+int launch_grm(const double* Zt, int64_t ldz, int64_t p, int64_t n, double* G, int64_t ldg, void* ws,
+               int64_t ws_bytes, hipStream_t s) {
+  const int64_t npad = npad_of(n);
+  if (!Zt || !G || p < 1 || n < 1 || ldz < npad || ldg < npad || (ldz & 1))
+    return fail(GBM_E_ARG, "gbm_dev_grm: bad arguments (need ldz, ldg >= npad(n), even ldz)");
+  if (((uintptr_t)Zt & 15) != 0) return fail(GBM_E_ARG, "gbm_dev_grm: Zt must be 16-byte aligned");
+  int64_t ntiles, sps;
+  int S;
+  plan(n, p, ntiles, S, sps);
+  const int64_t need = S > 1 ? (int64_t)S * ntiles * BT * BT * (int64_t)sizeof(double) : 0;
+  if (need > 0 && (!ws || ws_bytes < need))
+    return fail(GBM_E_ARG, "gbm_dev_grm: workspace too small (" + std::to_string(ws_bytes) + " < " +
+                               std::to_string(need) + ")");
+  grm_syrk_kernel<<<(unsigned)(ntiles * S), 256, 0, s>>>(Zt, ldz, p, G, ldg, (double*)ws, ntiles, S, sps);
+  GBM_LAUNCH_CHECK();
+  if (S > 1) {
+    grm_slab_reduce_kernel<<<(unsigned)ntiles, 256, 0, s>>>((const double*)ws, ntiles, S, G, ldg);
+    GBM_LAUNCH_CHECK();
+  }
+  return GBM_OK;
+}
+
+}  // namespace gbm
+
+extern "C" int64_t gbm_dev_grm_workspace(int64_t n, int64_t p) { return gbm::grm_workspace_bytes(n, p); }
+
+extern "C" int gbm_dev_grm(const double* Zt, int64_t ldz, int64_t p, int64_t n, double* G, int64_t ldg,
+                           void* workspace, int64_t ws_bytes, void* stream) {
+  return gbm::launch_grm(Zt, ldz, p, n, G, ldg, workspace, ws_bytes, (hipStream_t)stream);
+}
+
+namespace gbm {
+// out[i, j] = inv_q * G[max(i,j), min(i,j)] for i, j < n (full symmetric export of the GRM)
+__global__ void __launch_bounds__(256) grm_export_kernel(const double* __restrict__ G, int64_t ldg, int64_t n,
+                                                         double inv_q, double* __restrict__ out, int64_t ldo) {
+  const int64_t i = blockIdx.x;
+  for (int64_t j = threadIdx.x; j < n; j += 256)
+    out[i * ldo + j] = inv_q * (j <= i ? G[i * ldg + j] : G[j * ldg + i]);
+}
+
+int launch_grm_export(const double* G, int64_t ldg, int64_t n, double inv_q, double* out, int64_t ldo, hipStream_t s) {
+  grm_export_kernel<<<(unsigned)n, 256, 0, s>>>(G, ldg, n, inv_q, out, ldo);
+  GBM_LAUNCH_CHECK();
+  return GBM_OK;
+}
+}  // namespace gbm

@@ -1,0 +1,181 @@
+// Locus-row streaming kernels: synthetic genotypes, int8 dosage expansion and the column
+// standardisation of reference src/gwas.jl:112-115,127-130 (HBM-bound; one pass over X).
+#include "gbm_internal.h"
+
+namespace gbm {
+
+// ---- counter-based genotype generator (bit-identical to oracle/gbm_oracle.c) -------------
+__device__ __forceinline__ uint64_t mix64(uint64_t z) {
+  z += 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+// One workgroup strip of 1024 columns of one locus row per blockIdx.x; rows grid-strided on y.
+__global__ void __launch_bounds__(256) synth_kernel(double* __restrict__ Xt, int64_t ldx, int64_t p,
+                                                    int64_t n, uint64_t seed, int64_t j0) {
+  for (int64_t j = blockIdx.y; j < p; j += gridDim.y) {
+    const uint64_t base = mix64(seed * 0xD1B54A32D192ED03ull + (uint64_t)(j0 + j));
+    const uint64_t thr = 214748364ull + (((base >> 32) * 1932735283ull) >> 32);
+    double* row = Xt + j * ldx;
+    for (int64_t i = (int64_t)blockIdx.x * 1024 + threadIdx.x; i < (int64_t)(blockIdx.x + 1) * 1024 && i < ldx;
+         i += 256) {
+      double v = 0.0;
+      if (i < n) {
+        const uint64_t h = mix64(base ^ ((uint64_t)i * 0x8CB92BA72F3D8DD7ull));
+        const int d = ((h & 0xFFFFFFFFull) < thr) + ((h >> 32) < thr);
+        v = 0.5 * (double)d;
+      }
+      row[i] = v;
+    }
+  }
+}
+
+// D column-major n x p int8 (ldd) -> Xt row-major p x ldx, X = d / ploidy.
+__global__ void __launch_bounds__(256) expand_i8_kernel(const int8_t* __restrict__ D, int64_t ldd,
+                                                        int64_t n, int64_t p, double inv_ploidy,
+                                                        double* __restrict__ Xt, int64_t ldx) {
+  for (int64_t j = blockIdx.y; j < p; j += gridDim.y) {
+    const int8_t* col = D + j * ldd;
+    double* row = Xt + j * ldx;
+    for (int64_t i = (int64_t)blockIdx.x * 1024 + threadIdx.x; i < (int64_t)(blockIdx.x + 1) * 1024 && i < ldx;
+         i += 256)
+      row[i] = i < n ? (double)col[i] * inv_ploidy : 0.0;
+  }
+}
+
+// ---- standardisation ---------------------------------------------------------------------
+template <int BS>
+__device__ __forceinline__ double block_sum(double v, double* red) {
+  // wave reduction (64 lanes) then across the BS/64 waves through LDS
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  __syncthreads();
+  if (lane == 0) red[w] = v;
+  __syncthreads();
+  double s = 0.0;
+#pragma unroll
+  for (int k = 0; k < BS / 64; k++) s += red[k];  // fixed order: deterministic
+  return s;
+}
+
+// One workgroup per locus row (grid-strided). NPT = values cached in registers per thread
+// (0 = generic path re-reading the row from L2/MALL).
+template <int BS, int NPT>
+__global__ void __launch_bounds__(BS) standardize_kernel(double* __restrict__ Xt, int64_t ldx, int64_t p,
+                                                         int64_t n, double* __restrict__ mean,
+                                                         double* __restrict__ sd, int32_t* __restrict__ keep,
+                                                         unsigned long long* __restrict__ q_dev) {
+  __shared__ double red[BS / 64];
+  unsigned long long kept_local = 0;
+  for (int64_t j = blockIdx.x; j < p; j += gridDim.x) {
+    double* row = Xt + j * ldx;
+    double m, v;
+    if constexpr (NPT > 0) {
+      double x[NPT];
+      double s = 0.0;
+#pragma unroll
+      for (int k = 0; k < NPT; k++) {
+        const int64_t i = (int64_t)k * BS + threadIdx.x;
+        x[k] = i < n ? row[i] : 0.0;
+        s += x[k];
+      }
+      m = block_sum<BS>(s, red) / (double)n;
+      double ss = 0.0;
+#pragma unroll
+      for (int k = 0; k < NPT; k++) {
+        const int64_t i = (int64_t)k * BS + threadIdx.x;
+        const double d = x[k] - m;
+        ss += i < n ? d * d : 0.0;
+      }
+      v = n > 1 ? sqrt(block_sum<BS>(ss, red) / (double)(n - 1)) : __builtin_nan("");
+      const bool kp = (v > 2.220446049250313e-16) && isfinite(v);
+      const double r = kp ? 1.0 / v : 0.0;
+#pragma unroll
+      for (int k = 0; k < NPT; k++) {
+        const int64_t i = (int64_t)k * BS + threadIdx.x;
+        if (i < ldx) row[i] = (kp && i < n) ? (x[k] - m) * r : 0.0;
+      }
+      for (int64_t i = (int64_t)NPT * BS + threadIdx.x; i < ldx; i += BS) row[i] = 0.0;
+      if (threadIdx.x == 0) {
+        mean[j] = m;
+        sd[j] = v;
+        keep[j] = kp ? 1 : 0;
+        kept_local += kp ? 1 : 0;
+      }
+    } else {
+      double s = 0.0;
+      for (int64_t i = threadIdx.x; i < n; i += BS) s += row[i];
+      m = block_sum<BS>(s, red) / (double)n;
+      double ss = 0.0;
+      for (int64_t i = threadIdx.x; i < n; i += BS) {
+        const double d = row[i] - m;
+        ss += d * d;
+      }
+      v = n > 1 ? sqrt(block_sum<BS>(ss, red) / (double)(n - 1)) : __builtin_nan("");
+      const bool kp = (v > 2.220446049250313e-16) && isfinite(v);
+      const double r = kp ? 1.0 / v : 0.0;
+      for (int64_t i = threadIdx.x; i < ldx; i += BS) row[i] = (kp && i < n) ? (row[i] - m) * r : 0.0;
+      if (threadIdx.x == 0) {
+        mean[j] = m;
+        sd[j] = v;
+        keep[j] = kp ? 1 : 0;
+        kept_local += kp ? 1 : 0;
+      }
+    }
+  }
+  if (threadIdx.x == 0 && kept_local) atomicAdd(q_dev, kept_local);
+}
+
+static dim3 row_grid(int64_t ldx, int64_t p) {
+  const int64_t gx = (ldx + 1023) / 1024;
+  const int64_t gy = p < 65535 ? p : 65535;
+  return dim3((unsigned)gx, (unsigned)(gy > 0 ? gy : 1));
+}
+
+}  // namespace gbm
+
+using namespace gbm;
+
+extern "C" int gbm_dev_synth_genotypes(double* Xt, int64_t ldx, int64_t p, int64_t n, uint64_t seed,
+                                       int64_t j0, void* stream) {
+  if (!Xt || p < 0 || n < 0 || ldx < n) return fail(GBM_E_ARG, "gbm_dev_synth_genotypes: bad arguments");
+  if (p == 0 || ldx == 0) return GBM_OK;
+  synth_kernel<<<row_grid(ldx, p), 256, 0, (hipStream_t)stream>>>(Xt, ldx, p, n, seed, j0);
+  GBM_LAUNCH_CHECK();
+  return GBM_OK;
+}
+
+extern "C" int gbm_dev_expand_dosage_i8(const int8_t* D, int64_t ldd, int64_t n, int64_t p, int ploidy,
+                                        double* Xt, int64_t ldx, void* stream) {
+  if (!D || !Xt || p < 0 || n < 0 || ldd < n || ldx < n || ploidy < 1)
+    return fail(GBM_E_ARG, "gbm_dev_expand_dosage_i8: bad arguments");
+  if (p == 0 || ldx == 0) return GBM_OK;
+  expand_i8_kernel<<<row_grid(ldx, p), 256, 0, (hipStream_t)stream>>>(D, ldd, n, p, 1.0 / ploidy, Xt, ldx);
+  GBM_LAUNCH_CHECK();
+  return GBM_OK;
+}
+
+extern "C" int gbm_dev_standardize(double* Xt, int64_t ldx, int64_t p, int64_t n, double* mean, double* sd,
+                                   int32_t* keep, int64_t* q_dev, void* stream) {
+  if (!Xt || !mean || !sd || !keep || !q_dev || p < 0 || n < 1 || ldx < n)
+    return fail(GBM_E_ARG, "gbm_dev_standardize: bad arguments");
+  if (p == 0) return GBM_OK;
+  hipStream_t s = (hipStream_t)stream;
+  const unsigned grid = (unsigned)(p < 256 * 16 ? p : 256 * 16);
+  auto q = reinterpret_cast<unsigned long long*>(q_dev);
+  if (n <= 256 * 4)
+    standardize_kernel<256, 4><<<grid, 256, 0, s>>>(Xt, ldx, p, n, mean, sd, keep, q);
+  else if (n <= 256 * 8)
+    standardize_kernel<256, 8><<<grid, 256, 0, s>>>(Xt, ldx, p, n, mean, sd, keep, q);
+  else if (n <= 256 * 16)
+    standardize_kernel<256, 16><<<grid, 256, 0, s>>>(Xt, ldx, p, n, mean, sd, keep, q);
+  else if (n <= 256 * 32)
+    standardize_kernel<256, 32><<<grid, 256, 0, s>>>(Xt, ldx, p, n, mean, sd, keep, q);
+  else
+    standardize_kernel<256, 0><<<grid, 256, 0, s>>>(Xt, ldx, p, n, mean, sd, keep, q);
+  GBM_LAUNCH_CHECK();
+  return GBM_OK;
+}

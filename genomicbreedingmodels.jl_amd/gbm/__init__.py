@@ -1,0 +1,18 @@
+"""gbm — host-side mirror of GenomicBreedingModels.jl's GBLUP path on MI355X.
+
+Public API mirrors the reference's model-function interface (src/GenomicBreedingModels.jl:35-48):
+``extractxyetc``, ``gblup`` (new, beside ``ridge``), ``predict``, ``metrics`` and the data types.
+The numerics run in libgbm.so (HIP, gfx950); nothing here falls back to a CPU path.
+"""
+from ._lib import ArgumentError, GBMError, device_count, load as load_library
+from .linear import gblup, gblup_arrays
+from .metrics import heritabilitynarrow_sense, metrics, pearsonscorrelation, r2
+from .prediction import LINEAR_MODELS, extractxyetc, predict
+from .types import Fit, Genomes, Phenomes
+from .arrays import colstats, grm
+
+__all__ = [
+    "ArgumentError", "GBMError", "device_count", "load_library",
+    "gblup", "gblup_arrays", "metrics", "pearsonscorrelation", "r2", "heritabilitynarrow_sense",
+    "LINEAR_MODELS", "extractxyetc", "predict", "Fit", "Genomes", "Phenomes", "colstats", "grm",
+]

@@ -1,0 +1,134 @@
+"""ctypes binding of libgbm.so (include/gbm.h) — the same C ABI a Julia ``ccall`` binds.
+
+The library is loaded from this package directory (built in-tree by ``__graft_entry__.build()``).
+There is no fallback: if the HIP library is missing or no GPU is visible, calls raise.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+import numpy as np
+
+GBM_OK = 0
+GBM_E_ARG = -1
+GBM_E_NOTPD = -2
+GBM_E_HIP = -3
+GBM_E_RCCL = -4
+GBM_E_OOM = -5
+GBM_E_NODEV = -6
+GBM_E_DATA = -7
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libgbm.so")
+
+# Every symbol include/gbm.h declares (tests check the export table against this list).
+EXPORTS = (
+    "gbm_version", "gbm_last_error", "gbm_device_count",
+    "gbm_gblup_fit", "gbm_gblup_fit_dosage_i8", "gbm_grm", "gbm_colstats", "gbm_predict",
+    "gbm_dev_npad", "gbm_dev_gdim", "gbm_dev_grm_workspace", "gbm_dev_solve_workspace",
+    "gbm_dev_synth_genotypes", "gbm_dev_expand_dosage_i8", "gbm_dev_standardize", "gbm_dev_grm",
+    "gbm_dev_gblup_solve", "gbm_dev_marker_effects",
+)
+
+
+class ArgumentError(ValueError):
+    """Mirrors Julia's ArgumentError thrown by the reference (e.g. src/prediction.jl:67-112)."""
+
+
+class GBMError(RuntimeError):
+    """Mirrors Julia's ErrorException (e.g. src/linear.jl:235-237, src/prediction.jl:125-127)."""
+
+
+_lock = threading.Lock()
+_lib = None
+
+P = ctypes.c_void_p
+I64 = ctypes.c_int64
+I32 = ctypes.c_int
+D = ctypes.c_double
+U64 = ctypes.c_uint64
+
+
+def _declare(lib):
+    lib.gbm_version.restype = I32
+    lib.gbm_version.argtypes = []
+    lib.gbm_last_error.restype = ctypes.c_char_p
+    lib.gbm_last_error.argtypes = []
+    lib.gbm_device_count.restype = I32
+    lib.gbm_device_count.argtypes = [ctypes.POINTER(I32)]
+    lib.gbm_gblup_fit.restype = I32
+    lib.gbm_gblup_fit.argtypes = [P, I64, I64, I64, P, I64, I64, D, P, I32, P, P, P, P]
+    lib.gbm_gblup_fit_dosage_i8.restype = I32
+    lib.gbm_gblup_fit_dosage_i8.argtypes = [P, I64, I64, I64, I32, P, I64, I64, D, P, I32, P, P, P, P]
+    lib.gbm_grm.restype = I32
+    lib.gbm_grm.argtypes = [P, I64, I64, I64, P, I32, P, I64, P]
+    lib.gbm_colstats.restype = I32
+    lib.gbm_colstats.argtypes = [P, I64, I64, I64, I32, P, P, P, P]
+    lib.gbm_predict.restype = I32
+    lib.gbm_predict.argtypes = [P, I64, I64, I64, P, I64, I64, I32, P, I64]
+    for f in ("gbm_dev_npad", "gbm_dev_gdim"):
+        getattr(lib, f).restype = I64
+        getattr(lib, f).argtypes = [I64]
+    for f in ("gbm_dev_grm_workspace", "gbm_dev_solve_workspace"):
+        getattr(lib, f).restype = I64
+        getattr(lib, f).argtypes = [I64, I64]
+    lib.gbm_dev_synth_genotypes.restype = I32
+    lib.gbm_dev_synth_genotypes.argtypes = [P, I64, I64, I64, U64, I64, P]
+    lib.gbm_dev_expand_dosage_i8.restype = I32
+    lib.gbm_dev_expand_dosage_i8.argtypes = [P, I64, I64, I64, I32, P, I64, P]
+    lib.gbm_dev_standardize.restype = I32
+    lib.gbm_dev_standardize.argtypes = [P, I64, I64, I64, P, P, P, P, P]
+    lib.gbm_dev_grm.restype = I32
+    lib.gbm_dev_grm.argtypes = [P, I64, I64, I64, P, I64, P, I64, P]
+    lib.gbm_dev_gblup_solve.restype = I32
+    lib.gbm_dev_gblup_solve.argtypes = [P, I64, I64, D, D, P, I64, I64, P, P, I64, P, P, P, I64, P]
+    lib.gbm_dev_marker_effects.restype = I32
+    lib.gbm_dev_marker_effects.argtypes = [P, I64, I64, I64, P, I64, I64, D, P, P, P, P, I64, P, P]
+    return lib
+
+
+def load():
+    """Load libgbm.so (once). Raises ImportError if the HIP library has not been built."""
+    global _lib
+    with _lock:
+        if _lib is None:
+            if not os.path.exists(LIB_PATH):
+                raise ImportError(
+                    f"libgbm.so not found at {LIB_PATH}: build it with `python -c 'import __graft_entry__ as g; g.build()'`"
+                    " (the GBLUP path has no CPU fallback)")
+            _lib = _declare(ctypes.CDLL(LIB_PATH))
+            v = _lib.gbm_version()
+            if v != 100:
+                raise ImportError(f"libgbm.so ABI version {v} != 100")
+        return _lib
+
+
+def last_error() -> str:
+    return load().gbm_last_error().decode("utf-8", "replace")
+
+
+def check(rc: int, what: str):
+    if rc == GBM_OK:
+        return
+    msg = f"{what}: {last_error()} (code {rc})"
+    if rc == GBM_E_ARG:
+        raise ArgumentError(msg)
+    raise GBMError(msg)
+
+
+def device_count() -> int:
+    c = I32(0)
+    check(load().gbm_device_count(ctypes.byref(c)), "gbm_device_count")
+    return c.value
+
+
+def ptr(a: np.ndarray):
+    return ctypes.c_void_p(a.ctypes.data) if a is not None else None
+
+
+def devices_arg(devices):
+    if devices is None:
+        return None, 0
+    arr = (ctypes.c_int * len(devices))(*devices)
+    return arr, len(devices)

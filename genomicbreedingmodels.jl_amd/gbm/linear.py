@@ -1,0 +1,69 @@
+"""``gblup`` model function — the drop-in beside reference ``ridge`` (src/linear.jl:162-239).
+
+Same keyword signature as every reference model function (the six keywords
+``cvmultithread!`` passes at src/cross_validation.jl:170-177, plus ``lambda_`` with a default),
+same Fit assembly sequence (src/linear.jl:185-191,223-238); where ``ridge`` calls
+``GLMNet.glmnetcv`` (src/linear.jl:193-203) this calls ``gbm_gblup_fit`` in libgbm.so
+(GRM on fp64 MFMA + blocked Cholesky on the MI355X).
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from . import _lib
+from ._lib import GBMError
+from .metrics import metrics
+from .prediction import extractxyetc
+from .types import Fit, Genomes, Phenomes
+
+
+def gblup_arrays(X: np.ndarray, Y: np.ndarray, lambda_: float = 1.0, devices=None):
+    """Array-level GBLUP through the C ABI. X (n, p) any order, Y (n,) or (n, t).
+
+    Returns (b_hat (p+1, t), y_pred (n, t), mu (t,), q)."""
+    X = np.asfortranarray(np.asarray(X, dtype=np.float64))
+    Y = np.asarray(Y, dtype=np.float64)
+    if Y.ndim == 1:
+        Y = Y[:, None]
+    Y = np.asfortranarray(Y)
+    n, p = X.shape
+    t = Y.shape[1]
+    b_hat = np.zeros((p + 1, t), order="F")
+    y_pred = np.zeros((n, t), order="F")
+    mu = np.zeros(t)
+    q = np.zeros(1, dtype=np.int64)
+    devs, ndev = _lib.devices_arg(devices)
+    lib = _lib.load()
+    rc = lib.gbm_gblup_fit(_lib.ptr(X), n, p, n, _lib.ptr(Y), n, t, float(lambda_), devs, ndev,
+                           _lib.ptr(b_hat), _lib.ptr(y_pred), _lib.ptr(mu), _lib.ptr(q))
+    _lib.check(rc, "gbm_gblup_fit")
+    return b_hat, y_pred, mu, int(q[0])
+
+
+def gblup(*, genomes: Genomes, phenomes: Phenomes, idx_entries=None, idx_loci_alleles=None,
+          idx_trait: int = 1, verbose: bool = False, lambda_: float = 1.0, devices=None,
+          model_label: str = "gblup") -> Fit:
+    """GBLUP / RR-BLUP fit returning a ``Fit`` exactly like ``ridge`` does.
+
+    ``model_label="ridge"`` lets the fit flow through an unmodified reference ``predict``
+    whitelist (src/prediction.jl:225): GBLUP ≡ RR-BLUP, so the linear predictor is valid."""
+    X, y, entries, populations, loci_alleles = extractxyetc(
+        genomes, phenomes, idx_entries=idx_entries, idx_loci_alleles=idx_loci_alleles,
+        idx_trait=idx_trait, add_intercept=False)
+    fit = Fit(n=X.shape[0], l=X.shape[1])
+    fit.model = model_label
+    fit.b_hat_labels = ["intercept"] + list(loci_alleles)
+    fit.trait = phenomes.traits[idx_trait - 1]
+    fit.entries = entries
+    fit.populations = populations
+    fit.y_true = y
+    b_hat, y_pred, mu, q = gblup_arrays(X, y, lambda_=lambda_, devices=devices)
+    fit.b_hat = b_hat[:, 0].copy()
+    fit.y_pred = y_pred[:, 0].copy()
+    fit.metrics = metrics(y, fit.y_pred)
+    if verbose:
+        print(f"gblup: n={X.shape[0]} p={X.shape[1]} q={q} mu={mu[0]:.6g} lambda={lambda_}")
+        print(fit.metrics)
+    if not fit.checkdims():
+        raise GBMError("Error fitting " + fit.model + ".")
+    return fit

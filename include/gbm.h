@@ -1,0 +1,186 @@
+/*
+ * gbm.h — C ABI of the MI355X-native GRM + GBLUP core (libgbm.so).
+ *
+ * This is the drop-in boundary for GenomicBreedingModels.jl's model-function path
+ * (SURVEY.md §8b). A Julia `gblup(; genomes, phenomes, idx_entries, idx_loci_alleles,
+ * idx_trait, verbose, λ)::Fit` built exactly like `ridge` (reference src/linear.jl:162-239)
+ * calls `gbm_gblup_fit` where `ridge` calls `GLMNet.glmnetcv` (src/linear.jl:193-203);
+ * the Julia/ctypes bindings are shown in INTEGRATION.md.
+ *
+ * Conventions
+ *  - All matrices crossing the host entry points are Julia column-major Float64:
+ *    X[i, j] lives at X[i + j*ldx] (i = entry/individual, j = locus-allele/SNP).
+ *    A SNP column is therefore contiguous, and the device view of X is the row-major
+ *    p x n matrix Xt ("locus rows"), whose rows are loaded coalesced along individuals.
+ *  - The model is V = G + λI with G = Z Zᵀ / q, Z the column-standardised (ddof = 1)
+ *    genotypes over the q non-monomorphic loci (reference src/gwas.jl:112-115,127-130;
+ *    V = σ²_u·GRM + σ²_e·I with Z = I at src/gwas.jl:462-471, λ = σ²_e/σ²_u).
+ *  - Fixed effect: GLS intercept μ̂ = 1ᵀV⁻¹y / 1ᵀV⁻¹1 (src/gwas.jl:596-597 with X = 1).
+ *  - GEBVs / y_pred = μ̂ + G·a with a = V⁻¹(y − 1μ̂).
+ *  - b_hat = [b0; b] with b_j = (Zᵀa)_j / (q·s_j) for kept loci (0 for monomorphic ones)
+ *    and b0 = μ̂ − Σ_j m_j b_j, so the reference's linear `predict`
+ *    (`b_hat[1] .+ X*b_hat[2:end]`, src/prediction.jl:228) reproduces y_pred exactly.
+ *  - Return codes: 0 on success, negative GBM_E_* on failure; gbm_last_error() returns a
+ *    thread-local message for the last failing call on the calling thread.
+ *  - Re-entrant: every call allocates its own stream and device workspace; concurrent
+ *    calls (as `cvmultithread!` makes, src/cross_validation.jl:159) do not share state.
+ */
+#ifndef GBM_H
+#define GBM_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GBM_VERSION 100 /* 0.1.0 */
+
+#define GBM_OK 0
+#define GBM_E_ARG (-1)    /* bad argument (ArgumentError on the Julia side, src/prediction.jl:67-127 style) */
+#define GBM_E_NOTPD (-2)  /* G + λI not positive definite (non-finite input or λ <= 0) */
+#define GBM_E_HIP (-3)    /* HIP runtime error */
+#define GBM_E_RCCL (-4)   /* RCCL error */
+#define GBM_E_OOM (-5)    /* device allocation failed */
+#define GBM_E_NODEV (-6)  /* no usable MI355X device */
+#define GBM_E_DATA (-7)   /* data problem: < 2 entries, zero phenotype variance, no polymorphic locus */
+
+/* Library version (GBM_VERSION) — used by bindings to check the ABI. */
+int gbm_version(void);
+
+/* Message for the last failing call on this thread ("" if none). Never NULL. */
+const char* gbm_last_error(void);
+
+/* Number of visible HIP devices (0 when none). Returns GBM_OK or GBM_E_HIP. */
+int gbm_device_count(int* count);
+
+/* --------------------------------------------------------------------------------------
+ * Host-buffer entry points (what a Julia `ccall` binds; buffers owned by the caller,
+ * no pointer is retained after return).
+ * ------------------------------------------------------------------------------------ */
+
+/*
+ * GBLUP fit of nrhs traits that share the same entries and loci.
+ *   X          n x p column-major allele frequencies (ldx >= n); replaces the matrix that
+ *              `extractxyetc(...; add_intercept=false)` returns (src/prediction.jl:129)
+ *   Y          n x nrhs column-major phenotypes (ldy >= n), already filtered for missing
+ *              values (src/prediction.jl:114-124)
+ *   lambda     λ = σ²_e/σ²_u > 0
+ *   devices    device ordinals (NULL/ndev = 0: device 0). With ndev > 1 SNP columns are
+ *              sharded into contiguous blocks, one per device, and the partial GRMs are
+ *              summed with an RCCL all-reduce.
+ * Outputs (caller allocated):
+ *   b_hat_out  (p+1) x nrhs column-major: [b0; b_1..b_p] per trait (src/linear.jl:218-221 layout)
+ *   y_pred_out n x nrhs column-major GEBVs (= fitted values)
+ *   mu_out     nrhs GLS intercepts μ̂ (may be NULL)
+ *   q_out      number of polymorphic loci used (may be NULL)
+ * Replaces: GLMNet.glmnetcv(X, y; alpha=0, ...) + coefficient selection, src/linear.jl:193-221.
+ */
+int gbm_gblup_fit(const double* X, int64_t n, int64_t p, int64_t ldx,
+                  const double* Y, int64_t ldy, int64_t nrhs, double lambda,
+                  const int* devices, int ndev,
+                  double* b_hat_out, double* y_pred_out, double* mu_out, int64_t* q_out);
+
+/*
+ * Same as gbm_gblup_fit for int8 dosages: X[i, j] = D[i + j*ldd] / ploidy (exact in fp64).
+ * 1 byte per genotype cell over PCIe instead of 8.
+ */
+int gbm_gblup_fit_dosage_i8(const int8_t* D, int64_t n, int64_t p, int64_t ldd, int ploidy,
+                            const double* Y, int64_t ldy, int64_t nrhs, double lambda,
+                            const int* devices, int ndev,
+                            double* b_hat_out, double* y_pred_out, double* mu_out, int64_t* q_out);
+
+/*
+ * Genomic relationship matrix only: G = Z Zᵀ / q (n x n, column-major == row-major since
+ * symmetric, ldg >= n). Replaces GenomicBreedingCore.grmsimple(genomes).genomic_relationship_matrix
+ * at src/gwas.jl:124-125 under the north-star formula (the Core implementation is un-vendored).
+ */
+int gbm_grm(const double* X, int64_t n, int64_t p, int64_t ldx, const int* devices, int ndev,
+            double* G_out, int64_t ldg, int64_t* q_out);
+
+/*
+ * Column statistics of X: mean, std (ddof = 1, Julia `std`), keep = (std > eps(Float64) and
+ * finite), q = Σ keep. Mirrors src/gwas.jl:112-113. Any of mean/sd/keep may be NULL.
+ */
+int gbm_colstats(const double* X, int64_t n, int64_t p, int64_t ldx, int device,
+                 double* mean_out, double* sd_out, uint8_t* keep_out, int64_t* q_out);
+
+/*
+ * Linear predictor of `predict` (src/prediction.jl:228): out[i, t] = b_hat[0, t] + Σ_j X[i, j] b_hat[1 + j, t].
+ * X n x p column-major (ldx >= n); b_hat (p+1) x nrhs column-major; out n x nrhs column-major.
+ */
+int gbm_predict(const double* X, int64_t n, int64_t p, int64_t ldx,
+                const double* b_hat, int64_t ldb, int64_t nrhs, int device,
+                double* out, int64_t ldo);
+
+/* --------------------------------------------------------------------------------------
+ * Device-level, stream-ordered entry points (all pointers are device pointers, `stream`
+ * is a hipStream_t or NULL for the null stream). Nothing here synchronises the stream.
+ * These are the stages the host entry points are built from; the multi-process
+ * (one rank per GPU, RCCL all-reduce between grm and solve) path calls them directly.
+ *
+ * Device layout ("plan geometry", all row-major):
+ *   Xt  p x ldx,  ldx >= gbm_dev_npad(n): locus j's n genotypes in Xt[j*ldx + 0..n-1]
+ *   G   gbm_dev_gdim(n) x gbm_dev_gdim(n) with ld == gbm_dev_gdim(n): the GRM occupies
+ *       rows/cols [0, npad); rows [npad, gdim) are the bordered right-hand sides used by
+ *       the fused forward substitution of the Cholesky.
+ * ------------------------------------------------------------------------------------ */
+
+/* Padded individual count (multiple of the 128-row tile). */
+int64_t gbm_dev_npad(int64_t n);
+/* Dimension of the bordered V matrix: npad + 64 (room for 1 + nrhs <= 64 right-hand sides). */
+int64_t gbm_dev_gdim(int64_t n);
+/* Bytes of device workspace gbm_dev_grm needs for (n, p). */
+int64_t gbm_dev_grm_workspace(int64_t n, int64_t p);
+/* Bytes of device workspace gbm_dev_gblup_solve needs for (n, nrhs). */
+int64_t gbm_dev_solve_workspace(int64_t n, int64_t nrhs);
+
+/* Fill Xt with synthetic genotypes: locus (j0 + j) of a counter-based hash of (seed, i, j0 + j);
+ * MAF f ~ U(0.05, 0.5) per locus, dosage ~ Binomial(2, f), X = dosage / 2.
+ * Bit-identical to oracle/gbm_oracle.c:gbm_ref_synth_genotype. Zero-fills columns [n, ldx). */
+int gbm_dev_synth_genotypes(double* Xt, int64_t ldx, int64_t p, int64_t n, uint64_t seed,
+                            int64_t j0, void* stream);
+
+/* Expand int8 dosages (column-major D, n x p, ldd) into Xt (row-major p x ldx) as D/ploidy. */
+int gbm_dev_expand_dosage_i8(const int8_t* D, int64_t ldd, int64_t n, int64_t p, int ploidy,
+                             double* Xt, int64_t ldx, void* stream);
+
+/* In place: Xt row j <- (x_j − m_j)/s_j for kept loci, 0 for dropped ones and for the
+ * padding columns [n, ldx). Writes mean/sd (p each), keep (p, int32) and atomically adds
+ * the kept count into *q_dev (caller zeroes it). src/gwas.jl:112-115,127-130. */
+int gbm_dev_standardize(double* Xt, int64_t ldx, int64_t p, int64_t n,
+                        double* mean, double* sd, int32_t* keep, int64_t* q_dev, void* stream);
+
+/* G[0:npad, 0:npad] (lower triangle and diagonal tiles) = Σ_j z_j z_jᵀ over the p locus rows
+ * of Zt (unscaled; the all-reduce of multi-GPU shards happens on this). fp64 MFMA SYRK. */
+int gbm_dev_grm(const double* Zt, int64_t ldz, int64_t p, int64_t n, double* G, int64_t ldg,
+                void* workspace, int64_t ws_bytes, void* stream);
+
+/*
+ * Solve the GBLUP system on G (as left by gbm_dev_grm, summed over shards):
+ *   V = G·inv_q + λI ; LLᵀ = V (blocked fp64 Cholesky, in place) ; μ̂, a = V⁻¹(y − 1μ̂),
+ *   gebv = μ̂ + (y − 1μ̂) − λa.
+ *   Y      nrhs x ldy row-major (trait t's n phenotypes contiguous), 1 <= nrhs <= 63
+ *   A_out  nrhs x lda row-major: a vectors (lda >= npad; zero in the padding)
+ *   gebv   nrhs x lda row-major; mu nrhs; info (device int32): 0 or the 1-based failing pivot.
+ */
+int gbm_dev_gblup_solve(double* G, int64_t ldg, int64_t n, double inv_q, double lambda,
+                        const double* Y, int64_t ldy, int64_t nrhs,
+                        double* A_out, double* gebv, int64_t lda, double* mu, int32_t* info,
+                        void* workspace, int64_t ws_bytes, void* stream);
+
+/*
+ * Marker effects on the standardised locus rows: B[t, j] = (Zt_j · a_t)·inv_q / sd_j for kept
+ * loci, 0 otherwise (B nrhs x ldb row-major), and msum[t] = Σ_j mean_j B[t, j] over this
+ * shard (so that b0 = μ̂ − Σ_shards msum).
+ */
+int gbm_dev_marker_effects(const double* Zt, int64_t ldz, int64_t p, int64_t n,
+                           const double* A, int64_t lda, int64_t nrhs, double inv_q,
+                           const double* mean, const double* sd, const int32_t* keep,
+                           double* B, int64_t ldb, double* msum, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* GBM_H */

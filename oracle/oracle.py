@@ -1,0 +1,211 @@
+"""CPU oracle (fp64 numpy/LAPACK) for the GRM + GBLUP hot path — TEST INFRASTRUCTURE ONLY.
+
+This module is the checker, never the product: only ``tests/``, ``__graft_entry__.smoke()`` and
+``bench.py``'s ``cpu_baseline`` leg may import it. The product path (``gbm.gblup`` → libgbm.so →
+HIP kernels) never calls into ``oracle/`` and fails loudly when the HIP library is missing.
+
+Parity status: **parity unpinned against the reference itself.** The reference is Julia
+(GenomicBreedingModels.jl v0.3.0) and the GRM lives in the un-vendored GenomicBreedingCore
+(called at reference src/gwas.jl:117-126); ``julia`` is absent from the image and the
+reference ships no numeric golden vectors. This file is an
+independent restatement of the reference's conventions, pinned by (i) the reference's own
+doctest properties (standardised moments within 1e-10, src/gwas.jl:55-62; extractxyetc shape
+and content, src/prediction.jl:44-50), (ii) the primal RR-BLUP ≡ dual GBLUP identity and
+(iii) a second, independent C restatement (oracle/gbm_oracle.c). See DESIGN.md "Oracle".
+
+Every function cites the reference lines it restates.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+EPS64 = np.finfo(np.float64).eps
+
+# ----------------------------------------------------------------------------------------
+# Synthetic genotypes: counter-based hash. Identical integer arithmetic to
+# oracle/gbm_oracle.c and the HIP generator kernel, so X is bit-identical everywhere.
+# ----------------------------------------------------------------------------------------
+_M64 = np.uint64(0xFFFFFFFFFFFFFFFF)
+_GOLD = np.uint64(0x9E3779B97F4A7C15)
+_C1 = np.uint64(0xBF58476D1CE4E5B9)
+_C2 = np.uint64(0x94D049BB133111EB)
+_KJ = np.uint64(0xD1B54A32D192ED03)
+_KI = np.uint64(0x8CB92BA72F3D8DD7)
+_F_LO = np.uint64(214748364)     # floor(0.05 * 2^32)
+_F_SPAN = np.uint64(1932735283)  # floor(0.45 * 2^32)
+
+
+def _mix64(z):
+    """splitmix64 finalizer on uint64 arrays (wrapping arithmetic)."""
+    with np.errstate(over="ignore"):
+        z = (z + _GOLD).astype(np.uint64)
+        z = ((z ^ (z >> np.uint64(30))) * _C1).astype(np.uint64)
+        z = ((z ^ (z >> np.uint64(27))) * _C2).astype(np.uint64)
+        return z ^ (z >> np.uint64(31))
+
+
+def synth_locus_threshold(seed: int, j):
+    """32-bit threshold t_j with f_j = t_j / 2^32 ∈ [0.05, 0.5)."""
+    j = np.asarray(j, dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        base = _mix64(np.uint64(seed) * _KJ + j)
+    return _F_LO + (((base >> np.uint64(32)) * _F_SPAN) >> np.uint64(32))
+
+
+def synth_genotypes(seed: int, n: int, p: int, j0: int = 0) -> np.ndarray:
+    """X (n x p, Fortran order like Julia) with X[i, j] = dosage/2 of locus j0 + j."""
+    j = np.arange(j0, j0 + p, dtype=np.uint64)
+    i = np.arange(n, dtype=np.uint64)
+    thr = synth_locus_threshold(seed, j)  # (p,)
+    with np.errstate(over="ignore"):
+        base = _mix64(np.uint64(seed) * _KJ + j)  # (p,)
+        h = _mix64(base[None, :] ^ (i[:, None] * _KI))  # (n, p)
+    u1 = h & np.uint64(0xFFFFFFFF)
+    u2 = h >> np.uint64(32)
+    d = (u1 < thr[None, :]).astype(np.int8) + (u2 < thr[None, :]).astype(np.int8)
+    return np.asfortranarray(d.astype(np.float64) * 0.5)
+
+
+def synth_phenotypes(X: np.ndarray, seed: int, ntraits: int = 1, qtl_frac: float = 0.01,
+                     h2: float = 0.5) -> np.ndarray:
+    """y = Xβ + e with 1% QTL effects N(0,1) and e ~ N(0, var(g)(1-h²)/h²)."""
+    n, p = X.shape
+    rng = np.random.default_rng(seed)
+    Y = np.empty((n, ntraits))
+    for t in range(ntraits):
+        nq = max(1, int(round(qtl_frac * p)))
+        idx = rng.choice(p, size=nq, replace=False)
+        beta = rng.standard_normal(nq)
+        g = X[:, idx] @ beta
+        vg = g.var(ddof=1) if n > 1 else 1.0
+        ve = vg * (1.0 - h2) / h2 if vg > 0 else 1.0
+        Y[:, t] = g + rng.standard_normal(n) * np.sqrt(ve)
+    return Y
+
+
+# ----------------------------------------------------------------------------------------
+# The hot path restated.
+# ----------------------------------------------------------------------------------------
+
+def colstats(X: np.ndarray):
+    """mean, std (ddof=1, Julia ``std``) and the keep mask of reference src/gwas.jl:112-113:
+    ``v = std(G, dims=1)``; keep ``v .> eps(Float64)`` and finite."""
+    n = X.shape[0]
+    m = X.mean(axis=0)
+    if n > 1:
+        s = np.sqrt(((X - m) ** 2).sum(axis=0) / (n - 1))
+    else:
+        s = np.full(X.shape[1], np.nan)
+    keep = (s > EPS64) & np.isfinite(s)
+    return m, s, keep
+
+
+def standardize(X: np.ndarray, m: np.ndarray, s: np.ndarray, keep: np.ndarray) -> np.ndarray:
+    """Z = (X − m)/s over kept columns (reference src/gwas.jl:114,129)."""
+    return (X[:, keep] - m[keep]) / s[keep]
+
+
+def grm(X: np.ndarray):
+    """G = Z Zᵀ / q (north_star; replaces Core's grmsimple called at src/gwas.jl:124)."""
+    m, s, keep = colstats(X)
+    Z = standardize(X, m, s, keep)
+    q = Z.shape[1]
+    if q == 0:
+        raise ValueError("no polymorphic locus")
+    return (Z @ Z.T) / q, q
+
+
+def gblup_fit(X: np.ndarray, Y: np.ndarray, lam: float = 1.0) -> dict:
+    """GBLUP on V = G + λI (reference src/gwas.jl:462-471 with σ²_u = 1, σ²_e = λ).
+
+    μ̂ = 1ᵀV⁻¹y / 1ᵀV⁻¹1 (GLS, src/gwas.jl:596 with X = 1), a = V⁻¹(y − 1μ̂),
+    GEBV = μ̂ + G a, marker effects b_j = (Zᵀa)_j/(q s_j), b0 = μ̂ − Σ m_j b_j so that
+    ``b_hat[1] .+ X*b_hat[2:end]`` (src/prediction.jl:228) reproduces the GEBVs.
+    Y may be (n,) or (n, t). Returns a dict of fp64 arrays (trait along the last axis).
+    """
+    import scipy.linalg as sla
+
+    X = np.asarray(X, dtype=np.float64)
+    Y = np.asarray(Y, dtype=np.float64)
+    if Y.ndim == 1:
+        Y = Y[:, None]
+    n, p = X.shape
+    m, s, keep = colstats(X)
+    Z = standardize(X, m, s, keep)
+    q = Z.shape[1]
+    if q == 0:
+        raise ValueError("no polymorphic locus")
+    G = (Z @ Z.T) / q
+    V = G + lam * np.eye(n)
+    c = sla.cho_factor(V, lower=True)
+    ones = np.ones(n)
+    vi1 = sla.cho_solve(c, ones)
+    viy = sla.cho_solve(c, Y)
+    mu = (ones @ viy) / (ones @ vi1)
+    R = Y - mu[None, :]
+    A = sla.cho_solve(c, R)
+    U = R - lam * A  # = G a  (since (G + λI) a = R)
+    gebv = mu[None, :] + U
+    beta_std = (Z.T @ A) / q  # (q, t)
+    B = np.zeros((p, Y.shape[1]))
+    B[keep, :] = beta_std / s[keep][:, None]
+    b0 = mu - m @ B
+    b_hat = np.vstack([b0[None, :], B])
+    return dict(b_hat=b_hat, y_pred=gebv, mu=mu, q=q, a=A, G=G, mean=m, sd=s, keep=keep)
+
+
+def rrblup_primal(X: np.ndarray, y: np.ndarray, lam: float, mu: float):
+    """Primal ridge form (ZᵀZ + qλI)β = Zᵀ(y − μ̂) — must equal the dual GBLUP β̃ (known-answer
+    identity used to pin the oracle)."""
+    m, s, keep = colstats(X)
+    Z = standardize(X, m, s, keep)
+    q = Z.shape[1]
+    lhs = Z.T @ Z + q * lam * np.eye(q)
+    return np.linalg.solve(lhs, Z.T @ (y - mu))
+
+
+def predict_linear(X: np.ndarray, b_hat: np.ndarray) -> np.ndarray:
+    """``b_hat[1] .+ X*b_hat[2:end]`` (reference src/prediction.jl:228)."""
+    return b_hat[0] + X @ b_hat[1:]
+
+
+# ----------------------------------------------------------------------------------------
+# metrics (reference src/metrics.jl:23-128; Distances.jl semantics restated)
+# ----------------------------------------------------------------------------------------
+
+def metrics(y_true: np.ndarray, y_pred: np.ndarray) -> dict:
+    y_true = np.asarray(y_true, dtype=np.float64)
+    y_pred = np.asarray(y_pred, dtype=np.float64)
+
+    def var(v):
+        return v.var(ddof=1) if v.size > 1 else np.nan
+
+    low = (var(y_true) < 1e-10) or (var(y_pred) < 1e-10)
+    d = y_true - y_pred
+    if low:
+        cor = 0.0
+        r2 = 0.0
+        h2 = 0.0
+    else:
+        a = y_true - y_true.mean()
+        b = y_pred - y_pred.mean()
+        cor = float(1.0 - (1.0 - (a @ b) / np.sqrt((a @ a) * (b @ b))))
+        r2 = float(1.0 - var(d) / var(y_true))
+        s2a = var(y_pred)
+        s2e = var(d)
+        h2 = s2a / (s2a + s2e) if (s2a + s2e) >= 1e-20 else 0.0
+        h2 = float(min(max(h2, 0.0), 1.0))
+    msd = float(np.mean(d * d))
+    rmsd = float(np.sqrt(msd))
+    return {
+        "cor": cor,
+        "mad": float(np.mean(np.abs(d))),
+        "msd": msd,
+        "rmsd": rmsd,
+        "nrmsd": float(rmsd / (y_true.max() - y_true.min())),
+        "euc": float(np.sqrt(np.sum(d * d))),
+        "jac": float(1.0 - np.sum(np.minimum(y_true, y_pred)) / np.sum(np.maximum(y_true, y_pred))),
+        "tvar": float(0.5 * np.sum(np.abs(d))),
+        "h²": h2,
+        "r²": r2,
+    }

@@ -1,0 +1,117 @@
+"""HIP path vs the CPU oracle (numpy/LAPACK restatement) — the parity tests proper.
+
+Tolerance (north_star): GEBVs within 1e-6 relative in fp64; b_hat within 1e-6 relative to
+max|b|. In practice the fp64 MFMA path agrees to ~1e-12 at these sizes, and we assert 1e-9 on
+y_pred as a tighter regression guard (still far inside the contract)."""
+import numpy as np
+import pytest
+
+import oracle
+import gbm
+
+pytestmark = pytest.mark.gpu
+
+TOL_CONTRACT = 1e-6
+TOL_TIGHT = 1e-9
+
+
+def rel(a, b):
+    return float(np.abs(np.asarray(a) - np.asarray(b)).max() / max(np.abs(np.asarray(b)).max(), 1e-300))
+
+
+@pytest.mark.parametrize("n,p,t,seed", [
+    (200, 1000, 1, 42),      # config C1 shape
+    (333, 1777, 3, 7),       # ragged: n, p not tile multiples; 3 traits
+    (129, 64, 1, 3),         # p < n (G rank deficient; λ keeps V SPD)
+    (64, 5000, 2, 5),        # single tile, many loci
+    (1000, 3000, 1, 11),     # several Cholesky panels
+])
+def test_gblup_matches_oracle(n, p, t, seed):
+    X = oracle.synth_genotypes(seed, n, p)
+    Y = oracle.synth_phenotypes(X, seed + 1, ntraits=t)
+    b_hat, y_pred, mu, q = gbm.gblup_arrays(X, Y, lambda_=1.0)
+    ref = oracle.gblup_fit(X, Y, 1.0)
+    assert q == ref["q"]
+    assert rel(y_pred, ref["y_pred"]) < TOL_TIGHT
+    assert rel(mu, ref["mu"]) < TOL_TIGHT
+    assert rel(b_hat, ref["b_hat"]) < TOL_CONTRACT
+    # predict-form identity (src/prediction.jl:228): b0 + X b reproduces the GEBVs
+    assert rel(oracle.predict_linear(X, b_hat), y_pred) < TOL_TIGHT
+
+
+def test_monomorphic_and_lambda():
+    n, p = 150, 400
+    X = oracle.synth_genotypes(99, n, p)
+    X[:, 5] = 0.0      # monomorphic (dropped, b = 0)
+    X[:, 17] = 0.5     # monomorphic
+    X[:, 399] = 1.0
+    Y = oracle.synth_phenotypes(X, 3)
+    for lam in (0.1, 1.0, 10.0):
+        b_hat, y_pred, mu, q = gbm.gblup_arrays(X, Y, lambda_=lam)
+        ref = oracle.gblup_fit(X, Y, lam)
+        assert q == ref["q"] == p - 3
+        assert b_hat[1 + 5, 0] == 0.0 and b_hat[1 + 17, 0] == 0.0 and b_hat[1 + 399, 0] == 0.0
+        assert rel(y_pred, ref["y_pred"]) < TOL_TIGHT
+        assert rel(b_hat, ref["b_hat"]) < TOL_CONTRACT
+
+
+def test_grm_and_colstats_match_oracle():
+    n, p = 257, 900
+    X = oracle.synth_genotypes(5, n, p)
+    X[:, 3] = 0.5
+    G, q = gbm.grm(X)
+    Gr, qr = oracle.grm(X)
+    assert q == qr
+    assert rel(G, Gr) < 1e-12
+    assert np.array_equal(G, G.T)
+    m, s, k, q2 = gbm.colstats(X)
+    mr, sr, kr = oracle.colstats(X)
+    assert q2 == qr and np.array_equal(k, kr)
+    assert rel(m, mr) < 1e-14 and rel(s[k], sr[kr]) < 1e-13
+
+
+def test_dosage_i8_path_equals_f64_path():
+    n, p, ploidy = 180, 700, 4
+    rng = np.random.default_rng(1)
+    D = np.asfortranarray(rng.integers(0, ploidy + 1, size=(n, p)).astype(np.int8))
+    X = D.astype(np.float64) / ploidy
+    Y = oracle.synth_phenotypes(X, 2, ntraits=2)
+    lib = gbm.load_library()
+    from gbm import _lib
+    Yf = np.asfortranarray(Y)
+    b_hat = np.zeros((p + 1, 2), order="F")
+    y_pred = np.zeros((n, 2), order="F")
+    mu = np.zeros(2)
+    q = np.zeros(1, dtype=np.int64)
+    rc = lib.gbm_gblup_fit_dosage_i8(_lib.ptr(D), n, p, n, ploidy, _lib.ptr(Yf), n, 2, 1.0, None, 0,
+                                     _lib.ptr(b_hat), _lib.ptr(y_pred), _lib.ptr(mu), _lib.ptr(q))
+    _lib.check(rc, "dosage")
+    b2, y2, mu2, q2 = gbm.gblup_arrays(X, Y, 1.0)
+    assert q[0] == q2
+    assert np.array_equal(y_pred, y2) and np.array_equal(b_hat, b2)
+
+
+def test_predict_gpu_matches_linear_predictor():
+    n, p = 300, 1200
+    X = oracle.synth_genotypes(21, n, p)
+    Y = oracle.synth_phenotypes(X, 4)
+    b_hat, y_pred, _, _ = gbm.gblup_arrays(X, Y)
+    names = [f"e{i}" for i in range(n)]
+    loci = [f"l{j}" for j in range(p)]
+    genomes = gbm.Genomes(names, ["pop"] * n, loci, X)
+    fit = gbm.Fit(n=n, l=p + 1, model="gblup", b_hat_labels=["intercept"] + loci, b_hat=b_hat[:, 0],
+                  entries=names, populations=["pop"] * n, y_true=Y[:, 0], y_pred=y_pred[:, 0])
+    out = gbm.predict(fit, genomes, np.arange(1, n + 1))
+    assert rel(out, y_pred[:, 0]) < TOL_TIGHT
+
+
+def test_errors_are_loud():
+    X = oracle.synth_genotypes(1, 50, 100)
+    with pytest.raises(gbm.ArgumentError):
+        gbm.gblup_arrays(X, np.full(50, np.nan))
+    with pytest.raises(gbm.GBMError):
+        gbm.gblup_arrays(X, np.ones(50))  # zero variance
+    with pytest.raises(gbm.GBMError):
+        gbm.gblup_arrays(np.zeros((50, 10)), np.arange(50.0))  # no polymorphic locus
+    with pytest.raises(gbm.ArgumentError):
+        gbm.gblup_arrays(X, np.arange(50.0), lambda_=0.0)
