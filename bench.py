@@ -1,0 +1,242 @@
+#!/usr/bin/env python3
+"""GRM + GBLUP benchmark (BASELINE.json metric: genotype-cells/s = n·p / wall time).
+
+Workload (config C2 of BASELINE.json, per GPU): GBLUP on n = 5 000 individuals × p = 50 000 loci,
+fp64, λ = 1, one trait. Genotypes are generated on the device by the counter-based hash of
+SURVEY.md §8d (bit-identical to the oracle's generator), so they are resident in HBM before the
+timed region. With N ranks (torchrun, one process per GPU) each rank owns a different block of
+50 000 loci (weak scaling over loci: p_total = 50 000·N); the partial GRMs are summed by an RCCL
+all-reduce over xGMI.
+
+A step = standardise → fp64-MFMA GRM → (all-reduce) → Cholesky GBLUP solve → marker effects →
+results (b, GEBVs, μ̂) copied to pinned host memory.
+
+Prints ONE JSON line on rank 0.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "genomicbreedingmodels.jl_amd"))
+
+PEAK_F64_TFLOPS = 78.6  # MI355X fp64 matrix peak (AMD datasheet)
+PEAK_HBM_GBS = 8000.0
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--n", type=int, default=5000)
+    ap.add_argument("--p", type=int, default=50000, help="loci per GPU")
+    ap.add_argument("--nrhs", type=int, default=1)
+    ap.add_argument("--lam", type=float, default=1.0)
+    ap.add_argument("--seed", type=int, default=4242)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-sample-p", type=int, default=0, help="loci in the CPU baseline sample (0 = all)")
+    return ap.parse_args()
+
+
+def phenotypes(seed: int, n: int, p_total: int, nrhs: int) -> np.ndarray:
+    """y = Xβ + e on 1 % QTL loci (h² = 0.5), X regenerated on the host for the QTL columns only
+    with the same counter hash (identical on every rank)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O  # host-side genotype hash (numpy), used here only to synthesise y
+
+    rng = np.random.default_rng(seed + 1)
+    Y = np.empty((n, nrhs))
+    for t in range(nrhs):
+        nq = max(1, p_total // 100)
+        idx = np.sort(rng.choice(p_total, size=nq, replace=False))
+        beta = rng.standard_normal(nq)
+        g = np.zeros(n)
+        for j, b in zip(idx, beta):
+            g += O.synth_genotypes(seed, n, 1, j0=int(j))[:, 0] * b
+        e = rng.standard_normal(n) * np.sqrt(g.var(ddof=1))
+        Y[:, t] = g + e
+    return Y
+
+
+def cpu_baseline(args):
+    """The CPU oracle (numpy/OpenBLAS restatement, oracle/oracle.py) on the same workload
+    (rank 0, N = 1): GRM + GBLUP on n x p_sample, timed without data generation."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import ctypes
+
+    import oracle as O
+
+    try:
+        from threadpoolctl import threadpool_info
+        threads = max([d.get("num_threads", 1) for d in threadpool_info() if d.get("internal_api") == "openblas"] or [1])
+    except Exception:  # pragma: no cover
+        threads = len(os.sched_getaffinity(0))
+    n = args.n
+    p = args.cpu_sample_p or args.p
+    so = os.path.join(ROOT, "oracle", "build", "libgbm_oracle.so")
+    X = np.zeros((n, p), order="F")
+    if os.path.exists(so):
+        lib = ctypes.CDLL(so)
+        lib.gbm_ref_synth_matrix.argtypes = [ctypes.c_uint64, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64,
+                                             ctypes.c_void_p, ctypes.c_int64]
+        lib.gbm_ref_synth_matrix(args.seed, n, p, 0, X.ctypes.data, n)
+    else:
+        X = O.synth_genotypes(args.seed, n, p)
+    Y = phenotypes(args.seed, n, p, args.nrhs)
+    t0 = time.perf_counter()
+    O.gblup_fit(X, Y, args.lam)
+    dt = time.perf_counter() - t0
+    return {"value": n * p / dt, "unit": "genotype-cells/s", "cores": int(threads), "kind": "port",
+            "sample": f"numpy/OpenBLAS fp64 restatement (oracle/oracle.py gblup_fit) on n={n} x p={p}, 1 trait, "
+                      f"one full fit in {dt:.2f} s (standardise + GRM + Cholesky + marker effects; generation untimed)"}
+
+
+def load_pmc(n, p):
+    """HBM traffic per GRM launch from the committed rocprofv3 PMC summary, if one matches."""
+    path = os.path.join(ROOT, "profiles", "pmc_grm.json")
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        if d.get("n") == n and d.get("p") == p:
+            return d.get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        pass
+    return None
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    else:
+        torch.cuda.set_device(0)
+    dev = torch.cuda.current_device()
+
+    import gbm
+    from gbm.sharded import HipShardStages, LocalComm, TorchComm, sharded_gblup_step
+
+    comm = TorchComm() if world > 1 else LocalComm()
+    n, p_local = args.n, args.p
+    p_total = p_local * world
+    j0 = rank * p_local
+    st = HipShardStages(n, p_local, nrhs=args.nrhs, lambda_=args.lam, device=dev)
+    st.generate(args.seed, j0)
+    st.load_phenotypes(phenotypes(args.seed, n, p_total, args.nrhs))
+    torch.cuda.synchronize()
+
+    labels = ["begin", "standardize", "grm_syrk", "grm_reduce", "allreduce", "solve", "effects", "download"]
+    recs = []
+
+    def make_marks():
+        evs = {}
+
+        def mark(label):
+            e = torch.cuda.Event(enable_timing=True)
+            e.record()
+            evs[label] = e
+        return evs, mark
+
+    for _ in range(args.warmup):
+        sharded_gblup_step(st, comm)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    out = None
+    for _ in range(args.steps):
+        evs, mark = make_marks()
+        out = sharded_gblup_step(st, comm, events=mark)
+        recs.append(evs)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    stage_ms = {}
+    for a, b in zip(labels[:-1], labels[1:]):
+        stage_ms[b] = float(np.mean([r[a].elapsed_time(r[b]) for r in recs]))
+    syrk_ms = stage_ms["grm_syrk"]
+    ms_per_step = elapsed * 1000.0 / args.steps
+    value = n * p_total / (ms_per_step / 1000.0)
+
+    # sanity: finite GEBVs, b0 assembled
+    assert np.all(np.isfinite(out["y_pred"])) and np.all(np.isfinite(out["B"]))
+
+    if rank != 0:
+        if world > 1:
+            dist.destroy_process_group()
+        return
+
+    grm_flops = float(n) * (n + 1) * p_local           # unique triangle of the rank-p update
+    chol_flops = st.npad ** 3 / 3.0
+    solve_flops = 8.0 * st.npad ** 2 * (1 + args.nrhs) + 2.0 * n * p_local * args.nrhs
+    achieved = grm_flops / (syrk_ms / 1000.0) / 1e12
+    traffic = load_pmc(n, p_local)
+    e2e_frac = (grm_flops + chol_flops + solve_flops) / (ms_per_step / 1000.0) / (PEAK_F64_TFLOPS * 1e12)
+
+    rec = {
+        "metric": "GRM+GBLUP genotype-cells/s (n x p)",
+        "value": value,
+        "unit": "genotype-cells/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": ms_per_step,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic: counter-hash genotypes (MAF U(0.05,0.5), dosage Binomial(2,f), X=d/2) generated in HBM; "
+                "1% QTL phenotype, h2=0.5",
+        "config": {
+            "workload": f"C2 GBLUP n={n} x p={p_local} loci per GPU (BASELINE.json configs[1]); "
+                        f"p_total={p_total} over {world} GPU(s), loci-sharded, partial GRMs all-reduced",
+            "n": n, "p_per_gpu": p_local, "p_total": p_total, "traits": args.nrhs, "lambda": args.lam,
+            "grm_slices": int(st.lib.gbm_dev_grm_slices(n, p_local)),
+            "parallelism": f"loci-shard x{world}",
+        },
+        "roofline": {
+            "bound": "mfma",
+            "kernel": "grm_syrk_kernel (fp64 v_mfma_f64_16x16x4_f64)",
+            "achieved": achieved,
+            "peak": PEAK_F64_TFLOPS,
+            "unit": "TFLOP/s",
+            "frac": achieved / PEAK_F64_TFLOPS,
+            "traffic": traffic,
+            "flops_per_launch": grm_flops,
+            "ms_per_launch": syrk_ms,
+        },
+        "stage_ms": stage_ms,
+        "e2e_fp64_frac_of_peak": e2e_frac,
+    }
+    if world == 1 and not args.no_cpu_baseline:
+        rec["cpu_baseline"] = cpu_baseline(args)
+    else:
+        rec["cpu_baseline"] = None
+    print(json.dumps(rec), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

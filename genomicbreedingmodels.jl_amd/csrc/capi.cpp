@@ -136,7 +136,8 @@ int prepare_shard(const Problem& pr, Shard& sh) {
     GBM_TRY(gbm_dev_expand_dosage_i8((const int8_t*)sh.D8.p, n, n, pl, pr.ploidy, (double*)sh.Xt.p, npad, s));
   }
   GBM_HIP_TRY(hipMemsetAsync(sh.q.p, 0, 8, s));
-  GBM_TRY(gbm_dev_standardize((double*)sh.Xt.p, npad, pl, n, (double*)sh.mean.p, (double*)sh.sd.p,
+  GBM_TRY(gbm_dev_standardize((const double*)sh.Xt.p, npad, pl, n, (double*)sh.Xt.p, npad, (double*)sh.mean.p,
+                              (double*)sh.sd.p,
                               (int32_t*)sh.keep.p, (int64_t*)sh.q.p, s));
   GBM_HIP_TRY(hipMemcpyAsync(&sh.q_host, sh.q.p, 8, hipMemcpyDeviceToHost, s));
   GBM_HIP_TRY(hipStreamSynchronize(s));
@@ -248,7 +249,7 @@ int run_fit(const Problem& pr, const double* Y, int64_t ldy, int64_t nrhs, doubl
     GBM_HIP_TRY(hipMemcpy2DAsync(sh.Y.p, npad * 8, Y, ldy * 8, n * 8, nrhs, hipMemcpyHostToDevice, s));
     // every shard solves the (identical) n x n system redundantly: a is then local to each
     // shard's marker back-solve with no broadcast
-    GBM_TRY(gbm_dev_gblup_solve((double*)sh.G.p, gdim, n, inv_q, lambda, (const double*)sh.Y.p, npad, nrhs,
+    GBM_TRY(gbm_dev_gblup_solve((double*)sh.G.p, gdim, n, inv_q, nullptr, lambda, (const double*)sh.Y.p, npad, nrhs,
                                 (double*)sh.A.p, (double*)sh.gebv.p, npad, (double*)sh.mu.p, (int32_t*)sh.info.p,
                                 sh.wss.p, wss, s));
     int32_t info = 0;
@@ -258,7 +259,7 @@ int run_fit(const Problem& pr, const double* Y, int64_t ldy, int64_t nrhs, doubl
       return fail(GBM_E_NOTPD, "G/q + lambda*I is not positive definite (pivot " + std::to_string(info) +
                                    "); check for non-finite genotypes");
     GBM_TRY(gbm_dev_marker_effects((const double*)sh.Xt.p, npad, sh.p, n, (const double*)sh.A.p, npad, nrhs, inv_q,
-                                   (const double*)sh.mean.p, (const double*)sh.sd.p, (const int32_t*)sh.keep.p,
+                                   nullptr, (const double*)sh.mean.p, (const double*)sh.sd.p, (const int32_t*)sh.keep.p,
                                    (double*)sh.B.p, sh.p, (double*)sh.msum.p, s));
     GBM_HIP_TRY(hipMemcpy2DAsync(b_hat_out + 1 + sh.j0, (p + 1) * 8, sh.B.p, sh.p * 8, sh.p * 8, nrhs,
                                  hipMemcpyDeviceToHost, s));

@@ -20,10 +20,12 @@ constexpr int NB = kCholNB;  // 64
 
 // ---- V = G/q + λI, padding = identity, bordered RHS rows ------------------------------
 __global__ void __launch_bounds__(256) prepare_v_kernel(double* __restrict__ G, int64_t ld, int64_t n,
-                                                        int64_t npad, int64_t gdim, double inv_q, double lambda,
+                                                        int64_t npad, int64_t gdim, double inv_q,
+                                                        const int64_t* __restrict__ q_dev, double lambda,
                                                         const double* __restrict__ Y, int64_t ldy, int64_t nrhs,
                                                         int32_t* __restrict__ info) {
   const int64_t i = blockIdx.x;  // row
+  if (q_dev) inv_q = 1.0 / (double)(*q_dev);
   if (i == 0 && threadIdx.x == 0) *info = 0;
   double* row = G + i * ld;
   if (i < npad) {
@@ -272,13 +274,14 @@ extern "C" int64_t gbm_dev_solve_workspace(int64_t n, int64_t nrhs) {
   return npad_of(n) * NB * (int64_t)sizeof(double);
 }
 
-extern "C" int gbm_dev_gblup_solve(double* G, int64_t ldg, int64_t n, double inv_q, double lambda,
+extern "C" int gbm_dev_gblup_solve(double* G, int64_t ldg, int64_t n, double inv_q, const int64_t* q_dev,
+                                   double lambda,
                                    const double* Y, int64_t ldy, int64_t nrhs, double* A_out, double* gebv,
                                    int64_t lda, double* mu, int32_t* info, void* workspace, int64_t ws_bytes,
                                    void* stream) {
   const int64_t npad = npad_of(n), gdim = gdim_of(n);
   if (!G || !Y || !A_out || !gebv || !mu || !info || n < 1 || ldg < gdim || ldy < n || lda < npad || nrhs < 1 ||
-      nrhs > MAXRHS || !(lambda > 0.0) || !(inv_q > 0.0))
+      nrhs > MAXRHS || !(lambda > 0.0) || !(q_dev || inv_q > 0.0))
     return fail(GBM_E_ARG, "gbm_dev_gblup_solve: bad arguments (need ldg >= gdim(n), lda >= npad(n), "
                            "1 <= nrhs <= 63, lambda > 0, inv_q > 0)");
   if ((ldg & 1) || ((uintptr_t)G & 15)) return fail(GBM_E_ARG, "gbm_dev_gblup_solve: G must be 16-byte aligned, even ld");
@@ -286,7 +289,7 @@ extern "C" int gbm_dev_gblup_solve(double* G, int64_t ldg, int64_t n, double inv
     return fail(GBM_E_ARG, "gbm_dev_gblup_solve: workspace too small (see gbm_dev_solve_workspace)");
   double* Ld = (double*)workspace;
   hipStream_t s = (hipStream_t)stream;
-  prepare_v_kernel<<<(unsigned)gdim, 256, 0, s>>>(G, ldg, n, npad, gdim, inv_q, lambda, Y, ldy, nrhs, info);
+  prepare_v_kernel<<<(unsigned)gdim, 256, 0, s>>>(G, ldg, n, npad, gdim, inv_q, q_dev, lambda, Y, ldy, nrhs, info);
   GBM_LAUNCH_CHECK();
   const int64_t nb = npad / NB;
   for (int64_t kb = 0; kb < nb; kb++) {

@@ -11,6 +11,7 @@ namespace gbm {
 __global__ void __launch_bounds__(256) marker_effects_kernel(const double* __restrict__ Zt, int64_t ldz, int64_t p,
                                                              int64_t n, const double* __restrict__ A, int64_t lda,
                                                              int64_t nrhs, double inv_q,
+                                                             const int64_t* __restrict__ q_dev,
                                                              const double* __restrict__ sd,
                                                              const int32_t* __restrict__ keep,
                                                              double* __restrict__ B, int64_t ldb) {
@@ -18,6 +19,7 @@ __global__ void __launch_bounds__(256) marker_effects_kernel(const double* __res
   const int64_t wave_g = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   const int64_t nwaves = (int64_t)gridDim.x * 4;
   const int64_t n2 = (n + 1) & ~(int64_t)1;  // ldz is even and the padding is zero
+  if (q_dev) inv_q = 1.0 / (double)(*q_dev);
   for (int64_t j = wave_g; j < p; j += nwaves) {
     const double* z = Zt + j * ldz;
     const bool kp = keep[j] != 0;
@@ -123,14 +125,16 @@ int64_t predict_chunks(int64_t n, int64_t p) {
 using namespace gbm;
 
 extern "C" int gbm_dev_marker_effects(const double* Zt, int64_t ldz, int64_t p, int64_t n, const double* A,
-                                      int64_t lda, int64_t nrhs, double inv_q, const double* mean, const double* sd,
+                                      int64_t lda, int64_t nrhs, double inv_q, const int64_t* q_dev,
+                                      const double* mean, const double* sd,
                                       const int32_t* keep, double* B, int64_t ldb, double* msum, void* stream) {
   if (!Zt || !A || !mean || !sd || !keep || !B || !msum || p < 1 || n < 1 || ldz < n || (ldz & 1) ||
-      lda < ldz || (lda & 1) || nrhs < 1 || ldb < p || !(inv_q > 0.0))
+      lda < ldz || (lda & 1) || nrhs < 1 || ldb < p || !(q_dev || inv_q > 0.0))
     return fail(GBM_E_ARG, "gbm_dev_marker_effects: bad arguments (need ldz >= n even, lda >= ldz even, ldb >= p)");
   hipStream_t s = (hipStream_t)stream;
   const int64_t blocks = (p + 3) / 4 < 8192 ? (p + 3) / 4 : 8192;
-  marker_effects_kernel<<<(unsigned)blocks, 256, 0, s>>>(Zt, ldz, p, n, A, lda, nrhs, inv_q, sd, keep, B, ldb);
+  marker_effects_kernel<<<(unsigned)blocks, 256, 0, s>>>(Zt, ldz, p, n, A, lda, nrhs, inv_q, q_dev, sd, keep, B,
+                                                          ldb);
   GBM_LAUNCH_CHECK();
   weighted_sum_kernel<<<(unsigned)nrhs, 1024, 0, s>>>(mean, B, ldb, p, msum);
   GBM_LAUNCH_CHECK();

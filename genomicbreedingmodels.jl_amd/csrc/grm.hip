@@ -190,12 +190,19 @@ int64_t grm_workspace_bytes(int64_t n, int64_t p) {
   return S > 1 ? (int64_t)S * ntiles * BT * BT * (int64_t)sizeof(double) : 0;
 }
 
-int launch_grm(const double* Zt, int64_t ldz, int64_t p, int64_t n, double* G, int64_t ldg, void* ws,
-               int64_t ws_bytes, hipStream_t s) {
+static int check_grm_args(const double* Zt, int64_t ldz, int64_t p, int64_t n, double* G, int64_t ldg) {
   const int64_t npad = npad_of(n);
   if (!Zt || !G || p < 1 || n < 1 || ldz < npad || ldg < npad || (ldz & 1))
     return fail(GBM_E_ARG, "gbm_dev_grm: bad arguments (need ldz, ldg >= npad(n), even ldz)");
   if (((uintptr_t)Zt & 15) != 0) return fail(GBM_E_ARG, "gbm_dev_grm: Zt must be 16-byte aligned");
+  return GBM_OK;
+}
+
+// stage 1: the MFMA SYRK (writes G directly, or per-slice slabs into ws when split over loci)
+int launch_grm_syrk(const double* Zt, int64_t ldz, int64_t p, int64_t n, double* G, int64_t ldg, void* ws,
+                    int64_t ws_bytes, hipStream_t s) {
+  int rc = check_grm_args(Zt, ldz, p, n, G, ldg);
+  if (rc != GBM_OK) return rc;
   int64_t ntiles, sps;
   int S;
   plan(n, p, ntiles, S, sps);
@@ -205,11 +212,26 @@ int launch_grm(const double* Zt, int64_t ldz, int64_t p, int64_t n, double* G, i
                                std::to_string(need) + ")");
   grm_syrk_kernel<<<(unsigned)(ntiles * S), 256, 0, s>>>(Zt, ldz, p, G, ldg, (double*)ws, ntiles, S, sps);
   GBM_LAUNCH_CHECK();
+  return GBM_OK;
+}
+
+// stage 2: sum the slabs (no-op when the plan did not split over loci)
+int launch_grm_reduce(int64_t n, int64_t p, double* G, int64_t ldg, const void* ws, hipStream_t s) {
+  int64_t ntiles, sps;
+  int S;
+  plan(n, p, ntiles, S, sps);
   if (S > 1) {
     grm_slab_reduce_kernel<<<(unsigned)ntiles, 256, 0, s>>>((const double*)ws, ntiles, S, G, ldg);
     GBM_LAUNCH_CHECK();
   }
   return GBM_OK;
+}
+
+int launch_grm(const double* Zt, int64_t ldz, int64_t p, int64_t n, double* G, int64_t ldg, void* ws,
+               int64_t ws_bytes, hipStream_t s) {
+  int rc = launch_grm_syrk(Zt, ldz, p, n, G, ldg, ws, ws_bytes, s);
+  if (rc != GBM_OK) return rc;
+  return launch_grm_reduce(n, p, G, ldg, ws, s);
 }
 
 }  // namespace gbm
@@ -219,6 +241,23 @@ extern "C" int64_t gbm_dev_grm_workspace(int64_t n, int64_t p) { return gbm::grm
 extern "C" int gbm_dev_grm(const double* Zt, int64_t ldz, int64_t p, int64_t n, double* G, int64_t ldg,
                            void* workspace, int64_t ws_bytes, void* stream) {
   return gbm::launch_grm(Zt, ldz, p, n, G, ldg, workspace, ws_bytes, (hipStream_t)stream);
+}
+
+extern "C" int gbm_dev_grm_syrk(const double* Zt, int64_t ldz, int64_t p, int64_t n, double* G, int64_t ldg,
+                                void* workspace, int64_t ws_bytes, void* stream) {
+  return gbm::launch_grm_syrk(Zt, ldz, p, n, G, ldg, workspace, ws_bytes, (hipStream_t)stream);
+}
+
+extern "C" int gbm_dev_grm_reduce(int64_t n, int64_t p, double* G, int64_t ldg, const void* workspace, void* stream) {
+  if (!G || n < 1 || p < 1 || ldg < gbm::npad_of(n)) return gbm::fail(GBM_E_ARG, "gbm_dev_grm_reduce: bad arguments");
+  return gbm::launch_grm_reduce(n, p, G, ldg, workspace, (hipStream_t)stream);
+}
+
+extern "C" int gbm_dev_grm_slices(int64_t n, int64_t p) {
+  int64_t ntiles, sps;
+  int S;
+  gbm::plan(n, p, ntiles, S, sps);
+  return S;
 }
 
 namespace gbm {

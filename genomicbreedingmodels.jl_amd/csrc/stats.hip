@@ -64,14 +64,16 @@ __device__ __forceinline__ double block_sum(double v, double* red) {
 // One workgroup per locus row (grid-strided). NPT = values cached in registers per thread
 // (0 = generic path re-reading the row from L2/MALL).
 template <int BS, int NPT>
-__global__ void __launch_bounds__(BS) standardize_kernel(double* __restrict__ Xt, int64_t ldx, int64_t p,
-                                                         int64_t n, double* __restrict__ mean,
+__global__ void __launch_bounds__(BS) standardize_kernel(const double* Xt, int64_t ldx, int64_t p,
+                                                         int64_t n, double* Zt, int64_t ldz,
+                                                         double* __restrict__ mean,
                                                          double* __restrict__ sd, int32_t* __restrict__ keep,
                                                          unsigned long long* __restrict__ q_dev) {
   __shared__ double red[BS / 64];
   unsigned long long kept_local = 0;
   for (int64_t j = blockIdx.x; j < p; j += gridDim.x) {
-    double* row = Xt + j * ldx;
+    const double* row = Xt + j * ldx;
+    double* zrow = Zt + j * ldz;  // may alias row (in place)
     double m, v;
     if constexpr (NPT > 0) {
       double x[NPT];
@@ -96,9 +98,9 @@ __global__ void __launch_bounds__(BS) standardize_kernel(double* __restrict__ Xt
 #pragma unroll
       for (int k = 0; k < NPT; k++) {
         const int64_t i = (int64_t)k * BS + threadIdx.x;
-        if (i < ldx) row[i] = (kp && i < n) ? (x[k] - m) * r : 0.0;
+        if (i < ldz) zrow[i] = (kp && i < n) ? (x[k] - m) * r : 0.0;
       }
-      for (int64_t i = (int64_t)NPT * BS + threadIdx.x; i < ldx; i += BS) row[i] = 0.0;
+      for (int64_t i = (int64_t)NPT * BS + threadIdx.x; i < ldz; i += BS) zrow[i] = 0.0;
       if (threadIdx.x == 0) {
         mean[j] = m;
         sd[j] = v;
@@ -117,7 +119,7 @@ __global__ void __launch_bounds__(BS) standardize_kernel(double* __restrict__ Xt
       v = n > 1 ? sqrt(block_sum<BS>(ss, red) / (double)(n - 1)) : __builtin_nan("");
       const bool kp = (v > 2.220446049250313e-16) && isfinite(v);
       const double r = kp ? 1.0 / v : 0.0;
-      for (int64_t i = threadIdx.x; i < ldx; i += BS) row[i] = (kp && i < n) ? (row[i] - m) * r : 0.0;
+      for (int64_t i = threadIdx.x; i < ldz; i += BS) zrow[i] = (kp && i < n) ? (row[i] - m) * r : 0.0;
       if (threadIdx.x == 0) {
         mean[j] = m;
         sd[j] = v;
@@ -158,24 +160,25 @@ extern "C" int gbm_dev_expand_dosage_i8(const int8_t* D, int64_t ldd, int64_t n,
   return GBM_OK;
 }
 
-extern "C" int gbm_dev_standardize(double* Xt, int64_t ldx, int64_t p, int64_t n, double* mean, double* sd,
-                                   int32_t* keep, int64_t* q_dev, void* stream) {
-  if (!Xt || !mean || !sd || !keep || !q_dev || p < 0 || n < 1 || ldx < n)
+extern "C" int gbm_dev_standardize(const double* Xt, int64_t ldx, int64_t p, int64_t n, double* Zt, int64_t ldz,
+                                   double* mean, double* sd, int32_t* keep, int64_t* q_dev, void* stream) {
+  if (!Xt || !Zt || !mean || !sd || !keep || !q_dev || p < 0 || n < 1 || ldx < n || ldz < n ||
+      ((const double*)Zt == Xt && ldz != ldx))
     return fail(GBM_E_ARG, "gbm_dev_standardize: bad arguments");
   if (p == 0) return GBM_OK;
   hipStream_t s = (hipStream_t)stream;
   const unsigned grid = (unsigned)(p < 256 * 16 ? p : 256 * 16);
   auto q = reinterpret_cast<unsigned long long*>(q_dev);
   if (n <= 256 * 4)
-    standardize_kernel<256, 4><<<grid, 256, 0, s>>>(Xt, ldx, p, n, mean, sd, keep, q);
+    standardize_kernel<256, 4><<<grid, 256, 0, s>>>(Xt, ldx, p, n, Zt, ldz, mean, sd, keep, q);
   else if (n <= 256 * 8)
-    standardize_kernel<256, 8><<<grid, 256, 0, s>>>(Xt, ldx, p, n, mean, sd, keep, q);
+    standardize_kernel<256, 8><<<grid, 256, 0, s>>>(Xt, ldx, p, n, Zt, ldz, mean, sd, keep, q);
   else if (n <= 256 * 16)
-    standardize_kernel<256, 16><<<grid, 256, 0, s>>>(Xt, ldx, p, n, mean, sd, keep, q);
+    standardize_kernel<256, 16><<<grid, 256, 0, s>>>(Xt, ldx, p, n, Zt, ldz, mean, sd, keep, q);
   else if (n <= 256 * 32)
-    standardize_kernel<256, 32><<<grid, 256, 0, s>>>(Xt, ldx, p, n, mean, sd, keep, q);
+    standardize_kernel<256, 32><<<grid, 256, 0, s>>>(Xt, ldx, p, n, Zt, ldz, mean, sd, keep, q);
   else
-    standardize_kernel<256, 0><<<grid, 256, 0, s>>>(Xt, ldx, p, n, mean, sd, keep, q);
+    standardize_kernel<256, 0><<<grid, 256, 0, s>>>(Xt, ldx, p, n, Zt, ldz, mean, sd, keep, q);
   GBM_LAUNCH_CHECK();
   return GBM_OK;
 }

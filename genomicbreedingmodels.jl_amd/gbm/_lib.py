@@ -28,6 +28,7 @@ EXPORTS = (
     "gbm_gblup_fit", "gbm_gblup_fit_dosage_i8", "gbm_grm", "gbm_colstats", "gbm_predict",
     "gbm_dev_npad", "gbm_dev_gdim", "gbm_dev_grm_workspace", "gbm_dev_solve_workspace",
     "gbm_dev_synth_genotypes", "gbm_dev_expand_dosage_i8", "gbm_dev_standardize", "gbm_dev_grm",
+    "gbm_dev_grm_syrk", "gbm_dev_grm_reduce", "gbm_dev_grm_slices",
     "gbm_dev_gblup_solve", "gbm_dev_marker_effects",
 )
 
@@ -78,14 +79,33 @@ def _declare(lib):
     lib.gbm_dev_expand_dosage_i8.restype = I32
     lib.gbm_dev_expand_dosage_i8.argtypes = [P, I64, I64, I64, I32, P, I64, P]
     lib.gbm_dev_standardize.restype = I32
-    lib.gbm_dev_standardize.argtypes = [P, I64, I64, I64, P, P, P, P, P]
-    lib.gbm_dev_grm.restype = I32
-    lib.gbm_dev_grm.argtypes = [P, I64, I64, I64, P, I64, P, I64, P]
+    lib.gbm_dev_standardize.argtypes = [P, I64, I64, I64, P, I64, P, P, P, P, P]
+    for f in ("gbm_dev_grm", "gbm_dev_grm_syrk"):
+        getattr(lib, f).restype = I32
+        getattr(lib, f).argtypes = [P, I64, I64, I64, P, I64, P, I64, P]
+    lib.gbm_dev_grm_reduce.restype = I32
+    lib.gbm_dev_grm_reduce.argtypes = [I64, I64, P, I64, P, P]
+    lib.gbm_dev_grm_slices.restype = I32
+    lib.gbm_dev_grm_slices.argtypes = [I64, I64]
     lib.gbm_dev_gblup_solve.restype = I32
-    lib.gbm_dev_gblup_solve.argtypes = [P, I64, I64, D, D, P, I64, I64, P, P, I64, P, P, P, I64, P]
+    lib.gbm_dev_gblup_solve.argtypes = [P, I64, I64, D, P, D, P, I64, I64, P, P, I64, P, P, P, I64, P]
     lib.gbm_dev_marker_effects.restype = I32
-    lib.gbm_dev_marker_effects.argtypes = [P, I64, I64, I64, P, I64, I64, D, P, P, P, P, I64, P, P]
+    lib.gbm_dev_marker_effects.argtypes = [P, I64, I64, I64, P, I64, I64, D, P, P, P, P, P, I64, P, P]
     return lib
+
+
+def _bind_runtime_first():
+    """One HIP runtime per process. PyTorch-ROCm bundles its own libamdhip64 (soname
+    libamdhip64.so.7) and librccl (librccl.so.1); if torch is importable we load it first so
+    that libgbm's NEEDED entries resolve to the already-loaded copies instead of mapping a
+    second HIP/HSA runtime from /opt/rocm (two runtimes in one process cannot both own the GPU).
+    Set GBM_NO_TORCH=1 to skip this in torch-free processes."""
+    if os.environ.get("GBM_NO_TORCH") == "1":
+        return
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        return
 
 
 def load():
@@ -97,6 +117,7 @@ def load():
                 raise ImportError(
                     f"libgbm.so not found at {LIB_PATH}: build it with `python -c 'import __graft_entry__ as g; g.build()'`"
                     " (the GBLUP path has no CPU fallback)")
+            _bind_runtime_first()
             _lib = _declare(ctypes.CDLL(LIB_PATH))
             v = _lib.gbm_version()
             if v != 100:

@@ -145,37 +145,49 @@ int gbm_dev_synth_genotypes(double* Xt, int64_t ldx, int64_t p, int64_t n, uint6
 int gbm_dev_expand_dosage_i8(const int8_t* D, int64_t ldd, int64_t n, int64_t p, int ploidy,
                              double* Xt, int64_t ldx, void* stream);
 
-/* In place: Xt row j <- (x_j − m_j)/s_j for kept loci, 0 for dropped ones and for the
- * padding columns [n, ldx). Writes mean/sd (p each), keep (p, int32) and atomically adds
- * the kept count into *q_dev (caller zeroes it). src/gwas.jl:112-115,127-130. */
-int gbm_dev_standardize(double* Xt, int64_t ldx, int64_t p, int64_t n,
+/* Zt row j <- (x_j − m_j)/s_j for kept loci, 0 for dropped ones and for the padding columns
+ * [n, ldz). Zt may be Xt itself (in place, ldz == ldx). Writes mean/sd (p each), keep (p, int32)
+ * and atomically adds the kept count into *q_dev (caller zeroes it). Replaces the column std,
+ * monomorphic filter and standardisation of reference src/gwas.jl:112-115,127-130. */
+int gbm_dev_standardize(const double* Xt, int64_t ldx, int64_t p, int64_t n, double* Zt, int64_t ldz,
                         double* mean, double* sd, int32_t* keep, int64_t* q_dev, void* stream);
 
-/* G[0:npad, 0:npad] (lower triangle and diagonal tiles) = Σ_j z_j z_jᵀ over the p locus rows
- * of Zt (unscaled; the all-reduce of multi-GPU shards happens on this). fp64 MFMA SYRK. */
+/* G[0:npad, 0:npad] (lower-triangular 128x128 tiles, diagonal tiles in full) = Σ_j z_j z_jᵀ over
+ * the p locus rows of Zt (unscaled: the RCCL all-reduce of multi-GPU shards sums this).
+ * fp64 MFMA SYRK; = gbm_dev_grm_syrk followed by gbm_dev_grm_reduce. Replaces the GRM product
+ * of GenomicBreedingCore.grmsimple (called at reference src/gwas.jl:124). */
 int gbm_dev_grm(const double* Zt, int64_t ldz, int64_t p, int64_t n, double* G, int64_t ldg,
                 void* workspace, int64_t ws_bytes, void* stream);
+/* The two launches of gbm_dev_grm, separately (so a caller can time the SYRK kernel alone).
+ * When gbm_dev_grm_slices(n, p) == 1 the SYRK writes G directly and the reduce is a no-op. */
+int gbm_dev_grm_syrk(const double* Zt, int64_t ldz, int64_t p, int64_t n, double* G, int64_t ldg,
+                     void* workspace, int64_t ws_bytes, void* stream);
+int gbm_dev_grm_reduce(int64_t n, int64_t p, double* G, int64_t ldg, const void* workspace, void* stream);
+/* Number of loci slices (split-K) the GRM plan uses for (n, p) on the current device. */
+int gbm_dev_grm_slices(int64_t n, int64_t p);
 
 /*
  * Solve the GBLUP system on G (as left by gbm_dev_grm, summed over shards):
- *   V = G·inv_q + λI ; LLᵀ = V (blocked fp64 Cholesky, in place) ; μ̂, a = V⁻¹(y − 1μ̂),
- *   gebv = μ̂ + (y − 1μ̂) − λa.
+ *   V = G/q + λI ; LLᵀ = V (blocked fp64 Cholesky, in place) ; μ̂ = 1ᵀV⁻¹y/1ᵀV⁻¹1,
+ *   a = V⁻¹(y − 1μ̂), gebv = μ̂ + (y − 1μ̂) − λa  (reference src/gwas.jl:462-472,591-597).
+ *   inv_q / q_dev  1/q given on the host, or (q_dev != NULL) read on the device from *q_dev
  *   Y      nrhs x ldy row-major (trait t's n phenotypes contiguous), 1 <= nrhs <= 63
  *   A_out  nrhs x lda row-major: a vectors (lda >= npad; zero in the padding)
  *   gebv   nrhs x lda row-major; mu nrhs; info (device int32): 0 or the 1-based failing pivot.
+ *   workspace  >= gbm_dev_solve_workspace(n, nrhs) bytes.
  */
-int gbm_dev_gblup_solve(double* G, int64_t ldg, int64_t n, double inv_q, double lambda,
+int gbm_dev_gblup_solve(double* G, int64_t ldg, int64_t n, double inv_q, const int64_t* q_dev, double lambda,
                         const double* Y, int64_t ldy, int64_t nrhs,
                         double* A_out, double* gebv, int64_t lda, double* mu, int32_t* info,
                         void* workspace, int64_t ws_bytes, void* stream);
 
 /*
- * Marker effects on the standardised locus rows: B[t, j] = (Zt_j · a_t)·inv_q / sd_j for kept
+ * Marker effects on the standardised locus rows: B[t, j] = (Zt_j · a_t)/(q·sd_j) for kept
  * loci, 0 otherwise (B nrhs x ldb row-major), and msum[t] = Σ_j mean_j B[t, j] over this
- * shard (so that b0 = μ̂ − Σ_shards msum).
+ * shard (so that b0 = μ̂ − Σ_shards msum). q from inv_q or, if q_dev != NULL, from *q_dev.
  */
 int gbm_dev_marker_effects(const double* Zt, int64_t ldz, int64_t p, int64_t n,
-                           const double* A, int64_t lda, int64_t nrhs, double inv_q,
+                           const double* A, int64_t lda, int64_t nrhs, double inv_q, const int64_t* q_dev,
                            const double* mean, const double* sd, const int32_t* keep,
                            double* B, int64_t ldb, double* msum, void* stream);
 

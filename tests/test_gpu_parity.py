@@ -115,3 +115,27 @@ def test_errors_are_loud():
         gbm.gblup_arrays(np.zeros((50, 10)), np.arange(50.0))  # no polymorphic locus
     with pytest.raises(gbm.ArgumentError):
         gbm.gblup_arrays(X, np.arange(50.0), lambda_=0.0)
+
+
+def test_sharded_stages_single_rank_match_oracle():
+    """The device-level stage API (as bench.py drives it) on one rank == the oracle, with the
+    on-device genotype generator bit-identical to the oracle's."""
+    import torch
+    from gbm.sharded import HipShardStages, LocalComm, assemble_b_hat, sharded_gblup_step
+
+    n, p, seed = 700, 2500, 77
+    st = HipShardStages(n, p, nrhs=2, lambda_=1.0, device=0)
+    st.generate(seed, 0)
+    X = oracle.synth_genotypes(seed, n, p)
+    Xd = st.X[:, :n].cpu().numpy().T
+    assert np.array_equal(Xd, X)  # bit-exact generator
+    assert torch.count_nonzero(st.X[:, n:]).item() == 0
+    Y = oracle.synth_phenotypes(X, 3, ntraits=2)
+    st.load_phenotypes(Y)
+    out = sharded_gblup_step(st, LocalComm())
+    out2 = sharded_gblup_step(st, LocalComm())  # steps are repeatable (X kept intact)
+    ref = oracle.gblup_fit(X, Y, 1.0)
+    assert rel(out["y_pred"], ref["y_pred"]) < TOL_TIGHT
+    assert np.array_equal(out["y_pred"], out2["y_pred"])
+    b_hat = assemble_b_hat(out["mu"], out["msum"], [out["B"]], p)
+    assert rel(b_hat, ref["b_hat"]) < TOL_CONTRACT
