@@ -1,0 +1,83 @@
+# gblup.jl — the reference-side binding a GenomicBreedingModels.jl maintainer adds to call
+# libgbm.so (MI355X GRM + GBLUP core). Drop into src/ next to linear.jl, `include("gblup.jl")`
+# after linear.jl (src/GenomicBreedingModels.jl:25-33), export `gblup` next to `ridge`
+# (src/GenomicBreedingModels.jl:46) and add "gblup" to `linear_models` in predict
+# (src/prediction.jl:225). Julia is not available in the build container, so this file is not
+# executed by the test suite; the Python mirror (gbm/linear.py) exercises the same C ABI with
+# the same argument layout (column-major Float64, Int64 dimensions).
+
+const LIBGBM = get(ENV, "GBM_LIBRARY", joinpath(@__DIR__, "..", "gbm", "libgbm.so"))
+
+function gbm_last_error()::String
+    unsafe_string(ccall((:gbm_last_error, LIBGBM), Cstring, ()))
+end
+
+function gbm_check(rc::Cint, what::String)
+    rc == 0 && return nothing
+    msg = what * ": " * gbm_last_error()
+    rc == -1 ? throw(ArgumentError(msg)) : throw(ErrorException(msg))
+end
+
+"""
+    gblup(; genomes, phenomes, idx_entries=nothing, idx_loci_alleles=nothing, idx_trait=1,
+          verbose=false, λ=1.0, devices=Int32[], model_label="gblup")::Fit
+
+GBLUP / RR-BLUP on V = G + λI with G = ZZᵀ/q, fitted on MI355X GPUs through libgbm.so.
+Same keywords and Fit assembly as `ridge` (src/linear.jl:162-239), so it runs unchanged under
+`cvbulk`/`cvmultithread!` (src/cross_validation.jl:170-177) and `predict`.
+"""
+function gblup(;
+    genomes::Genomes,
+    phenomes::Phenomes,
+    idx_entries::Union{Nothing,Vector{Int64}} = nothing,
+    idx_loci_alleles::Union{Nothing,Vector{Int64}} = nothing,
+    idx_trait::Int64 = 1,
+    verbose::Bool = false,
+    λ::Float64 = 1.0,
+    devices::Vector{Int32} = Int32[],
+    model_label::String = "gblup",
+)::Fit
+    X, y, entries, populations, loci_alleles = extractxyetc(
+        genomes,
+        phenomes,
+        idx_entries = idx_entries,
+        idx_loci_alleles = idx_loci_alleles,
+        idx_trait = idx_trait,
+        add_intercept = false,
+    )
+    n, p = size(X)
+    fit::Fit = Fit(n = n, l = p)
+    fit.model = model_label
+    fit.b_hat_labels = vcat(["intercept"], loci_alleles)
+    fit.trait = phenomes.traits[idx_trait]
+    fit.entries = entries
+    fit.populations = populations
+    fit.y_true = y
+    b_hat = zeros(p + 1)
+    y_pred = zeros(n)
+    mu = zeros(1)
+    q = zeros(Int64, 1)
+    GC.@preserve X y b_hat y_pred mu q devices begin
+        rc = ccall(
+            (:gbm_gblup_fit, LIBGBM),
+            Cint,
+            (Ptr{Float64}, Int64, Int64, Int64, Ptr{Float64}, Int64, Int64, Float64,
+             Ptr{Int32}, Cint, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Int64}),
+            X, n, p, stride(X, 2), y, n, 1, λ,
+            isempty(devices) ? C_NULL : pointer(devices), length(devices),
+            b_hat, y_pred, mu, q,
+        )
+        gbm_check(rc, "gblup")
+    end
+    fit.b_hat = b_hat
+    fit.y_pred = y_pred
+    fit.metrics = metrics(y, y_pred)
+    if verbose
+        println("gblup: n=$n p=$p q=$(q[1]) μ̂=$(mu[1]) λ=$λ")
+        println(fit.metrics)
+    end
+    if !checkdims(fit)
+        throw(ErrorException("Error fitting " * fit.model * "."))
+    end
+    fit
+end
