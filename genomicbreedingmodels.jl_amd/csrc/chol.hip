@@ -50,74 +50,150 @@ __global__ void __launch_bounds__(256) prepare_v_kernel(double* __restrict__ G, 
   }
 }
 
-// ---- panel: factor the 64x64 diagonal block (every workgroup, redundantly) and solve the
-//      64 panel rows of this workgroup: L21 = A21 L11⁻ᵀ. One wave per workgroup, lane = row.
-__global__ void __launch_bounds__(64) chol_panel_kernel(double* __restrict__ G, int64_t ld, int64_t k0,
-                                                        double* __restrict__ Ld, int32_t* __restrict__ info) {
-  __shared__ double colbuf[2][NB];
-  __shared__ double Ls[NB][NB + 1];
-  const int r = threadIdx.x;
-  double a[NB];
+// ---- panel: 256 threads, 64x64 diagonal block factored as four
+//      16-wide sub-panels whose trailing updates run on the matrix cores; the 64 panel rows of
+//      this workgroup are then solved against L11 block-column by block-column (MFMA for the
+//      off-diagonal part, a 16-column lane-per-row substitution for the diagonal part).
+//      The serial chain is 4 x (16 short columns) instead of 64 long ones.
+constexpr int PS = NB + 2;  // LDS pitch (66 doubles): MFMA fragment reads conflict-free
+
+__device__ __forceinline__ double rsqrt_nr(double a) {  // v_rsq_f64 + one Newton step
+  double y = __builtin_amdgcn_rsq(a);
+  const double h = 0.5 * a * y;
+  return y * fma(-h, y, 1.5);
+}
+__device__ __forceinline__ double rcp_nr(double a) {  // v_rcp_f64 + one Newton step
+  double y = __builtin_amdgcn_rcp(a);
+  const double e = fma(-a, y, 1.0);
+  return fma(y, e, y);
+}
+
+__device__ __forceinline__ double readlane_d(double x, int lane) {
+  union {
+    double d;
+    int i[2];
+  } u;
+  u.d = x;
+  u.i[0] = __builtin_amdgcn_readlane(u.i[0], lane);
+  u.i[1] = __builtin_amdgcn_readlane(u.i[1], lane);
+  return u.d;
+}
+
+// C(16x16 at (r0, c0) of dst) -= A(rows ra.., k) * B(rows rb.., k)ᵀ for k in [k0, k0 + 4*ksteps)
+__device__ __forceinline__ void mfma_tile_sub(double* dst, int r0, int c0, const double* A, int ra,
+                                              const double* B, int rb, int kbase, int ksteps, int lane) {
+  d4 acc = (d4){0.0, 0.0, 0.0, 0.0};
+  const int fr = lane >> 4, fc = lane & 15;
+  for (int ks = 0; ks < ksteps; ks++) {
+    const double a = A[(ra + fc) * PS + kbase + ks * 4 + fr];
+    const double b = B[(rb + fc) * PS + kbase + ks * 4 + fr];
+    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc, 0, 0, 0);
+  }
+#pragma unroll
+  for (int r = 0; r < 4; r++) dst[(r0 + fr + 4 * r) * PS + c0 + fc] -= acc[r];
+}
+
+__global__ void __launch_bounds__(256) chol_panel_blocked_kernel(double* __restrict__ G, int64_t ld, int64_t k0,
+                                                                 double* __restrict__ Ld,
+                                                                 int32_t* __restrict__ info) {
+  __shared__ __attribute__((aligned(16))) double L[NB * PS];
+  __shared__ __attribute__((aligned(16))) double X[NB * PS];
+  __shared__ double rinv[NB];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const bool diag_wg = blockIdx.x == 0;
   {
-    const double* src = G + (k0 + r) * ld + k0;
+    const int row = tid >> 2, quarter = tid & 3;
+    const double* sa = G + (k0 + row) * ld + k0 + quarter * 16;
+    const double* sx = G + (k0 + (int64_t)blockIdx.x * NB + row) * ld + k0 + quarter * 16;
 #pragma unroll
-    for (int t = 0; t < NB; t += 2) {
-      const double2 v = *reinterpret_cast<const double2*>(src + t);
-      a[t] = v.x;
-      a[t + 1] = v.y;
+    for (int e = 0; e < 16; e += 2) {
+      *reinterpret_cast<double2*>(&L[row * PS + quarter * 16 + e]) = *reinterpret_cast<const double2*>(sa + e);
+      if (!diag_wg)
+        *reinterpret_cast<double2*>(&X[row * PS + quarter * 16 + e]) = *reinterpret_cast<const double2*>(sx + e);
     }
-  }
-  bool bad = false;
-  int badcol = 0;
-#pragma unroll
-  for (int c = 0; c < NB; c++) {
-    colbuf[c & 1][r] = a[c];
-    __syncthreads();
-    const double piv = colbuf[c & 1][c];
-    if (!(piv > 0.0) || !isfinite(piv)) {
-      if (!bad) badcol = c;
-      bad = true;
-    }
-    const double d = sqrt(piv);
-    const double rd = 1.0 / d;
-    const double lr = (r > c) ? a[c] * rd : (r == c ? d : 0.0);
-    a[c] = lr;
-#pragma unroll
-    for (int s = c + 1; s < NB; s++) a[s] -= lr * (colbuf[c & 1][s] * rd);
-    __builtin_amdgcn_sched_barrier(0);  // keep each column's LDS reads local (register pressure)
-  }
-  // L11 into LDS (lower part; zeros above)
-#pragma unroll
-  for (int t = 0; t < NB; t++) Ls[r][t] = (t <= r) ? a[t] : 0.0;
-  if (blockIdx.x == 0) {
-    // The factored block goes to the scratch Ld (not in place): the other workgroups of this
-    // launch are still reading the unfactored block from G.
-    if (bad && r == 0) atomicCAS(info, 0, (int32_t)(k0 + badcol + 1));
-    double* dst = Ld + (k0 + r) * NB;
-#pragma unroll
-    for (int t = 0; t < NB; t += 2)
-      *reinterpret_cast<double2*>(dst + t) = make_double2(t <= r ? a[t] : 0.0, t + 1 <= r ? a[t + 1] : 0.0);
-    return;
   }
   __syncthreads();
-  // panel rows: x Lᵀ = a  ->  x_c = (a_c − Σ_{t<c} x_t L[c][t]) / L[c][c]
-  double* rowp = G + (k0 + (int64_t)blockIdx.x * NB + r) * ld + k0;
-  double x[NB];
+  bool bad = false;
+  int badcol = 0;
+  for (int kb = 0; kb < 4; kb++) {
+    const int o = kb * 16;
+    if (wave == 0) {
+      // (a+b) right-looking factorisation of the tall 16-column sub-panel L11[o:64, o:o+16]:
+      // lane r owns row o + r; rows o..o+15 form the diagonal sub-block, the rest are solved
+      // in the same 16-step loop (l_sc broadcast from lane s by v_readlane).
+      const int nrows = NB - o;
+      const int rr = o + (lane < nrows ? lane : 0);
+      double x[16];
 #pragma unroll
-  for (int t = 0; t < NB; t += 2) {
-    const double2 v = *reinterpret_cast<const double2*>(rowp + t);
-    x[t] = v.x;
-    x[t + 1] = v.y;
+      for (int t = 0; t < 16; t++) x[t] = L[rr * PS + o + t];
+#pragma unroll
+      for (int c = 0; c < 16; c++) {
+        const double piv = readlane_d(x[c], c);
+        if (!(piv > 0.0) || !isfinite(piv)) {
+          if (!bad) badcol = o + c;
+          bad = true;
+        }
+        const double lc = x[c] * rsqrt_nr(piv);  // lane c: piv/sqrt(piv) = L[c][c]
+#pragma unroll
+        for (int sidx = c + 1; sidx < 16; sidx++) x[sidx] -= lc * readlane_d(lc, sidx);
+        x[c] = lc;
+      }
+      if (lane < nrows) {
+#pragma unroll
+        for (int t = 0; t < 16; t++) L[rr * PS + o + t] = (lane < 16 && t > lane) ? 0.0 : x[t];
+      }
+      if (lane < 16) rinv[o + lane] = rcp_nr(x[lane & 15]);
+    }
+    __syncthreads();
+    // (c) trailing update of L11 (16x16 lower tiles of block rows/cols > kb) on the matrix cores
+    const int m = 3 - kb;
+    const int ntile = m * (m + 1) / 2;
+    for (int t = wave; t < ntile; t += 4) {
+      int ti = 0;
+      while ((ti + 1) * (ti + 2) / 2 <= t) ti++;
+      const int tj = t - ti * (ti + 1) / 2;
+      const int r0 = o + 16 + ti * 16, c0 = o + 16 + tj * 16;
+      mfma_tile_sub(L, r0, c0, L, r0, L, c0, o, 4, lane);
+    }
+    __syncthreads();
   }
+  if (diag_wg) {
+    if (bad && lane == 0 && wave == 0) atomicCAS(info, 0, (int32_t)(k0 + badcol + 1));
+    // factored block -> scratch Ld (other workgroups of this launch still read G's copy)
+    const int row = tid >> 2, quarter = tid & 3;
+    double* dst = Ld + (k0 + row) * NB + quarter * 16;
 #pragma unroll
-  for (int c = 0; c < NB; c++) {
-    x[c] = x[c] / Ls[c][c];
-#pragma unroll
-    for (int s = c + 1; s < NB; s++) x[s] -= x[c] * Ls[s][c];
-    __builtin_amdgcn_sched_barrier(0);
+    for (int e = 0; e < 16; e += 2)
+      *reinterpret_cast<double2*>(dst + e) = *reinterpret_cast<const double2*>(&L[row * PS + quarter * 16 + e]);
+    return;
   }
+  // panel rows: X L11ᵀ = A21, block column by block column
+  for (int cb = 0; cb < 4; cb++) {
+    const int o = cb * 16;
+    if (cb > 0) mfma_tile_sub(X, wave * 16, o, X, wave * 16, L, o, 0, cb * 4, lane);
+    __syncthreads();
+    if (wave == 0) {
+      double x[16];
 #pragma unroll
-  for (int t = 0; t < NB; t += 2) *reinterpret_cast<double2*>(rowp + t) = make_double2(x[t], x[t + 1]);
+      for (int t = 0; t < 16; t++) x[t] = X[lane * PS + o + t];
+#pragma unroll
+      for (int c = 0; c < 16; c++) {
+        x[c] *= rinv[o + c];
+#pragma unroll
+        for (int sidx = c + 1; sidx < 16; sidx++) x[sidx] -= x[c] * L[(o + sidx) * PS + o + c];
+      }
+#pragma unroll
+      for (int t = 0; t < 16; t++) X[lane * PS + o + t] = x[t];
+    }
+    __syncthreads();
+  }
+  {
+    const int row = tid >> 2, quarter = tid & 3;
+    double* dx = G + (k0 + (int64_t)blockIdx.x * NB + row) * ld + k0 + quarter * 16;
+#pragma unroll
+    for (int e = 0; e < 16; e += 2)
+      *reinterpret_cast<double2*>(dx + e) = *reinterpret_cast<const double2*>(&X[row * PS + quarter * 16 + e]);
+  }
 }
 
 // ---- trailing update: C -= L21 L21ᵀ on lower 64x64 tiles of rows/cols >= k1 (fp64 MFMA) ----
@@ -205,50 +281,85 @@ __global__ void __launch_bounds__(256) gls_mu_kernel(const double* __restrict__ 
 // its 256-column chunk of w[0, b*64):
 //   w_i -= Σ_r L[b*64 + r][i] a_b[r].
 constexpr int MAXRHS = 63;
+// ---- back substitution Lᵀ a = w over super-blocks of up to 4 x 64 rows --------------------
+// Launch per super-block [s0, s0 + 64*nsub), last to first. Every workgroup redundantly solves
+// the super-block's triangular system in LDS (4 diagonal 64-blocks from Ld + the in-block GEMV
+// updates read from G), workgroup 0 stores a, and each workgroup then applies the super-block's
+// contribution to its 256 columns of w[0, s0):  w_i -= Σ_r L[s0 + r][i] a_r.
+// Right-hand sides are processed in chunks of 8 (LDS: 4 x 32 KB L blocks + 16 KB of w).
+constexpr int SB = 4;   // 64-blocks per super-block
+constexpr int RC = 8;   // rhs per chunk
 __global__ void __launch_bounds__(256) back_subst_kernel(const double* __restrict__ G, int64_t ld,
-                                                         const double* __restrict__ Ld, int64_t b,
+                                                         const double* __restrict__ Ld, int64_t s0, int nsub,
                                                          double* __restrict__ W, double* __restrict__ A,
                                                          int64_t lda, int64_t nrhs) {
-  __shared__ double Lb[NB][NB + 1];
-  __shared__ double ab[MAXRHS][NB];
-  const int64_t r0 = b * NB;
-  for (int e = threadIdx.x; e < NB * NB; e += 256) {
-    const int rr = e / NB, cc = e % NB;
-    Lb[rr][cc] = Ld[(r0 + rr) * NB + cc];
+  __shared__ __attribute__((aligned(16))) double Lb[SB][NB][NB];
+  __shared__ double wl[RC][SB * NB];
+  __shared__ double rdiag[SB * NB];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int len = nsub * NB;
+  for (int e = tid * 2; e < len * NB; e += 512) {
+    const int rr = e / NB, cc = e % NB;  // row within the super-block, column within its block
+    *reinterpret_cast<double2*>(&Lb[rr / NB][rr % NB][cc]) =
+        *reinterpret_cast<const double2*>(Ld + (s0 + rr) * NB + cc);
   }
   __syncthreads();
-  if (threadIdx.x < 64) {
-    const int r = threadIdx.x;
-    for (int64_t t = 0; t < nrhs; t++) {
-      double x = W[t * lda + r0 + r];
-      for (int i = NB - 1; i >= 0; i--) {
-        const double xi = x / Lb[i][i];
-        const double ai = __shfl(xi, i, 64);
-        if (r == i) x = ai;
-        else if (r < i) x -= Lb[i][r] * ai;
-      }
-      ab[t][r] = x;
-      if (blockIdx.x == 0) A[t * lda + r0 + r] = x;
-    }
-  }
-  __syncthreads();
-  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (i < r0) {
-    double acc[4] = {0.0, 0.0, 0.0, 0.0};
-    for (int64_t t0 = 0; t0 < nrhs; t0 += 4) {
-      for (int r = 0; r < NB; r++) {
-        const double l = G[(r0 + r) * ld + i];
+  if (tid < len) rdiag[tid] = rcp_nr(Lb[tid / NB][tid % NB][tid % NB]);
+  for (int64_t t0 = 0; t0 < nrhs; t0 += RC) {
+    const int tc = (int)(nrhs - t0 < RC ? nrhs - t0 : RC);
+    for (int e = tid; e < tc * len; e += 256) wl[e / len][e % len] = W[(t0 + e / len) * lda + s0 + e % len];
+    __syncthreads();
+    for (int sb = nsub - 1; sb >= 0; sb--) {
+      if (wave == 0) {
+        for (int t = 0; t < tc; t++) {
+          double x = wl[t][sb * NB + lane];
 #pragma unroll
-        for (int u = 0; u < 4; u++)
-          if (t0 + u < nrhs) acc[u] += l * ab[t0 + u][r];
-      }
-#pragma unroll
-      for (int u = 0; u < 4; u++)
-        if (t0 + u < nrhs) {
-          W[(t0 + u) * lda + i] -= acc[u];
-          acc[u] = 0.0;
+          for (int i = NB - 1; i >= 0; i--) {
+            const double ai = readlane_d(x, i) * rdiag[sb * NB + i];
+            x = (lane < i) ? x - Lb[sb][i][lane] * ai : (lane == i ? ai : x);
+          }
+          wl[t][sb * NB + lane] = x;
         }
+      }
+      __syncthreads();
+      if (sb > 0 && tid < sb * NB) {  // in-super-block update of earlier rows (column tid)
+        double acc[RC];
+#pragma unroll
+        for (int t = 0; t < RC; t++) acc[t] = 0.0;
+        const double* lp = G + (s0 + sb * NB) * ld + s0 + tid;
+        for (int r = 0; r < NB; r += 16) {
+          double l[16];
+#pragma unroll
+          for (int u = 0; u < 16; u++) l[u] = lp[(int64_t)(r + u) * ld];
+#pragma unroll
+          for (int u = 0; u < 16; u++)
+#pragma unroll
+            for (int t = 0; t < RC; t++) acc[t] += l[u] * wl[t][sb * NB + r + u];
+        }
+        for (int t = 0; t < tc; t++) wl[t][tid] -= acc[t];
+      }
+      __syncthreads();
     }
+    if (blockIdx.x == 0)
+      for (int e = tid; e < tc * len; e += 256) A[(t0 + e / len) * lda + s0 + e % len] = wl[e / len][e % len];
+    const int64_t i = (int64_t)blockIdx.x * 256 + tid;
+    if (i < s0) {
+      double acc[RC];
+#pragma unroll
+      for (int t = 0; t < RC; t++) acc[t] = 0.0;
+      const double* lp = G + s0 * ld + i;
+      for (int r = 0; r < len; r += 16) {
+        double l[16];
+#pragma unroll
+        for (int u = 0; u < 16; u++) l[u] = lp[(int64_t)(r + u) * ld];
+#pragma unroll
+        for (int u = 0; u < 16; u++)
+#pragma unroll
+          for (int t = 0; t < RC; t++) acc[t] += l[u] * wl[t][r + u];
+      }
+      for (int t = 0; t < tc; t++) W[(t0 + t) * lda + i] -= acc[t];
+    }
+    __syncthreads();
   }
 }
 
@@ -295,7 +406,7 @@ extern "C" int gbm_dev_gblup_solve(double* G, int64_t ldg, int64_t n, double inv
   for (int64_t kb = 0; kb < nb; kb++) {
     const int64_t k0 = kb * NB;
     const int64_t rows_blocks = (gdim - k0) / NB;  // diagonal block + panel blocks
-    chol_panel_kernel<<<(unsigned)rows_blocks, 64, 0, s>>>(G, ldg, k0, Ld, info);
+    chol_panel_blocked_kernel<<<(unsigned)rows_blocks, 256, 0, s>>>(G, ldg, k0, Ld, info);
     GBM_LAUNCH_CHECK();
     const int64_t nt2 = rows_blocks - 1;
     if (nt2 > 0) {
@@ -307,10 +418,13 @@ extern "C" int gbm_dev_gblup_solve(double* G, int64_t ldg, int64_t n, double inv
   // the gebv buffer doubles as the w scratch: gebv_kernel (last) reads only Y and A
   gls_mu_kernel<<<dim3(gx, (unsigned)nrhs), 256, 0, s>>>(G, ldg, npad, nrhs, gebv, lda, mu);
   GBM_LAUNCH_CHECK();
-  for (int64_t b = nb - 1; b >= 0; b--) {
-    const int64_t chunks = (b * NB + 255) / 256;
-    back_subst_kernel<<<(unsigned)(chunks > 0 ? chunks : 1), 256, 0, s>>>(G, ldg, Ld, b, gebv, A_out, lda, nrhs);
+  for (int64_t end_blk = nb; end_blk > 0;) {
+    const int nsub = (int)(end_blk >= SB ? SB : end_blk);
+    const int64_t s0 = (end_blk - nsub) * NB;
+    const int64_t chunks = (s0 + 255) / 256;
+    back_subst_kernel<<<(unsigned)(chunks > 0 ? chunks : 1), 256, 0, s>>>(G, ldg, Ld, s0, nsub, gebv, A_out, lda, nrhs);
     GBM_LAUNCH_CHECK();
+    end_blk -= nsub;
   }
   gebv_kernel<<<dim3(gx, (unsigned)nrhs), 256, 0, s>>>(Y, ldy, n, A_out, gebv, lda, mu, lambda);
   GBM_LAUNCH_CHECK();
