@@ -2,7 +2,7 @@
 // CDNA4 matrix cores (v_mfma_f64_16x16x4_f64), the dominant cost of the path.
 //
 // Geometry (DESIGN.md "GRM kernel"):
-//   * workgroup tile 128 x 128 of G (lower-triangular tiles only: nt(nt+1)/2 tiles),
+//   * workgroup tile 128 x 128 of G (upper-triangular tiles only: nt(nt+1)/2 tiles),
 //     256 threads = 4 waves in 2 x 2, each wave a 64 x 64 sub-tile = 4 x 4 MFMA 16x16 tiles
 //     (16 f64x4 accumulators per lane);
 //   * K (= loci) consumed in stages of 16 rows; each stage is 2 x 16 rows x 1 KB of Zt brought
@@ -12,6 +12,8 @@
 //   * split-K over loci ("slices") when the triangular tile count alone cannot fill the
 //     256 CUs x 2 resident workgroups; slices write private slabs that a second kernel sums in
 //     a fixed order (deterministic, no float atomics).
+#include <cstdlib>
+
 #include "gbm_internal.h"
 
 namespace gbm {
@@ -24,17 +26,29 @@ constexpr int LROW = BT + 16;      // LDS row pitch in doubles (1152 B)
 constexpr int STAGE = 2 * BK * LROW;  // doubles per stage (A rows then B rows)
 
 __device__ __forceinline__ void tile_of(int64_t t, int64_t& ti, int64_t& tj) {
-  // t -> (ti, tj), tj <= ti, row-major over the lower triangle
+  // t -> upper-triangular tile (ti <= tj): enumerate the lower triangle row-major, then swap
   int64_t r = (int64_t)((sqrt(8.0 * (double)t + 1.0) - 1.0) * 0.5);
   while ((r + 1) * (r + 2) / 2 <= t) r++;
   while (r * (r + 1) / 2 > t) r--;
-  ti = r;
-  tj = t - r * (r + 1) / 2;
+  tj = r;
+  ti = t - r * (r + 1) / 2;
 }
 
+enum SyrkMode { kStore = 0, kSlab = 1, kSub = 2 };
+
+// One kernel, three epilogues:
+//   kStore  C[i][j]  = Σ_k U[k][i] U[k][j]     (the GRM, single slice)
+//   kSlab   slab     = Σ_{k in slice} ...      (the GRM, split over loci)
+//   kSub    C[i][j] -= Σ_k U[k][i] U[k][j]     (the upper-Cholesky trailing update, K = 64)
+// U is k-major: row k holds columns c contiguous (U[k*ldu + c]); the tiles are the upper
+// (ti <= tj) BT x BT tiles of the square [c0, c0 + lim)^2, in absolute column coordinates of U
+// and C. Wave quadrants entirely outside `lim` skip their MFMAs and stores (padding / ragged
+// last tile); their operand columns may be read past `lim` (the caller guarantees those reads
+// stay inside the allocation).
+template <int MODE>
 __global__ void __launch_bounds__(256, 2)
-grm_syrk_kernel(const double* __restrict__ Zt, int64_t ldz, int64_t p, double* __restrict__ G, int64_t ldg,
-                double* __restrict__ slab, int64_t ntiles, int nslices, int64_t steps_per_slice) {
+syrk_kernel(const double* __restrict__ U, int64_t ldu, int64_t K, int64_t c0, int64_t lim,
+            double* __restrict__ C, int64_t ldc, double* __restrict__ slab, int64_t ntiles, int64_t steps_per_slice) {
   __shared__ __attribute__((aligned(16))) double lds[2 * STAGE];  // 2 stages, 72 KB
 
   const int64_t wg = blockIdx.x;
@@ -43,9 +57,9 @@ grm_syrk_kernel(const double* __restrict__ Zt, int64_t ldz, int64_t p, double* _
   int64_t ti, tj;
   tile_of(t, ti, tj);
   const bool diag = (ti == tj);
-  const int64_t i0 = ti * BT, j0 = tj * BT;
+  const int64_t i0 = c0 + ti * BT, j0 = c0 + tj * BT;
 
-  const int64_t nsteps_total = (p + BK - 1) / BK;
+  const int64_t nsteps_total = (K + BK - 1) / BK;
   const int64_t kstep0 = (int64_t)s * steps_per_slice;
   int64_t kstep1 = kstep0 + steps_per_slice;
   if (kstep1 > nsteps_total) kstep1 = nsteps_total;
@@ -54,6 +68,7 @@ grm_syrk_kernel(const double* __restrict__ Zt, int64_t ldz, int64_t p, double* _
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int wm = wave >> 1, wn = wave & 1;
+  const bool active = (i0 - c0 + wm * 64 < lim) && (j0 - c0 + wn * 64 < lim);
 
   // each wave stages rows r = wave*4 .. wave*4+3 of A (and of B off-diagonal)
   auto stage = [&](int64_t kstep, int buf) {
@@ -64,8 +79,8 @@ grm_syrk_kernel(const double* __restrict__ Zt, int64_t ldz, int64_t p, double* _
       const int64_t k = kstep * BK + r;
       double* la = base + r * LROW;
       double* lb = base + (BK + r) * LROW;
-      if (k < p) {
-        const double* src = Zt + k * ldz;
+      if (k < K) {
+        const double* src = U + k * ldu;
         __builtin_amdgcn_global_load_lds((const void*)(src + i0 + lane * 2), (void*)la, 16, 0, 0);
         if (!diag) __builtin_amdgcn_global_load_lds((const void*)(src + j0 + lane * 2), (void*)lb, 16, 0, 0);
       } else {
@@ -89,37 +104,30 @@ grm_syrk_kernel(const double* __restrict__ Zt, int64_t ldz, int64_t p, double* _
   for (int64_t st = 0; st < nsteps; st++) {
     const int buf = (int)(st & 1);
     if (st + 1 < nsteps) stage(kstep0 + st + 1, buf ^ 1);
-    const double* A = lds + buf * STAGE;
-    const double* B = diag ? A : A + BK * LROW;
+    if (active) {
+      const double* A = lds + buf * STAGE;
+      const double* B = diag ? A : A + BK * LROW;
 #pragma unroll
-    for (int ks = 0; ks < BK / 4; ks++) {
-      const int kr = ks * 4 + frag_row;
-      double af[4], bf[4];
+      for (int ks = 0; ks < BK / 4; ks++) {
+        const int kr = ks * 4 + frag_row;
+        double af[4], bf[4];
 #pragma unroll
-      for (int m = 0; m < 4; m++) af[m] = A[kr * LROW + wm * 64 + m * 16 + frag_col];
+        for (int m = 0; m < 4; m++) af[m] = A[kr * LROW + wm * 64 + m * 16 + frag_col];
 #pragma unroll
-      for (int q = 0; q < 4; q++) bf[q] = B[kr * LROW + wn * 64 + q * 16 + frag_col];
+        for (int q = 0; q < 4; q++) bf[q] = B[kr * LROW + wn * 64 + q * 16 + frag_col];
 #pragma unroll
-      for (int m = 0; m < 4; m++)
+        for (int m = 0; m < 4; m++)
 #pragma unroll
-        for (int q = 0; q < 4; q++) acc[m][q] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[m], bf[q], acc[m][q], 0, 0, 0);
+          for (int q = 0; q < 4; q++)
+            acc[m][q] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[m], bf[q], acc[m][q], 0, 0, 0);
+      }
     }
     __syncthreads();
   }
+  if (!active) return;
 
   // epilogue: f64 MFMA C/D map: col = lane & 15, row = (lane >> 4) + 4 * reg
-  if (nslices == 1) {
-#pragma unroll
-    for (int m = 0; m < 4; m++)
-#pragma unroll
-      for (int q = 0; q < 4; q++)
-#pragma unroll
-        for (int r = 0; r < 4; r++) {
-          const int64_t row = i0 + wm * 64 + m * 16 + frag_row + 4 * r;
-          const int64_t col = j0 + wn * 64 + q * 16 + frag_col;
-          G[row * ldg + col] = acc[m][q][r];
-        }
-  } else {
+  if constexpr (MODE == kSlab) {
     double* out = slab + ((int64_t)s * ntiles + t) * (int64_t)(BT * BT);
 #pragma unroll
     for (int m = 0; m < 4; m++)
@@ -130,6 +138,21 @@ grm_syrk_kernel(const double* __restrict__ Zt, int64_t ldz, int64_t p, double* _
           const int row = wm * 64 + m * 16 + frag_row + 4 * r;
           const int col = wn * 64 + q * 16 + frag_col;
           out[row * BT + col] = acc[m][q][r];
+        }
+  } else {
+    const int64_t rlim = c0 + lim;
+#pragma unroll
+    for (int m = 0; m < 4; m++)
+#pragma unroll
+      for (int q = 0; q < 4; q++)
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+          const int64_t row = i0 + wm * 64 + m * 16 + frag_row + 4 * r;
+          const int64_t col = j0 + wn * 64 + q * 16 + frag_col;
+          if (row < rlim && col < rlim) {
+            if constexpr (MODE == kStore) C[row * ldc + col] = acc[m][q][r];
+            else C[row * ldc + col] -= acc[m][q][r];
+          }
         }
   }
 }
@@ -183,6 +206,99 @@ static void plan(int64_t n, int64_t p, int64_t& ntiles, int& nslices, int64_t& s
   steps_per_slice = (nsteps + nslices - 1) / nslices;
 }
 
+// Small-tile variant of the Cholesky trailing update (64x64 upper tiles, K = 64, 4 waves of
+// 32x32): more workgroups for the small trailing matrices of late panels. The C tile is loaded
+// into the accumulators first and the A fragments are negated, so the MFMA chain itself
+// produces C − Σ_k U[k][i] U[k][j] (no separate read-modify-write).
+constexpr int P64 = 80;  // LDS pitch: the two 16-lane halves of a fragment read hit disjoint banks
+__global__ void __launch_bounds__(256, 2)
+syrk64_sub_kernel(const double* __restrict__ U, int64_t ldu, int64_t c0, int64_t lim, double* __restrict__ C,
+                  int64_t ldc) {
+  __shared__ __attribute__((aligned(16))) double As[64 * P64];
+  __shared__ __attribute__((aligned(16))) double Bs[64 * P64];
+  int64_t ti, tj;
+  tile_of(blockIdx.x, ti, tj);
+  const bool diag = ti == tj;
+  const int64_t i0 = c0 + ti * 64, j0 = c0 + tj * 64;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int fr = lane >> 4, fc = lane & 15;
+  const int64_t rlim = c0 + lim;
+  const bool active = (i0 + wm * 32 < rlim) && (j0 + wn * 32 < rlim);
+  d4 acc[2][2];
+  if (active) {
+#pragma unroll
+    for (int m = 0; m < 2; m++)
+#pragma unroll
+      for (int q = 0; q < 2; q++)
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+          const int64_t row = i0 + wm * 32 + m * 16 + fr + 4 * r;
+          const int64_t col = j0 + wn * 32 + q * 16 + fc;
+          acc[m][q][r] = (row < rlim && col < rlim) ? C[row * ldc + col] : 0.0;
+        }
+  }
+  {
+    const int k = tid >> 2, quarter = tid & 3;
+    const double* sa = U + k * ldu + i0 + quarter * 16;
+    const double* sb = U + k * ldu + j0 + quarter * 16;
+#pragma unroll
+    for (int e = 0; e < 16; e += 2) {
+      *reinterpret_cast<double2*>(&As[k * P64 + quarter * 16 + e]) = *reinterpret_cast<const double2*>(sa + e);
+      if (!diag)
+        *reinterpret_cast<double2*>(&Bs[k * P64 + quarter * 16 + e]) = *reinterpret_cast<const double2*>(sb + e);
+    }
+  }
+  __syncthreads();
+  if (!active) return;
+  const double* B = diag ? As : Bs;
+#pragma unroll
+  for (int ks = 0; ks < 16; ks++) {
+    double af[2], bf[2];
+#pragma unroll
+    for (int m = 0; m < 2; m++) af[m] = -As[(ks * 4 + fr) * P64 + wm * 32 + m * 16 + fc];
+#pragma unroll
+    for (int q = 0; q < 2; q++) bf[q] = B[(ks * 4 + fr) * P64 + wn * 32 + q * 16 + fc];
+#pragma unroll
+    for (int m = 0; m < 2; m++)
+#pragma unroll
+      for (int q = 0; q < 2; q++) acc[m][q] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[m], bf[q], acc[m][q], 0, 0, 0);
+  }
+#pragma unroll
+  for (int m = 0; m < 2; m++)
+#pragma unroll
+    for (int q = 0; q < 2; q++)
+#pragma unroll
+      for (int r = 0; r < 4; r++) {
+        const int64_t row = i0 + wm * 32 + m * 16 + fr + 4 * r;
+        const int64_t col = j0 + wn * 32 + q * 16 + fc;
+        if (row < rlim && col < rlim) C[row * ldc + col] = acc[m][q][r];
+      }
+}
+
+// Upper-Cholesky trailing update: C[k1:gdim, k1:gdim] (upper tiles) -= U[k0:k1, k1:]ᵀ U[k0:k1, k1:]
+int launch_chol_update(double* G, int64_t ldg, int64_t k0, int64_t nb, int64_t gdim, hipStream_t s) {
+  const int64_t k1 = k0 + nb;
+  const int64_t lim = gdim - k1;
+  if (lim <= 0) return GBM_OK;
+  static const int64_t small_lim = [] {
+    const char* e = getenv("GBM_UPD64_LIM");
+    return e ? (int64_t)atoll(e) : (int64_t)3968;
+  }();
+  if (nb == 64 && lim <= small_lim) {
+    const int64_t m = (lim + 63) / 64;
+    syrk64_sub_kernel<<<(unsigned)(m * (m + 1) / 2), 256, 0, s>>>(G + k0 * ldg, ldg, k1, lim, G, ldg);
+    GBM_LAUNCH_CHECK();
+    return GBM_OK;
+  }
+  const int64_t m = (lim + BT - 1) / BT;
+  const int64_t ntiles = m * (m + 1) / 2;
+  const int64_t steps = (nb + BK - 1) / BK;
+  syrk_kernel<kSub><<<(unsigned)ntiles, 256, 0, s>>>(G + k0 * ldg, ldg, nb, k1, lim, G, ldg, nullptr, ntiles, steps);
+  GBM_LAUNCH_CHECK();
+  return GBM_OK;
+}
+
 int64_t grm_workspace_bytes(int64_t n, int64_t p) {
   int64_t ntiles, sps;
   int S;
@@ -210,7 +326,10 @@ int launch_grm_syrk(const double* Zt, int64_t ldz, int64_t p, int64_t n, double*
   if (need > 0 && (!ws || ws_bytes < need))
     return fail(GBM_E_ARG, "gbm_dev_grm: workspace too small (" + std::to_string(ws_bytes) + " < " +
                                std::to_string(need) + ")");
-  grm_syrk_kernel<<<(unsigned)(ntiles * S), 256, 0, s>>>(Zt, ldz, p, G, ldg, (double*)ws, ntiles, S, sps);
+  if (S == 1)
+    syrk_kernel<kStore><<<(unsigned)ntiles, 256, 0, s>>>(Zt, ldz, p, 0, n, G, ldg, nullptr, ntiles, sps);
+  else
+    syrk_kernel<kSlab><<<(unsigned)(ntiles * S), 256, 0, s>>>(Zt, ldz, p, 0, n, G, ldg, (double*)ws, ntiles, sps);
   GBM_LAUNCH_CHECK();
   return GBM_OK;
 }
@@ -261,12 +380,12 @@ extern "C" int gbm_dev_grm_slices(int64_t n, int64_t p) {
 }
 
 namespace gbm {
-// out[i, j] = inv_q * G[max(i,j), min(i,j)] for i, j < n (full symmetric export of the GRM)
+// out[i, j] = inv_q * G[min(i,j), max(i,j)] for i, j < n (full symmetric export of the upper-stored GRM)
 __global__ void __launch_bounds__(256) grm_export_kernel(const double* __restrict__ G, int64_t ldg, int64_t n,
                                                          double inv_q, double* __restrict__ out, int64_t ldo) {
   const int64_t i = blockIdx.x;
   for (int64_t j = threadIdx.x; j < n; j += 256)
-    out[i * ldo + j] = inv_q * (j <= i ? G[i * ldg + j] : G[j * ldg + i]);
+    out[i * ldo + j] = inv_q * (j >= i ? G[i * ldg + j] : G[j * ldg + i]);
 }
 
 int launch_grm_export(const double* G, int64_t ldg, int64_t n, double inv_q, double* out, int64_t ldo, hipStream_t s) {

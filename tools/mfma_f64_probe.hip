@@ -41,6 +41,38 @@ __global__ void __launch_bounds__(256) mfma_rate(double* out, int iters, double 
   out[blockIdx.x * blockDim.x + threadIdx.x] = s;
 }
 
+// GEMM-shaped: 4x4 accumulators fed by 4 A and 4 B fragments per k-step (the GRM inner loop)
+__global__ void __launch_bounds__(256, 2) mfma_rate_gemm(double* out, int iters, double seed) {
+  double af[4], bf[4];
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    af[i] = seed + threadIdx.x * 1e-3 + i;
+    bf[i] = seed - threadIdx.x * 1e-3 - i;
+  }
+  d4 acc[4][4];
+#pragma unroll
+  for (int a = 0; a < 4; a++)
+#pragma unroll
+    for (int b = 0; b < 4; b++) acc[a][b] = (d4){0, 0, 0, 0};
+  for (int it = 0; it < iters; it++) {
+#pragma unroll
+    for (int a = 0; a < 4; a++)
+#pragma unroll
+      for (int b = 0; b < 4; b++) acc[a][b] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[a], bf[b], acc[a][b], 0, 0, 0);
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      af[i] = af[i] * 0.999 + 1e-3;
+      bf[i] = bf[i] * 0.999 - 1e-3;
+    }
+  }
+  double s = 0;
+#pragma unroll
+  for (int a = 0; a < 4; a++)
+#pragma unroll
+    for (int b = 0; b < 4; b++) s += acc[a][b][0] + acc[a][b][3];
+  out[blockIdx.x * blockDim.x + threadIdx.x] = s;
+}
+
 __global__ void __launch_bounds__(256) valu_rate(double* out, int iters, double seed) {
   double x[8];
 #pragma unroll
@@ -95,6 +127,17 @@ int main() {
       printf("{\"probe\":\"mfma_f64_16x16x4\",\"waves_per_simd\":%d,\"nacc\":%d,\"tflops\":%.2f,\"ms\":%.3f}\n", \
              bpc, NA, (double)blocks * 4 * iters * NA * 2.0 * 16 * 16 * 4 / ms / 1e9, ms);
       RUN(1) RUN(4) RUN(8)
+    }
+    for (int bpc = 1; bpc <= 2; bpc++) {
+      int blocks = cus * bpc;
+      int it2 = 5000;
+      mfma_rate_gemm<<<blocks, 256>>>(dO, it2, 1.0);
+      CK(hipEventRecord(e0));
+      mfma_rate_gemm<<<blocks, 256>>>(dO, it2, 1.0);
+      CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
+      CK(hipEventElapsedTime(&ms, e0, e1));
+      printf("{\"probe\":\"mfma_f64_gemm_4x4acc\",\"waves_per_simd\":%d,\"tflops\":%.2f,\"ms\":%.3f}\n", bpc,
+             (double)blocks * 4 * it2 * 16 * 2.0 * 16 * 16 * 4 / ms / 1e9, ms);
     }
     for (int bpc = 1; bpc <= 8; bpc *= 2) {
       int blocks = cus * bpc;
