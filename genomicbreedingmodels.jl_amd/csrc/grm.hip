@@ -90,17 +90,34 @@ syrk_kernel(const double* __restrict__ U, int64_t ldu, int64_t K, int64_t c0, in
     }
   };
 
+  const int frag_row = lane >> 4;  // k within a 4-deep MFMA step
+  const int frag_col = lane & 15;
+  const int64_t rlim = c0 + lim;
+
   d4 acc[4][4];
+  if constexpr (MODE == kSub) {
+    // the C tile goes straight into the accumulators (its loads overlap the operand staging)
+    // and the A fragments are negated below: the MFMA chain produces C − Σ_k U[k][i] U[k][j]
 #pragma unroll
-  for (int a = 0; a < 4; a++)
+    for (int m = 0; m < 4; m++)
 #pragma unroll
-    for (int b = 0; b < 4; b++) acc[a][b] = (d4){0.0, 0.0, 0.0, 0.0};
+      for (int q = 0; q < 4; q++)
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+          const int64_t row = i0 + wm * 64 + m * 16 + frag_row + 4 * r;
+          const int64_t col = j0 + wn * 64 + q * 16 + frag_col;
+          acc[m][q][r] = (active && row < rlim && col < rlim) ? C[row * ldc + col] : 0.0;
+        }
+  } else {
+#pragma unroll
+    for (int a = 0; a < 4; a++)
+#pragma unroll
+      for (int b = 0; b < 4; b++) acc[a][b] = (d4){0.0, 0.0, 0.0, 0.0};
+  }
 
   if (nsteps > 0) stage(kstep0, 0);
   __syncthreads();
 
-  const int frag_row = lane >> 4;  // k within a 4-deep MFMA step
-  const int frag_col = lane & 15;
   for (int64_t st = 0; st < nsteps; st++) {
     const int buf = (int)(st & 1);
     if (st + 1 < nsteps) stage(kstep0 + st + 1, buf ^ 1);
@@ -112,7 +129,10 @@ syrk_kernel(const double* __restrict__ U, int64_t ldu, int64_t K, int64_t c0, in
         const int kr = ks * 4 + frag_row;
         double af[4], bf[4];
 #pragma unroll
-        for (int m = 0; m < 4; m++) af[m] = A[kr * LROW + wm * 64 + m * 16 + frag_col];
+        for (int m = 0; m < 4; m++) {
+          af[m] = A[kr * LROW + wm * 64 + m * 16 + frag_col];
+          if constexpr (MODE == kSub) af[m] = -af[m];
+        }
 #pragma unroll
         for (int q = 0; q < 4; q++) bf[q] = B[kr * LROW + wn * 64 + q * 16 + frag_col];
 #pragma unroll
@@ -140,7 +160,6 @@ syrk_kernel(const double* __restrict__ U, int64_t ldu, int64_t K, int64_t c0, in
           out[row * BT + col] = acc[m][q][r];
         }
   } else {
-    const int64_t rlim = c0 + lim;
 #pragma unroll
     for (int m = 0; m < 4; m++)
 #pragma unroll
@@ -150,8 +169,7 @@ syrk_kernel(const double* __restrict__ U, int64_t ldu, int64_t K, int64_t c0, in
           const int64_t row = i0 + wm * 64 + m * 16 + frag_row + 4 * r;
           const int64_t col = j0 + wn * 64 + q * 16 + frag_col;
           if (row < rlim && col < rlim) {
-            if constexpr (MODE == kStore) C[row * ldc + col] = acc[m][q][r];
-            else C[row * ldc + col] -= acc[m][q][r];
+            C[row * ldc + col] = acc[m][q][r];
           }
         }
   }
@@ -283,7 +301,7 @@ int launch_chol_update(double* G, int64_t ldg, int64_t k0, int64_t nb, int64_t g
   if (lim <= 0) return GBM_OK;
   static const int64_t small_lim = [] {
     const char* e = getenv("GBM_UPD64_LIM");
-    return e ? (int64_t)atoll(e) : (int64_t)3968;
+    return e ? (int64_t)atoll(e) : (int64_t)2048;
   }();
   if (nb == 64 && lim <= small_lim) {
     const int64_t m = (lim + 63) / 64;
