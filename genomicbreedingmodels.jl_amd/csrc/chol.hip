@@ -14,36 +14,17 @@
 // a blocked back substitution, and GEBV = μ̂ + (y − μ̂) − λa (= μ̂ + G a).
 // The reference inverts V with pinv/SVD (src/gwas.jl:472,595); for λ > 0 V is SPD and the
 // Cholesky solution is the same up to rounding.
-#include "gbm_internal.h"
+#include <cstdlib>
+
+#include "chol_device.h"
 
 namespace gbm {
 
-typedef double d4 __attribute__((ext_vector_type(4)));
 constexpr int NB = kCholNB;  // 64
 constexpr int MAXRHS = 63;
 
-int launch_chol_update(double* G, int64_t ldg, int64_t k0, int64_t nb, int64_t gdim, hipStream_t s);
-
-__device__ __forceinline__ double rsqrt_nr(double a) {  // v_rsq_f64 + one Newton step
-  double y = __builtin_amdgcn_rsq(a);
-  const double h = 0.5 * a * y;
-  return y * fma(-h, y, 1.5);
-}
-__device__ __forceinline__ double rcp_nr(double a) {  // v_rcp_f64 + one Newton step
-  double y = __builtin_amdgcn_rcp(a);
-  const double e = fma(-a, y, 1.0);
-  return fma(y, e, y);
-}
-__device__ __forceinline__ double readlane_d(double x, int lane) {
-  union {
-    double d;
-    int i[2];
-  } u;
-  u.d = x;
-  u.i[0] = __builtin_amdgcn_readlane(u.i[0], lane);
-  u.i[1] = __builtin_amdgcn_readlane(u.i[1], lane);
-  return u.d;
-}
+int launch_chol_update(double* G, int64_t ldg, int64_t k0, int64_t nb, int64_t gdim, double* Ld, double* Dinv,
+                       int32_t* info, int64_t next_k0, hipStream_t s);
 
 // ---- V = G/q + λI (upper part), padding = identity, bordered R columns -----------------------
 __global__ void __launch_bounds__(256) prepare_v_kernel(double* __restrict__ G, int64_t ld, int64_t n,
@@ -70,137 +51,80 @@ __global__ void __launch_bounds__(256) prepare_v_kernel(double* __restrict__ G, 
   }
 }
 
-// ---- panel k ---------------------------------------------------------------------------------
-// Workgroup 0: factor the 64x64 diagonal block and store U_kk into the scratch Ld (not in place:
-// the other workgroups of this launch read the unfactored block from G). Workgroup g >= 1:
-// factor the same block redundantly (4 x 16-row sub-panels, MFMA for the inner updates), then
-// solve its 64-column chunk X = A[k0:k0+64, k0+64g : k0+64g+64] in place: X <- U_kk⁻ᵀ X.
-// LDS images are U-layout (row i, column j, upper part valid); pitch 80 doubles puts the two
-// 16-lane halves of every MFMA fragment read on disjoint bank halves.
-constexpr int PS = NB + 16;
-
-// D(16x16 at (r0, c0) of dst) -= Σ_k S[kb + k][ra + row] T[kb + k][cb + col], k < 4*ksteps
-__device__ __forceinline__ void mfma_tile_sub_t(double* dst, int r0, int c0, const double* S, int ra,
-                                                const double* T, int cb, int kb, int ksteps, int lane) {
-  d4 acc = (d4){0.0, 0.0, 0.0, 0.0};
-  const int fr = lane >> 4, fc = lane & 15;
-  for (int ks = 0; ks < ksteps; ks++) {
-    const double a = S[(kb + ks * 4 + fr) * PS + ra + fc];
-    const double b = T[(kb + ks * 4 + fr) * PS + cb + fc];
-    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc, 0, 0, 0);
-  }
-#pragma unroll
-  for (int r = 0; r < 4; r++) dst[(r0 + fr + 4 * r) * PS + c0 + fc] -= acc[r];
-}
-
-__global__ void __launch_bounds__(256) chol_panel_kernel(double* __restrict__ G, int64_t ld, int64_t k0,
-                                                         double* __restrict__ Ld, int32_t* __restrict__ info) {
-  __shared__ __attribute__((aligned(16))) double Us[NB * PS];
-  __shared__ __attribute__((aligned(16))) double X[NB * PS];
-  __shared__ double rinv[NB];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const bool diag_wg = blockIdx.x == 0;
+// ---- first diagonal block (the later ones are factored by the previous trailing update) -----
+__global__ void __launch_bounds__(256) factor_first_kernel(const double* __restrict__ G, int64_t ld,
+                                                           double* __restrict__ Ld, double* __restrict__ Dinv,
+                                                           int32_t* __restrict__ info) {
+  __shared__ __attribute__((aligned(16))) double Us[CNB * PS];
+  __shared__ double rinv[CNB];
+  const int tid = threadIdx.x;
   {
     const int row = tid >> 2, quarter = tid & 3;
-    const double* sa = G + (k0 + row) * ld + k0 + quarter * 16;
-    const double* sx = G + (k0 + row) * ld + k0 + (int64_t)blockIdx.x * NB + quarter * 16;
+    const double* sa = G + row * ld + quarter * 16;
 #pragma unroll
-    for (int e = 0; e < 16; e += 2) {
+    for (int e = 0; e < 16; e += 2)
       *reinterpret_cast<double2*>(&Us[row * PS + quarter * 16 + e]) = *reinterpret_cast<const double2*>(sa + e);
-      if (!diag_wg)
-        *reinterpret_cast<double2*>(&X[row * PS + quarter * 16 + e]) = *reinterpret_cast<const double2*>(sx + e);
-    }
   }
   __syncthreads();
-  bool bad = false;
-  int badcol = 0;
-  for (int kb = 0; kb < 4; kb++) {
-    const int o = kb * 16;
-    if (wave == 0) {
-      // right-looking factorisation of the 16-row sub-panel U[o:o+16, o:64]: lane r owns
-      // column o + r (= row o + r of L = Uᵀ); columns o..o+15 form the diagonal sub-block, the
-      // others are solved in the same 16-step loop (u_cs broadcast from lane s by v_readlane)
-      const int ncols = NB - o;
-      const int cc = o + (lane < ncols ? lane : 0);
-      double x[16];
-#pragma unroll
-      for (int t = 0; t < 16; t++) x[t] = Us[(o + t) * PS + cc];
-#pragma unroll
-      for (int c = 0; c < 16; c++) {
-        const double piv = readlane_d(x[c], c);
-        if (!(piv > 0.0) || !isfinite(piv)) {
-          if (!bad) badcol = o + c;
-          bad = true;
-        }
-        const double lc = x[c] * rsqrt_nr(piv);  // lane c: piv/sqrt(piv) = U[c][c]
-#pragma unroll
-        for (int sidx = c + 1; sidx < 16; sidx++) x[sidx] -= lc * readlane_d(lc, sidx);
-        x[c] = lc;
-      }
-      if (lane < ncols) {
-#pragma unroll
-        for (int t = 0; t < 16; t++) Us[(o + t) * PS + cc] = (lane < 16 && t > lane) ? 0.0 : x[t];
-      }
-      if (lane < 16) rinv[o + lane] = rcp_nr(x[lane & 15]);
-    }
-    __syncthreads();
-    // trailing update of the block's remaining upper 16x16 tiles on the matrix cores:
-    // U[i][j] -= Σ_{t in [o, o+16)} U[t][i] U[t][j]
-    const int m = 3 - kb;
-    const int ntile = m * (m + 1) / 2;
-    for (int t = wave; t < ntile; t += 4) {
-      int a = 0;
-      while ((a + 1) * (a + 2) / 2 <= t) a++;
-      const int b = t - a * (a + 1) / 2;  // b <= a  -> tile (row b, col a)
-      const int r0 = o + 16 + b * 16, c0 = o + 16 + a * 16;
-      mfma_tile_sub_t(Us, r0, c0, Us, r0, Us, c0, o, 4, lane);
-    }
-    __syncthreads();
-  }
-  if (diag_wg) {
-    if (bad && tid == 0) atomicCAS(info, 0, (int32_t)(k0 + badcol + 1));
-    const int row = tid >> 2, quarter = tid & 3;
-    double* dst = Ld + (k0 + row) * NB + quarter * 16;
-#pragma unroll
-    for (int e = 0; e < 16; e += 2) {
-      const int c = quarter * 16 + e;
-      *reinterpret_cast<double2*>(dst + e) =
-          make_double2(c >= row ? Us[row * PS + c] : 0.0, c + 1 >= row ? Us[row * PS + c + 1] : 0.0);
-    }
-    return;
-  }
-  // X <- U_kk⁻ᵀ X, 16-row block by 16-row block
-  for (int rb = 0; rb < 4; rb++) {
-    const int o = rb * 16;
-    // X[o:o+16, :] -= U[0:o, o:o+16]ᵀ X[0:o, :]   (wave w: columns 16w..16w+15)
-    if (rb > 0) mfma_tile_sub_t(X, o, wave * 16, Us, o, X, wave * 16, 0, rb * 4, lane);
-    __syncthreads();
-    if (wave == 0) {
-      // forward substitution on the 16x16 diagonal sub-block, lane = column of X
-      double x[16];
-#pragma unroll
-      for (int t = 0; t < 16; t++) x[t] = X[(o + t) * PS + lane];
-#pragma unroll
-      for (int c = 0; c < 16; c++) {
-        x[c] *= rinv[o + c];
-#pragma unroll
-        for (int sidx = c + 1; sidx < 16; sidx++) x[sidx] -= Us[(o + c) * PS + o + sidx] * x[c];
-      }
-#pragma unroll
-      for (int t = 0; t < 16; t++) X[(o + t) * PS + lane] = x[t];
-    }
-    __syncthreads();
-  }
+  const int bad = factor_diag_block(Us, rinv, tid);
+  if (tid == 0 && bad >= 0) atomicCAS(info, 0, (int32_t)(bad + 1));
+  store_factor(Us, rinv, Ld, Dinv, tid);
+}
+
+// ---- panel k: U_k,J = U_kk⁻ᵀ A_k,J for the column chunks J > k ----------------------------------
+// U_kk arrives factored (Ld) together with the inverses of its four 16x16 diagonal sub-blocks
+// (Dinv), so the block forward substitution is all MFMA, no serial chain:
+//   X_rb <- (D_rb⁻¹)ᵀ (X_rb − U[0:o, rb]ᵀ X[0:o])  for 16-row blocks rb = 0..3.
+// Wave w owns columns 16w..16w+15 of the chunk, so the four waves never touch each other's data.
+// The solved chunk is also written transposed into the (otherwise unused) lower triangle: L = Uᵀ
+// row-major, so the back substitution and the μ̂ kernel read coalesced rows. Those entries are
+// never overwritten later: every later trailing update covers only rows/cols >= its own origin.
+__global__ void __launch_bounds__(256) chol_panel_kernel(double* __restrict__ G, int64_t ld, int64_t k0,
+                                                         const double* __restrict__ Ld,
+                                                         const double* __restrict__ Dinv) {
+  __shared__ __attribute__((aligned(16))) double Us[CNB * PS];
+  __shared__ __attribute__((aligned(16))) double X[CNB * PS];
+  __shared__ __attribute__((aligned(16))) double Di[4 * 256];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int64_t jx = k0 + ((int64_t)blockIdx.x + 1) * CNB;
   {
     const int row = tid >> 2, quarter = tid & 3;
-    double* dx = G + (k0 + row) * ld + k0 + (int64_t)blockIdx.x * NB + quarter * 16;
+    const double* sl = Ld + (k0 + row) * CNB + quarter * 16;
+    const double* sx = G + (k0 + row) * ld + jx + quarter * 16;
+#pragma unroll
+    for (int e = 0; e < 16; e += 2) {
+      *reinterpret_cast<double2*>(&Us[row * PS + quarter * 16 + e]) = *reinterpret_cast<const double2*>(sl + e);
+      *reinterpret_cast<double2*>(&X[row * PS + quarter * 16 + e]) = *reinterpret_cast<const double2*>(sx + e);
+    }
+    const double* sd = Dinv + (k0 / 16) * 256;
+    *reinterpret_cast<double2*>(&Di[tid * 2]) = *reinterpret_cast<const double2*>(sd + tid * 2);
+    *reinterpret_cast<double2*>(&Di[512 + tid * 2]) = *reinterpret_cast<const double2*>(sd + 512 + tid * 2);
+  }
+  __syncthreads();
+  const int fr = lane >> 4, fc = lane & 15;
+  const int cw = wave * 16;
+  for (int rb = 0; rb < 4; rb++) {
+    const int o = rb * 16;
+    if (rb > 0) mfma_tile_sub_t(X, o, cw, Us, o, X, cw, 0, rb * 4, lane);  // X_rb -= U[0:o,rb]ᵀ X[0:o]
+    // X_rb = (D_rb⁻¹)ᵀ X_rb : A[i][k] = Dinv[k][i], B[k][j] = X[o+k][cw+j]
+    d4 acc = (d4){0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int ks = 0; ks < 4; ks++) {
+      const double a = Di[rb * 256 + (ks * 4 + fr) * 16 + fc];
+      const double bv = X[(o + ks * 4 + fr) * PS + cw + fc];
+      acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, bv, acc, 0, 0, 0);
+    }
+#pragma unroll
+    for (int r = 0; r < 4; r++) X[(o + fr + 4 * r) * PS + cw + fc] = acc[r];
+  }
+  __syncthreads();
+  {
+    const int row = tid >> 2, quarter = tid & 3;
+    double* dx = G + (k0 + row) * ld + jx + quarter * 16;
 #pragma unroll
     for (int e = 0; e < 16; e += 2)
       *reinterpret_cast<double2*>(dx + e) = *reinterpret_cast<const double2*>(&X[row * PS + quarter * 16 + e]);
-    // the same chunk transposed into the (otherwise unused) lower triangle: L = Uᵀ row-major,
-    // so the back substitution and the μ̂ kernel read coalesced rows. Never overwritten later:
-    // every later trailing update covers only rows/cols >= its own k1 > these columns.
-    double* dl = G + (k0 + (int64_t)blockIdx.x * NB + row) * ld + k0 + quarter * 16;
+    double* dl = G + (jx + row) * ld + k0 + quarter * 16;
 #pragma unroll
     for (int e = 0; e < 16; e += 2)
       *reinterpret_cast<double2*>(dl + e) =
@@ -359,10 +283,12 @@ using namespace gbm;
 
 extern "C" int64_t gbm_dev_npad(int64_t n) { return npad_of(n); }
 extern "C" int64_t gbm_dev_gdim(int64_t n) { return gdim_of(n); }
-// scratch: the factored 64x64 diagonal blocks and their inverses, 2 x npad x 64 doubles
+// scratch: the factored 64x64 diagonal blocks (npad x 64), their inverses (npad x 64) and the
+// inverses of their 16x16 diagonal sub-blocks (npad x 16)
+static int64_t solve_ws_doubles(int64_t n) { return npad_of(n) * (2 * NB + 16); }
 extern "C" int64_t gbm_dev_solve_workspace(int64_t n, int64_t nrhs) {
   (void)nrhs;
-  return 2 * npad_of(n) * NB * (int64_t)sizeof(double);
+  return solve_ws_doubles(n) * (int64_t)sizeof(double);
 }
 
 extern "C" int gbm_dev_gblup_solve(double* G, int64_t ldg, int64_t n, double inv_q, const int64_t* q_dev,
@@ -375,20 +301,24 @@ extern "C" int gbm_dev_gblup_solve(double* G, int64_t ldg, int64_t n, double inv
     return fail(GBM_E_ARG, "gbm_dev_gblup_solve: bad arguments (need ldg >= gdim(n), lda >= npad(n), "
                            "1 <= nrhs <= 63, lambda > 0, inv_q > 0)");
   if ((ldg & 1) || ((uintptr_t)G & 15)) return fail(GBM_E_ARG, "gbm_dev_gblup_solve: G must be 16-byte aligned, even ld");
-  if (!workspace || ws_bytes < 2 * npad * NB * (int64_t)sizeof(double) || ((uintptr_t)workspace & 15))
+  if (!workspace || ws_bytes < solve_ws_doubles(n) * (int64_t)sizeof(double) || ((uintptr_t)workspace & 15))
     return fail(GBM_E_ARG, "gbm_dev_gblup_solve: workspace too small (see gbm_dev_solve_workspace)");
   double* Ld = (double*)workspace;
   double* Linv = Ld + npad * NB;
+  double* Dinv = Linv + npad * NB;
   hipStream_t s = (hipStream_t)stream;
   prepare_v_kernel<<<(unsigned)gdim, 256, 0, s>>>(G, ldg, n, npad, gdim, inv_q, q_dev, lambda, Y, ldy, nrhs, info);
   GBM_LAUNCH_CHECK();
   const int64_t nb = npad / NB;
+  factor_first_kernel<<<1, 256, 0, s>>>(G, ldg, Ld, Dinv, info);
+  GBM_LAUNCH_CHECK();
   for (int64_t kb = 0; kb < nb; kb++) {
     const int64_t k0 = kb * NB;
-    const int64_t col_blocks = (gdim - k0) / NB;  // diagonal block + column chunks
-    chol_panel_kernel<<<(unsigned)col_blocks, 256, 0, s>>>(G, ldg, k0, Ld, info);
+    const int64_t chunks = (gdim - k0) / NB - 1;  // column chunks right of the diagonal block
+    chol_panel_kernel<<<(unsigned)chunks, 256, 0, s>>>(G, ldg, k0, Ld, Dinv);
     GBM_LAUNCH_CHECK();
-    int rc = launch_chol_update(G, ldg, k0, NB, gdim, s);
+    // trailing update; its first workgroup also factors the next diagonal block
+    int rc = launch_chol_update(G, ldg, k0, NB, gdim, Ld, Dinv, info, kb + 1 < nb ? k0 + NB : -1, s);
     if (rc != GBM_OK) return rc;
   }
   diag_inverse_kernel<<<(unsigned)nb, 64, 0, s>>>(Ld, Linv);

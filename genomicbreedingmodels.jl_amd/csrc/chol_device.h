@@ -1,0 +1,133 @@
+// Device helpers shared by the Cholesky kernels (chol.hip) and the trailing-update kernels
+// (grm.hip), which factor the next diagonal block in their first workgroup.
+#pragma once
+#include "gbm_internal.h"
+
+namespace gbm {
+
+typedef double d4 __attribute__((ext_vector_type(4)));
+
+constexpr int CNB = 64;        // Cholesky block (== kCholNB)
+constexpr int PS = CNB + 16;   // LDS pitch of 64x64 images: fragment reads conflict-free
+
+__device__ __forceinline__ double rsqrt_nr(double a) {  // v_rsq_f64 + one Newton step
+  double y = __builtin_amdgcn_rsq(a);
+  const double h = 0.5 * a * y;
+  return y * fma(-h, y, 1.5);
+}
+__device__ __forceinline__ double rcp_nr(double a) {  // v_rcp_f64 + one Newton step
+  double y = __builtin_amdgcn_rcp(a);
+  const double e = fma(-a, y, 1.0);
+  return fma(y, e, y);
+}
+__device__ __forceinline__ double readlane_d(double x, int lane) {
+  union {
+    double d;
+    int i[2];
+  } u;
+  u.d = x;
+  u.i[0] = __builtin_amdgcn_readlane(u.i[0], lane);
+  u.i[1] = __builtin_amdgcn_readlane(u.i[1], lane);
+  return u.d;
+}
+
+// D(16x16 at (r0, c0) of dst) -= Σ_k S[kb + k][ra + row] T[kb + k][cb + col], k < 4*ksteps
+// (all operands pitch PS)
+__device__ __forceinline__ void mfma_tile_sub_t(double* dst, int r0, int c0, const double* S, int ra,
+                                                const double* T, int cb, int kb, int ksteps, int lane) {
+  d4 acc = (d4){0.0, 0.0, 0.0, 0.0};
+  const int fr = lane >> 4, fc = lane & 15;
+  for (int ks = 0; ks < ksteps; ks++) {
+    const double a = S[(kb + ks * 4 + fr) * PS + ra + fc];
+    const double b = T[(kb + ks * 4 + fr) * PS + cb + fc];
+    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc, 0, 0, 0);
+  }
+#pragma unroll
+  for (int r = 0; r < 4; r++) dst[(r0 + fr + 4 * r) * PS + c0 + fc] -= acc[r];
+}
+
+// Upper Cholesky of the 64x64 block in Us (U-layout, pitch PS, upper part valid) by a
+// 256-thread workgroup: four 16-row sub-panels, each a right-looking 16-step loop on wave 0
+// (lane r owns column o + r; u_cs broadcast by v_readlane) followed by the MFMA update of the
+// block's remaining upper 16x16 tiles on all waves. Leaves U in Us (zeros below the diagonal)
+// and 1/U_ii in rinv. Returns, in every lane of wave 0, the first failing column or -1.
+__device__ __forceinline__ int factor_diag_block(double* Us, double* rinv, int tid) {
+  const int lane = tid & 63, wave = tid >> 6;
+  int badcol = -1;
+  for (int kb = 0; kb < 4; kb++) {
+    const int o = kb * 16;
+    if (wave == 0) {
+      const int ncols = CNB - o;
+      const int cc = o + (lane < ncols ? lane : 0);
+      double x[16];
+#pragma unroll
+      for (int t = 0; t < 16; t++) x[t] = Us[(o + t) * PS + cc];
+#pragma unroll
+      for (int c = 0; c < 16; c++) {
+        const double piv = readlane_d(x[c], c);
+        if ((!(piv > 0.0) || !isfinite(piv)) && badcol < 0) badcol = o + c;
+        const double lc = x[c] * rsqrt_nr(piv);  // lane c: piv/sqrt(piv) = U[c][c]
+#pragma unroll
+        for (int sidx = c + 1; sidx < 16; sidx++) x[sidx] -= lc * readlane_d(lc, sidx);
+        x[c] = lc;
+      }
+      if (lane < ncols) {
+#pragma unroll
+        for (int t = 0; t < 16; t++) Us[(o + t) * PS + cc] = (lane < 16 && t > lane) ? 0.0 : x[t];
+      }
+      if (lane < 16) rinv[o + lane] = rcp_nr(x[lane & 15]);
+    }
+    __syncthreads();
+    const int m = 3 - kb;  // remaining 16-blocks
+    const int ntile = m * (m + 1) / 2;
+    for (int t = wave; t < ntile; t += 4) {
+      int a = 0;
+      while ((a + 1) * (a + 2) / 2 <= t) a++;
+      const int b = t - a * (a + 1) / 2;  // b <= a: tile (row b, col a)
+      const int r0 = o + 16 + b * 16, c0 = o + 16 + a * 16;
+      mfma_tile_sub_t(Us, r0, c0, Us, r0, Us, c0, o, 4, lane);
+    }
+    __syncthreads();
+  }
+  // the 16x16 lower parts of the trailing diagonal sub-blocks were touched by the MFMA updates
+  for (int e = tid; e < CNB * CNB; e += 256) {
+    const int r = e / CNB, c = e % CNB;
+    if (c < r) Us[r * PS + c] = 0.0;
+  }
+  __syncthreads();
+  return badcol;
+}
+
+// Store a factored block: Ld_blk (64x64 row-major, upper, zeros below) and the inverses of its
+// four 16x16 diagonal sub-blocks Dinv_blk[w][i][j] = (D_w⁻¹)[i][j] (upper). Wave w computes D_w⁻¹
+// column by column (lane j < 16), the dot products split over 2 partial sums.
+__device__ __forceinline__ void store_factor(const double* Us, const double* rinv, double* Ld_blk,
+                                             double* Dinv_blk, int tid) {
+  const int lane = tid & 63, wave = tid >> 6;
+  {
+    const int row = tid >> 2, quarter = tid & 3;
+    double* dst = Ld_blk + row * CNB + quarter * 16;
+#pragma unroll
+    for (int e = 0; e < 16; e += 2)
+      *reinterpret_cast<double2*>(dst + e) = *reinterpret_cast<const double2*>(&Us[row * PS + quarter * 16 + e]);
+  }
+  const int o = wave * 16;
+  const int j = lane & 15;
+  double x[16];
+#pragma unroll
+  for (int i = 15; i >= 0; i--) {
+    double p0 = 0.0, p1 = 0.0;
+#pragma unroll
+    for (int k = i + 1; k < 16; k += 2) {
+      p0 = fma(Us[(o + i) * PS + o + k], x[k], p0);
+      if (k + 1 < 16) p1 = fma(Us[(o + i) * PS + o + k + 1], x[k + 1], p1);
+    }
+    x[i] = (i <= j) ? (((i == j) ? 1.0 : 0.0) - (p0 + p1)) * rinv[o + i] : 0.0;
+  }
+  if (lane < 16) {
+#pragma unroll
+    for (int i = 0; i < 16; i++) Dinv_blk[wave * 256 + i * 16 + j] = x[i];
+  }
+}
+
+}  // namespace gbm

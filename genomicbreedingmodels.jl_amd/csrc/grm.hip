@@ -14,11 +14,9 @@
 //     a fixed order (deterministic, no float atomics).
 #include <cstdlib>
 
-#include "gbm_internal.h"
+#include "chol_device.h"
 
 namespace gbm {
-
-typedef double d4 __attribute__((ext_vector_type(4)));
 
 constexpr int BT = 128;            // tile edge
 constexpr int BK = 16;             // loci per stage
@@ -48,7 +46,8 @@ enum SyrkMode { kStore = 0, kSlab = 1, kSub = 2 };
 template <int MODE>
 __global__ void __launch_bounds__(256, 2)
 syrk_kernel(const double* __restrict__ U, int64_t ldu, int64_t K, int64_t c0, int64_t lim,
-            double* __restrict__ C, int64_t ldc, double* __restrict__ slab, int64_t ntiles, int64_t steps_per_slice) {
+            double* __restrict__ C, int64_t ldc, double* __restrict__ slab, int64_t ntiles, int64_t steps_per_slice,
+            double* __restrict__ Ld, double* __restrict__ Dinv, int32_t* __restrict__ info, int64_t fk0) {
   __shared__ __attribute__((aligned(16))) double lds[2 * STAGE];  // 2 stages, 72 KB
 
   const int64_t wg = blockIdx.x;
@@ -144,7 +143,9 @@ syrk_kernel(const double* __restrict__ U, int64_t ldu, int64_t K, int64_t c0, in
     }
     __syncthreads();
   }
-  if (!active) return;
+  // kSub, first workgroup (tile (0,0)), fk0 >= 0: factor the next diagonal block afterwards
+  const bool factor_next = (MODE == kSub) && fk0 >= 0 && wg == 0;
+  if (!active && !factor_next) return;
 
   // epilogue: f64 MFMA C/D map: col = lane & 15, row = (lane >> 4) + 4 * reg
   if constexpr (MODE == kSlab) {
@@ -168,10 +169,29 @@ syrk_kernel(const double* __restrict__ U, int64_t ldu, int64_t K, int64_t c0, in
         for (int r = 0; r < 4; r++) {
           const int64_t row = i0 + wm * 64 + m * 16 + frag_row + 4 * r;
           const int64_t col = j0 + wn * 64 + q * 16 + frag_col;
-          if (row < rlim && col < rlim) {
+          if (active && row < rlim && col < rlim) {
             C[row * ldc + col] = acc[m][q][r];
           }
         }
+  }
+  if constexpr (MODE == kSub) {
+    if (factor_next) {
+      // the next panel's diagonal block [c0, c0+64)^2 is wave (0,0)'s 64x64 quadrant of this tile
+      double* Us = lds;  // the staging buffers are free now (last loop iteration ended in a barrier)
+      double* rinv = lds + CNB * PS;
+      if (wave == 0) {
+#pragma unroll
+        for (int m = 0; m < 4; m++)
+#pragma unroll
+          for (int q = 0; q < 4; q++)
+#pragma unroll
+            for (int r = 0; r < 4; r++) Us[(m * 16 + frag_row + 4 * r) * PS + q * 16 + frag_col] = acc[m][q][r];
+      }
+      __syncthreads();
+      const int bad = factor_diag_block(Us, rinv, threadIdx.x);
+      if (threadIdx.x == 0 && bad >= 0) atomicCAS(info, 0, (int32_t)(fk0 + bad + 1));
+      store_factor(Us, rinv, Ld + fk0 * CNB, Dinv + (fk0 / 16) * 256, threadIdx.x);
+    }
   }
 }
 
@@ -231,7 +251,8 @@ static void plan(int64_t n, int64_t p, int64_t& ntiles, int& nslices, int64_t& s
 constexpr int P64 = 80;  // LDS pitch: the two 16-lane halves of a fragment read hit disjoint banks
 __global__ void __launch_bounds__(256, 2)
 syrk64_sub_kernel(const double* __restrict__ U, int64_t ldu, int64_t c0, int64_t lim, double* __restrict__ C,
-                  int64_t ldc) {
+                  int64_t ldc, double* __restrict__ Ld, double* __restrict__ Dinv, int32_t* __restrict__ info,
+                  int64_t fk0) {
   __shared__ __attribute__((aligned(16))) double As[64 * P64];
   __shared__ __attribute__((aligned(16))) double Bs[64 * P64];
   int64_t ti, tj;
@@ -268,10 +289,11 @@ syrk64_sub_kernel(const double* __restrict__ U, int64_t ldu, int64_t c0, int64_t
     }
   }
   __syncthreads();
-  if (!active) return;
+  const bool factor_next = fk0 >= 0 && blockIdx.x == 0;
+  if (!active && !factor_next) return;
   const double* B = diag ? As : Bs;
 #pragma unroll
-  for (int ks = 0; ks < 16; ks++) {
+  for (int ks = 0; ks < (active ? 16 : 0); ks++) {
     double af[2], bf[2];
 #pragma unroll
     for (int m = 0; m < 2; m++) af[m] = -As[(ks * 4 + fr) * P64 + wm * 32 + m * 16 + fc];
@@ -290,12 +312,29 @@ syrk64_sub_kernel(const double* __restrict__ U, int64_t ldu, int64_t c0, int64_t
       for (int r = 0; r < 4; r++) {
         const int64_t row = i0 + wm * 32 + m * 16 + fr + 4 * r;
         const int64_t col = j0 + wn * 32 + q * 16 + fc;
-        if (row < rlim && col < rlim) C[row * ldc + col] = acc[m][q][r];
+        if (active && row < rlim && col < rlim) C[row * ldc + col] = acc[m][q][r];
       }
+  if (factor_next) {
+    // this tile is the next panel's diagonal block: factor it straight from the accumulators
+    __syncthreads();  // every wave is done reading As/Bs
+    double* Us = As;  // pitch P64 == PS
+    double* rinv = Bs;
+#pragma unroll
+    for (int m = 0; m < 2; m++)
+#pragma unroll
+      for (int q = 0; q < 2; q++)
+#pragma unroll
+        for (int r = 0; r < 4; r++) Us[(wm * 32 + m * 16 + fr + 4 * r) * PS + wn * 32 + q * 16 + fc] = acc[m][q][r];
+    __syncthreads();
+    const int bad = factor_diag_block(Us, rinv, tid);
+    if (tid == 0 && bad >= 0) atomicCAS(info, 0, (int32_t)(fk0 + bad + 1));
+    store_factor(Us, rinv, Ld + fk0 * CNB, Dinv + (fk0 / 16) * 256, tid);
+  }
 }
 
 // Upper-Cholesky trailing update: C[k1:gdim, k1:gdim] (upper tiles) -= U[k0:k1, k1:]ᵀ U[k0:k1, k1:]
-int launch_chol_update(double* G, int64_t ldg, int64_t k0, int64_t nb, int64_t gdim, hipStream_t s) {
+int launch_chol_update(double* G, int64_t ldg, int64_t k0, int64_t nb, int64_t gdim, double* Ld, double* Dinv,
+                       int32_t* info, int64_t next_k0, hipStream_t s) {
   const int64_t k1 = k0 + nb;
   const int64_t lim = gdim - k1;
   if (lim <= 0) return GBM_OK;
@@ -305,14 +344,16 @@ int launch_chol_update(double* G, int64_t ldg, int64_t k0, int64_t nb, int64_t g
   }();
   if (nb == 64 && lim <= small_lim) {
     const int64_t m = (lim + 63) / 64;
-    syrk64_sub_kernel<<<(unsigned)(m * (m + 1) / 2), 256, 0, s>>>(G + k0 * ldg, ldg, k1, lim, G, ldg);
+    syrk64_sub_kernel<<<(unsigned)(m * (m + 1) / 2), 256, 0, s>>>(G + k0 * ldg, ldg, k1, lim, G, ldg, Ld, Dinv, info,
+                                                                  next_k0);
     GBM_LAUNCH_CHECK();
     return GBM_OK;
   }
   const int64_t m = (lim + BT - 1) / BT;
   const int64_t ntiles = m * (m + 1) / 2;
   const int64_t steps = (nb + BK - 1) / BK;
-  syrk_kernel<kSub><<<(unsigned)ntiles, 256, 0, s>>>(G + k0 * ldg, ldg, nb, k1, lim, G, ldg, nullptr, ntiles, steps);
+  syrk_kernel<kSub><<<(unsigned)ntiles, 256, 0, s>>>(G + k0 * ldg, ldg, nb, k1, lim, G, ldg, nullptr, ntiles, steps,
+                                                     Ld, Dinv, info, next_k0);
   GBM_LAUNCH_CHECK();
   return GBM_OK;
 }
@@ -345,9 +386,11 @@ int launch_grm_syrk(const double* Zt, int64_t ldz, int64_t p, int64_t n, double*
     return fail(GBM_E_ARG, "gbm_dev_grm: workspace too small (" + std::to_string(ws_bytes) + " < " +
                                std::to_string(need) + ")");
   if (S == 1)
-    syrk_kernel<kStore><<<(unsigned)ntiles, 256, 0, s>>>(Zt, ldz, p, 0, n, G, ldg, nullptr, ntiles, sps);
+    syrk_kernel<kStore><<<(unsigned)ntiles, 256, 0, s>>>(Zt, ldz, p, 0, n, G, ldg, nullptr, ntiles, sps, nullptr,
+                                                         nullptr, nullptr, -1);
   else
-    syrk_kernel<kSlab><<<(unsigned)(ntiles * S), 256, 0, s>>>(Zt, ldz, p, 0, n, G, ldg, (double*)ws, ntiles, sps);
+    syrk_kernel<kSlab><<<(unsigned)(ntiles * S), 256, 0, s>>>(Zt, ldz, p, 0, n, G, ldg, (double*)ws, ntiles, sps,
+                                                              nullptr, nullptr, nullptr, -1);
   GBM_LAUNCH_CHECK();
   return GBM_OK;
 }

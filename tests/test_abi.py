@@ -44,7 +44,7 @@ def test_geometry_helpers():
     lib = gbm.load_library()
     assert lib.gbm_dev_npad(1) == 128 and lib.gbm_dev_npad(5000) == 5120 and lib.gbm_dev_npad(5120) == 5120
     assert lib.gbm_dev_gdim(5000) == 5120 + 64
-    assert lib.gbm_dev_solve_workspace(5000, 1) == 2 * 5120 * 64 * 8
+    assert lib.gbm_dev_solve_workspace(5000, 1) == 5120 * (2 * 64 + 16) * 8
 
 
 def test_no_gpu_means_loud_error():
