@@ -67,7 +67,8 @@ syrk_kernel(const double* __restrict__ U, int64_t ldu, int64_t K, int64_t c0, in
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int wm = wave >> 1, wn = wave & 1;
-  const bool active = (i0 - c0 + wm * 64 < lim) && (j0 - c0 + wn * 64 < lim);
+  // (the strictly-lower quadrant of a diagonal tile is never needed: upper storage)
+  const bool active = (i0 - c0 + wm * 64 < lim) && (j0 - c0 + wn * 64 < lim) && !(diag && wm == 1 && wn == 0);
 
   // each wave stages rows r = wave*4 .. wave*4+3 of A (and of B off-diagonal)
   auto stage = [&](int64_t kstep, int buf) {

@@ -73,6 +73,46 @@ __global__ void __launch_bounds__(256, 2) mfma_rate_gemm(double* out, int iters,
   out[blockIdx.x * blockDim.x + threadIdx.x] = s;
 }
 
+// Mixed: even waves run the GEMM-shaped MFMA loop, odd waves a VALU f64 FMA loop, to see whether
+// the f64 matrix and vector pipes add up on gfx950.
+__global__ void __launch_bounds__(256, 2) mixed_rate(double* out, int iters_m, int iters_v, double seed, int mode) {
+  const int wave = threadIdx.x >> 6;
+  double s = 0;
+  const bool do_mfma = (mode == 0) ? true : (mode == 1 ? false : ((wave & 1) == 0));
+  if (do_mfma) {
+    double af[4], bf[4];
+#pragma unroll
+    for (int i = 0; i < 4; i++) { af[i] = seed + threadIdx.x * 1e-3 + i; bf[i] = seed - threadIdx.x * 1e-3 - i; }
+    d4 acc[4][4];
+#pragma unroll
+    for (int a = 0; a < 4; a++)
+#pragma unroll
+      for (int b = 0; b < 4; b++) acc[a][b] = (d4){0, 0, 0, 0};
+    for (int it = 0; it < iters_m; it++) {
+#pragma unroll
+      for (int a = 0; a < 4; a++)
+#pragma unroll
+        for (int b = 0; b < 4; b++) acc[a][b] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[a], bf[b], acc[a][b], 0, 0, 0);
+    }
+#pragma unroll
+    for (int a = 0; a < 4; a++)
+#pragma unroll
+      for (int b = 0; b < 4; b++) s += acc[a][b][0] + acc[a][b][3];
+  } else {
+    double x[16];
+#pragma unroll
+    for (int i = 0; i < 16; i++) x[i] = seed + i + threadIdx.x;
+    const double m = 0.999999, c = 1e-7;
+    for (int it = 0; it < iters_v; it++) {
+#pragma unroll
+      for (int i = 0; i < 16; i++) x[i] = fma(x[i], m, c);
+    }
+#pragma unroll
+    for (int i = 0; i < 16; i++) s += x[i];
+  }
+  out[blockIdx.x * blockDim.x + threadIdx.x] = s;
+}
+
 __global__ void __launch_bounds__(256) valu_rate(double* out, int iters, double seed) {
   double x[8];
 #pragma unroll
@@ -148,6 +188,23 @@ int main() {
       CK(hipEventElapsedTime(&ms, e0, e1));
       double flops = (double)blocks * 256 * iters * 8 * 2.0;
       printf("{\"probe\":\"valu_fma_f64\",\"waves_per_simd\":%d,\"tflops\":%.2f,\"ms\":%.3f}\n", bpc, flops / ms / 1e9, ms);
+    }
+  }
+  {
+    // mixed MFMA + VALU: per wave, MFMA work = it_m*16*2048 flops, VALU work = it_v*16*2*64 flops
+    const int it_m = 5000, it_v = 40000;
+    const int blocks = cus * 2;
+    for (int mode = 0; mode < 3; mode++) {
+      mixed_rate<<<blocks, 256>>>(dO, it_m, it_v, 1.0, mode);
+      CK(hipEventRecord(e0));
+      mixed_rate<<<blocks, 256>>>(dO, it_m, it_v, 1.0, mode);
+      CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
+      CK(hipEventElapsedTime(&ms, e0, e1));
+      const double wm = (double)it_m * 16 * 2048, wv = (double)it_v * 16 * 2 * 64;
+      const double waves = (double)blocks * 4;
+      double fl = mode == 0 ? waves * wm : (mode == 1 ? waves * wv : waves / 2 * (wm + wv));
+      printf("{\"probe\":\"mixed\",\"mode\":\"%s\",\"tflops\":%.2f,\"ms\":%.3f}\n",
+             mode == 0 ? "mfma_only" : (mode == 1 ? "valu_only" : "half_half"), fl / ms / 1e9, ms);
     }
   }
   return bad ? 1 : 0;
