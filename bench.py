@@ -35,13 +35,15 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--n", type=int, default=5000)
-    ap.add_argument("--p", type=int, default=50000, help="loci per GPU")
+    ap.add_argument("--individuals", type=int, default=5000)
+    ap.add_argument("--loci", type=int, default=50000, help="loci per GPU")
     ap.add_argument("--nrhs", type=int, default=1)
     ap.add_argument("--lam", type=float, default=1.0)
     ap.add_argument("--seed", type=int, default=4242)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-p", type=int, default=0, help="loci in the CPU baseline sample (0 = all)")
+    ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL); gloo only to rehearse N ranks on one GPU")
+    ap.add_argument("--same-device", action="store_true", help="all ranks on cuda:0 (rehearsal on a 1-GPU box)")
     return ap.parse_args()
 
 
@@ -78,8 +80,8 @@ def cpu_baseline(args):
         threads = max([d.get("num_threads", 1) for d in threadpool_info() if d.get("internal_api") == "openblas"] or [1])
     except Exception:  # pragma: no cover
         threads = len(os.sched_getaffinity(0))
-    n = args.n
-    p = args.cpu_sample_p or args.p
+    n = args.individuals
+    p = args.cpu_sample_p or args.loci
     so = os.path.join(ROOT, "oracle", "build", "libgbm_oracle.so")
     X = np.zeros((n, p), order="F")
     if os.path.exists(so):
@@ -120,8 +122,12 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        dev_idx = 0 if args.same_device else local_rank
+        torch.cuda.set_device(dev_idx)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev_idx))
+        else:
+            dist.init_process_group(args.dist_backend)
     else:
         torch.cuda.set_device(0)
     dev = torch.cuda.current_device()
@@ -130,7 +136,7 @@ def main():
     from gbm.sharded import HipShardStages, LocalComm, TorchComm, sharded_gblup_step
 
     comm = TorchComm() if world > 1 else LocalComm()
-    n, p_local = args.n, args.p
+    n, p_local = args.individuals, args.loci
     p_total = p_local * world
     j0 = rank * p_local
     st = HipShardStages(n, p_local, nrhs=args.nrhs, lambda_=args.lam, device=dev)
