@@ -19,7 +19,14 @@
 namespace gbm {
 
 constexpr int BT = 128;            // tile edge
-constexpr int BK = 16;             // loci per stage
+#ifndef GBM_BK
+#define GBM_BK 16
+#endif
+#ifndef GBM_WPS
+#define GBM_WPS 2
+#endif
+constexpr int BK = GBM_BK;         // loci per stage
+constexpr int WPS = GBM_WPS;       // target waves per SIMD (= resident 256-thread workgroups per CU)
 constexpr int LROW = BT + 16;      // LDS row pitch in doubles (1152 B)
 constexpr int STAGE = 2 * BK * LROW;  // doubles per stage (A rows then B rows)
 
@@ -44,11 +51,13 @@ enum SyrkMode { kStore = 0, kSlab = 1, kSub = 2 };
 // last tile); their operand columns may be read past `lim` (the caller guarantees those reads
 // stay inside the allocation).
 template <int MODE>
-__global__ void __launch_bounds__(256, 2)
+__global__ void __launch_bounds__(256, WPS)
 syrk_kernel(const double* __restrict__ U, int64_t ldu, int64_t K, int64_t c0, int64_t lim,
             double* __restrict__ C, int64_t ldc, double* __restrict__ slab, int64_t ntiles, int64_t steps_per_slice,
             double* __restrict__ Ld, double* __restrict__ Dinv, int32_t* __restrict__ info, int64_t fk0) {
-  __shared__ __attribute__((aligned(16))) double lds[2 * STAGE];  // 2 stages, 72 KB
+  // 2 stages (72 KB at BK = 16); kSub's first workgroup reuses it for the 64x64 factor image
+  constexpr int LDS_DOUBLES = (2 * STAGE > CNB * PS + CNB) ? 2 * STAGE : CNB * PS + CNB;
+  __shared__ __attribute__((aligned(16))) double lds[LDS_DOUBLES];
 
   const int64_t wg = blockIdx.x;
   const int s = (int)(wg / ntiles);
@@ -70,12 +79,12 @@ syrk_kernel(const double* __restrict__ U, int64_t ldu, int64_t K, int64_t c0, in
   // (the strictly-lower quadrant of a diagonal tile is never needed: upper storage)
   const bool active = (i0 - c0 + wm * 64 < lim) && (j0 - c0 + wn * 64 < lim) && !(diag && wm == 1 && wn == 0);
 
-  // each wave stages rows r = wave*4 .. wave*4+3 of A (and of B off-diagonal)
+  // each wave stages BK/4 rows r = wave*BK/4 .. of A (and of B off-diagonal)
   auto stage = [&](int64_t kstep, int buf) {
     double* base = lds + buf * STAGE;
 #pragma unroll
-    for (int rr = 0; rr < 4; rr++) {
-      const int r = wave * 4 + rr;
+    for (int rr = 0; rr < BK / 4; rr++) {
+      const int r = wave * (BK / 4) + rr;
       const int64_t k = kstep * BK + r;
       double* la = base + r * LROW;
       double* lb = base + (BK + r) * LROW;
@@ -221,7 +230,7 @@ static int resident_wgs() {
     int v = 0;
     if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0) cus = v;
   }
-  return cus * 2;  // 2 workgroups per CU (LDS 72 KB each, 2 waves per SIMD)
+  return cus * WPS;  // WPS workgroups per CU (LDS 2 x 2 x BK x 1152 B each)
 }
 
 static void plan(int64_t n, int64_t p, int64_t& ntiles, int& nslices, int64_t& steps_per_slice) {

@@ -20,7 +20,7 @@ GBM_E_OOM = -5
 GBM_E_NODEV = -6
 GBM_E_DATA = -7
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libgbm.so")
+LIB_PATH = os.environ.get("GBM_LIBGBM") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "libgbm.so")
 
 # Every symbol include/gbm.h declares (tests check the export table against this list).
 EXPORTS = (
