@@ -9,10 +9,16 @@
 //     straight into LDS by global_load_lds_dwordx4 (one wave-instruction = one 1-KB locus row
 //     segment), double-buffered; LDS rows padded to 1152 B so the two 16-lane halves of a
 //     ds_read_b64 fragment load land on disjoint bank halves;
-//   * split-K over loci ("slices") when the triangular tile count alone cannot fill the
-//     256 CUs x 2 resident workgroups; slices write private slabs that a second kernel sums in
-//     a fixed order (deterministic, no float atomics).
+//   * stream-K over loci: the (tile, stage) units are cut into equal contiguous ranges, one per
+//     resident workgroup slot (256 CUs x 2), so there is no tail round; partial tiles go to
+//     workspace slabs that a second kernel sums in a fixed order (deterministic, no float atomics).
+#include <cmath>
 #include <cstdlib>
+#include <map>
+#include <mutex>
+#include <queue>
+#include <tuple>
+#include <vector>
 
 #include "chol_device.h"
 
@@ -39,47 +45,22 @@ __device__ __forceinline__ void tile_of(int64_t t, int64_t& ti, int64_t& tj) {
   ti = t - r * (r + 1) / 2;
 }
 
-enum SyrkMode { kStore = 0, kSlab = 1, kSub = 2 };
+enum SyrkMode { kSub = 0, kSplit = 1 };
 
-// One kernel, three epilogues:
-//   kStore  C[i][j]  = Σ_k U[k][i] U[k][j]     (the GRM, single slice)
-//   kSlab   slab     = Σ_{k in slice} ...      (the GRM, split over loci)
-//   kSub    C[i][j] -= Σ_k U[k][i] U[k][j]     (the upper-Cholesky trailing update, K = 64)
-// U is k-major: row k holds columns c contiguous (U[k*ldu + c]); the tiles are the upper
-// (ti <= tj) BT x BT tiles of the square [c0, c0 + lim)^2, in absolute column coordinates of U
-// and C. Wave quadrants entirely outside `lim` skip their MFMAs and stores (padding / ragged
-// last tile); their operand columns may be read past `lim` (the caller guarantees those reads
-// stay inside the allocation).
-template <int MODE>
-__global__ void __launch_bounds__(256, WPS)
-syrk_kernel(const double* __restrict__ U, int64_t ldu, int64_t K, int64_t c0, int64_t lim,
-            double* __restrict__ C, int64_t ldc, double* __restrict__ slab, int64_t ntiles, int64_t steps_per_slice,
-            double* __restrict__ Ld, double* __restrict__ Dinv, int32_t* __restrict__ info, int64_t fk0) {
-  // 2 stages (72 KB at BK = 16); kSub's first workgroup reuses it for the 64x64 factor image
-  constexpr int LDS_DOUBLES = (2 * STAGE > CNB * PS + CNB) ? 2 * STAGE : CNB * PS + CNB;
-  __shared__ __attribute__((aligned(16))) double lds[LDS_DOUBLES];
+#ifdef GBM_DEBUG_WGTIME  // timing experiment only: per-workgroup start/end clocks + hardware id
+__device__ unsigned long long g_wgtime[3 * 16384];
+#endif
 
-  const int64_t wg = blockIdx.x;
-  const int s = (int)(wg / ntiles);
-  const int64_t t = wg - (int64_t)s * ntiles;
-  int64_t ti, tj;
-  tile_of(t, ti, tj);
-  const bool diag = (ti == tj);
-  const int64_t i0 = c0 + ti * BT, j0 = c0 + tj * BT;
-
-  const int64_t nsteps_total = (K + BK - 1) / BK;
-  const int64_t kstep0 = (int64_t)s * steps_per_slice;
-  int64_t kstep1 = kstep0 + steps_per_slice;
-  if (kstep1 > nsteps_total) kstep1 = nsteps_total;
-  const int64_t nsteps = kstep1 > kstep0 ? kstep1 - kstep0 : 0;
-
-  const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
+// acc[m][q] += (NEG ? −1 : 1) Σ_k U[k][i0 + ·] U[k][j0 + ·] over the stages [kstep0, kstep0 + nsteps)
+// (BK loci each) of one BT x BT tile. Operands are staged by global_load_lds into the two LDS
+// buffers (double-buffered); returns after a barrier, so the buffers are free again. `wave` is
+// wave-uniform (SGPR): the staging branches are scalar.
+template <bool NEG>
+__device__ __forceinline__ void tile_pass(const double* __restrict__ U, int64_t ldu, int64_t K, int64_t i0,
+                                          int64_t j0, bool diag, bool active, int64_t kstep0, int64_t nsteps,
+                                          double* lds, d4 (&acc)[4][4], int wave, int lane) {
   const int wm = wave >> 1, wn = wave & 1;
-  // (the strictly-lower quadrant of a diagonal tile is never needed: upper storage)
-  const bool active = (i0 - c0 + wm * 64 < lim) && (j0 - c0 + wn * 64 < lim) && !(diag && wm == 1 && wn == 0);
-
-  // each wave stages BK/4 rows r = wave*BK/4 .. of A (and of B off-diagonal)
+  // each wave stages BK/4 locus rows r = wave*BK/4 .. of A (and of B off-diagonal)
   auto stage = [&](int64_t kstep, int buf) {
     double* base = lds + buf * STAGE;
 #pragma unroll
@@ -89,7 +70,11 @@ syrk_kernel(const double* __restrict__ U, int64_t ldu, int64_t K, int64_t c0, in
       double* la = base + r * LROW;
       double* lb = base + (BK + r) * LROW;
       if (k < K) {
+#ifdef GBM_DEBUG_SAMEROWS  // timing experiment only: operands stay L2-resident (wrong results)
+        const double* src = U + (k & 63) * ldu;
+#else
         const double* src = U + k * ldu;
+#endif
         __builtin_amdgcn_global_load_lds((const void*)(src + i0 + lane * 2), (void*)la, 16, 0, 0);
         if (!diag) __builtin_amdgcn_global_load_lds((const void*)(src + j0 + lane * 2), (void*)lb, 16, 0, 0);
       } else {
@@ -98,35 +83,11 @@ syrk_kernel(const double* __restrict__ U, int64_t ldu, int64_t K, int64_t c0, in
       }
     }
   };
-
   const int frag_row = lane >> 4;  // k within a 4-deep MFMA step
   const int frag_col = lane & 15;
-  const int64_t rlim = c0 + lim;
-
-  d4 acc[4][4];
-  if constexpr (MODE == kSub) {
-    // the C tile goes straight into the accumulators (its loads overlap the operand staging)
-    // and the A fragments are negated below: the MFMA chain produces C − Σ_k U[k][i] U[k][j]
-#pragma unroll
-    for (int m = 0; m < 4; m++)
-#pragma unroll
-      for (int q = 0; q < 4; q++)
-#pragma unroll
-        for (int r = 0; r < 4; r++) {
-          const int64_t row = i0 + wm * 64 + m * 16 + frag_row + 4 * r;
-          const int64_t col = j0 + wn * 64 + q * 16 + frag_col;
-          acc[m][q][r] = (active && row < rlim && col < rlim) ? C[row * ldc + col] : 0.0;
-        }
-  } else {
-#pragma unroll
-    for (int a = 0; a < 4; a++)
-#pragma unroll
-      for (int b = 0; b < 4; b++) acc[a][b] = (d4){0.0, 0.0, 0.0, 0.0};
-  }
 
   if (nsteps > 0) stage(kstep0, 0);
   __syncthreads();
-
   for (int64_t st = 0; st < nsteps; st++) {
     const int buf = (int)(st & 1);
     if (st + 1 < nsteps) stage(kstep0 + st + 1, buf ^ 1);
@@ -140,7 +101,7 @@ syrk_kernel(const double* __restrict__ U, int64_t ldu, int64_t K, int64_t c0, in
 #pragma unroll
         for (int m = 0; m < 4; m++) {
           af[m] = A[kr * LROW + wm * 64 + m * 16 + frag_col];
-          if constexpr (MODE == kSub) af[m] = -af[m];
+          if constexpr (NEG) af[m] = -af[m];
         }
 #pragma unroll
         for (int q = 0; q < 4; q++) bf[q] = B[kr * LROW + wn * 64 + q * 16 + frag_col];
@@ -153,24 +114,94 @@ syrk_kernel(const double* __restrict__ U, int64_t ldu, int64_t K, int64_t c0, in
     }
     __syncthreads();
   }
-  // kSub, first workgroup (tile (0,0)), fk0 >= 0: factor the next diagonal block afterwards
-  const bool factor_next = (MODE == kSub) && fk0 >= 0 && wg == 0;
-  if (!active && !factor_next) return;
+}
 
-  // epilogue: f64 MFMA C/D map: col = lane & 15, row = (lane >> 4) + 4 * reg
-  if constexpr (MODE == kSlab) {
-    double* out = slab + ((int64_t)s * ntiles + t) * (int64_t)(BT * BT);
+// Loci split of the GRM: every tile is cut into the same nslices stage ranges
+// [b[s], b[s+1]); workgroup (s, t) = blockIdx s * ntiles + t sums range s of tile t into slab
+// slot (s, t). The ranges shrink from first to last (plan() below), so the hardware's in-order
+// dispatch onto freed slots works like guided self-scheduling: large chunks first, small ones
+// fill the tail.
+constexpr int kMaxSlices = 12;
+struct SliceBounds {
+  int32_t n;
+  int32_t b[kMaxSlices + 1];
+};
+
+// Two epilogues over one staging/MFMA core:
+//   kSplit   slab[s][t] = Σ_{k in range s} U[k][i] U[k][j]   (the GRM, split over loci)
+//   kSub     C[i][j]   -= Σ_k U[k][i] U[k][j]               (the upper-Cholesky trailing update, K = 64)
+// U is k-major: row k holds columns c contiguous (U[k*ldu + c]); the tiles are the upper
+// (ti <= tj) BT x BT tiles of the square [c0, c0 + lim)^2, in absolute column coordinates of U
+// and C. Wave quadrants entirely outside `lim` skip their MFMAs and stores (padding / ragged
+// last tile), as does the strictly-lower quadrant of a diagonal tile (upper storage); their
+// operand columns may be read past `lim` (the caller guarantees those reads stay inside the
+// allocation).
+template <int MODE>
+__global__ void __launch_bounds__(256, WPS)
+syrk_kernel(const double* __restrict__ U, int64_t ldu, int64_t K, int64_t c0, int64_t lim,
+            double* __restrict__ C, int64_t ldc, double* __restrict__ slab, int64_t ntiles, SliceBounds sb,
+            double* __restrict__ Ld, double* __restrict__ Dinv, int32_t* __restrict__ info, int64_t fk0) {
+  // 2 stages (72 KB at BK = 16); kSub's first workgroup reuses it for the 64x64 factor image
+  constexpr int LDS_DOUBLES = (2 * STAGE > CNB * PS + CNB) ? 2 * STAGE : CNB * PS + CNB;
+  __shared__ __attribute__((aligned(16))) double lds[LDS_DOUBLES];
+
+  const int64_t wg = blockIdx.x;
+#ifdef GBM_DEBUG_WGTIME
+  const unsigned long long dbg_t0 = wall_clock64();
+#endif
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  const int frag_row = lane >> 4, frag_col = lane & 15;  // f64 MFMA C/D map: col = lane & 15, row = (lane >> 4) + 4 * reg
+  const int64_t nst = (K + BK - 1) / BK;
+  const int64_t rlim = c0 + lim;
+
+  if constexpr (MODE == kSplit) {
+    const int sl = (int)(wg / ntiles);
+    const int64_t t = wg - (int64_t)sl * ntiles;
+    int64_t ti, tj;
+    tile_of(t, ti, tj);
+    const bool diag = (ti == tj);
+    const int64_t i0 = c0 + ti * BT, j0 = c0 + tj * BT;
+    const bool active = (i0 + wm * 64 < rlim) && (j0 + wn * 64 < rlim) && !(diag && wm == 1 && wn == 0);
+    d4 acc[4][4];
 #pragma unroll
-    for (int m = 0; m < 4; m++)
+    for (int a = 0; a < 4; a++)
 #pragma unroll
-      for (int q = 0; q < 4; q++)
+      for (int b = 0; b < 4; b++) acc[a][b] = (d4){0.0, 0.0, 0.0, 0.0};
+    const int64_t ks0 = sb.b[sl];
+    const int64_t ks1 = sb.b[sl + 1] < nst ? sb.b[sl + 1] : nst;
+    tile_pass<false>(U, ldu, K, i0, j0, diag, active, ks0, ks1 > ks0 ? ks1 - ks0 : 0, lds, acc, wave, lane);
+    if (active) {
+      // a single slice stores straight into G (no workspace, the reduce is a no-op)
+      const int64_t ld = sb.n == 1 ? ldc : BT;
+      double* out = (sb.n == 1 ? C + i0 * ldc + j0 : slab + wg * (int64_t)(BT * BT)) + (wm * 64 + frag_row) * ld +
+                    wn * 64 + frag_col;
 #pragma unroll
-        for (int r = 0; r < 4; r++) {
-          const int row = wm * 64 + m * 16 + frag_row + 4 * r;
-          const int col = wn * 64 + q * 16 + frag_col;
-          out[row * BT + col] = acc[m][q][r];
-        }
+      for (int m = 0; m < 4; m++)
+#pragma unroll
+        for (int r = 0; r < 4; r++)
+#pragma unroll
+          for (int q = 0; q < 4; q++) out[(m * 16 + 4 * r) * ld + q * 16] = acc[m][q][r];
+    }
+#ifdef GBM_DEBUG_WGTIME
+    if (threadIdx.x == 0 && wg < 16384) {
+      g_wgtime[3 * wg] = dbg_t0;
+      g_wgtime[3 * wg + 1] = wall_clock64();
+      g_wgtime[3 * wg + 2] = (unsigned long long)__builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11)) |
+                             ((unsigned long long)__builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (31 << 11)) << 32);
+    }
+#endif
+    return;
   } else {
+    int64_t ti, tj;
+    tile_of(wg, ti, tj);
+    const bool diag = (ti == tj);
+    const int64_t i0 = c0 + ti * BT, j0 = c0 + tj * BT;
+    const bool active = (i0 + wm * 64 < rlim) && (j0 + wn * 64 < rlim) && !(diag && wm == 1 && wn == 0);
+    // the C tile goes straight into the accumulators (its loads overlap the operand staging)
+    // and the A fragments are negated: the MFMA chain produces C − Σ_k U[k][i] U[k][j]
+    d4 acc[4][4];
 #pragma unroll
     for (int m = 0; m < 4; m++)
 #pragma unroll
@@ -179,15 +210,25 @@ syrk_kernel(const double* __restrict__ U, int64_t ldu, int64_t K, int64_t c0, in
         for (int r = 0; r < 4; r++) {
           const int64_t row = i0 + wm * 64 + m * 16 + frag_row + 4 * r;
           const int64_t col = j0 + wn * 64 + q * 16 + frag_col;
-          if (active && row < rlim && col < rlim) {
-            C[row * ldc + col] = acc[m][q][r];
-          }
+          acc[m][q][r] = (active && row < rlim && col < rlim) ? C[row * ldc + col] : 0.0;
         }
-  }
-  if constexpr (MODE == kSub) {
+    tile_pass<true>(U, ldu, K, i0, j0, diag, active, 0, nst, lds, acc, wave, lane);
+    // first workgroup (tile (0,0)), fk0 >= 0: factor the next diagonal block afterwards
+    const bool factor_next = fk0 >= 0 && wg == 0;
+    if (!active && !factor_next) return;
+#pragma unroll
+    for (int m = 0; m < 4; m++)
+#pragma unroll
+      for (int q = 0; q < 4; q++)
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+          const int64_t row = i0 + wm * 64 + m * 16 + frag_row + 4 * r;
+          const int64_t col = j0 + wn * 64 + q * 16 + frag_col;
+          if (active && row < rlim && col < rlim) C[row * ldc + col] = acc[m][q][r];
+        }
     if (factor_next) {
       // the next panel's diagonal block [c0, c0+64)^2 is wave (0,0)'s 64x64 quadrant of this tile
-      double* Us = lds;  // the staging buffers are free now (last loop iteration ended in a barrier)
+      double* Us = lds;  // the staging buffers are free now (tile_pass ended in a barrier)
       double* rinv = lds + CNB * PS;
       if (wave == 0) {
 #pragma unroll
@@ -205,7 +246,7 @@ syrk_kernel(const double* __restrict__ U, int64_t ldu, int64_t K, int64_t c0, in
   }
 }
 
-// G tile = Σ_s slab[s][tile] in slice order (deterministic).
+// G tile = Σ_s slab[s][tile] in slice order (deterministic, no float atomics).
 __global__ void __launch_bounds__(256) grm_slab_reduce_kernel(const double* __restrict__ slab, int64_t ntiles,
                                                               int nslices, double* __restrict__ G, int64_t ldg) {
   const int64_t t = blockIdx.x;
@@ -214,8 +255,8 @@ __global__ void __launch_bounds__(256) grm_slab_reduce_kernel(const double* __re
   const int64_t per = (int64_t)BT * BT;
   for (int e = threadIdx.x * 2; e < BT * BT; e += 256 * 2) {
     double2 acc = make_double2(0.0, 0.0);
-    for (int s = 0; s < nslices; s++) {
-      const double2 v = *reinterpret_cast<const double2*>(slab + ((int64_t)s * ntiles + t) * per + e);
+    for (int sl = 0; sl < nslices; sl++) {
+      const double2 v = *reinterpret_cast<const double2*>(slab + ((int64_t)sl * ntiles + t) * per + e);
       acc.x += v.x;
       acc.y += v.y;
     }
@@ -233,25 +274,98 @@ static int resident_wgs() {
   return cus * WPS;  // WPS workgroups per CU (LDS 2 x 2 x BK x 1152 B each)
 }
 
-static void plan(int64_t n, int64_t p, int64_t& ntiles, int& nslices, int64_t& steps_per_slice) {
-  const int64_t nt = npad_of(n) / BT;
-  ntiles = nt * (nt + 1) / 2;
-  const int64_t nsteps = (p + BK - 1) / BK;
-  const int64_t R = resident_wgs();
-  int best = 1;
-  double best_eff = 0.0;
-  for (int S = 1; S <= 8; S++) {
-    if (S > 1 && nsteps / S < 16) break;  // keep >= 16 stages per workgroup
-    const int64_t w = ntiles * S;
-    const double eff = (double)w / (double)(R * ((w + R - 1) / R));
-    if (eff > best_eff + 0.05) {
-      best_eff = eff;
-      best = S;
-    }
-    if (eff >= 0.92) break;
+// Plan of the GRM loci split. Candidate partitions of a tile's nst stages — uniform (1..8
+// slices) and guided (one large first range, then geometrically shrinking ones) — are scored by
+// simulating the in-order dispatch of the ntiles x nslices workgroups onto the resident slots
+// (list scheduling; diagonal tiles ~7 % cheaper; slot speeds jittered by ~2 %, as measured with
+// GBM_DEBUG_WGTIME), plus the slab-reduce cost; the fastest wins. Cached per (n, p, slots).
+struct GrmPlan {
+  int64_t ntiles, nst;
+  SliceBounds sb;
+};
+
+static double simulate_split(const std::vector<int64_t>& sizes, int64_t nt, int64_t R) {
+  std::vector<double> speed(R);
+  uint64_t h = 0x9E3779B97F4A7C15ull;
+  for (int64_t k = 0; k < R; k++) {  // deterministic jitter, sd ≈ 2 %
+    h = h * 6364136223846793005ull + 1442695040888963407ull;
+    speed[k] = 1.0 + 0.035 * (((double)(h >> 11) / 9007199254740992.0) * 2.0 - 1.0);
   }
-  nslices = best;
-  steps_per_slice = (nsteps + nslices - 1) / nslices;
+  std::priority_queue<std::pair<double, int64_t>, std::vector<std::pair<double, int64_t>>, std::greater<>> slots;
+  for (int64_t k = 0; k < R; k++) slots.push({0.0, k});
+  double makespan = 0.0;
+  for (int64_t sz : sizes) {
+    int64_t t = 0;
+    for (int64_t tj = 0; tj < nt; tj++)
+      for (int64_t ti = 0; ti <= tj; ti++, t++) {
+        auto [f, k] = slots.top();
+        slots.pop();
+        f += (double)sz * (ti == tj ? 0.93 : 1.0) / speed[k];
+        if (f > makespan) makespan = f;
+        slots.push({f, k});
+      }
+  }
+  // slab reduce: one 128 KB tile partial read per (slice, tile) at ~4 TB/s, in units of stage
+  // time (~3.9 us per 16-locus stage of a 128x128 tile at 2 workgroups per CU)
+  const double reduce_stages = (double)sizes.size() * (double)(nt * (nt + 1) / 2) * 131072.0 / 4e12 / 3.9e-6;
+  return makespan + reduce_stages;
+}
+
+static GrmPlan plan(int64_t n, int64_t p) {
+  GrmPlan g;
+  const int64_t nt = npad_of(n) / BT;
+  g.ntiles = nt * (nt + 1) / 2;
+  g.nst = (p + BK - 1) / BK;
+  const int64_t R = resident_wgs();
+  static std::mutex mu;
+  static std::map<std::tuple<int64_t, int64_t, int64_t>, SliceBounds> cache;
+  std::lock_guard<std::mutex> lock(mu);
+  auto key = std::make_tuple(nt, g.nst, R);
+  auto it = cache.find(key);
+  if (it != cache.end()) {
+    g.sb = it->second;
+    return g;
+  }
+  const int64_t minc = 16;  // stages per workgroup at least
+  std::vector<std::vector<int64_t>> cands;
+  const bool big = g.ntiles > 2048;  // keep the one-off planning cost small for large n
+  for (int S = 1; S <= (big ? 3 : 8); S++) {
+    if (S > 1 && g.nst / S < minc) break;
+    std::vector<int64_t> v;
+    for (int i = 0; i < S; i++) v.push_back((g.nst * (i + 1)) / S - (g.nst * i) / S);
+    cands.push_back(v);
+  }
+  for (double f = big ? 0.60 : 0.40; f < 0.90; f += big ? 0.10 : 0.05)
+    for (double r : {0.3, 0.4, 0.5, 0.6, 0.7}) {
+      if (big && r != 0.5) continue;
+      std::vector<int64_t> v;
+      int64_t first = (int64_t)(f * (double)g.nst);
+      if (first < minc || g.nst - first < minc) continue;
+      v.push_back(first);
+      int64_t rem = g.nst - first;
+      while (rem > 0) {
+        int64_t c = (int64_t)std::ceil(r * (double)rem);
+        if (c < minc) c = minc;
+        if (rem - c < minc || (int)v.size() == kMaxSlices - 1) c = rem;
+        v.push_back(c);
+        rem -= c;
+      }
+      cands.push_back(v);
+    }
+  double best = 1e300;
+  std::vector<int64_t> bestv{g.nst};
+  for (const auto& v : cands) {
+    const double m = simulate_split(v, nt, R);
+    if (m < best * 0.999) {
+      best = m;
+      bestv = v;
+    }
+  }
+  g.sb.n = (int32_t)bestv.size();
+  g.sb.b[0] = 0;
+  for (int i = 0; i < g.sb.n; i++) g.sb.b[i + 1] = g.sb.b[i] + (int32_t)bestv[i];
+  cache.emplace(key, g.sb);
+  return g;
 }
 
 // Small-tile variant of the Cholesky trailing update (64x64 upper tiles, K = 64, 4 waves of
@@ -361,18 +475,15 @@ int launch_chol_update(double* G, int64_t ldg, int64_t k0, int64_t nb, int64_t g
   }
   const int64_t m = (lim + BT - 1) / BT;
   const int64_t ntiles = m * (m + 1) / 2;
-  const int64_t steps = (nb + BK - 1) / BK;
-  syrk_kernel<kSub><<<(unsigned)ntiles, 256, 0, s>>>(G + k0 * ldg, ldg, nb, k1, lim, G, ldg, nullptr, ntiles, steps,
-                                                     Ld, Dinv, info, next_k0);
+  syrk_kernel<kSub><<<(unsigned)ntiles, 256, 0, s>>>(G + k0 * ldg, ldg, nb, k1, lim, G, ldg, nullptr, ntiles, SliceBounds{}, Ld,
+                                                     Dinv, info, next_k0);
   GBM_LAUNCH_CHECK();
   return GBM_OK;
 }
 
 int64_t grm_workspace_bytes(int64_t n, int64_t p) {
-  int64_t ntiles, sps;
-  int S;
-  plan(n, p, ntiles, S, sps);
-  return S > 1 ? (int64_t)S * ntiles * BT * BT * (int64_t)sizeof(double) : 0;
+  const GrmPlan g = plan(n, p);
+  return g.sb.n == 1 ? 0 : (int64_t)g.sb.n * g.ntiles * BT * BT * (int64_t)sizeof(double);
 }
 
 static int check_grm_args(const double* Zt, int64_t ldz, int64_t p, int64_t n, double* G, int64_t ldg) {
@@ -383,37 +494,29 @@ static int check_grm_args(const double* Zt, int64_t ldz, int64_t p, int64_t n, d
   return GBM_OK;
 }
 
-// stage 1: the MFMA SYRK (writes G directly, or per-slice slabs into ws when split over loci)
+// stage 1: the MFMA SYRK (one partial tile per (slice, tile) into the workspace slabs)
 int launch_grm_syrk(const double* Zt, int64_t ldz, int64_t p, int64_t n, double* G, int64_t ldg, void* ws,
                     int64_t ws_bytes, hipStream_t s) {
   int rc = check_grm_args(Zt, ldz, p, n, G, ldg);
   if (rc != GBM_OK) return rc;
-  int64_t ntiles, sps;
-  int S;
-  plan(n, p, ntiles, S, sps);
-  const int64_t need = S > 1 ? (int64_t)S * ntiles * BT * BT * (int64_t)sizeof(double) : 0;
+  const GrmPlan g = plan(n, p);
+  const int64_t need = grm_workspace_bytes(n, p);
   if (need > 0 && (!ws || ws_bytes < need))
     return fail(GBM_E_ARG, "gbm_dev_grm: workspace too small (" + std::to_string(ws_bytes) + " < " +
                                std::to_string(need) + ")");
-  if (S == 1)
-    syrk_kernel<kStore><<<(unsigned)ntiles, 256, 0, s>>>(Zt, ldz, p, 0, n, G, ldg, nullptr, ntiles, sps, nullptr,
-                                                         nullptr, nullptr, -1);
-  else
-    syrk_kernel<kSlab><<<(unsigned)(ntiles * S), 256, 0, s>>>(Zt, ldz, p, 0, n, G, ldg, (double*)ws, ntiles, sps,
-                                                              nullptr, nullptr, nullptr, -1);
+  syrk_kernel<kSplit><<<(unsigned)(g.sb.n * g.ntiles), 256, 0, s>>>(Zt, ldz, p, 0, n, G, ldg, (double*)ws, g.ntiles,
+                                                                    g.sb, nullptr, nullptr, nullptr, -1);
   GBM_LAUNCH_CHECK();
   return GBM_OK;
 }
 
-// stage 2: sum the slabs (no-op when the plan did not split over loci)
+// stage 2: sum the slice partials of each tile into G
 int launch_grm_reduce(int64_t n, int64_t p, double* G, int64_t ldg, const void* ws, hipStream_t s) {
-  int64_t ntiles, sps;
-  int S;
-  plan(n, p, ntiles, S, sps);
-  if (S > 1) {
-    grm_slab_reduce_kernel<<<(unsigned)ntiles, 256, 0, s>>>((const double*)ws, ntiles, S, G, ldg);
-    GBM_LAUNCH_CHECK();
-  }
+  const GrmPlan g = plan(n, p);
+  if (g.sb.n == 1) return GBM_OK;
+  if (!ws) return fail(GBM_E_ARG, "gbm_dev_grm_reduce: workspace required");
+  grm_slab_reduce_kernel<<<(unsigned)g.ntiles, 256, 0, s>>>((const double*)ws, g.ntiles, g.sb.n, G, ldg);
+  GBM_LAUNCH_CHECK();
   return GBM_OK;
 }
 
@@ -443,11 +546,14 @@ extern "C" int gbm_dev_grm_reduce(int64_t n, int64_t p, double* G, int64_t ldg, 
   return gbm::launch_grm_reduce(n, p, G, ldg, workspace, (hipStream_t)stream);
 }
 
+#ifdef GBM_DEBUG_WGTIME
+extern "C" int gbm_debug_wgtime(void* host, int64_t count) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(gbm::g_wgtime), count * 3 * sizeof(unsigned long long)) == hipSuccess ? 0 : -1;
+}
+#endif
+
 extern "C" int gbm_dev_grm_slices(int64_t n, int64_t p) {
-  int64_t ntiles, sps;
-  int S;
-  gbm::plan(n, p, ntiles, S, sps);
-  return S;
+  return gbm::plan(n, p).sb.n;
 }
 
 namespace gbm {

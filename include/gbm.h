@@ -152,18 +152,20 @@ int gbm_dev_expand_dosage_i8(const int8_t* D, int64_t ldd, int64_t n, int64_t p,
 int gbm_dev_standardize(const double* Xt, int64_t ldx, int64_t p, int64_t n, double* Zt, int64_t ldz,
                         double* mean, double* sd, int32_t* keep, int64_t* q_dev, void* stream);
 
-/* G[0:npad, 0:npad] (lower-triangular 128x128 tiles, diagonal tiles in full) = Σ_j z_j z_jᵀ over
+/* G[0:npad, 0:npad] (upper-triangular 128x128 tiles: rows <= columns) = Σ_j z_j z_jᵀ over
  * the p locus rows of Zt (unscaled: the RCCL all-reduce of multi-GPU shards sums this).
  * fp64 MFMA SYRK; = gbm_dev_grm_syrk followed by gbm_dev_grm_reduce. Replaces the GRM product
  * of GenomicBreedingCore.grmsimple (called at reference src/gwas.jl:124). */
 int gbm_dev_grm(const double* Zt, int64_t ldz, int64_t p, int64_t n, double* G, int64_t ldg,
                 void* workspace, int64_t ws_bytes, void* stream);
 /* The two launches of gbm_dev_grm, separately (so a caller can time the SYRK kernel alone).
- * When gbm_dev_grm_slices(n, p) == 1 the SYRK writes G directly and the reduce is a no-op. */
+ * The SYRK splits the loci into ranges (gbm_dev_grm_slices of them) and writes one partial tile
+ * per range into the workspace, which the reduce sums into G in a fixed order (bit-reproducible
+ * run to run); with a single range the SYRK writes G directly and the reduce is a no-op. */
 int gbm_dev_grm_syrk(const double* Zt, int64_t ldz, int64_t p, int64_t n, double* G, int64_t ldg,
                      void* workspace, int64_t ws_bytes, void* stream);
 int gbm_dev_grm_reduce(int64_t n, int64_t p, double* G, int64_t ldg, const void* workspace, void* stream);
-/* Number of loci slices (split-K) the GRM plan uses for (n, p) on the current device. */
+/* Number of loci ranges (split-K slices) the GRM plan uses for (n, p) on the current device. */
 int gbm_dev_grm_slices(int64_t n, int64_t p);
 
 /*
