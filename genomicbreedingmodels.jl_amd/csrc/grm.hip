@@ -33,7 +33,7 @@ constexpr int BT = 128;            // tile edge
 #endif
 constexpr int BK = GBM_BK;         // loci per stage
 constexpr int WPS = GBM_WPS;       // target waves per SIMD (= resident 256-thread workgroups per CU)
-constexpr int LROW = BT + 16;      // LDS row pitch in doubles (1152 B)
+constexpr int LROW = BT + 2;       // LDS row pitch in doubles (1040 B ≡ 4 dwords mod 64 banks)
 constexpr int STAGE = 2 * BK * LROW;  // doubles per stage (A rows then B rows)
 
 __device__ __forceinline__ void tile_of(int64_t t, int64_t& ti, int64_t& tj) {
@@ -60,51 +60,67 @@ __device__ __forceinline__ void tile_pass(const double* __restrict__ U, int64_t 
                                           int64_t j0, bool diag, bool active, int64_t kstep0, int64_t nsteps,
                                           double* lds, d4 (&acc)[4][4], int wave, int lane) {
   const int wm = wave >> 1, wn = wave & 1;
-  // each wave stages BK/4 locus rows r = wave*BK/4 .. of A (and of B off-diagonal)
-  auto stage = [&](int64_t kstep, int buf) {
+  // each wave stages BK/4 locus rows r = wave*BK/4 + rr of A (and of B off-diagonal)
+  auto stage_row = [&](int64_t kstep, int buf, int rr) {
     double* base = lds + buf * STAGE;
-#pragma unroll
-    for (int rr = 0; rr < BK / 4; rr++) {
-      const int r = wave * (BK / 4) + rr;
-      const int64_t k = kstep * BK + r;
-      double* la = base + r * LROW;
-      double* lb = base + (BK + r) * LROW;
-      if (k < K) {
-#ifdef GBM_DEBUG_SAMEROWS  // timing experiment only: operands stay L2-resident (wrong results)
-        const double* src = U + (k & 63) * ldu;
+    const int r = wave * (BK / 4) + rr;
+    const int64_t k = kstep * BK + r;
+    double* la = base + r * LROW;
+    double* lb = base + (BK + r) * LROW;
+#ifdef GBM_DEBUG_NOKCHECK  // timing experiment only: no ragged-K guard (reads past K)
+    if (true) {
 #else
-        const double* src = U + k * ldu;
+    if (k < K) {
 #endif
-        __builtin_amdgcn_global_load_lds((const void*)(src + i0 + lane * 2), (void*)la, 16, 0, 0);
-        if (!diag) __builtin_amdgcn_global_load_lds((const void*)(src + j0 + lane * 2), (void*)lb, 16, 0, 0);
-      } else {
-        *reinterpret_cast<double2*>(la + lane * 2) = make_double2(0.0, 0.0);
-        if (!diag) *reinterpret_cast<double2*>(lb + lane * 2) = make_double2(0.0, 0.0);
-      }
+#ifdef GBM_DEBUG_SAMEROWS  // timing experiment only: operands stay L2-resident (wrong results)
+      const double* src = U + (k & 63) * ldu;
+#else
+      const double* src = U + k * ldu;
+#endif
+      __builtin_amdgcn_global_load_lds((const void*)(src + i0 + lane * 2), (void*)la, 16, 0, 0);
+      if (!diag) __builtin_amdgcn_global_load_lds((const void*)(src + j0 + lane * 2), (void*)lb, 16, 0, 0);
+    } else {
+      *reinterpret_cast<double2*>(la + lane * 2) = make_double2(0.0, 0.0);
+      if (!diag) *reinterpret_cast<double2*>(lb + lane * 2) = make_double2(0.0, 0.0);
     }
   };
   const int frag_row = lane >> 4;  // k within a 4-deep MFMA step
   const int frag_col = lane & 15;
 
-  if (nsteps > 0) stage(kstep0, 0);
+  if (nsteps > 0) {
+#pragma unroll
+    for (int rr = 0; rr < BK / 4; rr++) stage_row(kstep0, 0, rr);
+  }
   __syncthreads();
   for (int64_t st = 0; st < nsteps; st++) {
     const int buf = (int)(st & 1);
-    if (st + 1 < nsteps) stage(kstep0 + st + 1, buf ^ 1);
-    if (active) {
-      const double* A = lds + buf * STAGE;
-      const double* B = diag ? A : A + BK * LROW;
+    // the next stage's rows go out first, all together (issuing them one per k-step between
+    // the MFMA groups measured 3 % slower)
+#ifndef GBM_DEBUG_NOSTAGE  // timing experiment only: operands never refreshed (wrong results)
+    if (st + 1 < nsteps) {
 #pragma unroll
-      for (int ks = 0; ks < BK / 4; ks++) {
+      for (int rr = 0; rr < BK / 4; rr++) stage_row(kstep0 + st + 1, buf ^ 1, rr);
+    }
+#endif
+    const double* A = lds + buf * STAGE;
+    const double* B = diag ? A : A + BK * LROW;
+#pragma unroll
+    for (int ks = 0; ks < BK / 4; ks++) {
+      if (active) {
         const int kr = ks * 4 + frag_row;
-        double af[4], bf[4];
+        // interleaved wave tile: MFMA tile m holds quadrant rows 4ρ + m (ρ = MFMA row), tile q
+        // holds quadrant columns 4γ + q, so a lane's four A (B) operands are adjacent: two
+        // ds_read_b128 each (conflict-free at the 1040-B pitch)
+        const double2 a01 = *reinterpret_cast<const double2*>(&A[kr * LROW + wm * 64 + 4 * frag_col]);
+        const double2 a23 = *reinterpret_cast<const double2*>(&A[kr * LROW + wm * 64 + 4 * frag_col + 2]);
+        const double2 b01 = *reinterpret_cast<const double2*>(&B[kr * LROW + wn * 64 + 4 * frag_col]);
+        const double2 b23 = *reinterpret_cast<const double2*>(&B[kr * LROW + wn * 64 + 4 * frag_col + 2]);
+        double af[4] = {a01.x, a01.y, a23.x, a23.y};
+        const double bf[4] = {b01.x, b01.y, b23.x, b23.y};
+        if constexpr (NEG) {
 #pragma unroll
-        for (int m = 0; m < 4; m++) {
-          af[m] = A[kr * LROW + wm * 64 + m * 16 + frag_col];
-          if constexpr (NEG) af[m] = -af[m];
+          for (int m = 0; m < 4; m++) af[m] = -af[m];
         }
-#pragma unroll
-        for (int q = 0; q < 4; q++) bf[q] = B[kr * LROW + wn * 64 + q * 16 + frag_col];
 #pragma unroll
         for (int m = 0; m < 4; m++)
 #pragma unroll
@@ -112,8 +128,13 @@ __device__ __forceinline__ void tile_pass(const double* __restrict__ U, int64_t 
             acc[m][q] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[m], bf[q], acc[m][q], 0, 0, 0);
       }
     }
+#ifdef GBM_DEBUG_NOBARRIER  // timing experiment only: racy (wrong results)
+    __builtin_amdgcn_s_waitcnt(0);
+#else
     __syncthreads();
+#endif
   }
+  __syncthreads();
 }
 
 // Loci split of the GRM: every tile is cut into the same nslices stage ranges
@@ -152,7 +173,10 @@ syrk_kernel(const double* __restrict__ U, int64_t ldu, int64_t K, int64_t c0, in
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wm = wave >> 1, wn = wave & 1;
-  const int frag_row = lane >> 4, frag_col = lane & 15;  // f64 MFMA C/D map: col = lane & 15, row = (lane >> 4) + 4 * reg
+  // f64 MFMA C/D map: MFMA column = lane & 15, MFMA row = (lane >> 4) + 4 * reg; with the
+  // interleaved wave tile (tile_pass), acc[m][q][r] is quadrant element
+  // (row 4 * frag_row + 16 * r + m, column 4 * frag_col + q)
+  const int frag_row = lane >> 4, frag_col = lane & 15;
   const int64_t nst = (K + BK - 1) / BK;
   const int64_t rlim = c0 + lim;
 
@@ -175,14 +199,16 @@ syrk_kernel(const double* __restrict__ U, int64_t ldu, int64_t K, int64_t c0, in
     if (active) {
       // a single slice stores straight into G (no workspace, the reduce is a no-op)
       const int64_t ld = sb.n == 1 ? ldc : BT;
-      double* out = (sb.n == 1 ? C + i0 * ldc + j0 : slab + wg * (int64_t)(BT * BT)) + (wm * 64 + frag_row) * ld +
-                    wn * 64 + frag_col;
+      double* out = (sb.n == 1 ? C + i0 * ldc + j0 : slab + wg * (int64_t)(BT * BT)) +
+                    (wm * 64 + 4 * frag_row) * ld + wn * 64 + 4 * frag_col;
 #pragma unroll
       for (int m = 0; m < 4; m++)
 #pragma unroll
-        for (int r = 0; r < 4; r++)
-#pragma unroll
-          for (int q = 0; q < 4; q++) out[(m * 16 + 4 * r) * ld + q * 16] = acc[m][q][r];
+        for (int r = 0; r < 4; r++) {
+          double* o = out + (16 * r + m) * ld;
+          *reinterpret_cast<double2*>(o) = make_double2(acc[m][0][r], acc[m][1][r]);
+          *reinterpret_cast<double2*>(o + 2) = make_double2(acc[m][2][r], acc[m][3][r]);
+        }
     }
 #ifdef GBM_DEBUG_WGTIME
     if (threadIdx.x == 0 && wg < 16384) {
@@ -202,16 +228,23 @@ syrk_kernel(const double* __restrict__ U, int64_t ldu, int64_t K, int64_t c0, in
     // the C tile goes straight into the accumulators (its loads overlap the operand staging)
     // and the A fragments are negated: the MFMA chain produces C − Σ_k U[k][i] U[k][j]
     d4 acc[4][4];
+    // (rlim is a multiple of 4: a lane's 4 adjacent columns are in or out together)
+    const int64_t col0 = j0 + wn * 64 + 4 * frag_col;
 #pragma unroll
     for (int m = 0; m < 4; m++)
 #pragma unroll
-      for (int q = 0; q < 4; q++)
-#pragma unroll
-        for (int r = 0; r < 4; r++) {
-          const int64_t row = i0 + wm * 64 + m * 16 + frag_row + 4 * r;
-          const int64_t col = j0 + wn * 64 + q * 16 + frag_col;
-          acc[m][q][r] = (active && row < rlim && col < rlim) ? C[row * ldc + col] : 0.0;
+      for (int r = 0; r < 4; r++) {
+        const int64_t row = i0 + wm * 64 + 4 * frag_row + 16 * r + m;
+        double2 c01 = make_double2(0.0, 0.0), c23 = make_double2(0.0, 0.0);
+        if (active && row < rlim && col0 < rlim) {
+          c01 = *reinterpret_cast<const double2*>(C + row * ldc + col0);
+          c23 = *reinterpret_cast<const double2*>(C + row * ldc + col0 + 2);
         }
+        acc[m][0][r] = c01.x;
+        acc[m][1][r] = c01.y;
+        acc[m][2][r] = c23.x;
+        acc[m][3][r] = c23.y;
+      }
     tile_pass<true>(U, ldu, K, i0, j0, diag, active, 0, nst, lds, acc, wave, lane);
     // first workgroup (tile (0,0)), fk0 >= 0: factor the next diagonal block afterwards
     const bool factor_next = fk0 >= 0 && wg == 0;
@@ -219,13 +252,13 @@ syrk_kernel(const double* __restrict__ U, int64_t ldu, int64_t K, int64_t c0, in
 #pragma unroll
     for (int m = 0; m < 4; m++)
 #pragma unroll
-      for (int q = 0; q < 4; q++)
-#pragma unroll
-        for (int r = 0; r < 4; r++) {
-          const int64_t row = i0 + wm * 64 + m * 16 + frag_row + 4 * r;
-          const int64_t col = j0 + wn * 64 + q * 16 + frag_col;
-          if (active && row < rlim && col < rlim) C[row * ldc + col] = acc[m][q][r];
+      for (int r = 0; r < 4; r++) {
+        const int64_t row = i0 + wm * 64 + 4 * frag_row + 16 * r + m;
+        if (active && row < rlim && col0 < rlim) {
+          *reinterpret_cast<double2*>(C + row * ldc + col0) = make_double2(acc[m][0][r], acc[m][1][r]);
+          *reinterpret_cast<double2*>(C + row * ldc + col0 + 2) = make_double2(acc[m][2][r], acc[m][3][r]);
         }
+      }
     if (factor_next) {
       // the next panel's diagonal block [c0, c0+64)^2 is wave (0,0)'s 64x64 quadrant of this tile
       double* Us = lds;  // the staging buffers are free now (tile_pass ended in a barrier)
@@ -236,7 +269,7 @@ syrk_kernel(const double* __restrict__ U, int64_t ldu, int64_t K, int64_t c0, in
 #pragma unroll
           for (int q = 0; q < 4; q++)
 #pragma unroll
-            for (int r = 0; r < 4; r++) Us[(m * 16 + frag_row + 4 * r) * PS + q * 16 + frag_col] = acc[m][q][r];
+            for (int r = 0; r < 4; r++) Us[(4 * frag_row + 16 * r + m) * PS + 4 * frag_col + q] = acc[m][q][r];
       }
       __syncthreads();
       const int bad = factor_diag_block(Us, rinv, threadIdx.x);
@@ -488,9 +521,10 @@ int64_t grm_workspace_bytes(int64_t n, int64_t p) {
 
 static int check_grm_args(const double* Zt, int64_t ldz, int64_t p, int64_t n, double* G, int64_t ldg) {
   const int64_t npad = npad_of(n);
-  if (!Zt || !G || p < 1 || n < 1 || ldz < npad || ldg < npad || (ldz & 1))
-    return fail(GBM_E_ARG, "gbm_dev_grm: bad arguments (need ldz, ldg >= npad(n), even ldz)");
-  if (((uintptr_t)Zt & 15) != 0) return fail(GBM_E_ARG, "gbm_dev_grm: Zt must be 16-byte aligned");
+  if (!Zt || !G || p < 1 || n < 1 || ldz < npad || ldg < npad || (ldz & 1) || (ldg & 1))
+    return fail(GBM_E_ARG, "gbm_dev_grm: bad arguments (need ldz, ldg >= npad(n), both even)");
+  if (((uintptr_t)Zt & 15) != 0 || ((uintptr_t)G & 15) != 0)
+    return fail(GBM_E_ARG, "gbm_dev_grm: Zt and G must be 16-byte aligned");
   return GBM_OK;
 }
 

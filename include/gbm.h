@@ -154,6 +154,7 @@ int gbm_dev_standardize(const double* Xt, int64_t ldx, int64_t p, int64_t n, dou
 
 /* G[0:npad, 0:npad] (upper-triangular 128x128 tiles: rows <= columns) = Σ_j z_j z_jᵀ over
  * the p locus rows of Zt (unscaled: the RCCL all-reduce of multi-GPU shards sums this).
+ * Zt and G 16-byte aligned, ldz and ldg even and >= gbm_dev_npad(n).
  * fp64 MFMA SYRK; = gbm_dev_grm_syrk followed by gbm_dev_grm_reduce. Replaces the GRM product
  * of GenomicBreedingCore.grmsimple (called at reference src/gwas.jl:124). */
 int gbm_dev_grm(const double* Zt, int64_t ldz, int64_t p, int64_t n, double* G, int64_t ldg,
