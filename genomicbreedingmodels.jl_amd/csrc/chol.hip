@@ -25,6 +25,9 @@ constexpr int MAXRHS = 63;
 
 int launch_chol_update(double* G, int64_t ldg, int64_t k0, int64_t nb, int64_t gdim, double* Ld, double* Dinv,
                        int32_t* info, int64_t next_k0, hipStream_t s);
+int launch_chol_row_update(double* G, int64_t ldg, int64_t k0, int64_t gdim, double* Ld, double* Dinv,
+                           int32_t* info, hipStream_t s);
+int64_t chol_small_lim();
 
 // ---- V = G/q + λI (upper part), padding = identity, bordered R columns -----------------------
 __global__ void __launch_bounds__(256) prepare_v_kernel(double* __restrict__ G, int64_t ld, int64_t n,
@@ -188,35 +191,55 @@ __global__ void __launch_bounds__(256) back_diag_kernel(const double* __restrict
                                                         int64_t lda, int64_t nrhs) {
   __shared__ double Ui[SB][NB][NB + 1];  // Ui[sb][i][j] = (U_bb⁻¹)[i][j], b = s0/64 + sb
   __shared__ double wl[RC][SB * NB];
+  __shared__ double part[4][RC][NB];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int len = nsub * NB;
-  for (int e = tid * 2; e < len * NB; e += 512) {
-    const int rr = e / NB, cc = e % NB;
-    const double2 v = *reinterpret_cast<const double2*>(Linv + (s0 + rr) * NB + cc);
-    Ui[rr / NB][rr % NB][cc] = v.x;
-    Ui[rr / NB][rr % NB][cc + 1] = v.y;
+  // stage the inverses with every load in flight before the first LDS store (latency-bound kernel)
+  for (int base = 0; base < len * NB; base += 16 * 512) {
+    double2 v[16];
+#pragma unroll
+    for (int u = 0; u < 16; u++) {
+      const int e = base + u * 512 + tid * 2;
+      v[u] = e < len * NB ? *reinterpret_cast<const double2*>(Linv + s0 * NB + e) : make_double2(0.0, 0.0);
+    }
+#pragma unroll
+    for (int u = 0; u < 16; u++) {
+      const int e = base + u * 512 + tid * 2;
+      if (e < len * NB) {
+        const int rr = e / NB, cc = e % NB;
+        Ui[rr / NB][rr % NB][cc] = v[u].x;
+        Ui[rr / NB][rr % NB][cc + 1] = v[u].y;
+      }
+    }
   }
   for (int64_t t0 = 0; t0 < nrhs; t0 += RC) {
     const int tc = (int)(nrhs - t0 < RC ? nrhs - t0 : RC);
     for (int e = tid; e < tc * len; e += 256) wl[e / len][e % len] = W[(t0 + e / len) * lda + s0 + e % len];
     __syncthreads();
     for (int sb = nsub - 1; sb >= 0; sb--) {
-      if (wave == 0) {
-        // a_b = U_bb⁻ᵀ... in Lᵀ-form: Lᵀ = U, so a_b = U_bb⁻¹ w_b — a 64x64 GEMV, no serial chain
-        for (int t = 0; t < tc; t++) {
-          double acc = 0.0;
-#pragma unroll 16
-          for (int j = 0; j < NB; j++) acc += Ui[sb][lane][j] * wl[t][sb * NB + j];
-          wl[t][sb * NB + lane] = acc;
-        }
-      }
-      __syncthreads();
-      if (sb > 0 && tid < sb * NB) {  // earlier rows of the super-block (column tid)
-        double acc[RC] = {0.0, 0.0, 0.0, 0.0};
+      // couplings of the earlier rows of the super-block to this block (column tid): loads first,
+      // they do not depend on a_b
+      const bool couple = sb > 0 && tid < sb * NB;
+      double l[NB];
+      if (couple) {
         const double* lp = G + (s0 + sb * NB) * ld + s0 + tid;
-        double l[NB];
 #pragma unroll
         for (int u = 0; u < NB; u++) l[u] = lp[(int64_t)u * ld];
+      }
+      // a_b = U_bb⁻¹ w_b (Lᵀ = U): a 64x64 GEMV, the j range split over the 4 waves
+      for (int t = 0; t < tc; t++) {
+        double acc = 0.0;
+#pragma unroll
+        for (int j = 0; j < 16; j++) acc += Ui[sb][lane][wave * 16 + j] * wl[t][sb * NB + wave * 16 + j];
+        part[wave][t][lane] = acc;
+      }
+      __syncthreads();
+      if (wave == 0)
+        for (int t = 0; t < tc; t++)
+          wl[t][sb * NB + lane] = ((part[0][t][lane] + part[1][t][lane]) + part[2][t][lane]) + part[3][t][lane];
+      __syncthreads();
+      if (couple) {
+        double acc[RC] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
         for (int u = 0; u < NB; u++)
 #pragma unroll
@@ -312,13 +335,32 @@ extern "C" int gbm_dev_gblup_solve(double* G, int64_t ldg, int64_t n, double inv
   const int64_t nb = npad / NB;
   factor_first_kernel<<<1, 256, 0, s>>>(G, ldg, Ld, Dinv, info);
   GBM_LAUNCH_CHECK();
-  for (int64_t kb = 0; kb < nb; kb++) {
-    const int64_t k0 = kb * NB;
+  static const bool pair_panels = [] {
+    const char* e = getenv("GBM_CHOL_PAIRS");
+    return !e || atoi(e) != 0;
+  }();
+  auto panel = [&](int64_t k0) {
     const int64_t chunks = (gdim - k0) / NB - 1;  // column chunks right of the diagonal block
     chol_panel_kernel<<<(unsigned)chunks, 256, 0, s>>>(G, ldg, k0, Ld, Dinv);
-    GBM_LAUNCH_CHECK();
-    // trailing update; its first workgroup also factors the next diagonal block
-    int rc = launch_chol_update(G, ldg, k0, NB, gdim, Ld, Dinv, info, kb + 1 < nb ? k0 + NB : -1, s);
+    return hipGetLastError() == hipSuccess;
+  };
+  for (int64_t kb = 0; kb < nb;) {
+    const int64_t k0 = kb * NB;
+    if (!panel(k0)) return fail(GBM_E_HIP, "chol_panel_kernel launch failed");
+    int rc;
+    if (pair_panels && kb + 2 < nb && gdim - (k0 + 2 * NB) > chol_small_lim()) {
+      // two panels per pass over the trailing matrix (it is HBM/MALL-bound at K = 64): update
+      // only the next panel's rows, factor that panel, then one K = 128 trailing update
+      rc = launch_chol_row_update(G, ldg, k0, gdim, Ld, Dinv, info, s);
+      if (rc != GBM_OK) return rc;
+      if (!panel(k0 + NB)) return fail(GBM_E_HIP, "chol_panel_kernel launch failed");
+      rc = launch_chol_update(G, ldg, k0, 2 * NB, gdim, Ld, Dinv, info, k0 + 2 * NB, s);
+      kb += 2;
+    } else {
+      // trailing update; its first workgroup also factors the next diagonal block
+      rc = launch_chol_update(G, ldg, k0, NB, gdim, Ld, Dinv, info, kb + 1 < nb ? k0 + NB : -1, s);
+      kb += 1;
+    }
     if (rc != GBM_OK) return rc;
   }
   diag_inverse_kernel<<<(unsigned)nb, 64, 0, s>>>(Ld, Linv);

@@ -409,11 +409,11 @@ constexpr int P64 = 80;  // LDS pitch: the two 16-lane halves of a fragment read
 __global__ void __launch_bounds__(256, 2)
 syrk64_sub_kernel(const double* __restrict__ U, int64_t ldu, int64_t c0, int64_t lim, double* __restrict__ C,
                   int64_t ldc, double* __restrict__ Ld, double* __restrict__ Dinv, int32_t* __restrict__ info,
-                  int64_t fk0) {
+                  int64_t fk0, int rowonly) {
   __shared__ __attribute__((aligned(16))) double As[64 * P64];
   __shared__ __attribute__((aligned(16))) double Bs[64 * P64];
-  int64_t ti, tj;
-  tile_of(blockIdx.x, ti, tj);
+  int64_t ti = 0, tj = blockIdx.x;  // rowonly: the first tile row only (the next panel's rows)
+  if (!rowonly) tile_of(blockIdx.x, ti, tj);
   const bool diag = ti == tj;
   const int64_t i0 = c0 + ti * 64, j0 = c0 + tj * 64;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -489,20 +489,37 @@ syrk64_sub_kernel(const double* __restrict__ U, int64_t ldu, int64_t c0, int64_t
   }
 }
 
+int64_t chol_small_lim() {
+  static const int64_t v = [] {
+    const char* e = getenv("GBM_UPD64_LIM");
+    return e ? (int64_t)atoll(e) : (int64_t)2048;
+  }();
+  return v;
+}
+
+// Block row [k0+64, k0+128) only: C[k0+64 : k0+128, k0+64 : gdim] -= U[k0:k0+64, ·]ᵀ U[k0:k0+64, ·]
+// (the next panel's rows, so that two panels can share one K = 128 trailing update); the first
+// workgroup factors the diagonal block at k0+64 afterwards.
+int launch_chol_row_update(double* G, int64_t ldg, int64_t k0, int64_t gdim, double* Ld, double* Dinv,
+                           int32_t* info, hipStream_t s) {
+  const int64_t k1 = k0 + 64;
+  const int64_t lim = gdim - k1;
+  syrk64_sub_kernel<<<(unsigned)(lim / 64), 256, 0, s>>>(G + k0 * ldg, ldg, k1, lim, G, ldg, Ld, Dinv, info, k1, 1);
+  GBM_LAUNCH_CHECK();
+  return GBM_OK;
+}
+
 // Upper-Cholesky trailing update: C[k1:gdim, k1:gdim] (upper tiles) -= U[k0:k1, k1:]ᵀ U[k0:k1, k1:]
+// with k1 = k0 + nb (nb = 64, or 128 for two panels at once)
 int launch_chol_update(double* G, int64_t ldg, int64_t k0, int64_t nb, int64_t gdim, double* Ld, double* Dinv,
                        int32_t* info, int64_t next_k0, hipStream_t s) {
   const int64_t k1 = k0 + nb;
   const int64_t lim = gdim - k1;
   if (lim <= 0) return GBM_OK;
-  static const int64_t small_lim = [] {
-    const char* e = getenv("GBM_UPD64_LIM");
-    return e ? (int64_t)atoll(e) : (int64_t)2048;
-  }();
-  if (nb == 64 && lim <= small_lim) {
+  if (nb == 64 && lim <= chol_small_lim()) {
     const int64_t m = (lim + 63) / 64;
     syrk64_sub_kernel<<<(unsigned)(m * (m + 1) / 2), 256, 0, s>>>(G + k0 * ldg, ldg, k1, lim, G, ldg, Ld, Dinv, info,
-                                                                  next_k0);
+                                                                  next_k0, 0);
     GBM_LAUNCH_CHECK();
     return GBM_OK;
   }
