@@ -12,6 +12,7 @@
 #include <vector>
 
 #include "gbm_internal.h"
+#include "host_util.h"
 
 namespace gbm {
 
@@ -24,78 +25,6 @@ int fail(int code, const std::string& msg) {
 }
 
 namespace {
-
-// RAII device allocation on a given device
-struct DevMem {
-  void* p = nullptr;
-  int dev = 0;
-  DevMem() = default;
-  DevMem(const DevMem&) = delete;
-  DevMem& operator=(const DevMem&) = delete;
-  ~DevMem() {
-    if (p) {
-      int cur = 0;
-      (void)hipGetDevice(&cur);
-      (void)hipSetDevice(dev);
-      (void)hipFree(p);
-      (void)hipSetDevice(cur);
-    }
-  }
-};
-
-int dalloc(DevMem& m, int dev, int64_t bytes) {
-  m.dev = dev;
-  if (bytes <= 0) bytes = 16;
-  hipError_t e = hipMalloc(&m.p, (size_t)bytes);
-  if (e != hipSuccess) {
-    m.p = nullptr;
-    (void)hipGetLastError();
-    return fail(e == hipErrorOutOfMemory ? GBM_E_OOM : GBM_E_HIP,
-                std::string("device allocation of ") + std::to_string(bytes) + " bytes on device " + std::to_string(dev) +
-                    " failed: " + hipGetErrorString(e));
-  }
-  return GBM_OK;
-}
-
-struct Stream {
-  hipStream_t s = nullptr;
-  int dev = 0;
-  ~Stream() {
-    if (s) {
-      (void)hipSetDevice(dev);
-      (void)hipStreamDestroy(s);
-    }
-  }
-};
-
-#define GBM_TRY(expr)            \
-  do {                           \
-    int rc_ = (expr);            \
-    if (rc_ != GBM_OK) return rc_; \
-  } while (0)
-
-int check_devices(const int* devices, int ndev, std::vector<int>& out) {
-  int count = 0;
-  hipError_t e = hipGetDeviceCount(&count);
-  if (e != hipSuccess || count < 1) {
-    (void)hipGetLastError();
-    return fail(GBM_E_NODEV, "no HIP device available (libgbm requires an MI355X / gfx950 GPU)");
-  }
-  out.clear();
-  if (!devices || ndev <= 0) {
-    out.push_back(0);
-  } else {
-    for (int k = 0; k < ndev; k++) {
-      if (devices[k] < 0 || devices[k] >= count)
-        return fail(GBM_E_ARG, "device ordinal " + std::to_string(devices[k]) + " out of range [0, " +
-                                   std::to_string(count) + ")");
-      for (int d : out)
-        if (d == devices[k]) return fail(GBM_E_ARG, "duplicate device ordinal " + std::to_string(d));
-      out.push_back(devices[k]);
-    }
-  }
-  return GBM_OK;
-}
 
 // One SNP-column shard resident on one device.
 struct Shard {
@@ -178,26 +107,6 @@ int allreduce_grm(std::vector<std::unique_ptr<Shard>>& shards, int64_t n) {
   }
   for (auto c : comms) (void)ncclCommDestroy(c);
   return rc;
-}
-
-int check_y(const double* Y, int64_t n, int64_t ldy, int64_t nrhs) {
-  for (int64_t t = 0; t < nrhs; t++) {
-    const double* y = Y + t * ldy;
-    double s = 0.0;
-    for (int64_t i = 0; i < n; i++) {
-      if (!std::isfinite(y[i]))
-        return fail(GBM_E_ARG, "phenotype " + std::to_string(t + 1) + " has a missing/NaN/Inf value at entry " +
-                                   std::to_string(i + 1) + " (filter it first, reference src/prediction.jl:114-124)");
-      s += y[i];
-    }
-    const double m = s / (double)n;
-    double ss = 0.0;
-    for (int64_t i = 0; i < n; i++) ss += (y[i] - m) * (y[i] - m);
-    if (ss / (double)(n - 1) < 1e-20)
-      return fail(GBM_E_DATA, "very low or zero variance in trait " + std::to_string(t + 1) +
-                                  " (reference src/prediction.jl:125-127)");
-  }
-  return GBM_OK;
 }
 
 int run_fit(const Problem& pr, const double* Y, int64_t ldy, int64_t nrhs, double lambda, const int* devices, int ndev,

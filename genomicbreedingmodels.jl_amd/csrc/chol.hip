@@ -176,6 +176,32 @@ __global__ void __launch_bounds__(256) gls_mu_kernel(const double* __restrict__ 
     W[t * lda + i] = i < npad ? G[(npad + 1 + t) * ld + i] - m * G[npad * ld + i] : 0.0;
 }
 
+// ---- REML ingredients of a finished solve (one workgroup) ------------------------------------
+// terms[0] = logdet V = 2 Σ_i log U_ii (from the factored diagonal blocks in Ld; padding rows are
+// identity and add log 1 = 0); terms[1] = 1ᵀV⁻¹1; terms[2 + 2t] = 1ᵀV⁻¹y_t; terms[3 + 2t] =
+// y_tᵀV⁻¹y_t — the bordered Schur block ends as −WᵀW with W = U⁻ᵀ[1, y].
+__global__ void __launch_bounds__(256) gblup_terms_kernel(const double* __restrict__ G, int64_t ld, int64_t npad,
+                                                          int64_t nrhs, const double* __restrict__ Ld,
+                                                          double* __restrict__ terms) {
+  __shared__ double red[256];
+  double sacc = 0.0;
+  for (int64_t r = threadIdx.x; r < npad; r += 256) sacc += log(Ld[r * NB + (r % NB)]);
+  red[threadIdx.x] = sacc;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    terms[0] = 2.0 * red[0];
+    terms[1] = -G[npad * ld + npad];
+  }
+  for (int64_t t = threadIdx.x; t < nrhs; t += 256) {
+    terms[2 + 2 * t] = -G[npad * ld + npad + 1 + t];
+    terms[3 + 2 * t] = -G[(npad + 1 + t) * ld + npad + 1 + t];
+  }
+}
+
 // ---- back substitution Lᵀ a = w (L = Uᵀ in the lower triangle) over super-blocks --------------
 // Per super-block [s0, s0 + 64*nsub), last to first, two launches:
 //   back_diag_kernel (1 workgroup): solve the super-block — diagonal 64-blocks from Ld (stored as
@@ -381,6 +407,16 @@ extern "C" int gbm_dev_gblup_solve(double* G, int64_t ldg, int64_t n, double inv
     end_blk -= nsub;
   }
   gebv_kernel<<<dim3(gx, (unsigned)nrhs), 256, 0, s>>>(Y, ldy, n, A_out, gebv, lda, mu, lambda);
+  GBM_LAUNCH_CHECK();
+  return GBM_OK;
+}
+
+extern "C" int gbm_dev_gblup_terms(const double* G, int64_t ldg, int64_t n, int64_t nrhs, const void* workspace,
+                                   double* terms, void* stream) {
+  if (!G || !workspace || !terms || n < 1 || nrhs < 1 || nrhs > MAXRHS || ldg < gdim_of(n))
+    return fail(GBM_E_ARG, "gbm_dev_gblup_terms: bad arguments");
+  gblup_terms_kernel<<<1, 256, 0, (hipStream_t)stream>>>(G, ldg, npad_of(n), nrhs, (const double*)workspace,
+                                                         terms);
   GBM_LAUNCH_CHECK();
   return GBM_OK;
 }

@@ -63,8 +63,9 @@ __device__ __forceinline__ double block_sum(double v, double* red) {
 
 // One workgroup per locus row (grid-strided). NPT = values cached in registers per thread
 // (0 = generic path re-reading the row from L2/MALL).
-template <int BS, int NPT>
+template <int BS, int NPT, bool GATHER>
 __global__ void __launch_bounds__(BS) standardize_kernel(const double* Xt, int64_t ldx, int64_t p,
+                                                         const int32_t* __restrict__ idx,
                                                          int64_t n, double* Zt, int64_t ldz,
                                                          double* __restrict__ mean,
                                                          double* __restrict__ sd, int32_t* __restrict__ keep,
@@ -81,7 +82,7 @@ __global__ void __launch_bounds__(BS) standardize_kernel(const double* Xt, int64
 #pragma unroll
       for (int k = 0; k < NPT; k++) {
         const int64_t i = (int64_t)k * BS + threadIdx.x;
-        x[k] = i < n ? row[i] : 0.0;
+        x[k] = i < n ? row[GATHER ? idx[i] : i] : 0.0;
         s += x[k];
       }
       m = block_sum<BS>(s, red) / (double)n;
@@ -109,17 +110,17 @@ __global__ void __launch_bounds__(BS) standardize_kernel(const double* Xt, int64
       }
     } else {
       double s = 0.0;
-      for (int64_t i = threadIdx.x; i < n; i += BS) s += row[i];
+      for (int64_t i = threadIdx.x; i < n; i += BS) s += row[GATHER ? idx[i] : i];
       m = block_sum<BS>(s, red) / (double)n;
       double ss = 0.0;
       for (int64_t i = threadIdx.x; i < n; i += BS) {
-        const double d = row[i] - m;
+        const double d = row[GATHER ? idx[i] : i] - m;
         ss += d * d;
       }
       v = n > 1 ? sqrt(block_sum<BS>(ss, red) / (double)(n - 1)) : __builtin_nan("");
       const bool kp = (v > 2.220446049250313e-16) && isfinite(v);
       const double r = kp ? 1.0 / v : 0.0;
-      for (int64_t i = threadIdx.x; i < ldz; i += BS) zrow[i] = (kp && i < n) ? (row[i] - m) * r : 0.0;
+      for (int64_t i = threadIdx.x; i < ldz; i += BS) zrow[i] = (kp && i < n) ? (row[GATHER ? idx[i] : i] - m) * r : 0.0;
       if (threadIdx.x == 0) {
         mean[j] = m;
         sd[j] = v;
@@ -160,25 +161,40 @@ extern "C" int gbm_dev_expand_dosage_i8(const int8_t* D, int64_t ldd, int64_t n,
   return GBM_OK;
 }
 
+template <bool GATHER>
+static int launch_standardize(const double* Xt, int64_t ldx, int64_t p, const int32_t* idx, int64_t n, double* Zt,
+                              int64_t ldz, double* mean, double* sd, int32_t* keep, int64_t* q_dev, hipStream_t s) {
+  const unsigned grid = (unsigned)(p < 256 * 16 ? p : 256 * 16);
+  auto q = reinterpret_cast<unsigned long long*>(q_dev);
+  if (n <= 256 * 4)
+    standardize_kernel<256, 4, GATHER><<<grid, 256, 0, s>>>(Xt, ldx, p, idx, n, Zt, ldz, mean, sd, keep, q);
+  else if (n <= 256 * 8)
+    standardize_kernel<256, 8, GATHER><<<grid, 256, 0, s>>>(Xt, ldx, p, idx, n, Zt, ldz, mean, sd, keep, q);
+  else if (n <= 256 * 16)
+    standardize_kernel<256, 16, GATHER><<<grid, 256, 0, s>>>(Xt, ldx, p, idx, n, Zt, ldz, mean, sd, keep, q);
+  else if (n <= 256 * 32)
+    standardize_kernel<256, 32, GATHER><<<grid, 256, 0, s>>>(Xt, ldx, p, idx, n, Zt, ldz, mean, sd, keep, q);
+  else
+    standardize_kernel<256, 0, GATHER><<<grid, 256, 0, s>>>(Xt, ldx, p, idx, n, Zt, ldz, mean, sd, keep, q);
+  GBM_LAUNCH_CHECK();
+  return GBM_OK;
+}
+
 extern "C" int gbm_dev_standardize(const double* Xt, int64_t ldx, int64_t p, int64_t n, double* Zt, int64_t ldz,
                                    double* mean, double* sd, int32_t* keep, int64_t* q_dev, void* stream) {
   if (!Xt || !Zt || !mean || !sd || !keep || !q_dev || p < 0 || n < 1 || ldx < n || ldz < n ||
       ((const double*)Zt == Xt && ldz != ldx))
     return fail(GBM_E_ARG, "gbm_dev_standardize: bad arguments");
   if (p == 0) return GBM_OK;
-  hipStream_t s = (hipStream_t)stream;
-  const unsigned grid = (unsigned)(p < 256 * 16 ? p : 256 * 16);
-  auto q = reinterpret_cast<unsigned long long*>(q_dev);
-  if (n <= 256 * 4)
-    standardize_kernel<256, 4><<<grid, 256, 0, s>>>(Xt, ldx, p, n, Zt, ldz, mean, sd, keep, q);
-  else if (n <= 256 * 8)
-    standardize_kernel<256, 8><<<grid, 256, 0, s>>>(Xt, ldx, p, n, Zt, ldz, mean, sd, keep, q);
-  else if (n <= 256 * 16)
-    standardize_kernel<256, 16><<<grid, 256, 0, s>>>(Xt, ldx, p, n, Zt, ldz, mean, sd, keep, q);
-  else if (n <= 256 * 32)
-    standardize_kernel<256, 32><<<grid, 256, 0, s>>>(Xt, ldx, p, n, Zt, ldz, mean, sd, keep, q);
-  else
-    standardize_kernel<256, 0><<<grid, 256, 0, s>>>(Xt, ldx, p, n, Zt, ldz, mean, sd, keep, q);
-  GBM_LAUNCH_CHECK();
-  return GBM_OK;
+  return launch_standardize<false>(Xt, ldx, p, nullptr, n, Zt, ldz, mean, sd, keep, q_dev, (hipStream_t)stream);
+}
+
+extern "C" int gbm_dev_standardize_gather(const double* Xt, int64_t ldx, int64_t p, const int32_t* idx, int64_t n,
+                                          double* Zt, int64_t ldz, double* mean, double* sd, int32_t* keep,
+                                          int64_t* q_dev, void* stream) {
+  if (!Xt || !idx || !Zt || !mean || !sd || !keep || !q_dev || p < 0 || n < 1 || ldz < n ||
+      (const double*)Zt == Xt)
+    return fail(GBM_E_ARG, "gbm_dev_standardize_gather: bad arguments (out of place only)");
+  if (p == 0) return GBM_OK;
+  return launch_standardize<true>(Xt, ldx, p, idx, n, Zt, ldz, mean, sd, keep, q_dev, (hipStream_t)stream);
 }

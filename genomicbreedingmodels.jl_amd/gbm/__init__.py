@@ -10,9 +10,12 @@ from .metrics import heritabilitynarrow_sense, metrics, pearsonscorrelation, r2
 from .prediction import LINEAR_MODELS, extractxyetc, predict
 from .types import Fit, Genomes, Phenomes
 from .arrays import colstats, grm
+from .session import GenotypeSession
+from .cv import CV, cvbulk, cvbulk_setup, cvmultithread, fold_assignments, validate
 
 __all__ = [
     "ArgumentError", "GBMError", "device_count", "load_library",
     "gblup", "gblup_arrays", "metrics", "pearsonscorrelation", "r2", "heritabilitynarrow_sense",
     "LINEAR_MODELS", "extractxyetc", "predict", "Fit", "Genomes", "Phenomes", "colstats", "grm",
+    "GenotypeSession", "CV", "cvbulk", "cvbulk_setup", "cvmultithread", "fold_assignments", "validate",
 ]

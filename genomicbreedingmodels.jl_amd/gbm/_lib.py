@@ -30,6 +30,9 @@ EXPORTS = (
     "gbm_dev_synth_genotypes", "gbm_dev_expand_dosage_i8", "gbm_dev_standardize", "gbm_dev_grm",
     "gbm_dev_grm_syrk", "gbm_dev_grm_reduce", "gbm_dev_grm_slices",
     "gbm_dev_gblup_solve", "gbm_dev_marker_effects",
+    "gbm_dev_standardize_gather", "gbm_dev_gblup_terms",
+    "gbm_session_create", "gbm_session_create_dosage_i8", "gbm_session_destroy", "gbm_session_gblup_fit",
+    "gbm_session_predict", "gbm_session_reml_objective", "gbm_session_reml", "gbm_session_stats",
 )
 
 
@@ -91,6 +94,26 @@ def _declare(lib):
     lib.gbm_dev_gblup_solve.argtypes = [P, I64, I64, D, P, D, P, I64, I64, P, P, I64, P, P, P, I64, P]
     lib.gbm_dev_marker_effects.restype = I32
     lib.gbm_dev_marker_effects.argtypes = [P, I64, I64, I64, P, I64, I64, D, P, P, P, P, P, I64, P, P]
+    lib.gbm_dev_standardize_gather.restype = I32
+    lib.gbm_dev_standardize_gather.argtypes = [P, I64, I64, P, I64, P, I64, P, P, P, P, P]
+    lib.gbm_dev_gblup_terms.restype = I32
+    lib.gbm_dev_gblup_terms.argtypes = [P, I64, I64, I64, P, P, P]
+    lib.gbm_session_create.restype = I32
+    lib.gbm_session_create.argtypes = [P, I64, I64, I64, I32, ctypes.POINTER(P)]
+    lib.gbm_session_create_dosage_i8.restype = I32
+    lib.gbm_session_create_dosage_i8.argtypes = [P, I64, I64, I64, I32, I32, ctypes.POINTER(P)]
+    lib.gbm_session_destroy.restype = None
+    lib.gbm_session_destroy.argtypes = [P]
+    lib.gbm_session_gblup_fit.restype = I32
+    lib.gbm_session_gblup_fit.argtypes = [P, P, I64, P, I64, I64, D, P, P, P, P]
+    lib.gbm_session_predict.restype = I32
+    lib.gbm_session_predict.argtypes = [P, P, I64, P, I64, I64, P, I64]
+    lib.gbm_session_reml_objective.restype = I32
+    lib.gbm_session_reml_objective.argtypes = [P, P, I64, P, P, P, I64, P]
+    lib.gbm_session_reml.restype = I32
+    lib.gbm_session_reml.argtypes = [P, P, I64, P, P, P, P, P]
+    lib.gbm_session_stats.restype = I32
+    lib.gbm_session_stats.argtypes = [P, P, P]
     return lib
 
 

@@ -11,7 +11,7 @@ from __future__ import annotations
 import numpy as np
 
 from . import _lib
-from ._lib import GBMError
+from ._lib import ArgumentError, GBMError
 from .metrics import metrics
 from .prediction import extractxyetc
 from .types import Fit, Genomes, Phenomes
@@ -46,7 +46,9 @@ def gblup(*, genomes: Genomes, phenomes: Phenomes, idx_entries=None, idx_loci_al
     """GBLUP / RR-BLUP fit returning a ``Fit`` exactly like ``ridge`` does.
 
     ``model_label="ridge"`` lets the fit flow through an unmodified reference ``predict``
-    whitelist (src/prediction.jl:225): GBLUP ≡ RR-BLUP, so the linear predictor is valid."""
+    whitelist (src/prediction.jl:225): GBLUP ≡ RR-BLUP, so the linear predictor is valid.
+    ``lambda_="reml"`` chooses λ = σ²_e/σ²_u by REML first (the REML result is kept in
+    ``fit.metrics_reml``)."""
     X, y, entries, populations, loci_alleles = extractxyetc(
         genomes, phenomes, idx_entries=idx_entries, idx_loci_alleles=idx_loci_alleles,
         idx_trait=idx_trait, add_intercept=False)
@@ -57,7 +59,21 @@ def gblup(*, genomes: Genomes, phenomes: Phenomes, idx_entries=None, idx_loci_al
     fit.entries = entries
     fit.populations = populations
     fit.y_true = y
-    b_hat, y_pred, mu, q = gblup_arrays(X, y, lambda_=lambda_, devices=devices)
+    if isinstance(lambda_, str):
+        # REML choice of λ: one GRM on a device session, REML over the
+        # reference's loglikreml objective (src/gwas.jl:450-483), then the fit on the cached GRM
+        if lambda_ != "reml":
+            raise ArgumentError(f"lambda_ must be a positive number or \"reml\", got {lambda_!r}")
+        from .session import GenotypeSession
+        dev = (devices[0] if devices else 0) if not isinstance(devices, int) else devices
+        with GenotypeSession(X, device=dev) as s:
+            idx = np.arange(X.shape[0])
+            r = s.reml(idx, y)
+            lambda_ = r["lambda"]
+            b_hat, y_pred, mu, q = s.gblup(idx, y, lambda_)
+        fit.metrics_reml = r
+    else:
+        b_hat, y_pred, mu, q = gblup_arrays(X, y, lambda_=lambda_, devices=devices)
     fit.b_hat = b_hat[:, 0].copy()
     fit.y_pred = y_pred[:, 0].copy()
     fit.metrics = metrics(y, fit.y_pred)

@@ -151,6 +151,12 @@ int gbm_dev_expand_dosage_i8(const int8_t* D, int64_t ldd, int64_t n, int64_t p,
  * monomorphic filter and standardisation of reference src/gwas.jl:112-115,127-130. */
 int gbm_dev_standardize(const double* Xt, int64_t ldx, int64_t p, int64_t n, double* Zt, int64_t ldz,
                         double* mean, double* sd, int32_t* keep, int64_t* q_dev, void* stream);
+/* As gbm_dev_standardize over the entry subset idx[0..n) of Xt's columns (gathered in the same
+ * pass; out of place): the training-set extraction of reference src/prediction.jl:129 fused
+ * with the standardisation. */
+int gbm_dev_standardize_gather(const double* Xt, int64_t ldx, int64_t p, const int32_t* idx, int64_t n,
+                               double* Zt, int64_t ldz, double* mean, double* sd, int32_t* keep,
+                               int64_t* q_dev, void* stream);
 
 /* G[0:npad, 0:npad] (upper-triangular 128x128 tiles: rows <= columns) = Σ_j z_j z_jᵀ over
  * the p locus rows of Zt (unscaled: the RCCL all-reduce of multi-GPU shards sums this).
@@ -184,6 +190,13 @@ int gbm_dev_gblup_solve(double* G, int64_t ldg, int64_t n, double inv_q, const i
                         double* A_out, double* gebv, int64_t lda, double* mu, int32_t* info,
                         void* workspace, int64_t ws_bytes, void* stream);
 
+/* REML ingredients of a finished gbm_dev_gblup_solve (same G, workspace, n, nrhs), into device
+ * memory: terms[0] = logdet(G/q + λI), terms[1] = 1ᵀV⁻¹1, terms[2+2t] = 1ᵀV⁻¹y_t,
+ * terms[3+2t] = y_tᵀV⁻¹y_t — everything reference loglikreml (src/gwas.jl:450-483) needs with
+ * X = 1, read off the bordered factorisation. */
+int gbm_dev_gblup_terms(const double* G, int64_t ldg, int64_t n, int64_t nrhs, const void* workspace,
+                        double* terms, void* stream);
+
 /*
  * Marker effects on the standardised locus rows: B[t, j] = (Zt_j · a_t)/(q·sd_j) for kept
  * loci, 0 otherwise (B nrhs x ldb row-major), and msum[t] = Σ_j mean_j B[t, j] over this
@@ -193,6 +206,41 @@ int gbm_dev_marker_effects(const double* Zt, int64_t ldz, int64_t p, int64_t n,
                            const double* A, int64_t lda, int64_t nrhs, double inv_q, const int64_t* q_dev,
                            const double* mean, const double* sd, const int32_t* keep,
                            double* B, int64_t ldb, double* msum, void* stream);
+
+/*
+ * ---- Device-resident genotype sessions: cross-validation fold farming and REML λ -----------
+ * A session holds X (n x p, uploaded once) on one device and fits GBLUP on entry subsets; the
+ * standardised training genotypes and their GRM are cached per training set, so further traits,
+ * λ values and REML evaluations on the same set skip the SYRK. Replaces the per-fold model calls
+ * of reference cvmultithread! (src/cross_validation.jl:151-207); use one session per device and
+ * one host thread per session. Entry indices are 0-based rows of X, strictly increasing.
+ */
+typedef struct gbm_session gbm_session;
+int gbm_session_create(const double* X, int64_t n, int64_t p, int64_t ldx, int device, gbm_session** out);
+int gbm_session_create_dosage_i8(const int8_t* D, int64_t n, int64_t p, int64_t ldd, int ploidy, int device,
+                                 gbm_session** out);
+void gbm_session_destroy(gbm_session* s);
+/* gbm_gblup_fit on the rows idx[0..n_train) of the session's X; Y holds the training phenotypes
+ * (n_train x nrhs, column-major). */
+int gbm_session_gblup_fit(gbm_session* s, const int64_t* idx, int64_t n_train, const double* Y, int64_t ldy,
+                          int64_t nrhs, double lambda, double* b_hat_out, double* y_pred_out, double* mu_out,
+                          int64_t* q_out);
+/* out[t*ldo + i] = b_hat[t*ldb] + X[idx[i], :] · b_hat[t*ldb + 1 : t*ldb + 1 + p] on the device
+ * (reference predict, src/prediction.jl:228). */
+int gbm_session_predict(gbm_session* s, const int64_t* idx, int64_t n_val, const double* b_hat, int64_t ldb,
+                        int64_t nrhs, double* out, int64_t ldo);
+/* Reference loglikreml (src/gwas.jl:450-483) with X = 1 (intercept) and GRM = ZZᵀ/q of the
+ * training rows: out[k] = 0.5 logdet V + yᵀPy + logdet(XᵀV⁻¹X), V = σ²_u[k] GRM + σ²_e[k] I, for
+ * y as given. One Cholesky per (σ²_e, σ²_u) pair. */
+int gbm_session_reml_objective(gbm_session* s, const int64_t* idx, int64_t n_train, const double* y,
+                               const double* sigma2_e, const double* sigma2_u, int64_t m, double* out);
+/* REML choice of λ = σ²_e/σ²_u: minimises that objective for y standardised as gwasprep does
+ * (src/gwas.jl:127-128) over the reference's box σ²_e, σ²_u ∈ [eps, 1] (src/gwas.jl:585), with
+ * σ²_u profiled in closed form per λ and a scan + golden-section search over log λ. */
+int gbm_session_reml(gbm_session* s, const int64_t* idx, int64_t n_train, const double* y, double* lambda_out,
+                     double* sigma2_e_out, double* sigma2_u_out, double* objective_out);
+/* GRM builds and cache hits so far. */
+int gbm_session_stats(gbm_session* s, int64_t* grm_builds, int64_t* grm_hits);
 
 #ifdef __cplusplus
 }

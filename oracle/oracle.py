@@ -209,3 +209,32 @@ def metrics(y_true: np.ndarray, y_pred: np.ndarray) -> dict:
         "h²": h2,
         "r²": r2,
     }
+
+
+# ----------------------------------------------------------------------------------------
+# REML
+# ----------------------------------------------------------------------------------------
+def loglikreml(theta, y: np.ndarray, Xf: np.ndarray, GRM: np.ndarray) -> float:
+    """Reference ``loglikreml`` (src/gwas.jl:450-483) restated line for line: V = σ²_u GRM + σ²_e I,
+    V⁻¹ by pinv, P = V⁻¹ − V⁻¹X(XᵀV⁻¹X)⁻¹XᵀV⁻¹, objective 0.5 log det V + yᵀPy + log det(XᵀV⁻¹X)."""
+    s2e, s2u = float(theta[0]), float(theta[1])
+    V = s2u * GRM + s2e * np.eye(GRM.shape[0])
+    Vi = np.linalg.pinv(V)
+    XtViX = Xf.T @ Vi @ Xf
+    P = Vi - Vi @ Xf @ np.linalg.inv(XtViX) @ Xf.T @ Vi
+    sign, logdet = np.linalg.slogdet(V)
+    return 0.5 * logdet + float(y @ (P @ y)) + float(np.log(np.linalg.det(XtViX)))
+
+
+def reml_reference(y: np.ndarray, GRM: np.ndarray) -> dict:
+    """What the reference's REML does for an intercept-only model: y standardised as in gwasprep
+    (src/gwas.jl:127-128), L-BFGS over θ = [σ²_e, σ²_u] ∈ [eps, 1]² from [0.5, 0.5] with
+    g_tol 1e-4 (src/gwas.jl:577-590; Optimization.jl's LBFGS there, scipy's L-BFGS-B here)."""
+    from scipy.optimize import minimize
+
+    ys = (y - y.mean()) / y.std(ddof=1)
+    Xf = np.ones((y.size, 1))
+    res = minimize(lambda th: loglikreml(th, ys, Xf, GRM), x0=[0.5, 0.5], method="L-BFGS-B",
+                   bounds=[(EPS64, 1.0), (EPS64, 1.0)], options={"gtol": 1e-10, "ftol": 1e-15, "maxiter": 500})
+    return {"sigma2_e": float(res.x[0]), "sigma2_u": float(res.x[1]), "lambda": float(res.x[0] / res.x[1]),
+            "objective": float(res.fun), "y_std": ys}
