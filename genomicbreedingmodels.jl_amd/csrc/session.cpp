@@ -24,8 +24,9 @@ struct gbm_session {
   gbm::Stream stream;
   int64_t n = 0, p = 0, npad = 0;
   gbm::DevMem Xt;  // p x npad raw genotypes
-  // training-set cache
+  // training-set cache (key: the entry set and the standardisation mode)
   std::vector<int64_t> key;
+  int mode = -1;  // 0: GBLUP standardisation, 1: centre only (glmnet standardize=false)
   int64_t nT = 0, npadT = 0, gdimT = 0, q = 0;
   gbm::DevMem idx32, Z, mean, sd, keep, qd, Gc, wsg;
   // per-fit buffers (sized for the cached training set)
@@ -61,11 +62,11 @@ int check_idx(const gbm_session* s, const int64_t* idx, int64_t m, const char* w
   return GBM_OK;
 }
 
-// Standardise + GRM of the training set idx (cached).
-int ensure_training(gbm_session* s, const int64_t* idx, int64_t nT) {
+// Standardise (mode 0) or centre (mode 1) the training set idx and build its GRM (cached).
+int ensure_training(gbm_session* s, const int64_t* idx, int64_t nT, int mode = 0) {
   GBM_TRY(check_idx(s, idx, nT, "gbm_session"));
   if (nT < 2) return fail(GBM_E_DATA, "there are less than 2 entries (reference src/prediction.jl:117-123)");
-  if ((int64_t)s->key.size() == nT && std::memcmp(s->key.data(), idx, (size_t)nT * 8) == 0) {
+  if (s->mode == mode && (int64_t)s->key.size() == nT && std::memcmp(s->key.data(), idx, (size_t)nT * 8) == 0) {
     s->hits++;
     return GBM_OK;
   }
@@ -95,7 +96,7 @@ int ensure_training(gbm_session* s, const int64_t* idx, int64_t nT) {
   GBM_HIP_TRY(hipMemsetAsync(s->qd.p, 0, 8, st));
   GBM_TRY(gbm_dev_standardize_gather((const double*)s->Xt.p, s->npad, s->p, (const int32_t*)s->idx32.p, nT,
                                      (double*)s->Z.p, npadT, (double*)s->mean.p, (double*)s->sd.p,
-                                     (int32_t*)s->keep.p, (int64_t*)s->qd.p, st));
+                                     (int32_t*)s->keep.p, (int64_t*)s->qd.p, mode, st));
   int64_t q = 0;
   GBM_HIP_TRY(hipMemcpyAsync(&q, s->qd.p, 8, hipMemcpyDeviceToHost, st));
   GBM_HIP_TRY(hipStreamSynchronize(st));
@@ -104,6 +105,7 @@ int ensure_training(gbm_session* s, const int64_t* idx, int64_t nT) {
   s->nT = nT;
   s->q = q;
   s->key.assign(idx, idx + nT);
+  s->mode = mode;
   s->builds++;
   return GBM_OK;
 }
@@ -123,12 +125,13 @@ int ensure_rhs(gbm_session* s, int64_t nrhs) {
   return GBM_OK;
 }
 
-// Solve (G/q + λI) on the cached GRM for the nrhs phenotype columns already in s->Y.
-int solve_cached(gbm_session* s, int64_t nrhs, double lambda) {
+// Solve (G·inv_q + λI) on the cached GRM for the nrhs phenotype columns already in s->Y
+// (inv_q = 1/q for GBLUP, 1 for the unscaled ridge kernel).
+int solve_cached(gbm_session* s, int64_t nrhs, double lambda, double inv_q) {
   hipStream_t st = s->stream.s;
   // the solve factors in place: work on a copy of the cached GRM (rows [0, npad) are read)
   GBM_HIP_TRY(hipMemcpyAsync(s->Gw.p, s->Gc.p, (size_t)(s->npadT * s->gdimT * 8), hipMemcpyDeviceToDevice, st));
-  GBM_TRY(gbm_dev_gblup_solve((double*)s->Gw.p, s->gdimT, s->nT, 1.0 / (double)s->q, nullptr, lambda,
+  GBM_TRY(gbm_dev_gblup_solve((double*)s->Gw.p, s->gdimT, s->nT, inv_q, nullptr, lambda,
                               (const double*)s->Y.p, s->npadT, nrhs, (double*)s->A.p, (double*)s->gebv.p, s->npadT,
                               (double*)s->mu_d.p, (int32_t*)s->info.p, s->wss.p,
                               gbm_dev_solve_workspace(s->nT, 63), st));
@@ -161,7 +164,7 @@ struct RemlEval {
 };
 
 int reml_eval(gbm_session* s, double lambda, RemlEval& out) {
-  GBM_TRY(solve_cached(s, 1, lambda));
+  GBM_TRY(solve_cached(s, 1, lambda, 1.0 / (double)s->q));
   double t[4];
   GBM_TRY(gbm_dev_gblup_terms((const double*)s->Gw.p, s->gdimT, s->nT, 1, s->wss.p, (double*)s->terms.p,
                               s->stream.s));
@@ -256,7 +259,7 @@ extern "C" int gbm_session_gblup_fit(gbm_session* s, const int64_t* idx, int64_t
   GBM_TRY(ensure_training(s, idx, n_train));
   GBM_TRY(ensure_rhs(s, nrhs));
   GBM_TRY(upload_y(s, Y, ldy, nrhs));
-  GBM_TRY(solve_cached(s, nrhs, lambda));
+  GBM_TRY(solve_cached(s, nrhs, lambda, 1.0 / (double)s->q));
   hipStream_t st = s->stream.s;
   const int64_t p = s->p;
   GBM_TRY(gbm_dev_marker_effects((const double*)s->Z.p, s->npadT, p, s->nT, (const double*)s->A.p, s->npadT, nrhs,
@@ -315,7 +318,7 @@ extern "C" int gbm_session_reml_objective(gbm_session* s, const int64_t* idx, in
   for (int64_t k = 0; k < m; k++) {
     if (!(sigma2_e[k] > 0.0) || !(sigma2_u[k] > 0.0))
       return fail(GBM_E_ARG, "gbm_session_reml_objective: variance components must be > 0");
-    GBM_TRY(solve_cached(s, 1, sigma2_e[k] / sigma2_u[k]));
+    GBM_TRY(solve_cached(s, 1, sigma2_e[k] / sigma2_u[k], 1.0 / (double)s->q));
     double t[4];
     GBM_TRY(gbm_dev_gblup_terms((const double*)s->Gw.p, s->gdimT, s->nT, 1, s->wss.p, (double*)s->terms.p,
                                 s->stream.s));
@@ -398,5 +401,87 @@ extern "C" int gbm_session_stats(gbm_session* s, int64_t* grm_builds, int64_t* g
   std::lock_guard<std::mutex> lock(s->mu);
   if (grm_builds) *grm_builds = s->builds;
   if (grm_hits) *grm_hits = s->hits;
+  return GBM_OK;
+}
+
+// ---- ridge path (glmnet alpha = 0, standardize = false; reference ridge, src/linear.jl:193-203) --
+// glmnet minimises (1/2n)‖y − a0 − Xb‖² + (λ/2)‖b‖², i.e. (X_cᵀX_c + nλI) b = X_cᵀ(y − ȳ) on the
+// centred X: the GBLUP system on the unscaled centred-X kernel K = X_cX_cᵀ with λ' = nλ, whose GLS
+// intercept is ȳ (K1 = 0) and whose marker effects are b = X_cᵀa.
+
+extern "C" int gbm_session_ridge_lambda_max(gbm_session* s, const int64_t* idx, int64_t n_train, const double* y,
+                                            double* lambda_max) {
+  if (!s || !y || !lambda_max) return fail(GBM_E_ARG, "gbm_session_ridge_lambda_max: bad arguments");
+  std::lock_guard<std::mutex> lock(s->mu);
+  GBM_HIP_TRY(hipSetDevice(s->dev));
+  GBM_TRY(check_y(y, n_train, n_train, 1));
+  GBM_TRY(ensure_training(s, idx, n_train, 1));
+  GBM_TRY(ensure_rhs(s, 1));
+  // glmnet's first λ for alpha < 1e-3: max_j |x_cjᵀ(y − ȳ)|/n / 1e-3
+  double m = 0.0;
+  for (int64_t i = 0; i < n_train; i++) m += y[i];
+  m /= (double)n_train;
+  std::vector<double> r(s->npadT, 0.0);
+  for (int64_t i = 0; i < n_train; i++) r[i] = y[i] - m;
+  hipStream_t st = s->stream.s;
+  GBM_HIP_TRY(hipMemcpyAsync(s->A.p, r.data(), s->npadT * 8, hipMemcpyHostToDevice, st));
+  GBM_TRY(gbm_dev_marker_effects((const double*)s->Z.p, s->npadT, s->p, s->nT, (const double*)s->A.p, s->npadT, 1,
+                                 1.0, nullptr, (const double*)s->mean.p, (const double*)s->sd.p,
+                                 (const int32_t*)s->keep.p, (double*)s->B.p, s->p, (double*)s->msum.p, st));
+  std::vector<double> g(s->p);
+  GBM_HIP_TRY(hipMemcpyAsync(g.data(), s->B.p, s->p * 8, hipMemcpyDeviceToHost, st));
+  GBM_HIP_TRY(hipStreamSynchronize(st));
+  double gmax = 0.0;
+  for (double v : g) gmax = std::max(gmax, std::fabs(v));
+  *lambda_max = gmax / (double)n_train / 1e-3;
+  return GBM_OK;
+}
+
+extern "C" int gbm_session_ridge_path(gbm_session* s, const int64_t* idx, int64_t n_train, const double* y,
+                                      const double* lambdas, int64_t nl, double* b_path_out, const int64_t* idx_eval,
+                                      int64_t n_eval, double* pred_out) {
+  if (!s || !y || !lambdas || nl < 1 || !b_path_out || (n_eval > 0 && (!idx_eval || !pred_out)))
+    return fail(GBM_E_ARG, "gbm_session_ridge_path: bad arguments");
+  for (int64_t k = 0; k < nl; k++)
+    if (!(lambdas[k] > 0.0) || !std::isfinite(lambdas[k]))
+      return fail(GBM_E_ARG, "gbm_session_ridge_path: lambdas must be finite and > 0");
+  std::lock_guard<std::mutex> lock(s->mu);
+  GBM_HIP_TRY(hipSetDevice(s->dev));
+  GBM_TRY(check_y(y, n_train, n_train, 1));
+  if (n_eval > 0) GBM_TRY(check_idx(s, idx_eval, n_eval, "gbm_session_ridge_path (eval)"));
+  GBM_TRY(ensure_training(s, idx, n_train, 1));
+  GBM_TRY(ensure_rhs(s, 1));
+  GBM_TRY(upload_y(s, y, n_train, 1));
+  hipStream_t st = s->stream.s;
+  const int64_t p = s->p, n = s->n, npad = s->npad;
+  const int64_t nchunks = predict_chunks(n, p);
+  if (n_eval > 0) {
+    GBM_TRY(dalloc(s->bvec, s->dev, (p + 1) * 8));
+    GBM_TRY(dalloc(s->part, s->dev, nchunks * npad * 8));
+    GBM_TRY(dalloc(s->pout, s->dev, npad * 8));
+  }
+  std::vector<double> all(n_eval > 0 ? npad : 0);
+  for (int64_t k = 0; k < nl; k++) {
+    GBM_TRY(solve_cached(s, 1, (double)n_train * lambdas[k], 1.0));
+    GBM_TRY(gbm_dev_marker_effects((const double*)s->Z.p, s->npadT, p, s->nT, (const double*)s->A.p, s->npadT, 1,
+                                   1.0, nullptr, (const double*)s->mean.p, (const double*)s->sd.p,
+                                   (const int32_t*)s->keep.p, (double*)s->B.p, p, (double*)s->msum.p, st));
+    double mu = 0.0, msum = 0.0;
+    double* bk = b_path_out + k * (p + 1);
+    GBM_HIP_TRY(hipMemcpyAsync(bk + 1, s->B.p, p * 8, hipMemcpyDeviceToHost, st));
+    GBM_HIP_TRY(hipMemcpyAsync(&mu, s->mu_d.p, 8, hipMemcpyDeviceToHost, st));
+    GBM_HIP_TRY(hipMemcpyAsync(&msum, s->msum.p, 8, hipMemcpyDeviceToHost, st));
+    GBM_HIP_TRY(hipStreamSynchronize(st));
+    bk[0] = mu - msum;
+    if (n_eval > 0) {
+      GBM_HIP_TRY(hipMemcpyAsync(s->bvec.p, bk, 8, hipMemcpyHostToDevice, st));
+      GBM_HIP_TRY(hipMemcpyAsync((double*)s->bvec.p + 1, s->B.p, p * 8, hipMemcpyDeviceToDevice, st));
+      GBM_TRY(launch_predict((const double*)s->Xt.p, npad, p, n, (const double*)s->bvec.p, p + 1, 1,
+                             (double*)s->part.p, nchunks, (double*)s->pout.p, npad, st));
+      GBM_HIP_TRY(hipMemcpyAsync(all.data(), s->pout.p, npad * 8, hipMemcpyDeviceToHost, st));
+      GBM_HIP_TRY(hipStreamSynchronize(st));
+      for (int64_t i = 0; i < n_eval; i++) pred_out[k * n_eval + i] = all[idx_eval[i]];
+    }
+  }
   return GBM_OK;
 }

@@ -69,7 +69,7 @@ __global__ void __launch_bounds__(BS) standardize_kernel(const double* Xt, int64
                                                          int64_t n, double* Zt, int64_t ldz,
                                                          double* __restrict__ mean,
                                                          double* __restrict__ sd, int32_t* __restrict__ keep,
-                                                         unsigned long long* __restrict__ q_dev) {
+                                                         unsigned long long* __restrict__ q_dev, int center_only) {
   __shared__ double red[BS / 64];
   unsigned long long kept_local = 0;
   for (int64_t j = blockIdx.x; j < p; j += gridDim.x) {
@@ -94,6 +94,7 @@ __global__ void __launch_bounds__(BS) standardize_kernel(const double* Xt, int64
         ss += i < n ? d * d : 0.0;
       }
       v = n > 1 ? sqrt(block_sum<BS>(ss, red) / (double)(n - 1)) : __builtin_nan("");
+      if (center_only) v = 1.0;  // glmnet standardize=false: centre only, keep every column
       const bool kp = (v > 2.220446049250313e-16) && isfinite(v);
       const double r = kp ? 1.0 / v : 0.0;
 #pragma unroll
@@ -118,6 +119,7 @@ __global__ void __launch_bounds__(BS) standardize_kernel(const double* Xt, int64
         ss += d * d;
       }
       v = n > 1 ? sqrt(block_sum<BS>(ss, red) / (double)(n - 1)) : __builtin_nan("");
+      if (center_only) v = 1.0;  // glmnet standardize=false: centre only, keep every column
       const bool kp = (v > 2.220446049250313e-16) && isfinite(v);
       const double r = kp ? 1.0 / v : 0.0;
       for (int64_t i = threadIdx.x; i < ldz; i += BS) zrow[i] = (kp && i < n) ? (row[GATHER ? idx[i] : i] - m) * r : 0.0;
@@ -163,19 +165,20 @@ extern "C" int gbm_dev_expand_dosage_i8(const int8_t* D, int64_t ldd, int64_t n,
 
 template <bool GATHER>
 static int launch_standardize(const double* Xt, int64_t ldx, int64_t p, const int32_t* idx, int64_t n, double* Zt,
-                              int64_t ldz, double* mean, double* sd, int32_t* keep, int64_t* q_dev, hipStream_t s) {
+                              int64_t ldz, double* mean, double* sd, int32_t* keep, int64_t* q_dev, int center_only,
+                              hipStream_t s) {
   const unsigned grid = (unsigned)(p < 256 * 16 ? p : 256 * 16);
   auto q = reinterpret_cast<unsigned long long*>(q_dev);
   if (n <= 256 * 4)
-    standardize_kernel<256, 4, GATHER><<<grid, 256, 0, s>>>(Xt, ldx, p, idx, n, Zt, ldz, mean, sd, keep, q);
+    standardize_kernel<256, 4, GATHER><<<grid, 256, 0, s>>>(Xt, ldx, p, idx, n, Zt, ldz, mean, sd, keep, q, center_only);
   else if (n <= 256 * 8)
-    standardize_kernel<256, 8, GATHER><<<grid, 256, 0, s>>>(Xt, ldx, p, idx, n, Zt, ldz, mean, sd, keep, q);
+    standardize_kernel<256, 8, GATHER><<<grid, 256, 0, s>>>(Xt, ldx, p, idx, n, Zt, ldz, mean, sd, keep, q, center_only);
   else if (n <= 256 * 16)
-    standardize_kernel<256, 16, GATHER><<<grid, 256, 0, s>>>(Xt, ldx, p, idx, n, Zt, ldz, mean, sd, keep, q);
+    standardize_kernel<256, 16, GATHER><<<grid, 256, 0, s>>>(Xt, ldx, p, idx, n, Zt, ldz, mean, sd, keep, q, center_only);
   else if (n <= 256 * 32)
-    standardize_kernel<256, 32, GATHER><<<grid, 256, 0, s>>>(Xt, ldx, p, idx, n, Zt, ldz, mean, sd, keep, q);
+    standardize_kernel<256, 32, GATHER><<<grid, 256, 0, s>>>(Xt, ldx, p, idx, n, Zt, ldz, mean, sd, keep, q, center_only);
   else
-    standardize_kernel<256, 0, GATHER><<<grid, 256, 0, s>>>(Xt, ldx, p, idx, n, Zt, ldz, mean, sd, keep, q);
+    standardize_kernel<256, 0, GATHER><<<grid, 256, 0, s>>>(Xt, ldx, p, idx, n, Zt, ldz, mean, sd, keep, q, center_only);
   GBM_LAUNCH_CHECK();
   return GBM_OK;
 }
@@ -186,15 +189,16 @@ extern "C" int gbm_dev_standardize(const double* Xt, int64_t ldx, int64_t p, int
       ((const double*)Zt == Xt && ldz != ldx))
     return fail(GBM_E_ARG, "gbm_dev_standardize: bad arguments");
   if (p == 0) return GBM_OK;
-  return launch_standardize<false>(Xt, ldx, p, nullptr, n, Zt, ldz, mean, sd, keep, q_dev, (hipStream_t)stream);
+  return launch_standardize<false>(Xt, ldx, p, nullptr, n, Zt, ldz, mean, sd, keep, q_dev, 0, (hipStream_t)stream);
 }
 
 extern "C" int gbm_dev_standardize_gather(const double* Xt, int64_t ldx, int64_t p, const int32_t* idx, int64_t n,
                                           double* Zt, int64_t ldz, double* mean, double* sd, int32_t* keep,
-                                          int64_t* q_dev, void* stream) {
+                                          int64_t* q_dev, int center_only, void* stream) {
   if (!Xt || !idx || !Zt || !mean || !sd || !keep || !q_dev || p < 0 || n < 1 || ldz < n ||
       (const double*)Zt == Xt)
     return fail(GBM_E_ARG, "gbm_dev_standardize_gather: bad arguments (out of place only)");
   if (p == 0) return GBM_OK;
-  return launch_standardize<true>(Xt, ldx, p, idx, n, Zt, ldz, mean, sd, keep, q_dev, (hipStream_t)stream);
+  return launch_standardize<true>(Xt, ldx, p, idx, n, Zt, ldz, mean, sd, keep, q_dev, center_only,
+                                  (hipStream_t)stream);
 }

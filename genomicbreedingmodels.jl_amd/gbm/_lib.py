@@ -33,6 +33,7 @@ EXPORTS = (
     "gbm_dev_standardize_gather", "gbm_dev_gblup_terms",
     "gbm_session_create", "gbm_session_create_dosage_i8", "gbm_session_destroy", "gbm_session_gblup_fit",
     "gbm_session_predict", "gbm_session_reml_objective", "gbm_session_reml", "gbm_session_stats",
+    "gbm_session_ridge_path", "gbm_session_ridge_lambda_max",
 )
 
 
@@ -95,7 +96,7 @@ def _declare(lib):
     lib.gbm_dev_marker_effects.restype = I32
     lib.gbm_dev_marker_effects.argtypes = [P, I64, I64, I64, P, I64, I64, D, P, P, P, P, P, I64, P, P]
     lib.gbm_dev_standardize_gather.restype = I32
-    lib.gbm_dev_standardize_gather.argtypes = [P, I64, I64, P, I64, P, I64, P, P, P, P, P]
+    lib.gbm_dev_standardize_gather.argtypes = [P, I64, I64, P, I64, P, I64, P, P, P, P, I32, P]
     lib.gbm_dev_gblup_terms.restype = I32
     lib.gbm_dev_gblup_terms.argtypes = [P, I64, I64, I64, P, P, P]
     lib.gbm_session_create.restype = I32
@@ -112,6 +113,10 @@ def _declare(lib):
     lib.gbm_session_reml_objective.argtypes = [P, P, I64, P, P, P, I64, P]
     lib.gbm_session_reml.restype = I32
     lib.gbm_session_reml.argtypes = [P, P, I64, P, P, P, P, P]
+    lib.gbm_session_ridge_path.restype = I32
+    lib.gbm_session_ridge_path.argtypes = [P, P, I64, P, P, I64, P, P, I64, P]
+    lib.gbm_session_ridge_lambda_max.restype = I32
+    lib.gbm_session_ridge_lambda_max.argtypes = [P, P, I64, P, P]
     lib.gbm_session_stats.restype = I32
     lib.gbm_session_stats.argtypes = [P, P, P]
     return lib

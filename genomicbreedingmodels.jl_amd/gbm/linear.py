@@ -83,3 +83,86 @@ def gblup(*, genomes: Genomes, phenomes: Phenomes, idx_entries=None, idx_loci_al
     if not fit.checkdims():
         raise GBMError("Error fitting " + fit.model + ".")
     return fit
+
+
+def glmnet_folds(n: int, nfolds: int, rng) -> np.ndarray:
+    """GLMNet.jl glmnetcv's default folds: ``nfolds = min(10, n ÷ 3)`` balanced labels
+    ``[repeat(1:nfolds, n ÷ nfolds); 1:(n % nfolds)]`` shuffled (unseeded there; ``rng`` here)."""
+    q, r = divmod(n, nfolds)
+    f = np.concatenate([np.tile(np.arange(1, nfolds + 1), q), np.arange(1, r + 1)])
+    rng.shuffle(f)
+    return f
+
+
+def ridge_path_cv(X: np.ndarray, y: np.ndarray, *, nlambda: int = 100, lambda_min_ratio: float = 0.01,
+                  nfolds: int | None = None, seed: int = 42, device: int = 0):
+    """``GLMNet.glmnetcv(X, y, alpha=0, standardize=false, nlambda=100, lambda_min_ratio=0.01,
+    intercept=true)`` as called by reference ridge (src/linear.jl:193-203), on the GPU: the λ path
+    from the full data, every path solved exactly (kernel form, one Cholesky per λ on the cached
+    centred-X kernel), k-fold CV mean squared error per λ. Returns dict(lambda, a0, betas (p, nl),
+    meanloss)."""
+    X = np.asarray(X, dtype=np.float64)
+    y = np.asarray(y, dtype=np.float64)
+    n = X.shape[0]
+    nf = nfolds if nfolds is not None else min(10, n // 3)
+    if nf < 2:
+        raise ArgumentError("glmnetcv needs at least 2 folds (n >= 6)")
+    from .session import GenotypeSession
+    with GenotypeSession(X, device=device) as s:
+        idx = np.arange(n)
+        lmax = s.ridge_lambda_max(idx, y)
+        lam = lmax * lambda_min_ratio ** (np.arange(nlambda) / (nlambda - 1))
+        path = s.ridge_path(idx, y, lam)
+        folds = glmnet_folds(n, nf, np.random.default_rng(seed))
+        loss = np.zeros((nlambda, nf))
+        for f in range(1, nf + 1):
+            tr, ho = np.flatnonzero(folds != f), np.flatnonzero(folds == f)
+            _, pred = s.ridge_path(tr, y[tr], lam, idx_eval=ho)
+            loss[:, f - 1] = ((pred - y[ho, None]) ** 2).mean(axis=0)
+    return {"lambda": lam, "a0": path[0].copy(), "betas": path[1:].copy(), "meanloss": loss.mean(axis=1)}
+
+
+def ridge_select(a0: np.ndarray, betas: np.ndarray, meanloss: np.ndarray) -> np.ndarray:
+    """The coefficient choice of reference ridge (src/linear.jl:213-223), quirks included: λs
+    sorted by CV loss; the intercept taken as ``a0[idx_sort][idx_sort[i]]`` (a double
+    permutation) and the first solution whose slopes have variance >= 1e-10 kept."""
+    idx_sort = np.argsort(meanloss, kind="stable")
+    intercepts = a0[idx_sort]
+    nl = betas.shape[1]
+    b_hat = np.zeros(betas.shape[0] + 1)
+    i = 0
+    while np.var(b_hat[1:], ddof=1) < 1e-10 or i == nl - 1:
+        if i >= nl:
+            break
+        b_hat = np.concatenate([[intercepts[idx_sort[i]]], betas[:, idx_sort[i]]])
+        i += 1
+    return b_hat
+
+
+def ridge(*, genomes: Genomes, phenomes: Phenomes, idx_entries=None, idx_loci_alleles=None, idx_trait: int = 1,
+          verbose: bool = False, seed: int = 42, device: int = 0) -> Fit:
+    """Mirror of reference ``ridge`` (src/linear.jl:162-239) with the GLMNet path on the GPU."""
+    X, y, entries, populations, loci_alleles = extractxyetc(
+        genomes, phenomes, idx_entries=idx_entries, idx_loci_alleles=idx_loci_alleles,
+        idx_trait=idx_trait, add_intercept=False)
+    fit = Fit(n=X.shape[0], l=X.shape[1])
+    fit.model = "ridge"
+    fit.b_hat_labels = ["intercept"] + list(loci_alleles)
+    fit.trait = phenomes.traits[idx_trait - 1]
+    fit.entries = entries
+    fit.populations = populations
+    fit.y_true = y
+    cv = ridge_path_cv(X, y, seed=seed, device=device)
+    b_hat = ridge_select(cv["a0"], cv["betas"], cv["meanloss"])
+    from .session import GenotypeSession
+    with GenotypeSession(X, device=device) as s:
+        y_pred = s.predict(np.arange(X.shape[0]), b_hat)
+    fit.b_hat = b_hat
+    fit.y_pred = y_pred
+    fit.metrics = metrics(y, y_pred)
+    if verbose:
+        print("argmin =", int(np.argmin(cv["meanloss"])) + 1)
+        print(fit.metrics)
+    if not fit.checkdims():
+        raise GBMError("Error fitting " + fit.model + ".")
+    return fit

@@ -129,6 +129,35 @@ class GenotypeSession:
         _lib.check(rc, "gbm_session_reml")
         return {"lambda": float(v[0]), "sigma2_e": float(v[1]), "sigma2_u": float(v[2]), "objective": float(v[3])}
 
+    def ridge_lambda_max(self, idx, y) -> float:
+        """glmnet's first λ for alpha = 0 on rows ``idx`` (standardize = false)."""
+        idx = _idx(idx)
+        y = np.ascontiguousarray(np.asarray(y, dtype=np.float64))
+        out = np.zeros(1)
+        rc = self.lib.gbm_session_ridge_lambda_max(self._h, _lib.ptr(idx), idx.size, _lib.ptr(y), _lib.ptr(out))
+        _lib.check(rc, "gbm_session_ridge_lambda_max")
+        return float(out[0])
+
+    def ridge_path(self, idx, y, lambdas, idx_eval=None):
+        """Exact glmnet ridge solutions (alpha = 0, standardize = false, intercept) on rows ``idx``
+        at each λ. Returns b_path (p+1, nl) [intercept first] and, with ``idx_eval``, the
+        predictions (n_eval, nl)."""
+        idx = _idx(idx)
+        y = np.ascontiguousarray(np.asarray(y, dtype=np.float64))
+        lam = np.ascontiguousarray(np.atleast_1d(np.asarray(lambdas, dtype=np.float64)))
+        b = np.zeros((self.p + 1, lam.size), order="F")
+        if idx_eval is not None:
+            ie = _idx(idx_eval)
+            pred = np.zeros((ie.size, lam.size), order="F")
+            rc = self.lib.gbm_session_ridge_path(self._h, _lib.ptr(idx), idx.size, _lib.ptr(y), _lib.ptr(lam),
+                                                 lam.size, _lib.ptr(b), _lib.ptr(ie), ie.size, _lib.ptr(pred))
+            _lib.check(rc, "gbm_session_ridge_path")
+            return b, pred
+        rc = self.lib.gbm_session_ridge_path(self._h, _lib.ptr(idx), idx.size, _lib.ptr(y), _lib.ptr(lam), lam.size,
+                                             _lib.ptr(b), None, 0, None)
+        _lib.check(rc, "gbm_session_ridge_path")
+        return b
+
     def stats(self):
         """(GRM builds, GRM cache hits)."""
         v = np.zeros(2, dtype=np.int64)

@@ -153,10 +153,11 @@ int gbm_dev_standardize(const double* Xt, int64_t ldx, int64_t p, int64_t n, dou
                         double* mean, double* sd, int32_t* keep, int64_t* q_dev, void* stream);
 /* As gbm_dev_standardize over the entry subset idx[0..n) of Xt's columns (gathered in the same
  * pass; out of place): the training-set extraction of reference src/prediction.jl:129 fused
- * with the standardisation. */
+ * with the standardisation. center_only != 0 centres without scaling and keeps every column
+ * (sd reported as 1): the X that GLMNet sees with standardize=false (src/linear.jl:193-203). */
 int gbm_dev_standardize_gather(const double* Xt, int64_t ldx, int64_t p, const int32_t* idx, int64_t n,
                                double* Zt, int64_t ldz, double* mean, double* sd, int32_t* keep,
-                               int64_t* q_dev, void* stream);
+                               int64_t* q_dev, int center_only, void* stream);
 
 /* G[0:npad, 0:npad] (upper-triangular 128x128 tiles: rows <= columns) = Σ_j z_j z_jᵀ over
  * the p locus rows of Zt (unscaled: the RCCL all-reduce of multi-GPU shards sums this).
@@ -239,6 +240,16 @@ int gbm_session_reml_objective(gbm_session* s, const int64_t* idx, int64_t n_tra
  * σ²_u profiled in closed form per λ and a scan + golden-section search over log λ. */
 int gbm_session_reml(gbm_session* s, const int64_t* idx, int64_t n_train, const double* y, double* lambda_out,
                      double* sigma2_e_out, double* sigma2_u_out, double* objective_out);
+/* Ridge path of reference ridge (GLMNet alpha = 0, standardize = false, intercept;
+ * src/linear.jl:193-203) on the rows idx[0..n_train): for each lambdas[k] (glmnet scale, objective
+ * (1/2n)‖y − a0 − Xb‖² + (λ/2)‖b‖²) the exact minimiser, b_path_out[k*(p+1)] = a0 and
+ * b_path_out[k*(p+1) + 1 + j] = b_j; optionally pred_out[k*n_eval + i] = a0 + X[idx_eval[i], :] b. */
+int gbm_session_ridge_path(gbm_session* s, const int64_t* idx, int64_t n_train, const double* y,
+                           const double* lambdas, int64_t nl, double* b_path_out, const int64_t* idx_eval,
+                           int64_t n_eval, double* pred_out);
+/* glmnet's largest λ for alpha = 0 (alpha floored at 1e-3): max_j |x_cjᵀ(y − ȳ)| / n / 1e-3. */
+int gbm_session_ridge_lambda_max(gbm_session* s, const int64_t* idx, int64_t n_train, const double* y,
+                                 double* lambda_max);
 /* GRM builds and cache hits so far. */
 int gbm_session_stats(gbm_session* s, int64_t* grm_builds, int64_t* grm_hits);
 

@@ -238,3 +238,44 @@ def reml_reference(y: np.ndarray, GRM: np.ndarray) -> dict:
                    bounds=[(EPS64, 1.0), (EPS64, 1.0)], options={"gtol": 1e-10, "ftol": 1e-15, "maxiter": 500})
     return {"sigma2_e": float(res.x[0]), "sigma2_u": float(res.x[1]), "lambda": float(res.x[0] / res.x[1]),
             "objective": float(res.fun), "y_std": ys}
+
+
+# ----------------------------------------------------------------------------------------
+# Ridge path: GLMNet alpha = 0, standardize = false, intercept
+# (reference ridge, src/linear.jl:193-203). glmnet is un-vendored; restated from its published
+# objective (1/2n)‖y − a0 − Xb‖² + (λ/2)‖b‖² and pinned by R-glmnet known answers
+# (tests/golden/glmnet_ridge_r.npz).
+# ----------------------------------------------------------------------------------------
+def ridge_exact(X: np.ndarray, y: np.ndarray, lam: float):
+    """Exact glmnet ridge minimiser: (X_cᵀX_c + nλI) b = X_cᵀ(y − ȳ), a0 = ȳ − x̄ᵀb."""
+    n, p = X.shape
+    xm, ym = X.mean(axis=0), y.mean()
+    Xc = X - xm
+    if p <= n:
+        b = np.linalg.solve(Xc.T @ Xc + n * lam * np.eye(p), Xc.T @ (y - ym))
+    else:
+        b = Xc.T @ np.linalg.solve(Xc @ Xc.T + n * lam * np.eye(n), y - ym)
+    return ym - xm @ b, b
+
+
+def ridge_lambda_max(X: np.ndarray, y: np.ndarray) -> float:
+    """glmnet's first λ for alpha = 0 (alpha floored at 1e-3 in the λ_max formula)."""
+    Xc = X - X.mean(axis=0)
+    return float(np.abs(Xc.T @ (y - y.mean())).max() / X.shape[0] / 1e-3)
+
+
+def ridge_path_cv(X, y, folds, nlambda=100, lambda_min_ratio=0.01):
+    """glmnetcv's λ path, exact path solutions and CV mean squared error for given fold labels."""
+    lam = ridge_lambda_max(X, y) * lambda_min_ratio ** (np.arange(nlambda) / (nlambda - 1))
+    a0 = np.zeros(nlambda)
+    betas = np.zeros((X.shape[1], nlambda))
+    for k, l in enumerate(lam):
+        a0[k], betas[:, k] = ridge_exact(X, y, l)
+    nf = int(folds.max())
+    loss = np.zeros((nlambda, nf))
+    for f in range(1, nf + 1):
+        tr, ho = folds != f, folds == f
+        for k, l in enumerate(lam):
+            a, b = ridge_exact(X[tr], y[tr], l)
+            loss[k, f - 1] = np.mean((a + X[ho] @ b - y[ho]) ** 2)
+    return {"lambda": lam, "a0": a0, "betas": betas, "meanloss": loss.mean(axis=1)}
