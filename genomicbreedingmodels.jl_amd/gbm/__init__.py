@@ -11,11 +11,12 @@ from .prediction import LINEAR_MODELS, extractxyetc, predict
 from .types import Fit, Genomes, Phenomes
 from .arrays import colstats, grm
 from .session import GenotypeSession
+from .bayes import bayesian, brr_arrays
 from .cv import CV, cvbulk, cvbulk_setup, cvmultithread, fold_assignments, validate
 
 __all__ = [
     "ArgumentError", "GBMError", "device_count", "load_library",
     "gblup", "gblup_arrays", "ridge", "ridge_path_cv", "ridge_select", "glmnet_folds", "metrics", "pearsonscorrelation", "r2", "heritabilitynarrow_sense",
     "LINEAR_MODELS", "extractxyetc", "predict", "Fit", "Genomes", "Phenomes", "colstats", "grm",
-    "GenotypeSession", "CV", "cvbulk", "cvbulk_setup", "cvmultithread", "fold_assignments", "validate",
+    "GenotypeSession", "bayesian", "brr_arrays", "CV", "cvbulk", "cvbulk_setup", "cvmultithread", "fold_assignments", "validate",
 ]

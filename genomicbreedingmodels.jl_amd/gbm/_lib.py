@@ -33,7 +33,7 @@ EXPORTS = (
     "gbm_dev_standardize_gather", "gbm_dev_gblup_terms",
     "gbm_session_create", "gbm_session_create_dosage_i8", "gbm_session_destroy", "gbm_session_gblup_fit",
     "gbm_session_predict", "gbm_session_reml_objective", "gbm_session_reml", "gbm_session_stats",
-    "gbm_session_ridge_path", "gbm_session_ridge_lambda_max",
+    "gbm_session_ridge_path", "gbm_session_ridge_lambda_max", "gbm_brr_fit",
 )
 
 
@@ -117,6 +117,8 @@ def _declare(lib):
     lib.gbm_session_ridge_path.argtypes = [P, P, I64, P, P, I64, P, P, I64, P]
     lib.gbm_session_ridge_lambda_max.restype = I32
     lib.gbm_session_ridge_lambda_max.argtypes = [P, P, I64, P, P]
+    lib.gbm_brr_fit.restype = I32
+    lib.gbm_brr_fit.argtypes = [P, I64, I64, I64, P, I64, I64, I64, D, D, U64, I32, P, P, P]
     lib.gbm_session_stats.restype = I32
     lib.gbm_session_stats.argtypes = [P, P, P]
     return lib

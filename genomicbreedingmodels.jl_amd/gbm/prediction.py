@@ -13,7 +13,7 @@ from ._lib import ArgumentError, GBMError
 from .types import Fit, Genomes, Phenomes
 
 # src/prediction.jl:225 plus the new "gblup" (SURVEY.md §8b decision)
-LINEAR_MODELS = ("ols", "ridge", "lasso", "bayesa", "bayesb", "bayesc", "gblup")
+LINEAR_MODELS = ("ols", "ridge", "lasso", "bayesa", "bayesb", "bayesc", "gblup", "BRR")
 
 
 def extractxyetc(genomes: Genomes, phenomes: Phenomes, idx_entries=None, idx_loci_alleles=None,

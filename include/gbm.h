@@ -253,6 +253,21 @@ int gbm_session_ridge_lambda_max(gbm_session* s, const int64_t* idx, int64_t n_t
 /* GRM builds and cache hits so far. */
 int gbm_session_stats(gbm_session* s, int64_t* grm_builds, int64_t* grm_hits);
 
+/*
+ * ---- Bayesian ridge regression (BGLR model "BRR") by Gibbs sampling -------------------------
+ * Replaces the Rscript/BGLR call of reference bglr()/bayesian() (src/bayes.jl:28-105,158-224)
+ * for bglr_model = "BRR": BGLR's single-site sampler (intercept, markers in order with residual
+ * updates, σ²_b and σ²_e scaled-inverse-χ² draws; priors df0, R2 as BGLR's defaults 5 and 0.5),
+ * n_iter iterations, running posterior means every `thin` iterations after n_burnin.
+ * b_hat_out (p+1) = [posterior mean of μ; posterior means of b]; y_pred_out (n, optional) =
+ * b0 + X b; var_out (2, optional) = posterior means of [σ²_e, σ²_b]. X column-major n x p.
+ * Counter-based random numbers from `seed` (no R RNG stream: results are reproducible but the
+ * chain is not BGLR's sample path).
+ */
+int gbm_brr_fit(const double* X, int64_t n, int64_t p, int64_t ldx, const double* y, int64_t n_iter,
+                int64_t n_burnin, int64_t thin, double r2, double df0, uint64_t seed, int device,
+                double* b_hat_out, double* y_pred_out, double* var_out);
+
 #ifdef __cplusplus
 }
 #endif

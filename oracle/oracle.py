@@ -279,3 +279,91 @@ def ridge_path_cv(X, y, folds, nlambda=100, lambda_min_ratio=0.01):
             a, b = ridge_exact(X[tr], y[tr], l)
             loss[k, f - 1] = np.mean((a + X[ho] @ b - y[ho]) ** 2)
     return {"lambda": lam, "a0": a0, "betas": betas, "meanloss": loss.mean(axis=1)}
+
+
+# ----------------------------------------------------------------------------------------
+# Bayesian ridge regression, BGLR model "BRR" (SURVEY.md §8f row 3). BGLR (R, C sampler) is
+# un-vendored and absent: restated from its published algorithm (setLT.BRR priors, sample_beta
+# single-site updates, scaled-inverse-χ² variance draws, running means every `thin` after
+# burn-in), driven by the same counter-based random numbers as the device sampler
+# (genomicbreedingmodels.jl_amd/csrc/gibbs.hip) so both follow one sample path.
+# ----------------------------------------------------------------------------------------
+_U64 = (1 << 64) - 1
+
+
+def _mix_int(z: int) -> int:
+    z = (z + 0x9E3779B97F4A7C15) & _U64
+    z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & _U64
+    z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & _U64
+    return z ^ (z >> 31)
+
+
+def brr_u01(seed: int, a: int, b: int) -> float:
+    h = _mix_int(_mix_int(seed ^ ((a * 0xD1B54A32D192ED03) & _U64)) ^ ((b * 0x8CB92BA72F3D8DD7) & _U64))
+    return ((h >> 11) + 0.5) * 2.0 ** -53
+
+
+def brr_normal(seed: int, a: int, b: int) -> float:
+    import math
+    u1, u2 = brr_u01(seed, a, 2 * b), brr_u01(seed, a, 2 * b + 1)
+    return math.sqrt(-2.0 * math.log(u1)) * math.cos(6.283185307179586 * u2)
+
+
+def brr_chisq(seed: int, a: int, df: float) -> float:
+    """χ²(df) = 2 Gamma(df/2), Marsaglia-Tsang; attempt t: normal (a, 2t), uniform (a, 4t+2)."""
+    import math
+    d = 0.5 * df - 1.0 / 3.0
+    c = 1.0 / math.sqrt(9.0 * d)
+    for t in range(1000):
+        x = brr_normal(seed, a, 2 * t)
+        v = 1.0 + c * x
+        if v <= 0.0:
+            continue
+        v = v * v * v
+        u = brr_u01(seed, a, 4 * t + 2)
+        if math.log(u) < 0.5 * x * x + d - d * v + d * math.log(v):
+            return 2.0 * d * v
+    return df
+
+
+def brr_gibbs(X: np.ndarray, y: np.ndarray, n_iter: int, n_burnin: int, thin: int = 5, r2: float = 0.5,
+              df0: float = 5.0, seed: int = 42) -> dict:
+    """BGLR's BRR Gibbs sampler (single site, un-blocked) — the oracle for gbm_brr_fit."""
+    n, p = X.shape
+    X = np.asarray(X, dtype=np.float64)
+    x2 = (X * X).sum(axis=0)
+    msx = x2.sum() / n - (X.mean(axis=0) ** 2).sum()
+    vy = y.var(ddof=1)
+    S0e, S0b = vy * (1 - r2) * (df0 + 2), vy * r2 / msx * (df0 + 2)
+    varE, varB = S0e / (df0 + 2), S0b / (df0 + 2)
+    mu = y.mean()
+    e = y - mu
+    b = np.zeros(p)
+    bbar = np.zeros(p)
+    mubar = varEbar = varBbar = 0.0
+    nsum = 0
+    for it in range(n_iter):
+        a = 4 * it
+        s = (e + mu).sum()
+        mu_new = s / n + np.sqrt(varE / n) * brr_normal(seed, a, 0xFFFFFFFF)
+        e = (e + mu) - mu_new
+        mu = mu_new
+        for j in range(p):
+            xj = X[:, j]
+            rhs = (xj @ e) / varE + x2[j] * b[j] / varE
+            c = x2[j] / varE + 1.0 / varB
+            bn = rhs / c + np.sqrt(1.0 / c) * brr_normal(seed, a, j)
+            e += (b[j] - bn) * xj
+            b[j] = bn
+        varB = ((b * b).sum() + S0b) / brr_chisq(seed, a + 1, df0 + p)
+        varE = ((e * e).sum() + S0e) / brr_chisq(seed, a + 2, df0 + n)
+        i = it + 1
+        if i % thin == 0 and i > n_burnin:
+            nsum += 1
+            k = float(nsum)
+            bbar = bbar * ((k - 1) / k) + b / k
+            mubar = mubar * ((k - 1) / k) + mu / k
+            varEbar = varEbar * ((k - 1) / k) + varE / k
+            varBbar = varBbar * ((k - 1) / k) + varB / k
+    b_hat = np.concatenate([[mubar], bbar])
+    return {"b_hat": b_hat, "y_pred": mubar + X @ bbar, "varE": varEbar, "varB": varBbar, "b_last": b, "mu_last": mu}

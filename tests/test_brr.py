@@ -1,0 +1,66 @@
+"""Bayesian ridge regression (BGLR "BRR") Gibbs sampler — SURVEY.md §8f row 3 (config C4).
+BGLR is un-vendored and stochastic: parity vs BGLR itself is unpinned. Pinned instead: the device
+sampler (blocked, Gram-based) against the oracle's literal single-site BGLR loop on the same
+counter-based random numbers (same sample path), plus distributional checks (posterior-mean GEBVs
+vs GBLUP at the matching λ; the reference doctest's cor > 0.5, src/bayes.jl:155-158)."""
+import numpy as np
+import pytest
+
+import gbm
+import oracle
+
+
+def test_oracle_rng_properties():
+    z = np.array([oracle.brr_normal(7, 3, k) for k in range(4000)])
+    assert abs(z.mean()) < 0.06 and abs(z.std() - 1) < 0.05
+    c = np.array([oracle.brr_chisq(7, k, 9.0) for k in range(2000)])
+    assert abs(c.mean() - 9.0) < 0.3 and abs(c.var() - 18.0) < 2.5
+
+
+def test_oracle_brr_shrinks_like_ridge():
+    X = oracle.synth_genotypes(51, 120, 200)
+    y = oracle.synth_phenotypes(X, 52)[:, 0]
+    r = oracle.brr_gibbs(X, y, n_iter=150, n_burnin=50, thin=5, seed=1)
+    assert np.corrcoef(r["y_pred"], y)[0, 1] > 0.5
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,p,iters", [(100, 300, 12), (77, 130, 9), (200, 64, 7)])
+def test_gpu_brr_same_sample_path_as_oracle(n, p, iters):
+    X = oracle.synth_genotypes(61 + p, n, p)
+    y = oracle.synth_phenotypes(X, 62)[:, 0]
+    ref = oracle.brr_gibbs(X, y, n_iter=iters, n_burnin=2, thin=1, seed=99)
+    b_hat, y_pred, var = gbm.brr_arrays(X, y, n_iter=iters, n_burnin=2, thin=1, seed=99)
+    rel = lambda a, b: np.abs(a - b).max() / np.abs(b).max()
+    assert rel(b_hat, ref["b_hat"]) < 1e-9
+    assert rel(y_pred, ref["y_pred"]) < 1e-9
+    assert abs(var[0] - ref["varE"]) < 1e-9 * ref["varE"] and abs(var[1] - ref["varB"]) < 1e-9 * ref["varB"]
+
+
+@pytest.mark.gpu
+def test_gpu_brr_posterior_mean_close_to_gblup():
+    """With σ²_b, σ²_e near their posterior the BRR posterior mean of Xb is the ridge/GBLUP BLUP:
+    compare GEBVs with GBLUP at λ = σ²_e/σ²_b (posterior means) — distributional, not exact."""
+    X = oracle.synth_genotypes(71, 400, 2000)
+    y = oracle.synth_phenotypes(X, 72)[:, 0]
+    b_hat, y_pred, var = gbm.brr_arrays(X, y, n_iter=1500, n_burnin=500, thin=5, seed=3)
+    lam_rr = var[0] / var[1]  # per-marker ridge λ on unscaled X
+    a0, b = oracle.ridge_exact(X, y, lam_rr / X.shape[0])
+    ridge_pred = a0 + X @ b
+    assert np.corrcoef(y_pred, ridge_pred)[0, 1] > 0.98
+    assert np.corrcoef(y_pred, y)[0, 1] > 0.5
+
+
+@pytest.mark.gpu
+def test_gpu_bayesian_model_function():
+    X = oracle.synth_genotypes(81, 150, 500)
+    Y = oracle.synth_phenotypes(X, 82)
+    ent = [f"e{i}" for i in range(150)]
+    g = gbm.Genomes(ent, ["p"] * 150, [f"l{j}" for j in range(500)], X)
+    ph = gbm.Phenomes(ent, ["p"] * 150, ["t"], Y)
+    fit = gbm.bayesian("BRR", genomes=g, phenomes=ph, n_iter=300, n_burnin=100)
+    assert fit.model == "BRR" and fit.checkdims() and fit.metrics["cor"] > 0.5
+    pred = gbm.predict(fit, g, list(range(1, 151)))
+    assert np.abs(pred - fit.y_pred).max() < 1e-9 * np.abs(fit.y_pred).max()
+    with pytest.raises(gbm.ArgumentError):
+        gbm.bayesian("BayesA", genomes=g, phenomes=ph)
