@@ -144,75 +144,185 @@ __global__ void __launch_bounds__(1024) brr_mu_kernel(double* __restrict__ e, in
   if (threadIdx.x == 0) st->mu = mu;
 }
 
-// r[k] = x_{j0+k}ᵀ e (one workgroup per marker of the block)
-__global__ void __launch_bounds__(256) brr_dots_kernel(const double* __restrict__ Xt, int64_t ldx, int64_t n,
-                                                       const double* __restrict__ e, int64_t j0,
-                                                       double* __restrict__ r) {
-  __shared__ double red[4];
-  const double* row = Xt + (j0 + blockIdx.x) * ldx;
+constexpr int IW = 256;  // individuals per workgroup in the block kernels
+
+// partial[c][k] = Σ_{i in chunk c} x_{j0+k, i} e_i over this workgroup's IW individuals, from es
+// (the chunk of e in LDS): thread (k = tid/4, quarter) sums 64 contiguous individuals
+__device__ __forceinline__ void brr_partials(const double* __restrict__ Xt, int64_t ldx, int64_t n, int64_t i0,
+                                             int64_t j0, int nb, const double* es, double* __restrict__ out) {
+  const int tid = threadIdx.x, k = tid >> 2, qt = tid & 3;
   double s = 0.0;
-  for (int64_t i = threadIdx.x; i < n; i += 256) s += row[i] * e[i];
-  s = brr_block_sum<256>(s, red);
-  if (threadIdx.x == 0) r[blockIdx.x] = s;
+  if (k < nb) {
+    // 64 contiguous individuals per thread, all loads in flight (rows are zero-padded to ldx, a
+    // multiple of IW, and es is 0 past n)
+    const double* row = Xt + (j0 + k) * ldx + i0 + qt * 64;
+    double2 v[32];
+#pragma unroll
+    for (int u = 0; u < 32; u++) v[u] = *reinterpret_cast<const double2*>(row + 2 * u);
+    double s1 = 0.0;
+#pragma unroll
+    for (int u = 0; u < 32; u++) {
+      s = fma(v[u].x, es[qt * 64 + 2 * u], s);
+      s1 = fma(v[u].y, es[qt * 64 + 2 * u + 1], s1);
+    }
+    s += s1;
+  }
+  s += __shfl_xor(s, 1);
+  s += __shfl_xor(s, 2);
+  if (qt == 0) out[blockIdx.x * BB + k] = s;  // k >= nb writes 0
 }
 
-// The block's 64 single-site steps (wave 0 of every workgroup, from identical inputs), then
-// e += X_B δ for this workgroup's 256 individuals; workgroup 0 stores b and the running mean.
-__global__ void __launch_bounds__(256) brr_block_kernel(const double* __restrict__ Xt, int64_t ldx, int64_t n,
-                                                        const double* __restrict__ W, int64_t j0, int nb,
-                                                        const double* __restrict__ r, double* __restrict__ b,
-                                                        double* __restrict__ bbar, const double* __restrict__ x2,
-                                                        double* __restrict__ e, const BrrState* __restrict__ st) {
-  __shared__ double Ws[BB][BB + 1];
+// partials of block 0 at the start of an iteration (after the intercept update)
+__global__ void __launch_bounds__(256) brr_dots0_kernel(const double* __restrict__ Xt, int64_t ldx, int64_t n,
+                                                        int64_t p, const double* __restrict__ e,
+                                                        double* __restrict__ partial) {
+  __shared__ double es[IW];
+  const int64_t i0 = (int64_t)blockIdx.x * IW;
+  es[threadIdx.x] = i0 + threadIdx.x < n ? e[i0 + threadIdx.x] : 0.0;
+  __syncthreads();
+  brr_partials(Xt, ldx, n, i0, 0, (int)(p < BB ? p : BB), es, partial);
+}
+
+// One block of 64 markers: r = Σ_c partial_in[c] (fixed order), the 64 single-site steps (wave 0
+// of every workgroup, identical inputs → identical results; the Gram row of lane k in registers,
+// δ_s broadcast by v_readlane), e += X_B δ on this workgroup's individuals, then the partials of
+// the next block from the updated e. Workgroup 0 stores b and the running posterior mean.
+__global__ void __launch_bounds__(256) brr_step_kernel(const double* __restrict__ Xt, int64_t ldx, int64_t n,
+                                                       int64_t p, const double* __restrict__ W, int64_t blk,
+                                                       int64_t nblk, const double* __restrict__ partial_in,
+                                                       double* __restrict__ partial_out, double* __restrict__ b,
+                                                       double* __restrict__ bbar, const double* __restrict__ x2,
+                                                       double* __restrict__ e, const BrrState* __restrict__ st) {
+  // next block's genotypes for this chunk of individuals: 64 rows x IW, row pitch 2064 B
+  // (≡ 16 B mod 256 B: the ds_read_b128 lane groups of the partials loop are conflict-free)
+  constexpr int RP = IW + 2;  // doubles
+  __shared__ __attribute__((aligned(16))) double Xn[BB * RP];
   __shared__ double delta[BB];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const double* Wb = W + (j0 / BB) * BB * BB;
-  for (int q = tid; q < BB * BB; q += 256) Ws[q / BB][q % BB] = Wb[q];
+  __shared__ double es[IW];
+  __shared__ double part4[4][BB];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int64_t j0 = blk * BB;
+  const int nb = (int)((p - j0) < BB ? (p - j0) : BB);
+  const int C = (int)gridDim.x;
+  const int64_t i0 = (int64_t)blockIdx.x * IW;
+  const int64_t i = i0 + tid;
+  const bool more = blk + 1 < nblk;
+  const int64_t j1 = j0 + BB;
+  const int nb1 = more ? (int)((p - j1) < BB ? (p - j1) : BB) : 0;
+  // every load that does not depend on this block's δ goes out first:
+  // (1) the next block's rows into LDS (global_load_lds: 1 KB per wave instruction)
+  for (int q = wave; q < 2 * nb1; q += 4) {
+    const int k = q >> 1, h = q & 1;
+    const double* src = Xt + (j1 + k) * ldx + i0 + h * 128 + lane * 2;
+    __builtin_amdgcn_global_load_lds((const void*)src, (void*)(Xn + k * RP + h * 128), 16, 0, 0);
+  }
+  // (2) this thread's 64 genotypes of the block, for e += X_B δ (rows past p clamped; δ = 0)
+  double xv[BB];
+#pragma unroll
+  for (int s2 = 0; s2 < BB; s2++) xv[s2] = Xt[(j0 + (s2 < nb ? s2 : 0)) * ldx + i];
+  const double e_old = e[i];
+  // (3) wave 0's operands
+  double w[BB];
+  double xx = 0.0, bo = 0.0, varE = 0.0, varB = 0.0;
+  const bool on = lane < nb;
+  const int64_t j = j0 + lane;
+  if (tid < 64) {
+    const double* wr = W + (blk * BB + lane) * BB;  // row `lane` = column `lane` (symmetric)
+#pragma unroll
+    for (int q = 0; q < BB; q += 2) {
+      const double2 v = *reinterpret_cast<const double2*>(wr + q);
+      w[q] = v.x;
+      w[q + 1] = v.y;
+    }
+    xx = on ? x2[j] : 0.0;
+    bo = on ? b[j] : 0.0;
+    varE = st->varE;
+    varB = st->varB;
+  }
+  {
+    // r = Σ_c partial_in[c]: wave w sums c ≡ w (mod 4), 16 loads in flight per round, then a
+    // fixed-order combine — every workgroup gets bit-identical r
+    double a = 0.0;
+    for (int c0 = wave; c0 < C; c0 += 64) {
+      double v[16];
+#pragma unroll
+      for (int m = 0; m < 16; m++) v[m] = (c0 + 4 * m < C) ? partial_in[(c0 + 4 * m) * BB + lane] : 0.0;
+#pragma unroll
+      for (int m = 0; m < 16; m++) a += v[m];
+    }
+    part4[wave][lane] = a;
+  }
   __syncthreads();
   if (tid < 64) {
-    const double varE = st->varE, varB = st->varB;
-    const bool on = lane < nb;
-    const int64_t j = j0 + lane;
-    const double xx = on ? x2[j] : 0.0;
-    const double bo = on ? b[j] : 0.0;
+    double d = ((part4[0][lane] + part4[1][lane]) + part4[2][lane]) + part4[3][lane];
     // c = x2/σ²_e + 1/σ²_b; b_new = (d + x2 b)/σ²_e / c + sqrt(1/c) ξ = d α + β
     const double cinv = 1.0 / (xx / varE + 1.0 / varB);
-    const double alpha = cinv / varE;
+    const double alpha = on ? cinv / varE : 0.0;
     const double xi = on ? brr_normal(st->seed, 4 * (uint64_t)st->it, (uint64_t)j) : 0.0;
-    const double beta = xx * bo * alpha + sqrt(cinv) * xi;
-    double d = on ? r[lane] : 0.0;
-    double bn = bo;
-    for (int s = 0; s < nb; s++) {
-      double dl = 0.0;
-      if (lane == s) {
-        bn = fma(d, alpha, beta);
-        dl = bo - bn;
-      }
-      // broadcast δ_s (v_readlane of both halves)
+    const double beta = on ? xx * bo * alpha + sqrt(cinv) * xi : 0.0;
+    double bfin = bo;
+#ifdef GBM_DEBUG_BRR_NOSEQ  // timing experiment only
+    constexpr int NSEQ = 0;
+#else
+    constexpr int NSEQ = BB;
+#endif
+#pragma unroll
+    for (int s2 = 0; s2 < NSEQ; s2++) {
+      const double bn = fma(d, alpha, beta);
+      bfin = lane == s2 ? bn : bfin;
       union {
         double f;
-        int w[2];
+        int i[2];
       } u;
-      u.f = dl;
-      u.w[0] = __builtin_amdgcn_readlane(u.w[0], s);
-      u.w[1] = __builtin_amdgcn_readlane(u.w[1], s);
-      d = fma(u.f, Ws[s][lane], d);
-      if (lane == 0) delta[s] = u.f;
+      u.f = bo - bn;
+      u.i[0] = __builtin_amdgcn_readlane(u.i[0], s2);
+      u.i[1] = __builtin_amdgcn_readlane(u.i[1], s2);
+      d = fma(u.f, w[s2], d);
     }
+    delta[lane] = bo - bfin;
     if (blockIdx.x == 0 && on) {
-      b[j] = bn;
+      b[j] = bfin;
       if (brr_accumulate(st)) {
         const double k = (double)(st->nsum + 1);
-        bbar[j] = bbar[j] * ((k - 1.0) / k) + bn / k;
+        bbar[j] = bbar[j] * ((k - 1.0) / k) + bfin / k;
       }
     }
   }
   __syncthreads();
-  const int64_t i = (int64_t)blockIdx.x * 256 + tid;
+  double ei = 0.0;
   if (i < n) {
-    double acc = 0.0;
-    for (int s = 0; s < nb; s++) acc = fma(delta[s], Xt[(j0 + s) * ldx + i], acc);
-    e[i] += acc;
+    double acc0 = 0.0, acc1 = 0.0;
+#pragma unroll
+    for (int s2 = 0; s2 < BB; s2 += 2) {
+      acc0 = fma(delta[s2], xv[s2], acc0);
+      acc1 = fma(delta[s2 + 1], xv[s2 + 1], acc1);
+    }
+    ei = e_old + (acc0 + acc1);
+    e[i] = ei;
+  }
+#ifdef GBM_DEBUG_BRR_NOPART  // timing experiment only
+  if (false) {
+#else
+  if (more) {
+#endif
+    es[tid] = ei;
+    __syncthreads();  // also completes the global_load_lds of Xn
+    // partial[c][k] = Σ_u Xn[k][w*64 + u] es[w*64 + u]: lane k = marker, wave w = quarter
+    double s0 = 0.0, s1 = 0.0;
+    if (lane < nb1) {
+      const double* xr = Xn + lane * RP + wave * 64;
+      const double* er = es + wave * 64;
+#pragma unroll
+      for (int u = 0; u < 64; u += 2) {
+        const double2 xv2 = *reinterpret_cast<const double2*>(xr + u);
+        s0 = fma(xv2.x, er[u], s0);
+        s1 = fma(xv2.y, er[u + 1], s1);
+      }
+    }
+    part4[wave][lane] = s0 + s1;
+    __syncthreads();
+    if (tid < 64)
+      partial_out[blockIdx.x * BB + lane] = ((part4[0][lane] + part4[1][lane]) + part4[2][lane]) + part4[3][lane];
   }
 }
 
@@ -264,7 +374,8 @@ extern "C" int gbm_brr_fit(const double* X, int64_t n, int64_t p, int64_t ldx, c
   stw.dev = dev;
   GBM_HIP_TRY(hipStreamCreateWithFlags(&stw.s, hipStreamNonBlocking));
   hipStream_t s = stw.s;
-  const int64_t npad = npad_of(n), nblk = (p + BB - 1) / BB;
+  // Xt rows and e padded to whole IW-individual chunks (the block kernels read full chunks)
+  const int64_t npad = round_up(n, IW), nblk = (p + BB - 1) / BB;
   DevMem Xt, colmean, x2, W, e, b, bbar, r, stm, pb, part, pout;
   GBM_TRY(dalloc(Xt, dev, p * npad * 8));
   GBM_TRY(dalloc(colmean, dev, p * 8));
@@ -273,7 +384,7 @@ extern "C" int gbm_brr_fit(const double* X, int64_t n, int64_t p, int64_t ldx, c
   GBM_TRY(dalloc(e, dev, npad * 8));
   GBM_TRY(dalloc(b, dev, p * 8));
   GBM_TRY(dalloc(bbar, dev, p * 8));
-  GBM_TRY(dalloc(r, dev, BB * 8));
+  GBM_TRY(dalloc(r, dev, 2 * ((n + IW - 1) / IW) * BB * 8));  // ping-pong partial dots
   GBM_TRY(dalloc(stm, dev, sizeof(BrrState)));
   GBM_HIP_TRY(hipMemsetAsync(Xt.p, 0, (size_t)(p * npad * 8), s));
   GBM_HIP_TRY(hipMemcpy2DAsync(Xt.p, npad * 8, X, ldx * 8, n * 8, p, hipMemcpyHostToDevice, s));
@@ -320,17 +431,15 @@ extern "C" int gbm_brr_fit(const double* X, int64_t n, int64_t p, int64_t ldx, c
   GBM_HIP_TRY(hipStreamSynchronize(s));
   // one Gibbs iteration, captured once and replayed
   auto* stp = (BrrState*)stm.p;
-  const unsigned eblocks = (unsigned)((n + 255) / 256);
+  const unsigned C = (unsigned)((n + IW - 1) / IW);
   auto enqueue_iteration = [&]() -> int {
     brr_mu_kernel<<<1, 1024, 0, s>>>((double*)e.p, n, stp);
+    brr_dots0_kernel<<<C, 256, 0, s>>>((const double*)Xt.p, npad, n, p, (const double*)e.p, (double*)r.p);
     for (int64_t k = 0; k < nblk; k++) {
-      const int64_t j0 = k * BB;
-      const int nb = (int)std::min<int64_t>(BB, p - j0);
-      brr_dots_kernel<<<(unsigned)nb, 256, 0, s>>>((const double*)Xt.p, npad, n, (const double*)e.p, j0,
-                                                   (double*)r.p);
-      brr_block_kernel<<<eblocks, 256, 0, s>>>((const double*)Xt.p, npad, n, (const double*)W.p, j0, nb,
-                                               (const double*)r.p, (double*)b.p, (double*)bbar.p,
-                                               (const double*)x2.p, (double*)e.p, stp);
+      double* pin = (double*)r.p + (k & 1) * (int64_t)C * BB;
+      double* pout = (double*)r.p + ((k + 1) & 1) * (int64_t)C * BB;
+      brr_step_kernel<<<C, 256, 0, s>>>((const double*)Xt.p, npad, n, p, (const double*)W.p, k, nblk, pin, pout,
+                                        (double*)b.p, (double*)bbar.p, (const double*)x2.p, (double*)e.p, stp);
     }
     brr_var_kernel<<<1, 1024, 0, s>>>((const double*)b.p, p, (const double*)e.p, n, stp);
     return hipGetLastError() == hipSuccess ? GBM_OK : fail(GBM_E_HIP, "gbm_brr_fit: launch failed");
