@@ -223,7 +223,7 @@ def main():
         },
         "roofline": {
             "bound": "mfma",
-            "kernel": "syrk_kernel<kStore|kSlab> (GRM, fp64 v_mfma_f64_16x16x4_f64)",
+            "kernel": "syrk_kernel<kSplit> (GRM, fp64 v_mfma_f64_16x16x4_f64)",
             "achieved": achieved,
             "peak": PEAK_F64_TFLOPS,
             "unit": "TFLOP/s",

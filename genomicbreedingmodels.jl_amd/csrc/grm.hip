@@ -181,8 +181,15 @@ syrk_kernel(const double* __restrict__ U, int64_t ldu, int64_t K, int64_t c0, in
   const int64_t rlim = c0 + lim;
 
   if constexpr (MODE == kSplit) {
-    const int sl = (int)(wg / ntiles);
-    const int64_t t = wg - (int64_t)sl * ntiles;
+    // XCD-aware order: workgroups are dispatched round-robin over the 8 XCDs (id mod 8), so each
+    // slice is launched as T8 = round_up(ntiles, 8) workgroups and XCD x takes the contiguous tile
+    // range [x T8/8, (x+1) T8/8) of every slice — neighbouring tiles share A/B strips in that
+    // XCD's L2, and later slices revisit the same range
+    const int64_t T8 = (ntiles + 7) & ~(int64_t)7;
+    const int sl = (int)(wg / T8);
+    const int64_t u = wg - (int64_t)sl * T8;
+    const int64_t t = (u & 7) * (T8 >> 3) + (u >> 3);
+    if (t >= ntiles) return;
     int64_t ti, tj;
     tile_of(t, ti, tj);
     const bool diag = (ti == tj);
@@ -199,7 +206,7 @@ syrk_kernel(const double* __restrict__ U, int64_t ldu, int64_t K, int64_t c0, in
     if (active) {
       // a single slice stores straight into G (no workspace, the reduce is a no-op)
       const int64_t ld = sb.n == 1 ? ldc : BT;
-      double* out = (sb.n == 1 ? C + i0 * ldc + j0 : slab + wg * (int64_t)(BT * BT)) +
+      double* out = (sb.n == 1 ? C + i0 * ldc + j0 : slab + ((int64_t)sl * ntiles + t) * (BT * BT)) +
                     (wm * 64 + 4 * frag_row) * ld + wn * 64 + 4 * frag_col;
 #pragma unroll
       for (int m = 0; m < 4; m++)
@@ -555,7 +562,7 @@ int launch_grm_syrk(const double* Zt, int64_t ldz, int64_t p, int64_t n, double*
   if (need > 0 && (!ws || ws_bytes < need))
     return fail(GBM_E_ARG, "gbm_dev_grm: workspace too small (" + std::to_string(ws_bytes) + " < " +
                                std::to_string(need) + ")");
-  syrk_kernel<kSplit><<<(unsigned)(g.sb.n * g.ntiles), 256, 0, s>>>(Zt, ldz, p, 0, n, G, ldg, (double*)ws, g.ntiles,
+  syrk_kernel<kSplit><<<(unsigned)(g.sb.n * ((g.ntiles + 7) & ~(int64_t)7)), 256, 0, s>>>(Zt, ldz, p, 0, n, G, ldg, (double*)ws, g.ntiles,
                                                                     g.sb, nullptr, nullptr, nullptr, -1);
   GBM_LAUNCH_CHECK();
   return GBM_OK;

@@ -9,8 +9,8 @@ for V in $VARIANTS; do
   IFS=: read -r BKV WPSV XDEF <<< "$V"
   set -- $BKV $WPSV
   D=$OUT/bk$1_w$2$XDEF; mkdir -p $D
-  for f in stats grm chol effects; do hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 -DGBM_BK=$1 -DGBM_WPS=$2 ${XDEF:+-D${XDEF//+/ -D}} -c $C/$f.hip -o $D/$f.o || exit 1; done
-  hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 -c $C/capi.cpp -o $D/capi.o || exit 1
+  for f in stats grm chol effects gibbs; do hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 -DGBM_BK=$1 -DGBM_WPS=$2 ${XDEF:+-D${XDEF//+/ -D}} -c $C/$f.hip -o $D/$f.o || exit 1; done
+  hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 -c $C/capi.cpp -o $D/capi.o && hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 -c $C/session.cpp -o $D/session.o || exit 1
   hipcc --offload-arch=gfx950 -shared -fPIC $D/*.o -lrccl -o $D/libgbm.so || exit 1
   case "$XDEF" in GBM_DEBUG_NO*|GBM_DEBUG_SAME*|TIME*) echo -n "BK $1 WPS $2 $XDEF: "; GBM_LIBGBM=$PWD/$D/libgbm.so timeout -k 10 200 python tools/time_grm.py || exit 1; continue;; esac
   if [ "$XDEF" = GBM_DEBUG_WGTIME ]; then GBM_LIBGBM=$PWD/$D/libgbm.so timeout -k 10 200 python tools/wgtime.py; continue; fi

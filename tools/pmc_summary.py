@@ -34,8 +34,8 @@ def main(root):
             "fetch_kib_raw": fk, "write_kib": wk,
             "hbm_bytes_per_launch": ((2 * fk if fk else 0) + (wk or 0)) * 1024 if (fk or wk) else None,
         }
-    syrk = [v for k, v in out["kernels"].items()
-            if "grm_syrk_kernel" in k or "syrk_kernel<0>" in k or "syrk_kernel<1>" in k]
+    # the GRM SYRK is syrk_kernel<1> (kSplit); syrk_kernel<0> is the Cholesky trailing update
+    syrk = [v for k, v in out["kernels"].items() if "syrk_kernel<1>" in k]
     if syrk:
         out["hbm_bytes_per_launch"] = syrk[0]["hbm_bytes_per_launch"]
         out["algorithmic_bytes_per_launch"] = 8.0 * out["n"] * out["p"]
