@@ -59,7 +59,7 @@ __global__ void __launch_bounds__(256) factor_first_kernel(const double* __restr
                                                            double* __restrict__ Ld, double* __restrict__ Dinv,
                                                            int32_t* __restrict__ info) {
   __shared__ __attribute__((aligned(16))) double Us[CNB * PS];
-  __shared__ double rinv[CNB];
+  __shared__ double rinv[CNB + 16];
   const int tid = threadIdx.x;
   {
     const int row = tid >> 2, quarter = tid & 3;

@@ -46,14 +46,14 @@ __device__ __forceinline__ void mfma_tile_sub_t(double* dst, int r0, int c0, con
   for (int r = 0; r < 4; r++) dst[(r0 + fr + 4 * r) * PS + c0 + fc] -= acc[r];
 }
 
+// rinv must hold CNB + 16 doubles (the last 16 are scratch).
 // Upper Cholesky of the 64x64 block in Us (U-layout, pitch PS, upper part valid) by a
 // 256-thread workgroup: four 16-row sub-panels, each a right-looking 16-step loop on wave 0
 // (lane r owns column o + r; u_cs broadcast by v_readlane) followed by the MFMA update of the
 // block's remaining upper 16x16 tiles on all waves. Leaves U in Us (zeros below the diagonal)
-// and 1/U_ii in rinv. Returns, in every lane of wave 0, the first failing column or -1.
+// and 1/U_ii in rinv. Returns, in every lane, the first failing column or -1.
 __device__ __forceinline__ int factor_diag_block(double* Us, double* rinv, int tid) {
   const int lane = tid & 63, wave = tid >> 6;
-  int badcol = -1;
   for (int kb = 0; kb < 4; kb++) {
     const int o = kb * 16;
     if (wave == 0) {
@@ -62,13 +62,20 @@ __device__ __forceinline__ int factor_diag_block(double* Us, double* rinv, int t
       double x[16];
 #pragma unroll
       for (int t = 0; t < 16; t++) x[t] = Us[(o + t) * PS + cc];
+      // serial chain per step: readlane pivot → rsqrt → scale → row c of U through LDS (one
+      // store, broadcast reads; LDS ops of one wave complete in order) → update. A
+      // non-positive or non-finite pivot propagates NaN/≤0 onto the diagonal (checked below),
+      // so the loop has no branches.
+      double* bc = rinv + CNB;  // 16-double broadcast row
 #pragma unroll
       for (int c = 0; c < 16; c++) {
         const double piv = readlane_d(x[c], c);
-        if ((!(piv > 0.0) || !isfinite(piv)) && badcol < 0) badcol = o + c;
         const double lc = x[c] * rsqrt_nr(piv);  // lane c: piv/sqrt(piv) = U[c][c]
+        if (lane < 16) bc[lane] = lc;
+        __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): the row is in LDS before it is read
+        __builtin_amdgcn_wave_barrier();
 #pragma unroll
-        for (int sidx = c + 1; sidx < 16; sidx++) x[sidx] -= lc * readlane_d(lc, sidx);
+        for (int sidx = c + 1; sidx < 16; sidx++) x[sidx] = fma(-lc, bc[sidx], x[sidx]);
         x[c] = lc;
       }
       if (lane < ncols) {
@@ -95,7 +102,11 @@ __device__ __forceinline__ int factor_diag_block(double* Us, double* rinv, int t
     if (c < r) Us[r * PS + c] = 0.0;
   }
   __syncthreads();
-  return badcol;
+  // first failing column: U_cc = sqrt(pivot) is not a positive finite number
+  const double dg = Us[lane * PS + lane];
+  const bool bad = !(dg > 0.0) || !isfinite(dg);
+  const unsigned long long m = __ballot(bad);
+  return m ? (int)__builtin_ctzll(m) : -1;
 }
 
 // Store a factored block: Ld_blk (64x64 row-major, upper, zeros below) and the inverses of its

@@ -50,6 +50,10 @@ enum SyrkMode { kSub = 0, kSplit = 1 };
 #ifdef GBM_DEBUG_WGTIME  // timing experiment only: per-workgroup start/end clocks + hardware id
 __device__ unsigned long long g_wgtime[3 * 16384];
 #endif
+#ifdef GBM_DEBUG_FACTIME  // timing experiment only: phases of the in-update diagonal factor
+__device__ unsigned long long g_factime[4 * 1024];
+__device__ unsigned long long g_factime_n;
+#endif
 
 // acc[m][q] += (NEG ? −1 : 1) Σ_k U[k][i0 + ·] U[k][j0 + ·] over the stages [kstep0, kstep0 + nsteps)
 // (BK loci each) of one BT x BT tile. Operands are staged by global_load_lds into the two LDS
@@ -78,7 +82,9 @@ __device__ __forceinline__ void tile_pass(const double* __restrict__ U, int64_t 
       const double* src = U + k * ldu;
 #endif
       __builtin_amdgcn_global_load_lds((const void*)(src + i0 + lane * 2), (void*)la, 16, 0, 0);
+#ifndef GBM_DEBUG_AONLY  // timing experiment only: B operand never staged (wrong results)
       if (!diag) __builtin_amdgcn_global_load_lds((const void*)(src + j0 + lane * 2), (void*)lb, 16, 0, 0);
+#endif
     } else {
       *reinterpret_cast<double2*>(la + lane * 2) = make_double2(0.0, 0.0);
       if (!diag) *reinterpret_cast<double2*>(lb + lane * 2) = make_double2(0.0, 0.0);
@@ -130,6 +136,9 @@ __device__ __forceinline__ void tile_pass(const double* __restrict__ U, int64_t 
     }
 #ifdef GBM_DEBUG_NOBARRIER  // timing experiment only: racy (wrong results)
     __builtin_amdgcn_s_waitcnt(0);
+#elif defined(GBM_DEBUG_NOVMWAIT)  // timing experiment only: barrier without waiting for the loads
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    __builtin_amdgcn_s_barrier();
 #else
     __syncthreads();
 #endif
@@ -163,7 +172,7 @@ syrk_kernel(const double* __restrict__ U, int64_t ldu, int64_t K, int64_t c0, in
             double* __restrict__ C, int64_t ldc, double* __restrict__ slab, int64_t ntiles, SliceBounds sb,
             double* __restrict__ Ld, double* __restrict__ Dinv, int32_t* __restrict__ info, int64_t fk0) {
   // 2 stages (72 KB at BK = 16); kSub's first workgroup reuses it for the 64x64 factor image
-  constexpr int LDS_DOUBLES = (2 * STAGE > CNB * PS + CNB) ? 2 * STAGE : CNB * PS + CNB;
+  constexpr int LDS_DOUBLES = (2 * STAGE > CNB * PS + CNB + 16) ? 2 * STAGE : CNB * PS + CNB + 16;
   __shared__ __attribute__((aligned(16))) double lds[LDS_DOUBLES];
 
   const int64_t wg = blockIdx.x;
@@ -417,6 +426,9 @@ __global__ void __launch_bounds__(256, 2)
 syrk64_sub_kernel(const double* __restrict__ U, int64_t ldu, int64_t c0, int64_t lim, double* __restrict__ C,
                   int64_t ldc, double* __restrict__ Ld, double* __restrict__ Dinv, int32_t* __restrict__ info,
                   int64_t fk0, int rowonly) {
+#ifdef GBM_DEBUG_FACTIME
+  const unsigned long long ft0 = wall_clock64();
+#endif
   __shared__ __attribute__((aligned(16))) double As[64 * P64];
   __shared__ __attribute__((aligned(16))) double Bs[64 * P64];
   int64_t ti = 0, tj = blockIdx.x;  // rowonly: the first tile row only (the next panel's rows)
@@ -490,9 +502,26 @@ syrk64_sub_kernel(const double* __restrict__ U, int64_t ldu, int64_t c0, int64_t
 #pragma unroll
         for (int r = 0; r < 4; r++) Us[(wm * 32 + m * 16 + fr + 4 * r) * PS + wn * 32 + q * 16 + fc] = acc[m][q][r];
     __syncthreads();
+#ifdef GBM_DEBUG_FACTIME
+    const unsigned long long ft1 = wall_clock64();
+#endif
     const int bad = factor_diag_block(Us, rinv, tid);
+#ifdef GBM_DEBUG_FACTIME
+    const unsigned long long ft2 = wall_clock64();
+#endif
     if (tid == 0 && bad >= 0) atomicCAS(info, 0, (int32_t)(fk0 + bad + 1));
     store_factor(Us, rinv, Ld + fk0 * CNB, Dinv + (fk0 / 16) * 256, tid);
+#ifdef GBM_DEBUG_FACTIME
+    if (tid == 0) {
+      const unsigned long long k = atomicAdd(&g_factime_n, 1ull);
+      if (k < 1024) {
+        g_factime[4 * k] = ft0;
+        g_factime[4 * k + 1] = ft1;
+        g_factime[4 * k + 2] = ft2;
+        g_factime[4 * k + 3] = wall_clock64();
+      }
+    }
+#endif
   }
 }
 
@@ -603,6 +632,15 @@ extern "C" int gbm_dev_grm_reduce(int64_t n, int64_t p, double* G, int64_t ldg, 
   if (!G || n < 1 || p < 1 || ldg < gbm::npad_of(n)) return gbm::fail(GBM_E_ARG, "gbm_dev_grm_reduce: bad arguments");
   return gbm::launch_grm_reduce(n, p, G, ldg, workspace, (hipStream_t)stream);
 }
+
+#ifdef GBM_DEBUG_FACTIME
+extern "C" int gbm_debug_factime(void* host, int64_t* count) {
+  unsigned long long n = 0;
+  if (hipMemcpyFromSymbol(&n, HIP_SYMBOL(gbm::g_factime_n), 8) != hipSuccess) return -1;
+  *count = (int64_t)n;
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(gbm::g_factime), 4 * 1024 * 8) == hipSuccess ? 0 : -1;
+}
+#endif
 
 #ifdef GBM_DEBUG_WGTIME
 extern "C" int gbm_debug_wgtime(void* host, int64_t count) {
