@@ -146,6 +146,97 @@ __device__ __forceinline__ void tile_pass(const double* __restrict__ U, int64_t 
   __syncthreads();
 }
 
+// s_waitcnt immediate for vmcnt(v) lgkmcnt(0) (expcnt untouched): vmcnt bits [3:0] + [15:14]
+constexpr int waitcnt_vm_lgkm0(int v) { return 0x70 | (v & 0xF) | ((v >> 4) << 14); }
+
+#ifndef GBM_DEEP_BK
+// 0: the GRM uses tile_pass (BK = 16, 2 buffers). Measured at C2: (8, 4) 20.6 ms, (12, 3)
+// 20.9 ms vs 19.6 ms — deeper prefetch does not pay for the extra barriers
+#define GBM_DEEP_BK 0
+#endif
+#ifndef GBM_DEEP_NBUF
+#define GBM_DEEP_NBUF 3
+#endif
+constexpr int DBK = GBM_DEEP_BK > 0 ? GBM_DEEP_BK : 4;
+constexpr int DNBUF = GBM_DEEP_NBUF;
+constexpr int DSTAGE = 2 * DBK * LROW;
+
+// GRM variant of tile_pass with DNBUF LDS stages of DBK loci: the loads of stage st + DNBUF - 1
+// are issued while stage st is computed, and the per-stage wait keeps the newest DNBUF - 2 stages'
+// loads in flight (s_waitcnt vmcnt(n), one barrier per stage). The DMA is inline asm so that the
+// compiler does not order every LDS read after it (see grm_syrk8_kernel).
+// Loci [kb, ke) in stages of DBK rows (rows past ke are zero-filled in LDS).
+__device__ __forceinline__ void tile_pass_deep(const double* __restrict__ U, int64_t ldu, int64_t kb, int64_t ke,
+                                               int64_t i0, int64_t j0, bool diag, bool active, double* lds,
+                                               d4 (&acc)[4][4], int wave, int lane) {
+  const int wm = wave >> 1, wn = wave & 1;
+  constexpr int RPW = DBK / 4;  // locus rows staged per wave
+  const int64_t nsteps = ke > kb ? (ke - kb + DBK - 1) / DBK : 0;
+  const int64_t K = ke;
+  auto stage = [&](int64_t sidx, int buf) {
+    double* base = lds + buf * DSTAGE;
+#pragma unroll
+    for (int rr = 0; rr < RPW; rr++) {
+      const int r = wave * RPW + rr;
+      const int64_t k = kb + sidx * DBK + r;
+      double* la = base + r * LROW;
+      double* lb = base + (DBK + r) * LROW;
+      if (k < K) {
+        const double* src = U + k * ldu;
+        const unsigned ma = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)la);
+        asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off"
+                     : : "s"(ma), "v"(src + i0 + lane * 2) : "memory");
+        if (!diag) {
+          const unsigned mb = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)lb);
+          asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off"
+                       : : "s"(mb), "v"(src + j0 + lane * 2) : "memory");
+        }
+      } else {
+        *reinterpret_cast<double2*>(la + lane * 2) = make_double2(0.0, 0.0);
+        if (!diag) *reinterpret_cast<double2*>(lb + lane * 2) = make_double2(0.0, 0.0);
+      }
+    }
+  };
+  const int frag_row = lane >> 4, frag_col = lane & 15;
+#pragma unroll
+  for (int q = 0; q < DNBUF - 1; q++)
+    if (q < nsteps) stage(q, q);
+  for (int64_t st = 0; st < nsteps; st++) {
+    // stage st complete and visible; stages st+1 .. st+DNBUF-2 may stay in flight unless one of
+    // them runs past ke (fewer loads issued: then wait for everything)
+    const int64_t ahead = (nsteps - 1 - st) < (DNBUF - 2) ? (nsteps - 1 - st) : (DNBUF - 2);
+    const bool full = kb + (st + ahead + 1) * DBK <= K;
+    if (ahead == DNBUF - 2 && full) {
+      if (diag) __builtin_amdgcn_s_waitcnt(waitcnt_vm_lgkm0((DNBUF - 2) * RPW));
+      else __builtin_amdgcn_s_waitcnt(waitcnt_vm_lgkm0((DNBUF - 2) * RPW * 2));
+    } else {
+      __builtin_amdgcn_s_waitcnt(waitcnt_vm_lgkm0(0));
+    }
+    __builtin_amdgcn_s_barrier();
+    if (st + DNBUF - 1 < nsteps) stage(st + DNBUF - 1, (int)((st + DNBUF - 1) % DNBUF));
+    if (active) {
+      const double* A = lds + (int)(st % DNBUF) * DSTAGE;
+      const double* B = diag ? A : A + DBK * LROW;
+#pragma unroll
+      for (int ks = 0; ks < DBK / 4; ks++) {
+        const int kr = ks * 4 + frag_row;
+        const double2 a01 = *reinterpret_cast<const double2*>(&A[kr * LROW + wm * 64 + 4 * frag_col]);
+        const double2 a23 = *reinterpret_cast<const double2*>(&A[kr * LROW + wm * 64 + 4 * frag_col + 2]);
+        const double2 b01 = *reinterpret_cast<const double2*>(&B[kr * LROW + wn * 64 + 4 * frag_col]);
+        const double2 b23 = *reinterpret_cast<const double2*>(&B[kr * LROW + wn * 64 + 4 * frag_col + 2]);
+        const double af[4] = {a01.x, a01.y, a23.x, a23.y};
+        const double bf[4] = {b01.x, b01.y, b23.x, b23.y};
+#pragma unroll
+        for (int m = 0; m < 4; m++)
+#pragma unroll
+          for (int q = 0; q < 4; q++)
+            acc[m][q] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[m], bf[q], acc[m][q], 0, 0, 0);
+      }
+    }
+  }
+  __syncthreads();
+}
+
 // Loci split of the GRM: every tile is cut into the same nslices stage ranges
 // [b[s], b[s+1]); workgroup (s, t) = blockIdx s * ntiles + t sums range s of tile t into slab
 // slot (s, t). The ranges shrink from first to last (plan() below), so the hardware's in-order
@@ -172,7 +263,8 @@ syrk_kernel(const double* __restrict__ U, int64_t ldu, int64_t K, int64_t c0, in
             double* __restrict__ C, int64_t ldc, double* __restrict__ slab, int64_t ntiles, SliceBounds sb,
             double* __restrict__ Ld, double* __restrict__ Dinv, int32_t* __restrict__ info, int64_t fk0) {
   // 2 stages (72 KB at BK = 16); kSub's first workgroup reuses it for the 64x64 factor image
-  constexpr int LDS_DOUBLES = (2 * STAGE > CNB * PS + CNB + 16) ? 2 * STAGE : CNB * PS + CNB + 16;
+  constexpr int LDS_A = (2 * STAGE > CNB * PS + CNB + 16) ? 2 * STAGE : CNB * PS + CNB + 16;
+  constexpr int LDS_DOUBLES = (GBM_DEEP_BK > 0 && DNBUF * DSTAGE > LDS_A) ? DNBUF * DSTAGE : LDS_A;
   __shared__ __attribute__((aligned(16))) double lds[LDS_DOUBLES];
 
   const int64_t wg = blockIdx.x;
@@ -211,7 +303,10 @@ syrk_kernel(const double* __restrict__ U, int64_t ldu, int64_t K, int64_t c0, in
       for (int b = 0; b < 4; b++) acc[a][b] = (d4){0.0, 0.0, 0.0, 0.0};
     const int64_t ks0 = sb.b[sl];
     const int64_t ks1 = sb.b[sl + 1] < nst ? sb.b[sl + 1] : nst;
-    tile_pass<false>(U, ldu, K, i0, j0, diag, active, ks0, ks1 > ks0 ? ks1 - ks0 : 0, lds, acc, wave, lane);
+    if constexpr (GBM_DEEP_BK > 0)
+      tile_pass_deep(U, ldu, ks0 * BK, (ks1 * BK < K ? ks1 * BK : K), i0, j0, diag, active, lds, acc, wave, lane);
+    else
+      tile_pass<false>(U, ldu, K, i0, j0, diag, active, ks0, ks1 > ks0 ? ks1 - ks0 : 0, lds, acc, wave, lane);
     if (active) {
       // a single slice stores straight into G (no workspace, the reduce is a no-op)
       const int64_t ld = sb.n == 1 ? ldc : BT;
@@ -314,6 +409,173 @@ __global__ void __launch_bounds__(256) grm_slab_reduce_kernel(const double* __re
   }
 }
 
+// ---- GRM SYRK, wide variant: 256x128 tiles, 8 waves, 3-stage LDS pipeline ------------------
+// One 512-thread workgroup per CU (2 waves per SIMD, as the 128x128 kernel at 2 workgroups per
+// CU), tile rows 256 (A strip) x cols 128 (B strip): 25 % fewer staged bytes per flop, and the
+// 149 KB of LDS hold three stages, so the loads of stage st+2 are issued while stage st is
+// computed and the per-stage wait leaves stage st+1's loads in flight (s_waitcnt vmcnt(n), not
+// vmcnt(0)). Tiles: for tile column tj, row pairs ti2 = 0 .. tj/2 (the 128-row block 2 ti2 <= tj).
+constexpr int W8R = 256, W8C = 128;
+constexpr int LRA = W8R + 2;  // 2064 B: ≡ 16 B mod 256 B, conflict-free ds_read_b128 fragments
+constexpr int LRB = W8C + 2;  // 1040 B
+constexpr int ST8 = BK * (LRA + LRB);
+constexpr int NBUF8 = 3;
+
+__host__ __device__ inline int64_t tiles8_of_nt(int64_t nt) {
+  const int64_t M = nt / 2;
+  return (nt & 1) ? (M + 1) * (M + 1) : M * (M + 1);
+}
+__device__ __forceinline__ void tile8_of(int64_t t, int64_t& ti2, int64_t& tj) {
+  // columns 2m and 2m+1 hold m+1 tiles each; column 2m starts at m(m+1), column 2m+1 at (m+1)^2
+  int64_t m = (int64_t)((sqrt(4.0 * (double)t + 1.0) - 1.0) * 0.5);
+  while ((m + 1) * (m + 2) <= t) m++;
+  while (m * (m + 1) > t) m--;
+  if (t < (m + 1) * (m + 1)) {
+    tj = 2 * m;
+    ti2 = t - m * (m + 1);
+  } else {
+    tj = 2 * m + 1;
+    ti2 = t - (m + 1) * (m + 1);
+  }
+}
+
+__global__ void __launch_bounds__(512, 1)
+grm_syrk8_kernel(const double* __restrict__ U, int64_t ldu, int64_t K, int64_t lim, double* __restrict__ C,
+                 int64_t ldc, double* __restrict__ slab, int64_t ntiles, SliceBounds sb) {
+  __shared__ __attribute__((aligned(16))) double lds[NBUF8 * ST8];
+  const int64_t wg = blockIdx.x;
+  const int64_t T8 = (ntiles + 7) & ~(int64_t)7;  // XCD-aware order, as syrk_kernel<kSplit>
+  const int sl = (int)(wg / T8);
+  const int64_t u = wg - (int64_t)sl * T8;
+  const int64_t t = (u & 7) * (T8 >> 3) + (u >> 3);
+  if (t >= ntiles) return;
+  int64_t ti2, tj;
+  tile8_of(t, ti2, tj);
+  const int64_t i0 = ti2 * W8R, j0 = tj * W8C;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  const int frag_row = lane >> 4, frag_col = lane & 15;
+  // B strip inside the A strip (tile columns 2 ti2 and 2 ti2 + 1): read B from A's LDS rows
+  const int bshare = (tj == 2 * ti2) ? 0 : (tj == 2 * ti2 + 1 ? W8C : -1);
+  const bool active = (i0 / 64 + wm <= j0 / 64 + wn) && (i0 + 64 * wm < lim) && (j0 + 64 * wn < lim);
+  const int64_t nst = (K + BK - 1) / BK;
+  const int64_t ks0 = sb.b[sl];
+  const int64_t ks1 = sb.b[sl + 1] < nst ? sb.b[sl + 1] : nst;
+  const int64_t nsteps = ks1 > ks0 ? ks1 - ks0 : 0;
+  // per stage: A = BK rows x 2 KB (2 wave instructions each), B = BK rows x 1 KB; spread over the
+  // 8 waves: instruction q = wave + 8 m; every wave issues the same count (vmcnt bookkeeping)
+  const int nA = 2 * BK, nq = bshare < 0 ? 3 * BK : 2 * BK;
+  const int nload = nq / 8;
+  auto stage = [&](int64_t kstep, int buf) {
+    double* base = lds + buf * ST8;
+#pragma unroll
+    for (int m = 0; m < 6; m++) {
+      if (m >= nload) break;
+      const int q = wave + 8 * m;
+      int r, h;
+      double* dst;
+      int64_t col;
+      if (q < nA) {
+        r = q >> 1;
+        h = q & 1;
+        dst = base + r * LRA + h * 128;
+        col = i0 + h * 128;
+      } else {
+        r = q - nA;
+        h = 0;
+        dst = base + BK * LRA + r * LRB;
+        col = j0;
+      }
+      const int64_t k = kstep * BK + r;
+      if (k < K) {
+        // inline asm, not the builtin: the compiler's waitcnt pass would otherwise order every
+        // later LDS read after this DMA (vmcnt(0) before the MFMA fragments), which defeats the
+        // three-stage pipeline; the explicit s_waitcnt vmcnt(n) below does the ordering
+        const unsigned m0v = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)dst);
+        const double* g = U + k * ldu + col + lane * 2;
+        asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off" : : "s"(m0v), "v"(g) : "memory");
+      } else {
+        *reinterpret_cast<double2*>(dst + lane * 2) = make_double2(0.0, 0.0);
+      }
+    }
+  };
+  d4 acc[4][4];
+#pragma unroll
+  for (int a = 0; a < 4; a++)
+#pragma unroll
+    for (int b = 0; b < 4; b++) acc[a][b] = (d4){0.0, 0.0, 0.0, 0.0};
+  if (nsteps > 0) stage(ks0, 0);
+  if (nsteps > 1) stage(ks0 + 1, 1);
+  for (int64_t st = 0; st < nsteps; st++) {
+    // stage st complete (stage st+1's loads may stay in flight), visible to every wave, and every
+    // wave done with stage st-1's buffer, which the loads of stage st+2 reuse
+    // (a partial last stage past K issues fewer loads: wait for everything then)
+    if (st + 1 < nsteps && (ks0 + st + 2) * BK <= K) {
+      if (nload == 6) __builtin_amdgcn_s_waitcnt(0x0076);  // vmcnt(6) lgkmcnt(0)
+      else __builtin_amdgcn_s_waitcnt(0x0074);             // vmcnt(4) lgkmcnt(0)
+    } else {
+      __builtin_amdgcn_s_waitcnt(0x0070);  // vmcnt(0) lgkmcnt(0)
+    }
+    __builtin_amdgcn_s_barrier();
+    if (st + 2 < nsteps) stage(ks0 + st + 2, (int)((st + 2) % NBUF8));
+    if (active) {
+      const double* A = lds + (int)(st % NBUF8) * ST8;
+      const double* B = bshare < 0 ? A + BK * LRA : A + bshare;
+      const int ldb = bshare < 0 ? LRB : LRA;
+#pragma unroll
+      for (int ks = 0; ks < BK / 4; ks++) {
+        const int kr = ks * 4 + frag_row;
+        const double2 a01 = *reinterpret_cast<const double2*>(&A[kr * LRA + wm * 64 + 4 * frag_col]);
+        const double2 a23 = *reinterpret_cast<const double2*>(&A[kr * LRA + wm * 64 + 4 * frag_col + 2]);
+        const double2 b01 = *reinterpret_cast<const double2*>(&B[kr * ldb + wn * 64 + 4 * frag_col]);
+        const double2 b23 = *reinterpret_cast<const double2*>(&B[kr * ldb + wn * 64 + 4 * frag_col + 2]);
+        const double af[4] = {a01.x, a01.y, a23.x, a23.y};
+        const double bf[4] = {b01.x, b01.y, b23.x, b23.y};
+#pragma unroll
+        for (int m = 0; m < 4; m++)
+#pragma unroll
+          for (int q = 0; q < 4; q++)
+            acc[m][q] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[m], bf[q], acc[m][q], 0, 0, 0);
+      }
+    }
+  }
+  // every quadrant stores (inactive ones write zeros): the reduce reads whole tiles
+  const int64_t ld = sb.n == 1 ? ldc : W8C;
+  if (sb.n == 1 && !active) return;
+  double* out = (sb.n == 1 ? C + i0 * ldc + j0 : slab + ((int64_t)sl * ntiles + t) * (W8R * W8C)) +
+                (wm * 64 + 4 * frag_row) * ld + wn * 64 + 4 * frag_col;
+#pragma unroll
+  for (int m = 0; m < 4; m++)
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+      double* o = out + (16 * r + m) * ld;
+      *reinterpret_cast<double2*>(o) = make_double2(acc[m][0][r], acc[m][1][r]);
+      *reinterpret_cast<double2*>(o + 2) = make_double2(acc[m][2][r], acc[m][3][r]);
+    }
+}
+
+// G tile (256 x 128) = Σ_s slab[s][tile] in slice order
+__global__ void __launch_bounds__(256) grm_slab_reduce8_kernel(const double* __restrict__ slab, int64_t ntiles,
+                                                               int nslices, double* __restrict__ G, int64_t ldg,
+                                                               int64_t rows) {
+  const int64_t t = blockIdx.x;
+  int64_t ti2, tj;
+  tile8_of(t, ti2, tj);
+  const int64_t per = (int64_t)W8R * W8C;
+  for (int e = threadIdx.x * 2; e < W8R * W8C; e += 256 * 2) {
+    const int row = e / W8C, col = e % W8C;
+    if (ti2 * W8R + row >= rows) continue;  // past npad
+    double2 acc = make_double2(0.0, 0.0);
+    for (int sl = 0; sl < nslices; sl++) {
+      const double2 v = *reinterpret_cast<const double2*>(slab + ((int64_t)sl * ntiles + t) * per + e);
+      acc.x += v.x;
+      acc.y += v.y;
+    }
+    *reinterpret_cast<double2*>(G + (ti2 * W8R + row) * ldg + tj * W8C + col) = acc;
+  }
+}
+
 static int resident_wgs() {
   int dev = 0, cus = 256;
   if (hipGetDevice(&dev) == hipSuccess) {
@@ -326,14 +588,26 @@ static int resident_wgs() {
 // Plan of the GRM loci split. Candidate partitions of a tile's nst stages — uniform (1..8
 // slices) and guided (one large first range, then geometrically shrinking ones) — are scored by
 // simulating the in-order dispatch of the ntiles x nslices workgroups onto the resident slots
-// (list scheduling; diagonal tiles ~7 % cheaper; slot speeds jittered by ~2 %, as measured with
-// GBM_DEBUG_WGTIME), plus the slab-reduce cost; the fastest wins. Cached per (n, p, slots).
+// (list scheduling with per-tile costs; slot speeds jittered by ~2 %, as measured with
+// GBM_DEBUG_WGTIME), plus the slab-reduce cost; the fastest wins. Cached per (kernel, n, p, slots).
+// Kernel: the 128x128 4-wave one (default) or the 256x128 8-wave variant (GBM_GRM_KERNEL=w8;
+// 22.1 vs 19.6 ms at C2: with one workgroup per CU every barrier stalls both waves of a SIMD).
 struct GrmPlan {
-  int64_t ntiles, nst;
+  int wide;  // 1: grm_syrk8_kernel, 0: syrk_kernel<kSplit>
+  int64_t ntiles, nst, tile_elems;
   SliceBounds sb;
 };
 
-static double simulate_split(const std::vector<int64_t>& sizes, int64_t nt, int64_t R) {
+static bool grm_wide() {
+  static const bool w = [] {
+    const char* e = getenv("GBM_GRM_KERNEL");
+    return e && std::string(e) == "w8";
+  }();
+  return w;
+}
+
+static double simulate_split(const std::vector<int64_t>& sizes, const std::vector<double>& cost, int64_t R,
+                             double tile_bytes, double stage_s) {
   std::vector<double> speed(R);
   uint64_t h = 0x9E3779B97F4A7C15ull;
   for (int64_t k = 0; k < R; k++) {  // deterministic jitter, sd ≈ 2 %
@@ -343,33 +617,44 @@ static double simulate_split(const std::vector<int64_t>& sizes, int64_t nt, int6
   std::priority_queue<std::pair<double, int64_t>, std::vector<std::pair<double, int64_t>>, std::greater<>> slots;
   for (int64_t k = 0; k < R; k++) slots.push({0.0, k});
   double makespan = 0.0;
-  for (int64_t sz : sizes) {
-    int64_t t = 0;
-    for (int64_t tj = 0; tj < nt; tj++)
-      for (int64_t ti = 0; ti <= tj; ti++, t++) {
-        auto [f, k] = slots.top();
-        slots.pop();
-        f += (double)sz * (ti == tj ? 0.93 : 1.0) / speed[k];
-        if (f > makespan) makespan = f;
-        slots.push({f, k});
-      }
-  }
-  // slab reduce: one 128 KB tile partial read per (slice, tile) at ~4 TB/s, in units of stage
-  // time (~3.9 us per 16-locus stage of a 128x128 tile at 2 workgroups per CU)
-  const double reduce_stages = (double)sizes.size() * (double)(nt * (nt + 1) / 2) * 131072.0 / 4e12 / 3.9e-6;
+  for (int64_t sz : sizes)
+    for (double c : cost) {
+      auto [f, k] = slots.top();
+      slots.pop();
+      f += (double)sz * c / speed[k];
+      if (f > makespan) makespan = f;
+      slots.push({f, k});
+    }
+  // slab reduce: one tile partial read per (slice, tile) at ~4 TB/s, in stage-time units
+  const double reduce_stages = (double)sizes.size() * (double)cost.size() * tile_bytes / 4e12 / stage_s;
   return makespan + reduce_stages;
 }
 
 static GrmPlan plan(int64_t n, int64_t p) {
   GrmPlan g;
   const int64_t nt = npad_of(n) / BT;
-  g.ntiles = nt * (nt + 1) / 2;
+  g.wide = grm_wide() ? 1 : 0;
   g.nst = (p + BK - 1) / BK;
-  const int64_t R = resident_wgs();
+  std::vector<double> cost;
+  int64_t R = resident_wgs();
+  if (g.wide) {
+    // tile column tj even: the second 128-row block is below the diagonal, its 4 waves idle and
+    // the other 4 get their SIMDs alone (~0.6 of a full tile)
+    for (int64_t tj = 0; tj < nt; tj++)
+      for (int64_t ti2 = 0; ti2 <= tj / 2; ti2++) cost.push_back((tj == 2 * ti2) ? 0.6 : 1.0);
+    g.ntiles = tiles8_of_nt(nt);
+    g.tile_elems = (int64_t)W8R * W8C;
+    R = R / WPS;  // one 512-thread workgroup per CU
+  } else {
+    for (int64_t tj = 0; tj < nt; tj++)
+      for (int64_t ti = 0; ti <= tj; ti++) cost.push_back(ti == tj ? 0.93 : 1.0);
+    g.ntiles = nt * (nt + 1) / 2;
+    g.tile_elems = (int64_t)BT * BT;
+  }
   static std::mutex mu;
-  static std::map<std::tuple<int64_t, int64_t, int64_t>, SliceBounds> cache;
+  static std::map<std::tuple<int, int64_t, int64_t, int64_t>, SliceBounds> cache;
   std::lock_guard<std::mutex> lock(mu);
-  auto key = std::make_tuple(nt, g.nst, R);
+  auto key = std::make_tuple(g.wide, nt, g.nst, R);
   auto it = cache.find(key);
   if (it != cache.end()) {
     g.sb = it->second;
@@ -401,10 +686,13 @@ static GrmPlan plan(int64_t n, int64_t p) {
       }
       cands.push_back(v);
     }
+  // stage time: ~3.9 us per 16-locus stage of a 128x128 tile at 2 workgroups per CU (7.8 us per
+  // 256x128 stage at one workgroup per CU)
+  const double stage_s = g.wide ? 7.8e-6 : 3.9e-6;
   double best = 1e300;
   std::vector<int64_t> bestv{g.nst};
   for (const auto& v : cands) {
-    const double m = simulate_split(v, nt, R);
+    const double m = simulate_split(v, cost, R, (double)g.tile_elems * 8.0, stage_s);
     if (m < best * 0.999) {
       best = m;
       bestv = v;
@@ -569,7 +857,7 @@ int launch_chol_update(double* G, int64_t ldg, int64_t k0, int64_t nb, int64_t g
 
 int64_t grm_workspace_bytes(int64_t n, int64_t p) {
   const GrmPlan g = plan(n, p);
-  return g.sb.n == 1 ? 0 : (int64_t)g.sb.n * g.ntiles * BT * BT * (int64_t)sizeof(double);
+  return g.sb.n == 1 ? 0 : (int64_t)g.sb.n * g.ntiles * g.tile_elems * (int64_t)sizeof(double);
 }
 
 static int check_grm_args(const double* Zt, int64_t ldz, int64_t p, int64_t n, double* G, int64_t ldg) {
@@ -591,8 +879,12 @@ int launch_grm_syrk(const double* Zt, int64_t ldz, int64_t p, int64_t n, double*
   if (need > 0 && (!ws || ws_bytes < need))
     return fail(GBM_E_ARG, "gbm_dev_grm: workspace too small (" + std::to_string(ws_bytes) + " < " +
                                std::to_string(need) + ")");
-  syrk_kernel<kSplit><<<(unsigned)(g.sb.n * ((g.ntiles + 7) & ~(int64_t)7)), 256, 0, s>>>(Zt, ldz, p, 0, n, G, ldg, (double*)ws, g.ntiles,
-                                                                    g.sb, nullptr, nullptr, nullptr, -1);
+  const unsigned grid = (unsigned)(g.sb.n * ((g.ntiles + 7) & ~(int64_t)7));
+  if (g.wide)
+    grm_syrk8_kernel<<<grid, 512, 0, s>>>(Zt, ldz, p, n, G, ldg, (double*)ws, g.ntiles, g.sb);
+  else
+    syrk_kernel<kSplit><<<grid, 256, 0, s>>>(Zt, ldz, p, 0, n, G, ldg, (double*)ws, g.ntiles, g.sb, nullptr, nullptr,
+                                             nullptr, -1);
   GBM_LAUNCH_CHECK();
   return GBM_OK;
 }
@@ -602,7 +894,11 @@ int launch_grm_reduce(int64_t n, int64_t p, double* G, int64_t ldg, const void* 
   const GrmPlan g = plan(n, p);
   if (g.sb.n == 1) return GBM_OK;
   if (!ws) return fail(GBM_E_ARG, "gbm_dev_grm_reduce: workspace required");
-  grm_slab_reduce_kernel<<<(unsigned)g.ntiles, 256, 0, s>>>((const double*)ws, g.ntiles, g.sb.n, G, ldg);
+  if (g.wide)
+    grm_slab_reduce8_kernel<<<(unsigned)g.ntiles, 256, 0, s>>>((const double*)ws, g.ntiles, g.sb.n, G, ldg,
+                                                               npad_of(n));
+  else
+    grm_slab_reduce_kernel<<<(unsigned)g.ntiles, 256, 0, s>>>((const double*)ws, g.ntiles, g.sb.n, G, ldg);
   GBM_LAUNCH_CHECK();
   return GBM_OK;
 }
