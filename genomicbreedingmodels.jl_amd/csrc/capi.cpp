@@ -84,23 +84,34 @@ int grm_shard(const Problem& pr, Shard& sh) {
 
 const char* nccl_msg(ncclResult_t r) { return ncclGetErrorString(r); }
 
-// Sum the partial GRMs (rows [0, npad) of every shard's G) across devices.
+// Sum the partial GRMs across devices: the upper 128-tiles packed contiguously (half the bytes
+// of G's rows), all-reduced, unpacked.
 int allreduce_grm(std::vector<std::unique_ptr<Shard>>& shards, int64_t n) {
   if (shards.size() < 2) return GBM_OK;
-  const int64_t npad = npad_of(n), gdim = gdim_of(n);
+  const int64_t gdim = gdim_of(n), psz = gbm_dev_grm_packed_size(n);
   std::vector<int> devs;
   for (auto& sh : shards) devs.push_back(sh->dev);
+  std::vector<std::unique_ptr<DevMem>> packed;
+  for (auto& sh : shards) {
+    packed.push_back(std::make_unique<DevMem>());
+    GBM_HIP_TRY(hipSetDevice(sh->dev));
+    GBM_TRY(dalloc(*packed.back(), sh->dev, psz * 8));
+    GBM_TRY(gbm_dev_grm_pack((const double*)sh->G.p, gdim, n, (double*)packed.back()->p, sh->stream.s));
+  }
   std::vector<ncclComm_t> comms(shards.size());
   ncclResult_t r = ncclCommInitAll(comms.data(), (int)devs.size(), devs.data());
   if (r != ncclSuccess) return fail(GBM_E_RCCL, std::string("ncclCommInitAll: ") + nccl_msg(r));
   int rc = GBM_OK;
   r = ncclGroupStart();
   for (size_t k = 0; k < shards.size() && r == ncclSuccess; k++)
-    r = ncclAllReduce(shards[k]->G.p, shards[k]->G.p, (size_t)(npad * gdim), ncclDouble, ncclSum, comms[k],
-                      shards[k]->stream.s);
+    r = ncclAllReduce(packed[k]->p, packed[k]->p, (size_t)psz, ncclDouble, ncclSum, comms[k], shards[k]->stream.s);
   ncclResult_t r2 = ncclGroupEnd();
   if (r != ncclSuccess || r2 != ncclSuccess)
     rc = fail(GBM_E_RCCL, std::string("ncclAllReduce(partial GRM): ") + nccl_msg(r != ncclSuccess ? r : r2));
+  for (size_t k = 0; k < shards.size() && rc == GBM_OK; k++) {
+    (void)hipSetDevice(shards[k]->dev);
+    rc = gbm_dev_grm_unpack((const double*)packed[k]->p, n, (double*)shards[k]->G.p, gdim, shards[k]->stream.s);
+  }
   for (auto& sh : shards) {
     (void)hipSetDevice(sh->dev);
     if (hipStreamSynchronize(sh->stream.s) != hipSuccess && rc == GBM_OK) rc = fail(GBM_E_HIP, "stream sync after all-reduce");

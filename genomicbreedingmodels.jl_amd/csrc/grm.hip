@@ -912,6 +912,47 @@ int launch_grm(const double* Zt, int64_t ldz, int64_t p, int64_t n, double* G, i
 
 }  // namespace gbm
 
+namespace gbm {
+// Upper 128x128 tiles of G <-> a contiguous tile array (half the bytes of the npad x gdim rows):
+// the form the multi-GPU all-reduce moves.
+__global__ void __launch_bounds__(256) grm_pack_kernel(const double* __restrict__ G, int64_t ldg,
+                                                       double* __restrict__ packed, int unpack) {
+  const int64_t t = blockIdx.x;
+  int64_t ti, tj;
+  tile_of(t, ti, tj);
+  double* pt = packed + t * (int64_t)(BT * BT);
+  for (int e = threadIdx.x * 2; e < BT * BT; e += 512) {
+    const int r = e / BT, c = e % BT;
+    double* g = const_cast<double*>(G) + (ti * BT + r) * ldg + tj * BT + c;
+    if (unpack)
+      *reinterpret_cast<double2*>(g) = *reinterpret_cast<const double2*>(pt + e);
+    else
+      *reinterpret_cast<double2*>(pt + e) = *reinterpret_cast<const double2*>(g);
+  }
+}
+}  // namespace gbm
+
+extern "C" int64_t gbm_dev_grm_packed_size(int64_t n) {
+  const int64_t nt = gbm::npad_of(n) / gbm::BT;
+  return nt * (nt + 1) / 2 * gbm::BT * gbm::BT;
+}
+
+extern "C" int gbm_dev_grm_pack(const double* G, int64_t ldg, int64_t n, double* packed, void* stream) {
+  if (!G || !packed || n < 1 || ldg < gbm::npad_of(n) || (ldg & 1)) return gbm::fail(GBM_E_ARG, "gbm_dev_grm_pack: bad arguments");
+  const int64_t nt = gbm::npad_of(n) / gbm::BT;
+  gbm::grm_pack_kernel<<<(unsigned)(nt * (nt + 1) / 2), 256, 0, (hipStream_t)stream>>>(G, ldg, packed, 0);
+  GBM_LAUNCH_CHECK();
+  return GBM_OK;
+}
+
+extern "C" int gbm_dev_grm_unpack(const double* packed, int64_t n, double* G, int64_t ldg, void* stream) {
+  if (!G || !packed || n < 1 || ldg < gbm::npad_of(n) || (ldg & 1)) return gbm::fail(GBM_E_ARG, "gbm_dev_grm_unpack: bad arguments");
+  const int64_t nt = gbm::npad_of(n) / gbm::BT;
+  gbm::grm_pack_kernel<<<(unsigned)(nt * (nt + 1) / 2), 256, 0, (hipStream_t)stream>>>(G, ldg, const_cast<double*>(packed), 1);
+  GBM_LAUNCH_CHECK();
+  return GBM_OK;
+}
+
 extern "C" int64_t gbm_dev_grm_workspace(int64_t n, int64_t p) { return gbm::grm_workspace_bytes(n, p); }
 
 extern "C" int gbm_dev_grm(const double* Zt, int64_t ldz, int64_t p, int64_t n, double* G, int64_t ldg,

@@ -34,6 +34,7 @@ EXPORTS = (
     "gbm_session_create", "gbm_session_create_dosage_i8", "gbm_session_destroy", "gbm_session_gblup_fit",
     "gbm_session_predict", "gbm_session_reml_objective", "gbm_session_reml", "gbm_session_stats",
     "gbm_session_ridge_path", "gbm_session_ridge_lambda_max", "gbm_brr_fit",
+    "gbm_dev_grm_packed_size", "gbm_dev_grm_pack", "gbm_dev_grm_unpack",
 )
 
 
@@ -117,6 +118,12 @@ def _declare(lib):
     lib.gbm_session_ridge_path.argtypes = [P, P, I64, P, P, I64, P, P, I64, P]
     lib.gbm_session_ridge_lambda_max.restype = I32
     lib.gbm_session_ridge_lambda_max.argtypes = [P, P, I64, P, P]
+    lib.gbm_dev_grm_packed_size.restype = I64
+    lib.gbm_dev_grm_packed_size.argtypes = [I64]
+    lib.gbm_dev_grm_pack.restype = I32
+    lib.gbm_dev_grm_pack.argtypes = [P, I64, I64, P, P]
+    lib.gbm_dev_grm_unpack.restype = I32
+    lib.gbm_dev_grm_unpack.argtypes = [P, I64, P, I64, P]
     lib.gbm_brr_fit.restype = I32
     lib.gbm_brr_fit.argtypes = [P, I64, I64, I64, P, I64, I64, I64, D, D, U64, I32, P, P, P]
     lib.gbm_session_stats.restype = I32

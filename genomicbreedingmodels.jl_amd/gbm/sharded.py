@@ -56,7 +56,14 @@ def sharded_gblup_step(stages, comm, events=None):
     mark("grm_syrk")
     stages.grm_reduce()
     mark("grm_reduce")
-    comm.all_reduce_sum(stages.grm_rows())
+    if comm.world_size > 1:
+        # the upper GRM tiles only (half of G's rows), when the stages can pack them
+        pack = getattr(stages, "grm_pack", None)
+        if pack is not None:
+            comm.all_reduce_sum(pack())
+            stages.grm_unpack()
+        else:
+            comm.all_reduce_sum(stages.grm_rows())
     comm.all_reduce_sum(stages.q)
     mark("allreduce")
     stages.solve()
@@ -162,6 +169,19 @@ class HipShardStages:
 
     def grm_rows(self):
         return self.G[: self.npad]
+
+    def grm_pack(self):
+        """Upper GRM tiles as one contiguous tensor (the multi-GPU all-reduce operand)."""
+        if getattr(self, "Gp", None) is None:
+            self.Gp = self.torch.empty(self.lib.gbm_dev_grm_packed_size(self.n), dtype=self.torch.float64,
+                                       device=self.dev)
+        _lib.check(self.lib.gbm_dev_grm_pack(self._p(self.G), self.gdim, self.n, self._p(self.Gp), self._stream()),
+                   "grm_pack")
+        return self.Gp
+
+    def grm_unpack(self):
+        _lib.check(self.lib.gbm_dev_grm_unpack(self._p(self.Gp), self.n, self._p(self.G), self.gdim, self._stream()),
+                   "grm_unpack")
 
     def solve(self):
         _lib.check(self.lib.gbm_dev_gblup_solve(self._p(self.G), self.gdim, self.n, 0.0, self._p(self.q), self.lam,

@@ -173,6 +173,11 @@ int gbm_dev_grm(const double* Zt, int64_t ldz, int64_t p, int64_t n, double* G, 
 int gbm_dev_grm_syrk(const double* Zt, int64_t ldz, int64_t p, int64_t n, double* G, int64_t ldg,
                      void* workspace, int64_t ws_bytes, void* stream);
 int gbm_dev_grm_reduce(int64_t n, int64_t p, double* G, int64_t ldg, const void* workspace, void* stream);
+/* The upper 128x128 tiles of G as one contiguous array (packed size in doubles; pack; unpack):
+ * half the bytes of G's npad x gdim rows, the form the multi-GPU partial-GRM all-reduce moves. */
+int64_t gbm_dev_grm_packed_size(int64_t n);
+int gbm_dev_grm_pack(const double* G, int64_t ldg, int64_t n, double* packed, void* stream);
+int gbm_dev_grm_unpack(const double* packed, int64_t n, double* G, int64_t ldg, void* stream);
 /* Number of loci ranges (split-K slices) the GRM plan uses for (n, p) on the current device. */
 int gbm_dev_grm_slices(int64_t n, int64_t p);
 
