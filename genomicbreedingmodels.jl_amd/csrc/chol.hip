@@ -25,7 +25,7 @@ constexpr int MAXRHS = 63;
 
 int launch_chol_update(double* G, int64_t ldg, int64_t k0, int64_t nb, int64_t gdim, double* Ld, double* Dinv,
                        int32_t* info, int64_t next_k0, hipStream_t s);
-int launch_chol_row_update(double* G, int64_t ldg, int64_t k0, int64_t gdim, double* Ld, double* Dinv,
+int launch_chol_row_update(double* G, int64_t ldg, int64_t k0, int kch, int64_t gdim, double* Ld, double* Dinv,
                            int32_t* info, hipStream_t s);
 int64_t chol_small_lim();
 
@@ -370,18 +370,32 @@ extern "C" int gbm_dev_gblup_solve(double* G, int64_t ldg, int64_t n, double inv
     chol_panel_kernel<<<(unsigned)chunks, 256, 0, s>>>(G, ldg, k0, Ld, Dinv);
     return hipGetLastError() == hipSuccess;
   };
+  // 4-panel groups (one K = 256 trailing update) while the trailing matrix exceeds this many rows
+  static const int64_t group4_lim = [] {
+    const char* e = getenv("GBM_CHOL_G4_LIM");
+    return e ? (int64_t)atoll(e) : (int64_t)8192;
+  }();
   for (int64_t kb = 0; kb < nb;) {
     const int64_t k0 = kb * NB;
     if (!panel(k0)) return fail(GBM_E_HIP, "chol_panel_kernel launch failed");
     int rc;
-    if (pair_panels && kb + 2 < nb && gdim - (k0 + 2 * NB) > chol_small_lim()) {
-      // two panels per pass over the trailing matrix (it is HBM/MALL-bound at K = 64): update
-      // only the next panel's rows, factor that panel, then one K = 128 trailing update
-      rc = launch_chol_row_update(G, ldg, k0, gdim, Ld, Dinv, info, s);
-      if (rc != GBM_OK) return rc;
-      if (!panel(k0 + NB)) return fail(GBM_E_HIP, "chol_panel_kernel launch failed");
-      rc = launch_chol_update(G, ldg, k0, 2 * NB, gdim, Ld, Dinv, info, k0 + 2 * NB, s);
-      kb += 2;
+    // groups of g panels share one pass over the trailing matrix (HBM/MALL-bound at K = 64,
+    // balanced at K = 128, MFMA-bound at K = 256): the rows of panels 2..g of the group are
+    // brought up to date with the group's earlier panels (row update with K = 64 j), factored and
+    // solved one after the other, then one K = 64 g trailing update
+    int g = 1;
+    if (pair_panels && group4_lim >= 0 && kb + 4 < nb && gdim - (k0 + 4 * NB) > group4_lim)
+      g = 4;
+    else if (pair_panels && kb + 2 < nb && gdim - (k0 + 2 * NB) > chol_small_lim())
+      g = 2;
+    if (g > 1) {
+      for (int j = 1; j < g; j++) {
+        rc = launch_chol_row_update(G, ldg, k0, j, gdim, Ld, Dinv, info, s);
+        if (rc != GBM_OK) return rc;
+        if (!panel(k0 + j * NB)) return fail(GBM_E_HIP, "chol_panel_kernel launch failed");
+      }
+      rc = launch_chol_update(G, ldg, k0, g * NB, gdim, Ld, Dinv, info, k0 + g * NB, s);
+      kb += g;
     } else {
       // trailing update; its first workgroup also factors the next diagonal block
       rc = launch_chol_update(G, ldg, k0, NB, gdim, Ld, Dinv, info, kb + 1 < nb ? k0 + NB : -1, s);

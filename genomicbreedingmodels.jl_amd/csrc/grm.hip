@@ -713,7 +713,7 @@ constexpr int P64 = 80;  // LDS pitch: the two 16-lane halves of a fragment read
 __global__ void __launch_bounds__(256, 2)
 syrk64_sub_kernel(const double* __restrict__ U, int64_t ldu, int64_t c0, int64_t lim, double* __restrict__ C,
                   int64_t ldc, double* __restrict__ Ld, double* __restrict__ Dinv, int32_t* __restrict__ info,
-                  int64_t fk0, int rowonly) {
+                  int64_t fk0, int rowonly, int kchunks) {
 #ifdef GBM_DEBUG_FACTIME
   const unsigned long long ft0 = wall_clock64();
 #endif
@@ -741,33 +741,41 @@ syrk64_sub_kernel(const double* __restrict__ U, int64_t ldu, int64_t c0, int64_t
           acc[m][q][r] = (row < rlim && col < rlim) ? C[row * ldc + col] : 0.0;
         }
   }
-  {
-    const int k = tid >> 2, quarter = tid & 3;
-    const double* sa = U + k * ldu + i0 + quarter * 16;
-    const double* sb = U + k * ldu + j0 + quarter * 16;
+  // K = 64 kchunks: the chunks are staged one after the other (kchunks > 1 only for the row
+  // updates that bring a later panel of a 4-panel group up to date)
+  const double* B = diag ? As : Bs;
+  for (int c = 0; c < kchunks; c++) {
+    if (c > 0) __syncthreads();  // every wave is done with the previous chunk
+    {
+      const int k = tid >> 2, quarter = tid & 3;
+      const double* sa = U + (c * 64 + k) * ldu + i0 + quarter * 16;
+      const double* sb = U + (c * 64 + k) * ldu + j0 + quarter * 16;
 #pragma unroll
-    for (int e = 0; e < 16; e += 2) {
-      *reinterpret_cast<double2*>(&As[k * P64 + quarter * 16 + e]) = *reinterpret_cast<const double2*>(sa + e);
-      if (!diag)
-        *reinterpret_cast<double2*>(&Bs[k * P64 + quarter * 16 + e]) = *reinterpret_cast<const double2*>(sb + e);
+      for (int e = 0; e < 16; e += 2) {
+        *reinterpret_cast<double2*>(&As[k * P64 + quarter * 16 + e]) = *reinterpret_cast<const double2*>(sa + e);
+        if (!diag)
+          *reinterpret_cast<double2*>(&Bs[k * P64 + quarter * 16 + e]) = *reinterpret_cast<const double2*>(sb + e);
+      }
+    }
+    __syncthreads();
+    if (active) {
+#pragma unroll
+      for (int ks = 0; ks < 16; ks++) {
+        double af[2], bf[2];
+#pragma unroll
+        for (int m = 0; m < 2; m++) af[m] = -As[(ks * 4 + fr) * P64 + wm * 32 + m * 16 + fc];
+#pragma unroll
+        for (int q = 0; q < 2; q++) bf[q] = B[(ks * 4 + fr) * P64 + wn * 32 + q * 16 + fc];
+#pragma unroll
+        for (int m = 0; m < 2; m++)
+#pragma unroll
+          for (int q = 0; q < 2; q++)
+            acc[m][q] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[m], bf[q], acc[m][q], 0, 0, 0);
+      }
     }
   }
-  __syncthreads();
   const bool factor_next = fk0 >= 0 && blockIdx.x == 0;
   if (!active && !factor_next) return;
-  const double* B = diag ? As : Bs;
-#pragma unroll
-  for (int ks = 0; ks < (active ? 16 : 0); ks++) {
-    double af[2], bf[2];
-#pragma unroll
-    for (int m = 0; m < 2; m++) af[m] = -As[(ks * 4 + fr) * P64 + wm * 32 + m * 16 + fc];
-#pragma unroll
-    for (int q = 0; q < 2; q++) bf[q] = B[(ks * 4 + fr) * P64 + wn * 32 + q * 16 + fc];
-#pragma unroll
-    for (int m = 0; m < 2; m++)
-#pragma unroll
-      for (int q = 0; q < 2; q++) acc[m][q] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[m], bf[q], acc[m][q], 0, 0, 0);
-  }
 #pragma unroll
   for (int m = 0; m < 2; m++)
 #pragma unroll
@@ -821,14 +829,16 @@ int64_t chol_small_lim() {
   return v;
 }
 
-// Block row [k0+64, k0+128) only: C[k0+64 : k0+128, k0+64 : gdim] -= U[k0:k0+64, ·]ᵀ U[k0:k0+64, ·]
-// (the next panel's rows, so that two panels can share one K = 128 trailing update); the first
-// workgroup factors the diagonal block at k0+64 afterwards.
-int launch_chol_row_update(double* G, int64_t ldg, int64_t k0, int64_t gdim, double* Ld, double* Dinv,
+// Block row [k1, k1+64) only, k1 = k0 + 64 kch: C[k1 : k1+64, k1 : gdim] -= U[k0:k1, ·]ᵀ U[k0:k1, ·]
+// (a later panel's rows of a 2- or 4-panel group, brought up to date with the group's earlier
+// panels so that the whole group shares one K = 128 / 256 trailing update); the first workgroup
+// factors the diagonal block at k1 afterwards.
+int launch_chol_row_update(double* G, int64_t ldg, int64_t k0, int kch, int64_t gdim, double* Ld, double* Dinv,
                            int32_t* info, hipStream_t s) {
-  const int64_t k1 = k0 + 64;
+  const int64_t k1 = k0 + 64 * (int64_t)kch;
   const int64_t lim = gdim - k1;
-  syrk64_sub_kernel<<<(unsigned)(lim / 64), 256, 0, s>>>(G + k0 * ldg, ldg, k1, lim, G, ldg, Ld, Dinv, info, k1, 1);
+  syrk64_sub_kernel<<<(unsigned)(lim / 64), 256, 0, s>>>(G + k0 * ldg, ldg, k1, lim, G, ldg, Ld, Dinv, info, k1, 1,
+                                                         kch);
   GBM_LAUNCH_CHECK();
   return GBM_OK;
 }
@@ -843,7 +853,7 @@ int launch_chol_update(double* G, int64_t ldg, int64_t k0, int64_t nb, int64_t g
   if (nb == 64 && lim <= chol_small_lim()) {
     const int64_t m = (lim + 63) / 64;
     syrk64_sub_kernel<<<(unsigned)(m * (m + 1) / 2), 256, 0, s>>>(G + k0 * ldg, ldg, k1, lim, G, ldg, Ld, Dinv, info,
-                                                                  next_k0, 0);
+                                                                  next_k0, 0, 1);
     GBM_LAUNCH_CHECK();
     return GBM_OK;
   }
