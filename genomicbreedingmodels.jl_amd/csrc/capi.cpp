@@ -175,6 +175,7 @@ int run_fit(const Problem& pr, const double* Y, int64_t ldy, int64_t nrhs, doubl
     int32_t info = 0;
     GBM_HIP_TRY(hipMemcpyAsync(&info, sh.info.p, 4, hipMemcpyDeviceToHost, s));
     GBM_HIP_TRY(hipStreamSynchronize(s));
+    if (info < 0) return fail(GBM_E_HIP, "back substitution: block synchronisation timed out");
     if (info != 0)
       return fail(GBM_E_NOTPD, "G/q + lambda*I is not positive definite (pivot " + std::to_string(info) +
                                    "); check for non-finite genotypes");

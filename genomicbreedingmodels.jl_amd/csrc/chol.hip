@@ -15,6 +15,7 @@
 // The reference inverts V with pinv/SVD (src/gwas.jl:472,595); for λ > 0 V is SPD and the
 // Cholesky solution is the same up to rounding.
 #include <cstdlib>
+#include <string>
 
 #include "chol_device.h"
 
@@ -164,14 +165,17 @@ __global__ void __launch_bounds__(64) diag_inverse_kernel(const double* __restri
 // ---- μ̂ and the back-substitution right-hand sides w_t = W_{1+t} − μ̂_t W_0 ---------------------
 // W_s is column npad + s of the factored rows (row npad + s of the lower copy); the Schur
 // block holds −W_sᵀW_t.
+// (also clears the per-block flags of back_solve_kernel, which runs next)
 __global__ void __launch_bounds__(256) gls_mu_kernel(const double* __restrict__ G, int64_t ld, int64_t npad,
                                                      int64_t nrhs, double* __restrict__ W, int64_t lda,
-                                                     double* __restrict__ mu) {
+                                                     double* __restrict__ mu, int32_t* __restrict__ flags) {
   const int64_t t = blockIdx.y;
   const double c11 = -G[npad * ld + npad];
   const double c1y = -G[npad * ld + npad + 1 + t];
   const double m = c1y / c11;
   if (blockIdx.x == 0 && threadIdx.x == 0) mu[t] = m;
+  if (t == 0)
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < npad / NB; i += (int64_t)gridDim.x * 256) flags[i] = 0;
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < lda; i += (int64_t)gridDim.x * 256)
     W[t * lda + i] = i < npad ? G[(npad + 1 + t) * ld + i] - m * G[npad * ld + i] : 0.0;
 }
@@ -316,6 +320,103 @@ __global__ void __launch_bounds__(256) back_update_kernel(const double* __restri
   }
 }
 
+// ---- sync-free blocked back substitution: one workgroup per 64-block, flags between them ------
+// U a = w with U's off-diagonal blocks read from the lower copy L = Uᵀ (coalesced along the rows
+// i of block b) and the diagonal blocks through their inverses (Linv). Workgroup w owns block
+// b = nb − 1 − w: it folds in U_bc a_c for every c > b as soon as block c publishes a_c (flag[c]
+// = pass), then a_b = U_bb⁻¹ (w_b − Σ_c U_bc a_c) and publishes its own flag. A workgroup only
+// waits for lower-numbered workgroups, which the in-order dispatch has already placed, so the
+// chain cannot deadlock whatever the residency. The critical path is one 64x64 step per block
+// (the L blocks are loaded before the wait). a travels through agent-scope (L2-bypassing)
+// atomic loads/stores: the 8 XCD L2s are not coherent with each other. A wait that does not end
+// (it cannot in a correct run) gives up after ~1 s and reports info = −1 instead of hanging.
+__device__ __forceinline__ double ld_agent(const double* p) {
+  return __builtin_bit_cast(double, __hip_atomic_load(reinterpret_cast<const uint64_t*>(p), __ATOMIC_RELAXED,
+                                                      __HIP_MEMORY_SCOPE_AGENT));
+}
+__device__ __forceinline__ void st_agent(double* p, double v) {
+  __hip_atomic_store(reinterpret_cast<uint64_t*>(p), __builtin_bit_cast(uint64_t, v), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ bool wait_flag(int32_t* flag, int32_t pass, int32_t* info) {
+  for (int64_t it = 0;; it++) {
+    if (__hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) >= pass) return true;
+    if ((it & 255) == 255) {
+      if (__hip_atomic_load(info, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < 0) return false;
+      if (it > (int64_t)1 << 22) {
+        __hip_atomic_store(info, -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return false;
+      }
+    }
+    __builtin_amdgcn_s_sleep(2);
+  }
+}
+__global__ void __launch_bounds__(256) back_solve_kernel(const double* __restrict__ G, int64_t ld,
+                                                         const double* __restrict__ Linv, int64_t nb,
+                                                         const double* __restrict__ W, double* __restrict__ A,
+                                                         int64_t lda, int64_t nrhs, int32_t* __restrict__ flags,
+                                                         int32_t* __restrict__ info) {
+  __shared__ double part[4][RC][NB];
+  __shared__ double rl[RC][NB];
+  __shared__ int ok_s;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int64_t b = nb - 1 - (int64_t)blockIdx.x;
+  const int64_t b0 = b * NB;
+  const int j0 = wave * 16;  // this wave's 16 of the 64 block columns
+  double ui[16];             // (U_bb⁻¹)[lane][j0 + jj]
+#pragma unroll
+  for (int jj = 0; jj < 16; jj++) ui[jj] = Linv[(b0 + lane) * NB + j0 + jj];
+  if (tid == 0) ok_s = 1;
+  int32_t pass = 0;
+  for (int64_t t0 = 0; t0 < nrhs; t0 += RC) {
+    pass++;
+    const int tc = (int)(nrhs - t0 < RC ? nrhs - t0 : RC);
+    double acc[RC] = {0.0, 0.0, 0.0, 0.0};
+    bool ok = true;
+    for (int64_t c = nb - 1; c > b && ok; c--) {
+      double l[16];  // L[64c + j0 + jj][b0 + lane] = U[b0 + lane][64c + j0 + jj]
+      const double* lp = G + (c * NB + j0) * ld + b0 + lane;
+#pragma unroll
+      for (int jj = 0; jj < 16; jj++) l[jj] = lp[(int64_t)jj * ld];
+      if (lane == 0) ok = wait_flag(&flags[c], pass, info);
+      ok = __builtin_amdgcn_readfirstlane((int)ok) != 0;
+      for (int t = 0; t < tc; t++) {
+        const double* ac = A + (t0 + t) * lda + c * NB + j0;
+        double s = 0.0;
+#pragma unroll
+        for (int jj = 0; jj < 16; jj++) s = fma(l[jj], ld_agent(ac + jj), s);
+        acc[t] += s;
+      }
+    }
+    if (!ok) ok_s = 0;
+#pragma unroll
+    for (int t = 0; t < RC; t++) part[wave][t][lane] = acc[t];
+    __syncthreads();
+    if (wave == 0)
+      for (int t = 0; t < tc; t++)
+        rl[t][lane] = W[(t0 + t) * lda + b0 + lane] -
+                      (((part[0][t][lane] + part[1][t][lane]) + part[2][t][lane]) + part[3][t][lane]);
+    __syncthreads();
+    for (int t = 0; t < tc; t++) {
+      double s = 0.0;
+#pragma unroll
+      for (int jj = 0; jj < 16; jj++) s = fma(ui[jj], rl[t][j0 + jj], s);
+      part[wave][t][lane] = s;
+    }
+    __syncthreads();
+    if (wave == 0) {
+      for (int t = 0; t < tc; t++)
+        st_agent(A + (t0 + t) * lda + b0 + lane,
+                 ((part[0][t][lane] + part[1][t][lane]) + part[2][t][lane]) + part[3][t][lane]);
+      // publish (release: the wave's a stores above are complete and visible at agent scope);
+      // a failed wait still publishes, so the workgroups behind it end quickly
+      if (lane == 0) __hip_atomic_store(&flags[b], pass, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    if (!ok_s) return;
+  }
+}
+
 // ---- GEBV = μ̂ + (y − μ̂) − λ a ------------------------------------------------------------
 __global__ void __launch_bounds__(256) gebv_kernel(const double* __restrict__ Y, int64_t ldy, int64_t n,
                                                    const double* __restrict__ A, double* __restrict__ gebv,
@@ -334,7 +435,8 @@ extern "C" int64_t gbm_dev_npad(int64_t n) { return npad_of(n); }
 extern "C" int64_t gbm_dev_gdim(int64_t n) { return gdim_of(n); }
 // scratch: the factored 64x64 diagonal blocks (npad x 64), their inverses (npad x 64) and the
 // inverses of their 16x16 diagonal sub-blocks (npad x 16)
-static int64_t solve_ws_doubles(int64_t n) { return npad_of(n) * (2 * NB + 16); }
+// + one int32 flag per 64-block for back_solve_kernel (npad/64 ints, rounded up to whole doubles)
+static int64_t solve_ws_doubles(int64_t n) { return npad_of(n) * (2 * NB + 16) + (npad_of(n) / NB + 1) / 2 + 1; }
 extern "C" int64_t gbm_dev_solve_workspace(int64_t n, int64_t nrhs) {
   (void)nrhs;
   return solve_ws_doubles(n) * (int64_t)sizeof(double);
@@ -407,9 +509,18 @@ extern "C" int gbm_dev_gblup_solve(double* G, int64_t ldg, int64_t n, double inv
   GBM_LAUNCH_CHECK();
   const unsigned gx = (unsigned)((lda + 255) / 256 < 1024 ? (lda + 255) / 256 : 1024);
   // the gebv buffer doubles as the w scratch: gebv_kernel (last) reads only Y and A
-  gls_mu_kernel<<<dim3(gx, (unsigned)nrhs), 256, 0, s>>>(G, ldg, npad, nrhs, gebv, lda, mu);
+  int32_t* flags = reinterpret_cast<int32_t*>(Dinv + npad * 16);
+  gls_mu_kernel<<<dim3(gx, (unsigned)nrhs), 256, 0, s>>>(G, ldg, npad, nrhs, gebv, lda, mu, flags);
   GBM_LAUNCH_CHECK();
-  for (int64_t end_blk = nb; end_blk > 0;) {
+  static const bool super_blocks = [] {  // GBM_BACK_SOLVE=super: the two-kernel super-block chain
+    const char* e = getenv("GBM_BACK_SOLVE");
+    return e && std::string(e) == "super";
+  }();
+  if (!super_blocks) {
+    back_solve_kernel<<<(unsigned)nb, 256, 0, s>>>(G, ldg, Linv, nb, gebv, A_out, lda, nrhs, flags, info);
+    GBM_LAUNCH_CHECK();
+  }
+  for (int64_t end_blk = super_blocks ? nb : 0; end_blk > 0;) {
     const int nsub = (int)(end_blk >= SB ? SB : end_blk);
     const int64_t s0 = (end_blk - nsub) * NB;
     back_diag_kernel<<<1, 256, 0, s>>>(G, ldg, Linv, s0, nsub, gebv, A_out, lda, nrhs);

@@ -13,6 +13,7 @@
 //     resident workgroup slot (256 CUs x 2), so there is no tail round; partial tiles go to
 //     workspace slabs that a second kernel sums in a fixed order (deterministic, no float atomics).
 #include <cmath>
+#include <cstdio>
 #include <cstdlib>
 #include <map>
 #include <mutex>
@@ -246,7 +247,88 @@ constexpr int kMaxSlices = 12;
 struct SliceBounds {
   int32_t n;
   int32_t b[kMaxSlices + 1];
+  // ragged last tile column (grm_edge_pass): columns [e0, e0 + er) of G, er <= 64, in et 16-column
+  // MFMA tiles, for all rows, by erb x es extra workgroups (256-row blocks x ekper-loci ranges)
+  // appended to the grid; partials at slab + eslab_off, summed by grm_edge_reduce_kernel
+  int32_t er, et, erb, es, ekper;
+  int64_t e0, eslab_off;
 };
+
+// Ragged last tile column of the GRM: when n = 128 (nt − 1) + r with small r, the last tile
+// column would cost nt full 128x128 tiles (a workgroup whose waves idle still holds its slot
+// for the whole tile time) for r useful columns. Instead the tiles cover [0, e0)^2 and extra
+// workgroups compute G[i][e0 + c] = Σ_k U[k][i] U[k][e0 + c], c < r, for every row i: a
+// 256-row block over a loci range per workgroup, operands straight from global memory into
+// MFMA registers (A: 4 row tiles of 16 per wave, B: et column tiles), HBM-bound (one extra
+// read of U). A separate launch after the tiles: as extra workgroups of the tile kernel it
+// raised that kernel's VGPR allocation and slowed its tiles by ~2 %.
+__device__ __forceinline__ void grm_edge_pass(const double* __restrict__ U, int64_t ldu, int64_t K,
+                                              const SliceBounds& sb, int64_t e, double* __restrict__ part,
+                                              int lane, int wave) {
+  const int rb = (int)(e % sb.erb), ks = (int)(e / sb.erb);
+  const int64_t k0 = (int64_t)ks * sb.ekper;
+  const int64_t k1 = (k0 + sb.ekper < K) ? k0 + sb.ekper : K;
+  const int64_t i0 = (int64_t)rb * 256 + wave * 64;
+  const int fr = lane >> 4, fc = lane & 15;
+  const int et = sb.et;
+  d4 acc[4][4];
+#pragma unroll
+  for (int m = 0; m < 4; m++)
+#pragma unroll
+    for (int q = 0; q < 4; q++) acc[m][q] = (d4){0.0, 0.0, 0.0, 0.0};
+  for (int64_t k = k0; k < k1; k += 16) {  // 4 MFMA k-steps per iteration, all loads first
+    double a[4][4], b[4][4];
+#pragma unroll
+    for (int st = 0; st < 4; st++) {
+      const int64_t kk = k + st * 4 + fr;
+      const bool kv = kk < k1;
+      const double* row = U + kk * ldu;
+#pragma unroll
+      for (int m = 0; m < 4; m++) {
+        const int64_t i = i0 + m * 16 + fc;
+        a[st][m] = (kv && i < ldu) ? row[i] : 0.0;
+      }
+#pragma unroll
+      for (int q = 0; q < 4; q++) b[st][q] = (kv && q < et) ? row[sb.e0 + q * 16 + fc] : 0.0;
+    }
+#pragma unroll
+    for (int st = 0; st < 4; st++)
+#pragma unroll
+      for (int q = 0; q < 4; q++)
+        if (q < et)
+#pragma unroll
+          for (int m = 0; m < 4; m++) acc[m][q] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[st][m], b[st][q], acc[m][q], 0, 0, 0);
+  }
+  const int64_t rows = (int64_t)sb.erb * 256;
+  const int w = 16 * et;
+#pragma unroll
+  for (int m = 0; m < 4; m++)
+#pragma unroll
+    for (int q = 0; q < 4; q++)
+      if (q < et)
+#pragma unroll
+        for (int r = 0; r < 4; r++)
+          part[((int64_t)ks * rows + i0 + m * 16 + fr + 4 * r) * w + q * 16 + fc] = acc[m][q][r];
+}
+
+__global__ void __launch_bounds__(256) grm_edge_kernel(const double* __restrict__ U, int64_t ldu, int64_t K,
+                                                       SliceBounds sb, double* __restrict__ part) {
+  grm_edge_pass(U, ldu, K, sb, blockIdx.x, part, threadIdx.x & 63, threadIdx.x >> 6);
+}
+
+// G[i][e0 + c] = Σ_s part[s][i][c] in range order (deterministic), i < n, c < er
+__global__ void __launch_bounds__(256) grm_edge_reduce_kernel(const double* __restrict__ part, int64_t n,
+                                                              SliceBounds sb, double* __restrict__ G, int64_t ldg) {
+  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= n * sb.er) return;
+  const int64_t i = idx / sb.er;
+  const int c = (int)(idx - i * sb.er);
+  const int64_t rows = (int64_t)sb.erb * 256;
+  const int w = 16 * sb.et;
+  double acc = 0.0;
+  for (int s = 0; s < sb.es; s++) acc += part[((int64_t)s * rows + i) * w + c];
+  G[i * ldg + sb.e0 + c] = acc;
+}
 
 // Two epilogues over one staging/MFMA core:
 //   kSplit   slab[s][t] = Σ_{k in range s} U[k][i] U[k][j]   (the GRM, split over loci)
@@ -596,6 +678,7 @@ struct GrmPlan {
   int wide;  // 1: grm_syrk8_kernel, 0: syrk_kernel<kSplit>
   int64_t ntiles, nst, tile_elems;
   SliceBounds sb;
+  int64_t main_doubles, edge_doubles;  // workspace: loci-slice partial tiles, edge partials
 };
 
 static bool grm_wide() {
@@ -617,11 +700,14 @@ static double simulate_split(const std::vector<int64_t>& sizes, const std::vecto
   std::priority_queue<std::pair<double, int64_t>, std::vector<std::pair<double, int64_t>>, std::greater<>> slots;
   for (int64_t k = 0; k < R; k++) slots.push({0.0, k});
   double makespan = 0.0;
-  for (int64_t sz : sizes)
+  for (size_t s = 0; s < sizes.size(); s++)
     for (double c : cost) {
       auto [f, k] = slots.top();
       slots.pop();
-      f += (double)sz * c / speed[k];
+      // first-range units that start after the first round run ~10 % slower (measured: they
+      // overlap other K ranges instead of streaming the same strips as their XCD's neighbours,
+      // so fewer of their operand rows hit L2); fitted on 11 measured splits at C2
+      f += (double)sizes[s] * c * ((s == 0 && f > 0.0) ? 1.10 : 1.0) / speed[k];
       if (f > makespan) makespan = f;
       slots.push({f, k});
     }
@@ -630,10 +716,22 @@ static double simulate_split(const std::vector<int64_t>& sizes, const std::vecto
   return makespan + reduce_stages;
 }
 
+static bool grm_edge_enabled() {
+  static const bool v = [] {
+    const char* e = getenv("GBM_GRM_EDGE");
+    return !e || atoi(e) != 0;
+  }();
+  return v;
+}
+
 static GrmPlan plan(int64_t n, int64_t p) {
   GrmPlan g;
-  const int64_t nt = npad_of(n) / BT;
+  const int64_t nt_all = npad_of(n) / BT;
   g.wide = grm_wide() ? 1 : 0;
+  // ragged last tile column with r <= 64 useful columns: computed by the edge workgroups
+  const int64_t r_last = n - (nt_all - 1) * BT;
+  const bool edge = !g.wide && grm_edge_enabled() && nt_all >= 8 && r_last <= 64;
+  const int64_t nt = edge ? nt_all - 1 : nt_all;
   g.nst = (p + BK - 1) / BK;
   std::vector<double> cost;
   int64_t R = resident_wgs();
@@ -655,9 +753,27 @@ static GrmPlan plan(int64_t n, int64_t p) {
   static std::map<std::tuple<int, int64_t, int64_t, int64_t>, SliceBounds> cache;
   std::lock_guard<std::mutex> lock(mu);
   auto key = std::make_tuple(g.wide, nt, g.nst, R);
+  auto finish = [&](GrmPlan& gp) {
+    gp.main_doubles = gp.sb.n == 1 ? 0 : (int64_t)gp.sb.n * gp.ntiles * gp.tile_elems;
+    gp.sb.er = 0;
+    gp.sb.et = gp.sb.erb = gp.sb.es = gp.sb.ekper = 0;
+    gp.sb.e0 = gp.sb.eslab_off = 0;
+    gp.edge_doubles = 0;
+    if (edge) {
+      gp.sb.e0 = nt * BT;
+      gp.sb.er = (int32_t)r_last;
+      gp.sb.et = (int32_t)((r_last + 15) / 16);
+      gp.sb.erb = (int32_t)((n + 255) / 256);
+      gp.sb.ekper = 512;
+      gp.sb.es = (int32_t)((p + gp.sb.ekper - 1) / gp.sb.ekper);
+      gp.sb.eslab_off = gp.main_doubles;
+      gp.edge_doubles = (int64_t)gp.sb.es * gp.sb.erb * 256 * 16 * gp.sb.et;
+    }
+  };
   auto it = cache.find(key);
   if (it != cache.end()) {
     g.sb = it->second;
+    finish(g);
     return g;
   }
   const int64_t minc = 16;  // stages per workgroup at least
@@ -691,6 +807,31 @@ static GrmPlan plan(int64_t n, int64_t p) {
   const double stage_s = g.wide ? 7.8e-6 : 3.9e-6;
   double best = 1e300;
   std::vector<int64_t> bestv{g.nst};
+  if (const char* ov = getenv("GBM_GRM_SPLIT")) {  // tuning experiments: "w0,w1,..." relative sizes
+    std::vector<double> w;
+    for (const char* q = ov; *q;) {
+      char* end = nullptr;
+      const double x = strtod(q, &end);
+      if (end == q) break;
+      if (x > 0) w.push_back(x);
+      q = (*end == ',') ? end + 1 : end;
+    }
+    if (!w.empty() && (int)w.size() <= kMaxSlices) {
+      double tot = 0;
+      for (double x : w) tot += x;
+      cands.clear();
+      std::vector<int64_t> v;
+      int64_t acc = 0;
+      double cum = 0;
+      for (size_t i = 0; i < w.size(); i++) {
+        cum += w[i];
+        const int64_t e = (i + 1 == w.size()) ? g.nst : (int64_t)std::llround(cum / tot * (double)g.nst);
+        if (e > acc) v.push_back(e - acc);
+        acc = e > acc ? e : acc;
+      }
+      cands.push_back(v);
+    }
+  }
   for (const auto& v : cands) {
     const double m = simulate_split(v, cost, R, (double)g.tile_elems * 8.0, stage_s);
     if (m < best * 0.999) {
@@ -701,7 +842,14 @@ static GrmPlan plan(int64_t n, int64_t p) {
   g.sb.n = (int32_t)bestv.size();
   g.sb.b[0] = 0;
   for (int i = 0; i < g.sb.n; i++) g.sb.b[i + 1] = g.sb.b[i] + (int32_t)bestv[i];
+  if (getenv("GBM_DEBUG_PLAN")) {
+    fprintf(stderr, "grm plan nt=%lld nst=%lld slots=%lld makespan=%.1f stages:", (long long)nt, (long long)g.nst,
+            (long long)R, best);
+    for (int i = 0; i < g.sb.n; i++) fprintf(stderr, " %lld", (long long)bestv[i]);
+    fprintf(stderr, "\n");
+  }
   cache.emplace(key, g.sb);
+  finish(g);
   return g;
 }
 
@@ -850,10 +998,16 @@ int launch_chol_update(double* G, int64_t ldg, int64_t k0, int64_t nb, int64_t g
   const int64_t k1 = k0 + nb;
   const int64_t lim = gdim - k1;
   if (lim <= 0) return GBM_OK;
-  if (nb == 64 && lim <= chol_small_lim()) {
+  // 64x64 tiles below chol_small_lim() (K = 64), or below GBM_UPD64_LIM2 rows for a K = 128
+  // pair update (more workgroups for trailing matrices that fill few 128-tile rounds)
+  static const int64_t lim2 = [] {
+    const char* e = getenv("GBM_UPD64_LIM2");
+    return e ? (int64_t)atoll(e) : (int64_t)-1;
+  }();
+  if ((nb == 64 && lim <= chol_small_lim()) || (nb == 128 && lim <= lim2)) {
     const int64_t m = (lim + 63) / 64;
     syrk64_sub_kernel<<<(unsigned)(m * (m + 1) / 2), 256, 0, s>>>(G + k0 * ldg, ldg, k1, lim, G, ldg, Ld, Dinv, info,
-                                                                  next_k0, 0, 1);
+                                                                  next_k0, 0, (int)(nb / 64));
     GBM_LAUNCH_CHECK();
     return GBM_OK;
   }
@@ -867,7 +1021,7 @@ int launch_chol_update(double* G, int64_t ldg, int64_t k0, int64_t nb, int64_t g
 
 int64_t grm_workspace_bytes(int64_t n, int64_t p) {
   const GrmPlan g = plan(n, p);
-  return g.sb.n == 1 ? 0 : (int64_t)g.sb.n * g.ntiles * g.tile_elems * (int64_t)sizeof(double);
+  return (g.main_doubles + g.edge_doubles) * (int64_t)sizeof(double);
 }
 
 static int check_grm_args(const double* Zt, int64_t ldz, int64_t p, int64_t n, double* G, int64_t ldg) {
@@ -892,18 +1046,29 @@ int launch_grm_syrk(const double* Zt, int64_t ldz, int64_t p, int64_t n, double*
   const unsigned grid = (unsigned)(g.sb.n * ((g.ntiles + 7) & ~(int64_t)7));
   if (g.wide)
     grm_syrk8_kernel<<<grid, 512, 0, s>>>(Zt, ldz, p, n, G, ldg, (double*)ws, g.ntiles, g.sb);
-  else
-    syrk_kernel<kSplit><<<grid, 256, 0, s>>>(Zt, ldz, p, 0, n, G, ldg, (double*)ws, g.ntiles, g.sb, nullptr, nullptr,
-                                             nullptr, -1);
+  else  // with an edge, the tiles cover [0, e0)^2 exactly
+    syrk_kernel<kSplit><<<grid, 256, 0, s>>>(Zt, ldz, p, 0, g.sb.er > 0 ? g.sb.e0 : n, G, ldg, (double*)ws, g.ntiles,
+                                             g.sb, nullptr, nullptr, nullptr, -1);
   GBM_LAUNCH_CHECK();
+  if (g.sb.er > 0) {
+    grm_edge_kernel<<<(unsigned)((int64_t)g.sb.erb * g.sb.es), 256, 0, s>>>(Zt, ldz, p, g.sb,
+                                                                           (double*)ws + g.sb.eslab_off);
+    GBM_LAUNCH_CHECK();
+  }
   return GBM_OK;
 }
 
 // stage 2: sum the slice partials of each tile into G
 int launch_grm_reduce(int64_t n, int64_t p, double* G, int64_t ldg, const void* ws, hipStream_t s) {
   const GrmPlan g = plan(n, p);
-  if (g.sb.n == 1) return GBM_OK;
+  if (g.sb.n == 1 && g.sb.er == 0) return GBM_OK;
   if (!ws) return fail(GBM_E_ARG, "gbm_dev_grm_reduce: workspace required");
+  if (g.sb.er > 0) {
+    grm_edge_reduce_kernel<<<(unsigned)((n * g.sb.er + 255) / 256), 256, 0, s>>>((const double*)ws + g.sb.eslab_off, n,
+                                                                                 g.sb, G, ldg);
+    GBM_LAUNCH_CHECK();
+  }
+  if (g.sb.n == 1) return GBM_OK;
   if (g.wide)
     grm_slab_reduce8_kernel<<<(unsigned)g.ntiles, 256, 0, s>>>((const double*)ws, g.ntiles, g.sb.n, G, ldg,
                                                                npad_of(n));

@@ -202,6 +202,8 @@ class HipShardStages:
         self.h_msum.copy_(self.msum, non_blocking=True)
         self.h_info.copy_(self.info, non_blocking=True)
         self.torch.cuda.current_stream(self.dev).synchronize()
+        if int(self.h_info[0]) < 0:
+            raise _lib.GBMError("back substitution: block synchronisation timed out")
         if int(self.h_info[0]) != 0:
             raise _lib.GBMError(f"G/q + λI not positive definite (pivot {int(self.h_info[0])})")
         return dict(B=self.h_B.numpy(), y_pred=self.h_gebv.numpy()[:, : self.n].T, mu=self.h_mu.numpy(),

@@ -139,3 +139,29 @@ def test_sharded_stages_single_rank_match_oracle():
     assert np.array_equal(out["y_pred"], out2["y_pred"])
     b_hat = assemble_b_hat(out["mu"], out["msum"], [out["B"]], p)
     assert rel(b_hat, ref["b_hat"]) < TOL_CONTRACT
+
+
+@pytest.mark.parametrize("n,p", [
+    (1030, 1234),   # ragged last tile column of 6: the GRM's edge workgroups
+    (1088, 37),     # edge of exactly 64 columns; fewer loci than one MFMA k-block batch
+    (1100, 2049),   # last column of 76: the ordinary (masked) tile path
+    (4999, 600),    # C2-like ragged n (edge of 7), 10 loci-range partials
+])
+def test_grm_ragged_last_tile_column(n, p):
+    X = oracle.synth_genotypes(n + p, n, p)
+    G, q = gbm.grm(X)
+    Gr, qr = oracle.grm(X)
+    assert q == qr
+    assert rel(G, Gr) < 1e-12
+    assert np.array_equal(G, G.T)
+
+
+def test_gblup_with_grm_edge_matches_oracle():
+    n, p = 1030, 1500
+    X = oracle.synth_genotypes(8, n, p)
+    Y = oracle.synth_phenotypes(X, 9, ntraits=2)
+    b_hat, y_pred, mu, q = gbm.gblup_arrays(X, Y, lambda_=1.0)
+    ref = oracle.gblup_fit(X, Y, 1.0)
+    assert q == ref["q"]
+    assert rel(y_pred, ref["y_pred"]) < TOL_TIGHT
+    assert rel(b_hat, ref["b_hat"]) < TOL_CONTRACT

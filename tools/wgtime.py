@@ -45,3 +45,26 @@ for x in range(8):
 key = (xcc.astype(np.int64) << 8) | ((hw >> 8) & 0xFF).astype(np.int64)
 u, inv, cnt = np.unique(key, return_inverse=True, return_counts=True)
 print("WGs per (xcc, se/sh/cu) slot histogram:", np.bincount(cnt))
+# per tile class within each loci slice: interior, diagonal, ragged last tile column (tj = nt-1)
+nt = (n + 127) // 128
+if nt >= 8 and n - (nt - 1) * 128 <= 64 and os.environ.get("GBM_GRM_EDGE", "1") != "0":
+    nt -= 1  # ragged last column handled by grm_edge_kernel
+ntiles = nt * (nt + 1) // 2
+T8 = (ntiles + 7) & ~7
+wg_all = np.arange(len(buf) // 3)
+rec = buf.reshape(-1, 3)[:, 1] > 0
+wgi = wg_all[rec]
+sl = wgi // T8
+u = wgi - sl * T8
+tt = (u & 7) * (T8 >> 3) + (u >> 3)
+tj = np.floor((np.sqrt(8.0 * tt + 1.0) - 1.0) / 2.0).astype(np.int64)
+tj = np.where((tj + 1) * (tj + 2) // 2 <= tt, tj + 1, tj)
+tj = np.where(tj * (tj + 1) // 2 > tt, tj - 1, tj)
+ti = tt - tj * (tj + 1) // 2
+for s_ in range(int(sl.max()) + 1):
+    m = sl == s_
+    inter = m & (ti != tj) & (tj != nt - 1)
+    dg = m & (ti == tj) & (tj != nt - 1)
+    edge = m & (tj == nt - 1)
+    print(f"slice {s_}: interior n={inter.sum()} med {np.median(dur[inter]):.1f} us | diag {np.median(dur[dg]) if dg.any() else 0:.1f}"
+          f" | last column n={edge.sum()} med {np.median(dur[edge]) if edge.any() else 0:.1f} us (ragged cols {n - (nt - 1) * 128})")
