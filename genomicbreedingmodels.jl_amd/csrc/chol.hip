@@ -25,9 +25,9 @@ constexpr int NB = kCholNB;  // 64
 constexpr int MAXRHS = 63;
 
 int launch_chol_update(double* G, int64_t ldg, int64_t k0, int64_t nb, int64_t gdim, double* Ld, double* Dinv,
-                       int32_t* info, int64_t next_k0, hipStream_t s);
+                       int32_t* info, int64_t next_k0, int32_t* fflags, bool* fused, hipStream_t s);
 int launch_chol_row_update(double* G, int64_t ldg, int64_t k0, int kch, int64_t gdim, double* Ld, double* Dinv,
-                           int32_t* info, hipStream_t s);
+                           int32_t* info, int32_t* fflags, hipStream_t s);
 int64_t chol_small_lim();
 
 // ---- V = G/q + λI (upper part), padding = identity, bordered R columns -----------------------
@@ -35,9 +35,11 @@ __global__ void __launch_bounds__(256) prepare_v_kernel(double* __restrict__ G, 
                                                         int64_t npad, int64_t gdim, double inv_q,
                                                         const int64_t* __restrict__ q_dev, double lambda,
                                                         const double* __restrict__ Y, int64_t ldy, int64_t nrhs,
-                                                        int32_t* __restrict__ info) {
+                                                        int32_t* __restrict__ info, int32_t* __restrict__ fflags) {
   const int64_t i = blockIdx.x;  // row
   if (i == 0 && threadIdx.x == 0) *info = 0;
+  if (i == 0)  // factor-published flags of the fused panels (one per 64-block)
+    for (int64_t b = threadIdx.x; b < npad / NB; b += 256) fflags[b] = 0;
   if (q_dev) inv_q = 1.0 / (double)(*q_dev);
   double* row = G + i * ld;
   const int64_t jbeg = (i / NB) * NB;  // from the start of the diagonal block
@@ -105,22 +107,8 @@ __global__ void __launch_bounds__(256) chol_panel_kernel(double* __restrict__ G,
     *reinterpret_cast<double2*>(&Di[512 + tid * 2]) = *reinterpret_cast<const double2*>(sd + 512 + tid * 2);
   }
   __syncthreads();
-  const int fr = lane >> 4, fc = lane & 15;
-  const int cw = wave * 16;
-  for (int rb = 0; rb < 4; rb++) {
-    const int o = rb * 16;
-    if (rb > 0) mfma_tile_sub_t(X, o, cw, Us, o, X, cw, 0, rb * 4, lane);  // X_rb -= U[0:o,rb]ᵀ X[0:o]
-    // X_rb = (D_rb⁻¹)ᵀ X_rb : A[i][k] = Dinv[k][i], B[k][j] = X[o+k][cw+j]
-    d4 acc = (d4){0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-    for (int ks = 0; ks < 4; ks++) {
-      const double a = Di[rb * 256 + (ks * 4 + fr) * 16 + fc];
-      const double bv = X[(o + ks * 4 + fr) * PS + cw + fc];
-      acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, bv, acc, 0, 0, 0);
-    }
-#pragma unroll
-    for (int r = 0; r < 4; r++) X[(o + fr + 4 * r) * PS + cw + fc] = acc[r];
-  }
+  panel_chunk_solve(X, Us, [&](int rb, int ks) { return Di[rb * 256 + (ks * 4 + (lane >> 4)) * 16 + (lane & 15)]; },
+                    lane, wave);
   __syncthreads();
   {
     const int row = tid >> 2, quarter = tid & 3;
@@ -330,30 +318,9 @@ __global__ void __launch_bounds__(256) back_update_kernel(const double* __restri
 // (the L blocks are loaded before the wait). a travels through agent-scope (L2-bypassing)
 // atomic loads/stores: the 8 XCD L2s are not coherent with each other. A wait that does not end
 // (it cannot in a correct run) gives up after ~1 s and reports info = −1 instead of hanging.
-__device__ __forceinline__ double ld_agent(const double* p) {
-  return __builtin_bit_cast(double, __hip_atomic_load(reinterpret_cast<const uint64_t*>(p), __ATOMIC_RELAXED,
-                                                      __HIP_MEMORY_SCOPE_AGENT));
-}
-__device__ __forceinline__ void st_agent(double* p, double v) {
-  __hip_atomic_store(reinterpret_cast<uint64_t*>(p), __builtin_bit_cast(uint64_t, v), __ATOMIC_RELAXED,
-                     __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ bool wait_flag(int32_t* flag, int32_t pass, int32_t* info) {
-  for (int64_t it = 0;; it++) {
-    if (__hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) >= pass) return true;
-    if ((it & 255) == 255) {
-      if (__hip_atomic_load(info, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < 0) return false;
-      if (it > (int64_t)1 << 22) {
-        __hip_atomic_store(info, -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        return false;
-      }
-    }
-    __builtin_amdgcn_s_sleep(2);
-  }
-}
 __global__ void __launch_bounds__(256) back_solve_kernel(const double* __restrict__ G, int64_t ld,
                                                          const double* __restrict__ Linv, int64_t nb,
-                                                         const double* __restrict__ W, double* __restrict__ A,
+                                                         const double* __restrict__ W, double* A,
                                                          int64_t lda, int64_t nrhs, int32_t* __restrict__ flags,
                                                          int32_t* __restrict__ info) {
   __shared__ double part[4][RC][NB];
@@ -380,11 +347,18 @@ __global__ void __launch_bounds__(256) back_solve_kernel(const double* __restric
       for (int jj = 0; jj < 16; jj++) l[jj] = lp[(int64_t)jj * ld];
       if (lane == 0) ok = wait_flag(&flags[c], pass, info);
       ok = __builtin_amdgcn_readfirstlane((int)ok) != 0;
+      // a_c was written through (agent-scope stores) before its flag was released; after the
+      // acquire, plain loads (all 16 in flight at once — per-element atomic loads were each
+      // waited for) read it from beyond this XCD's invalidated L2
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       for (int t = 0; t < tc; t++) {
         const double* ac = A + (t0 + t) * lda + c * NB + j0;
+        double av[16];
+#pragma unroll
+        for (int jj = 0; jj < 16; jj++) av[jj] = ac[jj];
         double s = 0.0;
 #pragma unroll
-        for (int jj = 0; jj < 16; jj++) s = fma(l[jj], ld_agent(ac + jj), s);
+        for (int jj = 0; jj < 16; jj++) s = fma(l[jj], av[jj], s);
         acc[t] += s;
       }
     }
@@ -404,15 +378,13 @@ __global__ void __launch_bounds__(256) back_solve_kernel(const double* __restric
       part[wave][t][lane] = s;
     }
     __syncthreads();
-    if (wave == 0) {
+    if (wave == 0)
       for (int t = 0; t < tc; t++)
         st_agent(A + (t0 + t) * lda + b0 + lane,
                  ((part[0][t][lane] + part[1][t][lane]) + part[2][t][lane]) + part[3][t][lane]);
-      // publish (release: the wave's a stores above are complete and visible at agent scope);
-      // a failed wait still publishes, so the workgroups behind it end quickly
-      if (lane == 0) __hip_atomic_store(&flags[b], pass, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    __syncthreads();
+    // publish once the write-through stores of a_b are complete (a failed wait still publishes,
+    // so the workgroups behind it end quickly)
+    publish_flag(&flags[b], pass, tid);
     if (!ok_s) return;
   }
 }
@@ -435,8 +407,8 @@ extern "C" int64_t gbm_dev_npad(int64_t n) { return npad_of(n); }
 extern "C" int64_t gbm_dev_gdim(int64_t n) { return gdim_of(n); }
 // scratch: the factored 64x64 diagonal blocks (npad x 64), their inverses (npad x 64) and the
 // inverses of their 16x16 diagonal sub-blocks (npad x 16)
-// + one int32 flag per 64-block for back_solve_kernel (npad/64 ints, rounded up to whole doubles)
-static int64_t solve_ws_doubles(int64_t n) { return npad_of(n) * (2 * NB + 16) + (npad_of(n) / NB + 1) / 2 + 1; }
+// + two int32 flags per 64-block (back_solve_kernel; factor published for the fused panels)
+static int64_t solve_ws_doubles(int64_t n) { return npad_of(n) * (2 * NB + 16) + npad_of(n) / NB + 1; }
 extern "C" int64_t gbm_dev_solve_workspace(int64_t n, int64_t nrhs) {
   (void)nrhs;
   return solve_ws_doubles(n) * (int64_t)sizeof(double);
@@ -458,7 +430,10 @@ extern "C" int gbm_dev_gblup_solve(double* G, int64_t ldg, int64_t n, double inv
   double* Linv = Ld + npad * NB;
   double* Dinv = Linv + npad * NB;
   hipStream_t s = (hipStream_t)stream;
-  prepare_v_kernel<<<(unsigned)gdim, 256, 0, s>>>(G, ldg, n, npad, gdim, inv_q, q_dev, lambda, Y, ldy, nrhs, info);
+  int32_t* flags = reinterpret_cast<int32_t*>(Dinv + npad * 16);
+  int32_t* fflags = flags + npad / NB;
+  prepare_v_kernel<<<(unsigned)gdim, 256, 0, s>>>(G, ldg, n, npad, gdim, inv_q, q_dev, lambda, Y, ldy, nrhs, info,
+                                                  fflags);
   GBM_LAUNCH_CHECK();
   const int64_t nb = npad / NB;
   factor_first_kernel<<<1, 256, 0, s>>>(G, ldg, Ld, Dinv, info);
@@ -477,9 +452,19 @@ extern "C" int gbm_dev_gblup_solve(double* G, int64_t ldg, int64_t n, double inv
     const char* e = getenv("GBM_CHOL_G4_LIM");
     return e ? (int64_t)atoll(e) : (int64_t)8192;
   }();
+  // GBM_CHOL_FUSE=1: the small updates also solve the next panel (first tile row, after the
+  // first workgroup publishes the factored block). Correct, but measured slower than separate
+  // panel launches (33.5 vs 20.3 + 8.9 µs per step at C2: the publish + wait + reload costs more
+  // than a launch), so off by default.
+  static const bool fuse = [] {
+    const char* e = getenv("GBM_CHOL_FUSE");
+    return e && atoi(e) != 0;
+  }();
+  int32_t* ff = fuse ? fflags : nullptr;
+  bool panel_done = false;  // the previous update already solved this panel (fused)
   for (int64_t kb = 0; kb < nb;) {
     const int64_t k0 = kb * NB;
-    if (!panel(k0)) return fail(GBM_E_HIP, "chol_panel_kernel launch failed");
+    if (!panel_done && !panel(k0)) return fail(GBM_E_HIP, "chol_panel_kernel launch failed");
     int rc;
     // groups of g panels share one pass over the trailing matrix (HBM/MALL-bound at K = 64,
     // balanced at K = 128, MFMA-bound at K = 256): the rows of panels 2..g of the group are
@@ -492,15 +477,16 @@ extern "C" int gbm_dev_gblup_solve(double* G, int64_t ldg, int64_t n, double inv
       g = 2;
     if (g > 1) {
       for (int j = 1; j < g; j++) {
-        rc = launch_chol_row_update(G, ldg, k0, j, gdim, Ld, Dinv, info, s);
+        rc = launch_chol_row_update(G, ldg, k0, j, gdim, Ld, Dinv, info, ff, s);
         if (rc != GBM_OK) return rc;
-        if (!panel(k0 + j * NB)) return fail(GBM_E_HIP, "chol_panel_kernel launch failed");
+        if (!ff && !panel(k0 + j * NB)) return fail(GBM_E_HIP, "chol_panel_kernel launch failed");
       }
-      rc = launch_chol_update(G, ldg, k0, g * NB, gdim, Ld, Dinv, info, k0 + g * NB, s);
+      rc = launch_chol_update(G, ldg, k0, g * NB, gdim, Ld, Dinv, info, k0 + g * NB, ff, &panel_done, s);
       kb += g;
     } else {
-      // trailing update; its first workgroup also factors the next diagonal block
-      rc = launch_chol_update(G, ldg, k0, NB, gdim, Ld, Dinv, info, kb + 1 < nb ? k0 + NB : -1, s);
+      // trailing update; its first workgroup also factors the next diagonal block (and, fused,
+      // the first tile row solves the next panel)
+      rc = launch_chol_update(G, ldg, k0, NB, gdim, Ld, Dinv, info, kb + 1 < nb ? k0 + NB : -1, ff, &panel_done, s);
       kb += 1;
     }
     if (rc != GBM_OK) return rc;
@@ -509,7 +495,6 @@ extern "C" int gbm_dev_gblup_solve(double* G, int64_t ldg, int64_t n, double inv
   GBM_LAUNCH_CHECK();
   const unsigned gx = (unsigned)((lda + 255) / 256 < 1024 ? (lda + 255) / 256 : 1024);
   // the gebv buffer doubles as the w scratch: gebv_kernel (last) reads only Y and A
-  int32_t* flags = reinterpret_cast<int32_t*>(Dinv + npad * 16);
   gls_mu_kernel<<<dim3(gx, (unsigned)nrhs), 256, 0, s>>>(G, ldg, npad, nrhs, gebv, lda, mu, flags);
   GBM_LAUNCH_CHECK();
   static const bool super_blocks = [] {  // GBM_BACK_SOLVE=super: the two-kernel super-block chain

@@ -31,6 +31,46 @@ __device__ __forceinline__ double readlane_d(double x, int lane) {
   return u.d;
 }
 
+// Agent-scope (L2-bypassing) 64-bit accesses and a bounded flag wait, for data exchanged
+// between workgroups of one launch (the 8 XCD L2s are not coherent with each other)
+__device__ __forceinline__ double ld_agent(const double* p) {
+  return __builtin_bit_cast(double, __hip_atomic_load(reinterpret_cast<const uint64_t*>(p), __ATOMIC_RELAXED,
+                                                      __HIP_MEMORY_SCOPE_AGENT));
+}
+__device__ __forceinline__ void st_agent(double* p, double v) {
+  __hip_atomic_store(reinterpret_cast<uint64_t*>(p), __builtin_bit_cast(uint64_t, v), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+}
+// spin until *flag >= value; gives up (info = −1, every waiter then ends) after ~1 s — a wait
+// that cannot end in a correct run must not hang the device
+// The spin itself is relaxed (an acquire per iteration would invalidate this XCD's L2 every
+// time, for every waiting wave); one acquire fence once the flag is seen.
+__device__ __forceinline__ bool wait_flag(int32_t* flag, int32_t value, int32_t* info) {
+  for (int64_t it = 0;; it++) {
+    if (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= value) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      return true;
+    }
+    if ((it & 255) == 255) {
+      if (__hip_atomic_load(info, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < 0) return false;
+      if (it > (int64_t)1 << 22) {
+        __hip_atomic_store(info, -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return false;
+      }
+    }
+    __builtin_amdgcn_s_sleep(2);
+  }
+}
+
+// Publish a flag after this workgroup's agent-scope (write-through) stores: wait for the
+// stores to complete, barrier, then one relaxed agent-scope store. (A release store would first
+// write back the XCD's whole L2 — every dirty tile of the launch — which costs several µs.)
+__device__ __forceinline__ void publish_flag(int32_t* flag, int32_t value, int tid) {
+  __builtin_amdgcn_s_waitcnt(0);  // vmcnt(0) expcnt(0) lgkmcnt(0): this wave's stores are done
+  __syncthreads();
+  if (tid == 0) __hip_atomic_store(flag, value, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // D(16x16 at (r0, c0) of dst) -= Σ_k S[kb + k][ra + row] T[kb + k][cb + col], k < 4*ksteps
 // (all operands pitch PS)
 __device__ __forceinline__ void mfma_tile_sub_t(double* dst, int r0, int c0, const double* S, int ra,
@@ -112,6 +152,8 @@ __device__ __forceinline__ int factor_diag_block(double* Us, double* rinv, int t
 // Store a factored block: Ld_blk (64x64 row-major, upper, zeros below) and the inverses of its
 // four 16x16 diagonal sub-blocks Dinv_blk[w][i][j] = (D_w⁻¹)[i][j] (upper). Wave w computes D_w⁻¹
 // column by column (lane j < 16), the dot products split over 2 partial sums.
+// AGENT: agent-scope stores, for workgroups of the same launch that read the block (fused panels).
+template <bool AGENT = false>
 __device__ __forceinline__ void store_factor(const double* Us, const double* rinv, double* Ld_blk,
                                              double* Dinv_blk, int tid) {
   const int lane = tid & 63, wave = tid >> 6;
@@ -119,8 +161,14 @@ __device__ __forceinline__ void store_factor(const double* Us, const double* rin
     const int row = tid >> 2, quarter = tid & 3;
     double* dst = Ld_blk + row * CNB + quarter * 16;
 #pragma unroll
-    for (int e = 0; e < 16; e += 2)
-      *reinterpret_cast<double2*>(dst + e) = *reinterpret_cast<const double2*>(&Us[row * PS + quarter * 16 + e]);
+    for (int e = 0; e < 16; e += 2) {
+      if constexpr (AGENT) {
+        st_agent(dst + e, Us[row * PS + quarter * 16 + e]);
+        st_agent(dst + e + 1, Us[row * PS + quarter * 16 + e + 1]);
+      } else {
+        *reinterpret_cast<double2*>(dst + e) = *reinterpret_cast<const double2*>(&Us[row * PS + quarter * 16 + e]);
+      }
+    }
   }
   const int o = wave * 16;
   const int j = lane & 15;
@@ -137,7 +185,39 @@ __device__ __forceinline__ void store_factor(const double* Us, const double* rin
   }
   if (lane < 16) {
 #pragma unroll
-    for (int i = 0; i < 16; i++) Dinv_blk[wave * 256 + i * 16 + j] = x[i];
+    for (int i = 0; i < 16; i++) {
+      if constexpr (AGENT)
+        st_agent(&Dinv_blk[wave * 256 + i * 16 + j], x[i]);
+      else
+        Dinv_blk[wave * 256 + i * 16 + j] = x[i];
+    }
+  }
+}
+
+// Block forward substitution of one 64-column chunk X (LDS, pitch PS) of a panel row, given the
+// factored diagonal block U_kk (LDS Us, pitch PS) and the inverses of its four 16x16 diagonal
+// sub-blocks: load(rb, ks) returns this lane's MFMA A operand Dinv_rb[ks*4 + (lane>>4)][lane&15]
+// (rb, ks compile-time after unrolling, so a register array can back it):
+//   X_rb <- (D_rb⁻¹)ᵀ (X_rb − U[0:o, rb]ᵀ X[0:o])  for the 16-row blocks rb = 0..3.
+// Wave w owns columns 16w..16w+15 of the chunk. All MFMA, no serial chain.
+template <typename LoadDi>
+__device__ __forceinline__ void panel_chunk_solve(double* X, const double* Us, LoadDi load, int lane, int wave) {
+  const int fr = lane >> 4, fc = lane & 15;
+  const int cw = wave * 16;
+#pragma unroll
+  for (int rb = 0; rb < 4; rb++) {
+    const int o = rb * 16;
+    if (rb > 0) mfma_tile_sub_t(X, o, cw, Us, o, X, cw, 0, rb * 4, lane);  // X_rb -= U[0:o,rb]ᵀ X[0:o]
+    // X_rb = (D_rb⁻¹)ᵀ X_rb : A[i][k] = Dinv[k][i], B[k][j] = X[o+k][cw+j]
+    d4 acc = (d4){0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int ks = 0; ks < 4; ks++) {
+      const double a = load(rb, ks);
+      const double bv = X[(o + ks * 4 + fr) * PS + cw + fc];
+      acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, bv, acc, 0, 0, 0);
+    }
+#pragma unroll
+    for (int r = 0; r < 4; r++) X[(o + fr + 4 * r) * PS + cw + fc] = acc[r];
   }
 }
 

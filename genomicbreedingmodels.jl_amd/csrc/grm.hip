@@ -12,6 +12,7 @@
 //   * stream-K over loci: the (tile, stage) units are cut into equal contiguous ranges, one per
 //     resident workgroup slot (256 CUs x 2), so there is no tail round; partial tiles go to
 //     workspace slabs that a second kernel sums in a fixed order (deterministic, no float atomics).
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -54,6 +55,9 @@ __device__ unsigned long long g_wgtime[3 * 16384];
 #ifdef GBM_DEBUG_FACTIME  // timing experiment only: phases of the in-update diagonal factor
 __device__ unsigned long long g_factime[4 * 1024];
 __device__ unsigned long long g_factime_n;
+// fused panel tiles: fk0, entry, wait begin, wait end, end, (unused)
+__device__ unsigned long long g_paneltime[6 * 16384];
+__device__ unsigned long long g_paneltime_n;
 #endif
 
 // acc[m][q] += (NEG ? −1 : 1) Σ_k U[k][i0 + ·] U[k][j0 + ·] over the stages [kstep0, kstep0 + nsteps)
@@ -243,10 +247,14 @@ __device__ __forceinline__ void tile_pass_deep(const double* __restrict__ U, int
 // slot (s, t). The ranges shrink from first to last (plan() below), so the hardware's in-order
 // dispatch onto freed slots works like guided self-scheduling: large chunks first, small ones
 // fill the tail.
-constexpr int kMaxSlices = 12;
+constexpr int kMaxSlices = 32;
 struct SliceBounds {
   int32_t n;
   int32_t b[kMaxSlices + 1];
+  // carry = 1: the loci ranges of a tile are summed in order straight into G (range s waits for
+  // range s − 1's flag, adds its partial, stores, flags s + 1); workspace = ntiles flags + 1.
+  // carry = 0: one workspace slab per (range, tile), summed by grm_slab_reduce_kernel.
+  int32_t carry;
   // ragged last tile column (grm_edge_pass): columns [e0, e0 + er) of G, er <= 64, in et 16-column
   // MFMA tiles, for all rows, by erb x es extra workgroups (256-row blocks x ekper-loci ranges)
   // appended to the grid; partials at slab + eslab_off, summed by grm_edge_reduce_kernel
@@ -389,7 +397,50 @@ syrk_kernel(const double* __restrict__ U, int64_t ldu, int64_t K, int64_t c0, in
       tile_pass_deep(U, ldu, ks0 * BK, (ks1 * BK < K ? ks1 * BK : K), i0, j0, diag, active, lds, acc, wave, lane);
     else
       tile_pass<false>(U, ldu, K, i0, j0, diag, active, ks0, ks1 > ks0 ? ks1 - ks0 : 0, lds, acc, wave, lane);
-    if (active) {
+    if (sb.carry && sb.n > 1) {
+      // in-order carry: G tile = ((P_0 + P_1) + P_2) + ..., the same order (and rounding) as the
+      // slab reduce. Range sl's predecessor was dispatched 1+ rounds earlier (lower workgroup
+      // id), so the wait is normally already satisfied and can never deadlock. The tile goes
+      // through agent-scope (write-through) stores; the successor may run on another XCD.
+      int32_t* tflags = reinterpret_cast<int32_t*>(slab);
+      double* out = C + i0 * ldc + j0 + (wm * 64 + 4 * frag_row) * ldc + wn * 64 + 4 * frag_col;
+      if (sl > 0) {
+        if (threadIdx.x == 0) wait_flag(&tflags[t], sl, tflags + ntiles);
+        __syncthreads();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        if (active) {
+          double2 prev[4][4][2];
+#pragma unroll
+          for (int m = 0; m < 4; m++)
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+              const double* o = out + (16 * r + m) * ldc;
+              prev[m][r][0] = *reinterpret_cast<const double2*>(o);
+              prev[m][r][1] = *reinterpret_cast<const double2*>(o + 2);
+            }
+#pragma unroll
+          for (int m = 0; m < 4; m++)
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+              acc[m][0][r] = prev[m][r][0].x + acc[m][0][r];
+              acc[m][1][r] = prev[m][r][0].y + acc[m][1][r];
+              acc[m][2][r] = prev[m][r][1].x + acc[m][2][r];
+              acc[m][3][r] = prev[m][r][1].y + acc[m][3][r];
+            }
+        }
+      }
+      if (active) {
+#pragma unroll
+        for (int m = 0; m < 4; m++)
+#pragma unroll
+          for (int r = 0; r < 4; r++) {
+            double* o = out + (16 * r + m) * ldc;
+#pragma unroll
+            for (int q = 0; q < 4; q++) st_agent(o + q, acc[m][q][r]);
+          }
+      }
+      publish_flag(&tflags[t], sl + 1, threadIdx.x);
+    } else if (active) {
       // a single slice stores straight into G (no workspace, the reduce is a no-op)
       const int64_t ld = sb.n == 1 ? ldc : BT;
       double* out = (sb.n == 1 ? C + i0 * ldc + j0 : slab + ((int64_t)sl * ntiles + t) * (BT * BT)) +
@@ -690,7 +741,7 @@ static bool grm_wide() {
 }
 
 static double simulate_split(const std::vector<int64_t>& sizes, const std::vector<double>& cost, int64_t R,
-                             double tile_bytes, double stage_s) {
+                             double tile_bytes, double stage_s, bool carry) {
   std::vector<double> speed(R);
   uint64_t h = 0x9E3779B97F4A7C15ull;
   for (int64_t k = 0; k < R; k++) {  // deterministic jitter, sd ≈ 2 %
@@ -708,12 +759,22 @@ static double simulate_split(const std::vector<int64_t>& sizes, const std::vecto
       // overlap other K ranges instead of streaming the same strips as their XCD's neighbours,
       // so fewer of their operand rows hit L2); fitted on 11 measured splits at C2
       f += (double)sizes[s] * c * ((s == 0 && f > 0.0) ? 1.10 : 1.0) / speed[k];
+      if (carry && s > 0) f += 0.5;  // read-add-write of the running tile sum (~2 µs)
       if (f > makespan) makespan = f;
       slots.push({f, k});
     }
   // slab reduce: one tile partial read per (slice, tile) at ~4 TB/s, in stage-time units
-  const double reduce_stages = (double)sizes.size() * (double)cost.size() * tile_bytes / 4e12 / stage_s;
+  const double reduce_stages =
+      carry ? 0.0 : (double)sizes.size() * (double)cost.size() * tile_bytes / 4e12 / stage_s;
   return makespan + reduce_stages;
+}
+
+static int grm_carry_env() {  // GBM_GRM_CARRY=0/1 forces slabs / in-order carry; -1 = automatic
+  static const int v = [] {
+    const char* e = getenv("GBM_GRM_CARRY");
+    return e ? (atoi(e) != 0 ? 1 : 0) : -1;
+  }();
+  return v;
 }
 
 static bool grm_edge_enabled() {
@@ -754,7 +815,9 @@ static GrmPlan plan(int64_t n, int64_t p) {
   std::lock_guard<std::mutex> lock(mu);
   auto key = std::make_tuple(g.wide, nt, g.nst, R);
   auto finish = [&](GrmPlan& gp) {
-    gp.main_doubles = gp.sb.n == 1 ? 0 : (int64_t)gp.sb.n * gp.ntiles * gp.tile_elems;
+    gp.main_doubles = gp.sb.n == 1 ? 0
+                      : gp.sb.carry ? (gp.ntiles + 1 + 1) / 2 + 1  // int32 flags + error cell
+                                    : (int64_t)gp.sb.n * gp.ntiles * gp.tile_elems;
     gp.sb.er = 0;
     gp.sb.et = gp.sb.erb = gp.sb.es = gp.sb.ekper = 0;
     gp.sb.e0 = gp.sb.eslab_off = 0;
@@ -764,7 +827,9 @@ static GrmPlan plan(int64_t n, int64_t p) {
       gp.sb.er = (int32_t)r_last;
       gp.sb.et = (int32_t)((r_last + 15) / 16);
       gp.sb.erb = (int32_t)((n + 255) / 256);
-      gp.sb.ekper = 512;
+      // ~2048 edge workgroups in all (loci ranges of >= 256, multiples of 16): bounded partials
+      const int64_t es_want = std::max<int64_t>(1, std::min<int64_t>((2048 + gp.sb.erb - 1) / gp.sb.erb, (p + 255) / 256));
+      gp.sb.ekper = (int32_t)(((p + es_want - 1) / es_want + 15) / 16 * 16);
       gp.sb.es = (int32_t)((p + gp.sb.ekper - 1) / gp.sb.ekper);
       gp.sb.eslab_off = gp.main_doubles;
       gp.edge_doubles = (int64_t)gp.sb.es * gp.sb.erb * 256 * 16 * gp.sb.et;
@@ -777,68 +842,83 @@ static GrmPlan plan(int64_t n, int64_t p) {
     return g;
   }
   const int64_t minc = 16;  // stages per workgroup at least
-  std::vector<std::vector<int64_t>> cands;
   const bool big = g.ntiles > 2048;  // keep the one-off planning cost small for large n
-  for (int S = 1; S <= (big ? 3 : 8); S++) {
-    if (S > 1 && g.nst / S < minc) break;
-    std::vector<int64_t> v;
-    for (int i = 0; i < S; i++) v.push_back((g.nst * (i + 1)) / S - (g.nst * i) / S);
-    cands.push_back(v);
-  }
-  for (double f = big ? 0.60 : 0.40; f < 0.90; f += big ? 0.10 : 0.05)
-    for (double r : {0.3, 0.4, 0.5, 0.6, 0.7}) {
-      if (big && r != 0.5) continue;
-      std::vector<int64_t> v;
-      int64_t first = (int64_t)(f * (double)g.nst);
-      if (first < minc || g.nst - first < minc) continue;
-      v.push_back(first);
-      int64_t rem = g.nst - first;
-      while (rem > 0) {
-        int64_t c = (int64_t)std::ceil(r * (double)rem);
-        if (c < minc) c = minc;
-        if (rem - c < minc || (int)v.size() == kMaxSlices - 1) c = rem;
-        v.push_back(c);
-        rem -= c;
-      }
-      cands.push_back(v);
-    }
   // stage time: ~3.9 us per 16-locus stage of a 128x128 tile at 2 workgroups per CU (7.8 us per
   // 256x128 stage at one workgroup per CU)
   const double stage_s = g.wide ? 7.8e-6 : 3.9e-6;
   double best = 1e300;
-  std::vector<int64_t> bestv{g.nst};
-  if (const char* ov = getenv("GBM_GRM_SPLIT")) {  // tuning experiments: "w0,w1,..." relative sizes
-    std::vector<double> w;
-    for (const char* q = ov; *q;) {
-      char* end = nullptr;
-      const double x = strtod(q, &end);
-      if (end == q) break;
-      if (x > 0) w.push_back(x);
-      q = (*end == ',') ? end + 1 : end;
-    }
-    if (!w.empty() && (int)w.size() <= kMaxSlices) {
-      double tot = 0;
-      for (double x : w) tot += x;
-      cands.clear();
+  auto choose = [&](bool carry) {
+    std::vector<std::vector<int64_t>> cands;
+    const int max_uniform = big ? 3 : (carry ? kMaxSlices : 8);
+    for (int S = 1; S <= max_uniform; S++) {
+      if (S > 1 && g.nst / S < minc) break;
       std::vector<int64_t> v;
-      int64_t acc = 0;
-      double cum = 0;
-      for (size_t i = 0; i < w.size(); i++) {
-        cum += w[i];
-        const int64_t e = (i + 1 == w.size()) ? g.nst : (int64_t)std::llround(cum / tot * (double)g.nst);
-        if (e > acc) v.push_back(e - acc);
-        acc = e > acc ? e : acc;
-      }
+      for (int i = 0; i < S; i++) v.push_back((g.nst * (i + 1)) / S - (g.nst * i) / S);
       cands.push_back(v);
     }
-  }
-  for (const auto& v : cands) {
-    const double m = simulate_split(v, cost, R, (double)g.tile_elems * 8.0, stage_s);
-    if (m < best * 0.999) {
-      best = m;
-      bestv = v;
+    for (double f = big ? 0.60 : 0.40; f < 0.90; f += big ? 0.10 : 0.05)
+      for (double r : {0.3, 0.4, 0.5, 0.6, 0.7}) {
+        if (big && r != 0.5) continue;
+        std::vector<int64_t> v;
+        int64_t first = (int64_t)(f * (double)g.nst);
+        if (first < minc || g.nst - first < minc) continue;
+        v.push_back(first);
+        int64_t rem = g.nst - first;
+        while (rem > 0) {
+          int64_t c = (int64_t)std::ceil(r * (double)rem);
+          if (c < minc) c = minc;
+          if (rem - c < minc || (int)v.size() == (carry ? kMaxSlices : 12) - 1) c = rem;
+          v.push_back(c);
+          rem -= c;
+        }
+        cands.push_back(v);
+      }
+    if (const char* ov = getenv("GBM_GRM_SPLIT")) {  // tuning experiments: "w0,w1,..." relative sizes
+      std::vector<double> w;
+      for (const char* q = ov; *q;) {
+        char* end = nullptr;
+        const double x = strtod(q, &end);
+        if (end == q) break;
+        if (x > 0) w.push_back(x);
+        q = (*end == ',') ? end + 1 : end;
+      }
+      if (!w.empty() && (int)w.size() <= kMaxSlices) {
+        double tot = 0;
+        for (double x : w) tot += x;
+        cands.clear();
+        std::vector<int64_t> v;
+        int64_t acc = 0;
+        double cum = 0;
+        for (size_t i = 0; i < w.size(); i++) {
+          cum += w[i];
+          const int64_t e = (i + 1 == w.size()) ? g.nst : (int64_t)std::llround(cum / tot * (double)g.nst);
+          if (e > acc) v.push_back(e - acc);
+          acc = e > acc ? e : acc;
+        }
+        cands.push_back(v);
+      }
     }
+    std::vector<int64_t> bv{g.nst};
+    best = 1e300;
+    for (const auto& v : cands) {
+      const double m = simulate_split(v, cost, R, (double)g.tile_elems * 8.0, stage_s, carry);
+      if (m < best * 0.999) {
+        best = m;
+        bv = v;
+      }
+    }
+    return bv;
+  };
+  // slabs (+ reduce kernel) unless they would exceed 4 GiB (or GBM_GRM_CARRY forces a mode):
+  // the in-order carry needs no workspace but its write-through epilogue costs ~1 % at C2
+  int carry_mode = grm_carry_env();
+  std::vector<int64_t> bestv = choose(carry_mode == 1);
+  if (carry_mode < 0 && !g.wide && bestv.size() > 1 &&
+      (double)bestv.size() * (double)g.ntiles * (double)g.tile_elems * 8.0 > 4.0 * 1073741824.0) {
+    carry_mode = 1;
+    bestv = choose(true);
   }
+  g.sb.carry = (!g.wide && carry_mode == 1 && bestv.size() > 1) ? 1 : 0;
   g.sb.n = (int32_t)bestv.size();
   g.sb.b[0] = 0;
   for (int i = 0; i < g.sb.n; i++) g.sb.b[i + 1] = g.sb.b[i] + (int32_t)bestv[i];
@@ -860,8 +940,8 @@ static GrmPlan plan(int64_t n, int64_t p) {
 constexpr int P64 = 80;  // LDS pitch: the two 16-lane halves of a fragment read hit disjoint banks
 __global__ void __launch_bounds__(256, 2)
 syrk64_sub_kernel(const double* __restrict__ U, int64_t ldu, int64_t c0, int64_t lim, double* __restrict__ C,
-                  int64_t ldc, double* __restrict__ Ld, double* __restrict__ Dinv, int32_t* __restrict__ info,
-                  int64_t fk0, int rowonly, int kchunks) {
+                  int64_t ldc, double* Ld, double* Dinv, int32_t* __restrict__ info,
+                  int64_t fk0, int rowonly, int kchunks, int32_t* __restrict__ fflags) {
 #ifdef GBM_DEBUG_FACTIME
   const unsigned long long ft0 = wall_clock64();
 #endif
@@ -891,18 +971,25 @@ syrk64_sub_kernel(const double* __restrict__ U, int64_t ldu, int64_t c0, int64_t
   }
   // K = 64 kchunks: the chunks are staged one after the other (kchunks > 1 only for the row
   // updates that bring a later panel of a 4-panel group up to date)
-  const double* B = diag ? As : Bs;
+  const double* B = Bs;
   for (int c = 0; c < kchunks; c++) {
     if (c > 0) __syncthreads();  // every wave is done with the previous chunk
     {
+      // all 16 loads in flight before the LDS stores (interleaving them with the diag-conditional
+      // stores made the compiler wait for each load in turn)
       const int k = tid >> 2, quarter = tid & 3;
       const double* sa = U + (c * 64 + k) * ldu + i0 + quarter * 16;
       const double* sb = U + (c * 64 + k) * ldu + j0 + quarter * 16;
+      double2 va[8], vb[8];
 #pragma unroll
-      for (int e = 0; e < 16; e += 2) {
-        *reinterpret_cast<double2*>(&As[k * P64 + quarter * 16 + e]) = *reinterpret_cast<const double2*>(sa + e);
-        if (!diag)
-          *reinterpret_cast<double2*>(&Bs[k * P64 + quarter * 16 + e]) = *reinterpret_cast<const double2*>(sb + e);
+      for (int e = 0; e < 8; e++) {
+        va[e] = *reinterpret_cast<const double2*>(sa + 2 * e);
+        vb[e] = *reinterpret_cast<const double2*>(sb + 2 * e);
+      }
+#pragma unroll
+      for (int e = 0; e < 8; e++) {  // (on diagonal tiles vb == va: storing it anyway keeps this branch-free)
+        *reinterpret_cast<double2*>(&As[k * P64 + quarter * 16 + 2 * e]) = va[e];
+        *reinterpret_cast<double2*>(&Bs[k * P64 + quarter * 16 + 2 * e]) = vb[e];
       }
     }
     __syncthreads();
@@ -923,7 +1010,84 @@ syrk64_sub_kernel(const double* __restrict__ U, int64_t ldu, int64_t c0, int64_t
     }
   }
   const bool factor_next = fk0 >= 0 && blockIdx.x == 0;
-  if (!active && !factor_next) return;
+  // fused panel: the other tiles of the first tile row are the next panel's column chunks
+  // (rows fk0 .. fk0+64): once the first workgroup has published the factored diagonal block,
+  // each solves its chunk in place of a separate chol_panel_kernel launch
+  const bool panel_tile = fflags != nullptr && fk0 >= 0 && ti == 0 && tj > 0;
+  if (!active && !factor_next && !panel_tile) return;
+  if (panel_tile) {
+#ifdef GBM_DEBUG_FACTIME
+    const unsigned long long pt1 = wall_clock64();
+#endif
+    __syncthreads();  // every wave is done reading As/Bs
+    double* X = Bs;   // pitch P64 == PS
+    double* Us = As;
+#pragma unroll
+    for (int m = 0; m < 2; m++)
+#pragma unroll
+      for (int q = 0; q < 2; q++)
+#pragma unroll
+        for (int r = 0; r < 4; r++) X[(wm * 32 + m * 16 + fr + 4 * r) * PS + wn * 32 + q * 16 + fc] = acc[m][q][r];
+    if (tid == 0) wait_flag(&fflags[fk0 / 64], 1, info);
+    __syncthreads();
+#ifdef GBM_DEBUG_FACTIME
+    const unsigned long long pt2 = wall_clock64();
+#endif
+    // the block was written through (agent-scope stores) before the flag's release; after the
+    // acquire (every wave) plain loads — all of this lane's 32 in flight at once — read it
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    double di[4][4], us[16];
+    {
+      const double* Di = Dinv + (fk0 / 16) * 256 + (fr * 16 + fc);
+      const int row = tid >> 2, quarter = tid & 3;
+      const double* src = Ld + (fk0 + row) * CNB + quarter * 16;
+#pragma unroll
+      for (int e = 0; e < 16; e += 2) {
+        const double2 v = *reinterpret_cast<const double2*>(src + e);
+        us[e] = v.x;
+        us[e + 1] = v.y;
+      }
+#pragma unroll
+      for (int rb = 0; rb < 4; rb++)
+#pragma unroll
+        for (int ks = 0; ks < 4; ks++) di[rb][ks] = Di[rb * 256 + ks * 64];
+#pragma unroll
+      for (int e = 0; e < 16; e++) Us[row * PS + quarter * 16 + e] = us[e];
+    }
+    __syncthreads();
+    panel_chunk_solve(X, Us, [&](int rb, int ks) { return di[rb][ks]; }, lane, wave);
+    __syncthreads();
+    {
+      // solved chunk -> the U rows, and transposed into the lower triangle (L = Uᵀ, read by the
+      // back substitution)
+      const int row = tid >> 2, quarter = tid & 3;
+      double* dx = C + (i0 + row) * ldc + j0 + quarter * 16;
+#pragma unroll
+      for (int e = 0; e < 16; e += 2)
+        *reinterpret_cast<double2*>(dx + e) = *reinterpret_cast<const double2*>(&X[row * PS + quarter * 16 + e]);
+      double* dl = C + (j0 + row) * ldc + i0 + quarter * 16;
+#pragma unroll
+      for (int e = 0; e < 16; e += 2)
+        *reinterpret_cast<double2*>(dl + e) =
+            make_double2(X[(quarter * 16 + e) * PS + row], X[(quarter * 16 + e + 1) * PS + row]);
+    }
+#ifdef GBM_DEBUG_FACTIME
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
+    if (tid == 0) {
+      const unsigned long long k = atomicAdd(&g_paneltime_n, 1ull);
+      if (k < 16384) {
+        g_paneltime[6 * k] = (unsigned long long)fk0;
+        g_paneltime[6 * k + 1] = ft0;
+        g_paneltime[6 * k + 2] = pt1;
+        g_paneltime[6 * k + 3] = pt2;
+        g_paneltime[6 * k + 4] = wall_clock64();
+        g_paneltime[6 * k + 5] = (unsigned long long)tj;
+      }
+    }
+#endif
+    return;
+  }
 #pragma unroll
   for (int m = 0; m < 2; m++)
 #pragma unroll
@@ -954,7 +1118,12 @@ syrk64_sub_kernel(const double* __restrict__ U, int64_t ldu, int64_t c0, int64_t
     const unsigned long long ft2 = wall_clock64();
 #endif
     if (tid == 0 && bad >= 0) atomicCAS(info, 0, (int32_t)(fk0 + bad + 1));
-    store_factor(Us, rinv, Ld + fk0 * CNB, Dinv + (fk0 / 16) * 256, tid);
+    if (fflags) {
+      store_factor<true>(Us, rinv, Ld + fk0 * CNB, Dinv + (fk0 / 16) * 256, tid);
+      publish_flag(&fflags[fk0 / 64], 1, tid);
+    } else {
+      store_factor(Us, rinv, Ld + fk0 * CNB, Dinv + (fk0 / 16) * 256, tid);
+    }
 #ifdef GBM_DEBUG_FACTIME
     if (tid == 0) {
       const unsigned long long k = atomicAdd(&g_factime_n, 1ull);
@@ -982,21 +1151,24 @@ int64_t chol_small_lim() {
 // panels so that the whole group shares one K = 128 / 256 trailing update); the first workgroup
 // factors the diagonal block at k1 afterwards.
 int launch_chol_row_update(double* G, int64_t ldg, int64_t k0, int kch, int64_t gdim, double* Ld, double* Dinv,
-                           int32_t* info, hipStream_t s) {
+                           int32_t* info, int32_t* fflags, hipStream_t s) {
   const int64_t k1 = k0 + 64 * (int64_t)kch;
   const int64_t lim = gdim - k1;
   syrk64_sub_kernel<<<(unsigned)(lim / 64), 256, 0, s>>>(G + k0 * ldg, ldg, k1, lim, G, ldg, Ld, Dinv, info, k1, 1,
-                                                         kch);
+                                                         kch, fflags);
   GBM_LAUNCH_CHECK();
   return GBM_OK;
 }
 
 // Upper-Cholesky trailing update: C[k1:gdim, k1:gdim] (upper tiles) -= U[k0:k1, k1:]ᵀ U[k0:k1, k1:]
 // with k1 = k0 + nb (nb = 64, or 128 for two panels at once)
+// fflags != nullptr: fuse the next panel into the update where the kernel supports it; *fused
+// tells the caller whether the panel of next_k0 is done
 int launch_chol_update(double* G, int64_t ldg, int64_t k0, int64_t nb, int64_t gdim, double* Ld, double* Dinv,
-                       int32_t* info, int64_t next_k0, hipStream_t s) {
+                       int32_t* info, int64_t next_k0, int32_t* fflags, bool* fused, hipStream_t s) {
   const int64_t k1 = k0 + nb;
   const int64_t lim = gdim - k1;
+  *fused = false;
   if (lim <= 0) return GBM_OK;
   // 64x64 tiles below chol_small_lim() (K = 64), or below GBM_UPD64_LIM2 rows for a K = 128
   // pair update (more workgroups for trailing matrices that fill few 128-tile rounds)
@@ -1007,8 +1179,9 @@ int launch_chol_update(double* G, int64_t ldg, int64_t k0, int64_t nb, int64_t g
   if ((nb == 64 && lim <= chol_small_lim()) || (nb == 128 && lim <= lim2)) {
     const int64_t m = (lim + 63) / 64;
     syrk64_sub_kernel<<<(unsigned)(m * (m + 1) / 2), 256, 0, s>>>(G + k0 * ldg, ldg, k1, lim, G, ldg, Ld, Dinv, info,
-                                                                  next_k0, 0, (int)(nb / 64));
+                                                                  next_k0, 0, (int)(nb / 64), fflags);
     GBM_LAUNCH_CHECK();
+    *fused = fflags != nullptr && next_k0 >= 0;
     return GBM_OK;
   }
   const int64_t m = (lim + BT - 1) / BT;
@@ -1044,6 +1217,7 @@ int launch_grm_syrk(const double* Zt, int64_t ldz, int64_t p, int64_t n, double*
     return fail(GBM_E_ARG, "gbm_dev_grm: workspace too small (" + std::to_string(ws_bytes) + " < " +
                                std::to_string(need) + ")");
   const unsigned grid = (unsigned)(g.sb.n * ((g.ntiles + 7) & ~(int64_t)7));
+  if (g.sb.carry) GBM_HIP_TRY(hipMemsetAsync(ws, 0, (size_t)(g.ntiles + 1) * sizeof(int32_t), s));
   if (g.wide)
     grm_syrk8_kernel<<<grid, 512, 0, s>>>(Zt, ldz, p, n, G, ldg, (double*)ws, g.ntiles, g.sb);
   else  // with an edge, the tiles cover [0, e0)^2 exactly
@@ -1068,7 +1242,7 @@ int launch_grm_reduce(int64_t n, int64_t p, double* G, int64_t ldg, const void* 
                                                                                  g.sb, G, ldg);
     GBM_LAUNCH_CHECK();
   }
-  if (g.sb.n == 1) return GBM_OK;
+  if (g.sb.n == 1 || g.sb.carry) return GBM_OK;
   if (g.wide)
     grm_slab_reduce8_kernel<<<(unsigned)g.ntiles, 256, 0, s>>>((const double*)ws, g.ntiles, g.sb.n, G, ldg,
                                                                npad_of(n));
@@ -1151,6 +1325,12 @@ extern "C" int gbm_debug_factime(void* host, int64_t* count) {
   if (hipMemcpyFromSymbol(&n, HIP_SYMBOL(gbm::g_factime_n), 8) != hipSuccess) return -1;
   *count = (int64_t)n;
   return hipMemcpyFromSymbol(host, HIP_SYMBOL(gbm::g_factime), 4 * 1024 * 8) == hipSuccess ? 0 : -1;
+}
+extern "C" int gbm_debug_paneltime(void* host, int64_t* count) {
+  unsigned long long n = 0;
+  if (hipMemcpyFromSymbol(&n, HIP_SYMBOL(gbm::g_paneltime_n), 8) != hipSuccess) return -1;
+  *count = (int64_t)n;
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(gbm::g_paneltime), 6 * 16384 * 8) == hipSuccess ? 0 : -1;
 }
 #endif
 

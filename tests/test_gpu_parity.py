@@ -165,3 +165,22 @@ def test_gblup_with_grm_edge_matches_oracle():
     assert q == ref["q"]
     assert rel(y_pred, ref["y_pred"]) < TOL_TIGHT
     assert rel(b_hat, ref["b_hat"]) < TOL_CONTRACT
+
+
+def test_repeated_solves_are_bit_identical():
+    """The fused panels and the back substitution exchange data between workgroups of one
+    launch through flags; a visibility race would show up as run-to-run differences."""
+    n, p = 1000, 800
+    X = oracle.synth_genotypes(31, n, p)
+    Y = oracle.synth_phenotypes(X, 32, ntraits=2)
+    s = gbm.GenotypeSession(X)
+    idx = np.arange(n)
+    ref = oracle.gblup_fit(X, Y, 0.5)
+    first = None
+    for _ in range(25):
+        _, y_pred, _, _ = s.gblup(idx, Y, lambda_=0.5)
+        if first is None:
+            first = np.array(y_pred, copy=True)
+            assert rel(first, ref["y_pred"]) < TOL_TIGHT
+        else:
+            assert np.array_equal(y_pred, first)

@@ -31,3 +31,22 @@ t = buf[: 4 * k].reshape(k, 4).astype(np.int64)
 d = np.diff(t, axis=1) / 100.0
 print(f"{k} syrk64 factor launches; median µs: tile {np.median(d[:, 0]):.2f} factor {np.median(d[:, 1]):.2f} "
       f"store {np.median(d[:, 2]):.2f}; max factor {d[:, 1].max():.2f}")
+# fused panel tiles vs their launch's factor workgroup (times from that WG's entry, µs)
+if hasattr(st.lib, "gbm_debug_paneltime"):
+    pb = np.zeros(6 * 16384, dtype=np.uint64)
+    pc = np.zeros(1, dtype=np.int64)
+    st.lib.gbm_debug_paneltime.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+    assert st.lib.gbm_debug_paneltime(pb.ctypes.data, pc.ctypes.data) == 0
+    m = int(min(pc[0], 16384))
+    P = pb[: 6 * m].reshape(m, 6).astype(np.int64)
+    # factor records in launch order map to fk0 = 64, 128, ... for the syrk64 launches; match by order
+    rows = []
+    for fk in np.unique(P[:, 0]):
+        sel = P[P[:, 0] == fk]
+        e0 = sel[:, 1].min()
+        rows.append(((sel[:, 2] - e0).mean() / 100, (sel[:, 3] - e0).mean() / 100, (sel[:, 3] - e0).max() / 100,
+                     (sel[:, 4] - e0).max() / 100, len(sel)))
+    r = np.array(rows)
+    print(f"{len(r)} fused launches; mean over launches (µs from first panel-tile entry): tile done {r[:,0].mean():.2f} "
+          f"wait end {r[:,1].mean():.2f} (max {r[:,2].mean():.2f}) last panel end {r[:,3].mean():.2f}; tiles/launch {r[:,4].mean():.1f}")
+    print(f"factor WG (µs from its entry): tile {np.median(d[:, 0]):.2f} factor {np.median(d[:, 1]):.2f} store+publish {np.median(d[:, 2]):.2f}")
