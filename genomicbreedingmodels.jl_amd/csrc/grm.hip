@@ -47,7 +47,7 @@ __device__ __forceinline__ void tile_of(int64_t t, int64_t& ti, int64_t& tj) {
   ti = t - r * (r + 1) / 2;
 }
 
-enum SyrkMode { kSub = 0, kSplit = 1 };
+enum SyrkMode { kSub = 0, kSplit = 1, kPersist = 2 };
 
 #ifdef GBM_DEBUG_WGTIME  // timing experiment only: per-workgroup start/end clocks + hardware id
 __device__ unsigned long long g_wgtime[3 * 16384];
@@ -371,16 +371,10 @@ syrk_kernel(const double* __restrict__ U, int64_t ldu, int64_t K, int64_t c0, in
   const int64_t nst = (K + BK - 1) / BK;
   const int64_t rlim = c0 + lim;
 
-  if constexpr (MODE == kSplit) {
-    // XCD-aware order: workgroups are dispatched round-robin over the 8 XCDs (id mod 8), so each
-    // slice is launched as T8 = round_up(ntiles, 8) workgroups and XCD x takes the contiguous tile
-    // range [x T8/8, (x+1) T8/8) of every slice — neighbouring tiles share A/B strips in that
-    // XCD's L2, and later slices revisit the same range
-    const int64_t T8 = (ntiles + 7) & ~(int64_t)7;
-    const int sl = (int)(wg / T8);
-    const int64_t u = wg - (int64_t)sl * T8;
-    const int64_t t = (u & 7) * (T8 >> 3) + (u >> 3);
-    if (t >= ntiles) return;
+  if constexpr (MODE == kSplit || MODE == kPersist) {
+    // one (loci range sl, tile t) unit: the tile's partial sum over the range, then the slab /
+    // carry / direct epilogue
+    auto run_unit = [&](int sl, int64_t t) {
     int64_t ti, tj;
     tile_of(t, ti, tj);
     const bool diag = (ti == tj);
@@ -397,7 +391,7 @@ syrk_kernel(const double* __restrict__ U, int64_t ldu, int64_t K, int64_t c0, in
       tile_pass_deep(U, ldu, ks0 * BK, (ks1 * BK < K ? ks1 * BK : K), i0, j0, diag, active, lds, acc, wave, lane);
     else
       tile_pass<false>(U, ldu, K, i0, j0, diag, active, ks0, ks1 > ks0 ? ks1 - ks0 : 0, lds, acc, wave, lane);
-    if (sb.carry && sb.n > 1) {
+    if (MODE == kSplit && sb.carry && sb.n > 1) {  // (not compiled into the persistent kernel)
       // in-order carry: G tile = ((P_0 + P_1) + P_2) + ..., the same order (and rounding) as the
       // slab reduce. Range sl's predecessor was dispatched 1+ rounds earlier (lower workgroup
       // id), so the wait is normally already satisfied and can never deadlock. The tile goes
@@ -453,6 +447,62 @@ syrk_kernel(const double* __restrict__ U, int64_t ldu, int64_t K, int64_t c0, in
           *reinterpret_cast<double2*>(o) = make_double2(acc[m][0][r], acc[m][1][r]);
           *reinterpret_cast<double2*>(o + 2) = make_double2(acc[m][2][r], acc[m][3][r]);
         }
+    }
+    };
+    // XCD-aware order: XCD x owns the contiguous tile range [x T8/8, (x+1) T8/8) of every loci
+    // range (T8 = round_up(ntiles, 8)), so neighbouring tiles share A/B strips in that XCD's L2
+    // and later ranges revisit the same tiles
+    const int64_t T8 = (ntiles + 7) & ~(int64_t)7;
+    if constexpr (MODE == kPersist) {
+      // persistent workgroups (one per resident slot): each takes units from its own XCD's queue
+      // (XCC_ID hardware register; units in range-major order over the XCD's tiles) through an
+      // atomic counter, then steals from the other XCDs' queues once its own is empty. Dynamic
+      // to the last unit, so the XCDs finish together (with hardware dispatch every XCD ran a
+      // fixed 1/8 of the workgroups and they ended up to 1 ms apart).
+      __shared__ int64_t s_unit;
+      int32_t* ctr = info;  // 8 queue counters, zeroed before the launch
+      const int xcc = (int)(__builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (31 << 11)) & 7);
+      const int64_t per = T8 >> 3;
+      int q = xcc;
+      for (int tries = 0; tries < 8;) {
+        const int64_t qt0 = q * per;
+        const int64_t qt1 = qt0 + per < ntiles ? qt0 + per : ntiles;
+        const int64_t nq = qt1 > qt0 ? qt1 - qt0 : 0;
+        if (threadIdx.x == 0) s_unit = atomicAdd(&ctr[q], 1);
+        __syncthreads();
+        const int64_t u = s_unit;
+        __syncthreads();
+        if (u >= nq * sb.n) {
+          q = (q + 1) & 7;
+          tries++;
+          continue;
+        }
+        const int sl = (int)(u / nq);
+#ifdef GBM_DEBUG_WGTIME
+        const unsigned long long ut0 = wall_clock64();
+        const unsigned long long uc0 = __builtin_amdgcn_s_memtime();
+#endif
+        run_unit(sl, qt0 + (u - (int64_t)sl * nq));
+#ifdef GBM_DEBUG_WGTIME
+        const int64_t rec = (int64_t)sl * ntiles + qt0 + (u - (int64_t)sl * nq);
+        if (threadIdx.x == 0 && rec < 16384) {  // per unit: start, end, (wg << 8 | xcc), shader cycles
+          g_wgtime[3 * rec] = ut0;
+          g_wgtime[3 * rec + 1] = wall_clock64();
+          const unsigned hwid = __builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11));
+          g_wgtime[3 * rec + 2] = (unsigned long long)xcc | ((unsigned long long)((hwid >> 8) & 0xFF) << 8) |
+                                  ((unsigned long long)wg << 16) | ((__builtin_amdgcn_s_memtime() - uc0) << 28);
+        }
+#endif
+      }
+      return;
+    } else {
+      // hardware dispatch is round-robin over the 8 XCDs (workgroup id mod 8): each range is
+      // launched as T8 workgroups and id u of a range maps to tile (u & 7) T8/8 + (u >> 3)
+      const int sl = (int)(wg / T8);
+      const int64_t u = wg - (int64_t)sl * T8;
+      const int64_t t = (u & 7) * (T8 >> 3) + (u >> 3);
+      if (t >= ntiles) return;
+      run_unit(sl, t);
     }
 #ifdef GBM_DEBUG_WGTIME
     if (threadIdx.x == 0 && wg < 16384) {
@@ -1192,9 +1242,18 @@ int launch_chol_update(double* G, int64_t ldg, int64_t k0, int64_t nb, int64_t g
   return GBM_OK;
 }
 
+static bool grm_persist() {  // GBM_GRM_PERSIST=0: hardware-dispatched workgroups instead
+  static const bool v = [] {
+    const char* e = getenv("GBM_GRM_PERSIST");
+    return !e || atoi(e) != 0;
+  }();
+  return v;
+}
+
+// workspace: [slabs or carry flags][edge partials][8 queue counters of the persistent launch]
 int64_t grm_workspace_bytes(int64_t n, int64_t p) {
   const GrmPlan g = plan(n, p);
-  return (g.main_doubles + g.edge_doubles) * (int64_t)sizeof(double);
+  return (g.main_doubles + g.edge_doubles + 4) * (int64_t)sizeof(double);
 }
 
 static int check_grm_args(const double* Zt, int64_t ldz, int64_t p, int64_t n, double* G, int64_t ldg) {
@@ -1218,11 +1277,20 @@ int launch_grm_syrk(const double* Zt, int64_t ldz, int64_t p, int64_t n, double*
                                std::to_string(need) + ")");
   const unsigned grid = (unsigned)(g.sb.n * ((g.ntiles + 7) & ~(int64_t)7));
   if (g.sb.carry) GBM_HIP_TRY(hipMemsetAsync(ws, 0, (size_t)(g.ntiles + 1) * sizeof(int32_t), s));
-  if (g.wide)
+  int32_t* ctr = reinterpret_cast<int32_t*>((double*)ws + g.main_doubles + g.edge_doubles);
+  const int64_t lim = g.sb.er > 0 ? g.sb.e0 : n;  // with an edge, the tiles cover [0, e0)^2 exactly
+  if (g.wide) {
     grm_syrk8_kernel<<<grid, 512, 0, s>>>(Zt, ldz, p, n, G, ldg, (double*)ws, g.ntiles, g.sb);
-  else  // with an edge, the tiles cover [0, e0)^2 exactly
-    syrk_kernel<kSplit><<<grid, 256, 0, s>>>(Zt, ldz, p, 0, g.sb.er > 0 ? g.sb.e0 : n, G, ldg, (double*)ws, g.ntiles,
-                                             g.sb, nullptr, nullptr, nullptr, -1);
+  } else if (grm_persist() && !g.sb.carry) {
+    GBM_HIP_TRY(hipMemsetAsync(ctr, 0, 8 * sizeof(int32_t), s));
+    const int64_t units = (int64_t)g.sb.n * g.ntiles;
+    const unsigned pgrid = (unsigned)(units < resident_wgs() ? units : resident_wgs());
+    syrk_kernel<kPersist><<<pgrid, 256, 0, s>>>(Zt, ldz, p, 0, lim, G, ldg, (double*)ws, g.ntiles, g.sb, nullptr,
+                                                nullptr, ctr, -1);
+  } else {
+    syrk_kernel<kSplit><<<grid, 256, 0, s>>>(Zt, ldz, p, 0, lim, G, ldg, (double*)ws, g.ntiles, g.sb, nullptr, nullptr,
+                                             nullptr, -1);
+  }
   GBM_LAUNCH_CHECK();
   if (g.sb.er > 0) {
     grm_edge_kernel<<<(unsigned)((int64_t)g.sb.erb * g.sb.es), 256, 0, s>>>(Zt, ldz, p, g.sb,
