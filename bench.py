@@ -223,7 +223,8 @@ def main():
         },
         "roofline": {
             "bound": "mfma",
-            "kernel": "syrk_kernel<kSplit> (GRM, fp64 v_mfma_f64_16x16x4_f64)",
+            "kernel": "GRM stage: syrk_kernel<kPersist> (fp64 v_mfma_f64_16x16x4_f64 128x128 tiles) + "
+                      "grm_edge_kernel (ragged last column); achieved = all n(n+1)p flops / stage time",
             "achieved": achieved,
             "peak": PEAK_F64_TFLOPS,
             "unit": "TFLOP/s",

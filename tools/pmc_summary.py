@@ -34,10 +34,14 @@ def main(root):
             "fetch_kib_raw": fk, "write_kib": wk,
             "hbm_bytes_per_launch": ((2 * fk if fk else 0) + (wk or 0)) * 1024 if (fk or wk) else None,
         }
-    # the GRM SYRK is syrk_kernel<1> (kSplit); syrk_kernel<0> is the Cholesky trailing update
-    syrk = [v for k, v in out["kernels"].items() if "syrk_kernel<1>" in k]
+    # the GRM stage = syrk_kernel<2> (kPersist; <1> = kSplit when persistence is off) + the
+    # ragged-column grm_edge_kernel; syrk_kernel<0> is the Cholesky trailing update
+    syrk = [v for k, v in out["kernels"].items() if "syrk_kernel<2>" in k or "syrk_kernel<1>" in k]
+    edge = [v for k, v in out["kernels"].items() if "grm_edge_kernel" in k]
     if syrk:
-        out["hbm_bytes_per_launch"] = syrk[0]["hbm_bytes_per_launch"]
+        out["syrk_bytes_per_launch"] = syrk[0]["hbm_bytes_per_launch"]
+        out["edge_bytes_per_launch"] = edge[0]["hbm_bytes_per_launch"] if edge else 0
+        out["hbm_bytes_per_launch"] = (syrk[0]["hbm_bytes_per_launch"] or 0) + (out["edge_bytes_per_launch"] or 0)
         out["algorithmic_bytes_per_launch"] = 8.0 * out["n"] * out["p"]
     print(json.dumps(out, indent=1))
 
