@@ -47,21 +47,32 @@ def parse():
     return ap.parse_args()
 
 
-def phenotypes(seed: int, n: int, p_total: int, nrhs: int) -> np.ndarray:
-    """y = Xβ + e on 1 % QTL loci (h² = 0.5), X regenerated on the host for the QTL columns only
-    with the same counter hash (identical on every rank)."""
-    sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    import oracle as O  # host-side genotype hash (numpy), used here only to synthesise y
+def phenotypes(lib, device, seed: int, n: int, p_total: int, nrhs: int) -> np.ndarray:
+    """y = Xβ + e on 1 % QTL loci (h² = 0.5). The QTL genotype columns come from libgbm's device
+    generator (the same counter hash as the rank's resident shard), identical on every rank."""
+    import ctypes
+
+    import torch
+
+    from gbm import _lib
 
     rng = np.random.default_rng(seed + 1)
+    npad = lib.gbm_dev_npad(n)
+    col = torch.empty(npad, dtype=torch.float64, device=device)
+    stream = ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
     Y = np.empty((n, nrhs))
     for t in range(nrhs):
         nq = max(1, p_total // 100)
         idx = np.sort(rng.choice(p_total, size=nq, replace=False))
         beta = rng.standard_normal(nq)
+        Xq = torch.empty((nq, npad), dtype=torch.float64, device=device)
+        for k, j in enumerate(idx):
+            _lib.check(lib.gbm_dev_synth_genotypes(ctypes.c_void_p(Xq[k].data_ptr()), npad, 1, n, seed, int(j),
+                                                   stream), "synth")
+        Xq = Xq[:, :n].cpu().numpy()
         g = np.zeros(n)
-        for j, b in zip(idx, beta):
-            g += O.synth_genotypes(seed, n, 1, j0=int(j))[:, 0] * b
+        for k in range(nq):
+            g += Xq[k] * beta[k]
         e = rng.standard_normal(n) * np.sqrt(g.var(ddof=1))
         Y[:, t] = g + e
     return Y
@@ -91,7 +102,7 @@ def cpu_baseline(args):
         lib.gbm_ref_synth_matrix(args.seed, n, p, 0, X.ctypes.data, n)
     else:
         X = O.synth_genotypes(args.seed, n, p)
-    Y = phenotypes(args.seed, n, p, args.nrhs)
+    Y = O.synth_phenotypes(X, args.seed + 1, args.nrhs)
     t0 = time.perf_counter()
     O.gblup_fit(X, Y, args.lam)
     dt = time.perf_counter() - t0
@@ -141,7 +152,7 @@ def main():
     j0 = rank * p_local
     st = HipShardStages(n, p_local, nrhs=args.nrhs, lambda_=args.lam, device=dev)
     st.generate(args.seed, j0)
-    st.load_phenotypes(phenotypes(args.seed, n, p_total, args.nrhs))
+    st.load_phenotypes(phenotypes(st.lib, st.dev, args.seed, n, p_total, args.nrhs))
     torch.cuda.synchronize()
 
     labels = ["begin", "standardize", "grm_syrk", "grm_reduce", "allreduce", "solve", "effects", "download"]
