@@ -33,6 +33,13 @@ constexpr int BT = 128;            // tile edge
 #ifndef GBM_WPS
 #define GBM_WPS 2
 #endif
+#ifndef GBM_PRIO
+// s_setprio(1) around each k-step's MFMA group (2, the default): the wave in its MFMA group wins
+// issue arbitration over its SIMD partner's staging and LDS instructions. GRM at C2 on one box:
+// 18.87 ms (0) -> 18.68 ms (2); 1 (higher static priority for the second-dispatched workgroup
+// of each CU) 18.84 ms; 3 (priority around the staging instead) 18.73 ms
+#define GBM_PRIO 2
+#endif
 constexpr int BK = GBM_BK;         // loci per stage
 constexpr int WPS = GBM_WPS;       // target waves per SIMD (= resident 256-thread workgroups per CU)
 constexpr int LROW = BT + 2;       // LDS row pitch in doubles (1040 B ≡ 4 dwords mod 64 banks)
@@ -109,8 +116,14 @@ __device__ __forceinline__ void tile_pass(const double* __restrict__ U, int64_t 
     // the MFMA groups measured 3 % slower)
 #ifndef GBM_DEBUG_NOSTAGE  // timing experiment only: operands never refreshed (wrong results)
     if (st + 1 < nsteps) {
+#if GBM_PRIO == 3
+      __builtin_amdgcn_s_setprio(1);
+#endif
 #pragma unroll
       for (int rr = 0; rr < BK / 4; rr++) stage_row(kstep0 + st + 1, buf ^ 1, rr);
+#if GBM_PRIO == 3
+      __builtin_amdgcn_s_setprio(0);
+#endif
     }
 #endif
     const double* A = lds + buf * STAGE;
@@ -132,11 +145,17 @@ __device__ __forceinline__ void tile_pass(const double* __restrict__ U, int64_t 
 #pragma unroll
           for (int m = 0; m < 4; m++) af[m] = -af[m];
         }
+#if GBM_PRIO == 2
+        __builtin_amdgcn_s_setprio(1);
+#endif
 #pragma unroll
         for (int m = 0; m < 4; m++)
 #pragma unroll
           for (int q = 0; q < 4; q++)
             acc[m][q] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[m], bf[q], acc[m][q], 0, 0, 0);
+#if GBM_PRIO == 2
+        __builtin_amdgcn_s_setprio(0);
+#endif
       }
     }
 #ifdef GBM_DEBUG_NOBARRIER  // timing experiment only: racy (wrong results)
@@ -231,11 +250,17 @@ __device__ __forceinline__ void tile_pass_deep(const double* __restrict__ U, int
         const double2 b23 = *reinterpret_cast<const double2*>(&B[kr * LROW + wn * 64 + 4 * frag_col + 2]);
         const double af[4] = {a01.x, a01.y, a23.x, a23.y};
         const double bf[4] = {b01.x, b01.y, b23.x, b23.y};
+#if GBM_PRIO == 2
+        __builtin_amdgcn_s_setprio(1);
+#endif
 #pragma unroll
         for (int m = 0; m < 4; m++)
 #pragma unroll
           for (int q = 0; q < 4; q++)
             acc[m][q] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[m], bf[q], acc[m][q], 0, 0, 0);
+#if GBM_PRIO == 2
+        __builtin_amdgcn_s_setprio(0);
+#endif
       }
     }
   }
@@ -269,7 +294,9 @@ struct SliceBounds {
 // 256-row block over a loci range per workgroup, operands straight from global memory into
 // MFMA registers (A: 4 row tiles of 16 per wave, B: et column tiles), HBM-bound (one extra
 // read of U). A separate launch after the tiles: as extra workgroups of the tile kernel it
-// raised that kernel's VGPR allocation and slowed its tiles by ~2 %.
+// raised that kernel's VGPR allocation and slowed its tiles by ~2 %. Behind the persistent tile
+// kernel it runs concurrently, on a helper stream (launch_grm_syrk).
+template <int ET>
 __device__ __forceinline__ void grm_edge_pass(const double* __restrict__ U, int64_t ldu, int64_t K,
                                               const SliceBounds& sb, int64_t e, double* __restrict__ part,
                                               int lane, int wave) {
@@ -278,14 +305,13 @@ __device__ __forceinline__ void grm_edge_pass(const double* __restrict__ U, int6
   const int64_t k1 = (k0 + sb.ekper < K) ? k0 + sb.ekper : K;
   const int64_t i0 = (int64_t)rb * 256 + wave * 64;
   const int fr = lane >> 4, fc = lane & 15;
-  const int et = sb.et;
-  d4 acc[4][4];
+  d4 acc[4][ET];
 #pragma unroll
   for (int m = 0; m < 4; m++)
 #pragma unroll
-    for (int q = 0; q < 4; q++) acc[m][q] = (d4){0.0, 0.0, 0.0, 0.0};
+    for (int q = 0; q < ET; q++) acc[m][q] = (d4){0.0, 0.0, 0.0, 0.0};
   for (int64_t k = k0; k < k1; k += 16) {  // 4 MFMA k-steps per iteration, all loads first
-    double a[4][4], b[4][4];
+    double a[4][4], b[4][ET];
 #pragma unroll
     for (int st = 0; st < 4; st++) {
       const int64_t kk = k + st * 4 + fr;
@@ -297,31 +323,32 @@ __device__ __forceinline__ void grm_edge_pass(const double* __restrict__ U, int6
         a[st][m] = (kv && i < ldu) ? row[i] : 0.0;
       }
 #pragma unroll
-      for (int q = 0; q < 4; q++) b[st][q] = (kv && q < et) ? row[sb.e0 + q * 16 + fc] : 0.0;
+      for (int q = 0; q < ET; q++) b[st][q] = kv ? row[sb.e0 + q * 16 + fc] : 0.0;
     }
 #pragma unroll
     for (int st = 0; st < 4; st++)
 #pragma unroll
-      for (int q = 0; q < 4; q++)
-        if (q < et)
+      for (int q = 0; q < ET; q++)
 #pragma unroll
-          for (int m = 0; m < 4; m++) acc[m][q] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[st][m], b[st][q], acc[m][q], 0, 0, 0);
+        for (int m = 0; m < 4; m++) acc[m][q] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[st][m], b[st][q], acc[m][q], 0, 0, 0);
   }
   const int64_t rows = (int64_t)sb.erb * 256;
-  const int w = 16 * et;
+  constexpr int w = 16 * ET;
 #pragma unroll
   for (int m = 0; m < 4; m++)
 #pragma unroll
-    for (int q = 0; q < 4; q++)
-      if (q < et)
+    for (int q = 0; q < ET; q++)
 #pragma unroll
-        for (int r = 0; r < 4; r++)
-          part[((int64_t)ks * rows + i0 + m * 16 + fr + 4 * r) * w + q * 16 + fc] = acc[m][q][r];
+      for (int r = 0; r < 4; r++)
+        part[((int64_t)ks * rows + i0 + m * 16 + fr + 4 * r) * w + q * 16 + fc] = acc[m][q][r];
 }
 
-__global__ void __launch_bounds__(256) grm_edge_kernel(const double* __restrict__ U, int64_t ldu, int64_t K,
+// ET = ⌈r/16⌉ column tiles: few enough registers (ET = 1: ≤ 128) that the edge workgroups fit
+// beside the persistent tile kernel's two workgroups per CU and run concurrently with it
+template <int ET>
+__global__ void __launch_bounds__(256, ET == 1 ? 4 : 1) grm_edge_kernel(const double* __restrict__ U, int64_t ldu, int64_t K,
                                                        SliceBounds sb, double* __restrict__ part) {
-  grm_edge_pass(U, ldu, K, sb, blockIdx.x, part, threadIdx.x & 63, threadIdx.x >> 6);
+  grm_edge_pass<ET>(U, ldu, K, sb, blockIdx.x, part, threadIdx.x & 63, threadIdx.x >> 6);
 }
 
 // G[i][e0 + c] = Σ_s part[s][i][c] in range order (deterministic), i < n, c < er
@@ -460,6 +487,11 @@ syrk_kernel(const double* __restrict__ U, int64_t ldu, int64_t K, int64_t c0, in
       // to the last unit, so the XCDs finish together (with hardware dispatch every XCD ran a
       // fixed 1/8 of the workgroups and they ended up to 1 ms apart).
       __shared__ int64_t s_unit;
+#if GBM_PRIO == 1
+      // the second-dispatched workgroup of each CU gets the higher wave priority (arbitration
+      // otherwise favours the older wave of each SIMD pair)
+      if (wg >= (int64_t)gridDim.x / 2) __builtin_amdgcn_s_setprio(1);
+#endif
       int32_t* ctr = info;  // 8 queue counters, zeroed before the launch
       const int xcc = (int)(__builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (31 << 11)) & 7);
       const int64_t per = T8 >> 3;
@@ -715,11 +747,17 @@ grm_syrk8_kernel(const double* __restrict__ U, int64_t ldu, int64_t K, int64_t l
         const double2 b23 = *reinterpret_cast<const double2*>(&B[kr * ldb + wn * 64 + 4 * frag_col + 2]);
         const double af[4] = {a01.x, a01.y, a23.x, a23.y};
         const double bf[4] = {b01.x, b01.y, b23.x, b23.y};
+#if GBM_PRIO == 2
+        __builtin_amdgcn_s_setprio(1);
+#endif
 #pragma unroll
         for (int m = 0; m < 4; m++)
 #pragma unroll
           for (int q = 0; q < 4; q++)
             acc[m][q] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[m], bf[q], acc[m][q], 0, 0, 0);
+#if GBM_PRIO == 2
+        __builtin_amdgcn_s_setprio(0);
+#endif
       }
     }
   }
@@ -1250,6 +1288,38 @@ static bool grm_persist() {  // GBM_GRM_PERSIST=0: hardware-dispatched workgroup
   return v;
 }
 
+static bool grm_edge_concurrent() {  // GBM_GRM_EDGE_CONCURRENT=0: edge kernel after the tiles
+  static const bool v = [] {
+    const char* e = getenv("GBM_GRM_EDGE_CONCURRENT");
+    return !e || atoi(e) != 0;
+  }();
+  return v;
+}
+
+// one helper stream + fork/join events per (host thread, device): calls from different threads
+// never share events, and calls from one thread are ordered by the caller's stream anyway
+struct AuxStream {
+  hipStream_t s = nullptr;
+  hipEvent_t fork = nullptr, join = nullptr;
+};
+static int aux_stream(AuxStream** out) {
+  thread_local std::map<int, AuxStream> per_dev;
+  int dev = 0;
+  GBM_HIP_TRY(hipGetDevice(&dev));
+  AuxStream& a = per_dev[dev];
+  if (!a.s) {
+    GBM_HIP_TRY(hipStreamCreateWithFlags(&a.s, hipStreamNonBlocking));
+    GBM_HIP_TRY(hipEventCreateWithFlags(&a.fork, hipEventDisableTiming));
+    GBM_HIP_TRY(hipEventCreateWithFlags(&a.join, hipEventDisableTiming));
+  }
+  *out = &a;
+  return GBM_OK;
+}
+
+static bool persistent_launch(const GrmPlan& g) { return !g.wide && grm_persist() && !g.sb.carry; }
+// the ragged-column kernel and its reduce run on the helper stream, beside the persistent tiles
+static bool edge_on_aux(const GrmPlan& g) { return g.sb.er > 0 && persistent_launch(g) && grm_edge_concurrent(); }
+
 // workspace: [slabs or carry flags][edge partials][8 queue counters of the persistent launch]
 int64_t grm_workspace_bytes(int64_t n, int64_t p) {
   const GrmPlan g = plan(n, p);
@@ -1279,9 +1349,20 @@ int launch_grm_syrk(const double* Zt, int64_t ldz, int64_t p, int64_t n, double*
   if (g.sb.carry) GBM_HIP_TRY(hipMemsetAsync(ws, 0, (size_t)(g.ntiles + 1) * sizeof(int32_t), s));
   int32_t* ctr = reinterpret_cast<int32_t*>((double*)ws + g.main_doubles + g.edge_doubles);
   const int64_t lim = g.sb.er > 0 ? g.sb.e0 : n;  // with an edge, the tiles cover [0, e0)^2 exactly
+  const bool persist = persistent_launch(g);
+  // the ragged-column kernel beside the persistent tiles: forked (before the tile launch) onto
+  // this thread's helper stream for the device; its workgroups fit in the registers the two tile
+  // workgroups of a CU leave free. Joined back before the reduce.
+  AuxStream* ax = nullptr;
+  if (edge_on_aux(g)) {
+    rc = aux_stream(&ax);
+    if (rc != GBM_OK) return rc;
+    GBM_HIP_TRY(hipEventRecord(ax->fork, s));
+    GBM_HIP_TRY(hipStreamWaitEvent(ax->s, ax->fork, 0));
+  }
   if (g.wide) {
     grm_syrk8_kernel<<<grid, 512, 0, s>>>(Zt, ldz, p, n, G, ldg, (double*)ws, g.ntiles, g.sb);
-  } else if (grm_persist() && !g.sb.carry) {
+  } else if (persist) {
     GBM_HIP_TRY(hipMemsetAsync(ctr, 0, 8 * sizeof(int32_t), s));
     const int64_t units = (int64_t)g.sb.n * g.ntiles;
     const unsigned pgrid = (unsigned)(units < resident_wgs() ? units : resident_wgs());
@@ -1293,9 +1374,24 @@ int launch_grm_syrk(const double* Zt, int64_t ldz, int64_t p, int64_t n, double*
   }
   GBM_LAUNCH_CHECK();
   if (g.sb.er > 0) {
-    grm_edge_kernel<<<(unsigned)((int64_t)g.sb.erb * g.sb.es), 256, 0, s>>>(Zt, ldz, p, g.sb,
-                                                                           (double*)ws + g.sb.eslab_off);
+    const hipStream_t es = ax ? ax->s : s;
+    const unsigned eg = (unsigned)((int64_t)g.sb.erb * g.sb.es);
+    double* part = (double*)ws + g.sb.eslab_off;
+    switch (g.sb.et) {
+      case 1: grm_edge_kernel<1><<<eg, 256, 0, es>>>(Zt, ldz, p, g.sb, part); break;
+      case 2: grm_edge_kernel<2><<<eg, 256, 0, es>>>(Zt, ldz, p, g.sb, part); break;
+      case 3: grm_edge_kernel<3><<<eg, 256, 0, es>>>(Zt, ldz, p, g.sb, part); break;
+      default: grm_edge_kernel<4><<<eg, 256, 0, es>>>(Zt, ldz, p, g.sb, part); break;
+    }
     GBM_LAUNCH_CHECK();
+    if (ax) {
+      // the edge columns of G are disjoint from the tiles: sum their partials on the helper
+      // stream too (launch_grm_reduce then skips them)
+      grm_edge_reduce_kernel<<<(unsigned)((n * g.sb.er + 255) / 256), 256, 0, ax->s>>>(part, n, g.sb, G, ldg);
+      GBM_LAUNCH_CHECK();
+      GBM_HIP_TRY(hipEventRecord(ax->join, ax->s));
+      GBM_HIP_TRY(hipStreamWaitEvent(s, ax->join, 0));
+    }
   }
   return GBM_OK;
 }
@@ -1305,7 +1401,7 @@ int launch_grm_reduce(int64_t n, int64_t p, double* G, int64_t ldg, const void* 
   const GrmPlan g = plan(n, p);
   if (g.sb.n == 1 && g.sb.er == 0) return GBM_OK;
   if (!ws) return fail(GBM_E_ARG, "gbm_dev_grm_reduce: workspace required");
-  if (g.sb.er > 0) {
+  if (g.sb.er > 0 && !edge_on_aux(g)) {
     grm_edge_reduce_kernel<<<(unsigned)((n * g.sb.er + 255) / 256), 256, 0, s>>>((const double*)ws + g.sb.eslab_off, n,
                                                                                  g.sb, G, ldg);
     GBM_LAUNCH_CHECK();
