@@ -452,6 +452,16 @@ extern "C" int gbm_dev_gblup_solve(double* G, int64_t ldg, int64_t n, double inv
     const char* e = getenv("GBM_CHOL_G4_LIM");
     return e ? (int64_t)atoll(e) : (int64_t)8192;
   }();
+  // 8-panel groups (K = 512) while the trailing matrix exceeds this many rows. Solve at
+  // n = 50 000: 798 ms (4-panel groups only) -> 746 ms; n = 20 000: 67.1 -> 64.0 ms
+  static const int64_t group8_lim = [] {
+    const char* e = getenv("GBM_CHOL_G8_LIM");
+    return e ? (int64_t)atoll(e) : (int64_t)8192;
+  }();
+  static const int64_t group16_lim = [] {  // 16-panel groups (K = 1024): n = 50 000 746 -> 735 ms
+    const char* e = getenv("GBM_CHOL_G16_LIM");
+    return e ? (int64_t)atoll(e) : (int64_t)16384;
+  }();
   // GBM_CHOL_FUSE=1: the small updates also solve the next panel (first tile row, after the
   // first workgroup publishes the factored block). Correct, but measured slower than separate
   // panel launches (33.5 vs 20.3 + 8.9 µs per step at C2: the publish + wait + reload costs more
@@ -471,7 +481,11 @@ extern "C" int gbm_dev_gblup_solve(double* G, int64_t ldg, int64_t n, double inv
     // brought up to date with the group's earlier panels (row update with K = 64 j), factored and
     // solved one after the other, then one K = 64 g trailing update
     int g = 1;
-    if (pair_panels && group4_lim >= 0 && kb + 4 < nb && gdim - (k0 + 4 * NB) > group4_lim)
+    if (pair_panels && group16_lim >= 0 && kb + 16 < nb && gdim - (k0 + 16 * NB) > group16_lim)
+      g = 16;
+    else if (pair_panels && group8_lim >= 0 && kb + 8 < nb && gdim - (k0 + 8 * NB) > group8_lim)
+      g = 8;
+    else if (pair_panels && group4_lim >= 0 && kb + 4 < nb && gdim - (k0 + 4 * NB) > group4_lim)
       g = 4;
     else if (pair_panels && kb + 2 < nb && gdim - (k0 + 2 * NB) > chol_small_lim())
       g = 2;
