@@ -47,37 +47,6 @@ def parse():
     return ap.parse_args()
 
 
-def phenotypes(lib, device, seed: int, n: int, p_total: int, nrhs: int) -> np.ndarray:
-    """y = Xβ + e on 1 % QTL loci (h² = 0.5). The QTL genotype columns come from libgbm's device
-    generator (the same counter hash as the rank's resident shard), identical on every rank."""
-    import ctypes
-
-    import torch
-
-    from gbm import _lib
-
-    rng = np.random.default_rng(seed + 1)
-    npad = lib.gbm_dev_npad(n)
-    col = torch.empty(npad, dtype=torch.float64, device=device)
-    stream = ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
-    Y = np.empty((n, nrhs))
-    for t in range(nrhs):
-        nq = max(1, p_total // 100)
-        idx = np.sort(rng.choice(p_total, size=nq, replace=False))
-        beta = rng.standard_normal(nq)
-        Xq = torch.empty((nq, npad), dtype=torch.float64, device=device)
-        for k, j in enumerate(idx):
-            _lib.check(lib.gbm_dev_synth_genotypes(ctypes.c_void_p(Xq[k].data_ptr()), npad, 1, n, seed, int(j),
-                                                   stream), "synth")
-        Xq = Xq[:, :n].cpu().numpy()
-        g = np.zeros(n)
-        for k in range(nq):
-            g += Xq[k] * beta[k]
-        e = rng.standard_normal(n) * np.sqrt(g.var(ddof=1))
-        Y[:, t] = g + e
-    return Y
-
-
 def cpu_baseline(args):
     """The CPU oracle (numpy/OpenBLAS restatement, oracle/oracle.py) on the same workload
     (rank 0, N = 1): GRM + GBLUP on n x p_sample, timed without data generation."""
@@ -144,6 +113,7 @@ def main():
     dev = torch.cuda.current_device()
 
     import gbm
+    from gbm import synth
     from gbm.sharded import HipShardStages, LocalComm, TorchComm, sharded_gblup_step
 
     comm = TorchComm() if world > 1 else LocalComm()
@@ -152,7 +122,7 @@ def main():
     j0 = rank * p_local
     st = HipShardStages(n, p_local, nrhs=args.nrhs, lambda_=args.lam, device=dev)
     st.generate(args.seed, j0)
-    st.load_phenotypes(phenotypes(st.lib, st.dev, args.seed, n, p_total, args.nrhs))
+    st.load_phenotypes(synth.qtl_phenotypes(args.seed, n, p_total, args.nrhs, device=dev))
     torch.cuda.synchronize()
 
     labels = ["begin", "standardize", "grm_syrk", "grm_reduce", "allreduce", "solve", "effects", "download"]

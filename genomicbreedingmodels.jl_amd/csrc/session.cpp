@@ -213,6 +213,28 @@ extern "C" int gbm_session_create(const double* X, int64_t n, int64_t p, int64_t
   return GBM_OK;
 }
 
+extern "C" int gbm_session_create_synthetic(uint64_t seed, int64_t n, int64_t p, int device, gbm_session** out) {
+  if (!out) return fail(GBM_E_ARG, "gbm_session_create_synthetic: out is NULL");
+  *out = nullptr;
+  if (n < 1 || p < 1) return fail(GBM_E_ARG, "gbm_session_create_synthetic: bad arguments");
+  std::vector<int> devs;
+  GBM_TRY(check_devices(&device, 1, devs));
+  auto s = new gbm_session();
+  s->dev = devs[0];
+  s->n = n;
+  s->p = p;
+  int rc = session_alloc_x(s);
+  if (rc == GBM_OK) rc = gbm_dev_synth_genotypes((double*)s->Xt.p, s->npad, p, n, seed, 0, s->stream.s);
+  if (rc == GBM_OK && hipStreamSynchronize(s->stream.s) != hipSuccess)
+    rc = fail(GBM_E_HIP, "gbm_session_create_synthetic: generation failed");
+  if (rc != GBM_OK) {
+    delete s;
+    return rc;
+  }
+  *out = s;
+  return GBM_OK;
+}
+
 extern "C" int gbm_session_create_dosage_i8(const int8_t* D, int64_t n, int64_t p, int64_t ldd, int ploidy,
                                             int device, gbm_session** out) {
   if (!out) return fail(GBM_E_ARG, "gbm_session_create_dosage_i8: out is NULL");

@@ -31,7 +31,7 @@ EXPORTS = (
     "gbm_dev_grm_syrk", "gbm_dev_grm_reduce", "gbm_dev_grm_slices",
     "gbm_dev_gblup_solve", "gbm_dev_marker_effects",
     "gbm_dev_standardize_gather", "gbm_dev_gblup_terms",
-    "gbm_session_create", "gbm_session_create_dosage_i8", "gbm_session_destroy", "gbm_session_gblup_fit",
+    "gbm_session_create", "gbm_session_create_dosage_i8", "gbm_session_create_synthetic", "gbm_session_destroy", "gbm_session_gblup_fit",
     "gbm_session_predict", "gbm_session_reml_objective", "gbm_session_reml", "gbm_session_stats",
     "gbm_session_ridge_path", "gbm_session_ridge_lambda_max", "gbm_brr_fit",
     "gbm_dev_grm_packed_size", "gbm_dev_grm_pack", "gbm_dev_grm_unpack",
@@ -102,6 +102,8 @@ def _declare(lib):
     lib.gbm_dev_gblup_terms.argtypes = [P, I64, I64, I64, P, P, P]
     lib.gbm_session_create.restype = I32
     lib.gbm_session_create.argtypes = [P, I64, I64, I64, I32, ctypes.POINTER(P)]
+    lib.gbm_session_create_synthetic.restype = I32
+    lib.gbm_session_create_synthetic.argtypes = [U64, I64, I64, I32, ctypes.POINTER(P)]
     lib.gbm_session_create_dosage_i8.restype = I32
     lib.gbm_session_create_dosage_i8.argtypes = [P, I64, I64, I64, I32, I32, ctypes.POINTER(P)]
     lib.gbm_session_destroy.restype = None

@@ -47,6 +47,19 @@ class GenotypeSession:
             rc = self.lib.gbm_session_create(_lib.ptr(X), self.n, self.p, self.n, self.device, ctypes.byref(self._h))
             _lib.check(rc, "gbm_session_create")
 
+    @classmethod
+    def synthetic(cls, seed: int, n: int, p: int, *, device: int = 0) -> "GenotypeSession":
+        """Session over the counter-hash synthetic genotypes of loci 0..p-1, generated
+        on the device (benchmark-scale configs without a host copy of X)."""
+        self = cls.__new__(cls)
+        self.lib = _lib.load()
+        self._h = ctypes.c_void_p()
+        self.device = int(device)
+        self.n, self.p = int(n), int(p)
+        _lib.check(self.lib.gbm_session_create_synthetic(int(seed), self.n, self.p, self.device, ctypes.byref(self._h)),
+                   "gbm_session_create_synthetic")
+        return self
+
     # ---- lifetime -------------------------------------------------------------------------
     def close(self):
         if self._h:

@@ -225,6 +225,9 @@ typedef struct gbm_session gbm_session;
 int gbm_session_create(const double* X, int64_t n, int64_t p, int64_t ldx, int device, gbm_session** out);
 int gbm_session_create_dosage_i8(const int8_t* D, int64_t n, int64_t p, int64_t ldd, int ploidy, int device,
                                  gbm_session** out);
+/* A session over the synthetic genotypes of gbm_dev_synth_genotypes (seed, loci 0..p-1), generated
+ * on the device: benchmark-scale sessions (configs C4/C5) without a host copy of X. */
+int gbm_session_create_synthetic(uint64_t seed, int64_t n, int64_t p, int device, gbm_session** out);
 void gbm_session_destroy(gbm_session* s);
 /* gbm_gblup_fit on the rows idx[0..n_train) of the session's X; Y holds the training phenotypes
  * (n_train x nrhs, column-major). */

@@ -144,3 +144,19 @@ def test_validate_mirrors_reference():
     assert cv.checkdims() and cv.fold == "f"
     with pytest.raises(gbm.ArgumentError, match="leakage"):
         gbm.validate(fit, g, ph, idx_validation=[5, 120])
+
+
+def test_synthetic_session_matches_host_session(data):
+    """gbm_session_create_synthetic: X generated on the device is the oracle's synthetic X, so the
+    session fits equal the oracle's on the same rows; gbm.synth's host copy is bit-exact."""
+    from gbm import synth
+    X = oracle.synth_genotypes(4242, 257, 700)
+    assert np.array_equal(synth.genotypes(4242, 257, 700), X)
+    assert np.array_equal(synth.genotypes(4242, 257, 300, j0=400), X[:, 400:])
+    Y = oracle.synth_phenotypes(X, 5, ntraits=2)
+    idx = np.arange(0, 257, 2)
+    with gbm.GenotypeSession.synthetic(4242, 257, 700) as s:
+        b, yp, mu, q = s.gblup(idx, Y[idx], 1.0)
+    ref = oracle.gblup_fit(X[idx], Y[idx], 1.0)
+    assert q == ref["q"]
+    assert rel(yp, ref["y_pred"]) < 1e-9 and rel(b, ref["b_hat"]) < 1e-6
