@@ -29,6 +29,7 @@ int launch_chol_update(double* G, int64_t ldg, int64_t k0, int64_t nb, int64_t g
 int launch_chol_row_update(double* G, int64_t ldg, int64_t k0, int kch, int64_t gdim, double* Ld, double* Dinv,
                            int32_t* info, int32_t* fflags, hipStream_t s);
 int64_t chol_small_lim();
+void chol_refresh_tuning();
 
 // ---- V = G/q + λI (upper part), padding = identity, bordered R columns -----------------------
 __global__ void __launch_bounds__(256) prepare_v_kernel(double* __restrict__ G, int64_t ld, int64_t n,
@@ -447,18 +448,19 @@ extern "C" int gbm_dev_gblup_solve(double* G, int64_t ldg, int64_t n, double inv
     chol_panel_kernel<<<(unsigned)chunks, 256, 0, s>>>(G, ldg, k0, Ld, Dinv);
     return hipGetLastError() == hipSuccess;
   };
+  chol_refresh_tuning();
   // 4-panel groups (one K = 256 trailing update) while the trailing matrix exceeds this many rows
-  static const int64_t group4_lim = [] {
+  const int64_t group4_lim = [] {  // read per call (tests force the groups on small matrices)
     const char* e = getenv("GBM_CHOL_G4_LIM");
     return e ? (int64_t)atoll(e) : (int64_t)8192;
   }();
   // 8-panel groups (K = 512) while the trailing matrix exceeds this many rows. Solve at
   // n = 50 000: 798 ms (4-panel groups only) -> 746 ms; n = 20 000: 67.1 -> 64.0 ms
-  static const int64_t group8_lim = [] {
+  const int64_t group8_lim = [] {
     const char* e = getenv("GBM_CHOL_G8_LIM");
     return e ? (int64_t)atoll(e) : (int64_t)8192;
   }();
-  static const int64_t group16_lim = [] {  // 16-panel groups (K = 1024): n = 50 000 746 -> 735 ms
+  const int64_t group16_lim = [] {  // 16-panel groups (K = 1024): n = 50 000 746 -> 735 ms
     const char* e = getenv("GBM_CHOL_G16_LIM");
     return e ? (int64_t)atoll(e) : (int64_t)16384;
   }();

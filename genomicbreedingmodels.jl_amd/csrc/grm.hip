@@ -13,6 +13,7 @@
 //     resident workgroup slot (256 CUs x 2), so there is no tail round; partial tiles go to
 //     workspace slabs that a second kernel sums in a fixed order (deterministic, no float atomics).
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -1226,13 +1227,14 @@ syrk64_sub_kernel(const double* __restrict__ U, int64_t ldu, int64_t c0, int64_t
   }
 }
 
-int64_t chol_small_lim() {
-  static const int64_t v = [] {
-    const char* e = getenv("GBM_UPD64_LIM");
-    return e ? (int64_t)atoll(e) : (int64_t)2048;
-  }();
-  return v;
+// single-panel steps with 64x64-tile updates below this many trailing rows (GBM_UPD64_LIM,
+// re-read at every solve so tests can force the grouped paths on small matrices)
+static std::atomic<int64_t> g_small_lim{2048};
+void chol_refresh_tuning() {
+  const char* e = getenv("GBM_UPD64_LIM");
+  g_small_lim.store(e ? (int64_t)atoll(e) : (int64_t)2048, std::memory_order_relaxed);
 }
+int64_t chol_small_lim() { return g_small_lim.load(std::memory_order_relaxed); }
 
 // Block row [k1, k1+64) only, k1 = k0 + 64 kch: C[k1 : k1+64, k1 : gdim] -= U[k0:k1, ·]ᵀ U[k0:k1, ·]
 // (a later panel's rows of a 2- or 4-panel group, brought up to date with the group's earlier

@@ -184,3 +184,69 @@ def test_repeated_solves_are_bit_identical():
             assert rel(first, ref["y_pred"]) < TOL_TIGHT
         else:
             assert np.array_equal(y_pred, first)
+
+
+@pytest.mark.parametrize("g4,g8,g16", [(0, -1, -1), (-1, 0, -1), (-1, -1, 0), (0, 0, 0)])
+def test_cholesky_panel_groups_forced(monkeypatch, g4, g8, g16):
+    """The 4/8/16-panel groups (K = 256/512/1024 trailing updates, row updates of K = 64 j) run
+    only on large trailing matrices by default; force them on a small one (the thresholds are
+    read at every solve) and compare with the oracle."""
+    monkeypatch.setenv("GBM_CHOL_G4_LIM", str(g4))
+    monkeypatch.setenv("GBM_CHOL_G8_LIM", str(g8))
+    monkeypatch.setenv("GBM_CHOL_G16_LIM", str(g16))
+    monkeypatch.setenv("GBM_UPD64_LIM", "128")
+    n, p = 1500, 900
+    X = oracle.synth_genotypes(77, n, p)
+    Y = oracle.synth_phenotypes(X, 78, ntraits=2)
+    b_hat, y_pred, mu, q = gbm.gblup_arrays(X, Y, lambda_=0.7)
+    ref = oracle.gblup_fit(X, Y, 0.7)
+    assert q == ref["q"]
+    assert rel(y_pred, ref["y_pred"]) < TOL_TIGHT
+    assert rel(mu, ref["mu"]) < TOL_TIGHT
+    assert rel(b_hat, ref["b_hat"]) < TOL_CONTRACT
+
+
+def test_full_size_c2_properties():
+    """Config C2 at full size (n = 5 000, p = 50 000, X generated on the device) through
+    size-independent properties of the exact solution:
+      * mean diag(G) = (n − 1)/n exactly in exact arithmetic (every kept standardised column has
+        Σ z² = n − 1, ddof = 1), and G is symmetric;
+      * (G + λI) a = y − μ̂1 (the solve's residual), and 1ᵀa = 0 (μ̂ is the GLS estimate);
+      * predict's b0 + X b reproduces the GEBVs (src/prediction.jl:228);
+      * a 500-row × 50 000-locus subset matches the oracle."""
+    import torch
+
+    from gbm import synth
+    from gbm.sharded import HipShardStages, LocalComm, assemble_b_hat, sharded_gblup_step
+
+    n, p, lam = 5000, 50000, 1.0
+    st = HipShardStages(n, p, nrhs=1, lambda_=lam, device=0)
+    st.generate(4242, 0)
+    Y = synth.qtl_phenotypes(4242, n, p, 1, device=0)
+    st.load_phenotypes(Y)
+    st.standardize()
+    st.grm_syrk()
+    st.grm_reduce()
+    q = int(st.q.item())
+    npad = st.npad
+    Gu = torch.triu(st.G[:npad, :npad]) / q  # the upper tiles hold G·q (scaled in the solve)
+    G = (Gu + Gu.T - torch.diag(torch.diagonal(Gu)))[:n, :n]
+    assert abs(float(torch.diagonal(G).mean()) - (n - 1) / n) < 1e-12
+    G_cpu = G.cpu().numpy()
+    assert np.array_equal(G_cpu, G_cpu.T)
+    out = sharded_gblup_step(st, LocalComm())
+    y_pred, mu = out["y_pred"][:, 0], out["mu"][0]
+    a = st.A[0, :n].cpu().numpy()
+    resid = G_cpu @ a + lam * a - (Y[:, 0] - mu)
+    assert np.abs(resid).max() / np.abs(Y[:, 0] - mu).max() < 1e-10
+    assert abs(a.sum()) / np.abs(a).sum() < 1e-10
+    b_hat = assemble_b_hat(out["mu"], out["msum"], [out["B"]], p)
+    X = st.X[:, :n].T  # device (n, p)
+    pred = b_hat[0, 0] + (X @ torch.from_numpy(b_hat[1:, 0]).to(X.device)).cpu().numpy()
+    assert rel(pred, y_pred) < TOL_TIGHT
+    # oracle on a subset of rows (its own fit on those rows)
+    rows = np.arange(0, n, 10)
+    Xs = st.X[:, rows].T.cpu().numpy()
+    b_s, yp_s, mu_s, q_s = gbm.gblup_arrays(np.asfortranarray(Xs), Y[rows], lambda_=lam)
+    ref = oracle.gblup_fit(np.asfortranarray(Xs), Y[rows], lam)
+    assert q_s == ref["q"] and rel(yp_s, ref["y_pred"]) < TOL_TIGHT and rel(b_s, ref["b_hat"]) < TOL_CONTRACT
