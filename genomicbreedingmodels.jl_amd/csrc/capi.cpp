@@ -35,7 +35,7 @@ struct Shard {
   int64_t q_host = 0;
 };
 
-enum class Source { F64, I8 };
+enum class Source { F64, I8, SYNTH };
 
 struct Problem {
   Source src;
@@ -43,6 +43,7 @@ struct Problem {
   const int8_t* D;
   int ploidy;
   int64_t n, p, ld;
+  uint64_t seed = 0;  // Source::SYNTH: genotypes generated on each device
 };
 
 // Upload the shard's columns and standardise them; reads back the shard's kept count.
@@ -59,6 +60,8 @@ int prepare_shard(const Problem& pr, Shard& sh) {
   GBM_TRY(dalloc(sh.q, sh.dev, 8));
   if (pr.src == Source::F64) {
     GBM_HIP_TRY(hipMemcpy2DAsync(sh.Xt.p, npad * 8, pr.X + sh.j0 * pr.ld, pr.ld * 8, n * 8, pl, hipMemcpyHostToDevice, s));
+  } else if (pr.src == Source::SYNTH) {
+    GBM_TRY(gbm_dev_synth_genotypes((double*)sh.Xt.p, npad, pl, n, pr.seed, sh.j0, s));
   } else {
     GBM_TRY(dalloc(sh.D8, sh.dev, pl * n));
     GBM_HIP_TRY(hipMemcpy2DAsync(sh.D8.p, n, pr.D + sh.j0 * pr.ld, pr.ld, n, pl, hipMemcpyHostToDevice, s));
@@ -152,7 +155,10 @@ int run_fit(const Problem& pr, const double* Y, int64_t ldy, int64_t nrhs, doubl
   for (auto& sh : shards) GBM_TRY(grm_shard(pr, *sh));
   GBM_TRY(allreduce_grm(shards, n));
   const double inv_q = 1.0 / (double)q;
-  std::vector<double> msum_total(nrhs, 0.0), mu(nrhs, 0.0), msum(nrhs);
+  std::vector<double> msum_total(nrhs, 0.0), mu(nrhs, 0.0);
+  // every shard solves the (identical) n x n system redundantly, all devices at once: a is then
+  // local to each shard's marker back-solve with no broadcast
+  std::vector<int32_t> infos(shards.size(), 0);
   for (size_t k = 0; k < shards.size(); k++) {
     Shard& sh = *shards[k];
     GBM_HIP_TRY(hipSetDevice(sh.dev));
@@ -167,14 +173,18 @@ int run_fit(const Problem& pr, const double* Y, int64_t ldy, int64_t nrhs, doubl
     GBM_TRY(dalloc(sh.B, sh.dev, nrhs * sh.p * 8));
     GBM_TRY(dalloc(sh.msum, sh.dev, nrhs * 8));
     GBM_HIP_TRY(hipMemcpy2DAsync(sh.Y.p, npad * 8, Y, ldy * 8, n * 8, nrhs, hipMemcpyHostToDevice, s));
-    // every shard solves the (identical) n x n system redundantly: a is then local to each
-    // shard's marker back-solve with no broadcast
     GBM_TRY(gbm_dev_gblup_solve((double*)sh.G.p, gdim, n, inv_q, nullptr, lambda, (const double*)sh.Y.p, npad, nrhs,
                                 (double*)sh.A.p, (double*)sh.gebv.p, npad, (double*)sh.mu.p, (int32_t*)sh.info.p,
                                 sh.wss.p, wss, s));
-    int32_t info = 0;
-    GBM_HIP_TRY(hipMemcpyAsync(&info, sh.info.p, 4, hipMemcpyDeviceToHost, s));
+    GBM_HIP_TRY(hipMemcpyAsync(&infos[k], sh.info.p, 4, hipMemcpyDeviceToHost, s));
+  }
+  std::vector<std::vector<double>> msums(shards.size(), std::vector<double>(nrhs, 0.0));
+  for (size_t k = 0; k < shards.size(); k++) {
+    Shard& sh = *shards[k];
+    GBM_HIP_TRY(hipSetDevice(sh.dev));
+    hipStream_t s = sh.stream.s;
     GBM_HIP_TRY(hipStreamSynchronize(s));
+    const int32_t info = infos[k];
     if (info < 0) return fail(GBM_E_HIP, "back substitution: block synchronisation timed out");
     if (info != 0)
       return fail(GBM_E_NOTPD, "G/q + lambda*I is not positive definite (pivot " + std::to_string(info) +
@@ -184,13 +194,16 @@ int run_fit(const Problem& pr, const double* Y, int64_t ldy, int64_t nrhs, doubl
                                    (double*)sh.B.p, sh.p, (double*)sh.msum.p, s));
     GBM_HIP_TRY(hipMemcpy2DAsync(b_hat_out + 1 + sh.j0, (p + 1) * 8, sh.B.p, sh.p * 8, sh.p * 8, nrhs,
                                  hipMemcpyDeviceToHost, s));
-    GBM_HIP_TRY(hipMemcpyAsync(msum.data(), sh.msum.p, nrhs * 8, hipMemcpyDeviceToHost, s));
+    GBM_HIP_TRY(hipMemcpyAsync(msums[k].data(), sh.msum.p, nrhs * 8, hipMemcpyDeviceToHost, s));
     if (k == 0) {
       GBM_HIP_TRY(hipMemcpy2DAsync(y_pred_out, n * 8, sh.gebv.p, npad * 8, n * 8, nrhs, hipMemcpyDeviceToHost, s));
       GBM_HIP_TRY(hipMemcpyAsync(mu.data(), sh.mu.p, nrhs * 8, hipMemcpyDeviceToHost, s));
     }
-    GBM_HIP_TRY(hipStreamSynchronize(s));
-    for (int64_t t = 0; t < nrhs; t++) msum_total[t] += msum[t];
+  }
+  for (size_t k = 0; k < shards.size(); k++) {
+    GBM_HIP_TRY(hipSetDevice(shards[k]->dev));
+    GBM_HIP_TRY(hipStreamSynchronize(shards[k]->stream.s));
+    for (int64_t t = 0; t < nrhs; t++) msum_total[t] += msums[k][t];  // shard order: deterministic
   }
   for (int64_t t = 0; t < nrhs; t++) {
     b_hat_out[t * (p + 1)] = mu[t] - msum_total[t];
@@ -226,6 +239,15 @@ extern "C" int gbm_gblup_fit(const double* X, int64_t n, int64_t p, int64_t ldx,
                              double* y_pred_out, double* mu_out, int64_t* q_out) {
   if (!X) return fail(GBM_E_ARG, "gbm_gblup_fit: X is NULL");
   Problem pr{Source::F64, X, nullptr, 1, n, p, ldx};
+  return run_fit(pr, Y, ldy, nrhs, lambda, devices, ndev, b_hat_out, y_pred_out, mu_out, q_out);
+}
+
+extern "C" int gbm_gblup_fit_synthetic(uint64_t seed, int64_t n, int64_t p, const double* Y, int64_t ldy, int64_t nrhs,
+                                       double lambda, const int* devices, int ndev, double* b_hat_out,
+                                       double* y_pred_out, double* mu_out, int64_t* q_out) {
+  if (n < 1 || p < 1) return fail(GBM_E_ARG, "gbm_gblup_fit_synthetic: bad arguments (n, p >= 1)");
+  Problem pr{Source::SYNTH, nullptr, nullptr, 1, n, p, n};
+  pr.seed = seed;
   return run_fit(pr, Y, ldy, nrhs, lambda, devices, ndev, b_hat_out, y_pred_out, mu_out, q_out);
 }
 

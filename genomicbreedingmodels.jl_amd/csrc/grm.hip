@@ -1298,23 +1298,41 @@ static bool grm_edge_concurrent() {  // GBM_GRM_EDGE_CONCURRENT=0: edge kernel a
   return v;
 }
 
-// one helper stream + fork/join events per (host thread, device): calls from different threads
-// never share events, and calls from one thread are ordered by the caller's stream anyway
+// The helper stream of the forked edge kernel: one per device for the process (bounded, created
+// on first use), with fork/join events made per call, so concurrent callers never share an event
+// (two callers on one device only queue their edge kernels behind each other). No fork when the
+// caller's stream belongs to another device than the current one.
 struct AuxStream {
   hipStream_t s = nullptr;
   hipEvent_t fork = nullptr, join = nullptr;
+  ~AuxStream() {
+    if (fork) (void)hipEventDestroy(fork);  // destruction is deferred until the event completes
+    if (join) (void)hipEventDestroy(join);
+  }
 };
-static int aux_stream(AuxStream** out) {
-  thread_local std::map<int, AuxStream> per_dev;
+static int aux_stream(hipStream_t caller, AuxStream& a, bool* usable) {
+  *usable = false;
   int dev = 0;
   GBM_HIP_TRY(hipGetDevice(&dev));
-  AuxStream& a = per_dev[dev];
-  if (!a.s) {
-    GBM_HIP_TRY(hipStreamCreateWithFlags(&a.s, hipStreamNonBlocking));
-    GBM_HIP_TRY(hipEventCreateWithFlags(&a.fork, hipEventDisableTiming));
-    GBM_HIP_TRY(hipEventCreateWithFlags(&a.join, hipEventDisableTiming));
+  if (caller) {
+    int sdev = -1;
+    if (hipStreamGetDevice(caller, &sdev) != hipSuccess) {
+      (void)hipGetLastError();
+      return GBM_OK;
+    }
+    if (sdev != dev) return GBM_OK;
   }
-  *out = &a;
+  static std::mutex mu;
+  static std::map<int, hipStream_t> streams;
+  {
+    std::lock_guard<std::mutex> lock(mu);
+    hipStream_t& hs = streams[dev];
+    if (!hs) GBM_HIP_TRY(hipStreamCreateWithFlags(&hs, hipStreamNonBlocking));
+    a.s = hs;
+  }
+  GBM_HIP_TRY(hipEventCreateWithFlags(&a.fork, hipEventDisableTiming));
+  GBM_HIP_TRY(hipEventCreateWithFlags(&a.join, hipEventDisableTiming));
+  *usable = true;
   return GBM_OK;
 }
 
@@ -1355,12 +1373,17 @@ int launch_grm_syrk(const double* Zt, int64_t ldz, int64_t p, int64_t n, double*
   // the ragged-column kernel beside the persistent tiles: forked (before the tile launch) onto
   // this thread's helper stream for the device; its workgroups fit in the registers the two tile
   // workgroups of a CU leave free. Joined back before the reduce.
+  AuxStream aux;
   AuxStream* ax = nullptr;
   if (edge_on_aux(g)) {
-    rc = aux_stream(&ax);
+    bool usable = false;
+    rc = aux_stream(s, aux, &usable);
     if (rc != GBM_OK) return rc;
-    GBM_HIP_TRY(hipEventRecord(ax->fork, s));
-    GBM_HIP_TRY(hipStreamWaitEvent(ax->s, ax->fork, 0));
+    if (usable) {
+      ax = &aux;
+      GBM_HIP_TRY(hipEventRecord(ax->fork, s));
+      GBM_HIP_TRY(hipStreamWaitEvent(ax->s, ax->fork, 0));
+    }
   }
   if (g.wide) {
     grm_syrk8_kernel<<<grid, 512, 0, s>>>(Zt, ldz, p, n, G, ldg, (double*)ws, g.ntiles, g.sb);
@@ -1386,11 +1409,13 @@ int launch_grm_syrk(const double* Zt, int64_t ldz, int64_t p, int64_t n, double*
       default: grm_edge_kernel<4><<<eg, 256, 0, es>>>(Zt, ldz, p, g.sb, part); break;
     }
     GBM_LAUNCH_CHECK();
-    if (ax) {
-      // the edge columns of G are disjoint from the tiles: sum their partials on the helper
-      // stream too (launch_grm_reduce then skips them)
-      grm_edge_reduce_kernel<<<(unsigned)((n * g.sb.er + 255) / 256), 256, 0, ax->s>>>(part, n, g.sb, G, ldg);
+    if (edge_on_aux(g)) {
+      // the edge columns of G are disjoint from the tiles: sum their partials here, on the helper
+      // stream when there is one (launch_grm_reduce then skips them)
+      grm_edge_reduce_kernel<<<(unsigned)((n * g.sb.er + 255) / 256), 256, 0, es>>>(part, n, g.sb, G, ldg);
       GBM_LAUNCH_CHECK();
+    }
+    if (ax) {
       GBM_HIP_TRY(hipEventRecord(ax->join, ax->s));
       GBM_HIP_TRY(hipStreamWaitEvent(s, ax->join, 0));
     }

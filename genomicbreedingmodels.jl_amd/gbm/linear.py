@@ -40,6 +40,28 @@ def gblup_arrays(X: np.ndarray, Y: np.ndarray, lambda_: float = 1.0, devices=Non
     return b_hat, y_pred, mu, int(q[0])
 
 
+def gblup_synthetic(seed: int, n: int, p: int, Y: np.ndarray, lambda_: float = 1.0, devices=None):
+    """GBLUP on the device-generated synthetic genotypes (gbm_gblup_fit_synthetic: loci 0..p-1 of the
+    SURVEY.md §8d generator, no host X). Returns (b_hat (p+1, t), y_pred (n, t), mu (t,), q)."""
+    Y = np.asarray(Y, dtype=np.float64)
+    if Y.ndim == 1:
+        Y = Y[:, None]
+    Y = np.asfortranarray(Y)
+    if Y.shape[0] != n:
+        raise ArgumentError("Y must have n rows")
+    t = Y.shape[1]
+    b_hat = np.zeros((p + 1, t), order="F")
+    y_pred = np.zeros((n, t), order="F")
+    mu = np.zeros(t)
+    q = np.zeros(1, dtype=np.int64)
+    devs, ndev = _lib.devices_arg(devices)
+    lib = _lib.load()
+    rc = lib.gbm_gblup_fit_synthetic(int(seed), n, p, _lib.ptr(Y), n, t, float(lambda_), devs, ndev,
+                                     _lib.ptr(b_hat), _lib.ptr(y_pred), _lib.ptr(mu), _lib.ptr(q))
+    _lib.check(rc, "gbm_gblup_fit_synthetic")
+    return b_hat, y_pred, mu, int(q[0])
+
+
 def gblup(*, genomes: Genomes, phenomes: Phenomes, idx_entries=None, idx_loci_alleles=None,
           idx_trait: int = 1, verbose: bool = False, lambda_: float = 1.0, devices=None,
           model_label: str = "gblup") -> Fit:

@@ -91,6 +91,16 @@ int gbm_gblup_fit_dosage_i8(const int8_t* D, int64_t n, int64_t p, int64_t ldd, 
                             double* b_hat_out, double* y_pred_out, double* mu_out, int64_t* q_out);
 
 /*
+ * Same as gbm_gblup_fit on the synthetic genotypes of gbm_dev_synth_genotypes (seed, loci
+ * 0..p-1), generated on each device for its SNP-column shard: benchmark-scale
+ * fits (config C3: 240 GB of fp64 X) with no host copy of X and no PCIe transfer.
+ */
+int gbm_gblup_fit_synthetic(uint64_t seed, int64_t n, int64_t p,
+                            const double* Y, int64_t ldy, int64_t nrhs, double lambda,
+                            const int* devices, int ndev,
+                            double* b_hat_out, double* y_pred_out, double* mu_out, int64_t* q_out);
+
+/*
  * Genomic relationship matrix only: G = Z Zᵀ / q (n x n, column-major == row-major since
  * symmetric, ldg >= n). Replaces GenomicBreedingCore.grmsimple(genomes).genomic_relationship_matrix
  * at src/gwas.jl:124-125 under the north-star formula (the Core implementation is un-vendored).

@@ -250,3 +250,48 @@ def test_full_size_c2_properties():
     b_s, yp_s, mu_s, q_s = gbm.gblup_arrays(np.asfortranarray(Xs), Y[rows], lambda_=lam)
     ref = oracle.gblup_fit(np.asfortranarray(Xs), Y[rows], lam)
     assert q_s == ref["q"] and rel(yp_s, ref["y_pred"]) < TOL_TIGHT and rel(b_s, ref["b_hat"]) < TOL_CONTRACT
+
+
+def test_gblup_fit_synthetic_matches_host_fit():
+    """gbm_gblup_fit_synthetic (genotypes generated on the device) equals the
+    host-buffer fit of the same synthetic X (and the oracle)."""
+    n, p = 1030, 2500
+    X = oracle.synth_genotypes(4242, n, p)
+    Y = oracle.synth_phenotypes(X, 6, ntraits=2)
+    b1, y1, mu1, q1 = gbm.gblup_synthetic(4242, n, p, Y, lambda_=1.0)
+    b2, y2, mu2, q2 = gbm.gblup_arrays(X, Y, lambda_=1.0)
+    assert q1 == q2 and np.array_equal(y1, y2) and np.array_equal(b1, b2) and np.array_equal(mu1, mu2)
+    ref = oracle.gblup_fit(X, Y, 1.0)
+    assert rel(y1, ref["y_pred"]) < TOL_TIGHT and rel(b1, ref["b_hat"]) < TOL_CONTRACT
+
+
+def test_concurrent_calls_from_threads():
+    """Re-entrancy as cvmultithread! needs (src/cross_validation.jl:159): eight host threads call
+    the C ABI at once on one device (own streams, workspaces, helper-stream events per call);
+    every result equals the serial one bit for bit."""
+    import threading
+
+    cases = []
+    for k in range(8):
+        n, p = (1030, 1400) if k % 2 == 0 else (333, 1777)
+        X = oracle.synth_genotypes(100 + k, n, p)
+        Y = oracle.synth_phenotypes(X, 200 + k, ntraits=1 + k % 3)
+        cases.append((X, Y))
+    serial = [gbm.gblup_arrays(X, Y, lambda_=0.8) for X, Y in cases]
+    out = [None] * len(cases)
+    errs = []
+
+    def run(k):
+        try:
+            out[k] = gbm.gblup_arrays(cases[k][0], cases[k][1], lambda_=0.8)
+        except Exception as e:  # reported below
+            errs.append(repr(e))
+
+    th = [threading.Thread(target=run, args=(k,)) for k in range(len(cases))]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not errs, errs
+    for a, b in zip(out, serial):
+        assert np.array_equal(a[1], b[1]) and np.array_equal(a[0], b[0])
