@@ -146,24 +146,59 @@ __global__ void __launch_bounds__(1024) brr_mu_kernel(double* __restrict__ e, in
 
 constexpr int IW = 256;  // individuals per workgroup in the block kernels
 
+// Genotype storage of the block kernels: fp64 (any allele frequencies), or bytes d with
+// x = d·xs when every x/xs is an integer in [0, 255] (xs = 1/2 for diploid dosages: exact, so
+// both storages run the identical chain with 8× fewer bytes per block for the bytes).
+// 64 byte-genotypes (4 × 16 B) times 64 values of es, accumulated in the fp64 path's order:
+// even individuals into s, odd ones into s1.
+__device__ __forceinline__ void brr_dot64_u8(const uint4 (&v)[4], const double* es, double xs, double& s,
+                                             double& s1) {
+#pragma unroll
+  for (int u = 0; u < 4; u++) {
+    const uint32_t wd[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+#pragma unroll
+    for (int w = 0; w < 4; w++)
+#pragma unroll
+      for (int b = 0; b < 4; b += 2) {
+        const int idx = 16 * u + 4 * w + b;
+        s = fma((double)((wd[w] >> (8 * b)) & 0xFFu) * xs, es[idx], s);
+        s1 = fma((double)((wd[w] >> (8 * b + 8)) & 0xFFu) * xs, es[idx + 1], s1);
+      }
+  }
+}
+template <typename T>
+__device__ __forceinline__ double gval(T v, double xs) {
+  if constexpr (sizeof(T) == 8) return (double)v;
+  else return (double)v * xs;
+}
+
 // partial[c][k] = Σ_{i in chunk c} x_{j0+k, i} e_i over this workgroup's IW individuals, from es
 // (the chunk of e in LDS): thread (k = tid/4, quarter) sums 64 contiguous individuals
-__device__ __forceinline__ void brr_partials(const double* __restrict__ Xt, int64_t ldx, int64_t n, int64_t i0,
-                                             int64_t j0, int nb, const double* es, double* __restrict__ out) {
+template <typename T>
+__device__ __forceinline__ void brr_partials(const T* __restrict__ Xt, int64_t ldx, int64_t n, int64_t i0,
+                                             int64_t j0, int nb, double xs, const double* es,
+                                             double* __restrict__ out) {
   const int tid = threadIdx.x, k = tid >> 2, qt = tid & 3;
   double s = 0.0;
   if (k < nb) {
     // 64 contiguous individuals per thread, all loads in flight (rows are zero-padded to ldx, a
     // multiple of IW, and es is 0 past n)
-    const double* row = Xt + (j0 + k) * ldx + i0 + qt * 64;
-    double2 v[32];
-#pragma unroll
-    for (int u = 0; u < 32; u++) v[u] = *reinterpret_cast<const double2*>(row + 2 * u);
+    const T* row = Xt + (j0 + k) * ldx + i0 + qt * 64;
     double s1 = 0.0;
+    if constexpr (sizeof(T) == 8) {
+      double2 v[32];
 #pragma unroll
-    for (int u = 0; u < 32; u++) {
-      s = fma(v[u].x, es[qt * 64 + 2 * u], s);
-      s1 = fma(v[u].y, es[qt * 64 + 2 * u + 1], s1);
+      for (int u = 0; u < 32; u++) v[u] = *reinterpret_cast<const double2*>(row + 2 * u);
+#pragma unroll
+      for (int u = 0; u < 32; u++) {
+        s = fma(v[u].x, es[qt * 64 + 2 * u], s);
+        s1 = fma(v[u].y, es[qt * 64 + 2 * u + 1], s1);
+      }
+    } else {
+      uint4 v[4];
+#pragma unroll
+      for (int u = 0; u < 4; u++) v[u] = *reinterpret_cast<const uint4*>(row + 16 * u);
+      brr_dot64_u8(v, es + qt * 64, xs, s, s1);
     }
     s += s1;
   }
@@ -173,22 +208,24 @@ __device__ __forceinline__ void brr_partials(const double* __restrict__ Xt, int6
 }
 
 // partials of block 0 at the start of an iteration (after the intercept update)
-__global__ void __launch_bounds__(256) brr_dots0_kernel(const double* __restrict__ Xt, int64_t ldx, int64_t n,
-                                                        int64_t p, const double* __restrict__ e,
+template <typename T>
+__global__ void __launch_bounds__(256) brr_dots0_kernel(const T* __restrict__ Xt, int64_t ldx, int64_t n,
+                                                        int64_t p, double xs, const double* __restrict__ e,
                                                         double* __restrict__ partial) {
   __shared__ double es[IW];
   const int64_t i0 = (int64_t)blockIdx.x * IW;
   es[threadIdx.x] = i0 + threadIdx.x < n ? e[i0 + threadIdx.x] : 0.0;
   __syncthreads();
-  brr_partials(Xt, ldx, n, i0, 0, (int)(p < BB ? p : BB), es, partial);
+  brr_partials<T>(Xt, ldx, n, i0, 0, (int)(p < BB ? p : BB), xs, es, partial);
 }
 
 // One block of 64 markers: r = Σ_c partial_in[c] (fixed order), the 64 single-site steps (wave 0
 // of every workgroup, identical inputs → identical results; the Gram row of lane k in registers,
 // δ_s broadcast by v_readlane), e += X_B δ on this workgroup's individuals, then the partials of
 // the next block from the updated e. Workgroup 0 stores b and the running posterior mean.
-__global__ void __launch_bounds__(256) brr_step_kernel(const double* __restrict__ Xt, int64_t ldx, int64_t n,
-                                                       int64_t p, const double* __restrict__ W, int64_t blk,
+template <typename T>
+__global__ void __launch_bounds__(256) brr_step_kernel(const T* __restrict__ Xt, int64_t ldx, int64_t n,
+                                                       int64_t p, double xs, const double* __restrict__ W, int64_t blk,
                                                        int64_t nblk, const double* __restrict__ partial_in,
                                                        double* __restrict__ partial_out, double* __restrict__ b,
                                                        double* __restrict__ bbar, const double* __restrict__ x2,
@@ -211,15 +248,27 @@ __global__ void __launch_bounds__(256) brr_step_kernel(const double* __restrict_
   const int nb1 = more ? (int)((p - j1) < BB ? (p - j1) : BB) : 0;
   // every load that does not depend on this block's δ goes out first:
   // (1) the next block's rows into LDS (global_load_lds: 1 KB per wave instruction)
-  for (int q = wave; q < 2 * nb1; q += 4) {
-    const int k = q >> 1, h = q & 1;
-    const double* src = Xt + (j1 + k) * ldx + i0 + h * 128 + lane * 2;
-    __builtin_amdgcn_global_load_lds((const void*)src, (void*)(Xn + k * RP + h * 128), 16, 0, 0);
+  uint8_t* Xb = reinterpret_cast<uint8_t*>(Xn);  // byte storage: rows of IW bytes, unpadded
+  if constexpr (sizeof(T) == 8) {
+    for (int q = wave; q < 2 * nb1; q += 4) {
+      const int k = q >> 1, h = q & 1;
+      const T* src = Xt + (j1 + k) * ldx + i0 + h * 128 + lane * 2;
+      __builtin_amdgcn_global_load_lds((const void*)src, (void*)(Xn + k * RP + h * 128), 16, 0, 0);
+    }
+  } else {
+    // 4 rows per wave instruction; row r's 16-byte chunk c is stored at position c ^ (r & 15)
+    // (swizzled source address), so the partials loop's lanes (one row each) read distinct banks.
+    // Rows past the block (last block) re-read row nb1 − 1: valid memory, never summed.
+    for (int q = wave; q < (nb1 + 3) / 4; q += 4) {
+      const int r = 4 * q + (lane >> 4), c = lane & 15;
+      const T* src = Xt + (j1 + (r < nb1 ? r : nb1 - 1)) * ldx + i0 + ((c ^ (r & 15)) * 16);
+      __builtin_amdgcn_global_load_lds((const void*)src, (void*)(Xb + q * 4 * IW), 16, 0, 0);
+    }
   }
   // (2) this thread's 64 genotypes of the block, for e += X_B δ (rows past p clamped; δ = 0)
   double xv[BB];
 #pragma unroll
-  for (int s2 = 0; s2 < BB; s2++) xv[s2] = Xt[(j0 + (s2 < nb ? s2 : 0)) * ldx + i];
+  for (int s2 = 0; s2 < BB; s2++) xv[s2] = gval<T>(Xt[(j0 + (s2 < nb ? s2 : 0)) * ldx + i], xs);
   const double e_old = e[i];
   // (3) wave 0's operands
   double w[BB];
@@ -235,7 +284,9 @@ __global__ void __launch_bounds__(256) brr_step_kernel(const double* __restrict_
       w[q + 1] = v.y;
     }
     xx = on ? x2[j] : 0.0;
-    bo = on ? b[j] : 0.0;
+    // b ping-pongs between two copies by iteration parity: a workgroup that starts late never
+    // reads a value workgroup 0 already updated in this iteration
+    bo = on ? b[(st->it & 1) * p + j] : 0.0;
     varE = st->varE;
     varB = st->varB;
   }
@@ -281,7 +332,7 @@ __global__ void __launch_bounds__(256) brr_step_kernel(const double* __restrict_
     }
     delta[lane] = bo - bfin;
     if (blockIdx.x == 0 && on) {
-      b[j] = bfin;
+      b[((st->it & 1) ^ 1) * p + j] = bfin;
       if (brr_accumulate(st)) {
         const double k = (double)(st->nsum + 1);
         bbar[j] = bbar[j] * ((k - 1.0) / k) + bfin / k;
@@ -310,13 +361,21 @@ __global__ void __launch_bounds__(256) brr_step_kernel(const double* __restrict_
     // partial[c][k] = Σ_u Xn[k][w*64 + u] es[w*64 + u]: lane k = marker, wave w = quarter
     double s0 = 0.0, s1 = 0.0;
     if (lane < nb1) {
-      const double* xr = Xn + lane * RP + wave * 64;
       const double* er = es + wave * 64;
+      if constexpr (sizeof(T) == 8) {
+        const double* xr = Xn + lane * RP + wave * 64;
 #pragma unroll
-      for (int u = 0; u < 64; u += 2) {
-        const double2 xv2 = *reinterpret_cast<const double2*>(xr + u);
-        s0 = fma(xv2.x, er[u], s0);
-        s1 = fma(xv2.y, er[u + 1], s1);
+        for (int u = 0; u < 64; u += 2) {
+          const double2 xv2 = *reinterpret_cast<const double2*>(xr + u);
+          s0 = fma(xv2.x, er[u], s0);
+          s1 = fma(xv2.y, er[u + 1], s1);
+        }
+      } else {
+        const uint8_t* xr = Xb + lane * IW;
+        uint4 v[4];
+#pragma unroll
+        for (int t = 0; t < 4; t++) v[t] = *reinterpret_cast<const uint4*>(xr + (((4 * wave + t) ^ (lane & 15)) * 16));
+        brr_dot64_u8(v, er, xs, s0, s1);
       }
     }
     part4[wave][lane] = s0 + s1;
@@ -332,7 +391,8 @@ __global__ void __launch_bounds__(1024) brr_var_kernel(const double* __restrict_
                                                        BrrState* __restrict__ st) {
   __shared__ double red[16];
   double sb = 0.0, se = 0.0;
-  for (int64_t j = threadIdx.x; j < p; j += 1024) sb += b[j] * b[j];
+  const double* bn = b + ((st->it & 1) ^ 1) * p;  // this iteration's samples
+  for (int64_t j = threadIdx.x; j < p; j += 1024) sb += bn[j] * bn[j];
   for (int64_t i = threadIdx.x; i < n; i += 1024) se += e[i] * e[i];
   sb = brr_block_sum<1024>(sb, red);
   se = brr_block_sum<1024>(se, red);
@@ -349,6 +409,21 @@ __global__ void __launch_bounds__(1024) brr_var_kernel(const double* __restrict_
     }
     st->it += 1;
   }
+}
+
+// D = X·s as bytes when that is exact for every stored value (padding included, which is 0);
+// *bad counts the values that are not integers in [0, 255] after scaling
+__global__ void __launch_bounds__(256) brr_quantize_kernel(const double* __restrict__ Xt, int64_t count, double s,
+                                                           uint8_t* __restrict__ D, int* __restrict__ bad) {
+  int nbad = 0;
+  for (int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x; t < count; t += (int64_t)gridDim.x * 256) {
+    const double v = Xt[t] * s;
+    const double r = rint(v);
+    const bool ok = r == v && r >= 0.0 && r <= 255.0;
+    nbad += ok ? 0 : 1;
+    D[t] = ok ? (uint8_t)r : (uint8_t)0;
+  }
+  if (nbad) atomicAdd(bad, nbad);
 }
 
 }  // namespace
@@ -382,7 +457,7 @@ extern "C" int gbm_brr_fit(const double* X, int64_t n, int64_t p, int64_t ldx, c
   GBM_TRY(dalloc(x2, dev, p * 8));
   GBM_TRY(dalloc(W, dev, nblk * BB * BB * 8));
   GBM_TRY(dalloc(e, dev, npad * 8));
-  GBM_TRY(dalloc(b, dev, p * 8));
+  GBM_TRY(dalloc(b, dev, 2 * p * 8));  // two copies (iteration parity)
   GBM_TRY(dalloc(bbar, dev, p * 8));
   GBM_TRY(dalloc(r, dev, 2 * ((n + IW - 1) / IW) * BB * 8));  // ping-pong partial dots
   GBM_TRY(dalloc(stm, dev, sizeof(BrrState)));
@@ -396,6 +471,31 @@ extern "C" int gbm_brr_fit(const double* X, int64_t n, int64_t p, int64_t ldx, c
   std::vector<double> cm(p), xx(p);
   GBM_HIP_TRY(hipMemcpyAsync(cm.data(), colmean.p, p * 8, hipMemcpyDeviceToHost, s));
   GBM_HIP_TRY(hipMemcpyAsync(xx.data(), x2.p, p * 8, hipMemcpyDeviceToHost, s));
+  // byte storage for the sampler's sweeps when X = D/s exactly (s = 2: diploid allele
+  // frequencies; then 4, 1): the chain is identical, the per-iteration stream 8× smaller.
+  // GBM_BRR_I8=0 keeps fp64 storage (read per call).
+  DevMem D, badm;
+  double xs = 0.0;  // 0: fp64 storage
+  {
+    const char* ev = std::getenv("GBM_BRR_I8");
+    if (!(ev && ev[0] == '0')) {
+      GBM_TRY(dalloc(D, dev, p * npad));
+      GBM_TRY(dalloc(badm, dev, sizeof(int)));
+      const double scales[3] = {2.0, 4.0, 1.0};
+      for (double sc : scales) {
+        int nbad = -1;
+        GBM_HIP_TRY(hipMemsetAsync(badm.p, 0, sizeof(int), s));
+        brr_quantize_kernel<<<2048, 256, 0, s>>>((const double*)Xt.p, p * npad, sc, (uint8_t*)D.p, (int*)badm.p);
+        GBM_LAUNCH_CHECK();
+        GBM_HIP_TRY(hipMemcpyAsync(&nbad, badm.p, sizeof(int), hipMemcpyDeviceToHost, s));
+        GBM_HIP_TRY(hipStreamSynchronize(s));
+        if (nbad == 0) {
+          xs = 1.0 / sc;
+          break;
+        }
+      }
+    }
+  }
   GBM_HIP_TRY(hipStreamSynchronize(s));
   // BGLR defaults (setLT.BRR and the residual prior): var(y) with ddof 1
   double ym = 0.0;
@@ -425,7 +525,7 @@ extern "C" int gbm_brr_fit(const double* X, int64_t n, int64_t p, int64_t ldx, c
   std::vector<double> e0(npad, 0.0);
   for (int64_t i = 0; i < n; i++) e0[i] = y[i] - ym;
   GBM_HIP_TRY(hipMemcpyAsync(e.p, e0.data(), npad * 8, hipMemcpyHostToDevice, s));
-  GBM_HIP_TRY(hipMemsetAsync(b.p, 0, p * 8, s));
+  GBM_HIP_TRY(hipMemsetAsync(b.p, 0, 2 * p * 8, s));
   GBM_HIP_TRY(hipMemsetAsync(bbar.p, 0, p * 8, s));
   GBM_HIP_TRY(hipMemcpyAsync(stm.p, &st0, sizeof(BrrState), hipMemcpyHostToDevice, s));
   GBM_HIP_TRY(hipStreamSynchronize(s));
@@ -434,12 +534,23 @@ extern "C" int gbm_brr_fit(const double* X, int64_t n, int64_t p, int64_t ldx, c
   const unsigned C = (unsigned)((n + IW - 1) / IW);
   auto enqueue_iteration = [&]() -> int {
     brr_mu_kernel<<<1, 1024, 0, s>>>((double*)e.p, n, stp);
-    brr_dots0_kernel<<<C, 256, 0, s>>>((const double*)Xt.p, npad, n, p, (const double*)e.p, (double*)r.p);
+    if (xs > 0.0)
+      brr_dots0_kernel<uint8_t><<<C, 256, 0, s>>>((const uint8_t*)D.p, npad, n, p, xs, (const double*)e.p,
+                                                  (double*)r.p);
+    else
+      brr_dots0_kernel<double><<<C, 256, 0, s>>>((const double*)Xt.p, npad, n, p, 1.0, (const double*)e.p,
+                                                 (double*)r.p);
     for (int64_t k = 0; k < nblk; k++) {
       double* pin = (double*)r.p + (k & 1) * (int64_t)C * BB;
       double* pout = (double*)r.p + ((k + 1) & 1) * (int64_t)C * BB;
-      brr_step_kernel<<<C, 256, 0, s>>>((const double*)Xt.p, npad, n, p, (const double*)W.p, k, nblk, pin, pout,
-                                        (double*)b.p, (double*)bbar.p, (const double*)x2.p, (double*)e.p, stp);
+      if (xs > 0.0)
+        brr_step_kernel<uint8_t><<<C, 256, 0, s>>>((const uint8_t*)D.p, npad, n, p, xs, (const double*)W.p, k, nblk,
+                                                   pin, pout, (double*)b.p, (double*)bbar.p, (const double*)x2.p,
+                                                   (double*)e.p, stp);
+      else
+        brr_step_kernel<double><<<C, 256, 0, s>>>((const double*)Xt.p, npad, n, p, 1.0, (const double*)W.p, k, nblk,
+                                                  pin, pout, (double*)b.p, (double*)bbar.p, (const double*)x2.p,
+                                                  (double*)e.p, stp);
     }
     brr_var_kernel<<<1, 1024, 0, s>>>((const double*)b.p, p, (const double*)e.p, n, stp);
     return hipGetLastError() == hipSuccess ? GBM_OK : fail(GBM_E_HIP, "gbm_brr_fit: launch failed");

@@ -38,6 +38,41 @@ def test_gpu_brr_same_sample_path_as_oracle(n, p, iters):
 
 
 @pytest.mark.gpu
+def test_gpu_brr_multi_chunk_matches_oracle():
+    """n = 1100: five 256-individual chunks, the partial-dot reduction across workgroups."""
+    X = oracle.synth_genotypes(91, 1100, 300)
+    y = oracle.synth_phenotypes(X, 92)[:, 0]
+    ref = oracle.brr_gibbs(X, y, n_iter=6, n_burnin=2, thin=1, seed=5)
+    b_hat, y_pred, var = gbm.brr_arrays(X, y, n_iter=6, n_burnin=2, thin=1, seed=5)
+    rel = lambda a, b: np.abs(a - b).max() / np.abs(b).max()
+    assert rel(b_hat, ref["b_hat"]) < 1e-9 and rel(y_pred, ref["y_pred"]) < 1e-9
+
+
+@pytest.mark.gpu
+def test_gpu_brr_byte_storage_identical_to_fp64(monkeypatch):
+    """Allele frequencies k/2 are stored as bytes for the sweeps (x = d/2 exactly): the chain must
+    be bit-identical to the fp64-storage chain (GBM_BRR_I8=0)."""
+    X = oracle.synth_genotypes(93, 700, 450)
+    y = oracle.synth_phenotypes(X, 94)[:, 0]
+    got = gbm.brr_arrays(X, y, n_iter=8, n_burnin=2, thin=1, seed=11)
+    monkeypatch.setenv("GBM_BRR_I8", "0")
+    ref = gbm.brr_arrays(X, y, n_iter=8, n_burnin=2, thin=1, seed=11)
+    for a, b in zip(got, ref):
+        assert np.array_equal(a, b)
+
+
+@pytest.mark.gpu
+def test_gpu_brr_non_dyadic_genotypes_use_fp64_storage():
+    """Values that are not k/s (s = 2, 4, 1) keep fp64 storage; the chain still follows the oracle."""
+    X = oracle.synth_genotypes(95, 300, 200) * 0.3 + 0.05
+    y = oracle.synth_phenotypes(X, 96)[:, 0]
+    ref = oracle.brr_gibbs(X, y, n_iter=6, n_burnin=2, thin=1, seed=13)
+    b_hat, y_pred, var = gbm.brr_arrays(X, y, n_iter=6, n_burnin=2, thin=1, seed=13)
+    rel = lambda a, b: np.abs(a - b).max() / np.abs(b).max()
+    assert rel(b_hat, ref["b_hat"]) < 1e-9 and rel(y_pred, ref["y_pred"]) < 1e-9
+
+
+@pytest.mark.gpu
 def test_gpu_brr_posterior_mean_close_to_gblup():
     """With σ²_b, σ²_e near their posterior the BRR posterior mean of Xb is the ridge/GBLUP BLUP:
     compare GEBVs with GBLUP at λ = σ²_e/σ²_b (posterior means) — distributional, not exact."""
