@@ -25,9 +25,9 @@ constexpr int NB = kCholNB;  // 64
 constexpr int MAXRHS = 63;
 
 int launch_chol_update(double* G, int64_t ldg, int64_t k0, int64_t nb, int64_t gdim, double* Ld, double* Dinv,
-                       int32_t* info, int64_t next_k0, int32_t* fflags, bool* fused, hipStream_t s);
+                       int32_t* info, int64_t next_k0, hipStream_t s);
 int launch_chol_row_update(double* G, int64_t ldg, int64_t k0, int kch, int64_t gdim, double* Ld, double* Dinv,
-                           int32_t* info, int32_t* fflags, hipStream_t s);
+                           int32_t* info, hipStream_t s);
 int64_t chol_small_lim();
 void chol_refresh_tuning();
 
@@ -36,11 +36,9 @@ __global__ void __launch_bounds__(256) prepare_v_kernel(double* __restrict__ G, 
                                                         int64_t npad, int64_t gdim, double inv_q,
                                                         const int64_t* __restrict__ q_dev, double lambda,
                                                         const double* __restrict__ Y, int64_t ldy, int64_t nrhs,
-                                                        int32_t* __restrict__ info, int32_t* __restrict__ fflags) {
+                                                        int32_t* __restrict__ info) {
   const int64_t i = blockIdx.x;  // row
   if (i == 0 && threadIdx.x == 0) *info = 0;
-  if (i == 0)  // factor-published flags of the fused panels (one per 64-block)
-    for (int64_t b = threadIdx.x; b < npad / NB; b += 256) fflags[b] = 0;
   if (q_dev) inv_q = 1.0 / (double)(*q_dev);
   double* row = G + i * ld;
   const int64_t jbeg = (i / NB) * NB;  // from the start of the diagonal block
@@ -195,119 +193,7 @@ __global__ void __launch_bounds__(256) gblup_terms_kernel(const double* __restri
   }
 }
 
-// ---- back substitution Lᵀ a = w (L = Uᵀ in the lower triangle) over super-blocks --------------
-// Per super-block [s0, s0 + 64*nsub), last to first, two launches:
-//   back_diag_kernel (1 workgroup): solve the super-block — diagonal 64-blocks from Ld (stored as
-//     U_bb, read transposed), in-super-block couplings w_i -= Σ_r L[s0+64sb+r][i] a_r as
-//     column-parallel GEMVs over coalesced rows of L; writes a.
-//   back_update_kernel (s0/64 workgroups): w_i -= Σ_r L[s0 + r][i] a_r for i < s0, a 64-column
-//     slice per workgroup, rows split over the 4 waves and reduced through LDS.
-constexpr int SB = 4;  // 64-blocks per super-block
-constexpr int RC = 4;  // right-hand sides per chunk
-__global__ void __launch_bounds__(256) back_diag_kernel(const double* __restrict__ G, int64_t ld,
-                                                        const double* __restrict__ Linv, int64_t s0, int nsub,
-                                                        const double* __restrict__ W, double* __restrict__ A,
-                                                        int64_t lda, int64_t nrhs) {
-  __shared__ double Ui[SB][NB][NB + 1];  // Ui[sb][i][j] = (U_bb⁻¹)[i][j], b = s0/64 + sb
-  __shared__ double wl[RC][SB * NB];
-  __shared__ double part[4][RC][NB];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int len = nsub * NB;
-  // stage the inverses with every load in flight before the first LDS store (latency-bound kernel)
-  for (int base = 0; base < len * NB; base += 16 * 512) {
-    double2 v[16];
-#pragma unroll
-    for (int u = 0; u < 16; u++) {
-      const int e = base + u * 512 + tid * 2;
-      v[u] = e < len * NB ? *reinterpret_cast<const double2*>(Linv + s0 * NB + e) : make_double2(0.0, 0.0);
-    }
-#pragma unroll
-    for (int u = 0; u < 16; u++) {
-      const int e = base + u * 512 + tid * 2;
-      if (e < len * NB) {
-        const int rr = e / NB, cc = e % NB;
-        Ui[rr / NB][rr % NB][cc] = v[u].x;
-        Ui[rr / NB][rr % NB][cc + 1] = v[u].y;
-      }
-    }
-  }
-  for (int64_t t0 = 0; t0 < nrhs; t0 += RC) {
-    const int tc = (int)(nrhs - t0 < RC ? nrhs - t0 : RC);
-    for (int e = tid; e < tc * len; e += 256) wl[e / len][e % len] = W[(t0 + e / len) * lda + s0 + e % len];
-    __syncthreads();
-    for (int sb = nsub - 1; sb >= 0; sb--) {
-      // couplings of the earlier rows of the super-block to this block (column tid): loads first,
-      // they do not depend on a_b
-      const bool couple = sb > 0 && tid < sb * NB;
-      double l[NB];
-      if (couple) {
-        const double* lp = G + (s0 + sb * NB) * ld + s0 + tid;
-#pragma unroll
-        for (int u = 0; u < NB; u++) l[u] = lp[(int64_t)u * ld];
-      }
-      // a_b = U_bb⁻¹ w_b (Lᵀ = U): a 64x64 GEMV, the j range split over the 4 waves
-      for (int t = 0; t < tc; t++) {
-        double acc = 0.0;
-#pragma unroll
-        for (int j = 0; j < 16; j++) acc += Ui[sb][lane][wave * 16 + j] * wl[t][sb * NB + wave * 16 + j];
-        part[wave][t][lane] = acc;
-      }
-      __syncthreads();
-      if (wave == 0)
-        for (int t = 0; t < tc; t++)
-          wl[t][sb * NB + lane] = ((part[0][t][lane] + part[1][t][lane]) + part[2][t][lane]) + part[3][t][lane];
-      __syncthreads();
-      if (couple) {
-        double acc[RC] = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-        for (int u = 0; u < NB; u++)
-#pragma unroll
-          for (int t = 0; t < RC; t++)
-            if (t < tc) acc[t] += l[u] * wl[t][sb * NB + u];
-        for (int t = 0; t < tc; t++) wl[t][tid] -= acc[t];
-      }
-      __syncthreads();
-    }
-    for (int e = tid; e < tc * len; e += 256) A[(t0 + e / len) * lda + s0 + e % len] = wl[e / len][e % len];
-    __syncthreads();
-  }
-}
-
-__global__ void __launch_bounds__(256) back_update_kernel(const double* __restrict__ G, int64_t ld, int64_t s0,
-                                                          int len, double* __restrict__ W,
-                                                          const double* __restrict__ A, int64_t lda, int64_t nrhs) {
-  __shared__ double part[4][RC][64];
-  __shared__ double as[RC][SB * NB];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int64_t i = (int64_t)blockIdx.x * 64 + lane;
-  const int rows_per_wave = len / 4;
-  for (int64_t t0 = 0; t0 < nrhs; t0 += RC) {
-    const int tc = (int)(nrhs - t0 < RC ? nrhs - t0 : RC);
-    for (int e = tid; e < tc * len; e += 256) as[e / len][e % len] = A[(t0 + e / len) * lda + s0 + e % len];
-    __syncthreads();
-    double acc[RC] = {0.0, 0.0, 0.0, 0.0};
-    if (i < s0) {
-      const double* lp = G + (s0 + wave * rows_per_wave) * ld + i;
-      for (int r = 0; r < rows_per_wave; r += 16) {
-        double l[16];
-#pragma unroll
-        for (int u = 0; u < 16; u++) l[u] = lp[(int64_t)(r + u) * ld];
-#pragma unroll
-        for (int u = 0; u < 16; u++)
-#pragma unroll
-          for (int t = 0; t < RC; t++)
-            if (t < tc) acc[t] += l[u] * as[t][wave * rows_per_wave + r + u];
-      }
-    }
-#pragma unroll
-    for (int t = 0; t < RC; t++) part[wave][t][lane] = acc[t];
-    __syncthreads();
-    if (wave == 0 && i < s0)
-      for (int t = 0; t < tc; t++)
-        W[(t0 + t) * lda + i] -= ((part[0][t][lane] + part[1][t][lane]) + part[2][t][lane]) + part[3][t][lane];
-    __syncthreads();
-  }
-}
+constexpr int RC = 4;  // right-hand sides per chunk of the back substitution
 
 // ---- sync-free blocked back substitution: one workgroup per 64-block, flags between them ------
 // U a = w with U's off-diagonal blocks read from the lower copy L = Uᵀ (coalesced along the rows
@@ -408,8 +294,8 @@ extern "C" int64_t gbm_dev_npad(int64_t n) { return npad_of(n); }
 extern "C" int64_t gbm_dev_gdim(int64_t n) { return gdim_of(n); }
 // scratch: the factored 64x64 diagonal blocks (npad x 64), their inverses (npad x 64) and the
 // inverses of their 16x16 diagonal sub-blocks (npad x 16)
-// + two int32 flags per 64-block (back_solve_kernel; factor published for the fused panels)
-static int64_t solve_ws_doubles(int64_t n) { return npad_of(n) * (2 * NB + 16) + npad_of(n) / NB + 1; }
+// + one int32 flag per 64-block (back_solve_kernel)
+static int64_t solve_ws_doubles(int64_t n) { return npad_of(n) * (2 * NB + 16) + npad_of(n) / NB / 2 + 1; }
 extern "C" int64_t gbm_dev_solve_workspace(int64_t n, int64_t nrhs) {
   (void)nrhs;
   return solve_ws_doubles(n) * (int64_t)sizeof(double);
@@ -432,17 +318,11 @@ extern "C" int gbm_dev_gblup_solve(double* G, int64_t ldg, int64_t n, double inv
   double* Dinv = Linv + npad * NB;
   hipStream_t s = (hipStream_t)stream;
   int32_t* flags = reinterpret_cast<int32_t*>(Dinv + npad * 16);
-  int32_t* fflags = flags + npad / NB;
-  prepare_v_kernel<<<(unsigned)gdim, 256, 0, s>>>(G, ldg, n, npad, gdim, inv_q, q_dev, lambda, Y, ldy, nrhs, info,
-                                                  fflags);
+  prepare_v_kernel<<<(unsigned)gdim, 256, 0, s>>>(G, ldg, n, npad, gdim, inv_q, q_dev, lambda, Y, ldy, nrhs, info);
   GBM_LAUNCH_CHECK();
   const int64_t nb = npad / NB;
   factor_first_kernel<<<1, 256, 0, s>>>(G, ldg, Ld, Dinv, info);
   GBM_LAUNCH_CHECK();
-  static const bool pair_panels = [] {
-    const char* e = getenv("GBM_CHOL_PAIRS");
-    return !e || atoi(e) != 0;
-  }();
   auto panel = [&](int64_t k0) {
     const int64_t chunks = (gdim - k0) / NB - 1;  // column chunks right of the diagonal block
     chol_panel_kernel<<<(unsigned)chunks, 256, 0, s>>>(G, ldg, k0, Ld, Dinv);
@@ -464,45 +344,34 @@ extern "C" int gbm_dev_gblup_solve(double* G, int64_t ldg, int64_t n, double inv
     const char* e = getenv("GBM_CHOL_G16_LIM");
     return e ? (int64_t)atoll(e) : (int64_t)16384;
   }();
-  // GBM_CHOL_FUSE=1: the small updates also solve the next panel (first tile row, after the
-  // first workgroup publishes the factored block). Correct, but measured slower than separate
-  // panel launches (33.5 vs 20.3 + 8.9 µs per step at C2: the publish + wait + reload costs more
-  // than a launch), so off by default.
-  static const bool fuse = [] {
-    const char* e = getenv("GBM_CHOL_FUSE");
-    return e && atoi(e) != 0;
-  }();
-  int32_t* ff = fuse ? fflags : nullptr;
-  bool panel_done = false;  // the previous update already solved this panel (fused)
   for (int64_t kb = 0; kb < nb;) {
     const int64_t k0 = kb * NB;
-    if (!panel_done && !panel(k0)) return fail(GBM_E_HIP, "chol_panel_kernel launch failed");
+    if (!panel(k0)) return fail(GBM_E_HIP, "chol_panel_kernel launch failed");
     int rc;
     // groups of g panels share one pass over the trailing matrix (HBM/MALL-bound at K = 64,
     // balanced at K = 128, MFMA-bound at K = 256): the rows of panels 2..g of the group are
     // brought up to date with the group's earlier panels (row update with K = 64 j), factored and
     // solved one after the other, then one K = 64 g trailing update
     int g = 1;
-    if (pair_panels && group16_lim >= 0 && kb + 16 < nb && gdim - (k0 + 16 * NB) > group16_lim)
+    if (group16_lim >= 0 && kb + 16 < nb && gdim - (k0 + 16 * NB) > group16_lim)
       g = 16;
-    else if (pair_panels && group8_lim >= 0 && kb + 8 < nb && gdim - (k0 + 8 * NB) > group8_lim)
+    else if (group8_lim >= 0 && kb + 8 < nb && gdim - (k0 + 8 * NB) > group8_lim)
       g = 8;
-    else if (pair_panels && group4_lim >= 0 && kb + 4 < nb && gdim - (k0 + 4 * NB) > group4_lim)
+    else if (group4_lim >= 0 && kb + 4 < nb && gdim - (k0 + 4 * NB) > group4_lim)
       g = 4;
-    else if (pair_panels && kb + 2 < nb && gdim - (k0 + 2 * NB) > chol_small_lim())
+    else if (kb + 2 < nb && gdim - (k0 + 2 * NB) > chol_small_lim())
       g = 2;
     if (g > 1) {
       for (int j = 1; j < g; j++) {
-        rc = launch_chol_row_update(G, ldg, k0, j, gdim, Ld, Dinv, info, ff, s);
+        rc = launch_chol_row_update(G, ldg, k0, j, gdim, Ld, Dinv, info, s);
         if (rc != GBM_OK) return rc;
-        if (!ff && !panel(k0 + j * NB)) return fail(GBM_E_HIP, "chol_panel_kernel launch failed");
+        if (!panel(k0 + j * NB)) return fail(GBM_E_HIP, "chol_panel_kernel launch failed");
       }
-      rc = launch_chol_update(G, ldg, k0, g * NB, gdim, Ld, Dinv, info, k0 + g * NB, ff, &panel_done, s);
+      rc = launch_chol_update(G, ldg, k0, g * NB, gdim, Ld, Dinv, info, k0 + g * NB, s);
       kb += g;
     } else {
-      // trailing update; its first workgroup also factors the next diagonal block (and, fused,
-      // the first tile row solves the next panel)
-      rc = launch_chol_update(G, ldg, k0, NB, gdim, Ld, Dinv, info, kb + 1 < nb ? k0 + NB : -1, ff, &panel_done, s);
+      // trailing update; its first workgroup also factors the next diagonal block
+      rc = launch_chol_update(G, ldg, k0, NB, gdim, Ld, Dinv, info, kb + 1 < nb ? k0 + NB : -1, s);
       kb += 1;
     }
     if (rc != GBM_OK) return rc;
@@ -513,25 +382,8 @@ extern "C" int gbm_dev_gblup_solve(double* G, int64_t ldg, int64_t n, double inv
   // the gebv buffer doubles as the w scratch: gebv_kernel (last) reads only Y and A
   gls_mu_kernel<<<dim3(gx, (unsigned)nrhs), 256, 0, s>>>(G, ldg, npad, nrhs, gebv, lda, mu, flags);
   GBM_LAUNCH_CHECK();
-  static const bool super_blocks = [] {  // GBM_BACK_SOLVE=super: the two-kernel super-block chain
-    const char* e = getenv("GBM_BACK_SOLVE");
-    return e && std::string(e) == "super";
-  }();
-  if (!super_blocks) {
-    back_solve_kernel<<<(unsigned)nb, 256, 0, s>>>(G, ldg, Linv, nb, gebv, A_out, lda, nrhs, flags, info);
-    GBM_LAUNCH_CHECK();
-  }
-  for (int64_t end_blk = super_blocks ? nb : 0; end_blk > 0;) {
-    const int nsub = (int)(end_blk >= SB ? SB : end_blk);
-    const int64_t s0 = (end_blk - nsub) * NB;
-    back_diag_kernel<<<1, 256, 0, s>>>(G, ldg, Linv, s0, nsub, gebv, A_out, lda, nrhs);
-    GBM_LAUNCH_CHECK();
-    if (s0 > 0) {
-      back_update_kernel<<<(unsigned)(s0 / 64), 256, 0, s>>>(G, ldg, s0, nsub * NB, gebv, A_out, lda, nrhs);
-      GBM_LAUNCH_CHECK();
-    }
-    end_blk -= nsub;
-  }
+  back_solve_kernel<<<(unsigned)nb, 256, 0, s>>>(G, ldg, Linv, nb, gebv, A_out, lda, nrhs, flags, info);
+  GBM_LAUNCH_CHECK();
   gebv_kernel<<<dim3(gx, (unsigned)nrhs), 256, 0, s>>>(Y, ldy, n, A_out, gebv, lda, mu, lambda);
   GBM_LAUNCH_CHECK();
   return GBM_OK;

@@ -152,8 +152,6 @@ __device__ __forceinline__ int factor_diag_block(double* Us, double* rinv, int t
 // Store a factored block: Ld_blk (64x64 row-major, upper, zeros below) and the inverses of its
 // four 16x16 diagonal sub-blocks Dinv_blk[w][i][j] = (D_w⁻¹)[i][j] (upper). Wave w computes D_w⁻¹
 // column by column (lane j < 16), the dot products split over 2 partial sums.
-// AGENT: agent-scope stores, for workgroups of the same launch that read the block (fused panels).
-template <bool AGENT = false>
 __device__ __forceinline__ void store_factor(const double* Us, const double* rinv, double* Ld_blk,
                                              double* Dinv_blk, int tid) {
   const int lane = tid & 63, wave = tid >> 6;
@@ -161,14 +159,8 @@ __device__ __forceinline__ void store_factor(const double* Us, const double* rin
     const int row = tid >> 2, quarter = tid & 3;
     double* dst = Ld_blk + row * CNB + quarter * 16;
 #pragma unroll
-    for (int e = 0; e < 16; e += 2) {
-      if constexpr (AGENT) {
-        st_agent(dst + e, Us[row * PS + quarter * 16 + e]);
-        st_agent(dst + e + 1, Us[row * PS + quarter * 16 + e + 1]);
-      } else {
-        *reinterpret_cast<double2*>(dst + e) = *reinterpret_cast<const double2*>(&Us[row * PS + quarter * 16 + e]);
-      }
-    }
+    for (int e = 0; e < 16; e += 2)
+      *reinterpret_cast<double2*>(dst + e) = *reinterpret_cast<const double2*>(&Us[row * PS + quarter * 16 + e]);
   }
   const int o = wave * 16;
   const int j = lane & 15;
@@ -185,12 +177,7 @@ __device__ __forceinline__ void store_factor(const double* Us, const double* rin
   }
   if (lane < 16) {
 #pragma unroll
-    for (int i = 0; i < 16; i++) {
-      if constexpr (AGENT)
-        st_agent(&Dinv_blk[wave * 256 + i * 16 + j], x[i]);
-      else
-        Dinv_blk[wave * 256 + i * 16 + j] = x[i];
-    }
+    for (int i = 0; i < 16; i++) Dinv_blk[wave * 256 + i * 16 + j] = x[i];
   }
 }
 

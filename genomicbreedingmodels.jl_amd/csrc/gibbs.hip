@@ -312,13 +312,8 @@ __global__ void __launch_bounds__(256) brr_step_kernel(const T* __restrict__ Xt,
     const double xi = on ? brr_normal(st->seed, 4 * (uint64_t)st->it, (uint64_t)j) : 0.0;
     const double beta = on ? xx * bo * alpha + sqrt(cinv) * xi : 0.0;
     double bfin = bo;
-#ifdef GBM_DEBUG_BRR_NOSEQ  // timing experiment only
-    constexpr int NSEQ = 0;
-#else
-    constexpr int NSEQ = BB;
-#endif
 #pragma unroll
-    for (int s2 = 0; s2 < NSEQ; s2++) {
+    for (int s2 = 0; s2 < BB; s2++) {
       const double bn = fma(d, alpha, beta);
       bfin = lane == s2 ? bn : bfin;
       union {
@@ -351,11 +346,7 @@ __global__ void __launch_bounds__(256) brr_step_kernel(const T* __restrict__ Xt,
     ei = e_old + (acc0 + acc1);
     e[i] = ei;
   }
-#ifdef GBM_DEBUG_BRR_NOPART  // timing experiment only
-  if (false) {
-#else
   if (more) {
-#endif
     es[tid] = ei;
     __syncthreads();  // also completes the global_load_lds of Xn
     // partial[c][k] = Σ_u Xn[k][w*64 + u] es[w*64 + u]: lane k = marker, wave w = quarter

@@ -1,17 +1,25 @@
 // GRM build: G = Σ_j z_j z_jᵀ over the standardised locus rows of Zt — an fp64 SYRK on the
 // CDNA4 matrix cores (v_mfma_f64_16x16x4_f64), the dominant cost of the path.
+// Also the trailing-update kernels of the upper Cholesky (chol.hip), which share the tile core.
 //
-// Geometry (DESIGN.md "GRM kernel"):
+// Geometry:
 //   * workgroup tile 128 x 128 of G (upper-triangular tiles only: nt(nt+1)/2 tiles),
 //     256 threads = 4 waves in 2 x 2, each wave a 64 x 64 sub-tile = 4 x 4 MFMA 16x16 tiles
 //     (16 f64x4 accumulators per lane);
 //   * K (= loci) consumed in stages of 16 rows; each stage is 2 x 16 rows x 1 KB of Zt brought
 //     straight into LDS by global_load_lds_dwordx4 (one wave-instruction = one 1-KB locus row
-//     segment), double-buffered; LDS rows padded to 1152 B so the two 16-lane halves of a
-//     ds_read_b64 fragment load land on disjoint bank halves;
-//   * stream-K over loci: the (tile, stage) units are cut into equal contiguous ranges, one per
-//     resident workgroup slot (256 CUs x 2), so there is no tail round; partial tiles go to
-//     workspace slabs that a second kernel sums in a fixed order (deterministic, no float atomics).
+//     segment), double-buffered; LDS row pitch 1040 B (≡ 4 dwords mod 64 banks), so the
+//     ds_read_b128 fragment reads are conflict-free;
+//   * work units (loci range, tile): every tile is cut into the same guided loci ranges (plan());
+//     persistent workgroups (one per resident slot) take units from per-XCD queues; partial
+//     tiles go to workspace slabs summed in a fixed order (deterministic, no float atomics), or,
+//     for large n, are accumulated in order straight into G (carry mode).
+//
+// Tuning knobs are read from the environment at every plan (grm_tuning()), so a test can force
+// a mode per call: GBM_GRM_CARRY (0/1: slabs / in-order carry; unset: automatic),
+// GBM_GRM_PERSIST=0 (hardware-dispatched workgroups), GBM_GRM_EDGE=0 (no ragged-edge kernel),
+// GBM_GRM_EDGE_CONCURRENT=0 (edge kernel after the tiles), GBM_GRM_SPLIT=w0,w1,... (relative
+// loci-range sizes instead of the planner's).
 #include <algorithm>
 #include <atomic>
 #include <cmath>
@@ -28,21 +36,8 @@
 namespace gbm {
 
 constexpr int BT = 128;            // tile edge
-#ifndef GBM_BK
-#define GBM_BK 16
-#endif
-#ifndef GBM_WPS
-#define GBM_WPS 2
-#endif
-#ifndef GBM_PRIO
-// s_setprio(1) around each k-step's MFMA group (2, the default): the wave in its MFMA group wins
-// issue arbitration over its SIMD partner's staging and LDS instructions. GRM at C2 on one box:
-// 18.87 ms (0) -> 18.68 ms (2); 1 (higher static priority for the second-dispatched workgroup
-// of each CU) 18.84 ms; 3 (priority around the staging instead) 18.73 ms
-#define GBM_PRIO 2
-#endif
-constexpr int BK = GBM_BK;         // loci per stage
-constexpr int WPS = GBM_WPS;       // target waves per SIMD (= resident 256-thread workgroups per CU)
+constexpr int BK = 16;             // loci per stage
+constexpr int WPS = 2;             // waves per SIMD (= resident 256-thread workgroups per CU)
 constexpr int LROW = BT + 2;       // LDS row pitch in doubles (1040 B ≡ 4 dwords mod 64 banks)
 constexpr int STAGE = 2 * BK * LROW;  // doubles per stage (A rows then B rows)
 
@@ -56,17 +51,6 @@ __device__ __forceinline__ void tile_of(int64_t t, int64_t& ti, int64_t& tj) {
 }
 
 enum SyrkMode { kSub = 0, kSplit = 1, kPersist = 2 };
-
-#ifdef GBM_DEBUG_WGTIME  // timing experiment only: per-workgroup start/end clocks + hardware id
-__device__ unsigned long long g_wgtime[3 * 16384];
-#endif
-#ifdef GBM_DEBUG_FACTIME  // timing experiment only: phases of the in-update diagonal factor
-__device__ unsigned long long g_factime[4 * 1024];
-__device__ unsigned long long g_factime_n;
-// fused panel tiles: fk0, entry, wait begin, wait end, end, (unused)
-__device__ unsigned long long g_paneltime[6 * 16384];
-__device__ unsigned long long g_paneltime_n;
-#endif
 
 // acc[m][q] += (NEG ? −1 : 1) Σ_k U[k][i0 + ·] U[k][j0 + ·] over the stages [kstep0, kstep0 + nsteps)
 // (BK loci each) of one BT x BT tile. Operands are staged by global_load_lds into the two LDS
@@ -84,20 +68,10 @@ __device__ __forceinline__ void tile_pass(const double* __restrict__ U, int64_t 
     const int64_t k = kstep * BK + r;
     double* la = base + r * LROW;
     double* lb = base + (BK + r) * LROW;
-#ifdef GBM_DEBUG_NOKCHECK  // timing experiment only: no ragged-K guard (reads past K)
-    if (true) {
-#else
     if (k < K) {
-#endif
-#ifdef GBM_DEBUG_SAMEROWS  // timing experiment only: operands stay L2-resident (wrong results)
-      const double* src = U + (k & 63) * ldu;
-#else
       const double* src = U + k * ldu;
-#endif
       __builtin_amdgcn_global_load_lds((const void*)(src + i0 + lane * 2), (void*)la, 16, 0, 0);
-#ifndef GBM_DEBUG_AONLY  // timing experiment only: B operand never staged (wrong results)
       if (!diag) __builtin_amdgcn_global_load_lds((const void*)(src + j0 + lane * 2), (void*)lb, 16, 0, 0);
-#endif
     } else {
       *reinterpret_cast<double2*>(la + lane * 2) = make_double2(0.0, 0.0);
       if (!diag) *reinterpret_cast<double2*>(lb + lane * 2) = make_double2(0.0, 0.0);
@@ -115,18 +89,10 @@ __device__ __forceinline__ void tile_pass(const double* __restrict__ U, int64_t 
     const int buf = (int)(st & 1);
     // the next stage's rows go out first, all together (issuing them one per k-step between
     // the MFMA groups measured 3 % slower)
-#ifndef GBM_DEBUG_NOSTAGE  // timing experiment only: operands never refreshed (wrong results)
     if (st + 1 < nsteps) {
-#if GBM_PRIO == 3
-      __builtin_amdgcn_s_setprio(1);
-#endif
 #pragma unroll
       for (int rr = 0; rr < BK / 4; rr++) stage_row(kstep0 + st + 1, buf ^ 1, rr);
-#if GBM_PRIO == 3
-      __builtin_amdgcn_s_setprio(0);
-#endif
     }
-#endif
     const double* A = lds + buf * STAGE;
     const double* B = diag ? A : A + BK * LROW;
 #pragma unroll
@@ -146,124 +112,18 @@ __device__ __forceinline__ void tile_pass(const double* __restrict__ U, int64_t 
 #pragma unroll
           for (int m = 0; m < 4; m++) af[m] = -af[m];
         }
-#if GBM_PRIO == 2
+        // the wave in its MFMA group wins issue arbitration over its SIMD partner's staging and
+        // LDS instructions (GRM at C2 on one box: 18.87 -> 18.68 ms)
         __builtin_amdgcn_s_setprio(1);
-#endif
 #pragma unroll
         for (int m = 0; m < 4; m++)
 #pragma unroll
           for (int q = 0; q < 4; q++)
             acc[m][q] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[m], bf[q], acc[m][q], 0, 0, 0);
-#if GBM_PRIO == 2
         __builtin_amdgcn_s_setprio(0);
-#endif
       }
     }
-#ifdef GBM_DEBUG_NOBARRIER  // timing experiment only: racy (wrong results)
-    __builtin_amdgcn_s_waitcnt(0);
-#elif defined(GBM_DEBUG_NOVMWAIT)  // timing experiment only: barrier without waiting for the loads
-    __builtin_amdgcn_s_waitcnt(0xC07F);
-    __builtin_amdgcn_s_barrier();
-#else
     __syncthreads();
-#endif
-  }
-  __syncthreads();
-}
-
-// s_waitcnt immediate for vmcnt(v) lgkmcnt(0) (expcnt untouched): vmcnt bits [3:0] + [15:14]
-constexpr int waitcnt_vm_lgkm0(int v) { return 0x70 | (v & 0xF) | ((v >> 4) << 14); }
-
-#ifndef GBM_DEEP_BK
-// 0: the GRM uses tile_pass (BK = 16, 2 buffers). Measured at C2: (8, 4) 20.6 ms, (12, 3)
-// 20.9 ms vs 19.6 ms — deeper prefetch does not pay for the extra barriers
-#define GBM_DEEP_BK 0
-#endif
-#ifndef GBM_DEEP_NBUF
-#define GBM_DEEP_NBUF 3
-#endif
-constexpr int DBK = GBM_DEEP_BK > 0 ? GBM_DEEP_BK : 4;
-constexpr int DNBUF = GBM_DEEP_NBUF;
-constexpr int DSTAGE = 2 * DBK * LROW;
-
-// GRM variant of tile_pass with DNBUF LDS stages of DBK loci: the loads of stage st + DNBUF - 1
-// are issued while stage st is computed, and the per-stage wait keeps the newest DNBUF - 2 stages'
-// loads in flight (s_waitcnt vmcnt(n), one barrier per stage). The DMA is inline asm so that the
-// compiler does not order every LDS read after it (see grm_syrk8_kernel).
-// Loci [kb, ke) in stages of DBK rows (rows past ke are zero-filled in LDS).
-__device__ __forceinline__ void tile_pass_deep(const double* __restrict__ U, int64_t ldu, int64_t kb, int64_t ke,
-                                               int64_t i0, int64_t j0, bool diag, bool active, double* lds,
-                                               d4 (&acc)[4][4], int wave, int lane) {
-  const int wm = wave >> 1, wn = wave & 1;
-  constexpr int RPW = DBK / 4;  // locus rows staged per wave
-  const int64_t nsteps = ke > kb ? (ke - kb + DBK - 1) / DBK : 0;
-  const int64_t K = ke;
-  auto stage = [&](int64_t sidx, int buf) {
-    double* base = lds + buf * DSTAGE;
-#pragma unroll
-    for (int rr = 0; rr < RPW; rr++) {
-      const int r = wave * RPW + rr;
-      const int64_t k = kb + sidx * DBK + r;
-      double* la = base + r * LROW;
-      double* lb = base + (DBK + r) * LROW;
-      if (k < K) {
-        const double* src = U + k * ldu;
-        const unsigned ma = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)la);
-        asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off"
-                     : : "s"(ma), "v"(src + i0 + lane * 2) : "memory");
-        if (!diag) {
-          const unsigned mb = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)lb);
-          asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off"
-                       : : "s"(mb), "v"(src + j0 + lane * 2) : "memory");
-        }
-      } else {
-        *reinterpret_cast<double2*>(la + lane * 2) = make_double2(0.0, 0.0);
-        if (!diag) *reinterpret_cast<double2*>(lb + lane * 2) = make_double2(0.0, 0.0);
-      }
-    }
-  };
-  const int frag_row = lane >> 4, frag_col = lane & 15;
-#pragma unroll
-  for (int q = 0; q < DNBUF - 1; q++)
-    if (q < nsteps) stage(q, q);
-  for (int64_t st = 0; st < nsteps; st++) {
-    // stage st complete and visible; stages st+1 .. st+DNBUF-2 may stay in flight unless one of
-    // them runs past ke (fewer loads issued: then wait for everything)
-    const int64_t ahead = (nsteps - 1 - st) < (DNBUF - 2) ? (nsteps - 1 - st) : (DNBUF - 2);
-    const bool full = kb + (st + ahead + 1) * DBK <= K;
-    if (ahead == DNBUF - 2 && full) {
-      if (diag) __builtin_amdgcn_s_waitcnt(waitcnt_vm_lgkm0((DNBUF - 2) * RPW));
-      else __builtin_amdgcn_s_waitcnt(waitcnt_vm_lgkm0((DNBUF - 2) * RPW * 2));
-    } else {
-      __builtin_amdgcn_s_waitcnt(waitcnt_vm_lgkm0(0));
-    }
-    __builtin_amdgcn_s_barrier();
-    if (st + DNBUF - 1 < nsteps) stage(st + DNBUF - 1, (int)((st + DNBUF - 1) % DNBUF));
-    if (active) {
-      const double* A = lds + (int)(st % DNBUF) * DSTAGE;
-      const double* B = diag ? A : A + DBK * LROW;
-#pragma unroll
-      for (int ks = 0; ks < DBK / 4; ks++) {
-        const int kr = ks * 4 + frag_row;
-        const double2 a01 = *reinterpret_cast<const double2*>(&A[kr * LROW + wm * 64 + 4 * frag_col]);
-        const double2 a23 = *reinterpret_cast<const double2*>(&A[kr * LROW + wm * 64 + 4 * frag_col + 2]);
-        const double2 b01 = *reinterpret_cast<const double2*>(&B[kr * LROW + wn * 64 + 4 * frag_col]);
-        const double2 b23 = *reinterpret_cast<const double2*>(&B[kr * LROW + wn * 64 + 4 * frag_col + 2]);
-        const double af[4] = {a01.x, a01.y, a23.x, a23.y};
-        const double bf[4] = {b01.x, b01.y, b23.x, b23.y};
-#if GBM_PRIO == 2
-        __builtin_amdgcn_s_setprio(1);
-#endif
-#pragma unroll
-        for (int m = 0; m < 4; m++)
-#pragma unroll
-          for (int q = 0; q < 4; q++)
-            acc[m][q] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[m], bf[q], acc[m][q], 0, 0, 0);
-#if GBM_PRIO == 2
-        __builtin_amdgcn_s_setprio(0);
-#endif
-      }
-    }
   }
   __syncthreads();
 }
@@ -381,14 +241,10 @@ syrk_kernel(const double* __restrict__ U, int64_t ldu, int64_t K, int64_t c0, in
             double* __restrict__ C, int64_t ldc, double* __restrict__ slab, int64_t ntiles, SliceBounds sb,
             double* __restrict__ Ld, double* __restrict__ Dinv, int32_t* __restrict__ info, int64_t fk0) {
   // 2 stages (72 KB at BK = 16); kSub's first workgroup reuses it for the 64x64 factor image
-  constexpr int LDS_A = (2 * STAGE > CNB * PS + CNB + 16) ? 2 * STAGE : CNB * PS + CNB + 16;
-  constexpr int LDS_DOUBLES = (GBM_DEEP_BK > 0 && DNBUF * DSTAGE > LDS_A) ? DNBUF * DSTAGE : LDS_A;
+  constexpr int LDS_DOUBLES = (2 * STAGE > CNB * PS + CNB + 16) ? 2 * STAGE : CNB * PS + CNB + 16;
   __shared__ __attribute__((aligned(16))) double lds[LDS_DOUBLES];
 
   const int64_t wg = blockIdx.x;
-#ifdef GBM_DEBUG_WGTIME
-  const unsigned long long dbg_t0 = wall_clock64();
-#endif
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wm = wave >> 1, wn = wave & 1;
@@ -415,10 +271,7 @@ syrk_kernel(const double* __restrict__ U, int64_t ldu, int64_t K, int64_t c0, in
       for (int b = 0; b < 4; b++) acc[a][b] = (d4){0.0, 0.0, 0.0, 0.0};
     const int64_t ks0 = sb.b[sl];
     const int64_t ks1 = sb.b[sl + 1] < nst ? sb.b[sl + 1] : nst;
-    if constexpr (GBM_DEEP_BK > 0)
-      tile_pass_deep(U, ldu, ks0 * BK, (ks1 * BK < K ? ks1 * BK : K), i0, j0, diag, active, lds, acc, wave, lane);
-    else
-      tile_pass<false>(U, ldu, K, i0, j0, diag, active, ks0, ks1 > ks0 ? ks1 - ks0 : 0, lds, acc, wave, lane);
+    tile_pass<false>(U, ldu, K, i0, j0, diag, active, ks0, ks1 > ks0 ? ks1 - ks0 : 0, lds, acc, wave, lane);
     if (MODE == kSplit && sb.carry && sb.n > 1) {  // (not compiled into the persistent kernel)
       // in-order carry: G tile = ((P_0 + P_1) + P_2) + ..., the same order (and rounding) as the
       // slab reduce. Range sl's predecessor was dispatched 1+ rounds earlier (lower workgroup
@@ -488,11 +341,6 @@ syrk_kernel(const double* __restrict__ U, int64_t ldu, int64_t K, int64_t c0, in
       // to the last unit, so the XCDs finish together (with hardware dispatch every XCD ran a
       // fixed 1/8 of the workgroups and they ended up to 1 ms apart).
       __shared__ int64_t s_unit;
-#if GBM_PRIO == 1
-      // the second-dispatched workgroup of each CU gets the higher wave priority (arbitration
-      // otherwise favours the older wave of each SIMD pair)
-      if (wg >= (int64_t)gridDim.x / 2) __builtin_amdgcn_s_setprio(1);
-#endif
       int32_t* ctr = info;  // 8 queue counters, zeroed before the launch
       const int xcc = (int)(__builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (31 << 11)) & 7);
       const int64_t per = T8 >> 3;
@@ -511,21 +359,7 @@ syrk_kernel(const double* __restrict__ U, int64_t ldu, int64_t K, int64_t c0, in
           continue;
         }
         const int sl = (int)(u / nq);
-#ifdef GBM_DEBUG_WGTIME
-        const unsigned long long ut0 = wall_clock64();
-        const unsigned long long uc0 = __builtin_amdgcn_s_memtime();
-#endif
         run_unit(sl, qt0 + (u - (int64_t)sl * nq));
-#ifdef GBM_DEBUG_WGTIME
-        const int64_t rec = (int64_t)sl * ntiles + qt0 + (u - (int64_t)sl * nq);
-        if (threadIdx.x == 0 && rec < 16384) {  // per unit: start, end, (wg << 8 | xcc), shader cycles
-          g_wgtime[3 * rec] = ut0;
-          g_wgtime[3 * rec + 1] = wall_clock64();
-          const unsigned hwid = __builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11));
-          g_wgtime[3 * rec + 2] = (unsigned long long)xcc | ((unsigned long long)((hwid >> 8) & 0xFF) << 8) |
-                                  ((unsigned long long)wg << 16) | ((__builtin_amdgcn_s_memtime() - uc0) << 28);
-        }
-#endif
       }
       return;
     } else {
@@ -537,14 +371,6 @@ syrk_kernel(const double* __restrict__ U, int64_t ldu, int64_t K, int64_t c0, in
       if (t >= ntiles) return;
       run_unit(sl, t);
     }
-#ifdef GBM_DEBUG_WGTIME
-    if (threadIdx.x == 0 && wg < 16384) {
-      g_wgtime[3 * wg] = dbg_t0;
-      g_wgtime[3 * wg + 1] = wall_clock64();
-      g_wgtime[3 * wg + 2] = (unsigned long long)__builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11)) |
-                             ((unsigned long long)__builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (31 << 11)) << 32);
-    }
-#endif
     return;
   } else {
     int64_t ti, tj;
@@ -625,179 +451,6 @@ __global__ void __launch_bounds__(256) grm_slab_reduce_kernel(const double* __re
   }
 }
 
-// ---- GRM SYRK, wide variant: 256x128 tiles, 8 waves, 3-stage LDS pipeline ------------------
-// One 512-thread workgroup per CU (2 waves per SIMD, as the 128x128 kernel at 2 workgroups per
-// CU), tile rows 256 (A strip) x cols 128 (B strip): 25 % fewer staged bytes per flop, and the
-// 149 KB of LDS hold three stages, so the loads of stage st+2 are issued while stage st is
-// computed and the per-stage wait leaves stage st+1's loads in flight (s_waitcnt vmcnt(n), not
-// vmcnt(0)). Tiles: for tile column tj, row pairs ti2 = 0 .. tj/2 (the 128-row block 2 ti2 <= tj).
-constexpr int W8R = 256, W8C = 128;
-constexpr int LRA = W8R + 2;  // 2064 B: ≡ 16 B mod 256 B, conflict-free ds_read_b128 fragments
-constexpr int LRB = W8C + 2;  // 1040 B
-constexpr int ST8 = BK * (LRA + LRB);
-constexpr int NBUF8 = 3;
-
-__host__ __device__ inline int64_t tiles8_of_nt(int64_t nt) {
-  const int64_t M = nt / 2;
-  return (nt & 1) ? (M + 1) * (M + 1) : M * (M + 1);
-}
-__device__ __forceinline__ void tile8_of(int64_t t, int64_t& ti2, int64_t& tj) {
-  // columns 2m and 2m+1 hold m+1 tiles each; column 2m starts at m(m+1), column 2m+1 at (m+1)^2
-  int64_t m = (int64_t)((sqrt(4.0 * (double)t + 1.0) - 1.0) * 0.5);
-  while ((m + 1) * (m + 2) <= t) m++;
-  while (m * (m + 1) > t) m--;
-  if (t < (m + 1) * (m + 1)) {
-    tj = 2 * m;
-    ti2 = t - m * (m + 1);
-  } else {
-    tj = 2 * m + 1;
-    ti2 = t - (m + 1) * (m + 1);
-  }
-}
-
-__global__ void __launch_bounds__(512, 1)
-grm_syrk8_kernel(const double* __restrict__ U, int64_t ldu, int64_t K, int64_t lim, double* __restrict__ C,
-                 int64_t ldc, double* __restrict__ slab, int64_t ntiles, SliceBounds sb) {
-  __shared__ __attribute__((aligned(16))) double lds[NBUF8 * ST8];
-  const int64_t wg = blockIdx.x;
-  const int64_t T8 = (ntiles + 7) & ~(int64_t)7;  // XCD-aware order, as syrk_kernel<kSplit>
-  const int sl = (int)(wg / T8);
-  const int64_t u = wg - (int64_t)sl * T8;
-  const int64_t t = (u & 7) * (T8 >> 3) + (u >> 3);
-  if (t >= ntiles) return;
-  int64_t ti2, tj;
-  tile8_of(t, ti2, tj);
-  const int64_t i0 = ti2 * W8R, j0 = tj * W8C;
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int wm = wave >> 1, wn = wave & 1;
-  const int frag_row = lane >> 4, frag_col = lane & 15;
-  // B strip inside the A strip (tile columns 2 ti2 and 2 ti2 + 1): read B from A's LDS rows
-  const int bshare = (tj == 2 * ti2) ? 0 : (tj == 2 * ti2 + 1 ? W8C : -1);
-  const bool active = (i0 / 64 + wm <= j0 / 64 + wn) && (i0 + 64 * wm < lim) && (j0 + 64 * wn < lim);
-  const int64_t nst = (K + BK - 1) / BK;
-  const int64_t ks0 = sb.b[sl];
-  const int64_t ks1 = sb.b[sl + 1] < nst ? sb.b[sl + 1] : nst;
-  const int64_t nsteps = ks1 > ks0 ? ks1 - ks0 : 0;
-  // per stage: A = BK rows x 2 KB (2 wave instructions each), B = BK rows x 1 KB; spread over the
-  // 8 waves: instruction q = wave + 8 m; every wave issues the same count (vmcnt bookkeeping)
-  const int nA = 2 * BK, nq = bshare < 0 ? 3 * BK : 2 * BK;
-  const int nload = nq / 8;
-  auto stage = [&](int64_t kstep, int buf) {
-    double* base = lds + buf * ST8;
-#pragma unroll
-    for (int m = 0; m < 6; m++) {
-      if (m >= nload) break;
-      const int q = wave + 8 * m;
-      int r, h;
-      double* dst;
-      int64_t col;
-      if (q < nA) {
-        r = q >> 1;
-        h = q & 1;
-        dst = base + r * LRA + h * 128;
-        col = i0 + h * 128;
-      } else {
-        r = q - nA;
-        h = 0;
-        dst = base + BK * LRA + r * LRB;
-        col = j0;
-      }
-      const int64_t k = kstep * BK + r;
-      if (k < K) {
-        // inline asm, not the builtin: the compiler's waitcnt pass would otherwise order every
-        // later LDS read after this DMA (vmcnt(0) before the MFMA fragments), which defeats the
-        // three-stage pipeline; the explicit s_waitcnt vmcnt(n) below does the ordering
-        const unsigned m0v = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)dst);
-        const double* g = U + k * ldu + col + lane * 2;
-        asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off" : : "s"(m0v), "v"(g) : "memory");
-      } else {
-        *reinterpret_cast<double2*>(dst + lane * 2) = make_double2(0.0, 0.0);
-      }
-    }
-  };
-  d4 acc[4][4];
-#pragma unroll
-  for (int a = 0; a < 4; a++)
-#pragma unroll
-    for (int b = 0; b < 4; b++) acc[a][b] = (d4){0.0, 0.0, 0.0, 0.0};
-  if (nsteps > 0) stage(ks0, 0);
-  if (nsteps > 1) stage(ks0 + 1, 1);
-  for (int64_t st = 0; st < nsteps; st++) {
-    // stage st complete (stage st+1's loads may stay in flight), visible to every wave, and every
-    // wave done with stage st-1's buffer, which the loads of stage st+2 reuse
-    // (a partial last stage past K issues fewer loads: wait for everything then)
-    if (st + 1 < nsteps && (ks0 + st + 2) * BK <= K) {
-      if (nload == 6) __builtin_amdgcn_s_waitcnt(0x0076);  // vmcnt(6) lgkmcnt(0)
-      else __builtin_amdgcn_s_waitcnt(0x0074);             // vmcnt(4) lgkmcnt(0)
-    } else {
-      __builtin_amdgcn_s_waitcnt(0x0070);  // vmcnt(0) lgkmcnt(0)
-    }
-    __builtin_amdgcn_s_barrier();
-    if (st + 2 < nsteps) stage(ks0 + st + 2, (int)((st + 2) % NBUF8));
-    if (active) {
-      const double* A = lds + (int)(st % NBUF8) * ST8;
-      const double* B = bshare < 0 ? A + BK * LRA : A + bshare;
-      const int ldb = bshare < 0 ? LRB : LRA;
-#pragma unroll
-      for (int ks = 0; ks < BK / 4; ks++) {
-        const int kr = ks * 4 + frag_row;
-        const double2 a01 = *reinterpret_cast<const double2*>(&A[kr * LRA + wm * 64 + 4 * frag_col]);
-        const double2 a23 = *reinterpret_cast<const double2*>(&A[kr * LRA + wm * 64 + 4 * frag_col + 2]);
-        const double2 b01 = *reinterpret_cast<const double2*>(&B[kr * ldb + wn * 64 + 4 * frag_col]);
-        const double2 b23 = *reinterpret_cast<const double2*>(&B[kr * ldb + wn * 64 + 4 * frag_col + 2]);
-        const double af[4] = {a01.x, a01.y, a23.x, a23.y};
-        const double bf[4] = {b01.x, b01.y, b23.x, b23.y};
-#if GBM_PRIO == 2
-        __builtin_amdgcn_s_setprio(1);
-#endif
-#pragma unroll
-        for (int m = 0; m < 4; m++)
-#pragma unroll
-          for (int q = 0; q < 4; q++)
-            acc[m][q] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[m], bf[q], acc[m][q], 0, 0, 0);
-#if GBM_PRIO == 2
-        __builtin_amdgcn_s_setprio(0);
-#endif
-      }
-    }
-  }
-  // every quadrant stores (inactive ones write zeros): the reduce reads whole tiles
-  const int64_t ld = sb.n == 1 ? ldc : W8C;
-  if (sb.n == 1 && !active) return;
-  double* out = (sb.n == 1 ? C + i0 * ldc + j0 : slab + ((int64_t)sl * ntiles + t) * (W8R * W8C)) +
-                (wm * 64 + 4 * frag_row) * ld + wn * 64 + 4 * frag_col;
-#pragma unroll
-  for (int m = 0; m < 4; m++)
-#pragma unroll
-    for (int r = 0; r < 4; r++) {
-      double* o = out + (16 * r + m) * ld;
-      *reinterpret_cast<double2*>(o) = make_double2(acc[m][0][r], acc[m][1][r]);
-      *reinterpret_cast<double2*>(o + 2) = make_double2(acc[m][2][r], acc[m][3][r]);
-    }
-}
-
-// G tile (256 x 128) = Σ_s slab[s][tile] in slice order
-__global__ void __launch_bounds__(256) grm_slab_reduce8_kernel(const double* __restrict__ slab, int64_t ntiles,
-                                                               int nslices, double* __restrict__ G, int64_t ldg,
-                                                               int64_t rows) {
-  const int64_t t = blockIdx.x;
-  int64_t ti2, tj;
-  tile8_of(t, ti2, tj);
-  const int64_t per = (int64_t)W8R * W8C;
-  for (int e = threadIdx.x * 2; e < W8R * W8C; e += 256 * 2) {
-    const int row = e / W8C, col = e % W8C;
-    if (ti2 * W8R + row >= rows) continue;  // past npad
-    double2 acc = make_double2(0.0, 0.0);
-    for (int sl = 0; sl < nslices; sl++) {
-      const double2 v = *reinterpret_cast<const double2*>(slab + ((int64_t)sl * ntiles + t) * per + e);
-      acc.x += v.x;
-      acc.y += v.y;
-    }
-    *reinterpret_cast<double2*>(G + (ti2 * W8R + row) * ldg + tj * W8C + col) = acc;
-  }
-}
-
 static int resident_wgs() {
   int dev = 0, cus = 256;
   if (hipGetDevice(&dev) == hipSuccess) {
@@ -807,27 +460,50 @@ static int resident_wgs() {
   return cus * WPS;  // WPS workgroups per CU (LDS 2 x 2 x BK x 1152 B each)
 }
 
-// Plan of the GRM loci split. Candidate partitions of a tile's nst stages — uniform (1..8
-// slices) and guided (one large first range, then geometrically shrinking ones) — are scored by
-// simulating the in-order dispatch of the ntiles x nslices workgroups onto the resident slots
-// (list scheduling with per-tile costs; slot speeds jittered by ~2 %, as measured with
-// GBM_DEBUG_WGTIME), plus the slab-reduce cost; the fastest wins. Cached per (kernel, n, p, slots).
-// Kernel: the 128x128 4-wave one (default) or the 256x128 8-wave variant (GBM_GRM_KERNEL=w8;
-// 22.1 vs 19.6 ms at C2: with one workgroup per CU every barrier stalls both waves of a SIMD).
-struct GrmPlan {
-  int wide;  // 1: grm_syrk8_kernel, 0: syrk_kernel<kSplit>
-  int64_t ntiles, nst, tile_elems;
-  SliceBounds sb;
-  int64_t main_doubles, edge_doubles;  // workspace: loci-slice partial tiles, edge partials
+// Environment tuning of the GRM launch, read at every plan (cheap: a few getenv calls), so the
+// modes can be forced per call (tests) without a process restart.
+struct GrmTuning {
+  int carry = -1;              // GBM_GRM_CARRY: 0 slabs, 1 in-order carry, -1 automatic
+  bool edge = true;            // GBM_GRM_EDGE: ragged-edge kernel for a last tile column of <= 64
+  bool persist = true;         // GBM_GRM_PERSIST: persistent workgroups with per-XCD queues
+  bool edge_concurrent = true; // GBM_GRM_EDGE_CONCURRENT: edge kernel on the helper stream
+  std::vector<double> split;   // GBM_GRM_SPLIT: relative loci-range sizes (tuning experiments)
 };
 
-static bool grm_wide() {
-  static const bool w = [] {
-    const char* e = getenv("GBM_GRM_KERNEL");
-    return e && std::string(e) == "w8";
-  }();
-  return w;
+static GrmTuning grm_tuning() {
+  GrmTuning t;
+  auto flag = [](const char* name, bool dflt) {
+    const char* e = getenv(name);
+    return e ? atoi(e) != 0 : dflt;
+  };
+  if (const char* e = getenv("GBM_GRM_CARRY")) t.carry = atoi(e) != 0 ? 1 : 0;
+  t.edge = flag("GBM_GRM_EDGE", true);
+  t.persist = flag("GBM_GRM_PERSIST", true);
+  t.edge_concurrent = flag("GBM_GRM_EDGE_CONCURRENT", true);
+  if (const char* ov = getenv("GBM_GRM_SPLIT")) {
+    for (const char* q = ov; *q;) {
+      char* end = nullptr;
+      const double x = strtod(q, &end);
+      if (end == q) break;
+      if (x > 0) t.split.push_back(x);
+      q = (*end == ',') ? end + 1 : end;
+    }
+    if ((int)t.split.size() > kMaxSlices) t.split.clear();
+  }
+  return t;
 }
+
+// Plan of the GRM loci split. Candidate partitions of a tile's nst stages — uniform (1..8
+// slices) and guided (one large first range, then geometrically shrinking ones) — are scored by
+// simulating the dispatch of the ntiles x nslices units onto the resident slots (list
+// scheduling with per-tile costs; slot speeds jittered by ~2 %, as measured with per-unit
+// timelines), plus the slab-reduce cost; the fastest wins. Cached per (n, p, slots, mode).
+struct GrmPlan {
+  int64_t ntiles, nst, tile_elems;
+  SliceBounds sb;
+  int64_t main_doubles, edge_doubles;  // workspace: loci-slice partial tiles (or carry flags), edge partials
+  bool persist, edge_concurrent;
+};
 
 static double simulate_split(const std::vector<int64_t>& sizes, const std::vector<double>& cost, int64_t R,
                              double tile_bytes, double stage_s, bool carry) {
@@ -858,51 +534,21 @@ static double simulate_split(const std::vector<int64_t>& sizes, const std::vecto
   return makespan + reduce_stages;
 }
 
-static int grm_carry_env() {  // GBM_GRM_CARRY=0/1 forces slabs / in-order carry; -1 = automatic
-  static const int v = [] {
-    const char* e = getenv("GBM_GRM_CARRY");
-    return e ? (atoi(e) != 0 ? 1 : 0) : -1;
-  }();
-  return v;
-}
-
-static bool grm_edge_enabled() {
-  static const bool v = [] {
-    const char* e = getenv("GBM_GRM_EDGE");
-    return !e || atoi(e) != 0;
-  }();
-  return v;
-}
-
 static GrmPlan plan(int64_t n, int64_t p) {
+  const GrmTuning tune = grm_tuning();
   GrmPlan g;
   const int64_t nt_all = npad_of(n) / BT;
-  g.wide = grm_wide() ? 1 : 0;
   // ragged last tile column with r <= 64 useful columns: computed by the edge workgroups
   const int64_t r_last = n - (nt_all - 1) * BT;
-  const bool edge = !g.wide && grm_edge_enabled() && nt_all >= 8 && r_last <= 64;
+  const bool edge = tune.edge && nt_all >= 8 && r_last <= 64;
   const int64_t nt = edge ? nt_all - 1 : nt_all;
   g.nst = (p + BK - 1) / BK;
   std::vector<double> cost;
-  int64_t R = resident_wgs();
-  if (g.wide) {
-    // tile column tj even: the second 128-row block is below the diagonal, its 4 waves idle and
-    // the other 4 get their SIMDs alone (~0.6 of a full tile)
-    for (int64_t tj = 0; tj < nt; tj++)
-      for (int64_t ti2 = 0; ti2 <= tj / 2; ti2++) cost.push_back((tj == 2 * ti2) ? 0.6 : 1.0);
-    g.ntiles = tiles8_of_nt(nt);
-    g.tile_elems = (int64_t)W8R * W8C;
-    R = R / WPS;  // one 512-thread workgroup per CU
-  } else {
-    for (int64_t tj = 0; tj < nt; tj++)
-      for (int64_t ti = 0; ti <= tj; ti++) cost.push_back(ti == tj ? 0.93 : 1.0);
-    g.ntiles = nt * (nt + 1) / 2;
-    g.tile_elems = (int64_t)BT * BT;
-  }
-  static std::mutex mu;
-  static std::map<std::tuple<int, int64_t, int64_t, int64_t>, SliceBounds> cache;
-  std::lock_guard<std::mutex> lock(mu);
-  auto key = std::make_tuple(g.wide, nt, g.nst, R);
+  const int64_t R = resident_wgs();
+  for (int64_t tj = 0; tj < nt; tj++)
+    for (int64_t ti = 0; ti <= tj; ti++) cost.push_back(ti == tj ? 0.93 : 1.0);
+  g.ntiles = nt * (nt + 1) / 2;
+  g.tile_elems = (int64_t)BT * BT;
   auto finish = [&](GrmPlan& gp) {
     gp.main_doubles = gp.sb.n == 1 ? 0
                       : gp.sb.carry ? (gp.ntiles + 1 + 1) / 2 + 1  // int32 flags + error cell
@@ -923,7 +569,14 @@ static GrmPlan plan(int64_t n, int64_t p) {
       gp.sb.eslab_off = gp.main_doubles;
       gp.edge_doubles = (int64_t)gp.sb.es * gp.sb.erb * 256 * 16 * gp.sb.et;
     }
+    gp.persist = tune.persist && !gp.sb.carry;
+    // the ragged-column kernel and its reduce run on the helper stream, beside the persistent tiles
+    gp.edge_concurrent = gp.sb.er > 0 && gp.persist && tune.edge_concurrent;
   };
+  static std::mutex mu;
+  static std::map<std::tuple<int64_t, int64_t, int64_t, int, std::vector<double>>, SliceBounds> cache;
+  std::lock_guard<std::mutex> lock(mu);
+  auto key = std::make_tuple(nt, g.nst, R, tune.carry, tune.split);
   auto it = cache.find(key);
   if (it != cache.end()) {
     g.sb = it->second;
@@ -932,9 +585,8 @@ static GrmPlan plan(int64_t n, int64_t p) {
   }
   const int64_t minc = 16;  // stages per workgroup at least
   const bool big = g.ntiles > 2048;  // keep the one-off planning cost small for large n
-  // stage time: ~3.9 us per 16-locus stage of a 128x128 tile at 2 workgroups per CU (7.8 us per
-  // 256x128 stage at one workgroup per CU)
-  const double stage_s = g.wide ? 7.8e-6 : 3.9e-6;
+  // stage time: ~3.9 us per 16-locus stage of a 128x128 tile at 2 workgroups per CU
+  const double stage_s = 3.9e-6;
   double best = 1e300;
   auto choose = [&](bool carry) {
     std::vector<std::vector<int64_t>> cands;
@@ -962,30 +614,20 @@ static GrmPlan plan(int64_t n, int64_t p) {
         }
         cands.push_back(v);
       }
-    if (const char* ov = getenv("GBM_GRM_SPLIT")) {  // tuning experiments: "w0,w1,..." relative sizes
-      std::vector<double> w;
-      for (const char* q = ov; *q;) {
-        char* end = nullptr;
-        const double x = strtod(q, &end);
-        if (end == q) break;
-        if (x > 0) w.push_back(x);
-        q = (*end == ',') ? end + 1 : end;
+    if (!tune.split.empty()) {
+      double tot = 0;
+      for (double x : tune.split) tot += x;
+      cands.clear();
+      std::vector<int64_t> v;
+      int64_t acc = 0;
+      double cum = 0;
+      for (size_t i = 0; i < tune.split.size(); i++) {
+        cum += tune.split[i];
+        const int64_t e = (i + 1 == tune.split.size()) ? g.nst : (int64_t)std::llround(cum / tot * (double)g.nst);
+        if (e > acc) v.push_back(e - acc);
+        acc = e > acc ? e : acc;
       }
-      if (!w.empty() && (int)w.size() <= kMaxSlices) {
-        double tot = 0;
-        for (double x : w) tot += x;
-        cands.clear();
-        std::vector<int64_t> v;
-        int64_t acc = 0;
-        double cum = 0;
-        for (size_t i = 0; i < w.size(); i++) {
-          cum += w[i];
-          const int64_t e = (i + 1 == w.size()) ? g.nst : (int64_t)std::llround(cum / tot * (double)g.nst);
-          if (e > acc) v.push_back(e - acc);
-          acc = e > acc ? e : acc;
-        }
-        cands.push_back(v);
-      }
+      cands.push_back(v);
     }
     std::vector<int64_t> bv{g.nst};
     best = 1e300;
@@ -1000,23 +642,17 @@ static GrmPlan plan(int64_t n, int64_t p) {
   };
   // slabs (+ reduce kernel) unless they would exceed 4 GiB (or GBM_GRM_CARRY forces a mode):
   // the in-order carry needs no workspace but its write-through epilogue costs ~1 % at C2
-  int carry_mode = grm_carry_env();
+  int carry_mode = tune.carry;
   std::vector<int64_t> bestv = choose(carry_mode == 1);
-  if (carry_mode < 0 && !g.wide && bestv.size() > 1 &&
+  if (carry_mode < 0 && bestv.size() > 1 &&
       (double)bestv.size() * (double)g.ntiles * (double)g.tile_elems * 8.0 > 4.0 * 1073741824.0) {
     carry_mode = 1;
     bestv = choose(true);
   }
-  g.sb.carry = (!g.wide && carry_mode == 1 && bestv.size() > 1) ? 1 : 0;
+  g.sb.carry = (carry_mode == 1 && bestv.size() > 1) ? 1 : 0;
   g.sb.n = (int32_t)bestv.size();
   g.sb.b[0] = 0;
   for (int i = 0; i < g.sb.n; i++) g.sb.b[i + 1] = g.sb.b[i] + (int32_t)bestv[i];
-  if (getenv("GBM_DEBUG_PLAN")) {
-    fprintf(stderr, "grm plan nt=%lld nst=%lld slots=%lld makespan=%.1f stages:", (long long)nt, (long long)g.nst,
-            (long long)R, best);
-    for (int i = 0; i < g.sb.n; i++) fprintf(stderr, " %lld", (long long)bestv[i]);
-    fprintf(stderr, "\n");
-  }
   cache.emplace(key, g.sb);
   finish(g);
   return g;
@@ -1030,10 +666,7 @@ constexpr int P64 = 80;  // LDS pitch: the two 16-lane halves of a fragment read
 __global__ void __launch_bounds__(256, 2)
 syrk64_sub_kernel(const double* __restrict__ U, int64_t ldu, int64_t c0, int64_t lim, double* __restrict__ C,
                   int64_t ldc, double* Ld, double* Dinv, int32_t* __restrict__ info,
-                  int64_t fk0, int rowonly, int kchunks, int32_t* __restrict__ fflags) {
-#ifdef GBM_DEBUG_FACTIME
-  const unsigned long long ft0 = wall_clock64();
-#endif
+                  int64_t fk0, int rowonly, int kchunks) {
   __shared__ __attribute__((aligned(16))) double As[64 * P64];
   __shared__ __attribute__((aligned(16))) double Bs[64 * P64];
   int64_t ti = 0, tj = blockIdx.x;  // rowonly: the first tile row only (the next panel's rows)
@@ -1099,84 +732,7 @@ syrk64_sub_kernel(const double* __restrict__ U, int64_t ldu, int64_t c0, int64_t
     }
   }
   const bool factor_next = fk0 >= 0 && blockIdx.x == 0;
-  // fused panel: the other tiles of the first tile row are the next panel's column chunks
-  // (rows fk0 .. fk0+64): once the first workgroup has published the factored diagonal block,
-  // each solves its chunk in place of a separate chol_panel_kernel launch
-  const bool panel_tile = fflags != nullptr && fk0 >= 0 && ti == 0 && tj > 0;
-  if (!active && !factor_next && !panel_tile) return;
-  if (panel_tile) {
-#ifdef GBM_DEBUG_FACTIME
-    const unsigned long long pt1 = wall_clock64();
-#endif
-    __syncthreads();  // every wave is done reading As/Bs
-    double* X = Bs;   // pitch P64 == PS
-    double* Us = As;
-#pragma unroll
-    for (int m = 0; m < 2; m++)
-#pragma unroll
-      for (int q = 0; q < 2; q++)
-#pragma unroll
-        for (int r = 0; r < 4; r++) X[(wm * 32 + m * 16 + fr + 4 * r) * PS + wn * 32 + q * 16 + fc] = acc[m][q][r];
-    if (tid == 0) wait_flag(&fflags[fk0 / 64], 1, info);
-    __syncthreads();
-#ifdef GBM_DEBUG_FACTIME
-    const unsigned long long pt2 = wall_clock64();
-#endif
-    // the block was written through (agent-scope stores) before the flag's release; after the
-    // acquire (every wave) plain loads — all of this lane's 32 in flight at once — read it
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    double di[4][4], us[16];
-    {
-      const double* Di = Dinv + (fk0 / 16) * 256 + (fr * 16 + fc);
-      const int row = tid >> 2, quarter = tid & 3;
-      const double* src = Ld + (fk0 + row) * CNB + quarter * 16;
-#pragma unroll
-      for (int e = 0; e < 16; e += 2) {
-        const double2 v = *reinterpret_cast<const double2*>(src + e);
-        us[e] = v.x;
-        us[e + 1] = v.y;
-      }
-#pragma unroll
-      for (int rb = 0; rb < 4; rb++)
-#pragma unroll
-        for (int ks = 0; ks < 4; ks++) di[rb][ks] = Di[rb * 256 + ks * 64];
-#pragma unroll
-      for (int e = 0; e < 16; e++) Us[row * PS + quarter * 16 + e] = us[e];
-    }
-    __syncthreads();
-    panel_chunk_solve(X, Us, [&](int rb, int ks) { return di[rb][ks]; }, lane, wave);
-    __syncthreads();
-    {
-      // solved chunk -> the U rows, and transposed into the lower triangle (L = Uᵀ, read by the
-      // back substitution)
-      const int row = tid >> 2, quarter = tid & 3;
-      double* dx = C + (i0 + row) * ldc + j0 + quarter * 16;
-#pragma unroll
-      for (int e = 0; e < 16; e += 2)
-        *reinterpret_cast<double2*>(dx + e) = *reinterpret_cast<const double2*>(&X[row * PS + quarter * 16 + e]);
-      double* dl = C + (j0 + row) * ldc + i0 + quarter * 16;
-#pragma unroll
-      for (int e = 0; e < 16; e += 2)
-        *reinterpret_cast<double2*>(dl + e) =
-            make_double2(X[(quarter * 16 + e) * PS + row], X[(quarter * 16 + e + 1) * PS + row]);
-    }
-#ifdef GBM_DEBUG_FACTIME
-    __builtin_amdgcn_s_waitcnt(0);
-    __syncthreads();
-    if (tid == 0) {
-      const unsigned long long k = atomicAdd(&g_paneltime_n, 1ull);
-      if (k < 16384) {
-        g_paneltime[6 * k] = (unsigned long long)fk0;
-        g_paneltime[6 * k + 1] = ft0;
-        g_paneltime[6 * k + 2] = pt1;
-        g_paneltime[6 * k + 3] = pt2;
-        g_paneltime[6 * k + 4] = wall_clock64();
-        g_paneltime[6 * k + 5] = (unsigned long long)tj;
-      }
-    }
-#endif
-    return;
-  }
+  if (!active && !factor_next) return;
 #pragma unroll
   for (int m = 0; m < 2; m++)
 #pragma unroll
@@ -1199,31 +755,9 @@ syrk64_sub_kernel(const double* __restrict__ U, int64_t ldu, int64_t c0, int64_t
 #pragma unroll
         for (int r = 0; r < 4; r++) Us[(wm * 32 + m * 16 + fr + 4 * r) * PS + wn * 32 + q * 16 + fc] = acc[m][q][r];
     __syncthreads();
-#ifdef GBM_DEBUG_FACTIME
-    const unsigned long long ft1 = wall_clock64();
-#endif
     const int bad = factor_diag_block(Us, rinv, tid);
-#ifdef GBM_DEBUG_FACTIME
-    const unsigned long long ft2 = wall_clock64();
-#endif
     if (tid == 0 && bad >= 0) atomicCAS(info, 0, (int32_t)(fk0 + bad + 1));
-    if (fflags) {
-      store_factor<true>(Us, rinv, Ld + fk0 * CNB, Dinv + (fk0 / 16) * 256, tid);
-      publish_flag(&fflags[fk0 / 64], 1, tid);
-    } else {
-      store_factor(Us, rinv, Ld + fk0 * CNB, Dinv + (fk0 / 16) * 256, tid);
-    }
-#ifdef GBM_DEBUG_FACTIME
-    if (tid == 0) {
-      const unsigned long long k = atomicAdd(&g_factime_n, 1ull);
-      if (k < 1024) {
-        g_factime[4 * k] = ft0;
-        g_factime[4 * k + 1] = ft1;
-        g_factime[4 * k + 2] = ft2;
-        g_factime[4 * k + 3] = wall_clock64();
-      }
-    }
-#endif
+    store_factor(Us, rinv, Ld + fk0 * CNB, Dinv + (fk0 / 16) * 256, tid);
   }
 }
 
@@ -1237,41 +771,33 @@ void chol_refresh_tuning() {
 int64_t chol_small_lim() { return g_small_lim.load(std::memory_order_relaxed); }
 
 // Block row [k1, k1+64) only, k1 = k0 + 64 kch: C[k1 : k1+64, k1 : gdim] -= U[k0:k1, ·]ᵀ U[k0:k1, ·]
-// (a later panel's rows of a 2- or 4-panel group, brought up to date with the group's earlier
-// panels so that the whole group shares one K = 128 / 256 trailing update); the first workgroup
-// factors the diagonal block at k1 afterwards.
+// (a later panel's rows of a panel group, brought up to date with the group's earlier panels so
+// that the whole group shares one K = 64 g trailing update); the first workgroup factors the
+// diagonal block at k1 afterwards.
 int launch_chol_row_update(double* G, int64_t ldg, int64_t k0, int kch, int64_t gdim, double* Ld, double* Dinv,
-                           int32_t* info, int32_t* fflags, hipStream_t s) {
+                           int32_t* info, hipStream_t s) {
   const int64_t k1 = k0 + 64 * (int64_t)kch;
   const int64_t lim = gdim - k1;
   syrk64_sub_kernel<<<(unsigned)(lim / 64), 256, 0, s>>>(G + k0 * ldg, ldg, k1, lim, G, ldg, Ld, Dinv, info, k1, 1,
-                                                         kch, fflags);
+                                                         kch);
   GBM_LAUNCH_CHECK();
   return GBM_OK;
 }
 
 // Upper-Cholesky trailing update: C[k1:gdim, k1:gdim] (upper tiles) -= U[k0:k1, k1:]ᵀ U[k0:k1, k1:]
-// with k1 = k0 + nb (nb = 64, or 128 for two panels at once)
-// fflags != nullptr: fuse the next panel into the update where the kernel supports it; *fused
-// tells the caller whether the panel of next_k0 is done
+// with k1 = k0 + nb; the first workgroup then factors the diagonal block at next_k0 (if >= 0).
+// 64x64 tiles (syrk64_sub_kernel) for single panels below chol_small_lim() trailing rows (more
+// workgroups for the small trailing matrices of late panels), else the 128x128 tile kernel.
 int launch_chol_update(double* G, int64_t ldg, int64_t k0, int64_t nb, int64_t gdim, double* Ld, double* Dinv,
-                       int32_t* info, int64_t next_k0, int32_t* fflags, bool* fused, hipStream_t s) {
+                       int32_t* info, int64_t next_k0, hipStream_t s) {
   const int64_t k1 = k0 + nb;
   const int64_t lim = gdim - k1;
-  *fused = false;
   if (lim <= 0) return GBM_OK;
-  // 64x64 tiles below chol_small_lim() (K = 64), or below GBM_UPD64_LIM2 rows for a K = 128
-  // pair update (more workgroups for trailing matrices that fill few 128-tile rounds)
-  static const int64_t lim2 = [] {
-    const char* e = getenv("GBM_UPD64_LIM2");
-    return e ? (int64_t)atoll(e) : (int64_t)-1;
-  }();
-  if ((nb == 64 && lim <= chol_small_lim()) || (nb == 128 && lim <= lim2)) {
+  if (nb == 64 && lim <= chol_small_lim()) {
     const int64_t m = (lim + 63) / 64;
     syrk64_sub_kernel<<<(unsigned)(m * (m + 1) / 2), 256, 0, s>>>(G + k0 * ldg, ldg, k1, lim, G, ldg, Ld, Dinv, info,
-                                                                  next_k0, 0, (int)(nb / 64), fflags);
+                                                                  next_k0, 0, (int)(nb / 64));
     GBM_LAUNCH_CHECK();
-    *fused = fflags != nullptr && next_k0 >= 0;
     return GBM_OK;
   }
   const int64_t m = (lim + BT - 1) / BT;
@@ -1280,22 +806,6 @@ int launch_chol_update(double* G, int64_t ldg, int64_t k0, int64_t nb, int64_t g
                                                      Dinv, info, next_k0);
   GBM_LAUNCH_CHECK();
   return GBM_OK;
-}
-
-static bool grm_persist() {  // GBM_GRM_PERSIST=0: hardware-dispatched workgroups instead
-  static const bool v = [] {
-    const char* e = getenv("GBM_GRM_PERSIST");
-    return !e || atoi(e) != 0;
-  }();
-  return v;
-}
-
-static bool grm_edge_concurrent() {  // GBM_GRM_EDGE_CONCURRENT=0: edge kernel after the tiles
-  static const bool v = [] {
-    const char* e = getenv("GBM_GRM_EDGE_CONCURRENT");
-    return !e || atoi(e) != 0;
-  }();
-  return v;
 }
 
 // The helper stream of the forked edge kernel: one per device for the process (bounded, created
@@ -1336,10 +846,6 @@ static int aux_stream(hipStream_t caller, AuxStream& a, bool* usable) {
   return GBM_OK;
 }
 
-static bool persistent_launch(const GrmPlan& g) { return !g.wide && grm_persist() && !g.sb.carry; }
-// the ragged-column kernel and its reduce run on the helper stream, beside the persistent tiles
-static bool edge_on_aux(const GrmPlan& g) { return g.sb.er > 0 && persistent_launch(g) && grm_edge_concurrent(); }
-
 // workspace: [slabs or carry flags][edge partials][8 queue counters of the persistent launch]
 int64_t grm_workspace_bytes(int64_t n, int64_t p) {
   const GrmPlan g = plan(n, p);
@@ -1355,13 +861,14 @@ static int check_grm_args(const double* Zt, int64_t ldz, int64_t p, int64_t n, d
   return GBM_OK;
 }
 
-// stage 1: the MFMA SYRK (one partial tile per (slice, tile) into the workspace slabs)
+// stage 1: the MFMA SYRK (one partial tile per (slice, tile) into the workspace slabs, or the
+// in-order carry into G)
 int launch_grm_syrk(const double* Zt, int64_t ldz, int64_t p, int64_t n, double* G, int64_t ldg, void* ws,
                     int64_t ws_bytes, hipStream_t s) {
   int rc = check_grm_args(Zt, ldz, p, n, G, ldg);
   if (rc != GBM_OK) return rc;
   const GrmPlan g = plan(n, p);
-  const int64_t need = grm_workspace_bytes(n, p);
+  const int64_t need = (g.main_doubles + g.edge_doubles + 4) * (int64_t)sizeof(double);
   if (need > 0 && (!ws || ws_bytes < need))
     return fail(GBM_E_ARG, "gbm_dev_grm: workspace too small (" + std::to_string(ws_bytes) + " < " +
                                std::to_string(need) + ")");
@@ -1369,13 +876,12 @@ int launch_grm_syrk(const double* Zt, int64_t ldz, int64_t p, int64_t n, double*
   if (g.sb.carry) GBM_HIP_TRY(hipMemsetAsync(ws, 0, (size_t)(g.ntiles + 1) * sizeof(int32_t), s));
   int32_t* ctr = reinterpret_cast<int32_t*>((double*)ws + g.main_doubles + g.edge_doubles);
   const int64_t lim = g.sb.er > 0 ? g.sb.e0 : n;  // with an edge, the tiles cover [0, e0)^2 exactly
-  const bool persist = persistent_launch(g);
   // the ragged-column kernel beside the persistent tiles: forked (before the tile launch) onto
-  // this thread's helper stream for the device; its workgroups fit in the registers the two tile
-  // workgroups of a CU leave free. Joined back before the reduce.
+  // the device's helper stream; its workgroups fit in the registers the two tile workgroups of a
+  // CU leave free. Joined back before returning.
   AuxStream aux;
   AuxStream* ax = nullptr;
-  if (edge_on_aux(g)) {
+  if (g.edge_concurrent) {
     bool usable = false;
     rc = aux_stream(s, aux, &usable);
     if (rc != GBM_OK) return rc;
@@ -1385,9 +891,7 @@ int launch_grm_syrk(const double* Zt, int64_t ldz, int64_t p, int64_t n, double*
       GBM_HIP_TRY(hipStreamWaitEvent(ax->s, ax->fork, 0));
     }
   }
-  if (g.wide) {
-    grm_syrk8_kernel<<<grid, 512, 0, s>>>(Zt, ldz, p, n, G, ldg, (double*)ws, g.ntiles, g.sb);
-  } else if (persist) {
+  if (g.persist) {
     GBM_HIP_TRY(hipMemsetAsync(ctr, 0, 8 * sizeof(int32_t), s));
     const int64_t units = (int64_t)g.sb.n * g.ntiles;
     const unsigned pgrid = (unsigned)(units < resident_wgs() ? units : resident_wgs());
@@ -1409,7 +913,7 @@ int launch_grm_syrk(const double* Zt, int64_t ldz, int64_t p, int64_t n, double*
       default: grm_edge_kernel<4><<<eg, 256, 0, es>>>(Zt, ldz, p, g.sb, part); break;
     }
     GBM_LAUNCH_CHECK();
-    if (edge_on_aux(g)) {
+    if (g.edge_concurrent) {
       // the edge columns of G are disjoint from the tiles: sum their partials here, on the helper
       // stream when there is one (launch_grm_reduce then skips them)
       grm_edge_reduce_kernel<<<(unsigned)((n * g.sb.er + 255) / 256), 256, 0, es>>>(part, n, g.sb, G, ldg);
@@ -1423,22 +927,28 @@ int launch_grm_syrk(const double* Zt, int64_t ldz, int64_t p, int64_t n, double*
   return GBM_OK;
 }
 
-// stage 2: sum the slice partials of each tile into G
+// stage 2: sum the slice partials of each tile into G. In carry mode, read back the error cell
+// of the inter-workgroup waits (tflags[ntiles]; set to −1 if a wait gave up) and fail loudly:
+// a timed-out wait would otherwise leave a silently wrong G.
 int launch_grm_reduce(int64_t n, int64_t p, double* G, int64_t ldg, const void* ws, hipStream_t s) {
   const GrmPlan g = plan(n, p);
   if (g.sb.n == 1 && g.sb.er == 0) return GBM_OK;
   if (!ws) return fail(GBM_E_ARG, "gbm_dev_grm_reduce: workspace required");
-  if (g.sb.er > 0 && !edge_on_aux(g)) {
+  if (g.sb.er > 0 && !g.edge_concurrent) {
     grm_edge_reduce_kernel<<<(unsigned)((n * g.sb.er + 255) / 256), 256, 0, s>>>((const double*)ws + g.sb.eslab_off, n,
                                                                                  g.sb, G, ldg);
     GBM_LAUNCH_CHECK();
   }
-  if (g.sb.n == 1 || g.sb.carry) return GBM_OK;
-  if (g.wide)
-    grm_slab_reduce8_kernel<<<(unsigned)g.ntiles, 256, 0, s>>>((const double*)ws, g.ntiles, g.sb.n, G, ldg,
-                                                               npad_of(n));
-  else
-    grm_slab_reduce_kernel<<<(unsigned)g.ntiles, 256, 0, s>>>((const double*)ws, g.ntiles, g.sb.n, G, ldg);
+  if (g.sb.n == 1) return GBM_OK;
+  if (g.sb.carry) {
+    int32_t err = 0;
+    GBM_HIP_TRY(hipMemcpyAsync(&err, (const int32_t*)ws + g.ntiles, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+    GBM_HIP_TRY(hipStreamSynchronize(s));
+    if (err < 0)
+      return fail(GBM_E_HIP, "GRM in-order carry accumulation: an inter-workgroup wait timed out (G is invalid)");
+    return GBM_OK;
+  }
+  grm_slab_reduce_kernel<<<(unsigned)g.ntiles, 256, 0, s>>>((const double*)ws, g.ntiles, g.sb.n, G, ldg);
   GBM_LAUNCH_CHECK();
   return GBM_OK;
 }
@@ -1509,27 +1019,6 @@ extern "C" int gbm_dev_grm_reduce(int64_t n, int64_t p, double* G, int64_t ldg, 
   if (!G || n < 1 || p < 1 || ldg < gbm::npad_of(n)) return gbm::fail(GBM_E_ARG, "gbm_dev_grm_reduce: bad arguments");
   return gbm::launch_grm_reduce(n, p, G, ldg, workspace, (hipStream_t)stream);
 }
-
-#ifdef GBM_DEBUG_FACTIME
-extern "C" int gbm_debug_factime(void* host, int64_t* count) {
-  unsigned long long n = 0;
-  if (hipMemcpyFromSymbol(&n, HIP_SYMBOL(gbm::g_factime_n), 8) != hipSuccess) return -1;
-  *count = (int64_t)n;
-  return hipMemcpyFromSymbol(host, HIP_SYMBOL(gbm::g_factime), 4 * 1024 * 8) == hipSuccess ? 0 : -1;
-}
-extern "C" int gbm_debug_paneltime(void* host, int64_t* count) {
-  unsigned long long n = 0;
-  if (hipMemcpyFromSymbol(&n, HIP_SYMBOL(gbm::g_paneltime_n), 8) != hipSuccess) return -1;
-  *count = (int64_t)n;
-  return hipMemcpyFromSymbol(host, HIP_SYMBOL(gbm::g_paneltime), 6 * 16384 * 8) == hipSuccess ? 0 : -1;
-}
-#endif
-
-#ifdef GBM_DEBUG_WGTIME
-extern "C" int gbm_debug_wgtime(void* host, int64_t count) {
-  return hipMemcpyFromSymbol(host, HIP_SYMBOL(gbm::g_wgtime), count * 3 * sizeof(unsigned long long)) == hipSuccess ? 0 : -1;
-}
-#endif
 
 extern "C" int gbm_dev_grm_slices(int64_t n, int64_t p) {
   return gbm::plan(n, p).sb.n;

@@ -428,9 +428,11 @@ extern "C" int gbm_session_stats(gbm_session* s, int64_t* grm_builds, int64_t* g
 }
 
 // ---- ridge path (glmnet alpha = 0, standardize = false; reference ridge, src/linear.jl:193-203) --
-// glmnet minimises (1/2n)‖y − a0 − Xb‖² + (λ/2)‖b‖², i.e. (X_cᵀX_c + nλI) b = X_cᵀ(y − ȳ) on the
-// centred X: the GBLUP system on the unscaled centred-X kernel K = X_cX_cᵀ with λ' = nλ, whose GLS
-// intercept is ȳ (K1 = 0) and whose marker effects are b = X_cᵀa.
+// glmnet minimises (1/2n)‖y − a0 − Xb‖² + (λ/2)‖b‖² on y scaled by its population sd σ_y, with the
+// user λ divided by the same σ_y (elnet: vlam = ulam/ys). On the original scale that is
+// (X_cᵀX_c + (nλ/σ_y)I) b = X_cᵀ(y − ȳ): the GBLUP system on the unscaled centred-X kernel
+// K = X_cX_cᵀ with λ' = nλ/σ_y, whose GLS intercept is ȳ (K1 = 0) and whose marker effects are
+// b = X_cᵀa. σ_y is taken over the training rows of each call (each CV fold has its own).
 
 extern "C" int gbm_session_ridge_lambda_max(gbm_session* s, const int64_t* idx, int64_t n_train, const double* y,
                                             double* lambda_max) {
@@ -475,6 +477,12 @@ extern "C" int gbm_session_ridge_path(gbm_session* s, const int64_t* idx, int64_
   GBM_TRY(ensure_training(s, idx, n_train, 1));
   GBM_TRY(ensure_rhs(s, 1));
   GBM_TRY(upload_y(s, y, n_train, 1));
+  double ym = 0.0, yss = 0.0;
+  for (int64_t i = 0; i < n_train; i++) ym += y[i];
+  ym /= (double)n_train;
+  for (int64_t i = 0; i < n_train; i++) yss += (y[i] - ym) * (y[i] - ym);
+  const double ys = std::sqrt(yss / (double)n_train);
+  if (!(ys > 0.0)) return fail(GBM_E_ARG, "gbm_session_ridge_path: y has zero variance");
   hipStream_t st = s->stream.s;
   const int64_t p = s->p, n = s->n, npad = s->npad;
   const int64_t nchunks = predict_chunks(n, p);
@@ -485,7 +493,7 @@ extern "C" int gbm_session_ridge_path(gbm_session* s, const int64_t* idx, int64_
   }
   std::vector<double> all(n_eval > 0 ? npad : 0);
   for (int64_t k = 0; k < nl; k++) {
-    GBM_TRY(solve_cached(s, 1, (double)n_train * lambdas[k], 1.0));
+    GBM_TRY(solve_cached(s, 1, (double)n_train * lambdas[k] / ys, 1.0));
     GBM_TRY(gbm_dev_marker_effects((const double*)s->Z.p, s->npadT, p, s->nT, (const double*)s->A.p, s->npadT, 1,
                                    1.0, nullptr, (const double*)s->mean.p, (const double*)s->sd.p,
                                    (const int32_t*)s->keep.p, (double*)s->B.p, p, (double*)s->msum.p, st));

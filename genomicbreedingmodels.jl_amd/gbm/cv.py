@@ -89,9 +89,32 @@ def _model_label(model) -> str:
 class _Job:
     i: int                   # position in cvs
     lam: object              # float or "reml"
-    idx_train: np.ndarray    # 0-based rows (strictly increasing)
-    idx_val: np.ndarray      # 0-based rows
+    idx_train: np.ndarray    # 0-based rows with finite phenotype, strictly increasing (the session's order)
+    order: np.ndarray        # caller order of the training rows: rows_caller = idx_train[order]
+    idx_val: np.ndarray      # 0-based rows, caller order
     trait: int               # 0-based trait column
+
+
+def _make_job(i, lam, rows, idx_val, trait, Y) -> _Job:
+    """extractxyetc's row handling (src/prediction.jl:114-131) for a fold job: drop training rows
+    whose phenotype is missing/NaN/Inf, keep the caller's order for Fit.entries, and give the
+    session the same rows sorted (its index sets are strictly increasing)."""
+    rows = np.asarray(rows, dtype=np.int64)
+    rows = rows[np.isfinite(Y[rows, trait])]
+    perm = np.argsort(rows, kind="stable")
+    order = np.empty_like(perm)
+    order[perm] = np.arange(perm.size)
+    return _Job(i, lam, rows[perm], order, np.asarray(idx_val, dtype=np.int64), trait)
+
+
+def _sorted_predict(session: GenotypeSession, rows: np.ndarray, b_hat: np.ndarray) -> np.ndarray:
+    """session.predict on rows in any order (predictions returned in that order)."""
+    if rows.size == 0:
+        return np.zeros(0)
+    perm = np.argsort(rows, kind="stable")
+    out = np.empty(rows.size)
+    out[perm] = session.predict(rows[perm], b_hat)
+    return out
 
 
 def _run_device_jobs(session: GenotypeSession, jobs, cvs, genomes, phenomes, errors, lock):
@@ -104,6 +127,9 @@ def _run_device_jobs(session: GenotypeSession, jobs, cvs, genomes, phenomes, err
     for (_, lam), grp in groups.items():
         idx = grp[0].idx_train
         try:
+            if idx.size < 2:
+                raise ArgumentError("There are less than 2 entries with non-missing phenotype data after merging "
+                                    "with the genotype data.")
             if lam == "reml":
                 outs = []
                 for jb in grp:
@@ -117,17 +143,22 @@ def _run_device_jobs(session: GenotypeSession, jobs, cvs, genomes, phenomes, err
                 fits = [(b_hat[:, k], y_pred[:, k]) for k in range(len(grp))]
             for jb, (b, yp) in zip(grp, fits):
                 cv0 = cvs[jb.i]
-                f = cv0.fit
+                rows = jb.idx_train[jb.order]  # the caller's order, missing phenotypes dropped
+                # a fresh Fit, as the model call of cvmultithread! returns (src/cross_validation.jl:170-177)
+                f = Fit(n=rows.size, l=len(cv0.fit.b_hat_labels), model=cv0.fit.model,
+                        b_hat_labels=list(cv0.fit.b_hat_labels), trait=cv0.fit.trait)
+                f.entries = [genomes.entries[r] for r in rows]
+                f.populations = [genomes.populations[r] for r in rows]
                 f.b_hat = b.copy()
-                f.y_pred = yp.copy()
-                f.y_true = Yall[idx, jb.trait].copy()
+                f.y_pred = yp[jb.order].copy()
+                f.y_true = Yall[rows, jb.trait].copy()
                 f.metrics = metrics(f.y_true, f.y_pred)
                 if not f.checkdims():
                     raise GBMError("Error fitting gblup.")
                 yv_true = Yall[jb.idx_val, jb.trait]
                 keep = np.isfinite(yv_true)
                 iv = jb.idx_val[keep]
-                yv_pred = session.predict(iv, f.b_hat) if iv.size else np.zeros(0)
+                yv_pred = _sorted_predict(session, iv, f.b_hat)
                 cv = CV(cv0.replication, cv0.fold, f, [phenomes.populations[r] for r in iv],
                         [phenomes.entries[r] for r in iv], yv_true[keep], yv_pred, metrics(yv_true[keep], yv_pred))
                 with lock:
@@ -148,13 +179,14 @@ def cvmultithread(cvs, *, genomes: Genomes, phenomes: Phenomes, models_vector, v
     pos_loci = {lab: k for k, lab in enumerate(genomes.loci_alleles)}
     pos_entry = {e: k for k, e in enumerate(genomes.entries)}
     gpu_jobs, other = [], []
+    Yall = np.asarray(phenomes.phenotypes, dtype=np.float64)
     for i, (cv, model) in enumerate(zip(cvs, models_vector)):
         lam = _gblup_lambda(model)
         loci = [pos_loci[lab] for lab in cv.fit.b_hat_labels[1:]]
         if lam is not None and loci == list(range(len(genomes.loci_alleles))):
-            gpu_jobs.append(_Job(i, lam, np.array(sorted(pos_entry[e] for e in cv.fit.entries), dtype=np.int64),
-                                 np.array([pos_entry[e] for e in cv.validation_entries], dtype=np.int64),
-                                 phenomes.traits.index(cv.fit.trait)))
+            gpu_jobs.append(_make_job(i, lam, [pos_entry[e] for e in cv.fit.entries],
+                                      [pos_entry[e] for e in cv.validation_entries],
+                                      phenomes.traits.index(cv.fit.trait), Yall))
         else:
             other.append((i, model, loci))
     errors, lock = [], threading.Lock()

@@ -247,14 +247,21 @@ def reml_reference(y: np.ndarray, GRM: np.ndarray) -> dict:
 # (tests/golden/glmnet_ridge_r.npz).
 # ----------------------------------------------------------------------------------------
 def ridge_exact(X: np.ndarray, y: np.ndarray, lam: float):
-    """Exact glmnet ridge minimiser: (X_cᵀX_c + nλI) b = X_cᵀ(y − ȳ), a0 = ȳ − x̄ᵀb."""
+    """Exact glmnet ridge minimiser: (X_cᵀX_c + (nλ/σ_y)I) b = X_cᵀ(y − ȳ), a0 = ȳ − x̄ᵀb.
+
+    glmnet's gaussian elnet (libglmnet, called by GLMNet.jl in the reference ``ridge``,
+    src/linear.jl:193-203) scales y by its population sd σ_y = sqrt(mean((y − ȳ)²)) and divides the
+    user λ by the same σ_y (vlam = ulam/ys) before its coordinate descent, then rescales b by σ_y:
+    on the original scale the penalty is λ/σ_y."""
     n, p = X.shape
     xm, ym = X.mean(axis=0), y.mean()
+    ys = float(np.sqrt(np.mean((y - ym) ** 2)))
     Xc = X - xm
+    pen = n * lam / ys
     if p <= n:
-        b = np.linalg.solve(Xc.T @ Xc + n * lam * np.eye(p), Xc.T @ (y - ym))
+        b = np.linalg.solve(Xc.T @ Xc + pen * np.eye(p), Xc.T @ (y - ym))
     else:
-        b = Xc.T @ np.linalg.solve(Xc @ Xc.T + n * lam * np.eye(n), y - ym)
+        b = Xc.T @ np.linalg.solve(Xc @ Xc.T + pen * np.eye(n), y - ym)
     return ym - xm @ b, b
 
 

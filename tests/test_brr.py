@@ -80,7 +80,8 @@ def test_gpu_brr_posterior_mean_close_to_gblup():
     y = oracle.synth_phenotypes(X, 72)[:, 0]
     b_hat, y_pred, var = gbm.brr_arrays(X, y, n_iter=1500, n_burnin=500, thin=5, seed=3)
     lam_rr = var[0] / var[1]  # per-marker ridge λ on unscaled X
-    a0, b = oracle.ridge_exact(X, y, lam_rr / X.shape[0])
+    # ridge_exact takes glmnet's λ, whose penalty is nλ/σ_y (σ_y = population sd of y)
+    a0, b = oracle.ridge_exact(X, y, lam_rr * y.std() / X.shape[0])
     ridge_pred = a0 + X @ b
     assert np.corrcoef(y_pred, ridge_pred)[0, 1] > 0.98
     assert np.corrcoef(y_pred, y)[0, 1] > 0.5

@@ -137,6 +137,40 @@ def test_cvbulk_gpu_matches_oracle_per_fold(devices):
         assert set(cv.metrics) == set(oracle.metrics(Y[va, t], cv.validation_y_pred))
 
 
+def test_cvmultithread_shuffled_entries_and_missing_training_phenotypes():
+    """cvmultithread! takes CVs whose entries come in any order and whose training phenotypes may
+    be missing (extractxyetc drops those rows, src/prediction.jl:114-131): Fit.entries, y_true and
+    y_pred keep the caller's order, validation predictions keep the validation order."""
+    g, ph = _cv_inputs()
+    X = g.allele_frequencies
+    cvs, notes, mv = gbm.cvbulk_setup(genomes=g, phenomes=ph, models=[gbm.gblup], n_replications=1,
+                                      n_folds=3, seed=7)
+    rng = np.random.default_rng(0)
+    for cv in cvs:
+        k = rng.permutation(len(cv.fit.entries))
+        cv.fit.entries = [cv.fit.entries[j] for j in k]
+        cv.fit.populations = [cv.fit.populations[j] for j in k]
+        k = rng.permutation(len(cv.validation_entries))
+        cv.validation_entries = [cv.validation_entries[j] for j in k]
+    Y = ph.phenotypes.copy()
+    pos = {e: i for i, e in enumerate(g.entries)}
+    drop = [pos[cvs[0].fit.entries[3]], pos[cvs[0].fit.entries[10]]]
+    ph.phenotypes[drop, ph.traits.index(cvs[0].fit.trait)] = np.inf  # missing after setup
+    entries_before = [list(cv.fit.entries) for cv in cvs]
+    gbm.cvmultithread(cvs, genomes=g, phenomes=ph, models_vector=mv, devices=[0])
+    for cv, before in zip(cvs, entries_before):
+        t = ph.traits.index(cv.fit.trait)
+        rows = [pos[e] for e in before if np.isfinite(ph.phenotypes[pos[e], t])]
+        assert [pos[e] for e in cv.fit.entries] == rows
+        assert np.array_equal(cv.fit.y_true, ph.phenotypes[rows, t])
+        ref = oracle.gblup_fit(X[rows], ph.phenotypes[rows, t], 1.0)
+        assert rel(cv.fit.y_pred, ref["y_pred"][:, 0]) < 1e-9
+        va = [pos[e] for e in cv.validation_entries]
+        assert rel(cv.validation_y_pred, oracle.predict_linear(X[va], ref["b_hat"][:, 0])) < 1e-8
+    assert len(cvs[0].fit.entries) == len(entries_before[0]) - 2
+    ph.phenotypes[:] = Y
+
+
 def test_validate_mirrors_reference():
     g, ph = _cv_inputs()
     fit = gbm.gblup(genomes=g, phenomes=ph, idx_entries=list(range(1, 101)))
