@@ -1,13 +1,19 @@
-// Host entry points of libgbm.so (include/gbm.h): argument checks, device buffers, H2D/D2H,
-// SNP-column sharding over devices and the RCCL all-reduce of partial GRMs.
-// Every call owns its streams and buffers (re-entrant, as cvmultithread! requires —
-// reference src/cross_validation.jl:159).
+// Host entry points of libgbm.so (include/gbm.h): argument checks, H2D/D2H, SNP-column sharding
+// over devices and the sum of partial GRMs (device-side for shards on one device, RCCL all-reduce
+// across devices).
+//
+// Re-entrant, as cvmultithread! requires (reference src/cross_validation.jl:159): a call leases
+// one pooled fit context per shard (its own stream and buffers) and returns it afterwards; the
+// contexts' buffers only grow, so repeated calls of one shape allocate no device memory. RCCL
+// communicators are created once per device set and reused.
 #include <rccl/rccl.h>
 
 #include <algorithm>
 #include <cmath>
 #include <cstring>
+#include <map>
 #include <memory>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -26,13 +32,73 @@ int fail(int code, const std::string& msg) {
 
 namespace {
 
-// One SNP-column shard resident on one device.
-struct Shard {
+// ---- pooled fit contexts -----------------------------------------------------------------------
+
+struct FitCtx {
   int dev = 0;
   Stream stream;
+  DevBuf Xt, D8, mean, sd, keep, q, G, wsg, Y, A, gebv, mu, info, wss, B, msum, packed, out, part;
+};
+
+class CtxPool {
+ public:
+  int acquire(int dev, std::unique_ptr<FitCtx>& out) {
+    {
+      std::lock_guard<std::mutex> lock(mu_);
+      auto& v = idle_[dev];
+      if (!v.empty()) {
+        out = std::move(v.back());
+        v.pop_back();
+        return GBM_OK;
+      }
+    }
+    auto c = std::make_unique<FitCtx>();
+    c->dev = dev;
+    c->stream.dev = dev;
+    GBM_HIP_TRY(hipSetDevice(dev));
+    GBM_HIP_TRY(hipStreamCreateWithFlags(&c->stream.s, hipStreamNonBlocking));
+    out = std::move(c);
+    return GBM_OK;
+  }
+  void release(std::unique_ptr<FitCtx> c) {
+    // nothing of this call may still run on the context's stream when another call takes it
+    (void)hipSetDevice(c->dev);
+    if (hipStreamSynchronize(c->stream.s) != hipSuccess) {
+      (void)hipGetLastError();
+      return;  // a broken context is dropped (its destructor frees what it can)
+    }
+    std::lock_guard<std::mutex> lock(mu_);
+    idle_[c->dev].push_back(std::move(c));
+  }
+  void clear() {
+    std::map<int, std::vector<std::unique_ptr<FitCtx>>> drop;
+    {
+      std::lock_guard<std::mutex> lock(mu_);
+      drop.swap(idle_);
+    }
+  }
+
+ private:
+  std::mutex mu_;
+  std::map<int, std::vector<std::unique_ptr<FitCtx>>> idle_;
+};
+
+// never destroyed: pooled device memory must not be freed after the HIP runtime tears down
+CtxPool& pool() {
+  static CtxPool* p = new CtxPool;
+  return *p;
+}
+
+// One SNP-column shard [j0, j0 + p) on a leased context.
+struct Shard {
+  std::unique_ptr<FitCtx> c;
   int64_t j0 = 0, p = 0;
-  DevMem Xt, D8, mean, sd, keep, q, G, wsg, Y, A, gebv, mu, info, wss, B, msum;
   int64_t q_host = 0;
+  int leader = -1;  // index of the shard that holds this device's summed GRM (itself if first)
+  ~Shard() {
+    if (c) pool().release(std::move(c));
+  }
+  FitCtx& x() { return *c; }
 };
 
 enum class Source { F64, I8, SYNTH };
@@ -46,81 +112,141 @@ struct Problem {
   uint64_t seed = 0;  // Source::SYNTH: genotypes generated on each device
 };
 
-// Upload the shard's columns and standardise them; reads back the shard's kept count.
-int prepare_shard(const Problem& pr, Shard& sh) {
-  const int64_t n = pr.n, npad = npad_of(n), pl = sh.p;
-  GBM_HIP_TRY(hipSetDevice(sh.dev));
-  sh.stream.dev = sh.dev;
-  GBM_HIP_TRY(hipStreamCreateWithFlags(&sh.stream.s, hipStreamNonBlocking));
-  hipStream_t s = sh.stream.s;
-  GBM_TRY(dalloc(sh.Xt, sh.dev, pl * npad * 8));
-  GBM_TRY(dalloc(sh.mean, sh.dev, pl * 8));
-  GBM_TRY(dalloc(sh.sd, sh.dev, pl * 8));
-  GBM_TRY(dalloc(sh.keep, sh.dev, pl * 4));
-  GBM_TRY(dalloc(sh.q, sh.dev, 8));
-  if (pr.src == Source::F64) {
-    GBM_HIP_TRY(hipMemcpy2DAsync(sh.Xt.p, npad * 8, pr.X + sh.j0 * pr.ld, pr.ld * 8, n * 8, pl, hipMemcpyHostToDevice, s));
-  } else if (pr.src == Source::SYNTH) {
-    GBM_TRY(gbm_dev_synth_genotypes((double*)sh.Xt.p, npad, pl, n, pr.seed, sh.j0, s));
-  } else {
-    GBM_TRY(dalloc(sh.D8, sh.dev, pl * n));
-    GBM_HIP_TRY(hipMemcpy2DAsync(sh.D8.p, n, pr.D + sh.j0 * pr.ld, pr.ld, n, pl, hipMemcpyHostToDevice, s));
-    GBM_TRY(gbm_dev_expand_dosage_i8((const int8_t*)sh.D8.p, n, n, pl, pr.ploidy, (double*)sh.Xt.p, npad, s));
+// Contiguous SNP-column blocks, one per listed device; leader = first shard on each device.
+int make_shards(const std::vector<int>& devs, int64_t p, std::vector<std::unique_ptr<Shard>>& shards) {
+  const int nd = (int)std::min<int64_t>((int64_t)devs.size(), p);
+  const int64_t per = (p + nd - 1) / nd;
+  for (int k = 0; k < nd; k++) {
+    const int64_t j0 = k * per;
+    if (j0 >= p) break;
+    auto sh = std::make_unique<Shard>();
+    GBM_TRY(pool().acquire(devs[k], sh->c));
+    sh->j0 = j0;
+    sh->p = std::min(per, p - j0);
+    for (size_t m = 0; m < shards.size(); m++)
+      if (shards[m]->x().dev == devs[k]) {
+        sh->leader = shards[m]->leader;
+        break;
+      }
+    if (sh->leader < 0) sh->leader = (int)shards.size();
+    shards.push_back(std::move(sh));
   }
-  GBM_HIP_TRY(hipMemsetAsync(sh.q.p, 0, 8, s));
-  GBM_TRY(gbm_dev_standardize((const double*)sh.Xt.p, npad, pl, n, (double*)sh.Xt.p, npad, (double*)sh.mean.p,
-                              (double*)sh.sd.p,
-                              (int32_t*)sh.keep.p, (int64_t*)sh.q.p, s));
-  GBM_HIP_TRY(hipMemcpyAsync(&sh.q_host, sh.q.p, 8, hipMemcpyDeviceToHost, s));
+  return GBM_OK;
+}
+
+// Upload the shard's columns and standardise them in place; reads back the shard's kept count.
+int prepare_shard(const Problem& pr, Shard& sh) {
+  FitCtx& c = sh.x();
+  const int64_t n = pr.n, npad = npad_of(n), pl = sh.p;
+  GBM_HIP_TRY(hipSetDevice(c.dev));
+  hipStream_t s = c.stream.s;
+  GBM_TRY(ensure(c.Xt, c.dev, pl * npad * 8));
+  GBM_TRY(ensure(c.mean, c.dev, pl * 8));
+  GBM_TRY(ensure(c.sd, c.dev, pl * 8));
+  GBM_TRY(ensure(c.keep, c.dev, pl * 4));
+  GBM_TRY(ensure(c.q, c.dev, 8));
+  if (pr.src == Source::F64) {
+    GBM_HIP_TRY(hipMemcpy2DAsync(c.Xt.p, npad * 8, pr.X + sh.j0 * pr.ld, pr.ld * 8, n * 8, pl, hipMemcpyHostToDevice, s));
+    if (npad > n) GBM_HIP_TRY(hipMemset2DAsync((double*)c.Xt.p + n, npad * 8, 0, (npad - n) * 8, pl, s));
+  } else if (pr.src == Source::SYNTH) {
+    GBM_TRY(gbm_dev_synth_genotypes((double*)c.Xt.p, npad, pl, n, pr.seed, sh.j0, s));
+  } else {
+    GBM_TRY(ensure(c.D8, c.dev, pl * n));
+    GBM_HIP_TRY(hipMemcpy2DAsync(c.D8.p, n, pr.D + sh.j0 * pr.ld, pr.ld, n, pl, hipMemcpyHostToDevice, s));
+    GBM_TRY(gbm_dev_expand_dosage_i8((const int8_t*)c.D8.p, n, n, pl, pr.ploidy, (double*)c.Xt.p, npad, s));
+  }
+  GBM_HIP_TRY(hipMemsetAsync(c.q.p, 0, 8, s));
+  GBM_TRY(gbm_dev_standardize((const double*)c.Xt.p, npad, pl, n, (double*)c.Xt.p, npad, (double*)c.mean.p,
+                              (double*)c.sd.p, (int32_t*)c.keep.p, (int64_t*)c.q.p, s));
+  GBM_HIP_TRY(hipMemcpyAsync(&sh.q_host, c.q.p, 8, hipMemcpyDeviceToHost, s));
   GBM_HIP_TRY(hipStreamSynchronize(s));
   return GBM_OK;
 }
 
 int grm_shard(const Problem& pr, Shard& sh) {
+  FitCtx& c = sh.x();
   const int64_t n = pr.n, npad = npad_of(n), gdim = gdim_of(n);
-  GBM_HIP_TRY(hipSetDevice(sh.dev));
-  GBM_TRY(dalloc(sh.G, sh.dev, gdim * gdim * 8));
+  GBM_HIP_TRY(hipSetDevice(c.dev));
+  GBM_TRY(ensure(c.G, c.dev, gdim * gdim * 8));
   const int64_t wsb = gbm_dev_grm_workspace(n, sh.p);
-  GBM_TRY(dalloc(sh.wsg, sh.dev, wsb));
-  return gbm_dev_grm((const double*)sh.Xt.p, npad, sh.p, n, (double*)sh.G.p, gdim, sh.wsg.p, wsb, sh.stream.s);
+  GBM_TRY(ensure(c.wsg, c.dev, wsb));
+  return gbm_dev_grm((const double*)c.Xt.p, npad, sh.p, n, (double*)c.G.p, gdim, c.wsg.p, wsb, c.stream.s);
 }
 
-const char* nccl_msg(ncclResult_t r) { return ncclGetErrorString(r); }
+// ---- RCCL communicators, one set per distinct device list, created once ----------------------
 
-// Sum the partial GRMs across devices: the upper 128-tiles packed contiguously (half the bytes
-// of G's rows), all-reduced, unpacked.
+struct CommSet {
+  std::vector<ncclComm_t> comms;
+  std::mutex mu;  // one collective at a time on a communicator (same op order on every device)
+};
+
+int comm_set(const std::vector<int>& devs, CommSet** out) {
+  static std::mutex mu;
+  static auto* cache = new std::map<std::vector<int>, std::unique_ptr<CommSet>>;  // never destroyed
+  std::lock_guard<std::mutex> lock(mu);
+  auto it = cache->find(devs);
+  if (it == cache->end()) {
+    auto cs = std::make_unique<CommSet>();
+    cs->comms.resize(devs.size());
+    ncclResult_t r = ncclCommInitAll(cs->comms.data(), (int)devs.size(), devs.data());
+    if (r != ncclSuccess) return fail(GBM_E_RCCL, std::string("ncclCommInitAll: ") + ncclGetErrorString(r));
+    it = cache->emplace(devs, std::move(cs)).first;
+  }
+  *out = it->second.get();
+  return GBM_OK;
+}
+
+// Sum the partial GRMs of all shards into each device leader's G: the upper 128-tiles packed
+// contiguously (half the bytes of G's rows); shards on one device added there in shard order,
+// then the leaders all-reduced over RCCL (xGMI), then unpacked.
 int allreduce_grm(std::vector<std::unique_ptr<Shard>>& shards, int64_t n) {
   if (shards.size() < 2) return GBM_OK;
   const int64_t gdim = gdim_of(n), psz = gbm_dev_grm_packed_size(n);
-  std::vector<int> devs;
-  for (auto& sh : shards) devs.push_back(sh->dev);
-  std::vector<std::unique_ptr<DevMem>> packed;
   for (auto& sh : shards) {
-    packed.push_back(std::make_unique<DevMem>());
-    GBM_HIP_TRY(hipSetDevice(sh->dev));
-    GBM_TRY(dalloc(*packed.back(), sh->dev, psz * 8));
-    GBM_TRY(gbm_dev_grm_pack((const double*)sh->G.p, gdim, n, (double*)packed.back()->p, sh->stream.s));
+    FitCtx& c = sh->x();
+    GBM_HIP_TRY(hipSetDevice(c.dev));
+    GBM_TRY(ensure(c.packed, c.dev, psz * 8));
+    GBM_TRY(gbm_dev_grm_pack((const double*)c.G.p, gdim, n, (double*)c.packed.p, c.stream.s));
   }
-  std::vector<ncclComm_t> comms(shards.size());
-  ncclResult_t r = ncclCommInitAll(comms.data(), (int)devs.size(), devs.data());
-  if (r != ncclSuccess) return fail(GBM_E_RCCL, std::string("ncclCommInitAll: ") + nccl_msg(r));
-  int rc = GBM_OK;
-  r = ncclGroupStart();
-  for (size_t k = 0; k < shards.size() && r == ncclSuccess; k++)
-    r = ncclAllReduce(packed[k]->p, packed[k]->p, (size_t)psz, ncclDouble, ncclSum, comms[k], shards[k]->stream.s);
-  ncclResult_t r2 = ncclGroupEnd();
-  if (r != ncclSuccess || r2 != ncclSuccess)
-    rc = fail(GBM_E_RCCL, std::string("ncclAllReduce(partial GRM): ") + nccl_msg(r != ncclSuccess ? r : r2));
-  for (size_t k = 0; k < shards.size() && rc == GBM_OK; k++) {
-    (void)hipSetDevice(shards[k]->dev);
-    rc = gbm_dev_grm_unpack((const double*)packed[k]->p, n, (double*)shards[k]->G.p, gdim, shards[k]->stream.s);
+  std::vector<int> leaders, devs;
+  for (size_t k = 0; k < shards.size(); k++) {
+    Shard& sh = *shards[k];
+    if (sh.leader == (int)k) {
+      leaders.push_back((int)k);
+      devs.push_back(sh.x().dev);
+      continue;
+    }
+    FitCtx& lc = shards[sh.leader]->x();
+    GBM_HIP_TRY(hipSetDevice(lc.dev));
+    GBM_HIP_TRY(hipStreamSynchronize(sh.x().stream.s));
+    GBM_TRY(launch_add_inplace((double*)lc.packed.p, (const double*)sh.x().packed.p, psz, lc.stream.s));
   }
-  for (auto& sh : shards) {
-    (void)hipSetDevice(sh->dev);
-    if (hipStreamSynchronize(sh->stream.s) != hipSuccess && rc == GBM_OK) rc = fail(GBM_E_HIP, "stream sync after all-reduce");
+  if (leaders.size() > 1) {
+    CommSet* cs = nullptr;
+    GBM_TRY(comm_set(devs, &cs));
+    std::lock_guard<std::mutex> lock(cs->mu);
+    int rc = GBM_OK;
+    ncclResult_t r = ncclGroupStart();
+    for (size_t k = 0; k < leaders.size() && r == ncclSuccess; k++) {
+      FitCtx& c = shards[leaders[k]]->x();
+      r = ncclAllReduce(c.packed.p, c.packed.p, (size_t)psz, ncclDouble, ncclSum, cs->comms[k], c.stream.s);
+    }
+    ncclResult_t r2 = ncclGroupEnd();
+    if (r != ncclSuccess || r2 != ncclSuccess)
+      rc = fail(GBM_E_RCCL, std::string("ncclAllReduce(partial GRM): ") + ncclGetErrorString(r != ncclSuccess ? r : r2));
+    for (int k : leaders) {  // complete the collective while holding the communicator
+      FitCtx& c = shards[k]->x();
+      (void)hipSetDevice(c.dev);
+      if (hipStreamSynchronize(c.stream.s) != hipSuccess && rc == GBM_OK) rc = fail(GBM_E_HIP, "stream sync after all-reduce");
+    }
+    if (rc != GBM_OK) return rc;
   }
-  for (auto c : comms) (void)ncclCommDestroy(c);
-  return rc;
+  for (int k : leaders) {
+    FitCtx& c = shards[k]->x();
+    GBM_HIP_TRY(hipSetDevice(c.dev));
+    GBM_TRY(gbm_dev_grm_unpack((const double*)c.packed.p, n, (double*)c.G.p, gdim, c.stream.s));
+  }
+  return GBM_OK;
 }
 
 int run_fit(const Problem& pr, const double* Y, int64_t ldy, int64_t nrhs, double lambda, const int* devices, int ndev,
@@ -134,17 +260,8 @@ int run_fit(const Problem& pr, const double* Y, int64_t ldy, int64_t nrhs, doubl
   std::vector<int> devs;
   GBM_TRY(check_devices(devices, ndev, devs));
   const int64_t npad = npad_of(n), gdim = gdim_of(n);
-  const int nd = (int)std::min<int64_t>((int64_t)devs.size(), p);
-  const int64_t per = (p + nd - 1) / nd;
   std::vector<std::unique_ptr<Shard>> shards;
-  for (int k = 0; k < nd; k++) {
-    auto sh = std::make_unique<Shard>();
-    sh->dev = devs[k];
-    sh->j0 = k * per;
-    sh->p = std::min(per, p - sh->j0);
-    if (sh->p <= 0) break;
-    shards.push_back(std::move(sh));
-  }
+  GBM_TRY(make_shards(devs, p, shards));
   int64_t q = 0;
   for (auto& sh : shards) {
     GBM_TRY(prepare_shard(pr, *sh));
@@ -155,54 +272,65 @@ int run_fit(const Problem& pr, const double* Y, int64_t ldy, int64_t nrhs, doubl
   for (auto& sh : shards) GBM_TRY(grm_shard(pr, *sh));
   GBM_TRY(allreduce_grm(shards, n));
   const double inv_q = 1.0 / (double)q;
-  std::vector<double> msum_total(nrhs, 0.0), mu(nrhs, 0.0);
-  // every shard solves the (identical) n x n system redundantly, all devices at once: a is then
-  // local to each shard's marker back-solve with no broadcast
+  // each device leader solves the (identical) n x n system, all devices at once: a is then local
+  // to every shard's marker back-solve (same-device shards copy it from their leader)
   std::vector<int32_t> infos(shards.size(), 0);
   for (size_t k = 0; k < shards.size(); k++) {
     Shard& sh = *shards[k];
-    GBM_HIP_TRY(hipSetDevice(sh.dev));
-    hipStream_t s = sh.stream.s;
-    GBM_TRY(dalloc(sh.Y, sh.dev, nrhs * npad * 8));
-    GBM_TRY(dalloc(sh.A, sh.dev, nrhs * npad * 8));
-    GBM_TRY(dalloc(sh.gebv, sh.dev, nrhs * npad * 8));
-    GBM_TRY(dalloc(sh.mu, sh.dev, nrhs * 8));
-    GBM_TRY(dalloc(sh.info, sh.dev, 4));
+    FitCtx& c = sh.x();
+    GBM_HIP_TRY(hipSetDevice(c.dev));
+    hipStream_t s = c.stream.s;
+    GBM_TRY(ensure(c.A, c.dev, nrhs * npad * 8));
+    GBM_TRY(ensure(c.B, c.dev, nrhs * sh.p * 8));
+    GBM_TRY(ensure(c.msum, c.dev, nrhs * 8));
+    if (sh.leader != (int)k) continue;
+    GBM_TRY(ensure(c.Y, c.dev, nrhs * npad * 8));
+    GBM_TRY(ensure(c.gebv, c.dev, nrhs * npad * 8));
+    GBM_TRY(ensure(c.mu, c.dev, nrhs * 8));
+    GBM_TRY(ensure(c.info, c.dev, 4));
     const int64_t wss = gbm_dev_solve_workspace(n, nrhs);
-    GBM_TRY(dalloc(sh.wss, sh.dev, wss));
-    GBM_TRY(dalloc(sh.B, sh.dev, nrhs * sh.p * 8));
-    GBM_TRY(dalloc(sh.msum, sh.dev, nrhs * 8));
-    GBM_HIP_TRY(hipMemcpy2DAsync(sh.Y.p, npad * 8, Y, ldy * 8, n * 8, nrhs, hipMemcpyHostToDevice, s));
-    GBM_TRY(gbm_dev_gblup_solve((double*)sh.G.p, gdim, n, inv_q, nullptr, lambda, (const double*)sh.Y.p, npad, nrhs,
-                                (double*)sh.A.p, (double*)sh.gebv.p, npad, (double*)sh.mu.p, (int32_t*)sh.info.p,
-                                sh.wss.p, wss, s));
-    GBM_HIP_TRY(hipMemcpyAsync(&infos[k], sh.info.p, 4, hipMemcpyDeviceToHost, s));
+    GBM_TRY(ensure(c.wss, c.dev, wss));
+    GBM_HIP_TRY(hipMemcpy2DAsync(c.Y.p, npad * 8, Y, ldy * 8, n * 8, nrhs, hipMemcpyHostToDevice, s));
+    GBM_TRY(gbm_dev_gblup_solve((double*)c.G.p, gdim, n, inv_q, nullptr, lambda, (const double*)c.Y.p, npad, nrhs,
+                                (double*)c.A.p, (double*)c.gebv.p, npad, (double*)c.mu.p, (int32_t*)c.info.p, c.wss.p,
+                                wss, s));
+    GBM_HIP_TRY(hipMemcpyAsync(&infos[k], c.info.p, 4, hipMemcpyDeviceToHost, s));
   }
-  std::vector<std::vector<double>> msums(shards.size(), std::vector<double>(nrhs, 0.0));
   for (size_t k = 0; k < shards.size(); k++) {
-    Shard& sh = *shards[k];
-    GBM_HIP_TRY(hipSetDevice(sh.dev));
-    hipStream_t s = sh.stream.s;
-    GBM_HIP_TRY(hipStreamSynchronize(s));
+    if (shards[k]->leader != (int)k) continue;
+    FitCtx& c = shards[k]->x();
+    GBM_HIP_TRY(hipSetDevice(c.dev));
+    GBM_HIP_TRY(hipStreamSynchronize(c.stream.s));
     const int32_t info = infos[k];
     if (info < 0) return fail(GBM_E_HIP, "back substitution: block synchronisation timed out");
     if (info != 0)
       return fail(GBM_E_NOTPD, "G/q + lambda*I is not positive definite (pivot " + std::to_string(info) +
                                    "); check for non-finite genotypes");
-    GBM_TRY(gbm_dev_marker_effects((const double*)sh.Xt.p, npad, sh.p, n, (const double*)sh.A.p, npad, nrhs, inv_q,
-                                   nullptr, (const double*)sh.mean.p, (const double*)sh.sd.p, (const int32_t*)sh.keep.p,
-                                   (double*)sh.B.p, sh.p, (double*)sh.msum.p, s));
-    GBM_HIP_TRY(hipMemcpy2DAsync(b_hat_out + 1 + sh.j0, (p + 1) * 8, sh.B.p, sh.p * 8, sh.p * 8, nrhs,
+  }
+  std::vector<std::vector<double>> msums(shards.size(), std::vector<double>(nrhs, 0.0));
+  std::vector<double> mu(nrhs, 0.0);
+  for (size_t k = 0; k < shards.size(); k++) {
+    Shard& sh = *shards[k];
+    FitCtx& c = sh.x();
+    GBM_HIP_TRY(hipSetDevice(c.dev));
+    hipStream_t s = c.stream.s;
+    if (sh.leader != (int)k)
+      GBM_HIP_TRY(hipMemcpyAsync(c.A.p, shards[sh.leader]->x().A.p, nrhs * npad * 8, hipMemcpyDeviceToDevice, s));
+    GBM_TRY(gbm_dev_marker_effects((const double*)c.Xt.p, npad, sh.p, n, (const double*)c.A.p, npad, nrhs, inv_q,
+                                   nullptr, (const double*)c.mean.p, (const double*)c.sd.p, (const int32_t*)c.keep.p,
+                                   (double*)c.B.p, sh.p, (double*)c.msum.p, s));
+    GBM_HIP_TRY(hipMemcpy2DAsync(b_hat_out + 1 + sh.j0, (p + 1) * 8, c.B.p, sh.p * 8, sh.p * 8, nrhs,
                                  hipMemcpyDeviceToHost, s));
-    GBM_HIP_TRY(hipMemcpyAsync(msums[k].data(), sh.msum.p, nrhs * 8, hipMemcpyDeviceToHost, s));
+    GBM_HIP_TRY(hipMemcpyAsync(msums[k].data(), c.msum.p, nrhs * 8, hipMemcpyDeviceToHost, s));
     if (k == 0) {
-      GBM_HIP_TRY(hipMemcpy2DAsync(y_pred_out, n * 8, sh.gebv.p, npad * 8, n * 8, nrhs, hipMemcpyDeviceToHost, s));
-      GBM_HIP_TRY(hipMemcpyAsync(mu.data(), sh.mu.p, nrhs * 8, hipMemcpyDeviceToHost, s));
+      GBM_HIP_TRY(hipMemcpy2DAsync(y_pred_out, n * 8, c.gebv.p, npad * 8, n * 8, nrhs, hipMemcpyDeviceToHost, s));
+      GBM_HIP_TRY(hipMemcpyAsync(mu.data(), c.mu.p, nrhs * 8, hipMemcpyDeviceToHost, s));
     }
   }
+  std::vector<double> msum_total(nrhs, 0.0);
   for (size_t k = 0; k < shards.size(); k++) {
-    GBM_HIP_TRY(hipSetDevice(shards[k]->dev));
-    GBM_HIP_TRY(hipStreamSynchronize(shards[k]->stream.s));
+    GBM_HIP_TRY(hipSetDevice(shards[k]->x().dev));
+    GBM_HIP_TRY(hipStreamSynchronize(shards[k]->x().stream.s));
     for (int64_t t = 0; t < nrhs; t++) msum_total[t] += msums[k][t];  // shard order: deterministic
   }
   for (int64_t t = 0; t < nrhs; t++) {
@@ -231,6 +359,13 @@ extern "C" int gbm_device_count(int* count) {
     return e == hipErrorNoDevice ? GBM_OK : fail(GBM_E_HIP, std::string("hipGetDeviceCount: ") + hipGetErrorString(e));
   }
   *count = c;
+  return GBM_OK;
+}
+
+extern "C" int64_t gbm_device_allocations(void) { return alloc_counter().load(std::memory_order_relaxed); }
+
+extern "C" int gbm_release_device_cache(void) {
+  pool().clear();
   return GBM_OK;
 }
 
@@ -265,17 +400,8 @@ extern "C" int gbm_grm(const double* X, int64_t n, int64_t p, int64_t ldx, const
   std::vector<int> devs;
   GBM_TRY(check_devices(devices, ndev, devs));
   Problem pr{Source::F64, X, nullptr, 1, n, p, ldx};
-  const int nd = (int)std::min<int64_t>((int64_t)devs.size(), p);
-  const int64_t per = (p + nd - 1) / nd;
   std::vector<std::unique_ptr<Shard>> shards;
-  for (int k = 0; k < nd; k++) {
-    auto sh = std::make_unique<Shard>();
-    sh->dev = devs[k];
-    sh->j0 = k * per;
-    sh->p = std::min(per, p - sh->j0);
-    if (sh->p <= 0) break;
-    shards.push_back(std::move(sh));
-  }
+  GBM_TRY(make_shards(devs, p, shards));
   int64_t q = 0;
   for (auto& sh : shards) {
     GBM_TRY(prepare_shard(pr, *sh));
@@ -285,13 +411,12 @@ extern "C" int gbm_grm(const double* X, int64_t n, int64_t p, int64_t ldx, const
   if (q == 0) return fail(GBM_E_DATA, "no polymorphic locus-allele");
   for (auto& sh : shards) GBM_TRY(grm_shard(pr, *sh));
   GBM_TRY(allreduce_grm(shards, n));
-  Shard& sh = *shards[0];
-  GBM_HIP_TRY(hipSetDevice(sh.dev));
-  DevMem out;
-  GBM_TRY(dalloc(out, sh.dev, n * n * 8));
-  GBM_TRY(launch_grm_export((const double*)sh.G.p, gdim_of(n), n, 1.0 / (double)q, (double*)out.p, n, sh.stream.s));
-  GBM_HIP_TRY(hipMemcpy2DAsync(G_out, ldg * 8, out.p, n * 8, n * 8, n, hipMemcpyDeviceToHost, sh.stream.s));
-  GBM_HIP_TRY(hipStreamSynchronize(sh.stream.s));
+  FitCtx& c = shards[0]->x();
+  GBM_HIP_TRY(hipSetDevice(c.dev));
+  GBM_TRY(ensure(c.out, c.dev, n * n * 8));
+  GBM_TRY(launch_grm_export((const double*)c.G.p, gdim_of(n), n, 1.0 / (double)q, (double*)c.out.p, n, c.stream.s));
+  GBM_HIP_TRY(hipMemcpy2DAsync(G_out, ldg * 8, c.out.p, n * 8, n * 8, n, hipMemcpyDeviceToHost, c.stream.s));
+  GBM_HIP_TRY(hipStreamSynchronize(c.stream.s));
   return GBM_OK;
 }
 
@@ -301,19 +426,19 @@ extern "C" int gbm_colstats(const double* X, int64_t n, int64_t p, int64_t ldx, 
   std::vector<int> devs;
   GBM_TRY(check_devices(&device, 1, devs));
   Problem pr{Source::F64, X, nullptr, 1, n, p, ldx};
-  Shard sh;
-  sh.dev = devs[0];
-  sh.j0 = 0;
-  sh.p = p;
+  std::vector<std::unique_ptr<Shard>> shards;
+  GBM_TRY(make_shards(devs, p, shards));
+  Shard& sh = *shards[0];
   GBM_TRY(prepare_shard(pr, sh));
   if (q_out) *q_out = sh.q_host;
-  hipStream_t s = sh.stream.s;
-  if (mean_out) GBM_HIP_TRY(hipMemcpyAsync(mean_out, sh.mean.p, p * 8, hipMemcpyDeviceToHost, s));
-  if (sd_out) GBM_HIP_TRY(hipMemcpyAsync(sd_out, sh.sd.p, p * 8, hipMemcpyDeviceToHost, s));
+  FitCtx& c = sh.x();
+  hipStream_t s = c.stream.s;
+  if (mean_out) GBM_HIP_TRY(hipMemcpyAsync(mean_out, c.mean.p, p * 8, hipMemcpyDeviceToHost, s));
+  if (sd_out) GBM_HIP_TRY(hipMemcpyAsync(sd_out, c.sd.p, p * 8, hipMemcpyDeviceToHost, s));
   std::vector<int32_t> k32;
   if (keep_out) {
     k32.resize(p);
-    GBM_HIP_TRY(hipMemcpyAsync(k32.data(), sh.keep.p, p * 4, hipMemcpyDeviceToHost, s));
+    GBM_HIP_TRY(hipMemcpyAsync(k32.data(), c.keep.p, p * 4, hipMemcpyDeviceToHost, s));
   }
   GBM_HIP_TRY(hipStreamSynchronize(s));
   if (keep_out)
@@ -327,22 +452,25 @@ extern "C" int gbm_predict(const double* X, int64_t n, int64_t p, int64_t ldx, c
     return fail(GBM_E_ARG, "gbm_predict: bad arguments");
   std::vector<int> devs;
   GBM_TRY(check_devices(&device, 1, devs));
-  const int dev = devs[0];
-  GBM_HIP_TRY(hipSetDevice(dev));
-  Stream st;
-  st.dev = dev;
-  GBM_HIP_TRY(hipStreamCreateWithFlags(&st.s, hipStreamNonBlocking));
-  DevMem Xt, b, part, o;
+  std::unique_ptr<FitCtx> lease;
+  GBM_TRY(pool().acquire(devs[0], lease));
+  struct Release {
+    std::unique_ptr<FitCtx>& c;
+    ~Release() { pool().release(std::move(c)); }
+  } release{lease};
+  FitCtx& c = *lease;
+  GBM_HIP_TRY(hipSetDevice(c.dev));
+  hipStream_t s = c.stream.s;
   const int64_t nchunks = predict_chunks(n, p);
-  GBM_TRY(dalloc(Xt, dev, p * n * 8));
-  GBM_TRY(dalloc(b, dev, nrhs * (p + 1) * 8));
-  GBM_TRY(dalloc(part, dev, nchunks * nrhs * n * 8));
-  GBM_TRY(dalloc(o, dev, nrhs * n * 8));
-  GBM_HIP_TRY(hipMemcpy2DAsync(Xt.p, n * 8, X, ldx * 8, n * 8, p, hipMemcpyHostToDevice, st.s));
-  GBM_HIP_TRY(hipMemcpy2DAsync(b.p, (p + 1) * 8, b_hat, ldb * 8, (p + 1) * 8, nrhs, hipMemcpyHostToDevice, st.s));
-  GBM_TRY(launch_predict((const double*)Xt.p, n, p, n, (const double*)b.p, p + 1, nrhs, (double*)part.p, nchunks,
-                         (double*)o.p, n, st.s));
-  GBM_HIP_TRY(hipMemcpy2DAsync(out, ldo * 8, o.p, n * 8, n * 8, nrhs, hipMemcpyDeviceToHost, st.s));
-  GBM_HIP_TRY(hipStreamSynchronize(st.s));
+  GBM_TRY(ensure(c.Xt, c.dev, p * n * 8));
+  GBM_TRY(ensure(c.B, c.dev, nrhs * (p + 1) * 8));
+  GBM_TRY(ensure(c.part, c.dev, nchunks * nrhs * n * 8));
+  GBM_TRY(ensure(c.out, c.dev, nrhs * n * 8));
+  GBM_HIP_TRY(hipMemcpy2DAsync(c.Xt.p, n * 8, X, ldx * 8, n * 8, p, hipMemcpyHostToDevice, s));
+  GBM_HIP_TRY(hipMemcpy2DAsync(c.B.p, (p + 1) * 8, b_hat, ldb * 8, (p + 1) * 8, nrhs, hipMemcpyHostToDevice, s));
+  GBM_TRY(launch_predict((const double*)c.Xt.p, n, p, n, (const double*)c.B.p, p + 1, nrhs, (double*)c.part.p, nchunks,
+                         (double*)c.out.p, n, s));
+  GBM_HIP_TRY(hipMemcpy2DAsync(out, ldo * 8, c.out.p, n * 8, n * 8, nrhs, hipMemcpyDeviceToHost, s));
+  GBM_HIP_TRY(hipStreamSynchronize(s));
   return GBM_OK;
 }

@@ -38,5 +38,6 @@ int launch_grm_export(const double* G, int64_t ldg, int64_t n, double inv_q, dou
 int launch_predict(const double* Xt, int64_t ldx, int64_t p, int64_t n, const double* b, int64_t ldb, int64_t nrhs,
                    double* partial, int64_t nchunks, double* out, int64_t ldo, hipStream_t s);
 int64_t predict_chunks(int64_t n, int64_t p);
+int launch_add_inplace(double* a, const double* b, int64_t n, hipStream_t s);
 
 }  // namespace gbm

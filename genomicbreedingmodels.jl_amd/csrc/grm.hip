@@ -1025,6 +1025,31 @@ extern "C" int gbm_dev_grm_slices(int64_t n, int64_t p) {
 }
 
 namespace gbm {
+// a += b over n doubles (fixed order per element): the sum of two packed partial GRMs of SNP
+// shards that live on the same device (capi.cpp), before the RCCL all-reduce across devices.
+__global__ void __launch_bounds__(256) add_inplace_kernel(double* __restrict__ a, const double* __restrict__ b,
+                                                          int64_t n) {
+  for (int64_t i = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 2; i < n; i += (int64_t)gridDim.x * 512) {
+    if (i + 1 < n) {
+      double2 x = *reinterpret_cast<const double2*>(a + i);
+      const double2 y = *reinterpret_cast<const double2*>(b + i);
+      x.x += y.x;
+      x.y += y.y;
+      *reinterpret_cast<double2*>(a + i) = x;
+    } else {
+      a[i] += b[i];
+    }
+  }
+}
+
+int launch_add_inplace(double* a, const double* b, int64_t n, hipStream_t s) {
+  if (n <= 0) return GBM_OK;
+  const int64_t want = (n + 511) / 512;
+  add_inplace_kernel<<<(unsigned)(want < 8192 ? want : 8192), 256, 0, s>>>(a, b, n);
+  GBM_LAUNCH_CHECK();
+  return GBM_OK;
+}
+
 // out[i, j] = inv_q * G[min(i,j), max(i,j)] for i, j < n (full symmetric export of the upper-stored GRM)
 __global__ void __launch_bounds__(256) grm_export_kernel(const double* __restrict__ G, int64_t ldg, int64_t n,
                                                          double inv_q, double* __restrict__ out, int64_t ldo) {

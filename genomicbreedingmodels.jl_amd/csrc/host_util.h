@@ -1,7 +1,9 @@
 // Host-side helpers shared by the libgbm entry points (capi.cpp, session.cpp): RAII device
 // buffers and streams, device-list and phenotype validation. Not part of the ABI.
 #pragma once
+#include <atomic>
 #include <cmath>
+#include <cstdlib>
 #include <string>
 #include <vector>
 
@@ -29,10 +31,18 @@ struct DevMem {
   }
 };
 
+// Device allocations made by libgbm since load (gbm_device_allocations): the pooled fit
+// contexts make a repeated call allocate nothing.
+inline std::atomic<int64_t>& alloc_counter() {
+  static std::atomic<int64_t> c{0};
+  return c;
+}
+
 inline int dalloc(DevMem& m, int dev, int64_t bytes) {
   m.reset();
   m.dev = dev;
   if (bytes <= 0) bytes = 16;
+  alloc_counter().fetch_add(1, std::memory_order_relaxed);
   hipError_t e = hipMalloc(&m.p, (size_t)bytes);
   if (e != hipSuccess) {
     m.p = nullptr;
@@ -42,6 +52,20 @@ inline int dalloc(DevMem& m, int dev, int64_t bytes) {
                     " failed: " + hipGetErrorString(e));
   }
   return GBM_OK;
+}
+
+// A device buffer that only grows: ensure() reallocates when the capacity is short, so a pooled
+// context reused for same-sized (or smaller) problems never calls hipMalloc again.
+struct DevBuf : DevMem {
+  int64_t cap = 0;
+};
+inline int ensure(DevBuf& b, int dev, int64_t bytes) {
+  if (bytes <= 0) bytes = 16;
+  if (b.p && b.dev == dev && b.cap >= bytes) return GBM_OK;
+  b.cap = 0;
+  int rc = dalloc(b, dev, bytes);
+  if (rc == GBM_OK) b.cap = bytes;
+  return rc;
 }
 
 struct Stream {
@@ -61,6 +85,12 @@ struct Stream {
     if (rc_ != GBM_OK) return rc_; \
   } while (0)
 
+// Device list of a call. Explicit `devices` (one SNP-column shard per entry; an ordinal may
+// repeat: shards on one device are summed on that device). With none given, the calling thread
+// gets ONE device, round-robin over GBM_DEVICES ("0,1,...", re-read per call; repeats allowed)
+// or over all visible devices: thread k (in order of first call) -> entry k mod len. That is the
+// thread -> GPU farming of SURVEY.md §8b under an unchanged cvmultithread! (reference
+// src/cross_validation.jl:159, Threads.@threads over model calls that pass no devices).
 inline int check_devices(const int* devices, int ndev, std::vector<int>& out) {
   int count = 0;
   hipError_t e = hipGetDeviceCount(&count);
@@ -70,14 +100,33 @@ inline int check_devices(const int* devices, int ndev, std::vector<int>& out) {
   }
   out.clear();
   if (!devices || ndev <= 0) {
-    out.push_back(0);
+    std::vector<int> pool;
+    if (const char* env = getenv("GBM_DEVICES")) {
+      for (const char* q = env; *q;) {
+        char* end = nullptr;
+        const long v = strtol(q, &end, 10);
+        if (end == q) {
+          q++;
+          continue;
+        }
+        if (v < 0 || v >= count)
+          return fail(GBM_E_ARG, "GBM_DEVICES: device ordinal " + std::to_string(v) + " out of range [0, " +
+                                     std::to_string(count) + ")");
+        pool.push_back((int)v);
+        q = end;
+      }
+    }
+    if (pool.empty())
+      for (int d = 0; d < count; d++) pool.push_back(d);
+    static std::atomic<int> next_slot{0};
+    thread_local int slot = -1;
+    if (slot < 0) slot = next_slot.fetch_add(1, std::memory_order_relaxed);
+    out.push_back(pool[(size_t)slot % pool.size()]);
   } else {
     for (int k = 0; k < ndev; k++) {
       if (devices[k] < 0 || devices[k] >= count)
         return fail(GBM_E_ARG, "device ordinal " + std::to_string(devices[k]) + " out of range [0, " +
                                    std::to_string(count) + ")");
-      for (int d : out)
-        if (d == devices[k]) return fail(GBM_E_ARG, "duplicate device ordinal " + std::to_string(d));
       out.push_back(devices[k]);
     }
   }

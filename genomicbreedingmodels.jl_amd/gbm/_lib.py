@@ -11,6 +11,7 @@ import threading
 
 import numpy as np
 
+ABI_VERSION = 200  # GBM_VERSION in include/gbm.h
 GBM_OK = 0
 GBM_E_ARG = -1
 GBM_E_NOTPD = -2
@@ -24,7 +25,7 @@ LIB_PATH = os.environ.get("GBM_LIBGBM") or os.path.join(os.path.dirname(os.path.
 
 # Every symbol include/gbm.h declares (tests check the export table against this list).
 EXPORTS = (
-    "gbm_version", "gbm_last_error", "gbm_device_count",
+    "gbm_version", "gbm_last_error", "gbm_device_count", "gbm_device_allocations", "gbm_release_device_cache",
     "gbm_gblup_fit", "gbm_gblup_fit_dosage_i8", "gbm_gblup_fit_synthetic", "gbm_grm", "gbm_colstats", "gbm_predict",
     "gbm_dev_npad", "gbm_dev_gdim", "gbm_dev_grm_workspace", "gbm_dev_solve_workspace",
     "gbm_dev_synth_genotypes", "gbm_dev_expand_dosage_i8", "gbm_dev_standardize", "gbm_dev_grm",
@@ -63,6 +64,10 @@ def _declare(lib):
     lib.gbm_last_error.argtypes = []
     lib.gbm_device_count.restype = I32
     lib.gbm_device_count.argtypes = [ctypes.POINTER(I32)]
+    lib.gbm_device_allocations.restype = I64
+    lib.gbm_device_allocations.argtypes = []
+    lib.gbm_release_device_cache.restype = I32
+    lib.gbm_release_device_cache.argtypes = []
     lib.gbm_gblup_fit.restype = I32
     lib.gbm_gblup_fit.argtypes = [P, I64, I64, I64, P, I64, I64, D, P, I32, P, P, P, P]
     lib.gbm_gblup_fit_dosage_i8.restype = I32
@@ -161,8 +166,8 @@ def load():
             _bind_runtime_first()
             _lib = _declare(ctypes.CDLL(LIB_PATH))
             v = _lib.gbm_version()
-            if v != 100:
-                raise ImportError(f"libgbm.so ABI version {v} != 100")
+            if v != ABI_VERSION:
+                raise ImportError(f"libgbm.so ABI version {v} != {ABI_VERSION}")
         return _lib
 
 

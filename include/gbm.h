@@ -22,8 +22,16 @@
  *    (`b_hat[1] .+ X*b_hat[2:end]`, src/prediction.jl:228) reproduces y_pred exactly.
  *  - Return codes: 0 on success, negative GBM_E_* on failure; gbm_last_error() returns a
  *    thread-local message for the last failing call on the calling thread.
- *  - Re-entrant: every call allocates its own stream and device workspace; concurrent
- *    calls (as `cvmultithread!` makes, src/cross_validation.jl:159) do not share state.
+ *  - Re-entrant: every call leases its own pooled context (stream + device buffers) per
+ *    SNP shard and returns it afterwards; concurrent calls (as `cvmultithread!` makes,
+ *    src/cross_validation.jl:159) never share one. Pooled buffers only grow, so repeated calls
+ *    of one shape allocate no device memory (gbm_device_allocations); gbm_release_device_cache
+ *    frees the idle ones.
+ *  - Devices: an explicit `devices` list gives one SNP-column shard per entry (an ordinal may
+ *    repeat). With devices == NULL / ndev == 0, each calling thread is given one device,
+ *    round-robin over GBM_DEVICES ("0,1,2,..."; re-read per call) or over all visible devices:
+ *    the k-th thread to call gets entry k mod len — folds farmed over the GPUs under an
+ *    unchanged `cvmultithread!`.
  */
 #ifndef GBM_H
 #define GBM_H
@@ -34,7 +42,7 @@
 extern "C" {
 #endif
 
-#define GBM_VERSION 100 /* 0.1.0 */
+#define GBM_VERSION 200 /* 0.2.0: pooled contexts, device farming, repeated device ordinals */
 
 #define GBM_OK 0
 #define GBM_E_ARG (-1)    /* bad argument (ArgumentError on the Julia side, src/prediction.jl:67-127 style) */
@@ -54,6 +62,12 @@ const char* gbm_last_error(void);
 /* Number of visible HIP devices (0 when none). Returns GBM_OK or GBM_E_HIP. */
 int gbm_device_count(int* count);
 
+/* Device allocations (hipMalloc calls) libgbm has made since it was loaded. */
+int64_t gbm_device_allocations(void);
+
+/* Free the idle pooled fit contexts (device buffers and streams kept between calls). */
+int gbm_release_device_cache(void);
+
 /* --------------------------------------------------------------------------------------
  * Host-buffer entry points (what a Julia `ccall` binds; buffers owned by the caller,
  * no pointer is retained after return).
@@ -66,9 +80,10 @@ int gbm_device_count(int* count);
  *   Y          n x nrhs column-major phenotypes (ldy >= n), already filtered for missing
  *              values (src/prediction.jl:114-124)
  *   lambda     λ = σ²_e/σ²_u > 0
- *   devices    device ordinals (NULL/ndev = 0: device 0). With ndev > 1 SNP columns are
- *              sharded into contiguous blocks, one per device, and the partial GRMs are
- *              summed with an RCCL all-reduce.
+ *   devices    device ordinals (NULL/ndev = 0: this thread's device, see "Devices" above).
+ *              With ndev > 1 SNP columns are sharded into contiguous blocks, one per entry;
+ *              the partial GRMs of shards on one device are added there, and summed across
+ *              devices with an RCCL all-reduce (communicators cached per device set).
  * Outputs (caller allocated):
  *   b_hat_out  (p+1) x nrhs column-major: [b0; b_1..b_p] per trait (src/linear.jl:218-221 layout)
  *   y_pred_out n x nrhs column-major GEBVs (= fitted values)

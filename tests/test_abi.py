@@ -34,7 +34,7 @@ def test_library_exports_every_header_symbol():
 
 def test_library_loads_and_reports_version():
     lib = gbm.load_library()
-    assert lib.gbm_version() == 100
+    assert lib.gbm_version() == 200
     assert isinstance(_lib.last_error(), str)
     for s in _lib.EXPORTS:
         assert hasattr(lib, s)

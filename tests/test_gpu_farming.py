@@ -1,0 +1,115 @@
+"""Drop-in device farming and the in-process multi-shard path of the C ABI (SURVEY.md §8b
+Threading, §8e):
+
+* explicit device lists with a repeated ordinal (devices=[0, 0]): SNP-column shards on one
+  device, their packed partial GRMs added on the device, the b_hat shard offsets and the Σ m_j b_j
+  assembly — against the oracle;
+* devices=NULL under an unchanged cvmultithread!: each calling thread is given one device from
+  GBM_DEVICES (round-robin by first call); eight threads at once are bit-identical to serial;
+* pooled contexts: after a warm-up call, a call of the same shape makes no device allocation.
+"""
+import threading
+
+import numpy as np
+import pytest
+
+import gbm
+import oracle
+from gbm import _lib
+
+pytestmark = pytest.mark.gpu
+
+
+def rel(a, b):
+    return float(np.abs(np.asarray(a) - np.asarray(b)).max() / max(np.abs(np.asarray(b)).max(), 1e-300))
+
+
+@pytest.mark.parametrize("devices", [[0, 0], [0, 0, 0]])
+@pytest.mark.parametrize("n,p,t", [(333, 1777, 3), (1030, 2501, 1)])
+def test_same_device_shards_match_oracle(devices, n, p, t):
+    X = oracle.synth_genotypes(n + p, n, p)
+    X[:, 5] = 0.5  # monomorphic locus inside shard 0
+    Y = oracle.synth_phenotypes(X, 11, ntraits=t)
+    b_hat, y_pred, mu, q = gbm.gblup_arrays(X, Y, lambda_=0.9, devices=devices)
+    ref = oracle.gblup_fit(X, Y, 0.9)
+    assert q == ref["q"]
+    assert rel(y_pred, ref["y_pred"]) < 1e-9
+    assert rel(mu, ref["mu"]) < 1e-9
+    assert rel(b_hat, ref["b_hat"]) < 1e-6
+    assert b_hat[1 + 5].tolist() == [0.0] * t
+    G, qg = gbm.grm(X, devices=devices)
+    Gr, qr = oracle.grm(X)
+    assert qg == qr and rel(G, Gr) < 1e-12
+
+
+def test_synthetic_fit_two_shards_one_device():
+    n, p = 700, 3001
+    X = oracle.synth_genotypes(4242, n, p)
+    Y = oracle.synth_phenotypes(X, 5, ntraits=2)
+    b1, y1, mu1, q1 = gbm.gblup_synthetic(4242, n, p, Y, devices=[0, 0])
+    ref = oracle.gblup_fit(X, Y, 1.0)
+    assert q1 == ref["q"] and rel(y1, ref["y_pred"]) < 1e-9 and rel(b1, ref["b_hat"]) < 1e-6
+
+
+def test_no_device_allocation_after_warmup():
+    lib = gbm.load_library()
+    X = oracle.synth_genotypes(21, 1030, 2000)
+    Y = oracle.synth_phenotypes(X, 22, ntraits=2)
+    first = gbm.gblup_arrays(X, Y, lambda_=1.0)
+    a0 = lib.gbm_device_allocations()
+    for _ in range(3):
+        again = gbm.gblup_arrays(X, Y, lambda_=1.0)
+        assert np.array_equal(again[1], first[1]) and np.array_equal(again[0], first[0])
+    gbm.gblup_arrays(X[:500], Y[:500], lambda_=1.0)  # smaller: fits the pooled buffers
+    assert lib.gbm_device_allocations() == a0
+    gbm.grm(X)
+    a1 = lib.gbm_device_allocations()
+    gbm.grm(X)
+    assert lib.gbm_device_allocations() == a1
+    _lib.check(lib.gbm_release_device_cache(), "release")
+    gbm.gblup_arrays(X, Y, lambda_=1.0)
+    assert lib.gbm_device_allocations() > a1  # the cache was really dropped
+
+
+def test_gbm_devices_farming_eight_threads(monkeypatch):
+    """cvmultithread! calls the model from Threads.@threads with no devices argument: every
+    thread takes its own slot of GBM_DEVICES. Eight threads on a one-GPU box (GBM_DEVICES lists
+    device 0 eight times) give the serial results bit for bit, and a second round of the same
+    shapes allocates nothing (each thread's call leases a pooled context)."""
+    monkeypatch.setenv("GBM_DEVICES", ",".join(["0"] * 8))
+    lib = gbm.load_library()
+    X = oracle.synth_genotypes(5, 1030, 1400)
+    cases = [oracle.synth_phenotypes(X, 300 + k, ntraits=2) for k in range(8)]
+    serial = [gbm.gblup_arrays(X, Y, lambda_=0.7) for Y in cases]
+
+    def round_of_threads():
+        out, errs = [None] * 8, []
+
+        def run(k):
+            try:
+                out[k] = gbm.gblup_arrays(X, cases[k], lambda_=0.7)
+            except Exception as e:  # reported below
+                errs.append(repr(e))
+
+        th = [threading.Thread(target=run, args=(k,)) for k in range(8)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        assert not errs, errs
+        return out
+
+    for a, b in zip(round_of_threads(), serial):
+        assert np.array_equal(a[1], b[1]) and np.array_equal(a[0], b[0])
+    a0 = lib.gbm_device_allocations()
+    for a, b in zip(round_of_threads(), serial):
+        assert np.array_equal(a[1], b[1]) and np.array_equal(a[0], b[0])
+    # new threads lease the pooled contexts of this shape: no allocation
+    assert lib.gbm_device_allocations() == a0
+
+
+def test_gbm_devices_bad_ordinal_is_an_argument_error(monkeypatch):
+    monkeypatch.setenv("GBM_DEVICES", "0,4096")
+    X = oracle.synth_genotypes(1, 50, 100)
+    with pytest.raises(gbm.ArgumentError):
+        gbm.gblup_arrays(X, np.arange(50.0))
