@@ -1,0 +1,172 @@
+"""The large BASELINE configs on one MI355X, checked (not just timed):
+
+* C3's per-GPU shape (n = 50 000 individuals, 75 000 loci = 600 000 / 8), X generated on the
+  device. At this n the GRM runs in its in-order carry accumulation mode (the slabs would exceed
+  4 GiB). Properties of the exact solution, the host entry (gbm_gblup_fit_synthetic) against the
+  stage path, and a subset of rows against the oracle.
+* One C5 fold at full size (20 000 × 300 000, three traits, fold 1 of 10 held out: ≈18 000
+  training rows) on a device genotype session, against an independent stage-API fit of the
+  gathered training rows, and a subset against the oracle.
+* C4 (Bayesian ridge, 10 000 × 100 000, 5 000 Gibbs iterations): the posterior-mean GEBVs agree
+  with ridge at the posterior λ (cor > 0.98) and predict the phenotype (cor > 0.5, the
+  reference doctest's bar, src/bayes.jl:155-158).
+
+Each test prints its timings (pytest -s / the log) for DESIGN.md.
+"""
+import time
+
+import numpy as np
+import pytest
+
+import gbm
+import oracle
+from gbm import synth
+
+pytestmark = [pytest.mark.gpu, pytest.mark.slow]
+
+
+def rel(a, b):
+    return float(np.abs(np.asarray(a) - np.asarray(b)).max() / max(np.abs(np.asarray(b)).max(), 1e-300))
+
+
+def _free():
+    import torch
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    gbm.load_library().gbm_release_device_cache()
+
+
+def test_c3_per_gpu_shape():
+    import torch
+    from gbm.sharded import HipShardStages, assemble_b_hat
+
+    n, p, lam, seed = 50000, 75000, 1.0, 424242
+    lib = gbm.load_library()
+    assert lib.gbm_dev_grm_workspace(n, p) < (1 << 30)  # carry mode: no loci-range slabs
+    t0 = time.perf_counter()
+    st = HipShardStages(n, p, nrhs=1, lambda_=lam, device=0)
+    st.generate(seed, 0)
+    Y = synth.qtl_phenotypes(seed, n, p, 1, device=0)
+    st.load_phenotypes(Y)
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    st.standardize()
+    st.grm_syrk()
+    st.grm_reduce()
+    torch.cuda.synchronize()
+    t2 = time.perf_counter()
+    q = int(st.q.item())
+    G = st.G[:n, :n]  # upper triangle: G·q
+    diag = torch.diagonal(G).clone() / q
+    assert abs(float(diag.mean()) - (n - 1) / n) < 1e-12
+    U = torch.triu(G)  # kept for the residual: the solve factors G in place
+    st.solve()
+    st.effects()
+    torch.cuda.synchronize()
+    t3 = time.perf_counter()
+    out = st.download()
+    y_pred, mu = out["y_pred"][:, 0], float(out["mu"][0])
+    a = st.A[0, :n].clone()
+    Ga = (U @ a + U.T @ a) / q - diag * a  # the symmetric G = (U + Uᵀ)/q − diag
+    r = (Ga + lam * a - (torch.from_numpy(Y[:, 0]).to(a.device) - mu)).abs().max().item()
+    assert r / np.abs(Y[:, 0] - mu).max() < 1e-10
+    assert abs(float(a.sum())) / float(a.abs().sum()) < 1e-10
+    del U, Ga
+    b_hat = assemble_b_hat(out["mu"], out["msum"], [out["B"]], p)
+    bd = torch.from_numpy(b_hat[1:, 0]).to(st.X.device)
+    pred = b_hat[0, 0] + (st.X[:, :n].T @ bd).cpu().numpy()
+    assert rel(pred, y_pred) < 1e-9
+    rows = np.arange(0, n, 100)
+    Xs = np.asfortranarray(st.X[:, rows].T.cpu().numpy())
+    print(f"\nC3 per-GPU shape: generate {t1 - t0:.2f} s, standardise+GRM {t2 - t1:.2f} s, "
+          f"solve+effects {t3 - t2:.2f} s (q = {q})")
+    del st, bd, a
+    _free()
+    # the host entry point on the same synthetic X (carry-mode GRM, pooled context)
+    t4 = time.perf_counter()
+    b2, y2, mu2, q2 = gbm.gblup_synthetic(seed, n, p, Y, lambda_=lam, devices=[0])
+    t5 = time.perf_counter()
+    print(f"gbm_gblup_fit_synthetic at 50000 x 75000: {t5 - t4:.2f} s")
+    _free()
+    assert q2 == q and rel(y2[:, 0], y_pred) < 1e-12 and rel(b2, b_hat) < 1e-10
+    # a subset of rows against the oracle (its own fit on those rows)
+    bs, ys, mus, qs = gbm.gblup_arrays(Xs, Y[rows], lambda_=lam)
+    ref = oracle.gblup_fit(Xs, Y[rows], lam)
+    assert qs == ref["q"] and rel(ys, ref["y_pred"]) < 1e-9 and rel(bs, ref["b_hat"]) < 1e-6
+
+
+def test_c5_fold_full_size():
+    import torch
+    from gbm.sharded import HipShardStages, assemble_b_hat
+
+    n, p, seed, lam = 20000, 300000, 42, 1.0
+    fold = np.random.default_rng(seed).integers(1, 11, size=n)  # cvbulk's sampling (src/cross_validation.jl:359)
+    train, val = np.flatnonzero(fold != 1), np.flatnonzero(fold == 1)
+    Y = synth.qtl_phenotypes(seed, n, p, 3, device=0)
+    t0 = time.perf_counter()
+    with gbm.GenotypeSession.synthetic(seed, n, p, device=0) as s:
+        t1 = time.perf_counter()
+        b, yp, mu, q = s.gblup(train, Y[train], lam)
+        t2 = time.perf_counter()
+        pv = s.predict(val, b)
+        t3 = time.perf_counter()
+    print(f"\nC5 fold (n_train = {train.size}, p = {p}, 3 traits): session {t1 - t0:.2f} s, "
+          f"fit {t2 - t1:.2f} s, validation predict {t3 - t2:.3f} s")
+    _free()
+    # independent path: the stage API on the gathered training rows
+    Xfull = synth.genotypes_device(seed, n, p, device=0)
+    nT = train.size
+    st = HipShardStages(nT, p, nrhs=3, lambda_=lam, device=0)
+    st.X.zero_()
+    tr = torch.from_numpy(train).to(Xfull.device)
+    for j0 in range(0, p, 25000):
+        st.X[j0:j0 + 25000, :nT] = Xfull[j0:j0 + 25000].index_select(1, tr)
+    vr = torch.from_numpy(val).to(Xfull.device)
+    pred_val = torch.from_numpy(b[0]).to(Xfull.device) + Xfull.index_select(1, vr).T @ torch.from_numpy(b[1:]).to(
+        Xfull.device)
+    assert rel(pv, pred_val.cpu().numpy()) < 1e-9
+    rows = train[::45]
+    Xs = np.asfortranarray(Xfull.index_select(1, torch.from_numpy(rows).to(Xfull.device)).T.cpu().numpy())
+    del Xfull, tr, vr, pred_val
+    torch.cuda.empty_cache()
+    st.load_phenotypes(Y[train])
+    st.standardize()
+    st.grm_syrk()
+    st.grm_reduce()
+    qs = int(st.q.item())
+    dg = torch.diagonal(st.G[:nT, :nT]) / qs
+    assert abs(float(dg.mean()) - (nT - 1) / nT) < 1e-12
+    st.solve()
+    st.effects()
+    out = st.download()
+    assert qs == q
+    assert rel(out["y_pred"], yp) < 1e-10
+    assert rel(assemble_b_hat(out["mu"], out["msum"], [out["B"]], p), b) < 1e-8
+    del st, dg
+    _free()
+    # a subset of the training rows against the oracle
+    b2, y2, mu2, q2 = gbm.gblup_arrays(Xs, Y[rows], lambda_=lam)
+    ref = oracle.gblup_fit(Xs, Y[rows], lam)
+    assert q2 == ref["q"] and rel(y2, ref["y_pred"]) < 1e-9 and rel(b2, ref["b_hat"]) < 1e-6
+
+
+def test_c4_bayesian_ridge_5000_iterations():
+    n, p, seed = 10000, 100000, 4242
+    X = synth.genotypes(seed, n, p, device=0)
+    y = synth.qtl_phenotypes(seed, n, p, 1, device=0)[:, 0]
+    _free()
+    t0 = time.perf_counter()
+    b_hat, y_pred, var = gbm.brr_arrays(X, y, n_iter=5000, n_burnin=1000, thin=5, seed=7)
+    t1 = time.perf_counter()
+    print(f"\nC4 BRR 10000 x 100000, 5000 iterations: {t1 - t0:.1f} s "
+          f"(posterior means: varE {var[0]:.4g}, varB {var[1]:.4g})")
+    assert np.isfinite(b_hat).all() and np.isfinite(y_pred).all()
+    _free()
+    # ridge at the posterior λ_rr = σ²_e/σ²_b (penalty on unscaled X): glmnet's λ = λ_rr σ_y / n
+    lam_glmnet = var[0] / var[1] * y.std() / n
+    with gbm.GenotypeSession(X, device=0) as s:
+        idx = np.arange(n)
+        br = s.ridge_path(idx, y, [lam_glmnet])[:, 0]
+        ridge_pred = s.predict(idx, br)
+    assert np.corrcoef(y_pred, ridge_pred)[0, 1] > 0.98
+    assert np.corrcoef(y_pred, y)[0, 1] > 0.5
