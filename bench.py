@@ -41,6 +41,7 @@ def parse():
     ap.add_argument("--lam", type=float, default=1.0)
     ap.add_argument("--seed", type=int, default=4242)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-host-path", action="store_true", help="skip the C-ABI (host buffer) timings")
     ap.add_argument("--cpu-sample-p", type=int, default=0, help="loci in the CPU baseline sample (0 = all)")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL); gloo only to rehearse N ranks on one GPU")
     ap.add_argument("--same-device", action="store_true", help="all ranks on cuda:0 (rehearsal on a 1-GPU box)")
@@ -78,6 +79,74 @@ def cpu_baseline(args):
     return {"value": n * p / dt, "unit": "genotype-cells/s", "cores": int(threads), "kind": "port",
             "sample": f"numpy/OpenBLAS fp64 restatement (oracle/oracle.py gblup_fit) on n={n} x p={p}, 1 trait, "
                       f"one full fit in {dt:.2f} s (standardise + GRM + Cholesky + marker effects; generation untimed)"}
+
+
+def host_path(args, torch):
+    """The product entry a Julia ccall binds (gbm_gblup_fit, X handed over in host memory), on the
+    same workload (rank 0, N = 1): pageable and pinned X, the int8-dosage entry, and the H2D copy
+    of X alone. PCIe-inclusive, so never the bench `value` (which starts with X in HBM)."""
+    import ctypes
+
+    import gbm
+    from gbm import _lib, synth
+
+    n, p, t = args.individuals, args.loci, args.nrhs
+    lib = gbm.load_library()
+    Xd = synth.genotypes_device(args.seed, n, p)  # (p, npad) locus rows
+    Y = np.asfortranarray(synth.qtl_phenotypes(args.seed, n, p, t))
+    pinned = torch.empty((p, n), dtype=torch.float64, pin_memory=True)
+    pinned.copy_(Xd[:, :n])
+    X_pin = pinned.numpy().T  # (n, p) column-major view of pinned memory
+    X_page = np.asfortranarray(X_pin.copy())
+    D_page = np.asfortranarray(np.rint(X_page * 2.0).astype(np.int8))
+    del Xd
+    torch.cuda.empty_cache()
+    b = np.zeros((p + 1, t), order="F")
+    yp = np.zeros((n, t), order="F")
+    mu = np.zeros(t)
+    q = np.zeros(1, dtype=np.int64)
+
+    def fit_f64(X):
+        _lib.check(lib.gbm_gblup_fit(_lib.ptr(X), n, p, n, _lib.ptr(Y), n, t, args.lam, None, 0, _lib.ptr(b),
+                                     _lib.ptr(yp), _lib.ptr(mu), _lib.ptr(q)), "gbm_gblup_fit")
+
+    def fit_i8():
+        _lib.check(lib.gbm_gblup_fit_dosage_i8(_lib.ptr(D_page), n, p, n, 2, _lib.ptr(Y), n, t, args.lam, None, 0,
+                                               _lib.ptr(b), _lib.ptr(yp), _lib.ptr(mu), _lib.ptr(q)),
+                   "gbm_gblup_fit_dosage_i8")
+
+    def timed(fn, reps=3):
+        fn()  # warm-up: pooled context allocated
+        a0 = lib.gbm_device_allocations()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            fn()
+        dt = (time.perf_counter() - t0) / reps
+        assert lib.gbm_device_allocations() == a0
+        return dt * 1000.0
+
+    ms_page = timed(lambda: fit_f64(X_page))
+    ms_pin = timed(lambda: fit_f64(X_pin))
+    ms_i8 = timed(fit_i8)
+    dev_buf = torch.empty((p, n), dtype=torch.float64, device="cuda")
+
+    def h2d(src):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(3):
+            dev_buf.copy_(src)
+        torch.cuda.synchronize()
+        return (time.perf_counter() - t0) / 3 * 1000.0
+
+    h2d_pin = h2d(pinned)
+    h2d_page = h2d(torch.from_numpy(np.ascontiguousarray(X_page.T)))
+    del dev_buf
+    return {
+        "entry": "gbm_gblup_fit (C ABI, host X column-major n x p; Julia ccall path) on the same workload",
+        "ms_per_call_pageable_x": ms_page, "ms_per_call_pinned_x": ms_pin, "ms_per_call_dosage_i8": ms_i8,
+        "h2d_x_ms_pinned": h2d_pin, "h2d_x_ms_pageable": h2d_page, "x_bytes": 8 * n * p,
+        "cells_per_s_pinned_x": n * p / (ms_pin / 1000.0), "device_allocations_per_call_after_warmup": 0,
+    }
 
 
 def load_pmc(n, p):
@@ -211,12 +280,18 @@ def main():
             "unit": "TFLOP/s",
             "frac": achieved / PEAK_F64_TFLOPS,
             "traffic": traffic,
+            "traffic_source": "profiles/pmc_grm.json: rocprofv3 --pmc FETCH_SIZE (x2, gfx950 16 B/lane "
+                              "under-count) + WRITE_SIZE per GRM launch, separate passes of this command"
+                              if traffic is not None else None,
             "flops_per_launch": grm_flops,
             "ms_per_launch": syrk_ms,
         },
         "stage_ms": stage_ms,
         "e2e_fp64_frac_of_peak": e2e_frac,
     }
+    if world == 1 and not args.no_host_path:
+        rec["host_path"] = host_path(args, torch)
+        rec["stage_ms"]["h2d_x_pinned"] = rec["host_path"]["h2d_x_ms_pinned"]
     if world == 1 and not args.no_cpu_baseline:
         rec["cpu_baseline"] = cpu_baseline(args)
     else:
