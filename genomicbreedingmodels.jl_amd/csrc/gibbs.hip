@@ -102,12 +102,19 @@ __global__ void __launch_bounds__(256) brr_colstats_kernel(const double* __restr
   }
 }
 
-// W[blk] = X_BᵀX_B (64x64, row-major; rows/cols past p are zero), individuals in chunks of 64
-// staged through LDS. One-time setup.
+// Gram blocks, one 64x64 block per workgroup (row-major; rows/cols past p are zero), individuals
+// in chunks of 64 staged through LDS; one-time setup. nw = 1: W[b] = X_BᵀX_B for the 64-marker
+// blocks B = [64b, 64b + 64). nw = 3 (128-marker launches of the byte path, halves A and B of
+// block b = [128b, 128b + 128)): W[3b] = X_AᵀX_A, W[3b + 1] = X_BᵀX_A (row k = marker B_k),
+// W[3b + 2] = X_BᵀX_B.
 __global__ void __launch_bounds__(256) brr_gram_kernel(const double* __restrict__ Xt, int64_t ldx, int64_t p,
-                                                       int64_t n, double* __restrict__ W) {
-  __shared__ double T[BB][BB + 1];
-  const int64_t j0 = (int64_t)blockIdx.x * BB;
+                                                       int64_t n, int nw, double* __restrict__ W) {
+  __shared__ double TR[BB][BB + 1];
+  __shared__ double TC[BB][BB + 1];
+  const int64_t blk = blockIdx.x / nw;
+  const int w = (int)(blockIdx.x % nw);
+  const int64_t r0 = nw == 1 ? blk * BB : blk * 2 * BB + (w >= 1 ? BB : 0);
+  const int64_t c0 = nw == 1 ? blk * BB : blk * 2 * BB + (w == 2 ? BB : 0);
   const int tid = threadIdx.x, a = tid >> 2, b0 = (tid & 3) * 16;
   double acc[16];
 #pragma unroll
@@ -115,13 +122,14 @@ __global__ void __launch_bounds__(256) brr_gram_kernel(const double* __restrict_
   for (int64_t k0 = 0; k0 < n; k0 += BB) {
     for (int e = tid; e < BB * BB; e += 256) {
       const int r = e / BB, c = e % BB;
-      T[r][c] = (j0 + r < p && k0 + c < n) ? Xt[(j0 + r) * ldx + k0 + c] : 0.0;
+      TR[r][c] = (r0 + r < p && k0 + c < n) ? Xt[(r0 + r) * ldx + k0 + c] : 0.0;
+      TC[r][c] = (c0 + r < p && k0 + c < n) ? Xt[(c0 + r) * ldx + k0 + c] : 0.0;
     }
     __syncthreads();
     for (int k = 0; k < BB; k++) {
-      const double xa = T[a][k];
+      const double xa = TR[a][k];
 #pragma unroll
-      for (int u = 0; u < 16; u++) acc[u] += xa * T[b0 + u][k];
+      for (int u = 0; u < 16; u++) acc[u] += xa * TC[b0 + u][k];
     }
     __syncthreads();
   }
@@ -207,6 +215,29 @@ __device__ __forceinline__ void brr_partials(const T* __restrict__ Xt, int64_t l
   if (qt == 0) out[blockIdx.x * BB + k] = s;  // k >= nb writes 0
 }
 
+// The 64 single-site steps of one 64-marker block on one wave. Lane k holds marker k: d = x_kᵀe
+// (kept current), its Gram row w, and the conditional draw b_new = α d + β folded into
+// δ = b_old − b_new = γ − α d (γ = b_old − β). Step s: lane s's δ_s is broadcast (v_readlane) and
+// d_k += δ_s W[s][k]; the dependent chain per step is fma -> readlane -> fma (lane s keeps its own
+// δ_s off the chain). Returns δ_k in lane k.
+__device__ __forceinline__ double brr_block_steps(double d, const double (&w)[BB], double nalpha, double gamma,
+                                                  int lane) {
+  double dk = 0.0;
+#pragma unroll
+  for (int s2 = 0; s2 < BB; s2++) {
+    union {
+      double f;
+      int i[2];
+    } u;
+    u.f = fma(d, nalpha, gamma);
+    dk = lane == s2 ? u.f : dk;
+    u.i[0] = __builtin_amdgcn_readlane(u.i[0], s2);
+    u.i[1] = __builtin_amdgcn_readlane(u.i[1], s2);
+    d = fma(u.f, w[s2], d);
+  }
+  return dk;
+}
+
 // partials of block 0 at the start of an iteration (after the intercept update)
 template <typename T>
 __global__ void __launch_bounds__(256) brr_dots0_kernel(const T* __restrict__ Xt, int64_t ldx, int64_t n,
@@ -285,11 +316,14 @@ __global__ void __launch_bounds__(256) brr_step_kernel(const T* __restrict__ Xt,
     }
     xx = on ? x2[j] : 0.0;
     // b ping-pongs between two copies by iteration parity: a workgroup that starts late never
-    // reads a value workgroup 0 already updated in this iteration
-    bo = on ? b[(st->it & 1) * p + j] : 0.0;
+    // reads a value workgroup 0 already updated in this iteration (both copies load at once with
+    // st: no st -> b dependent round trip)
+    const double b0 = on ? b[j] : 0.0, b1 = on ? b[p + j] : 0.0;
     varE = st->varE;
     varB = st->varB;
+    bo = (st->it & 1) ? b1 : b0;
   }
+  const double bb_old = (blockIdx.x == 0 && tid < 64 && on) ? bbar[j] : 0.0;
   {
     // r = Σ_c partial_in[c]: wave w sums c ≡ w (mod 4), 16 loads in flight per round, then a
     // fixed-order combine — every workgroup gets bit-identical r
@@ -311,26 +345,14 @@ __global__ void __launch_bounds__(256) brr_step_kernel(const T* __restrict__ Xt,
     const double alpha = on ? cinv / varE : 0.0;
     const double xi = on ? brr_normal(st->seed, 4 * (uint64_t)st->it, (uint64_t)j) : 0.0;
     const double beta = on ? xx * bo * alpha + sqrt(cinv) * xi : 0.0;
-    double bfin = bo;
-#pragma unroll
-    for (int s2 = 0; s2 < BB; s2++) {
-      const double bn = fma(d, alpha, beta);
-      bfin = lane == s2 ? bn : bfin;
-      union {
-        double f;
-        int i[2];
-      } u;
-      u.f = bo - bn;
-      u.i[0] = __builtin_amdgcn_readlane(u.i[0], s2);
-      u.i[1] = __builtin_amdgcn_readlane(u.i[1], s2);
-      d = fma(u.f, w[s2], d);
-    }
-    delta[lane] = bo - bfin;
+    const double dlt = brr_block_steps(d, w, -alpha, bo - beta, lane);
+    const double bfin = bo - dlt;
+    delta[lane] = dlt;
     if (blockIdx.x == 0 && on) {
       b[((st->it & 1) ^ 1) * p + j] = bfin;
       if (brr_accumulate(st)) {
         const double k = (double)(st->nsum + 1);
-        bbar[j] = bbar[j] * ((k - 1.0) / k) + bfin / k;
+        bbar[j] = bb_old * ((k - 1.0) / k) + bfin / k;
       }
     }
   }
@@ -373,6 +395,272 @@ __global__ void __launch_bounds__(256) brr_step_kernel(const T* __restrict__ Xt,
     __syncthreads();
     if (tid < 64)
       partial_out[blockIdx.x * BB + lane] = ((part4[0][lane] + part4[1][lane]) + part4[2][lane]) + part4[3][lane];
+  }
+}
+
+// ---- byte storage: 128-marker launches ------------------------------------------------------
+// With genotypes stored as bytes (x = d·xs exact), one launch runs 128 markers as two halves
+// A = [j0, j0 + 64) and B = [j0 + 64, j0 + 128): wave 0 runs A's 64 single-site steps from W_AA,
+// wave 1 then brings B's x_kᵀe up to date with A's changes (d_B += W_BA δ_A, a 64x64 GEMV), and
+// wave 0 runs B's 64 steps from W_BB (prefetched into LDS by waves 2-3 during A). Half the
+// dependent launches per iteration of the 64-marker kernel, same sample path (markers in order).
+constexpr int BK2 = 2 * BB;  // markers per launch
+constexpr int WP = BB + 2;   // LDS pitch of W_BB (528 B ≡ 16 B mod 256 B: conflict-free b128 row reads)
+
+// Dt[b][i][s] = D[(128 b + s) ldx + i] (0 for markers past p): the e update reads its 128
+// genotypes of block b as 128 contiguous bytes per individual (coalesced b128 loads).
+__global__ void __launch_bounds__(256) brr_block_transpose_kernel(const uint8_t* __restrict__ D, int64_t ldx,
+                                                                  int64_t p, uint8_t* __restrict__ Dt) {
+  __shared__ uint8_t T[BK2][65];
+  const int64_t b = blockIdx.y, i0 = (int64_t)blockIdx.x * 64;
+  const int tid = threadIdx.x;
+  for (int e = tid; e < BK2 * 64; e += 256) {
+    const int s = e >> 6, i = e & 63;
+    const int64_t j = b * BK2 + s;
+    T[s][i] = j < p ? D[j * ldx + i0 + i] : (uint8_t)0;
+  }
+  __syncthreads();
+  for (int e = tid; e < BK2 * 64; e += 256) {
+    const int i = e >> 7, s = e & 127;
+    Dt[(b * ldx + i0 + i) * BK2 + s] = T[s][i];
+  }
+}
+
+// partials of the 128 markers of block j0 (two rows per thread pair of passes), from es
+__device__ __forceinline__ void brr_partials128(const uint8_t* __restrict__ D, int64_t ldx, int64_t i0, int64_t j0,
+                                                int nb, double xs, const double* es, double* __restrict__ out) {
+  const int tid = threadIdx.x, k = tid >> 2, qt = tid & 3;
+#pragma unroll
+  for (int h = 0; h < 2; h++) {
+    const int kk = k + 64 * h;
+    double s = 0.0, s1 = 0.0;
+    if (kk < nb) {
+      const uint8_t* row = D + (j0 + kk) * ldx + i0 + qt * 64;
+      uint4 v[4];
+#pragma unroll
+      for (int u = 0; u < 4; u++) v[u] = *reinterpret_cast<const uint4*>(row + 16 * u);
+      brr_dot64_u8(v, es + qt * 64, xs, s, s1);
+      s += s1;
+    }
+    s += __shfl_xor(s, 1);
+    s += __shfl_xor(s, 2);
+    if (qt == 0) out[blockIdx.x * BK2 + kk] = s;  // kk >= nb writes 0
+  }
+}
+
+__global__ void __launch_bounds__(256) brr_dots0_128_kernel(const uint8_t* __restrict__ D, int64_t ldx, int64_t n,
+                                                            int64_t p, double xs, const double* __restrict__ e,
+                                                            double* __restrict__ partial) {
+  __shared__ double es[IW];
+  const int64_t i0 = (int64_t)blockIdx.x * IW;
+  es[threadIdx.x] = i0 + threadIdx.x < n ? e[i0 + threadIdx.x] : 0.0;
+  __syncthreads();
+  brr_partials128(D, ldx, i0, 0, (int)(p < BK2 ? p : BK2), xs, es, partial);
+}
+
+// Workgroup barrier that waits for this wave's LDS operations only (__syncthreads also waits for
+// every outstanding global load, e.g. the next block's rows that are needed much later).
+__device__ __forceinline__ void lds_barrier() {
+  __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+  __builtin_amdgcn_s_barrier();
+}
+
+__global__ void __launch_bounds__(256) brr_step128_kernel(const uint8_t* __restrict__ D, const uint8_t* __restrict__ Dt,
+                                                          int64_t ldx, int64_t n, int64_t p, double xs,
+                                                          const double* __restrict__ W, int64_t blk, int64_t nblk,
+                                                          const double* __restrict__ partial_in,
+                                                          double* __restrict__ partial_out, double* __restrict__ b,
+                                                          double* __restrict__ bbar, const double* __restrict__ x2,
+                                                          double* __restrict__ e, const BrrState* __restrict__ st) {
+  __shared__ __attribute__((aligned(16))) uint8_t Xb[BK2 * IW];  // next block's rows (swizzled 16-B chunks)
+  __shared__ __attribute__((aligned(16))) double Wbb[BB * WP];
+  __shared__ double delta[BK2];
+  __shared__ double rs[BK2];     // x_kᵀe of the block's markers at launch start
+  __shared__ double dB[BB];
+  __shared__ double cst[3][BB];  // half B: alpha, beta, b_old
+  __shared__ double es[IW];
+  __shared__ double part4[4][BK2];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int64_t j0 = blk * BK2;
+  const int C = (int)gridDim.x;
+  const int64_t i0 = (int64_t)blockIdx.x * IW;
+  const int64_t i = i0 + tid;
+  const bool more = blk + 1 < nblk;
+  const int64_t j1 = j0 + BK2;
+  const int nb1 = more ? (int)((p - j1) < BK2 ? (p - j1) : BK2) : 0;
+  const double* Wb = W + blk * 3 * BB * BB;
+  // Loads are issued in the order they are needed: vmcnt retires in order, so a load queued behind
+  // the next block's rows would wait for them.
+  // (1) the critical ones: waves 2-3 sum the partial dots of halves A and B over the C chunks (in
+  // chunk order: bit-identical in every workgroup); waves 0-1 load their Gram rows (W_AA, W_BA)
+  // and their half's marker state
+  double w[BB];
+  double xx = 0.0, bo = 0.0, varE = 0.0, varB = 0.0;
+  const int64_t jm = j0 + (wave == 1 ? BB : 0) + lane;  // wave 0: marker A_lane, wave 1: B_lane
+  const bool on = jm < p;
+  if (wave >= 2) {
+    const double* pin = partial_in + (wave - 2) * BB + lane;
+    double r = 0.0;
+    for (int c0 = 0; c0 < C; c0 += 64) {  // one batch of loads in flight (C <= 64 up to n = 16 384)
+      double v[64];
+#pragma unroll
+      for (int m = 0; m < 64; m++) v[m] = c0 + m < C ? pin[(int64_t)(c0 + m) * BK2] : 0.0;
+#pragma unroll
+      for (int m = 0; m < 64; m++) r += v[m];
+    }
+    rs[(wave - 2) * BB + lane] = r;
+  } else {
+    const double* wr = Wb + (wave == 0 ? 0 : BB * BB) + lane * BB;
+#pragma unroll
+    for (int q = 0; q < BB; q += 2) {
+      const double2 v = *reinterpret_cast<const double2*>(wr + q);
+      w[q] = v.x;
+      w[q + 1] = v.y;
+    }
+    // both parity copies of b load at once with st (no st -> b dependent round trip)
+    const double b0 = on ? b[jm] : 0.0, b1 = on ? b[p + jm] : 0.0;
+    xx = on ? x2[jm] : 0.0;
+    varE = st->varE;
+    varB = st->varB;
+    bo = (st->it & 1) ? b1 : b0;
+  }
+  // WG 0 keeps the running means: their old values load now, not after the serial steps
+  double bbA = 0.0, bbB = 0.0;
+  if (blockIdx.x == 0 && wave == 0) {
+    bbA = on ? bbar[jm] : 0.0;
+    bbB = jm + BB < p ? bbar[jm + BB] : 0.0;
+  }
+  // (2) needed later: this individual's 128 genotypes of the block (8 x 16 B) for e += X_B δ,
+  // and the next block's rows into LDS (4 rows per wave instruction, row r's 16-byte chunk c at
+  // position c ^ (r & 15); rows past the block re-read row nb1 − 1, never summed). The DMA is
+  // inline asm: with the builtin the compiler would wait for it before every LDS read.
+  uint4 xv[8];
+  {
+    const uint4* src = reinterpret_cast<const uint4*>(Dt + (blk * ldx + i) * BK2);
+#pragma unroll
+    for (int u = 0; u < 8; u++) xv[u] = src[u];
+  }
+  const double e_old = e[i];
+  for (int q = wave; q < (nb1 + 3) / 4; q += 4) {
+    const int r = 4 * q + (lane >> 4), c = lane & 15;
+    const uint8_t* src = D + (j1 + (r < nb1 ? r : nb1 - 1)) * ldx + i0 + ((c ^ (r & 15)) * 16);
+    const unsigned m0v = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(Xb + q * 4 * IW));
+    asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off" : : "s"(m0v), "v"(src) : "memory");
+  }
+  lds_barrier();
+  // (3) half A on wave 0; meanwhile wave 1 prepares half B's step constants and waves 2-3 put
+  // W_BB into LDS
+  if (wave == 0) {
+    const double c = 1.0 / (xx / varE + 1.0 / varB);
+    const double alpha = on ? c / varE : 0.0;
+    const double xi = on ? brr_normal(st->seed, 4 * (uint64_t)st->it, (uint64_t)jm) : 0.0;
+    const double beta = on ? xx * bo * alpha + sqrt(c) * xi : 0.0;
+    const double dlt = brr_block_steps(rs[lane], w, -alpha, bo - beta, lane);
+    delta[lane] = dlt;
+    if (blockIdx.x == 0 && on) {
+      const double bA = bo - dlt;
+      b[((st->it & 1) ^ 1) * p + jm] = bA;
+      if (brr_accumulate(st)) {
+        const double k = (double)(st->nsum + 1);
+        bbar[jm] = bbA * ((k - 1.0) / k) + bA / k;
+      }
+    }
+  } else if (wave == 1) {
+    const double c = 1.0 / (xx / varE + 1.0 / varB);
+    const double alpha = on ? c / varE : 0.0;
+    const double xi = on ? brr_normal(st->seed, 4 * (uint64_t)st->it, (uint64_t)jm) : 0.0;
+    cst[0][lane] = alpha;
+    cst[1][lane] = on ? xx * bo * alpha + sqrt(c) * xi : 0.0;
+    cst[2][lane] = bo;
+  } else {
+    const int t = tid - 128;  // 128 threads x 16 double2 = the 64x64 block
+#pragma unroll
+    for (int u = 0; u < 16; u++) {
+      const double2 v = *reinterpret_cast<const double2*>(Wb + 2 * BB * BB + 2 * (t + 128 * u));
+      w[2 * u] = v.x;
+      w[2 * u + 1] = v.y;
+    }
+#pragma unroll
+    for (int u = 0; u < 16; u++) {
+      const int e2 = 2 * (t + 128 * u), r = e2 / BB, c = e2 % BB;
+      *reinterpret_cast<double2*>(&Wbb[r * WP + c]) = make_double2(w[2 * u], w[2 * u + 1]);
+    }
+  }
+  lds_barrier();
+  // (4) wave 1: d_B = r_B + Σ_s W_BA[k][s] δ_A[s] (four partial chains); wave 0 takes its W_BB row
+  // from LDS
+  if (wave == 1) {
+    double d0 = rs[BB + lane], d1 = 0.0, d2 = 0.0, d3 = 0.0;
+#pragma unroll
+    for (int s2 = 0; s2 < BB; s2 += 4) {
+      d0 = fma(delta[s2], w[s2], d0);
+      d1 = fma(delta[s2 + 1], w[s2 + 1], d1);
+      d2 = fma(delta[s2 + 2], w[s2 + 2], d2);
+      d3 = fma(delta[s2 + 3], w[s2 + 3], d3);
+    }
+    dB[lane] = (d0 + d1) + (d2 + d3);
+  } else if (wave == 0) {
+#pragma unroll
+    for (int q = 0; q < BB; q += 2) {
+      const double2 v = *reinterpret_cast<const double2*>(&Wbb[lane * WP + q]);
+      w[q] = v.x;
+      w[q + 1] = v.y;
+    }
+  }
+  lds_barrier();
+  // (5) half B on wave 0
+  if (wave == 0) {
+    const int64_t jB = j0 + BB + lane;
+    const double boB = cst[2][lane];
+    const double dlt = brr_block_steps(dB[lane], w, -cst[0][lane], boB - cst[1][lane], lane);
+    delta[BB + lane] = dlt;
+    if (blockIdx.x == 0 && jB < p) {
+      const double bBn = boB - dlt;
+      b[((st->it & 1) ^ 1) * p + jB] = bBn;
+      if (brr_accumulate(st)) {
+        const double k = (double)(st->nsum + 1);
+        bbar[jB] = bbB * ((k - 1.0) / k) + bBn / k;
+      }
+    }
+  }
+  lds_barrier();
+  // (6) e += X_B δ over this workgroup's individuals (markers past p have δ = 0), four chains
+  double ei = 0.0;
+  if (i < n) {
+    double acc[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+      const uint32_t wd[4] = {xv[u].x, xv[u].y, xv[u].z, xv[u].w};
+#pragma unroll
+      for (int q = 0; q < 4; q++)
+#pragma unroll
+        for (int bb = 0; bb < 4; bb++)
+          acc[bb] = fma(delta[16 * u + 4 * q + bb], (double)((wd[q] >> (8 * bb)) & 0xFFu), acc[bb]);
+    }
+    ei = e_old + ((acc[0] + acc[1]) + (acc[2] + acc[3])) * xs;
+    e[i] = ei;
+  }
+  // (7) the next block's partial dots from the updated e
+  if (more) {
+    es[tid] = ei;
+    __builtin_amdgcn_s_waitcnt(0x0070);  // vmcnt(0) lgkmcnt(0): this wave's rows of Xb have landed
+    __syncthreads();
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+      const int k = lane + BB * h;
+      double s0 = 0.0, s1 = 0.0;
+      if (k < nb1) {
+        const uint8_t* xr = Xb + k * IW;
+        uint4 v[4];
+#pragma unroll
+        for (int t = 0; t < 4; t++) v[t] = *reinterpret_cast<const uint4*>(xr + (((4 * wave + t) ^ (k & 15)) * 16));
+        brr_dot64_u8(v, es + wave * 64, xs, s0, s1);
+      }
+      part4[wave][k] = s0 + s1;
+    }
+    lds_barrier();
+    if (tid < BK2)
+      partial_out[blockIdx.x * BK2 + tid] = ((part4[0][tid] + part4[1][tid]) + part4[2][tid]) + part4[3][tid];
   }
 }
 
@@ -441,23 +729,20 @@ extern "C" int gbm_brr_fit(const double* X, int64_t n, int64_t p, int64_t ldx, c
   GBM_HIP_TRY(hipStreamCreateWithFlags(&stw.s, hipStreamNonBlocking));
   hipStream_t s = stw.s;
   // Xt rows and e padded to whole IW-individual chunks (the block kernels read full chunks)
-  const int64_t npad = round_up(n, IW), nblk = (p + BB - 1) / BB;
-  DevMem Xt, colmean, x2, W, e, b, bbar, r, stm, pb, part, pout;
+  const int64_t npad = round_up(n, IW);
+  DevMem Xt, colmean, x2, W, e, b, bbar, r, stm, pb, part, pout, Dt;
   GBM_TRY(dalloc(Xt, dev, p * npad * 8));
   GBM_TRY(dalloc(colmean, dev, p * 8));
   GBM_TRY(dalloc(x2, dev, p * 8));
-  GBM_TRY(dalloc(W, dev, nblk * BB * BB * 8));
   GBM_TRY(dalloc(e, dev, npad * 8));
   GBM_TRY(dalloc(b, dev, 2 * p * 8));  // two copies (iteration parity)
   GBM_TRY(dalloc(bbar, dev, p * 8));
-  GBM_TRY(dalloc(r, dev, 2 * ((n + IW - 1) / IW) * BB * 8));  // ping-pong partial dots
+  GBM_TRY(dalloc(r, dev, 2 * ((n + IW - 1) / IW) * BK2 * 8));  // ping-pong partial dots
   GBM_TRY(dalloc(stm, dev, sizeof(BrrState)));
   GBM_HIP_TRY(hipMemsetAsync(Xt.p, 0, (size_t)(p * npad * 8), s));
   GBM_HIP_TRY(hipMemcpy2DAsync(Xt.p, npad * 8, X, ldx * 8, n * 8, p, hipMemcpyHostToDevice, s));
   brr_colstats_kernel<<<(unsigned)std::min<int64_t>(p, 4096), 256, 0, s>>>((const double*)Xt.p, npad, p, n,
                                                                            (double*)colmean.p, (double*)x2.p);
-  GBM_LAUNCH_CHECK();
-  brr_gram_kernel<<<(unsigned)nblk, 256, 0, s>>>((const double*)Xt.p, npad, p, n, (double*)W.p);
   GBM_LAUNCH_CHECK();
   std::vector<double> cm(p), xx(p);
   GBM_HIP_TRY(hipMemcpyAsync(cm.data(), colmean.p, p * 8, hipMemcpyDeviceToHost, s));
@@ -486,6 +771,19 @@ extern "C" int gbm_brr_fit(const double* X, int64_t n, int64_t p, int64_t ldx, c
         }
       }
     }
+  }
+  // markers per launch: 128 with byte storage (two halves), 64 with fp64 storage; the Gram blocks
+  // each launch needs (brr_gram_kernel), and the block-transposed bytes of the byte path
+  const int64_t bk = xs > 0.0 ? BK2 : BB, nblk = (p + bk - 1) / bk;
+  const int nw = xs > 0.0 ? 3 : 1;
+  GBM_TRY(dalloc(W, dev, nblk * nw * BB * BB * 8));
+  brr_gram_kernel<<<(unsigned)(nblk * nw), 256, 0, s>>>((const double*)Xt.p, npad, p, n, nw, (double*)W.p);
+  GBM_LAUNCH_CHECK();
+  if (xs > 0.0) {
+    GBM_TRY(dalloc(Dt, dev, nblk * npad * BK2));
+    brr_block_transpose_kernel<<<dim3((unsigned)(npad / 64), (unsigned)nblk), 256, 0, s>>>((const uint8_t*)D.p, npad, p,
+                                                                                            (uint8_t*)Dt.p);
+    GBM_LAUNCH_CHECK();
   }
   GBM_HIP_TRY(hipStreamSynchronize(s));
   // BGLR defaults (setLT.BRR and the residual prior): var(y) with ddof 1
@@ -526,18 +824,17 @@ extern "C" int gbm_brr_fit(const double* X, int64_t n, int64_t p, int64_t ldx, c
   auto enqueue_iteration = [&]() -> int {
     brr_mu_kernel<<<1, 1024, 0, s>>>((double*)e.p, n, stp);
     if (xs > 0.0)
-      brr_dots0_kernel<uint8_t><<<C, 256, 0, s>>>((const uint8_t*)D.p, npad, n, p, xs, (const double*)e.p,
-                                                  (double*)r.p);
+      brr_dots0_128_kernel<<<C, 256, 0, s>>>((const uint8_t*)D.p, npad, n, p, xs, (const double*)e.p, (double*)r.p);
     else
       brr_dots0_kernel<double><<<C, 256, 0, s>>>((const double*)Xt.p, npad, n, p, 1.0, (const double*)e.p,
                                                  (double*)r.p);
     for (int64_t k = 0; k < nblk; k++) {
-      double* pin = (double*)r.p + (k & 1) * (int64_t)C * BB;
-      double* pout = (double*)r.p + ((k + 1) & 1) * (int64_t)C * BB;
+      double* pin = (double*)r.p + (k & 1) * (int64_t)C * bk;
+      double* pout = (double*)r.p + ((k + 1) & 1) * (int64_t)C * bk;
       if (xs > 0.0)
-        brr_step_kernel<uint8_t><<<C, 256, 0, s>>>((const uint8_t*)D.p, npad, n, p, xs, (const double*)W.p, k, nblk,
-                                                   pin, pout, (double*)b.p, (double*)bbar.p, (const double*)x2.p,
-                                                   (double*)e.p, stp);
+        brr_step128_kernel<<<C, 256, 0, s>>>((const uint8_t*)D.p, (const uint8_t*)Dt.p, npad, n, p, xs,
+                                             (const double*)W.p, k, nblk, pin, pout, (double*)b.p, (double*)bbar.p,
+                                             (const double*)x2.p, (double*)e.p, stp);
       else
         brr_step_kernel<double><<<C, 256, 0, s>>>((const double*)Xt.p, npad, n, p, 1.0, (const double*)W.p, k, nblk,
                                                   pin, pout, (double*)b.p, (double*)bbar.p, (const double*)x2.p,
