@@ -25,7 +25,7 @@ constexpr int NB = kCholNB;  // 64
 constexpr int MAXRHS = 63;
 
 int launch_chol_update(double* G, int64_t ldg, int64_t k0, int64_t nb, int64_t gdim, double* Ld, double* Dinv,
-                       int32_t* info, int64_t next_k0, hipStream_t s);
+                       int32_t* info, int64_t next_k0, int rank, int nranks, hipStream_t s);
 int launch_chol_row_update(double* G, int64_t ldg, int64_t k0, int kch, int64_t gdim, double* Ld, double* Dinv,
                            int32_t* info, hipStream_t s);
 int64_t chol_small_lim();
@@ -56,24 +56,54 @@ __global__ void __launch_bounds__(256) prepare_v_kernel(double* __restrict__ G, 
   }
 }
 
-// ---- first diagonal block (the later ones are factored by the previous trailing update) -----
-__global__ void __launch_bounds__(256) factor_first_kernel(const double* __restrict__ G, int64_t ld,
-                                                           double* __restrict__ Ld, double* __restrict__ Dinv,
-                                                           int32_t* __restrict__ info) {
+// ---- a diagonal block on its own: the first one, and in a distributed factorisation the first of
+// each panel group after the strip exchange (otherwise the previous trailing update factors it) --
+__global__ void __launch_bounds__(256) factor_diag_kernel(const double* __restrict__ G, int64_t ld, int64_t k,
+                                                          double* __restrict__ Ld, double* __restrict__ Dinv,
+                                                          int32_t* __restrict__ info) {
   __shared__ __attribute__((aligned(16))) double Us[CNB * PS];
   __shared__ double rinv[CNB + 16];
   const int tid = threadIdx.x;
   {
     const int row = tid >> 2, quarter = tid & 3;
-    const double* sa = G + row * ld + quarter * 16;
+    const double* sa = G + (k + row) * ld + k + quarter * 16;
 #pragma unroll
     for (int e = 0; e < 16; e += 2)
       *reinterpret_cast<double2*>(&Us[row * PS + quarter * 16 + e]) = *reinterpret_cast<const double2*>(sa + e);
   }
   __syncthreads();
   const int bad = factor_diag_block(Us, rinv, tid);
-  if (tid == 0 && bad >= 0) atomicCAS(info, 0, (int32_t)(bad + 1));
-  store_factor(Us, rinv, Ld, Dinv, tid);
+  if (tid == 0 && bad >= 0) atomicCAS(info, 0, (int32_t)(k + bad + 1));
+  store_factor(Us, rinv, Ld + k * CNB, Dinv + (k / 16) * 256, tid);
+}
+
+// ---- strips of a distributed factorisation: rows [r0, r0 + rows) x the 128-column tiles
+// J in [r0/128, npad/128) that one rank owns (J ≡ owner mod nranks), packed [m][row][128] with
+// m < cnt = ⌈(npad/128 − r0/128)/nranks⌉ (the rank's m-th tile J = J0 + ((owner − J0) mod nranks)
+// + m·nranks; absent tiles past the end are zero-filled). unpack: every rank's pack of an
+// all-gather, written back into G.
+__global__ void __launch_bounds__(256) chol_strip_kernel(double* __restrict__ G, int64_t ld, int64_t r0,
+                                                         int64_t rows, int64_t J0, int64_t Jend, int64_t cnt,
+                                                         int owner, int nranks, double* __restrict__ buf,
+                                                         int unpack) {
+  const int64_t per = cnt * rows * 64;  // double2 per rank
+  const int64_t total = unpack ? per * nranks : per;
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total; e += (int64_t)gridDim.x * 256) {
+    const int src = unpack ? (int)(e / per) : owner;
+    const int64_t r = e - (unpack ? (int64_t)src * per : 0);
+    const int64_t m = r / (rows * 64), row = (r / 64) % rows, c2 = r % 64;
+    const int64_t J = J0 + (((int64_t)src - J0) % nranks + nranks) % nranks + m * nranks;
+    double2* b2 = reinterpret_cast<double2*>(buf) + (unpack ? e : r);
+    if (J >= Jend) {
+      if (!unpack) *b2 = make_double2(0.0, 0.0);
+      continue;
+    }
+    double2* g2 = reinterpret_cast<double2*>(G + (r0 + row) * ld + J * 128) + c2;
+    if (unpack)
+      *g2 = *b2;
+    else
+      *b2 = *g2;
+  }
 }
 
 // ---- panel k: U_k,J = U_kk⁻ᵀ A_k,J for the column chunks J > k ----------------------------------
@@ -301,92 +331,225 @@ extern "C" int64_t gbm_dev_solve_workspace(int64_t n, int64_t nrhs) {
   return solve_ws_doubles(n) * (int64_t)sizeof(double);
 }
 
-extern "C" int gbm_dev_gblup_solve(double* G, int64_t ldg, int64_t n, double inv_q, const int64_t* q_dev,
-                                   double lambda, const double* Y, int64_t ldy, int64_t nrhs, double* A_out,
-                                   double* gebv, int64_t lda, double* mu, int32_t* info, void* workspace,
-                                   int64_t ws_bytes, void* stream) {
-  const int64_t npad = npad_of(n), gdim = gdim_of(n);
-  if (!G || !Y || !A_out || !gebv || !mu || !info || n < 1 || ldg < gdim || ldy < n || lda < npad || nrhs < 1 ||
-      nrhs > MAXRHS || !(lambda > 0.0) || !(q_dev || inv_q > 0.0))
-    return fail(GBM_E_ARG, "gbm_dev_gblup_solve: bad arguments (need ldg >= gdim(n), lda >= npad(n), "
-                           "1 <= nrhs <= 63, lambda > 0, inv_q > 0)");
-  if ((ldg & 1) || ((uintptr_t)G & 15)) return fail(GBM_E_ARG, "gbm_dev_gblup_solve: G must be 16-byte aligned, even ld");
+namespace {
+
+struct SolveWs {
+  double *Ld, *Linv, *Dinv;
+  int32_t* flags;
+};
+SolveWs solve_ws(void* workspace, int64_t npad) {
+  SolveWs w;
+  w.Ld = (double*)workspace;
+  w.Linv = w.Ld + npad * NB;
+  w.Dinv = w.Linv + npad * NB;
+  w.flags = reinterpret_cast<int32_t*>(w.Dinv + npad * 16);
+  return w;
+}
+
+int check_solve_args(const double* G, int64_t ldg, int64_t n, const int32_t* info, const void* workspace,
+                     int64_t ws_bytes, const char* who) {
+  if (!G || !info || n < 1 || ldg < gdim_of(n) || (ldg & 1) || ((uintptr_t)G & 15))
+    return fail(GBM_E_ARG, std::string(who) + ": bad arguments (G 16-byte aligned, even ldg >= gdim(n))");
   if (!workspace || ws_bytes < solve_ws_doubles(n) * (int64_t)sizeof(double) || ((uintptr_t)workspace & 15))
-    return fail(GBM_E_ARG, "gbm_dev_gblup_solve: workspace too small (see gbm_dev_solve_workspace)");
-  double* Ld = (double*)workspace;
-  double* Linv = Ld + npad * NB;
-  double* Dinv = Linv + npad * NB;
-  hipStream_t s = (hipStream_t)stream;
-  int32_t* flags = reinterpret_cast<int32_t*>(Dinv + npad * 16);
+    return fail(GBM_E_ARG, std::string(who) + ": workspace too small (see gbm_dev_solve_workspace)");
+  return GBM_OK;
+}
+
+// Panels per group of the factorisation step at 64-block kb: groups of g panels share one K = 64g
+// trailing update (HBM/MALL-bound at K = 64, balanced at K = 128, MFMA-bound at K = 256). The
+// thresholds are read at every call, so tests can force the grouped paths on small matrices.
+int group_size(int64_t kb, int64_t nb, int64_t gdim) {
+  auto lim = [](const char* name, int64_t dflt) {
+    const char* e = getenv(name);
+    return e ? (int64_t)atoll(e) : dflt;
+  };
+  // 4-panel groups while the trailing matrix exceeds 8192 rows; 8-panel (K = 512) above 8192 and
+  // 16-panel (K = 1024) above 16384: n = 50 000 solve 798 -> 746 -> 735 ms
+  const int64_t g4 = lim("GBM_CHOL_G4_LIM", 8192), g8 = lim("GBM_CHOL_G8_LIM", 8192),
+                g16 = lim("GBM_CHOL_G16_LIM", 16384);
+  const int64_t k0 = kb * NB;
+  if (g16 >= 0 && kb + 16 < nb && gdim - (k0 + 16 * NB) > g16) return 16;
+  if (g8 >= 0 && kb + 8 < nb && gdim - (k0 + 8 * NB) > g8) return 8;
+  if (g4 >= 0 && kb + 4 < nb && gdim - (k0 + 4 * NB) > g4) return 4;
+  if (kb + 2 < nb && gdim - (k0 + 2 * NB) > chol_small_lim()) return 2;
+  return 1;
+}
+
+int solve_prepare(double* G, int64_t ldg, int64_t n, double inv_q, const int64_t* q_dev, double lambda,
+                  const double* Y, int64_t ldy, int64_t nrhs, int32_t* info, void* workspace, hipStream_t s) {
+  const int64_t npad = npad_of(n), gdim = gdim_of(n);
+  const SolveWs w = solve_ws(workspace, npad);
+  chol_refresh_tuning();
   prepare_v_kernel<<<(unsigned)gdim, 256, 0, s>>>(G, ldg, n, npad, gdim, inv_q, q_dev, lambda, Y, ldy, nrhs, info);
   GBM_LAUNCH_CHECK();
-  const int64_t nb = npad / NB;
-  factor_first_kernel<<<1, 256, 0, s>>>(G, ldg, Ld, Dinv, info);
+  factor_diag_kernel<<<1, 256, 0, s>>>(G, ldg, 0, w.Ld, w.Dinv, info);
   GBM_LAUNCH_CHECK();
-  auto panel = [&](int64_t k0) {
-    const int64_t chunks = (gdim - k0) / NB - 1;  // column chunks right of the diagonal block
-    chol_panel_kernel<<<(unsigned)chunks, 256, 0, s>>>(G, ldg, k0, Ld, Dinv);
+  return GBM_OK;
+}
+
+// One panel group at 64-block kb (its diagonal block already factored): the group's first panel,
+// the rows of its later panels brought up to date with the earlier ones (row updates, K = 64 j,
+// each factoring its diagonal block), their panels, then one K = 64 g trailing update, whose first
+// workgroup factors the next diagonal block. Distributed (nranks > 1): everything but the trailing
+// update is done by every rank over the full width; the trailing update covers this rank's tile
+// columns only, and the next diagonal block is left to gbm_dev_chol_factor_diag after the strip
+// exchange.
+int solve_group(double* G, int64_t ldg, int64_t n, int64_t kb, int rank, int nranks, int32_t* info, void* workspace,
+                hipStream_t s, int64_t* g_out) {
+  const int64_t npad = npad_of(n), gdim = gdim_of(n), nb = npad / NB;
+  const SolveWs w = solve_ws(workspace, npad);
+  const int64_t k0 = kb * NB;
+  const int g = group_size(kb, nb, gdim);
+  if (nranks > 1 && (g < 2 || (k0 % 128) != 0))
+    return fail(GBM_E_ARG, "gbm_dev_chol_group: a distributed step needs a panel group of >= 2 panels on a 128-row "
+                           "boundary (finish the tail with nranks = 1)");
+  auto panel = [&](int64_t k) {
+    const int64_t chunks = (gdim - k) / NB - 1;  // column chunks right of the diagonal block
+    chol_panel_kernel<<<(unsigned)chunks, 256, 0, s>>>(G, ldg, k, w.Ld, w.Dinv);
     return hipGetLastError() == hipSuccess;
   };
-  chol_refresh_tuning();
-  // 4-panel groups (one K = 256 trailing update) while the trailing matrix exceeds this many rows
-  const int64_t group4_lim = [] {  // read per call (tests force the groups on small matrices)
-    const char* e = getenv("GBM_CHOL_G4_LIM");
-    return e ? (int64_t)atoll(e) : (int64_t)8192;
-  }();
-  // 8-panel groups (K = 512) while the trailing matrix exceeds this many rows. Solve at
-  // n = 50 000: 798 ms (4-panel groups only) -> 746 ms; n = 20 000: 67.1 -> 64.0 ms
-  const int64_t group8_lim = [] {
-    const char* e = getenv("GBM_CHOL_G8_LIM");
-    return e ? (int64_t)atoll(e) : (int64_t)8192;
-  }();
-  const int64_t group16_lim = [] {  // 16-panel groups (K = 1024): n = 50 000 746 -> 735 ms
-    const char* e = getenv("GBM_CHOL_G16_LIM");
-    return e ? (int64_t)atoll(e) : (int64_t)16384;
-  }();
-  for (int64_t kb = 0; kb < nb;) {
-    const int64_t k0 = kb * NB;
-    if (!panel(k0)) return fail(GBM_E_HIP, "chol_panel_kernel launch failed");
-    int rc;
-    // groups of g panels share one pass over the trailing matrix (HBM/MALL-bound at K = 64,
-    // balanced at K = 128, MFMA-bound at K = 256): the rows of panels 2..g of the group are
-    // brought up to date with the group's earlier panels (row update with K = 64 j), factored and
-    // solved one after the other, then one K = 64 g trailing update
-    int g = 1;
-    if (group16_lim >= 0 && kb + 16 < nb && gdim - (k0 + 16 * NB) > group16_lim)
-      g = 16;
-    else if (group8_lim >= 0 && kb + 8 < nb && gdim - (k0 + 8 * NB) > group8_lim)
-      g = 8;
-    else if (group4_lim >= 0 && kb + 4 < nb && gdim - (k0 + 4 * NB) > group4_lim)
-      g = 4;
-    else if (kb + 2 < nb && gdim - (k0 + 2 * NB) > chol_small_lim())
-      g = 2;
-    if (g > 1) {
-      for (int j = 1; j < g; j++) {
-        rc = launch_chol_row_update(G, ldg, k0, j, gdim, Ld, Dinv, info, s);
-        if (rc != GBM_OK) return rc;
-        if (!panel(k0 + j * NB)) return fail(GBM_E_HIP, "chol_panel_kernel launch failed");
-      }
-      rc = launch_chol_update(G, ldg, k0, g * NB, gdim, Ld, Dinv, info, k0 + g * NB, s);
-      kb += g;
-    } else {
-      // trailing update; its first workgroup also factors the next diagonal block
-      rc = launch_chol_update(G, ldg, k0, NB, gdim, Ld, Dinv, info, kb + 1 < nb ? k0 + NB : -1, s);
-      kb += 1;
+  if (!panel(k0)) return fail(GBM_E_HIP, "chol_panel_kernel launch failed");
+  int rc;
+  if (g > 1) {
+    for (int j = 1; j < g; j++) {
+      rc = launch_chol_row_update(G, ldg, k0, j, gdim, w.Ld, w.Dinv, info, s);
+      if (rc != GBM_OK) return rc;
+      if (!panel(k0 + j * NB)) return fail(GBM_E_HIP, "chol_panel_kernel launch failed");
     }
-    if (rc != GBM_OK) return rc;
+    rc = launch_chol_update(G, ldg, k0, g * NB, gdim, w.Ld, w.Dinv, info, k0 + g * NB, rank, nranks, s);
+  } else {
+    rc = launch_chol_update(G, ldg, k0, NB, gdim, w.Ld, w.Dinv, info, kb + 1 < nb ? k0 + NB : -1, 0, 1, s);
   }
-  diag_inverse_kernel<<<(unsigned)nb, 64, 0, s>>>(Ld, Linv);
+  if (g_out) *g_out = g;
+  return rc;
+}
+
+// After the last panel: inverses of the diagonal blocks, μ̂ and the back-substitution right-hand
+// sides from the bordered Schur block, the sync-free back substitution, GEBVs.
+int solve_finish(double* G, int64_t ldg, int64_t n, const double* Y, int64_t ldy, int64_t nrhs, double lambda,
+                 double* A_out, double* gebv, int64_t lda, double* mu, int32_t* info, void* workspace, hipStream_t s) {
+  const int64_t npad = npad_of(n), nb = npad / NB;
+  const SolveWs w = solve_ws(workspace, npad);
+  diag_inverse_kernel<<<(unsigned)nb, 64, 0, s>>>(w.Ld, w.Linv);
   GBM_LAUNCH_CHECK();
   const unsigned gx = (unsigned)((lda + 255) / 256 < 1024 ? (lda + 255) / 256 : 1024);
   // the gebv buffer doubles as the w scratch: gebv_kernel (last) reads only Y and A
-  gls_mu_kernel<<<dim3(gx, (unsigned)nrhs), 256, 0, s>>>(G, ldg, npad, nrhs, gebv, lda, mu, flags);
+  gls_mu_kernel<<<dim3(gx, (unsigned)nrhs), 256, 0, s>>>(G, ldg, npad, nrhs, gebv, lda, mu, w.flags);
   GBM_LAUNCH_CHECK();
-  back_solve_kernel<<<(unsigned)nb, 256, 0, s>>>(G, ldg, Linv, nb, gebv, A_out, lda, nrhs, flags, info);
+  back_solve_kernel<<<(unsigned)nb, 256, 0, s>>>(G, ldg, w.Linv, nb, gebv, A_out, lda, nrhs, w.flags, info);
   GBM_LAUNCH_CHECK();
   gebv_kernel<<<dim3(gx, (unsigned)nrhs), 256, 0, s>>>(Y, ldy, n, A_out, gebv, lda, mu, lambda);
   GBM_LAUNCH_CHECK();
   return GBM_OK;
+}
+
+void strip_geometry(int64_t n, int64_t kb, int64_t rows64, int nranks, int64_t& r0, int64_t& rows, int64_t& J0,
+                    int64_t& Jend, int64_t& cnt) {
+  r0 = kb * NB;
+  rows = rows64 * NB;
+  J0 = r0 / 128;
+  Jend = npad_of(n) / 128;
+  cnt = Jend > J0 ? (Jend - J0 + nranks - 1) / nranks : 0;
+}
+
+}  // namespace
+
+extern "C" int gbm_dev_gblup_solve(double* G, int64_t ldg, int64_t n, double inv_q, const int64_t* q_dev,
+                                   double lambda, const double* Y, int64_t ldy, int64_t nrhs, double* A_out,
+                                   double* gebv, int64_t lda, double* mu, int32_t* info, void* workspace,
+                                   int64_t ws_bytes, void* stream) {
+  const int64_t npad = npad_of(n);
+  if (!Y || !A_out || !gebv || !mu || ldy < n || lda < npad || nrhs < 1 || nrhs > MAXRHS || !(lambda > 0.0) ||
+      !(q_dev || inv_q > 0.0))
+    return fail(GBM_E_ARG, "gbm_dev_gblup_solve: bad arguments (need ldg >= gdim(n), lda >= npad(n), "
+                           "1 <= nrhs <= 63, lambda > 0, inv_q > 0)");
+  GBM_TRY(check_solve_args(G, ldg, n, info, workspace, ws_bytes, "gbm_dev_gblup_solve"));
+  hipStream_t s = (hipStream_t)stream;
+  GBM_TRY(solve_prepare(G, ldg, n, inv_q, q_dev, lambda, Y, ldy, nrhs, info, workspace, s));
+  const int64_t nb = npad / NB;
+  for (int64_t kb = 0; kb < nb;) {
+    int64_t g = 1;
+    GBM_TRY(solve_group(G, ldg, n, kb, 0, 1, info, workspace, s, &g));
+    kb += g;
+  }
+  return solve_finish(G, ldg, n, Y, ldy, nrhs, lambda, A_out, gebv, lda, mu, info, workspace, s);
+}
+
+extern "C" int gbm_dev_chol_prepare(double* G, int64_t ldg, int64_t n, double inv_q, const int64_t* q_dev,
+                                    double lambda, const double* Y, int64_t ldy, int64_t nrhs, int32_t* info,
+                                    void* workspace, int64_t ws_bytes, void* stream) {
+  if (!Y || ldy < n || nrhs < 1 || nrhs > MAXRHS || !(lambda > 0.0) || !(q_dev || inv_q > 0.0))
+    return fail(GBM_E_ARG, "gbm_dev_chol_prepare: bad arguments");
+  GBM_TRY(check_solve_args(G, ldg, n, info, workspace, ws_bytes, "gbm_dev_chol_prepare"));
+  return solve_prepare(G, ldg, n, inv_q, q_dev, lambda, Y, ldy, nrhs, info, workspace, (hipStream_t)stream);
+}
+
+extern "C" int64_t gbm_dev_chol_group_size(int64_t n, int64_t kb) {
+  const int64_t nb = npad_of(n) / NB;
+  if (kb < 0 || kb >= nb) return 0;
+  chol_refresh_tuning();
+  return group_size(kb, nb, gdim_of(n));
+}
+
+extern "C" int gbm_dev_chol_group(double* G, int64_t ldg, int64_t n, int64_t kb, int rank, int nranks, int32_t* info,
+                                  void* workspace, int64_t ws_bytes, void* stream) {
+  GBM_TRY(check_solve_args(G, ldg, n, info, workspace, ws_bytes, "gbm_dev_chol_group"));
+  if (kb < 0 || kb >= npad_of(n) / NB || nranks < 1 || rank < 0 || rank >= nranks)
+    return fail(GBM_E_ARG, "gbm_dev_chol_group: bad step or rank");
+  return solve_group(G, ldg, n, kb, rank, nranks, info, workspace, (hipStream_t)stream, nullptr);
+}
+
+extern "C" int gbm_dev_chol_factor_diag(double* G, int64_t ldg, int64_t n, int64_t kb, int32_t* info, void* workspace,
+                                        int64_t ws_bytes, void* stream) {
+  GBM_TRY(check_solve_args(G, ldg, n, info, workspace, ws_bytes, "gbm_dev_chol_factor_diag"));
+  if (kb < 0 || kb >= npad_of(n) / NB) return fail(GBM_E_ARG, "gbm_dev_chol_factor_diag: bad step");
+  const SolveWs w = solve_ws(workspace, npad_of(n));
+  factor_diag_kernel<<<1, 256, 0, (hipStream_t)stream>>>(G, ldg, kb * NB, w.Ld, w.Dinv, info);
+  GBM_LAUNCH_CHECK();
+  return GBM_OK;
+}
+
+extern "C" int64_t gbm_dev_chol_strip_doubles(int64_t n, int64_t kb, int64_t rows64, int nranks) {
+  if (nranks < 1 || kb < 0 || rows64 < 1) return 0;
+  int64_t r0, rows, J0, Jend, cnt;
+  strip_geometry(n, kb, rows64, nranks, r0, rows, J0, Jend, cnt);
+  return cnt * rows * 128;
+}
+
+static int strip_launch(double* G, int64_t ldg, int64_t n, int64_t kb, int64_t rows64, int rank, int nranks,
+                        double* buf, int unpack, hipStream_t s) {
+  if (!G || !buf || n < 1 || ldg < gdim_of(n) || kb < 0 || rows64 < 1 || (kb * NB) % 128 != 0 || nranks < 1 ||
+      rank < 0 || rank >= nranks || (kb + rows64) * NB > npad_of(n))
+    return fail(GBM_E_ARG, "gbm_dev_chol_strip_pack/unpack: bad arguments (strip rows inside [0, npad), "
+                           "starting on a 128-row boundary)");
+  int64_t r0, rows, J0, Jend, cnt;
+  strip_geometry(n, kb, rows64, nranks, r0, rows, J0, Jend, cnt);
+  if (cnt == 0) return GBM_OK;
+  const int64_t total = cnt * rows * 64 * (unpack ? nranks : 1);
+  const int64_t want = (total + 255) / 256;
+  chol_strip_kernel<<<(unsigned)(want < 16384 ? want : 16384), 256, 0, s>>>(G, ldg, r0, rows, J0, Jend, cnt, rank, nranks,
+                                                                           buf, unpack);
+  GBM_LAUNCH_CHECK();
+  return GBM_OK;
+}
+
+extern "C" int gbm_dev_chol_strip_pack(const double* G, int64_t ldg, int64_t n, int64_t kb, int64_t rows64, int rank,
+                                       int nranks, double* buf, void* stream) {
+  return strip_launch(const_cast<double*>(G), ldg, n, kb, rows64, rank, nranks, buf, 0, (hipStream_t)stream);
+}
+
+extern "C" int gbm_dev_chol_strip_unpack(double* G, int64_t ldg, int64_t n, int64_t kb, int64_t rows64, int nranks,
+                                         const double* gathered, void* stream) {
+  return strip_launch(G, ldg, n, kb, rows64, 0, nranks, const_cast<double*>(gathered), 1, (hipStream_t)stream);
+}
+
+extern "C" int gbm_dev_chol_finish(double* G, int64_t ldg, int64_t n, const double* Y, int64_t ldy, int64_t nrhs,
+                                   double lambda, double* A_out, double* gebv, int64_t lda, double* mu, int32_t* info,
+                                   void* workspace, int64_t ws_bytes, void* stream) {
+  if (!Y || !A_out || !gebv || !mu || ldy < n || lda < npad_of(n) || nrhs < 1 || nrhs > MAXRHS)
+    return fail(GBM_E_ARG, "gbm_dev_chol_finish: bad arguments");
+  GBM_TRY(check_solve_args(G, ldg, n, info, workspace, ws_bytes, "gbm_dev_chol_finish"));
+  return solve_finish(G, ldg, n, Y, ldy, nrhs, lambda, A_out, gebv, lda, mu, info, workspace, (hipStream_t)stream);
 }
 
 extern "C" int gbm_dev_gblup_terms(const double* G, int64_t ldg, int64_t n, int64_t nrhs, const void* workspace,

@@ -30,6 +30,12 @@ int fail(int code, const std::string& msg);
 
 #define GBM_LAUNCH_CHECK() GBM_HIP_TRY(hipGetLastError())
 
+#define GBM_TRY(expr)              \
+  do {                             \
+    int rc_ = (expr);              \
+    if (rc_ != GBM_OK) return rc_; \
+  } while (0)
+
 // Stage launchers (device pointers, stream-ordered); defined in the .hip files.
 int launch_grm(const double* Zt, int64_t ldz, int64_t p, int64_t n, double* G, int64_t ldg,
                void* ws, int64_t ws_bytes, hipStream_t s);

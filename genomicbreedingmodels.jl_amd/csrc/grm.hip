@@ -52,6 +52,14 @@ __device__ __forceinline__ void tile_of(int64_t t, int64_t& ti, int64_t& tj) {
 
 enum SyrkMode { kSub = 0, kSplit = 1, kPersist = 2 };
 
+// Column ownership of a distributed Cholesky trailing update (kSub): with nranks > 1 this rank
+// updates only the 128-column tiles J (absolute, column J·128) with J mod nranks == rank, plus the
+// bordered right-hand-side tile column rhs_tile, which every rank keeps current.
+struct TileOwner {
+  int32_t rank = 0, nranks = 1;
+  int64_t rhs_tile = -1;
+};
+
 // acc[m][q] += (NEG ? −1 : 1) Σ_k U[k][i0 + ·] U[k][j0 + ·] over the stages [kstep0, kstep0 + nsteps)
 // (BK loci each) of one BT x BT tile. Operands are staged by global_load_lds into the two LDS
 // buffers (double-buffered); returns after a barrier, so the buffers are free again. `wave` is
@@ -239,7 +247,8 @@ template <int MODE>
 __global__ void __launch_bounds__(256, WPS)
 syrk_kernel(const double* __restrict__ U, int64_t ldu, int64_t K, int64_t c0, int64_t lim,
             double* __restrict__ C, int64_t ldc, double* __restrict__ slab, int64_t ntiles, SliceBounds sb,
-            double* __restrict__ Ld, double* __restrict__ Dinv, int32_t* __restrict__ info, int64_t fk0) {
+            double* __restrict__ Ld, double* __restrict__ Dinv, int32_t* __restrict__ info, int64_t fk0,
+            TileOwner own) {
   // 2 stages (72 KB at BK = 16); kSub's first workgroup reuses it for the 64x64 factor image
   constexpr int LDS_DOUBLES = (2 * STAGE > CNB * PS + CNB + 16) ? 2 * STAGE : CNB * PS + CNB + 16;
   __shared__ __attribute__((aligned(16))) double lds[LDS_DOUBLES];
@@ -375,6 +384,10 @@ syrk_kernel(const double* __restrict__ U, int64_t ldu, int64_t K, int64_t c0, in
   } else {
     int64_t ti, tj;
     tile_of(wg, ti, tj);
+    if (own.nranks > 1) {  // (workgroup-uniform) another rank's column
+      const int64_t J = c0 / BT + tj;
+      if (J != own.rhs_tile && J % own.nranks != own.rank) return;
+    }
     const bool diag = (ti == tj);
     const int64_t i0 = c0 + ti * BT, j0 = c0 + tj * BT;
     const bool active = (i0 + wm * 64 < rlim) && (j0 + wn * 64 < rlim) && !(diag && wm == 1 && wn == 0);
@@ -789,10 +802,19 @@ int launch_chol_row_update(double* G, int64_t ldg, int64_t k0, int kch, int64_t 
 // 64x64 tiles (syrk64_sub_kernel) for single panels below chol_small_lim() trailing rows (more
 // workgroups for the small trailing matrices of late panels), else the 128x128 tile kernel.
 int launch_chol_update(double* G, int64_t ldg, int64_t k0, int64_t nb, int64_t gdim, double* Ld, double* Dinv,
-                       int32_t* info, int64_t next_k0, hipStream_t s) {
+                       int32_t* info, int64_t next_k0, int rank, int nranks, hipStream_t s) {
   const int64_t k1 = k0 + nb;
   const int64_t lim = gdim - k1;
   if (lim <= 0) return GBM_OK;
+  TileOwner own;
+  if (nranks > 1) {
+    if ((k1 % BT) != 0 || nb == 64)
+      return fail(GBM_E_ARG, "distributed Cholesky update: panel groups must start on 128-column tiles");
+    own.rank = rank;
+    own.nranks = nranks;
+    own.rhs_tile = (gdim - kRhsRows) / BT;
+    next_k0 = -1;  // the next diagonal block is factored after the strip exchange
+  }
   if (nb == 64 && lim <= chol_small_lim()) {
     const int64_t m = (lim + 63) / 64;
     syrk64_sub_kernel<<<(unsigned)(m * (m + 1) / 2), 256, 0, s>>>(G + k0 * ldg, ldg, k1, lim, G, ldg, Ld, Dinv, info,
@@ -803,7 +825,7 @@ int launch_chol_update(double* G, int64_t ldg, int64_t k0, int64_t nb, int64_t g
   const int64_t m = (lim + BT - 1) / BT;
   const int64_t ntiles = m * (m + 1) / 2;
   syrk_kernel<kSub><<<(unsigned)ntiles, 256, 0, s>>>(G + k0 * ldg, ldg, nb, k1, lim, G, ldg, nullptr, ntiles, SliceBounds{}, Ld,
-                                                     Dinv, info, next_k0);
+                                                     Dinv, info, next_k0, own);
   GBM_LAUNCH_CHECK();
   return GBM_OK;
 }
@@ -896,10 +918,10 @@ int launch_grm_syrk(const double* Zt, int64_t ldz, int64_t p, int64_t n, double*
     const int64_t units = (int64_t)g.sb.n * g.ntiles;
     const unsigned pgrid = (unsigned)(units < resident_wgs() ? units : resident_wgs());
     syrk_kernel<kPersist><<<pgrid, 256, 0, s>>>(Zt, ldz, p, 0, lim, G, ldg, (double*)ws, g.ntiles, g.sb, nullptr,
-                                                nullptr, ctr, -1);
+                                                nullptr, ctr, -1, TileOwner{});
   } else {
     syrk_kernel<kSplit><<<grid, 256, 0, s>>>(Zt, ldz, p, 0, lim, G, ldg, (double*)ws, g.ntiles, g.sb, nullptr, nullptr,
-                                             nullptr, -1);
+                                             nullptr, -1, TileOwner{});
   }
   GBM_LAUNCH_CHECK();
   if (g.sb.er > 0) {

@@ -79,11 +79,6 @@ struct Stream {
   }
 };
 
-#define GBM_TRY(expr)            \
-  do {                           \
-    int rc_ = (expr);            \
-    if (rc_ != GBM_OK) return rc_; \
-  } while (0)
 
 // Device list of a call. Explicit `devices` (one SNP-column shard per entry; an ordinal may
 // repeat: shards on one device are summed on that device). With none given, the calling thread

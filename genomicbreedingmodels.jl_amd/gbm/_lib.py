@@ -35,6 +35,8 @@ EXPORTS = (
     "gbm_session_create", "gbm_session_create_dosage_i8", "gbm_session_create_synthetic", "gbm_session_destroy", "gbm_session_gblup_fit",
     "gbm_session_predict", "gbm_session_reml_objective", "gbm_session_reml", "gbm_session_stats",
     "gbm_session_ridge_path", "gbm_session_ridge_lambda_max", "gbm_brr_fit",
+    "gbm_dev_chol_prepare", "gbm_dev_chol_group_size", "gbm_dev_chol_group", "gbm_dev_chol_factor_diag",
+    "gbm_dev_chol_strip_doubles", "gbm_dev_chol_strip_pack", "gbm_dev_chol_strip_unpack", "gbm_dev_chol_finish",
     "gbm_dev_grm_packed_size", "gbm_dev_grm_pack", "gbm_dev_grm_unpack",
 )
 
@@ -68,6 +70,22 @@ def _declare(lib):
     lib.gbm_device_allocations.argtypes = []
     lib.gbm_release_device_cache.restype = I32
     lib.gbm_release_device_cache.argtypes = []
+    lib.gbm_dev_chol_prepare.restype = I32
+    lib.gbm_dev_chol_prepare.argtypes = [P, I64, I64, D, P, D, P, I64, I64, P, P, I64, P]
+    lib.gbm_dev_chol_group_size.restype = I64
+    lib.gbm_dev_chol_group_size.argtypes = [I64, I64]
+    lib.gbm_dev_chol_group.restype = I32
+    lib.gbm_dev_chol_group.argtypes = [P, I64, I64, I64, I32, I32, P, P, I64, P]
+    lib.gbm_dev_chol_factor_diag.restype = I32
+    lib.gbm_dev_chol_factor_diag.argtypes = [P, I64, I64, I64, P, P, I64, P]
+    lib.gbm_dev_chol_strip_doubles.restype = I64
+    lib.gbm_dev_chol_strip_doubles.argtypes = [I64, I64, I64, I32]
+    lib.gbm_dev_chol_strip_pack.restype = I32
+    lib.gbm_dev_chol_strip_pack.argtypes = [P, I64, I64, I64, I64, I32, I32, P, P]
+    lib.gbm_dev_chol_strip_unpack.restype = I32
+    lib.gbm_dev_chol_strip_unpack.argtypes = [P, I64, I64, I64, I64, I32, P, P]
+    lib.gbm_dev_chol_finish.restype = I32
+    lib.gbm_dev_chol_finish.argtypes = [P, I64, I64, P, I64, I64, D, P, P, I64, P, P, P, I64, P]
     lib.gbm_gblup_fit.restype = I32
     lib.gbm_gblup_fit.argtypes = [P, I64, I64, I64, P, I64, I64, D, P, I32, P, P, P, P]
     lib.gbm_gblup_fit_dosage_i8.restype = I32

@@ -4,7 +4,9 @@ Each rank owns a contiguous block of loci (SNP columns) resident in its GPU's HB
 
     standardise (local) → partial GRM Σ_j z_j z_jᵀ (local, fp64 MFMA)
       → all-reduce(sum) of the partial GRMs and of the kept-loci counts q      [RCCL]
-      → GBLUP solve on G/q + λI (every rank, redundantly: a stays local)
+      → GBLUP solve on G/q + λI: at large n a distributed Cholesky (each rank the trailing
+        updates of its own 128-column tiles, a strip all-gather per panel group; chol_distributed),
+        otherwise every rank redundantly (a stays local either way)
       → marker effects b_j for the rank's loci and Σ m_j b_j partials
       → all-reduce(sum) of the Σ m_j b_j partials (b0 = μ̂ − Σ)                 [RCCL]
       → results to the host.
@@ -36,6 +38,17 @@ class TorchComm:
         if self.world_size > 1:
             self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM)
 
+    def all_gather(self, t):
+        """Every rank's t, concatenated in rank order (one flat tensor)."""
+        import torch
+        out = torch.empty(self.world_size * t.numel(), dtype=t.dtype, device=t.device)
+        if self.dist.get_backend() == "nccl":
+            self.dist.all_gather_into_tensor(out, t.reshape(-1))
+        else:  # gloo: list form
+            parts = list(out.chunk(self.world_size))
+            self.dist.all_gather(parts, t.reshape(-1).contiguous())
+        return out
+
 
 class LocalComm:
     world_size = 1
@@ -66,7 +79,10 @@ def sharded_gblup_step(stages, comm, events=None):
             comm.all_reduce_sum(stages.grm_rows())
     comm.all_reduce_sum(stages.q)
     mark("allreduce")
-    stages.solve()
+    if comm.world_size > 1 and hasattr(stages, "chol_group") and stages.n >= dist_solve_min_n():
+        chol_distributed([stages], [comm.rank], comm.world_size, lambda packs: [comm.all_gather(packs[0])])
+    else:
+        stages.solve()
     mark("solve")
     stages.effects()
     comm.all_reduce_sum(stages.msum)
@@ -74,6 +90,63 @@ def sharded_gblup_step(stages, comm, events=None):
     out = stages.download()
     mark("download")
     return out
+
+
+def dist_solve_min_n() -> int:
+    """Individuals from which a multi-rank step factors V distributed (below, the latency-bound
+    solve is cheaper redundantly). GBM_DIST_SOLVE_MIN_N overrides (tests)."""
+    import os
+    return int(os.environ.get("GBM_DIST_SOLVE_MIN_N", "16384"))
+
+
+def chol_distributed(stages, ranks, nranks, allgather, tail_rows=None):
+    """GBLUP solve of V = G/q + λI distributed over ``nranks`` ranks, replacing the
+    redundant per-rank factorisation (the reference's pinv(V), src/gwas.jl:472,595).
+
+    ``stages``: the ranks this process drives (HipShardStages, each holding the full summed G) —
+    one in the one-process-per-GPU run, all of them in a single-process rehearsal; ``ranks``: their
+    rank ids; ``allgather(packs)``: one packed strip per local rank -> per local rank the flat
+    concatenation of all ranks' packs. Panel groups run on every rank over the full width, each
+    group's trailing update only on the rank's own 128-column tiles (gbm_dev_chol_group); the next
+    group's rows are then all-gathered and its diagonal block factored. Once the trailing matrix is
+    small (``tail_rows``, GBM_DIST_TAIL_ROWS, default 8192) or the groups shrink to single panels,
+    every remaining row is gathered once and the tail runs redundantly. The result is bit-identical
+    to the redundant solve (the same kernel computes every tile)."""
+    import os
+    st0 = stages[0]
+    lib, n = st0.lib, st0.n
+    nb = st0.npad // 64
+    gdim = st0.gdim
+    if tail_rows is None:
+        tail_rows = int(os.environ.get("GBM_DIST_TAIL_ROWS", "8192"))
+
+    def distributable(kb):
+        return (gdim - 64 * kb > tail_rows and lib.gbm_dev_chol_group_size(n, kb) >= 2 and (64 * kb) % 128 == 0)
+
+    for st in stages:
+        st.chol_prepare()
+    kb = 0
+    dist = nranks > 1 and distributable(0)
+    while kb < nb:
+        g = int(lib.gbm_dev_chol_group_size(n, kb))
+        if not dist:
+            for st in stages:
+                st.chol_group(kb, 0, 1)
+            kb += g
+            continue
+        for st, r in zip(stages, ranks):
+            st.chol_group(kb, r, nranks)
+        kb += g
+        if kb >= nb:
+            break
+        dist = distributable(kb)
+        rows64 = int(lib.gbm_dev_chol_group_size(n, kb)) if dist else nb - kb
+        packs = [st.strip_pack(kb, rows64, r, nranks) for st, r in zip(stages, ranks)]
+        for st, gathered in zip(stages, allgather(packs)):
+            st.strip_unpack(kb, rows64, nranks, gathered)
+            st.chol_factor_diag(kb)
+    for st in stages:
+        st.chol_finish()
 
 
 def assemble_b_hat(mu, msum, B_shards, p_total):
@@ -188,6 +261,40 @@ class HipShardStages:
                                                 self._p(self.Y), self.npad, self.nrhs, self._p(self.A),
                                                 self._p(self.gebv), self.npad, self._p(self.mu), self._p(self.info),
                                                 self._p(self.ws_solve), self.ws_solve_bytes, self._stream()), "solve")
+
+    # ---- the solve in phases (distributed factorisation, chol_distributed) -------------------------
+    def chol_prepare(self):
+        _lib.check(self.lib.gbm_dev_chol_prepare(self._p(self.G), self.gdim, self.n, 0.0, self._p(self.q), self.lam,
+                                                 self._p(self.Y), self.npad, self.nrhs, self._p(self.info),
+                                                 self._p(self.ws_solve), self.ws_solve_bytes, self._stream()),
+                   "chol_prepare")
+
+    def chol_group(self, kb: int, rank: int, nranks: int):
+        _lib.check(self.lib.gbm_dev_chol_group(self._p(self.G), self.gdim, self.n, kb, rank, nranks, self._p(self.info),
+                                               self._p(self.ws_solve), self.ws_solve_bytes, self._stream()),
+                   "chol_group")
+
+    def chol_factor_diag(self, kb: int):
+        _lib.check(self.lib.gbm_dev_chol_factor_diag(self._p(self.G), self.gdim, self.n, kb, self._p(self.info),
+                                                     self._p(self.ws_solve), self.ws_solve_bytes, self._stream()),
+                   "chol_factor_diag")
+
+    def strip_pack(self, kb: int, rows64: int, rank: int, nranks: int):
+        size = self.lib.gbm_dev_chol_strip_doubles(self.n, kb, rows64, nranks)
+        buf = self.torch.empty(max(size, 2), dtype=self.torch.float64, device=self.dev)[:size]
+        _lib.check(self.lib.gbm_dev_chol_strip_pack(self._p(self.G), self.gdim, self.n, kb, rows64, rank, nranks,
+                                                    self._p(buf), self._stream()), "strip_pack")
+        return buf
+
+    def strip_unpack(self, kb: int, rows64: int, nranks: int, gathered):
+        _lib.check(self.lib.gbm_dev_chol_strip_unpack(self._p(self.G), self.gdim, self.n, kb, rows64, nranks,
+                                                      self._p(gathered), self._stream()), "strip_unpack")
+
+    def chol_finish(self):
+        _lib.check(self.lib.gbm_dev_chol_finish(self._p(self.G), self.gdim, self.n, self._p(self.Y), self.npad,
+                                                self.nrhs, self.lam, self._p(self.A), self._p(self.gebv), self.npad,
+                                                self._p(self.mu), self._p(self.info), self._p(self.ws_solve),
+                                                self.ws_solve_bytes, self._stream()), "chol_finish")
 
     def effects(self):
         _lib.check(self.lib.gbm_dev_marker_effects(self._p(self.Z), self.npad, self.p, self.n, self._p(self.A),

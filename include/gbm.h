@@ -221,6 +221,39 @@ int gbm_dev_gblup_solve(double* G, int64_t ldg, int64_t n, double inv_q, const i
                         double* A_out, double* gebv, int64_t lda, double* mu, int32_t* info,
                         void* workspace, int64_t ws_bytes, void* stream);
 
+/*
+ * The same solve in phases, for a factorisation distributed over ranks (one process or device per
+ * rank, each holding the full summed G): gbm_dev_gblup_solve == prepare; for kb = 0 .. npad/64 − 1
+ * step gbm_dev_chol_group_size(n, kb): group(kb, rank = 0, nranks = 1); finish.
+ * Distributed (nranks > 1, steps whose group has >= 2 panels and starts on a 128-row boundary):
+ * every rank runs each group's panels over the full width, but the group's trailing update only on
+ * its own 128-column tiles (J ≡ rank mod nranks; the bordered right-hand-side tile on every rank) —
+ * 1/nranks of the O(n³) work. Before the next group, the ranks exchange that group's rows of their
+ * tiles (strip_pack → all-gather of gbm_dev_chol_strip_doubles per rank → strip_unpack) and factor
+ * its diagonal block (factor_diag); before switching back to nranks = 1 for the tail, they exchange
+ * all remaining rows the same way. Replaces the redundant per-rank pinv/Cholesky of V at
+ * reference src/gwas.jl:472,595 at multi-GPU scale.
+ */
+int gbm_dev_chol_prepare(double* G, int64_t ldg, int64_t n, double inv_q, const int64_t* q_dev, double lambda,
+                         const double* Y, int64_t ldy, int64_t nrhs, int32_t* info, void* workspace,
+                         int64_t ws_bytes, void* stream);
+/* Panels in the group that starts at 64-row block kb (0 past the end). */
+int64_t gbm_dev_chol_group_size(int64_t n, int64_t kb);
+int gbm_dev_chol_group(double* G, int64_t ldg, int64_t n, int64_t kb, int rank, int nranks, int32_t* info,
+                       void* workspace, int64_t ws_bytes, void* stream);
+int gbm_dev_chol_factor_diag(double* G, int64_t ldg, int64_t n, int64_t kb, int32_t* info, void* workspace,
+                             int64_t ws_bytes, void* stream);
+/* Doubles per rank of the strip of rows [64 kb, 64 (kb + rows64)) over the tiles from column 64 kb. */
+int64_t gbm_dev_chol_strip_doubles(int64_t n, int64_t kb, int64_t rows64, int nranks);
+int gbm_dev_chol_strip_pack(const double* G, int64_t ldg, int64_t n, int64_t kb, int64_t rows64, int rank,
+                            int nranks, double* buf, void* stream);
+/* gathered: nranks consecutive packs (rank order), e.g. the output of an all-gather. */
+int gbm_dev_chol_strip_unpack(double* G, int64_t ldg, int64_t n, int64_t kb, int64_t rows64, int nranks,
+                              const double* gathered, void* stream);
+int gbm_dev_chol_finish(double* G, int64_t ldg, int64_t n, const double* Y, int64_t ldy, int64_t nrhs,
+                        double lambda, double* A_out, double* gebv, int64_t lda, double* mu, int32_t* info,
+                        void* workspace, int64_t ws_bytes, void* stream);
+
 /* REML ingredients of a finished gbm_dev_gblup_solve (same G, workspace, n, nrhs), into device
  * memory: terms[0] = logdet(G/q + λI), terms[1] = 1ᵀV⁻¹1, terms[2+2t] = 1ᵀV⁻¹y_t,
  * terms[3+2t] = y_tᵀV⁻¹y_t — everything reference loglikreml (src/gwas.jl:450-483) needs with
