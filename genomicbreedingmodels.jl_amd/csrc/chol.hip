@@ -30,6 +30,10 @@ int launch_chol_row_update(double* G, int64_t ldg, int64_t k0, int kch, int64_t 
                            int32_t* info, hipStream_t s);
 int64_t chol_small_lim();
 void chol_refresh_tuning();
+int64_t chol_flow_flag_bytes(int64_t gdim);
+bool chol_flow_enabled(int64_t npad);
+int launch_chol_flow(double* G, int64_t ldg, int64_t gdim, double* Ld, double* Dinv, void* flag_block, int32_t* info,
+                     hipStream_t s);
 
 // ---- V = G/q + λI (upper part), padding = identity, bordered R columns -----------------------
 __global__ void __launch_bounds__(256) prepare_v_kernel(double* __restrict__ G, int64_t ld, int64_t n,
@@ -324,8 +328,10 @@ extern "C" int64_t gbm_dev_npad(int64_t n) { return npad_of(n); }
 extern "C" int64_t gbm_dev_gdim(int64_t n) { return gdim_of(n); }
 // scratch: the factored 64x64 diagonal blocks (npad x 64), their inverses (npad x 64) and the
 // inverses of their 16x16 diagonal sub-blocks (npad x 16)
-// + one int32 flag per 64-block (back_solve_kernel)
-static int64_t solve_ws_doubles(int64_t n) { return npad_of(n) * (2 * NB + 16) + npad_of(n) / NB / 2 + 1; }
+// + one int32 flag per 64-block (back_solve_kernel), then (16-byte aligned) the dataflow
+// factorisation's queue word and per-tile flags (chol_flow.hip)
+static int64_t flow_block_offset(int64_t n) { return round_up(npad_of(n) * (2 * NB + 16) + npad_of(n) / NB / 2 + 1, 2); }
+static int64_t solve_ws_doubles(int64_t n) { return flow_block_offset(n) + chol_flow_flag_bytes(gdim_of(n)) / 8; }
 extern "C" int64_t gbm_dev_solve_workspace(int64_t n, int64_t nrhs) {
   (void)nrhs;
   return solve_ws_doubles(n) * (int64_t)sizeof(double);
@@ -336,6 +342,7 @@ namespace {
 struct SolveWs {
   double *Ld, *Linv, *Dinv;
   int32_t* flags;
+  void* flow;
 };
 SolveWs solve_ws(void* workspace, int64_t npad) {
   SolveWs w;
@@ -343,6 +350,7 @@ SolveWs solve_ws(void* workspace, int64_t npad) {
   w.Linv = w.Ld + npad * NB;
   w.Dinv = w.Linv + npad * NB;
   w.flags = reinterpret_cast<int32_t*>(w.Dinv + npad * 16);
+  w.flow = (double*)workspace + flow_block_offset(npad);
   return w;
 }
 
@@ -376,12 +384,14 @@ int group_size(int64_t kb, int64_t nb, int64_t gdim) {
 }
 
 int solve_prepare(double* G, int64_t ldg, int64_t n, double inv_q, const int64_t* q_dev, double lambda,
-                  const double* Y, int64_t ldy, int64_t nrhs, int32_t* info, void* workspace, hipStream_t s) {
+                  const double* Y, int64_t ldy, int64_t nrhs, int32_t* info, void* workspace, hipStream_t s,
+                  bool factor_first = true) {
   const int64_t npad = npad_of(n), gdim = gdim_of(n);
   const SolveWs w = solve_ws(workspace, npad);
   chol_refresh_tuning();
   prepare_v_kernel<<<(unsigned)gdim, 256, 0, s>>>(G, ldg, n, npad, gdim, inv_q, q_dev, lambda, Y, ldy, nrhs, info);
   GBM_LAUNCH_CHECK();
+  if (!factor_first) return GBM_OK;
   factor_diag_kernel<<<1, 256, 0, s>>>(G, ldg, 0, w.Ld, w.Dinv, info);
   GBM_LAUNCH_CHECK();
   return GBM_OK;
@@ -465,6 +475,13 @@ extern "C" int gbm_dev_gblup_solve(double* G, int64_t ldg, int64_t n, double inv
                            "1 <= nrhs <= 63, lambda > 0, inv_q > 0)");
   GBM_TRY(check_solve_args(G, ldg, n, info, workspace, ws_bytes, "gbm_dev_gblup_solve"));
   hipStream_t s = (hipStream_t)stream;
+  if (chol_flow_enabled(npad)) {
+    // one persistent dataflow launch factors the whole bordered matrix (chol_flow.hip)
+    GBM_TRY(solve_prepare(G, ldg, n, inv_q, q_dev, lambda, Y, ldy, nrhs, info, workspace, s, false));
+    const SolveWs w = solve_ws(workspace, npad);
+    GBM_TRY(launch_chol_flow(G, ldg, gdim_of(n), w.Ld, w.Dinv, w.flow, info, s));
+    return solve_finish(G, ldg, n, Y, ldy, nrhs, lambda, A_out, gebv, lda, mu, info, workspace, s);
+  }
   GBM_TRY(solve_prepare(G, ldg, n, inv_q, q_dev, lambda, Y, ldy, nrhs, info, workspace, s));
   const int64_t nb = npad / NB;
   for (int64_t kb = 0; kb < nb;) {

@@ -44,8 +44,9 @@ def test_geometry_helpers():
     lib = gbm.load_library()
     assert lib.gbm_dev_npad(1) == 128 and lib.gbm_dev_npad(5000) == 5120 and lib.gbm_dev_npad(5120) == 5120
     assert lib.gbm_dev_gdim(5000) == 5120 + 64
-    # factored blocks + their inverses + 16x16 inverses, then one int32 flag per 64-block
-    assert lib.gbm_dev_solve_workspace(5000, 1) == (5120 * (2 * 64 + 16) + 40 + 1) * 8
+    # Ld, Linv, Dinv, back-substitution flags; then (16-byte aligned) the dataflow queue + tile flags
+    nbc = (5120 + 64) // 64
+    assert lib.gbm_dev_solve_workspace(5000, 1) == (5120 * (2 * 64 + 16) + 40 + 1 + 1) * 8 + (16 + nbc * nbc * 4 + 15) // 16 * 16
     # GRM workspace: loci-slice partial tiles (+ the ragged-column partials when n % 128 <= 64)
     # (+ 32 bytes of queue counters for the persistent launch)
     assert (lib.gbm_dev_grm_workspace(5120, 50000) - 32) % (128 * 128 * 8) == 0

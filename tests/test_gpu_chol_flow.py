@@ -1,0 +1,105 @@
+"""The dataflow factorisation (csrc/chol_flow.hip: one persistent launch, left-looking 64x64
+tiles handed over between workgroups through write-through stores and per-tile flags) against
+the oracle and against the launch-per-panel path it replaces in gbm_dev_gblup_solve.
+
+GBM_CHOL_FLOW_MAX (re-read at every solve) selects the path: npad <= limit → dataflow."""
+import numpy as np
+import pytest
+
+import oracle
+
+pytestmark = pytest.mark.gpu
+
+
+def rel(a, b):
+    return float(np.abs(np.asarray(a) - np.asarray(b)).max() / max(np.abs(np.asarray(b)).max(), 1e-300))
+
+
+def _pair(n, p, t, seed, lam):
+    """Two stage objects holding the same summed G, q and Y (GRM computed once)."""
+    import torch
+
+    from gbm.sharded import HipShardStages
+    X = oracle.synth_genotypes(seed, n, p)
+    Y = oracle.synth_phenotypes(X, seed + 1, ntraits=t)
+    a = HipShardStages(n, p, nrhs=t, lambda_=lam, device=0)
+    a.upload_genotypes(X)
+    a.load_phenotypes(Y)
+    a.standardize()
+    a.grm_syrk()
+    a.grm_reduce()
+    b = HipShardStages(n, p, nrhs=t, lambda_=lam, device=0)
+    b.G.copy_(a.G)
+    b.q.copy_(a.q)
+    b.Y.copy_(a.Y)
+    torch.cuda.synchronize()
+    return X, Y, a, b
+
+
+@pytest.mark.parametrize("n,p,t,seed,lam", [
+    (64, 500, 1, 3, 1.0),        # one diagonal tile + the bordered column: 3 tiles in all
+    (200, 1000, 2, 42, 1.0),     # C1 shape
+    (1030, 1400, 3, 7, 0.5),     # ragged n (npad 1152)
+    (3000, 2000, 2, 11, 0.8),    # 48 tile rows
+    (5000, 1500, 1, 19, 1.0),    # the C2 individual count (80 tile rows)
+])
+def test_flow_matches_oracle_and_panel_path(monkeypatch, n, p, t, seed, lam):
+    import torch
+    X, Y, flow, panel = _pair(n, p, t, seed, lam)
+    monkeypatch.setenv("GBM_CHOL_FLOW_MAX", "1000000")
+    flow.solve()
+    monkeypatch.setenv("GBM_CHOL_FLOW_MAX", "0")
+    panel.solve()
+    torch.cuda.synchronize()
+    assert int(flow.info.item()) == 0 and int(panel.info.item()) == 0
+    gf = flow.gebv[:, :n].cpu().numpy().T
+    gp = panel.gebv[:, :n].cpu().numpy().T
+    af = flow.A[:, :n].cpu().numpy()
+    ap = panel.A[:, :n].cpu().numpy()
+    # the two paths sum the same updates in a different grouping: rounding-level differences only
+    assert rel(gf, gp) < 1e-11
+    assert rel(af, ap) < 1e-9
+    assert rel(flow.mu.cpu().numpy(), panel.mu.cpu().numpy()) < 1e-11
+    ref = oracle.gblup_fit(X, Y, lam)
+    assert rel(gf, ref["y_pred"]) < 1e-9
+    assert rel(flow.mu.cpu().numpy(), ref["mu"]) < 1e-9
+
+
+def test_flow_repeated_solves_bit_identical(monkeypatch):
+    """Each tile's updates are summed in k order in its own accumulators, whatever the schedule:
+    repeated solves (different workgroup placement and timing) give identical bits."""
+    import torch
+    monkeypatch.setenv("GBM_CHOL_FLOW_MAX", "1000000")
+    X, Y, a, b = _pair(2100, 900, 2, 5, 1.0)
+    G0 = a.G.clone()
+    first = None
+    for _ in range(6):
+        a.G.copy_(G0)
+        a.solve()
+        torch.cuda.synchronize()
+        assert int(a.info.item()) == 0
+        cur = (a.gebv.clone(), a.A.clone(), a.mu.clone())
+        if first is None:
+            first = cur
+        else:
+            assert all(torch.equal(x, y) for x, y in zip(cur, first))
+
+
+@pytest.mark.parametrize("bad", [0, 700, 1029])
+def test_flow_reports_first_failing_pivot(monkeypatch, bad):
+    """A matrix that is not positive definite: the factorisation ends (no hang) and info is the
+    first failing column + 1, as in the launch-per-panel path."""
+    import torch
+    _, _, a, b = _pair(1030, 300, 1, 9, 1.0)
+    for st in (a, b):
+        st.G.zero_()
+        st.G[:st.npad, :st.npad].fill_diagonal_(1.0)
+        st.G[bad, bad] = -5.0
+        st.q.fill_(1)
+    monkeypatch.setenv("GBM_CHOL_FLOW_MAX", "1000000")
+    a.solve()
+    monkeypatch.setenv("GBM_CHOL_FLOW_MAX", "0")
+    b.solve()
+    torch.cuda.synchronize()
+    assert int(a.info.item()) == bad + 1
+    assert int(b.info.item()) == bad + 1

@@ -49,6 +49,7 @@ def test_distributed_factorisation_bit_identical(monkeypatch, R, n, lims, tail):
     monkeypatch.setenv("GBM_CHOL_G8_LIM", lims[1])
     monkeypatch.setenv("GBM_CHOL_G16_LIM", lims[2])
     monkeypatch.setenv("GBM_UPD64_LIM", "128")
+    monkeypatch.setenv("GBM_CHOL_FLOW_MAX", "0")  # reference: the redundant launch-per-panel solve
     X = oracle.synth_genotypes(n + R, n, 1200)
     Y = oracle.synth_phenotypes(X, 3, ntraits=2)
     ref_st, ranks = _stages(R, X, Y, 0.8)

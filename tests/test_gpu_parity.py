@@ -195,6 +195,7 @@ def test_cholesky_panel_groups_forced(monkeypatch, g4, g8, g16):
     monkeypatch.setenv("GBM_CHOL_G8_LIM", str(g8))
     monkeypatch.setenv("GBM_CHOL_G16_LIM", str(g16))
     monkeypatch.setenv("GBM_UPD64_LIM", "128")
+    monkeypatch.setenv("GBM_CHOL_FLOW_MAX", "0")  # the launch-per-panel path (not the dataflow one)
     n, p = 1500, 900
     X = oracle.synth_genotypes(77, n, p)
     Y = oracle.synth_phenotypes(X, 78, ntraits=2)

@@ -32,4 +32,4 @@ for r in range(reps + 1):
     torch.cuda.synchronize()
     if r:
         ts.append(e0.elapsed_time(e1))
-print(f"solve n={n}: {np.mean(ts):.3f} ms (min {np.min(ts):.3f}) diag={os.environ.get('GBM_PANEL_DIAG', '0')}")
+print(f"solve n={n}: {np.mean(ts):.3f} ms (min {np.min(ts):.3f}) flow_max={os.environ.get('GBM_CHOL_FLOW_MAX', 'default')} info={int(st.info.item())}")
