@@ -407,11 +407,15 @@ chol_flow_kernel(double* __restrict__ G, int64_t ld, int nbc, double* __restrict
           }
         }
         {
+          // Ld: the six off-diagonal 16x16 blocks that the row's other solves read, write-through
+          // now; the diagonal blocks (read only by later kernels) after the flags
           const int row = tid >> 2, quarter = tid & 3;
           const uint32_t base = (uint32_t)(((i0 + row) * CNB + quarter * 16) * 8);
+          if (quarter > (row >> 4)) {
 #pragma unroll
-          for (int e = 0; e < 16; e += 2)
-            st2(rLd, base + e * 8, *reinterpret_cast<const dbl2*>(&X[row * PS + quarter * 16 + e]));
+            for (int e = 0; e < 16; e += 2)
+              st2(rLd, base + e * 8, *reinterpret_cast<const dbl2*>(&X[row * PS + quarter * 16 + e]));
+          }
         }
 #pragma unroll
         for (int q = 0; q < 8; q++) {
@@ -491,6 +495,14 @@ chol_flow_kernel(double* __restrict__ G, int64_t ld, int nbc, double* __restrict
         __hip_atomic_store(flags + (int64_t)i * nbc + j + 1, kFinal, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     if (low) store_lower(low, i0, lj0);
+    if (diag && i < nb) {
+      const int row = tid >> 2, quarter = tid & 3;
+      if (quarter == (row >> 4)) {
+        double* d = Ld + (i0 + row) * CNB + quarter * 16;
+#pragma unroll
+        for (int e = 0; e < 16; e += 2) *reinterpret_cast<dbl2*>(d + e) = *reinterpret_cast<const dbl2*>(&X[row * PS + quarter * 16 + e]);
+      }
+    }
     __builtin_amdgcn_s_setprio(0);
     if (kTrace && tid == 0) {
       tr[5] = (int64_t)__builtin_amdgcn_s_memrealtime();
