@@ -263,18 +263,28 @@ int run_fit(const Problem& pr, const double* Y, int64_t ldy, int64_t nrhs, doubl
   std::vector<std::unique_ptr<Shard>> shards;
   GBM_TRY(make_shards(devs, p, shards));
   int64_t q = 0;
-  for (auto& sh : shards) {
-    GBM_TRY(prepare_shard(pr, *sh));
-    q += sh->q_host;
+  {
+    RoctxRange r("gbm: upload + standardise");
+    for (auto& sh : shards) {
+      GBM_TRY(prepare_shard(pr, *sh));
+      q += sh->q_host;
+    }
   }
   if (q_out) *q_out = q;
   if (q == 0) return fail(GBM_E_DATA, "no polymorphic locus-allele (all standard deviations <= eps, src/gwas.jl:112-115)");
-  for (auto& sh : shards) GBM_TRY(grm_shard(pr, *sh));
-  GBM_TRY(allreduce_grm(shards, n));
+  {
+    RoctxRange r("gbm: GRM");
+    for (auto& sh : shards) GBM_TRY(grm_shard(pr, *sh));
+  }
+  {
+    RoctxRange r("gbm: partial-GRM all-reduce");
+    GBM_TRY(allreduce_grm(shards, n));
+  }
   const double inv_q = 1.0 / (double)q;
   // each device leader solves the (identical) n x n system, all devices at once: a is then local
   // to every shard's marker back-solve (same-device shards copy it from their leader)
   std::vector<int32_t> infos(shards.size(), 0);
+  RoctxRange rsolve("gbm: solve");
   for (size_t k = 0; k < shards.size(); k++) {
     Shard& sh = *shards[k];
     FitCtx& c = sh.x();
@@ -307,6 +317,7 @@ int run_fit(const Problem& pr, const double* Y, int64_t ldy, int64_t nrhs, doubl
       return fail(GBM_E_NOTPD, "G/q + lambda*I is not positive definite (pivot " + std::to_string(info) +
                                    "); check for non-finite genotypes");
   }
+  RoctxRange reff("gbm: marker effects + download");
   std::vector<std::vector<double>> msums(shards.size(), std::vector<double>(nrhs, 0.0));
   std::vector<double> mu(nrhs, 0.0);
   for (size_t k = 0; k < shards.size(); k++) {
@@ -372,6 +383,7 @@ extern "C" int gbm_release_device_cache(void) {
 extern "C" int gbm_gblup_fit(const double* X, int64_t n, int64_t p, int64_t ldx, const double* Y, int64_t ldy,
                              int64_t nrhs, double lambda, const int* devices, int ndev, double* b_hat_out,
                              double* y_pred_out, double* mu_out, int64_t* q_out) {
+  RoctxRange r_("gbm_gblup_fit");
   if (!X) return fail(GBM_E_ARG, "gbm_gblup_fit: X is NULL");
   Problem pr{Source::F64, X, nullptr, 1, n, p, ldx};
   return run_fit(pr, Y, ldy, nrhs, lambda, devices, ndev, b_hat_out, y_pred_out, mu_out, q_out);
@@ -380,6 +392,7 @@ extern "C" int gbm_gblup_fit(const double* X, int64_t n, int64_t p, int64_t ldx,
 extern "C" int gbm_gblup_fit_synthetic(uint64_t seed, int64_t n, int64_t p, const double* Y, int64_t ldy, int64_t nrhs,
                                        double lambda, const int* devices, int ndev, double* b_hat_out,
                                        double* y_pred_out, double* mu_out, int64_t* q_out) {
+  RoctxRange r_("gbm_gblup_fit_synthetic");
   if (n < 1 || p < 1) return fail(GBM_E_ARG, "gbm_gblup_fit_synthetic: bad arguments (n, p >= 1)");
   Problem pr{Source::SYNTH, nullptr, nullptr, 1, n, p, n};
   pr.seed = seed;
@@ -389,6 +402,7 @@ extern "C" int gbm_gblup_fit_synthetic(uint64_t seed, int64_t n, int64_t p, cons
 extern "C" int gbm_gblup_fit_dosage_i8(const int8_t* D, int64_t n, int64_t p, int64_t ldd, int ploidy, const double* Y,
                                        int64_t ldy, int64_t nrhs, double lambda, const int* devices, int ndev,
                                        double* b_hat_out, double* y_pred_out, double* mu_out, int64_t* q_out) {
+  RoctxRange r_("gbm_gblup_fit_dosage_i8");
   if (!D || ploidy < 1) return fail(GBM_E_ARG, "gbm_gblup_fit_dosage_i8: D is NULL or ploidy < 1");
   Problem pr{Source::I8, nullptr, D, ploidy, n, p, ldd};
   return run_fit(pr, Y, ldy, nrhs, lambda, devices, ndev, b_hat_out, y_pred_out, mu_out, q_out);
@@ -396,6 +410,7 @@ extern "C" int gbm_gblup_fit_dosage_i8(const int8_t* D, int64_t n, int64_t p, in
 
 extern "C" int gbm_grm(const double* X, int64_t n, int64_t p, int64_t ldx, const int* devices, int ndev, double* G_out,
                        int64_t ldg, int64_t* q_out) {
+  RoctxRange r_("gbm_grm");
   if (!X || !G_out || n < 1 || p < 1 || ldx < n || ldg < n) return fail(GBM_E_ARG, "gbm_grm: bad arguments");
   std::vector<int> devs;
   GBM_TRY(check_devices(devices, ndev, devs));
@@ -403,14 +418,23 @@ extern "C" int gbm_grm(const double* X, int64_t n, int64_t p, int64_t ldx, const
   std::vector<std::unique_ptr<Shard>> shards;
   GBM_TRY(make_shards(devs, p, shards));
   int64_t q = 0;
-  for (auto& sh : shards) {
-    GBM_TRY(prepare_shard(pr, *sh));
-    q += sh->q_host;
+  {
+    RoctxRange r("gbm: upload + standardise");
+    for (auto& sh : shards) {
+      GBM_TRY(prepare_shard(pr, *sh));
+      q += sh->q_host;
+    }
   }
   if (q_out) *q_out = q;
   if (q == 0) return fail(GBM_E_DATA, "no polymorphic locus-allele");
-  for (auto& sh : shards) GBM_TRY(grm_shard(pr, *sh));
-  GBM_TRY(allreduce_grm(shards, n));
+  {
+    RoctxRange r("gbm: GRM");
+    for (auto& sh : shards) GBM_TRY(grm_shard(pr, *sh));
+  }
+  {
+    RoctxRange r("gbm: partial-GRM all-reduce");
+    GBM_TRY(allreduce_grm(shards, n));
+  }
   FitCtx& c = shards[0]->x();
   GBM_HIP_TRY(hipSetDevice(c.dev));
   GBM_TRY(ensure(c.out, c.dev, n * n * 8));
@@ -448,6 +472,7 @@ extern "C" int gbm_colstats(const double* X, int64_t n, int64_t p, int64_t ldx, 
 
 extern "C" int gbm_predict(const double* X, int64_t n, int64_t p, int64_t ldx, const double* b_hat, int64_t ldb,
                            int64_t nrhs, int device, double* out, int64_t ldo) {
+  RoctxRange r_("gbm_predict");
   if (!X || !b_hat || !out || n < 1 || p < 1 || ldx < n || ldb < p + 1 || nrhs < 1 || ldo < n)
     return fail(GBM_E_ARG, "gbm_predict: bad arguments");
   std::vector<int> devs;

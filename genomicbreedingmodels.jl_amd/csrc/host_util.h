@@ -7,9 +7,20 @@
 #include <string>
 #include <vector>
 
+#include <rocprofiler-sdk-roctx/roctx.h>
+
 #include "gbm_internal.h"
 
 namespace gbm {
+
+// roctx range over a host phase (rocprofv3 --marker-trace shows the fit's phases beside the
+// kernel trace): an entry point, or one stage of it
+struct RoctxRange {
+  explicit RoctxRange(const char* name) { roctxRangePushA(name); }
+  ~RoctxRange() { roctxRangePop(); }
+  RoctxRange(const RoctxRange&) = delete;
+  RoctxRange& operator=(const RoctxRange&) = delete;
+};
 
 // RAII device allocation on a given device
 struct DevMem {

@@ -189,6 +189,7 @@ int reml_eval(gbm_session* s, double lambda, RemlEval& out) {
 using namespace gbm;
 
 extern "C" int gbm_session_create(const double* X, int64_t n, int64_t p, int64_t ldx, int device, gbm_session** out) {
+  RoctxRange r_("gbm_session_create");
   if (!out) return fail(GBM_E_ARG, "gbm_session_create: out is NULL");
   *out = nullptr;
   if (!X || n < 1 || p < 1 || ldx < n) return fail(GBM_E_ARG, "gbm_session_create: bad arguments");
@@ -214,6 +215,7 @@ extern "C" int gbm_session_create(const double* X, int64_t n, int64_t p, int64_t
 }
 
 extern "C" int gbm_session_create_synthetic(uint64_t seed, int64_t n, int64_t p, int device, gbm_session** out) {
+  RoctxRange r_("gbm_session_create_synthetic");
   if (!out) return fail(GBM_E_ARG, "gbm_session_create_synthetic: out is NULL");
   *out = nullptr;
   if (n < 1 || p < 1) return fail(GBM_E_ARG, "gbm_session_create_synthetic: bad arguments");
@@ -237,6 +239,7 @@ extern "C" int gbm_session_create_synthetic(uint64_t seed, int64_t n, int64_t p,
 
 extern "C" int gbm_session_create_dosage_i8(const int8_t* D, int64_t n, int64_t p, int64_t ldd, int ploidy,
                                             int device, gbm_session** out) {
+  RoctxRange r_("gbm_session_create_dosage_i8");
   if (!out) return fail(GBM_E_ARG, "gbm_session_create_dosage_i8: out is NULL");
   *out = nullptr;
   if (!D || n < 1 || p < 1 || ldd < n || ploidy < 1)
@@ -272,6 +275,7 @@ extern "C" void gbm_session_destroy(gbm_session* s) {
 extern "C" int gbm_session_gblup_fit(gbm_session* s, const int64_t* idx, int64_t n_train, const double* Y, int64_t ldy,
                                      int64_t nrhs, double lambda, double* b_hat_out, double* y_pred_out, double* mu_out,
                                      int64_t* q_out) {
+  RoctxRange r_("gbm_session_gblup_fit");
   if (!s) return fail(GBM_E_ARG, "gbm_session_gblup_fit: session is NULL");
   if (!Y || ldy < n_train || nrhs < 1 || nrhs > 63 || !b_hat_out || !y_pred_out)
     return fail(GBM_E_ARG, "gbm_session_gblup_fit: bad arguments (ldy >= n_train, 1 <= nrhs <= 63, outputs)");
@@ -305,6 +309,7 @@ extern "C" int gbm_session_gblup_fit(gbm_session* s, const int64_t* idx, int64_t
 
 extern "C" int gbm_session_predict(gbm_session* s, const int64_t* idx, int64_t n_val, const double* b_hat, int64_t ldb,
                                    int64_t nrhs, double* out, int64_t ldo) {
+  RoctxRange r_("gbm_session_predict");
   if (!s) return fail(GBM_E_ARG, "gbm_session_predict: session is NULL");
   if (!b_hat || ldb < s->p + 1 || nrhs < 1 || !out || ldo < n_val)
     return fail(GBM_E_ARG, "gbm_session_predict: bad arguments");
@@ -355,6 +360,7 @@ extern "C" int gbm_session_reml_objective(gbm_session* s, const int64_t* idx, in
 
 extern "C" int gbm_session_reml(gbm_session* s, const int64_t* idx, int64_t n_train, const double* y,
                                 double* lambda_out, double* sigma2_e_out, double* sigma2_u_out, double* objective_out) {
+  RoctxRange r_("gbm_session_reml");
   if (!s) return fail(GBM_E_ARG, "gbm_session_reml: session is NULL");
   if (!y) return fail(GBM_E_ARG, "gbm_session_reml: y is NULL");
   std::lock_guard<std::mutex> lock(s->mu);
@@ -465,6 +471,7 @@ extern "C" int gbm_session_ridge_lambda_max(gbm_session* s, const int64_t* idx, 
 extern "C" int gbm_session_ridge_path(gbm_session* s, const int64_t* idx, int64_t n_train, const double* y,
                                       const double* lambdas, int64_t nl, double* b_path_out, const int64_t* idx_eval,
                                       int64_t n_eval, double* pred_out) {
+  RoctxRange r_("gbm_session_ridge_path");
   if (!s || !y || !lambdas || nl < 1 || !b_path_out || (n_eval > 0 && (!idx_eval || !pred_out)))
     return fail(GBM_E_ARG, "gbm_session_ridge_path: bad arguments");
   for (int64_t k = 0; k < nl; k++)
