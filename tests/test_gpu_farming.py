@@ -118,3 +118,35 @@ def test_gbm_devices_bad_ordinal_is_an_argument_error(monkeypatch):
     X = oracle.synth_genotypes(1, 50, 100)
     with pytest.raises(gbm.ArgumentError):
         gbm.gblup_arrays(X, np.arange(50.0))
+
+
+@pytest.mark.parametrize("chunk", [500, 1024])
+def test_pipelined_host_upload_matches_oracle(monkeypatch, chunk):
+    """gbm_gblup_fit with the host genotypes uploaded in loci chunks overlapped with the device
+    work (GBM_HOST_CHUNK, re-read per call): chunk GRMs summed in order into G. Matches the oracle
+    and the one-piece upload to rounding; the int8 entry (same chunks) stays bit-identical."""
+    n, p = 700, 2300
+    X = oracle.synth_genotypes(31, n, p)
+    Y = oracle.synth_phenotypes(X, 32, ntraits=2)
+    monkeypatch.setenv("GBM_HOST_CHUNK", str(chunk))
+    b_hat, y_pred, mu, q = gbm.gblup_arrays(X, Y, lambda_=0.8)
+    ref = oracle.gblup_fit(X, Y, 0.8)
+    assert q == ref["q"]
+    assert np.abs(y_pred - ref["y_pred"]).max() < 1e-9 * np.abs(ref["y_pred"]).max()
+    assert np.abs(b_hat - ref["b_hat"]).max() < 1e-6 * np.abs(ref["b_hat"]).max()
+    D = np.rint(X * 2).astype(np.int8)
+    lib = gbm.load_library()
+    nrhs = Y.shape[1]
+    Yf = np.asfortranarray(Y)
+    b2 = np.zeros((p + 1, nrhs), order="F")
+    y2 = np.zeros((n, nrhs), order="F")
+    mu2 = np.zeros(nrhs)
+    q2 = np.zeros(1, dtype=np.int64)
+    Df = np.asfortranarray(D)
+    rc = lib.gbm_gblup_fit_dosage_i8(Df.ctypes.data, n, p, n, 2, Yf.ctypes.data, n, nrhs, 0.8, None, 0,
+                                     b2.ctypes.data, y2.ctypes.data, mu2.ctypes.data, q2.ctypes.data)
+    assert rc == 0, lib.gbm_last_error()
+    assert np.array_equal(y2, y_pred) and np.array_equal(b2, b_hat)
+    monkeypatch.setenv("GBM_HOST_CHUNK", "0")
+    b3, y3, mu3, q3 = gbm.gblup_arrays(X, Y, lambda_=0.8)
+    assert q3 == q and np.abs(y3 - y_pred).max() < 1e-11 * np.abs(y3).max()
