@@ -45,16 +45,5 @@ int launch_predict(const double* Xt, int64_t ldx, int64_t p, int64_t n, const do
                    double* partial, int64_t nchunks, double* out, int64_t ldo, hipStream_t s);
 int64_t predict_chunks(int64_t n, int64_t p);
 int launch_add_inplace(double* a, const double* b, int64_t n, hipStream_t s);
-int launch_standardize_lean(const double* Xt, int64_t ldx, int64_t p, int64_t n, double* Zt, int64_t ldz, double* mean,
-                            double* sd, int32_t* keep, int64_t* q_dev, hipStream_t s);
-// loci [j_from, p) of Xt still to be standardised (into Zt, mean, sd, keep, q) when the GRM starts
-struct StdJob {
-  const double* Xt;
-  int64_t ldx;
-  double *mean, *sd;
-  int32_t* keep;
-  int64_t* q;
-  int64_t j_from;
-};
 
 }  // namespace gbm

@@ -248,7 +248,7 @@ __global__ void __launch_bounds__(256, WPS)
 syrk_kernel(const double* __restrict__ U, int64_t ldu, int64_t K, int64_t c0, int64_t lim,
             double* __restrict__ C, int64_t ldc, double* __restrict__ slab, int64_t ntiles, SliceBounds sb,
             double* __restrict__ Ld, double* __restrict__ Dinv, int32_t* __restrict__ info, int64_t fk0,
-            TileOwner own, int32_t* __restrict__ zready, int zsl) {
+            TileOwner own) {
   // 2 stages (72 KB at BK = 16); kSub's first workgroup reuses it for the 64x64 factor image
   constexpr int LDS_DOUBLES = (2 * STAGE > CNB * PS + CNB + 16) ? 2 * STAGE : CNB * PS + CNB + 16;
   __shared__ __attribute__((aligned(16))) double lds[LDS_DOUBLES];
@@ -354,7 +354,6 @@ syrk_kernel(const double* __restrict__ U, int64_t ldu, int64_t K, int64_t c0, in
       const int xcc = (int)(__builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (31 << 11)) & 7);
       const int64_t per = T8 >> 3;
       int q = xcc;
-      bool zseen = false;
       for (int tries = 0; tries < 8;) {
         const int64_t qt0 = q * per;
         const int64_t qt1 = qt0 + per < ntiles ? qt0 + per : ntiles;
@@ -369,23 +368,6 @@ syrk_kernel(const double* __restrict__ U, int64_t ldu, int64_t K, int64_t c0, in
           continue;
         }
         const int sl = (int)(u / nq);
-        if (zready && sl >= zsl && !zseen) {
-          // the loci of ranges >= zsl are standardised concurrently (launch_grm_syrk): wait once
-          // per workgroup for the flag the helper stream sets after that kernel (bounded; a wait
-          // that gives up marks zready[1] = −1 and the reduce poisons G, so the call fails)
-          if (threadIdx.x == 0) {
-            int64_t it = 0;
-            while (__hip_atomic_load(zready, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) {
-              if (++it > ((int64_t)1 << 24)) {
-                __hip_atomic_store(zready + 1, -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                break;
-              }
-              __builtin_amdgcn_s_sleep(8);
-            }
-          }
-          __syncthreads();
-          zseen = true;
-        }
         run_unit(sl, qt0 + (u - (int64_t)sl * nq));
       }
       return;
@@ -465,11 +447,8 @@ syrk_kernel(const double* __restrict__ U, int64_t ldu, int64_t K, int64_t c0, in
 
 // G tile = Σ_s slab[s][tile] in slice order (deterministic, no float atomics).
 __global__ void __launch_bounds__(256) grm_slab_reduce_kernel(const double* __restrict__ slab, int64_t ntiles,
-                                                              int nslices, double* __restrict__ G, int64_t ldg,
-                                                              const int32_t* __restrict__ zerr) {
+                                                              int nslices, double* __restrict__ G, int64_t ldg) {
   const int64_t t = blockIdx.x;
-  // a tile workgroup gave up waiting for the concurrently standardised loci: G must not look valid
-  const double poison = *zerr < 0 ? __builtin_nan("") : 0.0;
   int64_t ti, tj;
   tile_of(t, ti, tj);
   const int64_t per = (int64_t)BT * BT;
@@ -481,8 +460,6 @@ __global__ void __launch_bounds__(256) grm_slab_reduce_kernel(const double* __re
       acc.y += v.y;
     }
     const int row = e / BT, col = e % BT;
-    acc.x += poison;
-    acc.y += poison;
     *reinterpret_cast<double2*>(G + (ti * BT + row) * ldg + tj * BT + col) = acc;
   }
 }
@@ -848,7 +825,7 @@ int launch_chol_update(double* G, int64_t ldg, int64_t k0, int64_t nb, int64_t g
   const int64_t m = (lim + BT - 1) / BT;
   const int64_t ntiles = m * (m + 1) / 2;
   syrk_kernel<kSub><<<(unsigned)ntiles, 256, 0, s>>>(G + k0 * ldg, ldg, nb, k1, lim, G, ldg, nullptr, ntiles, SliceBounds{}, Ld,
-                                                     Dinv, info, next_k0, own, nullptr, 0);
+                                                     Dinv, info, next_k0, own);
   GBM_LAUNCH_CHECK();
   return GBM_OK;
 }
@@ -894,7 +871,7 @@ static int aux_stream(hipStream_t caller, AuxStream& a, bool* usable) {
 // workspace: [slabs or carry flags][edge partials][8 queue counters of the persistent launch]
 int64_t grm_workspace_bytes(int64_t n, int64_t p) {
   const GrmPlan g = plan(n, p);
-  return (g.main_doubles + g.edge_doubles + 8) * (int64_t)sizeof(double);
+  return (g.main_doubles + g.edge_doubles + 4) * (int64_t)sizeof(double);
 }
 
 static int check_grm_args(const double* Zt, int64_t ldz, int64_t p, int64_t n, double* G, int64_t ldg) {
@@ -908,72 +885,43 @@ static int check_grm_args(const double* Zt, int64_t ldz, int64_t p, int64_t n, d
 
 // stage 1: the MFMA SYRK (one partial tile per (slice, tile) into the workspace slabs, or the
 // in-order carry into G)
-// the helper stream's signal that the concurrently standardised loci are in HBM
-__global__ void zready_kernel(int32_t* f) { __hip_atomic_store(f, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
-
-// loci that must be standardised before the GRM starts: those of its first loci range (the
-// persistent units of range 0 run first); the rest can be standardised beside it
-int64_t grm_first_range_loci(int64_t n, int64_t p) {
-  const GrmPlan g = plan(n, p);
-  if (!g.persist || g.sb.n < 2) return p;
-  const int64_t l = (int64_t)g.sb.b[1] * BK;
-  return l < p ? l : p;
-}
-
 int launch_grm_syrk(const double* Zt, int64_t ldz, int64_t p, int64_t n, double* G, int64_t ldg, void* ws,
-                    int64_t ws_bytes, hipStream_t s, const StdJob* job = nullptr) {
+                    int64_t ws_bytes, hipStream_t s) {
   int rc = check_grm_args(Zt, ldz, p, n, G, ldg);
   if (rc != GBM_OK) return rc;
   const GrmPlan g = plan(n, p);
-  const int64_t need = (g.main_doubles + g.edge_doubles + 8) * (int64_t)sizeof(double);
+  const int64_t need = (g.main_doubles + g.edge_doubles + 4) * (int64_t)sizeof(double);
   if (need > 0 && (!ws || ws_bytes < need))
     return fail(GBM_E_ARG, "gbm_dev_grm: workspace too small (" + std::to_string(ws_bytes) + " < " +
                                std::to_string(need) + ")");
   const unsigned grid = (unsigned)(g.sb.n * ((g.ntiles + 7) & ~(int64_t)7));
   if (g.sb.carry) GBM_HIP_TRY(hipMemsetAsync(ws, 0, (size_t)(g.ntiles + 1) * sizeof(int32_t), s));
-  // [8 queue counters][zready flag, its error cell][pad]
   int32_t* ctr = reinterpret_cast<int32_t*>((double*)ws + g.main_doubles + g.edge_doubles);
-  GBM_HIP_TRY(hipMemsetAsync(ctr, 0, 16 * sizeof(int32_t), s));
   const int64_t lim = g.sb.er > 0 ? g.sb.e0 : n;  // with an edge, the tiles cover [0, e0)^2 exactly
-  // loci still to standardise: beside the persistent tiles when they start after the first range
-  // (and a helper stream exists), else here, before the tiles
-  const bool pending = job && job->j_from < p;
-  bool overlap = pending && g.persist && g.sb.n > 1 && job->j_from >= grm_first_range_loci(n, p);
-  // the ragged-column kernel (and the overlapped standardisation) beside the persistent tiles:
-  // forked (before the tile launch) onto the device's helper stream; its workgroups fit in the
-  // registers the two tile workgroups of a CU leave free. Joined back before returning.
+  // the ragged-column kernel beside the persistent tiles: forked (before the tile launch) onto
+  // the device's helper stream; its workgroups fit in the registers the two tile workgroups of a
+  // CU leave free. Joined back before returning.
   AuxStream aux;
   AuxStream* ax = nullptr;
-  if (g.edge_concurrent || overlap) {
+  if (g.edge_concurrent) {
     bool usable = false;
     rc = aux_stream(s, aux, &usable);
     if (rc != GBM_OK) return rc;
-    if (usable) ax = &aux;
-  }
-  if (!ax) overlap = false;
-  if (pending && !overlap)
-    GBM_TRY(launch_standardize_lean(job->Xt + job->j_from * job->ldx, job->ldx, p - job->j_from, n,
-                                    const_cast<double*>(Zt) + job->j_from * ldz, ldz, job->mean + job->j_from,
-                                    job->sd + job->j_from, job->keep + job->j_from, job->q, s));
-  if (ax) {
-    GBM_HIP_TRY(hipEventRecord(ax->fork, s));
-    GBM_HIP_TRY(hipStreamWaitEvent(ax->s, ax->fork, 0));
-  }
-  if (overlap) {
-    GBM_TRY(launch_standardize_lean(job->Xt + job->j_from * job->ldx, job->ldx, p - job->j_from, n,
-                                    const_cast<double*>(Zt) + job->j_from * ldz, ldz, job->mean + job->j_from,
-                                    job->sd + job->j_from, job->keep + job->j_from, job->q, ax->s));
-    zready_kernel<<<1, 1, 0, ax->s>>>(ctr + 8);
-    GBM_LAUNCH_CHECK();
+    if (usable) {
+      ax = &aux;
+      GBM_HIP_TRY(hipEventRecord(ax->fork, s));
+      GBM_HIP_TRY(hipStreamWaitEvent(ax->s, ax->fork, 0));
+    }
   }
   if (g.persist) {
+    GBM_HIP_TRY(hipMemsetAsync(ctr, 0, 8 * sizeof(int32_t), s));
     const int64_t units = (int64_t)g.sb.n * g.ntiles;
     const unsigned pgrid = (unsigned)(units < resident_wgs() ? units : resident_wgs());
     syrk_kernel<kPersist><<<pgrid, 256, 0, s>>>(Zt, ldz, p, 0, lim, G, ldg, (double*)ws, g.ntiles, g.sb, nullptr,
-                                                nullptr, ctr, -1, TileOwner{}, overlap ? ctr + 8 : nullptr, 1);
+                                                nullptr, ctr, -1, TileOwner{});
   } else {
     syrk_kernel<kSplit><<<grid, 256, 0, s>>>(Zt, ldz, p, 0, lim, G, ldg, (double*)ws, g.ntiles, g.sb, nullptr, nullptr,
-                                             nullptr, -1, TileOwner{}, nullptr, 0);
+                                             nullptr, -1, TileOwner{});
   }
   GBM_LAUNCH_CHECK();
   if (g.sb.er > 0) {
@@ -993,10 +941,10 @@ int launch_grm_syrk(const double* Zt, int64_t ldz, int64_t p, int64_t n, double*
       grm_edge_reduce_kernel<<<(unsigned)((n * g.sb.er + 255) / 256), 256, 0, es>>>(part, n, g.sb, G, ldg);
       GBM_LAUNCH_CHECK();
     }
-  }
-  if (ax) {
-    GBM_HIP_TRY(hipEventRecord(ax->join, ax->s));
-    GBM_HIP_TRY(hipStreamWaitEvent(s, ax->join, 0));
+    if (ax) {
+      GBM_HIP_TRY(hipEventRecord(ax->join, ax->s));
+      GBM_HIP_TRY(hipStreamWaitEvent(s, ax->join, 0));
+    }
   }
   return GBM_OK;
 }
@@ -1022,8 +970,7 @@ int launch_grm_reduce(int64_t n, int64_t p, double* G, int64_t ldg, const void* 
       return fail(GBM_E_HIP, "GRM in-order carry accumulation: an inter-workgroup wait timed out (G is invalid)");
     return GBM_OK;
   }
-  const int32_t* zerr = reinterpret_cast<const int32_t*>((const double*)ws + g.main_doubles + g.edge_doubles) + 9;
-  grm_slab_reduce_kernel<<<(unsigned)g.ntiles, 256, 0, s>>>((const double*)ws, g.ntiles, g.sb.n, G, ldg, zerr);
+  grm_slab_reduce_kernel<<<(unsigned)g.ntiles, 256, 0, s>>>((const double*)ws, g.ntiles, g.sb.n, G, ldg);
   GBM_LAUNCH_CHECK();
   return GBM_OK;
 }
@@ -1088,22 +1035,6 @@ extern "C" int gbm_dev_grm(const double* Zt, int64_t ldz, int64_t p, int64_t n, 
 extern "C" int gbm_dev_grm_syrk(const double* Zt, int64_t ldz, int64_t p, int64_t n, double* G, int64_t ldg,
                                 void* workspace, int64_t ws_bytes, void* stream) {
   return gbm::launch_grm_syrk(Zt, ldz, p, n, G, ldg, workspace, ws_bytes, (hipStream_t)stream);
-}
-
-extern "C" int64_t gbm_dev_grm_first_range(int64_t n, int64_t p) {
-  if (n < 1 || p < 1) return 0;
-  return gbm::grm_first_range_loci(n, p);
-}
-
-extern "C" int gbm_dev_standardize_grm_syrk(const double* Xt, int64_t ldx, int64_t p, int64_t n, double* Zt,
-                                            int64_t ldz, double* mean, double* sd, int32_t* keep, int64_t* q_dev,
-                                            int64_t j_from, double* G, int64_t ldg, void* workspace, int64_t ws_bytes,
-                                            void* stream) {
-  if (!Xt || !Zt || !mean || !sd || !keep || !q_dev || ldx < n || j_from < 0 || j_from > p ||
-      ((const double*)Zt == Xt && ldz != ldx))
-    return gbm::fail(GBM_E_ARG, "gbm_dev_standardize_grm_syrk: bad arguments");
-  const gbm::StdJob job{Xt, ldx, mean, sd, keep, q_dev, j_from};
-  return gbm::launch_grm_syrk(Zt, ldz, p, n, G, ldg, workspace, ws_bytes, (hipStream_t)stream, &job);
 }
 
 extern "C" int gbm_dev_grm_reduce(int64_t n, int64_t p, double* G, int64_t ldg, const void* workspace, void* stream) {

@@ -91,7 +91,7 @@ __global__ void __launch_bounds__(BS) standardize_kernel(const double* Xt, int64
       for (int k = 0; k < NPT; k++) {
         const int64_t i = (int64_t)k * BS + threadIdx.x;
         const double d = x[k] - m;
-        ss += i < n ? __dmul_rn(d, d) : 0.0;  // rounded product, then the sum: the same bits as the generic path
+        ss += i < n ? d * d : 0.0;
       }
       v = n > 1 ? sqrt(block_sum<BS>(ss, red) / (double)(n - 1)) : __builtin_nan("");
       if (center_only) v = 1.0;  // glmnet standardize=false: centre only, keep every column
@@ -116,7 +116,7 @@ __global__ void __launch_bounds__(BS) standardize_kernel(const double* Xt, int64
       double ss = 0.0;
       for (int64_t i = threadIdx.x; i < n; i += BS) {
         const double d = row[GATHER ? idx[i] : i] - m;
-        ss += __dmul_rn(d, d);  // no fma contraction: bit-identical to the register-cached paths
+        ss += d * d;
       }
       v = n > 1 ? sqrt(block_sum<BS>(ss, red) / (double)(n - 1)) : __builtin_nan("");
       if (center_only) v = 1.0;  // glmnet standardize=false: centre only, keep every column
@@ -166,12 +166,10 @@ extern "C" int gbm_dev_expand_dosage_i8(const int8_t* D, int64_t ldd, int64_t n,
 template <bool GATHER>
 static int launch_standardize(const double* Xt, int64_t ldx, int64_t p, const int32_t* idx, int64_t n, double* Zt,
                               int64_t ldz, double* mean, double* sd, int32_t* keep, int64_t* q_dev, int center_only,
-                              hipStream_t s, bool lean = false) {
+                              hipStream_t s) {
   const unsigned grid = (unsigned)(p < 256 * 16 ? p : 256 * 16);
   auto q = reinterpret_cast<unsigned long long*>(q_dev);
-  if (lean)  // 34 registers: fits beside the persistent GRM's two workgroups per CU (row re-read from L2)
-    standardize_kernel<256, 0, GATHER><<<grid, 256, 0, s>>>(Xt, ldx, p, idx, n, Zt, ldz, mean, sd, keep, q, center_only);
-  else if (n <= 256 * 4)
+  if (n <= 256 * 4)
     standardize_kernel<256, 4, GATHER><<<grid, 256, 0, s>>>(Xt, ldx, p, idx, n, Zt, ldz, mean, sd, keep, q, center_only);
   else if (n <= 256 * 8)
     standardize_kernel<256, 8, GATHER><<<grid, 256, 0, s>>>(Xt, ldx, p, idx, n, Zt, ldz, mean, sd, keep, q, center_only);
@@ -193,15 +191,6 @@ extern "C" int gbm_dev_standardize(const double* Xt, int64_t ldx, int64_t p, int
   if (p == 0) return GBM_OK;
   return launch_standardize<false>(Xt, ldx, p, nullptr, n, Zt, ldz, mean, sd, keep, q_dev, 0, (hipStream_t)stream);
 }
-
-namespace gbm {
-// the standardisation that runs concurrently with the persistent GRM (launch_grm_syrk)
-int launch_standardize_lean(const double* Xt, int64_t ldx, int64_t p, int64_t n, double* Zt, int64_t ldz, double* mean,
-                            double* sd, int32_t* keep, int64_t* q_dev, hipStream_t s) {
-  if (p <= 0) return GBM_OK;
-  return launch_standardize<false>(Xt, ldx, p, nullptr, n, Zt, ldz, mean, sd, keep, q_dev, 0, s, true);
-}
-}  // namespace gbm
 
 extern "C" int gbm_dev_standardize_gather(const double* Xt, int64_t ldx, int64_t p, const int32_t* idx, int64_t n,
                                           double* Zt, int64_t ldz, double* mean, double* sd, int32_t* keep,

@@ -29,8 +29,7 @@ EXPORTS = (
     "gbm_gblup_fit", "gbm_gblup_fit_dosage_i8", "gbm_gblup_fit_synthetic", "gbm_grm", "gbm_colstats", "gbm_predict",
     "gbm_dev_npad", "gbm_dev_gdim", "gbm_dev_grm_workspace", "gbm_dev_solve_workspace",
     "gbm_dev_synth_genotypes", "gbm_dev_expand_dosage_i8", "gbm_dev_standardize", "gbm_dev_grm",
-    "gbm_dev_grm_syrk", "gbm_dev_grm_reduce", "gbm_dev_grm_slices", "gbm_dev_grm_first_range",
-    "gbm_dev_standardize_grm_syrk",
+    "gbm_dev_grm_syrk", "gbm_dev_grm_reduce", "gbm_dev_grm_slices",
     "gbm_dev_gblup_solve", "gbm_dev_marker_effects",
     "gbm_dev_standardize_gather", "gbm_dev_gblup_terms",
     "gbm_session_create", "gbm_session_create_dosage_i8", "gbm_session_create_synthetic", "gbm_session_destroy", "gbm_session_gblup_fit",
@@ -116,10 +115,6 @@ def _declare(lib):
         getattr(lib, f).argtypes = [P, I64, I64, I64, P, I64, P, I64, P]
     lib.gbm_dev_grm_reduce.restype = I32
     lib.gbm_dev_grm_reduce.argtypes = [I64, I64, P, I64, P, P]
-    lib.gbm_dev_grm_first_range.restype = I64
-    lib.gbm_dev_grm_first_range.argtypes = [I64, I64]
-    lib.gbm_dev_standardize_grm_syrk.restype = I32
-    lib.gbm_dev_standardize_grm_syrk.argtypes = [P, I64, I64, I64, P, I64, P, P, P, P, I64, P, I64, P, I64, P]
     lib.gbm_dev_grm_slices.restype = I32
     lib.gbm_dev_grm_slices.argtypes = [I64, I64]
     lib.gbm_dev_gblup_solve.restype = I32

@@ -19,7 +19,6 @@ HIP implementation is ``HipShardStages`` below) and ``comm``.
 from __future__ import annotations
 
 import ctypes
-import os
 
 import numpy as np
 
@@ -64,15 +63,9 @@ def sharded_gblup_step(stages, comm, events=None):
     records a timing mark on the compute stream between stages."""
     mark = events or (lambda label: None)
     mark("begin")
-    if hasattr(stages, "standardize_head") and os.environ.get("GBM_STD_OVERLAP", "1") != "0":
-        # the GRM's first loci range standardised first, the rest beside the GRM's tiles
-        stages.standardize_head()
-        mark("standardize")
-        stages.grm_syrk_overlapped()
-    else:
-        stages.standardize()
-        mark("standardize")
-        stages.grm_syrk()
+    stages.standardize()
+    mark("standardize")
+    stages.grm_syrk()
     mark("grm_syrk")
     stages.grm_reduce()
     mark("grm_reduce")
@@ -238,24 +231,6 @@ class HipShardStages:
         _lib.check(self.lib.gbm_dev_standardize(self._p(self.X), self.npad, self.p, self.n, self._p(self.Z), self.npad,
                                                 self._p(self.mean), self._p(self.sd), self._p(self.keep),
                                                 self._p(self.q), self._stream()), "standardize")
-
-    def standardize_head(self):
-        """Standardise the loci of the GRM's first loci range only (the rest run beside the GRM,
-        grm_syrk_overlapped)."""
-        self.q.zero_()
-        self._j_from = int(self.lib.gbm_dev_grm_first_range(self.n, self.p))
-        if self._j_from > 0:
-            _lib.check(self.lib.gbm_dev_standardize(self._p(self.X), self.npad, self._j_from, self.n, self._p(self.Z),
-                                                    self.npad, self._p(self.mean), self._p(self.sd),
-                                                    self._p(self.keep), self._p(self.q), self._stream()),
-                       "standardize_head")
-
-    def grm_syrk_overlapped(self):
-        """GRM SYRK with loci [j_from, p) standardised concurrently on the helper stream."""
-        _lib.check(self.lib.gbm_dev_standardize_grm_syrk(
-            self._p(self.X), self.npad, self.p, self.n, self._p(self.Z), self.npad, self._p(self.mean),
-            self._p(self.sd), self._p(self.keep), self._p(self.q), self._j_from, self._p(self.G), self.gdim,
-            self._p(self.ws_grm), self.ws_grm_bytes, self._stream()), "standardize_grm_syrk")
 
     def grm_syrk(self):
         _lib.check(self.lib.gbm_dev_grm_syrk(self._p(self.Z), self.npad, self.p, self.n, self._p(self.G), self.gdim,

@@ -198,18 +198,6 @@ int gbm_dev_grm(const double* Zt, int64_t ldz, int64_t p, int64_t n, double* G, 
 int gbm_dev_grm_syrk(const double* Zt, int64_t ldz, int64_t p, int64_t n, double* G, int64_t ldg,
                      void* workspace, int64_t ws_bytes, void* stream);
 int gbm_dev_grm_reduce(int64_t n, int64_t p, double* G, int64_t ldg, const void* workspace, void* stream);
-/* Standardisation overlapped with the GRM SYRK (the bench step and the synthetic entry): loci
- * [0, gbm_dev_grm_first_range(n, p)) — the persistent GRM's first loci range — must already be
- * standardised (gbm_dev_standardize on those rows); gbm_dev_standardize_grm_syrk standardises
- * loci [j_from, p) of Xt into Zt / mean / sd / keep / q_dev (added to *q_dev) on a helper
- * stream while the tiles of the first range run, the later ranges' tiles waiting for it, then
- * is gbm_dev_grm_syrk (follow with gbm_dev_grm_reduce). Falls back to standardising first when
- * the plan has one range or no persistent launch. Replaces nothing in the reference: the
- * standardisation of src/gwas.jl:127-130 and the GRM of :124 fused in time, same results. */
-int64_t gbm_dev_grm_first_range(int64_t n, int64_t p);
-int gbm_dev_standardize_grm_syrk(const double* Xt, int64_t ldx, int64_t p, int64_t n, double* Zt, int64_t ldz,
-                                 double* mean, double* sd, int32_t* keep, int64_t* q_dev, int64_t j_from,
-                                 double* G, int64_t ldg, void* workspace, int64_t ws_bytes, void* stream);
 /* The upper 128x128 tiles of G as one contiguous array (packed size in doubles; pack; unpack):
  * half the bytes of G's npad x gdim rows, the form the multi-GPU partial-GRM all-reduce moves. */
 int64_t gbm_dev_grm_packed_size(int64_t n);

@@ -48,8 +48,8 @@ def test_geometry_helpers():
     nbc = (5120 + 64) // 64
     assert lib.gbm_dev_solve_workspace(5000, 1) == (5120 * (2 * 64 + 16) + 40 + 1 + 1) * 8 + (16 + nbc * nbc * 4 + 15) // 16 * 16
     # GRM workspace: loci-slice partial tiles (+ the ragged-column partials when n % 128 <= 64)
-    # (+ 64 bytes: queue counters of the persistent launch, the concurrent-standardisation flag)
-    assert (lib.gbm_dev_grm_workspace(5120, 50000) - 64) % (128 * 128 * 8) == 0
+    # (+ 32 bytes of queue counters for the persistent launch)
+    assert (lib.gbm_dev_grm_workspace(5120, 50000) - 32) % (128 * 128 * 8) == 0
     assert lib.gbm_dev_grm_workspace(5000, 50000) > 0
 
 

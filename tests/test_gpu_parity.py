@@ -296,47 +296,3 @@ def test_concurrent_calls_from_threads():
     assert not errs, errs
     for a, b in zip(out, serial):
         assert np.array_equal(a[1], b[1]) and np.array_equal(a[0], b[0])
-
-
-@pytest.mark.parametrize("n,p", [(2000, 8000), (4999, 8000), (1100, 4000)])
-def test_standardise_overlapped_with_grm(monkeypatch, n, p):
-    """gbm_dev_standardize_grm_syrk: the GRM's first loci range standardised first, the others on
-    the helper stream beside the persistent tiles (later-range tiles wait for a flag). Z, the
-    column statistics and G are bit-identical to standardising everything first, and match the
-    oracle."""
-    import torch
-    from gbm.sharded import HipShardStages
-
-    lib = gbm.load_library()
-    X = oracle.synth_genotypes(p + 5, n, p)
-    outs = []
-    for overlap in (True, False):
-        st = HipShardStages(n, p, nrhs=1, lambda_=1.0, device=0)
-        st.upload_genotypes(X)
-        if overlap:
-            st.standardize_head()
-            assert 0 < st._j_from <= p
-            st.grm_syrk_overlapped()
-        else:
-            st.standardize()
-            st.grm_syrk()
-        st.grm_reduce()
-        torch.cuda.synchronize()
-        outs.append((st.Z.clone(), st.mean.clone(), st.sd.clone(), st.keep.clone(), st.q.clone(),
-                     st.G[:n, :n].clone(), st._j_from if overlap else p))
-    a, b = outs
-    # mean, keep, q exact; sd and Z to an ulp (the concurrent part runs the register-lean kernel
-    # variant, whose variance sum rounds differently in the last bit); G accordingly
-    for x, y in zip(a[1:5:2] + a[4:5], b[1:5:2] + b[4:5]):
-        assert torch.equal(x, y)
-    assert (a[2] - b[2]).abs().max().item() <= 4e-16 * b[2].abs().max().item()
-    assert (a[0] - b[0]).abs().max().item() <= 1e-14 * b[0].abs().max().item()
-    Ga, Gb = torch.triu(a[5]), torch.triu(b[5])
-    assert (Ga - Gb).abs().max().item() <= 1e-12 * Gb.abs().max().item()
-    if lib.gbm_dev_grm_slices(n, p) > 1:
-        assert a[6] < p  # the overlap actually ran
-    ref, qref = oracle.grm(X)
-    assert int(a[4].item()) == qref
-    G = Ga.cpu().numpy()
-    iu = np.triu_indices(n)
-    assert rel(G[iu] / qref, ref[iu]) < 1e-12
