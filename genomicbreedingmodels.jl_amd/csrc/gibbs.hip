@@ -4,14 +4,13 @@
 // The chain is BGLR's single-site sampler (intercept, then every marker j in order with the
 // residual update e += (b_old − b_new) x_j, then σ²_b and σ²_e from scaled-inverse-χ² draws;
 // BGLR defaults df0 = 5, R2 = 0.5; running posterior means every `thin` iterations after
-// burn-in). MI355X mapping: markers go in blocks of 64. For a block, x_jᵀe of all 64 markers
-// is computed at once (one workgroup per marker), then the 64 sequential single-site steps run
-// inside one wave from the block's 64x64 Gram matrix W = X_BᵀX_B (precomputed once):
-// d_k = x_kᵀe is kept current by d_k += δ_j W[j][k] — exactly the residual update restricted to
-// the block — and finally e += X_B δ over all individuals. Every workgroup of that last kernel
-// replays the 64 steps redundantly from identical inputs (deterministic), so the block costs two
-// launches and no device-wide synchronisation; one Gibbs iteration is captured as a hipGraph and
-// replayed.
+// burn-in). MI355X mapping: markers go in blocks of 64 (128 per launch with byte storage). For a
+// block, x_kᵀe of its markers comes from per-chunk partial dots (computed by the previous launch),
+// and the block's sequential single-site steps are one unit-lower-triangular solve (I + L) δ = r̃
+// whose inverse M is rebuilt for every block once per iteration (it depends on σ²_e/σ²_b): every
+// workgroup applies δ = M r̃ redundantly from identical inputs (deterministic), updates e += X_B δ
+// on its individuals and computes the next block's partial dots, so a block costs one launch and
+// no device-wide synchronisation; one Gibbs iteration is captured as a hipGraph and replayed.
 //
 // Random numbers: a counter-based hash of (seed, stream, counter) (no sampler state), Box-Muller
 // normals and Marsaglia-Tsang gammas, restated bit-for-bit in oracle/oracle.py (brr_*), so the
@@ -158,9 +157,9 @@ constexpr int IW = 256;  // individuals per workgroup in the block kernels
 // x = d·xs when every x/xs is an integer in [0, 255] (xs = 1/2 for diploid dosages: exact, so
 // both storages run the identical chain with 8× fewer bytes per block for the bytes).
 // 64 byte-genotypes (4 × 16 B) times 64 values of es, accumulated in the fp64 path's order:
-// even individuals into s, odd ones into s1.
-__device__ __forceinline__ void brr_dot64_u8(const uint4 (&v)[4], const double* es, double xs, double& s,
-                                             double& s1) {
+// even individuals into s, odd ones into s1. The bytes are summed unscaled and the caller scales
+// both sums by xs: xs is a power of two, so (Σ d e)·xs has the bits of Σ (d·xs) e.
+__device__ __forceinline__ void brr_dot64_u8(const uint4 (&v)[4], const double* es, double& s, double& s1) {
 #pragma unroll
   for (int u = 0; u < 4; u++) {
     const uint32_t wd[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
@@ -169,8 +168,8 @@ __device__ __forceinline__ void brr_dot64_u8(const uint4 (&v)[4], const double* 
 #pragma unroll
       for (int b = 0; b < 4; b += 2) {
         const int idx = 16 * u + 4 * w + b;
-        s = fma((double)((wd[w] >> (8 * b)) & 0xFFu) * xs, es[idx], s);
-        s1 = fma((double)((wd[w] >> (8 * b + 8)) & 0xFFu) * xs, es[idx + 1], s1);
+        s = fma((double)((wd[w] >> (8 * b)) & 0xFFu), es[idx], s);
+        s1 = fma((double)((wd[w] >> (8 * b + 8)) & 0xFFu), es[idx + 1], s1);
       }
   }
 }
@@ -206,7 +205,9 @@ __device__ __forceinline__ void brr_partials(const T* __restrict__ Xt, int64_t l
       uint4 v[4];
 #pragma unroll
       for (int u = 0; u < 4; u++) v[u] = *reinterpret_cast<const uint4*>(row + 16 * u);
-      brr_dot64_u8(v, es + qt * 64, xs, s, s1);
+      brr_dot64_u8(v, es + qt * 64, s, s1);
+      s *= xs;
+      s1 *= xs;
     }
     s += s1;
   }
@@ -215,27 +216,160 @@ __device__ __forceinline__ void brr_partials(const T* __restrict__ Xt, int64_t l
   if (qt == 0) out[blockIdx.x * BB + k] = s;  // k >= nb writes 0
 }
 
-// The 64 single-site steps of one 64-marker block on one wave. Lane k holds marker k: d = x_kᵀe
-// (kept current), its Gram row w, and the conditional draw b_new = α d + β folded into
-// δ = b_old − b_new = γ − α d (γ = b_old − β). Step s: lane s's δ_s is broadcast (v_readlane) and
-// d_k += δ_s W[s][k]; the dependent chain per step is fma -> readlane -> fma (lane s keeps its own
-// δ_s off the chain). Returns δ_k in lane k.
-__device__ __forceinline__ double brr_block_steps(double d, const double (&w)[BB], double nalpha, double gamma,
-                                                  int lane) {
-  double dk = 0.0;
+// The single-site steps of a 64-marker block as one triangular solve. Marker k's conditional draw
+// is b_new = α_k d_k + β_k with d_k = x_kᵀe at its turn, so δ_k = b_old − b_new = γ_k − α_k d_k
+// (γ = b_old − β). Step s changes every later d_k by δ_s W[s][k], hence with d⁰ = x_kᵀe at block
+// start and r̃ = γ − α∘d⁰:
+//   δ_s + α_s Σ_{t<s} W[s][t] δ_t = r̃_s,  i.e.  (I + L) δ = r̃,  L[s][t] = α_s W[s][t] (t < s).
+// α_k = 1 / (x_kᵀx_k + σ²_e/σ²_b) and γ depend only on the iteration's variances, b_old and the
+// iteration's normals, so M = (I + L)⁻¹ (unit lower triangular) and γ are computed for every block
+// once per iteration (brr_prep_kernel) and a launch applies δ = M r̃ as one GEMV — no chain of 64
+// dependent steps. Two halves A, B of a 128-marker launch: B's d⁰ also misses A's changes
+// (d_B = d⁰_B + W_BA δ_A), so δ_B = M_B r̃_B + O r̃_A with O = −M_B diag(α_B) W_BA M_A.
+//
+// brr_prep_kernel: α, γ of every marker; per 64-marker half-block, lane j of one wave solves column
+// j of M by forward substitution (its column in registers, W's rows broadcast from LDS).
+// nw = 1 (64-marker launches): 4 blocks per workgroup, Mb[b] = M_b. nw = 3 (128-marker launches):
+// one 128-marker block per workgroup, Mb[3b] = M_A, Mb[3b + 1] = O, Mb[3b + 2] = M_B (row-major).
+__global__ void __launch_bounds__(256) brr_prep_kernel(const double* __restrict__ W, int64_t p, int64_t nblk, int nw,
+                                                       const double* __restrict__ x2, const double* __restrict__ b,
+                                                       const BrrState* __restrict__ st, double* __restrict__ Mb,
+                                                       double* __restrict__ alpha, double* __restrict__ gamma) {
+  __shared__ __attribute__((aligned(16))) double S[4][BB * BB];
+  __shared__ double alB[BB];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // the 64-marker half-block this wave inverts (nw = 3: waves 0, 1 = halves A, B)
+  const bool solver = nw == 1 ? (int64_t)blockIdx.x * 4 + wave < nblk : wave < 2;
+  const int64_t hb = nw == 1 ? (int64_t)blockIdx.x * 4 + wave : 2 * (int64_t)blockIdx.x + wave;
+  double* Sw = S[wave];
+  if (solver) {
+    const double* Wsrc = W + (nw == 1 ? hb : 3 * (int64_t)blockIdx.x + (wave == 0 ? 0 : 2)) * BB * BB;
+    double2 v[32];
 #pragma unroll
-  for (int s2 = 0; s2 < BB; s2++) {
-    union {
-      double f;
-      int i[2];
-    } u;
-    u.f = fma(d, nalpha, gamma);
-    dk = lane == s2 ? u.f : dk;
-    u.i[0] = __builtin_amdgcn_readlane(u.i[0], s2);
-    u.i[1] = __builtin_amdgcn_readlane(u.i[1], s2);
-    d = fma(u.f, w[s2], d);
+    for (int u = 0; u < 32; u++) v[u] = *reinterpret_cast<const double2*>(Wsrc + 2 * (lane + 64 * u));
+    const int64_t j = hb * BB + lane;
+    const bool on = j < p;
+    const double varE = st->varE, varB = st->varB;
+    const double xx = on ? x2[j] : 0.0;
+    const double bo = on ? b[(st->it & 1) * p + j] : 0.0;
+    const double c = 1.0 / (xx / varE + 1.0 / varB);
+    const double al = on ? c / varE : 0.0;
+    const double xi = on ? brr_normal(st->seed, 4 * (uint64_t)st->it, (uint64_t)j) : 0.0;
+    alpha[j] = al;  // padded to whole launches
+    gamma[j] = on ? bo - (xx * bo * al + sqrt(c) * xi) : 0.0;
+    if (nw == 3 && wave == 1) alB[lane] = al;
+#pragma unroll
+    for (int u = 0; u < 32; u++) *reinterpret_cast<double2*>(Sw + 2 * (lane + 64 * u)) = v[u];
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the wave's W rows are in LDS
+    // column `lane` of M: m_t = [t = lane] − α_t Σ_{u<t} W[t][u] m_u
+    double m[BB];
+#pragma unroll
+    for (int t = 0; t < BB; t++) {
+      double a0 = 0.0, a1 = 0.0;
+      if (t > 0) asm volatile("" : "+v"(m[t - 1])::"memory");  // row t's loads after row t − 1
+#pragma unroll
+      for (int c = 0; c < t; c += 32) {
+        // at most 32 values of W's row in flight: this chunk's loads wait for the previous
+        // chunk's FMAs (else the scheduler hoists every load of the solve and spills)
+        asm volatile("" : "+v"(a0), "+v"(a1)::"memory");
+#pragma unroll
+        for (int u = c; u + 1 < t && u < c + 32; u += 2) {
+          const double2 w2 = *reinterpret_cast<const double2*>(Sw + t * BB + u);
+          a0 = fma(w2.x, m[u], a0);
+          a1 = fma(w2.y, m[u + 1], a1);
+        }
+      }
+      if (t & 1) a0 = fma(Sw[t * BB + t - 1], m[t - 1], a0);
+      union {
+        double f;
+        int i[2];
+      } at;
+      at.f = al;
+      at.i[0] = __builtin_amdgcn_readlane(at.i[0], t);
+      at.i[1] = __builtin_amdgcn_readlane(at.i[1], t);
+      m[t] = (lane == t ? 1.0 : 0.0) - at.f * (a0 + a1);
+    }
+    // M[t][lane] (coalesced rows); nw = 3 keeps M_A, M_B in LDS (this wave's W is no longer read)
+    double* Mo = Mb + (nw == 1 ? hb : 3 * (int64_t)blockIdx.x + (wave == 0 ? 0 : 2)) * BB * BB + lane;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int t = 0; t < BB; t++) {
+      Mo[t * BB] = m[t];
+      if (nw == 3) Sw[t * BB + lane] = m[t];
+    }
+  } else if (nw == 3) {
+    // waves 2-3 stage W_BA (row k = marker B_k) into S[2] meanwhile
+    const double* Wsrc = W + (3 * (int64_t)blockIdx.x + 1) * BB * BB;
+    const int t = tid - 128;
+    double2 v[16];
+#pragma unroll
+    for (int u = 0; u < 16; u++) v[u] = *reinterpret_cast<const double2*>(Wsrc + 2 * (t + 128 * u));
+#pragma unroll
+    for (int u = 0; u < 16; u++) *reinterpret_cast<double2*>(S[2] + 2 * (t + 128 * u)) = v[u];
   }
-  return dk;
+  if (nw != 3) return;
+  __syncthreads();
+  // K = diag(α_B) W_BA M_A into S[3]: thread (wave w, lane j) makes K[16w .. 16w + 15][j]
+  {
+    double col[BB];
+#pragma unroll
+    for (int s = 0; s < BB; s++) col[s] = S[0][s * BB + lane];
+#pragma unroll 1
+    for (int kk = 0; kk < 16; kk++) {
+      const int k = 16 * wave + kk;
+      double a0 = 0.0, a1 = 0.0;
+#pragma unroll
+      for (int c = 0; c < BB; c += 32) {
+        asm volatile("" : "+v"(a0), "+v"(a1)::"memory");
+#pragma unroll
+        for (int s = c; s < c + 32; s += 2) {
+          const double2 w2 = *reinterpret_cast<const double2*>(S[2] + k * BB + s);
+          a0 = fma(w2.x, col[s], a0);
+          a1 = fma(w2.y, col[s + 1], a1);
+        }
+      }
+      S[3][k * BB + lane] = alB[k] * (a0 + a1);
+    }
+  }
+  __syncthreads();
+  // O = −M_B K
+  {
+    double col[BB];
+#pragma unroll
+    for (int s = 0; s < BB; s++) col[s] = S[3][s * BB + lane];
+    double* Oo = Mb + (3 * (int64_t)blockIdx.x + 1) * BB * BB + lane;
+#pragma unroll 1
+    for (int kk = 0; kk < 16; kk++) {
+      const int k = 16 * wave + kk;
+      double a0 = 0.0, a1 = 0.0;
+#pragma unroll
+      for (int c = 0; c < BB; c += 32) {
+        asm volatile("" : "+v"(a0), "+v"(a1)::"memory");
+#pragma unroll
+        for (int s = c; s < c + 32; s += 2) {
+          const double2 w2 = *reinterpret_cast<const double2*>(S[1] + k * BB + s);
+          a0 = fma(w2.x, col[s], a0);
+          a1 = fma(w2.y, col[s + 1], a1);
+        }
+      }
+      Oo[k * BB] = -(a0 + a1);
+    }
+  }
+}
+
+// δ_k = Σ_s M[k][s] r̃_s with lane k's row of M in registers and r̃ broadcast from LDS (four chains)
+__device__ __forceinline__ double brr_apply_row(const double (&w)[BB], const double* rt) {
+  double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+#pragma unroll
+  for (int s = 0; s < BB; s += 4) {
+    const double2 r01 = *reinterpret_cast<const double2*>(rt + s);
+    const double2 r23 = *reinterpret_cast<const double2*>(rt + s + 2);
+    a0 = fma(w[s], r01.x, a0);
+    a1 = fma(w[s + 1], r01.y, a1);
+    a2 = fma(w[s + 2], r23.x, a2);
+    a3 = fma(w[s + 3], r23.y, a3);
+  }
+  return (a0 + a1) + (a2 + a3);
 }
 
 // partials of block 0 at the start of an iteration (after the intercept update)
@@ -250,22 +384,24 @@ __global__ void __launch_bounds__(256) brr_dots0_kernel(const T* __restrict__ Xt
   brr_partials<T>(Xt, ldx, n, i0, 0, (int)(p < BB ? p : BB), xs, es, partial);
 }
 
-// One block of 64 markers: r = Σ_c partial_in[c] (fixed order), the 64 single-site steps (wave 0
-// of every workgroup, identical inputs → identical results; the Gram row of lane k in registers,
-// δ_s broadcast by v_readlane), e += X_B δ on this workgroup's individuals, then the partials of
-// the next block from the updated e. Workgroup 0 stores b and the running posterior mean.
+// One block of 64 markers: d⁰ = Σ_c partial_in[c] (fixed order), the block's single-site steps as
+// δ = M r̃ (wave 0 of every workgroup, identical inputs → identical results; lane k's row of M in
+// registers, r̃ broadcast from LDS), e += X_B δ on this workgroup's individuals, then the partials
+// of the next block from the updated e. Workgroup 0 stores b and the running posterior mean.
 template <typename T>
 __global__ void __launch_bounds__(256) brr_step_kernel(const T* __restrict__ Xt, int64_t ldx, int64_t n,
-                                                       int64_t p, double xs, const double* __restrict__ W, int64_t blk,
+                                                       int64_t p, double xs, const double* __restrict__ Mb, int64_t blk,
                                                        int64_t nblk, const double* __restrict__ partial_in,
                                                        double* __restrict__ partial_out, double* __restrict__ b,
-                                                       double* __restrict__ bbar, const double* __restrict__ x2,
-                                                       double* __restrict__ e, const BrrState* __restrict__ st) {
+                                                       double* __restrict__ bbar, const double* __restrict__ alpha,
+                                                       const double* __restrict__ gamma, double* __restrict__ e,
+                                                       const BrrState* __restrict__ st) {
   // next block's genotypes for this chunk of individuals: 64 rows x IW, row pitch 2064 B
   // (≡ 16 B mod 256 B: the ds_read_b128 lane groups of the partials loop are conflict-free)
   constexpr int RP = IW + 2;  // doubles
   __shared__ __attribute__((aligned(16))) double Xn[BB * RP];
   __shared__ double delta[BB];
+  __shared__ __attribute__((aligned(16))) double rt[BB];
   __shared__ double es[IW];
   __shared__ double part4[4][BB];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -301,27 +437,28 @@ __global__ void __launch_bounds__(256) brr_step_kernel(const T* __restrict__ Xt,
 #pragma unroll
   for (int s2 = 0; s2 < BB; s2++) xv[s2] = gval<T>(Xt[(j0 + (s2 < nb ? s2 : 0)) * ldx + i], xs);
   const double e_old = e[i];
-  // (3) wave 0's operands
+  // (3) wave 0's operands: its row of M, α, γ (padded arrays)
   double w[BB];
-  double xx = 0.0, bo = 0.0, varE = 0.0, varB = 0.0;
+  double al = 0.0, ga = 0.0, bo = 0.0;
   const bool on = lane < nb;
   const int64_t j = j0 + lane;
   if (tid < 64) {
-    const double* wr = W + (blk * BB + lane) * BB;  // row `lane` = column `lane` (symmetric)
+    const double* wr = Mb + (blk * BB + lane) * BB;
 #pragma unroll
     for (int q = 0; q < BB; q += 2) {
       const double2 v = *reinterpret_cast<const double2*>(wr + q);
       w[q] = v.x;
       w[q + 1] = v.y;
     }
-    xx = on ? x2[j] : 0.0;
+    al = alpha[j];
+    ga = gamma[j];
     // b ping-pongs between two copies by iteration parity: a workgroup that starts late never
     // reads a value workgroup 0 already updated in this iteration (both copies load at once with
     // st: no st -> b dependent round trip)
-    const double b0 = on ? b[j] : 0.0, b1 = on ? b[p + j] : 0.0;
-    varE = st->varE;
-    varB = st->varB;
-    bo = (st->it & 1) ? b1 : b0;
+    if (blockIdx.x == 0) {
+      const double b0 = on ? b[j] : 0.0, b1 = on ? b[p + j] : 0.0;
+      bo = (st->it & 1) ? b1 : b0;
+    }
   }
   const double bb_old = (blockIdx.x == 0 && tid < 64 && on) ? bbar[j] : 0.0;
   {
@@ -331,21 +468,18 @@ __global__ void __launch_bounds__(256) brr_step_kernel(const T* __restrict__ Xt,
     for (int c0 = wave; c0 < C; c0 += 64) {
       double v[16];
 #pragma unroll
-      for (int m = 0; m < 16; m++) v[m] = (c0 + 4 * m < C) ? partial_in[(c0 + 4 * m) * BB + lane] : 0.0;
+      for (int m = 0; m < 16; m++) v[m] = partial_in[min(c0 + 4 * m, C - 1) * BB + lane];  // unconditional loads
 #pragma unroll
-      for (int m = 0; m < 16; m++) a += v[m];
+      for (int m = 0; m < 16; m++) a += c0 + 4 * m < C ? v[m] : 0.0;
     }
     part4[wave][lane] = a;
   }
   __syncthreads();
   if (tid < 64) {
-    double d = ((part4[0][lane] + part4[1][lane]) + part4[2][lane]) + part4[3][lane];
-    // c = x2/σ²_e + 1/σ²_b; b_new = (d + x2 b)/σ²_e / c + sqrt(1/c) ξ = d α + β
-    const double cinv = 1.0 / (xx / varE + 1.0 / varB);
-    const double alpha = on ? cinv / varE : 0.0;
-    const double xi = on ? brr_normal(st->seed, 4 * (uint64_t)st->it, (uint64_t)j) : 0.0;
-    const double beta = on ? xx * bo * alpha + sqrt(cinv) * xi : 0.0;
-    const double dlt = brr_block_steps(d, w, -alpha, bo - beta, lane);
+    const double d = ((part4[0][lane] + part4[1][lane]) + part4[2][lane]) + part4[3][lane];
+    rt[lane] = fma(d, -al, ga);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the wave's r̃ is in LDS
+    const double dlt = brr_apply_row(w, rt);
     const double bfin = bo - dlt;
     delta[lane] = dlt;
     if (blockIdx.x == 0 && on) {
@@ -388,7 +522,9 @@ __global__ void __launch_bounds__(256) brr_step_kernel(const T* __restrict__ Xt,
         uint4 v[4];
 #pragma unroll
         for (int t = 0; t < 4; t++) v[t] = *reinterpret_cast<const uint4*>(xr + (((4 * wave + t) ^ (lane & 15)) * 16));
-        brr_dot64_u8(v, er, xs, s0, s1);
+        brr_dot64_u8(v, er, s0, s1);
+        s0 *= xs;
+        s1 *= xs;
       }
     }
     part4[wave][lane] = s0 + s1;
@@ -400,10 +536,10 @@ __global__ void __launch_bounds__(256) brr_step_kernel(const T* __restrict__ Xt,
 
 // ---- byte storage: 128-marker launches ------------------------------------------------------
 // With genotypes stored as bytes (x = d·xs exact), one launch runs 128 markers as two halves
-// A = [j0, j0 + 64) and B = [j0 + 64, j0 + 128): wave 0 runs A's 64 single-site steps from W_AA,
-// wave 1 then brings B's x_kᵀe up to date with A's changes (d_B += W_BA δ_A, a 64x64 GEMV), and
-// wave 0 runs B's 64 steps from W_BB (prefetched into LDS by waves 2-3 during A). Half the
-// dependent launches per iteration of the 64-marker kernel, same sample path (markers in order).
+// A = [j0, j0 + 64) and B = [j0 + 64, j0 + 128): wave 3 forms r̃ of both halves from the partial
+// dots, then waves 0-2 apply δ_A = M_A r̃_A and δ_B = M_B r̃_B + O r̃_A (brr_prep_kernel) at once.
+// Half the dependent launches per iteration of the 64-marker kernel, same sample path (markers
+// in order).
 constexpr int BK2 = 2 * BB;  // markers per launch
 constexpr int WP = BB + 2;   // LDS pitch of W_BB (528 B ≡ 16 B mod 256 B: conflict-free b128 row reads)
 
@@ -439,12 +575,12 @@ __device__ __forceinline__ void brr_partials128(const uint8_t* __restrict__ D, i
       uint4 v[4];
 #pragma unroll
       for (int u = 0; u < 4; u++) v[u] = *reinterpret_cast<const uint4*>(row + 16 * u);
-      brr_dot64_u8(v, es + qt * 64, xs, s, s1);
-      s += s1;
+      brr_dot64_u8(v, es + qt * 64, s, s1);
+      s = s * xs + s1 * xs;
     }
     s += __shfl_xor(s, 1);
     s += __shfl_xor(s, 2);
-    if (qt == 0) out[blockIdx.x * BK2 + kk] = s;  // kk >= nb writes 0
+    if (qt == 0) out[blockIdx.x * BK2 + 2 * k + h] = s;  // interleaved halves; kk >= nb writes 0
   }
 }
 
@@ -467,17 +603,15 @@ __device__ __forceinline__ void lds_barrier() {
 
 __global__ void __launch_bounds__(256) brr_step128_kernel(const uint8_t* __restrict__ D, const uint8_t* __restrict__ Dt,
                                                           int64_t ldx, int64_t n, int64_t p, double xs,
-                                                          const double* __restrict__ W, int64_t blk, int64_t nblk,
+                                                          const double* __restrict__ Mb, int64_t blk, int64_t nblk,
                                                           const double* __restrict__ partial_in,
                                                           double* __restrict__ partial_out, double* __restrict__ b,
-                                                          double* __restrict__ bbar, const double* __restrict__ x2,
-                                                          double* __restrict__ e, const BrrState* __restrict__ st) {
+                                                          double* __restrict__ bbar, const double* __restrict__ alpha,
+                                                          const double* __restrict__ gamma, double* __restrict__ e,
+                                                          const BrrState* __restrict__ st) {
   __shared__ __attribute__((aligned(16))) uint8_t Xb[BK2 * IW];  // next block's rows (swizzled 16-B chunks)
-  __shared__ __attribute__((aligned(16))) double Wbb[BB * WP];
-  __shared__ double delta[BK2];
-  __shared__ double rs[BK2];     // x_kᵀe of the block's markers at launch start
-  __shared__ double dB[BB];
-  __shared__ double cst[3][BB];  // half B: alpha, beta, b_old
+  __shared__ __attribute__((aligned(16))) double rt[BK2];        // r̃ = γ − α∘d⁰ of the block's markers
+  __shared__ double dA[BB], dU[BB], dV[BB];                      // δ_A, M_B r̃_B, O r̃_A (δ_B = dU + dV)
   __shared__ double es[IW];
   __shared__ double part4[4][BK2];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -488,47 +622,56 @@ __global__ void __launch_bounds__(256) brr_step128_kernel(const uint8_t* __restr
   const bool more = blk + 1 < nblk;
   const int64_t j1 = j0 + BK2;
   const int nb1 = more ? (int)((p - j1) < BK2 ? (p - j1) : BK2) : 0;
-  const double* Wb = W + blk * 3 * BB * BB;
+  const double* Mblk = Mb + blk * 3 * BB * BB;
   // Loads are issued in the order they are needed: vmcnt retires in order, so a load queued behind
   // the next block's rows would wait for them.
-  // (1) the critical ones: waves 2-3 sum the partial dots of halves A and B over the C chunks (in
-  // chunk order: bit-identical in every workgroup); waves 0-1 load their Gram rows (W_AA, W_BA)
-  // and their half's marker state
+  // (1) the critical ones: wave 3 sums the partial dots of both halves over the C chunks (in chunk
+  // order: bit-identical in every workgroup) and forms r̃; waves 0-2 load their rows of M_A, M_B, O
   double w[BB];
-  double xx = 0.0, bo = 0.0, varE = 0.0, varB = 0.0;
+  double bo = 0.0, bbo = 0.0;
   const int64_t jm = j0 + (wave == 1 ? BB : 0) + lane;  // wave 0: marker A_lane, wave 1: B_lane
   const bool on = jm < p;
-  if (wave >= 2) {
-    const double* pin = partial_in + (wave - 2) * BB + lane;
-    double r = 0.0;
-    for (int c0 = 0; c0 < C; c0 += 64) {  // one batch of loads in flight (C <= 64 up to n = 16 384)
-      double v[64];
+  if (wave == 3) {
+    // partials are stored interleaved (A_k, B_k adjacent): one 16-B load per chunk
+    const double2* pin = reinterpret_cast<const double2*>(partial_in) + lane;
+    const double alA = alpha[j0 + lane], alBv = alpha[j0 + BB + lane];
+    const double gaA = gamma[j0 + lane], gaB = gamma[j0 + BB + lane];
+    double rA = 0.0, rB = 0.0;
+    // one batch of loads in flight (C <= 48 up to n = 12 288), issued unconditionally (clamped
+    // index): a branch or loop between them makes the compiler wait on earlier loads
+    auto batch = [&](int c0) {
+      double2 v[48];
 #pragma unroll
-      for (int m = 0; m < 64; m++) v[m] = c0 + m < C ? pin[(int64_t)(c0 + m) * BK2] : 0.0;
+      for (int m = 0; m < 48; m++) v[m] = pin[(int64_t)min(c0 + m, C - 1) * BB];
 #pragma unroll
-      for (int m = 0; m < 64; m++) r += v[m];
+      for (int m = 0; m < 48; m++) {
+        rA += c0 + m < C ? v[m].x : 0.0;
+        rB += c0 + m < C ? v[m].y : 0.0;
+      }
+    };
+    if (C <= 48) {
+      batch(0);
+    } else {
+      for (int c0 = 0; c0 < C; c0 += 48) batch(c0);
     }
-    rs[(wave - 2) * BB + lane] = r;
+    rt[lane] = fma(rA, -alA, gaA);
+    rt[BB + lane] = fma(rB, -alBv, gaB);
   } else {
-    const double* wr = Wb + (wave == 0 ? 0 : BB * BB) + lane * BB;
+    const double* wr = Mblk + (wave == 0 ? 0 : wave == 1 ? 2 * BB * BB : BB * BB) + lane * BB;
 #pragma unroll
     for (int q = 0; q < BB; q += 2) {
       const double2 v = *reinterpret_cast<const double2*>(wr + q);
       w[q] = v.x;
       w[q + 1] = v.y;
     }
-    // both parity copies of b load at once with st (no st -> b dependent round trip)
-    const double b0 = on ? b[jm] : 0.0, b1 = on ? b[p + jm] : 0.0;
-    xx = on ? x2[jm] : 0.0;
-    varE = st->varE;
-    varB = st->varB;
-    bo = (st->it & 1) ? b1 : b0;
-  }
-  // WG 0 keeps the running means: their old values load now, not after the serial steps
-  double bbA = 0.0, bbB = 0.0;
-  if (blockIdx.x == 0 && wave == 0) {
-    bbA = on ? bbar[jm] : 0.0;
-    bbB = jm + BB < p ? bbar[jm + BB] : 0.0;
+    // WG 0 stores b and keeps the running means: both parity copies of b and the old means load
+    // now, not after the GEMVs
+    if (blockIdx.x == 0 && wave < 2) {
+      const int64_t jc = on ? jm : 0;  // unconditional loads (no branch between them)
+      const double b0 = b[jc], b1 = b[p + jc];
+      bbo = bbar[jc];
+      bo = (st->it & 1) ? b1 : b0;
+    }
   }
   // (2) needed later: this individual's 128 genotypes of the block (8 x 16 B) for e += X_B δ,
   // and the next block's rows into LDS (4 rows per wave instruction, row r's 16-byte chunk c at
@@ -548,83 +691,23 @@ __global__ void __launch_bounds__(256) brr_step128_kernel(const uint8_t* __restr
     asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off" : : "s"(m0v), "v"(src) : "memory");
   }
   lds_barrier();
-  // (3) half A on wave 0; meanwhile wave 1 prepares half B's step constants and waves 2-3 put
-  // W_BB into LDS
-  if (wave == 0) {
-    const double c = 1.0 / (xx / varE + 1.0 / varB);
-    const double alpha = on ? c / varE : 0.0;
-    const double xi = on ? brr_normal(st->seed, 4 * (uint64_t)st->it, (uint64_t)jm) : 0.0;
-    const double beta = on ? xx * bo * alpha + sqrt(c) * xi : 0.0;
-    const double dlt = brr_block_steps(rs[lane], w, -alpha, bo - beta, lane);
-    delta[lane] = dlt;
-    if (blockIdx.x == 0 && on) {
-      const double bA = bo - dlt;
-      b[((st->it & 1) ^ 1) * p + jm] = bA;
-      if (brr_accumulate(st)) {
-        const double k = (double)(st->nsum + 1);
-        bbar[jm] = bbA * ((k - 1.0) / k) + bA / k;
-      }
-    }
-  } else if (wave == 1) {
-    const double c = 1.0 / (xx / varE + 1.0 / varB);
-    const double alpha = on ? c / varE : 0.0;
-    const double xi = on ? brr_normal(st->seed, 4 * (uint64_t)st->it, (uint64_t)jm) : 0.0;
-    cst[0][lane] = alpha;
-    cst[1][lane] = on ? xx * bo * alpha + sqrt(c) * xi : 0.0;
-    cst[2][lane] = bo;
-  } else {
-    const int t = tid - 128;  // 128 threads x 16 double2 = the 64x64 block
-#pragma unroll
-    for (int u = 0; u < 16; u++) {
-      const double2 v = *reinterpret_cast<const double2*>(Wb + 2 * BB * BB + 2 * (t + 128 * u));
-      w[2 * u] = v.x;
-      w[2 * u + 1] = v.y;
-    }
-#pragma unroll
-    for (int u = 0; u < 16; u++) {
-      const int e2 = 2 * (t + 128 * u), r = e2 / BB, c = e2 % BB;
-      *reinterpret_cast<double2*>(&Wbb[r * WP + c]) = make_double2(w[2 * u], w[2 * u + 1]);
-    }
+  // (3) the block's steps as three GEMVs: δ_A = M_A r̃_A (wave 0), M_B r̃_B (wave 1), O r̃_A (wave 2)
+  if (wave < 3) {
+    const double v = brr_apply_row(w, rt + (wave == 1 ? BB : 0));
+    (wave == 0 ? dA : wave == 1 ? dU : dV)[lane] = v;
   }
   lds_barrier();
-  // (4) wave 1: d_B = r_B + Σ_s W_BA[k][s] δ_A[s] (four partial chains); wave 0 takes its W_BB row
-  // from LDS
-  if (wave == 1) {
-    double d0 = rs[BB + lane], d1 = 0.0, d2 = 0.0, d3 = 0.0;
-#pragma unroll
-    for (int s2 = 0; s2 < BB; s2 += 4) {
-      d0 = fma(delta[s2], w[s2], d0);
-      d1 = fma(delta[s2 + 1], w[s2 + 1], d1);
-      d2 = fma(delta[s2 + 2], w[s2 + 2], d2);
-      d3 = fma(delta[s2 + 3], w[s2 + 3], d3);
-    }
-    dB[lane] = (d0 + d1) + (d2 + d3);
-  } else if (wave == 0) {
-#pragma unroll
-    for (int q = 0; q < BB; q += 2) {
-      const double2 v = *reinterpret_cast<const double2*>(&Wbb[lane * WP + q]);
-      w[q] = v.x;
-      w[q + 1] = v.y;
+  // (4) workgroup 0 stores b and the running means
+  if (blockIdx.x == 0 && wave < 2 && on) {
+    const double dlt = wave == 0 ? dA[lane] : dU[lane] + dV[lane];
+    const double bn = bo - dlt;
+    b[((st->it & 1) ^ 1) * p + jm] = bn;
+    if (brr_accumulate(st)) {
+      const double k = (double)(st->nsum + 1);
+      bbar[jm] = bbo * ((k - 1.0) / k) + bn / k;
     }
   }
-  lds_barrier();
-  // (5) half B on wave 0
-  if (wave == 0) {
-    const int64_t jB = j0 + BB + lane;
-    const double boB = cst[2][lane];
-    const double dlt = brr_block_steps(dB[lane], w, -cst[0][lane], boB - cst[1][lane], lane);
-    delta[BB + lane] = dlt;
-    if (blockIdx.x == 0 && jB < p) {
-      const double bBn = boB - dlt;
-      b[((st->it & 1) ^ 1) * p + jB] = bBn;
-      if (brr_accumulate(st)) {
-        const double k = (double)(st->nsum + 1);
-        bbar[jB] = bbB * ((k - 1.0) / k) + bBn / k;
-      }
-    }
-  }
-  lds_barrier();
-  // (6) e += X_B δ over this workgroup's individuals (markers past p have δ = 0), four chains
+  // (5) e += X_B δ over this workgroup's individuals (markers past p have δ = 0), four chains
   double ei = 0.0;
   if (i < n) {
     double acc[4] = {0.0, 0.0, 0.0, 0.0};
@@ -634,13 +717,16 @@ __global__ void __launch_bounds__(256) brr_step128_kernel(const uint8_t* __restr
 #pragma unroll
       for (int q = 0; q < 4; q++)
 #pragma unroll
-        for (int bb = 0; bb < 4; bb++)
-          acc[bb] = fma(delta[16 * u + 4 * q + bb], (double)((wd[q] >> (8 * bb)) & 0xFFu), acc[bb]);
+        for (int bb = 0; bb < 4; bb++) {
+          const int s = 16 * u + 4 * q + bb;
+          const double dl = s < BB ? dA[s] : dU[s - BB] + dV[s - BB];
+          acc[bb] = fma(dl, (double)((wd[q] >> (8 * bb)) & 0xFFu), acc[bb]);
+        }
     }
     ei = e_old + ((acc[0] + acc[1]) + (acc[2] + acc[3])) * xs;
     e[i] = ei;
   }
-  // (7) the next block's partial dots from the updated e
+  // (6) the next block's partial dots from the updated e
   if (more) {
     es[tid] = ei;
     __builtin_amdgcn_s_waitcnt(0x0070);  // vmcnt(0) lgkmcnt(0): this wave's rows of Xb have landed
@@ -654,13 +740,14 @@ __global__ void __launch_bounds__(256) brr_step128_kernel(const uint8_t* __restr
         uint4 v[4];
 #pragma unroll
         for (int t = 0; t < 4; t++) v[t] = *reinterpret_cast<const uint4*>(xr + (((4 * wave + t) ^ (k & 15)) * 16));
-        brr_dot64_u8(v, es + wave * 64, xs, s0, s1);
+        brr_dot64_u8(v, es + wave * 64, s0, s1);
       }
-      part4[wave][k] = s0 + s1;
+      part4[wave][k] = s0 * xs + s1 * xs;
     }
     lds_barrier();
     if (tid < BK2)
-      partial_out[blockIdx.x * BK2 + tid] = ((part4[0][tid] + part4[1][tid]) + part4[2][tid]) + part4[3][tid];
+      partial_out[blockIdx.x * BK2 + 2 * (tid & 63) + (tid >> 6)] =
+          ((part4[0][tid] + part4[1][tid]) + part4[2][tid]) + part4[3][tid];
   }
 }
 
@@ -709,6 +796,7 @@ __global__ void __launch_bounds__(256) brr_quantize_kernel(const double* __restr
 }  // namespace gbm
 
 using namespace gbm;
+
 
 extern "C" int gbm_brr_fit(const double* X, int64_t n, int64_t p, int64_t ldx, const double* y, int64_t n_iter,
                            int64_t n_burnin, int64_t thin, double r2, double df0, uint64_t seed, int device,
@@ -777,6 +865,11 @@ extern "C" int gbm_brr_fit(const double* X, int64_t n, int64_t p, int64_t ldx, c
   const int64_t bk = xs > 0.0 ? BK2 : BB, nblk = (p + bk - 1) / bk;
   const int nw = xs > 0.0 ? 3 : 1;
   GBM_TRY(dalloc(W, dev, nblk * nw * BB * BB * 8));
+  // per-iteration block inverses (same shape as W) and step constants α, γ (padded to whole launches)
+  DevMem Mb, alph, gamm;
+  GBM_TRY(dalloc(Mb, dev, nblk * nw * BB * BB * 8));
+  GBM_TRY(dalloc(alph, dev, nblk * bk * 8));
+  GBM_TRY(dalloc(gamm, dev, nblk * bk * 8));
   brr_gram_kernel<<<(unsigned)(nblk * nw), 256, 0, s>>>((const double*)Xt.p, npad, p, n, nw, (double*)W.p);
   GBM_LAUNCH_CHECK();
   if (xs > 0.0) {
@@ -821,7 +914,11 @@ extern "C" int gbm_brr_fit(const double* X, int64_t n, int64_t p, int64_t ldx, c
   // one Gibbs iteration, captured once and replayed
   auto* stp = (BrrState*)stm.p;
   const unsigned C = (unsigned)((n + IW - 1) / IW);
+  const unsigned prep_grid = (unsigned)(xs > 0.0 ? nblk : (nblk + 3) / 4);
   auto enqueue_iteration = [&]() -> int {
+    brr_prep_kernel<<<prep_grid, 256, 0, s>>>((const double*)W.p, p, nblk, nw,
+                                              (const double*)x2.p, (const double*)b.p, stp, (double*)Mb.p,
+                                              (double*)alph.p, (double*)gamm.p);
     brr_mu_kernel<<<1, 1024, 0, s>>>((double*)e.p, n, stp);
     if (xs > 0.0)
       brr_dots0_128_kernel<<<C, 256, 0, s>>>((const uint8_t*)D.p, npad, n, p, xs, (const double*)e.p, (double*)r.p);
@@ -833,12 +930,12 @@ extern "C" int gbm_brr_fit(const double* X, int64_t n, int64_t p, int64_t ldx, c
       double* pout = (double*)r.p + ((k + 1) & 1) * (int64_t)C * bk;
       if (xs > 0.0)
         brr_step128_kernel<<<C, 256, 0, s>>>((const uint8_t*)D.p, (const uint8_t*)Dt.p, npad, n, p, xs,
-                                             (const double*)W.p, k, nblk, pin, pout, (double*)b.p, (double*)bbar.p,
-                                             (const double*)x2.p, (double*)e.p, stp);
+                                             (const double*)Mb.p, k, nblk, pin, pout, (double*)b.p, (double*)bbar.p,
+                                             (const double*)alph.p, (const double*)gamm.p, (double*)e.p, stp);
       else
-        brr_step_kernel<double><<<C, 256, 0, s>>>((const double*)Xt.p, npad, n, p, 1.0, (const double*)W.p, k, nblk,
-                                                  pin, pout, (double*)b.p, (double*)bbar.p, (const double*)x2.p,
-                                                  (double*)e.p, stp);
+        brr_step_kernel<double><<<C, 256, 0, s>>>((const double*)Xt.p, npad, n, p, 1.0, (const double*)Mb.p, k,
+                                                  nblk, pin, pout, (double*)b.p, (double*)bbar.p,
+                                                  (const double*)alph.p, (const double*)gamm.p, (double*)e.p, stp);
     }
     brr_var_kernel<<<1, 1024, 0, s>>>((const double*)b.p, p, (const double*)e.p, n, stp);
     return hipGetLastError() == hipSuccess ? GBM_OK : fail(GBM_E_HIP, "gbm_brr_fit: launch failed");
