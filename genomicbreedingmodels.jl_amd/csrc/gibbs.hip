@@ -751,6 +751,217 @@ __global__ void __launch_bounds__(256) brr_step128_kernel(const uint8_t* __restr
   }
 }
 
+// ---- byte storage: one persistent launch per sweep ------------------------------------------
+// The C workgroups (one per 256-individual chunk, all resident: C <= CUs) run every 128-marker
+// block of the sweep in one launch instead of one launch each. Block k's partial dots are handed
+// between workgroups as in the dataflow Cholesky (chol_flow.hip; per-XCD L2s are not coherent):
+// the storing wave writes them through (`sc1` buffer stores), drains (`s_waitcnt vmcnt(0)`) and
+// one lane stores the workgroup's flag = k + 1 (relaxed, agent scope); wave 3 of every workgroup
+// polls the C flags and reads the partials only through `sc1` loads. Two partial buffers (block
+// parity) suffice: a workgroup writes block k + 2's partials only after every workgroup published
+// block k + 1's, i.e. after all have read block k's. The next block's operands — M rows (waves
+// 0-2), α/γ (wave 3) and the next rows of D (for the dots, then kept in LDS for that block's
+// e update) — are loaded while the current block computes: off the hand-off's critical path. e
+// stays in registers for the whole sweep. Waits are bounded (~1 s): a timed-out workgroup sets
+// *info = −1 and every workgroup leaves.
+constexpr int kSweepBatch = 40;  // partial loads in flight per batch (C <= 40: n <= 10 240 in one)
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t brr_rsrc(const void* p, int64_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
+}
+
+__global__ void __launch_bounds__(256) brr_sweep128_kernel(const uint8_t* __restrict__ D, int64_t ldx, int64_t p, double xs,
+                                                           const double* __restrict__ Mb, int64_t nblk,
+                                                           double* __restrict__ part, int32_t* __restrict__ flags,
+                                                           int32_t* __restrict__ info, double* __restrict__ b,
+                                                           double* __restrict__ bbar, const double* __restrict__ alpha,
+                                                           const double* __restrict__ gamma, double* __restrict__ e,
+                                                           const BrrState* __restrict__ st) {
+  __shared__ __attribute__((aligned(16))) double rt[BK2];  // r̃ = γ − α∘d⁰ of the block's markers
+  __shared__ double dA[BB], dU[BB], dV[BB];                // δ_A, M_B r̃_B, O r̃_A (δ_B = dU + dV)
+  __shared__ double es[IW];
+  __shared__ double part4[4][BK2];
+  // each wave's quarter of a block's rows (128 rows x 64 individuals, pitch 68 B: conflict-free
+  // dword writes of a row per lane, and byte reads of a column per lane), kept from the dots that
+  // used them (partials of block k) for block k's e update: each genotype is read from HBM once
+  __shared__ uint32_t T[4][BK2 * 17];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int C = (int)gridDim.x;
+  const int64_t i0 = (int64_t)blockIdx.x * IW, i = i0 + tid;
+  const __amdgpu_buffer_rsrc_t rP = brr_rsrc(part, (int64_t)2 * C * BK2 * 8);
+  const int it_odd = (int)(st->it & 1);
+  const bool acc = brr_accumulate(st);
+  const double kk = (double)(st->nsum + 1);
+  // operand loaders (each wave loads only what it uses)
+  double w[BB];
+  auto load_rows_of_M = [&](int64_t k) {  // waves 0-2: M_A, M_B, O rows of block k
+    const double* wr = Mb + k * 3 * BB * BB + (wave == 0 ? 0 : wave == 1 ? 2 * BB * BB : BB * BB) + lane * BB;
+#pragma unroll
+    for (int q = 0; q < BB; q += 2) {
+      const double2 v = *reinterpret_cast<const double2*>(wr + q);
+      w[q] = v.x;
+      w[q + 1] = v.y;
+    }
+  };
+  uint4 rv[8];  // rows lane and lane + 64 of a block, individuals [64 wave, 64 wave + 64) of the chunk
+  auto load_rows = [&](int64_t k) {
+    const int64_t j = k * BK2;
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+      const int64_t r = min(j + lane + BB * h, p - 1);  // past p: a valid row, never summed
+      const uint4* src = reinterpret_cast<const uint4*>(D + r * ldx + i0 + wave * 64);
+#pragma unroll
+      for (int u = 0; u < 4; u++) rv[4 * h + u] = src[u];
+    }
+  };
+  double alA = 0.0, alB = 0.0, gaA = 0.0, gaB = 0.0;  // wave 3
+  auto load_ag = [&](int64_t k) {
+    alA = alpha[k * BK2 + lane];
+    alB = alpha[k * BK2 + BB + lane];
+    gaA = gamma[k * BK2 + lane];
+    gaB = gamma[k * BK2 + BB + lane];
+  };
+  double bo = 0.0, bbo = 0.0;  // workgroup 0, waves 0-1: marker (k, wave, lane)'s b (this parity) and b̄
+  auto load_b = [&](int64_t k) {
+    const int64_t jm = k * BK2 + wave * BB + lane, jc = jm < p ? jm : 0;
+    const double b0 = b[jc], b1 = b[p + jc];
+    bbo = bbar[jc];
+    bo = it_odd ? b1 : b0;
+  };
+  // partials of block k + 1 from es and rv (rows of block k + 1): part4, then wave 3 publishes
+  auto dots_publish = [&](int64_t k1) {
+    const int nb1 = (int)((p - k1 * BK2) < BK2 ? (p - k1 * BK2) : BK2);
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+      const int kr = lane + BB * h;
+      double s0 = 0.0, s1 = 0.0;
+      const uint4 v[4] = {rv[4 * h], rv[4 * h + 1], rv[4 * h + 2], rv[4 * h + 3]};
+      brr_dot64_u8(v, es + wave * 64, s0, s1);
+      part4[wave][kr] = kr < nb1 ? s0 * xs + s1 * xs : 0.0;
+    }
+    // the rows into T for block k1's e update (this wave's region, read by this wave only)
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+      uint32_t* tr = T[wave] + (lane + BB * h) * 17;
+#pragma unroll
+      for (int u = 0; u < 4; u++) {
+        tr[4 * u] = rv[4 * h + u].x;
+        tr[4 * u + 1] = rv[4 * h + u].y;
+        tr[4 * u + 2] = rv[4 * h + u].z;
+        tr[4 * u + 3] = rv[4 * h + u].w;
+      }
+    }
+    lds_barrier();
+    if (wave == 3) {
+      __amdgpu_buffer_rsrc_t r = rP;
+      const double pa = ((part4[0][lane] + part4[1][lane]) + part4[2][lane]) + part4[3][lane];
+      const double pb = ((part4[0][BB + lane] + part4[1][BB + lane]) + part4[2][BB + lane]) + part4[3][BB + lane];
+      const uint32_t off = (uint32_t)((((k1 & 1) * C + blockIdx.x) * BK2 + 2 * lane) * 8);
+      typedef unsigned int u4v __attribute__((ext_vector_type(4)));
+      typedef double d2v __attribute__((ext_vector_type(2)));
+      const d2v val = {pa, pb};
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4v, val), r, (int)off, 0, 16);  // sc1
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (lane == 0) __hip_atomic_store(flags + blockIdx.x, (int32_t)(k1 + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  };
+
+  // ---- prologue: block 0's partials from e, then block 0's operands
+  double ei = e[i];
+  load_rows(0);
+  es[tid] = ei;
+  lds_barrier();
+  dots_publish(0);
+  if (wave < 3) load_rows_of_M(0);
+  else load_ag(0);
+  if (blockIdx.x == 0 && wave < 2) load_b(0);
+  if (nblk > 1) load_rows(1);
+
+  for (int64_t k = 0; k < nblk; k++) {
+    // (1) wave 3: wait until every workgroup published block k's partials, sum them in chunk
+    // order (bit-identical in every workgroup), form r̃
+    if (wave == 3) {
+      bool ok = true;
+      for (int64_t spin = 0;; spin++) {
+        int ready = 1;
+        for (int c = lane; c < C; c += 64)
+          ready &= __hip_atomic_load(flags + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= (int32_t)(k + 1);
+        if (__builtin_amdgcn_read_exec() == __builtin_amdgcn_ballot_w64(ready != 0)) break;
+        if ((spin & 255) == 255) {
+          if (__hip_atomic_load(info, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < 0) { ok = false; break; }
+          if (spin > ((int64_t)1 << 22)) {
+            if (lane == 0) __hip_atomic_store(info, -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            ok = false;
+            break;
+          }
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // the sc1 loads stay below the poll
+      if (!ok) rt[0] = __builtin_nan("");                    // poison: every wave leaves below
+      double rA = 0.0, rB = 0.0;
+      const uint32_t base = (uint32_t)(((k & 1) * C * BK2 + 2 * lane) * 8);
+      for (int c0 = 0; c0 < C; c0 += kSweepBatch) {
+        typedef double d2v __attribute__((ext_vector_type(2)));
+        d2v v[kSweepBatch];
+#pragma unroll
+        for (int m = 0; m < kSweepBatch; m++)
+          v[m] = __builtin_bit_cast(d2v, __builtin_amdgcn_raw_buffer_load_b128(
+                                              rP, (int)(base + (uint32_t)min(c0 + m, C - 1) * BK2 * 8), 0, 16));
+#pragma unroll
+        for (int m = 0; m < kSweepBatch; m++) {
+          rA += c0 + m < C ? v[m].x : 0.0;
+          rB += c0 + m < C ? v[m].y : 0.0;
+        }
+      }
+      if (ok) {
+        rt[lane] = fma(rA, -alA, gaA);
+        rt[BB + lane] = fma(rB, -alB, gaB);
+      }
+    }
+    lds_barrier();
+    if (__builtin_isnan(rt[0]) && __hip_atomic_load(info, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < 0) return;
+    // (2) δ as three GEMVs (waves 0-2), then the next block's M rows
+    if (wave < 3) {
+      const double v = brr_apply_row(w, rt + (wave == 1 ? BB : 0));
+      (wave == 0 ? dA : wave == 1 ? dU : dV)[lane] = v;
+      if (k + 1 < nblk) load_rows_of_M(k + 1);
+    }
+    lds_barrier();
+    // (3) workgroup 0 stores b and the running means of block k
+    if (blockIdx.x == 0 && wave < 2) {
+      const int64_t jm = k * BK2 + wave * BB + lane;
+      if (jm < p) {
+        const double dlt = wave == 0 ? dA[lane] : dU[lane] + dV[lane];
+        const double bn = bo - dlt;
+        b[(it_odd ^ 1) * p + jm] = bn;
+        if (acc) bbar[jm] = bbo * ((kk - 1.0) / kk) + bn / kk;
+      }
+      if (k + 1 < nblk) load_b(k + 1);
+    }
+    // (4) e += X_B δ (markers past p have δ = 0), four chains, genotypes from T (column `lane`)
+    {
+      double a4[4] = {0.0, 0.0, 0.0, 0.0};
+      const uint8_t* tc = reinterpret_cast<const uint8_t*>(T[wave]) + lane;
+#pragma unroll
+      for (int s = 0; s < BK2; s++) {
+        const double dl = s < BB ? dA[s] : dU[s - BB] + dV[s - BB];
+        a4[s & 3] = fma(dl, (double)tc[s * 68], a4[s & 3]);
+      }
+      ei = ei + ((a4[0] + a4[1]) + (a4[2] + a4[3])) * xs;
+    }
+    if (k + 1 >= nblk) break;
+    es[tid] = ei;
+    lds_barrier();
+    // (5) block k + 1's partials from the updated e, published by wave 3; then the operands of
+    // block k + 1 (wave 3) and the rows of block k + 2
+    dots_publish(k + 1);
+    if (wave == 3) load_ag(k + 1);
+    if (k + 2 < nblk) load_rows(k + 2);
+  }
+  e[i] = ei;  // rows past n stay 0: their genotypes are 0
+}
+
 // σ²_b, σ²_e draws, running means of μ and the variances, next iteration (one workgroup)
 __global__ void __launch_bounds__(1024) brr_var_kernel(const double* __restrict__ b, int64_t p,
                                                        const double* __restrict__ e, int64_t n,
@@ -872,7 +1083,21 @@ extern "C" int gbm_brr_fit(const double* X, int64_t n, int64_t p, int64_t ldx, c
   GBM_TRY(dalloc(gamm, dev, nblk * bk * 8));
   brr_gram_kernel<<<(unsigned)(nblk * nw), 256, 0, s>>>((const double*)Xt.p, npad, p, n, nw, (double*)W.p);
   GBM_LAUNCH_CHECK();
+  // byte storage: one persistent sweep launch per iteration when the C chunk workgroups can all be
+  // resident (one per CU); GBM_BRR_SWEEP=0 keeps one launch per block (read per call)
+  bool sweep = false;
+  DevMem flg;
   if (xs > 0.0) {
+    int cus = 0;
+    const char* ev = std::getenv("GBM_BRR_SWEEP");
+    GBM_HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    sweep = !(ev && ev[0] == '0') && (int64_t)((n + IW - 1) / IW) <= cus && (int64_t)2 * ((n + IW - 1) / IW) * BK2 * 8 < 0x7fffffff;
+    if (sweep) {
+      GBM_TRY(dalloc(flg, dev, (((n + IW - 1) / IW) + 1) * sizeof(int32_t)));
+      GBM_HIP_TRY(hipMemsetAsync(flg.p, 0, (((n + IW - 1) / IW) + 1) * sizeof(int32_t), s));
+    }
+  }
+  if (xs > 0.0 && !sweep) {  // the per-launch path's individual-major copy of the bytes
     GBM_TRY(dalloc(Dt, dev, nblk * npad * BK2));
     brr_block_transpose_kernel<<<dim3((unsigned)(npad / 64), (unsigned)nblk), 256, 0, s>>>((const uint8_t*)D.p, npad, p,
                                                                                             (uint8_t*)Dt.p);
@@ -920,6 +1145,15 @@ extern "C" int gbm_brr_fit(const double* X, int64_t n, int64_t p, int64_t ldx, c
                                               (const double*)x2.p, (const double*)b.p, stp, (double*)Mb.p,
                                               (double*)alph.p, (double*)gamm.p);
     brr_mu_kernel<<<1, 1024, 0, s>>>((double*)e.p, n, stp);
+    if (sweep) {
+      int32_t* fl = (int32_t*)flg.p;
+      if (hipMemsetAsync(fl, 0, C * sizeof(int32_t), s) != hipSuccess) return fail(GBM_E_HIP, "gbm_brr_fit: memset failed");
+      brr_sweep128_kernel<<<C, 256, 0, s>>>((const uint8_t*)D.p, npad, p, xs, (const double*)Mb.p,
+                                            nblk, (double*)r.p, fl, fl + C, (double*)b.p, (double*)bbar.p,
+                                            (const double*)alph.p, (const double*)gamm.p, (double*)e.p, stp);
+      brr_var_kernel<<<1, 1024, 0, s>>>((const double*)b.p, p, (const double*)e.p, n, stp);
+      return hipGetLastError() == hipSuccess ? GBM_OK : fail(GBM_E_HIP, "gbm_brr_fit: launch failed");
+    }
     if (xs > 0.0)
       brr_dots0_128_kernel<<<C, 256, 0, s>>>((const uint8_t*)D.p, npad, n, p, xs, (const double*)e.p, (double*)r.p);
     else
@@ -962,6 +1196,12 @@ extern "C" int gbm_brr_fit(const double* X, int64_t n, int64_t p, int64_t ldx, c
   if (exec) (void)hipGraphExecDestroy(exec);
   if (graph) (void)hipGraphDestroy(graph);
   if (rc != GBM_OK) return rc;
+  if (sweep) {
+    int32_t inf = 0;
+    GBM_HIP_TRY(hipMemcpyAsync(&inf, (int32_t*)flg.p + C, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+    GBM_HIP_TRY(hipStreamSynchronize(s));
+    if (inf < 0) return fail(GBM_E_HIP, "gbm_brr_fit: a sweep hand-off between workgroups timed out");
+  }
   BrrState fin{};
   GBM_HIP_TRY(hipMemcpyAsync(&fin, stm.p, sizeof(BrrState), hipMemcpyDeviceToHost, s));
   GBM_HIP_TRY(hipMemcpyAsync(b_hat_out + 1, bbar.p, p * 8, hipMemcpyDeviceToHost, s));

@@ -52,8 +52,8 @@ def test_gpu_brr_multi_chunk_matches_oracle():
 @pytest.mark.parametrize("n,p", [(700, 450), (1100, 129), (300, 128), (513, 1000)])
 def test_gpu_brr_byte_storage_matches_fp64_and_oracle(monkeypatch, n, p):
     """Allele frequencies k/2 are stored as bytes for the sweeps (x = d/2 exactly) and run in
-    128-marker launches (two 64-marker halves, the second brought up to date by W_BA δ_A); the
-    fp64 storage (GBM_BRR_I8=0) runs 64-marker launches. Same sample path: both agree with each
+    128-marker blocks (two 64-marker halves: δ_A = M_A r̃_A, δ_B = M_B r̃_B + O r̃_A) inside one
+    persistent sweep launch; the fp64 storage (GBM_BRR_I8=0) runs one launch per 64-marker block. Same sample path: both agree with each
     other and with the oracle's literal loop to rounding (ragged last blocks: p mod 128 = 66, 1,
     0, 104)."""
     X = oracle.synth_genotypes(93 + p, n, p)
@@ -66,6 +66,25 @@ def test_gpu_brr_byte_storage_matches_fp64_and_oracle(monkeypatch, n, p):
     for a, b in zip(got, f64):
         assert rel(a, b) < 1e-10
     assert rel(got[0], ref["b_hat"]) < 1e-9 and rel(got[1], ref["y_pred"]) < 1e-9
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,p", [(1100, 300), (12000, 260)])
+def test_gpu_brr_sweep_matches_per_launch_path_and_oracle(monkeypatch, n, p):
+    """Byte storage: the persistent sweep (one launch per iteration, partial dots handed between
+    the ⌈n/256⌉ workgroups through write-through stores and flags) against one launch per
+    128-marker block (GBM_BRR_SWEEP=0) and the oracle's literal loop. n = 12 000: 47 workgroups,
+    more than one batch of partial loads."""
+    X = oracle.synth_genotypes(97 + n, n, p)
+    y = oracle.synth_phenotypes(X, 98)[:, 0]
+    sweep = gbm.brr_arrays(X, y, n_iter=5, n_burnin=1, thin=1, seed=17)
+    monkeypatch.setenv("GBM_BRR_SWEEP", "0")
+    launches = gbm.brr_arrays(X, y, n_iter=5, n_burnin=1, thin=1, seed=17)
+    ref = oracle.brr_gibbs(X, y, n_iter=5, n_burnin=1, thin=1, seed=17)
+    rel = lambda a, b: np.abs(a - b).max() / np.abs(b).max()
+    for a, b in zip(sweep, launches):
+        assert rel(a, b) < 1e-11
+    assert rel(sweep[0], ref["b_hat"]) < 1e-9 and rel(sweep[1], ref["y_pred"]) < 1e-9
 
 
 @pytest.mark.gpu
