@@ -759,12 +759,12 @@ __global__ void __launch_bounds__(256) brr_step128_kernel(const uint8_t* __restr
 // one lane stores the workgroup's flag = k + 1 (relaxed, agent scope); wave 3 of every workgroup
 // polls the C flags and reads the partials only through `sc1` loads. Two partial buffers (block
 // parity) suffice: a workgroup writes block k + 2's partials only after every workgroup published
-// block k + 1's, i.e. after all have read block k's. The next block's operands — M rows (waves
-// 0-2), α/γ (wave 3) and the next rows of D (for the dots, then kept in LDS for that block's
+// block k + 1's, i.e. after all have read block k's. The next block's operands — M (waves 0-2,
+// LDS DMA), α/γ (wave 3) and the next rows of D (for the dots, then kept in LDS for that block's
 // e update) — are loaded while the current block computes: off the hand-off's critical path. e
 // stays in registers for the whole sweep. Waits are bounded (~1 s): a timed-out workgroup sets
 // *info = −1 and every workgroup leaves.
-constexpr int kSweepBatch = 40;  // partial loads in flight per batch (C <= 40: n <= 10 240 in one)
+constexpr int kSweepBatch = 20;  // partial loads in flight per batch (registers: C = 40 in two batches)
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t brr_rsrc(const void* p, int64_t bytes) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
@@ -785,6 +785,10 @@ __global__ void __launch_bounds__(256) brr_sweep128_kernel(const uint8_t* __rest
   // dword writes of a row per lane, and byte reads of a column per lane), kept from the dots that
   // used them (partials of block k) for block k's e update: each genotype is read from HBM once
   __shared__ uint32_t T[4][BK2 * 17];
+  // the block's M_A, M_B, O (row k's 16-B chunk c at position c ^ (k & 31): conflict-free row
+  // reads), DMA'd from HBM while the previous block finishes — in LDS, not registers, so that the
+  // sweep's live state fits the VGPRs
+  __shared__ __attribute__((aligned(16))) double Ms[3][BB * BB];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int C = (int)gridDim.x;
   const int64_t i0 = (int64_t)blockIdx.x * IW, i = i0 + tid;
@@ -793,14 +797,16 @@ __global__ void __launch_bounds__(256) brr_sweep128_kernel(const uint8_t* __rest
   const bool acc = brr_accumulate(st);
   const double kk = (double)(st->nsum + 1);
   // operand loaders (each wave loads only what it uses)
-  double w[BB];
-  auto load_rows_of_M = [&](int64_t k) {  // waves 0-2: M_A, M_B, O rows of block k
-    const double* wr = Mb + k * 3 * BB * BB + (wave == 0 ? 0 : wave == 1 ? 2 * BB * BB : BB * BB) + lane * BB;
-#pragma unroll
-    for (int q = 0; q < BB; q += 2) {
-      const double2 v = *reinterpret_cast<const double2*>(wr + q);
-      w[q] = v.x;
-      w[q + 1] = v.y;
+  auto dma_M = [&](int64_t k) {  // waves 0-2: M_A, M_B, O of block k into Ms[wave], 2 rows per instruction
+    const uint8_t* src0 = reinterpret_cast<const uint8_t*>(
+        Mb + k * 3 * BB * BB + (wave == 0 ? 0 : wave == 1 ? 2 * BB * BB : BB * BB));
+    const int rr = lane >> 5, pos = lane & 31;
+#pragma unroll 4
+    for (int q = 0; q < BB / 2; q++) {
+      const int row = 2 * q + rr;
+      const uint8_t* src = src0 + row * BB * 8 + ((pos ^ (row & 31)) * 16);
+      const unsigned m0v = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(&Ms[wave][q * 2 * BB]));
+      asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off" : : "s"(m0v), "v"(src) : "memory");
     }
   };
   uint4 rv[8];  // rows lane and lane + 64 of a block, individuals [64 wave, 64 wave + 64) of the chunk
@@ -872,7 +878,7 @@ __global__ void __launch_bounds__(256) brr_sweep128_kernel(const uint8_t* __rest
   es[tid] = ei;
   lds_barrier();
   dots_publish(0);
-  if (wave < 3) load_rows_of_M(0);
+  if (wave < 3) dma_M(0);
   else load_ag(0);
   if (blockIdx.x == 0 && wave < 2) load_b(0);
   if (nblk > 1) load_rows(1);
@@ -921,13 +927,28 @@ __global__ void __launch_bounds__(256) brr_sweep128_kernel(const uint8_t* __rest
     }
     lds_barrier();
     if (__builtin_isnan(rt[0]) && __hip_atomic_load(info, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < 0) return;
-    // (2) δ as three GEMVs (waves 0-2), then the next block's M rows
+    // (2) δ as three GEMVs (waves 0-2; this wave's DMA of M has landed), then the next block's M
     if (wave < 3) {
-      const double v = brr_apply_row(w, rt + (wave == 1 ? BB : 0));
-      (wave == 0 ? dA : wave == 1 ? dU : dV)[lane] = v;
-      if (k + 1 < nblk) load_rows_of_M(k + 1);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const double* mr = Ms[wave] + lane * BB;
+      const double* r = rt + (wave == 1 ? BB : 0);
+      const int sw = lane & 31;
+      double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+#pragma unroll
+      for (int c = 0; c < BB / 2; c += 2) {
+        const double2 m01 = *reinterpret_cast<const double2*>(mr + 2 * (c ^ sw));
+        const double2 m23 = *reinterpret_cast<const double2*>(mr + 2 * ((c + 1) ^ sw));
+        const double2 r01 = *reinterpret_cast<const double2*>(r + 2 * c);
+        const double2 r23 = *reinterpret_cast<const double2*>(r + 2 * c + 2);
+        a0 = fma(m01.x, r01.x, a0);
+        a1 = fma(m01.y, r01.y, a1);
+        a2 = fma(m23.x, r23.x, a2);
+        a3 = fma(m23.y, r23.y, a3);
+      }
+      (wave == 0 ? dA : wave == 1 ? dU : dV)[lane] = (a0 + a1) + (a2 + a3);
     }
     lds_barrier();
+    if (wave < 3 && k + 1 < nblk) dma_M(k + 1);  // every wave's GEMV has read Ms
     // (3) workgroup 0 stores b and the running means of block k
     if (blockIdx.x == 0 && wave < 2) {
       const int64_t jm = k * BK2 + wave * BB + lane;
