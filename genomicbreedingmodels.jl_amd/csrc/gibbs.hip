@@ -778,7 +778,7 @@ __global__ void __launch_bounds__(256) brr_sweep128_kernel(const uint8_t* __rest
                                                            const double* __restrict__ gamma, double* __restrict__ e,
                                                            const BrrState* __restrict__ st) {
   __shared__ __attribute__((aligned(16))) double rt[BK2];  // r̃ = γ − α∘d⁰ of the block's markers
-  __shared__ double dA[BB], dU[BB], dV[BB];                // δ_A, M_B r̃_B, O r̃_A (δ_B = dU + dV)
+  __shared__ __attribute__((aligned(16))) double dl[BK2];   // δ of the block's markers
   __shared__ double es[IW];
   __shared__ double part4[4][BK2];
   // each wave's quarter of a block's rows (128 rows x 64 individuals, pitch 68 B: conflict-free
@@ -837,13 +837,29 @@ __global__ void __launch_bounds__(256) brr_sweep128_kernel(const uint8_t* __rest
   // partials of block k + 1 from es and rv (rows of block k + 1): part4, then wave 3 publishes
   auto dots_publish = [&](int64_t k1) {
     const int nb1 = (int)((p - k1 * BK2) < BK2 ? (p - k1 * BK2) : BK2);
+    {
+      // both rows (lane, lane + 64) over this wave's 64 individuals, 16 at a time: each es value
+      // is read once for the two rows; even/odd individuals in separate sums as brr_dot64_u8
+      double s0 = 0.0, s1 = 0.0, t0 = 0.0, t1 = 0.0;
+      const double* ew = es + wave * 64;
 #pragma unroll
-    for (int h = 0; h < 2; h++) {
-      const int kr = lane + BB * h;
-      double s0 = 0.0, s1 = 0.0;
-      const uint4 v[4] = {rv[4 * h], rv[4 * h + 1], rv[4 * h + 2], rv[4 * h + 3]};
-      brr_dot64_u8(v, es + wave * 64, s0, s1);
-      part4[wave][kr] = kr < nb1 ? s0 * xs + s1 * xs : 0.0;
+      for (int u = 0; u < 4; u++) {
+        asm volatile("" : "+v"(s0), "+v"(s1), "+v"(t0), "+v"(t1)::"memory");
+        const uint32_t wa[4] = {rv[u].x, rv[u].y, rv[u].z, rv[u].w};
+        const uint32_t wb[4] = {rv[4 + u].x, rv[4 + u].y, rv[4 + u].z, rv[4 + u].w};
+#pragma unroll
+        for (int q = 0; q < 4; q++)
+#pragma unroll
+          for (int bb = 0; bb < 4; bb += 2) {
+            const double2 e2 = *reinterpret_cast<const double2*>(ew + 16 * u + 4 * q + bb);
+            s0 = fma((double)((wa[q] >> (8 * bb)) & 0xFFu), e2.x, s0);
+            s1 = fma((double)((wa[q] >> (8 * bb + 8)) & 0xFFu), e2.y, s1);
+            t0 = fma((double)((wb[q] >> (8 * bb)) & 0xFFu), e2.x, t0);
+            t1 = fma((double)((wb[q] >> (8 * bb + 8)) & 0xFFu), e2.y, t1);
+          }
+      }
+      part4[wave][lane] = lane < nb1 ? s0 * xs + s1 * xs : 0.0;
+      part4[wave][BB + lane] = BB + lane < nb1 ? t0 * xs + t1 * xs : 0.0;
     }
     // the rows into T for block k1's e update (this wave's region, read by this wave only)
 #pragma unroll
@@ -927,25 +943,32 @@ __global__ void __launch_bounds__(256) brr_sweep128_kernel(const uint8_t* __rest
     }
     lds_barrier();
     if (__builtin_isnan(rt[0]) && __hip_atomic_load(info, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < 0) return;
-    // (2) δ as three GEMVs (waves 0-2; this wave's DMA of M has landed), then the next block's M
-    if (wave < 3) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      const double* mr = Ms[wave] + lane * BB;
-      const double* r = rt + (wave == 1 ? BB : 0);
+    // (2) δ_A = M_A r̃_A (wave 0), δ_B = O r̃_A + M_B r̃_B (wave 1); every DMA of M has landed
+    if (wave < 3) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's part of Ms
+    lds_barrier();
+    if (wave < 2) {
       const int sw = lane & 31;
       double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+      auto row_dot = [&](const double* mr, const double* r) {
 #pragma unroll
-      for (int c = 0; c < BB / 2; c += 2) {
-        const double2 m01 = *reinterpret_cast<const double2*>(mr + 2 * (c ^ sw));
-        const double2 m23 = *reinterpret_cast<const double2*>(mr + 2 * ((c + 1) ^ sw));
-        const double2 r01 = *reinterpret_cast<const double2*>(r + 2 * c);
-        const double2 r23 = *reinterpret_cast<const double2*>(r + 2 * c + 2);
-        a0 = fma(m01.x, r01.x, a0);
-        a1 = fma(m01.y, r01.y, a1);
-        a2 = fma(m23.x, r23.x, a2);
-        a3 = fma(m23.y, r23.y, a3);
+        for (int c = 0; c < BB / 2; c += 2) {
+          const double2 m01 = *reinterpret_cast<const double2*>(mr + 2 * (c ^ sw));
+          const double2 m23 = *reinterpret_cast<const double2*>(mr + 2 * ((c + 1) ^ sw));
+          const double2 r01 = *reinterpret_cast<const double2*>(r + 2 * c);
+          const double2 r23 = *reinterpret_cast<const double2*>(r + 2 * c + 2);
+          a0 = fma(m01.x, r01.x, a0);
+          a1 = fma(m01.y, r01.y, a1);
+          a2 = fma(m23.x, r23.x, a2);
+          a3 = fma(m23.y, r23.y, a3);
+        }
+      };
+      if (wave == 0) {
+        row_dot(Ms[0] + lane * BB, rt);
+      } else {
+        row_dot(Ms[2] + lane * BB, rt);       // O r̃_A
+        row_dot(Ms[1] + lane * BB, rt + BB);  // M_B r̃_B
       }
-      (wave == 0 ? dA : wave == 1 ? dU : dV)[lane] = (a0 + a1) + (a2 + a3);
+      dl[wave * BB + lane] = (a0 + a1) + (a2 + a3);
     }
     lds_barrier();
     if (wave < 3 && k + 1 < nblk) dma_M(k + 1);  // every wave's GEMV has read Ms
@@ -953,7 +976,7 @@ __global__ void __launch_bounds__(256) brr_sweep128_kernel(const uint8_t* __rest
     if (blockIdx.x == 0 && wave < 2) {
       const int64_t jm = k * BK2 + wave * BB + lane;
       if (jm < p) {
-        const double dlt = wave == 0 ? dA[lane] : dU[lane] + dV[lane];
+        const double dlt = dl[wave * BB + lane];
         const double bn = bo - dlt;
         b[(it_odd ^ 1) * p + jm] = bn;
         if (acc) bbar[jm] = bbo * ((kk - 1.0) / kk) + bn / kk;
@@ -965,9 +988,15 @@ __global__ void __launch_bounds__(256) brr_sweep128_kernel(const uint8_t* __rest
       double a4[4] = {0.0, 0.0, 0.0, 0.0};
       const uint8_t* tc = reinterpret_cast<const uint8_t*>(T[wave]) + lane;
 #pragma unroll
-      for (int s = 0; s < BK2; s++) {
-        const double dl = s < BB ? dA[s] : dU[s - BB] + dV[s - BB];
-        a4[s & 3] = fma(dl, (double)tc[s * 68], a4[s & 3]);
+      for (int c = 0; c < BK2; c += 32) {
+        // 32 markers' operands in flight at a time (the fully hoisted loop needs ~200 registers)
+        asm volatile("" : "+v"(a4[0]), "+v"(a4[1]), "+v"(a4[2]), "+v"(a4[3])::"memory");
+#pragma unroll
+        for (int s = c; s < c + 32; s += 2) {
+          const double2 d2 = *reinterpret_cast<const double2*>(dl + s);
+          a4[s & 3] = fma(d2.x, (double)tc[s * 68], a4[s & 3]);
+          a4[(s + 1) & 3] = fma(d2.y, (double)tc[(s + 1) * 68], a4[(s + 1) & 3]);
+        }
       }
       ei = ei + ((a4[0] + a4[1]) + (a4[2] + a4[3])) * xs;
     }
