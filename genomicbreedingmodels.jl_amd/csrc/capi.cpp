@@ -140,8 +140,9 @@ int make_shards(const std::vector<int>& devs, int64_t p, std::vector<std::unique
   return GBM_OK;
 }
 
-// Upload the shard's columns and standardise them in place; reads back the shard's kept count.
-int prepare_shard(const Problem& pr, Shard& sh) {
+// Upload the shard's columns and standardise them in place (center_only: centre them only, the
+// ploidy-aware GRM); reads back the shard's kept count.
+int prepare_shard(const Problem& pr, Shard& sh, bool center_only = false) {
   FitCtx& c = sh.x();
   const int64_t n = pr.n, npad = npad_of(n), pl = sh.p;
   GBM_HIP_TRY(hipSetDevice(c.dev));
@@ -162,8 +163,12 @@ int prepare_shard(const Problem& pr, Shard& sh) {
     GBM_TRY(gbm_dev_expand_dosage_i8((const int8_t*)c.D8.p, n, n, pl, pr.ploidy, (double*)c.Xt.p, npad, s));
   }
   GBM_HIP_TRY(hipMemsetAsync(c.q.p, 0, 8, s));
-  GBM_TRY(gbm_dev_standardize((const double*)c.Xt.p, npad, pl, n, (double*)c.Xt.p, npad, (double*)c.mean.p,
-                              (double*)c.sd.p, (int32_t*)c.keep.p, (int64_t*)c.q.p, s));
+  if (center_only)
+    GBM_TRY(launch_center_columns((const double*)c.Xt.p, npad, pl, n, (double*)c.Xt.p, npad, (double*)c.mean.p,
+                                  (double*)c.sd.p, (int32_t*)c.keep.p, (int64_t*)c.q.p, s));
+  else
+    GBM_TRY(gbm_dev_standardize((const double*)c.Xt.p, npad, pl, n, (double*)c.Xt.p, npad, (double*)c.mean.p,
+                                (double*)c.sd.p, (int32_t*)c.keep.p, (int64_t*)c.q.p, s));
   GBM_HIP_TRY(hipMemcpyAsync(&sh.q_host, c.q.p, 8, hipMemcpyDeviceToHost, s));
   GBM_HIP_TRY(hipStreamSynchronize(s));
   return GBM_OK;
@@ -526,6 +531,50 @@ extern "C" int gbm_grm(const double* X, int64_t n, int64_t p, int64_t ldx, const
   GBM_HIP_TRY(hipSetDevice(c.dev));
   GBM_TRY(ensure(c.out, c.dev, n * n * 8));
   GBM_TRY(launch_grm_export((const double*)c.G.p, gdim_of(n), n, 1.0 / (double)q, (double*)c.out.p, n, c.stream.s));
+  GBM_HIP_TRY(hipMemcpy2DAsync(G_out, ldg * 8, c.out.p, n * 8, n * 8, n, hipMemcpyDeviceToHost, c.stream.s));
+  GBM_HIP_TRY(hipStreamSynchronize(c.stream.s));
+  return GBM_OK;
+}
+
+extern "C" int gbm_grm_ploidy_aware(const double* X, int64_t n, int64_t p, int64_t ldx, int ploidy, const int* devices,
+                                    int ndev, double* G_out, int64_t ldg, double* denom_out) {
+  RoctxRange r_("gbm_grm_ploidy_aware");
+  if (!X || !G_out || n < 1 || p < 1 || ldx < n || ldg < n || ploidy < 1)
+    return fail(GBM_E_ARG, "gbm_grm_ploidy_aware: bad arguments");
+  std::vector<int> devs;
+  GBM_TRY(check_devices(devices, ndev, devs));
+  Problem pr{Source::F64, X, nullptr, 1, n, p, ldx};
+  std::vector<std::unique_ptr<Shard>> shards;
+  GBM_TRY(make_shards(devs, p, shards));
+  // X_c = X − 1 fᵀ (f_j = column mean = allele frequency); denominator Σ_j f_j (1 − f_j) in locus
+  // order over the shards (host, from the device means)
+  double den = 0.0;
+  {
+    RoctxRange r("gbm: upload + centre");
+    std::vector<double> f;
+    for (auto& sh : shards) {
+      GBM_TRY(prepare_shard(pr, *sh, true));
+      FitCtx& c = sh->x();
+      f.resize(sh->p);
+      GBM_HIP_TRY(hipMemcpyAsync(f.data(), c.mean.p, sh->p * 8, hipMemcpyDeviceToHost, c.stream.s));
+      GBM_HIP_TRY(hipStreamSynchronize(c.stream.s));
+      for (double v : f) den += v * (1.0 - v);
+    }
+  }
+  if (denom_out) *denom_out = den;
+  if (!(den > 0.0) || !std::isfinite(den)) return fail(GBM_E_DATA, "gbm_grm_ploidy_aware: no polymorphic locus-allele");
+  {
+    RoctxRange r("gbm: GRM");
+    for (auto& sh : shards) GBM_TRY(grm_shard(pr, *sh));
+  }
+  {
+    RoctxRange r("gbm: partial-GRM all-reduce");
+    GBM_TRY(allreduce_grm(shards, n));
+  }
+  FitCtx& c = shards[0]->x();
+  GBM_HIP_TRY(hipSetDevice(c.dev));
+  GBM_TRY(ensure(c.out, c.dev, n * n * 8));
+  GBM_TRY(launch_grm_export((const double*)c.G.p, gdim_of(n), n, (double)ploidy / den, (double*)c.out.p, n, c.stream.s));
   GBM_HIP_TRY(hipMemcpy2DAsync(G_out, ldg * 8, c.out.p, n * 8, n * 8, n, hipMemcpyDeviceToHost, c.stream.s));
   GBM_HIP_TRY(hipStreamSynchronize(c.stream.s));
   return GBM_OK;

@@ -183,6 +183,14 @@ static int launch_standardize(const double* Xt, int64_t ldx, int64_t p, const in
   return GBM_OK;
 }
 
+namespace gbm {
+int launch_center_columns(const double* Xt, int64_t ldx, int64_t p, int64_t n, double* Zt, int64_t ldz, double* mean,
+                          double* sd, int32_t* keep, int64_t* q_dev, hipStream_t s) {
+  if (p == 0) return GBM_OK;
+  return launch_standardize<false>(Xt, ldx, p, nullptr, n, Zt, ldz, mean, sd, keep, q_dev, 1, s);
+}
+}  // namespace gbm
+
 extern "C" int gbm_dev_standardize(const double* Xt, int64_t ldx, int64_t p, int64_t n, double* Zt, int64_t ldz,
                                    double* mean, double* sd, int32_t* keep, int64_t* q_dev, void* stream) {
   if (!Xt || !Zt || !mean || !sd || !keep || !q_dev || p < 0 || n < 1 || ldx < n || ldz < n ||

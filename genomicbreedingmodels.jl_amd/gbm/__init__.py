@@ -9,7 +9,7 @@ from .linear import gblup, gblup_arrays, gblup_synthetic, glmnet_folds, ridge, r
 from .metrics import heritabilitynarrow_sense, metrics, pearsonscorrelation, r2
 from .prediction import LINEAR_MODELS, extractxyetc, predict
 from .types import Fit, Genomes, Phenomes
-from .arrays import colstats, grm
+from .arrays import colstats, grm, grm_ploidy_aware, infer_ploidy
 from .session import GenotypeSession
 from .bayes import bayesian, brr_arrays
 from .cv import CV, cvbulk, cvbulk_setup, cvmultithread, fold_assignments, validate
@@ -17,6 +17,6 @@ from .cv import CV, cvbulk, cvbulk_setup, cvmultithread, fold_assignments, valid
 __all__ = [
     "ArgumentError", "GBMError", "device_count", "load_library",
     "gblup", "gblup_arrays", "gblup_synthetic", "ridge", "ridge_path_cv", "ridge_select", "glmnet_folds", "metrics", "pearsonscorrelation", "r2", "heritabilitynarrow_sense",
-    "LINEAR_MODELS", "extractxyetc", "predict", "Fit", "Genomes", "Phenomes", "colstats", "grm",
+    "LINEAR_MODELS", "extractxyetc", "predict", "Fit", "Genomes", "Phenomes", "colstats", "grm", "grm_ploidy_aware", "infer_ploidy",
     "GenotypeSession", "bayesian", "brr_arrays", "CV", "cvbulk", "cvbulk_setup", "cvmultithread", "fold_assignments", "validate",
 ]

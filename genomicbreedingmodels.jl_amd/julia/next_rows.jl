@@ -147,3 +147,26 @@ function bglr_brr_gpu(; G::Matrix{Float64}, y::Vector{Float64}, n_iter::Int64 = 
     gbm_check(rc, "bglr_brr_gpu")
     b_hat
 end
+
+# ---- ploidy-aware GRM -----------------------------------------------------------------------
+"""
+    grmploidyaware_gpu(X::Matrix{Float64}; ploidy=round(Int, 1 / minimum(X[X .!= 0.0])))
+
+Replaces `grmploidyaware(genomes, ploidy=ploidy).genomic_relationship_matrix` at
+src/gwas.jl:117-121 (X = the allele frequencies `gwasprep` extracted; the default ploidy is the
+caller's own inference, :119). G = k (X − 1fᵀ)(X − 1fᵀ)ᵀ / Σ f(1 − f), f = column means (VanRaden
+2008 for ploidy k; GenomicBreedingCore's implementation is un-vendored, so this is the restated
+standard form).
+"""
+function grmploidyaware_gpu(X::Matrix{Float64}; ploidy::Integer = Int(round(1 / minimum(X[X .!= 0.0]))))
+    n, p = size(X)
+    G = Matrix{Float64}(undef, n, n)
+    den = Ref{Float64}(0.0)
+    GC.@preserve X G begin
+        rc = ccall((:gbm_grm_ploidy_aware, LIBGBM), Cint,
+                   (Ptr{Float64}, Int64, Int64, Int64, Cint, Ptr{Int32}, Cint, Ptr{Float64}, Int64, Ptr{Float64}),
+                   X, n, p, stride(X, 2), ploidy, C_NULL, 0, G, n, den)
+    end
+    gbm_check(rc, "grmploidyaware_gpu")
+    return G
+end

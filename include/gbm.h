@@ -124,6 +124,19 @@ int gbm_grm(const double* X, int64_t n, int64_t p, int64_t ldx, const int* devic
             double* G_out, int64_t ldg, int64_t* q_out);
 
 /*
+ * Ploidy-aware genomic relationship matrix, replacing
+ * GenomicBreedingCore.grmploidyaware(genomes, ploidy=ploidy).genomic_relationship_matrix at
+ * src/gwas.jl:117-121 (its caller infers ploidy = round(1 / min nonzero X), :119). The Core
+ * implementation is un-vendored (parity unpinned); restated as VanRaden (2008) generalised to
+ * ploidy k: with f_j = mean_i X[i, j] (allele frequency) and dosages kX,
+ *   G = (kX − k1fᵀ)(kX − k1fᵀ)ᵀ / (k Σ_j f_j (1 − f_j)) = k (X − 1fᵀ)(X − 1fᵀ)ᵀ / Σ_j f_j (1 − f_j).
+ * Every column is used (monomorphic ones centre to zero). denom_out (may be NULL) = Σ_j f_j (1 − f_j).
+ * Same sharding over devices as gbm_grm.
+ */
+int gbm_grm_ploidy_aware(const double* X, int64_t n, int64_t p, int64_t ldx, int ploidy,
+                         const int* devices, int ndev, double* G_out, int64_t ldg, double* denom_out);
+
+/*
  * Column statistics of X: mean, std (ddof = 1, Julia `std`), keep = (std > eps(Float64) and
  * finite), q = Σ keep. Mirrors src/gwas.jl:112-113. Any of mean/sd/keep may be NULL.
  */

@@ -115,6 +115,20 @@ def grm(X: np.ndarray):
     return (Z @ Z.T) / q, q
 
 
+def grm_ploidy_aware(X: np.ndarray, ploidy: int):
+    """Ploidy-aware GRM for GenomicBreedingCore.grmploidyaware, called at src/gwas.jl:117-121 —
+    un-vendored, so this is a restatement of VanRaden (2008) generalised to ploidy k (parity
+    unpinned): dosages kX, f = column means, G = (kX − k1fᵀ)(kX − k1fᵀ)ᵀ / (k Σ f(1 − f)).
+    Written in dosage units, independently of the device's centred-frequency form."""
+    D = ploidy * X
+    f = X.mean(axis=0)
+    P = ploidy * f
+    den = float((f * (1.0 - f)).sum())
+    if not den > 0.0:
+        raise ValueError("no polymorphic locus")
+    return ((D - P) @ (D - P).T) / (ploidy * den), den
+
+
 def gblup_fit(X: np.ndarray, Y: np.ndarray, lam: float = 1.0) -> dict:
     """GBLUP on V = G + λI (reference src/gwas.jl:462-471 with σ²_u = 1, σ²_e = λ).
 

@@ -70,6 +70,27 @@ def test_grm_and_colstats_match_oracle():
     assert rel(m, mr) < 1e-14 and rel(s[k], sr[kr]) < 1e-13
 
 
+@pytest.mark.parametrize("n,p,ploidy,devices", [
+    (200, 1000, 2, None),
+    (333, 1777, 4, None),     # ragged n and p (edge kernel), tetraploid frequencies k/4
+    (1030, 900, 4, [0, 0]),   # two same-device loci shards summed on the device
+])
+def test_grm_ploidy_aware_matches_oracle(n, p, ploidy, devices):
+    """gbm_grm_ploidy_aware (replaces Core's grmploidyaware at src/gwas.jl:117-121; the Core
+    formula is un-vendored, so the pin is the oracle's VanRaden-for-ploidy-k restatement, parity
+    unpinned): centred frequencies on the device, the MFMA GRM, scaled by k / Σ f(1 − f); ploidy
+    inferred as the reference does (src/gwas.jl:119)."""
+    rng = np.random.default_rng(n + p)
+    X = np.round(rng.random((n, p)) ** 2 * ploidy) / ploidy  # frequencies k/ploidy, skewed
+    X[:, 3] = 0.5                                              # a monomorphic column
+    G, den = gbm.grm_ploidy_aware(X, devices=devices)
+    ref, den_ref = oracle.grm_ploidy_aware(X, ploidy)
+    assert gbm.infer_ploidy(X) == ploidy
+    assert G.shape == (n, n) and abs(den - den_ref) <= 1e-12 * den_ref
+    assert rel(G, ref) < 1e-12
+    assert np.array_equal(G, G.T)
+
+
 def test_dosage_i8_path_equals_f64_path():
     n, p, ploidy = 180, 700, 4
     rng = np.random.default_rng(1)

@@ -123,3 +123,25 @@ def test_gebv_correlation_doctest_property():
     y = oracle.synth_phenotypes(X, 5)[:, 0]
     r = oracle.gblup_fit(X, y, 1.0)
     assert oracle.metrics(y, r["y_pred"][:, 0])["cor"] > 0.5
+
+
+def test_ploidy_aware_grm_restatement():
+    """The ploidy-aware GRM restatement (Core's grmploidyaware is un-vendored: parity unpinned)
+    against VanRaden's method 1 written directly on 0/1/2 dosages (Z = M − 2p, G = ZZᵀ / (2Σp(1−p)))
+    and, for ploidy 4, an element-wise loop; the reference's ploidy inference (src/gwas.jl:119) on
+    the doctest's rounding of frequencies to k/4 (src/gwas.jl:43-45)."""
+    import gbm
+    rng = np.random.default_rng(5)
+    M = rng.integers(0, 3, size=(40, 90)).astype(np.float64)
+    M[:, 7] = 1.0  # monomorphic: contributes nothing
+    G, den = oracle.grm_ploidy_aware(M / 2.0, 2)
+    p = M.mean(axis=0) / 2.0
+    Z = M - 2.0 * p
+    assert np.allclose(G, Z @ Z.T / (2.0 * (p * (1.0 - p)).sum()), rtol=1e-13, atol=1e-13)
+    X4 = np.round(rng.random((12, 30)) * 4.0) / 4.0
+    G4, den4 = oracle.grm_ploidy_aware(X4, 4)
+    f = X4.mean(axis=0)
+    want = np.array([[sum(4 * (X4[i, j] - f[j]) * 4 * (X4[k, j] - f[j]) for j in range(30)) for k in range(12)]
+                     for i in range(12)]) / (4.0 * (f * (1 - f)).sum())
+    assert np.allclose(G4, want, rtol=1e-12, atol=1e-12)
+    assert gbm.infer_ploidy(X4) == 4 and gbm.infer_ploidy(M / 2.0) == 2
