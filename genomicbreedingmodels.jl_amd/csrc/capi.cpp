@@ -40,6 +40,7 @@ struct FitCtx {
   Stream copy;                   // host -> device copies of the pipelined upload (created on first use)
   std::vector<hipEvent_t> ev;    // one per upload chunk
   DevBuf Xt, D8, mean, sd, keep, q, G, Gc, wsg, Y, A, gebv, mu, info, wss, B, msum, packed, out, part;
+  DevBuf tmp, strip, gathered;   // copy exchanges; the distributed factorisation's strip all-gather
   ~FitCtx() {
     (void)hipSetDevice(dev);
     for (hipEvent_t e : ev) (void)hipEventDestroy(e);
@@ -118,10 +119,25 @@ struct Problem {
   uint64_t seed = 0;  // Source::SYNTH: genotypes generated on each device
 };
 
+int64_t env_i64(const char* name, int64_t def) {
+  const char* e = getenv(name);
+  return e && *e ? (int64_t)atoll(e) : def;
+}
+
+// GBM_SHARD_LEADERS=each (re-read per call): every shard keeps its own full G and is a rank of its
+// own in the GRM sum and the distributed factorisation, its exchanges done by device copies. That
+// is the one-GPU rehearsal of the multi-device path (devices = [0, 0, ...]; RCCL cannot put two
+// ranks on one device). Default: one leader per device, RCCL between the leaders.
+bool each_shard_leads() {
+  const char* e = getenv("GBM_SHARD_LEADERS");
+  return e && strcmp(e, "each") == 0;
+}
+
 // Contiguous SNP-column blocks, one per listed device; leader = first shard on each device.
 int make_shards(const std::vector<int>& devs, int64_t p, std::vector<std::unique_ptr<Shard>>& shards) {
   const int nd = (int)std::min<int64_t>((int64_t)devs.size(), p);
   const int64_t per = (p + nd - 1) / nd;
+  const bool each = each_shard_leads();
   for (int k = 0; k < nd; k++) {
     const int64_t j0 = k * per;
     if (j0 >= p) break;
@@ -129,7 +145,7 @@ int make_shards(const std::vector<int>& devs, int64_t p, std::vector<std::unique
     GBM_TRY(pool().acquire(devs[k], sh->c));
     sh->j0 = j0;
     sh->p = std::min(per, p - j0);
-    for (size_t m = 0; m < shards.size(); m++)
+    for (size_t m = 0; m < shards.size() && !each; m++)
       if (shards[m]->x().dev == devs[k]) {
         sh->leader = shards[m]->leader;
         break;
@@ -278,6 +294,45 @@ int comm_set(const std::vector<int>& devs, CommSet** out) {
   return GBM_OK;
 }
 
+// Copy bytes from one context's buffer to another's on dst's stream (same device or peer).
+int copy_dd(FitCtx& dst, void* d, const FitCtx& src, const void* s, int64_t bytes) {
+  GBM_HIP_TRY(hipSetDevice(dst.dev));
+  if (dst.dev == src.dev)
+    GBM_HIP_TRY(hipMemcpyAsync(d, s, (size_t)bytes, hipMemcpyDeviceToDevice, dst.stream.s));
+  else
+    GBM_HIP_TRY(hipMemcpyPeerAsync(d, dst.dev, s, src.dev, (size_t)bytes, dst.stream.s));
+  return GBM_OK;
+}
+
+int sync_all(std::vector<std::unique_ptr<Shard>>& shards, const std::vector<int>& which) {
+  for (int k : which) {
+    FitCtx& c = shards[k]->x();
+    GBM_HIP_TRY(hipSetDevice(c.dev));
+    GBM_HIP_TRY(hipStreamSynchronize(c.stream.s));
+  }
+  return GBM_OK;
+}
+
+// All-reduce by copies (leaders sharing a device, GBM_SHARD_LEADERS=each): the packed partials
+// summed in leader order on the first leader (the order of the same-device sum), then copied back.
+int copy_allreduce(std::vector<std::unique_ptr<Shard>>& shards, const std::vector<int>& leaders, int64_t psz) {
+  GBM_TRY(sync_all(shards, leaders));
+  FitCtx& c0 = shards[leaders[0]]->x();
+  GBM_HIP_TRY(hipSetDevice(c0.dev));
+  GBM_TRY(ensure(c0.tmp, c0.dev, psz * 8));
+  for (size_t k = 1; k < leaders.size(); k++) {
+    FitCtx& ck = shards[leaders[k]]->x();
+    GBM_TRY(copy_dd(c0, c0.tmp.p, ck, ck.packed.p, psz * 8));
+    GBM_TRY(launch_add_inplace((double*)c0.packed.p, (const double*)c0.tmp.p, psz, c0.stream.s));
+  }
+  GBM_TRY(sync_all(shards, {leaders[0]}));
+  for (size_t k = 1; k < leaders.size(); k++) {
+    FitCtx& ck = shards[leaders[k]]->x();
+    GBM_TRY(copy_dd(ck, ck.packed.p, c0, c0.packed.p, psz * 8));
+  }
+  return GBM_OK;
+}
+
 // Sum the partial GRMs of all shards into each device leader's G: the upper 128-tiles packed
 // contiguously (half the bytes of G's rows); shards on one device added there in shard order,
 // then the leaders all-reduced over RCCL (xGMI), then unpacked.
@@ -303,7 +358,12 @@ int allreduce_grm(std::vector<std::unique_ptr<Shard>>& shards, int64_t n) {
     GBM_HIP_TRY(hipStreamSynchronize(sh.x().stream.s));
     GBM_TRY(launch_add_inplace((double*)lc.packed.p, (const double*)sh.x().packed.p, psz, lc.stream.s));
   }
-  if (leaders.size() > 1) {
+  std::vector<int> sorted = devs;
+  std::sort(sorted.begin(), sorted.end());
+  const bool shared_dev = std::adjacent_find(sorted.begin(), sorted.end()) != sorted.end();
+  if (leaders.size() > 1 && shared_dev) {
+    GBM_TRY(copy_allreduce(shards, leaders, psz));
+  } else if (leaders.size() > 1) {
     CommSet* cs = nullptr;
     GBM_TRY(comm_set(devs, &cs));
     std::lock_guard<std::mutex> lock(cs->mu);
@@ -329,6 +389,97 @@ int allreduce_grm(std::vector<std::unique_ptr<Shard>>& shards, int64_t n) {
     GBM_TRY(gbm_dev_grm_unpack((const double*)c.packed.p, n, (double*)c.G.p, gdim, c.stream.s));
   }
   return GBM_OK;
+}
+
+// All-gather of the leaders' strip packs (cnt doubles each) into every leader's `gathered`, in
+// leader (= rank) order: RCCL across distinct devices, device copies when leaders share one.
+int allgather_strips(std::vector<std::unique_ptr<Shard>>& shards, const std::vector<int>& leaders, CommSet* cs,
+                     int64_t cnt) {
+  if (cs) {
+    ncclResult_t r = ncclGroupStart();
+    for (size_t k = 0; k < leaders.size() && r == ncclSuccess; k++) {
+      FitCtx& c = shards[leaders[k]]->x();
+      r = ncclAllGather(c.strip.p, c.gathered.p, (size_t)cnt, ncclDouble, cs->comms[k], c.stream.s);
+    }
+    ncclResult_t r2 = ncclGroupEnd();
+    if (r != ncclSuccess || r2 != ncclSuccess)
+      return fail(GBM_E_RCCL, std::string("ncclAllGather(Cholesky strip): ") + ncclGetErrorString(r != ncclSuccess ? r : r2));
+    return GBM_OK;
+  }
+  GBM_TRY(sync_all(shards, leaders));  // every pack is complete
+  for (int d : leaders) {
+    FitCtx& cd = shards[d]->x();
+    for (size_t r = 0; r < leaders.size(); r++) {
+      FitCtx& cr = shards[leaders[r]]->x();
+      GBM_TRY(copy_dd(cd, (double*)cd.gathered.p + r * cnt, cr, cr.strip.p, cnt * 8));
+    }
+  }
+  return sync_all(shards, leaders);  // no copy still reads a pack the next step overwrites
+}
+
+// GBLUP solve of V = G/q + λI factored across the device leaders (each holding the summed G): the
+// C-ABI counterpart of gbm.sharded.chol_distributed. Every leader runs each panel
+// group over the full width but the group's trailing update only on its own 128-column tiles; the
+// next group's rows are all-gathered and its diagonal block factored on every leader; once the
+// trailing matrix is small (GBM_DIST_TAIL_ROWS, default 8192) every remaining row is gathered once
+// and the tail and the back substitution run on every leader. Bit-identical to the redundant
+// launch-per-panel solve (the same kernel computes every tile). Replaces the per-device pinv/
+// Cholesky of V (reference src/gwas.jl:472,595) at multi-GPU scale.
+int solve_distributed(std::vector<std::unique_ptr<Shard>>& shards, const std::vector<int>& leaders,
+                      const std::vector<int>& ldevs, int64_t n, double inv_q, double lambda, int64_t nrhs) {
+  const int64_t npad = npad_of(n), gdim = gdim_of(n), nb = npad / kCholNB;
+  const int R = (int)leaders.size();
+  const int64_t tail_rows = env_i64("GBM_DIST_TAIL_ROWS", 8192);
+  std::vector<int> sorted = ldevs;
+  std::sort(sorted.begin(), sorted.end());
+  CommSet* cs = nullptr;
+  if (std::adjacent_find(sorted.begin(), sorted.end()) == sorted.end()) GBM_TRY(comm_set(ldevs, &cs));
+  std::unique_lock<std::mutex> lock;
+  if (cs) lock = std::unique_lock<std::mutex>(cs->mu);  // this solve's collectives in one order on every device
+  auto each = [&](auto&& fn) -> int {
+    for (int r = 0; r < R; r++) {
+      FitCtx& c = shards[leaders[r]]->x();
+      GBM_HIP_TRY(hipSetDevice(c.dev));
+      GBM_TRY(fn(r, c));
+    }
+    return GBM_OK;
+  };
+  auto distributable = [&](int64_t kb) {
+    return gdim - kCholNB * kb > tail_rows && gbm_dev_chol_group_size(n, kb) >= 2 && (kCholNB * kb) % 128 == 0;
+  };
+  GBM_TRY(each([&](int, FitCtx& c) {
+    return gbm_dev_chol_prepare((double*)c.G.p, gdim, n, inv_q, nullptr, lambda, (const double*)c.Y.p, npad, nrhs,
+                                (int32_t*)c.info.p, c.wss.p, c.wss.cap, c.stream.s);
+  }));
+  bool dist = distributable(0);
+  for (int64_t kb = 0; kb < nb;) {
+    const int64_t g = gbm_dev_chol_group_size(n, kb);
+    const int nr = dist ? R : 1;
+    GBM_TRY(each([&](int r, FitCtx& c) {
+      return gbm_dev_chol_group((double*)c.G.p, gdim, n, kb, dist ? r : 0, nr, (int32_t*)c.info.p, c.wss.p, c.wss.cap,
+                                c.stream.s);
+    }));
+    kb += g;
+    if (!dist || kb >= nb) continue;
+    dist = distributable(kb);
+    const int64_t rows64 = dist ? gbm_dev_chol_group_size(n, kb) : nb - kb;
+    const int64_t cnt = gbm_dev_chol_strip_doubles(n, kb, rows64, R);
+    GBM_TRY(each([&](int r, FitCtx& c) {
+      GBM_TRY(ensure(c.strip, c.dev, cnt * 8));
+      GBM_TRY(ensure(c.gathered, c.dev, R * cnt * 8));
+      return gbm_dev_chol_strip_pack((const double*)c.G.p, gdim, n, kb, rows64, r, R, (double*)c.strip.p, c.stream.s);
+    }));
+    GBM_TRY(allgather_strips(shards, leaders, cs, cnt));
+    GBM_TRY(each([&](int, FitCtx& c) {
+      GBM_TRY(gbm_dev_chol_strip_unpack((double*)c.G.p, gdim, n, kb, rows64, R, (const double*)c.gathered.p, c.stream.s));
+      return gbm_dev_chol_factor_diag((double*)c.G.p, gdim, n, kb, (int32_t*)c.info.p, c.wss.p, c.wss.cap, c.stream.s);
+    }));
+  }
+  return each([&](int, FitCtx& c) {
+    return gbm_dev_chol_finish((double*)c.G.p, gdim, n, (const double*)c.Y.p, npad, nrhs, lambda, (double*)c.A.p,
+                               (double*)c.gebv.p, npad, (double*)c.mu.p, (int32_t*)c.info.p, c.wss.p, c.wss.cap,
+                               c.stream.s);
+  });
 }
 
 int run_fit(const Problem& pr, const double* Y, int64_t ldy, int64_t nrhs, double lambda, const int* devices, int ndev,
@@ -373,10 +524,19 @@ int run_fit(const Problem& pr, const double* Y, int64_t ldy, int64_t nrhs, doubl
     GBM_TRY(allreduce_grm(shards, n));
   }
   const double inv_q = 1.0 / (double)q;
-  // each device leader solves the (identical) n x n system, all devices at once: a is then local
-  // to every shard's marker back-solve (same-device shards copy it from their leader)
+  // Below GBM_DIST_SOLVE_MIN_N individuals (default 16384, re-read per call; the knob of
+  // gbm.sharded.dist_solve_min_n) each device leader solves the (identical) n x n system, all
+  // devices at once; from there the leaders factor it together (solve_distributed). Either way a
+  // ends up on every leader for the marker back-solve (same-device shards copy it from theirs).
+  std::vector<int> leaders, ldevs;
+  for (size_t k = 0; k < shards.size(); k++)
+    if (shards[k]->leader == (int)k) {
+      leaders.push_back((int)k);
+      ldevs.push_back(shards[k]->x().dev);
+    }
+  const bool distributed = leaders.size() > 1 && n >= env_i64("GBM_DIST_SOLVE_MIN_N", 16384);
   std::vector<int32_t> infos(shards.size(), 0);
-  RoctxRange rsolve("gbm: solve");
+  RoctxRange rsolve(distributed ? "gbm: distributed solve" : "gbm: solve");
   for (size_t k = 0; k < shards.size(); k++) {
     Shard& sh = *shards[k];
     FitCtx& c = sh.x();
@@ -393,10 +553,16 @@ int run_fit(const Problem& pr, const double* Y, int64_t ldy, int64_t nrhs, doubl
     const int64_t wss = gbm_dev_solve_workspace(n, nrhs);
     GBM_TRY(ensure(c.wss, c.dev, wss));
     GBM_HIP_TRY(hipMemcpy2DAsync(c.Y.p, npad * 8, Y, ldy * 8, n * 8, nrhs, hipMemcpyHostToDevice, s));
-    GBM_TRY(gbm_dev_gblup_solve((double*)c.G.p, gdim, n, inv_q, nullptr, lambda, (const double*)c.Y.p, npad, nrhs,
-                                (double*)c.A.p, (double*)c.gebv.p, npad, (double*)c.mu.p, (int32_t*)c.info.p, c.wss.p,
-                                wss, s));
-    GBM_HIP_TRY(hipMemcpyAsync(&infos[k], c.info.p, 4, hipMemcpyDeviceToHost, s));
+    if (!distributed)
+      GBM_TRY(gbm_dev_gblup_solve((double*)c.G.p, gdim, n, inv_q, nullptr, lambda, (const double*)c.Y.p, npad, nrhs,
+                                  (double*)c.A.p, (double*)c.gebv.p, npad, (double*)c.mu.p, (int32_t*)c.info.p,
+                                  c.wss.p, wss, s));
+  }
+  if (distributed) GBM_TRY(solve_distributed(shards, leaders, ldevs, n, inv_q, lambda, nrhs));
+  for (int k : leaders) {
+    FitCtx& c = shards[k]->x();
+    GBM_HIP_TRY(hipSetDevice(c.dev));
+    GBM_HIP_TRY(hipMemcpyAsync(&infos[k], c.info.p, 4, hipMemcpyDeviceToHost, c.stream.s));
   }
   for (size_t k = 0; k < shards.size(); k++) {
     if (shards[k]->leader != (int)k) continue;

@@ -42,6 +42,39 @@ def test_same_device_shards_match_oracle(devices, n, p, t):
     assert qg == qr and rel(G, Gr) < 1e-12
 
 
+@pytest.mark.parametrize("devices,n,lims,tail", [
+    ([0, 0], 1500, ("0", "-1", "-1"), "256"),       # 4-panel groups, early switch to the redundant tail
+    ([0, 0, 0], 1500, ("0", "-1", "-1"), "0"),      # 4-panel groups down to the 2-panel / single-panel tail
+    ([0, 0, 0, 0], 3000, ("0", "0", "0"), "0"),     # 16, 8, 4, 2-panel groups, then single panels
+    ([0, 0], 1030, ("0", "0", "0"), "512"),         # ragged n
+])
+def test_cabi_distributed_factorisation_bit_identical(monkeypatch, devices, n, lims, tail):
+    """gbm_gblup_fit with several device leaders factors V across them (solve_distributed in
+    capi.cpp: own-tile trailing updates, strip all-gathers, redundant tail). Rehearsed on one GPU
+    with every shard its own leader (GBM_SHARD_LEADERS=each: copy all-reduce and copy all-gather
+    in place of RCCL); bit-identical to the default path, where the shards' partial GRMs are summed
+    on the device and one leader solves redundantly."""
+    monkeypatch.setenv("GBM_CHOL_G4_LIM", lims[0])
+    monkeypatch.setenv("GBM_CHOL_G8_LIM", lims[1])
+    monkeypatch.setenv("GBM_CHOL_G16_LIM", lims[2])
+    monkeypatch.setenv("GBM_UPD64_LIM", "128")
+    monkeypatch.setenv("GBM_CHOL_FLOW_MAX", "0")  # both sides on the launch-per-panel solve
+    X = oracle.synth_genotypes(n + len(devices), n, 1900)
+    Y = oracle.synth_phenotypes(X, 3, ntraits=2)
+    ref = gbm.gblup_arrays(X, Y, lambda_=0.8, devices=devices)
+    monkeypatch.setenv("GBM_SHARD_LEADERS", "each")
+    monkeypatch.setenv("GBM_DIST_SOLVE_MIN_N", "0")
+    monkeypatch.setenv("GBM_DIST_TAIL_ROWS", tail)
+    got = gbm.gblup_arrays(X, Y, lambda_=0.8, devices=devices)
+    for a, b in zip(got, ref):
+        assert np.array_equal(np.asarray(a), np.asarray(b))
+    fit = oracle.gblup_fit(X, Y, 0.8)
+    assert rel(got[1], fit["y_pred"]) < 1e-9 and rel(got[0], fit["b_hat"]) < 1e-6
+    G, qg = gbm.grm(X, devices=devices)  # the copy all-reduce of the GRM entry
+    Gr, qr = oracle.grm(X)
+    assert qg == qr and rel(G, Gr) < 1e-12
+
+
 def test_synthetic_fit_two_shards_one_device():
     n, p = 700, 3001
     X = oracle.synth_genotypes(4242, n, p)
