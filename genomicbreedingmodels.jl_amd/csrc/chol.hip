@@ -251,6 +251,9 @@ __global__ void __launch_bounds__(256) back_solve_kernel(const double* __restric
   const int64_t b = nb - 1 - (int64_t)blockIdx.x;
   const int64_t b0 = b * NB;
   const int j0 = wave * 16;  // this wave's 16 of the 64 block columns
+  const int64_t a_bytes = nrhs * lda * 8;
+  const __amdgpu_buffer_rsrc_t rA =
+      __builtin_amdgcn_make_buffer_rsrc(A, (short)0, (int)(a_bytes < 0x7fffffff ? a_bytes : 0x7fffffff), 0x00020000);
   double ui[16];             // (U_bb⁻¹)[lane][j0 + jj]
 #pragma unroll
   for (int jj = 0; jj < 16; jj++) ui[jj] = Linv[(b0 + lane) * NB + j0 + jj];
@@ -266,17 +269,19 @@ __global__ void __launch_bounds__(256) back_solve_kernel(const double* __restric
       const double* lp = G + (c * NB + j0) * ld + b0 + lane;
 #pragma unroll
       for (int jj = 0; jj < 16; jj++) l[jj] = lp[(int64_t)jj * ld];
-      if (lane == 0) ok = wait_flag(&flags[c], pass, info);
+      if (lane == 0) ok = wait_flag<false>(&flags[c], pass, info);
       ok = __builtin_amdgcn_readfirstlane((int)ok) != 0;
-      // a_c was written through (agent-scope stores) before its flag was released; after the
-      // acquire, plain loads (all 16 in flight at once — per-element atomic loads were each
-      // waited for) read it from beyond this XCD's invalidated L2
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      // a_c was written through (agent-scope stores) before its flag was published; it is read
+      // with sc1 buffer loads (all 16 in flight at once), so no agent acquire — an L1/L2
+      // invalidate of ~1.7 µs that sat on the chain at every block — is needed. The wavefront
+      // fence only keeps the compiler from hoisting the loads above the poll.
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
       for (int t = 0; t < tc; t++) {
-        const double* ac = A + (t0 + t) * lda + c * NB + j0;
+        const uint32_t voff = (uint32_t)(((t0 + t) * lda + c * NB + j0) * 8);
         double av[16];
 #pragma unroll
-        for (int jj = 0; jj < 16; jj++) av[jj] = ac[jj];
+        for (int jj = 0; jj < 16; jj++)
+          av[jj] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rA, (int)(voff + jj * 8), 0, 16));
         double s = 0.0;
 #pragma unroll
         for (int jj = 0; jj < 16; jj++) s = fma(l[jj], av[jj], s);

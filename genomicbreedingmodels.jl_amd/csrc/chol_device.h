@@ -45,10 +45,14 @@ __device__ __forceinline__ void st_agent(double* p, double v) {
 // that cannot end in a correct run must not hang the device
 // The spin itself is relaxed (an acquire per iteration would invalidate this XCD's L2 every
 // time, for every waiting wave); one acquire fence once the flag is seen.
+// kAcquire = false: no fence at all — for a consumer that reads the payload only through sc1
+// (L1-bypassing) buffer loads of write-through stores, as chol_flow.hip does; an agent acquire
+// (the cache invalidate) costs ~1.7 µs per hand-off.
+template <bool kAcquire = true>
 __device__ __forceinline__ bool wait_flag(int32_t* flag, int32_t value, int32_t* info) {
   for (int64_t it = 0;; it++) {
     if (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= value) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      if constexpr (kAcquire) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       return true;
     }
     if ((it & 255) == 255) {
