@@ -779,6 +779,7 @@ __global__ void __launch_bounds__(256) brr_sweep128_kernel(const uint8_t* __rest
                                                            const BrrState* __restrict__ st) {
   __shared__ __attribute__((aligned(16))) double rt[BK2];  // r̃ = γ − α∘d⁰ of the block's markers
   __shared__ __attribute__((aligned(16))) double dl[BK2];   // δ of the block's markers
+  __shared__ double dU[BB], dV[BB];                         // M_B r̃_B, O r̃_A (δ_B = dU + dV)
   __shared__ double es[IW];
   __shared__ double part4[4][BK2];
   // each wave's quarter of a block's rows (128 rows x 64 individuals, pitch 68 B: conflict-free
@@ -943,35 +944,32 @@ __global__ void __launch_bounds__(256) brr_sweep128_kernel(const uint8_t* __rest
     }
     lds_barrier();
     if (__builtin_isnan(rt[0]) && __hip_atomic_load(info, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < 0) return;
-    // (2) δ_A = M_A r̃_A (wave 0), δ_B = O r̃_A + M_B r̃_B (wave 1); every DMA of M has landed
+    // (2) the three GEMVs on three waves: δ_A = M_A r̃_A (wave 0), M_B r̃_B (wave 1), O r̃_A
+    // (wave 2); δ_B = M_B r̃_B + O r̃_A (as brr_step128_kernel). Every DMA of M has landed.
     if (wave < 3) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's part of Ms
     lds_barrier();
-    if (wave < 2) {
+    if (wave < 3) {
       const int sw = lane & 31;
       double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
-      auto row_dot = [&](const double* mr, const double* r) {
+      const double* mr = Ms[wave] + lane * BB;  // Ms[0] = M_A, Ms[1] = M_B, Ms[2] = O
+      const double* r = rt + (wave == 1 ? BB : 0);
 #pragma unroll
-        for (int c = 0; c < BB / 2; c += 2) {
-          const double2 m01 = *reinterpret_cast<const double2*>(mr + 2 * (c ^ sw));
-          const double2 m23 = *reinterpret_cast<const double2*>(mr + 2 * ((c + 1) ^ sw));
-          const double2 r01 = *reinterpret_cast<const double2*>(r + 2 * c);
-          const double2 r23 = *reinterpret_cast<const double2*>(r + 2 * c + 2);
-          a0 = fma(m01.x, r01.x, a0);
-          a1 = fma(m01.y, r01.y, a1);
-          a2 = fma(m23.x, r23.x, a2);
-          a3 = fma(m23.y, r23.y, a3);
-        }
-      };
-      if (wave == 0) {
-        row_dot(Ms[0] + lane * BB, rt);
-      } else {
-        row_dot(Ms[2] + lane * BB, rt);       // O r̃_A
-        row_dot(Ms[1] + lane * BB, rt + BB);  // M_B r̃_B
+      for (int c = 0; c < BB / 2; c += 2) {
+        const double2 m01 = *reinterpret_cast<const double2*>(mr + 2 * (c ^ sw));
+        const double2 m23 = *reinterpret_cast<const double2*>(mr + 2 * ((c + 1) ^ sw));
+        const double2 r01 = *reinterpret_cast<const double2*>(r + 2 * c);
+        const double2 r23 = *reinterpret_cast<const double2*>(r + 2 * c + 2);
+        a0 = fma(m01.x, r01.x, a0);
+        a1 = fma(m01.y, r01.y, a1);
+        a2 = fma(m23.x, r23.x, a2);
+        a3 = fma(m23.y, r23.y, a3);
       }
-      dl[wave * BB + lane] = (a0 + a1) + (a2 + a3);
+      (wave == 0 ? dl : wave == 1 ? dU : dV)[lane] = (a0 + a1) + (a2 + a3);
     }
     lds_barrier();
     if (wave < 3 && k + 1 < nblk) dma_M(k + 1);  // every wave's GEMV has read Ms
+    if (wave == 3) dl[BB + lane] = dU[lane] + dV[lane];
+    lds_barrier();
     // (3) workgroup 0 stores b and the running means of block k
     if (blockIdx.x == 0 && wave < 2) {
       const int64_t jm = k * BK2 + wave * BB + lane;
