@@ -764,7 +764,7 @@ __global__ void __launch_bounds__(256) brr_step128_kernel(const uint8_t* __restr
 // e update) — are loaded while the current block computes: off the hand-off's critical path. e
 // stays in registers for the whole sweep. Waits are bounded (~1 s): a timed-out workgroup sets
 // *info = −1 and every workgroup leaves.
-constexpr int kSweepBatch = 20;  // partial loads in flight per batch (registers: C = 40 in two batches)
+constexpr int kSweepBatch = 40;  // partial loads in flight per batch (C4: C = 40 in one batch)
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t brr_rsrc(const void* p, int64_t bytes) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
@@ -942,12 +942,12 @@ __global__ void __launch_bounds__(256) brr_sweep128_kernel(const uint8_t* __rest
         rt[BB + lane] = fma(rB, -alB, gaB);
       }
     }
+    // (waves 0-2 meanwhile: this wave's DMA of Ms has landed; one barrier then covers both)
+    if (wave < 3) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     lds_barrier();
     if (__builtin_isnan(rt[0]) && __hip_atomic_load(info, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < 0) return;
     // (2) the three GEMVs on three waves: δ_A = M_A r̃_A (wave 0), M_B r̃_B (wave 1), O r̃_A
     // (wave 2); δ_B = M_B r̃_B + O r̃_A (as brr_step128_kernel). Every DMA of M has landed.
-    if (wave < 3) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's part of Ms
-    lds_barrier();
     if (wave < 3) {
       const int sw = lane & 31;
       double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
