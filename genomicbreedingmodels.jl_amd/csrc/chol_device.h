@@ -191,8 +191,11 @@ __device__ __forceinline__ void store_factor(const double* Us, const double* rin
 // (rb, ks compile-time after unrolling, so a register array can back it):
 //   X_rb <- (D_rb⁻¹)ᵀ (X_rb − U[0:o, rb]ᵀ X[0:o])  for the 16-row blocks rb = 0..3.
 // Wave w owns columns 16w..16w+15 of the chunk. All MFMA, no serial chain.
-template <typename LoadDi>
-__device__ __forceinline__ void panel_chunk_solve(double* X, const double* Us, LoadDi load, int lane, int wave) {
+// emit(rb, acc): block row rb of the wave's 16 columns is final (acc[r] = X[16 rb + fr + 4 r][cw + fc]),
+// e.g. to store it while the later block rows are solved
+template <typename LoadDi, typename Emit>
+__device__ __forceinline__ void panel_chunk_solve(double* X, const double* Us, LoadDi load, int lane, int wave,
+                                                  Emit emit) {
   const int fr = lane >> 4, fc = lane & 15;
   const int cw = wave * 16;
 #pragma unroll
@@ -209,7 +212,12 @@ __device__ __forceinline__ void panel_chunk_solve(double* X, const double* Us, L
     }
 #pragma unroll
     for (int r = 0; r < 4; r++) X[(o + fr + 4 * r) * PS + cw + fc] = acc[r];
+    emit(rb, acc);
   }
+}
+template <typename LoadDi>
+__device__ __forceinline__ void panel_chunk_solve(double* X, const double* Us, LoadDi load, int lane, int wave) {
+  panel_chunk_solve(X, Us, load, lane, wave, [](int, const d4&) {});
 }
 
 }  // namespace gbm

@@ -424,11 +424,19 @@ chol_flow_kernel(double* __restrict__ G, int64_t ld, int nbc, double* __restrict
         }
         __syncthreads();
         if (kTrace) tr[14] = (int64_t)__builtin_amdgcn_s_memrealtime();
-        // ---- the right neighbour: U_i,i+1 = U_ii⁻ᵀ A_i,i+1 (all MFMA, operands in LDS)
-        panel_chunk_solve(X2, X, [&](int rb, int ks) { return Dl[rb * 256 + (ks * 4 + fr) * 16 + fc]; }, lane, wave);
+        // ---- the right neighbour: U_i,i+1 = U_ii⁻ᵀ A_i,i+1 (all MFMA, operands in LDS); each
+        // 16-row block of a wave's columns is stored (write-through) as soon as it is final, so
+        // the hand-off's stores overlap the rest of the solve
+        const __amdgpu_buffer_rsrc_t rN = rsrc(G + i0 * ld, gbytes_rowblk);
+        panel_chunk_solve(
+            X2, X, [&](int rb, int ks) { return Dl[rb * 256 + (ks * 4 + fr) * 16 + fc]; }, lane, wave,
+            [&](int rb, const d4& a) {
+#pragma unroll
+              for (int r = 0; r < 4; r++)
+                st1(rN, (uint32_t)(((int64_t)(rb * 16 + fr + 4 * r) * ld + j0 + FT + wave * 16 + fc) * 8), a[r]);
+            });
         __syncthreads();
         if (kTrace) tr[15] = (int64_t)__builtin_amdgcn_s_memrealtime();
-        store_upper(X2, i0, j0 + FT);
         low = X2;
         lj0 = j0 + FT;
       } else if (!diag) {
