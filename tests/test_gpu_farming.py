@@ -75,6 +75,30 @@ def test_cabi_distributed_factorisation_bit_identical(monkeypatch, devices, n, l
     assert qg == qr and rel(G, Gr) < 1e-12
 
 
+@pytest.mark.slow
+def test_cabi_distributed_factorisation_default_thresholds():
+    """The same at a size where the default thresholds choose the distributed solve themselves
+    (n = 20 000 >= GBM_DIST_SOLVE_MIN_N = 16 384; 16- to 2-panel groups, the tail below 8 192
+    rows): two device leaders (GBM_SHARD_LEADERS=each on one GPU) against one leader solving
+    redundantly, bit for bit; genotypes generated on the device."""
+    import os
+    n, p = 20000, 6000
+    rng = np.random.default_rng(7)
+    Y = np.asfortranarray(rng.standard_normal((n, 2)))
+    assert "GBM_DIST_SOLVE_MIN_N" not in os.environ
+    ref = gbm.gblup_synthetic(99, n, p, Y, lambda_=0.5, devices=[0, 0])
+    os.environ["GBM_SHARD_LEADERS"] = "each"
+    try:
+        got = gbm.gblup_synthetic(99, n, p, Y, lambda_=0.5, devices=[0, 0])
+    finally:
+        del os.environ["GBM_SHARD_LEADERS"]
+        gbm.load_library().gbm_release_device_cache()
+    for a, b in zip(got, ref):
+        assert np.array_equal(np.asarray(a), np.asarray(b))
+    b_hat, y_pred, mu, q = got
+    assert q == p and np.all(np.isfinite(y_pred))
+
+
 def test_synthetic_fit_two_shards_one_device():
     n, p = 700, 3001
     X = oracle.synth_genotypes(4242, n, p)
