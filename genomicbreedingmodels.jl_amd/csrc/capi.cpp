@@ -475,11 +475,14 @@ int solve_distributed(std::vector<std::unique_ptr<Shard>>& shards, const std::ve
       return gbm_dev_chol_factor_diag((double*)c.G.p, gdim, n, kb, (int32_t*)c.info.p, c.wss.p, c.wss.cap, c.stream.s);
     }));
   }
-  return each([&](int, FitCtx& c) {
+  GBM_TRY(each([&](int, FitCtx& c) {
     return gbm_dev_chol_finish((double*)c.G.p, gdim, n, (const double*)c.Y.p, npad, nrhs, lambda, (double*)c.A.p,
                                (double*)c.gebv.p, npad, (double*)c.mu.p, (int32_t*)c.info.p, c.wss.p, c.wss.cap,
                                c.stream.s);
-  });
+  }));
+  // the solve's collectives complete while this call still holds the communicators (as in
+  // allreduce_grm): another call's collectives on the same device set come strictly after
+  return cs ? sync_all(shards, leaders) : GBM_OK;
 }
 
 int run_fit(const Problem& pr, const double* Y, int64_t ldy, int64_t nrhs, double lambda, const int* devices, int ndev,
