@@ -186,19 +186,22 @@ class HipShardStages:
         self.ws_grm = torch.empty(max(self.ws_grm_bytes, 16), dtype=torch.uint8, device=self.dev)
         self.Y = torch.zeros((nrhs, self.npad), **f64)
         self.A = torch.zeros((nrhs, self.npad), **f64)
-        self.gebv = torch.zeros((nrhs, self.npad), **f64)
-        self.mu = torch.zeros(nrhs, **f64)
-        self.info = torch.zeros(1, dtype=torch.int32, device=self.dev)
         self.ws_solve_bytes = lib.gbm_dev_solve_workspace(n, nrhs)
         self.ws_solve = torch.empty(max(self.ws_solve_bytes, 16), dtype=torch.uint8, device=self.dev)
-        self.B = torch.zeros((nrhs, p_local), **f64)
-        self.msum = torch.zeros(nrhs, **f64)
-        pin = dict(dtype=torch.float64, pin_memory=True)
-        self.h_B = torch.empty((nrhs, p_local), **pin)
-        self.h_gebv = torch.empty((nrhs, self.npad), **pin)
-        self.h_mu = torch.empty(nrhs, **pin)
-        self.h_msum = torch.empty(nrhs, **pin)
-        self.h_info = torch.empty(1, dtype=torch.int32, pin_memory=True)
+        # the step's host-bound results (b, GEBVs, μ̂, Σb, info) are views of one device buffer,
+        # so that download() is a single D2H copy into a pinned mirror of the same layout
+        shapes = [("B", (nrhs, p_local)), ("gebv", (nrhs, self.npad)), ("mu", (nrhs,)), ("msum", (nrhs,))]
+        nout = sum(int(np.prod(sh)) for _, sh in shapes) + 1  # + one 8-byte slot for info
+        self.out = torch.zeros(nout, **f64)
+        self.h_out = torch.empty(nout, dtype=torch.float64, pin_memory=True)
+        off = 0
+        for name, sh in shapes:
+            k = int(np.prod(sh))
+            setattr(self, name, self.out[off:off + k].view(sh))
+            setattr(self, "h_" + name, self.h_out[off:off + k].view(sh))
+            off += k
+        self.info = self.out[off:].view(torch.int32)[:1]
+        self.h_info = self.h_out[off:].view(torch.int32)[:1]
 
     @staticmethod
     def _p(t):
@@ -303,11 +306,7 @@ class HipShardStages:
                                                    self._p(self.msum), self._stream()), "effects")
 
     def download(self):
-        self.h_B.copy_(self.B, non_blocking=True)
-        self.h_gebv.copy_(self.gebv, non_blocking=True)
-        self.h_mu.copy_(self.mu, non_blocking=True)
-        self.h_msum.copy_(self.msum, non_blocking=True)
-        self.h_info.copy_(self.info, non_blocking=True)
+        self.h_out.copy_(self.out, non_blocking=True)
         self.torch.cuda.current_stream(self.dev).synchronize()
         if int(self.h_info[0]) < 0:
             raise _lib.GBMError("back substitution: block synchronisation timed out")
