@@ -70,14 +70,15 @@ def sharded_gblup_step(stages, comm, events=None):
     stages.grm_reduce()
     mark("grm_reduce")
     if comm.world_size > 1:
-        # the upper GRM tiles only (half of G's rows), when the stages can pack them
+        # the upper GRM tiles only (half of G's rows) with q in the packed buffer's last slot (one
+        # collective instead of two), when the stages can pack them
         pack = getattr(stages, "grm_pack", None)
         if pack is not None:
             comm.all_reduce_sum(pack())
             stages.grm_unpack()
         else:
             comm.all_reduce_sum(stages.grm_rows())
-    comm.all_reduce_sum(stages.q)
+            comm.all_reduce_sum(stages.q)
     mark("allreduce")
     if comm.world_size > 1 and hasattr(stages, "chol_group") and stages.n >= dist_solve_min_n():
         chol_distributed([stages], [comm.rank], comm.world_size, lambda packs: [comm.all_gather(packs[0])])
@@ -247,17 +248,20 @@ class HipShardStages:
         return self.G[: self.npad]
 
     def grm_pack(self):
-        """Upper GRM tiles as one contiguous tensor (the multi-GPU all-reduce operand)."""
+        """Upper GRM tiles as one contiguous tensor, followed by q (exact as fp64: q < 2⁵³): the
+        multi-GPU all-reduce operand."""
         if getattr(self, "Gp", None) is None:
-            self.Gp = self.torch.empty(self.lib.gbm_dev_grm_packed_size(self.n), dtype=self.torch.float64,
+            self.Gp = self.torch.empty(self.lib.gbm_dev_grm_packed_size(self.n) + 1, dtype=self.torch.float64,
                                        device=self.dev)
         _lib.check(self.lib.gbm_dev_grm_pack(self._p(self.G), self.gdim, self.n, self._p(self.Gp), self._stream()),
                    "grm_pack")
+        self.Gp[-1:].copy_(self.q)
         return self.Gp
 
     def grm_unpack(self):
         _lib.check(self.lib.gbm_dev_grm_unpack(self._p(self.Gp), self.n, self._p(self.G), self.gdim, self._stream()),
                    "grm_unpack")
+        self.q.copy_(self.Gp[-1:])
 
     def solve(self):
         _lib.check(self.lib.gbm_dev_gblup_solve(self._p(self.G), self.gdim, self.n, 0.0, self._p(self.q), self.lam,
