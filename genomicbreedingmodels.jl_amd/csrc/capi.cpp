@@ -204,12 +204,35 @@ int64_t host_chunk(int64_t p) {
   return c >= p ? 0 : c;
 }
 
+// Chunk schedule of the pipelined upload: chunks of `chunk` loci, the last full-size piece cut
+// into halving pieces (1/2, 1/4, 1/8, 1/8 of it, none below 1024 loci) when the upload is
+// copy-bound (fp64 X), so that the device work left after the last byte has landed is a small
+// chunk's GRM rather than a full one's (C2 host path: 40.7 -> 39.8 ms). The int8 upload is
+// device-bound (an eighth of the bytes), where extra chunks only add launches (25.5 -> 26.2 ms).
+static std::vector<std::pair<int64_t, int64_t>> chunk_schedule(int64_t pl, int64_t chunk, bool halve_tail) {
+  std::vector<std::pair<int64_t, int64_t>> cs;
+  int64_t j = 0;
+  while (pl - j > chunk) {
+    cs.emplace_back(j, chunk);
+    j += chunk;
+  }
+  int64_t r = pl - j;
+  for (int d = 0; halve_tail && d < 3 && r / 2 >= 1024; d++) {
+    const int64_t h = r / 2;
+    cs.emplace_back(j, r - h);
+    j += r - h;
+    r = h;
+  }
+  if (r > 0) cs.emplace_back(j, r);
+  return cs;
+}
+
 // Upload, standardise and GRM of one shard with the PCIe transfer of the genotypes overlapped
 // with the device work: chunk k's copy (on the context's copy stream; from pageable memory the
 // call itself returns when the copy is done) runs while the compute stream standardises chunk
 // k − 1 and adds its loci to G (chunk GRMs summed in chunk order: deterministic). At C2 the
 // 2 GB of fp64 X take ~35 ms over PCIe and the GRM ~19 ms: pipelined, the call costs about the
-// copy plus one chunk's GRM instead of their sum.
+// copy plus the last (small) chunk's GRM instead of their sum.
 int upload_grm_pipelined(const Problem& pr, Shard& sh, int64_t chunk) {
   FitCtx& c = sh.x();
   const int64_t n = pr.n, npad = npad_of(n), gdim = gdim_of(n), pl = sh.p;
@@ -219,7 +242,8 @@ int upload_grm_pipelined(const Problem& pr, Shard& sh, int64_t chunk) {
     c.copy.dev = c.dev;
     GBM_HIP_TRY(hipStreamCreateWithFlags(&c.copy.s, hipStreamNonBlocking));
   }
-  const int64_t nch = (pl + chunk - 1) / chunk;
+  const std::vector<std::pair<int64_t, int64_t>> sched = chunk_schedule(pl, chunk, pr.src == Source::F64);
+  const int64_t nch = (int64_t)sched.size();
   while ((int64_t)c.ev.size() < nch) {
     hipEvent_t e;
     GBM_HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
@@ -233,12 +257,13 @@ int upload_grm_pipelined(const Problem& pr, Shard& sh, int64_t chunk) {
   GBM_TRY(ensure(c.G, c.dev, gdim * gdim * 8));
   GBM_TRY(ensure(c.Gc, c.dev, gdim * gdim * 8));
   if (pr.src == Source::I8) GBM_TRY(ensure(c.D8, c.dev, pl * n));
-  const int64_t wsb = gbm_dev_grm_workspace(n, std::min(chunk, pl));
+  int64_t wsb = 0;  // the loci split (and so the workspace) is planned per chunk size
+  for (const auto& jc : sched) wsb = std::max(wsb, gbm_dev_grm_workspace(n, jc.second));
   GBM_TRY(ensure(c.wsg, c.dev, wsb));
   GBM_HIP_TRY(hipMemsetAsync(c.q.p, 0, 8, s));
   double* Xt = (double*)c.Xt.p;
   for (int64_t k = 0; k < nch; k++) {
-    const int64_t j = k * chunk, pc = std::min(chunk, pl - j);
+    const int64_t j = sched[k].first, pc = sched[k].second;
     if (pr.src == Source::F64)
       GBM_HIP_TRY(hipMemcpy2DAsync(Xt + j * npad, npad * 8, pr.X + (sh.j0 + j) * pr.ld, pr.ld * 8, n * 8, pc,
                                    hipMemcpyHostToDevice, c.copy.s));
