@@ -205,10 +205,12 @@ int64_t host_chunk(int64_t p) {
 }
 
 // Chunk schedule of the pipelined upload: chunks of `chunk` loci, the last full-size piece cut
-// into halving pieces (1/2, 1/4, 1/8, 1/8 of it, none below 1024 loci) when the upload is
-// copy-bound (fp64 X), so that the device work left after the last byte has landed is a small
-// chunk's GRM rather than a full one's (C2 host path: 40.7 -> 39.8 ms). The int8 upload is
-// device-bound (an eighth of the bytes), where extra chunks only add launches (25.5 -> 26.2 ms).
+// into halving pieces (1/2, 1/4, 1/8, 1/8 of it, none below 512 loci) when `halve_tail`, so that
+// the device work left after the last byte has landed is a small chunk's GRM rather than a full
+// one's. That pays where the upload is copy-bound (fp64 X at C2: 40.7 -> 39.9 ms); the int8 upload
+// (an eighth of the bytes) is device-bound, where three more chunks cost 0.9 ms (25.5 -> 26.4 ms),
+// so by default it keeps equal chunks. With GBM_HOST_CHUNK set, both entries halve the tail: the
+// same partition, chunk GRMs summed in the same order, bit-identical results.
 static std::vector<std::pair<int64_t, int64_t>> chunk_schedule(int64_t pl, int64_t chunk, bool halve_tail) {
   std::vector<std::pair<int64_t, int64_t>> cs;
   int64_t j = 0;
@@ -217,7 +219,7 @@ static std::vector<std::pair<int64_t, int64_t>> chunk_schedule(int64_t pl, int64
     j += chunk;
   }
   int64_t r = pl - j;
-  for (int d = 0; halve_tail && d < 3 && r / 2 >= 1024; d++) {
+  for (int d = 0; halve_tail && d < 3 && r / 2 >= 512; d++) {
     const int64_t h = r / 2;
     cs.emplace_back(j, r - h);
     j += r - h;
@@ -242,7 +244,7 @@ int upload_grm_pipelined(const Problem& pr, Shard& sh, int64_t chunk) {
     c.copy.dev = c.dev;
     GBM_HIP_TRY(hipStreamCreateWithFlags(&c.copy.s, hipStreamNonBlocking));
   }
-  const std::vector<std::pair<int64_t, int64_t>> sched = chunk_schedule(pl, chunk, pr.src == Source::F64);
+  const std::vector<std::pair<int64_t, int64_t>> sched = chunk_schedule(pl, chunk, pr.src == Source::F64 || getenv("GBM_HOST_CHUNK") != nullptr);
   const int64_t nch = (int64_t)sched.size();
   while ((int64_t)c.ev.size() < nch) {
     hipEvent_t e;
@@ -272,12 +274,16 @@ int upload_grm_pipelined(const Problem& pr, Shard& sh, int64_t chunk) {
                                    hipMemcpyHostToDevice, c.copy.s));
     GBM_HIP_TRY(hipEventRecord(c.ev[k], c.copy.s));
     GBM_HIP_TRY(hipStreamWaitEvent(s, c.ev[k], 0));
-    if (pr.src == Source::I8)
-      GBM_TRY(gbm_dev_expand_dosage_i8((const int8_t*)c.D8.p + j * n, n, n, pc, pr.ploidy, Xt + j * npad, npad, s));
-    else if (npad > n)
-      GBM_HIP_TRY(hipMemset2DAsync(Xt + j * npad + n, npad * 8, 0, (npad - n) * 8, pc, s));
-    GBM_TRY(gbm_dev_standardize(Xt + j * npad, npad, pc, n, Xt + j * npad, npad, (double*)c.mean.p + j,
-                                (double*)c.sd.p + j, (int32_t*)c.keep.p + j, (int64_t*)c.q.p, s));
+    if (pr.src == Source::I8) {
+      // straight from the dosage bytes (no fp64 copy of X; the kernel writes Z's padding zeros)
+      GBM_TRY(launch_standardize_i8((const int8_t*)c.D8.p + j * n, n, pc, n, pr.ploidy, Xt + j * npad, npad,
+                                    (double*)c.mean.p + j, (double*)c.sd.p + j, (int32_t*)c.keep.p + j,
+                                    (int64_t*)c.q.p, s));
+    } else {
+      if (npad > n) GBM_HIP_TRY(hipMemset2DAsync(Xt + j * npad + n, npad * 8, 0, (npad - n) * 8, pc, s));
+      GBM_TRY(gbm_dev_standardize(Xt + j * npad, npad, pc, n, Xt + j * npad, npad, (double*)c.mean.p + j,
+                                  (double*)c.sd.p + j, (int32_t*)c.keep.p + j, (int64_t*)c.q.p, s));
+    }
     GBM_TRY(gbm_dev_grm(Xt + j * npad, npad, pc, n, k == 0 ? (double*)c.G.p : (double*)c.Gc.p, gdim, c.wsg.p, wsb, s));
     if (k > 0) GBM_TRY(launch_add_inplace((double*)c.G.p, (const double*)c.Gc.p, gdim * gdim, s));
   }

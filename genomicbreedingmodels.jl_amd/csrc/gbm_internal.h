@@ -46,6 +46,9 @@ int launch_predict(const double* Xt, int64_t ldx, int64_t p, int64_t n, const do
 int64_t predict_chunks(int64_t n, int64_t p);
 int launch_add_inplace(double* a, const double* b, int64_t n, hipStream_t s);
 // centre the columns only (Z = X − m; every column kept, sd = 1): the ploidy-aware GRM
+// standardisation straight from int8 dosage rows (x = d / ploidy), out of place into Zt
+int launch_standardize_i8(const int8_t* D, int64_t ldd, int64_t p, int64_t n, int ploidy, double* Zt, int64_t ldz,
+                          double* mean, double* sd, int32_t* keep, int64_t* q_dev, hipStream_t s);
 int launch_center_columns(const double* Xt, int64_t ldx, int64_t p, int64_t n, double* Zt, int64_t ldz, double* mean,
                           double* sd, int32_t* keep, int64_t* q_dev, hipStream_t s);
 

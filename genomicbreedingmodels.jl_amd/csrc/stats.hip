@@ -1,5 +1,7 @@
 // Locus-row streaming kernels: synthetic genotypes, int8 dosage expansion and the column
 // standardisation of reference src/gwas.jl:112-115,127-130 (HBM-bound; one pass over X).
+#include <type_traits>
+
 #include "gbm_internal.h"
 
 namespace gbm {
@@ -62,19 +64,29 @@ __device__ __forceinline__ double block_sum(double v, double* red) {
 }
 
 // One workgroup per locus row (grid-strided). NPT = values cached in registers per thread
-// (0 = generic path re-reading the row from L2/MALL).
-template <int BS, int NPT, bool GATHER>
-__global__ void __launch_bounds__(BS) standardize_kernel(const double* Xt, int64_t ldx, int64_t p,
+// (0 = generic path re-reading the row from L2/MALL). T = int8_t reads dosage rows directly,
+// x = d·xs (the value expand_i8_kernel would have stored: bit-identical, without the fp64 copy).
+template <typename T>
+__device__ __forceinline__ double load_x(const T* row, int64_t i, double xs) {
+  if constexpr (std::is_same<T, int8_t>::value)
+    return (double)row[i] * xs;
+  else
+    return row[i];
+}
+
+template <int BS, int NPT, bool GATHER, typename T>
+__global__ void __launch_bounds__(BS) standardize_kernel(const T* Xt, int64_t ldx, int64_t p,
                                                          const int32_t* __restrict__ idx,
                                                          int64_t n, double* Zt, int64_t ldz,
                                                          double* __restrict__ mean,
                                                          double* __restrict__ sd, int32_t* __restrict__ keep,
-                                                         unsigned long long* __restrict__ q_dev, int center_only) {
+                                                         unsigned long long* __restrict__ q_dev, int center_only,
+                                                         double xs) {
   __shared__ double red[BS / 64];
   unsigned long long kept_local = 0;
   for (int64_t j = blockIdx.x; j < p; j += gridDim.x) {
-    const double* row = Xt + j * ldx;
-    double* zrow = Zt + j * ldz;  // may alias row (in place)
+    const T* row = Xt + j * ldx;
+    double* zrow = Zt + j * ldz;  // may alias row (in place, T = double)
     double m, v;
     if constexpr (NPT > 0) {
       double x[NPT];
@@ -82,7 +94,7 @@ __global__ void __launch_bounds__(BS) standardize_kernel(const double* Xt, int64
 #pragma unroll
       for (int k = 0; k < NPT; k++) {
         const int64_t i = (int64_t)k * BS + threadIdx.x;
-        x[k] = i < n ? row[GATHER ? idx[i] : i] : 0.0;
+        x[k] = i < n ? load_x(row, GATHER ? idx[i] : i, xs) : 0.0;
         s += x[k];
       }
       m = block_sum<BS>(s, red) / (double)n;
@@ -111,18 +123,18 @@ __global__ void __launch_bounds__(BS) standardize_kernel(const double* Xt, int64
       }
     } else {
       double s = 0.0;
-      for (int64_t i = threadIdx.x; i < n; i += BS) s += row[GATHER ? idx[i] : i];
+      for (int64_t i = threadIdx.x; i < n; i += BS) s += load_x(row, GATHER ? idx[i] : i, xs);
       m = block_sum<BS>(s, red) / (double)n;
       double ss = 0.0;
       for (int64_t i = threadIdx.x; i < n; i += BS) {
-        const double d = row[GATHER ? idx[i] : i] - m;
+        const double d = load_x(row, GATHER ? idx[i] : i, xs) - m;
         ss += d * d;
       }
       v = n > 1 ? sqrt(block_sum<BS>(ss, red) / (double)(n - 1)) : __builtin_nan("");
       if (center_only) v = 1.0;  // glmnet standardize=false: centre only, keep every column
       const bool kp = (v > 2.220446049250313e-16) && isfinite(v);
       const double r = kp ? 1.0 / v : 0.0;
-      for (int64_t i = threadIdx.x; i < ldz; i += BS) zrow[i] = (kp && i < n) ? (row[GATHER ? idx[i] : i] - m) * r : 0.0;
+      for (int64_t i = threadIdx.x; i < ldz; i += BS) zrow[i] = (kp && i < n) ? (load_x(row, GATHER ? idx[i] : i, xs) - m) * r : 0.0;
       if (threadIdx.x == 0) {
         mean[j] = m;
         sd[j] = v;
@@ -163,22 +175,22 @@ extern "C" int gbm_dev_expand_dosage_i8(const int8_t* D, int64_t ldd, int64_t n,
   return GBM_OK;
 }
 
-template <bool GATHER>
-static int launch_standardize(const double* Xt, int64_t ldx, int64_t p, const int32_t* idx, int64_t n, double* Zt,
+template <bool GATHER, typename T = double>
+static int launch_standardize(const T* Xt, int64_t ldx, int64_t p, const int32_t* idx, int64_t n, double* Zt,
                               int64_t ldz, double* mean, double* sd, int32_t* keep, int64_t* q_dev, int center_only,
-                              hipStream_t s) {
+                              hipStream_t s, double xs = 1.0) {
   const unsigned grid = (unsigned)(p < 256 * 16 ? p : 256 * 16);
   auto q = reinterpret_cast<unsigned long long*>(q_dev);
   if (n <= 256 * 4)
-    standardize_kernel<256, 4, GATHER><<<grid, 256, 0, s>>>(Xt, ldx, p, idx, n, Zt, ldz, mean, sd, keep, q, center_only);
+    standardize_kernel<256, 4, GATHER, T><<<grid, 256, 0, s>>>(Xt, ldx, p, idx, n, Zt, ldz, mean, sd, keep, q, center_only, xs);
   else if (n <= 256 * 8)
-    standardize_kernel<256, 8, GATHER><<<grid, 256, 0, s>>>(Xt, ldx, p, idx, n, Zt, ldz, mean, sd, keep, q, center_only);
+    standardize_kernel<256, 8, GATHER, T><<<grid, 256, 0, s>>>(Xt, ldx, p, idx, n, Zt, ldz, mean, sd, keep, q, center_only, xs);
   else if (n <= 256 * 16)
-    standardize_kernel<256, 16, GATHER><<<grid, 256, 0, s>>>(Xt, ldx, p, idx, n, Zt, ldz, mean, sd, keep, q, center_only);
+    standardize_kernel<256, 16, GATHER, T><<<grid, 256, 0, s>>>(Xt, ldx, p, idx, n, Zt, ldz, mean, sd, keep, q, center_only, xs);
   else if (n <= 256 * 32)
-    standardize_kernel<256, 32, GATHER><<<grid, 256, 0, s>>>(Xt, ldx, p, idx, n, Zt, ldz, mean, sd, keep, q, center_only);
+    standardize_kernel<256, 32, GATHER, T><<<grid, 256, 0, s>>>(Xt, ldx, p, idx, n, Zt, ldz, mean, sd, keep, q, center_only, xs);
   else
-    standardize_kernel<256, 0, GATHER><<<grid, 256, 0, s>>>(Xt, ldx, p, idx, n, Zt, ldz, mean, sd, keep, q, center_only);
+    standardize_kernel<256, 0, GATHER, T><<<grid, 256, 0, s>>>(Xt, ldx, p, idx, n, Zt, ldz, mean, sd, keep, q, center_only, xs);
   GBM_LAUNCH_CHECK();
   return GBM_OK;
 }
@@ -188,6 +200,14 @@ int launch_center_columns(const double* Xt, int64_t ldx, int64_t p, int64_t n, d
                           double* sd, int32_t* keep, int64_t* q_dev, hipStream_t s) {
   if (p == 0) return GBM_OK;
   return launch_standardize<false>(Xt, ldx, p, nullptr, n, Zt, ldz, mean, sd, keep, q_dev, 1, s);
+}
+
+int launch_standardize_i8(const int8_t* D, int64_t ldd, int64_t p, int64_t n, int ploidy, double* Zt, int64_t ldz,
+                          double* mean, double* sd, int32_t* keep, int64_t* q_dev, hipStream_t s) {
+  if (!D || !Zt || !mean || !sd || !keep || !q_dev || p < 0 || n < 1 || ldd < n || ldz < n || ploidy < 1)
+    return fail(GBM_E_ARG, "standardize (int8 dosages): bad arguments");
+  if (p == 0) return GBM_OK;
+  return launch_standardize<false, int8_t>(D, ldd, p, nullptr, n, Zt, ldz, mean, sd, keep, q_dev, 0, s, 1.0 / ploidy);
 }
 }  // namespace gbm
 

@@ -177,7 +177,7 @@ def test_gbm_devices_bad_ordinal_is_an_argument_error(monkeypatch):
         gbm.gblup_arrays(X, np.arange(50.0))
 
 
-@pytest.mark.parametrize("chunk", [500, 1024])
+@pytest.mark.parametrize("chunk", [500, 1024, 1200])  # 1200: 1200 + the halving tail 550 + 550
 def test_pipelined_host_upload_matches_oracle(monkeypatch, chunk):
     """gbm_gblup_fit with the host genotypes uploaded in loci chunks overlapped with the device
     work (GBM_HOST_CHUNK, re-read per call): chunk GRMs summed in order into G. Matches the oracle
