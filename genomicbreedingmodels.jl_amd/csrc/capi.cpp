@@ -207,10 +207,12 @@ int64_t host_chunk(int64_t p) {
 // Chunk schedule of the pipelined upload: chunks of `chunk` loci, the last full-size piece cut
 // into halving pieces (1/2, 1/4, 1/8, 1/8 of it, none below 512 loci) when `halve_tail`, so that
 // the device work left after the last byte has landed is a small chunk's GRM rather than a full
-// one's. That pays where the upload is copy-bound (fp64 X at C2: 40.7 -> 39.9 ms); the int8 upload
-// (an eighth of the bytes) is device-bound, where three more chunks cost 0.9 ms (25.5 -> 26.4 ms),
-// so by default it keeps equal chunks. With GBM_HOST_CHUNK set, both entries halve the tail: the
-// same partition, chunk GRMs summed in the same order, bit-identical results.
+// one's. That pays where the upload is copy-bound: fp64 X with n below ≈ 9 000 (PCIe ≈ 57 GB/s
+// moves 8np bytes while the GRM does n²p flops at ≈ 65 TF/s; C2: 40.7 -> 39.9 ms). Where the device
+// is the bound — int8 dosages (an eighth of the bytes; 25.5 -> 26.4 ms at C2) or large n (C3's
+// per-GPU shape: 4.06 -> 4.10 s) — extra chunks only add launches, so by default those keep equal
+// chunks. With GBM_HOST_CHUNK set, every entry halves the tail: the same partition, chunk GRMs
+// summed in the same order, bit-identical fp64 and int8 results.
 static std::vector<std::pair<int64_t, int64_t>> chunk_schedule(int64_t pl, int64_t chunk, bool halve_tail) {
   std::vector<std::pair<int64_t, int64_t>> cs;
   int64_t j = 0;
@@ -244,7 +246,7 @@ int upload_grm_pipelined(const Problem& pr, Shard& sh, int64_t chunk) {
     c.copy.dev = c.dev;
     GBM_HIP_TRY(hipStreamCreateWithFlags(&c.copy.s, hipStreamNonBlocking));
   }
-  const std::vector<std::pair<int64_t, int64_t>> sched = chunk_schedule(pl, chunk, pr.src == Source::F64 || getenv("GBM_HOST_CHUNK") != nullptr);
+  const std::vector<std::pair<int64_t, int64_t>> sched = chunk_schedule(pl, chunk, (pr.src == Source::F64 && n <= 8192) || getenv("GBM_HOST_CHUNK") != nullptr);
   const int64_t nch = (int64_t)sched.size();
   while ((int64_t)c.ev.size() < nch) {
     hipEvent_t e;
