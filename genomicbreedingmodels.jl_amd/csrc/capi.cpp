@@ -286,8 +286,13 @@ int upload_grm_pipelined(const Problem& pr, Shard& sh, int64_t chunk) {
       GBM_TRY(gbm_dev_standardize(Xt + j * npad, npad, pc, n, Xt + j * npad, npad, (double*)c.mean.p + j,
                                   (double*)c.sd.p + j, (int32_t*)c.keep.p + j, (int64_t*)c.q.p, s));
     }
-    GBM_TRY(gbm_dev_grm(Xt + j * npad, npad, pc, n, k == 0 ? (double*)c.G.p : (double*)c.Gc.p, gdim, c.wsg.p, wsb, s));
-    if (k > 0) GBM_TRY(launch_add_inplace((double*)c.G.p, (const double*)c.Gc.p, gdim * gdim, s));
+    if (k > 0 && grm_can_accumulate(n, pc)) {
+      // G += this chunk's GRM inside the reduce (same sums, same order as G + a separate chunk G)
+      GBM_TRY(launch_grm(Xt + j * npad, npad, pc, n, (double*)c.G.p, gdim, c.wsg.p, wsb, s, 1));
+    } else {
+      GBM_TRY(gbm_dev_grm(Xt + j * npad, npad, pc, n, k == 0 ? (double*)c.G.p : (double*)c.Gc.p, gdim, c.wsg.p, wsb, s));
+      if (k > 0) GBM_TRY(launch_add_inplace((double*)c.G.p, (const double*)c.Gc.p, gdim * gdim, s));
+    }
   }
   GBM_HIP_TRY(hipMemcpyAsync(&sh.q_host, c.q.p, 8, hipMemcpyDeviceToHost, s));
   GBM_HIP_TRY(hipStreamSynchronize(s));

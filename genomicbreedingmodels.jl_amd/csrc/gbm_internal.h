@@ -37,8 +37,10 @@ int fail(int code, const std::string& msg);
   } while (0)
 
 // Stage launchers (device pointers, stream-ordered); defined in the .hip files.
+// accum = 1: G += the GRM of these loci (only where grm_can_accumulate(n, p))
 int launch_grm(const double* Zt, int64_t ldz, int64_t p, int64_t n, double* G, int64_t ldg,
-               void* ws, int64_t ws_bytes, hipStream_t s);
+               void* ws, int64_t ws_bytes, hipStream_t s, int accum = 0);
+bool grm_can_accumulate(int64_t n, int64_t p);
 int64_t grm_workspace_bytes(int64_t n, int64_t p);
 int launch_grm_export(const double* G, int64_t ldg, int64_t n, double inv_q, double* out, int64_t ldo, hipStream_t s);
 int launch_predict(const double* Xt, int64_t ldx, int64_t p, int64_t n, const double* b, int64_t ldb, int64_t nrhs,

@@ -220,9 +220,11 @@ __global__ void __launch_bounds__(256, ET == 1 ? 4 : 1) grm_edge_kernel(const do
   grm_edge_pass<ET>(U, ldu, K, sb, blockIdx.x, part, threadIdx.x & 63, threadIdx.x >> 6);
 }
 
-// G[i][e0 + c] = Σ_s part[s][i][c] in range order (deterministic), i < n, c < er
+// G[i][e0 + c] = Σ_s part[s][i][c] in range order (deterministic), i < n, c < er; with `accum`,
+// G[i][e0 + c] += that sum (the chunked host upload adds each chunk's GRM into G)
 __global__ void __launch_bounds__(256) grm_edge_reduce_kernel(const double* __restrict__ part, int64_t n,
-                                                              SliceBounds sb, double* __restrict__ G, int64_t ldg) {
+                                                              SliceBounds sb, double* __restrict__ G, int64_t ldg,
+                                                              int accum) {
   const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (idx >= n * sb.er) return;
   const int64_t i = idx / sb.er;
@@ -231,7 +233,8 @@ __global__ void __launch_bounds__(256) grm_edge_reduce_kernel(const double* __re
   const int w = 16 * sb.et;
   double acc = 0.0;
   for (int s = 0; s < sb.es; s++) acc += part[((int64_t)s * rows + i) * w + c];
-  G[i * ldg + sb.e0 + c] = acc;
+  double* g = G + i * ldg + sb.e0 + c;
+  *g = accum ? *g + acc : acc;
 }
 
 // Two epilogues over one staging/MFMA core:
@@ -445,9 +448,11 @@ syrk_kernel(const double* __restrict__ U, int64_t ldu, int64_t K, int64_t c0, in
   }
 }
 
-// G tile = Σ_s slab[s][tile] in slice order (deterministic, no float atomics).
+// G tile = Σ_s slab[s][tile] in slice order (deterministic, no float atomics); with `accum`,
+// G tile += that sum.
 __global__ void __launch_bounds__(256) grm_slab_reduce_kernel(const double* __restrict__ slab, int64_t ntiles,
-                                                              int nslices, double* __restrict__ G, int64_t ldg) {
+                                                              int nslices, double* __restrict__ G, int64_t ldg,
+                                                              int accum) {
   const int64_t t = blockIdx.x;
   int64_t ti, tj;
   tile_of(t, ti, tj);
@@ -460,7 +465,13 @@ __global__ void __launch_bounds__(256) grm_slab_reduce_kernel(const double* __re
       acc.y += v.y;
     }
     const int row = e / BT, col = e % BT;
-    *reinterpret_cast<double2*>(G + (ti * BT + row) * ldg + tj * BT + col) = acc;
+    double2* g = reinterpret_cast<double2*>(G + (ti * BT + row) * ldg + tj * BT + col);
+    if (accum) {
+      const double2 old = *g;
+      acc.x = old.x + acc.x;
+      acc.y = old.y + acc.y;
+    }
+    *g = acc;
   }
 }
 
@@ -886,7 +897,7 @@ static int check_grm_args(const double* Zt, int64_t ldz, int64_t p, int64_t n, d
 // stage 1: the MFMA SYRK (one partial tile per (slice, tile) into the workspace slabs, or the
 // in-order carry into G)
 int launch_grm_syrk(const double* Zt, int64_t ldz, int64_t p, int64_t n, double* G, int64_t ldg, void* ws,
-                    int64_t ws_bytes, hipStream_t s) {
+                    int64_t ws_bytes, hipStream_t s, int accum = 0) {
   int rc = check_grm_args(Zt, ldz, p, n, G, ldg);
   if (rc != GBM_OK) return rc;
   const GrmPlan g = plan(n, p);
@@ -938,7 +949,7 @@ int launch_grm_syrk(const double* Zt, int64_t ldz, int64_t p, int64_t n, double*
     if (g.edge_concurrent) {
       // the edge columns of G are disjoint from the tiles: sum their partials here, on the helper
       // stream when there is one (launch_grm_reduce then skips them)
-      grm_edge_reduce_kernel<<<(unsigned)((n * g.sb.er + 255) / 256), 256, 0, es>>>(part, n, g.sb, G, ldg);
+      grm_edge_reduce_kernel<<<(unsigned)((n * g.sb.er + 255) / 256), 256, 0, es>>>(part, n, g.sb, G, ldg, accum);
       GBM_LAUNCH_CHECK();
     }
     if (ax) {
@@ -952,13 +963,13 @@ int launch_grm_syrk(const double* Zt, int64_t ldz, int64_t p, int64_t n, double*
 // stage 2: sum the slice partials of each tile into G. In carry mode, read back the error cell
 // of the inter-workgroup waits (tflags[ntiles]; set to −1 if a wait gave up) and fail loudly:
 // a timed-out wait would otherwise leave a silently wrong G.
-int launch_grm_reduce(int64_t n, int64_t p, double* G, int64_t ldg, const void* ws, hipStream_t s) {
+int launch_grm_reduce(int64_t n, int64_t p, double* G, int64_t ldg, const void* ws, hipStream_t s, int accum = 0) {
   const GrmPlan g = plan(n, p);
   if (g.sb.n == 1 && g.sb.er == 0) return GBM_OK;
   if (!ws) return fail(GBM_E_ARG, "gbm_dev_grm_reduce: workspace required");
   if (g.sb.er > 0 && !g.edge_concurrent) {
     grm_edge_reduce_kernel<<<(unsigned)((n * g.sb.er + 255) / 256), 256, 0, s>>>((const double*)ws + g.sb.eslab_off, n,
-                                                                                 g.sb, G, ldg);
+                                                                                 g.sb, G, ldg, accum);
     GBM_LAUNCH_CHECK();
   }
   if (g.sb.n == 1) return GBM_OK;
@@ -970,16 +981,24 @@ int launch_grm_reduce(int64_t n, int64_t p, double* G, int64_t ldg, const void* 
       return fail(GBM_E_HIP, "GRM in-order carry accumulation: an inter-workgroup wait timed out (G is invalid)");
     return GBM_OK;
   }
-  grm_slab_reduce_kernel<<<(unsigned)g.ntiles, 256, 0, s>>>((const double*)ws, g.ntiles, g.sb.n, G, ldg);
+  grm_slab_reduce_kernel<<<(unsigned)g.ntiles, 256, 0, s>>>((const double*)ws, g.ntiles, g.sb.n, G, ldg, accum);
   GBM_LAUNCH_CHECK();
   return GBM_OK;
 }
 
 int launch_grm(const double* Zt, int64_t ldz, int64_t p, int64_t n, double* G, int64_t ldg, void* ws,
-               int64_t ws_bytes, hipStream_t s) {
-  int rc = launch_grm_syrk(Zt, ldz, p, n, G, ldg, ws, ws_bytes, s);
+               int64_t ws_bytes, hipStream_t s, int accum) {
+  if (accum && !grm_can_accumulate(n, p)) return fail(GBM_E_ARG, "GRM: accumulation needs the slab split");
+  int rc = launch_grm_syrk(Zt, ldz, p, n, G, ldg, ws, ws_bytes, s, accum);
   if (rc != GBM_OK) return rc;
-  return launch_grm_reduce(n, p, G, ldg, ws, s);
+  return launch_grm_reduce(n, p, G, ldg, ws, s, accum);
+}
+
+// G += the GRM of these loci is possible when every element of G is written by a reduce kernel
+// (slabs over several loci ranges), not by the tile kernel itself (one range, or in-order carry).
+bool grm_can_accumulate(int64_t n, int64_t p) {
+  const GrmPlan g = plan(n, p);
+  return !g.sb.carry && g.sb.n > 1;
 }
 
 }  // namespace gbm
