@@ -154,6 +154,8 @@ struct SliceBounds {
   // appended to the grid; partials at slab + eslab_off, summed by grm_edge_reduce_kernel
   int32_t er, et, erb, es, ekper;
   int64_t e0, eslab_off;
+  // carry mode with accumulation (G += this GRM): range 0 adds G's existing tile as well
+  int32_t accum = 0;
 };
 
 // Ragged last tile column of the GRM: when n = 128 (nt − 1) + r with small r, the last tile
@@ -291,10 +293,12 @@ syrk_kernel(const double* __restrict__ U, int64_t ldu, int64_t K, int64_t c0, in
       // through agent-scope (write-through) stores; the successor may run on another XCD.
       int32_t* tflags = reinterpret_cast<int32_t*>(slab);
       double* out = C + i0 * ldc + j0 + (wm * 64 + 4 * frag_row) * ldc + wn * 64 + 4 * frag_col;
-      if (sl > 0) {
-        if (threadIdx.x == 0) wait_flag(&tflags[t], sl, tflags + ntiles);
-        __syncthreads();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      if (sl > 0 || sb.accum) {
+        if (sl > 0) {
+          if (threadIdx.x == 0) wait_flag(&tflags[t], sl, tflags + ntiles);
+          __syncthreads();
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        }
         if (active) {
           double2 prev[4][4][2];
 #pragma unroll
@@ -901,6 +905,8 @@ int launch_grm_syrk(const double* Zt, int64_t ldz, int64_t p, int64_t n, double*
   int rc = check_grm_args(Zt, ldz, p, n, G, ldg);
   if (rc != GBM_OK) return rc;
   const GrmPlan g = plan(n, p);
+  SliceBounds sb = g.sb;
+  sb.accum = accum;
   const int64_t need = (g.main_doubles + g.edge_doubles + 4) * (int64_t)sizeof(double);
   if (need > 0 && (!ws || ws_bytes < need))
     return fail(GBM_E_ARG, "gbm_dev_grm: workspace too small (" + std::to_string(ws_bytes) + " < " +
@@ -931,7 +937,7 @@ int launch_grm_syrk(const double* Zt, int64_t ldz, int64_t p, int64_t n, double*
     syrk_kernel<kPersist><<<pgrid, 256, 0, s>>>(Zt, ldz, p, 0, lim, G, ldg, (double*)ws, g.ntiles, g.sb, nullptr,
                                                 nullptr, ctr, -1, TileOwner{});
   } else {
-    syrk_kernel<kSplit><<<grid, 256, 0, s>>>(Zt, ldz, p, 0, lim, G, ldg, (double*)ws, g.ntiles, g.sb, nullptr, nullptr,
+    syrk_kernel<kSplit><<<grid, 256, 0, s>>>(Zt, ldz, p, 0, lim, G, ldg, (double*)ws, g.ntiles, sb, nullptr, nullptr,
                                              nullptr, -1, TileOwner{});
   }
   GBM_LAUNCH_CHECK();
@@ -994,11 +1000,11 @@ int launch_grm(const double* Zt, int64_t ldz, int64_t p, int64_t n, double* G, i
   return launch_grm_reduce(n, p, G, ldg, ws, s, accum);
 }
 
-// G += the GRM of these loci is possible when every element of G is written by a reduce kernel
-// (slabs over several loci ranges), not by the tile kernel itself (one range, or in-order carry).
+// G += the GRM of these loci is possible with several loci ranges: their slabs' reduce adds into G,
+// or, in the in-order carry, range 0 adds G's tile. A single range stores straight into G.
 bool grm_can_accumulate(int64_t n, int64_t p) {
   const GrmPlan g = plan(n, p);
-  return !g.sb.carry && g.sb.n > 1;
+  return g.sb.n > 1;
 }
 
 }  // namespace gbm

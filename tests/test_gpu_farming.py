@@ -177,11 +177,17 @@ def test_gbm_devices_bad_ordinal_is_an_argument_error(monkeypatch):
         gbm.gblup_arrays(X, np.arange(50.0))
 
 
-@pytest.mark.parametrize("chunk", [500, 1024, 1200])  # 1200: 1200 + the halving tail 550 + 550
-def test_pipelined_host_upload_matches_oracle(monkeypatch, chunk):
+@pytest.mark.parametrize("chunk,carry", [(500, None), (1024, None), (1200, None), (1200, "1")])
+def test_pipelined_host_upload_matches_oracle(monkeypatch, chunk, carry):
     """gbm_gblup_fit with the host genotypes uploaded in loci chunks overlapped with the device
     work (GBM_HOST_CHUNK, re-read per call): chunk GRMs summed in order into G. Matches the oracle
-    and the one-piece upload to rounding; the int8 entry (same chunks) stays bit-identical."""
+    and the one-piece upload to rounding; the int8 entry (same chunks) stays bit-identical. Chunks
+    after the first are added into G by the GRM itself (slab reduce, or range 0 of the in-order
+    carry when GBM_GRM_CARRY=1); 1200 = 1200 + the halving tail 550 + 550."""
+    if carry is None:
+        monkeypatch.delenv("GBM_GRM_CARRY", raising=False)  # the planner's choice (slabs here)
+    else:
+        monkeypatch.setenv("GBM_GRM_CARRY", carry)
     n, p = 700, 2300
     X = oracle.synth_genotypes(31, n, p)
     Y = oracle.synth_phenotypes(X, 32, ntraits=2)
