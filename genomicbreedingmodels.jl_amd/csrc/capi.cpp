@@ -259,11 +259,16 @@ int upload_grm_pipelined(const Problem& pr, Shard& sh, int64_t chunk) {
   GBM_TRY(ensure(c.keep, c.dev, pl * 4));
   GBM_TRY(ensure(c.q, c.dev, 8));
   GBM_TRY(ensure(c.G, c.dev, gdim * gdim * 8));
-  GBM_TRY(ensure(c.Gc, c.dev, gdim * gdim * 8));
   if (pr.src == Source::I8) GBM_TRY(ensure(c.D8, c.dev, pl * n));
   int64_t wsb = 0;  // the loci split (and so the workspace) is planned per chunk size
   for (const auto& jc : sched) wsb = std::max(wsb, gbm_dev_grm_workspace(n, jc.second));
   GBM_TRY(ensure(c.wsg, c.dev, wsb));
+  // a second G only for chunks whose GRM cannot be added into G in place (a single loci range)
+  for (int64_t k = 1; k < nch; k++)
+    if (!grm_can_accumulate(n, sched[k].second)) {
+      GBM_TRY(ensure(c.Gc, c.dev, gdim * gdim * 8));
+      break;
+    }
   GBM_HIP_TRY(hipMemsetAsync(c.q.p, 0, 8, s));
   double* Xt = (double*)c.Xt.p;
   for (int64_t k = 0; k < nch; k++) {
