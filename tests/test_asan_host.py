@@ -1,6 +1,6 @@
 """AddressSanitizer + UndefinedBehaviorSanitizer over libgbm's host code (SURVEY.md §5 "Race
 detection / sanitizers"): tools/asan_host.sh rebuilds the C-ABI shim and the kernels' host
-launchers with -fsanitize=address,undefined (host only; GPU sanitizers are not available on this
+launchers with host-only address + undefined-behaviour sanitizers (host only; GPU sanitizers are not available on this
 pool) and runs tests/native/asan_driver.cpp — every binding entry point with bad arguments, the
 no-device paths, and eight threads at once checking their thread-local error strings. CPU only."""
 import os

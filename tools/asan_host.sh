@@ -19,6 +19,6 @@ for f in stats.hip grm.hip chol.hip chol_flow.hip effects.hip gibbs.hip capi.cpp
 done
 for p in "${pids[@]}"; do wait "$p"; done
 $HIPCC -O1 -g -std=c++17 $SAN -c "$ROOT/tests/native/asan_driver.cpp" -o "$OUT/asan_driver.o"
-$HIPCC --offload-arch=gfx950 -fsanitize=address,undefined "$OUT/asan_driver.o" "${objs[@]}" -lrccl \
+$HIPCC --offload-arch=gfx950 -fno-gpu-sanitize -fsanitize=address,undefined "$OUT/asan_driver.o" "${objs[@]}" -lrccl \
   -lrocprofiler-sdk-roctx -o "$OUT/asan_driver"
 ASAN_OPTIONS=detect_leaks=0:halt_on_error=1 UBSAN_OPTIONS=halt_on_error=1:print_stacktrace=1 "$OUT/asan_driver"
