@@ -15,6 +15,7 @@
 #include <memory>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "gbm_internal.h"
@@ -84,6 +85,15 @@ class CtxPool {
       drop.swap(idle_);
     }
   }
+  // drops the idle contexts of one device (their buffers are freed outside the lock)
+  void trim(int dev) {
+    std::vector<std::unique_ptr<FitCtx>> drop;
+    {
+      std::lock_guard<std::mutex> lock(mu_);
+      auto it = idle_.find(dev);
+      if (it != idle_.end()) drop.swap(it->second);
+    }
+  }
 
  private:
   std::mutex mu_;
@@ -92,7 +102,13 @@ class CtxPool {
 
 // never destroyed: pooled device memory must not be freed after the HIP runtime tears down
 CtxPool& pool() {
-  static CtxPool* p = new CtxPool;
+  static CtxPool* p = [] {
+    auto* cp = new CtxPool;
+    // an allocation that runs out of device memory first frees the idle contexts of its device
+    // (they only grow and would otherwise hold e.g. ~50 GB each at C3's shape), then retries once
+    oom_trim_hook().store([](int dev) { pool().trim(dev); });
+    return cp;
+  }();
   return *p;
 }
 
@@ -157,8 +173,9 @@ int make_shards(const std::vector<int>& devs, int64_t p, std::vector<std::unique
 }
 
 // Upload the shard's columns and standardise them in place (center_only: centre them only, the
-// ploidy-aware GRM); reads back the shard's kept count.
-int prepare_shard(const Problem& pr, Shard& sh, bool center_only = false) {
+// ploidy-aware GRM); reads back the shard's kept count (valid once the stream has synchronised:
+// here with sync, else by the caller after it has queued more work behind it).
+int prepare_shard(const Problem& pr, Shard& sh, bool center_only = false, bool sync = true) {
   FitCtx& c = sh.x();
   const int64_t n = pr.n, npad = npad_of(n), pl = sh.p;
   GBM_HIP_TRY(hipSetDevice(c.dev));
@@ -186,7 +203,17 @@ int prepare_shard(const Problem& pr, Shard& sh, bool center_only = false) {
     GBM_TRY(gbm_dev_standardize((const double*)c.Xt.p, npad, pl, n, (double*)c.Xt.p, npad, (double*)c.mean.p,
                                 (double*)c.sd.p, (int32_t*)c.keep.p, (int64_t*)c.q.p, s));
   GBM_HIP_TRY(hipMemcpyAsync(&sh.q_host, c.q.p, 8, hipMemcpyDeviceToHost, s));
-  GBM_HIP_TRY(hipStreamSynchronize(s));
+  if (sync) GBM_HIP_TRY(hipStreamSynchronize(s));
+  return GBM_OK;
+}
+
+int grm_shard(const Problem& pr, Shard& sh);
+
+// Upload + standardise + partial GRM of one shard, queued back to back on its stream, then one sync.
+int prepare_grm_shard(const Problem& pr, Shard& sh) {
+  GBM_TRY(prepare_shard(pr, sh, false, false));
+  GBM_TRY(grm_shard(pr, sh));
+  GBM_HIP_TRY(hipStreamSynchronize(sh.x().stream.s));
   return GBM_OK;
 }
 
@@ -292,7 +319,10 @@ int upload_grm_pipelined(const Problem& pr, Shard& sh, int64_t chunk) {
                                   (double*)c.sd.p + j, (int32_t*)c.keep.p + j, (int64_t*)c.q.p, s));
     }
     if (k > 0 && grm_can_accumulate(n, pc)) {
-      // G += this chunk's GRM inside the reduce (same sums, same order as G + a separate chunk G)
+      // G += this chunk's GRM inside its reduce: with slabs G_old + ((P0 + P1) + ...), the sums of
+      // G plus a separate chunk G; in the in-order carry (large n) range 0 adds G_old first,
+      // ((G_old + P0) + P1) + ..., which agrees with that only to rounding (deterministic either
+      // way: the mode is fixed by n and the chunk size)
       GBM_TRY(launch_grm(Xt + j * npad, npad, pc, n, (double*)c.G.p, gdim, c.wsg.p, wsb, s, 1));
     } else {
       GBM_TRY(gbm_dev_grm(Xt + j * npad, npad, pc, n, k == 0 ? (double*)c.G.p : (double*)c.Gc.p, gdim, c.wsg.p, wsb, s));
@@ -312,6 +342,44 @@ int grm_shard(const Problem& pr, Shard& sh) {
   const int64_t wsb = gbm_dev_grm_workspace(n, sh.p);
   GBM_TRY(ensure(c.wsg, c.dev, wsb));
   return gbm_dev_grm((const double*)c.Xt.p, npad, sh.p, n, (double*)c.G.p, gdim, c.wsg.p, wsb, c.stream.s);
+}
+
+// Runs fn(shard) for every shard at once, one host thread per shard (shard 0 on the calling
+// thread): each device (and each shard sharing a device) uploads, standardises and builds its
+// partial GRM side by side with the others. A pageable hipMemcpy blocks its calling thread until
+// the copy is done, and each shard's final stream sync waits only for its own work, so driving the
+// shards from one thread would run them back to back. Every shard's device work is the same as
+// when run alone (fixed summation orders), so results do not depend on the interleaving. The
+// lowest-numbered failing shard's code and message become the call's (the thread-local error of
+// the worker is carried over to the caller).
+template <class Fn>
+int parallel_shards(std::vector<std::unique_ptr<Shard>>& shards, Fn&& fn) {
+  const size_t m = shards.size();
+  const char* e = getenv("GBM_SHARD_THREADS");  // "0": one shard after the other (A/B, tests)
+  if (m == 1 || (e && strcmp(e, "0") == 0)) {
+    for (size_t k = 0; k < m; k++) GBM_TRY(fn(k, *shards[k]));
+    return GBM_OK;
+  }
+  std::vector<int> rc(m, GBM_OK);
+  std::vector<std::string> msg(m);
+  auto run = [&](size_t k) {
+    rc[k] = fn(k, *shards[k]);
+    if (rc[k] != GBM_OK) msg[k] = g_last_error;
+  };
+  std::vector<std::thread> th;
+  th.reserve(m - 1);
+  for (size_t k = 1; k < m; k++) {
+    try {
+      th.emplace_back(run, k);
+    } catch (...) {  // no thread available: run this shard on the calling thread
+      run(k);
+    }
+  }
+  run(0);
+  for (auto& t : th) t.join();
+  for (size_t k = 0; k < m; k++)
+    if (rc[k] != GBM_OK) return fail(rc[k], msg[k]);
+  return GBM_OK;
 }
 
 // ---- RCCL communicators, one set per distinct device list, created once ----------------------
@@ -528,13 +596,146 @@ int solve_distributed(std::vector<std::unique_ptr<Shard>>& shards, const std::ve
   return cs ? sync_all(shards, leaders) : GBM_OK;
 }
 
+// Solve + marker effects for the traits [t0, t0 + nt) of Y at one λ on the summed G of every device
+// leader (factored in place), into the caller's output columns of those traits.
+int solve_effects(const Problem& pr, std::vector<std::unique_ptr<Shard>>& shards, const std::vector<int>& leaders,
+                  const std::vector<int>& ldevs, int64_t q, const double* Y, int64_t ldy, int64_t t0, int64_t nt,
+                  double lambda, double* b_hat_out, double* y_pred_out, double* mu_out) {
+  const int64_t n = pr.n, p = pr.p, npad = npad_of(n), gdim = gdim_of(n);
+  const double inv_q = 1.0 / (double)q;
+  // Below GBM_DIST_SOLVE_MIN_N individuals (default 16384, re-read per call; the knob of
+  // gbm.sharded.dist_solve_min_n) each device leader solves the (identical) n x n system, all
+  // devices at once; from there the leaders factor it together (solve_distributed). Either way a
+  // ends up on every leader for the marker back-solve (same-device shards copy it from theirs).
+  const bool distributed = leaders.size() > 1 && n >= env_i64("GBM_DIST_SOLVE_MIN_N", 16384);
+  std::vector<int32_t> infos(shards.size(), 0);
+  {
+    RoctxRange rsolve(distributed ? "gbm: distributed solve" : "gbm: solve");
+    for (size_t k = 0; k < shards.size(); k++) {
+      Shard& sh = *shards[k];
+      FitCtx& c = sh.x();
+      GBM_HIP_TRY(hipSetDevice(c.dev));
+      hipStream_t s = c.stream.s;
+      GBM_TRY(ensure(c.A, c.dev, nt * npad * 8));
+      GBM_TRY(ensure(c.B, c.dev, nt * sh.p * 8));
+      GBM_TRY(ensure(c.msum, c.dev, nt * 8));
+      if (sh.leader != (int)k) continue;
+      GBM_TRY(ensure(c.Y, c.dev, nt * npad * 8));
+      GBM_TRY(ensure(c.gebv, c.dev, nt * npad * 8));
+      GBM_TRY(ensure(c.mu, c.dev, nt * 8));
+      GBM_TRY(ensure(c.info, c.dev, 4));
+      const int64_t wss = gbm_dev_solve_workspace(n, nt);
+      GBM_TRY(ensure(c.wss, c.dev, wss));
+      GBM_HIP_TRY(hipMemcpy2DAsync(c.Y.p, npad * 8, Y + t0 * ldy, ldy * 8, n * 8, nt, hipMemcpyHostToDevice, s));
+      if (!distributed)
+        GBM_TRY(gbm_dev_gblup_solve((double*)c.G.p, gdim, n, inv_q, nullptr, lambda, (const double*)c.Y.p, npad, nt,
+                                    (double*)c.A.p, (double*)c.gebv.p, npad, (double*)c.mu.p, (int32_t*)c.info.p,
+                                    c.wss.p, wss, s));
+    }
+    if (distributed) GBM_TRY(solve_distributed(shards, leaders, ldevs, n, inv_q, lambda, nt));
+    for (int k : leaders) {
+      FitCtx& c = shards[k]->x();
+      GBM_HIP_TRY(hipSetDevice(c.dev));
+      GBM_HIP_TRY(hipMemcpyAsync(&infos[k], c.info.p, 4, hipMemcpyDeviceToHost, c.stream.s));
+    }
+    for (int k : leaders) {
+      FitCtx& c = shards[k]->x();
+      GBM_HIP_TRY(hipSetDevice(c.dev));
+      GBM_HIP_TRY(hipStreamSynchronize(c.stream.s));
+      const int32_t info = infos[k];
+      if (info < 0) return fail(GBM_E_HIP, "back substitution: block synchronisation timed out");
+      if (info != 0)
+        return fail(GBM_E_NOTPD, "G/q + lambda*I is not positive definite (pivot " + std::to_string(info) +
+                                     "); check for non-finite genotypes");
+    }
+  }
+  RoctxRange reff("gbm: marker effects + download");
+  std::vector<std::vector<double>> msums(shards.size(), std::vector<double>(nt, 0.0));
+  std::vector<double> mu(nt, 0.0);
+  double* bo = b_hat_out + t0 * (p + 1);
+  for (size_t k = 0; k < shards.size(); k++) {
+    Shard& sh = *shards[k];
+    FitCtx& c = sh.x();
+    GBM_HIP_TRY(hipSetDevice(c.dev));
+    hipStream_t s = c.stream.s;
+    if (sh.leader != (int)k)
+      GBM_HIP_TRY(hipMemcpyAsync(c.A.p, shards[sh.leader]->x().A.p, nt * npad * 8, hipMemcpyDeviceToDevice, s));
+    GBM_TRY(gbm_dev_marker_effects((const double*)c.Xt.p, npad, sh.p, n, (const double*)c.A.p, npad, nt, inv_q,
+                                   nullptr, (const double*)c.mean.p, (const double*)c.sd.p, (const int32_t*)c.keep.p,
+                                   (double*)c.B.p, sh.p, (double*)c.msum.p, s));
+    GBM_HIP_TRY(hipMemcpy2DAsync(bo + 1 + sh.j0, (p + 1) * 8, c.B.p, sh.p * 8, sh.p * 8, nt, hipMemcpyDeviceToHost, s));
+    GBM_HIP_TRY(hipMemcpyAsync(msums[k].data(), c.msum.p, nt * 8, hipMemcpyDeviceToHost, s));
+    if (k == 0) {
+      GBM_HIP_TRY(hipMemcpy2DAsync(y_pred_out + t0 * n, n * 8, c.gebv.p, npad * 8, n * 8, nt, hipMemcpyDeviceToHost, s));
+      GBM_HIP_TRY(hipMemcpyAsync(mu.data(), c.mu.p, nt * 8, hipMemcpyDeviceToHost, s));
+    }
+  }
+  std::vector<double> msum_total(nt, 0.0);
+  for (size_t k = 0; k < shards.size(); k++) {
+    GBM_HIP_TRY(hipSetDevice(shards[k]->x().dev));
+    GBM_HIP_TRY(hipStreamSynchronize(shards[k]->x().stream.s));
+    for (int64_t t = 0; t < nt; t++) msum_total[t] += msums[k][t];  // shard order: deterministic
+  }
+  for (int64_t t = 0; t < nt; t++) {
+    bo[t * (p + 1)] = mu[t] - msum_total[t];
+    if (mu_out) mu_out[t0 + t] = mu[t];
+  }
+  return GBM_OK;
+}
+
+// REML outputs of gbm_gblup_fit_reml (per trait; any may be NULL)
+struct RemlOut {
+  double* lambda;
+  double* s2e;
+  double* s2u;
+};
+
+// REML λ of trait column y on device leader `c`: each evaluation restores the summed G from its
+// pristine copy Gc, solves at λ for the standardised y (one right-hand side) and reads the
+// loglikreml terms off the bordered factorisation (as gbm_session_reml does on its cached GRM).
+int reml_lambda(FitCtx& c, int64_t n, int64_t q, const double* y, RemlResult& res) {
+  const int64_t npad = npad_of(n), gdim = gdim_of(n);
+  GBM_HIP_TRY(hipSetDevice(c.dev));
+  hipStream_t s = c.stream.s;
+  const int64_t wss = gbm_dev_solve_workspace(n, 1);
+  GBM_TRY(ensure(c.Y, c.dev, npad * 8));
+  GBM_TRY(ensure(c.A, c.dev, npad * 8));
+  GBM_TRY(ensure(c.gebv, c.dev, npad * 8));
+  GBM_TRY(ensure(c.mu, c.dev, 8));
+  GBM_TRY(ensure(c.info, c.dev, 4));
+  GBM_TRY(ensure(c.wss, c.dev, wss));
+  GBM_TRY(ensure(c.tmp, c.dev, 4 * 8));
+  const std::vector<double> ys = standardise_y(y, n);
+  GBM_HIP_TRY(hipMemsetAsync(c.Y.p, 0, (size_t)(npad * 8), s));
+  GBM_HIP_TRY(hipMemcpyAsync(c.Y.p, ys.data(), n * 8, hipMemcpyHostToDevice, s));
+  auto eval = [&](double lambda, RemlEval& e) -> int {
+    GBM_HIP_TRY(hipMemcpyAsync(c.G.p, c.Gc.p, (size_t)(npad * gdim * 8), hipMemcpyDeviceToDevice, s));
+    GBM_TRY(gbm_dev_gblup_solve((double*)c.G.p, gdim, n, 1.0 / (double)q, nullptr, lambda, (const double*)c.Y.p, npad,
+                                1, (double*)c.A.p, (double*)c.gebv.p, npad, (double*)c.mu.p, (int32_t*)c.info.p, c.wss.p,
+                                wss, s));
+    GBM_TRY(gbm_dev_gblup_terms((const double*)c.G.p, gdim, n, 1, c.wss.p, (double*)c.tmp.p, s));
+    double t[4];
+    int32_t info = 0;
+    GBM_HIP_TRY(hipMemcpyAsync(t, c.tmp.p, 4 * 8, hipMemcpyDeviceToHost, s));
+    GBM_HIP_TRY(hipMemcpyAsync(&info, c.info.p, 4, hipMemcpyDeviceToHost, s));
+    GBM_HIP_TRY(hipStreamSynchronize(s));
+    if (info < 0) return fail(GBM_E_HIP, "back substitution: block synchronisation timed out");
+    if (info != 0) return fail(GBM_E_NOTPD, "REML: G/q + lambda*I is not positive definite (pivot " + std::to_string(info) + ")");
+    e = reml_profile(n, lambda, t);
+    return GBM_OK;
+  };
+  return reml_search(eval, res);
+}
+
 int run_fit(const Problem& pr, const double* Y, int64_t ldy, int64_t nrhs, double lambda, const int* devices, int ndev,
-            double* b_hat_out, double* y_pred_out, double* mu_out, int64_t* q_out) {
+            double* b_hat_out, double* y_pred_out, double* mu_out, int64_t* q_out, const RemlOut* reml = nullptr) {
   const int64_t n = pr.n, p = pr.p;
   if (n < 2) return fail(GBM_E_DATA, "there are less than 2 entries (reference src/prediction.jl:117-123)");
   if (p < 1 || pr.ld < n || !Y || ldy < n || nrhs < 1 || nrhs > 63 || !b_hat_out || !y_pred_out)
     return fail(GBM_E_ARG, "gbm_gblup_fit: bad arguments (need p >= 1, ldx >= n, ldy >= n, 1 <= nrhs <= 63, outputs)");
-  if (!(lambda > 0.0) || !std::isfinite(lambda)) return fail(GBM_E_ARG, "gbm_gblup_fit: lambda must be finite and > 0");
+  if (!reml && (!(lambda > 0.0) || !std::isfinite(lambda)))
+    return fail(GBM_E_ARG, "gbm_gblup_fit: lambda must be finite and > 0");
+  if (reml && n < 3) return fail(GBM_E_DATA, "REML needs at least 3 entries");
   GBM_TRY(check_y(Y, n, ldy, nrhs));
   std::vector<int> devs;
   GBM_TRY(check_devices(devices, ndev, devs));
@@ -547,110 +748,55 @@ int run_fit(const Problem& pr, const double* Y, int64_t ldy, int64_t nrhs, doubl
   const int64_t chunk = pr.src == Source::SYNTH ? 0 : host_chunk(pmax);
   if (chunk > 0) {
     RoctxRange r("gbm: pipelined upload + standardise + GRM");
-    for (auto& sh : shards) {
-      GBM_TRY(upload_grm_pipelined(pr, *sh, chunk));
-      q += sh->q_host;
-    }
+    GBM_TRY(parallel_shards(shards, [&](size_t, Shard& sh) { return upload_grm_pipelined(pr, sh, chunk); }));
   } else {
-    {
-      RoctxRange r("gbm: upload + standardise");
-      for (auto& sh : shards) {
-        GBM_TRY(prepare_shard(pr, *sh));
-        q += sh->q_host;
-      }
-    }
-    if (q == 0) return fail(GBM_E_DATA, "no polymorphic locus-allele (all standard deviations <= eps, src/gwas.jl:112-115)");
-    RoctxRange r("gbm: GRM");
-    for (auto& sh : shards) GBM_TRY(grm_shard(pr, *sh));
+    // each shard's GRM is launched behind its own standardisation (a shard without polymorphic
+    // loci contributes a zero partial; q == 0 over all shards fails below)
+    RoctxRange r("gbm: upload + standardise + GRM");
+    GBM_TRY(parallel_shards(shards, [&](size_t, Shard& sh) { return prepare_grm_shard(pr, sh); }));
   }
+  for (auto& sh : shards) q += sh->q_host;
   if (q_out) *q_out = q;
   if (q == 0) return fail(GBM_E_DATA, "no polymorphic locus-allele (all standard deviations <= eps, src/gwas.jl:112-115)");
   {
     RoctxRange r("gbm: partial-GRM all-reduce");
     GBM_TRY(allreduce_grm(shards, n));
   }
-  const double inv_q = 1.0 / (double)q;
-  // Below GBM_DIST_SOLVE_MIN_N individuals (default 16384, re-read per call; the knob of
-  // gbm.sharded.dist_solve_min_n) each device leader solves the (identical) n x n system, all
-  // devices at once; from there the leaders factor it together (solve_distributed). Either way a
-  // ends up on every leader for the marker back-solve (same-device shards copy it from theirs).
   std::vector<int> leaders, ldevs;
   for (size_t k = 0; k < shards.size(); k++)
     if (shards[k]->leader == (int)k) {
       leaders.push_back((int)k);
       ldevs.push_back(shards[k]->x().dev);
     }
-  const bool distributed = leaders.size() > 1 && n >= env_i64("GBM_DIST_SOLVE_MIN_N", 16384);
-  std::vector<int32_t> infos(shards.size(), 0);
-  RoctxRange rsolve(distributed ? "gbm: distributed solve" : "gbm: solve");
-  for (size_t k = 0; k < shards.size(); k++) {
-    Shard& sh = *shards[k];
-    FitCtx& c = sh.x();
-    GBM_HIP_TRY(hipSetDevice(c.dev));
-    hipStream_t s = c.stream.s;
-    GBM_TRY(ensure(c.A, c.dev, nrhs * npad * 8));
-    GBM_TRY(ensure(c.B, c.dev, nrhs * sh.p * 8));
-    GBM_TRY(ensure(c.msum, c.dev, nrhs * 8));
-    if (sh.leader != (int)k) continue;
-    GBM_TRY(ensure(c.Y, c.dev, nrhs * npad * 8));
-    GBM_TRY(ensure(c.gebv, c.dev, nrhs * npad * 8));
-    GBM_TRY(ensure(c.mu, c.dev, nrhs * 8));
-    GBM_TRY(ensure(c.info, c.dev, 4));
-    const int64_t wss = gbm_dev_solve_workspace(n, nrhs);
-    GBM_TRY(ensure(c.wss, c.dev, wss));
-    GBM_HIP_TRY(hipMemcpy2DAsync(c.Y.p, npad * 8, Y, ldy * 8, n * 8, nrhs, hipMemcpyHostToDevice, s));
-    if (!distributed)
-      GBM_TRY(gbm_dev_gblup_solve((double*)c.G.p, gdim, n, inv_q, nullptr, lambda, (const double*)c.Y.p, npad, nrhs,
-                                  (double*)c.A.p, (double*)c.gebv.p, npad, (double*)c.mu.p, (int32_t*)c.info.p,
-                                  c.wss.p, wss, s));
-  }
-  if (distributed) GBM_TRY(solve_distributed(shards, leaders, ldevs, n, inv_q, lambda, nrhs));
+  if (!reml) return solve_effects(pr, shards, leaders, ldevs, q, Y, ldy, 0, nrhs, lambda, b_hat_out, y_pred_out, mu_out);
+  // REML (gbm_gblup_fit_reml): λ per trait chosen on the first leader's summed G, kept pristine in
+  // Gc on every leader (each solve factors G in place); then one solve + effects per trait at its λ.
+  const int64_t vbytes = npad * gdim * 8;  // rows [0, npad) of G: everything a solve reads of it
   for (int k : leaders) {
     FitCtx& c = shards[k]->x();
     GBM_HIP_TRY(hipSetDevice(c.dev));
-    GBM_HIP_TRY(hipMemcpyAsync(&infos[k], c.info.p, 4, hipMemcpyDeviceToHost, c.stream.s));
+    GBM_TRY(ensure(c.Gc, c.dev, gdim * gdim * 8));
+    GBM_HIP_TRY(hipMemcpyAsync(c.Gc.p, c.G.p, (size_t)vbytes, hipMemcpyDeviceToDevice, c.stream.s));
   }
-  for (size_t k = 0; k < shards.size(); k++) {
-    if (shards[k]->leader != (int)k) continue;
-    FitCtx& c = shards[k]->x();
-    GBM_HIP_TRY(hipSetDevice(c.dev));
-    GBM_HIP_TRY(hipStreamSynchronize(c.stream.s));
-    const int32_t info = infos[k];
-    if (info < 0) return fail(GBM_E_HIP, "back substitution: block synchronisation timed out");
-    if (info != 0)
-      return fail(GBM_E_NOTPD, "G/q + lambda*I is not positive definite (pivot " + std::to_string(info) +
-                                   "); check for non-finite genotypes");
-  }
-  RoctxRange reff("gbm: marker effects + download");
-  std::vector<std::vector<double>> msums(shards.size(), std::vector<double>(nrhs, 0.0));
-  std::vector<double> mu(nrhs, 0.0);
-  for (size_t k = 0; k < shards.size(); k++) {
-    Shard& sh = *shards[k];
-    FitCtx& c = sh.x();
-    GBM_HIP_TRY(hipSetDevice(c.dev));
-    hipStream_t s = c.stream.s;
-    if (sh.leader != (int)k)
-      GBM_HIP_TRY(hipMemcpyAsync(c.A.p, shards[sh.leader]->x().A.p, nrhs * npad * 8, hipMemcpyDeviceToDevice, s));
-    GBM_TRY(gbm_dev_marker_effects((const double*)c.Xt.p, npad, sh.p, n, (const double*)c.A.p, npad, nrhs, inv_q,
-                                   nullptr, (const double*)c.mean.p, (const double*)c.sd.p, (const int32_t*)c.keep.p,
-                                   (double*)c.B.p, sh.p, (double*)c.msum.p, s));
-    GBM_HIP_TRY(hipMemcpy2DAsync(b_hat_out + 1 + sh.j0, (p + 1) * 8, c.B.p, sh.p * 8, sh.p * 8, nrhs,
-                                 hipMemcpyDeviceToHost, s));
-    GBM_HIP_TRY(hipMemcpyAsync(msums[k].data(), c.msum.p, nrhs * 8, hipMemcpyDeviceToHost, s));
-    if (k == 0) {
-      GBM_HIP_TRY(hipMemcpy2DAsync(y_pred_out, n * 8, c.gebv.p, npad * 8, n * 8, nrhs, hipMemcpyDeviceToHost, s));
-      GBM_HIP_TRY(hipMemcpyAsync(mu.data(), c.mu.p, nrhs * 8, hipMemcpyDeviceToHost, s));
+  std::vector<double> lam(nrhs);
+  {
+    RoctxRange r("gbm: REML lambda");
+    for (int64_t t = 0; t < nrhs; t++) {
+      RemlResult res;
+      GBM_TRY(reml_lambda(shards[leaders[0]]->x(), n, q, Y + t * ldy, res));
+      lam[t] = res.lambda;
+      if (reml->lambda) reml->lambda[t] = res.lambda;
+      if (reml->s2e) reml->s2e[t] = res.s2e;
+      if (reml->s2u) reml->s2u[t] = res.s2u;
     }
   }
-  std::vector<double> msum_total(nrhs, 0.0);
-  for (size_t k = 0; k < shards.size(); k++) {
-    GBM_HIP_TRY(hipSetDevice(shards[k]->x().dev));
-    GBM_HIP_TRY(hipStreamSynchronize(shards[k]->x().stream.s));
-    for (int64_t t = 0; t < nrhs; t++) msum_total[t] += msums[k][t];  // shard order: deterministic
-  }
   for (int64_t t = 0; t < nrhs; t++) {
-    b_hat_out[t * (p + 1)] = mu[t] - msum_total[t];
-    if (mu_out) mu_out[t] = mu[t];
+    for (int k : leaders) {
+      FitCtx& c = shards[k]->x();
+      GBM_HIP_TRY(hipSetDevice(c.dev));
+      GBM_HIP_TRY(hipMemcpyAsync(c.G.p, c.Gc.p, (size_t)vbytes, hipMemcpyDeviceToDevice, c.stream.s));
+    }
+    GBM_TRY(solve_effects(pr, shards, leaders, ldevs, q, Y, ldy, t, 1, lam[t], b_hat_out, y_pred_out, mu_out));
   }
   return GBM_OK;
 }
@@ -693,6 +839,17 @@ extern "C" int gbm_gblup_fit(const double* X, int64_t n, int64_t p, int64_t ldx,
   return run_fit(pr, Y, ldy, nrhs, lambda, devices, ndev, b_hat_out, y_pred_out, mu_out, q_out);
 }
 
+extern "C" int gbm_gblup_fit_reml(const double* X, int64_t n, int64_t p, int64_t ldx, const double* Y, int64_t ldy,
+                                  int64_t nrhs, const int* devices, int ndev, double* b_hat_out, double* y_pred_out,
+                                  double* mu_out, int64_t* q_out, double* lambda_out, double* sigma2_e_out,
+                                  double* sigma2_u_out) {
+  RoctxRange r_("gbm_gblup_fit_reml");
+  if (!X) return fail(GBM_E_ARG, "gbm_gblup_fit_reml: X is NULL");
+  Problem pr{Source::F64, X, nullptr, 1, n, p, ldx};
+  const RemlOut ro{lambda_out, sigma2_e_out, sigma2_u_out};
+  return run_fit(pr, Y, ldy, nrhs, 0.0, devices, ndev, b_hat_out, y_pred_out, mu_out, q_out, &ro);
+}
+
 extern "C" int gbm_gblup_fit_synthetic(uint64_t seed, int64_t n, int64_t p, const double* Y, int64_t ldy, int64_t nrhs,
                                        double lambda, const int* devices, int ndev, double* b_hat_out,
                                        double* y_pred_out, double* mu_out, int64_t* q_out) {
@@ -723,18 +880,12 @@ extern "C" int gbm_grm(const double* X, int64_t n, int64_t p, int64_t ldx, const
   GBM_TRY(make_shards(devs, p, shards));
   int64_t q = 0;
   {
-    RoctxRange r("gbm: upload + standardise");
-    for (auto& sh : shards) {
-      GBM_TRY(prepare_shard(pr, *sh));
-      q += sh->q_host;
-    }
+    RoctxRange r("gbm: upload + standardise + GRM");
+    GBM_TRY(parallel_shards(shards, [&](size_t, Shard& sh) { return prepare_grm_shard(pr, sh); }));
   }
+  for (auto& sh : shards) q += sh->q_host;
   if (q_out) *q_out = q;
   if (q == 0) return fail(GBM_E_DATA, "no polymorphic locus-allele");
-  {
-    RoctxRange r("gbm: GRM");
-    for (auto& sh : shards) GBM_TRY(grm_shard(pr, *sh));
-  }
   {
     RoctxRange r("gbm: partial-GRM all-reduce");
     GBM_TRY(allreduce_grm(shards, n));
@@ -762,23 +913,22 @@ extern "C" int gbm_grm_ploidy_aware(const double* X, int64_t n, int64_t p, int64
   // order over the shards (host, from the device means)
   double den = 0.0;
   {
-    RoctxRange r("gbm: upload + centre");
-    std::vector<double> f;
-    for (auto& sh : shards) {
-      GBM_TRY(prepare_shard(pr, *sh, true));
-      FitCtx& c = sh->x();
-      f.resize(sh->p);
-      GBM_HIP_TRY(hipMemcpyAsync(f.data(), c.mean.p, sh->p * 8, hipMemcpyDeviceToHost, c.stream.s));
+    RoctxRange r("gbm: upload + centre + GRM");
+    std::vector<std::vector<double>> f(shards.size());
+    GBM_TRY(parallel_shards(shards, [&](size_t k, Shard& sh) {
+      GBM_TRY(prepare_shard(pr, sh, true, false));
+      FitCtx& c = sh.x();
+      f[k].resize(sh.p);
+      GBM_HIP_TRY(hipMemcpyAsync(f[k].data(), c.mean.p, sh.p * 8, hipMemcpyDeviceToHost, c.stream.s));
+      GBM_TRY(grm_shard(pr, sh));
       GBM_HIP_TRY(hipStreamSynchronize(c.stream.s));
-      for (double v : f) den += v * (1.0 - v);
-    }
+      return GBM_OK;
+    }));
+    for (const auto& fk : f)
+      for (double v : fk) den += v * (1.0 - v);  // locus order over the shards, as before
   }
   if (denom_out) *denom_out = den;
   if (!(den > 0.0) || !std::isfinite(den)) return fail(GBM_E_DATA, "gbm_grm_ploidy_aware: no polymorphic locus-allele");
-  {
-    RoctxRange r("gbm: GRM");
-    for (auto& sh : shards) GBM_TRY(grm_shard(pr, *sh));
-  }
   {
     RoctxRange r("gbm: partial-GRM all-reduce");
     GBM_TRY(allreduce_grm(shards, n));

@@ -49,12 +49,27 @@ inline std::atomic<int64_t>& alloc_counter() {
   return c;
 }
 
+// Called when a device allocation runs out of memory: frees what the pooled (idle) fit contexts
+// of that device hold, then the allocation is retried once. Set by capi.cpp's context pool.
+inline std::atomic<void (*)(int)>& oom_trim_hook() {
+  static std::atomic<void (*)(int)> h{nullptr};
+  return h;
+}
+
 inline int dalloc(DevMem& m, int dev, int64_t bytes) {
   m.reset();
   m.dev = dev;
   if (bytes <= 0) bytes = 16;
   alloc_counter().fetch_add(1, std::memory_order_relaxed);
   hipError_t e = hipMalloc(&m.p, (size_t)bytes);
+  if (e == hipErrorOutOfMemory) {
+    (void)hipGetLastError();
+    if (void (*trim)(int) = oom_trim_hook().load()) {
+      trim(dev);
+      (void)hipSetDevice(dev);
+      e = hipMalloc(&m.p, (size_t)bytes);
+    }
+  }
   if (e != hipSuccess) {
     m.p = nullptr;
     (void)hipGetLastError();
