@@ -28,6 +28,7 @@ sys.path.insert(0, os.path.join(ROOT, "genomicbreedingmodels.jl_amd"))
 
 PEAK_F64_TFLOPS = 78.6  # MI355X fp64 matrix peak (AMD datasheet)
 PEAK_HBM_GBS = 8000.0
+MEASURED_MFMA_F64_TFLOPS = 74.1  # back-to-back v_mfma_f64_16x16x4_f64 loop, tools/mfma_f64_probe.hip
 
 
 def parse():
@@ -41,6 +42,7 @@ def parse():
     ap.add_argument("--lam", type=float, default=1.0)
     ap.add_argument("--seed", type=int, default=4242)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-cpu-c3", action="store_true", help="skip the extrapolated C3 CPU baseline")
     ap.add_argument("--no-host-path", action="store_true", help="skip the C-ABI (host buffer) timings")
     ap.add_argument("--cpu-sample-p", type=int, default=0, help="loci in the CPU baseline sample (0 = all)")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL); gloo only to rehearse N ranks on one GPU")
@@ -48,37 +50,138 @@ def parse():
     return ap.parse_args()
 
 
-def cpu_baseline(args):
-    """The CPU oracle (numpy/OpenBLAS restatement, oracle/oracle.py) on the same workload
-    (rank 0, N = 1): GRM + GBLUP on n x p_sample, timed without data generation."""
-    sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    import ctypes
-
-    import oracle as O
-
+def _blas_threads():
     try:
         from threadpoolctl import threadpool_info
-        threads = max([d.get("num_threads", 1) for d in threadpool_info() if d.get("internal_api") == "openblas"] or [1])
+        return max([d.get("num_threads", 1) for d in threadpool_info() if d.get("internal_api") == "openblas"] or [1])
     except Exception:  # pragma: no cover
-        threads = len(os.sched_getaffinity(0))
+        return len(os.sched_getaffinity(0))
+
+
+def _oracle_c():
+    """The C/OpenMP restatement (oracle/gbm_oracle.c, built by build()), or None."""
+    import ctypes
+    so = os.path.join(ROOT, "oracle", "build", "libgbm_oracle.so")
+    if not os.path.exists(so):
+        return None
+    lib = ctypes.CDLL(so)
+    V, I = ctypes.c_void_p, ctypes.c_int64
+    lib.gbm_ref_synth_matrix.argtypes = [ctypes.c_uint64, I, I, I, V, I]
+    lib.gbm_ref_gblup_fit.restype = I
+    lib.gbm_ref_gblup_fit.argtypes = [V, I, I, I, V, I, I, ctypes.c_double, V, V, V, V]
+    return lib
+
+
+def cpu_baseline(args):
+    """The CPU restatements of the hot path on the same workload (rank 0, N = 1), each one full
+    GBLUP fit (standardise + GRM + Cholesky + solves + marker effects) on n x p_sample with the
+    genotypes generated beforehand (untimed): the numpy/OpenBLAS restatement (oracle/oracle.py,
+    the headline `value`) and the plain C/OpenMP restatement (oracle/gbm_oracle.c). Both are this
+    build's ports of the reference's equations (the Julia reference cannot run here: SURVEY §0.7)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+
+    threads = _blas_threads()
     n = args.individuals
     p = args.cpu_sample_p or args.loci
-    so = os.path.join(ROOT, "oracle", "build", "libgbm_oracle.so")
+    lib = _oracle_c()
     X = np.zeros((n, p), order="F")
-    if os.path.exists(so):
-        lib = ctypes.CDLL(so)
-        lib.gbm_ref_synth_matrix.argtypes = [ctypes.c_uint64, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64,
-                                             ctypes.c_void_p, ctypes.c_int64]
+    if lib is not None:
         lib.gbm_ref_synth_matrix(args.seed, n, p, 0, X.ctypes.data, n)
     else:
         X = O.synth_genotypes(args.seed, n, p)
-    Y = O.synth_phenotypes(X, args.seed + 1, args.nrhs)
+    Y = np.asfortranarray(O.synth_phenotypes(X, args.seed + 1, args.nrhs))
     t0 = time.perf_counter()
-    O.gblup_fit(X, Y, args.lam)
+    ref = O.gblup_fit(X, Y, args.lam)
     dt = time.perf_counter() - t0
-    return {"value": n * p / dt, "unit": "genotype-cells/s", "cores": int(threads), "kind": "port",
-            "sample": f"numpy/OpenBLAS fp64 restatement (oracle/oracle.py gblup_fit) on n={n} x p={p}, 1 trait, "
-                      f"one full fit in {dt:.2f} s (standardise + GRM + Cholesky + marker effects; generation untimed)"}
+    out = {"value": n * p / dt, "unit": "genotype-cells/s", "cores": int(threads), "kind": "port",
+           "sample": f"numpy/OpenBLAS fp64 restatement (oracle/oracle.py gblup_fit) on n={n} x p={p}, "
+                     f"{args.nrhs} trait(s), one full fit in {dt:.2f} s (standardise + GRM + Cholesky + solves + "
+                     f"marker effects; generation untimed)"}
+    if lib is not None:
+        t = args.nrhs
+        b = np.zeros((p + 1, t), order="F")
+        yp = np.zeros((n, t), order="F")
+        mu = np.zeros(t)
+        q = np.zeros(1, dtype=np.int64)
+        omp = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or len(os.sched_getaffinity(0))
+        t0 = time.perf_counter()
+        rc = lib.gbm_ref_gblup_fit(X.ctypes.data, n, p, n, Y.ctypes.data, n, t, args.lam, b.ctypes.data,
+                                   yp.ctypes.data, mu.ctypes.data, q.ctypes.data)
+        dtc = time.perf_counter() - t0
+        assert rc == 0 and np.abs(yp - ref["y_pred"]).max() < 1e-8 * np.abs(ref["y_pred"]).max()
+        out["c_openmp"] = {"value": n * p / dtc, "unit": "genotype-cells/s", "cores": omp, "kind": "port",
+                           "sample": f"plain C/OpenMP restatement (oracle/gbm_oracle.c gbm_ref_gblup_fit, gcc -O3 "
+                                     f"-fopenmp) on the same n={n} x p={p} fit: {dtc:.2f} s; GEBVs equal the numpy "
+                                     f"fit's to 1e-8"}
+    return out
+
+
+def cpu_baseline_c3(args):
+    """CPU time of config C3 (GBLUP n = 50 000 x p = 600 000), extrapolated: the full problem (240 GB
+    of fp64 X, 1.5e15 GRM flops) cannot run on the host in a bench. The numpy/OpenBLAS restatement's
+    per-fit costs are timed on samples and combined: standardise + GRM + marker effects at
+    n = 50 000 on p = 1 000 and 2 000 loci (linear in p: slope = cost per locus, intercept = the
+    n x n output), and the Cholesky + solves at n = 16 000 scaled by (50 000/16 000)^3. BASELINE.md
+    planned p = 60 000 and 120 000; those samples take ~10 min of CPU each, beyond a bench run."""
+    import scipy.linalg as sla
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O
+
+    lib = _oracle_c()
+    n, p3 = 50000, 600000
+
+    def gen(n, p):
+        X = np.zeros((n, p), order="F")
+        if lib is not None:
+            lib.gbm_ref_synth_matrix(424242, n, p, 0, X.ctypes.data, n)
+        else:
+            X = O.synth_genotypes(424242, n, p)
+        return X
+
+    def grm_effects(X):
+        # the unique triangle by dsyrk (numpy's own Z @ Z.T takes OpenBLAS's syrk path, which
+        # crashes at a 50 000 x 50 000 output on this image)
+        a = np.random.default_rng(1).standard_normal(X.shape[0])
+        t0 = time.perf_counter()
+        m, s, keep = O.colstats(X)
+        Z = np.asfortranarray(O.standardize(X, m, s, keep))
+        G = sla.blas.dsyrk(1.0 / Z.shape[1], Z)
+        (Z.T @ a) / Z.shape[1]
+        dt = time.perf_counter() - t0
+        del G, Z
+        return dt
+
+    samples = {}
+    for p in (1000, 2000):
+        X = gen(n, p)
+        samples[p] = grm_effects(X)
+        del X
+    slope = (samples[2000] - samples[1000]) / 1000.0
+    icpt = samples[1000] - 1000.0 * slope
+    nc = 16000
+    rng = np.random.default_rng(2)
+    Xc = gen(nc, 2000)
+    m, s, keep = O.colstats(Xc)
+    Z = np.asfortranarray(O.standardize(Xc, m, s, keep))
+    V = sla.blas.dsyrk(1.0 / Z.shape[1], Z)
+    V[np.diag_indices(nc)] += 1.0
+    del Z, Xc
+    rhs = np.column_stack([np.ones(nc), rng.standard_normal(nc)])
+    t0 = time.perf_counter()
+    c = sla.cho_factor(V, lower=False, overwrite_a=True, check_finite=False)  # dsyrk filled the upper triangle
+    sla.cho_solve(c, rhs, check_finite=False)
+    t_chol = time.perf_counter() - t0
+    del V, c
+    t_chol_c3 = t_chol * (n / nc) ** 3
+    t_c3 = slope * p3 + icpt + t_chol_c3
+    return {"value": n * p3 / t_c3, "unit": "genotype-cells/s", "cores": int(_blas_threads()), "kind": "port",
+            "extrapolated": True, "seconds_c3": t_c3,
+            "sample": f"EXTRAPOLATION of the numpy/OpenBLAS restatement to C3 (n=50000 x p=600000): standardise + "
+                      f"GRM + marker effects timed at n=50000 on p=1000 ({samples[1000]:.2f} s) and p=2000 "
+                      f"({samples[2000]:.2f} s), linear in p -> {slope * p3 + icpt:.1f} s at p=600000; Cholesky + "
+                      f"solves timed at n=16000 ({t_chol:.2f} s) x (50000/16000)^3 -> {t_chol_c3:.1f} s; "
+                      f"total {t_c3:.1f} s on one host"}
 
 
 def host_path(args, torch):
@@ -243,9 +346,11 @@ def main():
             dist.destroy_process_group()
         return
 
-    grm_flops = float(n) * (n + 1) * p_local           # unique triangle of the rank-p update
-    chol_flops = st.npad ** 3 / 3.0
-    solve_flops = 8.0 * st.npad ** 2 * (1 + args.nrhs) + 2.0 * n * p_local * args.nrhs
+    # algorithmic work of SURVEY.md §8d: GRM n(n+1)p (unique triangle of the rank-p update),
+    # Cholesky n³/3, solves 8n² per right-hand side (four triangular solves), back-solve 2np
+    grm_flops = float(n) * (n + 1) * p_local
+    chol_flops = float(n) ** 3 / 3.0
+    solve_flops = 8.0 * float(n) ** 2 * args.nrhs + 2.0 * n * p_local * args.nrhs
     achieved = grm_flops / (syrk_ms / 1000.0) / 1e12
     traffic = load_pmc(n, p_local)
     e2e_frac = (grm_flops + chol_flops + solve_flops) / (ms_per_step / 1000.0) / (PEAK_F64_TFLOPS * 1e12)
@@ -279,6 +384,8 @@ def main():
             "peak": PEAK_F64_TFLOPS,
             "unit": "TFLOP/s",
             "frac": achieved / PEAK_F64_TFLOPS,
+            "frac_of_measured_mfma": achieved / MEASURED_MFMA_F64_TFLOPS,
+            "measured_mfma_peak": MEASURED_MFMA_F64_TFLOPS,
             "traffic": traffic,
             "traffic_source": "profiles/pmc_grm.json: rocprofv3 --pmc FETCH_SIZE (x2, gfx950 16 B/lane "
                               "under-count) + WRITE_SIZE per GRM launch, separate passes of this command"
@@ -294,6 +401,8 @@ def main():
         rec["stage_ms"]["h2d_x_pinned"] = rec["host_path"]["h2d_x_ms_pinned"]
     if world == 1 and not args.no_cpu_baseline:
         rec["cpu_baseline"] = cpu_baseline(args)
+        if not args.no_cpu_c3:
+            rec["cpu_baseline_c3_extrapolated"] = cpu_baseline_c3(args)
     else:
         rec["cpu_baseline"] = None
     print(json.dumps(rec), flush=True)

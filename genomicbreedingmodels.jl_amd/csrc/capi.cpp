@@ -827,6 +827,7 @@ extern "C" int64_t gbm_device_allocations(void) { return alloc_counter().load(st
 
 extern "C" int gbm_release_device_cache(void) {
   pool().clear();
+  brr_release_cache();
   return GBM_OK;
 }
 

@@ -15,11 +15,13 @@
 // The C tile is read once and written once (the right-looking trailing updates re-read and
 // re-write the whole trailing matrix at every panel group, which made them HBM/MALL-bound).
 //
-// Scheduling. Workgroups (one per CU) take tiles from one atomic counter in row-major order. A
-// tile waits only for tiles of earlier rows, or for its own row's diagonal tile, which precede it
-// in that order and were therefore taken by running workgroups: the dependency chain always
-// ends in a running workgroup, whatever the residency, so the launch cannot deadlock. Waits are
-// bounded (~1 s, info = −1, as in chol_device.h).
+// Scheduling. Workgroups (one per CU) take tiles from one atomic counter in row-major order, except
+// that each row's right neighbour (i, i + 1) comes before its diagonal tile (i, i). A tile waits
+// only for tiles of earlier rows, for its row's diagonal tile (tiles right of the neighbour), or
+// for the neighbour's partial (the diagonal tile): every one precedes it in that order and was
+// therefore taken by a running workgroup, so the dependency chain always ends in a running
+// workgroup, whatever the residency (one resident workgroup suffices): the launch cannot
+// deadlock. Waits are bounded (~1 s, info = −1, as in chol_device.h).
 //
 // Hand-off between workgroups (MI355X: per-XCD L2s are not coherent): every byte another
 // workgroup of this launch reads — U tiles in G, Ld, Dinv — is stored write-through (`sc1`
@@ -224,6 +226,12 @@ __device__ __forceinline__ void task_tile(int t, int nbc, int& i, int& j) {
   while (r + 1 < nbc && start(r + 1) <= t) r++;
   i = r;
   j = r + (t - start(r));
+  // within a row the right neighbour (i, i + 1) is dequeued before the diagonal tile (i, i), which
+  // waits for the neighbour's partial: every wait then targets a task taken earlier
+  if (i + 1 < nbc) {
+    if (j == i) j = i + 1;
+    else if (j == i + 1) j = i;
+  }
 }
 
 // kTrace: per-task timestamps (s_memrealtime, 100 MHz) into trace[t * 24 ...] for the timeline tool
@@ -563,7 +571,10 @@ int launch_chol_flow(double* G, int64_t ldg, int64_t gdim, double* Ld, double* D
   if (nbc < 2 || (int64_t)FT * ldg * 8 > 0x7fffffff || nbc * nbc > 0x3fffffff)
     return fail(GBM_E_ARG, "dataflow Cholesky: matrix too large for 32-bit buffer offsets");
   GBM_HIP_TRY(hipMemsetAsync(flag_block, 0, (size_t)chol_flow_flag_bytes(gdim), s));
-  const int64_t slots = flow_cus();  // one workgroup per CU
+  // one workgroup per CU; GBM_CHOL_FLOW_WGS (re-read per solve) caps the grid: with 1 the whole
+  // factorisation runs on one workgroup, which checks that no wait targets a later task
+  const char* ew = getenv("GBM_CHOL_FLOW_WGS");
+  const int64_t slots = ew && atoll(ew) > 0 ? atoll(ew) : flow_cus();
   const unsigned grid = (unsigned)(ntasks < slots ? ntasks : slots);
   int32_t* q = (int32_t*)flag_block;
   if (getenv("GBM_CHOL_FLOW_TRACE")) {

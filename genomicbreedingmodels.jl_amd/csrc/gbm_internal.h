@@ -2,7 +2,9 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <functional>
 #include <string>
+#include <vector>
 
 #include "../../include/gbm.h"
 
@@ -53,5 +55,20 @@ int launch_standardize_i8(const int8_t* D, int64_t ldd, int64_t p, int64_t n, in
                           double* mean, double* sd, int32_t* keep, int64_t* q_dev, hipStream_t s);
 int launch_center_columns(const double* Xt, int64_t ldx, int64_t p, int64_t n, double* Zt, int64_t ldz, double* mean,
                           double* sd, int32_t* keep, int64_t* q_dev, hipStream_t s);
+
+
+// REML choice of λ (session.cpp; reference loglikreml src/gwas.jl:450-483 with X = 1)
+struct RemlEval {
+  double g, s2u, s2e;  // objective, σ²_u, σ²_e at one λ (σ²_u profiled inside the box [eps, 1]²)
+};
+struct RemlResult {
+  double lambda, s2e, s2u, objective;
+};
+double reml_objective(int64_t n, double logdet, double c11, double Q, double s2u);
+RemlEval reml_profile(int64_t n, double lambda, const double t[4]);
+int reml_search(const std::function<int(double, RemlEval&)>& eval, RemlResult& out);
+std::vector<double> standardise_y(const double* y, int64_t n);
+// frees the idle pooled BRR contexts (gibbs.hip; part of gbm_release_device_cache)
+void brr_release_cache();
 
 }  // namespace gbm

@@ -16,6 +16,9 @@
 // normals and Marsaglia-Tsang gammas, restated bit-for-bit in oracle/oracle.py (brr_*), so the
 // device chain and the oracle's un-blocked BGLR loop follow the same sample path.
 #include <cmath>
+#include <map>
+#include <memory>
+#include <mutex>
 #include <vector>
 
 #include "gbm_internal.h"
@@ -1057,60 +1060,148 @@ __global__ void __launch_bounds__(256) brr_quantize_kernel(const double* __restr
 using namespace gbm;
 
 
-extern "C" int gbm_brr_fit(const double* X, int64_t n, int64_t p, int64_t ldx, const double* y, int64_t n_iter,
-                           int64_t n_burnin, int64_t thin, double r2, double df0, uint64_t seed, int device,
-                           double* b_hat_out, double* y_pred_out, double* var_out) {
-  if (!X || !y || !b_hat_out || n < 3 || p < 1 || ldx < n || n_iter < 1 || n_burnin < 0 || thin < 1 ||
-      !(r2 > 0.0 && r2 < 1.0) || !(df0 > 0.0))
-    return fail(GBM_E_ARG, "gbm_brr_fit: bad arguments (n >= 3, p >= 1, ldx >= n, n_iter >= 1, n_burnin >= 0, "
-                           "thin >= 1, 0 < r2 < 1, df0 > 0)");
-  if (n_iter <= n_burnin || (n_iter / thin) <= (n_burnin / thin))
-    return fail(GBM_E_ARG, "gbm_brr_fit: no post-burn-in sample (need a multiple of thin in (n_burnin, n_iter])");
-  GBM_TRY(check_y(y, n, n, 1));
-  std::vector<int> devs;
-  GBM_TRY(check_devices(&device, 1, devs));
-  const int dev = devs[0];
+namespace gbm {
+namespace {
+
+// Pooled per-device BRR contexts (as capi.cpp pools the GBLUP fit contexts): a fit leases one, its
+// buffers only grow, so repeated fits of one shape allocate no device memory after the first
+// (cvmultithread! runs bayesian("BRR") once per fold). The captured iteration graph is kept with the
+// context and reused while the call's shape and buffers are unchanged.
+struct BrrCtx {
+  int dev = 0;
+  Stream stream;
+  DevBuf Xt, colmean, x2, e, b, bbar, r, stm, D, badm, W, Mb, alph, gamm, flg, Dt, pb, part, pout;
+  hipGraphExec_t exec = nullptr;
+  hipGraph_t graph = nullptr;
+  std::vector<int64_t> key;  // what the captured graph was built for
+  void drop_graph() {
+    if (exec) (void)hipGraphExecDestroy(exec);
+    if (graph) (void)hipGraphDestroy(graph);
+    exec = nullptr;
+    graph = nullptr;
+    key.clear();
+  }
+  ~BrrCtx() {
+    (void)hipSetDevice(dev);
+    drop_graph();
+  }
+};
+
+class BrrPool {
+ public:
+  int acquire(int dev, std::unique_ptr<BrrCtx>& out) {
+    {
+      std::lock_guard<std::mutex> lock(mu_);
+      auto& v = idle_[dev];
+      if (!v.empty()) {
+        out = std::move(v.back());
+        v.pop_back();
+        return GBM_OK;
+      }
+    }
+    auto c = std::make_unique<BrrCtx>();
+    c->dev = dev;
+    c->stream.dev = dev;
+    GBM_HIP_TRY(hipSetDevice(dev));
+    GBM_HIP_TRY(hipStreamCreateWithFlags(&c->stream.s, hipStreamNonBlocking));
+    out = std::move(c);
+    return GBM_OK;
+  }
+  void release(std::unique_ptr<BrrCtx> c) {
+    (void)hipSetDevice(c->dev);
+    if (hipStreamSynchronize(c->stream.s) != hipSuccess) {
+      (void)hipGetLastError();
+      return;
+    }
+    std::lock_guard<std::mutex> lock(mu_);
+    idle_[c->dev].push_back(std::move(c));
+  }
+  void clear() {
+    std::map<int, std::vector<std::unique_ptr<BrrCtx>>> drop;
+    std::lock_guard<std::mutex> lock(mu_);
+    drop.swap(idle_);
+  }
+  // the persistent sweep needs all its workgroups resident at once: sweeps of concurrent fits on one
+  // device take turns (held for a whole fit), so two of them can never be partly resident and spin
+  // on each other
+  std::mutex& sweep_lock(int dev) {
+    std::lock_guard<std::mutex> lock(mu_);
+    auto& m = sweep_mu_[dev];
+    if (!m) m = std::make_unique<std::mutex>();
+    return *m;
+  }
+
+ private:
+  std::mutex mu_;
+  std::map<int, std::vector<std::unique_ptr<BrrCtx>>> idle_;
+  std::map<int, std::unique_ptr<std::mutex>> sweep_mu_;
+};
+
+BrrPool& brr_pool() {
+  static BrrPool* p = new BrrPool;  // never destroyed (device memory outlives the runtime otherwise)
+  return *p;
+}
+
+struct BrrLease {
+  std::unique_ptr<BrrCtx> c;
+  ~BrrLease() {
+    if (c) brr_pool().release(std::move(c));
+  }
+};
+
+}  // namespace
+}  // namespace gbm
+
+namespace gbm {
+void brr_release_cache() { brr_pool().clear(); }
+}  // namespace gbm
+
+// One BRR fit on a leased context; sweep_mode: -1 = per GBM_BRR_SWEEP (default on), 0 = off.
+static int brr_fit_impl(const double* X, int64_t n, int64_t p, int64_t ldx, const double* y, int64_t n_iter,
+                        int64_t n_burnin, int64_t thin, double r2, double df0, uint64_t seed, int dev,
+                        int sweep_mode, double* b_hat_out, double* y_pred_out, double* var_out, bool* sweep_timeout) {
+  using namespace gbm;
+  *sweep_timeout = false;
+  BrrLease lease;
+  GBM_TRY(brr_pool().acquire(dev, lease.c));
+  BrrCtx& cx = *lease.c;
   GBM_HIP_TRY(hipSetDevice(dev));
-  Stream stw;
-  stw.dev = dev;
-  GBM_HIP_TRY(hipStreamCreateWithFlags(&stw.s, hipStreamNonBlocking));
-  hipStream_t s = stw.s;
+  hipStream_t s = cx.stream.s;
   // Xt rows and e padded to whole IW-individual chunks (the block kernels read full chunks)
   const int64_t npad = round_up(n, IW);
-  DevMem Xt, colmean, x2, W, e, b, bbar, r, stm, pb, part, pout, Dt;
-  GBM_TRY(dalloc(Xt, dev, p * npad * 8));
-  GBM_TRY(dalloc(colmean, dev, p * 8));
-  GBM_TRY(dalloc(x2, dev, p * 8));
-  GBM_TRY(dalloc(e, dev, npad * 8));
-  GBM_TRY(dalloc(b, dev, 2 * p * 8));  // two copies (iteration parity)
-  GBM_TRY(dalloc(bbar, dev, p * 8));
-  GBM_TRY(dalloc(r, dev, 2 * ((n + IW - 1) / IW) * BK2 * 8));  // ping-pong partial dots
-  GBM_TRY(dalloc(stm, dev, sizeof(BrrState)));
-  GBM_HIP_TRY(hipMemsetAsync(Xt.p, 0, (size_t)(p * npad * 8), s));
-  GBM_HIP_TRY(hipMemcpy2DAsync(Xt.p, npad * 8, X, ldx * 8, n * 8, p, hipMemcpyHostToDevice, s));
-  brr_colstats_kernel<<<(unsigned)std::min<int64_t>(p, 4096), 256, 0, s>>>((const double*)Xt.p, npad, p, n,
-                                                                           (double*)colmean.p, (double*)x2.p);
+  const int64_t C64 = (n + IW - 1) / IW;
+  GBM_TRY(ensure(cx.Xt, dev, p * npad * 8));
+  GBM_TRY(ensure(cx.colmean, dev, p * 8));
+  GBM_TRY(ensure(cx.x2, dev, p * 8));
+  GBM_TRY(ensure(cx.e, dev, npad * 8));
+  GBM_TRY(ensure(cx.b, dev, 2 * p * 8));  // two copies (iteration parity)
+  GBM_TRY(ensure(cx.bbar, dev, p * 8));
+  GBM_TRY(ensure(cx.r, dev, 2 * C64 * BK2 * 8));  // ping-pong partial dots
+  GBM_TRY(ensure(cx.stm, dev, sizeof(BrrState)));
+  GBM_HIP_TRY(hipMemsetAsync(cx.Xt.p, 0, (size_t)(p * npad * 8), s));
+  GBM_HIP_TRY(hipMemcpy2DAsync(cx.Xt.p, npad * 8, X, ldx * 8, n * 8, p, hipMemcpyHostToDevice, s));
+  brr_colstats_kernel<<<(unsigned)std::min<int64_t>(p, 4096), 256, 0, s>>>((const double*)cx.Xt.p, npad, p, n,
+                                                                           (double*)cx.colmean.p, (double*)cx.x2.p);
   GBM_LAUNCH_CHECK();
   std::vector<double> cm(p), xx(p);
-  GBM_HIP_TRY(hipMemcpyAsync(cm.data(), colmean.p, p * 8, hipMemcpyDeviceToHost, s));
-  GBM_HIP_TRY(hipMemcpyAsync(xx.data(), x2.p, p * 8, hipMemcpyDeviceToHost, s));
+  GBM_HIP_TRY(hipMemcpyAsync(cm.data(), cx.colmean.p, p * 8, hipMemcpyDeviceToHost, s));
+  GBM_HIP_TRY(hipMemcpyAsync(xx.data(), cx.x2.p, p * 8, hipMemcpyDeviceToHost, s));
   // byte storage for the sampler's sweeps when X = D/s exactly (s = 2: diploid allele
   // frequencies; then 4, 1): the chain is identical, the per-iteration stream 8× smaller.
   // GBM_BRR_I8=0 keeps fp64 storage (read per call).
-  DevMem D, badm;
   double xs = 0.0;  // 0: fp64 storage
   {
     const char* ev = std::getenv("GBM_BRR_I8");
     if (!(ev && ev[0] == '0')) {
-      GBM_TRY(dalloc(D, dev, p * npad));
-      GBM_TRY(dalloc(badm, dev, sizeof(int)));
+      GBM_TRY(ensure(cx.D, dev, p * npad));
+      GBM_TRY(ensure(cx.badm, dev, sizeof(int)));
       const double scales[3] = {2.0, 4.0, 1.0};
       for (double sc : scales) {
         int nbad = -1;
-        GBM_HIP_TRY(hipMemsetAsync(badm.p, 0, sizeof(int), s));
-        brr_quantize_kernel<<<2048, 256, 0, s>>>((const double*)Xt.p, p * npad, sc, (uint8_t*)D.p, (int*)badm.p);
+        GBM_HIP_TRY(hipMemsetAsync(cx.badm.p, 0, sizeof(int), s));
+        brr_quantize_kernel<<<2048, 256, 0, s>>>((const double*)cx.Xt.p, p * npad, sc, (uint8_t*)cx.D.p, (int*)cx.badm.p);
         GBM_LAUNCH_CHECK();
-        GBM_HIP_TRY(hipMemcpyAsync(&nbad, badm.p, sizeof(int), hipMemcpyDeviceToHost, s));
+        GBM_HIP_TRY(hipMemcpyAsync(&nbad, cx.badm.p, sizeof(int), hipMemcpyDeviceToHost, s));
         GBM_HIP_TRY(hipStreamSynchronize(s));
         if (nbad == 0) {
           xs = 1.0 / sc;
@@ -1123,32 +1214,33 @@ extern "C" int gbm_brr_fit(const double* X, int64_t n, int64_t p, int64_t ldx, c
   // each launch needs (brr_gram_kernel), and the block-transposed bytes of the byte path
   const int64_t bk = xs > 0.0 ? BK2 : BB, nblk = (p + bk - 1) / bk;
   const int nw = xs > 0.0 ? 3 : 1;
-  GBM_TRY(dalloc(W, dev, nblk * nw * BB * BB * 8));
+  GBM_TRY(ensure(cx.W, dev, nblk * nw * BB * BB * 8));
   // per-iteration block inverses (same shape as W) and step constants α, γ (padded to whole launches)
-  DevMem Mb, alph, gamm;
-  GBM_TRY(dalloc(Mb, dev, nblk * nw * BB * BB * 8));
-  GBM_TRY(dalloc(alph, dev, nblk * bk * 8));
-  GBM_TRY(dalloc(gamm, dev, nblk * bk * 8));
-  brr_gram_kernel<<<(unsigned)(nblk * nw), 256, 0, s>>>((const double*)Xt.p, npad, p, n, nw, (double*)W.p);
+  GBM_TRY(ensure(cx.Mb, dev, nblk * nw * BB * BB * 8));
+  GBM_TRY(ensure(cx.alph, dev, nblk * bk * 8));
+  GBM_TRY(ensure(cx.gamm, dev, nblk * bk * 8));
+  brr_gram_kernel<<<(unsigned)(nblk * nw), 256, 0, s>>>((const double*)cx.Xt.p, npad, p, n, nw, (double*)cx.W.p);
   GBM_LAUNCH_CHECK();
   // byte storage: one persistent sweep launch per iteration when the C chunk workgroups can all be
-  // resident (one per CU); GBM_BRR_SWEEP=0 keeps one launch per block (read per call)
+  // resident at once (the occupancy query times the CU count; one sweep per device at a time, see
+  // BrrPool::sweep_lock); GBM_BRR_SWEEP=0 keeps one launch per block (read per call)
   bool sweep = false;
-  DevMem flg;
   if (xs > 0.0) {
-    int cus = 0;
+    int cus = 0, per_cu = 0;
     const char* ev = std::getenv("GBM_BRR_SWEEP");
     GBM_HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-    sweep = !(ev && ev[0] == '0') && (int64_t)((n + IW - 1) / IW) <= cus && (int64_t)2 * ((n + IW - 1) / IW) * BK2 * 8 < 0x7fffffff;
+    GBM_HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, brr_sweep128_kernel, 256, 0));
+    sweep = sweep_mode != 0 && !(ev && ev[0] == '0') && per_cu >= 1 && C64 <= (int64_t)cus &&
+            (int64_t)2 * C64 * BK2 * 8 < 0x7fffffff;
     if (sweep) {
-      GBM_TRY(dalloc(flg, dev, (((n + IW - 1) / IW) + 1) * sizeof(int32_t)));
-      GBM_HIP_TRY(hipMemsetAsync(flg.p, 0, (((n + IW - 1) / IW) + 1) * sizeof(int32_t), s));
+      GBM_TRY(ensure(cx.flg, dev, (C64 + 1) * (int64_t)sizeof(int32_t)));
+      GBM_HIP_TRY(hipMemsetAsync(cx.flg.p, 0, (C64 + 1) * sizeof(int32_t), s));
     }
   }
   if (xs > 0.0 && !sweep) {  // the per-launch path's individual-major copy of the bytes
-    GBM_TRY(dalloc(Dt, dev, nblk * npad * BK2));
-    brr_block_transpose_kernel<<<dim3((unsigned)(npad / 64), (unsigned)nblk), 256, 0, s>>>((const uint8_t*)D.p, npad, p,
-                                                                                            (uint8_t*)Dt.p);
+    GBM_TRY(ensure(cx.Dt, dev, nblk * npad * BK2));
+    brr_block_transpose_kernel<<<dim3((unsigned)(npad / 64), (unsigned)nblk), 256, 0, s>>>((const uint8_t*)cx.D.p, npad,
+                                                                                            p, (uint8_t*)cx.Dt.p);
     GBM_LAUNCH_CHECK();
   }
   GBM_HIP_TRY(hipStreamSynchronize(s));
@@ -1179,80 +1271,100 @@ extern "C" int gbm_brr_fit(const double* X, int64_t n, int64_t p, int64_t ldx, c
   st0.seed = seed;
   std::vector<double> e0(npad, 0.0);
   for (int64_t i = 0; i < n; i++) e0[i] = y[i] - ym;
-  GBM_HIP_TRY(hipMemcpyAsync(e.p, e0.data(), npad * 8, hipMemcpyHostToDevice, s));
-  GBM_HIP_TRY(hipMemsetAsync(b.p, 0, 2 * p * 8, s));
-  GBM_HIP_TRY(hipMemsetAsync(bbar.p, 0, p * 8, s));
-  GBM_HIP_TRY(hipMemcpyAsync(stm.p, &st0, sizeof(BrrState), hipMemcpyHostToDevice, s));
+  GBM_HIP_TRY(hipMemcpyAsync(cx.e.p, e0.data(), npad * 8, hipMemcpyHostToDevice, s));
+  GBM_HIP_TRY(hipMemsetAsync(cx.b.p, 0, 2 * p * 8, s));
+  GBM_HIP_TRY(hipMemsetAsync(cx.bbar.p, 0, p * 8, s));
+  GBM_HIP_TRY(hipMemcpyAsync(cx.stm.p, &st0, sizeof(BrrState), hipMemcpyHostToDevice, s));
   GBM_HIP_TRY(hipStreamSynchronize(s));
-  // one Gibbs iteration, captured once and replayed
-  auto* stp = (BrrState*)stm.p;
-  const unsigned C = (unsigned)((n + IW - 1) / IW);
+  // one Gibbs iteration, captured once and replayed (kept with the context while the shape and the
+  // buffers are the same)
+  auto* stp = (BrrState*)cx.stm.p;
+  const unsigned C = (unsigned)C64;
   const unsigned prep_grid = (unsigned)(xs > 0.0 ? nblk : (nblk + 3) / 4);
   auto enqueue_iteration = [&]() -> int {
-    brr_prep_kernel<<<prep_grid, 256, 0, s>>>((const double*)W.p, p, nblk, nw,
-                                              (const double*)x2.p, (const double*)b.p, stp, (double*)Mb.p,
-                                              (double*)alph.p, (double*)gamm.p);
-    brr_mu_kernel<<<1, 1024, 0, s>>>((double*)e.p, n, stp);
+    brr_prep_kernel<<<prep_grid, 256, 0, s>>>((const double*)cx.W.p, p, nblk, nw, (const double*)cx.x2.p,
+                                              (const double*)cx.b.p, stp, (double*)cx.Mb.p, (double*)cx.alph.p,
+                                              (double*)cx.gamm.p);
+    brr_mu_kernel<<<1, 1024, 0, s>>>((double*)cx.e.p, n, stp);
     if (sweep) {
-      int32_t* fl = (int32_t*)flg.p;
+      int32_t* fl = (int32_t*)cx.flg.p;
       if (hipMemsetAsync(fl, 0, C * sizeof(int32_t), s) != hipSuccess) return fail(GBM_E_HIP, "gbm_brr_fit: memset failed");
-      brr_sweep128_kernel<<<C, 256, 0, s>>>((const uint8_t*)D.p, npad, p, xs, (const double*)Mb.p,
-                                            nblk, (double*)r.p, fl, fl + C, (double*)b.p, (double*)bbar.p,
-                                            (const double*)alph.p, (const double*)gamm.p, (double*)e.p, stp);
-      brr_var_kernel<<<1, 1024, 0, s>>>((const double*)b.p, p, (const double*)e.p, n, stp);
+      brr_sweep128_kernel<<<C, 256, 0, s>>>((const uint8_t*)cx.D.p, npad, p, xs, (const double*)cx.Mb.p, nblk,
+                                            (double*)cx.r.p, fl, fl + C, (double*)cx.b.p, (double*)cx.bbar.p,
+                                            (const double*)cx.alph.p, (const double*)cx.gamm.p, (double*)cx.e.p, stp);
+      brr_var_kernel<<<1, 1024, 0, s>>>((const double*)cx.b.p, p, (const double*)cx.e.p, n, stp);
       return hipGetLastError() == hipSuccess ? GBM_OK : fail(GBM_E_HIP, "gbm_brr_fit: launch failed");
     }
     if (xs > 0.0)
-      brr_dots0_128_kernel<<<C, 256, 0, s>>>((const uint8_t*)D.p, npad, n, p, xs, (const double*)e.p, (double*)r.p);
+      brr_dots0_128_kernel<<<C, 256, 0, s>>>((const uint8_t*)cx.D.p, npad, n, p, xs, (const double*)cx.e.p,
+                                             (double*)cx.r.p);
     else
-      brr_dots0_kernel<double><<<C, 256, 0, s>>>((const double*)Xt.p, npad, n, p, 1.0, (const double*)e.p,
-                                                 (double*)r.p);
+      brr_dots0_kernel<double><<<C, 256, 0, s>>>((const double*)cx.Xt.p, npad, n, p, 1.0, (const double*)cx.e.p,
+                                                 (double*)cx.r.p);
     for (int64_t k = 0; k < nblk; k++) {
-      double* pin = (double*)r.p + (k & 1) * (int64_t)C * bk;
-      double* pout = (double*)r.p + ((k + 1) & 1) * (int64_t)C * bk;
+      double* pin = (double*)cx.r.p + (k & 1) * (int64_t)C * bk;
+      double* pout = (double*)cx.r.p + ((k + 1) & 1) * (int64_t)C * bk;
       if (xs > 0.0)
-        brr_step128_kernel<<<C, 256, 0, s>>>((const uint8_t*)D.p, (const uint8_t*)Dt.p, npad, n, p, xs,
-                                             (const double*)Mb.p, k, nblk, pin, pout, (double*)b.p, (double*)bbar.p,
-                                             (const double*)alph.p, (const double*)gamm.p, (double*)e.p, stp);
+        brr_step128_kernel<<<C, 256, 0, s>>>((const uint8_t*)cx.D.p, (const uint8_t*)cx.Dt.p, npad, n, p, xs,
+                                             (const double*)cx.Mb.p, k, nblk, pin, pout, (double*)cx.b.p,
+                                             (double*)cx.bbar.p, (const double*)cx.alph.p, (const double*)cx.gamm.p,
+                                             (double*)cx.e.p, stp);
       else
-        brr_step_kernel<double><<<C, 256, 0, s>>>((const double*)Xt.p, npad, n, p, 1.0, (const double*)Mb.p, k,
-                                                  nblk, pin, pout, (double*)b.p, (double*)bbar.p,
-                                                  (const double*)alph.p, (const double*)gamm.p, (double*)e.p, stp);
+        brr_step_kernel<double><<<C, 256, 0, s>>>((const double*)cx.Xt.p, npad, n, p, 1.0, (const double*)cx.Mb.p, k,
+                                                  nblk, pin, pout, (double*)cx.b.p, (double*)cx.bbar.p,
+                                                  (const double*)cx.alph.p, (const double*)cx.gamm.p, (double*)cx.e.p,
+                                                  stp);
     }
-    brr_var_kernel<<<1, 1024, 0, s>>>((const double*)b.p, p, (const double*)e.p, n, stp);
+    brr_var_kernel<<<1, 1024, 0, s>>>((const double*)cx.b.p, p, (const double*)cx.e.p, n, stp);
     return hipGetLastError() == hipSuccess ? GBM_OK : fail(GBM_E_HIP, "gbm_brr_fit: launch failed");
   };
-  hipGraph_t graph = nullptr;
-  hipGraphExec_t exec = nullptr;
+  const std::vector<int64_t> key = {n, p, npad, (int64_t)(xs * 64.0), sweep ? 1 : 0,
+                                    (int64_t)(uintptr_t)cx.Xt.p, (int64_t)(uintptr_t)cx.D.p, (int64_t)(uintptr_t)cx.Dt.p,
+                                    (int64_t)(uintptr_t)cx.W.p, (int64_t)(uintptr_t)cx.Mb.p, (int64_t)(uintptr_t)cx.r.p,
+                                    (int64_t)(uintptr_t)cx.flg.p, (int64_t)(uintptr_t)cx.e.p, (int64_t)(uintptr_t)cx.b.p,
+                                    (int64_t)(uintptr_t)cx.bbar.p, (int64_t)(uintptr_t)cx.alph.p,
+                                    (int64_t)(uintptr_t)cx.gamm.p, (int64_t)(uintptr_t)cx.x2.p,
+                                    (int64_t)(uintptr_t)cx.stm.p};
   int rc = GBM_OK;
-  if (hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal) == hipSuccess) {
-    rc = enqueue_iteration();
-    if (hipStreamEndCapture(s, &graph) != hipSuccess || rc != GBM_OK ||
-        hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0) != hipSuccess) {
-      (void)hipGetLastError();
-      exec = nullptr;
-      rc = GBM_OK;  // fall back to direct launches (same kernels, same order)
-    }
-  }
-  for (int64_t it = 0; it < n_iter && rc == GBM_OK; it++) {
-    if (exec) {
-      if (hipGraphLaunch(exec, s) != hipSuccess) rc = fail(GBM_E_HIP, "gbm_brr_fit: graph launch failed");
-    } else {
+  if (cx.key != key) {
+    cx.drop_graph();
+    if (hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal) == hipSuccess) {
       rc = enqueue_iteration();
+      if (hipStreamEndCapture(s, &cx.graph) != hipSuccess || rc != GBM_OK ||
+          hipGraphInstantiate(&cx.exec, cx.graph, nullptr, nullptr, 0) != hipSuccess) {
+        (void)hipGetLastError();
+        cx.drop_graph();
+        rc = GBM_OK;  // fall back to direct launches (same kernels, same order)
+      } else {
+        cx.key = key;
+      }
     }
   }
-  if (exec) (void)hipGraphExecDestroy(exec);
-  if (graph) (void)hipGraphDestroy(graph);
+  {
+    std::unique_lock<std::mutex> sweep_guard;
+    if (sweep) sweep_guard = std::unique_lock<std::mutex>(brr_pool().sweep_lock(dev));
+    for (int64_t it = 0; it < n_iter && rc == GBM_OK; it++) {
+      if (cx.exec) {
+        if (hipGraphLaunch(cx.exec, s) != hipSuccess) rc = fail(GBM_E_HIP, "gbm_brr_fit: graph launch failed");
+      } else {
+        rc = enqueue_iteration();
+      }
+    }
+    if (rc == GBM_OK) GBM_HIP_TRY(hipStreamSynchronize(s));
+  }
   if (rc != GBM_OK) return rc;
   if (sweep) {
     int32_t inf = 0;
-    GBM_HIP_TRY(hipMemcpyAsync(&inf, (int32_t*)flg.p + C, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+    GBM_HIP_TRY(hipMemcpyAsync(&inf, (int32_t*)cx.flg.p + C, sizeof(int32_t), hipMemcpyDeviceToHost, s));
     GBM_HIP_TRY(hipStreamSynchronize(s));
-    if (inf < 0) return fail(GBM_E_HIP, "gbm_brr_fit: a sweep hand-off between workgroups timed out");
+    if (inf < 0) {
+      *sweep_timeout = true;
+      return fail(GBM_E_HIP, "gbm_brr_fit: a sweep hand-off between workgroups timed out");
+    }
   }
   BrrState fin{};
-  GBM_HIP_TRY(hipMemcpyAsync(&fin, stm.p, sizeof(BrrState), hipMemcpyDeviceToHost, s));
-  GBM_HIP_TRY(hipMemcpyAsync(b_hat_out + 1, bbar.p, p * 8, hipMemcpyDeviceToHost, s));
+  GBM_HIP_TRY(hipMemcpyAsync(&fin, cx.stm.p, sizeof(BrrState), hipMemcpyDeviceToHost, s));
+  GBM_HIP_TRY(hipMemcpyAsync(b_hat_out + 1, cx.bbar.p, p * 8, hipMemcpyDeviceToHost, s));
   GBM_HIP_TRY(hipStreamSynchronize(s));
   b_hat_out[0] = fin.mubar;
   if (var_out) {
@@ -1261,14 +1373,40 @@ extern "C" int gbm_brr_fit(const double* X, int64_t n, int64_t p, int64_t ldx, c
   }
   if (y_pred_out) {
     const int64_t nchunks = predict_chunks(n, p);
-    GBM_TRY(dalloc(pb, dev, (p + 1) * 8));
-    GBM_TRY(dalloc(part, dev, nchunks * npad * 8));
-    GBM_TRY(dalloc(pout, dev, npad * 8));
-    GBM_HIP_TRY(hipMemcpyAsync(pb.p, b_hat_out, (p + 1) * 8, hipMemcpyHostToDevice, s));
-    GBM_TRY(launch_predict((const double*)Xt.p, npad, p, n, (const double*)pb.p, p + 1, 1, (double*)part.p, nchunks,
-                           (double*)pout.p, npad, s));
-    GBM_HIP_TRY(hipMemcpyAsync(y_pred_out, pout.p, n * 8, hipMemcpyDeviceToHost, s));
+    GBM_TRY(ensure(cx.pb, dev, (p + 1) * 8));
+    GBM_TRY(ensure(cx.part, dev, nchunks * npad * 8));
+    GBM_TRY(ensure(cx.pout, dev, npad * 8));
+    GBM_HIP_TRY(hipMemcpyAsync(cx.pb.p, b_hat_out, (p + 1) * 8, hipMemcpyHostToDevice, s));
+    GBM_TRY(launch_predict((const double*)cx.Xt.p, npad, p, n, (const double*)cx.pb.p, p + 1, 1, (double*)cx.part.p,
+                           nchunks, (double*)cx.pout.p, npad, s));
+    GBM_HIP_TRY(hipMemcpyAsync(y_pred_out, cx.pout.p, n * 8, hipMemcpyDeviceToHost, s));
     GBM_HIP_TRY(hipStreamSynchronize(s));
   }
   return GBM_OK;
+}
+
+extern "C" int gbm_brr_fit(const double* X, int64_t n, int64_t p, int64_t ldx, const double* y, int64_t n_iter,
+                           int64_t n_burnin, int64_t thin, double r2, double df0, uint64_t seed, int device,
+                           double* b_hat_out, double* y_pred_out, double* var_out) {
+  using namespace gbm;
+  RoctxRange r_("gbm_brr_fit");
+  if (!X || !y || !b_hat_out || n < 3 || p < 1 || ldx < n || n_iter < 1 || n_burnin < 0 || thin < 1 ||
+      !(r2 > 0.0 && r2 < 1.0) || !(df0 > 0.0))
+    return fail(GBM_E_ARG, "gbm_brr_fit: bad arguments (n >= 3, p >= 1, ldx >= n, n_iter >= 1, n_burnin >= 0, "
+                           "thin >= 1, 0 < r2 < 1, df0 > 0)");
+  if (n_iter <= n_burnin || (n_iter / thin) <= (n_burnin / thin))
+    return fail(GBM_E_ARG, "gbm_brr_fit: no post-burn-in sample (need a multiple of thin in (n_burnin, n_iter])");
+  GBM_TRY(check_y(y, n, n, 1));
+  std::vector<int> devs;
+  GBM_TRY(check_devices(&device, 1, devs));
+  bool timeout = false;
+  int rc = brr_fit_impl(X, n, p, ldx, y, n_iter, n_burnin, thin, r2, df0, seed, devs[0], -1, b_hat_out, y_pred_out,
+                        var_out, &timeout);
+  // a sweep whose workgroups could not all be resident (another process or library filling the
+  // device) times out loudly on the device; the fit is then run again, from the start, on the
+  // per-launch path (same chain; the two paths agree to rounding)
+  if (rc != GBM_OK && timeout)
+    rc = brr_fit_impl(X, n, p, ldx, y, n_iter, n_burnin, thin, r2, df0, seed, devs[0], 0, b_hat_out, y_pred_out,
+                      var_out, &timeout);
+  return rc;
 }

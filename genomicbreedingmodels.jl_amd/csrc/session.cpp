@@ -9,8 +9,10 @@
 // reference src/cross_validation.jl:159-186 (cvmultithread!), which re-extract X and rebuild
 // everything per fold. One session per device; a session serialises its own calls (mutex),
 // sessions on different devices run concurrently (one host thread each).
+#include <algorithm>
 #include <cmath>
 #include <cstring>
+#include <functional>
 #include <limits>
 #include <mutex>
 #include <vector>
@@ -38,6 +40,87 @@ struct gbm_session {
 };
 
 namespace gbm {
+
+// Reference loglikreml (src/gwas.jl:450-483) with X = 1 and V = σ²_u GRM + σ²_e I, from the
+// terms of one solve at λ = σ²_e/σ²_u: logdet V = n log σ²_u + logdet V_λ, yᵀPy = Q_λ/σ²_u,
+// logdet XᵀV⁻¹X = log c11_λ − log σ²_u.
+double reml_objective(int64_t n, double logdet, double c11, double Q, double s2u) {
+  return 0.5 * ((double)n * std::log(s2u) + logdet) + Q / s2u + std::log(c11) - std::log(s2u);
+}
+
+// g(λ): the objective minimised over σ²_u inside the reference's box (σ²_e, σ²_u ∈ [eps, 1]),
+// σ²_e = λσ²_u. For fixed λ the objective is a log σ + Q/σ with a = n/2 − 1 > 0: unimodal, its
+// minimiser Q/a clamped to the box. t = {logdet V_λ, 1ᵀV_λ⁻¹1, 1ᵀV_λ⁻¹y, yᵀV_λ⁻¹y}.
+RemlEval reml_profile(int64_t n, double lambda, const double t[4]) {
+  const double logdet = t[0], c11 = t[1], c1y = t[2], yy = t[3];
+  const double Q = yy - c1y * c1y / c11;
+  const double eps = std::numeric_limits<double>::epsilon();
+  const double lo = std::max(eps, eps / lambda), hi = std::min(1.0, 1.0 / lambda);
+  const double a = 0.5 * (double)n - 1.0;
+  double s2u = Q / a;
+  if (!(s2u >= lo)) s2u = lo;
+  if (s2u > hi) s2u = hi;
+  return {reml_objective(n, logdet, c11, Q, s2u), s2u, lambda * s2u};
+}
+
+// The search of gbm_session_reml and gbm_gblup_fit_reml: a scan of log10 λ over [-6, 6] in steps of
+// 0.5, then golden-section refinement on [best − 0.5, best + 0.5] (to 1e-7 in log10 λ).
+int reml_search(const std::function<int(double, RemlEval&)>& eval, RemlResult& out) {
+  auto g = [&](double loglam, RemlEval& e) { return eval(std::pow(10.0, loglam), e); };
+  double best_x = 0.0;
+  RemlEval best{std::numeric_limits<double>::infinity(), 0.0, 0.0};
+  for (int k = -12; k <= 12; k++) {
+    RemlEval e;
+    GBM_TRY(g(0.5 * k, e));
+    if (e.g < best.g) {
+      best = e;
+      best_x = 0.5 * k;
+    }
+  }
+  double a = best_x - 0.5, b = best_x + 0.5;
+  const double r = 0.5 * (std::sqrt(5.0) - 1.0);
+  double c = b - r * (b - a), d = a + r * (b - a);
+  RemlEval ec, ed;
+  GBM_TRY(g(c, ec));
+  GBM_TRY(g(d, ed));
+  for (int it = 0; it < 60 && (b - a) > 1e-7; it++) {
+    if (ec.g < ed.g) {
+      b = d;
+      d = c;
+      ed = ec;
+      c = b - r * (b - a);
+      GBM_TRY(g(c, ec));
+    } else {
+      a = c;
+      c = d;
+      ec = ed;
+      d = a + r * (b - a);
+      GBM_TRY(g(d, ed));
+    }
+  }
+  const RemlEval& fin = ec.g < ed.g ? ec : ed;
+  const double fin_x = ec.g < ed.g ? c : d;
+  if (fin.g < best.g) {
+    best = fin;
+    best_x = fin_x;
+  }
+  out = {std::pow(10.0, best_x), best.s2e, best.s2u, best.g};
+  return GBM_OK;
+}
+
+// y standardised as the reference's gwasprep does before REML (src/gwas.jl:127-128; sd ddof = 1)
+std::vector<double> standardise_y(const double* y, int64_t n) {
+  std::vector<double> ys(y, y + n);
+  double m = 0.0;
+  for (double v : ys) m += v;
+  m /= (double)n;
+  double ss = 0.0;
+  for (double v : ys) ss += (v - m) * (v - m);
+  const double sdv = std::sqrt(ss / (double)(n - 1));
+  for (double& v : ys) v = (v - m) / sdv;
+  return ys;
+}
+
 namespace {
 
 int session_alloc_x(gbm_session* s) {
@@ -150,20 +233,6 @@ int upload_y(gbm_session* s, const double* Y, int64_t ldy, int64_t nrhs) {
   return GBM_OK;
 }
 
-// Reference loglikreml (src/gwas.jl:450-483) with X = 1 and V = σ²_u GRM + σ²_e I, from the
-// terms of one solve at λ = σ²_e/σ²_u: logdet V = n log σ²_u + logdet V_λ, yᵀPy = Q_λ/σ²_u,
-// logdet XᵀV⁻¹X = log c11_λ − log σ²_u.
-double reml_objective(int64_t n, double logdet, double c11, double Q, double s2u) {
-  return 0.5 * ((double)n * std::log(s2u) + logdet) + Q / s2u + std::log(c11) - std::log(s2u);
-}
-
-// g(λ): the objective minimised over σ²_u inside the reference's box (σ²_e, σ²_u ∈ [eps, 1]),
-// σ²_e = λσ²_u. For fixed λ the objective is a log σ + Q/σ with a = n/2 − 1 > 0: unimodal, its
-// minimiser Q/a clamped to the box.
-struct RemlEval {
-  double g, s2u, s2e;
-};
-
 int reml_eval(gbm_session* s, double lambda, RemlEval& out) {
   GBM_TRY(solve_cached(s, 1, lambda, 1.0 / (double)s->q));
   double t[4];
@@ -171,15 +240,7 @@ int reml_eval(gbm_session* s, double lambda, RemlEval& out) {
                               s->stream.s));
   GBM_HIP_TRY(hipMemcpyAsync(t, s->terms.p, 4 * 8, hipMemcpyDeviceToHost, s->stream.s));
   GBM_HIP_TRY(hipStreamSynchronize(s->stream.s));
-  const double logdet = t[0], c11 = t[1], c1y = t[2], yy = t[3];
-  const double Q = yy - c1y * c1y / c11;
-  const double eps = std::numeric_limits<double>::epsilon();
-  const double lo = std::max(eps, eps / lambda), hi = std::min(1.0, 1.0 / lambda);
-  const double a = 0.5 * (double)s->nT - 1.0;
-  double s2u = Q / a;
-  if (!(s2u >= lo)) s2u = lo;
-  if (s2u > hi) s2u = hi;
-  out = {reml_objective(s->nT, logdet, c11, Q, s2u), s2u, lambda * s2u};
+  out = reml_profile(s->nT, lambda, t);
   return GBM_OK;
 }
 
@@ -369,59 +430,14 @@ extern "C" int gbm_session_reml(gbm_session* s, const int64_t* idx, int64_t n_tr
   if (n_train < 3) return fail(GBM_E_DATA, "REML needs at least 3 entries");
   GBM_TRY(ensure_training(s, idx, n_train));
   GBM_TRY(ensure_rhs(s, 1));
-  // y standardised as the reference's gwasprep does before REML (src/gwas.jl:127-128)
-  std::vector<double> ys(y, y + n_train);
-  double m = 0.0;
-  for (double v : ys) m += v;
-  m /= (double)n_train;
-  double ss = 0.0;
-  for (double v : ys) ss += (v - m) * (v - m);
-  const double sdv = std::sqrt(ss / (double)(n_train - 1));
-  for (double& v : ys) v = (v - m) / sdv;
+  const std::vector<double> ys = standardise_y(y, n_train);
   GBM_TRY(upload_y(s, ys.data(), n_train, 1));
-  // coarse scan of log10 λ in [-6, 6], then golden-section refinement around the best point
-  auto g = [&](double loglam, RemlEval& e) { return reml_eval(s, std::pow(10.0, loglam), e); };
-  double best_x = 0.0;
-  RemlEval best{std::numeric_limits<double>::infinity(), 0.0, 0.0};
-  for (int k = -12; k <= 12; k++) {
-    RemlEval e;
-    GBM_TRY(g(0.5 * k, e));
-    if (e.g < best.g) {
-      best = e;
-      best_x = 0.5 * k;
-    }
-  }
-  double a = best_x - 0.5, b = best_x + 0.5;
-  const double r = 0.5 * (std::sqrt(5.0) - 1.0);
-  double c = b - r * (b - a), d = a + r * (b - a);
-  RemlEval ec, ed;
-  GBM_TRY(g(c, ec));
-  GBM_TRY(g(d, ed));
-  for (int it = 0; it < 60 && (b - a) > 1e-7; it++) {
-    if (ec.g < ed.g) {
-      b = d;
-      d = c;
-      ed = ec;
-      c = b - r * (b - a);
-      GBM_TRY(g(c, ec));
-    } else {
-      a = c;
-      c = d;
-      ec = ed;
-      d = a + r * (b - a);
-      GBM_TRY(g(d, ed));
-    }
-  }
-  const RemlEval& fin = ec.g < ed.g ? ec : ed;
-  const double fin_x = ec.g < ed.g ? c : d;
-  if (fin.g < best.g) {
-    best = fin;
-    best_x = fin_x;
-  }
-  if (lambda_out) *lambda_out = std::pow(10.0, best_x);
-  if (sigma2_e_out) *sigma2_e_out = best.s2e;
-  if (sigma2_u_out) *sigma2_u_out = best.s2u;
-  if (objective_out) *objective_out = best.g;
+  RemlResult res;
+  GBM_TRY(reml_search([&](double lambda, RemlEval& e) { return reml_eval(s, lambda, e); }, res));
+  if (lambda_out) *lambda_out = res.lambda;
+  if (sigma2_e_out) *sigma2_e_out = res.s2e;
+  if (sigma2_u_out) *sigma2_u_out = res.s2u;
+  if (objective_out) *objective_out = res.objective;
   return GBM_OK;
 }
 

@@ -26,7 +26,7 @@ LIB_PATH = os.environ.get("GBM_LIBGBM") or os.path.join(os.path.dirname(os.path.
 # Every symbol include/gbm.h declares (tests check the export table against this list).
 EXPORTS = (
     "gbm_version", "gbm_last_error", "gbm_device_count", "gbm_device_allocations", "gbm_release_device_cache",
-    "gbm_gblup_fit", "gbm_gblup_fit_dosage_i8", "gbm_gblup_fit_synthetic", "gbm_grm", "gbm_grm_ploidy_aware", "gbm_colstats", "gbm_predict",
+    "gbm_gblup_fit", "gbm_gblup_fit_reml", "gbm_gblup_fit_dosage_i8", "gbm_gblup_fit_synthetic", "gbm_grm", "gbm_grm_ploidy_aware", "gbm_colstats", "gbm_predict",
     "gbm_dev_npad", "gbm_dev_gdim", "gbm_dev_grm_workspace", "gbm_dev_solve_workspace",
     "gbm_dev_synth_genotypes", "gbm_dev_expand_dosage_i8", "gbm_dev_standardize", "gbm_dev_grm",
     "gbm_dev_grm_syrk", "gbm_dev_grm_reduce", "gbm_dev_grm_slices",
@@ -88,6 +88,8 @@ def _declare(lib):
     lib.gbm_dev_chol_finish.argtypes = [P, I64, I64, P, I64, I64, D, P, P, I64, P, P, P, I64, P]
     lib.gbm_gblup_fit.restype = I32
     lib.gbm_gblup_fit.argtypes = [P, I64, I64, I64, P, I64, I64, D, P, I32, P, P, P, P]
+    lib.gbm_gblup_fit_reml.restype = I32
+    lib.gbm_gblup_fit_reml.argtypes = [P, I64, I64, I64, P, I64, I64, P, I32, P, P, P, P, P, P, P]
     lib.gbm_gblup_fit_dosage_i8.restype = I32
     lib.gbm_gblup_fit_dosage_i8.argtypes = [P, I64, I64, I64, I32, P, I64, I64, D, P, I32, P, P, P, P]
     lib.gbm_gblup_fit_synthetic.restype = I32

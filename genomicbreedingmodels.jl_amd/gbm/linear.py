@@ -40,6 +40,31 @@ def gblup_arrays(X: np.ndarray, Y: np.ndarray, lambda_: float = 1.0, devices=Non
     return b_hat, y_pred, mu, int(q[0])
 
 
+def gblup_reml_arrays(X: np.ndarray, Y: np.ndarray, devices=None):
+    """Array-level GBLUP with λ chosen per trait by REML through the C ABI (gbm_gblup_fit_reml: the
+    reference's loglikreml objective, src/gwas.jl:450-483, on the call's own GRM). Returns
+    (b_hat (p+1, t), y_pred (n, t), mu (t,), q, reml) with reml = dict(lambda, sigma2_e, sigma2_u) of
+    (t,) arrays."""
+    X = np.asfortranarray(np.asarray(X, dtype=np.float64))
+    Y = np.asarray(Y, dtype=np.float64)
+    if Y.ndim == 1:
+        Y = Y[:, None]
+    Y = np.asfortranarray(Y)
+    n, p = X.shape
+    t = Y.shape[1]
+    b_hat = np.zeros((p + 1, t), order="F")
+    y_pred = np.zeros((n, t), order="F")
+    mu = np.zeros(t)
+    q = np.zeros(1, dtype=np.int64)
+    lam, s2e, s2u = np.zeros(t), np.zeros(t), np.zeros(t)
+    devs, ndev = _lib.devices_arg(devices)
+    rc = _lib.load().gbm_gblup_fit_reml(_lib.ptr(X), n, p, n, _lib.ptr(Y), n, t, devs, ndev, _lib.ptr(b_hat),
+                                        _lib.ptr(y_pred), _lib.ptr(mu), _lib.ptr(q), _lib.ptr(lam), _lib.ptr(s2e),
+                                        _lib.ptr(s2u))
+    _lib.check(rc, "gbm_gblup_fit_reml")
+    return b_hat, y_pred, mu, int(q[0]), {"lambda": lam, "sigma2_e": s2e, "sigma2_u": s2u}
+
+
 def gblup_synthetic(seed: int, n: int, p: int, Y: np.ndarray, lambda_: float = 1.0, devices=None):
     """GBLUP on the device-generated synthetic genotypes (gbm_gblup_fit_synthetic: loci 0..p-1 of the
     SURVEY.md §8d generator, no host X). Returns (b_hat (p+1, t), y_pred (n, t), mu (t,), q)."""
@@ -82,18 +107,13 @@ def gblup(*, genomes: Genomes, phenomes: Phenomes, idx_entries=None, idx_loci_al
     fit.populations = populations
     fit.y_true = y
     if isinstance(lambda_, str):
-        # REML choice of λ: one GRM on a device session, REML over the
-        # reference's loglikreml objective (src/gwas.jl:450-483), then the fit on the cached GRM
+        # REML choice of λ through the drop-in entry gbm_gblup_fit_reml: one
+        # GRM, REML over the reference's loglikreml objective (src/gwas.jl:450-483), then the fit
         if lambda_ != "reml":
             raise ArgumentError(f"lambda_ must be a positive number or \"reml\", got {lambda_!r}")
-        from .session import GenotypeSession
-        dev = (devices[0] if devices else 0) if not isinstance(devices, int) else devices
-        with GenotypeSession(X, device=dev) as s:
-            idx = np.arange(X.shape[0])
-            r = s.reml(idx, y)
-            lambda_ = r["lambda"]
-            b_hat, y_pred, mu, q = s.gblup(idx, y, lambda_)
-        fit.metrics_reml = r
+        b_hat, y_pred, mu, q, r = gblup_reml_arrays(X, y, devices=devices)
+        lambda_ = float(r["lambda"][0])
+        fit.metrics_reml = {k: float(v[0]) for k, v in r.items()}
     else:
         b_hat, y_pred, mu, q = gblup_arrays(X, y, lambda_=lambda_, devices=devices)
     fit.b_hat = b_hat[:, 0].copy()

@@ -25,6 +25,10 @@ end
 GBLUP / RR-BLUP on V = G + λI with G = ZZᵀ/q, fitted on MI355X GPUs through libgbm.so.
 Same keywords and Fit assembly as `ridge` (src/linear.jl:162-239), so it runs unchanged under
 `cvbulk`/`cvmultithread!` (src/cross_validation.jl:170-177) and `predict`.
+`λ = :reml` chooses λ = σ²_e/σ²_u by REML on the fit's own GRM first (gbm_gblup_fit_reml: the
+reference's loglikreml objective, src/gwas.jl:450-483, over gwasreml's box, :577-590); a partial
+of `gblup` with `λ = :reml` (e.g. `gblup_reml(; kw...) = gblup(; kw..., λ = :reml)`) then goes into
+`cvbulk(models = [...])` unchanged.
 """
 function gblup(;
     genomes::Genomes,
@@ -33,7 +37,7 @@ function gblup(;
     idx_loci_alleles::Union{Nothing,Vector{Int64}} = nothing,
     idx_trait::Int64 = 1,
     verbose::Bool = false,
-    λ::Float64 = 1.0,
+    λ::Union{Float64,Symbol} = 1.0,
     devices::Vector{Int32} = Int32[],
     model_label::String = "gblup",
 )::Fit
@@ -57,23 +61,40 @@ function gblup(;
     y_pred = zeros(n)
     mu = zeros(1)
     q = zeros(Int64, 1)
-    GC.@preserve X y b_hat y_pred mu q devices begin
-        rc = ccall(
-            (:gbm_gblup_fit, LIBGBM),
-            Cint,
-            (Ptr{Float64}, Int64, Int64, Int64, Ptr{Float64}, Int64, Int64, Float64,
-             Ptr{Int32}, Cint, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Int64}),
-            X, n, p, stride(X, 2), y, n, 1, λ,
-            isempty(devices) ? C_NULL : pointer(devices), length(devices),
-            b_hat, y_pred, mu, q,
-        )
-        gbm_check(rc, "gblup")
+    λ_used = zeros(1)
+    σ2 = zeros(2)
+    devs = isempty(devices) ? C_NULL : pointer(devices)
+    GC.@preserve X y b_hat y_pred mu q devices λ_used σ2 begin
+        if λ isa Symbol
+            λ === :reml || throw(ArgumentError("λ must be a Float64 or :reml, got :$λ"))
+            rc = ccall(
+                (:gbm_gblup_fit_reml, LIBGBM),
+                Cint,
+                (Ptr{Float64}, Int64, Int64, Int64, Ptr{Float64}, Int64, Int64, Ptr{Int32}, Cint,
+                 Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Int64}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}),
+                X, n, p, stride(X, 2), y, n, 1, devs, length(devices),
+                b_hat, y_pred, mu, q, λ_used, pointer(σ2, 1), pointer(σ2, 2),
+            )
+            gbm_check(rc, "gblup (REML)")
+        else
+            rc = ccall(
+                (:gbm_gblup_fit, LIBGBM),
+                Cint,
+                (Ptr{Float64}, Int64, Int64, Int64, Ptr{Float64}, Int64, Int64, Float64,
+                 Ptr{Int32}, Cint, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ptr{Int64}),
+                X, n, p, stride(X, 2), y, n, 1, λ,
+                devs, length(devices),
+                b_hat, y_pred, mu, q,
+            )
+            gbm_check(rc, "gblup")
+            λ_used[1] = λ
+        end
     end
     fit.b_hat = b_hat
     fit.y_pred = y_pred
     fit.metrics = metrics(y, y_pred)
     if verbose
-        println("gblup: n=$n p=$p q=$(q[1]) μ̂=$(mu[1]) λ=$λ")
+        println("gblup: n=$n p=$p q=$(q[1]) μ̂=$(mu[1]) λ=$(λ_used[1])" * (λ isa Symbol ? " (REML: σ²_e=$(σ2[1]), σ²_u=$(σ2[2]))" : ""))
         println(fit.metrics)
     end
     if !checkdims(fit)

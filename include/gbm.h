@@ -65,7 +65,8 @@ int gbm_device_count(int* count);
 /* Device allocations (hipMalloc calls) libgbm has made since it was loaded. */
 int64_t gbm_device_allocations(void);
 
-/* Free the idle pooled fit contexts (device buffers and streams kept between calls). */
+/* Free the idle pooled fit contexts of the GBLUP and BRR entries (device buffers, streams and the
+ * BRR iteration graphs kept between calls). */
 int gbm_release_device_cache(void);
 
 /* --------------------------------------------------------------------------------------
@@ -95,6 +96,22 @@ int gbm_gblup_fit(const double* X, int64_t n, int64_t p, int64_t ldx,
                   const double* Y, int64_t ldy, int64_t nrhs, double lambda,
                   const int* devices, int ndev,
                   double* b_hat_out, double* y_pred_out, double* mu_out, int64_t* q_out);
+
+/*
+ * gbm_gblup_fit with λ chosen per trait by REML — the drop-in `gblup(...; λ = :reml)` (Julia) /
+ * `lambda_="reml"` (Python mirror). For each trait column, on the summed GRM of the call (built
+ * once): minimise reference loglikreml (src/gwas.jl:450-483 with X = 1, V = σ²_u GRM + σ²_e I) for
+ * y standardised as gwasprep does (src/gwas.jl:127-128), over the box σ²_e, σ²_u ∈ [eps, 1]
+ * (src/gwas.jl:585; gwasreml's LBFGS at :577-590), σ²_u profiled in closed form per λ = σ²_e/σ²_u and
+ * a scan + golden-section search over log λ (the same search as gbm_session_reml); then the GBLUP fit
+ * of that trait at its λ (the original, unstandardised y). Outputs as gbm_gblup_fit, plus per trait
+ * (nrhs each, any may be NULL): lambda_out, sigma2_e_out, sigma2_u_out. n >= 3.
+ */
+int gbm_gblup_fit_reml(const double* X, int64_t n, int64_t p, int64_t ldx,
+                       const double* Y, int64_t ldy, int64_t nrhs,
+                       const int* devices, int ndev,
+                       double* b_hat_out, double* y_pred_out, double* mu_out, int64_t* q_out,
+                       double* lambda_out, double* sigma2_e_out, double* sigma2_u_out);
 
 /*
  * Same as gbm_gblup_fit for int8 dosages: X[i, j] = D[i + j*ldd] / ploidy (exact in fp64).

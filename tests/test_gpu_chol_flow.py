@@ -103,3 +103,20 @@ def test_flow_reports_first_failing_pivot(monkeypatch, bad):
     torch.cuda.synchronize()
     assert int(a.info.item()) == bad + 1
     assert int(b.info.item()) == bad + 1
+
+
+@pytest.mark.parametrize("wgs", ["1", "2", "7"])
+def test_flow_few_resident_workgroups_complete_bit_identical(monkeypatch, wgs):
+    """Deadlock freedom: every wait targets a task dequeued earlier (the right
+    neighbour precedes its diagonal tile), so the launch completes with any number of resident
+    workgroups — GBM_CHOL_FLOW_WGS caps the grid, down to one workgroup running every tile in
+    dequeue order — and gives the bits of the full-grid launch."""
+    import torch
+    monkeypatch.setenv("GBM_CHOL_FLOW_MAX", "1000000")
+    X, Y, a, b = _pair(1030, 700, 2, 13, 0.9)
+    a.solve()
+    monkeypatch.setenv("GBM_CHOL_FLOW_WGS", wgs)
+    b.solve()
+    torch.cuda.synchronize()
+    assert int(a.info.item()) == 0 and int(b.info.item()) == 0
+    assert torch.equal(a.gebv, b.gebv) and torch.equal(a.A, b.A) and torch.equal(a.mu, b.mu)

@@ -194,3 +194,35 @@ def test_synthetic_session_matches_host_session(data):
     ref = oracle.gblup_fit(X[idx], Y[idx], 1.0)
     assert q == ref["q"]
     assert rel(yp, ref["y_pred"]) < 1e-9 and rel(b, ref["b_hat"]) < 1e-6
+
+
+@pytest.mark.parametrize("devices", [None, [0, 0]])
+def test_cabi_reml_fit_matches_session_reml_and_oracle(data, devices):
+    """gbm_gblup_fit_reml (the drop-in gblup(λ = :reml); VERDICT r02 Missing #3): per trait the REML
+    λ on the call's own GRM equals gbm_session_reml's on the same rows (same objective, same search:
+    the GRMs agree to rounding, the λ to 1e-9), reaches the oracle's loglikreml optimum
+    (src/gwas.jl:450-483,577-590), and each trait's fit is the oracle's GBLUP at its λ."""
+    X, Y = data
+    idx = np.arange(260)
+    Xs, Ys = X[idx], Y[idx]
+    b, yp, mu, q, r = gbm.gblup_reml_arrays(Xs, Ys, devices=devices)
+    G, _ = oracle.grm(Xs)
+    with gbm.GenotypeSession(X) as s:
+        for t in range(Ys.shape[1]):
+            rs = s.reml(idx, Ys[:, t])
+            assert abs(np.log(r["lambda"][t]) - np.log(rs["lambda"])) < 1e-9
+            assert abs(r["sigma2_u"][t] - rs["sigma2_u"]) < 1e-9 * rs["sigma2_u"]
+            assert abs(r["sigma2_e"][t] - rs["sigma2_e"]) < 1e-9 * rs["sigma2_e"]
+            ref = oracle.reml_reference(Ys[:, t], G)
+            assert abs(np.log(r["lambda"][t]) - np.log(ref["lambda"])) < 1e-2
+            f_got = oracle.loglikreml((r["sigma2_e"][t], r["sigma2_u"][t]), ref["y_std"], np.ones((idx.size, 1)), G)
+            assert f_got <= ref["objective"] + 1e-7 * max(1.0, abs(ref["objective"]))
+            fit = oracle.gblup_fit(Xs, Ys[:, t], r["lambda"][t])
+            assert q == fit["q"]
+            assert rel(yp[:, t], fit["y_pred"][:, 0]) < 1e-9 and abs(mu[t] - fit["mu"][0]) < 1e-9 * abs(fit["mu"][0])
+            assert rel(b[:, t], fit["b_hat"][:, 0]) < 1e-6
+    # the model function takes the same route
+    g = gbm.Genomes([f"e{i}" for i in idx], ["p"] * idx.size, [f"l{j}" for j in range(X.shape[1])], Xs)
+    ph = gbm.Phenomes(g.entries, g.populations, ["t1"], Ys[:, :1])
+    f1 = gbm.gblup(genomes=g, phenomes=ph, lambda_="reml", devices=devices)
+    assert f1.metrics_reml["lambda"] == r["lambda"][0] and np.array_equal(f1.y_pred, yp[:, 0])
