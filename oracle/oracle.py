@@ -254,6 +254,30 @@ def reml_reference(y: np.ndarray, GRM: np.ndarray) -> dict:
             "objective": float(res.fun), "y_std": ys}
 
 
+def lmm_gls_loglik(y: np.ndarray, X: np.ndarray, V: np.ndarray, reml: bool) -> dict:
+    """Textbook linear-mixed-model quantities at given variance components, V = cov(y) (dense
+    Cholesky): GLS β̂ = (XᵀV⁻¹X)⁻¹XᵀV⁻¹y, vcov(β̂) = (XᵀV⁻¹X)⁻¹ and the ML or REML (Harville)
+    log-likelihood −½[(n − p_ml) log 2π + log det V (+ log det XᵀV⁻¹X) + (y − Xβ̂)ᵀV⁻¹(y − Xβ̂)].
+    The same GLS/logdet machinery as the reference's V/GLS equations (src/gwas.jl:462-472,591-597)
+    and loglikreml (:450-483), in the form R lme4 reports: it pins this oracle (and the device
+    solve's terms) against lme4 known answers (tests/golden/lmer_r.npz)."""
+    import scipy.linalg as sla
+
+    n, pf = X.shape
+    c = sla.cho_factor(V, lower=True)
+    ViX = sla.cho_solve(c, X)
+    Viy = sla.cho_solve(c, y)
+    M = X.T @ ViX
+    beta = np.linalg.solve(M, X.T @ Viy)
+    r = float(y @ Viy - beta @ (X.T @ Viy))
+    logdet = 2.0 * float(np.log(np.diag(c[0])).sum())
+    if reml:
+        ll = -0.5 * ((n - pf) * np.log(2 * np.pi) + logdet + np.linalg.slogdet(M)[1] + r)
+    else:
+        ll = -0.5 * (n * np.log(2 * np.pi) + logdet + r)
+    return {"beta": beta, "vcov": np.linalg.inv(M), "loglike": float(ll), "logdet": logdet}
+
+
 # ----------------------------------------------------------------------------------------
 # Ridge path (SURVEY.md §8f row 4): GLMNet alpha = 0, standardize = false, intercept
 # (reference ridge, src/linear.jl:193-203). glmnet is un-vendored; restated from its published
