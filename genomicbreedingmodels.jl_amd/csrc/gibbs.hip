@@ -15,6 +15,7 @@
 // Random numbers: a counter-based hash of (seed, stream, counter) (no sampler state), Box-Muller
 // normals and Marsaglia-Tsang gammas, restated bit-for-bit in oracle/oracle.py (brr_*), so the
 // device chain and the oracle's un-blocked BGLR loop follow the same sample path.
+#include <atomic>
 #include <cmath>
 #include <map>
 #include <memory>
@@ -63,6 +64,7 @@ struct BrrState {
   double mubar, varEbar, varBbar;
   int64_t it, burnin, thin, nsum;
   uint64_t seed;
+  uint64_t epoch;  // distinct per fit: part of the super-block sweep's hand-off tags (pooled buffers)
 };
 
 __device__ __forceinline__ bool brr_accumulate(const BrrState* st) {
@@ -1013,6 +1015,568 @@ __global__ void __launch_bounds__(256) brr_sweep128_kernel(const uint8_t* __rest
   e[i] = ei;  // rows past n stay 0: their genotypes are 0
 }
 
+// ---- byte storage: super-block sweep over all CUs (round 3) ------------------------------------
+// The per-block sweep above runs one 256-individual chunk per CU (⌈n/256⌉ = 40 CUs at C4) and
+// hands partial dots between them after every 128-marker block: bound by one CU's work per
+// block and one hand-off per block. Here the markers go in super-blocks of SBK = 512: the whole
+// super-block's single-site steps are ONE affine map of its start dots,
+//   δ_S = M_S (γ_S − α_S ∘ d⁰_S),  M_S = (I + D_S L_S)⁻¹  (unit lower, 512 x 512),
+// built once per iteration by block forward substitution over the four 128-marker sub-blocks
+// (brr_sb_prep_kernel, from brr_prep_kernel's 128-block inverses and the super-block's Gram
+// blocks). The individuals are split into chunks of K (<= 64) over (up to) every CU. Per super-
+// block, three hand-offs between all chunk workgroups:
+//   1. every chunk publishes its partial dots X_{S,c}ᵀ e_c (512 values);
+//   2. workgroup c sums the partials of its R owned rows of d⁰_S over all chunks (fixed order),
+//      forms r̃ = γ − α∘d⁰ there and publishes those rows;
+//   3. workgroup c computes its rows of δ_S = M_S r̃ from all of r̃, updates b and b̄ of those
+//      markers and publishes its δ rows;
+// then every chunk applies e += X_S δ_S to its individuals. Each hand-off: write-through (sc1)
+// stores, every storing wave drains, a workgroup barrier, one agent-scope atomic add per
+// workgroup onto an 8-way sharded counter (its XCD's shard); the consumer's wave 0 polls the 8
+// shards (sc1 loads) until they sum to the target, the others wait at a barrier, and every payload
+// load is an sc1 load (MI355X_MICROARCH.md hand-off table, row 1). Counters only grow within a
+// launch (target = (s + 1)·C), payload buffers alternate by super-block parity (a workgroup writes
+// super-block s + 2's payload only after every workgroup has passed s + 1's second hand-off, i.e.
+// finished reading s's). Each genotype byte is read from HBM once per iteration: the super-
+// block's rows of the chunk land in LDS by DMA (wave 3, during the previous super-block's hand-
+// offs) and serve both the dots and the e update. Same chain as the literal BGLR loop, rounding
+// aside. Waits are bounded (~1 s: *info = −1, every workgroup leaves; the host falls back).
+constexpr int SBK = 512;               // markers per super-block
+constexpr int SBN = SBK / BK2;         // 128-marker sub-blocks per super-block
+constexpr int SB_PAIRS = SBN * (SBN - 1) / 2;
+constexpr int SB_KMAX = 64;            // individuals per chunk (at most)
+constexpr int SB_RMAX = 8;             // owned rows per workgroup (at most)
+
+__device__ __forceinline__ int sb_pair_index(int i, int m) { return i * (i - 1) / 2 + m; }  // i > m
+
+// Wsb[s][pair(i, m)] = X_{4s+i}ᵀ X_{4s+m} over the 128-marker sub-blocks i > m of super-block s
+// (128 x 128 row-major; rows/columns past p are zero): one 64x64 quadrant per workgroup, as
+// brr_gram_kernel. One-time setup.
+__global__ void __launch_bounds__(256) brr_gram_sb_kernel(const double* __restrict__ Xt, int64_t ldx, int64_t p,
+                                                          int64_t n, double* __restrict__ Wsb) {
+  __shared__ double TR[BB][BB + 1];
+  __shared__ double TC[BB][BB + 1];
+  const int quad = (int)(blockIdx.x & 3);
+  const int64_t sp = blockIdx.x >> 2;
+  const int64_t s = sp / SB_PAIRS;
+  const int pair = (int)(sp % SB_PAIRS);
+  int i = 1;
+  while ((i + 1) * i / 2 <= pair) i++;
+  const int m = pair - i * (i - 1) / 2;
+  const int64_t r0 = s * SBK + i * BK2 + (quad >> 1) * BB, c0 = s * SBK + m * BK2 + (quad & 1) * BB;
+  const int tid = threadIdx.x, a = tid >> 2, b0 = (tid & 3) * 16;
+  double acc[16];
+#pragma unroll
+  for (int u = 0; u < 16; u++) acc[u] = 0.0;
+  for (int64_t k0 = 0; k0 < n; k0 += BB) {
+    for (int e = tid; e < BB * BB; e += 256) {
+      const int r = e / BB, c = e % BB;
+      TR[r][c] = (r0 + r < p && k0 + c < n) ? Xt[(r0 + r) * ldx + k0 + c] : 0.0;
+      TC[r][c] = (c0 + r < p && k0 + c < n) ? Xt[(c0 + r) * ldx + k0 + c] : 0.0;
+    }
+    __syncthreads();
+    for (int k = 0; k < BB; k++) {
+      const double xa = TR[a][k];
+#pragma unroll
+      for (int u = 0; u < 16; u++) acc[u] += xa * TC[b0 + u][k];
+    }
+    __syncthreads();
+  }
+  double* out = Wsb + sp * BK2 * BK2 + ((quad >> 1) * BB + a) * BK2 + (quad & 1) * BB + b0;
+#pragma unroll
+  for (int u = 0; u < 16; u++) out[u] = acc[u];
+}
+
+typedef double sbd4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ double ld_sc1_d(const double* p) {
+  return __builtin_bit_cast(double, __hip_atomic_load(reinterpret_cast<const uint64_t*>(p), __ATOMIC_RELAXED,
+                                                      __HIP_MEMORY_SCOPE_AGENT));
+}
+
+// acc (this wave's 64x64 quadrant wm, wn of a 128x128 product) += A · B over K = 128 on the fp64
+// MFMA, the operands staged through LDS in four 32-deep chunks (As[k][r] = A[r][k]: a lane's MFMA
+// A operand is then one LDS row read, like B's). ldA(r, k) / ldB(k, c) fetch from global memory.
+// acc[m][q][r] = C[64 wm + 16 m + fr + 4 r][64 wn + 16 q + fc].
+constexpr int SBP = BK2 + 4;  // LDS pitch (doubles)
+template <typename LA, typename LB>
+__device__ __forceinline__ void sb_gemm128(LA ldA, LB ldB, double* As, double* Bs, sbd4 (&acc)[4][4], int tid, int wm,
+                                           int wn, int fr, int fc) {
+  // chunk k0's operands: thread t holds A[t >> 1][k0 + 16 (t & 1) + u] and B[k0 + (t >> 3)][16 (t & 7) + u]; the
+  // next chunk's are loaded into registers while this one's MFMAs run
+  double va[16], vb[16];
+  auto fetch = [&](int k0) {
+#pragma unroll
+    for (int u = 0; u < 16; u++) {
+      va[u] = ldA(tid >> 1, k0 + (tid & 1) * 16 + u);
+      vb[u] = ldB(k0 + (tid >> 3), (tid & 7) * 16 + u);
+    }
+  };
+  fetch(0);
+#pragma unroll 1
+  for (int k0 = 0; k0 < BK2; k0 += 32) {
+    __syncthreads();  // the previous chunk's fragment reads are done
+#pragma unroll
+    for (int u = 0; u < 16; u++) {
+      As[((tid & 1) * 16 + u) * SBP + (tid >> 1)] = va[u];
+      Bs[(tid >> 3) * SBP + (tid & 7) * 16 + u] = vb[u];
+    }
+    __syncthreads();
+    if (k0 + 32 < BK2) fetch(k0 + 32);
+#pragma unroll
+    for (int ks = 0; ks < 32; ks += 4) {
+      double a[4], b[4];
+#pragma unroll
+      for (int u = 0; u < 4; u++) {
+        a[u] = As[(ks + fr) * SBP + wm * 64 + u * 16 + fc];
+        b[u] = Bs[(ks + fr) * SBP + wn * 64 + u * 16 + fc];
+      }
+#pragma unroll
+      for (int mm = 0; mm < 4; mm++)
+#pragma unroll
+        for (int q = 0; q < 4; q++) acc[mm][q] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[mm], b[q], acc[mm][q], 0, 0, 0);
+    }
+  }
+}
+
+// M_S of every super-block (row-major SBK x SBK; blocks above the diagonal stay zero from the
+// setup memset): the inverse of the unit lower triangular I + D L over its four 128-marker sub-blocks
+// (D = diag(α), L = the strictly lower part of the super-block's Gram), from
+//   M_ii = [[M_A, 0], [O, M_B]]   (brr_prep_kernel's inverse of sub-block i) and
+//   M_ij = −M_ii D_i Σ_{m=j}^{i−1} W_im M_mj  (i > j),
+// by recursive doubling in four launches (each workgroup one 128x128 output block, ≤ 2 GEMMs; the
+// blocks a level reads were written by an earlier launch):
+//   level 0: X_{a+1,a} = D_{a+1} W_{a+1,a} M_aa (a = 0, 2), and the diagonal blocks into M_S;
+//   level 1: M_{a+1,a} = −M_{a+1,a+1} X_{a+1,a};
+//   level 2: X_ij = D_i Σ_{m=j}^{1} W_im M_mj (i = 2, 3; j = 0, 1);
+//   level 3: M_ij = −Σ_{m=2}^{i} M_im X_mj.
+// X lives in the scratch Xsc: 6 blocks per super-block, slot(i, j) = {10: 0, 32: 1, 20: 2, 21: 3,
+// 30: 4, 31: 5}.
+__device__ __forceinline__ int sb_xslot(int i, int j) {
+  return i == 1 ? 0 : i == 2 ? (j == 0 ? 2 : 3) : (j == 2 ? 1 : j == 0 ? 4 : 5);
+}
+__global__ void __launch_bounds__(256, 1) brr_sb_prep_kernel(int level, const double* __restrict__ Mb,
+                                                             const double* __restrict__ Wsb,
+                                                             const double* __restrict__ alpha, double* __restrict__ MS,
+                                                             double* __restrict__ Xsc) {
+  __shared__ double As[32 * SBP], Bs[32 * SBP];
+  const int ntask = level < 2 ? 2 : 4;
+  const int64_t s = blockIdx.x / ntask;
+  const int task = (int)(blockIdx.x % ntask);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1, fr = lane >> 4, fc = lane & 15;
+  double* Ms = MS + s * (int64_t)SBK * SBK;
+  double* X = Xsc + s * 6 * (int64_t)BK2 * BK2;
+  // element (r, c) of the 128-block inverse M_kk of 128-block k = 4s + i
+  auto mkk = [&](int i, int r, int c) -> double {
+    const double* base = Mb + (s * SBN + i) * 3 * BB * BB;
+    if (r < BB) return c < BB ? base[r * BB + c] : 0.0;
+    return c < BB ? base[BB * BB + (r - BB) * BB + c] : base[2 * BB * BB + (r - BB) * BB + (c - BB)];
+  };
+  auto Wb = [&](int i, int m) { return Wsb + (s * SB_PAIRS + sb_pair_index(i, m)) * (int64_t)BK2 * BK2; };
+  auto Mblk = [&](int i, int j) { return Ms + (int64_t)(i * BK2) * SBK + j * BK2; };
+  auto Xblk = [&](int i, int j) { return X + sb_xslot(i, j) * (int64_t)BK2 * BK2; };
+  // B operand M_mj (diagonal: from Mb; below: from M_S)
+  auto gemm_W_M = [&](int i, int m, int j, sbd4 (&acc)[4][4]) {
+    const double* W = Wb(i, m);
+    if (m == j) {
+      sb_gemm128([&](int r, int k) { return W[r * BK2 + k]; }, [&](int k, int c) { return mkk(m, k, c); }, As, Bs, acc,
+                 tid, wm, wn, fr, fc);
+    } else {
+      const double* B = Mblk(m, j);
+      sb_gemm128([&](int r, int k) { return W[r * BK2 + k]; }, [&](int k, int c) { return B[(int64_t)k * SBK + c]; }, As,
+                 Bs, acc, tid, wm, wn, fr, fc);
+    }
+  };
+  // A operand M_im (diagonal: from Mb; below: from M_S), B operand X_mj
+  auto gemm_M_X = [&](int i, int m, int j, sbd4 (&acc)[4][4]) {
+    const double* B = Xblk(m, j);
+    if (i == m) {
+      sb_gemm128([&](int r, int k) { return mkk(i, r, k); }, [&](int k, int c) { return B[k * BK2 + c]; }, As, Bs, acc,
+                 tid, wm, wn, fr, fc);
+    } else {
+      const double* A = Mblk(i, m);
+      sb_gemm128([&](int r, int k) { return A[(int64_t)r * SBK + k]; }, [&](int k, int c) { return B[k * BK2 + c]; }, As,
+                 Bs, acc, tid, wm, wn, fr, fc);
+    }
+  };
+  // epilogues: rows scaled by α of sub-block i (into X), or negated (into M_S)
+  auto store_scaled = [&](const sbd4 (&acc)[4][4], double* out, int64_t ld, int i) {
+    const double* al = alpha + (s * SBN + i) * BK2;
+#pragma unroll
+    for (int mm = 0; mm < 4; mm++)
+#pragma unroll
+      for (int q = 0; q < 4; q++)
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+          const int row = wm * 64 + mm * 16 + fr + 4 * r;
+          out[(int64_t)row * ld + wn * 64 + q * 16 + fc] = acc[mm][q][r] * al[row];
+        }
+  };
+  auto store_neg = [&](const sbd4 (&acc)[4][4], double* out, int64_t ld) {
+#pragma unroll
+    for (int mm = 0; mm < 4; mm++)
+#pragma unroll
+      for (int q = 0; q < 4; q++)
+#pragma unroll
+        for (int r = 0; r < 4; r++)
+          out[(int64_t)(wm * 64 + mm * 16 + fr + 4 * r) * ld + wn * 64 + q * 16 + fc] = -acc[mm][q][r];
+  };
+  sbd4 acc[4][4];
+#pragma unroll
+  for (int mm = 0; mm < 4; mm++)
+#pragma unroll
+    for (int q = 0; q < 4; q++) acc[mm][q] = (sbd4){0.0, 0.0, 0.0, 0.0};
+  if (level == 0) {
+    const int a = 2 * task;
+    for (int d = a; d < a + 2; d++)
+      for (int e = tid; e < BK2 * BK2; e += 256) {
+        const int r = e / BK2, c = e % BK2;
+        Mblk(d, d)[(int64_t)r * SBK + c] = mkk(d, r, c);
+      }
+    gemm_W_M(a + 1, a, a, acc);
+    store_scaled(acc, Xblk(a + 1, a), BK2, a + 1);
+  } else if (level == 1) {
+    const int a = 2 * task;
+    gemm_M_X(a + 1, a + 1, a, acc);
+    store_neg(acc, Mblk(a + 1, a), SBK);
+  } else if (level == 2) {
+    const int i = 2 + task / 2, j = task % 2;
+    for (int m = j; m <= 1; m++) gemm_W_M(i, m, j, acc);
+    store_scaled(acc, Xblk(i, j), BK2, i);
+  } else {
+    const int i = 2 + task / 2, j = task % 2;
+    for (int m = 2; m <= i; m++) gemm_M_X(i, m, j, acc);
+    store_neg(acc, Mblk(i, j), SBK);
+  }
+}
+
+// Hand-off granules of the super-block sweep: 16 bytes {v, bits(v) XOR key(tag)} written by one
+// write-through (sc1) store; a reader polls the granule with sc1 loads until the second half
+// matches the first for the tag it expects (tag = iteration · nsb + super-block: never reused), so
+// no flag, counter or drain is needed, and a torn or stale read can only fail the check and be
+// read again.
+typedef unsigned int sbu4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint64_t sb_key(uint64_t tag) { return bmix64(tag * 0x9E3779B97F4A7C15ull + 0x5DEECE66Dull); }
+__device__ __forceinline__ void sb_put(__amdgpu_buffer_rsrc_t r, uint32_t off, double v, uint64_t key) {
+  const uint64_t a = __builtin_bit_cast(uint64_t, v), b = a ^ key;
+  const sbu4 w = {(unsigned)a, (unsigned)(a >> 32), (unsigned)b, (unsigned)(b >> 32)};
+  __builtin_amdgcn_raw_buffer_store_b128(w, r, (int)off, 0, 16);  // sc1
+}
+// A poll's load is inline asm (volatile: the compiler hoisted the builtin's read-only load out of
+// the spin and polled a register); the caller waits with sb_landed() before using the values.
+__device__ __forceinline__ sbu4 sb_get(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  sbu4 v;
+  asm volatile("buffer_load_dwordx4 %0, %1, %2, 0 offen sc1" : "=v"(v) : "v"(off), "s"(r) : "memory");
+  return v;
+}
+__device__ __forceinline__ void sb_landed() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+__device__ __forceinline__ bool sb_ok(const sbu4& w, uint64_t key, double& v) {
+  const uint64_t a = (uint64_t)w.x | ((uint64_t)w.y << 32), b = (uint64_t)w.z | ((uint64_t)w.w << 32);
+  v = __builtin_bit_cast(double, a);
+  return (a ^ key) == b;
+}
+// poll bookkeeping of one wave: true while some lane still waits; gives up (*info = −1) after
+// ~1 s or when another workgroup gave up
+__device__ __forceinline__ bool sb_spin(bool lane_done, int64_t& spin, int32_t* info, bool& failed) {
+  if (__builtin_amdgcn_ballot_w64(!lane_done) == 0) return false;
+  if ((++spin & 255) == 255) {
+    if (__hip_atomic_load(info, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < 0 || spin > ((int64_t)1 << 22)) {
+      __hip_atomic_store(info, -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      failed = true;
+      return false;
+    }
+  }
+  __builtin_amdgcn_s_sleep(1);
+  return true;
+}
+
+// K individuals per chunk workgroup (a multiple of 16, <= SB_KMAX); R owned rows (even, <= SB_RMAX).
+// kTrace (timing tool, GBM_BRR_TRACE=1): workgroups 0 and C − 1 record 8 timestamps per super-block.
+template <bool kTrace>
+__global__ void __launch_bounds__(256) brr_sweep_sb_kernel(const uint8_t* __restrict__ D, int64_t ldx, int64_t n,
+                                                           int64_t p, double xs, const double* __restrict__ MS,
+                                                           int64_t nsb, int K, int R, double* __restrict__ Pb,
+                                                           double* __restrict__ Rt, double* __restrict__ Dl,
+                                                           int32_t* __restrict__ info, double* __restrict__ b,
+                                                           double* __restrict__ bbar, const double* __restrict__ alpha,
+                                                           const double* __restrict__ gamma, double* __restrict__ e,
+                                                           const BrrState* __restrict__ st, int64_t* __restrict__ trace) {
+  __shared__ __attribute__((aligned(16))) uint8_t Drow[2][SBK * SB_KMAX];  // a super-block's rows of the chunk
+  __shared__ __attribute__((aligned(16))) double es[SB_KMAX];
+  __shared__ __attribute__((aligned(16))) double rt[SBK];
+  __shared__ __attribute__((aligned(16))) double dl[SBK];
+  __shared__ double red[4][SB_RMAX];
+  __shared__ double eacc[4096 + SB_KMAX];  // e update partial sums [individual][slice]: K x (nsl_used | 1)
+  __shared__ double eq[4][SB_KMAX];
+  __shared__ int s_fail;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int C = (int)gridDim.x, c = (int)blockIdx.x;
+  const int64_t i0 = (int64_t)c * K;
+  const int r0 = c * R;  // owned rows [r0, r0 + R) of every super-block (those < SBK)
+  const int nown = r0 >= SBK ? 0 : (SBK - r0 < R ? SBK - r0 : R);
+  const bool tr_on = kTrace && (c == 0 || c == C - 1) && threadIdx.x == 0;
+  int64_t* trw = kTrace ? trace + (c == 0 ? 0 : 1) * nsb * 12 : nullptr;
+  auto mark = [&](int64_t s, int k) {
+    if (tr_on) trw[s * 12 + k] = (int64_t)__builtin_amdgcn_s_memrealtime();
+  };
+  const int it_odd = (int)(st->it & 1);
+  const bool accum = brr_accumulate(st);
+  const double kk = (double)(st->nsum + 1);
+  const uint64_t tag0 = (st->epoch << 40) + (uint64_t)st->it * (uint64_t)nsb;
+  const __amdgpu_buffer_rsrc_t rP = brr_rsrc(Pb, (int64_t)2 * C * SBK * 16);
+  const __amdgpu_buffer_rsrc_t rR = brr_rsrc(Rt, (int64_t)2 * SBK * 16);
+  const __amdgpu_buffer_rsrc_t rD = brr_rsrc(Dl, (int64_t)2 * SBK * 16);
+  if (tid == 0) s_fail = 0;
+  // wave 3: the chunk's rows of super-block sb into Drow[sb & 1] (16-B pieces; row j's K bytes at
+  // j * K; rows past p re-read row p − 1, never used: δ = 0 there)
+  auto dma_rows = [&](int64_t sb) {
+    const int pieces = SBK * (K / 16);
+    uint8_t* dst = Drow[sb & 1];
+    for (int q0 = 0; q0 < pieces; q0 += 64) {
+      const int q = q0 + lane;
+      const int row = q / (K / 16), part = q % (K / 16);
+      int64_t jr = sb * SBK + row;
+      jr = jr < p ? jr : p - 1;
+      const uint8_t* src = D + jr * ldx + i0 + part * 16;
+      const unsigned m0v = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(dst + q0 * 16));
+      asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off" : : "s"(m0v), "v"(src) : "memory");
+    }
+  };
+  if (tid < SB_KMAX) es[tid] = (tid < K && i0 + tid < n) ? e[i0 + tid] : 0.0;
+  if (wave == 3) {
+    dma_rows(0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+  // e update: thread t -> 16-individual piece t % nch of slice t / nch (rows [sl·rps, (sl+1)·rps))
+  const int nch = K / 16, nsl = 256 / nch, rps = (SBK + nsl - 1) / nsl;
+  const int ech = tid % nch, esl = tid / nch;
+  const int nsl_used = (SBK + rps - 1) / rps;
+  const int slp = nsl_used | 1;  // odd pitch of eacc's slice rows (bank-conflict-free writes and reads)
+  for (int64_t s = 0; s < nsb; s++) {
+    const int par = (int)(s & 1);
+    const uint8_t* Dr = Drow[par];
+    const int64_t j0 = s * SBK;
+    const uint64_t key = sb_key(tag0 + (uint64_t)s);
+    mark(s, 0);
+    // (1) partial dots of the super-block's 512 markers over this chunk: thread t -> rows 2t, 2t + 1,
+    // published as granules P[par][c][row]
+    {
+      double a0 = 0.0, a1 = 0.0, c0 = 0.0, c1 = 0.0;
+      const uint8_t* ra = Dr + (2 * tid) * K;
+      const uint8_t* rb = ra + K;
+      for (int u = 0; u < K; u += 16) {
+        const uint4 va = *reinterpret_cast<const uint4*>(ra + u);
+        const uint4 vb = *reinterpret_cast<const uint4*>(rb + u);
+        const uint32_t wa[4] = {va.x, va.y, va.z, va.w};
+        const uint32_t wb[4] = {vb.x, vb.y, vb.z, vb.w};
+#pragma unroll
+        for (int q = 0; q < 4; q++)
+#pragma unroll
+          for (int bb = 0; bb < 4; bb += 2) {
+            const double2 e2 = *reinterpret_cast<const double2*>(es + u + 4 * q + bb);
+            a0 = fma((double)((wa[q] >> (8 * bb)) & 0xFFu), e2.x, a0);
+            a1 = fma((double)((wa[q] >> (8 * bb + 8)) & 0xFFu), e2.y, a1);
+            c0 = fma((double)((wb[q] >> (8 * bb)) & 0xFFu), e2.x, c0);
+            c1 = fma((double)((wb[q] >> (8 * bb + 8)) & 0xFFu), e2.y, c1);
+          }
+      }
+      const uint32_t off = (uint32_t)((((int64_t)par * C + c) * SBK + 2 * tid) * 16);
+      sb_put(rP, off, a0 * xs + a1 * xs, key);
+      sb_put(rP, off + 16, c0 * xs + c1 * xs, key);
+    }
+    // wave 3: the next super-block's rows (land during the hand-offs; Drow[par ^ 1] was last read
+    // by the previous super-block's e update, before the barrier that ended it)
+    if (wave == 3 && s + 1 < nsb) dma_rows(s + 1);
+    mark(s, 1);
+    // this super-block's operands of the owned rows (plain loads: written before this launch)
+    double mrow[2][8];
+    double alv = 0.0, gav = 0.0, bo = 0.0, bbo = 0.0;
+    const int wrow0 = wave, wrow1 = wave + 4;  // owned-row indices of this wave's δ dots (< nown)
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+      const int w = h ? wrow1 : wrow0;
+      const int jr = w < nown ? r0 + w : 0;
+      const double* mr = MS + (s * SBK + jr) * (int64_t)SBK;
+#pragma unroll
+      for (int t = 0; t < 8; t++) mrow[h][t] = (w < nown) ? mr[lane + 64 * t] : 0.0;
+    }
+    if (wave == 0 && lane < nown) {
+      const int64_t jm = j0 + r0 + lane;
+      alv = alpha[jm];
+      gav = gamma[jm];
+      const int64_t jc = jm < p ? jm : 0;
+      const double b0v = b[jc], b1v = b[p + jc];
+      bbo = bbar[jc];
+      bo = it_odd ? b1v : b0v;
+    }
+    // (2) d⁰ of the owned rows: waves 0-2, lane -> chunks lane + 64 w and + 192, summed in that
+    // order, xor-tree across the wave, then the waves in order
+    if (wave < 3) {
+      double v[SB_RMAX];
+#pragma unroll
+      for (int r = 0; r < SB_RMAX; r++) v[r] = 0.0;
+      if (nown > 0) {
+#pragma unroll
+        for (int h = 0; h < 2; h++) {
+          const int cc = lane + 64 * wave + 192 * h;
+          const bool has = cc < C;
+          const uint32_t base = (uint32_t)((((int64_t)par * C + (has ? cc : 0)) * SBK + r0) * 16);
+          bool failed = false;
+          int64_t spin = 0;
+          bool done = !has;
+          double x[SB_RMAX];
+#pragma unroll
+          for (int r = 0; r < SB_RMAX; r++) x[r] = 0.0;
+          do {
+            if (!done) {
+              sbu4 w[SB_RMAX];
+#pragma unroll
+              for (int r = 0; r < SB_RMAX; r++)
+                if (r < R) w[r] = sb_get(rP, base + r * 16);
+              sb_landed();
+              bool all = true;
+#pragma unroll
+              for (int r = 0; r < SB_RMAX; r++)
+                if (r < R && r < nown) all = sb_ok(w[r], key, x[r]) && all;
+              done = all;
+            }
+          } while (sb_spin(done, spin, info, failed));
+          if (failed) s_fail = 1;
+#pragma unroll
+          for (int r = 0; r < SB_RMAX; r++) v[r] += (has && r < nown) ? x[r] : 0.0;
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < SB_RMAX; r++) {
+        double x = v[r];
+        x += __shfl_xor(x, 32);
+        x += __shfl_xor(x, 16);
+        x += __shfl_xor(x, 8);
+        x += __shfl_xor(x, 4);
+        x += __shfl_xor(x, 2);
+        x += __shfl_xor(x, 1);
+        if (lane == 0) red[wave][r] = x;
+      }
+    }
+    lds_barrier();
+    mark(s, 2);
+    if (s_fail) return;
+    if (wave == 0 && lane < nown) {
+      const double d0 = (red[0][lane] + red[1][lane]) + red[2][lane];
+      sb_put(rR, (uint32_t)(((int64_t)par * SBK + r0 + lane) * 16), fma(d0, -alv, gav), key);
+    }
+    mark(s, 3);
+    // (3) all of r̃ (waves 0-1, 4 granules per lane), then δ of the owned rows (wave w: rows w, w + 4)
+    if (wave < 2) {
+      bool failed = false, done = false;
+      int64_t spin = 0;
+      double x[4];
+      do {
+        sbu4 w[4];
+#pragma unroll
+        for (int q = 0; q < 4; q++) w[q] = sb_get(rR, (uint32_t)(((int64_t)par * SBK + tid * 4 + q) * 16));
+        sb_landed();
+        bool all = true;
+#pragma unroll
+        for (int q = 0; q < 4; q++) all = sb_ok(w[q], key, x[q]) && all;
+        done = all;
+      } while (sb_spin(done, spin, info, failed));
+      if (failed) s_fail = 1;
+#pragma unroll
+      for (int q = 0; q < 4; q++) rt[tid * 4 + q] = x[q];
+    }
+    lds_barrier();
+    mark(s, 4);
+    if (s_fail) return;
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+      const int w = h ? wrow1 : wrow0;
+      double a = 0.0;
+#pragma unroll
+      for (int t = 0; t < 8; t++) a = fma(mrow[h][t], rt[lane + 64 * t], a);
+      a += __shfl_xor(a, 32);
+      a += __shfl_xor(a, 16);
+      a += __shfl_xor(a, 8);
+      a += __shfl_xor(a, 4);
+      a += __shfl_xor(a, 2);
+      a += __shfl_xor(a, 1);
+      if (lane == 0 && w < nown) red[3][w] = a;
+    }
+    lds_barrier();
+    if (wave == 0 && lane < nown) {
+      const double dlt = red[3][lane];
+      const int64_t jm = j0 + r0 + lane;
+      if (jm < p) {
+        const double bn = bo - dlt;
+        b[(it_odd ^ 1) * p + jm] = bn;
+        if (accum) bbar[jm] = bbo * ((kk - 1.0) / kk) + bn / kk;
+      }
+      sb_put(rD, (uint32_t)(((int64_t)par * SBK + r0 + lane) * 16), dlt, key);
+    }
+    mark(s, 5);
+    // (4) all of δ, then e += X_S δ over the chunk's individuals (rows from Drow[par]): thread ->
+    // one 16-individual piece of a slice of rows, partial sums by slice in LDS, summed in slice order
+    if (wave < 2) {
+      bool failed = false, done = false;
+      int64_t spin = 0;
+      double x[4];
+      do {
+        sbu4 w[4];
+#pragma unroll
+        for (int q = 0; q < 4; q++) w[q] = sb_get(rD, (uint32_t)(((int64_t)par * SBK + tid * 4 + q) * 16));
+        sb_landed();
+        bool all = true;
+#pragma unroll
+        for (int q = 0; q < 4; q++) all = sb_ok(w[q], key, x[q]) && all;
+        done = all;
+      } while (sb_spin(done, spin, info, failed));
+      if (failed) s_fail = 1;
+#pragma unroll
+      for (int q = 0; q < 4; q++) dl[tid * 4 + q] = x[q];
+    }
+    lds_barrier();
+    mark(s, 6);
+    if (s_fail) return;
+    if (esl < nsl_used) {
+      double acc[16];
+#pragma unroll
+      for (int u = 0; u < 16; u++) acc[u] = 0.0;
+      const int jb = esl * rps, je = (jb + rps < SBK) ? jb + rps : SBK;
+      for (int jj = jb; jj < je; jj++) {
+        const uint4 w4 = *reinterpret_cast<const uint4*>(Dr + jj * K + ech * 16);
+        const double d = dl[jj];
+        const uint32_t wd[4] = {w4.x, w4.y, w4.z, w4.w};
+#pragma unroll
+        for (int q = 0; q < 4; q++)
+#pragma unroll
+          for (int bb = 0; bb < 4; bb++) acc[4 * q + bb] = fma((double)((wd[q] >> (8 * bb)) & 0xFFu), d, acc[4 * q + bb]);
+      }
+#pragma unroll
+      for (int u = 0; u < 16; u++) eacc[(ech * 16 + u) * slp + esl] = acc[u];  // [individual][slice]
+    }
+    mark(s, 8);
+    // the next super-block's rows have landed (wave 3's DMA) before the barrier; an LDS-only barrier
+    // otherwise (__syncthreads would also wait for this super-block's write-through stores)
+    if (wave == 3) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    lds_barrier();
+    mark(s, 9);
+    if (tid < 4 * K) {
+      const int ind = tid % K, q = tid / K;  // four partial sums per individual, slices ≡ q (mod 4)
+      double u = 0.0;
+      for (int t = q; t < nsl_used; t += 4) u += eacc[ind * slp + t];
+      eq[q][ind] = u;
+    }
+    lds_barrier();
+    mark(s, 10);
+    if (tid < K && i0 + tid < n) es[tid] += (((eq[0][tid] + eq[1][tid]) + eq[2][tid]) + eq[3][tid]) * xs;
+    lds_barrier();
+    mark(s, 7);
+  }
+  if (tid < K && i0 + tid < n) e[i0 + tid] = es[tid];
+}
+
 // σ²_b, σ²_e draws, running means of μ and the variances, next iteration (one workgroup)
 __global__ void __launch_bounds__(1024) brr_var_kernel(const double* __restrict__ b, int64_t p,
                                                        const double* __restrict__ e, int64_t n,
@@ -1071,6 +1635,7 @@ struct BrrCtx {
   int dev = 0;
   Stream stream;
   DevBuf Xt, colmean, x2, e, b, bbar, r, stm, D, badm, W, Mb, alph, gamm, flg, Dt, pb, part, pout;
+  DevBuf Wsb, MS, Ssc, Pb, Rt, Dl, sbcnt;  // the super-block sweep
   hipGraphExec_t exec = nullptr;
   hipGraph_t graph = nullptr;
   std::vector<int64_t> key;  // what the captured graph was built for
@@ -1156,6 +1721,30 @@ namespace gbm {
 void brr_release_cache() { brr_pool().clear(); }
 }  // namespace gbm
 
+// Timing tool (GBM_BRR_TRACE=1): per super-block timestamps of workgroups 0 and C − 1 of the last
+// super-block sweep (2 x nsb x 8 int64, s_memrealtime at 100 MHz), read by gbm_debug_brr_trace.
+static int64_t* g_brr_trace = nullptr;
+static int64_t g_brr_trace_n = 0;
+
+extern "C" int64_t gbm_debug_brr_trace(int64_t* host, int64_t cap) {
+  if (!g_brr_trace || !host) return 0;
+  const int64_t n = g_brr_trace_n < cap ? g_brr_trace_n : cap;
+  if (hipDeviceSynchronize() != hipSuccess ||
+      hipMemcpy(host, g_brr_trace, (size_t)n * 8, hipMemcpyDeviceToHost) != hipSuccess)
+    return -1;
+  return n;
+}
+
+// Which path the last completed fit took (0 per-launch, 1 128-block sweep, 2 super-block sweep) and
+// how many fits fell back to the per-launch path after a sweep hand-off timed out (tests).
+static std::atomic<int> g_brr_last_path{-1};
+static std::atomic<int64_t> g_brr_fallbacks{0};
+extern "C" int gbm_debug_brr_stats(int* last_path, int64_t* fallbacks) {
+  if (last_path) *last_path = g_brr_last_path.load();
+  if (fallbacks) *fallbacks = g_brr_fallbacks.load();
+  return GBM_OK;
+}
+
 // One BRR fit on a leased context; sweep_mode: -1 = per GBM_BRR_SWEEP (default on), 0 = off.
 static int brr_fit_impl(const double* X, int64_t n, int64_t p, int64_t ldx, const double* y, int64_t n_iter,
                         int64_t n_burnin, int64_t thin, double r2, double df0, uint64_t seed, int dev,
@@ -1193,7 +1782,7 @@ static int brr_fit_impl(const double* X, int64_t n, int64_t p, int64_t ldx, cons
   {
     const char* ev = std::getenv("GBM_BRR_I8");
     if (!(ev && ev[0] == '0')) {
-      GBM_TRY(ensure(cx.D, dev, p * npad));
+      GBM_TRY(ensure(cx.D, dev, p * npad + 4096));  // + slack: the super-block sweep's last chunk reads past n
       GBM_TRY(ensure(cx.badm, dev, sizeof(int)));
       const double scales[3] = {2.0, 4.0, 1.0};
       for (double sc : scales) {
@@ -1210,9 +1799,32 @@ static int brr_fit_impl(const double* X, int64_t n, int64_t p, int64_t ldx, cons
       }
     }
   }
+  // byte storage on (up to) every CU: the super-block sweep (brr_sweep_sb_kernel) when its chunk
+  // workgroups (K <= 64 individuals each) can all be resident, one per CU, and own <= 8 rows of a
+  // super-block each (1 024 <= n <= 64 CUs); GBM_BRR_SB=0 (read per call) keeps the 128-block sweep
+  int cus = 0;
+  GBM_HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+  bool sbmode = false;
+  int sbK = 0, sbC = 0, sbR = 0;
+  if (xs > 0.0 && sweep_mode != 0) {
+    const char* ev = std::getenv("GBM_BRR_SB");
+    const char* ev2 = std::getenv("GBM_BRR_SWEEP");
+    int per_cu = 0;
+    GBM_HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, brr_sweep_sb_kernel<false>, 256, 0));
+    sbK = (int)round_up(std::max<int64_t>(16, (n + cus - 1) / cus), 16);
+    if (const char* ek = std::getenv("GBM_BRR_SB_K"))  // (timing experiments) a larger chunk
+      sbK = std::max<int>(sbK, (int)round_up(std::max<int64_t>(16, atoll(ek)), 16));
+    sbC = (int)((n + sbK - 1) / sbK);
+    sbR = (int)round_up((SBK + sbC - 1) / sbC, 2);
+    sbmode = !(ev && ev[0] == '0') && !(ev2 && ev2[0] == '0') && per_cu >= 1 && sbK <= SB_KMAX && sbC <= cus &&
+             sbR <= SB_RMAX;
+  }
   // markers per launch: 128 with byte storage (two halves), 64 with fp64 storage; the Gram blocks
-  // each launch needs (brr_gram_kernel), and the block-transposed bytes of the byte path
-  const int64_t bk = xs > 0.0 ? BK2 : BB, nblk = (p + bk - 1) / bk;
+  // each launch needs (brr_gram_kernel), and the block-transposed bytes of the byte path. The
+  // super-block sweep rounds the 128-blocks up to whole super-blocks (α = γ = 0 past p).
+  const int64_t bk = xs > 0.0 ? BK2 : BB;
+  const int64_t nsb = (p + SBK - 1) / SBK;
+  const int64_t nblk = sbmode ? nsb * SBN : (p + bk - 1) / bk;
   const int nw = xs > 0.0 ? 3 : 1;
   GBM_TRY(ensure(cx.W, dev, nblk * nw * BB * BB * 8));
   // per-iteration block inverses (same shape as W) and step constants α, γ (padded to whole launches)
@@ -1224,11 +1836,34 @@ static int brr_fit_impl(const double* X, int64_t n, int64_t p, int64_t ldx, cons
   // byte storage: one persistent sweep launch per iteration when the C chunk workgroups can all be
   // resident at once (the occupancy query times the CU count; one sweep per device at a time, see
   // BrrPool::sweep_lock); GBM_BRR_SWEEP=0 keeps one launch per block (read per call)
-  bool sweep = false;
-  if (xs > 0.0) {
-    int cus = 0, per_cu = 0;
+  bool sweep = sbmode;
+  if (sbmode) {
+    GBM_TRY(ensure(cx.Wsb, dev, nsb * SB_PAIRS * BK2 * BK2 * 8));
+    GBM_TRY(ensure(cx.MS, dev, nsb * SBK * SBK * 8));
+    GBM_TRY(ensure(cx.Ssc, dev, nsb * 6 * BK2 * BK2 * 8));
+    GBM_TRY(ensure(cx.Pb, dev, (int64_t)2 * sbC * SBK * 16));  // 16-B hand-off granules
+    GBM_TRY(ensure(cx.Rt, dev, 2 * SBK * 16));
+    GBM_TRY(ensure(cx.Dl, dev, 2 * SBK * 16));
+    GBM_TRY(ensure(cx.sbcnt, dev, 32 * sizeof(int32_t)));
+    GBM_HIP_TRY(hipMemsetAsync(cx.MS.p, 0, (size_t)(nsb * SBK * SBK * 8), s));  // blocks above the diagonal
+    GBM_HIP_TRY(hipMemsetAsync(cx.sbcnt.p, 0, 32 * sizeof(int32_t), s));
+    GBM_HIP_TRY(hipMemsetAsync(cx.alph.p, 0, (size_t)(nblk * bk * 8), s));
+    GBM_HIP_TRY(hipMemsetAsync(cx.gamm.p, 0, (size_t)(nblk * bk * 8), s));
+    brr_gram_sb_kernel<<<(unsigned)(nsb * SB_PAIRS * 4), 256, 0, s>>>((const double*)cx.Xt.p, npad, p, n, (double*)cx.Wsb.p);
+    GBM_LAUNCH_CHECK();
+    if (std::getenv("GBM_BRR_TRACE")) {
+      if (g_brr_trace) (void)hipFree(g_brr_trace);
+      g_brr_trace = nullptr;
+      GBM_HIP_TRY(hipMalloc((void**)&g_brr_trace, (size_t)(2 * nsb * 12 * 8)));
+      g_brr_trace_n = 2 * nsb * 12;
+    } else if (g_brr_trace) {
+      (void)hipFree(g_brr_trace);
+      g_brr_trace = nullptr;
+    }
+  }
+  if (xs > 0.0 && !sbmode) {
+    int per_cu = 0;
     const char* ev = std::getenv("GBM_BRR_SWEEP");
-    GBM_HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
     GBM_HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, brr_sweep128_kernel, 256, 0));
     sweep = sweep_mode != 0 && !(ev && ev[0] == '0') && per_cu >= 1 && C64 <= (int64_t)cus &&
             (int64_t)2 * C64 * BK2 * 8 < 0x7fffffff;
@@ -1269,6 +1904,8 @@ static int brr_fit_impl(const double* X, int64_t n, int64_t p, int64_t ldx, cons
   st0.burnin = n_burnin;
   st0.thin = thin;
   st0.seed = seed;
+  static std::atomic<uint64_t> fit_epoch{1};
+  st0.epoch = fit_epoch.fetch_add(1, std::memory_order_relaxed);
   std::vector<double> e0(npad, 0.0);
   for (int64_t i = 0; i < n; i++) e0[i] = y[i] - ym;
   GBM_HIP_TRY(hipMemcpyAsync(cx.e.p, e0.data(), npad * 8, hipMemcpyHostToDevice, s));
@@ -1286,6 +1923,25 @@ static int brr_fit_impl(const double* X, int64_t n, int64_t p, int64_t ldx, cons
                                               (const double*)cx.b.p, stp, (double*)cx.Mb.p, (double*)cx.alph.p,
                                               (double*)cx.gamm.p);
     brr_mu_kernel<<<1, 1024, 0, s>>>((double*)cx.e.p, n, stp);
+    if (sbmode) {
+      for (int level = 0; level < 4; level++)
+        brr_sb_prep_kernel<<<(unsigned)(nsb * (level < 2 ? 2 : 4)), 256, 0, s>>>(
+            level, (const double*)cx.Mb.p, (const double*)cx.Wsb.p, (const double*)cx.alph.p, (double*)cx.MS.p,
+            (double*)cx.Ssc.p);
+      int32_t* cn = (int32_t*)cx.sbcnt.p + 24;  // the error cell (zeroed at setup)
+      if (g_brr_trace)
+        brr_sweep_sb_kernel<true><<<(unsigned)sbC, 256, 0, s>>>(
+            (const uint8_t*)cx.D.p, npad, n, p, xs, (const double*)cx.MS.p, nsb, sbK, sbR, (double*)cx.Pb.p,
+            (double*)cx.Rt.p, (double*)cx.Dl.p, cn, (double*)cx.b.p, (double*)cx.bbar.p, (const double*)cx.alph.p,
+            (const double*)cx.gamm.p, (double*)cx.e.p, stp, g_brr_trace);
+      else
+        brr_sweep_sb_kernel<false><<<(unsigned)sbC, 256, 0, s>>>(
+            (const uint8_t*)cx.D.p, npad, n, p, xs, (const double*)cx.MS.p, nsb, sbK, sbR, (double*)cx.Pb.p,
+            (double*)cx.Rt.p, (double*)cx.Dl.p, cn, (double*)cx.b.p, (double*)cx.bbar.p, (const double*)cx.alph.p,
+            (const double*)cx.gamm.p, (double*)cx.e.p, stp, nullptr);
+      brr_var_kernel<<<1, 1024, 0, s>>>((const double*)cx.b.p, p, (const double*)cx.e.p, n, stp);
+      return hipGetLastError() == hipSuccess ? GBM_OK : fail(GBM_E_HIP, "gbm_brr_fit: launch failed");
+    }
     if (sweep) {
       int32_t* fl = (int32_t*)cx.flg.p;
       if (hipMemsetAsync(fl, 0, C * sizeof(int32_t), s) != hipSuccess) return fail(GBM_E_HIP, "gbm_brr_fit: memset failed");
@@ -1324,7 +1980,10 @@ static int brr_fit_impl(const double* X, int64_t n, int64_t p, int64_t ldx, cons
                                     (int64_t)(uintptr_t)cx.flg.p, (int64_t)(uintptr_t)cx.e.p, (int64_t)(uintptr_t)cx.b.p,
                                     (int64_t)(uintptr_t)cx.bbar.p, (int64_t)(uintptr_t)cx.alph.p,
                                     (int64_t)(uintptr_t)cx.gamm.p, (int64_t)(uintptr_t)cx.x2.p,
-                                    (int64_t)(uintptr_t)cx.stm.p};
+                                    (int64_t)(uintptr_t)cx.stm.p, sbmode ? 1 : 0, sbK, sbC, sbR,
+                                    (int64_t)(uintptr_t)cx.MS.p, (int64_t)(uintptr_t)cx.Wsb.p, (int64_t)(uintptr_t)cx.Ssc.p,
+                                    (int64_t)(uintptr_t)cx.Pb.p, (int64_t)(uintptr_t)cx.Rt.p, (int64_t)(uintptr_t)cx.Dl.p,
+                                    (int64_t)(uintptr_t)cx.sbcnt.p, (int64_t)(uintptr_t)g_brr_trace};
   int rc = GBM_OK;
   if (cx.key != key) {
     cx.drop_graph();
@@ -1355,13 +2014,15 @@ static int brr_fit_impl(const double* X, int64_t n, int64_t p, int64_t ldx, cons
   if (rc != GBM_OK) return rc;
   if (sweep) {
     int32_t inf = 0;
-    GBM_HIP_TRY(hipMemcpyAsync(&inf, (int32_t*)cx.flg.p + C, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+    GBM_HIP_TRY(hipMemcpyAsync(&inf, sbmode ? (int32_t*)cx.sbcnt.p + 24 : (int32_t*)cx.flg.p + C, sizeof(int32_t),
+                               hipMemcpyDeviceToHost, s));
     GBM_HIP_TRY(hipStreamSynchronize(s));
     if (inf < 0) {
       *sweep_timeout = true;
       return fail(GBM_E_HIP, "gbm_brr_fit: a sweep hand-off between workgroups timed out");
     }
   }
+  g_brr_last_path.store(sbmode ? 2 : sweep ? 1 : 0);
   BrrState fin{};
   GBM_HIP_TRY(hipMemcpyAsync(&fin, cx.stm.p, sizeof(BrrState), hipMemcpyDeviceToHost, s));
   GBM_HIP_TRY(hipMemcpyAsync(b_hat_out + 1, cx.bbar.p, p * 8, hipMemcpyDeviceToHost, s));
@@ -1405,8 +2066,10 @@ extern "C" int gbm_brr_fit(const double* X, int64_t n, int64_t p, int64_t ldx, c
   // a sweep whose workgroups could not all be resident (another process or library filling the
   // device) times out loudly on the device; the fit is then run again, from the start, on the
   // per-launch path (same chain; the two paths agree to rounding)
-  if (rc != GBM_OK && timeout)
+  if (rc != GBM_OK && timeout) {
+    g_brr_fallbacks.fetch_add(1);
     rc = brr_fit_impl(X, n, p, ldx, y, n_iter, n_burnin, thin, r2, df0, seed, devs[0], 0, b_hat_out, y_pred_out,
                       var_out, &timeout);
+  }
   return rc;
 }

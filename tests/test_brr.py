@@ -165,3 +165,39 @@ def test_gpu_brr_pooled_no_allocation_after_warmup_and_threads(monkeypatch, swee
     for a, b in zip(out, serial):
         for u, v in zip(a, b):
             assert np.array_equal(u, v)
+
+
+def brr_path():
+    import ctypes
+    lib = gbm.load_library()
+    path, fb = ctypes.c_int(-1), ctypes.c_int64(0)
+    lib.gbm_debug_brr_stats(ctypes.byref(path), ctypes.byref(fb))
+    return path.value, fb.value
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,p,K", [(1100, 300, None), (12000, 1300, None), (5000, 777, "64"), (3000, 1025, "32")])
+def test_gpu_brr_super_block_sweep_runs_and_matches(monkeypatch, n, p, K):
+    """The super-block sweep (brr_sweep_sb_kernel: 512-marker super-blocks, chunks of K individuals
+    on up to every CU, three granule hand-offs per super-block) really runs (no fall-back to the
+    per-launch path) and agrees with the 128-block sweep (GBM_BRR_SB=0), the per-launch path and
+    the oracle's literal loop; ragged p (p mod 512 = 300, 276, 265, 1), several chunk sizes."""
+    if K:
+        monkeypatch.setenv("GBM_BRR_SB_K", K)
+    X = oracle.synth_genotypes(n + p, n, p)
+    y = oracle.synth_phenotypes(X, 17)[:, 0]
+    _, fb0 = brr_path()
+    sb = gbm.brr_arrays(X, y, n_iter=4, n_burnin=1, thin=1, seed=23)
+    path, fb = brr_path()
+    assert path == 2 and fb == fb0
+    monkeypatch.setenv("GBM_BRR_SB", "0")
+    s128 = gbm.brr_arrays(X, y, n_iter=4, n_burnin=1, thin=1, seed=23)
+    monkeypatch.setenv("GBM_BRR_SWEEP", "0")
+    launches = gbm.brr_arrays(X, y, n_iter=4, n_burnin=1, thin=1, seed=23)
+    assert brr_path()[0] == 0
+    rel = lambda a, b: np.abs(a - b).max() / np.abs(b).max()
+    for a, b, c in zip(sb, s128, launches):
+        assert rel(a, b) < 1e-10 and rel(a, c) < 1e-10
+    if n * p <= 5000 * 1000:
+        ref = oracle.brr_gibbs(X, y, n_iter=4, n_burnin=1, thin=1, seed=23)
+        assert rel(sb[0], ref["b_hat"]) < 1e-9 and rel(sb[1], ref["y_pred"]) < 1e-9
