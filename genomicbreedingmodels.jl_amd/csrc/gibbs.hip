@@ -29,6 +29,8 @@ namespace gbm {
 namespace {
 
 constexpr int BB = 64;  // markers per block (one wave)
+constexpr int SBK = 512;  // markers per super-block (the super-block sweep, below)
+constexpr int SBN = SBK / (2 * BB);  // 128-marker sub-blocks per super-block
 
 __device__ __forceinline__ uint64_t bmix64(uint64_t z) {
   z += 0x9E3779B97F4A7C15ull;
@@ -239,8 +241,13 @@ __device__ __forceinline__ void brr_partials(const T* __restrict__ Xt, int64_t l
 __global__ void __launch_bounds__(256) brr_prep_kernel(const double* __restrict__ W, int64_t p, int64_t nblk, int nw,
                                                        const double* __restrict__ x2, const double* __restrict__ b,
                                                        const BrrState* __restrict__ st, double* __restrict__ Mb,
-                                                       double* __restrict__ alpha, double* __restrict__ gamma) {
+                                                       double* __restrict__ alpha, double* __restrict__ gamma,
+                                                       double* __restrict__ MSd) {
   __shared__ __attribute__((aligned(16))) double S[4][BB * BB];
+  // nw = 3 outputs: Mb's three 64x64 blocks, or (MSd, the super-block sweep) the 128x128 diagonal
+  // block of M_S it belongs to (row pitch SBK; its upper right stays zero from the setup memset)
+  const int64_t sb_s = (int64_t)blockIdx.x / SBN, sb_i = (int64_t)blockIdx.x % SBN;
+  double* const dgo = MSd ? MSd + sb_s * SBK * SBK + sb_i * 2 * BB * (SBK + 1) : nullptr;
   __shared__ double alB[BB];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   // the 64-marker half-block this wave inverts (nw = 3: waves 0, 1 = halves A, B)
@@ -296,10 +303,15 @@ __global__ void __launch_bounds__(256) brr_prep_kernel(const double* __restrict_
     }
     // M[t][lane] (coalesced rows); nw = 3 keeps M_A, M_B in LDS (this wave's W is no longer read)
     double* Mo = Mb + (nw == 1 ? hb : 3 * (int64_t)blockIdx.x + (wave == 0 ? 0 : 2)) * BB * BB + lane;
+    int64_t mo_ld = BB;
+    if (dgo) {
+      Mo = dgo + (wave == 0 ? 0 : BB * (SBK + 1)) + lane;
+      mo_ld = SBK;
+    }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
     for (int t = 0; t < BB; t++) {
-      Mo[t * BB] = m[t];
+      Mo[t * mo_ld] = m[t];
       if (nw == 3) Sw[t * BB + lane] = m[t];
     }
   } else if (nw == 3) {
@@ -342,7 +354,8 @@ __global__ void __launch_bounds__(256) brr_prep_kernel(const double* __restrict_
     double col[BB];
 #pragma unroll
     for (int s = 0; s < BB; s++) col[s] = S[3][s * BB + lane];
-    double* Oo = Mb + (3 * (int64_t)blockIdx.x + 1) * BB * BB + lane;
+    double* Oo = dgo ? dgo + BB * SBK + lane : Mb + (3 * (int64_t)blockIdx.x + 1) * BB * BB + lane;
+    const int64_t oo_ld = dgo ? SBK : BB;
 #pragma unroll 1
     for (int kk = 0; kk < 16; kk++) {
       const int k = 16 * wave + kk;
@@ -357,7 +370,7 @@ __global__ void __launch_bounds__(256) brr_prep_kernel(const double* __restrict_
           a1 = fma(w2.y, col[s + 1], a1);
         }
       }
-      Oo[k * BB] = -(a0 + a1);
+      Oo[k * oo_ld] = -(a0 + a1);
     }
   }
 }
@@ -1041,8 +1054,7 @@ __global__ void __launch_bounds__(256) brr_sweep128_kernel(const uint8_t* __rest
 // block's rows of the chunk land in LDS by DMA (wave 3, during the previous super-block's hand-
 // offs) and serve both the dots and the e update. Same chain as the literal BGLR loop, rounding
 // aside. Waits are bounded (~1 s: *info = −1, every workgroup leaves; the host falls back).
-constexpr int SBK = 512;               // markers per super-block
-constexpr int SBN = SBK / BK2;         // 128-marker sub-blocks per super-block
+static_assert(SBN * BK2 == SBK, "super-blocks are whole 128-marker blocks");
 constexpr int SB_PAIRS = SBN * (SBN - 1) / 2;
 constexpr int SB_KMAX = 64;            // individuals per chunk (at most)
 constexpr int SB_RMAX = 8;             // owned rows per workgroup (at most)
@@ -1088,28 +1100,26 @@ __global__ void __launch_bounds__(256) brr_gram_sb_kernel(const double* __restri
 }
 
 typedef double sbd4 __attribute__((ext_vector_type(4)));
-
-__device__ __forceinline__ double ld_sc1_d(const double* p) {
-  return __builtin_bit_cast(double, __hip_atomic_load(reinterpret_cast<const uint64_t*>(p), __ATOMIC_RELAXED,
-                                                      __HIP_MEMORY_SCOPE_AGENT));
-}
+typedef double sbd2 __attribute__((ext_vector_type(2)));
 
 // acc (this wave's 64x64 quadrant wm, wn of a 128x128 product) += A · B over K = 128 on the fp64
-// MFMA, the operands staged through LDS in four 32-deep chunks (As[k][r] = A[r][k]: a lane's MFMA
-// A operand is then one LDS row read, like B's). ldA(r, k) / ldB(k, c) fetch from global memory.
+// MFMA (A, B row-major with pitches lda, ldb), the operands staged through LDS in four 32-deep
+// chunks (As[k][r] = A[r][k]: a lane's MFMA A operand is then one LDS row read, like B's). Thread t
+// fetches A[t >> 1][k0 + 16 (t & 1) .. + 16] and B[k0 + (t >> 3)][16 (t & 7) .. + 16] as 16-byte
+// loads; the next chunk's are in flight while this one's MFMAs run.
 // acc[m][q][r] = C[64 wm + 16 m + fr + 4 r][64 wn + 16 q + fc].
 constexpr int SBP = BK2 + 4;  // LDS pitch (doubles)
-template <typename LA, typename LB>
-__device__ __forceinline__ void sb_gemm128(LA ldA, LB ldB, double* As, double* Bs, sbd4 (&acc)[4][4], int tid, int wm,
+__device__ __forceinline__ void sb_gemm128(const double* __restrict__ A, int64_t lda, const double* __restrict__ B,
+                                           int64_t ldb, double* As, double* Bs, sbd4 (&acc)[4][4], int tid, int wm,
                                            int wn, int fr, int fc) {
-  // chunk k0's operands: thread t holds A[t >> 1][k0 + 16 (t & 1) + u] and B[k0 + (t >> 3)][16 (t & 7) + u]; the
-  // next chunk's are loaded into registers while this one's MFMAs run
-  double va[16], vb[16];
+  const double* pa = A + (int64_t)(tid >> 1) * lda + (tid & 1) * 16;
+  const double* pb = B + (int64_t)(tid >> 3) * ldb + (tid & 7) * 16;
+  sbd2 va[8], vb[8];
   auto fetch = [&](int k0) {
 #pragma unroll
-    for (int u = 0; u < 16; u++) {
-      va[u] = ldA(tid >> 1, k0 + (tid & 1) * 16 + u);
-      vb[u] = ldB(k0 + (tid >> 3), (tid & 7) * 16 + u);
+    for (int u = 0; u < 8; u++) {
+      va[u] = *reinterpret_cast<const sbd2*>(pa + k0 + 2 * u);
+      vb[u] = *reinterpret_cast<const sbd2*>(pb + (int64_t)k0 * ldb + 2 * u);
     }
   };
   fetch(0);
@@ -1117,9 +1127,10 @@ __device__ __forceinline__ void sb_gemm128(LA ldA, LB ldB, double* As, double* B
   for (int k0 = 0; k0 < BK2; k0 += 32) {
     __syncthreads();  // the previous chunk's fragment reads are done
 #pragma unroll
-    for (int u = 0; u < 16; u++) {
-      As[((tid & 1) * 16 + u) * SBP + (tid >> 1)] = va[u];
-      Bs[(tid >> 3) * SBP + (tid & 7) * 16 + u] = vb[u];
+    for (int u = 0; u < 8; u++) {
+      As[((tid & 1) * 16 + 2 * u) * SBP + (tid >> 1)] = va[u].x;
+      As[((tid & 1) * 16 + 2 * u + 1) * SBP + (tid >> 1)] = va[u].y;
+      *reinterpret_cast<sbd2*>(Bs + (tid >> 3) * SBP + (tid & 7) * 16 + 2 * u) = vb[u];
     }
     __syncthreads();
     if (k0 + 32 < BK2) fetch(k0 + 32);
@@ -1141,13 +1152,12 @@ __device__ __forceinline__ void sb_gemm128(LA ldA, LB ldB, double* As, double* B
 
 // M_S of every super-block (row-major SBK x SBK; blocks above the diagonal stay zero from the
 // setup memset): the inverse of the unit lower triangular I + D L over its four 128-marker sub-blocks
-// (D = diag(α), L = the strictly lower part of the super-block's Gram), from
-//   M_ii = [[M_A, 0], [O, M_B]]   (brr_prep_kernel's inverse of sub-block i) and
+// (D = diag(α), L = the strictly lower part of the super-block's Gram), from the diagonal blocks
+//   M_ii = [[M_A, 0], [O, M_B]]   (brr_prep_kernel writes them into M_S) and
 //   M_ij = −M_ii D_i Σ_{m=j}^{i−1} W_im M_mj  (i > j),
-// by recursive doubling in four launches (each workgroup one 128x128 output block, ≤ 2 GEMMs; the
-// blocks a level reads were written by an earlier launch):
-//   level 0: X_{a+1,a} = D_{a+1} W_{a+1,a} M_aa (a = 0, 2), and the diagonal blocks into M_S;
-//   level 1: M_{a+1,a} = −M_{a+1,a+1} X_{a+1,a};
+// by recursive doubling in three launches (each workgroup one 128x128 output block; the blocks a
+// level reads were written by an earlier launch or, level 0, by the same workgroup):
+//   level 0: X_{a+1,a} = D_{a+1} W_{a+1,a} M_aa, then M_{a+1,a} = −M_{a+1,a+1} X_{a+1,a} (a = 0, 2);
 //   level 2: X_ij = D_i Σ_{m=j}^{1} W_im M_mj (i = 2, 3; j = 0, 1);
 //   level 3: M_ij = −Σ_{m=2}^{i} M_im X_mj.
 // X lives in the scratch Xsc: 6 blocks per super-block, slot(i, j) = {10: 0, 32: 1, 20: 2, 21: 3,
@@ -1155,51 +1165,21 @@ __device__ __forceinline__ void sb_gemm128(LA ldA, LB ldB, double* As, double* B
 __device__ __forceinline__ int sb_xslot(int i, int j) {
   return i == 1 ? 0 : i == 2 ? (j == 0 ? 2 : 3) : (j == 2 ? 1 : j == 0 ? 4 : 5);
 }
-__global__ void __launch_bounds__(256, 1) brr_sb_prep_kernel(int level, const double* __restrict__ Mb,
-                                                             const double* __restrict__ Wsb,
+__global__ void __launch_bounds__(256, 1) brr_sb_prep_kernel(int level, const double* __restrict__ Wsb,
                                                              const double* __restrict__ alpha, double* __restrict__ MS,
                                                              double* __restrict__ Xsc) {
-  __shared__ double As[32 * SBP], Bs[32 * SBP];
-  const int ntask = level < 2 ? 2 : 4;
+  __shared__ __attribute__((aligned(16))) double As[32 * SBP];
+  __shared__ __attribute__((aligned(16))) double Bs[32 * SBP];
+  const int ntask = level == 0 ? 2 : 4;
   const int64_t s = blockIdx.x / ntask;
   const int task = (int)(blockIdx.x % ntask);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1, fr = lane >> 4, fc = lane & 15;
   double* Ms = MS + s * (int64_t)SBK * SBK;
   double* X = Xsc + s * 6 * (int64_t)BK2 * BK2;
-  // element (r, c) of the 128-block inverse M_kk of 128-block k = 4s + i
-  auto mkk = [&](int i, int r, int c) -> double {
-    const double* base = Mb + (s * SBN + i) * 3 * BB * BB;
-    if (r < BB) return c < BB ? base[r * BB + c] : 0.0;
-    return c < BB ? base[BB * BB + (r - BB) * BB + c] : base[2 * BB * BB + (r - BB) * BB + (c - BB)];
-  };
   auto Wb = [&](int i, int m) { return Wsb + (s * SB_PAIRS + sb_pair_index(i, m)) * (int64_t)BK2 * BK2; };
   auto Mblk = [&](int i, int j) { return Ms + (int64_t)(i * BK2) * SBK + j * BK2; };
   auto Xblk = [&](int i, int j) { return X + sb_xslot(i, j) * (int64_t)BK2 * BK2; };
-  // B operand M_mj (diagonal: from Mb; below: from M_S)
-  auto gemm_W_M = [&](int i, int m, int j, sbd4 (&acc)[4][4]) {
-    const double* W = Wb(i, m);
-    if (m == j) {
-      sb_gemm128([&](int r, int k) { return W[r * BK2 + k]; }, [&](int k, int c) { return mkk(m, k, c); }, As, Bs, acc,
-                 tid, wm, wn, fr, fc);
-    } else {
-      const double* B = Mblk(m, j);
-      sb_gemm128([&](int r, int k) { return W[r * BK2 + k]; }, [&](int k, int c) { return B[(int64_t)k * SBK + c]; }, As,
-                 Bs, acc, tid, wm, wn, fr, fc);
-    }
-  };
-  // A operand M_im (diagonal: from Mb; below: from M_S), B operand X_mj
-  auto gemm_M_X = [&](int i, int m, int j, sbd4 (&acc)[4][4]) {
-    const double* B = Xblk(m, j);
-    if (i == m) {
-      sb_gemm128([&](int r, int k) { return mkk(i, r, k); }, [&](int k, int c) { return B[k * BK2 + c]; }, As, Bs, acc,
-                 tid, wm, wn, fr, fc);
-    } else {
-      const double* A = Mblk(i, m);
-      sb_gemm128([&](int r, int k) { return A[(int64_t)r * SBK + k]; }, [&](int k, int c) { return B[k * BK2 + c]; }, As,
-                 Bs, acc, tid, wm, wn, fr, fc);
-    }
-  };
   // epilogues: rows scaled by α of sub-block i (into X), or negated (into M_S)
   auto store_scaled = [&](const sbd4 (&acc)[4][4], double* out, int64_t ld, int i) {
     const double* al = alpha + (s * SBN + i) * BK2;
@@ -1223,30 +1203,29 @@ __global__ void __launch_bounds__(256, 1) brr_sb_prep_kernel(int level, const do
           out[(int64_t)(wm * 64 + mm * 16 + fr + 4 * r) * ld + wn * 64 + q * 16 + fc] = -acc[mm][q][r];
   };
   sbd4 acc[4][4];
+  auto zero = [&]() {
 #pragma unroll
-  for (int mm = 0; mm < 4; mm++)
+    for (int mm = 0; mm < 4; mm++)
 #pragma unroll
-    for (int q = 0; q < 4; q++) acc[mm][q] = (sbd4){0.0, 0.0, 0.0, 0.0};
+      for (int q = 0; q < 4; q++) acc[mm][q] = (sbd4){0.0, 0.0, 0.0, 0.0};
+  };
+  zero();
   if (level == 0) {
     const int a = 2 * task;
-    for (int d = a; d < a + 2; d++)
-      for (int e = tid; e < BK2 * BK2; e += 256) {
-        const int r = e / BK2, c = e % BK2;
-        Mblk(d, d)[(int64_t)r * SBK + c] = mkk(d, r, c);
-      }
-    gemm_W_M(a + 1, a, a, acc);
+    sb_gemm128(Wb(a + 1, a), BK2, Mblk(a, a), SBK, As, Bs, acc, tid, wm, wn, fr, fc);
     store_scaled(acc, Xblk(a + 1, a), BK2, a + 1);
-  } else if (level == 1) {
-    const int a = 2 * task;
-    gemm_M_X(a + 1, a + 1, a, acc);
+    __threadfence_block();
+    __syncthreads();  // X_{a+1,a} (this workgroup's stores) before it is read back as B
+    zero();
+    sb_gemm128(Mblk(a + 1, a + 1), SBK, Xblk(a + 1, a), BK2, As, Bs, acc, tid, wm, wn, fr, fc);
     store_neg(acc, Mblk(a + 1, a), SBK);
   } else if (level == 2) {
     const int i = 2 + task / 2, j = task % 2;
-    for (int m = j; m <= 1; m++) gemm_W_M(i, m, j, acc);
+    for (int m = j; m <= 1; m++) sb_gemm128(Wb(i, m), BK2, Mblk(m, j), SBK, As, Bs, acc, tid, wm, wn, fr, fc);
     store_scaled(acc, Xblk(i, j), BK2, i);
   } else {
     const int i = 2 + task / 2, j = task % 2;
-    for (int m = 2; m <= i; m++) gemm_M_X(i, m, j, acc);
+    for (int m = 2; m <= i; m++) sb_gemm128(Mblk(i, m), SBK, Xblk(m, j), BK2, As, Bs, acc, tid, wm, wn, fr, fc);
     store_neg(acc, Mblk(i, j), SBK);
   }
 }
@@ -1584,8 +1563,23 @@ __global__ void __launch_bounds__(1024) brr_var_kernel(const double* __restrict_
   __shared__ double red[16];
   double sb = 0.0, se = 0.0;
   const double* bn = b + ((st->it & 1) ^ 1) * p;  // this iteration's samples
-  for (int64_t j = threadIdx.x; j < p; j += 1024) sb += bn[j] * bn[j];
-  for (int64_t i = threadIdx.x; i < n; i += 1024) se += e[i] * e[i];
+  // eight loads in flight per thread (one 1024-thread workgroup: latency, not bandwidth, bound)
+  {
+    double a[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    int64_t j = threadIdx.x;
+    for (; j + 7 * 1024 < p; j += 8 * 1024)
+#pragma unroll
+      for (int u = 0; u < 8; u++) a[u] = fma(bn[j + u * 1024], bn[j + u * 1024], a[u]);
+    for (; j < p; j += 1024) a[0] = fma(bn[j], bn[j], a[0]);
+    sb = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
+    double c[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    int64_t i = threadIdx.x;
+    for (; i + 7 * 1024 < n; i += 8 * 1024)
+#pragma unroll
+      for (int u = 0; u < 8; u++) c[u] = fma(e[i + u * 1024], e[i + u * 1024], c[u]);
+    for (; i < n; i += 1024) c[0] = fma(e[i], e[i], c[0]);
+    se = ((c[0] + c[1]) + (c[2] + c[3])) + ((c[4] + c[5]) + (c[6] + c[7]));
+  }
   sb = brr_block_sum<1024>(sb, red);
   se = brr_block_sum<1024>(se, red);
   if (threadIdx.x == 0) {
@@ -1921,13 +1915,12 @@ static int brr_fit_impl(const double* X, int64_t n, int64_t p, int64_t ldx, cons
   auto enqueue_iteration = [&]() -> int {
     brr_prep_kernel<<<prep_grid, 256, 0, s>>>((const double*)cx.W.p, p, nblk, nw, (const double*)cx.x2.p,
                                               (const double*)cx.b.p, stp, (double*)cx.Mb.p, (double*)cx.alph.p,
-                                              (double*)cx.gamm.p);
+                                              (double*)cx.gamm.p, sbmode ? (double*)cx.MS.p : nullptr);
     brr_mu_kernel<<<1, 1024, 0, s>>>((double*)cx.e.p, n, stp);
     if (sbmode) {
-      for (int level = 0; level < 4; level++)
-        brr_sb_prep_kernel<<<(unsigned)(nsb * (level < 2 ? 2 : 4)), 256, 0, s>>>(
-            level, (const double*)cx.Mb.p, (const double*)cx.Wsb.p, (const double*)cx.alph.p, (double*)cx.MS.p,
-            (double*)cx.Ssc.p);
+      for (int level : {0, 2, 3})
+        brr_sb_prep_kernel<<<(unsigned)(nsb * (level == 0 ? 2 : 4)), 256, 0, s>>>(
+            level, (const double*)cx.Wsb.p, (const double*)cx.alph.p, (double*)cx.MS.p, (double*)cx.Ssc.p);
       int32_t* cn = (int32_t*)cx.sbcnt.p + 24;  // the error cell (zeroed at setup)
       if (g_brr_trace)
         brr_sweep_sb_kernel<true><<<(unsigned)sbC, 256, 0, s>>>(
