@@ -1103,50 +1103,66 @@ typedef double sbd4 __attribute__((ext_vector_type(4)));
 typedef double sbd2 __attribute__((ext_vector_type(2)));
 
 // acc (this wave's 64x64 quadrant wm, wn of a 128x128 product) += A · B over K = 128 on the fp64
-// MFMA (A, B row-major with pitches lda, ldb), the operands staged through LDS in four 32-deep
-// chunks (As[k][r] = A[r][k]: a lane's MFMA A operand is then one LDS row read, like B's). Thread t
-// fetches A[t >> 1][k0 + 16 (t & 1) .. + 16] and B[k0 + (t >> 3)][16 (t & 7) .. + 16] as 16-byte
-// loads; the next chunk's are in flight while this one's MFMAs run.
+// MFMA (A, B row-major with pitches lda, ldb). The operands go global -> LDS by DMA
+// (global_load_lds, no registers) in eight 16-deep chunks, double-buffered: chunk c + 1 is in
+// flight while chunk c's MFMAs run, and two workgroups share a CU, so one's loads, barriers and
+// epilogue overlap the other's MFMAs. A lands row-major with its 16-byte pairs XOR-swizzled by row
+// (pair p of row r at slot p ^ (r & 7)): a lane's MFMA A operand A[r][k] (r = 16 rows, k = 4 deep)
+// is then a near conflict-free LDS read. B lands row-major, one 1 KB row per wave instruction.
 // acc[m][q][r] = C[64 wm + 16 m + fr + 4 r][64 wn + 16 q + fc].
-constexpr int SBP = BK2 + 4;  // LDS pitch (doubles)
+constexpr int SBP = BK2 + 4;       // LDS pitch of B rows (doubles)
+constexpr int GK = 16;             // k per chunk
+constexpr int GA = BK2 * GK;       // A chunk (doubles)
+constexpr int GBUF = GA + GK * SBP;  // one buffer: A chunk + B chunk
 __device__ __forceinline__ void sb_gemm128(const double* __restrict__ A, int64_t lda, const double* __restrict__ B,
-                                           int64_t ldb, double* As, double* Bs, sbd4 (&acc)[4][4], int tid, int wm,
+                                           int64_t ldb, double* lds, sbd4 (&acc)[4][4], int lane, int wave, int wm,
                                            int wn, int fr, int fc) {
-  const double* pa = A + (int64_t)(tid >> 1) * lda + (tid & 1) * 16;
-  const double* pb = B + (int64_t)(tid >> 3) * ldb + (tid & 7) * 16;
-  sbd2 va[8], vb[8];
-  auto fetch = [&](int k0) {
+  auto stage = [&](int c, int bf) {
+    const int k0 = c * GK;
+    double* base = lds + bf * GBUF;
 #pragma unroll
-    for (int u = 0; u < 8; u++) {
-      va[u] = *reinterpret_cast<const sbd2*>(pa + k0 + 2 * u);
-      vb[u] = *reinterpret_cast<const sbd2*>(pb + (int64_t)k0 * ldb + 2 * u);
+    for (int jj = 0; jj < 4; jj++) {
+      const int j = wave * 4 + jj;  // A: 16 instructions of 64 16-byte slots
+      const int slot = j * 64 + lane, r = slot >> 3, p = (slot & 7) ^ (r & 7);
+      __builtin_amdgcn_global_load_lds((const void*)(A + (int64_t)r * lda + k0 + 2 * p), (void*)(base + j * 128), 16, 0, 0);
+    }
+#pragma unroll
+    for (int jj = 0; jj < 4; jj++) {
+      const int k = wave * 4 + jj;  // B: one row per instruction
+      __builtin_amdgcn_global_load_lds((const void*)(B + (int64_t)(k0 + k) * ldb + 2 * lane), (void*)(base + GA + k * SBP),
+                                       16, 0, 0);
     }
   };
-  fetch(0);
+  stage(0, 0);
 #pragma unroll 1
-  for (int k0 = 0; k0 < BK2; k0 += 32) {
-    __syncthreads();  // the previous chunk's fragment reads are done
-#pragma unroll
-    for (int u = 0; u < 8; u++) {
-      As[((tid & 1) * 16 + 2 * u) * SBP + (tid >> 1)] = va[u].x;
-      As[((tid & 1) * 16 + 2 * u + 1) * SBP + (tid >> 1)] = va[u].y;
-      *reinterpret_cast<sbd2*>(Bs + (tid >> 3) * SBP + (tid & 7) * 16 + 2 * u) = vb[u];
+  for (int c = 0; c < BK2 / GK; c++) {
+    if (c + 1 < BK2 / GK) {
+      stage(c + 1, (c + 1) & 1);
+      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // chunk c's eight DMAs of this wave have landed
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
-    __syncthreads();
-    if (k0 + 32 < BK2) fetch(k0 + 32);
+    __syncthreads();  // ... and every wave's
+    const double* As = lds + (c & 1) * GBUF;
+    const double* Bs = As + GA;
 #pragma unroll
-    for (int ks = 0; ks < 32; ks += 4) {
+    for (int ks = 0; ks < GK; ks += 4) {
       double a[4], b[4];
+      const int k = ks + fr;
 #pragma unroll
       for (int u = 0; u < 4; u++) {
-        a[u] = As[(ks + fr) * SBP + wm * 64 + u * 16 + fc];
-        b[u] = Bs[(ks + fr) * SBP + wn * 64 + u * 16 + fc];
+        const int r = wm * 64 + u * 16 + fc;
+        a[u] = As[(r * 8 + ((k >> 1) ^ (r & 7))) * 2 + (k & 1)];
+        b[u] = Bs[k * SBP + wn * 64 + u * 16 + fc];
       }
+      __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int mm = 0; mm < 4; mm++)
 #pragma unroll
         for (int q = 0; q < 4; q++) acc[mm][q] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[mm], b[q], acc[mm][q], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
     }
+    __syncthreads();  // buffer c & 1 is free for chunk c + 2
   }
 }
 
@@ -1161,15 +1177,14 @@ __device__ __forceinline__ void sb_gemm128(const double* __restrict__ A, int64_t
 //   level 2: X_ij = D_i Σ_{m=j}^{1} W_im M_mj (i = 2, 3; j = 0, 1);
 //   level 3: M_ij = −Σ_{m=2}^{i} M_im X_mj.
 // X lives in the scratch Xsc: 6 blocks per super-block, slot(i, j) = {10: 0, 32: 1, 20: 2, 21: 3,
-// 30: 4, 31: 5}.
+// 30: 4, 31: 5}. Two workgroups per CU (67 KB of LDS each).
 __device__ __forceinline__ int sb_xslot(int i, int j) {
   return i == 1 ? 0 : i == 2 ? (j == 0 ? 2 : 3) : (j == 2 ? 1 : j == 0 ? 4 : 5);
 }
-__global__ void __launch_bounds__(256, 1) brr_sb_prep_kernel(int level, const double* __restrict__ Wsb,
+__global__ void __launch_bounds__(256, 2) brr_sb_prep_kernel(int level, const double* __restrict__ Wsb,
                                                              const double* __restrict__ alpha, double* __restrict__ MS,
                                                              double* __restrict__ Xsc) {
-  __shared__ __attribute__((aligned(16))) double As[32 * SBP];
-  __shared__ __attribute__((aligned(16))) double Bs[32 * SBP];
+  __shared__ __attribute__((aligned(16))) double lds[2 * GBUF];
   const int ntask = level == 0 ? 2 : 4;
   const int64_t s = blockIdx.x / ntask;
   const int task = (int)(blockIdx.x % ntask);
@@ -1212,20 +1227,20 @@ __global__ void __launch_bounds__(256, 1) brr_sb_prep_kernel(int level, const do
   zero();
   if (level == 0) {
     const int a = 2 * task;
-    sb_gemm128(Wb(a + 1, a), BK2, Mblk(a, a), SBK, As, Bs, acc, tid, wm, wn, fr, fc);
+    sb_gemm128(Wb(a + 1, a), BK2, Mblk(a, a), SBK, lds, acc, lane, wave, wm, wn, fr, fc);
     store_scaled(acc, Xblk(a + 1, a), BK2, a + 1);
     __threadfence_block();
     __syncthreads();  // X_{a+1,a} (this workgroup's stores) before it is read back as B
     zero();
-    sb_gemm128(Mblk(a + 1, a + 1), SBK, Xblk(a + 1, a), BK2, As, Bs, acc, tid, wm, wn, fr, fc);
+    sb_gemm128(Mblk(a + 1, a + 1), SBK, Xblk(a + 1, a), BK2, lds, acc, lane, wave, wm, wn, fr, fc);
     store_neg(acc, Mblk(a + 1, a), SBK);
   } else if (level == 2) {
     const int i = 2 + task / 2, j = task % 2;
-    for (int m = j; m <= 1; m++) sb_gemm128(Wb(i, m), BK2, Mblk(m, j), SBK, As, Bs, acc, tid, wm, wn, fr, fc);
+    for (int m = j; m <= 1; m++) sb_gemm128(Wb(i, m), BK2, Mblk(m, j), SBK, lds, acc, lane, wave, wm, wn, fr, fc);
     store_scaled(acc, Xblk(i, j), BK2, i);
   } else {
     const int i = 2 + task / 2, j = task % 2;
-    for (int m = 2; m <= i; m++) sb_gemm128(Mblk(i, m), SBK, Xblk(m, j), BK2, As, Bs, acc, tid, wm, wn, fr, fc);
+    for (int m = 2; m <= i; m++) sb_gemm128(Mblk(i, m), SBK, Xblk(m, j), BK2, lds, acc, lane, wave, wm, wn, fr, fc);
     store_neg(acc, Mblk(i, j), SBK);
   }
 }
