@@ -1571,6 +1571,431 @@ __global__ void __launch_bounds__(256) brr_sweep_sb_kernel(const uint8_t* __rest
   if (tid < K && i0 + tid < n) e[i0 + tid] = es[tid];
 }
 
+// ---- byte storage: look-ahead super-block sweep (round 3) -----------------------------------------
+// brr_sweep_sb_kernel runs three hand-offs per super-block in a row: partial dots -> owners, r̃ ->
+// everyone, δ -> everyone, with the e update and the next dots between them. Here the dots leave
+// the chain: with e⁽ˢ⁾ the residual after super-block s,
+//   d⁰_s = X_sᵀ e⁽ˢ⁻¹⁾ = X_sᵀ e⁽ˢ⁻²⁾ + X_sᵀ X_{s−1} δ_{s−1} = Q_s + C_s δ_{s−1},
+// so Q_s (partial dots over chunks of individuals, summed by the row owners) is computed from the
+// residual one super-block earlier, and only the 512 x 512 cross-Gram C_s = X_sᵀ X_{s−1} (one-time
+// setup, brr_xgram_kernel) applied to δ_{s−1} sits on the chain. Step s of the launch:
+//   (A) every workgroup gathers δ_{s−1}; the owners also sum their rows of Q_s over the chunks;
+//   (B) owners: r̃_s = γ − α ∘ (Q_s + C_s δ_{s−1}) on their rows, published;
+//   (C) every workgroup: e += X_{s−1} δ_{s−1} on its chunk, then the partial dots X_{s+1}ᵀ e of
+//       Q_{s+1}, published (this runs while r̃_s travels);
+//   (D) owners: gather r̃_s, δ_s = M_s r̃_s on their rows, b and b̄ updated, δ_s published.
+// Two hand-offs per super-block on the chain (δ, r̃) and the e update and dots beside the second.
+// A chunk's rows of super-blocks s − 1 .. s + 2 are in LDS (four buffers; s + 2 lands by DMA during
+// step s). Granule slots rotate over four super-blocks (a slot is rewritten only after every
+// reader of its previous tag has passed a later hand-off). Same chain as the literal loop, rounding
+// aside; waits bounded as in brr_sweep_sb_kernel.
+constexpr int LA_KMAX = 48;  // individuals per chunk (at most)
+
+// C_s = X_sᵀ X_{s−1} for s = 1 .. nsb − 1 (row-major 512 x 512 at CS + s·512²; rows of markers past
+// p repeat marker p − 1: they meet α = γ = δ = 0): one 128x128 block per workgroup, fp64 MFMA over
+// the individuals in 16-deep chunks staged by DMA (both operands marker-major, XOR-swizzled as A in
+// sb_gemm128), double-buffered, two workgroups per CU. One-time setup.
+__global__ void __launch_bounds__(256, 2) brr_xgram_kernel(const double* __restrict__ Xt, int64_t ldx, int64_t p,
+                                                           int64_t npad, double* __restrict__ CS) {
+  __shared__ __attribute__((aligned(16))) double lds[2 * 2 * GA];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1, fr = lane >> 4, fc = lane & 15;
+  const int64_t s = 1 + blockIdx.x / 16;
+  const int ti = (int)((blockIdx.x >> 2) & 3), tj = (int)(blockIdx.x & 3);
+  const int64_t ra = s * SBK + ti * BK2, rb = (s - 1) * SBK + tj * BK2;
+  auto stage = [&](int64_t k0, int bf) {
+    double* base = lds + bf * 2 * GA;
+#pragma unroll
+    for (int o = 0; o < 2; o++) {
+      const int64_t r0 = o ? rb : ra;
+#pragma unroll
+      for (int jj = 0; jj < 4; jj++) {
+        const int j = wave * 4 + jj;
+        const int slot = j * 64 + lane, r = slot >> 3, pp = (slot & 7) ^ (r & 7);
+        int64_t row = r0 + r;
+        row = row < p ? row : p - 1;
+        __builtin_amdgcn_global_load_lds((const void*)(Xt + row * ldx + k0 + 2 * pp), (void*)(base + o * GA + j * 128), 16,
+                                         0, 0);
+      }
+    }
+  };
+  sbd4 acc[4][4];
+#pragma unroll
+  for (int mm = 0; mm < 4; mm++)
+#pragma unroll
+    for (int q = 0; q < 4; q++) acc[mm][q] = (sbd4){0.0, 0.0, 0.0, 0.0};
+  const int64_t nch = npad / GK;
+  stage(0, 0);
+#pragma unroll 1
+  for (int64_t c = 0; c < nch; c++) {
+    if (c + 1 < nch) {
+      stage((c + 1) * GK, (int)((c + 1) & 1));
+      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+    const double* As = lds + (c & 1) * 2 * GA;
+    const double* Bs = As + GA;
+#pragma unroll
+    for (int ks = 0; ks < GK; ks += 4) {
+      double a[4], bq[4];
+      const int k = ks + fr;
+#pragma unroll
+      for (int u = 0; u < 4; u++) {
+        const int r = wm * 64 + u * 16 + fc, cc = wn * 64 + u * 16 + fc;
+        a[u] = As[(r * 8 + ((k >> 1) ^ (r & 7))) * 2 + (k & 1)];
+        bq[u] = Bs[(cc * 8 + ((k >> 1) ^ (cc & 7))) * 2 + (k & 1)];
+      }
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int mm = 0; mm < 4; mm++)
+#pragma unroll
+        for (int q = 0; q < 4; q++) acc[mm][q] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[mm], bq[q], acc[mm][q], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+    }
+    __syncthreads();
+  }
+  double* out = CS + s * (int64_t)SBK * SBK + (int64_t)(ti * BK2) * SBK + tj * BK2;
+#pragma unroll
+  for (int mm = 0; mm < 4; mm++)
+#pragma unroll
+    for (int q = 0; q < 4; q++)
+#pragma unroll
+      for (int r = 0; r < 4; r++)
+        out[(int64_t)(wm * 64 + mm * 16 + fr + 4 * r) * SBK + wn * 64 + q * 16 + fc] = acc[mm][q][r];
+}
+
+// K individuals per chunk workgroup (a multiple of 16, <= LA_KMAX); R owned rows (<= SB_RMAX).
+// kTrace: workgroups 0 and C − 1 record 5 timestamps per super-block (ends of A, B, C, D).
+template <bool kTrace>
+__global__ void __launch_bounds__(256) brr_sweep_la_kernel(const uint8_t* __restrict__ D, int64_t ldx, int64_t n,
+                                                           int64_t p, double xs, const double* __restrict__ MS,
+                                                           const double* __restrict__ CS, int64_t nsb, int K, int R,
+                                                           double* __restrict__ Pb, double* __restrict__ Rt,
+                                                           double* __restrict__ Dl, int32_t* __restrict__ info,
+                                                           double* __restrict__ b, double* __restrict__ bbar,
+                                                           const double* __restrict__ alpha,
+                                                           const double* __restrict__ gamma, double* __restrict__ e,
+                                                           const BrrState* __restrict__ st, int64_t* __restrict__ trace) {
+  __shared__ __attribute__((aligned(16))) uint8_t Drow[4][SBK * LA_KMAX];
+  __shared__ __attribute__((aligned(16))) double es[LA_KMAX];
+  __shared__ __attribute__((aligned(16))) double rt[SBK];
+  __shared__ __attribute__((aligned(16))) double dl[SBK];
+  __shared__ double red[4][SB_RMAX];
+  __shared__ double cd[1][SB_RMAX];
+  __shared__ double eacc[4160];  // e update partial sums [individual][slice]: K x (nsl_used | 1) <= 32 x 129
+  __shared__ double eq[4][LA_KMAX];
+  __shared__ int s_fail;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int C = (int)gridDim.x, c = (int)blockIdx.x;
+  const int64_t i0 = (int64_t)c * K;
+  const int r0 = c * R;
+  const int nown = r0 >= SBK ? 0 : (SBK - r0 < R ? SBK - r0 : R);
+  const bool tr_on = kTrace && threadIdx.x == 0;
+  int64_t* trw = kTrace ? trace + (int64_t)c * nsb * 8 : nullptr;  // every workgroup: 8 per super-block
+  auto mark = [&](int64_t s, int k) {
+    if (tr_on) trw[s * 8 + k] = (int64_t)__builtin_amdgcn_s_memrealtime();
+  };
+  const int it_odd = (int)(st->it & 1);
+  const bool accum = brr_accumulate(st);
+  const double kk = (double)(st->nsum + 1);
+  const uint64_t tag0 = (st->epoch << 40) + (uint64_t)st->it * (uint64_t)nsb;
+  const __amdgpu_buffer_rsrc_t rP = brr_rsrc(Pb, (int64_t)4 * C * SBK * 16);
+  const __amdgpu_buffer_rsrc_t rR = brr_rsrc(Rt, (int64_t)4 * SBK * 16);
+  const __amdgpu_buffer_rsrc_t rD = brr_rsrc(Dl, (int64_t)4 * SBK * 16);
+  if (tid == 0) s_fail = 0;
+  const int kpc = K / 16, kinv = (65536 + kpc - 1) / kpc;  // q / kpc = (q · kinv) >> 16 for q < 2^14
+  auto dma_rows = [&](int64_t sb) {  // wave 3: the chunk's rows of super-block sb -> Drow[sb & 3]
+    const int pieces = SBK * kpc;
+    uint8_t* dst = Drow[sb & 3];
+    for (int q0 = 0; q0 < pieces; q0 += 64) {
+      const int q = q0 + lane;
+      const int row = (q * kinv) >> 16, part = q - row * kpc;
+      int64_t jr = sb * SBK + row;
+      jr = jr < p ? jr : p - 1;
+      const uint8_t* src = D + jr * ldx + i0 + part * 16;
+      const unsigned m0v = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(dst + q0 * 16));
+      asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off" : : "s"(m0v), "v"(src) : "memory");
+    }
+  };
+  // partial dots of super-block sb over this chunk from es (thread t: rows 2t, 2t + 1) -> P granules
+  auto dots_publish = [&](int64_t sb) {
+    const uint8_t* Dr = Drow[sb & 3];
+    double a0 = 0.0, a1 = 0.0, c0 = 0.0, c1 = 0.0;
+    const uint8_t* ra = Dr + (2 * tid) * K;
+    const uint8_t* rb = ra + K;
+    for (int u = 0; u < K; u += 16) {
+      const uint4 va = *reinterpret_cast<const uint4*>(ra + u);
+      const uint4 vb = *reinterpret_cast<const uint4*>(rb + u);
+      const uint32_t wa[4] = {va.x, va.y, va.z, va.w};
+      const uint32_t wb[4] = {vb.x, vb.y, vb.z, vb.w};
+#pragma unroll
+      for (int q = 0; q < 4; q++)
+#pragma unroll
+        for (int bb = 0; bb < 4; bb += 2) {
+          const double2 e2 = *reinterpret_cast<const double2*>(es + u + 4 * q + bb);
+          a0 = fma((double)((wa[q] >> (8 * bb)) & 0xFFu), e2.x, a0);
+          a1 = fma((double)((wa[q] >> (8 * bb + 8)) & 0xFFu), e2.y, a1);
+          c0 = fma((double)((wb[q] >> (8 * bb)) & 0xFFu), e2.x, c0);
+          c1 = fma((double)((wb[q] >> (8 * bb + 8)) & 0xFFu), e2.y, c1);
+        }
+    }
+    const uint64_t key = sb_key(tag0 + (uint64_t)sb);
+    const uint32_t off = (uint32_t)((((int64_t)(sb & 3) * C + c) * SBK + 2 * tid) * 16);
+    sb_put(rP, off, a0 * xs + a1 * xs, key);
+    sb_put(rP, off + 16, c0 * xs + c1 * xs, key);
+  };
+  // all 512 granules of super-block sb from buffer r into LDS out (waves 0-1, four per lane); the
+  // pause between polls grows (up to ~0.2 µs) the longer the wait: 209 workgroups polling one 8 KB
+  // block is what the hop pays. (Every lane re-reads all four granules: an asm load under a
+  // divergent branch lets the compiler copy its register before the data lands.)
+  auto gather512 = [&](__amdgpu_buffer_rsrc_t r, int64_t sb, double* out) {
+    if (wave < 2) {
+      const uint64_t key = sb_key(tag0 + (uint64_t)sb);
+      bool failed = false;
+      int64_t spin = 0;
+      double x[4] = {0.0, 0.0, 0.0, 0.0};
+      for (;;) {
+        sbu4 w[4];
+#pragma unroll
+        for (int q = 0; q < 4; q++) w[q] = sb_get(r, (uint32_t)(((int64_t)(sb & 3) * SBK + tid * 4 + q) * 16));
+        sb_landed();
+        bool all = true;
+#pragma unroll
+        for (int q = 0; q < 4; q++) all = sb_ok(w[q], key, x[q]) && all;
+        if (!sb_spin(all, spin, info, failed)) break;
+        for (int64_t z = spin >> 3; z > 0 && z < 8; z--) __builtin_amdgcn_s_sleep(1);
+        if (spin >= 64) {
+#pragma unroll
+          for (int z = 0; z < 7; z++) __builtin_amdgcn_s_sleep(1);
+        }
+      }
+      if (failed) s_fail = 1;
+#pragma unroll
+      for (int q = 0; q < 4; q++) out[tid * 4 + q] = x[q];
+    }
+  };
+  // e update: thread t -> 16-individual piece t % nch of slice t / nch (rows [sl·rps, (sl+1)·rps))
+  const int nch = K / 16, nsl = 256 / nch, rps = (SBK + nsl - 1) / nsl;
+  const int ech = tid % nch, esl = tid / nch;
+  const int nsl_used = (SBK + rps - 1) / rps;
+  const int slp = nsl_used | 1;
+  // e += X_sb δ (δ in dl) over the chunk, rows from Drow[sb & 3]; ends with a barrier
+  auto e_update = [&](int64_t sb, auto&& between) {
+    const uint8_t* Dr = Drow[sb & 3];
+    if (esl < nsl_used) {
+      double acc[16];
+#pragma unroll
+      for (int u = 0; u < 16; u++) acc[u] = 0.0;
+      const int jb = esl * rps, je = (jb + rps < SBK) ? jb + rps : SBK;
+      for (int jj = jb; jj < je; jj++) {
+        const uint4 w4 = *reinterpret_cast<const uint4*>(Dr + jj * K + ech * 16);
+        const double d = dl[jj];
+        const uint32_t wd[4] = {w4.x, w4.y, w4.z, w4.w};
+#pragma unroll
+        for (int q = 0; q < 4; q++)
+#pragma unroll
+          for (int bb = 0; bb < 4; bb++) acc[4 * q + bb] = fma((double)((wd[q] >> (8 * bb)) & 0xFFu), d, acc[4 * q + bb]);
+      }
+#pragma unroll
+      for (int u = 0; u < 16; u++) eacc[(ech * 16 + u) * slp + esl] = acc[u];
+    }
+    lds_barrier();
+    between();  // runs beside the reduction (tid >= 4 K: wave 3 when K <= 48)
+    if (tid < 4 * K) {
+      const int ind = tid % K, q = tid / K;
+      double u = 0.0;
+      for (int t = q; t < nsl_used; t += 4) u += eacc[ind * slp + t];
+      eq[q][ind] = u;
+    }
+    lds_barrier();
+    if (tid < K && i0 + tid < n) es[tid] += (((eq[0][tid] + eq[1][tid]) + eq[2][tid]) + eq[3][tid]) * xs;
+    lds_barrier();
+  };
+
+  if (tid < LA_KMAX) es[tid] = (tid < K && i0 + tid < n) ? e[i0 + tid] : 0.0;
+  if (wave == 3) {
+    dma_rows(0);
+    if (nsb > 1) dma_rows(1);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+  dots_publish(0);  // Q_0 = X_0ᵀ e
+  // owners: their rows of Q_sb summed over all chunks (waves 0-2, lane -> chunks lane + 64 w and
+  // + 192, summed in that order, xor-tree; red[w][r], the waves summed in order by the reader)
+  auto gather_q = [&](int64_t sb) {
+    if (nown > 0 && wave < 3) {
+      const uint64_t key = sb_key(tag0 + (uint64_t)sb);
+      double v[SB_RMAX];
+#pragma unroll
+      for (int r = 0; r < SB_RMAX; r++) v[r] = 0.0;
+#pragma unroll
+      for (int h = 0; h < 2; h++) {
+        const int cc = lane + 64 * wave + 192 * h;
+        const bool has = cc < C;
+        const uint32_t base = (uint32_t)((((int64_t)(sb & 3) * C + (has ? cc : 0)) * SBK + r0) * 16);
+        bool failed = false, done = !has;
+        int64_t spin = 0;
+        double x[SB_RMAX];
+#pragma unroll
+        for (int r = 0; r < SB_RMAX; r++) x[r] = 0.0;
+        do {
+          if (!done) {
+            sbu4 w[SB_RMAX];
+#pragma unroll
+            for (int r = 0; r < SB_RMAX; r++)
+              if (r < R) w[r] = sb_get(rP, base + r * 16);
+            sb_landed();
+            bool all = true;
+#pragma unroll
+            for (int r = 0; r < SB_RMAX; r++)
+              if (r < R && r < nown) all = sb_ok(w[r], key, x[r]) && all;
+            done = all;
+          }
+        } while (sb_spin(done, spin, info, failed));
+        if (failed) s_fail = 1;
+#pragma unroll
+        for (int r = 0; r < SB_RMAX; r++) v[r] += (has && r < nown) ? x[r] : 0.0;
+      }
+#pragma unroll
+      for (int r = 0; r < SB_RMAX; r++) {
+        double x = v[r];
+        x += __shfl_xor(x, 32);
+        x += __shfl_xor(x, 16);
+        x += __shfl_xor(x, 8);
+        x += __shfl_xor(x, 4);
+        x += __shfl_xor(x, 2);
+        x += __shfl_xor(x, 1);
+        if (lane == 0) red[wave][r] = x;
+      }
+    }
+  };
+  gather_q(0);
+  const int wrow0 = wave, wrow1 = wave + 4;  // owned-row indices of this wave's GEMV rows
+  for (int64_t s = 0; s < nsb; s++) {
+    const int64_t j0 = s * SBK;
+    const uint64_t key = sb_key(tag0 + (uint64_t)s);
+    // operands of the owned rows (plain loads: written before this launch)
+    double mrow[2][8], crow[2][8];
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+      const int w = h ? wrow1 : wrow0;
+      const int jr = w < nown ? r0 + w : 0;
+      const double* mr = MS + (s * SBK + jr) * (int64_t)SBK;
+      const double* cr = CS + (s * SBK + jr) * (int64_t)SBK;
+#pragma unroll
+      for (int t = 0; t < 8; t++) {
+        mrow[h][t] = (w < nown) ? mr[lane + 64 * t] : 0.0;
+        crow[h][t] = (w < nown && s > 0) ? cr[lane + 64 * t] : 0.0;
+      }
+    }
+    double alv = 0.0, gav = 0.0, bo = 0.0, bbo = 0.0;
+    if (wave == 0 && lane < nown) {
+      const int64_t jm = j0 + r0 + lane;
+      alv = alpha[jm];
+      gav = gamma[jm];
+      const int64_t jc = jm < p ? jm : 0;
+      const double b0v = b[jc], b1v = b[p + jc];
+      bbo = bbar[jc];
+      bo = it_odd ? b1v : b0v;
+    }
+    // (A) δ_{s−1} -> dl (every workgroup; the owners' Q_s rows were gathered at the end of step s − 1)
+    if (s > 0) gather512(rD, s - 1, dl);
+    lds_barrier();
+    mark(s, 0);
+    if (s_fail) return;
+    // (B) owners: C_s δ_{s−1} on their rows (wave w: rows w, w + 4), then r̃_s published
+    if (nown > 0) {
+#pragma unroll
+      for (int h = 0; h < 2; h++) {
+        const int w = h ? wrow1 : wrow0;
+        double a = 0.0;
+        if (s > 0) {
+#pragma unroll
+          for (int t = 0; t < 8; t++) a = fma(crow[h][t], dl[lane + 64 * t], a);
+        }
+        a += __shfl_xor(a, 32);
+        a += __shfl_xor(a, 16);
+        a += __shfl_xor(a, 8);
+        a += __shfl_xor(a, 4);
+        a += __shfl_xor(a, 2);
+        a += __shfl_xor(a, 1);
+        if (lane == 0 && w < nown) cd[0][w] = a;
+      }
+    }
+    if (nown > 0) {
+      lds_barrier();
+      if (wave == 0 && lane < nown) {
+        const double d0 = ((red[0][lane] + red[1][lane]) + red[2][lane]) + cd[0][lane];
+        sb_put(rR, (uint32_t)(((int64_t)(s & 3) * SBK + r0 + lane) * 16), fma(d0, -alv, gav), key);
+      }
+    }
+    mark(s, 1);
+    // (C) e += X_{s−1} δ_{s−1}, then the partial dots of Q_{s+1}. Wave 3, idle in the e update's
+    // reduction: super-block s + 1's rows (DMA of step s − 1) have landed, and s + 2's go into the
+    // buffer that held s − 2's (last read by step s − 1's e update) while no gather of this
+    // workgroup runs (a gather queued behind the CU's own DMA burst is slower); waited for in step
+    // s + 1, before the dots read them
+    auto dma_next = [&]() {
+      if (wave == 3) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (s + 2 < nsb) dma_rows(s + 2);
+      }
+    };
+    if (s > 0) {
+      e_update(s - 1, dma_next);
+    } else {
+      dma_next();
+      lds_barrier();
+    }
+    mark(s, 5);
+    if (s + 1 < nsb) dots_publish(s + 1);
+    mark(s, 2);
+    // (D) owners: all of r̃_s, δ_s = M_s r̃_s on their rows, b and b̄, δ_s published; then their rows
+    // of Q_{s+1} (published in (C) by every workgroup) while δ_s travels
+    if (nown > 0) {
+      gather512(rR, s, rt);
+      lds_barrier();
+      if (s_fail) return;
+#pragma unroll
+      for (int h = 0; h < 2; h++) {
+        const int w = h ? wrow1 : wrow0;
+        double a = 0.0;
+#pragma unroll
+        for (int t = 0; t < 8; t++) a = fma(mrow[h][t], rt[lane + 64 * t], a);
+        a += __shfl_xor(a, 32);
+        a += __shfl_xor(a, 16);
+        a += __shfl_xor(a, 8);
+        a += __shfl_xor(a, 4);
+        a += __shfl_xor(a, 2);
+        a += __shfl_xor(a, 1);
+        if (lane == 0 && w < nown) red[3][w] = a;
+      }
+      lds_barrier();
+      if (wave == 0 && lane < nown) {
+        const double dlt = red[3][lane];
+        const int64_t jm = j0 + r0 + lane;
+        if (jm < p) {
+          const double bn = bo - dlt;
+          b[(it_odd ^ 1) * p + jm] = bn;
+          if (accum) bbar[jm] = bbo * ((kk - 1.0) / kk) + bn / kk;
+        }
+        sb_put(rD, (uint32_t)(((int64_t)(s & 3) * SBK + r0 + lane) * 16), dlt, key);
+      }
+      mark(s, 4);
+      if (s + 1 < nsb) gather_q(s + 1);
+    }
+    mark(s, 3);
+  }
+  // the last super-block's δ, and its e update
+  gather512(rD, nsb - 1, dl);
+  lds_barrier();
+  if (s_fail) return;
+  e_update(nsb - 1, [] {});
+  if (tid < K && i0 + tid < n) e[i0 + tid] = es[tid];
+}
+
 // σ²_b, σ²_e draws, running means of μ and the variances, next iteration (one workgroup)
 __global__ void __launch_bounds__(1024) brr_var_kernel(const double* __restrict__ b, int64_t p,
                                                        const double* __restrict__ e, int64_t n,
@@ -1645,6 +2070,7 @@ struct BrrCtx {
   Stream stream;
   DevBuf Xt, colmean, x2, e, b, bbar, r, stm, D, badm, W, Mb, alph, gamm, flg, Dt, pb, part, pout;
   DevBuf Wsb, MS, Ssc, Pb, Rt, Dl, sbcnt;  // the super-block sweep
+  DevBuf CS;                               // its look-ahead form: cross-Grams C_s = X_sᵀ X_{s−1}
   hipGraphExec_t exec = nullptr;
   hipGraph_t graph = nullptr;
   std::vector<int64_t> key;  // what the captured graph was built for
@@ -1744,7 +2170,8 @@ extern "C" int64_t gbm_debug_brr_trace(int64_t* host, int64_t cap) {
   return n;
 }
 
-// Which path the last completed fit took (0 per-launch, 1 128-block sweep, 2 super-block sweep) and
+// Which path the last completed fit took (0 per-launch, 1 128-block sweep, 2 super-block sweep, 3 its
+// look-ahead form) and
 // how many fits fell back to the per-launch path after a sweep hand-off timed out (tests).
 static std::atomic<int> g_brr_last_path{-1};
 static std::atomic<int64_t> g_brr_fallbacks{0};
@@ -1813,7 +2240,7 @@ static int brr_fit_impl(const double* X, int64_t n, int64_t p, int64_t ldx, cons
   // super-block each (1 024 <= n <= 64 CUs); GBM_BRR_SB=0 (read per call) keeps the 128-block sweep
   int cus = 0;
   GBM_HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-  bool sbmode = false;
+  bool sbmode = false, lamode = false;
   int sbK = 0, sbC = 0, sbR = 0;
   if (xs > 0.0 && sweep_mode != 0) {
     const char* ev = std::getenv("GBM_BRR_SB");
@@ -1827,6 +2254,12 @@ static int brr_fit_impl(const double* X, int64_t n, int64_t p, int64_t ldx, cons
     sbR = (int)round_up((SBK + sbC - 1) / sbC, 2);
     sbmode = !(ev && ev[0] == '0') && !(ev2 && ev2[0] == '0') && per_cu >= 1 && sbK <= SB_KMAX && sbC <= cus &&
              sbR <= SB_RMAX;
+    // the look-ahead form (brr_sweep_la_kernel) when a chunk is <= LA_KMAX individuals (n <= 48 x CUs);
+    // GBM_BRR_LA=0 (read per call) keeps brr_sweep_sb_kernel
+    const char* ev3 = std::getenv("GBM_BRR_LA");
+    int per_cu_la = 0;
+    GBM_HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu_la, brr_sweep_la_kernel<false>, 256, 0));
+    lamode = sbmode && !(ev3 && ev3[0] == '0') && per_cu_la >= 1 && sbK <= LA_KMAX;
   }
   // markers per launch: 128 with byte storage (two halves), 64 with fp64 storage; the Gram blocks
   // each launch needs (brr_gram_kernel), and the block-transposed bytes of the byte path. The
@@ -1850,9 +2283,16 @@ static int brr_fit_impl(const double* X, int64_t n, int64_t p, int64_t ldx, cons
     GBM_TRY(ensure(cx.Wsb, dev, nsb * SB_PAIRS * BK2 * BK2 * 8));
     GBM_TRY(ensure(cx.MS, dev, nsb * SBK * SBK * 8));
     GBM_TRY(ensure(cx.Ssc, dev, nsb * 6 * BK2 * BK2 * 8));
-    GBM_TRY(ensure(cx.Pb, dev, (int64_t)2 * sbC * SBK * 16));  // 16-B hand-off granules
-    GBM_TRY(ensure(cx.Rt, dev, 2 * SBK * 16));
-    GBM_TRY(ensure(cx.Dl, dev, 2 * SBK * 16));
+    GBM_TRY(ensure(cx.Pb, dev, (int64_t)4 * sbC * SBK * 16));  // 16-B hand-off granules (2 or 4 slots)
+    GBM_TRY(ensure(cx.Rt, dev, 4 * SBK * 16));
+    GBM_TRY(ensure(cx.Dl, dev, 4 * SBK * 16));
+    if (lamode) {
+      GBM_TRY(ensure(cx.CS, dev, nsb * SBK * SBK * 8));
+      if (nsb > 1) {
+        brr_xgram_kernel<<<(unsigned)((nsb - 1) * 16), 256, 0, s>>>((const double*)cx.Xt.p, npad, p, npad, (double*)cx.CS.p);
+        GBM_LAUNCH_CHECK();
+      }
+    }
     GBM_TRY(ensure(cx.sbcnt, dev, 32 * sizeof(int32_t)));
     GBM_HIP_TRY(hipMemsetAsync(cx.MS.p, 0, (size_t)(nsb * SBK * SBK * 8), s));  // blocks above the diagonal
     GBM_HIP_TRY(hipMemsetAsync(cx.sbcnt.p, 0, 32 * sizeof(int32_t), s));
@@ -1863,8 +2303,9 @@ static int brr_fit_impl(const double* X, int64_t n, int64_t p, int64_t ldx, cons
     if (std::getenv("GBM_BRR_TRACE")) {
       if (g_brr_trace) (void)hipFree(g_brr_trace);
       g_brr_trace = nullptr;
-      GBM_HIP_TRY(hipMalloc((void**)&g_brr_trace, (size_t)(2 * nsb * 12 * 8)));
-      g_brr_trace_n = 2 * nsb * 12;
+      const int64_t tn = std::max<int64_t>(2 * nsb * 12, (int64_t)sbC * nsb * 8);  // sb: 2 x 12, la: C x 8 per super-block
+      GBM_HIP_TRY(hipMalloc((void**)&g_brr_trace, (size_t)(tn * 8)));
+      g_brr_trace_n = tn;
     } else if (g_brr_trace) {
       (void)hipFree(g_brr_trace);
       g_brr_trace = nullptr;
@@ -1937,7 +2378,17 @@ static int brr_fit_impl(const double* X, int64_t n, int64_t p, int64_t ldx, cons
         brr_sb_prep_kernel<<<(unsigned)(nsb * (level == 0 ? 2 : 4)), 256, 0, s>>>(
             level, (const double*)cx.Wsb.p, (const double*)cx.alph.p, (double*)cx.MS.p, (double*)cx.Ssc.p);
       int32_t* cn = (int32_t*)cx.sbcnt.p + 24;  // the error cell (zeroed at setup)
-      if (g_brr_trace)
+      if (lamode && g_brr_trace)
+        brr_sweep_la_kernel<true><<<(unsigned)sbC, 256, 0, s>>>(
+            (const uint8_t*)cx.D.p, npad, n, p, xs, (const double*)cx.MS.p, (const double*)cx.CS.p, nsb, sbK, sbR,
+            (double*)cx.Pb.p, (double*)cx.Rt.p, (double*)cx.Dl.p, cn, (double*)cx.b.p, (double*)cx.bbar.p,
+            (const double*)cx.alph.p, (const double*)cx.gamm.p, (double*)cx.e.p, stp, g_brr_trace);
+      else if (lamode)
+        brr_sweep_la_kernel<false><<<(unsigned)sbC, 256, 0, s>>>(
+            (const uint8_t*)cx.D.p, npad, n, p, xs, (const double*)cx.MS.p, (const double*)cx.CS.p, nsb, sbK, sbR,
+            (double*)cx.Pb.p, (double*)cx.Rt.p, (double*)cx.Dl.p, cn, (double*)cx.b.p, (double*)cx.bbar.p,
+            (const double*)cx.alph.p, (const double*)cx.gamm.p, (double*)cx.e.p, stp, nullptr);
+      else if (g_brr_trace)
         brr_sweep_sb_kernel<true><<<(unsigned)sbC, 256, 0, s>>>(
             (const uint8_t*)cx.D.p, npad, n, p, xs, (const double*)cx.MS.p, nsb, sbK, sbR, (double*)cx.Pb.p,
             (double*)cx.Rt.p, (double*)cx.Dl.p, cn, (double*)cx.b.p, (double*)cx.bbar.p, (const double*)cx.alph.p,
@@ -1991,7 +2442,8 @@ static int brr_fit_impl(const double* X, int64_t n, int64_t p, int64_t ldx, cons
                                     (int64_t)(uintptr_t)cx.stm.p, sbmode ? 1 : 0, sbK, sbC, sbR,
                                     (int64_t)(uintptr_t)cx.MS.p, (int64_t)(uintptr_t)cx.Wsb.p, (int64_t)(uintptr_t)cx.Ssc.p,
                                     (int64_t)(uintptr_t)cx.Pb.p, (int64_t)(uintptr_t)cx.Rt.p, (int64_t)(uintptr_t)cx.Dl.p,
-                                    (int64_t)(uintptr_t)cx.sbcnt.p, (int64_t)(uintptr_t)g_brr_trace};
+                                    (int64_t)(uintptr_t)cx.sbcnt.p, (int64_t)(uintptr_t)g_brr_trace, lamode ? 1 : 0,
+                                    (int64_t)(uintptr_t)cx.CS.p};
   int rc = GBM_OK;
   if (cx.key != key) {
     cx.drop_graph();
@@ -2030,7 +2482,7 @@ static int brr_fit_impl(const double* X, int64_t n, int64_t p, int64_t ldx, cons
       return fail(GBM_E_HIP, "gbm_brr_fit: a sweep hand-off between workgroups timed out");
     }
   }
-  g_brr_last_path.store(sbmode ? 2 : sweep ? 1 : 0);
+  g_brr_last_path.store(lamode ? 3 : sbmode ? 2 : sweep ? 1 : 0);
   BrrState fin{};
   GBM_HIP_TRY(hipMemcpyAsync(&fin, cx.stm.p, sizeof(BrrState), hipMemcpyDeviceToHost, s));
   GBM_HIP_TRY(hipMemcpyAsync(b_hat_out + 1, cx.bbar.p, p * 8, hipMemcpyDeviceToHost, s));
