@@ -15,13 +15,15 @@
 // The C tile is read once and written once (the right-looking trailing updates re-read and
 // re-write the whole trailing matrix at every panel group, which made them HBM/MALL-bound).
 //
-// Scheduling. Workgroups (one per CU) take tiles from one atomic counter in row-major order, except
-// that each row's right neighbour (i, i + 1) comes before its diagonal tile (i, i). A tile waits
-// only for tiles of earlier rows, for its row's diagonal tile (tiles right of the neighbour), or
-// for the neighbour's partial (the diagonal tile): every one precedes it in that order and was
-// therefore taken by a running workgroup, so the dependency chain always ends in a running
-// workgroup, whatever the residency (one resident workgroup suffices): the launch cannot
-// deadlock. Waits are bounded (~1 s, info = −1, as in chol_device.h).
+// Scheduling (round 3). Workgroup 0 is the chain: it factors the diagonal tiles one after the
+// other, solves each right neighbour and applies the next diagonal tile's last update from LDS,
+// so the chain pays no hand-off of its own (chol_flow_kernel below). The other workgroups (one per
+// CU) take the remaining tiles from one atomic counter in row-major order (a row's right neighbour
+// before its diagonal tile); a diagonal or neighbour task hands the chain its accumulated partial.
+// A worker waits only for tiles of earlier rows or for the chain's step of its row; the chain's
+// step i waits only for the partials of (i, i + 1) and (i + 1, i + 1), which wait only for rows < i
+// and are dequeued first in row i: the launch completes with the chain and one resident worker. Waits are bounded (~1 s,
+// info = −1, as in chol_device.h).
 //
 // Hand-off between workgroups (MI355X: per-XCD L2s are not coherent): every byte another
 // workgroup of this launch reads — U tiles in G, Ld, Dinv — is stored write-through (`sc1`
@@ -60,6 +62,10 @@ __device__ __forceinline__ void st2(__amdgpu_buffer_rsrc_t r, uint32_t voff, dbl
 __device__ __forceinline__ void st1(__amdgpu_buffer_rsrc_t r, uint32_t voff, double v) {
   __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2, v), r, (int)voff, 0, kSc1);
 }
+
+// a workgroup barrier for LDS data only (__syncthreads also waits for every outstanding global load
+// and store of the calling wave: the write-through stores of a hand-off would sit on the chain)
+__device__ __forceinline__ void lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
 // tile flags: kPartial = the accumulated (not yet solved) right neighbour of a diagonal tile,
 // handed to the diagonal task; kFinal = the tile's U (or, on the diagonal, Ld + Dinv) is stored
@@ -111,9 +117,13 @@ __device__ __forceinline__ bool wave_ready2(const int32_t* fa, const int32_t* fb
 // neither the LDS round trip nor those updates sit on the pivot chain.
 // Between leaves all waves update the block's remaining upper 16x16 tiles by MFMA. Leaves U in X
 // (zeros below the diagonal); bc = 48 doubles of LDS scratch. Returns the first failing column or -1.
+// idle(kb): run by waves 1-3 beside leaf kb's steps, once their updates of the previous leaf are
+// done (rows < 16 kb of X are final then); row_out(kb, r, v): wave 0's final row r of U (lane =
+// column 16 kb + lane, valid lanes < 64 − 16 kb), e.g. to store it as soon as it is final.
+template <typename Idle, typename RowOut>
 __device__ __forceinline__ int factor_block_inv(double* X, double* bc, double* Dl, int tid,
                                                 __amdgpu_buffer_rsrc_t rDi, uint32_t dinv_base,
-                                                int64_t* tt = nullptr) {
+                                                int64_t* tt, Idle&& idle, RowOut&& row_out) {
   const int lane = tid & 63, wave = tid >> 6;
 #pragma unroll 1
   for (int kb = 0; kb < 4; kb++) {
@@ -172,21 +182,34 @@ __device__ __forceinline__ int factor_block_inv(double* X, double* bc, double* D
       if (tt) tt[kb] = (int64_t)__builtin_amdgcn_s_memrealtime();
       if (lane < ncols) {
 #pragma unroll
-        for (int t = 0; t < 16; t++) X[(o + t) * PS + cc] = (lane < 16 && t > lane) ? 0.0 : x[t];
+        for (int t = 0; t < 16; t++) {
+          const double v = (lane < 16 && t > lane) ? 0.0 : x[t];
+          X[(o + t) * PS + cc] = v;
+          row_out(kb, o + t, v);
+        }
       }
       if (lane < 16) {
-        const uint32_t b = dinv_base + (uint32_t)((kb * 256 + lane * 16) * 8);
 #pragma unroll
         for (int e = 0; e < 16; e += 2) {
           dbl2 v;
           v.x = y[e];
           v.y = y[e + 1];
-          st2(rDi, b + e * 8, v);
           *reinterpret_cast<dbl2*>(&Dl[kb * 256 + lane * 16 + e]) = v;
         }
       }
+      // Dinv (write-through) from Dl: two coalesced 1 KB stores (lane l's 128 B column stored by 16
+      // lanes as 8 scattered pieces cost ~1 µs)
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+      for (int q = 0; q < 2; q++) {
+        const int e = (q * 64 + lane) * 2;
+        st2(rDi, dinv_base + (uint32_t)((kb * 256 + e) * 8), *reinterpret_cast<const dbl2*>(&Dl[kb * 256 + e]));
+      }
     }
-    __syncthreads();
+    if (tt && kb == 1) tt[12] = (int64_t)__builtin_amdgcn_s_memrealtime();
+    if (wave >= 1) idle(kb);
+    lds_sync();
+    if (tt && kb == 1) tt[13] = (int64_t)__builtin_amdgcn_s_memrealtime();
     // update of the block's remaining upper 16x16 tiles (b <= a < m) by leaf kb's rows: the first
     // tile row (the next leaf's rows) by waves 1..m, then wave 0 goes on with the next leaf while
     // waves 1.. update the rest (done before the next leaf's closing barrier, i.e. before any
@@ -196,7 +219,7 @@ __device__ __forceinline__ int factor_block_inv(double* X, double* bc, double* D
       const int c0 = o + 16 + (wave - 1) * 16;
       mfma_tile_sub_t(X, o + 16, c0, X, o + 16, X, c0, o, 4, lane);
     }
-    __syncthreads();
+    lds_sync();
     if (wave >= 1) {
       for (int t = wave - 1; t < m * (m - 1) / 2; t += 3) {
         int a = 1;
@@ -210,13 +233,16 @@ __device__ __forceinline__ int factor_block_inv(double* X, double* bc, double* D
   }
   // (the lower parts of the diagonal 16x16 blocks hold leftovers of the MFMA updates; nothing
   // reads below the diagonal of a factored block)
-  __syncthreads();
+  lds_sync();
   const double dg = X[lane * PS + lane];
   const unsigned long long bm = __ballot(!(dg > 0.0) || !isfinite(dg));
   return bm ? (int)__builtin_ctzll(bm) : -1;
 }
 
-// task t (row-major over the upper tile triangle) -> tile (i, j)
+// task t -> tile (i, j): row-major over the upper tile triangle, except that row i's first two
+// slots hold its right neighbour (i, i + 1) and the NEXT row's diagonal tile (i + 1, i + 1), the two
+// partials the chain's step i waits for; so both are dequeued before any tile of row i that waits
+// for that step. (i, j) = (−1, −1): nothing to do (slot (nb − 1, nb)); A_00 needs no task.
 __device__ __forceinline__ void task_tile(int t, int nbc, int& i, int& j) {
   auto start = [nbc](int r) { return r * nbc - r * (r - 1) / 2; };
   const double b = 2.0 * nbc + 1.0;
@@ -226,32 +252,46 @@ __device__ __forceinline__ void task_tile(int t, int nbc, int& i, int& j) {
   while (r + 1 < nbc && start(r + 1) <= t) r++;
   i = r;
   j = r + (t - start(r));
-  // within a row the right neighbour (i, i + 1) is dequeued before the diagonal tile (i, i), which
-  // waits for the neighbour's partial: every wait then targets a task taken earlier
-  if (i + 1 < nbc) {
-    if (j == i) j = i + 1;
-    else if (j == i + 1) j = i;
+  const int nb = nbc - 1;
+  if (j == i) {
+    if (i < nb) j = i + 1;  // the right neighbour; slot (nb, nb) stays the Schur block
+  } else if (j == i + 1) {
+    if (i + 1 < nb) {
+      i = i + 1;  // the next row's diagonal tile
+      j = i;
+    } else {
+      i = j = -1;
+    }
   }
 }
 
-// kTrace: per-task timestamps (s_memrealtime, 100 MHz) into trace[t * 24 ...] for the timeline tool
+// kTrace: per-task timestamps (s_memrealtime, 100 MHz) into trace[t * 24 ...] for the timeline tool;
+// the chain workgroup's steps at trace[(ntasks + i) * 24 ...]
 //
-// Task kinds (tile (i, j)):
-//   diagonal (i == j < nb): k-loop; U_ii = chol(A_ii) with the 16x16 inverses (Ld, Dinv); then the
-//     right neighbour's U_i,i+1 = U_ii⁻ᵀ A_i,i+1 from the partial that the neighbour task handed
-//     over (waves 1-3 fetch it while wave 0 factors), so that the next diagonal tile's last
-//     update waits for one hand-off, not two; publishes (i, i) and (i, i+1) final.
-//   right neighbour (j == i + 1): k-loop, then the accumulated tile is stored as a partial.
-//   other (j > i + 1): k-loop; once (i, i) is final, U_ij = U_ii⁻ᵀ A_ij.
+// Workgroup 0 is the CHAIN: it factors every diagonal tile in turn and keeps the chain's data in LDS.
+// Step i: U_ii = chol(A_ii) with its 16x16 inverses (Ld, Dinv); meanwhile its idle waves fetch the
+// right neighbour's partial A_i,i+1 (all updates k < i) and the next diagonal tile's partial
+// A_i+1,i+1 (all updates k < i); U_i,i+1 = U_ii⁻ᵀ A_i,i+1 (all MFMA, in LDS), stored and published
+// with (i, i); then the next diagonal tile's last update A_i+1,i+1 −= U_i,i+1ᵀ U_i,i+1 straight
+// from LDS — so the chain never waits for its own hand-off. The other workgroups take tasks from
+// the queue (row-major; row i's right neighbour and row i + 1's diagonal tile first, task_tile):
+//   diagonal (i == j < nb, i >= 1): k-loop over k < i − 1, stored as a partial for the chain;
+//   right neighbour (j == i + 1): k-loop over k < i, stored as a partial for the chain;
+//   other (j > i + 1): k-loop; once (i, i) is final, U_ij = U_ii⁻ᵀ A_ij;
 //   Schur (i == j == nb): k-loop; −WᵀW for the later kernels.
+// Deadlock freedom: the chain's step i waits only for the partials of (i, i + 1) and (i + 1, i + 1),
+// which wait only for tiles of rows < i and are dequeued before every other tile of row i; every
+// worker wait targets the chain's earlier steps or a task dequeued earlier. So the launch completes
+// with the chain and ONE resident worker.
 template <bool kTrace>
 __global__ void __launch_bounds__(256, 1)
 chol_flow_kernel(double* __restrict__ G, int64_t ld, int nbc, double* __restrict__ Ld, double* __restrict__ Dinv,
                  int32_t* __restrict__ queue, int32_t* __restrict__ flags, int32_t* __restrict__ info,
                  int64_t* __restrict__ trace) {
-  // ≈ 90 KB: one workgroup per CU (the chain's serial steps then share no SIMD with other tiles)
+  // ≈ 130 KB: one workgroup per CU (the chain's serial steps then share no SIMD with other tiles)
   __shared__ __attribute__((aligned(16))) double X[FT * PS];
   __shared__ __attribute__((aligned(16))) double X2[FT * PS];
+  __shared__ __attribute__((aligned(16))) double X3[FT * PS];
   __shared__ __attribute__((aligned(16))) double Dl[4 * 256];
   __shared__ double bcast[48];
   __shared__ int s_task;
@@ -286,6 +326,173 @@ chol_flow_kernel(double* __restrict__ G, int64_t ld, int nbc, double* __restrict
     }
   };
 
+  if (blockIdx.x == 0) {
+    // ================================ the chain ================================
+    // A_00 has no update: straight from G (written before this launch)
+    for (int e = tid; e < FT * FT / 2; e += 256) {
+      const int r = e >> 5, c2 = (e & 31) * 2;
+      *reinterpret_cast<dbl2*>(&X[r * PS + c2]) = *reinterpret_cast<const dbl2*>(G + (int64_t)r * ld + c2);
+    }
+    lds_sync();
+    double* Xa = X;   // A_ii, then U_ii
+    double* Xn = X3;  // the next diagonal tile
+    for (int i = 0; i < nb; i++) {
+      const int64_t i0 = (int64_t)i * FT, j0 = i0 + FT;
+      const bool next_diag = i + 1 < nb;
+      // trace: 0 start, 1-4 leaf ends, 5-7 leaf update ends, 8 factored, 9 neighbour partial seen,
+      // 10 neighbour solved, 11 next tile updated, 12 published
+      int64_t ct[16] = {};
+      if (kTrace) ct[0] = (int64_t)__builtin_amdgcn_s_memrealtime();
+      __builtin_amdgcn_s_setprio(2);
+      // waves 1-3, beside the last leaf: the neighbour's partial -> X2, the next diagonal tile's -> Xn
+      // waves 1-3: the neighbour's partial A_i,i+1 -> X2 and (next_diag) the next diagonal tile's
+      // A_i+1,i+1 -> Xn (sc1: other workgroups' partials), 11 16-byte pieces of each per thread, the
+      // loads of both tiles in flight before any LDS write
+      auto fetch_partials = [&]() {
+        const int t = tid - 64;
+        const __amdgpu_buffer_rsrc_t rG = rsrc(G + i0 * ld, gbytes_rowblk);
+        const __amdgpu_buffer_rsrc_t rG1 = rsrc(G + j0 * ld, gbytes_rowblk);
+        const int32_t* fn = flags + (int64_t)i * nbc + i + 1;
+        const int32_t* fd = flags + (int64_t)(i + 1) * nbc + i + 1;
+        dbl2 vn[11], vd[11];
+        wave_wait2(fn, fn, info, lane, kPartial);
+#pragma unroll
+        for (int q = 0; q < 11; q++) {
+          const int e = t + q * 192;
+          if (e < FT * FT / 2) vn[q] = ld2(rG, (uint32_t)(((int64_t)(e >> 5) * ld + j0 + 2 * (e & 31)) * 8), 0);
+        }
+        if (next_diag) {
+          wave_wait2(fd, fd, info, lane, kPartial);
+#pragma unroll
+          for (int q = 0; q < 11; q++) {
+            const int e = t + q * 192;
+            if (e < FT * FT / 2) vd[q] = ld2(rG1, (uint32_t)(((int64_t)(e >> 5) * ld + j0 + 2 * (e & 31)) * 8), 0);
+          }
+        }
+#pragma unroll
+        for (int q = 0; q < 11; q++) {
+          const int e = t + q * 192;
+          if (e < FT * FT / 2) {
+            *reinterpret_cast<dbl2*>(&X2[(e >> 5) * PS + 2 * (e & 31)]) = vn[q];
+            if (next_diag) *reinterpret_cast<dbl2*>(&Xn[(e >> 5) * PS + 2 * (e & 31)]) = vd[q];
+          }
+        }
+      };
+      // waves 1-3 beside the leaves: leaf 0, the previous step's transposed copy of U_i−1,i (X2)
+      // below the diagonal of G (read only by later kernels); leaf kb >= 1, U_ii's final rows of
+      // leaf kb − 1 -> Ld (write-through: the row's other tiles read them); leaf 3, also the
+      // neighbour's partial A_i,i+1 -> X2 and the next diagonal tile's partial -> Xn
+      auto idle = [&](int kb) {
+        const int t = tid - 64;
+        if (kb == 0 && i > 0) {
+          for (int e = t; e < FT * 8; e += 192) {  // 64 rows x 8 pieces of 8 doubles
+            const int row = e >> 3, piece = e & 7;
+            double* dl = G + (i0 + row) * ld + (i0 - FT) + piece * 8;
+#pragma unroll
+            for (int u = 0; u < 8; u += 2) {
+              dbl2 v;
+              v.x = X2[(piece * 8 + u) * PS + row];
+              v.y = X2[(piece * 8 + u + 1) * PS + row];
+              *reinterpret_cast<dbl2*>(dl + u) = v;
+            }
+          }
+        }
+        if (kb >= 1) {
+          // rows 16 (kb − 1) .. + 15 from column 16 (kb − 1): w pieces of 16 bytes per row
+          const int rb = kb - 1, w = 32 - 8 * rb;
+          for (int e = t; e < 16 * w; e += 192) {
+            const int row = rb * 16 + e / w, col = rb * 16 + 2 * (e % w);
+            st2(rLd, (uint32_t)(((i0 + row) * CNB + col) * 8), *reinterpret_cast<const dbl2*>(&Xa[row * PS + col]));
+          }
+        }
+        if (kb == 3) fetch_partials();
+      };
+      // wave 0: the last leaf's rows of U_ii -> Ld
+      auto row_out = [&](int kb, int r, double v) {
+        if (kb == 3) st1(rLd, (uint32_t)(((i0 + r) * CNB + 48 + lane) * 8), v);
+      };
+      // ---- U_ii = chol(A_ii) -> Ld, its 16x16 diagonal inverses -> Dinv (and Dl)
+      const int bad = factor_block_inv(Xa, bcast, Dl, tid, rDi, (uint32_t)((i0 / 16) * 256 * 8), kTrace ? ct + 1 : nullptr,
+                                       idle, row_out);
+      if (tid == 0 && bad >= 0) atomicCAS(info, 0, (int32_t)(i0 + bad + 1));
+      if (kTrace) ct[8] = (int64_t)__builtin_amdgcn_s_memrealtime();
+      // ---- publish (i, i): Ld and Dinv were stored during the factor
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      lds_sync();
+      if (tid == 0) __hip_atomic_store(flags + (int64_t)i * nbc + i, kFinal, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      // ---- the right neighbour: U_i,i+1 = U_ii⁻ᵀ A_i,i+1 (all MFMA, operands in LDS); each 16-row
+      // block of a wave's columns is stored (write-through) as soon as it is final
+      const __amdgpu_buffer_rsrc_t rN = rsrc(G + i0 * ld, gbytes_rowblk);
+      panel_chunk_solve(
+          X2, Xa, [&](int rb, int ks) { return Dl[rb * 256 + (ks * 4 + fr) * 16 + fc]; }, lane, wave,
+          [&](int rb, const d4& acc) {
+#pragma unroll
+            for (int r = 0; r < 4; r++)
+              st1(rN, (uint32_t)(((int64_t)(rb * 16 + fr + 4 * r) * ld + j0 + wave * 16 + fc) * 8), acc[r]);
+          });
+      lds_sync();
+      if (kTrace) ct[10] = (int64_t)__builtin_amdgcn_s_memrealtime();
+      // ---- the next diagonal tile's last update, k = i, from LDS (the workers' k-loop step: same
+      // operands, order and lane layout, so the same bits)
+      if (next_diag && !(wr == 1 && wc == 0)) {
+        d4 acc[2][2];
+#pragma unroll
+        for (int m = 0; m < 2; m++)
+#pragma unroll
+          for (int r = 0; r < 4; r++) {
+            const int row = 32 * wr + 2 * (fr + 4 * r) + m;
+            const dbl2 v = *reinterpret_cast<const dbl2*>(&Xn[row * PS + 32 * wc + 2 * fc]);
+            acc[m][0][r] = v.x;
+            acc[m][1][r] = v.y;
+          }
+#pragma unroll
+        for (int ks = 0; ks < 16; ks++) {
+          const int kk = ks * 4 + fr;
+          const dbl2 av = *reinterpret_cast<const dbl2*>(&X2[kk * PS + 32 * wr + 2 * fc]);
+          const dbl2 bv = *reinterpret_cast<const dbl2*>(&X2[kk * PS + 32 * wc + 2 * fc]);
+          const double na0 = -av.x, na1 = -av.y;
+          acc[0][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(na0, bv.x, acc[0][0], 0, 0, 0);
+          acc[0][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(na0, bv.y, acc[0][1], 0, 0, 0);
+          acc[1][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(na1, bv.x, acc[1][0], 0, 0, 0);
+          acc[1][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(na1, bv.y, acc[1][1], 0, 0, 0);
+        }
+#pragma unroll
+        for (int m = 0; m < 2; m++)
+#pragma unroll
+          for (int r = 0; r < 4; r++) {
+            const int row = 32 * wr + 2 * (fr + 4 * r) + m;
+            dbl2 v;
+            v.x = acc[m][0][r];
+            v.y = acc[m][1][r];
+            *reinterpret_cast<dbl2*>(&Xn[row * PS + 32 * wc + 2 * fc]) = v;
+          }
+      }
+      // ---- publish (i, i + 1): every storing wave drains its write-through stores (the update above
+      // ran meanwhile), then one flag store
+      if (kTrace) ct[11] = (int64_t)__builtin_amdgcn_s_memrealtime();
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      lds_sync();
+      if (tid == 0)
+        __hip_atomic_store(flags + (int64_t)i * nbc + i + 1, kFinal, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (kTrace) ct[12] = (int64_t)__builtin_amdgcn_s_memrealtime();
+      if (i + 1 == nb) store_lower(X2, i0, j0);  // no next step to store it beside
+      __builtin_amdgcn_s_setprio(0);
+      if (kTrace && tid == 0) {
+        int64_t* o = trace + (int64_t)(ntasks + i) * 24;
+        o[0] = i;
+        o[1] = i;
+        o[2] = -1;
+#pragma unroll
+        for (int e = 0; e < 16; e++) o[3 + e] = ct[e];
+      }
+      double* t = Xa;
+      Xa = Xn;
+      Xn = t;
+    }
+    return;
+  }
+
+  // ================================ the workers ================================
   for (;;) {
     if (tid == 0) s_task = atomicAdd(queue, 1);
     __syncthreads();
@@ -295,11 +502,17 @@ chol_flow_kernel(double* __restrict__ G, int64_t ld, int nbc, double* __restrict
     task_tile(t, nbc, i, j);
     i = __builtin_amdgcn_readfirstlane(i);
     j = __builtin_amdgcn_readfirstlane(j);
+    if (i < 0) {
+      __syncthreads();  // every wave has read s_task before it is rewritten
+      continue;
+    }
     const bool diag = i == j;
     const bool nbr = j == i + 1;
-    // the factorisation chain runs through the diagonal tiles and their right neighbours
-    if (diag || nbr) __builtin_amdgcn_s_setprio(2);
+    // the chain waits for the diagonal tiles and right neighbours, which wait for the (i, i + 2) tiles
+    if ((diag && i < nb) || nbr || j == i + 2) __builtin_amdgcn_s_setprio(2);
     const int64_t i0 = (int64_t)i * FT, j0 = (int64_t)j * FT;
+    // a diagonal tile's last update (k = i − 1) is the chain's
+    const int kend = (diag && i < nb) ? i - 1 : i;
     int64_t tr[16] = {};
     if (kTrace) tr[0] = (int64_t)__builtin_amdgcn_s_memrealtime();
 
@@ -319,7 +532,7 @@ chol_flow_kernel(double* __restrict__ G, int64_t ld, int nbc, double* __restrict
     // ---- A_ij −= Σ_k U_kiᵀ U_kj, 64-deep steps in two 32-deep halves (8 k-steps of 4); the next
     // half's loads are in flight while this one's MFMAs run. The lower quadrant of a diagonal (or
     // Schur) tile is never read: that wave skips the loop.
-    if (i > 0 && !(diag && wr == 1 && wc == 0)) {
+    if (kend > 0 && !(diag && wr == 1 && wc == 0)) {
       const uint32_t offA = (uint32_t)(((int64_t)fr * ld + i0 + 32 * wr + 2 * fc) * 8);
       const uint32_t offB = (uint32_t)(((int64_t)fr * ld + j0 + 32 * wc + 2 * fc) * 8);
       const uint32_t kstep = (uint32_t)(4 * ld * 8);
@@ -348,9 +561,9 @@ chol_flow_kernel(double* __restrict__ G, int64_t ld, int nbc, double* __restrict
       wave_wait2(fa(0), fb(0), info, lane);
       issue(a0, b0, 0, 0);
       issue(a1, b1, 0, 1);
-      for (int k = 0; k < i; k++) {
+      for (int k = 0; k < kend; k++) {
         mfma(a0, b0);
-        const bool more = k + 1 < i;
+        const bool more = k + 1 < kend;
         if (more) {
           wave_wait2(fa(k + 1), fb(k + 1), info, lane);
           issue(a0, b0, k + 1, 0);
@@ -363,10 +576,9 @@ chol_flow_kernel(double* __restrict__ G, int64_t ld, int nbc, double* __restrict
 
     int32_t publish = kFinal;
     const double* low = nullptr;  // a solved tile whose lower copy is still to be stored
-    int64_t lj0 = j0;
-    if (nbr && i < nb) {
-      // ---- right neighbour: hand the accumulated tile to the diagonal task (sc1, straight from
-      // the accumulators into the tile's place in G; the diagonal task overwrites it with U)
+    if ((nbr && i < nb) || (diag && i < nb)) {
+      // ---- a partial for the chain (right neighbour: all k < i; diagonal: all k < i − 1), sc1,
+      // straight from the accumulators into the tile's place in G (the chain stores U over it)
       const __amdgpu_buffer_rsrc_t rG = rsrc(G + i0 * ld, gbytes_rowblk);
 #pragma unroll
       for (int m = 0; m < 2; m++)
@@ -393,61 +605,7 @@ chol_flow_kernel(double* __restrict__ G, int64_t ld, int nbc, double* __restrict
         }
       __syncthreads();
       if (kTrace) tr[2] = (int64_t)__builtin_amdgcn_s_memrealtime();
-
-      if (diag && i < nb) {
-        // ---- U_ii = chol(A_ii) -> Ld (row-major, zeros below), its 16x16 diagonal inverses ->
-        // Dinv (and Dl)
-        const int bad = factor_block_inv(X, bcast, Dl, tid, rDi, (uint32_t)((i0 / 16) * 256 * 8), kTrace ? tr + 6 : nullptr);
-        if (tid == 0 && bad >= 0) atomicCAS(info, 0, (int32_t)(i0 + bad + 1));
-        if (kTrace) tr[3] = (int64_t)__builtin_amdgcn_s_memrealtime();
-        // the neighbour's partial (its last update ran beside this factor; loads issued before the
-        // Ld stores so that waiting for them does not wait for the stores)
-        const int32_t* fn = flags + (int64_t)i * nbc + i + 1;
-        wave_wait2(fn, fn, info, lane, kPartial);
-        if (kTrace) tr[13] = (int64_t)__builtin_amdgcn_s_memrealtime();
-        dbl2 pv[8];
-        {
-          const __amdgpu_buffer_rsrc_t rG = rsrc(G + i0 * ld, gbytes_rowblk);
-#pragma unroll
-          for (int q = 0; q < 8; q++) {
-            const int e = tid + q * 256;
-            pv[q] = ld2(rG, (uint32_t)(((int64_t)(e >> 5) * ld + j0 + FT + 2 * (e & 31)) * 8), 0);
-          }
-        }
-        {
-          // Ld: the six off-diagonal 16x16 blocks that the row's other solves read, write-through
-          // now; the diagonal blocks (read only by later kernels) after the flags
-          const int row = tid >> 2, quarter = tid & 3;
-          const uint32_t base = (uint32_t)(((i0 + row) * CNB + quarter * 16) * 8);
-          if (quarter > (row >> 4)) {
-#pragma unroll
-            for (int e = 0; e < 16; e += 2)
-              st2(rLd, base + e * 8, *reinterpret_cast<const dbl2*>(&X[row * PS + quarter * 16 + e]));
-          }
-        }
-#pragma unroll
-        for (int q = 0; q < 8; q++) {
-          const int e = tid + q * 256;
-          *reinterpret_cast<dbl2*>(&X2[(e >> 5) * PS + 2 * (e & 31)]) = pv[q];
-        }
-        __syncthreads();
-        if (kTrace) tr[14] = (int64_t)__builtin_amdgcn_s_memrealtime();
-        // ---- the right neighbour: U_i,i+1 = U_ii⁻ᵀ A_i,i+1 (all MFMA, operands in LDS); each
-        // 16-row block of a wave's columns is stored (write-through) as soon as it is final, so
-        // the hand-off's stores overlap the rest of the solve
-        const __amdgpu_buffer_rsrc_t rN = rsrc(G + i0 * ld, gbytes_rowblk);
-        panel_chunk_solve(
-            X2, X, [&](int rb, int ks) { return Dl[rb * 256 + (ks * 4 + fr) * 16 + fc]; }, lane, wave,
-            [&](int rb, const d4& a) {
-#pragma unroll
-              for (int r = 0; r < 4; r++)
-                st1(rN, (uint32_t)(((int64_t)(rb * 16 + fr + 4 * r) * ld + j0 + FT + wave * 16 + fc) * 8), a[r]);
-            });
-        __syncthreads();
-        if (kTrace) tr[15] = (int64_t)__builtin_amdgcn_s_memrealtime();
-        low = X2;
-        lj0 = j0 + FT;
-      } else if (!diag) {
+      if (!diag) {
         // ---- U_ij = U_ii⁻ᵀ A_ij once U_ii is final. Operands of U_ii and its 16x16 inverses come
         // straight from the sc1-stored Ld / Dinv into registers; X (LDS) is solved in place:
         //   X_rb <- (D_rb⁻¹)ᵀ (X_rb − U[0:o, rb]ᵀ X[0:o]),  rb = 0..3, wave w on columns 16w..16w+15
@@ -474,19 +632,19 @@ chol_flow_kernel(double* __restrict__ G, int64_t ld, int nbc, double* __restrict
         for (int rb = 0; rb < 4; rb++) {
           const int o = rb * 16;
           if (rb > 0) {
-            d4 s = (d4){0.0, 0.0, 0.0, 0.0};
+            d4 sacc = (d4){0.0, 0.0, 0.0, 0.0};
 #pragma unroll
             for (int ks = 0; ks < 4 * rb; ks++)
-              s = __builtin_amdgcn_mfma_f64_16x16x4f64(u[c++], X[(ks * 4 + fr) * PS + cw + fc], s, 0, 0, 0);
+              sacc = __builtin_amdgcn_mfma_f64_16x16x4f64(u[c++], X[(ks * 4 + fr) * PS + cw + fc], sacc, 0, 0, 0);
 #pragma unroll
-            for (int r = 0; r < 4; r++) X[(o + fr + 4 * r) * PS + cw + fc] -= s[r];
+            for (int r = 0; r < 4; r++) X[(o + fr + 4 * r) * PS + cw + fc] -= sacc[r];
           }
-          d4 s = (d4){0.0, 0.0, 0.0, 0.0};
+          d4 sacc = (d4){0.0, 0.0, 0.0, 0.0};
 #pragma unroll
           for (int ks = 0; ks < 4; ks++)
-            s = __builtin_amdgcn_mfma_f64_16x16x4f64(di[rb * 4 + ks], X[(o + ks * 4 + fr) * PS + cw + fc], s, 0, 0, 0);
+            sacc = __builtin_amdgcn_mfma_f64_16x16x4f64(di[rb * 4 + ks], X[(o + ks * 4 + fr) * PS + cw + fc], sacc, 0, 0, 0);
 #pragma unroll
-          for (int r = 0; r < 4; r++) X[(o + fr + 4 * r) * PS + cw + fc] = s[r];
+          for (int r = 0; r < 4; r++) X[(o + fr + 4 * r) * PS + cw + fc] = sacc[r];
         }
         __syncthreads();
         store_upper(X, i0, j0);
@@ -500,25 +658,12 @@ chol_flow_kernel(double* __restrict__ G, int64_t ld, int nbc, double* __restrict
           *reinterpret_cast<dbl2*>(d + e) = *reinterpret_cast<const dbl2*>(&X[row * PS + quarter * 16 + e]);
       }
     }
-    // ---- publish: every storing wave drains its write-through stores, then one flag store (a
-    // diagonal task also publishes its right neighbour, whose U it stored)
+    // ---- publish: every storing wave drains its write-through stores, then one flag store
     if (kTrace) tr[4] = (int64_t)__builtin_amdgcn_s_memrealtime();
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (tid == 0) {
-      __hip_atomic_store(flags + (int64_t)i * nbc + j, publish, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (diag && i < nb)
-        __hip_atomic_store(flags + (int64_t)i * nbc + j + 1, kFinal, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    if (low) store_lower(low, i0, lj0);
-    if (diag && i < nb) {
-      const int row = tid >> 2, quarter = tid & 3;
-      if (quarter == (row >> 4)) {
-        double* d = Ld + (i0 + row) * CNB + quarter * 16;
-#pragma unroll
-        for (int e = 0; e < 16; e += 2) *reinterpret_cast<dbl2*>(d + e) = *reinterpret_cast<const dbl2*>(&X[row * PS + quarter * 16 + e]);
-      }
-    }
+    if (tid == 0) __hip_atomic_store(flags + (int64_t)i * nbc + j, publish, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (low) store_lower(low, i0, j0);
     __builtin_amdgcn_s_setprio(0);
     if (kTrace && tid == 0) {
       tr[5] = (int64_t)__builtin_amdgcn_s_memrealtime();
@@ -571,21 +716,24 @@ int launch_chol_flow(double* G, int64_t ldg, int64_t gdim, double* Ld, double* D
   if (nbc < 2 || (int64_t)FT * ldg * 8 > 0x7fffffff || nbc * nbc > 0x3fffffff)
     return fail(GBM_E_ARG, "dataflow Cholesky: matrix too large for 32-bit buffer offsets");
   GBM_HIP_TRY(hipMemsetAsync(flag_block, 0, (size_t)chol_flow_flag_bytes(gdim), s));
-  // one workgroup per CU; GBM_CHOL_FLOW_WGS (re-read per solve) caps the grid: with 1 the whole
-  // factorisation runs on one workgroup, which checks that no wait targets a later task
+  // one workgroup per CU; GBM_CHOL_FLOW_WGS (re-read per solve) caps the workers: with 1, one worker
+  // runs every tile task in dequeue order beside the chain, which checks that no wait targets a later
+  // task
   const char* ew = getenv("GBM_CHOL_FLOW_WGS");
-  const int64_t slots = ew && atoll(ew) > 0 ? atoll(ew) : flow_cus();
-  const unsigned grid = (unsigned)(ntasks < slots ? ntasks : slots);
+  const int64_t workers = ew && atoll(ew) > 0 ? atoll(ew) : flow_cus() - 1;
+  const unsigned grid = (unsigned)(1 + (ntasks < workers ? ntasks : (workers < 1 ? 1 : workers)));  // + the chain
   int32_t* q = (int32_t*)flag_block;
   if (getenv("GBM_CHOL_FLOW_TRACE")) {
     // timing tool only: one record of 16 int64 per task, read back by gbm_debug_chol_flow_trace
-    if (g_trace_cap < ntasks) {
+    const int64_t nrec = ntasks + nbc;  // the workers' tasks, then the chain's steps
+    if (g_trace_cap < nrec) {
       if (g_trace) (void)hipFree(g_trace);
       g_trace = nullptr;
-      GBM_HIP_TRY(hipMalloc((void**)&g_trace, (size_t)ntasks * 192));
-      g_trace_cap = ntasks;
+      GBM_HIP_TRY(hipMalloc((void**)&g_trace, (size_t)nrec * 192));
+      g_trace_cap = nrec;
     }
-    g_trace_n = ntasks;
+    GBM_HIP_TRY(hipMemsetAsync(g_trace, 0, (size_t)nrec * 192, s));
+    g_trace_n = nrec;
     chol_flow_kernel<true><<<grid, 256, 0, s>>>(G, ldg, (int)nbc, Ld, Dinv, q, q + 4, info, g_trace);
   } else {
     chol_flow_kernel<false><<<grid, 256, 0, s>>>(G, ldg, (int)nbc, Ld, Dinv, q, q + 4, info, nullptr);
