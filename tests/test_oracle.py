@@ -11,7 +11,9 @@ import pytest
 import oracle
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-GOLDEN = sorted(f for f in glob.glob(os.path.join(HERE, "golden", "*.npz")) if not f.endswith("glmnet_ridge_r.npz"))
+# the GBLUP golden fixtures (make_golden.py); the R known-answer files have their own tests
+GOLDEN = sorted(f for f in glob.glob(os.path.join(HERE, "golden", "*.npz"))
+                if not f.endswith(("glmnet_ridge_r.npz", "lmer_r.npz")))
 
 
 def rel(a, b):
