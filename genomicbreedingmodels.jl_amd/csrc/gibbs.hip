@@ -11,6 +11,10 @@
 // workgroup applies δ = M r̃ redundantly from identical inputs (deterministic), updates e += X_B δ
 // on its individuals and computes the next block's partial dots, so a block costs one launch and
 // no device-wide synchronisation; one Gibbs iteration is captured as a hipGraph and replayed.
+// With byte storage the iteration is instead one persistent sweep launch: over 128-marker blocks
+// (brr_sweep128_kernel, one 256-individual chunk per CU) or, round 3, over 512-marker super-blocks
+// on up to every CU (brr_sweep_sb_kernel, and its look-ahead form brr_sweep_la_kernel, the
+// default: see "super-block sweep" below).
 //
 // Random numbers: a counter-based hash of (seed, stream, counter) (no sampler state), Box-Muller
 // normals and Marsaglia-Tsang gammas, restated bit-for-bit in oracle/oracle.py (brr_*), so the
@@ -1043,17 +1047,14 @@ __global__ void __launch_bounds__(256) brr_sweep128_kernel(const uint8_t* __rest
 //      forms r̃ = γ − α∘d⁰ there and publishes those rows;
 //   3. workgroup c computes its rows of δ_S = M_S r̃ from all of r̃, updates b and b̄ of those
 //      markers and publishes its δ rows;
-// then every chunk applies e += X_S δ_S to its individuals. Each hand-off: write-through (sc1)
-// stores, every storing wave drains, a workgroup barrier, one agent-scope atomic add per
-// workgroup onto an 8-way sharded counter (its XCD's shard); the consumer's wave 0 polls the 8
-// shards (sc1 loads) until they sum to the target, the others wait at a barrier, and every payload
-// load is an sc1 load (MI355X_MICROARCH.md hand-off table, row 1). Counters only grow within a
-// launch (target = (s + 1)·C), payload buffers alternate by super-block parity (a workgroup writes
-// super-block s + 2's payload only after every workgroup has passed s + 1's second hand-off, i.e.
-// finished reading s's). Each genotype byte is read from HBM once per iteration: the super-
-// block's rows of the chunk land in LDS by DMA (wave 3, during the previous super-block's hand-
-// offs) and serve both the dots and the e update. Same chain as the literal BGLR loop, rounding
-// aside. Waits are bounded (~1 s: *info = −1, every workgroup leaves; the host falls back).
+// then every chunk applies e += X_S δ_S to its individuals. Each hand-off is a set of self-
+// validating granules (below: one write-through store per value, no flag, counter or drain).
+// Granule slots alternate by super-block parity (a workgroup writes super-block s + 2's values only
+// after every workgroup has passed s + 1's second hand-off, i.e. finished reading s's). Each
+// genotype byte is read from HBM once per iteration: the super-block's rows of the chunk land in
+// LDS by DMA (wave 3, during the previous super-block's hand-offs) and serve both the dots and the
+// e update. Same chain as the literal BGLR loop, rounding aside. Waits are bounded (~1 s:
+// *info = −1, every workgroup leaves; the host falls back).
 static_assert(SBN * BK2 == SBK, "super-blocks are whole 128-marker blocks");
 constexpr int SB_PAIRS = SBN * (SBN - 1) / 2;
 constexpr int SB_KMAX = 64;            // individuals per chunk (at most)
