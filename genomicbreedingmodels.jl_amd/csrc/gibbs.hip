@@ -2158,7 +2158,8 @@ void brr_release_cache() { brr_pool().clear(); }
 }  // namespace gbm
 
 // Timing tool (GBM_BRR_TRACE=1): per super-block timestamps of workgroups 0 and C − 1 of the last
-// super-block sweep (2 x nsb x 8 int64, s_memrealtime at 100 MHz), read by gbm_debug_brr_trace.
+// super-block sweep (brr_sweep_sb_kernel: 2 x nsb x 12 int64; brr_sweep_la_kernel: every workgroup,
+// C x nsb x 8; s_memrealtime at 100 MHz), read by gbm_debug_brr_trace.
 static int64_t* g_brr_trace = nullptr;
 static int64_t g_brr_trace_n = 0;
 

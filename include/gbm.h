@@ -364,6 +364,20 @@ int gbm_brr_fit(const double* X, int64_t n, int64_t p, int64_t ldx, const double
                 int64_t n_burnin, int64_t thin, double r2, double df0, uint64_t seed, int device,
                 double* b_hat_out, double* y_pred_out, double* var_out);
 
+/* --------------------------------------------------------------------------------------
+ * Diagnostics (tests and timing tools; no reference counterpart).
+ * ------------------------------------------------------------------------------------ */
+/* Which schedule the last completed gbm_brr_fit ran (*last_path: 0 one launch per block, 1 the
+ * 128-block sweep, 2 the super-block sweep, 3 its look-ahead form) and how many fits so far fell
+ * back to the per-launch schedule after a sweep hand-off timed out (*fallbacks). */
+int gbm_debug_brr_stats(int* last_path, int64_t* fallbacks);
+/* With GBM_BRR_TRACE=1 set for a fit: copies up to cap int64 timestamps (100 MHz) of the last
+ * super-block sweep into host; returns the count, 0 when no trace was taken, -1 on a HIP error. */
+int64_t gbm_debug_brr_trace(int64_t* host, int64_t cap);
+/* With GBM_CHOL_FLOW_TRACE=1 set for a solve: copies up to cap records of 24 int64 (tile, workgroup,
+ * 100 MHz timestamps) of the last dataflow factorisation into host; returns the record count. */
+int64_t gbm_debug_chol_flow_trace(int64_t* host, int64_t cap);
+
 #ifdef __cplusplus
 }
 #endif
