@@ -1877,19 +1877,17 @@ __global__ void __launch_bounds__(256) brr_sweep_la_kernel(const uint8_t* __rest
   for (int64_t s = 0; s < nsb; s++) {
     const int64_t j0 = s * SBK;
     const uint64_t key = sb_key(tag0 + (uint64_t)s);
-    // operands of the owned rows (plain loads: written before this launch)
+    // operands of the owned rows (plain loads: written before this launch): C_s's rows now (for
+    // (B)); M_s's rows once the δ gather is done (for (D)), so that gather queues behind 16 KB of
+    // loads in the CU's memory pipeline instead of 32 KB
     double mrow[2][8], crow[2][8];
 #pragma unroll
     for (int h = 0; h < 2; h++) {
       const int w = h ? wrow1 : wrow0;
       const int jr = w < nown ? r0 + w : 0;
-      const double* mr = MS + (s * SBK + jr) * (int64_t)SBK;
       const double* cr = CS + (s * SBK + jr) * (int64_t)SBK;
 #pragma unroll
-      for (int t = 0; t < 8; t++) {
-        mrow[h][t] = (w < nown) ? mr[lane + 64 * t] : 0.0;
-        crow[h][t] = (w < nown && s > 0) ? cr[lane + 64 * t] : 0.0;
-      }
+      for (int t = 0; t < 8; t++) crow[h][t] = (w < nown && s > 0) ? cr[lane + 64 * t] : 0.0;
     }
     double alv = 0.0, gav = 0.0, bo = 0.0, bbo = 0.0;
     if (wave == 0 && lane < nown) {
@@ -1903,6 +1901,14 @@ __global__ void __launch_bounds__(256) brr_sweep_la_kernel(const uint8_t* __rest
     }
     // (A) δ_{s−1} -> dl (every workgroup; the owners' Q_s rows were gathered at the end of step s − 1)
     if (s > 0) gather512(rD, s - 1, dl);
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+      const int w = h ? wrow1 : wrow0;
+      const int jr = w < nown ? r0 + w : 0;
+      const double* mr = MS + (s * SBK + jr) * (int64_t)SBK;
+#pragma unroll
+      for (int t = 0; t < 8; t++) mrow[h][t] = (w < nown) ? mr[lane + 64 * t] : 0.0;
+    }
     lds_barrier();
     mark(s, 0);
     if (s_fail) return;
