@@ -1592,18 +1592,18 @@ __global__ void __launch_bounds__(256) brr_sweep_sb_kernel(const uint8_t* __rest
 // aside; waits bounded as in brr_sweep_sb_kernel.
 constexpr int LA_KMAX = 48;  // individuals per chunk (at most)
 
-// C_s = X_sᵀ X_{s−1} for s = 1 .. nsb − 1 (row-major 512 x 512 at CS + s·512²; rows of markers past
+// C_s = X_sᵀ X_{s−dist} for s = dist .. nsb − 1 (row-major 512 x 512 at CS + s·512²; rows of markers past
 // p repeat marker p − 1: they meet α = γ = δ = 0): one 128x128 block per workgroup, fp64 MFMA over
 // the individuals in 16-deep chunks staged by DMA (both operands marker-major, XOR-swizzled as A in
 // sb_gemm128), double-buffered, two workgroups per CU. One-time setup.
 __global__ void __launch_bounds__(256, 2) brr_xgram_kernel(const double* __restrict__ Xt, int64_t ldx, int64_t p,
-                                                           int64_t npad, double* __restrict__ CS) {
+                                                           int64_t npad, int dist, double* __restrict__ CS) {
   __shared__ __attribute__((aligned(16))) double lds[2 * 2 * GA];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1, fr = lane >> 4, fc = lane & 15;
-  const int64_t s = 1 + blockIdx.x / 16;
+  const int64_t s = dist + blockIdx.x / 16;
   const int ti = (int)((blockIdx.x >> 2) & 3), tj = (int)(blockIdx.x & 3);
-  const int64_t ra = s * SBK + ti * BK2, rb = (s - 1) * SBK + tj * BK2;
+  const int64_t ra = s * SBK + ti * BK2, rb = (s - dist) * SBK + tj * BK2;
   auto stage = [&](int64_t k0, int bf) {
     double* base = lds + bf * 2 * GA;
 #pragma unroll
@@ -2003,6 +2003,360 @@ __global__ void __launch_bounds__(256) brr_sweep_la_kernel(const uint8_t* __rest
   if (tid < K && i0 + tid < n) e[i0 + tid] = es[tid];
 }
 
+// Two super-blocks of slack for the partial dots (the default look-ahead form): with the second
+// cross-Gram C2_s = X_sᵀX_{s−2},
+//   d⁰_s = X_sᵀ e⁽ˢ⁻³⁾ + C2_s δ_{s−2} + C_s δ_{s−1},
+// so step s's chunk dots are those of super-block s + 2 (from the residual after s − 1) and the
+// owners sum them a whole step later (end of step s + 1): no chunk's e update and dots sit between
+// a δ and the next r̃ any more. A chunk keeps the rows of five super-blocks in LDS (s − 1 for the e
+// update, s + 2 for the dots, s + 3 arriving; 120 KB at K = 48), so every genotype byte is brought
+// in once per iteration (24 KB of DMA per step at K = 48, beside the e update's reduction: the
+// chunks' DMA bursts run at HBM speed). δ_{s−2} stays in LDS from its own gather.
+template <bool kTrace>
+__global__ void __launch_bounds__(256) brr_sweep_la2_kernel(const uint8_t* __restrict__ D, int64_t ldx, int64_t n,
+                                                           int64_t p, double xs, const double* __restrict__ MS,
+                                                           const double* __restrict__ CS,
+                                                           const double* __restrict__ CS2, int64_t nsb, int K, int R,
+                                                           double* __restrict__ Pb, double* __restrict__ Rt,
+                                                           double* __restrict__ Dl, int32_t* __restrict__ info,
+                                                           double* __restrict__ b, double* __restrict__ bbar,
+                                                           const double* __restrict__ alpha,
+                                                           const double* __restrict__ gamma, double* __restrict__ e,
+                                                           const BrrState* __restrict__ st, int64_t* __restrict__ trace) {
+  __shared__ __attribute__((aligned(16))) uint8_t Drow[5][SBK * LA_KMAX];  // super-block j at Drow[j % 5]
+  __shared__ __attribute__((aligned(16))) double es[LA_KMAX];
+  __shared__ __attribute__((aligned(16))) double rt[SBK];
+  __shared__ __attribute__((aligned(16))) double dlb[2][SBK];  // δ_j at dlb[j & 1]
+  __shared__ double red[4][SB_RMAX];
+  __shared__ double cd[1][SB_RMAX];
+  __shared__ __attribute__((aligned(16))) double eacc[1024];  // e update partial sums [row group][individual]
+  __shared__ double eq[4][LA_KMAX];
+  __shared__ int s_fail;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int C = (int)gridDim.x, c = (int)blockIdx.x;
+  const int64_t i0 = (int64_t)c * K;
+  const int r0 = c * R;
+  const int nown = r0 >= SBK ? 0 : (SBK - r0 < R ? SBK - r0 : R);
+  const bool tr_on = kTrace && threadIdx.x == 0;
+  int64_t* trw = kTrace ? trace + (int64_t)c * nsb * 8 : nullptr;  // every workgroup: 8 per super-block
+  auto mark = [&](int64_t s, int k) {
+    if (tr_on) trw[s * 8 + k] = (int64_t)__builtin_amdgcn_s_memrealtime();
+  };
+  const int it_odd = (int)(st->it & 1);
+  const bool accum = brr_accumulate(st);
+  const double kk = (double)(st->nsum + 1);
+  const uint64_t tag0 = (st->epoch << 40) + (uint64_t)st->it * (uint64_t)nsb;
+  const __amdgpu_buffer_rsrc_t rP = brr_rsrc(Pb, (int64_t)4 * C * SBK * 16);
+  const __amdgpu_buffer_rsrc_t rR = brr_rsrc(Rt, (int64_t)4 * SBK * 16);
+  const __amdgpu_buffer_rsrc_t rD = brr_rsrc(Dl, (int64_t)4 * SBK * 16);
+  if (tid == 0) s_fail = 0;
+  const int kpc = K / 16, kinv = (65536 + kpc - 1) / kpc;  // q / kpc = (q · kinv) >> 16 for q < 2^14
+  auto xrow = [&](int64_t j) { return Drow[(int)j % 5]; };
+  auto dma_rows = [&](int64_t sb, uint8_t* dst) {  // wave 3: the chunk's rows of super-block sb -> dst
+    const int pieces = SBK * kpc;
+    for (int q0 = 0; q0 < pieces; q0 += 64) {
+      const int q = q0 + lane;
+      const int row = (q * kinv) >> 16, part = q - row * kpc;
+      int64_t jr = sb * SBK + row;
+      jr = jr < p ? jr : p - 1;
+      const uint8_t* src = D + jr * ldx + i0 + part * 16;
+      const unsigned m0v = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(dst + q0 * 16));
+      asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off" : : "s"(m0v), "v"(src) : "memory");
+    }
+  };
+  // partial dots of super-block sb over this chunk from es (thread t: rows 2t, 2t + 1) -> P granules
+  auto dots_publish = [&](int64_t sb, const uint8_t* Dr) {
+    double a0 = 0.0, a1 = 0.0, c0 = 0.0, c1 = 0.0;
+    const uint8_t* ra = Dr + (2 * tid) * K;
+    const uint8_t* rb = ra + K;
+    for (int u = 0; u < K; u += 16) {
+      const uint4 va = *reinterpret_cast<const uint4*>(ra + u);
+      const uint4 vb = *reinterpret_cast<const uint4*>(rb + u);
+      const uint32_t wa[4] = {va.x, va.y, va.z, va.w};
+      const uint32_t wb[4] = {vb.x, vb.y, vb.z, vb.w};
+#pragma unroll
+      for (int q = 0; q < 4; q++)
+#pragma unroll
+        for (int bb = 0; bb < 4; bb += 2) {
+          const double2 e2 = *reinterpret_cast<const double2*>(es + u + 4 * q + bb);
+          a0 = fma((double)((wa[q] >> (8 * bb)) & 0xFFu), e2.x, a0);
+          a1 = fma((double)((wa[q] >> (8 * bb + 8)) & 0xFFu), e2.y, a1);
+          c0 = fma((double)((wb[q] >> (8 * bb)) & 0xFFu), e2.x, c0);
+          c1 = fma((double)((wb[q] >> (8 * bb + 8)) & 0xFFu), e2.y, c1);
+        }
+    }
+    const uint64_t key = sb_key(tag0 + (uint64_t)sb);
+    const uint32_t off = (uint32_t)((((int64_t)(sb & 3) * C + c) * SBK + 2 * tid) * 16);
+    sb_put(rP, off, a0 * xs + a1 * xs, key);
+    sb_put(rP, off + 16, c0 * xs + c1 * xs, key);
+  };
+  // all 512 granules of super-block sb from buffer r into LDS out (waves 0-1, four per lane); the
+  // pause between polls grows (up to ~0.2 µs) the longer the wait: 209 workgroups polling one 8 KB
+  // block is what the hop pays. (Every lane re-reads all four granules: an asm load under a
+  // divergent branch lets the compiler copy its register before the data lands.)
+  auto gather512 = [&](__amdgpu_buffer_rsrc_t r, int64_t sb, double* out) {
+    if (wave < 2) {
+      const uint64_t key = sb_key(tag0 + (uint64_t)sb);
+      bool failed = false;
+      int64_t spin = 0;
+      double x[4] = {0.0, 0.0, 0.0, 0.0};
+      for (;;) {
+        sbu4 w[4];
+#pragma unroll
+        for (int q = 0; q < 4; q++) w[q] = sb_get(r, (uint32_t)(((int64_t)(sb & 3) * SBK + tid * 4 + q) * 16));
+        sb_landed();
+        bool all = true;
+#pragma unroll
+        for (int q = 0; q < 4; q++) all = sb_ok(w[q], key, x[q]) && all;
+        if (!sb_spin(all, spin, info, failed)) break;
+        for (int64_t z = spin >> 3; z > 0 && z < 8; z--) __builtin_amdgcn_s_sleep(1);
+        if (spin >= 64) {
+#pragma unroll
+          for (int z = 0; z < 7; z++) __builtin_amdgcn_s_sleep(1);
+        }
+      }
+      if (failed) s_fail = 1;
+#pragma unroll
+      for (int q = 0; q < 4; q++) out[tid * 4 + q] = x[q];
+    }
+  };
+  // e update: thread t -> 4 individuals (one dword column, t % kq) of row group t / kq (rows
+  // [g·rpg, (g+1)·rpg)); partial sums eacc[g][individual] summed over the groups by 4 K threads
+  const int kq = K / 4, ng = 256 / kq, rpg = (SBK + ng - 1) / ng;
+  const int ecq = tid % kq, eg = tid / kq;
+  // e += X_sb δ (δ in dl) over the chunk, rows from Dr; ends with a barrier
+  auto e_update = [&](const uint8_t* Dr, const double* dl, int64_t ms, auto&& between) {
+    if (eg < ng) {
+      double acc[4] = {0.0, 0.0, 0.0, 0.0};
+      const int jb = eg * rpg, je = (jb + rpg < SBK) ? jb + rpg : SBK;
+#pragma unroll 4
+      for (int jj = jb; jj < je; jj++) {
+        const uint32_t w = *reinterpret_cast<const uint32_t*>(Dr + jj * K + ecq * 4);
+        const double d = dl[jj];
+#pragma unroll
+        for (int bb = 0; bb < 4; bb++) acc[bb] = fma((double)((w >> (8 * bb)) & 0xFFu), d, acc[bb]);
+      }
+      double2* ea = reinterpret_cast<double2*>(eacc + eg * K + ecq * 4);
+      ea[0] = double2{acc[0], acc[1]};
+      ea[1] = double2{acc[2], acc[3]};
+    }
+    lds_barrier();
+    if (ms >= 0) mark(ms, 6);
+    between();  // runs beside the reduction (tid >= 4 K: wave 3 when K <= 48)
+    if (tid < 4 * K) {
+      const int ind = tid % K, q = tid / K;
+      double u = 0.0;
+      for (int g = q; g < ng; g += 4) u += eacc[g * K + ind];
+      eq[q][ind] = u;
+    }
+    lds_barrier();
+    if (ms >= 0) mark(ms, 7);
+    if (tid < K && i0 + tid < n) es[tid] += (((eq[0][tid] + eq[1][tid]) + eq[2][tid]) + eq[3][tid]) * xs;
+    lds_barrier();
+  };
+
+  if (tid < LA_KMAX) es[tid] = (tid < K && i0 + tid < n) ? e[i0 + tid] : 0.0;
+  if (wave == 3) {
+    for (int64_t j = 0; j < 3 && j < nsb; j++) dma_rows(j, xrow(j));
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+  dots_publish(0, xrow(0));  // Q_0 = X_0ᵀ e
+  if (nsb > 1) dots_publish(1, xrow(1));  // Q_1 = X_1ᵀ e
+  // owners: their rows of Q_sb summed over all chunks (waves 2-3, beside the δ gather of waves 0-1:
+  // lane -> chunks lane + 64 (w − 2) and + 128 (C <= 256), summed in that order, xor-tree;
+  // red[w − 2][r], the two waves summed in order by the reader)
+  auto gather_q = [&](int64_t sb) {
+    if (nown > 0 && wave >= 2) {
+      const int wv = wave - 2;
+      const uint64_t key = sb_key(tag0 + (uint64_t)sb);
+      double v[SB_RMAX];
+#pragma unroll
+      for (int r = 0; r < SB_RMAX; r++) v[r] = 0.0;
+      // both chunks' granules in one round trip: they were published a step ago, so the first poll
+      // normally finds them all
+      const int cc0 = lane + 64 * wv, cc1 = cc0 + 128;
+      const bool has1 = cc1 < C;
+      const uint32_t base0 = (uint32_t)((((int64_t)(sb & 3) * C + (cc0 < C ? cc0 : 0)) * SBK + r0) * 16);
+      const uint32_t base1 = (uint32_t)((((int64_t)(sb & 3) * C + (has1 ? cc1 : 0)) * SBK + r0) * 16);
+      bool failed = false;
+      int64_t spin = 0;
+      double x0[SB_RMAX], x1[SB_RMAX];
+#pragma unroll
+      for (int r = 0; r < SB_RMAX; r++) x0[r] = x1[r] = 0.0;
+      for (;;) {
+        sbu4 w0[SB_RMAX], w1[SB_RMAX];
+#pragma unroll
+        for (int r = 0; r < SB_RMAX; r++)
+          if (r < R) {
+            w0[r] = sb_get(rP, base0 + r * 16);
+            w1[r] = sb_get(rP, base1 + r * 16);
+          }
+        sb_landed();
+        bool all = true;
+#pragma unroll
+        for (int r = 0; r < SB_RMAX; r++)
+          if (r < R && r < nown) {
+            all = (cc0 >= C || sb_ok(w0[r], key, x0[r])) && all;
+            all = (!has1 || sb_ok(w1[r], key, x1[r])) && all;
+          }
+        if (!sb_spin(all, spin, info, failed)) break;
+      }
+      if (failed) s_fail = 1;
+#pragma unroll
+      for (int r = 0; r < SB_RMAX; r++) v[r] = (cc0 < C && r < nown ? x0[r] : 0.0) + (has1 && r < nown ? x1[r] : 0.0);
+#pragma unroll
+      for (int r = 0; r < SB_RMAX; r++) {
+        double x = v[r];
+        x += __shfl_xor(x, 32);
+        x += __shfl_xor(x, 16);
+        x += __shfl_xor(x, 8);
+        x += __shfl_xor(x, 4);
+        x += __shfl_xor(x, 2);
+        x += __shfl_xor(x, 1);
+        if (lane == 0) red[wv][r] = x;
+      }
+    }
+  };
+  const int wrow0 = wave, wrow1 = wave + 4;  // owned-row indices of this wave's GEMV rows
+  for (int64_t s = 0; s < nsb; s++) {
+    const int64_t j0 = s * SBK;
+    const uint64_t key = sb_key(tag0 + (uint64_t)s);
+    // operands of the owned rows (plain loads: written before this launch): C_s's rows now (for
+    // (B)); M_s's rows once the δ gather is done (for (D)), so that gather queues behind 16 KB of
+    // loads in the CU's memory pipeline instead of 32 KB
+    double mrow[2][8], crow[2][8], crow2[2][8];
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+      const int w = h ? wrow1 : wrow0;
+      const int jr = w < nown ? r0 + w : 0;
+      const double* cr = CS + (s * SBK + jr) * (int64_t)SBK;
+      const double* cr2 = CS2 + (s * SBK + jr) * (int64_t)SBK;
+#pragma unroll
+      for (int t = 0; t < 8; t++) {
+        crow[h][t] = (w < nown && s > 0) ? cr[lane + 64 * t] : 0.0;
+        crow2[h][t] = (w < nown && s > 1) ? cr2[lane + 64 * t] : 0.0;
+      }
+    }
+    double alv = 0.0, gav = 0.0, bo = 0.0, bbo = 0.0;
+    if (wave == 0 && lane < nown) {
+      const int64_t jm = j0 + r0 + lane;
+      alv = alpha[jm];
+      gav = gamma[jm];
+      const int64_t jc = jm < p ? jm : 0;
+      const double b0v = b[jc], b1v = b[p + jc];
+      bbo = bbar[jc];
+      bo = it_odd ? b1v : b0v;
+    }
+    // (A) δ_{s−1} -> dlb (every workgroup, waves 0-1) and the owners' rows of Q_s (waves 2-3; its
+    // partial dots were published in (C) of step s − 2); wave 3: the DMAs of step s − 1 have landed
+    // before this step's barrier
+    const double* dl1 = dlb[(s - 1) & 1];  // δ_{s−1}
+    const double* dl2 = dlb[s & 1];        // δ_{s−2}
+    if (s > 0) gather512(rD, s - 1, dlb[(s - 1) & 1]);
+    gather_q(s);
+    if (wave == 3) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+      const int w = h ? wrow1 : wrow0;
+      const int jr = w < nown ? r0 + w : 0;
+      const double* mr = MS + (s * SBK + jr) * (int64_t)SBK;
+#pragma unroll
+      for (int t = 0; t < 8; t++) mrow[h][t] = (w < nown) ? mr[lane + 64 * t] : 0.0;
+    }
+    lds_barrier();
+    mark(s, 0);
+    if (s_fail) return;
+    // (B) owners: C_s δ_{s−1} + C2_s δ_{s−2} on their rows (wave w: rows w, w + 4), then r̃_s published
+    if (nown > 0) {
+#pragma unroll
+      for (int h = 0; h < 2; h++) {
+        const int w = h ? wrow1 : wrow0;
+        double a = 0.0;
+        if (s > 1) {
+#pragma unroll
+          for (int t = 0; t < 8; t++) a = fma(crow2[h][t], dl2[lane + 64 * t], a);
+        }
+        if (s > 0) {
+#pragma unroll
+          for (int t = 0; t < 8; t++) a = fma(crow[h][t], dl1[lane + 64 * t], a);
+        }
+        a += __shfl_xor(a, 32);
+        a += __shfl_xor(a, 16);
+        a += __shfl_xor(a, 8);
+        a += __shfl_xor(a, 4);
+        a += __shfl_xor(a, 2);
+        a += __shfl_xor(a, 1);
+        if (lane == 0 && w < nown) cd[0][w] = a;
+      }
+    }
+    if (nown > 0) {
+      lds_barrier();
+      if (wave == 0 && lane < nown) {
+        const double d0 = (red[0][lane] + red[1][lane]) + cd[0][lane];
+        sb_put(rR, (uint32_t)(((int64_t)(s & 3) * SBK + r0 + lane) * 16), fma(d0, -alv, gav), key);
+      }
+    }
+    mark(s, 1);
+    // (C) e += X_{s−1} δ_{s−1}, then the partial dots of Q_{s+2} (from the residual after s − 1).
+    // Wave 3, idle in the e update's reduction, brings in the rows of super-block s + 3 (for step
+    // s + 1's dots) into the slot of s − 2, read by step s − 1's e update, while no gather of this
+    // workgroup runs
+    auto dma_next = [&]() {
+      if (wave == 3 && s + 3 < nsb) dma_rows(s + 3, xrow(s + 3));
+    };
+    if (s > 0) {
+      e_update(xrow(s - 1), dl1, s, dma_next);
+    } else {
+      dma_next();
+      lds_barrier();
+    }
+    mark(s, 5);
+    if (s + 2 < nsb) dots_publish(s + 2, xrow(s + 2));
+    mark(s, 2);
+    // (D) owners: all of r̃_s, δ_s = M_s r̃_s on their rows, b and b̄, δ_s published
+    if (nown > 0) {
+      gather512(rR, s, rt);
+      lds_barrier();
+      if (s_fail) return;
+#pragma unroll
+      for (int h = 0; h < 2; h++) {
+        const int w = h ? wrow1 : wrow0;
+        double a = 0.0;
+#pragma unroll
+        for (int t = 0; t < 8; t++) a = fma(mrow[h][t], rt[lane + 64 * t], a);
+        a += __shfl_xor(a, 32);
+        a += __shfl_xor(a, 16);
+        a += __shfl_xor(a, 8);
+        a += __shfl_xor(a, 4);
+        a += __shfl_xor(a, 2);
+        a += __shfl_xor(a, 1);
+        if (lane == 0 && w < nown) red[3][w] = a;
+      }
+      lds_barrier();
+      if (wave == 0 && lane < nown) {
+        const double dlt = red[3][lane];
+        const int64_t jm = j0 + r0 + lane;
+        if (jm < p) {
+          const double bn = bo - dlt;
+          b[(it_odd ^ 1) * p + jm] = bn;
+          if (accum) bbar[jm] = bbo * ((kk - 1.0) / kk) + bn / kk;
+        }
+        sb_put(rD, (uint32_t)(((int64_t)(s & 3) * SBK + r0 + lane) * 16), dlt, key);
+      }
+      mark(s, 4);
+    }
+    mark(s, 3);
+  }
+  // the last super-block's δ, and its e update
+  gather512(rD, nsb - 1, dlb[(nsb - 1) & 1]);
+  if (wave == 3) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  lds_barrier();
+  if (s_fail) return;
+  e_update(xrow(nsb - 1), dlb[(nsb - 1) & 1], -1, [] {});
+  if (tid < K && i0 + tid < n) e[i0 + tid] = es[tid];
+}
+
 // σ²_b, σ²_e draws, running means of μ and the variances, next iteration (one workgroup)
 __global__ void __launch_bounds__(1024) brr_var_kernel(const double* __restrict__ b, int64_t p,
                                                        const double* __restrict__ e, int64_t n,
@@ -2078,6 +2432,7 @@ struct BrrCtx {
   DevBuf Xt, colmean, x2, e, b, bbar, r, stm, D, badm, W, Mb, alph, gamm, flg, Dt, pb, part, pout;
   DevBuf Wsb, MS, Ssc, Pb, Rt, Dl, sbcnt;  // the super-block sweep
   DevBuf CS;                               // its look-ahead form: cross-Grams C_s = X_sᵀ X_{s−1}
+  DevBuf CS2;                              // and (two-step slack) C2_s = X_sᵀ X_{s−2}
   hipGraphExec_t exec = nullptr;
   hipGraph_t graph = nullptr;
   std::vector<int64_t> key;  // what the captured graph was built for
@@ -2248,7 +2603,7 @@ static int brr_fit_impl(const double* X, int64_t n, int64_t p, int64_t ldx, cons
   // super-block each (1 024 <= n <= 64 CUs); GBM_BRR_SB=0 (read per call) keeps the 128-block sweep
   int cus = 0;
   GBM_HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-  bool sbmode = false, lamode = false;
+  bool sbmode = false, lamode = false, la2mode = false;
   int sbK = 0, sbC = 0, sbR = 0;
   if (xs > 0.0 && sweep_mode != 0) {
     const char* ev = std::getenv("GBM_BRR_SB");
@@ -2268,6 +2623,12 @@ static int brr_fit_impl(const double* X, int64_t n, int64_t p, int64_t ldx, cons
     int per_cu_la = 0;
     GBM_HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu_la, brr_sweep_la_kernel<false>, 256, 0));
     lamode = sbmode && !(ev3 && ev3[0] == '0') && per_cu_la >= 1 && sbK <= LA_KMAX;
+    // its two-step-slack form (brr_sweep_la2_kernel) by default; GBM_BRR_LA2=0 (read per call) keeps
+    // the one-step form
+    const char* ev4 = std::getenv("GBM_BRR_LA2");
+    int per_cu_la2 = 0;
+    GBM_HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu_la2, brr_sweep_la2_kernel<false>, 256, 0));
+    la2mode = lamode && !(ev4 && ev4[0] == '0') && per_cu_la2 >= 1 && sbC <= 256;
   }
   // markers per launch: 128 with byte storage (two halves), 64 with fp64 storage; the Gram blocks
   // each launch needs (brr_gram_kernel), and the block-transposed bytes of the byte path. The
@@ -2297,8 +2658,17 @@ static int brr_fit_impl(const double* X, int64_t n, int64_t p, int64_t ldx, cons
     if (lamode) {
       GBM_TRY(ensure(cx.CS, dev, nsb * SBK * SBK * 8));
       if (nsb > 1) {
-        brr_xgram_kernel<<<(unsigned)((nsb - 1) * 16), 256, 0, s>>>((const double*)cx.Xt.p, npad, p, npad, (double*)cx.CS.p);
+        brr_xgram_kernel<<<(unsigned)((nsb - 1) * 16), 256, 0, s>>>((const double*)cx.Xt.p, npad, p, npad, 1,
+                                                                    (double*)cx.CS.p);
         GBM_LAUNCH_CHECK();
+      }
+      if (la2mode) {
+        GBM_TRY(ensure(cx.CS2, dev, nsb * SBK * SBK * 8));
+        if (nsb > 2) {
+          brr_xgram_kernel<<<(unsigned)((nsb - 2) * 16), 256, 0, s>>>((const double*)cx.Xt.p, npad, p, npad, 2,
+                                                                      (double*)cx.CS2.p);
+          GBM_LAUNCH_CHECK();
+        }
       }
     }
     GBM_TRY(ensure(cx.sbcnt, dev, 32 * sizeof(int32_t)));
@@ -2386,7 +2756,19 @@ static int brr_fit_impl(const double* X, int64_t n, int64_t p, int64_t ldx, cons
         brr_sb_prep_kernel<<<(unsigned)(nsb * (level == 0 ? 2 : 4)), 256, 0, s>>>(
             level, (const double*)cx.Wsb.p, (const double*)cx.alph.p, (double*)cx.MS.p, (double*)cx.Ssc.p);
       int32_t* cn = (int32_t*)cx.sbcnt.p + 24;  // the error cell (zeroed at setup)
-      if (lamode && g_brr_trace)
+      if (la2mode && g_brr_trace)
+        brr_sweep_la2_kernel<true><<<(unsigned)sbC, 256, 0, s>>>(
+            (const uint8_t*)cx.D.p, npad, n, p, xs, (const double*)cx.MS.p, (const double*)cx.CS.p,
+            (const double*)cx.CS2.p, nsb, sbK, sbR, (double*)cx.Pb.p, (double*)cx.Rt.p, (double*)cx.Dl.p, cn,
+            (double*)cx.b.p, (double*)cx.bbar.p, (const double*)cx.alph.p, (const double*)cx.gamm.p,
+            (double*)cx.e.p, stp, g_brr_trace);
+      else if (la2mode)
+        brr_sweep_la2_kernel<false><<<(unsigned)sbC, 256, 0, s>>>(
+            (const uint8_t*)cx.D.p, npad, n, p, xs, (const double*)cx.MS.p, (const double*)cx.CS.p,
+            (const double*)cx.CS2.p, nsb, sbK, sbR, (double*)cx.Pb.p, (double*)cx.Rt.p, (double*)cx.Dl.p, cn,
+            (double*)cx.b.p, (double*)cx.bbar.p, (const double*)cx.alph.p, (const double*)cx.gamm.p,
+            (double*)cx.e.p, stp, nullptr);
+      else if (lamode && g_brr_trace)
         brr_sweep_la_kernel<true><<<(unsigned)sbC, 256, 0, s>>>(
             (const uint8_t*)cx.D.p, npad, n, p, xs, (const double*)cx.MS.p, (const double*)cx.CS.p, nsb, sbK, sbR,
             (double*)cx.Pb.p, (double*)cx.Rt.p, (double*)cx.Dl.p, cn, (double*)cx.b.p, (double*)cx.bbar.p,
@@ -2451,7 +2833,7 @@ static int brr_fit_impl(const double* X, int64_t n, int64_t p, int64_t ldx, cons
                                     (int64_t)(uintptr_t)cx.MS.p, (int64_t)(uintptr_t)cx.Wsb.p, (int64_t)(uintptr_t)cx.Ssc.p,
                                     (int64_t)(uintptr_t)cx.Pb.p, (int64_t)(uintptr_t)cx.Rt.p, (int64_t)(uintptr_t)cx.Dl.p,
                                     (int64_t)(uintptr_t)cx.sbcnt.p, (int64_t)(uintptr_t)g_brr_trace, lamode ? 1 : 0,
-                                    (int64_t)(uintptr_t)cx.CS.p};
+                                    (int64_t)(uintptr_t)cx.CS.p, la2mode ? 1 : 0, (int64_t)(uintptr_t)cx.CS2.p};
   int rc = GBM_OK;
   if (cx.key != key) {
     cx.drop_graph();
@@ -2490,7 +2872,7 @@ static int brr_fit_impl(const double* X, int64_t n, int64_t p, int64_t ldx, cons
       return fail(GBM_E_HIP, "gbm_brr_fit: a sweep hand-off between workgroups timed out");
     }
   }
-  g_brr_last_path.store(lamode ? 3 : sbmode ? 2 : sweep ? 1 : 0);
+  g_brr_last_path.store(la2mode ? 4 : lamode ? 3 : sbmode ? 2 : sweep ? 1 : 0);
   BrrState fin{};
   GBM_HIP_TRY(hipMemcpyAsync(&fin, cx.stm.p, sizeof(BrrState), hipMemcpyDeviceToHost, s));
   GBM_HIP_TRY(hipMemcpyAsync(b_hat_out + 1, cx.bbar.p, p * 8, hipMemcpyDeviceToHost, s));

@@ -368,7 +368,8 @@ int gbm_brr_fit(const double* X, int64_t n, int64_t p, int64_t ldx, const double
  * Diagnostics (tests and timing tools; no reference counterpart).
  * ------------------------------------------------------------------------------------ */
 /* Which schedule the last completed gbm_brr_fit ran (*last_path: 0 one launch per block, 1 the
- * 128-block sweep, 2 the super-block sweep, 3 its look-ahead form) and how many fits so far fell
+ * 128-block sweep, 2 the super-block sweep, 3 its look-ahead form, 4 the look-ahead form with two
+ * super-blocks of slack for the partial dots) and how many fits so far fell
  * back to the per-launch schedule after a sweep hand-off timed out (*fallbacks). */
 int gbm_debug_brr_stats(int* last_path, int64_t* fallbacks);
 /* With GBM_BRR_TRACE=1 set for a fit: copies up to cap int64 timestamps (100 MHz) of the last

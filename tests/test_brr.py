@@ -177,18 +177,24 @@ def brr_path():
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("n,p,K", [(1100, 300, None), (12000, 1300, None), (5000, 777, "64"), (3000, 1025, "32"),
-                                   (10000, 1100, None)])
+                                   (10000, 1100, None), (4000, 900, None), (6000, 2600, None)])
 def test_gpu_brr_super_block_sweep_runs_and_matches(monkeypatch, n, p, K):
-    """The super-block sweeps really run (no fall-back to the per-launch path): the look-ahead form
-    (brr_sweep_la_kernel, path 3: chunks of <= 48 individuals, cross-Gram C_s δ_{s−1} on the chain,
-    two granule hand-offs per super-block) and brr_sweep_sb_kernel (path 2: three hand-offs; also
-    GBM_BRR_LA=0). Both agree with the 128-block sweep (GBM_BRR_SB=0), the per-launch path and
-    the oracle's literal loop; ragged p (p mod 512 = 300, 276, 265, 1, 76), several chunk sizes."""
+    """The super-block sweeps really run (no fall-back to the per-launch path): the look-ahead forms
+    (chunks of <= 48 individuals, two granule hand-offs per super-block) with two steps of slack
+    for the partial dots (brr_sweep_la2_kernel, path 4: C2_s δ_{s−2} + C_s δ_{s−1} on the chain) and
+    with one (brr_sweep_la_kernel, path 3, GBM_BRR_LA2=0), and brr_sweep_sb_kernel (path 2: three
+    hand-offs; also GBM_BRR_LA=0). All agree with the 128-block sweep (GBM_BRR_SB=0), the
+    per-launch path and the oracle's literal loop; ragged p (p mod 512 = 300, 276, 265, 1, 76)
+    including nsb = 1, 2, 3, 6; several chunk sizes."""
     if K:
         monkeypatch.setenv("GBM_BRR_SB_K", K)
     X = oracle.synth_genotypes(n + p, n, p)
     y = oracle.synth_phenotypes(X, 17)[:, 0]
     _, fb0 = brr_path()
+    la2 = gbm.brr_arrays(X, y, n_iter=4, n_burnin=1, thin=1, seed=23)
+    path, fb = brr_path()
+    assert path == (2 if K == "64" else 4) and fb == fb0
+    monkeypatch.setenv("GBM_BRR_LA2", "0")
     la = gbm.brr_arrays(X, y, n_iter=4, n_burnin=1, thin=1, seed=23)
     path, fb = brr_path()
     assert path == (2 if K == "64" else 3) and fb == fb0
@@ -202,9 +208,9 @@ def test_gpu_brr_super_block_sweep_runs_and_matches(monkeypatch, n, p, K):
     launches = gbm.brr_arrays(X, y, n_iter=4, n_burnin=1, thin=1, seed=23)
     assert brr_path()[0] == 0
     rel = lambda a, b: np.abs(a - b).max() / np.abs(b).max()
-    for a, b, c, d in zip(sb, s128, launches, la):
-        assert rel(a, b) < 1e-10 and rel(a, c) < 1e-10 and rel(d, c) < 1e-10
+    for a, b, c, d, e in zip(sb, s128, launches, la, la2):
+        assert rel(a, b) < 1e-10 and rel(a, c) < 1e-10 and rel(d, c) < 1e-10 and rel(e, c) < 1e-10
     if n * p <= 5000 * 1000:
         ref = oracle.brr_gibbs(X, y, n_iter=4, n_burnin=1, thin=1, seed=23)
-        for got in (sb, la):
+        for got in (sb, la, la2):
             assert rel(got[0], ref["b_hat"]) < 1e-9 and rel(got[1], ref["y_pred"]) < 1e-9

@@ -2,7 +2,8 @@
 iterations and prints, for workgroups 0 and C − 1 of the last sweep, the mean time per super-block
 of each phase (dots + publish, hand-off 1 wait, r̃ + publish, hand-off 2 wait, δ + b + publish,
 hand-off 3 wait, e update); for the look-ahead form (path 3) the steps (A) δ + partial gathers,
-(B) C δ + r̃ publish, (C) e update + dots, (D) r̃ gather + δ publish. GBM_BRR_LA=0 traces the
+(B) C δ + r̃ publish, (C) e update + dots, (D) r̃ gather + δ publish (path 4, the two-step-slack
+form, has the same marks: its dots are those of s + 2). GBM_BRR_LA2=0 traces path 3, GBM_BRR_LA=0 the
 three-hand-off sweep. Timing tool only; one JSON line."""
 import ctypes
 import json
@@ -34,7 +35,7 @@ buf = np.zeros(cap, dtype=np.int64)
 lib.gbm_debug_brr_trace.restype = ctypes.c_int64
 got = lib.gbm_debug_brr_trace(buf.ctypes.data_as(ctypes.c_void_p), ctypes.c_int64(buf.size))
 out = {"tool": "brr_trace", "n": n, "p": p, "nsb": nsb, "records": int(got), "path": path.value}
-if path.value == 3:
+if path.value in (3, 4):
     # every workgroup: marks 0 A end (δ_{s−1} seen), 1 B end (r̃ published), 5 e update end, 2 C end (P_{s+1}
     # published), 4 δ_s published, 3 step end (Q_{s+1} gathered); 100 MHz ticks -> µs
     T = buf[:C * nsb * 8].reshape(C, nsb, 8).astype(np.float64) / 100.0
@@ -44,6 +45,8 @@ if path.value == 3:
         prev = np.concatenate([[t[0, 0]], t[:-1, 3]])
         ph = {"A_delta_gather": t[:, 0] - prev, "B_cdelta_rtilde": t[:, 1] - t[:, 0], "C_eupdate": t[:, 5] - t[:, 1],
               "C_dots": t[:, 2] - t[:, 5], "D_rtilde_gather_delta": t[:, 4] - t[:, 2], "D_q_gather": t[:, 3] - t[:, 4]}
+        if path.value == 4:  # e update sub-phases: 6 slices done, 7 reduction done
+            ph.update({"C_e_slices": t[:, 6] - t[:, 1], "C_e_reduce": t[:, 7] - t[:, 6], "C_e_apply": t[:, 5] - t[:, 7]})
         if not own[w]:
             ph = {k: v for k, v in ph.items() if not k.startswith("D")}
             ph["C_to_step_end"] = t[:, 3] - t[:, 2]

@@ -9,3 +9,5 @@ cat $OUT/trace.json
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- python3 tools/bench_next.py brr-c4 --n 10000 --p 100000 --iters 60 > $OUT/prof.json 2> $OUT/prof.err || { tail $OUT/prof.err; exit 1; }
 cat $OUT/prof.json
 f=$(find $OUT/prof -name 'run_kernel_stats.csv' | head -1); head -6 "$f" | cut -c1-60,200-320
+GBM_BRR_LA2=0 timeout -k 10 300 python3 tools/bench_next.py brr-c4 --n 10000 --p 100000 --iters 60 > $OUT/v3.json 2> $OUT/v3.err || { tail $OUT/v3.err; exit 1; }
+cat $OUT/v3.json
