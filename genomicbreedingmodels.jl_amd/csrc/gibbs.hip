@@ -2120,9 +2120,9 @@ __global__ void __launch_bounds__(256) brr_sweep_la2_kernel(const uint8_t* __res
       for (int q = 0; q < 4; q++) out[tid * 4 + q] = x[q];
     }
   };
-  // e update: thread t -> 4 individuals (one dword column, t % kq) of row group t / kq (rows
+  // e update: thread t < 192 -> 4 individuals (one dword column, t % kq) of row group t / kq (rows
   // [g·rpg, (g+1)·rpg)); partial sums eacc[g][individual] summed over the groups by 4 K threads
-  const int kq = K / 4, ng = 256 / kq, rpg = (SBK + ng - 1) / ng;
+  const int kq = K / 4, ng = 192 / kq, rpg = (SBK + ng - 1) / ng;
   const int ecq = tid % kq, eg = tid / kq;
   // e += X_sb δ (δ in dl) over the chunk, rows from Dr; ends with a barrier
   auto e_update = [&](const uint8_t* Dr, const double* dl, int64_t ms, auto&& between) {
@@ -2249,8 +2249,8 @@ __global__ void __launch_bounds__(256) brr_sweep_la2_kernel(const uint8_t* __res
       bo = it_odd ? b1v : b0v;
     }
     // (A) δ_{s−1} -> dlb (every workgroup, waves 0-1) and the owners' rows of Q_s (waves 2-3; its
-    // partial dots were published in (C) of step s − 2); wave 3: the DMAs of step s − 1 have landed
-    // before this step's barrier
+    // partial dots were published in (C) of step s − 2); wave 3: the DMA of step s − 1 (rows of
+    // super-block s + 2) has landed before this step's barrier
     const double* dl1 = dlb[(s - 1) & 1];  // δ_{s−1}
     const double* dl2 = dlb[s & 1];        // δ_{s−2}
     if (s > 0) gather512(rD, s - 1, dlb[(s - 1) & 1]);
@@ -2299,18 +2299,12 @@ __global__ void __launch_bounds__(256) brr_sweep_la2_kernel(const uint8_t* __res
     }
     mark(s, 1);
     // (C) e += X_{s−1} δ_{s−1}, then the partial dots of Q_{s+2} (from the residual after s − 1).
-    // Wave 3, idle in the e update's reduction, brings in the rows of super-block s + 3 (for step
-    // s + 1's dots) into the slot of s − 2, read by step s − 1's e update, while no gather of this
-    // workgroup runs
-    auto dma_next = [&]() {
-      if (wave == 3 && s + 3 < nsb) dma_rows(s + 3, xrow(s + 3));
-    };
-    if (s > 0) {
-      e_update(xrow(s - 1), dl1, s, dma_next);
-    } else {
-      dma_next();
-      lds_barrier();
-    }
+    // Wave 3 brings in the rows of super-block s + 3 (for step s + 1's dots) into the slot of s − 2,
+    // read by step s − 1's e update, while waves 0-2 run the e update's row groups: the chunks' DMA
+    // bursts run at HBM speed (~1.2 µs at K = 48), so the wave that issues them takes no row group.
+    // (Issued in (A) instead, the burst slows the δ hop by more than that.)
+    if (wave == 3 && s + 3 < nsb) dma_rows(s + 3, xrow(s + 3));
+    if (s > 0) e_update(xrow(s - 1), dl1, s, [] {});
     mark(s, 5);
     if (s + 2 < nsb) dots_publish(s + 2, xrow(s + 2));
     mark(s, 2);
