@@ -2029,7 +2029,7 @@ __global__ void __launch_bounds__(256) brr_sweep_la2_kernel(const uint8_t* __res
   __shared__ __attribute__((aligned(16))) double dlb[2][SBK];  // δ_j at dlb[j & 1]
   __shared__ double red[4][SB_RMAX];
   __shared__ double cd[1][SB_RMAX];
-  __shared__ __attribute__((aligned(16))) double eacc[1024];  // e update partial sums [row group][individual]
+  __shared__ __attribute__((aligned(16))) double eacc[1536];  // e update partial sums [row group][individual]
   __shared__ double eq[4][LA_KMAX];
   __shared__ int s_fail;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -2120,25 +2120,38 @@ __global__ void __launch_bounds__(256) brr_sweep_la2_kernel(const uint8_t* __res
       for (int q = 0; q < 4; q++) out[tid * 4 + q] = x[q];
     }
   };
-  // e update: thread t < 192 -> 4 individuals (one dword column, t % kq) of row group t / kq (rows
-  // [g·rpg, (g+1)·rpg)); partial sums eacc[g][individual] summed over the groups by 4 K threads
-  const int kq = K / 4, ng = 192 / kq, rpg = (SBK + ng - 1) / ng;
+  // e update: thread t < 192 -> 8 individuals (column t % kq of 8 bytes) of row group g = t / kq:
+  // rows g, g + ng, g + 2 ng, ... (interleaved, so a wave's lanes read consecutive rows: no LDS bank
+  // conflicts); partial sums eacc[g][individual] summed over the groups by 4 K threads
+  const int kq = K / 8, ng = 192 / kq, rpg = (SBK + ng - 1) / ng;
   const int ecq = tid % kq, eg = tid / kq;
   // e += X_sb δ (δ in dl) over the chunk, rows from Dr; ends with a barrier
   auto e_update = [&](const uint8_t* Dr, const double* dl, int64_t ms, auto&& between) {
     if (eg < ng) {
-      double acc[4] = {0.0, 0.0, 0.0, 0.0};
-      const int jb = eg * rpg, je = (jb + rpg < SBK) ? jb + rpg : SBK;
-#pragma unroll 4
-      for (int jj = jb; jj < je; jj++) {
-        const uint32_t w = *reinterpret_cast<const uint32_t*>(Dr + jj * K + ecq * 4);
-        const double d = dl[jj];
+      double acc[8];
 #pragma unroll
-        for (int bb = 0; bb < 4; bb++) acc[bb] = fma((double)((w >> (8 * bb)) & 0xFFu), d, acc[bb]);
+      for (int bb = 0; bb < 8; bb++) acc[bb] = 0.0;
+      for (int k0 = 0; k0 < rpg; k0 += 8) {
+        uint2 w[8];
+        double d[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+          const int r = eg + (k0 + u) * ng;
+          const bool v = k0 + u < rpg && r < SBK;
+          w[u] = v ? *reinterpret_cast<const uint2*>(Dr + r * K + ecq * 8) : uint2{0u, 0u};
+          d[u] = v ? dl[r] : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < 8; u++)
+#pragma unroll
+          for (int bb = 0; bb < 4; bb++) {
+            acc[bb] = fma((double)((w[u].x >> (8 * bb)) & 0xFFu), d[u], acc[bb]);
+            acc[4 + bb] = fma((double)((w[u].y >> (8 * bb)) & 0xFFu), d[u], acc[4 + bb]);
+          }
       }
-      double2* ea = reinterpret_cast<double2*>(eacc + eg * K + ecq * 4);
-      ea[0] = double2{acc[0], acc[1]};
-      ea[1] = double2{acc[2], acc[3]};
+      double2* ea = reinterpret_cast<double2*>(eacc + eg * K + ecq * 8);
+#pragma unroll
+      for (int q = 0; q < 4; q++) ea[q] = double2{acc[2 * q], acc[2 * q + 1]};
     }
     lds_barrier();
     if (ms >= 0) mark(ms, 6);
