@@ -1266,6 +1266,14 @@ __device__ __forceinline__ sbu4 sb_get(__amdgpu_buffer_rsrc_t r, uint32_t off) {
   return v;
 }
 __device__ __forceinline__ void sb_landed() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+// The same poll as a compiler-visible load (cache policy sc1): the compiler counts it, waits just
+// before the first use of its value and never has to wait for everything in flight because of an
+// opaque asm load. A poll loop that uses it starts each round with sb_fence(), so that the load is
+// not hoisted out of the loop.
+__device__ __forceinline__ sbu4 sb_getv(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+  return __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 16);
+}
+__device__ __forceinline__ void sb_fence() { asm volatile("" ::: "memory"); }
 __device__ __forceinline__ bool sb_ok(const sbu4& w, uint64_t key, double& v) {
   const uint64_t a = (uint64_t)w.x | ((uint64_t)w.y << 32), b = (uint64_t)w.z | ((uint64_t)w.w << 32);
   v = __builtin_bit_cast(double, a);
@@ -2101,10 +2109,10 @@ __global__ void __launch_bounds__(256) brr_sweep_la2_kernel(const uint8_t* __res
       int64_t spin = 0;
       double x[4] = {0.0, 0.0, 0.0, 0.0};
       for (;;) {
+        sb_fence();
         sbu4 w[4];
 #pragma unroll
-        for (int q = 0; q < 4; q++) w[q] = sb_get(r, (uint32_t)(((int64_t)(sb & 3) * SBK + tid * 4 + q) * 16));
-        sb_landed();
+        for (int q = 0; q < 4; q++) w[q] = sb_getv(r, (uint32_t)(((int64_t)(sb & 3) * SBK + tid * 4 + q) * 16));
         bool all = true;
 #pragma unroll
         for (int q = 0; q < 4; q++) all = sb_ok(w[q], key, x[q]) && all;
@@ -2198,14 +2206,14 @@ __global__ void __launch_bounds__(256) brr_sweep_la2_kernel(const uint8_t* __res
 #pragma unroll
       for (int r = 0; r < SB_RMAX; r++) x0[r] = x1[r] = 0.0;
       for (;;) {
+        sb_fence();
         sbu4 w0[SB_RMAX], w1[SB_RMAX];
 #pragma unroll
         for (int r = 0; r < SB_RMAX; r++)
           if (r < R) {
-            w0[r] = sb_get(rP, base0 + r * 16);
-            w1[r] = sb_get(rP, base1 + r * 16);
+            w0[r] = sb_getv(rP, base0 + r * 16);
+            w1[r] = sb_getv(rP, base1 + r * 16);
           }
-        sb_landed();
         bool all = true;
 #pragma unroll
         for (int r = 0; r < SB_RMAX; r++)
@@ -2269,6 +2277,13 @@ __global__ void __launch_bounds__(256) brr_sweep_la2_kernel(const uint8_t* __res
     if (s > 0) gather512(rD, s - 1, dlb[(s - 1) & 1]);
     gather_q(s);
     if (wave == 3) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // C_s's rows are in registers by now; consumed here, so that the wait the compiler puts before
+    // their first use (it cannot count the gathers' loads, and waits for all) comes before M_s's
+    // loads are issued, not in (B) behind them
+#pragma unroll
+    for (int h = 0; h < 2; h++)
+#pragma unroll
+      for (int t = 0; t < 8; t++) asm volatile("" : "+v"(crow[h][t]), "+v"(crow2[h][t]));
 #pragma unroll
     for (int h = 0; h < 2; h++) {
       const int w = h ? wrow1 : wrow0;
