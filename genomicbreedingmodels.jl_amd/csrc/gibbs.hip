@@ -1274,6 +1274,29 @@ __device__ __forceinline__ sbu4 sb_getv(__amdgpu_buffer_rsrc_t r, uint32_t off) 
   return __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 16);
 }
 __device__ __forceinline__ void sb_fence() { asm volatile("" ::: "memory"); }
+// Sum over the wave, returned to every lane (wave-uniform): DPP within each row of 16 lanes (quad
+// swaps, half-row and row mirrors), then the four row sums read into scalars. Latency of a few
+// VALU ops per step instead of the LDS round trip of each __shfl_xor.
+template <int kCtrl>
+__device__ __forceinline__ double dpp_f64(double x) {
+  const uint64_t u = __builtin_bit_cast(uint64_t, x);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)u, kCtrl, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)(u >> 32), kCtrl, 0xF, 0xF, false);
+  return __builtin_bit_cast(double, (uint64_t)(uint32_t)lo | ((uint64_t)(uint32_t)hi << 32));
+}
+__device__ __forceinline__ double readlane_f64(double x, int l) {
+  const uint64_t u = __builtin_bit_cast(uint64_t, x);
+  const int lo = __builtin_amdgcn_readlane((int)(uint32_t)u, l);
+  const int hi = __builtin_amdgcn_readlane((int)(uint32_t)(u >> 32), l);
+  return __builtin_bit_cast(double, (uint64_t)(uint32_t)lo | ((uint64_t)(uint32_t)hi << 32));
+}
+__device__ __forceinline__ double wave_sum_f64(double x) {
+  x += dpp_f64<0xB1>(x);   // quad_perm [1,0,3,2]
+  x += dpp_f64<0x4E>(x);   // quad_perm [2,3,0,1]
+  x += dpp_f64<0x141>(x);  // row_half_mirror
+  x += dpp_f64<0x140>(x);  // row_mirror
+  return (readlane_f64(x, 0) + readlane_f64(x, 16)) + (readlane_f64(x, 32) + readlane_f64(x, 48));
+}
 __device__ __forceinline__ bool sb_ok(const sbu4& w, uint64_t key, double& v) {
   const uint64_t a = (uint64_t)w.x | ((uint64_t)w.y << 32), b = (uint64_t)w.z | ((uint64_t)w.w << 32);
   v = __builtin_bit_cast(double, a);
@@ -2036,7 +2059,6 @@ __global__ void __launch_bounds__(256) brr_sweep_la2_kernel(const uint8_t* __res
   __shared__ __attribute__((aligned(16))) double rt[SBK];
   __shared__ __attribute__((aligned(16))) double dlb[2][SBK];  // δ_j at dlb[j & 1]
   __shared__ double red[4][SB_RMAX];
-  __shared__ double cd[1][SB_RMAX];
   __shared__ __attribute__((aligned(16))) double eacc[1536];  // e update partial sums [row group][individual]
   __shared__ double eq[4][LA_KMAX];
   __shared__ int s_fail;
@@ -2228,18 +2250,13 @@ __global__ void __launch_bounds__(256) brr_sweep_la2_kernel(const uint8_t* __res
       for (int r = 0; r < SB_RMAX; r++) v[r] = (cc0 < C && r < nown ? x0[r] : 0.0) + (has1 && r < nown ? x1[r] : 0.0);
 #pragma unroll
       for (int r = 0; r < SB_RMAX; r++) {
-        double x = v[r];
-        x += __shfl_xor(x, 32);
-        x += __shfl_xor(x, 16);
-        x += __shfl_xor(x, 8);
-        x += __shfl_xor(x, 4);
-        x += __shfl_xor(x, 2);
-        x += __shfl_xor(x, 1);
+        const double x = wave_sum_f64(v[r]);
         if (lane == 0) red[wv][r] = x;
       }
     }
   };
-  const int wrow0 = wave, wrow1 = wave + 4;  // owned-row indices of this wave's GEMV rows
+  // owned-row indices of this wave's GEMV rows (wave-uniform)
+  const int wrow0 = __builtin_amdgcn_readfirstlane(wave), wrow1 = wrow0 + 4;
   for (int64_t s = 0; s < nsb; s++) {
     const int64_t j0 = s * SBK;
     const uint64_t key = sb_key(tag0 + (uint64_t)s);
@@ -2259,15 +2276,19 @@ __global__ void __launch_bounds__(256) brr_sweep_la2_kernel(const uint8_t* __res
         crow2[h][t] = (w < nown && s > 1) ? cr2[lane + 64 * t] : 0.0;
       }
     }
-    double alv = 0.0, gav = 0.0, bo = 0.0, bbo = 0.0;
-    if (wave == 0 && lane < nown) {
-      const int64_t jm = j0 + r0 + lane;
-      alv = alpha[jm];
-      gav = gamma[jm];
-      const int64_t jc = jm < p ? jm : 0;
-      const double b0v = b[jc], b1v = b[p + jc];
-      bbo = bbar[jc];
-      bo = it_odd ? b1v : b0v;
+    // the step constants and the sample of this wave's rows (each wave publishes its own rows)
+    double alv[2] = {0.0, 0.0}, gav[2] = {0.0, 0.0}, bo[2] = {0.0, 0.0}, bbo[2] = {0.0, 0.0};
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+      const int w = h ? wrow1 : wrow0;
+      if (w < nown) {
+        const int64_t jm = j0 + r0 + w;
+        alv[h] = alpha[jm];
+        gav[h] = gamma[jm];
+        const int64_t jc = jm < p ? jm : 0;
+        bbo[h] = bbar[jc];
+        bo[h] = b[it_odd * p + jc];
+      }
     }
     // (A) δ_{s−1} -> dlb (every workgroup, waves 0-1) and the owners' rows of Q_s (waves 2-3; its
     // partial dots were published in (C) of step s − 2); wave 3: the DMA of step s − 1 (rows of
@@ -2295,34 +2316,27 @@ __global__ void __launch_bounds__(256) brr_sweep_la2_kernel(const uint8_t* __res
     lds_barrier();
     mark(s, 0);
     if (s_fail) return;
-    // (B) owners: C_s δ_{s−1} + C2_s δ_{s−2} on their rows (wave w: rows w, w + 4), then r̃_s published
-    if (nown > 0) {
+    // (B) owners: C_s δ_{s−1} + C2_s δ_{s−2} on their rows (wave w: rows w, w + 4), and each wave
+    // publishes its rows of r̃_s (no barrier)
+    if (nown > 0 && wrow0 < nown) {
+      double dv1[8], dv2[8];
+#pragma unroll
+      for (int t = 0; t < 8; t++) {
+        dv1[t] = s > 0 ? dl1[lane + 64 * t] : 0.0;
+        dv2[t] = s > 1 ? dl2[lane + 64 * t] : 0.0;
+      }
 #pragma unroll
       for (int h = 0; h < 2; h++) {
         const int w = h ? wrow1 : wrow0;
-        double a = 0.0;
-        if (s > 1) {
+        if (w < nown) {
+          double a = 0.0;
 #pragma unroll
-          for (int t = 0; t < 8; t++) a = fma(crow2[h][t], dl2[lane + 64 * t], a);
-        }
-        if (s > 0) {
+          for (int t = 0; t < 8; t++) a = fma(crow2[h][t], dv2[t], a);
 #pragma unroll
-          for (int t = 0; t < 8; t++) a = fma(crow[h][t], dl1[lane + 64 * t], a);
+          for (int t = 0; t < 8; t++) a = fma(crow[h][t], dv1[t], a);
+          const double d0 = (red[0][w] + red[1][w]) + wave_sum_f64(a);
+          if (lane == 0) sb_put(rR, (uint32_t)(((int64_t)(s & 3) * SBK + r0 + w) * 16), fma(d0, -alv[h], gav[h]), key);
         }
-        a += __shfl_xor(a, 32);
-        a += __shfl_xor(a, 16);
-        a += __shfl_xor(a, 8);
-        a += __shfl_xor(a, 4);
-        a += __shfl_xor(a, 2);
-        a += __shfl_xor(a, 1);
-        if (lane == 0 && w < nown) cd[0][w] = a;
-      }
-    }
-    if (nown > 0) {
-      lds_barrier();
-      if (wave == 0 && lane < nown) {
-        const double d0 = (red[0][lane] + red[1][lane]) + cd[0][lane];
-        sb_put(rR, (uint32_t)(((int64_t)(s & 3) * SBK + r0 + lane) * 16), fma(d0, -alv, gav), key);
       }
     }
     mark(s, 1);
@@ -2341,30 +2355,25 @@ __global__ void __launch_bounds__(256) brr_sweep_la2_kernel(const uint8_t* __res
       gather512(rR, s, rt);
       lds_barrier();
       if (s_fail) return;
+      // each wave: δ_s, b and b̄ of its rows, δ_s published (no barrier)
 #pragma unroll
       for (int h = 0; h < 2; h++) {
         const int w = h ? wrow1 : wrow0;
-        double a = 0.0;
+        if (w < nown) {
+          double a = 0.0;
 #pragma unroll
-        for (int t = 0; t < 8; t++) a = fma(mrow[h][t], rt[lane + 64 * t], a);
-        a += __shfl_xor(a, 32);
-        a += __shfl_xor(a, 16);
-        a += __shfl_xor(a, 8);
-        a += __shfl_xor(a, 4);
-        a += __shfl_xor(a, 2);
-        a += __shfl_xor(a, 1);
-        if (lane == 0 && w < nown) red[3][w] = a;
-      }
-      lds_barrier();
-      if (wave == 0 && lane < nown) {
-        const double dlt = red[3][lane];
-        const int64_t jm = j0 + r0 + lane;
-        if (jm < p) {
-          const double bn = bo - dlt;
-          b[(it_odd ^ 1) * p + jm] = bn;
-          if (accum) bbar[jm] = bbo * ((kk - 1.0) / kk) + bn / kk;
+          for (int t = 0; t < 8; t++) a = fma(mrow[h][t], rt[lane + 64 * t], a);
+          const double dlt = wave_sum_f64(a);
+          if (lane == 0) {
+            const int64_t jm = j0 + r0 + w;
+            if (jm < p) {
+              const double bn = bo[h] - dlt;
+              b[(it_odd ^ 1) * p + jm] = bn;
+              if (accum) bbar[jm] = bbo[h] * ((kk - 1.0) / kk) + bn / kk;
+            }
+            sb_put(rD, (uint32_t)(((int64_t)(s & 3) * SBK + r0 + w) * 16), dlt, key);
+          }
         }
-        sb_put(rD, (uint32_t)(((int64_t)(s & 3) * SBK + r0 + lane) * 16), dlt, key);
       }
       mark(s, 4);
     }
