@@ -2043,11 +2043,15 @@ __global__ void __launch_bounds__(256) brr_sweep_la_kernel(const uint8_t* __rest
 // update, s + 2 for the dots, s + 3 arriving; 120 KB at K = 48), so every genotype byte is brought
 // in once per iteration (24 KB of DMA per step at K = 48, beside the e update's reduction: the
 // chunks' DMA bursts run at HBM speed). δ_{s−2} stays in LDS from its own gather.
+// The first O workgroups own R rows of every super-block each and take Ko individuals; the others
+// take Kn (both multiples of 16, <= LA_KMAX): the owners' e update and dots sit on the chain of
+// hand-offs, so they get the smaller chunks.
 template <bool kTrace>
 __global__ void __launch_bounds__(256) brr_sweep_la2_kernel(const uint8_t* __restrict__ D, int64_t ldx, int64_t n,
                                                            int64_t p, double xs, const double* __restrict__ MS,
                                                            const double* __restrict__ CS,
-                                                           const double* __restrict__ CS2, int64_t nsb, int K, int R,
+                                                           const double* __restrict__ CS2, int64_t nsb, int Ko, int O,
+                                                           int Kn, int R,
                                                            double* __restrict__ Pb, double* __restrict__ Rt,
                                                            double* __restrict__ Dl, int32_t* __restrict__ info,
                                                            double* __restrict__ b, double* __restrict__ bbar,
@@ -2064,7 +2068,8 @@ __global__ void __launch_bounds__(256) brr_sweep_la2_kernel(const uint8_t* __res
   __shared__ int s_fail;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int C = (int)gridDim.x, c = (int)blockIdx.x;
-  const int64_t i0 = (int64_t)c * K;
+  const int K = c < O ? Ko : Kn;
+  const int64_t i0 = c < O ? (int64_t)c * Ko : (int64_t)O * Ko + (int64_t)(c - O) * Kn;
   const int r0 = c * R;
   const int nown = r0 >= SBK ? 0 : (SBK - r0 < R ? SBK - r0 : R);
   const bool tr_on = kTrace && threadIdx.x == 0;
@@ -2295,7 +2300,28 @@ __global__ void __launch_bounds__(256) brr_sweep_la2_kernel(const uint8_t* __res
     // super-block s + 2) has landed before this step's barrier
     const double* dl1 = dlb[(s - 1) & 1];  // δ_{s−1}
     const double* dl2 = dlb[s & 1];        // δ_{s−2}
-    if (s > 0) gather512(rD, s - 1, dlb[(s - 1) & 1]);
+    if (s > 0) {
+      // a workgroup that owns no rows has slack (its dots are needed two steps on): it first waits
+      // for one granule of δ_{s−1}, one lane polling one line slowly, so that the owners' sweeps of
+      // the 8 KB do not queue behind its own
+      if (nown == 0 && wave == 0) {
+        const uint64_t key1 = sb_key(tag0 + (uint64_t)(s - 1));
+        const uint32_t off = (uint32_t)((((int64_t)((s - 1) & 3) * SBK) + SBK - 1) * 16);
+        bool failed = false;
+        int64_t spin = 0;
+        for (;;) {
+          sb_fence();
+          const sbu4 w = sb_getv(rD, off);
+          double x;
+          if (!sb_spin(sb_ok(w, key1, x), spin, info, failed)) break;
+#pragma unroll
+          for (int z = 0; z < 7; z++) __builtin_amdgcn_s_sleep(2);
+        }
+        if (failed) s_fail = 1;
+      }
+      if (nown == 0) lds_barrier();
+      gather512(rD, s - 1, dlb[(s - 1) & 1]);
+    }
     gather_q(s);
     if (wave == 3) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     // C_s's rows are in registers by now; consumed here, so that the wait the compiler puts before
@@ -2574,6 +2600,17 @@ extern "C" int gbm_debug_brr_stats(int* last_path, int64_t* fallbacks) {
   if (fallbacks) *fallbacks = g_brr_fallbacks.load();
   return GBM_OK;
 }
+// chunk shape of the last super-block sweep (C workgroups, O owners of R rows, Ko / Kn individuals)
+static std::atomic<int64_t> g_brr_shape{0};
+extern "C" int gbm_debug_brr_shape(int* C, int* O, int* R, int* Ko, int* Kn) {
+  const int64_t v = g_brr_shape.load();
+  if (C) *C = (int)(v & 0xFFF);
+  if (O) *O = (int)((v >> 12) & 0xFFF);
+  if (R) *R = (int)((v >> 24) & 0xFF);
+  if (Ko) *Ko = (int)((v >> 32) & 0xFFF);
+  if (Kn) *Kn = (int)((v >> 44) & 0xFFF);
+  return 0;
+}
 
 // One BRR fit on a leased context; sweep_mode: -1 = per GBM_BRR_SWEEP (default on), 0 = off.
 static int brr_fit_impl(const double* X, int64_t n, int64_t p, int64_t ldx, const double* y, int64_t n_iter,
@@ -2636,6 +2673,7 @@ static int brr_fit_impl(const double* X, int64_t n, int64_t p, int64_t ldx, cons
   GBM_HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
   bool sbmode = false, lamode = false, la2mode = false;
   int sbK = 0, sbC = 0, sbR = 0;
+  int la2Ko = 0, la2Kn = 0, la2R = 0, la2O = 0, la2C = 0;
   if (xs > 0.0 && sweep_mode != 0) {
     const char* ev = std::getenv("GBM_BRR_SB");
     const char* ev2 = std::getenv("GBM_BRR_SWEEP");
@@ -2660,6 +2698,35 @@ static int brr_fit_impl(const double* X, int64_t n, int64_t p, int64_t ldx, cons
     int per_cu_la2 = 0;
     GBM_HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu_la2, brr_sweep_la2_kernel<false>, 256, 0));
     la2mode = lamode && !(ev4 && ev4[0] == '0') && per_cu_la2 >= 1 && sbC <= 256;
+    // its chunk split: O = 512 / R owners of Ko individuals, the rest Kn (both <= LA_KMAX), all on
+    // <= min(CUs, 256) workgroups; the owners get the smallest Ko that fits. Off unless GBM_BRR_OWN_R=
+    // 2|4|6|8 (read per call) sets R: at C4 the extra workgroups' polls cost the hops more than the
+    // owners' lighter chunks save (2.58 ms at R = 4, 3.32 at R = 8, vs 2.41 uniform). Uniform
+    // chunks (Ko = Kn = K, O = 512 / R) otherwise.
+    la2Ko = sbK;
+    la2Kn = sbK;
+    la2R = sbR;
+    la2O = (SBK + sbR - 1) / sbR;
+    la2C = sbC;
+    if (la2mode) {
+      int R2 = 0;
+      if (const char* er = std::getenv("GBM_BRR_OWN_R")) R2 = std::max(2, std::min<int>(SB_RMAX, atoi(er) & ~1));
+      const int O2 = R2 > 0 ? (SBK + R2 - 1) / R2 : 0;
+      const int ncu = std::min(cus, 256);
+      for (int Ko = 16; R2 > 0 && Ko <= LA_KMAX && O2 < ncu; Ko += 16) {
+        const int64_t rest = n - (int64_t)O2 * Ko;
+        if (rest < 16) break;
+        const int Kn = (int)round_up(std::max<int64_t>(16, (rest + (ncu - O2) - 1) / (ncu - O2)), 16);
+        if (Kn > LA_KMAX) continue;
+        if (Kn <= Ko) break;  // no lighter owners than the uniform split
+        la2Ko = Ko;
+        la2Kn = Kn;
+        la2R = R2;
+        la2O = O2;
+        la2C = O2 + (int)((rest + Kn - 1) / Kn);
+        break;
+      }
+    }
   }
   // markers per launch: 128 with byte storage (two halves), 64 with fp64 storage; the Gram blocks
   // each launch needs (brr_gram_kernel), and the block-transposed bytes of the byte path. The
@@ -2683,7 +2750,7 @@ static int brr_fit_impl(const double* X, int64_t n, int64_t p, int64_t ldx, cons
     GBM_TRY(ensure(cx.Wsb, dev, nsb * SB_PAIRS * BK2 * BK2 * 8));
     GBM_TRY(ensure(cx.MS, dev, nsb * SBK * SBK * 8));
     GBM_TRY(ensure(cx.Ssc, dev, nsb * 6 * BK2 * BK2 * 8));
-    GBM_TRY(ensure(cx.Pb, dev, (int64_t)4 * sbC * SBK * 16));  // 16-B hand-off granules (2 or 4 slots)
+    GBM_TRY(ensure(cx.Pb, dev, (int64_t)4 * std::max(sbC, la2C) * SBK * 16));  // 16-B hand-off granules (2 or 4 slots)
     GBM_TRY(ensure(cx.Rt, dev, 4 * SBK * 16));
     GBM_TRY(ensure(cx.Dl, dev, 4 * SBK * 16));
     if (lamode) {
@@ -2712,7 +2779,7 @@ static int brr_fit_impl(const double* X, int64_t n, int64_t p, int64_t ldx, cons
     if (std::getenv("GBM_BRR_TRACE")) {
       if (g_brr_trace) (void)hipFree(g_brr_trace);
       g_brr_trace = nullptr;
-      const int64_t tn = std::max<int64_t>(2 * nsb * 12, (int64_t)sbC * nsb * 8);  // sb: 2 x 12, la: C x 8 per super-block
+      const int64_t tn = std::max<int64_t>(2 * nsb * 12, (int64_t)std::max(sbC, la2C) * nsb * 8);  // sb: 2 x 12, la: C x 8 per super-block
       GBM_HIP_TRY(hipMalloc((void**)&g_brr_trace, (size_t)(tn * 8)));
       g_brr_trace_n = tn;
     } else if (g_brr_trace) {
@@ -2788,15 +2855,15 @@ static int brr_fit_impl(const double* X, int64_t n, int64_t p, int64_t ldx, cons
             level, (const double*)cx.Wsb.p, (const double*)cx.alph.p, (double*)cx.MS.p, (double*)cx.Ssc.p);
       int32_t* cn = (int32_t*)cx.sbcnt.p + 24;  // the error cell (zeroed at setup)
       if (la2mode && g_brr_trace)
-        brr_sweep_la2_kernel<true><<<(unsigned)sbC, 256, 0, s>>>(
+        brr_sweep_la2_kernel<true><<<(unsigned)la2C, 256, 0, s>>>(
             (const uint8_t*)cx.D.p, npad, n, p, xs, (const double*)cx.MS.p, (const double*)cx.CS.p,
-            (const double*)cx.CS2.p, nsb, sbK, sbR, (double*)cx.Pb.p, (double*)cx.Rt.p, (double*)cx.Dl.p, cn,
+            (const double*)cx.CS2.p, nsb, la2Ko, la2O, la2Kn, la2R, (double*)cx.Pb.p, (double*)cx.Rt.p, (double*)cx.Dl.p, cn,
             (double*)cx.b.p, (double*)cx.bbar.p, (const double*)cx.alph.p, (const double*)cx.gamm.p,
             (double*)cx.e.p, stp, g_brr_trace);
       else if (la2mode)
-        brr_sweep_la2_kernel<false><<<(unsigned)sbC, 256, 0, s>>>(
+        brr_sweep_la2_kernel<false><<<(unsigned)la2C, 256, 0, s>>>(
             (const uint8_t*)cx.D.p, npad, n, p, xs, (const double*)cx.MS.p, (const double*)cx.CS.p,
-            (const double*)cx.CS2.p, nsb, sbK, sbR, (double*)cx.Pb.p, (double*)cx.Rt.p, (double*)cx.Dl.p, cn,
+            (const double*)cx.CS2.p, nsb, la2Ko, la2O, la2Kn, la2R, (double*)cx.Pb.p, (double*)cx.Rt.p, (double*)cx.Dl.p, cn,
             (double*)cx.b.p, (double*)cx.bbar.p, (const double*)cx.alph.p, (const double*)cx.gamm.p,
             (double*)cx.e.p, stp, nullptr);
       else if (lamode && g_brr_trace)
@@ -2860,7 +2927,7 @@ static int brr_fit_impl(const double* X, int64_t n, int64_t p, int64_t ldx, cons
                                     (int64_t)(uintptr_t)cx.flg.p, (int64_t)(uintptr_t)cx.e.p, (int64_t)(uintptr_t)cx.b.p,
                                     (int64_t)(uintptr_t)cx.bbar.p, (int64_t)(uintptr_t)cx.alph.p,
                                     (int64_t)(uintptr_t)cx.gamm.p, (int64_t)(uintptr_t)cx.x2.p,
-                                    (int64_t)(uintptr_t)cx.stm.p, sbmode ? 1 : 0, sbK, sbC, sbR,
+                                    (int64_t)(uintptr_t)cx.stm.p, sbmode ? 1 : 0, sbK, sbC, sbR, la2Ko, la2O, la2Kn, la2R, la2C,
                                     (int64_t)(uintptr_t)cx.MS.p, (int64_t)(uintptr_t)cx.Wsb.p, (int64_t)(uintptr_t)cx.Ssc.p,
                                     (int64_t)(uintptr_t)cx.Pb.p, (int64_t)(uintptr_t)cx.Rt.p, (int64_t)(uintptr_t)cx.Dl.p,
                                     (int64_t)(uintptr_t)cx.sbcnt.p, (int64_t)(uintptr_t)g_brr_trace, lamode ? 1 : 0,
@@ -2904,6 +2971,12 @@ static int brr_fit_impl(const double* X, int64_t n, int64_t p, int64_t ldx, cons
     }
   }
   g_brr_last_path.store(la2mode ? 4 : lamode ? 3 : sbmode ? 2 : sweep ? 1 : 0);
+  if (la2mode)
+    g_brr_shape.store((int64_t)la2C | ((int64_t)la2O << 12) | ((int64_t)la2R << 24) | ((int64_t)la2Ko << 32) |
+                      ((int64_t)la2Kn << 44));
+  else if (sbmode)
+    g_brr_shape.store((int64_t)sbC | ((int64_t)((SBK + sbR - 1) / sbR) << 12) | ((int64_t)sbR << 24) |
+                      ((int64_t)sbK << 32) | ((int64_t)sbK << 44));
   BrrState fin{};
   GBM_HIP_TRY(hipMemcpyAsync(&fin, cx.stm.p, sizeof(BrrState), hipMemcpyDeviceToHost, s));
   GBM_HIP_TRY(hipMemcpyAsync(b_hat_out + 1, cx.bbar.p, p * 8, hipMemcpyDeviceToHost, s));

@@ -38,7 +38,7 @@ EXPORTS = (
     "gbm_dev_chol_prepare", "gbm_dev_chol_group_size", "gbm_dev_chol_group", "gbm_dev_chol_factor_diag",
     "gbm_dev_chol_strip_doubles", "gbm_dev_chol_strip_pack", "gbm_dev_chol_strip_unpack", "gbm_dev_chol_finish",
     "gbm_dev_grm_packed_size", "gbm_dev_grm_pack", "gbm_dev_grm_unpack",
-    "gbm_debug_brr_stats", "gbm_debug_brr_trace", "gbm_debug_chol_flow_trace",
+    "gbm_debug_brr_stats", "gbm_debug_brr_shape", "gbm_debug_brr_trace", "gbm_debug_chol_flow_trace",
 )
 
 

@@ -372,6 +372,9 @@ int gbm_brr_fit(const double* X, int64_t n, int64_t p, int64_t ldx, const double
  * super-blocks of slack for the partial dots) and how many fits so far fell
  * back to the per-launch schedule after a sweep hand-off timed out (*fallbacks). */
 int gbm_debug_brr_stats(int* last_path, int64_t* fallbacks);
+/* Chunk shape of the last super-block sweep: C workgroups, the first O own R rows of every
+ * super-block and take Ko individuals each, the others Kn. */
+int gbm_debug_brr_shape(int* C, int* O, int* R, int* Ko, int* Kn);
 /* With GBM_BRR_TRACE=1 set for a fit: copies up to cap int64 timestamps (100 MHz) of the last
  * super-block sweep into host; returns the count, 0 when no trace was taken, -1 on a HIP error. */
 int64_t gbm_debug_brr_trace(int64_t* host, int64_t cap);

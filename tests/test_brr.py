@@ -177,7 +177,8 @@ def brr_path():
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("n,p,K", [(1100, 300, None), (12000, 1300, None), (5000, 777, "64"), (3000, 1025, "32"),
-                                   (10000, 1100, None), (4000, 900, None), (6000, 2600, None)])
+                                   (10000, 1100, None), (4000, 900, None), (6000, 2600, None), (10000, 1100, "R4"),
+                                   (9000, 2100, "R2")])
 def test_gpu_brr_super_block_sweep_runs_and_matches(monkeypatch, n, p, K):
     """The super-block sweeps really run (no fall-back to the per-launch path): the look-ahead forms
     (chunks of <= 48 individuals, two granule hand-offs per super-block) with two steps of slack
@@ -185,8 +186,11 @@ def test_gpu_brr_super_block_sweep_runs_and_matches(monkeypatch, n, p, K):
     with one (brr_sweep_la_kernel, path 3, GBM_BRR_LA2=0), and brr_sweep_sb_kernel (path 2: three
     hand-offs; also GBM_BRR_LA=0). All agree with the 128-block sweep (GBM_BRR_SB=0), the
     per-launch path and the oracle's literal loop; ragged p (p mod 512 = 300, 276, 265, 1, 76)
-    including nsb = 1, 2, 3, 6; several chunk sizes."""
-    if K:
+    including nsb = 1, 2, 3, 6; several chunk sizes, and the two-step form's owner/non-owner chunk
+    split (owners of R = 8, 4, 2 rows with smaller chunks)."""
+    if K and K.startswith("R"):  # owners of R rows in the two-step form's chunk split
+        monkeypatch.setenv("GBM_BRR_OWN_R", K[1:])
+    elif K:
         monkeypatch.setenv("GBM_BRR_SB_K", K)
     X = oracle.synth_genotypes(n + p, n, p)
     y = oracle.synth_phenotypes(X, 17)[:, 0]

@@ -27,19 +27,20 @@ lib = gbm.load_library()
 nsb = (p + 511) // 512
 path, fb = ctypes.c_int(-1), ctypes.c_int64(0)
 lib.gbm_debug_brr_stats(ctypes.byref(path), ctypes.byref(fb))
-K = max(16, -(-(-(-n // 256)) // 16) * 16)
-C = -(-n // K)
-R = -(-(-(-512 // C)) // 2) * 2
+sh = [ctypes.c_int(0) for _ in range(5)]
+lib.gbm_debug_brr_shape(*[ctypes.byref(v) for v in sh])
+C, O, R, Ko, Kn = [v.value for v in sh]
 cap = max(2 * nsb * 12, C * nsb * 8)
 buf = np.zeros(cap, dtype=np.int64)
 lib.gbm_debug_brr_trace.restype = ctypes.c_int64
 got = lib.gbm_debug_brr_trace(buf.ctypes.data_as(ctypes.c_void_p), ctypes.c_int64(buf.size))
-out = {"tool": "brr_trace", "n": n, "p": p, "nsb": nsb, "records": int(got), "path": path.value}
+out = {"tool": "brr_trace", "n": n, "p": p, "nsb": nsb, "records": int(got), "path": path.value,
+       "shape": {"C": C, "O": O, "R": R, "Ko": Ko, "Kn": Kn}}
 if path.value in (3, 4):
     # every workgroup: marks 0 A end (δ_{s−1} seen), 1 B end (r̃ published), 5 e update end, 2 C end (P_{s+1}
     # published), 4 δ_s published, 3 step end (Q_{s+1} gathered); 100 MHz ticks -> µs
     T = buf[:C * nsb * 8].reshape(C, nsb, 8).astype(np.float64) / 100.0
-    own = np.arange(C) * R < 512
+    own = np.arange(C) < O
     for w, tag in ((0, "wg0"), (C - 1, "wg_last")):
         t = T[w]
         prev = np.concatenate([[t[0, 0]], t[:-1, 3]])

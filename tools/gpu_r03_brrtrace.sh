@@ -11,3 +11,7 @@ cat $OUT/prof.json
 f=$(find $OUT/prof -name 'run_kernel_stats.csv' | head -1); head -6 "$f" | cut -c1-60,200-320
 GBM_BRR_LA2=0 timeout -k 10 300 python3 tools/bench_next.py brr-c4 --n 10000 --p 100000 --iters 60 > $OUT/v3.json 2> $OUT/v3.err || { tail $OUT/v3.err; exit 1; }
 cat $OUT/v3.json
+GBM_BRR_OWN_R=4 timeout -k 10 300 python3 tools/bench_next.py brr-c4 --n 10000 --p 100000 --iters 60 > $OUT/r4.json 2> $OUT/r4.err || { tail $OUT/r4.err; exit 1; }
+cat $OUT/r4.json
+GBM_BRR_OWN_R=4 timeout -k 10 300 python3 tools/brr_trace.py > $OUT/trace_r4.json 2> $OUT/trace_r4.err || { tail $OUT/trace_r4.err; exit 1; }
+cat $OUT/trace_r4.json
