@@ -171,6 +171,10 @@ __device__ __forceinline__ int factor_block_inv(double* X, double* bc, double* D
             y[t] = fma(-m2, b2[t], y[t]);
           }
         }
+        // y[c] is final here: pinned, so that LLVM cannot sink the identity columns' eliminations
+        // out of the loop into the lane < 16 block after it (it did: a serial chain of ~200
+        // dependent fp64 ops after every leaf, ≈1 µs on the pivot chain)
+        asm volatile("" : "+v"(y[c]));
         __builtin_amdgcn_sched_barrier(0);
         l2 = l1;
         m2 = m1;
@@ -385,6 +389,16 @@ chol_flow_kernel(double* __restrict__ G, int64_t ld, int nbc, double* __restrict
       auto idle = [&](int kb) {
         const int t = tid - 64;
         if (kb == 0 && i > 0) {
+          // the rest of this tile's last update (k = i − 1, from U_i−1,i in X2; rows 0-15 were done
+          // on the chain): 16x16 blocks (1,1) (1,2) | (1,3) (2,2) | (2,3) (3,3) on waves 1 | 2 | 3
+          const int b0 = 2 * (wave - 1);
+#pragma unroll
+          for (int q = 0; q < 2; q++) {
+            const int bb = b0 + q;  // 0..5 -> (row block, column block)
+            const int rb = bb < 3 ? 1 : (bb < 5 ? 2 : 3);
+            const int cb = bb < 3 ? 1 + bb : (bb < 5 ? bb - 1 : 3);
+            mfma_tile_sub_t(Xa, rb * 16, cb * 16, X2, rb * 16, X2, cb * 16, 0, 16, lane);
+          }
           for (int e = t; e < FT * 8; e += 192) {  // 64 rows x 8 pieces of 8 doubles
             const int row = e >> 3, piece = e & 7;
             double* dl = G + (i0 + row) * ld + (i0 - FT) + piece * 8;
@@ -432,41 +446,10 @@ chol_flow_kernel(double* __restrict__ G, int64_t ld, int nbc, double* __restrict
           });
       lds_sync();
       if (kTrace) ct[10] = (int64_t)__builtin_amdgcn_s_memrealtime();
-      // ---- the next diagonal tile's last update, k = i, from LDS (the workers' k-loop step: same
-      // operands, order and lane layout, so the same bits)
-      if (next_diag && !(wr == 1 && wc == 0)) {
-        d4 acc[2][2];
-#pragma unroll
-        for (int m = 0; m < 2; m++)
-#pragma unroll
-          for (int r = 0; r < 4; r++) {
-            const int row = 32 * wr + 2 * (fr + 4 * r) + m;
-            const dbl2 v = *reinterpret_cast<const dbl2*>(&Xn[row * PS + 32 * wc + 2 * fc]);
-            acc[m][0][r] = v.x;
-            acc[m][1][r] = v.y;
-          }
-#pragma unroll
-        for (int ks = 0; ks < 16; ks++) {
-          const int kk = ks * 4 + fr;
-          const dbl2 av = *reinterpret_cast<const dbl2*>(&X2[kk * PS + 32 * wr + 2 * fc]);
-          const dbl2 bv = *reinterpret_cast<const dbl2*>(&X2[kk * PS + 32 * wc + 2 * fc]);
-          const double na0 = -av.x, na1 = -av.y;
-          acc[0][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(na0, bv.x, acc[0][0], 0, 0, 0);
-          acc[0][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(na0, bv.y, acc[0][1], 0, 0, 0);
-          acc[1][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(na1, bv.x, acc[1][0], 0, 0, 0);
-          acc[1][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(na1, bv.y, acc[1][1], 0, 0, 0);
-        }
-#pragma unroll
-        for (int m = 0; m < 2; m++)
-#pragma unroll
-          for (int r = 0; r < 4; r++) {
-            const int row = 32 * wr + 2 * (fr + 4 * r) + m;
-            dbl2 v;
-            v.x = acc[m][0][r];
-            v.y = acc[m][1][r];
-            *reinterpret_cast<dbl2*>(&Xn[row * PS + 32 * wc + 2 * fc]) = v;
-          }
-      }
+      // ---- the next diagonal tile's last update, k = i, from LDS: on the chain only its first 16
+      // rows (block (0, w) on wave w), which the next factor's first leaf needs; the other six
+      // upper blocks run on waves 1-3 beside that leaf (idle(0) of the next step)
+      if (next_diag) mfma_tile_sub_t(Xn, 0, wave * 16, X2, 0, X2, wave * 16, 0, 16, lane);
       // ---- publish (i, i + 1): every storing wave drains its write-through stores (the update above
       // ran meanwhile), then one flag store
       if (kTrace) ct[11] = (int64_t)__builtin_amdgcn_s_memrealtime();
