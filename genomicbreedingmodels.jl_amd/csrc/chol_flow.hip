@@ -99,144 +99,285 @@ __device__ __forceinline__ void wave_wait2(const int32_t* fa, const int32_t* fb,
   // compiler from hoisting them above the poll
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
+// every lane of the calling wave: wait (one lane polls, bounded as poll2) until *f has every bit of mask
+__device__ __noinline__ bool poll_bits(const int32_t* f, int32_t mask, int32_t* info) {
+  for (int64_t it = 0;; it++) {
+    if ((__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & mask) == mask) return true;
+    if ((it & 255) == 255) {
+      if (__hip_atomic_load(info, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < 0) return false;
+      if (it > ((int64_t)1 << 22)) {
+        __hip_atomic_store(info, -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return false;
+      }
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+}
+__device__ __forceinline__ void wave_wait_bits(const int32_t* f, int32_t mask, int32_t* info, int lane) {
+  int ok = 1;
+  if (lane == 0) ok = poll_bits(f, mask, info) ? 1 : 0;
+  (void)__builtin_amdgcn_readfirstlane(ok);
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
 __device__ __forceinline__ bool wave_ready2(const int32_t* fa, const int32_t* fb, int lane) {
   int r = 0;
   if (lane == 0) r = (flag_set(fa) && flag_set(fb)) ? 1 : 0;
   return __builtin_amdgcn_readfirstlane(r) != 0;
 }
 
-// Upper Cholesky of the 64x64 block in X (LDS, pitch PS, upper part valid) by a 256-thread
-// workgroup, together with the inverses of its four 16x16 diagonal blocks. Four 16-row leaves:
-// wave 0 eliminates the leaf's rows over all remaining columns (lane l = column o + l) and, in
-// lanes 0..15, carries identity columns through the same eliminations, so that column l of
-// U_leaf⁻ᵀ (= row l of U_leaf⁻¹, the Dinv layout) comes out beside the factor and is stored
-// straight to Dinv (sc1) and to Dl (LDS, same layout). Step c is split so that only its first two
-// row updates are near the chain to the next pivot: rows c + 1, c + 2 are updated from v_readlane
-// of U[c][c+1], U[c][c+2]; the rows beyond take U[c][·]
-// from an LDS broadcast written in step c, read in step c + 1 and applied in step c + 2, so
-// neither the LDS round trip nor those updates sit on the pivot chain.
-// Between leaves all waves update the block's remaining upper 16x16 tiles by MFMA. Leaves U in X
-// (zeros below the diagonal); bc = 48 doubles of LDS scratch. Returns the first failing column or -1.
-// idle(kb): run by waves 1-3 beside leaf kb's steps, once their updates of the previous leaf are
-// done (rows < 16 kb of X are final then); row_out(kb, r, v): wave 0's final row r of U (lane =
-// column 16 kb + lane, valid lanes < 64 − 16 kb), e.g. to store it as soon as it is final.
-template <typename Idle, typename RowOut>
-__device__ __forceinline__ int factor_block_inv(double* X, double* bc, double* Dl, int tid,
-                                                __amdgpu_buffer_rsrc_t rDi, uint32_t dinv_base,
-                                                int64_t* tt, Idle&& idle, RowOut&& row_out) {
-  const int lane = tid & 63, wave = tid >> 6;
-#pragma unroll 1
-  for (int kb = 0; kb < 4; kb++) {
-    const int o = kb * 16;
-    if (wave == 0) {
-      const int ncols = CNB - o;
-      const int cc = o + (lane < ncols ? lane : 0);
-      double x[16], y[16], b1[16], b2[16];
-#pragma unroll
-      for (int t = 0; t < 16; t++) {
-        x[t] = X[(o + t) * PS + cc];
-        y[t] = t == lane ? 1.0 : 0.0;
-        b1[t] = 0.0;
-        b2[t] = 0.0;
-      }
-      double l1 = 0.0, m1 = 0.0, l2 = 0.0, m2 = 0.0;  // multipliers of steps c − 1 and c − 2
-#pragma unroll
-      for (int c = 0; c < 16; c++) {
-        // chain: pivot -> multipliers -> rows c + 1 and c + 2 (from v_readlane of U[c][c+1..c+2])
-        const double r = rsqrt_nr(readlane_d(x[c], c));  // a non-positive pivot propagates NaN
-        const double lc = x[c] * r, yc = y[c] * r;
-        x[c] = lc;
-        y[c] = yc;
-#pragma unroll
-        for (int d = 1; d <= 2; d++)
-          if (c + d < 16) {
-            const double u = readlane_d(lc, c + d);  // U[o + c][o + c + d]
-            x[c + d] = fma(-lc, u, x[c + d]);
-            y[c + d] = fma(-yc, u, y[c + d]);
-          }
-        __builtin_amdgcn_sched_barrier(0);
-        // U[c − 1][·] (written last step) -> b1; this step's row -> LDS (three buffers: a row is
-        // overwritten three steps after it was written, long after its reads completed)
-        __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
-        if (c >= 1 && c + 2 < 16) {
-#pragma unroll
-          for (int t = c + 2; t < 16; t++) b1[t] = bc[((c - 1) % 3) * 16 + t];
-        }
-        if (c + 3 < 16 && lane < 16) bc[(c % 3) * 16 + lane] = lc;
-        // step c − 2's updates of rows c + 1.. (rows c − 1 and c were its chain part)
-        if (c >= 2) {
-#pragma unroll
-          for (int t = c + 1; t < 16; t++) {
-            x[t] = fma(-l2, b2[t], x[t]);
-            y[t] = fma(-m2, b2[t], y[t]);
-          }
-        }
-        // y[c] is final here: pinned, so that LLVM cannot sink the identity columns' eliminations
-        // out of the loop into the lane < 16 block after it (it did: a serial chain of ~200
-        // dependent fp64 ops after every leaf, ≈1 µs on the pivot chain)
-        asm volatile("" : "+v"(y[c]));
-        __builtin_amdgcn_sched_barrier(0);
-        l2 = l1;
-        m2 = m1;
-        l1 = lc;
-        m1 = yc;
-#pragma unroll
-        for (int t = 0; t < 16; t++) b2[t] = b1[t];
-      }
-      if (tt) tt[kb] = (int64_t)__builtin_amdgcn_s_memrealtime();
-      if (lane < ncols) {
-#pragma unroll
-        for (int t = 0; t < 16; t++) {
-          const double v = (lane < 16 && t > lane) ? 0.0 : x[t];
-          X[(o + t) * PS + cc] = v;
-          row_out(kb, o + t, v);
-        }
-      }
-      if (lane < 16) {
-#pragma unroll
-        for (int e = 0; e < 16; e += 2) {
-          dbl2 v;
-          v.x = y[e];
-          v.y = y[e + 1];
-          *reinterpret_cast<dbl2*>(&Dl[kb * 256 + lane * 16 + e]) = v;
-        }
-      }
-      // Dinv (write-through) from Dl: two coalesced 1 KB stores (lane l's 128 B column stored by 16
-      // lanes as 8 scattered pieces cost ~1 µs)
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#pragma unroll
-      for (int q = 0; q < 2; q++) {
-        const int e = (q * 64 + lane) * 2;
-        st2(rDi, dinv_base + (uint32_t)((kb * 256 + e) * 8), *reinterpret_cast<const dbl2*>(&Dl[kb * 256 + e]));
-      }
+// LDS words the chain's four waves synchronise on inside a factor (monotonic over the steps, so
+// nothing is reset between steps)
+struct ChainSync {
+  int rows;    // 64 * step + the rows of U_ii final in X
+  int b13;     // step + 1 once block (1, 3) of the previous step's last update is in X
+  int pro;     // 3 per step: waves 1-3 have finished reading X2 for that last update
+  int x2;      // step + 1 once X2 holds the right neighbour's partial A_i,i+1
+  int dl;      // 4 * step + leaves whose inverse is in Dl
+  int nrow;    // 16 * step + finished 16x16 blocks of the neighbour solve
+  int item;    // the next of this step's 12 block-row-0..2 blocks to take (reset at the step's end)
+  int64_t tt[4];  // trace: leaf ends
+  int64_t ts[4];  // trace: own-leaf starts (after following the earlier leaves)
+  int64_t th[4];  // trace: X2 fetched, Xn fetched, helper waves 0 and 1 done
+};
+__device__ __forceinline__ int lds_poll(int* p) {
+  return __builtin_amdgcn_readfirstlane(__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+}
+__device__ __forceinline__ void lds_post(int* p, int v, int lane) {
+  if (lane == 0) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+// every lane of the calling wave: spin on an LDS word of this workgroup until it reaches v (bounded: the
+// writers never wait on anything outside the workgroup, so the bound only guards a bug)
+__device__ __forceinline__ int lds_wait(int* p, int v, int32_t* info, int lane) {
+  int s = lds_poll(p);
+  for (int it = 0; s < v; it++) {
+    __builtin_amdgcn_s_sleep(1);  // ~64 cycles: the spin shares the LDS pipe with the leaf owner
+    s = lds_poll(p);
+    if (it > (1 << 22)) {
+      if (lane == 0) atomicCAS(info, 0, -1);
+      return v;
     }
-    if (tt && kb == 1) tt[12] = (int64_t)__builtin_amdgcn_s_memrealtime();
-    if (wave >= 1) idle(kb);
-    lds_sync();
-    if (tt && kb == 1) tt[13] = (int64_t)__builtin_amdgcn_s_memrealtime();
-    // update of the block's remaining upper 16x16 tiles (b <= a < m) by leaf kb's rows: the first
-    // tile row (the next leaf's rows) by waves 1..m, then wave 0 goes on with the next leaf while
-    // waves 1.. update the rest (done before the next leaf's closing barrier, i.e. before any
-    // later leaf reads those rows)
-    const int m = 3 - kb;  // remaining 16-blocks
-    if (wave >= 1 && wave <= m) {
-      const int c0 = o + 16 + (wave - 1) * 16;
-      mfma_tile_sub_t(X, o + 16, c0, X, o + 16, X, c0, o, 4, lane);
-    }
-    lds_sync();
-    if (wave >= 1) {
-      for (int t = wave - 1; t < m * (m - 1) / 2; t += 3) {
-        int a = 1;
-        while (a * (a + 1) / 2 <= t) a++;
-        const int b = t - (a - 1) * a / 2 + 1;  // 1 <= b <= a: tile (row b, col a)
-        const int r0 = o + 16 + b * 16, c0 = o + 16 + a * 16;
-        mfma_tile_sub_t(X, r0, c0, X, r0, X, c0, o, 4, lane);
-      }
-    }
-    if (tt && kb < 3) tt[4 + kb] = (int64_t)__builtin_amdgcn_s_memrealtime();
   }
-  // (the lower parts of the diagonal 16x16 blocks hold leftovers of the MFMA updates; nothing
-  // reads below the diagonal of a factored block)
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // no LDS read of the payload above the poll
+  return s;
+}
+
+// Wave W (1..3) of the chain before its own leaf: the update of its rows 16W..16W+15 (column blocks
+// W..3) by every earlier row of U_ii, accumulated by MFMA in registers four rows at a time as the
+// owners publish them (sy->rows), then subtracted from the rows (x, lane = column 16W + lane) once. With prev, the accumulators start
+// with the previous step's last update (k = i − 1, from U_i−1,i in X2) of the same blocks; block
+// (1, 3) of it is wave 3's (applied to X, then sy->b13), so that wave 1, whose rows are needed
+// first, has two blocks of it instead of three. Four rows per MFMA group: five LDS reads per group
+// instead of a broadcast read per row and element (the LDS pipe is shared with the owner).
+template <int W>
+__device__ __forceinline__ void follow_leaves(double* X, const double* X2, bool prev, ChainSync* sy, int step,
+                                              int32_t* info, int lane, double (&x)[16]) {
+  constexpr int NB = 4 - W;
+  const int fr = lane >> 4, fc = lane & 15;
+  const int base = 64 * step;
+  d4 acc[NB];
+#pragma unroll
+  for (int b = 0; b < NB; b++) acc[b] = (d4){0.0, 0.0, 0.0, 0.0};
+  if (prev) {
+    d4 t13 = (d4){0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int ks = 0; ks < 16; ks++) {
+      const double* r = X2 + (ks * 4 + fr) * PS;
+      const double a = r[16 * W + fc];
+#pragma unroll
+      for (int b = 0; b < NB; b++)
+        if (!(W == 1 && b == 2)) acc[b] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, r[16 * (W + b) + fc], acc[b], 0, 0, 0);
+      if (W == 3) t13 = __builtin_amdgcn_mfma_f64_16x16x4f64(r[16 + fc], r[48 + fc], t13, 0, 0, 0);
+    }
+    if (W == 3) {
+#pragma unroll
+      for (int r = 0; r < 4; r++) X[(16 + fr + 4 * r) * PS + 48 + fc] -= t13[r];
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      lds_post(&sy->b13, step + 1, lane);
+    }
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // X2 read
+  if (lane == 0) __hip_atomic_fetch_add(&sy->pro, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  // the rows' current values (wave 1: with wave 3's block (1, 3) of the last update applied)
+  if (W == 1 && prev) lds_wait(&sy->b13, step + 1, info, lane);
+  const int cc = 16 * W + (lane < 64 - 16 * W ? lane : 0);
+#pragma unroll
+  for (int t = 0; t < 16; t++) x[t] = X[(16 * W + t) * PS + cc];
+  int seen = 0;
+#pragma unroll 1
+  for (int g = 0; g < 4 * W; g++) {
+    if (seen < 4 * g + 4) seen = lds_wait(&sy->rows, base + 4 * g + 4, info, lane) - base;
+    const double* r = X + (4 * g + fr) * PS;
+    const double a = r[16 * W + fc];
+#pragma unroll
+    for (int b = 0; b < NB; b++) acc[b] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, r[16 * (W + b) + fc], acc[b], 0, 0, 0);
+  }
+  // the accumulated update, transposed to the leaf layout (lane = column) through the rows' place in X
+#pragma unroll
+  for (int b = 0; b < NB; b++)
+#pragma unroll
+    for (int r = 0; r < 4; r++) X[(16 * W + fr + 4 * r) * PS + 16 * (W + b) + fc] = acc[b][r];
+  // (gfx950 does not order a wave's ds_read after its own ds_write)
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+  for (int t = 0; t < 16; t++) x[t] -= X[(16 * W + t) * PS + cc];
+}
+
+// Block row RB, column block cb of the right neighbour U_i,i+1 = U_ii⁻ᵀ A_i,i+1 (in X2, pitch PS), one
+// wave: X2_RB,cb <- (D_RB⁻¹)ᵀ (X2_RB,cb − U[0:16 RB, RB]ᵀ X2[0:16 RB, cb]). All operand reads are issued
+// before the first MFMA; the updated block is already in the B-operand layout of the D⁻¹ product
+// (lane (fr, fc) holds rows fr + 4r = the k-step r operand), so it needs no LDS round trip.
+// emit(row, v): the final value of row `row` (0..63), column 16 cb + (lane & 15).
+template <int RB, typename Emit>
+__device__ __forceinline__ void nbr_block(double* X2, const double* Xa, const double* Dl, int cb, int lane,
+                                          Emit&& emit) {
+  const int fr = lane >> 4, fc = lane & 15;
+  constexpr int KS = RB > 0 ? 4 * RB : 1;
+  double a[KS], b[KS], c[4];
+#pragma unroll
+  for (int r = 0; r < 4; r++) c[r] = X2[(16 * RB + fr + 4 * r) * PS + 16 * cb + fc];
+  if (RB > 0) {
+#pragma unroll
+    for (int ks = 0; ks < 4 * RB; ks++) {
+      a[ks] = Xa[(ks * 4 + fr) * PS + 16 * RB + fc];
+      b[ks] = X2[(ks * 4 + fr) * PS + 16 * cb + fc];
+    }
+    d4 sacc = (d4){0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int ks = 0; ks < 4 * RB; ks++) sacc = __builtin_amdgcn_mfma_f64_16x16x4f64(a[ks], b[ks], sacc, 0, 0, 0);
+#pragma unroll
+    for (int r = 0; r < 4; r++) c[r] -= sacc[r];
+  }
+  d4 acc = (d4){0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int ks = 0; ks < 4; ks++)
+    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(Dl[RB * 256 + (ks * 4 + fr) * 16 + fc], c[ks], acc, 0, 0, 0);
+#pragma unroll
+  for (int r = 0; r < 4; r++) {
+    const int row = 16 * RB + fr + 4 * r;
+    X2[row * PS + 16 * cb + fc] = acc[r];
+    emit(row, acc[r]);
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+}
+
+// Upper Cholesky of the 64x64 block in X (LDS, pitch PS) by the chain's 256 threads, with the inverses
+// of its four 16x16 diagonal blocks. Wave w owns leaf w (rows 16w..16w+15). While the earlier leaves
+// are factored it FOLLOWS them (follow_leaves: their final rows applied to its rows by MFMA, four at a
+// time, as the owners publish them), so when its own leaf begins its rows are up to date — no
+// workgroup barrier and no separate leaf update between leaves. The owner's 16-step loop (lane l =
+// column 16w + l): the pivot chain (readlane → rsqrt + Newton → scale) with rows c + 1, c + 2 updated
+// from v_readlane of U[c][c+1..c+2] and the rows beyond from the LDS row written the step before,
+// applied two steps behind; lanes 0..15 carry identity columns through the same eliminations, so
+// column l of U_leaf⁻ᵀ (= row l of U_leaf⁻¹, the Dinv layout) comes out beside the factor. Each
+// final row goes to X as soon as it is computed, and the row count to sy->rows one step later.
+// prev: the step's last update k = i − 1 of rows 16.. (from U_i−1,i in X2) is still to be applied
+// (row block 0 was, at the end of the previous step); the followers fold it into their accumulators.
+// Each owner stores its leaf's rows to Ld (rLd, write-through) and its Dinv block, then sets bit w
+// of leaf_bits; after_own(w) runs on wave w once its leaf is done. Returns the first failing column
+// or −1.
+template <typename AfterOwn>
+__device__ __forceinline__ int factor_block_pipe(double* X, const double* X2, bool prev, double* Dl, int tid,
+                                                 __amdgpu_buffer_rsrc_t rDi, uint32_t dinv_base,
+                                                 __amdgpu_buffer_rsrc_t rLd, int64_t i0, ChainSync* sy, int step,
+                                                 int32_t* info, int32_t* leaf_bits, AfterOwn&& after_own) {
+  const int lane = tid & 63, w = tid >> 6;
+  const int o = 16 * w, base = 64 * step;
+  const int ncols = CNB - o;
+  const int cc = o + (lane < ncols ? lane : 0);
+  // row writes: lanes beyond the block go to the pitch padding (never read), so the store needs no
+  // exec mask; nothing reads X below the diagonal of a factored block, so no zeros are written there
+  const int cw = lane < ncols ? o + lane : CNB + (lane & 15);
+  double x[16], y[16];
+  if (w == 1) follow_leaves<1>(X, X2, prev, sy, step, info, lane, x);
+  else if (w == 2) follow_leaves<2>(X, X2, prev, sy, step, info, lane, x);
+  else if (w == 3) follow_leaves<3>(X, X2, prev, sy, step, info, lane, x);
+  else {
+#pragma unroll
+    for (int t = 0; t < 16; t++) x[t] = X[(o + t) * PS + cc];
+  }
+  // ---- own leaf w
+  if (lane == 0) sy->ts[w] = (int64_t)__builtin_amdgcn_s_memrealtime();
+  double b1[16], b2[16];
+#pragma unroll
+  for (int t = 0; t < 16; t++) {
+    y[t] = t == lane ? 1.0 : 0.0;
+    b1[t] = 0.0;
+    b2[t] = 0.0;
+  }
+  double l1 = 0.0, m1 = 0.0, l2 = 0.0, m2 = 0.0;  // multipliers of steps c − 1 and c − 2
+#pragma unroll
+  for (int c = 0; c < 16; c++) {
+    // chain: pivot -> multipliers -> rows c + 1 and c + 2 (from v_readlane of U[c][c+1..c+2])
+    const double r = rsqrt_nr(readlane_d(x[c], c));  // a non-positive pivot propagates NaN
+    const double lc = x[c] * r, yc = y[c] * r;
+    x[c] = lc;
+    y[c] = yc;
+#pragma unroll
+    for (int d = 1; d <= 2; d++)
+      if (c + d < 16) {
+        const double u = readlane_d(lc, c + d);  // U[o + c][o + c + d]
+        x[c + d] = fma(-lc, u, x[c + d]);
+        y[c + d] = fma(-yc, u, y[c + d]);
+      }
+    __builtin_amdgcn_sched_barrier(0);
+    // row c − 1 (written last step) is in X: publish it to the followers, read U[c − 1][·] -> b1;
+    // this step's final row -> X
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+    if (c >= 1) lds_post(&sy->rows, base + o + c, lane);
+    X[(o + c) * PS + cw] = lc;
+    if (c >= 1 && c + 2 < 16) {
+#pragma unroll
+      for (int t = c + 2; t < 16; t++) b1[t] = X[(o + c - 1) * PS + o + t];
+    }
+    // step c − 2's updates of rows c + 1.. (rows c − 1 and c were its chain part)
+    if (c >= 2) {
+#pragma unroll
+      for (int t = c + 1; t < 16; t++) {
+        x[t] = fma(-l2, b2[t], x[t]);
+        y[t] = fma(-m2, b2[t], y[t]);
+      }
+    }
+    // y[c] is final here: pinned, so that LLVM cannot sink the identity columns' eliminations out of
+    // the loop (it did: a serial chain of ~200 dependent fp64 ops after every leaf)
+    asm volatile("" : "+v"(y[c]));
+    __builtin_amdgcn_sched_barrier(0);
+    l2 = l1;
+    m2 = m1;
+    l1 = lc;
+    m1 = yc;
+#pragma unroll
+    for (int t = 0; t < 16; t++) b2[t] = b1[t];
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  lds_post(&sy->rows, base + o + 16, lane);  // the next leaf's owner goes on from here
+  if (lane == 0) sy->tt[w] = (int64_t)__builtin_amdgcn_s_memrealtime();
+  // ---- off the chain: this leaf's rows -> Ld, its inverse -> Dl and Dinv (write-through)
+  if (lane < ncols) {
+#pragma unroll
+    for (int t = 0; t < 16; t++) st1(rLd, (uint32_t)(((i0 + o + t) * CNB + cc) * 8), (lane < 16 && t > lane) ? 0.0 : x[t]);
+  }
+  if (lane < 16) {
+#pragma unroll
+    for (int e = 0; e < 16; e += 2) {
+      dbl2 v;
+      v.x = y[e];
+      v.y = y[e + 1];
+      *reinterpret_cast<dbl2*>(&Dl[w * 256 + lane * 16 + e]) = v;
+    }
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  if (w > 0) lds_wait(&sy->dl, 4 * step + w, info, lane);  // keep sy->dl in leaf order
+  lds_post(&sy->dl, 4 * step + w + 1, lane);
+#pragma unroll
+  for (int q = 0; q < 2; q++) {
+    const int e = (q * 64 + lane) * 2;
+    st2(rDi, dinv_base + (uint32_t)((w * 256 + e) * 8), *reinterpret_cast<const dbl2*>(&Dl[w * 256 + e]));
+  }
+  // workers solving this row's tiles go on leaf by leaf: one bit per leaf once its Ld rows and Dinv
+  // block are stored (drained write-through stores, then a relaxed agent-scope atomic)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if (lane == 0) __hip_atomic_fetch_or(leaf_bits, 1 << w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  after_own(w);
   lds_sync();
   const double dg = X[lane * PS + lane];
   const unsigned long long bm = __ballot(!(dg > 0.0) || !isfinite(dg));
@@ -297,7 +438,7 @@ chol_flow_kernel(double* __restrict__ G, int64_t ld, int nbc, double* __restrict
   __shared__ __attribute__((aligned(16))) double X2[FT * PS];
   __shared__ __attribute__((aligned(16))) double X3[FT * PS];
   __shared__ __attribute__((aligned(16))) double Dl[4 * 256];
-  __shared__ double bcast[48];
+  __shared__ ChainSync sy;
   __shared__ int s_task;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wr = wave >> 1, wc = wave & 1;
@@ -308,15 +449,7 @@ chol_flow_kernel(double* __restrict__ G, int64_t ld, int nbc, double* __restrict
   const __amdgpu_buffer_rsrc_t rLd = rsrc(Ld, (int64_t)nb * FT * CNB * 8);
   const __amdgpu_buffer_rsrc_t rDi = rsrc(Dinv, (int64_t)nb * FT * 16 * 8);
 
-  // U_ij in X (LDS) -> G upper (sc1: later tiles of this launch read it) ...
-  auto store_upper = [&](const double* Xs, int64_t i0, int64_t j0) {
-    const int row = tid >> 2, quarter = tid & 3;
-    const __amdgpu_buffer_rsrc_t rG = rsrc(G + i0 * ld, gbytes_rowblk);
-    const uint32_t base = (uint32_t)(((int64_t)row * ld + j0 + quarter * 16) * 8);
-#pragma unroll
-    for (int e = 0; e < 16; e += 2) st2(rG, base + e * 8, *reinterpret_cast<const dbl2*>(&Xs[row * PS + quarter * 16 + e]));
-  };
-  // ... and its transposed copy -> G lower (rows j0.., columns i0..; read only by the back
+  // a solved tile's transposed copy -> G lower (rows j0.., columns i0..; read only by the back
   // substitution / μ̂ kernels after this launch, so stored after the tile's flag)
   auto store_lower = [&](const double* Xs, int64_t i0, int64_t j0) {
     const int row = tid >> 2, quarter = tid & 3;
@@ -332,6 +465,9 @@ chol_flow_kernel(double* __restrict__ G, int64_t ld, int nbc, double* __restrict
 
   if (blockIdx.x == 0) {
     // ================================ the chain ================================
+    if (tid == 0) {
+      sy.rows = sy.b13 = sy.pro = sy.x2 = sy.dl = sy.nrow = sy.item = 0;
+    }
     // A_00 has no update: straight from G (written before this launch)
     for (int e = tid; e < FT * FT / 2; e += 256) {
       const int r = e >> 5, c2 = (e & 31) * 2;
@@ -348,115 +484,119 @@ chol_flow_kernel(double* __restrict__ G, int64_t ld, int nbc, double* __restrict
       int64_t ct[16] = {};
       if (kTrace) ct[0] = (int64_t)__builtin_amdgcn_s_memrealtime();
       __builtin_amdgcn_s_setprio(2);
-      // waves 1-3, beside the last leaf: the neighbour's partial -> X2, the next diagonal tile's -> Xn
-      // waves 1-3: the neighbour's partial A_i,i+1 -> X2 and (next_diag) the next diagonal tile's
-      // A_i+1,i+1 -> Xn (sc1: other workgroups' partials), 11 16-byte pieces of each per thread, the
-      // loads of both tiles in flight before any LDS write
-      auto fetch_partials = [&]() {
-        const int t = tid - 64;
-        const __amdgpu_buffer_rsrc_t rG = rsrc(G + i0 * ld, gbytes_rowblk);
-        const __amdgpu_buffer_rsrc_t rG1 = rsrc(G + j0 * ld, gbytes_rowblk);
-        const int32_t* fn = flags + (int64_t)i * nbc + i + 1;
-        const int32_t* fd = flags + (int64_t)(i + 1) * nbc + i + 1;
-        dbl2 vn[11], vd[11];
-        wave_wait2(fn, fn, info, lane, kPartial);
+      // one wave: a partial tile of G (rows r0.., columns j0..; another workgroup's sc1 stores, seen
+      // through its flag) -> dst in LDS, all 32 pieces of 16 bytes per lane in flight at once; the LDS
+      // writes only after `gate` (the previous contents are no longer read)
+      auto fetch_tile = [&](double* dst, int64_t r0, const int32_t* f, auto&& gate) {
+        const __amdgpu_buffer_rsrc_t rG = rsrc(G + r0 * ld, gbytes_rowblk);
+        wave_wait2(f, f, info, lane, kPartial);
+        dbl2 v[32];
 #pragma unroll
-        for (int q = 0; q < 11; q++) {
-          const int e = t + q * 192;
-          if (e < FT * FT / 2) vn[q] = ld2(rG, (uint32_t)(((int64_t)(e >> 5) * ld + j0 + 2 * (e & 31)) * 8), 0);
+        for (int q = 0; q < 32; q++) {
+          const int e = lane + q * 64;
+          v[q] = ld2(rG, (uint32_t)(((int64_t)(e >> 5) * ld + j0 + 2 * (e & 31)) * 8), 0);
         }
-        if (next_diag) {
-          wave_wait2(fd, fd, info, lane, kPartial);
+        gate();
 #pragma unroll
-          for (int q = 0; q < 11; q++) {
-            const int e = t + q * 192;
-            if (e < FT * FT / 2) vd[q] = ld2(rG1, (uint32_t)(((int64_t)(e >> 5) * ld + j0 + 2 * (e & 31)) * 8), 0);
-          }
+        for (int q = 0; q < 32; q++) {
+          const int e = lane + q * 64;
+          *reinterpret_cast<dbl2*>(&dst[(e >> 5) * PS + 2 * (e & 31)]) = v[q];
         }
-#pragma unroll
-        for (int q = 0; q < 11; q++) {
-          const int e = t + q * 192;
-          if (e < FT * FT / 2) {
-            *reinterpret_cast<dbl2*>(&X2[(e >> 5) * PS + 2 * (e & 31)]) = vn[q];
-            if (next_diag) *reinterpret_cast<dbl2*>(&Xn[(e >> 5) * PS + 2 * (e & 31)]) = vd[q];
-          }
-        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       };
-      // waves 1-3 beside the leaves: leaf 0, the previous step's transposed copy of U_i−1,i (X2)
-      // below the diagonal of G (read only by later kernels); leaf kb >= 1, U_ii's final rows of
-      // leaf kb − 1 -> Ld (write-through: the row's other tiles read them); leaf 3, also the
-      // neighbour's partial A_i,i+1 -> X2 and the next diagonal tile's partial -> Xn
-      auto idle = [&](int kb) {
-        const int t = tid - 64;
-        if (kb == 0 && i > 0) {
-          // the rest of this tile's last update (k = i − 1, from U_i−1,i in X2; rows 0-15 were done
-          // on the chain): 16x16 blocks (1,1) (1,2) | (1,3) (2,2) | (2,3) (3,3) on waves 1 | 2 | 3
-          const int b0 = 2 * (wave - 1);
+      // the neighbour's blocks, stored write-through to G as soon as they are final
+      const __amdgpu_buffer_rsrc_t rN = rsrc(G + i0 * ld, gbytes_rowblk);
+      auto nbr_item = [&](int rb, int cb) {
+        auto emit = [&](int row, double v) { st1(rN, (uint32_t)(((int64_t)row * ld + j0 + 16 * cb + fc) * 8), v); };
+        if (rb == 0) nbr_block<0>(X2, Xa, Dl, cb, lane, emit);
+        else if (rb == 1) nbr_block<1>(X2, Xa, Dl, cb, lane, emit);
+        else if (rb == 2) nbr_block<2>(X2, Xa, Dl, cb, lane, emit);
+        else nbr_block<3>(X2, Xa, Dl, cb, lane, emit);
+      };
+      // wave w once leaf w is factored (beside the later leaves):
+      //   wave 0: the previous step's transposed copy of U_i−1,i (X2) below the diagonal of G (read
+      //   only by later kernels), then the neighbour's partial A_i,i+1 -> X2 (once waves 1-3 have read
+      //   X2 for this step's last update);
+      //   wave 1: the next diagonal tile's partial A_i+1,i+1 -> Xn (needed at the step's end);
+      //   waves 0-2: the neighbour solve's block rows 0-2 (12 16x16 blocks, taken in order from an LDS
+      //   counter; block row rb once leaf rb is factored and every block of row rb − 1 is done).
+      auto after_own = [&](int w) {
+        if (w == 0) {
+          if (i > 0) {
+            for (int e = lane; e < FT * 8; e += 64) {  // 64 rows x 8 pieces of 8 doubles
+              const int row = e >> 3, piece = e & 7;
+              double* dl = G + (i0 + row) * ld + (i0 - FT) + piece * 8;
 #pragma unroll
-          for (int q = 0; q < 2; q++) {
-            const int bb = b0 + q;  // 0..5 -> (row block, column block)
-            const int rb = bb < 3 ? 1 : (bb < 5 ? 2 : 3);
-            const int cb = bb < 3 ? 1 + bb : (bb < 5 ? bb - 1 : 3);
-            mfma_tile_sub_t(Xa, rb * 16, cb * 16, X2, rb * 16, X2, cb * 16, 0, 16, lane);
-          }
-          for (int e = t; e < FT * 8; e += 192) {  // 64 rows x 8 pieces of 8 doubles
-            const int row = e >> 3, piece = e & 7;
-            double* dl = G + (i0 + row) * ld + (i0 - FT) + piece * 8;
-#pragma unroll
-            for (int u = 0; u < 8; u += 2) {
-              dbl2 v;
-              v.x = X2[(piece * 8 + u) * PS + row];
-              v.y = X2[(piece * 8 + u + 1) * PS + row];
-              *reinterpret_cast<dbl2*>(dl + u) = v;
+              for (int u = 0; u < 8; u += 2) {
+                dbl2 v;
+                v.x = X2[(piece * 8 + u) * PS + row];
+                v.y = X2[(piece * 8 + u + 1) * PS + row];
+                *reinterpret_cast<dbl2*>(dl + u) = v;
+              }
             }
           }
+          fetch_tile(X2, i0, flags + (int64_t)i * nbc + i + 1,
+                     [&]() { lds_wait(&sy.pro, 3 * (i + 1), info, lane); });
+          lds_post(&sy.x2, i + 1, lane);
+          if (kTrace && lane == 0) sy.th[0] = (int64_t)__builtin_amdgcn_s_memrealtime();
         }
-        if (kb >= 1) {
-          // rows 16 (kb − 1) .. + 15 from column 16 (kb − 1): w pieces of 16 bytes per row
-          const int rb = kb - 1, w = 32 - 8 * rb;
-          for (int e = t; e < 16 * w; e += 192) {
-            const int row = rb * 16 + e / w, col = rb * 16 + 2 * (e % w);
-            st2(rLd, (uint32_t)(((i0 + row) * CNB + col) * 8), *reinterpret_cast<const dbl2*>(&Xa[row * PS + col]));
+        if (w == 1 && next_diag) {
+          fetch_tile(Xn, j0, flags + (int64_t)(i + 1) * nbc + i + 1, []() {});
+          if (kTrace && lane == 0) sy.th[1] = (int64_t)__builtin_amdgcn_s_memrealtime();
+        }
+        if (w <= 2) {
+#pragma unroll 1
+          for (;;) {
+            // every lane adds 1 (one ds_add_rtn of 64 per wave; no lane-0-only branch around the
+            // returned value): block index = the wave's first old value / 64
+            const int it =
+                __builtin_amdgcn_readfirstlane(__hip_atomic_fetch_add(&sy.item, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) >> 6;
+            if (it >= 12) break;
+            const int rb = it >> 2, cb = it & 3;
+            lds_wait(&sy.x2, i + 1, info, lane);
+            lds_wait(&sy.dl, 4 * i + rb + 1, info, lane);
+            lds_wait(&sy.nrow, 16 * i + 4 * rb, info, lane);
+            nbr_item(rb, cb);
+            if (lane == 0) __hip_atomic_fetch_add(&sy.nrow, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
           }
+          if (kTrace && lane == 0) sy.th[2 + (w & 1)] = (int64_t)__builtin_amdgcn_s_memrealtime();
         }
-        if (kb == 3) fetch_partials();
-      };
-      // wave 0: the last leaf's rows of U_ii -> Ld
-      auto row_out = [&](int kb, int r, double v) {
-        if (kb == 3) st1(rLd, (uint32_t)(((i0 + r) * CNB + 48 + lane) * 8), v);
       };
       // ---- U_ii = chol(A_ii) -> Ld, its 16x16 diagonal inverses -> Dinv (and Dl)
-      const int bad = factor_block_inv(Xa, bcast, Dl, tid, rDi, (uint32_t)((i0 / 16) * 256 * 8), kTrace ? ct + 1 : nullptr,
-                                       idle, row_out);
+      const int bad = factor_block_pipe(Xa, X2, i > 0, Dl, tid, rDi, (uint32_t)((i0 / 16) * 256 * 8), rLd, i0, &sy, i,
+                                        info, flags + (int64_t)(i + 1) * nbc + i, after_own);
       if (tid == 0 && bad >= 0) atomicCAS(info, 0, (int32_t)(i0 + bad + 1));
-      if (kTrace) ct[8] = (int64_t)__builtin_amdgcn_s_memrealtime();
-      // ---- publish (i, i): Ld and Dinv were stored during the factor
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      lds_sync();
-      if (tid == 0) __hip_atomic_store(flags + (int64_t)i * nbc + i, kFinal, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      // ---- the right neighbour: U_i,i+1 = U_ii⁻ᵀ A_i,i+1 (all MFMA, operands in LDS); each 16-row
-      // block of a wave's columns is stored (write-through) as soon as it is final
-      const __amdgpu_buffer_rsrc_t rN = rsrc(G + i0 * ld, gbytes_rowblk);
-      panel_chunk_solve(
-          X2, Xa, [&](int rb, int ks) { return Dl[rb * 256 + (ks * 4 + fr) * 16 + fc]; }, lane, wave,
-          [&](int rb, const d4& acc) {
+      if (kTrace) {
 #pragma unroll
-            for (int r = 0; r < 4; r++)
-              st1(rN, (uint32_t)(((int64_t)(rb * 16 + fr + 4 * r) * ld + j0 + wave * 16 + fc) * 8), acc[r]);
-          });
+        for (int kb = 0; kb < 4; kb++) ct[1 + kb] = sy.tt[kb];
+#pragma unroll
+        for (int kb = 0; kb < 3; kb++) ct[5 + kb] = sy.ts[kb + 1];  // the next leaf's own start
+        ct[13] = sy.ts[0];
+        ct[9] = sy.th[0];
+        ct[14] = sy.th[1];
+        ct[15] = sy.th[2] > sy.th[3] ? sy.th[2] : sy.th[3];
+      }
+      if (kTrace) ct[8] = (int64_t)__builtin_amdgcn_s_memrealtime();
+      // ---- the neighbour's last block row (wave w: column block w); its earlier rows were solved
+      // beside the factor
+      nbr_item(3, wave);
+      if (lane == 0) __hip_atomic_fetch_add(&sy.nrow, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      if (tid == 0) sy.item = 0;  // the next step's helpers start after its leaf 0, long after this barrier
       lds_sync();
       if (kTrace) ct[10] = (int64_t)__builtin_amdgcn_s_memrealtime();
       // ---- the next diagonal tile's last update, k = i, from LDS: on the chain only its first 16
       // rows (block (0, w) on wave w), which the next factor's first leaf needs; the other six
-      // upper blocks run on waves 1-3 beside that leaf (idle(0) of the next step)
+      // upper blocks are folded into the followers' accumulators of the next factor
       if (next_diag) mfma_tile_sub_t(Xn, 0, wave * 16, X2, 0, X2, wave * 16, 0, 16, lane);
-      // ---- publish (i, i + 1): every storing wave drains its write-through stores (the update above
-      // ran meanwhile), then one flag store
+      // ---- publish (i, i) and (i, i + 1): every storing wave drains its write-through stores (Ld and
+      // Dinv during the factor, U_i,i+1 block by block), then one flag store each
       if (kTrace) ct[11] = (int64_t)__builtin_amdgcn_s_memrealtime();
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       lds_sync();
-      if (tid == 0)
+      if (tid == 0) {
+        __hip_atomic_store(flags + (int64_t)i * nbc + i, kFinal, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(flags + (int64_t)i * nbc + i + 1, kFinal, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
       if (kTrace) ct[12] = (int64_t)__builtin_amdgcn_s_memrealtime();
       if (i + 1 == nb) store_lower(X2, i0, j0);  // no next step to store it beside
       __builtin_amdgcn_s_setprio(0);
@@ -592,45 +732,49 @@ chol_flow_kernel(double* __restrict__ G, int64_t ld, int nbc, double* __restrict
         // ---- U_ij = U_ii⁻ᵀ A_ij once U_ii is final. Operands of U_ii and its 16x16 inverses come
         // straight from the sc1-stored Ld / Dinv into registers; X (LDS) is solved in place:
         //   X_rb <- (D_rb⁻¹)ᵀ (X_rb − U[0:o, rb]ᵀ X[0:o]),  rb = 0..3, wave w on columns 16w..16w+15
-        const int32_t* fd = flags + (int64_t)i * nbc + i;
-        wave_wait2(fd, fd, info, lane);
-        if (kTrace) tr[3] = (int64_t)__builtin_amdgcn_s_memrealtime();
-        double u[24], di[16];
-        {
-          int c = 0;
-#pragma unroll
-          for (int rb = 1; rb < 4; rb++)
-#pragma unroll
-            for (int ks = 0; ks < 4 * rb; ks++)
-              u[c++] = ld1(rLd, (uint32_t)(((i0 + ks * 4 + fr) * CNB + rb * 16 + fc) * 8));
-#pragma unroll
-          for (int rb = 0; rb < 4; rb++)
-#pragma unroll
-            for (int ks = 0; ks < 4; ks++)
-              di[rb * 4 + ks] = ld1(rDi, (uint32_t)(((i0 / 16) * 256 + rb * 256 + (ks * 4 + fr) * 16 + fc) * 8));
-        }
+        // block row rb needs Dinv_rb (leaf rb of U_ii) and U[0:16 rb, rb] (leaves < rb): the chain
+        // sets one bit per stored leaf, so the solve runs leaf by leaf beside the factor and only the
+        // last block row is left once U_ii is final
+        const int32_t* fl = flags + (int64_t)(i + 1) * nbc + i;
+        const __amdgpu_buffer_rsrc_t rU = rsrc(G + i0 * ld, gbytes_rowblk);
+        double u[24], di[4];
         const int cw = wave * 16;
         int c = 0;
 #pragma unroll
         for (int rb = 0; rb < 4; rb++) {
           const int o = rb * 16;
+          wave_wait_bits(fl, (2 << rb) - 1, info, lane);
+          if (kTrace && rb == 3) tr[3] = (int64_t)__builtin_amdgcn_s_memrealtime();
+#pragma unroll
+          for (int ks = 0; ks < 4; ks++)
+            di[ks] = ld1(rDi, (uint32_t)(((i0 / 16) * 256 + rb * 256 + (ks * 4 + fr) * 16 + fc) * 8));
+          if (rb + 1 < 4) {  // the next block row's U operands (rows of leaves <= rb)
+#pragma unroll
+            for (int ks = 0; ks < 4 * (rb + 1); ks++)
+              u[c + 4 * rb + ks] = ld1(rLd, (uint32_t)(((i0 + ks * 4 + fr) * CNB + (rb + 1) * 16 + fc) * 8));
+          }
           if (rb > 0) {
             d4 sacc = (d4){0.0, 0.0, 0.0, 0.0};
 #pragma unroll
             for (int ks = 0; ks < 4 * rb; ks++)
-              sacc = __builtin_amdgcn_mfma_f64_16x16x4f64(u[c++], X[(ks * 4 + fr) * PS + cw + fc], sacc, 0, 0, 0);
+              sacc = __builtin_amdgcn_mfma_f64_16x16x4f64(u[c + ks], X[(ks * 4 + fr) * PS + cw + fc], sacc, 0, 0, 0);
+            c += 4 * rb;
 #pragma unroll
             for (int r = 0; r < 4; r++) X[(o + fr + 4 * r) * PS + cw + fc] -= sacc[r];
           }
           d4 sacc = (d4){0.0, 0.0, 0.0, 0.0};
 #pragma unroll
           for (int ks = 0; ks < 4; ks++)
-            sacc = __builtin_amdgcn_mfma_f64_16x16x4f64(di[rb * 4 + ks], X[(o + ks * 4 + fr) * PS + cw + fc], sacc, 0, 0, 0);
+            sacc = __builtin_amdgcn_mfma_f64_16x16x4f64(di[ks], X[(o + ks * 4 + fr) * PS + cw + fc], sacc, 0, 0, 0);
 #pragma unroll
-          for (int r = 0; r < 4; r++) X[(o + fr + 4 * r) * PS + cw + fc] = sacc[r];
+          for (int r = 0; r < 4; r++) {
+            X[(o + fr + 4 * r) * PS + cw + fc] = sacc[r];
+            // each final 16x16 block goes out at once (write-through): the drain before the flag then
+            // waits for the last block row only
+            st1(rU, (uint32_t)(((int64_t)(o + fr + 4 * r) * ld + j0 + cw + fc) * 8), sacc[r]);
+          }
         }
         __syncthreads();
-        store_upper(X, i0, j0);
         low = X;
       } else {
         // ---- the Schur block −WᵀW (read by later kernels only)

@@ -47,14 +47,16 @@ step = np.diff(ct[:, 0])
 print("chain step (start -> next start)        ", f(us(step)))
 print("  factor (start -> factored)             ", f(us(ct[:, 8] - ct[:, 0])))
 prev = ct[:, 0]
-for kb in range(4):
-    print(f"    leaf {kb} steps                       ", f(us(ct[:, 1 + kb] - prev)))
-    if kb < 3:
-        print(f"    leaf {kb} update + barriers           ", f(us(ct[:, 5 + kb] - ct[:, 1 + kb])))
-        prev = ct[:, 5 + kb]
-print("    leaf 1: X/Dinv writes issued        ", f(us(ct[:, 13] - ct[:, 2])))
-print("    leaf 1: first barrier               ", f(us(ct[:, 14] - ct[:, 13])))
-print("    leaf 1: first-row update + barrier  ", f(us(ct[:, 6] - ct[:, 14])))
+for kb in range(4):  # wave kb owns leaf kb; the next leaf's owner goes on as soon as it ends
+    print(f"    leaf {kb} (start / previous leaf end -> end)", f(us(ct[:, 1 + kb] - prev)))
+    own0 = ct[:, 13] if kb == 0 else ct[:, 4 + kb]
+    print(f"      leaf {kb}: hand-over (-> own start)   ", f(us(own0 - prev)))
+    print(f"      leaf {kb}: own 16 steps               ", f(us(ct[:, 1 + kb] - own0)))
+    prev = ct[:, 1 + kb]
+print("    last leaf end -> factored (sync)     ", f(us(ct[:, 8] - ct[:, 4])))
+print("    X2 (neighbour partial) in LDS, from start", f(us(ct[:, 9] - ct[:, 0])))
+print("    Xn (next diag partial) in LDS, from start", f(us(ct[:, 14] - ct[:, 0])))
+print("    helper block rows done, from start   ", f(us(ct[:, 15] - ct[:, 0])))
 print("  neighbour solve + Ld stores            ", f(us(ct[:, 10] - ct[:, 8])))
 print("  next tile update (k = i)               ", f(us(ct[:, 11] - ct[:, 10])))
 print("  drain + flags                          ", f(us(ct[:, 12] - ct[:, 11])))
@@ -66,6 +68,6 @@ dgp = np.array([rec[(i, i)][8] for i in range(1, nb)])
 print("neighbour partial published before factored", f(us(ct[:, 8] - nbp)))
 print("diag partial published before needed     ", f(us(ct[:-1, 8] - dgp)))
 O = np.array([r for r in W if int(r[1]) > int(r[0]) + 1 and int(r[0]) < nb and r[8] > 0])
-print("other tiles: diag seen -> published      ", f(us(O[:, 8] - O[:, 6])))
+print("other tiles: last leaf seen -> published  ", f(us(O[:, 8] - O[:, 6])))
 busy = (W[:, 8] - W[:, 3]).clip(0).sum() / 100
 print(f"worker task-time sum {busy:.0f} us over {span:.0f} us span")
