@@ -133,8 +133,6 @@ struct ChainSync {
   int pro;     // 3 per step: waves 1-3 have finished reading X2 for that last update
   int x2;      // step + 1 once X2 holds the right neighbour's partial A_i,i+1
   int dl;      // 4 * step + leaves whose inverse is in Dl
-  int nrow;    // 16 * step + finished 16x16 blocks of the neighbour solve
-  int item;    // the next of this step's 12 block-row-0..2 blocks to take (reset at the step's end)
   int64_t tt[4];  // trace: leaf ends
   int64_t ts[4];  // trace: own-leaf starts (after following the earlier leaves)
   int64_t th[4];  // trace: X2 fetched, Xn fetched, helper waves 0 and 1 done
@@ -212,6 +210,8 @@ __device__ __forceinline__ void follow_leaves(double* X, const double* X2, bool 
     for (int b = 0; b < NB; b++) acc[b] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, r[16 * (W + b) + fc], acc[b], 0, 0, 0);
   }
   // the accumulated update, transposed to the leaf layout (lane = column) through the rows' place in X
+  // (the previous leaf's last four rows applied one by one as rank-1 updates in the leaf layout
+  // instead measured slower: hand-over 0.65 -> 0.9-1.4 µs)
 #pragma unroll
   for (int b = 0; b < NB; b++)
 #pragma unroll
@@ -466,7 +466,7 @@ chol_flow_kernel(double* __restrict__ G, int64_t ld, int nbc, double* __restrict
   if (blockIdx.x == 0) {
     // ================================ the chain ================================
     if (tid == 0) {
-      sy.rows = sy.b13 = sy.pro = sy.x2 = sy.dl = sy.nrow = sy.item = 0;
+      sy.rows = sy.b13 = sy.pro = sy.x2 = sy.dl = 0;
     }
     // A_00 has no update: straight from G (written before this launch)
     for (int e = tid; e < FT * FT / 2; e += 256) {
@@ -479,8 +479,9 @@ chol_flow_kernel(double* __restrict__ G, int64_t ld, int nbc, double* __restrict
     for (int i = 0; i < nb; i++) {
       const int64_t i0 = (int64_t)i * FT, j0 = i0 + FT;
       const bool next_diag = i + 1 < nb;
-      // trace: 0 start, 1-4 leaf ends, 5-7 leaf update ends, 8 factored, 9 neighbour partial seen,
-      // 10 neighbour solved, 11 next tile updated, 12 published
+      // trace: 0 start, 1-4 leaf ends, 5-7 own starts of leaves 1-3, 8 factored, 9 X2 fetched,
+      // 10 neighbour solved and published, 11 next tile updated, 12 step end, 13 own start of leaf 0,
+      // 14 Xn fetched, 15 helpers done
       int64_t ct[16] = {};
       if (kTrace) ct[0] = (int64_t)__builtin_amdgcn_s_memrealtime();
       __builtin_amdgcn_s_setprio(2);
@@ -518,8 +519,8 @@ chol_flow_kernel(double* __restrict__ G, int64_t ld, int nbc, double* __restrict
       //   only by later kernels), then the neighbour's partial A_i,i+1 -> X2 (once waves 1-3 have read
       //   X2 for this step's last update);
       //   wave 1: the next diagonal tile's partial A_i+1,i+1 -> Xn (needed at the step's end);
-      //   waves 0-2: the neighbour solve's block rows 0-2 (12 16x16 blocks, taken in order from an LDS
-      //   counter; block row rb once leaf rb is factored and every block of row rb − 1 is done).
+      //   waves 0-2: the neighbour solve's block rows 0-2, column block by column block (block row rb
+      //   once leaf rb is factored).
       auto after_own = [&](int w) {
         if (w == 0) {
           if (i > 0) {
@@ -545,19 +546,14 @@ chol_flow_kernel(double* __restrict__ G, int64_t ld, int nbc, double* __restrict
           if (kTrace && lane == 0) sy.th[1] = (int64_t)__builtin_amdgcn_s_memrealtime();
         }
         if (w <= 2) {
+          // column blocks: wave 0 takes 0 and 3, waves 1 and 2 their own; a column's block rows run in
+          // order on one wave, so only the leaf (sy.dl) and X2 (sy.x2) are waited for
 #pragma unroll 1
-          for (;;) {
-            // every lane adds 1 (one ds_add_rtn of 64 per wave; no lane-0-only branch around the
-            // returned value): block index = the wave's first old value / 64
-            const int it =
-                __builtin_amdgcn_readfirstlane(__hip_atomic_fetch_add(&sy.item, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) >> 6;
-            if (it >= 12) break;
-            const int rb = it >> 2, cb = it & 3;
+          for (int rb = 0; rb < 3; rb++) {
             lds_wait(&sy.x2, i + 1, info, lane);
             lds_wait(&sy.dl, 4 * i + rb + 1, info, lane);
-            lds_wait(&sy.nrow, 16 * i + 4 * rb, info, lane);
-            nbr_item(rb, cb);
-            if (lane == 0) __hip_atomic_fetch_add(&sy.nrow, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            nbr_item(rb, w);
+            if (w == 0) nbr_item(rb, 3);
           }
           if (kTrace && lane == 0) sy.th[2 + (w & 1)] = (int64_t)__builtin_amdgcn_s_memrealtime();
         }
@@ -580,8 +576,6 @@ chol_flow_kernel(double* __restrict__ G, int64_t ld, int nbc, double* __restrict
       // ---- the neighbour's last block row (wave w: column block w); its earlier rows were solved
       // beside the factor
       nbr_item(3, wave);
-      if (lane == 0) __hip_atomic_fetch_add(&sy.nrow, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      if (tid == 0) sy.item = 0;  // the next step's helpers start after its leaf 0, long after this barrier
       lds_sync();
       if (kTrace) ct[10] = (int64_t)__builtin_amdgcn_s_memrealtime();
       // ---- the next diagonal tile's last update, k = i, from LDS: on the chain only its first 16
