@@ -129,7 +129,8 @@ __device__ __forceinline__ bool wave_ready2(const int32_t* fa, const int32_t* fb
 // nothing is reset between steps)
 struct ChainSync {
   int rows;    // 64 * step + the rows of U_ii final in X
-  int b13;     // step + 1 once block (1, 3) of the previous step's last update is in X
+  int b12;     // step + 1 once block (1, 2) of the previous step's last update is in X (wave 2)
+  int b13;     // step + 1 once block (1, 3) of the previous step's last update is in X (wave 3)
   int pro;     // 3 per step: waves 1-3 have finished reading X2 for that last update
   int x2;      // step + 1 once X2 holds the right neighbour's partial A_i,i+1
   int dl;      // 4 * step + leaves whose inverse is in Dl
@@ -162,9 +163,9 @@ __device__ __forceinline__ int lds_wait(int* p, int v, int32_t* info, int lane) 
 // Wave W (1..3) of the chain before its own leaf: the update of its rows 16W..16W+15 (column blocks
 // W..3) by every earlier row of U_ii, accumulated by MFMA in registers four rows at a time as the
 // owners publish them (sy->rows), then subtracted from the rows (x, lane = column 16W + lane) once. With prev, the accumulators start
-// with the previous step's last update (k = i − 1, from U_i−1,i in X2) of the same blocks; block
-// (1, 3) of it is wave 3's (applied to X, then sy->b13), so that wave 1, whose rows are needed
-// first, has two blocks of it instead of three. Four rows per MFMA group: five LDS reads per group
+// with the previous step's last update (k = i − 1, from U_i−1,i in X2) of the same blocks; blocks
+// (1, 2) and (1, 3) of it are waves 2 and 3's (applied to X first, then sy->b12 / b13), so that
+// wave 1, whose rows are needed first, has one block of it instead of three. Four rows per MFMA group: five LDS reads per group
 // instead of a broadcast read per row and element (the LDS pipe is shared with the owner).
 template <int W>
 __device__ __forceinline__ void follow_leaves(double* X, const double* X2, bool prev, ChainSync* sy, int step,
@@ -176,27 +177,35 @@ __device__ __forceinline__ void follow_leaves(double* X, const double* X2, bool 
 #pragma unroll
   for (int b = 0; b < NB; b++) acc[b] = (d4){0.0, 0.0, 0.0, 0.0};
   if (prev) {
-    d4 t13 = (d4){0.0, 0.0, 0.0, 0.0};
+    if (W >= 2) {
+      // first, block (1, W) of wave 1's rows (wave 1, whose leaf comes first, keeps only (1, 1))
+      d4 t1 = (d4){0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int ks = 0; ks < 16; ks++) {
+        const double* r = X2 + (ks * 4 + fr) * PS;
+        t1 = __builtin_amdgcn_mfma_f64_16x16x4f64(r[16 + fc], r[16 * W + fc], t1, 0, 0, 0);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; r++) X[(16 + fr + 4 * r) * PS + 16 * W + fc] -= t1[r];
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      lds_post(W == 2 ? &sy->b12 : &sy->b13, step + 1, lane);
+    }
 #pragma unroll
     for (int ks = 0; ks < 16; ks++) {
       const double* r = X2 + (ks * 4 + fr) * PS;
       const double a = r[16 * W + fc];
 #pragma unroll
       for (int b = 0; b < NB; b++)
-        if (!(W == 1 && b == 2)) acc[b] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, r[16 * (W + b) + fc], acc[b], 0, 0, 0);
-      if (W == 3) t13 = __builtin_amdgcn_mfma_f64_16x16x4f64(r[16 + fc], r[48 + fc], t13, 0, 0, 0);
-    }
-    if (W == 3) {
-#pragma unroll
-      for (int r = 0; r < 4; r++) X[(16 + fr + 4 * r) * PS + 48 + fc] -= t13[r];
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      lds_post(&sy->b13, step + 1, lane);
+        if (!(W == 1 && b >= 1)) acc[b] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, r[16 * (W + b) + fc], acc[b], 0, 0, 0);
     }
   }
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // X2 read
   if (lane == 0) __hip_atomic_fetch_add(&sy->pro, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-  // the rows' current values (wave 1: with wave 3's block (1, 3) of the last update applied)
-  if (W == 1 && prev) lds_wait(&sy->b13, step + 1, info, lane);
+  // the rows' current values (wave 1: with waves 2 and 3's blocks (1, 2) and (1, 3) of the last update)
+  if (W == 1 && prev) {
+    lds_wait(&sy->b12, step + 1, info, lane);
+    lds_wait(&sy->b13, step + 1, info, lane);
+  }
   const int cc = 16 * W + (lane < 64 - 16 * W ? lane : 0);
 #pragma unroll
   for (int t = 0; t < 16; t++) x[t] = X[(16 * W + t) * PS + cc];
@@ -466,7 +475,7 @@ chol_flow_kernel(double* __restrict__ G, int64_t ld, int nbc, double* __restrict
   if (blockIdx.x == 0) {
     // ================================ the chain ================================
     if (tid == 0) {
-      sy.rows = sy.b13 = sy.pro = sy.x2 = sy.dl = 0;
+      sy.rows = sy.b12 = sy.b13 = sy.pro = sy.x2 = sy.dl = 0;
     }
     // A_00 has no update: straight from G (written before this launch)
     for (int e = tid; e < FT * FT / 2; e += 256) {
