@@ -63,6 +63,17 @@ __device__ __forceinline__ void st1(__amdgpu_buffer_rsrc_t r, uint32_t voff, dou
   __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2, v), r, (int)voff, 0, kSc1);
 }
 
+// chain tuning (compile time; tools/build_flow_variants.sh builds timing variants): the leaf owner
+// publishes its row count every GBM_FLOW_POST_EVERY steps — the followers consume four rows at a
+// time, and a post per step (an exec-masked LDS store on the pivot chain) made each 16-pivot leaf
+// 1.93 instead of 1.58 µs; LDS polls sleep GBM_FLOW_POLL_SLEEP x 64 cycles between reads
+#ifndef GBM_FLOW_POST_EVERY
+#define GBM_FLOW_POST_EVERY 4
+#endif
+#ifndef GBM_FLOW_POLL_SLEEP
+#define GBM_FLOW_POLL_SLEEP 4
+#endif
+
 // a workgroup barrier for LDS data only (__syncthreads also waits for every outstanding global load
 // and store of the calling wave: the write-through stores of a hand-off would sit on the chain)
 __device__ __forceinline__ void lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
@@ -149,7 +160,7 @@ __device__ __forceinline__ void lds_post(int* p, int v, int lane) {
 __device__ __forceinline__ int lds_wait(int* p, int v, int32_t* info, int lane) {
   int s = lds_poll(p);
   for (int it = 0; s < v; it++) {
-    __builtin_amdgcn_s_sleep(1);  // ~64 cycles: the spin shares the LDS pipe with the leaf owner
+    __builtin_amdgcn_s_sleep(GBM_FLOW_POLL_SLEEP);  // the spin shares the LDS pipe with the leaf owner
     s = lds_poll(p);
     if (it > (1 << 22)) {
       if (lane == 0) atomicCAS(info, 0, -1);
@@ -332,7 +343,7 @@ __device__ __forceinline__ int factor_block_pipe(double* X, const double* X2, bo
     // row c − 1 (written last step) is in X: publish it to the followers, read U[c − 1][·] -> b1;
     // this step's final row -> X
     __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
-    if (c >= 1) lds_post(&sy->rows, base + o + c, lane);
+    if (c >= 1 && c % GBM_FLOW_POST_EVERY == 0) lds_post(&sy->rows, base + o + c, lane);
     X[(o + c) * PS + cw] = lc;
     if (c >= 1 && c + 2 < 16) {
 #pragma unroll
