@@ -11,6 +11,14 @@ all-reduce over xGMI.
 A step = standardise → fp64-MFMA GRM → (all-reduce) → Cholesky GBLUP solve → marker effects →
 results (b, GEBVs, μ̂) copied to pinned host memory.
 
+`--stream-chunk C` runs the loci-streamed mode instead (config C3 on one GPU: `--individuals 50000
+--loci 600000 --stream-chunk 75000`): the genotypes resident as int8 dosages (1 B per cell), each
+chunk of C loci standardised and added into G in place, the marker effects from the bytes.
+
+Parity (rank 0, N = 1, when the oracle can run the same problem): the numpy restatement fits the
+SAME genotypes and phenotypes the GPU step fitted; the line carries rel_err of y_pred, μ̂, b_hat and
+q equality.
+
 Prints ONE JSON line on rank 0.
 """
 from __future__ import annotations
@@ -47,7 +55,27 @@ def parse():
     ap.add_argument("--cpu-sample-p", type=int, default=0, help="loci in the CPU baseline sample (0 = all)")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL); gloo only to rehearse N ranks on one GPU")
     ap.add_argument("--same-device", action="store_true", help="all ranks on cuda:0 (rehearsal on a 1-GPU box)")
+    ap.add_argument("--stream-chunk", type=int, default=0,
+                    help="loci per chunk of the loci-streamed mode (int8 dosages resident); 0 = resident fp64 X")
     return ap.parse_args()
+
+
+# BASELINE.json configs this bench can run (n, loci in total); the line names the one it ran
+CONFIGS = {(5000, 50000): "C2 GBLUP 5 000 x 50 000 (BASELINE.json configs[1])",
+           (50000, 600000): "C3 GBLUP 50 000 x 600 000 (BASELINE.json configs[2])",
+           (50000, 75000): "C3's per-GPU shard 50 000 x 75 000 (1/8 of BASELINE.json configs[2])"}
+
+
+def workload_label(n, p_local, world, stream_chunk):
+    """config.workload from (n, p, N): weak scaling keeps p_local loci per GPU, so the per-GPU shape
+    names the config (C2: 5 000 x 50 000 per GPU), and a one-GPU run over all loci of C3 names C3."""
+    p_total = p_local * world
+    name = CONFIGS.get((n, p_local)) if world > 1 else CONFIGS.get((n, p_total))
+    name = name or f"custom GBLUP n={n} x p={p_total} (no BASELINE.json config)"
+    mode = (f"loci-streamed ({stream_chunk}-locus fp64 chunks, int8 dosages resident)" if stream_chunk
+            else "fp64 X resident")
+    return (f"{name}: n={n} x p={p_local} loci per GPU, p_total={p_total} over {world} GPU(s), {mode}"
+            + (", loci-sharded, partial GRMs all-reduced" if world > 1 else ""))
 
 
 def _blas_threads():
@@ -72,12 +100,16 @@ def _oracle_c():
     return lib
 
 
-def cpu_baseline(args):
+def cpu_baseline(args, Y, gpu):
     """The CPU restatements of the hot path on the same workload (rank 0, N = 1), each one full
     GBLUP fit (standardise + GRM + Cholesky + solves + marker effects) on n x p_sample with the
     genotypes generated beforehand (untimed): the numpy/OpenBLAS restatement (oracle/oracle.py,
     the headline `value`) and the plain C/OpenMP restatement (oracle/gbm_oracle.c). Both are this
-    build's ports of the reference's equations (the Julia reference cannot run here: SURVEY §0.7)."""
+    build's ports of the reference's equations (the Julia reference cannot run here: SURVEY §0.7).
+
+    The fit uses the phenotypes Y of the GPU step, so with the full sample (p_sample = p) it is the
+    same problem the GPU solved: returns (baseline, parity) with parity = rel_err of y_pred, μ̂,
+    b_hat against the GPU step's results and q equality."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
 
@@ -90,7 +122,7 @@ def cpu_baseline(args):
         lib.gbm_ref_synth_matrix(args.seed, n, p, 0, X.ctypes.data, n)
     else:
         X = O.synth_genotypes(args.seed, n, p)
-    Y = np.asfortranarray(O.synth_phenotypes(X, args.seed + 1, args.nrhs))
+    Y = np.asfortranarray(Y)
     t0 = time.perf_counter()
     ref = O.gblup_fit(X, Y, args.lam)
     dt = time.perf_counter() - t0
@@ -98,6 +130,17 @@ def cpu_baseline(args):
            "sample": f"numpy/OpenBLAS fp64 restatement (oracle/oracle.py gblup_fit) on n={n} x p={p}, "
                      f"{args.nrhs} trait(s), one full fit in {dt:.2f} s (standardise + GRM + Cholesky + solves + "
                      f"marker effects; generation untimed)"}
+    if p == args.loci:
+        def rel(a, b):
+            return float(np.abs(np.asarray(a) - np.asarray(b)).max() / max(np.abs(np.asarray(b)).max(), 1e-300))
+        parity = {"oracle": "oracle/oracle.py gblup_fit (numpy/LAPACK fp64) on the same X and Y as the GPU step",
+                  "n": n, "p": p, "q_equal": int(ref["q"]) == int(gpu["q"]),
+                  "rel_err_y_pred": rel(gpu["y_pred"], ref["y_pred"]), "rel_err_mu": rel(gpu["mu"], ref["mu"]),
+                  "rel_err_b_hat": rel(gpu["b_hat"], ref["b_hat"]), "tolerance_y_pred": 1e-9}
+        parity["pass"] = bool(parity["q_equal"] and parity["rel_err_y_pred"] < 1e-9 and parity["rel_err_mu"] < 1e-9
+                              and parity["rel_err_b_hat"] < 1e-6)
+    else:
+        parity = {"skipped": f"CPU sample p={p} differs from the GPU step's p={args.loci}"}
     if lib is not None:
         t = args.nrhs
         b = np.zeros((p + 1, t), order="F")
@@ -114,16 +157,17 @@ def cpu_baseline(args):
                            "sample": f"plain C/OpenMP restatement (oracle/gbm_oracle.c gbm_ref_gblup_fit, gcc -O3 "
                                      f"-fopenmp) on the same n={n} x p={p} fit: {dtc:.2f} s; GEBVs equal the numpy "
                                      f"fit's to 1e-8"}
-    return out
+    return out, parity
 
 
 def cpu_baseline_c3(args):
     """CPU time of config C3 (GBLUP n = 50 000 x p = 600 000), extrapolated: the full problem (240 GB
     of fp64 X, 1.5e15 GRM flops) cannot run on the host in a bench. The numpy/OpenBLAS restatement's
     per-fit costs are timed on samples and combined: standardise + GRM + marker effects at
-    n = 50 000 on p = 1 000 and 2 000 loci (linear in p: slope = cost per locus, intercept = the
+    n = 50 000 on p = 10 000 and 20 000 loci (linear in p: slope = cost per locus, intercept = the
     n x n output), and the Cholesky + solves at n = 16 000 scaled by (50 000/16 000)^3. BASELINE.md
-    planned p = 60 000 and 120 000; those samples take ~10 min of CPU each, beyond a bench run."""
+    planned p = 60 000 and 120 000; those samples take ~10 min of CPU each, beyond a bench run, so
+    the line uses the largest samples that keep this leg near half a minute."""
     import scipy.linalg as sla
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
@@ -153,12 +197,13 @@ def cpu_baseline_c3(args):
         return dt
 
     samples = {}
-    for p in (1000, 2000):
+    pa, pb = 10000, 20000
+    for p in (pa, pb):
         X = gen(n, p)
         samples[p] = grm_effects(X)
         del X
-    slope = (samples[2000] - samples[1000]) / 1000.0
-    icpt = samples[1000] - 1000.0 * slope
+    slope = (samples[pb] - samples[pa]) / float(pb - pa)
+    icpt = samples[pa] - pa * slope
     nc = 16000
     rng = np.random.default_rng(2)
     Xc = gen(nc, 2000)
@@ -178,8 +223,8 @@ def cpu_baseline_c3(args):
     return {"value": n * p3 / t_c3, "unit": "genotype-cells/s", "cores": int(_blas_threads()), "kind": "port",
             "extrapolated": True, "seconds_c3": t_c3,
             "sample": f"EXTRAPOLATION of the numpy/OpenBLAS restatement to C3 (n=50000 x p=600000): standardise + "
-                      f"GRM + marker effects timed at n=50000 on p=1000 ({samples[1000]:.2f} s) and p=2000 "
-                      f"({samples[2000]:.2f} s), linear in p -> {slope * p3 + icpt:.1f} s at p=600000; Cholesky + "
+                      f"GRM + marker effects timed at n=50000 on p={pa} ({samples[pa]:.2f} s) and p={pb} "
+                      f"({samples[pb]:.2f} s), linear in p -> {slope * p3 + icpt:.1f} s at p=600000; Cholesky + "
                       f"solves timed at n=16000 ({t_chol:.2f} s) x (50000/16000)^3 -> {t_chol_c3:.1f} s; "
                       f"total {t_c3:.1f} s on one host"}
 
@@ -253,16 +298,21 @@ def host_path(args, torch):
 
 
 def load_pmc(n, p):
-    """HBM traffic per GRM launch from the committed rocprofv3 PMC summary, if one matches."""
+    """HBM traffic per GRM launch from the committed rocprofv3 PMC summary, if one matches the shape.
+    Returns (bytes or None, stale): stale when the GRM kernel source has changed since the counters
+    were taken (the summary records the sha256 of csrc/grm.hip; tools/pmc_summary.py)."""
+    import hashlib
     path = os.path.join(ROOT, "profiles", "pmc_grm.json")
     try:
         with open(path) as f:
             d = json.load(f)
-        if d.get("n") == n and d.get("p") == p:
-            return d.get("hbm_bytes_per_launch")
     except (OSError, ValueError):
-        pass
-    return None
+        return None, None
+    if d.get("n") != n or d.get("p") != p:
+        return None, None
+    with open(os.path.join(ROOT, "genomicbreedingmodels.jl_amd", "csrc", "grm.hip"), "rb") as f:
+        sha = hashlib.sha256(f.read()).hexdigest()
+    return d.get("hbm_bytes_per_launch"), d.get("grm_hip_sha256") != sha
 
 
 def main():
@@ -286,15 +336,20 @@ def main():
 
     import gbm
     from gbm import synth
-    from gbm.sharded import HipShardStages, LocalComm, TorchComm, sharded_gblup_step
+    from gbm.sharded import (HipShardStages, HipStreamedShardStages, LocalComm, TorchComm, assemble_b_hat,
+                             sharded_gblup_step)
 
     comm = TorchComm() if world > 1 else LocalComm()
     n, p_local = args.individuals, args.loci
     p_total = p_local * world
     j0 = rank * p_local
-    st = HipShardStages(n, p_local, nrhs=args.nrhs, lambda_=args.lam, device=dev)
+    if args.stream_chunk:
+        st = HipStreamedShardStages(n, p_local, args.stream_chunk, nrhs=args.nrhs, lambda_=args.lam, device=dev)
+    else:
+        st = HipShardStages(n, p_local, nrhs=args.nrhs, lambda_=args.lam, device=dev)
     st.generate(args.seed, j0)
-    st.load_phenotypes(synth.qtl_phenotypes(args.seed, n, p_total, args.nrhs, device=dev))
+    Y = synth.qtl_phenotypes(args.seed, n, p_total, args.nrhs, device=dev)
+    st.load_phenotypes(Y)
     torch.cuda.synchronize()
 
     labels = ["begin", "standardize", "grm_syrk", "grm_reduce", "allreduce", "solve", "effects", "download"]
@@ -352,7 +407,7 @@ def main():
     chol_flops = float(n) ** 3 / 3.0
     solve_flops = 8.0 * float(n) ** 2 * args.nrhs + 2.0 * n * p_local * args.nrhs
     achieved = grm_flops / (syrk_ms / 1000.0) / 1e12
-    traffic = load_pmc(n, p_local)
+    traffic, traffic_stale = load_pmc(n, p_local) if not args.stream_chunk else (None, None)
     e2e_frac = (grm_flops + chol_flops + solve_flops) / (ms_per_step / 1000.0) / (PEAK_F64_TFLOPS * 1e12)
 
     rec = {
@@ -367,19 +422,21 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f64",
-        "data": "synthetic: counter-hash genotypes (MAF U(0.05,0.5), dosage Binomial(2,f), X=d/2) generated in HBM; "
-                "1% QTL phenotype, h2=0.5",
+        "data": "synthetic: counter-hash genotypes (MAF U(0.05,0.5), dosage Binomial(2,f), X=d/2) generated in HBM"
+                + (" as int8 dosages" if args.stream_chunk else " as fp64") + "; 1% QTL phenotype, h2=0.5",
         "config": {
-            "workload": f"C2 GBLUP n={n} x p={p_local} loci per GPU (BASELINE.json configs[1]); "
-                        f"p_total={p_total} over {world} GPU(s), loci-sharded, partial GRMs all-reduced",
+            "workload": workload_label(n, p_local, world, args.stream_chunk),
             "n": n, "p_per_gpu": p_local, "p_total": p_total, "traits": args.nrhs, "lambda": args.lam,
-            "grm_slices": int(st.lib.gbm_dev_grm_slices(n, p_local)),
+            "grm_slices": int(st.lib.gbm_dev_grm_slices(n, args.stream_chunk or p_local)),
+            "stream_chunk": args.stream_chunk or None,
             "parallelism": f"loci-shard x{world}",
         },
         "roofline": {
             "bound": "mfma",
             "kernel": "GRM stage: syrk_kernel<kPersist> (fp64 v_mfma_f64_16x16x4_f64 128x128 tiles) + "
-                      "grm_edge_kernel (ragged last column); achieved = all n(n+1)p flops / stage time",
+                      "grm_edge_kernel (ragged last column); achieved = all n(n+1)p flops / stage time"
+                      + ("; streamed: the stage also standardises each chunk from the int8 dosages"
+                         if args.stream_chunk else ""),
             "achieved": achieved,
             "peak": PEAK_F64_TFLOPS,
             "unit": "TFLOP/s",
@@ -390,21 +447,31 @@ def main():
             "traffic_source": "profiles/pmc_grm.json: rocprofv3 --pmc FETCH_SIZE (x2, gfx950 16 B/lane "
                               "under-count) + WRITE_SIZE per GRM launch, separate passes of this command"
                               if traffic is not None else None,
+            "traffic_stale": traffic_stale,
             "flops_per_launch": grm_flops,
             "ms_per_launch": syrk_ms,
         },
         "stage_ms": stage_ms,
         "e2e_fp64_frac_of_peak": e2e_frac,
     }
-    if world == 1 and not args.no_host_path:
+    if world == 1 and not args.no_host_path and not args.stream_chunk and float(n) * p_local <= 2e9:
         rec["host_path"] = host_path(args, torch)
         rec["stage_ms"]["h2d_x_pinned"] = rec["host_path"]["h2d_x_ms_pinned"]
-    if world == 1 and not args.no_cpu_baseline:
-        rec["cpu_baseline"] = cpu_baseline(args)
+    oracle_fits = float(n) * p_local <= 5e8 and args.cpu_sample_p in (0, p_local)  # ~seconds on the host
+    if world == 1 and not args.no_cpu_baseline and oracle_fits:
+        gpu = {"y_pred": out["y_pred"], "mu": out["mu"], "q": int(st.q.item()),
+               "b_hat": assemble_b_hat(out["mu"], out["msum"], [out["B"]], p_local)}
+        rec["cpu_baseline"], rec["parity"] = cpu_baseline(args, Y, gpu)
         if not args.no_cpu_c3:
             rec["cpu_baseline_c3_extrapolated"] = cpu_baseline_c3(args)
+    elif world == 1 and not args.no_cpu_baseline and (n, p_local) == (50000, 600000):
+        rec["cpu_baseline"] = cpu_baseline_c3(args)  # C3: the full fit cannot run on the host
+        rec["parity"] = {"skipped": "the oracle cannot fit 50 000 x 600 000 on the host; C3 is checked by "
+                                    "tests/test_gpu_large.py::test_c3_full_size_one_gpu_streamed (exact-solution "
+                                    "properties, C ABI vs stage path)"}
     else:
         rec["cpu_baseline"] = None
+        rec["parity"] = {"skipped": "multi-rank run, or --no-cpu-baseline, or a size the oracle cannot fit in seconds"}
     print(json.dumps(rec), flush=True)
     if world > 1:
         dist.destroy_process_group()

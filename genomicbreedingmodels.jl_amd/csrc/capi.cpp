@@ -42,6 +42,7 @@ struct FitCtx {
   std::vector<hipEvent_t> ev;    // one per upload chunk
   DevBuf Xt, D8, mean, sd, keep, q, G, Gc, wsg, Y, A, gebv, mu, info, wss, B, msum, packed, out, part;
   DevBuf tmp, strip, gathered;   // copy exchanges; the distributed factorisation's strip all-gather
+  DevBuf errs, q2;               // streamed fit: per-chunk carry error cells; scratch kept count
   ~FitCtx() {
     (void)hipSetDevice(dev);
     for (hipEvent_t e : ev) (void)hipEventDestroy(e);
@@ -117,6 +118,7 @@ struct Shard {
   std::unique_ptr<FitCtx> c;
   int64_t j0 = 0, p = 0;
   int64_t q_host = 0;
+  int64_t stream = 0;  // loci per chunk of the loci-streamed mode (plan_streaming); 0: resident
   int leader = -1;  // index of the shard that holds this device's summed GRM (itself if first)
   ~Shard() {
     if (c) pool().release(std::move(c));
@@ -332,6 +334,225 @@ int upload_grm_pipelined(const Problem& pr, Shard& sh, int64_t chunk) {
   GBM_HIP_TRY(hipMemcpyAsync(&sh.q_host, c.q.p, 8, hipMemcpyDeviceToHost, s));
   GBM_HIP_TRY(hipStreamSynchronize(s));
   return GBM_OK;
+}
+
+// ---- loci-streamed mode --------------------------------------------------------------------------
+// A shard whose fp64 locus rows do not fit its device next to G (config C3 on one GPU: 600 000 loci
+// x 50 048 individuals x 8 B = 240 GB beside a 20 GB G) is streamed. Its genotypes stay resident as
+// int8 dosages (synthetic and int8 sources: 1 B per cell, 30 GB at C3) or stay on the host (fp64
+// source), and the loci pass through one reusable fp64 chunk buffer: each chunk is standardised and
+// its GRM added into G in place (chunk GRMs summed in chunk order, as the pipelined host upload
+// does; same chunk partition => bit-identical G). After the solve the marker effects re-read the
+// dosages with z rebuilt in registers (bit-identical to the resident kernels), or re-upload the
+// fp64 chunks. Peak HBM: G + dosages + one or two chunk buffers.
+
+int ensure_copy_stream(FitCtx& c) {
+  if (!c.copy.s) {
+    c.copy.dev = c.dev;
+    GBM_HIP_TRY(hipStreamCreateWithFlags(&c.copy.s, hipStreamNonBlocking));
+  }
+  return GBM_OK;
+}
+
+int ensure_events(FitCtx& c, int64_t k) {
+  while ((int64_t)c.ev.size() < k) {
+    hipEvent_t e;
+    GBM_HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    c.ev.push_back(e);
+  }
+  return GBM_OK;
+}
+
+// The streamed shard's chunks: the pipelined upload's schedule rule (halving tail for copy-bound
+// fp64 at n <= 8192 or when GBM_HOST_CHUNK is set), so a streamed fit and a pipelined one over the
+// same chunk size sum the same chunk GRMs in the same order.
+std::vector<std::pair<int64_t, int64_t>> stream_schedule(const Problem& pr, const Shard& sh) {
+  return chunk_schedule(sh.p, sh.stream, (pr.src == Source::F64 && pr.n <= 8192) || getenv("GBM_HOST_CHUNK") != nullptr);
+}
+
+// Decide, per device, whether its shards' fp64 rows fit (resident, the default) or are streamed,
+// and the chunk size: GBM_STREAM_CHUNK (re-read per call) forces it (loci per chunk; 0 never
+// streams); otherwise a device streams when the resident buffers of its shards exceed its free
+// memory (plus what their pooled contexts already hold, minus a margin) even after its idle pooled
+// contexts are freed; the chunk is then the largest equal split of the shard whose buffers fit.
+int plan_streaming(const Problem& pr, std::vector<std::unique_ptr<Shard>>& shards, bool reml) {
+  const int64_t forced = env_i64("GBM_STREAM_CHUNK", -1);
+  const int64_t n = pr.n, npad = npad_of(n), gdim = gdim_of(n);
+  const bool bytes = pr.src != Source::F64;
+  if (forced >= 0) {
+    for (auto& sh : shards) sh->stream = (forced > 0 && forced < sh->p) ? forced : 0;
+    return GBM_OK;
+  }
+  std::map<int, std::vector<Shard*>> bydev;
+  for (auto& sh : shards) bydev[sh->x().dev].push_back(sh.get());
+  for (auto& dv : bydev) {
+    const int dev = dv.first;
+    std::vector<Shard*>& v = dv.second;
+    GBM_HIP_TRY(hipSetDevice(dev));
+    int64_t held = 0, fixed = 0, resident = 0, dosage = 0, pmax = 0;
+    for (Shard* sh : v) {
+      FitCtx& c = sh->x();
+      held += c.Xt.cap + c.D8.cap + c.G.cap + c.Gc.cap + c.wsg.cap;
+      fixed += gdim * gdim * 8 * (reml ? 2 : 1) + gbm_dev_solve_workspace(n, 63) + sh->p * 40;
+      resident += sh->p * npad * 8 + (pr.src == Source::I8 ? sh->p * n : 0) + gbm_dev_grm_workspace(n, sh->p);
+      dosage += bytes ? sh->p * n : 0;
+      pmax = std::max(pmax, sh->p);
+    }
+    size_t fr = 0, tot = 0;
+    GBM_HIP_TRY(hipMemGetInfo(&fr, &tot));
+    const int64_t margin = ((int64_t)1 << 30) + (int64_t)tot / 50;
+    if (resident + fixed + margin <= (int64_t)fr + held) continue;
+    pool().trim(dev);  // idle pooled contexts of this device hold memory the fit could use
+    GBM_HIP_TRY(hipMemGetInfo(&fr, &tot));
+    if (resident + fixed + margin <= (int64_t)fr + held) continue;
+    const int nbuf = bytes ? 1 : 2;
+    int64_t budget = (int64_t)fr + held - fixed - dosage - margin;
+    int64_t cmax = budget / ((int64_t)v.size() * nbuf * npad * 8);
+    if (cmax >= 16) budget -= (int64_t)v.size() * gbm_dev_grm_workspace(n, std::min(cmax, pmax));  // slabs at small n
+    cmax = budget / ((int64_t)v.size() * nbuf * npad * 8);
+    if (cmax < 512)
+      return fail(GBM_E_OOM, "device " + std::to_string(dev) + ": too little memory for a loci-streamed fit at n = " +
+                                 std::to_string(n) + " (need G " + std::to_string(gdim * gdim * 8) + " B plus chunk buffers)");
+    for (Shard* sh : v) {
+      const int64_t nch = (sh->p + cmax - 1) / cmax;
+      const int64_t chunk = round_up((sh->p + nch - 1) / nch, 16);
+      sh->stream = chunk < sh->p ? chunk : 0;
+    }
+  }
+  return GBM_OK;
+}
+
+// Upload (fp64: into its chunk buffer; int8: into the resident dosages) of chunk k on the copy
+// stream, recording ev[k]. An fp64 chunk reuses buffer k % 2 after the work that read chunk k − 2
+// (ev[nch + k % 2], recorded on the compute stream) is done.
+int stream_upload(const Problem& pr, Shard& sh, const std::vector<std::pair<int64_t, int64_t>>& sched, int64_t k) {
+  FitCtx& c = sh.x();
+  const int64_t n = pr.n, npad = npad_of(n), nch = (int64_t)sched.size();
+  const int64_t j = sched[k].first, pc = sched[k].second;
+  if (pr.src == Source::F64) {
+    if (k >= 2) GBM_HIP_TRY(hipStreamWaitEvent(c.copy.s, c.ev[nch + k % 2], 0));
+    double* Zb = (double*)c.Xt.p + (k % 2) * sh.stream * npad;
+    GBM_HIP_TRY(hipMemcpy2DAsync(Zb, npad * 8, pr.X + (sh.j0 + j) * pr.ld, pr.ld * 8, n * 8, pc, hipMemcpyHostToDevice,
+                                 c.copy.s));
+  } else if (pr.src == Source::I8) {
+    GBM_HIP_TRY(hipMemcpy2DAsync((int8_t*)c.D8.p + j * n, n, pr.D + (sh.j0 + j) * pr.ld, pr.ld, n, pc,
+                                 hipMemcpyHostToDevice, c.copy.s));
+  }
+  GBM_HIP_TRY(hipEventRecord(c.ev[k], c.copy.s));
+  return GBM_OK;
+}
+
+// Chunk k's standardised rows in its chunk buffer (mean/sd/keep at the chunk's loci, kept count into
+// q); returns the buffer.
+int stream_standardize(const Problem& pr, Shard& sh, const std::vector<std::pair<int64_t, int64_t>>& sched, int64_t k,
+                       int64_t* q, double** Zb_out) {
+  FitCtx& c = sh.x();
+  const int64_t n = pr.n, npad = npad_of(n);
+  const int64_t j = sched[k].first, pc = sched[k].second;
+  hipStream_t s = c.stream.s;
+  double* Zb = (double*)c.Xt.p + (pr.src == Source::F64 ? (k % 2) * sh.stream * npad : 0);
+  if (pr.src != Source::SYNTH) GBM_HIP_TRY(hipStreamWaitEvent(s, c.ev[k], 0));
+  if (pr.src == Source::F64) {
+    if (npad > n) GBM_HIP_TRY(hipMemset2DAsync(Zb + n, npad * 8, 0, (npad - n) * 8, pc, s));
+    GBM_TRY(gbm_dev_standardize(Zb, npad, pc, n, Zb, npad, (double*)c.mean.p + j, (double*)c.sd.p + j,
+                                (int32_t*)c.keep.p + j, q, s));
+  } else {
+    const int ploidy = pr.src == Source::SYNTH ? 2 : pr.ploidy;
+    GBM_TRY(launch_standardize_i8((const int8_t*)c.D8.p + j * n, n, pc, n, ploidy, Zb, npad, (double*)c.mean.p + j,
+                                  (double*)c.sd.p + j, (int32_t*)c.keep.p + j, q, s));
+  }
+  *Zb_out = Zb;
+  return GBM_OK;
+}
+
+// Standardise + GRM of a streamed shard: every chunk's GRM added into G (a chunk planned as a single
+// loci range goes through Gc), the copy of chunk k + 1 overlapping chunk k's GRM.
+int stream_grm_shard(const Problem& pr, Shard& sh) {
+  FitCtx& c = sh.x();
+  const int64_t n = pr.n, npad = npad_of(n), gdim = gdim_of(n), pl = sh.p;
+  GBM_HIP_TRY(hipSetDevice(c.dev));
+  hipStream_t s = c.stream.s;
+  const auto sched = stream_schedule(pr, sh);
+  const int64_t nch = (int64_t)sched.size();
+  const bool bytes = pr.src != Source::F64;
+  if (pr.src != Source::SYNTH) GBM_TRY(ensure_copy_stream(c));
+  GBM_TRY(ensure_events(c, nch + 2));
+  GBM_TRY(ensure(c.Xt, c.dev, (bytes ? 1 : 2) * sh.stream * npad * 8));
+  GBM_TRY(ensure(c.mean, c.dev, pl * 8));
+  GBM_TRY(ensure(c.sd, c.dev, pl * 8));
+  GBM_TRY(ensure(c.keep, c.dev, pl * 4));
+  GBM_TRY(ensure(c.q, c.dev, 8));
+  GBM_TRY(ensure(c.errs, c.dev, nch * 4));
+  GBM_TRY(ensure(c.G, c.dev, gdim * gdim * 8));
+  if (bytes) GBM_TRY(ensure(c.D8, c.dev, pl * n));
+  int64_t wsb = 0;
+  for (const auto& jc : sched) wsb = std::max(wsb, gbm_dev_grm_workspace(n, jc.second));
+  GBM_TRY(ensure(c.wsg, c.dev, wsb));
+  for (int64_t k = 1; k < nch; k++)
+    if (!grm_can_accumulate(n, sched[k].second)) {
+      GBM_TRY(ensure(c.Gc, c.dev, gdim * gdim * 8));
+      break;
+    }
+  GBM_HIP_TRY(hipMemsetAsync(c.q.p, 0, 8, s));
+  GBM_HIP_TRY(hipMemsetAsync(c.errs.p, 0, nch * 4, s));
+  if (pr.src == Source::SYNTH)
+    GBM_TRY(gbm_dev_synth_dosage_i8((int8_t*)c.D8.p, n, pl, n, pr.seed, sh.j0, s));
+  else
+    GBM_TRY(stream_upload(pr, sh, sched, 0));
+  for (int64_t k = 0; k < nch; k++) {
+    const int64_t pc = sched[k].second;
+    double* Zb = nullptr;
+    GBM_TRY(stream_standardize(pr, sh, sched, k, (int64_t*)c.q.p, &Zb));
+    int32_t* err = (int32_t*)c.errs.p + k;
+    if (k > 0 && grm_can_accumulate(n, pc)) {
+      GBM_TRY(launch_grm(Zb, npad, pc, n, (double*)c.G.p, gdim, c.wsg.p, wsb, s, 1, err));
+    } else {
+      GBM_TRY(launch_grm(Zb, npad, pc, n, k == 0 ? (double*)c.G.p : (double*)c.Gc.p, gdim, c.wsg.p, wsb, s, 0, err));
+      if (k > 0) GBM_TRY(launch_add_inplace((double*)c.G.p, (const double*)c.Gc.p, gdim * gdim, s));
+    }
+    if (pr.src == Source::F64) GBM_HIP_TRY(hipEventRecord(c.ev[nch + k % 2], s));
+    // queued behind chunk k's work (a pageable copy blocks this thread while the device computes)
+    if (pr.src != Source::SYNTH && k + 1 < nch) GBM_TRY(stream_upload(pr, sh, sched, k + 1));
+  }
+  std::vector<int32_t> errs(nch, 0);
+  GBM_HIP_TRY(hipMemcpyAsync(errs.data(), c.errs.p, nch * 4, hipMemcpyDeviceToHost, s));
+  GBM_HIP_TRY(hipMemcpyAsync(&sh.q_host, c.q.p, 8, hipMemcpyDeviceToHost, s));
+  GBM_HIP_TRY(hipStreamSynchronize(s));
+  for (int64_t k = 0; k < nch; k++)
+    if (errs[k] < 0)
+      return fail(GBM_E_HIP, "GRM in-order carry accumulation (streamed chunk " + std::to_string(k) +
+                                 "): an inter-workgroup wait timed out (G is invalid)");
+  return GBM_OK;
+}
+
+// Marker effects of a streamed shard into B (nt x p) and msum: from the resident dosages in one
+// pass (z rebuilt in registers), or chunk by chunk from re-uploaded fp64 rows (standardised again:
+// the same bits; kept count into a scratch cell).
+int stream_effects_shard(const Problem& pr, Shard& sh, int64_t nt, double inv_q) {
+  FitCtx& c = sh.x();
+  const int64_t n = pr.n, npad = npad_of(n), pl = sh.p;
+  hipStream_t s = c.stream.s;
+  if (pr.src != Source::F64) {
+    const int ploidy = pr.src == Source::SYNTH ? 2 : pr.ploidy;
+    GBM_TRY(launch_marker_rows_i8((const int8_t*)c.D8.p, n, pl, n, ploidy, (const double*)c.A.p, npad, nt, inv_q,
+                                  nullptr, (const double*)c.mean.p, (const double*)c.sd.p, (const int32_t*)c.keep.p,
+                                  (double*)c.B.p, pl, s));
+  } else {
+    const auto sched = stream_schedule(pr, sh);
+    const int64_t nch = (int64_t)sched.size();
+    GBM_TRY(ensure(c.q2, c.dev, 8));
+    GBM_TRY(stream_upload(pr, sh, sched, 0));
+    for (int64_t k = 0; k < nch; k++) {
+      const int64_t j = sched[k].first, pc = sched[k].second;
+      double* Zb = nullptr;
+      GBM_TRY(stream_standardize(pr, sh, sched, k, (int64_t*)c.q2.p, &Zb));
+      GBM_TRY(launch_marker_rows(Zb, npad, pc, n, (const double*)c.A.p, npad, nt, inv_q, nullptr,
+                                 (const double*)c.sd.p + j, (const int32_t*)c.keep.p + j, (double*)c.B.p + j, pl, s));
+      GBM_HIP_TRY(hipEventRecord(c.ev[nch + k % 2], s));
+      if (k + 1 < nch) GBM_TRY(stream_upload(pr, sh, sched, k + 1));
+    }
+  }
+  return launch_weighted_sum((const double*)c.mean.p, (const double*)c.B.p, pl, pl, nt, (double*)c.msum.p, s);
 }
 
 int grm_shard(const Problem& pr, Shard& sh) {
@@ -660,9 +881,12 @@ int solve_effects(const Problem& pr, std::vector<std::unique_ptr<Shard>>& shards
     hipStream_t s = c.stream.s;
     if (sh.leader != (int)k)
       GBM_HIP_TRY(hipMemcpyAsync(c.A.p, shards[sh.leader]->x().A.p, nt * npad * 8, hipMemcpyDeviceToDevice, s));
-    GBM_TRY(gbm_dev_marker_effects((const double*)c.Xt.p, npad, sh.p, n, (const double*)c.A.p, npad, nt, inv_q,
-                                   nullptr, (const double*)c.mean.p, (const double*)c.sd.p, (const int32_t*)c.keep.p,
-                                   (double*)c.B.p, sh.p, (double*)c.msum.p, s));
+    if (sh.stream)
+      GBM_TRY(stream_effects_shard(pr, sh, nt, inv_q));
+    else
+      GBM_TRY(gbm_dev_marker_effects((const double*)c.Xt.p, npad, sh.p, n, (const double*)c.A.p, npad, nt, inv_q,
+                                     nullptr, (const double*)c.mean.p, (const double*)c.sd.p, (const int32_t*)c.keep.p,
+                                     (double*)c.B.p, sh.p, (double*)c.msum.p, s));
     GBM_HIP_TRY(hipMemcpy2DAsync(bo + 1 + sh.j0, (p + 1) * 8, c.B.p, sh.p * 8, sh.p * 8, nt, hipMemcpyDeviceToHost, s));
     GBM_HIP_TRY(hipMemcpyAsync(msums[k].data(), c.msum.p, nt * 8, hipMemcpyDeviceToHost, s));
     if (k == 0) {
@@ -746,14 +970,17 @@ int run_fit(const Problem& pr, const double* Y, int64_t ldy, int64_t nrhs, doubl
   int64_t pmax = 0;
   for (auto& sh : shards) pmax = std::max(pmax, sh->p);
   const int64_t chunk = pr.src == Source::SYNTH ? 0 : host_chunk(pmax);
-  if (chunk > 0) {
-    RoctxRange r("gbm: pipelined upload + standardise + GRM");
-    GBM_TRY(parallel_shards(shards, [&](size_t, Shard& sh) { return upload_grm_pipelined(pr, sh, chunk); }));
-  } else {
+  GBM_TRY(plan_streaming(pr, shards, reml != nullptr));
+  {
     // each shard's GRM is launched behind its own standardisation (a shard without polymorphic
-    // loci contributes a zero partial; q == 0 over all shards fails below)
+    // loci contributes a zero partial; q == 0 over all shards fails below): streamed when its
+    // rows do not fit, else resident (host chunks pipelined with the GRM, or in one piece)
     RoctxRange r("gbm: upload + standardise + GRM");
-    GBM_TRY(parallel_shards(shards, [&](size_t, Shard& sh) { return prepare_grm_shard(pr, sh); }));
+    GBM_TRY(parallel_shards(shards, [&](size_t, Shard& sh) {
+      if (sh.stream) return stream_grm_shard(pr, sh);
+      if (chunk > 0) return upload_grm_pipelined(pr, sh, chunk);
+      return prepare_grm_shard(pr, sh);
+    }));
   }
   for (auto& sh : shards) q += sh->q_host;
   if (q_out) *q_out = q;

@@ -2,32 +2,56 @@
 //   B[t, j] = (z_j · a_t) / (q s_j)  — Fit.b_hat (pattern of reference src/linear.jl:218-221)
 //   msum[t] = Σ_j m_j B[t, j]        — b0 = μ̂ − msum makes `predict` exact
 //   out[t, i] = b0_t + Σ_j X[i, j] b_t[j]   — reference src/prediction.jl:228
+#include <type_traits>
+
 #include "gbm_internal.h"
 
 namespace gbm {
 
-// One wave per locus row; each lane reads 16-byte pairs along individuals; up to 4 traits per
-// pass over the row (the row stays in L1/L2 for later passes).
-__global__ void __launch_bounds__(256) marker_effects_kernel(const double* __restrict__ Zt, int64_t ldz, int64_t p,
+// The streamed fit's rows: int8 dosages, z = (d·xs − m)·r rebuilt exactly as the standardisation
+// computed it (x rounded on its own, r = 1/s), so B is bit-identical to the fp64-Z kernel's.
+__device__ __forceinline__ double dosage_z(int8_t d, double xs, double m, double r) {
+#pragma clang fp contract(off)
+  const double x = (double)d * xs;
+  return (x - m) * r;
+}
+
+// One wave per locus row; each lane reads 16-byte pairs along individuals (T = double: the
+// standardised row; T = int8_t: the dosage row, z rebuilt in registers); up to 4 traits per pass
+// over the row (the row stays in L1/L2 for later passes).
+template <typename T>
+__global__ void __launch_bounds__(256) marker_effects_kernel(const T* __restrict__ Zt, int64_t ldz, int64_t p,
                                                              int64_t n, const double* __restrict__ A, int64_t lda,
                                                              int64_t nrhs, double inv_q,
                                                              const int64_t* __restrict__ q_dev,
+                                                             const double* __restrict__ mean,
                                                              const double* __restrict__ sd,
                                                              const int32_t* __restrict__ keep,
-                                                             double* __restrict__ B, int64_t ldb) {
+                                                             double* __restrict__ B, int64_t ldb, double xs) {
   const int lane = threadIdx.x & 63;
   const int64_t wave_g = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   const int64_t nwaves = (int64_t)gridDim.x * 4;
   const int64_t n2 = (n + 1) & ~(int64_t)1;  // ldz is even and the padding is zero
   if (q_dev) inv_q = 1.0 / (double)(*q_dev);
   for (int64_t j = wave_g; j < p; j += nwaves) {
-    const double* z = Zt + j * ldz;
+    const T* z = Zt + j * ldz;
     const bool kp = keep[j] != 0;
+    double m = 0.0, r = 0.0;
+    if constexpr (std::is_same<T, int8_t>::value) {
+      m = mean[j];
+      r = kp ? 1.0 / sd[j] : 0.0;
+    }
     for (int64_t t0 = 0; t0 < nrhs; t0 += 4) {
       double acc[4] = {0.0, 0.0, 0.0, 0.0};
       if (kp) {
         for (int64_t i = (int64_t)lane * 2; i < n2; i += 128) {
-          const double2 zv = *reinterpret_cast<const double2*>(z + i);
+          double2 zv;
+          if constexpr (std::is_same<T, int8_t>::value) {
+            zv.x = dosage_z(z[i], xs, m, r);
+            zv.y = i + 1 < n ? dosage_z(z[i + 1], xs, m, r) : 0.0;
+          } else {
+            zv = *reinterpret_cast<const double2*>(z + i);
+          }
 #pragma unroll
           for (int u = 0; u < 4; u++)
             if (t0 + u < nrhs) {
@@ -113,6 +137,37 @@ int launch_predict(const double* Xt, int64_t ldx, int64_t p, int64_t n, const do
   return GBM_OK;
 }
 
+// B rows of p loci (rows of Zt: standardised fp64, ldz even) / msum = Σ_j mean_j B[t, j] (in a
+// separate launch, so a streamed fit computes B chunk by chunk and msum once over all its loci).
+int launch_marker_rows(const double* Zt, int64_t ldz, int64_t p, int64_t n, const double* A, int64_t lda, int64_t nrhs,
+                       double inv_q, const int64_t* q_dev, const double* sd, const int32_t* keep, double* B,
+                       int64_t ldb, hipStream_t s) {
+  if (p < 1) return GBM_OK;
+  const int64_t blocks = (p + 3) / 4 < 8192 ? (p + 3) / 4 : 8192;
+  marker_effects_kernel<double><<<(unsigned)blocks, 256, 0, s>>>(Zt, ldz, p, n, A, lda, nrhs, inv_q, q_dev, nullptr, sd,
+                                                                  keep, B, ldb, 1.0);
+  GBM_LAUNCH_CHECK();
+  return GBM_OK;
+}
+
+int launch_marker_rows_i8(const int8_t* D, int64_t ldd, int64_t p, int64_t n, int ploidy, const double* A, int64_t lda,
+                          int64_t nrhs, double inv_q, const int64_t* q_dev, const double* mean, const double* sd,
+                          const int32_t* keep, double* B, int64_t ldb, hipStream_t s) {
+  if (p < 1) return GBM_OK;
+  const int64_t blocks = (p + 3) / 4 < 8192 ? (p + 3) / 4 : 8192;
+  marker_effects_kernel<int8_t><<<(unsigned)blocks, 256, 0, s>>>(D, ldd, p, n, A, lda, nrhs, inv_q, q_dev, mean, sd,
+                                                                  keep, B, ldb, 1.0 / ploidy);
+  GBM_LAUNCH_CHECK();
+  return GBM_OK;
+}
+
+int launch_weighted_sum(const double* mean, const double* B, int64_t ldb, int64_t p, int64_t nrhs, double* msum,
+                        hipStream_t s) {
+  weighted_sum_kernel<<<(unsigned)nrhs, 1024, 0, s>>>(mean, B, ldb, p, msum);
+  GBM_LAUNCH_CHECK();
+  return GBM_OK;
+}
+
 int64_t predict_chunks(int64_t n, int64_t p) {
   const int64_t col_blocks = (n + 255) / 256;
   int64_t c = (2048 + col_blocks - 1) / col_blocks;
@@ -132,11 +187,18 @@ extern "C" int gbm_dev_marker_effects(const double* Zt, int64_t ldz, int64_t p, 
       lda < ldz || (lda & 1) || nrhs < 1 || ldb < p || !(q_dev || inv_q > 0.0))
     return fail(GBM_E_ARG, "gbm_dev_marker_effects: bad arguments (need ldz >= n even, lda >= ldz even, ldb >= p)");
   hipStream_t s = (hipStream_t)stream;
-  const int64_t blocks = (p + 3) / 4 < 8192 ? (p + 3) / 4 : 8192;
-  marker_effects_kernel<<<(unsigned)blocks, 256, 0, s>>>(Zt, ldz, p, n, A, lda, nrhs, inv_q, q_dev, sd, keep, B,
-                                                          ldb);
-  GBM_LAUNCH_CHECK();
-  weighted_sum_kernel<<<(unsigned)nrhs, 1024, 0, s>>>(mean, B, ldb, p, msum);
-  GBM_LAUNCH_CHECK();
-  return GBM_OK;
+  GBM_TRY(launch_marker_rows(Zt, ldz, p, n, A, lda, nrhs, inv_q, q_dev, sd, keep, B, ldb, s));
+  return launch_weighted_sum(mean, B, ldb, p, nrhs, msum, s);
+}
+
+extern "C" int gbm_dev_marker_effects_i8(const int8_t* D, int64_t ldd, int64_t p, int64_t n, int ploidy,
+                                         const double* A, int64_t lda, int64_t nrhs, double inv_q,
+                                         const int64_t* q_dev, const double* mean, const double* sd,
+                                         const int32_t* keep, double* B, int64_t ldb, double* msum, void* stream) {
+  if (!D || !A || !mean || !sd || !keep || !B || !msum || p < 1 || n < 1 || ldd < n || ploidy < 1 ||
+      lda < gbm::npad_of(n) || (lda & 1) || nrhs < 1 || ldb < p || !(q_dev || inv_q > 0.0))
+    return fail(GBM_E_ARG, "gbm_dev_marker_effects_i8: bad arguments (need ldd >= n, lda >= npad(n) even, ldb >= p)");
+  hipStream_t s = (hipStream_t)stream;
+  GBM_TRY(launch_marker_rows_i8(D, ldd, p, n, ploidy, A, lda, nrhs, inv_q, q_dev, mean, sd, keep, B, ldb, s));
+  return launch_weighted_sum(mean, B, ldb, p, nrhs, msum, s);
 }

@@ -39,9 +39,11 @@ int fail(int code, const std::string& msg);
   } while (0)
 
 // Stage launchers (device pointers, stream-ordered); defined in the .hip files.
-// accum = 1: G += the GRM of these loci (only where grm_can_accumulate(n, p))
+// accum = 1: G += the GRM of these loci (only where grm_can_accumulate(n, p)). err_out (device
+// int32, optional): the in-order carry's error cell is copied there (< 0: a wait timed out, G
+// invalid) instead of being read back with a stream sync.
 int launch_grm(const double* Zt, int64_t ldz, int64_t p, int64_t n, double* G, int64_t ldg,
-               void* ws, int64_t ws_bytes, hipStream_t s, int accum = 0);
+               void* ws, int64_t ws_bytes, hipStream_t s, int accum = 0, int32_t* err_out = nullptr);
 bool grm_can_accumulate(int64_t n, int64_t p);
 int64_t grm_workspace_bytes(int64_t n, int64_t p);
 int launch_grm_export(const double* G, int64_t ldg, int64_t n, double inv_q, double* out, int64_t ldo, hipStream_t s);
@@ -53,6 +55,16 @@ int launch_add_inplace(double* a, const double* b, int64_t n, hipStream_t s);
 // standardisation straight from int8 dosage rows (x = d / ploidy), out of place into Zt
 int launch_standardize_i8(const int8_t* D, int64_t ldd, int64_t p, int64_t n, int ploidy, double* Zt, int64_t ldz,
                           double* mean, double* sd, int32_t* keep, int64_t* q_dev, hipStream_t s);
+// marker effects in pieces (effects.hip): B rows of fp64 standardised rows or of int8 dosage rows
+// (z rebuilt bit-identically), and msum = Σ_j mean_j B[t, j] over p loci
+int launch_marker_rows(const double* Zt, int64_t ldz, int64_t p, int64_t n, const double* A, int64_t lda, int64_t nrhs,
+                       double inv_q, const int64_t* q_dev, const double* sd, const int32_t* keep, double* B,
+                       int64_t ldb, hipStream_t s);
+int launch_marker_rows_i8(const int8_t* D, int64_t ldd, int64_t p, int64_t n, int ploidy, const double* A, int64_t lda,
+                          int64_t nrhs, double inv_q, const int64_t* q_dev, const double* mean, const double* sd,
+                          const int32_t* keep, double* B, int64_t ldb, hipStream_t s);
+int launch_weighted_sum(const double* mean, const double* B, int64_t ldb, int64_t p, int64_t nrhs, double* msum,
+                        hipStream_t s);
 int launch_center_columns(const double* Xt, int64_t ldx, int64_t p, int64_t n, double* Zt, int64_t ldz, double* mean,
                           double* sd, int32_t* keep, int64_t* q_dev, hipStream_t s);
 

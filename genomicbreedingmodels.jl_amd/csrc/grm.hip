@@ -969,7 +969,10 @@ int launch_grm_syrk(const double* Zt, int64_t ldz, int64_t p, int64_t n, double*
 // stage 2: sum the slice partials of each tile into G. In carry mode, read back the error cell
 // of the inter-workgroup waits (tflags[ntiles]; set to −1 if a wait gave up) and fail loudly:
 // a timed-out wait would otherwise leave a silently wrong G.
-int launch_grm_reduce(int64_t n, int64_t p, double* G, int64_t ldg, const void* ws, hipStream_t s, int accum = 0) {
+// With err_out (device int32) the carry mode's error cell is copied there instead (no host sync: a
+// caller that queues several GRMs back to back checks them all at the end).
+int launch_grm_reduce(int64_t n, int64_t p, double* G, int64_t ldg, const void* ws, hipStream_t s, int accum = 0,
+                      int32_t* err_out = nullptr) {
   const GrmPlan g = plan(n, p);
   if (g.sb.n == 1 && g.sb.er == 0) return GBM_OK;
   if (!ws) return fail(GBM_E_ARG, "gbm_dev_grm_reduce: workspace required");
@@ -979,6 +982,10 @@ int launch_grm_reduce(int64_t n, int64_t p, double* G, int64_t ldg, const void* 
     GBM_LAUNCH_CHECK();
   }
   if (g.sb.n == 1) return GBM_OK;
+  if (g.sb.carry && err_out) {
+    GBM_HIP_TRY(hipMemcpyAsync(err_out, (const int32_t*)ws + g.ntiles, sizeof(int32_t), hipMemcpyDeviceToDevice, s));
+    return GBM_OK;
+  }
   if (g.sb.carry) {
     int32_t err = 0;
     GBM_HIP_TRY(hipMemcpyAsync(&err, (const int32_t*)ws + g.ntiles, sizeof(int32_t), hipMemcpyDeviceToHost, s));
@@ -993,11 +1000,11 @@ int launch_grm_reduce(int64_t n, int64_t p, double* G, int64_t ldg, const void* 
 }
 
 int launch_grm(const double* Zt, int64_t ldz, int64_t p, int64_t n, double* G, int64_t ldg, void* ws,
-               int64_t ws_bytes, hipStream_t s, int accum) {
+               int64_t ws_bytes, hipStream_t s, int accum, int32_t* err_out) {
   if (accum && !grm_can_accumulate(n, p)) return fail(GBM_E_ARG, "GRM: accumulation needs the slab split");
   int rc = launch_grm_syrk(Zt, ldz, p, n, G, ldg, ws, ws_bytes, s, accum);
   if (rc != GBM_OK) return rc;
-  return launch_grm_reduce(n, p, G, ldg, ws, s, accum);
+  return launch_grm_reduce(n, p, G, ldg, ws, s, accum, err_out);
 }
 
 // G += the GRM of these loci is possible with several loci ranges: their slabs' reduce adds into G,
@@ -1055,6 +1062,14 @@ extern "C" int64_t gbm_dev_grm_workspace(int64_t n, int64_t p) { return gbm::grm
 extern "C" int gbm_dev_grm(const double* Zt, int64_t ldz, int64_t p, int64_t n, double* G, int64_t ldg,
                            void* workspace, int64_t ws_bytes, void* stream) {
   return gbm::launch_grm(Zt, ldz, p, n, G, ldg, workspace, ws_bytes, (hipStream_t)stream);
+}
+
+extern "C" int gbm_dev_grm_accumulate(const double* Zt, int64_t ldz, int64_t p, int64_t n, double* G, int64_t ldg,
+                                      void* workspace, int64_t ws_bytes, void* stream) {
+  if (!gbm::grm_can_accumulate(n, p))
+    return gbm::fail(GBM_E_ARG, "gbm_dev_grm_accumulate: this (n, p) plans a single loci range (gbm_dev_grm_slices == 1); "
+                                "use more loci per call");
+  return gbm::launch_grm(Zt, ldz, p, n, G, ldg, workspace, ws_bytes, (hipStream_t)stream, 1);
 }
 
 extern "C" int gbm_dev_grm_syrk(const double* Zt, int64_t ldz, int64_t p, int64_t n, double* G, int64_t ldg,

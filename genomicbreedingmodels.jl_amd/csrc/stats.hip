@@ -34,6 +34,23 @@ __global__ void __launch_bounds__(256) synth_kernel(double* __restrict__ Xt, int
   }
 }
 
+// The same generator's dosages d (0, 1, 2) as bytes, column-major n x p (ldd): locus j0 + j's n
+// dosages at D + j*ldd. X = d/2 of synth_kernel exactly, at 1 B per cell: the device-resident input
+// of the loci-streamed fit (C3 on one GPU: 30 GB instead of 240 GB of fp64).
+__global__ void __launch_bounds__(256) synth_i8_kernel(int8_t* __restrict__ D, int64_t ldd, int64_t p, int64_t n,
+                                                       uint64_t seed, int64_t j0) {
+  for (int64_t j = blockIdx.y; j < p; j += gridDim.y) {
+    const uint64_t base = mix64(seed * 0xD1B54A32D192ED03ull + (uint64_t)(j0 + j));
+    const uint64_t thr = 214748364ull + (((base >> 32) * 1932735283ull) >> 32);
+    int8_t* col = D + j * ldd;
+    for (int64_t i = (int64_t)blockIdx.x * 1024 + threadIdx.x; i < (int64_t)(blockIdx.x + 1) * 1024 && i < n;
+         i += 256) {
+      const uint64_t h = mix64(base ^ ((uint64_t)i * 0x8CB92BA72F3D8DD7ull));
+      col[i] = (int8_t)(((h & 0xFFFFFFFFull) < thr) + ((h >> 32) < thr));
+    }
+  }
+}
+
 // D column-major n x p int8 (ldd) -> Xt row-major p x ldx, X = d / ploidy.
 __global__ void __launch_bounds__(256) expand_i8_kernel(const int8_t* __restrict__ D, int64_t ldd,
                                                         int64_t n, int64_t p, double inv_ploidy,
@@ -66,10 +83,18 @@ __device__ __forceinline__ double block_sum(double v, double* red) {
 // One workgroup per locus row (grid-strided). NPT = values cached in registers per thread
 // (0 = generic path re-reading the row from L2/MALL). T = int8_t reads dosage rows directly,
 // x = d·xs (the value expand_i8_kernel would have stored: bit-identical, without the fp64 copy).
+// The dosage product d·xs is rounded on its own (never fused into the caller's x − m): the value
+// expand_i8_kernel stores, so every kernel that rebuilds z from the bytes (standardise, the
+// streamed marker effects) gets the same bits as one that reads the expanded fp64 row.
+__device__ __forceinline__ double dosage_x(int8_t d, double xs) {
+#pragma clang fp contract(off)
+  return (double)d * xs;
+}
+
 template <typename T>
 __device__ __forceinline__ double load_x(const T* row, int64_t i, double xs) {
   if constexpr (std::is_same<T, int8_t>::value)
-    return (double)row[i] * xs;
+    return dosage_x(row[i], xs);
   else
     return row[i];
 }
@@ -165,6 +190,15 @@ extern "C" int gbm_dev_synth_genotypes(double* Xt, int64_t ldx, int64_t p, int64
   return GBM_OK;
 }
 
+extern "C" int gbm_dev_synth_dosage_i8(int8_t* D, int64_t ldd, int64_t p, int64_t n, uint64_t seed, int64_t j0,
+                                       void* stream) {
+  if (!D || p < 0 || n < 0 || ldd < n) return fail(GBM_E_ARG, "gbm_dev_synth_dosage_i8: bad arguments");
+  if (p == 0 || n == 0) return GBM_OK;
+  synth_i8_kernel<<<row_grid(n, p), 256, 0, (hipStream_t)stream>>>(D, ldd, p, n, seed, j0);
+  GBM_LAUNCH_CHECK();
+  return GBM_OK;
+}
+
 extern "C" int gbm_dev_expand_dosage_i8(const int8_t* D, int64_t ldd, int64_t n, int64_t p, int ploidy,
                                         double* Xt, int64_t ldx, void* stream) {
   if (!D || !Xt || p < 0 || n < 0 || ldd < n || ldx < n || ploidy < 1)
@@ -229,4 +263,10 @@ extern "C" int gbm_dev_standardize_gather(const double* Xt, int64_t ldx, int64_t
   if (p == 0) return GBM_OK;
   return launch_standardize<true>(Xt, ldx, p, idx, n, Zt, ldz, mean, sd, keep, q_dev, center_only,
                                   (hipStream_t)stream);
+}
+
+extern "C" int gbm_dev_standardize_i8(const int8_t* D, int64_t ldd, int64_t p, int64_t n, int ploidy, double* Zt,
+                                      int64_t ldz, double* mean, double* sd, int32_t* keep, int64_t* q_dev,
+                                      void* stream) {
+  return launch_standardize_i8(D, ldd, p, n, ploidy, Zt, ldz, mean, sd, keep, q_dev, (hipStream_t)stream);
 }

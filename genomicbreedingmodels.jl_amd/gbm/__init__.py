@@ -5,7 +5,7 @@ Public API mirrors the reference's model-function interface (src/GenomicBreeding
 The numerics run in libgbm.so (HIP, gfx950); nothing here falls back to a CPU path.
 """
 from ._lib import ArgumentError, GBMError, device_count, load as load_library
-from .linear import gblup, gblup_arrays, gblup_reml_arrays, gblup_synthetic, glmnet_folds, ridge, ridge_path_cv, ridge_select
+from .linear import gblup, gblup_arrays, gblup_dosage, gblup_reml_arrays, gblup_synthetic, glmnet_folds, ridge, ridge_path_cv, ridge_select
 from .metrics import heritabilitynarrow_sense, metrics, pearsonscorrelation, r2
 from .prediction import LINEAR_MODELS, extractxyetc, predict
 from .types import Fit, Genomes, Phenomes
@@ -16,7 +16,7 @@ from .cv import CV, cvbulk, cvbulk_setup, cvmultithread, fold_assignments, valid
 
 __all__ = [
     "ArgumentError", "GBMError", "device_count", "load_library",
-    "gblup", "gblup_arrays", "gblup_reml_arrays", "gblup_synthetic", "ridge", "ridge_path_cv", "ridge_select", "glmnet_folds", "metrics", "pearsonscorrelation", "r2", "heritabilitynarrow_sense",
+    "gblup", "gblup_arrays", "gblup_dosage", "gblup_reml_arrays", "gblup_synthetic", "ridge", "ridge_path_cv", "ridge_select", "glmnet_folds", "metrics", "pearsonscorrelation", "r2", "heritabilitynarrow_sense",
     "LINEAR_MODELS", "extractxyetc", "predict", "Fit", "Genomes", "Phenomes", "colstats", "grm", "grm_ploidy_aware", "infer_ploidy",
     "GenotypeSession", "bayesian", "brr_arrays", "CV", "cvbulk", "cvbulk_setup", "cvmultithread", "fold_assignments", "validate",
 ]

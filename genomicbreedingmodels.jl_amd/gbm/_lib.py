@@ -39,6 +39,7 @@ EXPORTS = (
     "gbm_dev_chol_strip_doubles", "gbm_dev_chol_strip_pack", "gbm_dev_chol_strip_unpack", "gbm_dev_chol_finish",
     "gbm_dev_grm_packed_size", "gbm_dev_grm_pack", "gbm_dev_grm_unpack",
     "gbm_debug_brr_stats", "gbm_debug_brr_shape", "gbm_debug_brr_trace", "gbm_debug_chol_flow_trace",
+    "gbm_dev_synth_dosage_i8", "gbm_dev_standardize_i8", "gbm_dev_grm_accumulate", "gbm_dev_marker_effects_i8",
 )
 
 
@@ -115,7 +116,13 @@ def _declare(lib):
     lib.gbm_dev_expand_dosage_i8.argtypes = [P, I64, I64, I64, I32, P, I64, P]
     lib.gbm_dev_standardize.restype = I32
     lib.gbm_dev_standardize.argtypes = [P, I64, I64, I64, P, I64, P, P, P, P, P]
-    for f in ("gbm_dev_grm", "gbm_dev_grm_syrk"):
+    lib.gbm_dev_synth_dosage_i8.restype = I32
+    lib.gbm_dev_synth_dosage_i8.argtypes = [P, I64, I64, I64, U64, I64, P]
+    lib.gbm_dev_standardize_i8.restype = I32
+    lib.gbm_dev_standardize_i8.argtypes = [P, I64, I64, I64, I32, P, I64, P, P, P, P, P]
+    lib.gbm_dev_marker_effects_i8.restype = I32
+    lib.gbm_dev_marker_effects_i8.argtypes = [P, I64, I64, I64, I32, P, I64, I64, D, P, P, P, P, P, I64, P, P]
+    for f in ("gbm_dev_grm", "gbm_dev_grm_syrk", "gbm_dev_grm_accumulate"):
         getattr(lib, f).restype = I32
         getattr(lib, f).argtypes = [P, I64, I64, I64, P, I64, P, I64, P]
     lib.gbm_dev_grm_reduce.restype = I32

@@ -65,6 +65,27 @@ def gblup_reml_arrays(X: np.ndarray, Y: np.ndarray, devices=None):
     return b_hat, y_pred, mu, int(q[0]), {"lambda": lam, "sigma2_e": s2e, "sigma2_u": s2u}
 
 
+def gblup_dosage(D: np.ndarray, ploidy: int, Y: np.ndarray, lambda_: float = 1.0, devices=None):
+    """GBLUP on int8 dosages (gbm_gblup_fit_dosage_i8: X = D/ploidy, 1 byte per cell over PCIe).
+    D (n, p) int8, any order. Returns (b_hat (p+1, t), y_pred (n, t), mu (t,), q)."""
+    D = np.asfortranarray(np.asarray(D, dtype=np.int8))
+    Y = np.asarray(Y, dtype=np.float64)
+    if Y.ndim == 1:
+        Y = Y[:, None]
+    Y = np.asfortranarray(Y)
+    n, p = D.shape
+    t = Y.shape[1]
+    b_hat = np.zeros((p + 1, t), order="F")
+    y_pred = np.zeros((n, t), order="F")
+    mu = np.zeros(t)
+    q = np.zeros(1, dtype=np.int64)
+    dev, nd = _lib.devices_arg(devices)
+    _lib.check(_lib.load().gbm_gblup_fit_dosage_i8(_lib.ptr(D), n, p, n, int(ploidy), _lib.ptr(Y), n, t,
+                                                  float(lambda_), dev, nd, _lib.ptr(b_hat), _lib.ptr(y_pred),
+                                                  _lib.ptr(mu), _lib.ptr(q)), "gbm_gblup_fit_dosage_i8")
+    return b_hat, y_pred, mu, int(q[0])
+
+
 def gblup_synthetic(seed: int, n: int, p: int, Y: np.ndarray, lambda_: float = 1.0, devices=None):
     """GBLUP on the device-generated synthetic genotypes (gbm_gblup_fit_synthetic: loci 0..p-1 of the
     SURVEY.md §8d generator, no host X). Returns (b_hat (p+1, t), y_pred (n, t), mu (t,), q)."""

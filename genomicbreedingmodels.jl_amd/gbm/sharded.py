@@ -176,14 +176,13 @@ class HipShardStages:
         self.npad = lib.gbm_dev_npad(n)
         self.gdim = lib.gbm_dev_gdim(n)
         f64 = dict(dtype=torch.float64, device=self.dev)
-        self.X = torch.empty((p_local, self.npad), **f64)   # raw genotypes (kept intact)
-        self.Z = torch.empty((p_local, self.npad), **f64)   # standardised (out of place)
+        self._alloc_rows(f64)
         self.mean = torch.empty(p_local, **f64)
         self.sd = torch.empty(p_local, **f64)
         self.keep = torch.empty(p_local, dtype=torch.int32, device=self.dev)
         self.q = torch.zeros(1, dtype=torch.int64, device=self.dev)
         self.G = torch.empty((self.gdim, self.gdim), **f64)
-        self.ws_grm_bytes = lib.gbm_dev_grm_workspace(n, p_local)
+        self.ws_grm_bytes = self._grm_workspace()
         self.ws_grm = torch.empty(max(self.ws_grm_bytes, 16), dtype=torch.uint8, device=self.dev)
         self.Y = torch.zeros((nrhs, self.npad), **f64)
         self.A = torch.zeros((nrhs, self.npad), **f64)
@@ -203,6 +202,13 @@ class HipShardStages:
             off += k
         self.info = self.out[off:].view(torch.int32)[:1]
         self.h_info = self.h_out[off:].view(torch.int32)[:1]
+
+    def _alloc_rows(self, f64):
+        self.X = self.torch.empty((self.p, self.npad), **f64)   # raw genotypes (kept intact)
+        self.Z = self.torch.empty((self.p, self.npad), **f64)   # standardised (out of place)
+
+    def _grm_workspace(self):
+        return self.lib.gbm_dev_grm_workspace(self.n, self.p)
 
     @staticmethod
     def _p(t):
@@ -318,3 +324,101 @@ class HipShardStages:
             raise _lib.GBMError(f"G/q + λI not positive definite (pivot {int(self.h_info[0])})")
         return dict(B=self.h_B.numpy(), y_pred=self.h_gebv.numpy()[:, : self.n].T, mu=self.h_mu.numpy(),
                     msum=self.h_msum.numpy())
+
+
+def chunk_schedule(p: int, chunk: int, halve_tail: bool = False):
+    """Loci chunks [(j, pc), ...] of a streamed shard: chunks of ``chunk`` loci; with ``halve_tail`` the
+    last full piece cut into halving pieces (none below 512 loci). Mirrors csrc/capi.cpp chunk_schedule
+    (the C ABI halves only for copy-bound fp64 uploads at n <= 8192 or when GBM_HOST_CHUNK is set)."""
+    cs, j = [], 0
+    while p - j > chunk:
+        cs.append((j, chunk))
+        j += chunk
+    r = p - j
+    d = 0
+    while halve_tail and d < 3 and r // 2 >= 512:
+        h = r // 2
+        cs.append((j, r - h))
+        j += r - h
+        r = h
+        d += 1
+    if r > 0:
+        cs.append((j, r))
+    return cs
+
+
+class HipStreamedShardStages(HipShardStages):
+    """A shard whose fp64 locus rows do not fit HBM (config C3 on one MI355X: 600 000 loci × 50 048 × 8 B
+    = 240 GB beside a 20 GB G): the genotypes stay resident as int8 dosages (1 B per cell, 30 GB), and
+    the loci pass through one fp64 chunk buffer — each chunk standardised from the bytes and its GRM
+    added into G in place (chunk GRMs summed in chunk order); the marker effects re-read the bytes with
+    z rebuilt in registers. The same chunks and kernels as the C ABI's loci-streamed mode
+    (csrc/capi.cpp stream_grm_shard / stream_effects_shard), so the results are the same bits."""
+
+    def __init__(self, n: int, p_local: int, chunk: int, nrhs: int = 1, lambda_: float = 1.0, device: int = 0,
+                 ploidy: int = 2, halve_tail: bool = False):
+        self.chunk = int(min(chunk, p_local))
+        self.ploidy = int(ploidy)
+        self.sched = chunk_schedule(p_local, self.chunk, halve_tail)
+        super().__init__(n, p_local, nrhs=nrhs, lambda_=lambda_, device=device)
+
+    def _alloc_rows(self, f64):
+        self.X = None
+        self.D = self.torch.empty((self.p, self.n), dtype=self.torch.int8, device=self.dev)  # Julia (n, p) layout
+        self.Z = self.torch.empty((self.chunk, self.npad), **f64)  # one chunk of standardised rows
+
+    def _grm_workspace(self):
+        return max(self.lib.gbm_dev_grm_workspace(self.n, pc) for _, pc in self.sched)
+
+    def generate(self, seed: int, j0: int):
+        """Synthetic dosages (counter hash) of global loci j0 .. j0+p-1: X = D/2."""
+        _lib.check(self.lib.gbm_dev_synth_dosage_i8(self._p(self.D), self.n, self.p, self.n, seed, j0, self._stream()),
+                   "synth_dosage_i8")
+        self.ploidy = 2
+
+    def upload_dosages(self, D_host_colmajor: np.ndarray, ploidy: int):
+        """Dosages D (n, p_local) int8 host array → resident bytes (X = D/ploidy)."""
+        self.D.copy_(self.torch.from_numpy(np.ascontiguousarray(np.asarray(D_host_colmajor, dtype=np.int8).T)))
+        self.ploidy = int(ploidy)
+
+    def upload_genotypes(self, X_host_colmajor: np.ndarray):
+        raise _lib.ArgumentError("a streamed shard holds int8 dosages: use upload_dosages")
+
+    # ---- stages: standardisation runs per chunk inside grm_syrk ------------------------------------
+    def standardize(self):
+        self.q.zero_()
+
+    def grm_syrk(self):
+        lib, Zp, Gp, s = self.lib, self._p(self.Z), self._p(self.G), self._stream()
+        for k, (j, pc) in enumerate(self.sched):
+            _lib.check(lib.gbm_dev_standardize_i8(ctypes.c_void_p(self.D.data_ptr() + j * self.n), self.n, pc, self.n,
+                                                  self.ploidy, Zp, self.npad, self._p(self.mean[j:]),
+                                                  self._p(self.sd[j:]), self._p(self.keep[j:]), self._p(self.q), s),
+                       "standardize_i8")
+            if k > 0 and lib.gbm_dev_grm_slices(self.n, pc) > 1:
+                _lib.check(lib.gbm_dev_grm_accumulate(Zp, self.npad, pc, self.n, Gp, self.gdim, self._p(self.ws_grm),
+                                                      self.ws_grm_bytes, s), "grm_accumulate")
+            elif k == 0:
+                _lib.check(lib.gbm_dev_grm(Zp, self.npad, pc, self.n, Gp, self.gdim, self._p(self.ws_grm),
+                                           self.ws_grm_bytes, s), "grm")
+            else:  # a single-range chunk: its own G, then added (the C ABI's Gc path)
+                Gc = self.torch.empty_like(self.G)
+                _lib.check(lib.gbm_dev_grm(Zp, self.npad, pc, self.n, self._p(Gc), self.gdim, self._p(self.ws_grm),
+                                           self.ws_grm_bytes, s), "grm")
+                self.G.add_(Gc)
+                del Gc
+
+    def grm_reduce(self):
+        pass
+
+    def effects(self):
+        _lib.check(self.lib.gbm_dev_marker_effects_i8(self._p(self.D), self.n, self.p, self.n, self.ploidy,
+                                                      self._p(self.A), self.npad, self.nrhs, 0.0, self._p(self.q),
+                                                      self._p(self.mean), self._p(self.sd), self._p(self.keep),
+                                                      self._p(self.B), self.p, self._p(self.msum), self._stream()),
+                   "effects_i8")
+
+    def genotype_chunks(self):
+        """(j, X[:, j:j+pc] as (pc, n) float64 on the device) over the schedule: the streamed X for checks."""
+        for j, pc in self.sched:
+            yield j, self.D[j:j + pc].to(self.torch.float64) / self.ploidy

@@ -196,6 +196,12 @@ int64_t gbm_dev_solve_workspace(int64_t n, int64_t nrhs);
 int gbm_dev_synth_genotypes(double* Xt, int64_t ldx, int64_t p, int64_t n, uint64_t seed,
                             int64_t j0, void* stream);
 
+/* The same synthetic genotypes as int8 dosages d = 2X (0, 1, 2), column-major n x p (ldd >= n):
+ * locus j0 + j's n dosages at D + j*ldd. 1 byte per cell — the device-resident input of the
+ * loci-streamed fit (config C3 on one GPU: 30 GB instead of 240 GB of fp64 X). */
+int gbm_dev_synth_dosage_i8(int8_t* D, int64_t ldd, int64_t p, int64_t n, uint64_t seed, int64_t j0,
+                            void* stream);
+
 /* Expand int8 dosages (column-major D, n x p, ldd) into Xt (row-major p x ldx) as D/ploidy. */
 int gbm_dev_expand_dosage_i8(const int8_t* D, int64_t ldd, int64_t n, int64_t p, int ploidy,
                              double* Xt, int64_t ldx, void* stream);
@@ -206,6 +212,10 @@ int gbm_dev_expand_dosage_i8(const int8_t* D, int64_t ldd, int64_t n, int64_t p,
  * monomorphic filter and standardisation of reference src/gwas.jl:112-115,127-130. */
 int gbm_dev_standardize(const double* Xt, int64_t ldx, int64_t p, int64_t n, double* Zt, int64_t ldz,
                         double* mean, double* sd, int32_t* keep, int64_t* q_dev, void* stream);
+/* As gbm_dev_standardize straight from int8 dosage rows (column-major D, n x p, ldd >= n; x = d/ploidy):
+ * bit-identical to gbm_dev_expand_dosage_i8 followed by gbm_dev_standardize, out of place into Zt. */
+int gbm_dev_standardize_i8(const int8_t* D, int64_t ldd, int64_t p, int64_t n, int ploidy, double* Zt, int64_t ldz,
+                           double* mean, double* sd, int32_t* keep, int64_t* q_dev, void* stream);
 /* As gbm_dev_standardize over the entry subset idx[0..n) of Xt's columns (gathered in the same
  * pass; out of place): the training-set extraction of reference src/prediction.jl:129 fused
  * with the standardisation. center_only != 0 centres without scaling and keeps every column
@@ -221,6 +231,10 @@ int gbm_dev_standardize_gather(const double* Xt, int64_t ldx, int64_t p, const i
  * of GenomicBreedingCore.grmsimple (called at reference src/gwas.jl:124). */
 int gbm_dev_grm(const double* Zt, int64_t ldz, int64_t p, int64_t n, double* G, int64_t ldg,
                 void* workspace, int64_t ws_bytes, void* stream);
+/* G += Σ_j z_j z_jᵀ over these p locus rows (same tiles and workspace as gbm_dev_grm): the loci-streamed
+ * fit adds each chunk of loci into one G. Needs a multi-range plan (gbm_dev_grm_slices(n, p) > 1). */
+int gbm_dev_grm_accumulate(const double* Zt, int64_t ldz, int64_t p, int64_t n, double* G, int64_t ldg,
+                           void* workspace, int64_t ws_bytes, void* stream);
 /* The two launches of gbm_dev_grm, separately (so a caller can time the SYRK kernel alone).
  * The SYRK splits the loci into ranges (gbm_dev_grm_slices of them) and writes one partial tile
  * per range into the workspace, which the reduce sums into G in a fixed order (bit-reproducible
@@ -300,6 +314,15 @@ int gbm_dev_marker_effects(const double* Zt, int64_t ldz, int64_t p, int64_t n,
                            const double* A, int64_t lda, int64_t nrhs, double inv_q, const int64_t* q_dev,
                            const double* mean, const double* sd, const int32_t* keep,
                            double* B, int64_t ldb, double* msum, void* stream);
+
+/* gbm_dev_marker_effects on int8 dosage rows (column-major D, n x p, ldd >= n, x = d/ploidy) instead of the
+ * standardised fp64 rows: z = (x − mean_j)/sd_j is rebuilt in registers exactly as gbm_dev_standardize_i8
+ * wrote it, so B and msum are bit-identical, at 1 byte read per cell (the loci-streamed fit's back-solve,
+ * which keeps no fp64 Z). lda >= gbm_dev_npad(n), even. */
+int gbm_dev_marker_effects_i8(const int8_t* D, int64_t ldd, int64_t p, int64_t n, int ploidy,
+                              const double* A, int64_t lda, int64_t nrhs, double inv_q, const int64_t* q_dev,
+                              const double* mean, const double* sd, const int32_t* keep,
+                              double* B, int64_t ldb, double* msum, void* stream);
 
 /*
  * ---- Device-resident genotype sessions: cross-validation fold farming and REML λ -----------

@@ -4,6 +4,8 @@
   device. At this n the GRM runs in its in-order carry accumulation mode (the slabs would exceed
   4 GiB). Properties of the exact solution, the host entry (gbm_gblup_fit_synthetic) against the
   stage path, and a subset of rows against the oracle.
+* C3 itself (50 000 × 600 000) on one GPU, loci-streamed (int8 dosages resident, fp64 chunks):
+  the same properties on the stage path, and the C ABI's automatic streamed mode against it.
 * One C5 fold at full size (20 000 × 300 000, three traits, fold 1 of 10 held out: ≈18 000
   training rows) on a device genotype session, against an independent stage-API fit of the
   gathered training rows, and a subset against the oracle.
@@ -93,6 +95,69 @@ def test_c3_per_gpu_shape():
     bs, ys, mus, qs = gbm.gblup_arrays(Xs, Y[rows], lambda_=lam)
     ref = oracle.gblup_fit(Xs, Y[rows], lam)
     assert qs == ref["q"] and rel(ys, ref["y_pred"]) < 1e-9 and rel(bs, ref["b_hat"]) < 1e-6
+
+
+def test_c3_full_size_one_gpu_streamed():
+    """Config C3 itself — n = 50 000 x p = 600 000 (BASELINE configs[2]; the GRM over all loci replaces
+    src/gwas.jl:117-126, the solve src/gwas.jl:591-597) — on ONE MI355X, loci-streamed: 30 GB of int8
+    dosages resident, 75 000-locus fp64 chunks standardised and added into the 20 GB G, marker
+    effects from the bytes. Exact-solution properties on the stage path, then the C ABI's automatic
+    streamed mode (gbm_gblup_fit_synthetic picks its own chunk) on the same problem."""
+    import torch
+    from gbm.sharded import HipStreamedShardStages, assemble_b_hat
+
+    n, p, lam, seed, chunk = 50000, 600000, 1.0, 424242, 75000
+    _free()
+    t0 = time.perf_counter()
+    st = HipStreamedShardStages(n, p, chunk, nrhs=1, lambda_=lam, device=0)
+    st.generate(seed, 0)
+    Y = synth.qtl_phenotypes(seed, n, p, 1, device=0)
+    st.load_phenotypes(Y)
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    st.standardize()
+    st.grm_syrk()
+    st.grm_reduce()
+    torch.cuda.synchronize()
+    t2 = time.perf_counter()
+    q = int(st.q.item())
+    assert q == p  # MAF >= 0.05 at n = 50 000: every locus polymorphic
+    G = st.G[:n, :n]
+    diag = torch.diagonal(G).clone() / q
+    assert abs(float(diag.mean()) - (n - 1) / n) < 1e-12
+    U = torch.triu(G)
+    t3 = time.perf_counter()
+    st.solve()
+    st.effects()
+    torch.cuda.synchronize()
+    t4 = time.perf_counter()
+    out = st.download()
+    y_pred, mu = out["y_pred"][:, 0], float(out["mu"][0])
+    a = st.A[0, :n].clone()
+    Ga = (U @ a + U.T @ a) / q - diag * a
+    r = (Ga + lam * a - (torch.from_numpy(Y[:, 0]).to(a.device) - mu)).abs().max().item()
+    assert r / np.abs(Y[:, 0] - mu).max() < 1e-10
+    assert abs(float(a.sum())) / float(a.abs().sum()) < 1e-10
+    del U, Ga, G
+    torch.cuda.empty_cache()
+    b_hat = assemble_b_hat(out["mu"], out["msum"], [out["B"]], p)
+    bd = torch.from_numpy(b_hat[1:, 0]).to(a.device)
+    pred = torch.full((n,), float(b_hat[0, 0]), dtype=torch.float64, device=a.device)
+    for j, Xc in st.genotype_chunks():  # predict's b0 + X b (src/prediction.jl:228), X streamed from the bytes
+        pred += Xc.T @ bd[j:j + Xc.shape[0]]
+        del Xc
+    assert rel(pred.cpu().numpy(), y_pred) < 1e-9
+    print(f"\nC3 full size on one GPU (streamed, {len(st.sched)} chunks of {chunk} loci): generate + phenotypes "
+          f"{t1 - t0:.2f} s, standardise + GRM {t2 - t1:.2f} s, solve + effects {t4 - t3:.2f} s (q = {q})")
+    del st, bd, a, pred
+    _free()
+    # the C ABI, its streamed mode chosen automatically (the fp64 rows cannot be resident next to G)
+    t5 = time.perf_counter()
+    b2, y2, mu2, q2 = gbm.gblup_synthetic(seed, n, p, Y, lambda_=lam, devices=[0])
+    t6 = time.perf_counter()
+    print(f"gbm_gblup_fit_synthetic at 50000 x 600000 on one GPU: {t6 - t5:.2f} s")
+    _free()
+    assert q2 == q and rel(y2[:, 0], y_pred) < 1e-12 and rel(b2, b_hat) < 1e-10
 
 
 def test_c5_fold_full_size():

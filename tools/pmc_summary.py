@@ -23,7 +23,11 @@ def main(root):
     fetch = per_kernel(os.path.join(root, "FETCH_SIZE", "**", "*counter_collection*.csv"), "FETCH_SIZE")
     write = per_kernel(os.path.join(root, "WRITE_SIZE", "**", "*counter_collection*.csv"), "WRITE_SIZE")
     bench = json.load(open(os.path.join(root, "bench_FETCH_SIZE.json")))
-    out = {"n": bench["config"]["n"], "p": bench["config"]["p_per_gpu"], "kernels": {}}
+    import hashlib
+    src = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "genomicbreedingmodels.jl_amd", "csrc", "grm.hip")
+    out = {"n": bench["config"]["n"], "p": bench["config"]["p_per_gpu"], "kernels": {},
+           # bench.py flags roofline.traffic stale once the GRM kernel source differs from this
+           "grm_hip_sha256": hashlib.sha256(open(src, "rb").read()).hexdigest()}
     for name in sorted(set(fetch) | set(write)):
         f = fetch.get(name, [])
         w = write.get(name, [])
