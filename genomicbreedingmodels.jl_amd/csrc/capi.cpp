@@ -86,14 +86,15 @@ class CtxPool {
       drop.swap(idle_);
     }
   }
-  // drops the idle contexts of one device (their buffers are freed outside the lock)
-  void trim(int dev) {
+  // drops the idle contexts of one device (their buffers are freed outside the lock); returns how many
+  int64_t trim(int dev) {
     std::vector<std::unique_ptr<FitCtx>> drop;
     {
       std::lock_guard<std::mutex> lock(mu_);
       auto it = idle_.find(dev);
       if (it != idle_.end()) drop.swap(it->second);
     }
+    return (int64_t)drop.size();
   }
 
  private:
@@ -107,7 +108,7 @@ CtxPool& pool() {
     auto* cp = new CtxPool;
     // an allocation that runs out of device memory first frees the idle contexts of its device
     // (they only grow and would otherwise hold e.g. ~50 GB each at C3's shape), then retries once
-    oom_trim_hook().store([](int dev) { pool().trim(dev); });
+    register_trim_hook([](int dev) { return pool().trim(dev); });
     return cp;
   }();
   return *p;
@@ -864,7 +865,7 @@ int solve_effects(const Problem& pr, std::vector<std::unique_ptr<Shard>>& shards
       GBM_HIP_TRY(hipSetDevice(c.dev));
       GBM_HIP_TRY(hipStreamSynchronize(c.stream.s));
       const int32_t info = infos[k];
-      if (info < 0) return fail(GBM_E_HIP, "back substitution: block synchronisation timed out");
+      if (info < 0) return fail(GBM_E_HIP, "solve: a wait between workgroups timed out (dataflow Cholesky or back substitution; the result is invalid)");
       if (info != 0)
         return fail(GBM_E_NOTPD, "G/q + lambda*I is not positive definite (pivot " + std::to_string(info) +
                                      "); check for non-finite genotypes");
@@ -943,7 +944,7 @@ int reml_lambda(FitCtx& c, int64_t n, int64_t q, const double* y, RemlResult& re
     GBM_HIP_TRY(hipMemcpyAsync(t, c.tmp.p, 4 * 8, hipMemcpyDeviceToHost, s));
     GBM_HIP_TRY(hipMemcpyAsync(&info, c.info.p, 4, hipMemcpyDeviceToHost, s));
     GBM_HIP_TRY(hipStreamSynchronize(s));
-    if (info < 0) return fail(GBM_E_HIP, "back substitution: block synchronisation timed out");
+    if (info < 0) return fail(GBM_E_HIP, "solve: a wait between workgroups timed out (dataflow Cholesky or back substitution; the result is invalid)");
     if (info != 0) return fail(GBM_E_NOTPD, "REML: G/q + lambda*I is not positive definite (pivot " + std::to_string(info) + ")");
     e = reml_profile(n, lambda, t);
     return GBM_OK;
@@ -997,14 +998,14 @@ int run_fit(const Problem& pr, const double* Y, int64_t ldy, int64_t nrhs, doubl
     }
   if (!reml) return solve_effects(pr, shards, leaders, ldevs, q, Y, ldy, 0, nrhs, lambda, b_hat_out, y_pred_out, mu_out);
   // REML (gbm_gblup_fit_reml): λ per trait chosen on the first leader's summed G, kept pristine in
-  // Gc on every leader (each solve factors G in place); then one solve + effects per trait at its λ.
+  // that leader's Gc only (each solve factors G in place; every leader restores its G from it:
+  // one extra n x n buffer per call, not per leader — 20 GB per device at C3); then one solve +
+  // effects per trait at its λ.
   const int64_t vbytes = npad * gdim * 8;  // rows [0, npad) of G: everything a solve reads of it
-  for (int k : leaders) {
-    FitCtx& c = shards[k]->x();
-    GBM_HIP_TRY(hipSetDevice(c.dev));
-    GBM_TRY(ensure(c.Gc, c.dev, gdim * gdim * 8));
-    GBM_HIP_TRY(hipMemcpyAsync(c.Gc.p, c.G.p, (size_t)vbytes, hipMemcpyDeviceToDevice, c.stream.s));
-  }
+  FitCtx& c0 = shards[leaders[0]]->x();
+  GBM_HIP_TRY(hipSetDevice(c0.dev));
+  GBM_TRY(ensure(c0.Gc, c0.dev, gdim * gdim * 8));
+  GBM_HIP_TRY(hipMemcpyAsync(c0.Gc.p, c0.G.p, (size_t)vbytes, hipMemcpyDeviceToDevice, c0.stream.s));
   std::vector<double> lam(nrhs);
   {
     RoctxRange r("gbm: REML lambda");
@@ -1017,11 +1018,12 @@ int run_fit(const Problem& pr, const double* Y, int64_t ldy, int64_t nrhs, doubl
       if (reml->s2u) reml->s2u[t] = res.s2u;
     }
   }
+  GBM_HIP_TRY(hipSetDevice(c0.dev));
+  GBM_HIP_TRY(hipStreamSynchronize(c0.stream.s));  // Gc complete before other leaders' streams read it
   for (int64_t t = 0; t < nrhs; t++) {
     for (int k : leaders) {
       FitCtx& c = shards[k]->x();
-      GBM_HIP_TRY(hipSetDevice(c.dev));
-      GBM_HIP_TRY(hipMemcpyAsync(c.G.p, c.Gc.p, (size_t)vbytes, hipMemcpyDeviceToDevice, c.stream.s));
+      GBM_TRY(copy_dd(c, c.G.p, c0, c0.Gc.p, vbytes));
     }
     GBM_TRY(solve_effects(pr, shards, leaders, ldevs, q, Y, ldy, t, 1, lam[t], b_hat_out, y_pred_out, mu_out));
   }
@@ -1051,6 +1053,12 @@ extern "C" int gbm_device_count(int* count) {
 }
 
 extern "C" int64_t gbm_device_allocations(void) { return alloc_counter().load(std::memory_order_relaxed); }
+
+extern "C" int gbm_debug_oom_retries(int64_t* retries, int64_t* contexts_freed) {
+  if (retries) *retries = oom_trim().retries.load();
+  if (contexts_freed) *contexts_freed = oom_trim().freed.load();
+  return GBM_OK;
+}
 
 extern "C" int gbm_release_device_cache(void) {
   pool().clear();

@@ -606,7 +606,11 @@ chol_flow_kernel(double* __restrict__ G, int64_t ld, int nbc, double* __restrict
       // Dinv during the factor, U_i,i+1 block by block), then one flag store each
       if (kTrace) ct[11] = (int64_t)__builtin_amdgcn_s_memrealtime();
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      // a wait timed out somewhere in the launch (info = −1; a bug guard): the chain stops here,
+      // before publishing tiles built from stale operands (read by every wave after the barrier)
+      if (tid == 0) s_task = __hip_atomic_load(info, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < 0 ? 1 : 0;
       lds_sync();
+      if (s_task) return;
       if (tid == 0) {
         __hip_atomic_store(flags + (int64_t)i * nbc + i, kFinal, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(flags + (int64_t)i * nbc + i + 1, kFinal, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -631,7 +635,10 @@ chol_flow_kernel(double* __restrict__ G, int64_t ld, int nbc, double* __restrict
 
   // ================================ the workers ================================
   for (;;) {
-    if (tid == 0) s_task = atomicAdd(queue, 1);
+    // no new task once a wait has timed out (info = −1): the launch drains instead of computing on
+    // tiles that will never be final
+    if (tid == 0)
+      s_task = __hip_atomic_load(info, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < 0 ? ntasks : atomicAdd(queue, 1);
     __syncthreads();
     const int t = __builtin_amdgcn_readfirstlane(s_task);
     if (t >= ntasks) return;
@@ -857,6 +864,9 @@ int launch_chol_flow(double* G, int64_t ldg, int64_t gdim, double* Ld, double* D
   if (nbc < 2 || (int64_t)FT * ldg * 8 > 0x7fffffff || nbc * nbc > 0x3fffffff)
     return fail(GBM_E_ARG, "dataflow Cholesky: matrix too large for 32-bit buffer offsets");
   GBM_HIP_TRY(hipMemsetAsync(flag_block, 0, (size_t)chol_flow_flag_bytes(gdim), s));
+  // GBM_TEST_CHOL_FLOW_ABORT (tests): start as if a wait had already timed out (info = −1), so the
+  // early exit of the chain and the workers runs; the solve then fails loudly, without a hang
+  if (getenv("GBM_TEST_CHOL_FLOW_ABORT")) GBM_HIP_TRY(hipMemsetAsync(info, 0xFF, sizeof(int32_t), s));
   // one workgroup per CU; GBM_CHOL_FLOW_WGS (re-read per solve) caps the workers: with 1, one worker
   // runs every tile task in dequeue order beside the chain, which checks that no wait targets a later
   // task

@@ -11,10 +11,10 @@
 // workgroup applies δ = M r̃ redundantly from identical inputs (deterministic), updates e += X_B δ
 // on its individuals and computes the next block's partial dots, so a block costs one launch and
 // no device-wide synchronisation; one Gibbs iteration is captured as a hipGraph and replayed.
-// With byte storage the iteration is instead one persistent sweep launch: over 128-marker blocks
-// (brr_sweep128_kernel, one 256-individual chunk per CU) or, round 3, over 512-marker super-blocks
-// on up to every CU (brr_sweep_sb_kernel, and its look-ahead form brr_sweep_la_kernel, the
-// default: see "super-block sweep" below).
+// With byte storage and n <= 48 x CUs the iteration is instead ONE persistent sweep launch over
+// 512-marker super-blocks on up to every CU (brr_sweep_la2_kernel: see "super-block sweep" below);
+// otherwise the per-block launches above run. (Rounds 2-3 also kept a 128-block sweep and two
+// earlier super-block schedules; they are in git history, e.g. `git show 3599bea:<this file>`.)
 //
 // Random numbers: a counter-based hash of (seed, stream, counter) (no sampler state), Box-Muller
 // normals and Marsaglia-Tsang gammas, restated bit-for-bit in oracle/oracle.py (brr_*), so the
@@ -563,7 +563,6 @@ __global__ void __launch_bounds__(256) brr_step_kernel(const T* __restrict__ Xt,
 // Half the dependent launches per iteration of the 64-marker kernel, same sample path (markers
 // in order).
 constexpr int BK2 = 2 * BB;  // markers per launch
-constexpr int WP = BB + 2;   // LDS pitch of W_BB (528 B ≡ 16 B mod 256 B: conflict-free b128 row reads)
 
 // Dt[b][i][s] = D[(128 b + s) ldx + i] (0 for markers past p): the e update reads its 128
 // genotypes of block b as 128 contiguous bytes per individual (coalesced b128 loads).
@@ -773,269 +772,17 @@ __global__ void __launch_bounds__(256) brr_step128_kernel(const uint8_t* __restr
   }
 }
 
-// ---- byte storage: one persistent launch per sweep ------------------------------------------
-// The C workgroups (one per 256-individual chunk, all resident: C <= CUs) run every 128-marker
-// block of the sweep in one launch instead of one launch each. Block k's partial dots are handed
-// between workgroups as in the dataflow Cholesky (chol_flow.hip; per-XCD L2s are not coherent):
-// the storing wave writes them through (`sc1` buffer stores), drains (`s_waitcnt vmcnt(0)`) and
-// one lane stores the workgroup's flag = k + 1 (relaxed, agent scope); wave 3 of every workgroup
-// polls the C flags and reads the partials only through `sc1` loads. Two partial buffers (block
-// parity) suffice: a workgroup writes block k + 2's partials only after every workgroup published
-// block k + 1's, i.e. after all have read block k's. The next block's operands — M (waves 0-2,
-// LDS DMA), α/γ (wave 3) and the next rows of D (for the dots, then kept in LDS for that block's
-// e update) — are loaded while the current block computes: off the hand-off's critical path. e
-// stays in registers for the whole sweep. Waits are bounded (~1 s): a timed-out workgroup sets
-// *info = −1 and every workgroup leaves.
-constexpr int kSweepBatch = 40;  // partial loads in flight per batch (C4: C = 40 in one batch)
-
+// ---- hand-off helpers of the persistent sweep ---------------------------------------------------
+// Buffer resource over a device array, for the `sc1` (write-through / L2-coherent) loads and stores
+// of the sweep's inter-workgroup hand-offs (per-XCD L2s are not coherent).
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t brr_rsrc(const void* p, int64_t bytes) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
 }
 
-__global__ void __launch_bounds__(256) brr_sweep128_kernel(const uint8_t* __restrict__ D, int64_t ldx, int64_t p, double xs,
-                                                           const double* __restrict__ Mb, int64_t nblk,
-                                                           double* __restrict__ part, int32_t* __restrict__ flags,
-                                                           int32_t* __restrict__ info, double* __restrict__ b,
-                                                           double* __restrict__ bbar, const double* __restrict__ alpha,
-                                                           const double* __restrict__ gamma, double* __restrict__ e,
-                                                           const BrrState* __restrict__ st) {
-  __shared__ __attribute__((aligned(16))) double rt[BK2];  // r̃ = γ − α∘d⁰ of the block's markers
-  __shared__ __attribute__((aligned(16))) double dl[BK2];   // δ of the block's markers
-  __shared__ double dU[BB], dV[BB];                         // M_B r̃_B, O r̃_A (δ_B = dU + dV)
-  __shared__ double es[IW];
-  __shared__ double part4[4][BK2];
-  // each wave's quarter of a block's rows (128 rows x 64 individuals, pitch 68 B: conflict-free
-  // dword writes of a row per lane, and byte reads of a column per lane), kept from the dots that
-  // used them (partials of block k) for block k's e update: each genotype is read from HBM once
-  __shared__ uint32_t T[4][BK2 * 17];
-  // the block's M_A, M_B, O (row k's 16-B chunk c at position c ^ (k & 31): conflict-free row
-  // reads), DMA'd from HBM while the previous block finishes — in LDS, not registers, so that the
-  // sweep's live state fits the VGPRs
-  __shared__ __attribute__((aligned(16))) double Ms[3][BB * BB];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int C = (int)gridDim.x;
-  const int64_t i0 = (int64_t)blockIdx.x * IW, i = i0 + tid;
-  const __amdgpu_buffer_rsrc_t rP = brr_rsrc(part, (int64_t)2 * C * BK2 * 8);
-  const int it_odd = (int)(st->it & 1);
-  const bool acc = brr_accumulate(st);
-  const double kk = (double)(st->nsum + 1);
-  // operand loaders (each wave loads only what it uses)
-  auto dma_M = [&](int64_t k) {  // waves 0-2: M_A, M_B, O of block k into Ms[wave], 2 rows per instruction
-    const uint8_t* src0 = reinterpret_cast<const uint8_t*>(
-        Mb + k * 3 * BB * BB + (wave == 0 ? 0 : wave == 1 ? 2 * BB * BB : BB * BB));
-    const int rr = lane >> 5, pos = lane & 31;
-#pragma unroll 4
-    for (int q = 0; q < BB / 2; q++) {
-      const int row = 2 * q + rr;
-      const uint8_t* src = src0 + row * BB * 8 + ((pos ^ (row & 31)) * 16);
-      const unsigned m0v = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(&Ms[wave][q * 2 * BB]));
-      asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off" : : "s"(m0v), "v"(src) : "memory");
-    }
-  };
-  uint4 rv[8];  // rows lane and lane + 64 of a block, individuals [64 wave, 64 wave + 64) of the chunk
-  auto load_rows = [&](int64_t k) {
-    const int64_t j = k * BK2;
-#pragma unroll
-    for (int h = 0; h < 2; h++) {
-      const int64_t r = min(j + lane + BB * h, p - 1);  // past p: a valid row, never summed
-      const uint4* src = reinterpret_cast<const uint4*>(D + r * ldx + i0 + wave * 64);
-#pragma unroll
-      for (int u = 0; u < 4; u++) rv[4 * h + u] = src[u];
-    }
-  };
-  double alA = 0.0, alB = 0.0, gaA = 0.0, gaB = 0.0;  // wave 3
-  auto load_ag = [&](int64_t k) {
-    alA = alpha[k * BK2 + lane];
-    alB = alpha[k * BK2 + BB + lane];
-    gaA = gamma[k * BK2 + lane];
-    gaB = gamma[k * BK2 + BB + lane];
-  };
-  double bo = 0.0, bbo = 0.0;  // workgroup 0, waves 0-1: marker (k, wave, lane)'s b (this parity) and b̄
-  auto load_b = [&](int64_t k) {
-    const int64_t jm = k * BK2 + wave * BB + lane, jc = jm < p ? jm : 0;
-    const double b0 = b[jc], b1 = b[p + jc];
-    bbo = bbar[jc];
-    bo = it_odd ? b1 : b0;
-  };
-  // partials of block k + 1 from es and rv (rows of block k + 1): part4, then wave 3 publishes
-  auto dots_publish = [&](int64_t k1) {
-    const int nb1 = (int)((p - k1 * BK2) < BK2 ? (p - k1 * BK2) : BK2);
-    {
-      // both rows (lane, lane + 64) over this wave's 64 individuals, 16 at a time: each es value
-      // is read once for the two rows; even/odd individuals in separate sums as brr_dot64_u8
-      double s0 = 0.0, s1 = 0.0, t0 = 0.0, t1 = 0.0;
-      const double* ew = es + wave * 64;
-#pragma unroll
-      for (int u = 0; u < 4; u++) {
-        asm volatile("" : "+v"(s0), "+v"(s1), "+v"(t0), "+v"(t1)::"memory");
-        const uint32_t wa[4] = {rv[u].x, rv[u].y, rv[u].z, rv[u].w};
-        const uint32_t wb[4] = {rv[4 + u].x, rv[4 + u].y, rv[4 + u].z, rv[4 + u].w};
-#pragma unroll
-        for (int q = 0; q < 4; q++)
-#pragma unroll
-          for (int bb = 0; bb < 4; bb += 2) {
-            const double2 e2 = *reinterpret_cast<const double2*>(ew + 16 * u + 4 * q + bb);
-            s0 = fma((double)((wa[q] >> (8 * bb)) & 0xFFu), e2.x, s0);
-            s1 = fma((double)((wa[q] >> (8 * bb + 8)) & 0xFFu), e2.y, s1);
-            t0 = fma((double)((wb[q] >> (8 * bb)) & 0xFFu), e2.x, t0);
-            t1 = fma((double)((wb[q] >> (8 * bb + 8)) & 0xFFu), e2.y, t1);
-          }
-      }
-      part4[wave][lane] = lane < nb1 ? s0 * xs + s1 * xs : 0.0;
-      part4[wave][BB + lane] = BB + lane < nb1 ? t0 * xs + t1 * xs : 0.0;
-    }
-    // the rows into T for block k1's e update (this wave's region, read by this wave only)
-#pragma unroll
-    for (int h = 0; h < 2; h++) {
-      uint32_t* tr = T[wave] + (lane + BB * h) * 17;
-#pragma unroll
-      for (int u = 0; u < 4; u++) {
-        tr[4 * u] = rv[4 * h + u].x;
-        tr[4 * u + 1] = rv[4 * h + u].y;
-        tr[4 * u + 2] = rv[4 * h + u].z;
-        tr[4 * u + 3] = rv[4 * h + u].w;
-      }
-    }
-    lds_barrier();
-    if (wave == 3) {
-      __amdgpu_buffer_rsrc_t r = rP;
-      const double pa = ((part4[0][lane] + part4[1][lane]) + part4[2][lane]) + part4[3][lane];
-      const double pb = ((part4[0][BB + lane] + part4[1][BB + lane]) + part4[2][BB + lane]) + part4[3][BB + lane];
-      const uint32_t off = (uint32_t)((((k1 & 1) * C + blockIdx.x) * BK2 + 2 * lane) * 8);
-      typedef unsigned int u4v __attribute__((ext_vector_type(4)));
-      typedef double d2v __attribute__((ext_vector_type(2)));
-      const d2v val = {pa, pb};
-      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4v, val), r, (int)off, 0, 16);  // sc1
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      if (lane == 0) __hip_atomic_store(flags + blockIdx.x, (int32_t)(k1 + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  };
-
-  // ---- prologue: block 0's partials from e, then block 0's operands
-  double ei = e[i];
-  load_rows(0);
-  es[tid] = ei;
-  lds_barrier();
-  dots_publish(0);
-  if (wave < 3) dma_M(0);
-  else load_ag(0);
-  if (blockIdx.x == 0 && wave < 2) load_b(0);
-  if (nblk > 1) load_rows(1);
-
-  for (int64_t k = 0; k < nblk; k++) {
-    // (1) wave 3: wait until every workgroup published block k's partials, sum them in chunk
-    // order (bit-identical in every workgroup), form r̃
-    if (wave == 3) {
-      bool ok = true;
-      for (int64_t spin = 0;; spin++) {
-        int ready = 1;
-        for (int c = lane; c < C; c += 64)
-          ready &= __hip_atomic_load(flags + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= (int32_t)(k + 1);
-        if (__builtin_amdgcn_read_exec() == __builtin_amdgcn_ballot_w64(ready != 0)) break;
-        if ((spin & 255) == 255) {
-          if (__hip_atomic_load(info, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < 0) { ok = false; break; }
-          if (spin > ((int64_t)1 << 22)) {
-            if (lane == 0) __hip_atomic_store(info, -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            ok = false;
-            break;
-          }
-        }
-        __builtin_amdgcn_s_sleep(1);
-      }
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // the sc1 loads stay below the poll
-      if (!ok) rt[0] = __builtin_nan("");                    // poison: every wave leaves below
-      double rA = 0.0, rB = 0.0;
-      const uint32_t base = (uint32_t)(((k & 1) * C * BK2 + 2 * lane) * 8);
-      for (int c0 = 0; c0 < C; c0 += kSweepBatch) {
-        typedef double d2v __attribute__((ext_vector_type(2)));
-        d2v v[kSweepBatch];
-#pragma unroll
-        for (int m = 0; m < kSweepBatch; m++)
-          v[m] = __builtin_bit_cast(d2v, __builtin_amdgcn_raw_buffer_load_b128(
-                                              rP, (int)(base + (uint32_t)min(c0 + m, C - 1) * BK2 * 8), 0, 16));
-#pragma unroll
-        for (int m = 0; m < kSweepBatch; m++) {
-          rA += c0 + m < C ? v[m].x : 0.0;
-          rB += c0 + m < C ? v[m].y : 0.0;
-        }
-      }
-      if (ok) {
-        rt[lane] = fma(rA, -alA, gaA);
-        rt[BB + lane] = fma(rB, -alB, gaB);
-      }
-    }
-    // (waves 0-2 meanwhile: this wave's DMA of Ms has landed; one barrier then covers both)
-    if (wave < 3) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    lds_barrier();
-    if (__builtin_isnan(rt[0]) && __hip_atomic_load(info, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < 0) return;
-    // (2) the three GEMVs on three waves: δ_A = M_A r̃_A (wave 0), M_B r̃_B (wave 1), O r̃_A
-    // (wave 2); δ_B = M_B r̃_B + O r̃_A (as brr_step128_kernel). Every DMA of M has landed.
-    if (wave < 3) {
-      const int sw = lane & 31;
-      double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
-      const double* mr = Ms[wave] + lane * BB;  // Ms[0] = M_A, Ms[1] = M_B, Ms[2] = O
-      const double* r = rt + (wave == 1 ? BB : 0);
-#pragma unroll
-      for (int c = 0; c < BB / 2; c += 2) {
-        const double2 m01 = *reinterpret_cast<const double2*>(mr + 2 * (c ^ sw));
-        const double2 m23 = *reinterpret_cast<const double2*>(mr + 2 * ((c + 1) ^ sw));
-        const double2 r01 = *reinterpret_cast<const double2*>(r + 2 * c);
-        const double2 r23 = *reinterpret_cast<const double2*>(r + 2 * c + 2);
-        a0 = fma(m01.x, r01.x, a0);
-        a1 = fma(m01.y, r01.y, a1);
-        a2 = fma(m23.x, r23.x, a2);
-        a3 = fma(m23.y, r23.y, a3);
-      }
-      (wave == 0 ? dl : wave == 1 ? dU : dV)[lane] = (a0 + a1) + (a2 + a3);
-    }
-    lds_barrier();
-    if (wave < 3 && k + 1 < nblk) dma_M(k + 1);  // every wave's GEMV has read Ms
-    if (wave == 3) dl[BB + lane] = dU[lane] + dV[lane];
-    lds_barrier();
-    // (3) workgroup 0 stores b and the running means of block k
-    if (blockIdx.x == 0 && wave < 2) {
-      const int64_t jm = k * BK2 + wave * BB + lane;
-      if (jm < p) {
-        const double dlt = dl[wave * BB + lane];
-        const double bn = bo - dlt;
-        b[(it_odd ^ 1) * p + jm] = bn;
-        if (acc) bbar[jm] = bbo * ((kk - 1.0) / kk) + bn / kk;
-      }
-      if (k + 1 < nblk) load_b(k + 1);
-    }
-    // (4) e += X_B δ (markers past p have δ = 0), four chains, genotypes from T (column `lane`)
-    {
-      double a4[4] = {0.0, 0.0, 0.0, 0.0};
-      const uint8_t* tc = reinterpret_cast<const uint8_t*>(T[wave]) + lane;
-#pragma unroll
-      for (int c = 0; c < BK2; c += 32) {
-        // 32 markers' operands in flight at a time (the fully hoisted loop needs ~200 registers)
-        asm volatile("" : "+v"(a4[0]), "+v"(a4[1]), "+v"(a4[2]), "+v"(a4[3])::"memory");
-#pragma unroll
-        for (int s = c; s < c + 32; s += 2) {
-          const double2 d2 = *reinterpret_cast<const double2*>(dl + s);
-          a4[s & 3] = fma(d2.x, (double)tc[s * 68], a4[s & 3]);
-          a4[(s + 1) & 3] = fma(d2.y, (double)tc[(s + 1) * 68], a4[(s + 1) & 3]);
-        }
-      }
-      ei = ei + ((a4[0] + a4[1]) + (a4[2] + a4[3])) * xs;
-    }
-    if (k + 1 >= nblk) break;
-    es[tid] = ei;
-    lds_barrier();
-    // (5) block k + 1's partials from the updated e, published by wave 3; then the operands of
-    // block k + 1 (wave 3) and the rows of block k + 2
-    dots_publish(k + 1);
-    if (wave == 3) load_ag(k + 1);
-    if (k + 2 < nblk) load_rows(k + 2);
-  }
-  e[i] = ei;  // rows past n stay 0: their genotypes are 0
-}
-
 // ---- byte storage: super-block sweep over all CUs (round 3) ------------------------------------
-// The per-block sweep above runs one 256-individual chunk per CU (⌈n/256⌉ = 40 CUs at C4) and
-// hands partial dots between them after every 128-marker block: bound by one CU's work per
-// block and one hand-off per block. Here the markers go in super-blocks of SBK = 512: the whole
+// One 256-individual chunk per CU (⌈n/256⌉ = 40 CUs at C4) with a hand-off after every 128-marker
+// block is bound by one CU's work per block and one hand-off per block. Instead the markers go in
+// super-blocks of SBK = 512: the whole
 // super-block's single-site steps are ONE affine map of its start dots,
 //   δ_S = M_S (γ_S − α_S ∘ d⁰_S),  M_S = (I + D_S L_S)⁻¹  (unit lower, 512 x 512),
 // built once per iteration by block forward substitution over the four 128-marker sub-blocks
@@ -1057,7 +804,6 @@ __global__ void __launch_bounds__(256) brr_sweep128_kernel(const uint8_t* __rest
 // *info = −1, every workgroup leaves; the host falls back).
 static_assert(SBN * BK2 == SBK, "super-blocks are whole 128-marker blocks");
 constexpr int SB_PAIRS = SBN * (SBN - 1) / 2;
-constexpr int SB_KMAX = 64;            // individuals per chunk (at most)
 constexpr int SB_RMAX = 8;             // owned rows per workgroup (at most)
 
 __device__ __forceinline__ int sb_pair_index(int i, int m) { return i * (i - 1) / 2 + m; }  // i > m
@@ -1258,18 +1004,11 @@ __device__ __forceinline__ void sb_put(__amdgpu_buffer_rsrc_t r, uint32_t off, d
   const sbu4 w = {(unsigned)a, (unsigned)(a >> 32), (unsigned)b, (unsigned)(b >> 32)};
   __builtin_amdgcn_raw_buffer_store_b128(w, r, (int)off, 0, 16);  // sc1
 }
-// A poll's load is inline asm (volatile: the compiler hoisted the builtin's read-only load out of
-// the spin and polled a register); the caller waits with sb_landed() before using the values.
-__device__ __forceinline__ sbu4 sb_get(__amdgpu_buffer_rsrc_t r, uint32_t off) {
-  sbu4 v;
-  asm volatile("buffer_load_dwordx4 %0, %1, %2, 0 offen sc1" : "=v"(v) : "v"(off), "s"(r) : "memory");
-  return v;
-}
-__device__ __forceinline__ void sb_landed() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
-// The same poll as a compiler-visible load (cache policy sc1): the compiler counts it, waits just
-// before the first use of its value and never has to wait for everything in flight because of an
-// opaque asm load. A poll loop that uses it starts each round with sb_fence(), so that the load is
-// not hoisted out of the loop.
+// A poll is a compiler-visible load with cache policy sc1 (so the compiler counts it and waits just
+// before the first use of its value; an inline-asm load made it wait for everything in flight). A
+// poll loop starts each round with sb_fence(), so that the load is not hoisted out of the loop (as
+// LLVM did with the builtin's "read-only" load before the fence). A poll must not sit under a
+// divergent branch: the compiler may then copy its register at the merge before the data lands.
 __device__ __forceinline__ sbu4 sb_getv(__amdgpu_buffer_rsrc_t r, uint32_t off) {
   return __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 16);
 }
@@ -1317,296 +1056,10 @@ __device__ __forceinline__ bool sb_spin(bool lane_done, int64_t& spin, int32_t* 
   return true;
 }
 
-// K individuals per chunk workgroup (a multiple of 16, <= SB_KMAX); R owned rows (even, <= SB_RMAX).
-// kTrace (timing tool, GBM_BRR_TRACE=1): workgroups 0 and C − 1 record 8 timestamps per super-block.
-template <bool kTrace>
-__global__ void __launch_bounds__(256) brr_sweep_sb_kernel(const uint8_t* __restrict__ D, int64_t ldx, int64_t n,
-                                                           int64_t p, double xs, const double* __restrict__ MS,
-                                                           int64_t nsb, int K, int R, double* __restrict__ Pb,
-                                                           double* __restrict__ Rt, double* __restrict__ Dl,
-                                                           int32_t* __restrict__ info, double* __restrict__ b,
-                                                           double* __restrict__ bbar, const double* __restrict__ alpha,
-                                                           const double* __restrict__ gamma, double* __restrict__ e,
-                                                           const BrrState* __restrict__ st, int64_t* __restrict__ trace) {
-  __shared__ __attribute__((aligned(16))) uint8_t Drow[2][SBK * SB_KMAX];  // a super-block's rows of the chunk
-  __shared__ __attribute__((aligned(16))) double es[SB_KMAX];
-  __shared__ __attribute__((aligned(16))) double rt[SBK];
-  __shared__ __attribute__((aligned(16))) double dl[SBK];
-  __shared__ double red[4][SB_RMAX];
-  __shared__ double eacc[4096 + SB_KMAX];  // e update partial sums [individual][slice]: K x (nsl_used | 1)
-  __shared__ double eq[4][SB_KMAX];
-  __shared__ int s_fail;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int C = (int)gridDim.x, c = (int)blockIdx.x;
-  const int64_t i0 = (int64_t)c * K;
-  const int r0 = c * R;  // owned rows [r0, r0 + R) of every super-block (those < SBK)
-  const int nown = r0 >= SBK ? 0 : (SBK - r0 < R ? SBK - r0 : R);
-  const bool tr_on = kTrace && (c == 0 || c == C - 1) && threadIdx.x == 0;
-  int64_t* trw = kTrace ? trace + (c == 0 ? 0 : 1) * nsb * 12 : nullptr;
-  auto mark = [&](int64_t s, int k) {
-    if (tr_on) trw[s * 12 + k] = (int64_t)__builtin_amdgcn_s_memrealtime();
-  };
-  const int it_odd = (int)(st->it & 1);
-  const bool accum = brr_accumulate(st);
-  const double kk = (double)(st->nsum + 1);
-  const uint64_t tag0 = (st->epoch << 40) + (uint64_t)st->it * (uint64_t)nsb;
-  const __amdgpu_buffer_rsrc_t rP = brr_rsrc(Pb, (int64_t)2 * C * SBK * 16);
-  const __amdgpu_buffer_rsrc_t rR = brr_rsrc(Rt, (int64_t)2 * SBK * 16);
-  const __amdgpu_buffer_rsrc_t rD = brr_rsrc(Dl, (int64_t)2 * SBK * 16);
-  if (tid == 0) s_fail = 0;
-  // wave 3: the chunk's rows of super-block sb into Drow[sb & 1] (16-B pieces; row j's K bytes at
-  // j * K; rows past p re-read row p − 1, never used: δ = 0 there)
-  auto dma_rows = [&](int64_t sb) {
-    const int pieces = SBK * (K / 16);
-    uint8_t* dst = Drow[sb & 1];
-    for (int q0 = 0; q0 < pieces; q0 += 64) {
-      const int q = q0 + lane;
-      const int row = q / (K / 16), part = q % (K / 16);
-      int64_t jr = sb * SBK + row;
-      jr = jr < p ? jr : p - 1;
-      const uint8_t* src = D + jr * ldx + i0 + part * 16;
-      const unsigned m0v = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(dst + q0 * 16));
-      asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off" : : "s"(m0v), "v"(src) : "memory");
-    }
-  };
-  if (tid < SB_KMAX) es[tid] = (tid < K && i0 + tid < n) ? e[i0 + tid] : 0.0;
-  if (wave == 3) {
-    dma_rows(0);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-  __syncthreads();
-  // e update: thread t -> 16-individual piece t % nch of slice t / nch (rows [sl·rps, (sl+1)·rps))
-  const int nch = K / 16, nsl = 256 / nch, rps = (SBK + nsl - 1) / nsl;
-  const int ech = tid % nch, esl = tid / nch;
-  const int nsl_used = (SBK + rps - 1) / rps;
-  const int slp = nsl_used | 1;  // odd pitch of eacc's slice rows (bank-conflict-free writes and reads)
-  for (int64_t s = 0; s < nsb; s++) {
-    const int par = (int)(s & 1);
-    const uint8_t* Dr = Drow[par];
-    const int64_t j0 = s * SBK;
-    const uint64_t key = sb_key(tag0 + (uint64_t)s);
-    mark(s, 0);
-    // (1) partial dots of the super-block's 512 markers over this chunk: thread t -> rows 2t, 2t + 1,
-    // published as granules P[par][c][row]
-    {
-      double a0 = 0.0, a1 = 0.0, c0 = 0.0, c1 = 0.0;
-      const uint8_t* ra = Dr + (2 * tid) * K;
-      const uint8_t* rb = ra + K;
-      for (int u = 0; u < K; u += 16) {
-        const uint4 va = *reinterpret_cast<const uint4*>(ra + u);
-        const uint4 vb = *reinterpret_cast<const uint4*>(rb + u);
-        const uint32_t wa[4] = {va.x, va.y, va.z, va.w};
-        const uint32_t wb[4] = {vb.x, vb.y, vb.z, vb.w};
-#pragma unroll
-        for (int q = 0; q < 4; q++)
-#pragma unroll
-          for (int bb = 0; bb < 4; bb += 2) {
-            const double2 e2 = *reinterpret_cast<const double2*>(es + u + 4 * q + bb);
-            a0 = fma((double)((wa[q] >> (8 * bb)) & 0xFFu), e2.x, a0);
-            a1 = fma((double)((wa[q] >> (8 * bb + 8)) & 0xFFu), e2.y, a1);
-            c0 = fma((double)((wb[q] >> (8 * bb)) & 0xFFu), e2.x, c0);
-            c1 = fma((double)((wb[q] >> (8 * bb + 8)) & 0xFFu), e2.y, c1);
-          }
-      }
-      const uint32_t off = (uint32_t)((((int64_t)par * C + c) * SBK + 2 * tid) * 16);
-      sb_put(rP, off, a0 * xs + a1 * xs, key);
-      sb_put(rP, off + 16, c0 * xs + c1 * xs, key);
-    }
-    // wave 3: the next super-block's rows (land during the hand-offs; Drow[par ^ 1] was last read
-    // by the previous super-block's e update, before the barrier that ended it)
-    if (wave == 3 && s + 1 < nsb) dma_rows(s + 1);
-    mark(s, 1);
-    // this super-block's operands of the owned rows (plain loads: written before this launch)
-    double mrow[2][8];
-    double alv = 0.0, gav = 0.0, bo = 0.0, bbo = 0.0;
-    const int wrow0 = wave, wrow1 = wave + 4;  // owned-row indices of this wave's δ dots (< nown)
-#pragma unroll
-    for (int h = 0; h < 2; h++) {
-      const int w = h ? wrow1 : wrow0;
-      const int jr = w < nown ? r0 + w : 0;
-      const double* mr = MS + (s * SBK + jr) * (int64_t)SBK;
-#pragma unroll
-      for (int t = 0; t < 8; t++) mrow[h][t] = (w < nown) ? mr[lane + 64 * t] : 0.0;
-    }
-    if (wave == 0 && lane < nown) {
-      const int64_t jm = j0 + r0 + lane;
-      alv = alpha[jm];
-      gav = gamma[jm];
-      const int64_t jc = jm < p ? jm : 0;
-      const double b0v = b[jc], b1v = b[p + jc];
-      bbo = bbar[jc];
-      bo = it_odd ? b1v : b0v;
-    }
-    // (2) d⁰ of the owned rows: waves 0-2, lane -> chunks lane + 64 w and + 192, summed in that
-    // order, xor-tree across the wave, then the waves in order
-    if (wave < 3) {
-      double v[SB_RMAX];
-#pragma unroll
-      for (int r = 0; r < SB_RMAX; r++) v[r] = 0.0;
-      if (nown > 0) {
-#pragma unroll
-        for (int h = 0; h < 2; h++) {
-          const int cc = lane + 64 * wave + 192 * h;
-          const bool has = cc < C;
-          const uint32_t base = (uint32_t)((((int64_t)par * C + (has ? cc : 0)) * SBK + r0) * 16);
-          bool failed = false;
-          int64_t spin = 0;
-          bool done = !has;
-          double x[SB_RMAX];
-#pragma unroll
-          for (int r = 0; r < SB_RMAX; r++) x[r] = 0.0;
-          do {
-            if (!done) {
-              sbu4 w[SB_RMAX];
-#pragma unroll
-              for (int r = 0; r < SB_RMAX; r++)
-                if (r < R) w[r] = sb_get(rP, base + r * 16);
-              sb_landed();
-              bool all = true;
-#pragma unroll
-              for (int r = 0; r < SB_RMAX; r++)
-                if (r < R && r < nown) all = sb_ok(w[r], key, x[r]) && all;
-              done = all;
-            }
-          } while (sb_spin(done, spin, info, failed));
-          if (failed) s_fail = 1;
-#pragma unroll
-          for (int r = 0; r < SB_RMAX; r++) v[r] += (has && r < nown) ? x[r] : 0.0;
-        }
-      }
-#pragma unroll
-      for (int r = 0; r < SB_RMAX; r++) {
-        double x = v[r];
-        x += __shfl_xor(x, 32);
-        x += __shfl_xor(x, 16);
-        x += __shfl_xor(x, 8);
-        x += __shfl_xor(x, 4);
-        x += __shfl_xor(x, 2);
-        x += __shfl_xor(x, 1);
-        if (lane == 0) red[wave][r] = x;
-      }
-    }
-    lds_barrier();
-    mark(s, 2);
-    if (s_fail) return;
-    if (wave == 0 && lane < nown) {
-      const double d0 = (red[0][lane] + red[1][lane]) + red[2][lane];
-      sb_put(rR, (uint32_t)(((int64_t)par * SBK + r0 + lane) * 16), fma(d0, -alv, gav), key);
-    }
-    mark(s, 3);
-    // (3) all of r̃ (waves 0-1, 4 granules per lane), then δ of the owned rows (wave w: rows w, w + 4)
-    if (wave < 2) {
-      bool failed = false, done = false;
-      int64_t spin = 0;
-      double x[4];
-      do {
-        sbu4 w[4];
-#pragma unroll
-        for (int q = 0; q < 4; q++) w[q] = sb_get(rR, (uint32_t)(((int64_t)par * SBK + tid * 4 + q) * 16));
-        sb_landed();
-        bool all = true;
-#pragma unroll
-        for (int q = 0; q < 4; q++) all = sb_ok(w[q], key, x[q]) && all;
-        done = all;
-      } while (sb_spin(done, spin, info, failed));
-      if (failed) s_fail = 1;
-#pragma unroll
-      for (int q = 0; q < 4; q++) rt[tid * 4 + q] = x[q];
-    }
-    lds_barrier();
-    mark(s, 4);
-    if (s_fail) return;
-#pragma unroll
-    for (int h = 0; h < 2; h++) {
-      const int w = h ? wrow1 : wrow0;
-      double a = 0.0;
-#pragma unroll
-      for (int t = 0; t < 8; t++) a = fma(mrow[h][t], rt[lane + 64 * t], a);
-      a += __shfl_xor(a, 32);
-      a += __shfl_xor(a, 16);
-      a += __shfl_xor(a, 8);
-      a += __shfl_xor(a, 4);
-      a += __shfl_xor(a, 2);
-      a += __shfl_xor(a, 1);
-      if (lane == 0 && w < nown) red[3][w] = a;
-    }
-    lds_barrier();
-    if (wave == 0 && lane < nown) {
-      const double dlt = red[3][lane];
-      const int64_t jm = j0 + r0 + lane;
-      if (jm < p) {
-        const double bn = bo - dlt;
-        b[(it_odd ^ 1) * p + jm] = bn;
-        if (accum) bbar[jm] = bbo * ((kk - 1.0) / kk) + bn / kk;
-      }
-      sb_put(rD, (uint32_t)(((int64_t)par * SBK + r0 + lane) * 16), dlt, key);
-    }
-    mark(s, 5);
-    // (4) all of δ, then e += X_S δ over the chunk's individuals (rows from Drow[par]): thread ->
-    // one 16-individual piece of a slice of rows, partial sums by slice in LDS, summed in slice order
-    if (wave < 2) {
-      bool failed = false, done = false;
-      int64_t spin = 0;
-      double x[4];
-      do {
-        sbu4 w[4];
-#pragma unroll
-        for (int q = 0; q < 4; q++) w[q] = sb_get(rD, (uint32_t)(((int64_t)par * SBK + tid * 4 + q) * 16));
-        sb_landed();
-        bool all = true;
-#pragma unroll
-        for (int q = 0; q < 4; q++) all = sb_ok(w[q], key, x[q]) && all;
-        done = all;
-      } while (sb_spin(done, spin, info, failed));
-      if (failed) s_fail = 1;
-#pragma unroll
-      for (int q = 0; q < 4; q++) dl[tid * 4 + q] = x[q];
-    }
-    lds_barrier();
-    mark(s, 6);
-    if (s_fail) return;
-    if (esl < nsl_used) {
-      double acc[16];
-#pragma unroll
-      for (int u = 0; u < 16; u++) acc[u] = 0.0;
-      const int jb = esl * rps, je = (jb + rps < SBK) ? jb + rps : SBK;
-      for (int jj = jb; jj < je; jj++) {
-        const uint4 w4 = *reinterpret_cast<const uint4*>(Dr + jj * K + ech * 16);
-        const double d = dl[jj];
-        const uint32_t wd[4] = {w4.x, w4.y, w4.z, w4.w};
-#pragma unroll
-        for (int q = 0; q < 4; q++)
-#pragma unroll
-          for (int bb = 0; bb < 4; bb++) acc[4 * q + bb] = fma((double)((wd[q] >> (8 * bb)) & 0xFFu), d, acc[4 * q + bb]);
-      }
-#pragma unroll
-      for (int u = 0; u < 16; u++) eacc[(ech * 16 + u) * slp + esl] = acc[u];  // [individual][slice]
-    }
-    mark(s, 8);
-    // the next super-block's rows have landed (wave 3's DMA) before the barrier; an LDS-only barrier
-    // otherwise (__syncthreads would also wait for this super-block's write-through stores)
-    if (wave == 3) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    lds_barrier();
-    mark(s, 9);
-    if (tid < 4 * K) {
-      const int ind = tid % K, q = tid / K;  // four partial sums per individual, slices ≡ q (mod 4)
-      double u = 0.0;
-      for (int t = q; t < nsl_used; t += 4) u += eacc[ind * slp + t];
-      eq[q][ind] = u;
-    }
-    lds_barrier();
-    mark(s, 10);
-    if (tid < K && i0 + tid < n) es[tid] += (((eq[0][tid] + eq[1][tid]) + eq[2][tid]) + eq[3][tid]) * xs;
-    lds_barrier();
-    mark(s, 7);
-  }
-  if (tid < K && i0 + tid < n) e[i0 + tid] = es[tid];
-}
-
 // ---- byte storage: look-ahead super-block sweep (round 3) -----------------------------------------
-// brr_sweep_sb_kernel runs three hand-offs per super-block in a row: partial dots -> owners, r̃ ->
-// everyone, δ -> everyone, with the e update and the next dots between them. Here the dots leave
-// the chain: with e⁽ˢ⁾ the residual after super-block s,
+// A plain super-block sweep would run three hand-offs per super-block in a row: partial dots ->
+// owners, r̃ -> everyone, δ -> everyone, with the e update and the next dots between them. Here the
+// dots leave the chain: with e⁽ˢ⁾ the residual after super-block s,
 //   d⁰_s = X_sᵀ e⁽ˢ⁻¹⁾ = X_sᵀ e⁽ˢ⁻²⁾ + X_sᵀ X_{s−1} δ_{s−1} = Q_s + C_s δ_{s−1},
 // so Q_s (partial dots over chunks of individuals, summed by the row owners) is computed from the
 // residual one super-block earlier, and only the 512 x 512 cross-Gram C_s = X_sᵀ X_{s−1} (one-time
@@ -1620,7 +1073,7 @@ __global__ void __launch_bounds__(256) brr_sweep_sb_kernel(const uint8_t* __rest
 // A chunk's rows of super-blocks s − 1 .. s + 2 are in LDS (four buffers; s + 2 lands by DMA during
 // step s). Granule slots rotate over four super-blocks (a slot is rewritten only after every
 // reader of its previous tag has passed a later hand-off). Same chain as the literal loop, rounding
-// aside; waits bounded as in brr_sweep_sb_kernel.
+// aside; waits bounded (sb_spin: ~1 s, then *info = −1 and every workgroup leaves).
 constexpr int LA_KMAX = 48;  // individuals per chunk (at most)
 
 // C_s = X_sᵀ X_{s−dist} for s = dist .. nsb − 1 (row-major 512 x 512 at CS + s·512²; rows of markers past
@@ -1696,342 +1149,6 @@ __global__ void __launch_bounds__(256, 2) brr_xgram_kernel(const double* __restr
 #pragma unroll
       for (int r = 0; r < 4; r++)
         out[(int64_t)(wm * 64 + mm * 16 + fr + 4 * r) * SBK + wn * 64 + q * 16 + fc] = acc[mm][q][r];
-}
-
-// K individuals per chunk workgroup (a multiple of 16, <= LA_KMAX); R owned rows (<= SB_RMAX).
-// kTrace: workgroups 0 and C − 1 record 5 timestamps per super-block (ends of A, B, C, D).
-template <bool kTrace>
-__global__ void __launch_bounds__(256) brr_sweep_la_kernel(const uint8_t* __restrict__ D, int64_t ldx, int64_t n,
-                                                           int64_t p, double xs, const double* __restrict__ MS,
-                                                           const double* __restrict__ CS, int64_t nsb, int K, int R,
-                                                           double* __restrict__ Pb, double* __restrict__ Rt,
-                                                           double* __restrict__ Dl, int32_t* __restrict__ info,
-                                                           double* __restrict__ b, double* __restrict__ bbar,
-                                                           const double* __restrict__ alpha,
-                                                           const double* __restrict__ gamma, double* __restrict__ e,
-                                                           const BrrState* __restrict__ st, int64_t* __restrict__ trace) {
-  __shared__ __attribute__((aligned(16))) uint8_t Drow[4][SBK * LA_KMAX];
-  __shared__ __attribute__((aligned(16))) double es[LA_KMAX];
-  __shared__ __attribute__((aligned(16))) double rt[SBK];
-  __shared__ __attribute__((aligned(16))) double dl[SBK];
-  __shared__ double red[4][SB_RMAX];
-  __shared__ double cd[1][SB_RMAX];
-  __shared__ double eacc[4160];  // e update partial sums [individual][slice]: K x (nsl_used | 1) <= 32 x 129
-  __shared__ double eq[4][LA_KMAX];
-  __shared__ int s_fail;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int C = (int)gridDim.x, c = (int)blockIdx.x;
-  const int64_t i0 = (int64_t)c * K;
-  const int r0 = c * R;
-  const int nown = r0 >= SBK ? 0 : (SBK - r0 < R ? SBK - r0 : R);
-  const bool tr_on = kTrace && threadIdx.x == 0;
-  int64_t* trw = kTrace ? trace + (int64_t)c * nsb * 8 : nullptr;  // every workgroup: 8 per super-block
-  auto mark = [&](int64_t s, int k) {
-    if (tr_on) trw[s * 8 + k] = (int64_t)__builtin_amdgcn_s_memrealtime();
-  };
-  const int it_odd = (int)(st->it & 1);
-  const bool accum = brr_accumulate(st);
-  const double kk = (double)(st->nsum + 1);
-  const uint64_t tag0 = (st->epoch << 40) + (uint64_t)st->it * (uint64_t)nsb;
-  const __amdgpu_buffer_rsrc_t rP = brr_rsrc(Pb, (int64_t)4 * C * SBK * 16);
-  const __amdgpu_buffer_rsrc_t rR = brr_rsrc(Rt, (int64_t)4 * SBK * 16);
-  const __amdgpu_buffer_rsrc_t rD = brr_rsrc(Dl, (int64_t)4 * SBK * 16);
-  if (tid == 0) s_fail = 0;
-  const int kpc = K / 16, kinv = (65536 + kpc - 1) / kpc;  // q / kpc = (q · kinv) >> 16 for q < 2^14
-  auto dma_rows = [&](int64_t sb) {  // wave 3: the chunk's rows of super-block sb -> Drow[sb & 3]
-    const int pieces = SBK * kpc;
-    uint8_t* dst = Drow[sb & 3];
-    for (int q0 = 0; q0 < pieces; q0 += 64) {
-      const int q = q0 + lane;
-      const int row = (q * kinv) >> 16, part = q - row * kpc;
-      int64_t jr = sb * SBK + row;
-      jr = jr < p ? jr : p - 1;
-      const uint8_t* src = D + jr * ldx + i0 + part * 16;
-      const unsigned m0v = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(dst + q0 * 16));
-      asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off" : : "s"(m0v), "v"(src) : "memory");
-    }
-  };
-  // partial dots of super-block sb over this chunk from es (thread t: rows 2t, 2t + 1) -> P granules
-  auto dots_publish = [&](int64_t sb) {
-    const uint8_t* Dr = Drow[sb & 3];
-    double a0 = 0.0, a1 = 0.0, c0 = 0.0, c1 = 0.0;
-    const uint8_t* ra = Dr + (2 * tid) * K;
-    const uint8_t* rb = ra + K;
-    for (int u = 0; u < K; u += 16) {
-      const uint4 va = *reinterpret_cast<const uint4*>(ra + u);
-      const uint4 vb = *reinterpret_cast<const uint4*>(rb + u);
-      const uint32_t wa[4] = {va.x, va.y, va.z, va.w};
-      const uint32_t wb[4] = {vb.x, vb.y, vb.z, vb.w};
-#pragma unroll
-      for (int q = 0; q < 4; q++)
-#pragma unroll
-        for (int bb = 0; bb < 4; bb += 2) {
-          const double2 e2 = *reinterpret_cast<const double2*>(es + u + 4 * q + bb);
-          a0 = fma((double)((wa[q] >> (8 * bb)) & 0xFFu), e2.x, a0);
-          a1 = fma((double)((wa[q] >> (8 * bb + 8)) & 0xFFu), e2.y, a1);
-          c0 = fma((double)((wb[q] >> (8 * bb)) & 0xFFu), e2.x, c0);
-          c1 = fma((double)((wb[q] >> (8 * bb + 8)) & 0xFFu), e2.y, c1);
-        }
-    }
-    const uint64_t key = sb_key(tag0 + (uint64_t)sb);
-    const uint32_t off = (uint32_t)((((int64_t)(sb & 3) * C + c) * SBK + 2 * tid) * 16);
-    sb_put(rP, off, a0 * xs + a1 * xs, key);
-    sb_put(rP, off + 16, c0 * xs + c1 * xs, key);
-  };
-  // all 512 granules of super-block sb from buffer r into LDS out (waves 0-1, four per lane); the
-  // pause between polls grows (up to ~0.2 µs) the longer the wait: 209 workgroups polling one 8 KB
-  // block is what the hop pays. (Every lane re-reads all four granules: an asm load under a
-  // divergent branch lets the compiler copy its register before the data lands.)
-  auto gather512 = [&](__amdgpu_buffer_rsrc_t r, int64_t sb, double* out) {
-    if (wave < 2) {
-      const uint64_t key = sb_key(tag0 + (uint64_t)sb);
-      bool failed = false;
-      int64_t spin = 0;
-      double x[4] = {0.0, 0.0, 0.0, 0.0};
-      for (;;) {
-        sbu4 w[4];
-#pragma unroll
-        for (int q = 0; q < 4; q++) w[q] = sb_get(r, (uint32_t)(((int64_t)(sb & 3) * SBK + tid * 4 + q) * 16));
-        sb_landed();
-        bool all = true;
-#pragma unroll
-        for (int q = 0; q < 4; q++) all = sb_ok(w[q], key, x[q]) && all;
-        if (!sb_spin(all, spin, info, failed)) break;
-        for (int64_t z = spin >> 3; z > 0 && z < 8; z--) __builtin_amdgcn_s_sleep(1);
-        if (spin >= 64) {
-#pragma unroll
-          for (int z = 0; z < 7; z++) __builtin_amdgcn_s_sleep(1);
-        }
-      }
-      if (failed) s_fail = 1;
-#pragma unroll
-      for (int q = 0; q < 4; q++) out[tid * 4 + q] = x[q];
-    }
-  };
-  // e update: thread t -> 16-individual piece t % nch of slice t / nch (rows [sl·rps, (sl+1)·rps))
-  const int nch = K / 16, nsl = 256 / nch, rps = (SBK + nsl - 1) / nsl;
-  const int ech = tid % nch, esl = tid / nch;
-  const int nsl_used = (SBK + rps - 1) / rps;
-  const int slp = nsl_used | 1;
-  // e += X_sb δ (δ in dl) over the chunk, rows from Drow[sb & 3]; ends with a barrier
-  auto e_update = [&](int64_t sb, auto&& between) {
-    const uint8_t* Dr = Drow[sb & 3];
-    if (esl < nsl_used) {
-      double acc[16];
-#pragma unroll
-      for (int u = 0; u < 16; u++) acc[u] = 0.0;
-      const int jb = esl * rps, je = (jb + rps < SBK) ? jb + rps : SBK;
-      for (int jj = jb; jj < je; jj++) {
-        const uint4 w4 = *reinterpret_cast<const uint4*>(Dr + jj * K + ech * 16);
-        const double d = dl[jj];
-        const uint32_t wd[4] = {w4.x, w4.y, w4.z, w4.w};
-#pragma unroll
-        for (int q = 0; q < 4; q++)
-#pragma unroll
-          for (int bb = 0; bb < 4; bb++) acc[4 * q + bb] = fma((double)((wd[q] >> (8 * bb)) & 0xFFu), d, acc[4 * q + bb]);
-      }
-#pragma unroll
-      for (int u = 0; u < 16; u++) eacc[(ech * 16 + u) * slp + esl] = acc[u];
-    }
-    lds_barrier();
-    between();  // runs beside the reduction (tid >= 4 K: wave 3 when K <= 48)
-    if (tid < 4 * K) {
-      const int ind = tid % K, q = tid / K;
-      double u = 0.0;
-      for (int t = q; t < nsl_used; t += 4) u += eacc[ind * slp + t];
-      eq[q][ind] = u;
-    }
-    lds_barrier();
-    if (tid < K && i0 + tid < n) es[tid] += (((eq[0][tid] + eq[1][tid]) + eq[2][tid]) + eq[3][tid]) * xs;
-    lds_barrier();
-  };
-
-  if (tid < LA_KMAX) es[tid] = (tid < K && i0 + tid < n) ? e[i0 + tid] : 0.0;
-  if (wave == 3) {
-    dma_rows(0);
-    if (nsb > 1) dma_rows(1);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-  __syncthreads();
-  dots_publish(0);  // Q_0 = X_0ᵀ e
-  // owners: their rows of Q_sb summed over all chunks (waves 0-2, lane -> chunks lane + 64 w and
-  // + 192, summed in that order, xor-tree; red[w][r], the waves summed in order by the reader)
-  auto gather_q = [&](int64_t sb) {
-    if (nown > 0 && wave < 3) {
-      const uint64_t key = sb_key(tag0 + (uint64_t)sb);
-      double v[SB_RMAX];
-#pragma unroll
-      for (int r = 0; r < SB_RMAX; r++) v[r] = 0.0;
-#pragma unroll
-      for (int h = 0; h < 2; h++) {
-        const int cc = lane + 64 * wave + 192 * h;
-        const bool has = cc < C;
-        const uint32_t base = (uint32_t)((((int64_t)(sb & 3) * C + (has ? cc : 0)) * SBK + r0) * 16);
-        bool failed = false, done = !has;
-        int64_t spin = 0;
-        double x[SB_RMAX];
-#pragma unroll
-        for (int r = 0; r < SB_RMAX; r++) x[r] = 0.0;
-        do {
-          if (!done) {
-            sbu4 w[SB_RMAX];
-#pragma unroll
-            for (int r = 0; r < SB_RMAX; r++)
-              if (r < R) w[r] = sb_get(rP, base + r * 16);
-            sb_landed();
-            bool all = true;
-#pragma unroll
-            for (int r = 0; r < SB_RMAX; r++)
-              if (r < R && r < nown) all = sb_ok(w[r], key, x[r]) && all;
-            done = all;
-          }
-        } while (sb_spin(done, spin, info, failed));
-        if (failed) s_fail = 1;
-#pragma unroll
-        for (int r = 0; r < SB_RMAX; r++) v[r] += (has && r < nown) ? x[r] : 0.0;
-      }
-#pragma unroll
-      for (int r = 0; r < SB_RMAX; r++) {
-        double x = v[r];
-        x += __shfl_xor(x, 32);
-        x += __shfl_xor(x, 16);
-        x += __shfl_xor(x, 8);
-        x += __shfl_xor(x, 4);
-        x += __shfl_xor(x, 2);
-        x += __shfl_xor(x, 1);
-        if (lane == 0) red[wave][r] = x;
-      }
-    }
-  };
-  gather_q(0);
-  const int wrow0 = wave, wrow1 = wave + 4;  // owned-row indices of this wave's GEMV rows
-  for (int64_t s = 0; s < nsb; s++) {
-    const int64_t j0 = s * SBK;
-    const uint64_t key = sb_key(tag0 + (uint64_t)s);
-    // operands of the owned rows (plain loads: written before this launch): C_s's rows now (for
-    // (B)); M_s's rows once the δ gather is done (for (D)), so that gather queues behind 16 KB of
-    // loads in the CU's memory pipeline instead of 32 KB
-    double mrow[2][8], crow[2][8];
-#pragma unroll
-    for (int h = 0; h < 2; h++) {
-      const int w = h ? wrow1 : wrow0;
-      const int jr = w < nown ? r0 + w : 0;
-      const double* cr = CS + (s * SBK + jr) * (int64_t)SBK;
-#pragma unroll
-      for (int t = 0; t < 8; t++) crow[h][t] = (w < nown && s > 0) ? cr[lane + 64 * t] : 0.0;
-    }
-    double alv = 0.0, gav = 0.0, bo = 0.0, bbo = 0.0;
-    if (wave == 0 && lane < nown) {
-      const int64_t jm = j0 + r0 + lane;
-      alv = alpha[jm];
-      gav = gamma[jm];
-      const int64_t jc = jm < p ? jm : 0;
-      const double b0v = b[jc], b1v = b[p + jc];
-      bbo = bbar[jc];
-      bo = it_odd ? b1v : b0v;
-    }
-    // (A) δ_{s−1} -> dl (every workgroup; the owners' Q_s rows were gathered at the end of step s − 1)
-    if (s > 0) gather512(rD, s - 1, dl);
-#pragma unroll
-    for (int h = 0; h < 2; h++) {
-      const int w = h ? wrow1 : wrow0;
-      const int jr = w < nown ? r0 + w : 0;
-      const double* mr = MS + (s * SBK + jr) * (int64_t)SBK;
-#pragma unroll
-      for (int t = 0; t < 8; t++) mrow[h][t] = (w < nown) ? mr[lane + 64 * t] : 0.0;
-    }
-    lds_barrier();
-    mark(s, 0);
-    if (s_fail) return;
-    // (B) owners: C_s δ_{s−1} on their rows (wave w: rows w, w + 4), then r̃_s published
-    if (nown > 0) {
-#pragma unroll
-      for (int h = 0; h < 2; h++) {
-        const int w = h ? wrow1 : wrow0;
-        double a = 0.0;
-        if (s > 0) {
-#pragma unroll
-          for (int t = 0; t < 8; t++) a = fma(crow[h][t], dl[lane + 64 * t], a);
-        }
-        a += __shfl_xor(a, 32);
-        a += __shfl_xor(a, 16);
-        a += __shfl_xor(a, 8);
-        a += __shfl_xor(a, 4);
-        a += __shfl_xor(a, 2);
-        a += __shfl_xor(a, 1);
-        if (lane == 0 && w < nown) cd[0][w] = a;
-      }
-    }
-    if (nown > 0) {
-      lds_barrier();
-      if (wave == 0 && lane < nown) {
-        const double d0 = ((red[0][lane] + red[1][lane]) + red[2][lane]) + cd[0][lane];
-        sb_put(rR, (uint32_t)(((int64_t)(s & 3) * SBK + r0 + lane) * 16), fma(d0, -alv, gav), key);
-      }
-    }
-    mark(s, 1);
-    // (C) e += X_{s−1} δ_{s−1}, then the partial dots of Q_{s+1}. Wave 3, idle in the e update's
-    // reduction: super-block s + 1's rows (DMA of step s − 1) have landed, and s + 2's go into the
-    // buffer that held s − 2's (last read by step s − 1's e update) while no gather of this
-    // workgroup runs (a gather queued behind the CU's own DMA burst is slower); waited for in step
-    // s + 1, before the dots read them
-    auto dma_next = [&]() {
-      if (wave == 3) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (s + 2 < nsb) dma_rows(s + 2);
-      }
-    };
-    if (s > 0) {
-      e_update(s - 1, dma_next);
-    } else {
-      dma_next();
-      lds_barrier();
-    }
-    mark(s, 5);
-    if (s + 1 < nsb) dots_publish(s + 1);
-    mark(s, 2);
-    // (D) owners: all of r̃_s, δ_s = M_s r̃_s on their rows, b and b̄, δ_s published; then their rows
-    // of Q_{s+1} (published in (C) by every workgroup) while δ_s travels
-    if (nown > 0) {
-      gather512(rR, s, rt);
-      lds_barrier();
-      if (s_fail) return;
-#pragma unroll
-      for (int h = 0; h < 2; h++) {
-        const int w = h ? wrow1 : wrow0;
-        double a = 0.0;
-#pragma unroll
-        for (int t = 0; t < 8; t++) a = fma(mrow[h][t], rt[lane + 64 * t], a);
-        a += __shfl_xor(a, 32);
-        a += __shfl_xor(a, 16);
-        a += __shfl_xor(a, 8);
-        a += __shfl_xor(a, 4);
-        a += __shfl_xor(a, 2);
-        a += __shfl_xor(a, 1);
-        if (lane == 0 && w < nown) red[3][w] = a;
-      }
-      lds_barrier();
-      if (wave == 0 && lane < nown) {
-        const double dlt = red[3][lane];
-        const int64_t jm = j0 + r0 + lane;
-        if (jm < p) {
-          const double bn = bo - dlt;
-          b[(it_odd ^ 1) * p + jm] = bn;
-          if (accum) bbar[jm] = bbo * ((kk - 1.0) / kk) + bn / kk;
-        }
-        sb_put(rD, (uint32_t)(((int64_t)(s & 3) * SBK + r0 + lane) * 16), dlt, key);
-      }
-      mark(s, 4);
-      if (s + 1 < nsb) gather_q(s + 1);
-    }
-    mark(s, 3);
-  }
-  // the last super-block's δ, and its e update
-  gather512(rD, nsb - 1, dl);
-  lds_barrier();
-  if (s_fail) return;
-  e_update(nsb - 1, [] {});
-  if (tid < K && i0 + tid < n) e[i0 + tid] = es[tid];
 }
 
 // Two super-blocks of slack for the partial dots (the default look-ahead form): with the second
@@ -2486,10 +1603,10 @@ namespace {
 struct BrrCtx {
   int dev = 0;
   Stream stream;
-  DevBuf Xt, colmean, x2, e, b, bbar, r, stm, D, badm, W, Mb, alph, gamm, flg, Dt, pb, part, pout;
+  DevBuf Xt, colmean, x2, e, b, bbar, r, stm, D, badm, W, Mb, alph, gamm, Dt, pb, part, pout;
   DevBuf Wsb, MS, Ssc, Pb, Rt, Dl, sbcnt;  // the super-block sweep
-  DevBuf CS;                               // its look-ahead form: cross-Grams C_s = X_sᵀ X_{s−1}
-  DevBuf CS2;                              // and (two-step slack) C2_s = X_sᵀ X_{s−2}
+  DevBuf CS, CS2;                          // its cross-Grams C_s = X_sᵀ X_{s−1}, C2_s = X_sᵀ X_{s−2}
+  DevBuf trace;                            // GBM_BRR_TRACE timestamps of this context's last sweep
   hipGraphExec_t exec = nullptr;
   hipGraph_t graph = nullptr;
   std::vector<int64_t> key;  // what the captured graph was built for
@@ -2540,6 +1657,16 @@ class BrrPool {
     std::lock_guard<std::mutex> lock(mu_);
     drop.swap(idle_);
   }
+  // drops the idle contexts of one device (buffers and graphs freed outside the lock); returns how many
+  int64_t trim(int dev) {
+    std::vector<std::unique_ptr<BrrCtx>> drop;
+    {
+      std::lock_guard<std::mutex> lock(mu_);
+      auto it = idle_.find(dev);
+      if (it != idle_.end()) drop.swap(it->second);
+    }
+    return (int64_t)drop.size();
+  }
   // the persistent sweep needs all its workgroups resident at once: sweeps of concurrent fits on one
   // device take turns (held for a whole fit), so two of them can never be partly resident and spin
   // on each other
@@ -2557,7 +1684,13 @@ class BrrPool {
 };
 
 BrrPool& brr_pool() {
-  static BrrPool* p = new BrrPool;  // never destroyed (device memory outlives the runtime otherwise)
+  static BrrPool* p = [] {
+    auto* bp = new BrrPool;  // never destroyed (device memory outlives the runtime otherwise)
+    // an allocation (of any entry point) that runs out of device memory also frees the idle BRR
+    // contexts of its device before its retry (host_util.h dalloc)
+    register_trim_hook([](int dev) { return brr_pool().trim(dev); });
+    return bp;
+  }();
   return *p;
 }
 
@@ -2575,24 +1708,24 @@ namespace gbm {
 void brr_release_cache() { brr_pool().clear(); }
 }  // namespace gbm
 
-// Timing tool (GBM_BRR_TRACE=1): per super-block timestamps of workgroups 0 and C − 1 of the last
-// super-block sweep (brr_sweep_sb_kernel: 2 x nsb x 12 int64; brr_sweep_la_kernel: every workgroup,
-// C x nsb x 8; s_memrealtime at 100 MHz), read by gbm_debug_brr_trace.
-static int64_t* g_brr_trace = nullptr;
-static int64_t g_brr_trace_n = 0;
+// Timing tool (GBM_BRR_TRACE=1): per super-block timestamps of every workgroup of a traced fit's
+// sweep (C x nsb x 8 int64, s_memrealtime at 100 MHz), recorded into the leasing context's own
+// buffer and copied to the host when that fit completes; gbm_debug_brr_trace reads the copy of the
+// last traced fit (no device buffer is shared between concurrent fits).
+static std::mutex g_brr_trace_mu;
+static std::vector<int64_t> g_brr_trace_host;
 
 extern "C" int64_t gbm_debug_brr_trace(int64_t* host, int64_t cap) {
-  if (!g_brr_trace || !host) return 0;
-  const int64_t n = g_brr_trace_n < cap ? g_brr_trace_n : cap;
-  if (hipDeviceSynchronize() != hipSuccess ||
-      hipMemcpy(host, g_brr_trace, (size_t)n * 8, hipMemcpyDeviceToHost) != hipSuccess)
-    return -1;
+  std::lock_guard<std::mutex> lock(g_brr_trace_mu);
+  if (!host || g_brr_trace_host.empty()) return 0;
+  const int64_t n = std::min<int64_t>((int64_t)g_brr_trace_host.size(), cap);
+  std::copy(g_brr_trace_host.begin(), g_brr_trace_host.begin() + n, host);
   return n;
 }
 
-// Which path the last completed fit took (0 per-launch, 1 128-block sweep, 2 super-block sweep, 3 its
-// look-ahead form) and
-// how many fits fell back to the per-launch path after a sweep hand-off timed out (tests).
+// Which schedule the last completed fit took (0 per-launch, 4 the super-block sweep; 1-3 were the
+// earlier sweeps of rounds 2-3, no longer built) and how many fits fell back to the per-launch path
+// after a sweep hand-off timed out (tests).
 static std::atomic<int> g_brr_last_path{-1};
 static std::atomic<int64_t> g_brr_fallbacks{0};
 extern "C" int gbm_debug_brr_stats(int* last_path, int64_t* fallbacks) {
@@ -2666,39 +1799,25 @@ static int brr_fit_impl(const double* X, int64_t n, int64_t p, int64_t ldx, cons
       }
     }
   }
-  // byte storage on (up to) every CU: the super-block sweep (brr_sweep_sb_kernel) when its chunk
-  // workgroups (K <= 64 individuals each) can all be resident, one per CU, and own <= 8 rows of a
-  // super-block each (1 024 <= n <= 64 CUs); GBM_BRR_SB=0 (read per call) keeps the 128-block sweep
+  // byte storage on (up to) every CU: the super-block sweep (brr_sweep_la2_kernel) when its chunk
+  // workgroups (K <= LA_KMAX individuals each: n <= 48 x CUs) can all be resident, one per CU, and own
+  // <= SB_RMAX rows of a super-block each; GBM_BRR_SWEEP=0 (read per call) keeps the per-launch path
   int cus = 0;
   GBM_HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-  bool sbmode = false, lamode = false, la2mode = false;
+  bool sweep = false;
   int sbK = 0, sbC = 0, sbR = 0;
   int la2Ko = 0, la2Kn = 0, la2R = 0, la2O = 0, la2C = 0;
   if (xs > 0.0 && sweep_mode != 0) {
-    const char* ev = std::getenv("GBM_BRR_SB");
-    const char* ev2 = std::getenv("GBM_BRR_SWEEP");
+    const char* ev = std::getenv("GBM_BRR_SWEEP");
     int per_cu = 0;
-    GBM_HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, brr_sweep_sb_kernel<false>, 256, 0));
+    GBM_HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, brr_sweep_la2_kernel<false>, 256, 0));
     sbK = (int)round_up(std::max<int64_t>(16, (n + cus - 1) / cus), 16);
     if (const char* ek = std::getenv("GBM_BRR_SB_K"))  // (timing experiments) a larger chunk
       sbK = std::max<int>(sbK, (int)round_up(std::max<int64_t>(16, atoll(ek)), 16));
     sbC = (int)((n + sbK - 1) / sbK);
     sbR = (int)round_up((SBK + sbC - 1) / sbC, 2);
-    sbmode = !(ev && ev[0] == '0') && !(ev2 && ev2[0] == '0') && per_cu >= 1 && sbK <= SB_KMAX && sbC <= cus &&
-             sbR <= SB_RMAX;
-    // the look-ahead form (brr_sweep_la_kernel) when a chunk is <= LA_KMAX individuals (n <= 48 x CUs);
-    // GBM_BRR_LA=0 (read per call) keeps brr_sweep_sb_kernel
-    const char* ev3 = std::getenv("GBM_BRR_LA");
-    int per_cu_la = 0;
-    GBM_HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu_la, brr_sweep_la_kernel<false>, 256, 0));
-    lamode = sbmode && !(ev3 && ev3[0] == '0') && per_cu_la >= 1 && sbK <= LA_KMAX;
-    // its two-step-slack form (brr_sweep_la2_kernel) by default; GBM_BRR_LA2=0 (read per call) keeps
-    // the one-step form
-    const char* ev4 = std::getenv("GBM_BRR_LA2");
-    int per_cu_la2 = 0;
-    GBM_HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu_la2, brr_sweep_la2_kernel<false>, 256, 0));
-    la2mode = lamode && !(ev4 && ev4[0] == '0') && per_cu_la2 >= 1 && sbC <= 256;
-    // its chunk split: O = 512 / R owners of Ko individuals, the rest Kn (both <= LA_KMAX), all on
+    sweep = !(ev && ev[0] == '0') && per_cu >= 1 && sbK <= LA_KMAX && sbC <= std::min(cus, 256) && sbR <= SB_RMAX;
+    // the chunk split: O = 512 / R owners of Ko individuals, the rest Kn (both <= LA_KMAX), all on
     // <= min(CUs, 256) workgroups; the owners get the smallest Ko that fits. Off unless GBM_BRR_OWN_R=
     // 2|4|6|8 (read per call) sets R: at C4 the extra workgroups' polls cost the hops more than the
     // owners' lighter chunks save (2.58 ms at R = 4, 3.32 at R = 8, vs 2.41 uniform). Uniform
@@ -2708,7 +1827,7 @@ static int brr_fit_impl(const double* X, int64_t n, int64_t p, int64_t ldx, cons
     la2R = sbR;
     la2O = (SBK + sbR - 1) / sbR;
     la2C = sbC;
-    if (la2mode) {
+    if (sweep) {
       int R2 = 0;
       if (const char* er = std::getenv("GBM_BRR_OWN_R")) R2 = std::max(2, std::min<int>(SB_RMAX, atoi(er) & ~1));
       const int O2 = R2 > 0 ? (SBK + R2 - 1) / R2 : 0;
@@ -2733,7 +1852,7 @@ static int brr_fit_impl(const double* X, int64_t n, int64_t p, int64_t ldx, cons
   // super-block sweep rounds the 128-blocks up to whole super-blocks (α = γ = 0 past p).
   const int64_t bk = xs > 0.0 ? BK2 : BB;
   const int64_t nsb = (p + SBK - 1) / SBK;
-  const int64_t nblk = sbmode ? nsb * SBN : (p + bk - 1) / bk;
+  const int64_t nblk = sweep ? nsb * SBN : (p + bk - 1) / bk;
   const int nw = xs > 0.0 ? 3 : 1;
   GBM_TRY(ensure(cx.W, dev, nblk * nw * BB * BB * 8));
   // per-iteration block inverses (same shape as W) and step constants α, γ (padded to whole launches)
@@ -2742,32 +1861,26 @@ static int brr_fit_impl(const double* X, int64_t n, int64_t p, int64_t ldx, cons
   GBM_TRY(ensure(cx.gamm, dev, nblk * bk * 8));
   brr_gram_kernel<<<(unsigned)(nblk * nw), 256, 0, s>>>((const double*)cx.Xt.p, npad, p, n, nw, (double*)cx.W.p);
   GBM_LAUNCH_CHECK();
-  // byte storage: one persistent sweep launch per iteration when the C chunk workgroups can all be
-  // resident at once (the occupancy query times the CU count; one sweep per device at a time, see
-  // BrrPool::sweep_lock); GBM_BRR_SWEEP=0 keeps one launch per block (read per call)
-  bool sweep = sbmode;
-  if (sbmode) {
+  const bool traced = sweep && std::getenv("GBM_BRR_TRACE") != nullptr;
+  const int64_t trace_n = traced ? (int64_t)la2C * nsb * 8 : 0;
+  if (sweep) {
     GBM_TRY(ensure(cx.Wsb, dev, nsb * SB_PAIRS * BK2 * BK2 * 8));
     GBM_TRY(ensure(cx.MS, dev, nsb * SBK * SBK * 8));
     GBM_TRY(ensure(cx.Ssc, dev, nsb * 6 * BK2 * BK2 * 8));
-    GBM_TRY(ensure(cx.Pb, dev, (int64_t)4 * std::max(sbC, la2C) * SBK * 16));  // 16-B hand-off granules (2 or 4 slots)
+    GBM_TRY(ensure(cx.Pb, dev, (int64_t)4 * la2C * SBK * 16));  // 16-B hand-off granules (4 slots)
     GBM_TRY(ensure(cx.Rt, dev, 4 * SBK * 16));
     GBM_TRY(ensure(cx.Dl, dev, 4 * SBK * 16));
-    if (lamode) {
-      GBM_TRY(ensure(cx.CS, dev, nsb * SBK * SBK * 8));
-      if (nsb > 1) {
-        brr_xgram_kernel<<<(unsigned)((nsb - 1) * 16), 256, 0, s>>>((const double*)cx.Xt.p, npad, p, npad, 1,
-                                                                    (double*)cx.CS.p);
-        GBM_LAUNCH_CHECK();
-      }
-      if (la2mode) {
-        GBM_TRY(ensure(cx.CS2, dev, nsb * SBK * SBK * 8));
-        if (nsb > 2) {
-          brr_xgram_kernel<<<(unsigned)((nsb - 2) * 16), 256, 0, s>>>((const double*)cx.Xt.p, npad, p, npad, 2,
-                                                                      (double*)cx.CS2.p);
-          GBM_LAUNCH_CHECK();
-        }
-      }
+    GBM_TRY(ensure(cx.CS, dev, nsb * SBK * SBK * 8));
+    if (nsb > 1) {
+      brr_xgram_kernel<<<(unsigned)((nsb - 1) * 16), 256, 0, s>>>((const double*)cx.Xt.p, npad, p, npad, 1,
+                                                                  (double*)cx.CS.p);
+      GBM_LAUNCH_CHECK();
+    }
+    GBM_TRY(ensure(cx.CS2, dev, nsb * SBK * SBK * 8));
+    if (nsb > 2) {
+      brr_xgram_kernel<<<(unsigned)((nsb - 2) * 16), 256, 0, s>>>((const double*)cx.Xt.p, npad, p, npad, 2,
+                                                                  (double*)cx.CS2.p);
+      GBM_LAUNCH_CHECK();
     }
     GBM_TRY(ensure(cx.sbcnt, dev, 32 * sizeof(int32_t)));
     GBM_HIP_TRY(hipMemsetAsync(cx.MS.p, 0, (size_t)(nsb * SBK * SBK * 8), s));  // blocks above the diagonal
@@ -2776,27 +1889,7 @@ static int brr_fit_impl(const double* X, int64_t n, int64_t p, int64_t ldx, cons
     GBM_HIP_TRY(hipMemsetAsync(cx.gamm.p, 0, (size_t)(nblk * bk * 8), s));
     brr_gram_sb_kernel<<<(unsigned)(nsb * SB_PAIRS * 4), 256, 0, s>>>((const double*)cx.Xt.p, npad, p, n, (double*)cx.Wsb.p);
     GBM_LAUNCH_CHECK();
-    if (std::getenv("GBM_BRR_TRACE")) {
-      if (g_brr_trace) (void)hipFree(g_brr_trace);
-      g_brr_trace = nullptr;
-      const int64_t tn = std::max<int64_t>(2 * nsb * 12, (int64_t)std::max(sbC, la2C) * nsb * 8);  // sb: 2 x 12, la: C x 8 per super-block
-      GBM_HIP_TRY(hipMalloc((void**)&g_brr_trace, (size_t)(tn * 8)));
-      g_brr_trace_n = tn;
-    } else if (g_brr_trace) {
-      (void)hipFree(g_brr_trace);
-      g_brr_trace = nullptr;
-    }
-  }
-  if (xs > 0.0 && !sbmode) {
-    int per_cu = 0;
-    const char* ev = std::getenv("GBM_BRR_SWEEP");
-    GBM_HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, brr_sweep128_kernel, 256, 0));
-    sweep = sweep_mode != 0 && !(ev && ev[0] == '0') && per_cu >= 1 && C64 <= (int64_t)cus &&
-            (int64_t)2 * C64 * BK2 * 8 < 0x7fffffff;
-    if (sweep) {
-      GBM_TRY(ensure(cx.flg, dev, (C64 + 1) * (int64_t)sizeof(int32_t)));
-      GBM_HIP_TRY(hipMemsetAsync(cx.flg.p, 0, (C64 + 1) * sizeof(int32_t), s));
-    }
+    if (traced) GBM_TRY(ensure(cx.trace, dev, trace_n * 8));
   }
   if (xs > 0.0 && !sweep) {  // the per-launch path's individual-major copy of the bytes
     GBM_TRY(ensure(cx.Dt, dev, nblk * npad * BK2));
@@ -2844,57 +1937,29 @@ static int brr_fit_impl(const double* X, int64_t n, int64_t p, int64_t ldx, cons
   auto* stp = (BrrState*)cx.stm.p;
   const unsigned C = (unsigned)C64;
   const unsigned prep_grid = (unsigned)(xs > 0.0 ? nblk : (nblk + 3) / 4);
+  int64_t* trace_dev = traced ? (int64_t*)cx.trace.p : nullptr;
   auto enqueue_iteration = [&]() -> int {
     brr_prep_kernel<<<prep_grid, 256, 0, s>>>((const double*)cx.W.p, p, nblk, nw, (const double*)cx.x2.p,
                                               (const double*)cx.b.p, stp, (double*)cx.Mb.p, (double*)cx.alph.p,
-                                              (double*)cx.gamm.p, sbmode ? (double*)cx.MS.p : nullptr);
+                                              (double*)cx.gamm.p, sweep ? (double*)cx.MS.p : nullptr);
     brr_mu_kernel<<<1, 1024, 0, s>>>((double*)cx.e.p, n, stp);
-    if (sbmode) {
+    if (sweep) {
       for (int level : {0, 2, 3})
         brr_sb_prep_kernel<<<(unsigned)(nsb * (level == 0 ? 2 : 4)), 256, 0, s>>>(
             level, (const double*)cx.Wsb.p, (const double*)cx.alph.p, (double*)cx.MS.p, (double*)cx.Ssc.p);
       int32_t* cn = (int32_t*)cx.sbcnt.p + 24;  // the error cell (zeroed at setup)
-      if (la2mode && g_brr_trace)
+      if (traced)
         brr_sweep_la2_kernel<true><<<(unsigned)la2C, 256, 0, s>>>(
             (const uint8_t*)cx.D.p, npad, n, p, xs, (const double*)cx.MS.p, (const double*)cx.CS.p,
             (const double*)cx.CS2.p, nsb, la2Ko, la2O, la2Kn, la2R, (double*)cx.Pb.p, (double*)cx.Rt.p, (double*)cx.Dl.p, cn,
             (double*)cx.b.p, (double*)cx.bbar.p, (const double*)cx.alph.p, (const double*)cx.gamm.p,
-            (double*)cx.e.p, stp, g_brr_trace);
-      else if (la2mode)
+            (double*)cx.e.p, stp, trace_dev);
+      else
         brr_sweep_la2_kernel<false><<<(unsigned)la2C, 256, 0, s>>>(
             (const uint8_t*)cx.D.p, npad, n, p, xs, (const double*)cx.MS.p, (const double*)cx.CS.p,
             (const double*)cx.CS2.p, nsb, la2Ko, la2O, la2Kn, la2R, (double*)cx.Pb.p, (double*)cx.Rt.p, (double*)cx.Dl.p, cn,
             (double*)cx.b.p, (double*)cx.bbar.p, (const double*)cx.alph.p, (const double*)cx.gamm.p,
             (double*)cx.e.p, stp, nullptr);
-      else if (lamode && g_brr_trace)
-        brr_sweep_la_kernel<true><<<(unsigned)sbC, 256, 0, s>>>(
-            (const uint8_t*)cx.D.p, npad, n, p, xs, (const double*)cx.MS.p, (const double*)cx.CS.p, nsb, sbK, sbR,
-            (double*)cx.Pb.p, (double*)cx.Rt.p, (double*)cx.Dl.p, cn, (double*)cx.b.p, (double*)cx.bbar.p,
-            (const double*)cx.alph.p, (const double*)cx.gamm.p, (double*)cx.e.p, stp, g_brr_trace);
-      else if (lamode)
-        brr_sweep_la_kernel<false><<<(unsigned)sbC, 256, 0, s>>>(
-            (const uint8_t*)cx.D.p, npad, n, p, xs, (const double*)cx.MS.p, (const double*)cx.CS.p, nsb, sbK, sbR,
-            (double*)cx.Pb.p, (double*)cx.Rt.p, (double*)cx.Dl.p, cn, (double*)cx.b.p, (double*)cx.bbar.p,
-            (const double*)cx.alph.p, (const double*)cx.gamm.p, (double*)cx.e.p, stp, nullptr);
-      else if (g_brr_trace)
-        brr_sweep_sb_kernel<true><<<(unsigned)sbC, 256, 0, s>>>(
-            (const uint8_t*)cx.D.p, npad, n, p, xs, (const double*)cx.MS.p, nsb, sbK, sbR, (double*)cx.Pb.p,
-            (double*)cx.Rt.p, (double*)cx.Dl.p, cn, (double*)cx.b.p, (double*)cx.bbar.p, (const double*)cx.alph.p,
-            (const double*)cx.gamm.p, (double*)cx.e.p, stp, g_brr_trace);
-      else
-        brr_sweep_sb_kernel<false><<<(unsigned)sbC, 256, 0, s>>>(
-            (const uint8_t*)cx.D.p, npad, n, p, xs, (const double*)cx.MS.p, nsb, sbK, sbR, (double*)cx.Pb.p,
-            (double*)cx.Rt.p, (double*)cx.Dl.p, cn, (double*)cx.b.p, (double*)cx.bbar.p, (const double*)cx.alph.p,
-            (const double*)cx.gamm.p, (double*)cx.e.p, stp, nullptr);
-      brr_var_kernel<<<1, 1024, 0, s>>>((const double*)cx.b.p, p, (const double*)cx.e.p, n, stp);
-      return hipGetLastError() == hipSuccess ? GBM_OK : fail(GBM_E_HIP, "gbm_brr_fit: launch failed");
-    }
-    if (sweep) {
-      int32_t* fl = (int32_t*)cx.flg.p;
-      if (hipMemsetAsync(fl, 0, C * sizeof(int32_t), s) != hipSuccess) return fail(GBM_E_HIP, "gbm_brr_fit: memset failed");
-      brr_sweep128_kernel<<<C, 256, 0, s>>>((const uint8_t*)cx.D.p, npad, p, xs, (const double*)cx.Mb.p, nblk,
-                                            (double*)cx.r.p, fl, fl + C, (double*)cx.b.p, (double*)cx.bbar.p,
-                                            (const double*)cx.alph.p, (const double*)cx.gamm.p, (double*)cx.e.p, stp);
       brr_var_kernel<<<1, 1024, 0, s>>>((const double*)cx.b.p, p, (const double*)cx.e.p, n, stp);
       return hipGetLastError() == hipSuccess ? GBM_OK : fail(GBM_E_HIP, "gbm_brr_fit: launch failed");
     }
@@ -2924,14 +1989,14 @@ static int brr_fit_impl(const double* X, int64_t n, int64_t p, int64_t ldx, cons
   const std::vector<int64_t> key = {n, p, npad, (int64_t)(xs * 64.0), sweep ? 1 : 0,
                                     (int64_t)(uintptr_t)cx.Xt.p, (int64_t)(uintptr_t)cx.D.p, (int64_t)(uintptr_t)cx.Dt.p,
                                     (int64_t)(uintptr_t)cx.W.p, (int64_t)(uintptr_t)cx.Mb.p, (int64_t)(uintptr_t)cx.r.p,
-                                    (int64_t)(uintptr_t)cx.flg.p, (int64_t)(uintptr_t)cx.e.p, (int64_t)(uintptr_t)cx.b.p,
+                                    (int64_t)(uintptr_t)cx.e.p, (int64_t)(uintptr_t)cx.b.p,
                                     (int64_t)(uintptr_t)cx.bbar.p, (int64_t)(uintptr_t)cx.alph.p,
                                     (int64_t)(uintptr_t)cx.gamm.p, (int64_t)(uintptr_t)cx.x2.p,
-                                    (int64_t)(uintptr_t)cx.stm.p, sbmode ? 1 : 0, sbK, sbC, sbR, la2Ko, la2O, la2Kn, la2R, la2C,
+                                    (int64_t)(uintptr_t)cx.stm.p, sbK, sbC, sbR, la2Ko, la2O, la2Kn, la2R, la2C,
                                     (int64_t)(uintptr_t)cx.MS.p, (int64_t)(uintptr_t)cx.Wsb.p, (int64_t)(uintptr_t)cx.Ssc.p,
                                     (int64_t)(uintptr_t)cx.Pb.p, (int64_t)(uintptr_t)cx.Rt.p, (int64_t)(uintptr_t)cx.Dl.p,
-                                    (int64_t)(uintptr_t)cx.sbcnt.p, (int64_t)(uintptr_t)g_brr_trace, lamode ? 1 : 0,
-                                    (int64_t)(uintptr_t)cx.CS.p, la2mode ? 1 : 0, (int64_t)(uintptr_t)cx.CS2.p};
+                                    (int64_t)(uintptr_t)cx.sbcnt.p, (int64_t)(uintptr_t)trace_dev,
+                                    (int64_t)(uintptr_t)cx.CS.p, (int64_t)(uintptr_t)cx.CS2.p};
   int rc = GBM_OK;
   if (cx.key != key) {
     cx.drop_graph();
@@ -2962,21 +2027,24 @@ static int brr_fit_impl(const double* X, int64_t n, int64_t p, int64_t ldx, cons
   if (rc != GBM_OK) return rc;
   if (sweep) {
     int32_t inf = 0;
-    GBM_HIP_TRY(hipMemcpyAsync(&inf, sbmode ? (int32_t*)cx.sbcnt.p + 24 : (int32_t*)cx.flg.p + C, sizeof(int32_t),
-                               hipMemcpyDeviceToHost, s));
+    GBM_HIP_TRY(hipMemcpyAsync(&inf, (int32_t*)cx.sbcnt.p + 24, sizeof(int32_t), hipMemcpyDeviceToHost, s));
     GBM_HIP_TRY(hipStreamSynchronize(s));
+    if (std::getenv("GBM_BRR_TEST_SWEEP_TIMEOUT")) inf = -1;  // tests: the fall-back's reporting, no device timeout
     if (inf < 0) {
       *sweep_timeout = true;
       return fail(GBM_E_HIP, "gbm_brr_fit: a sweep hand-off between workgroups timed out");
     }
+    if (traced) {
+      std::vector<int64_t> tr((size_t)trace_n);
+      GBM_HIP_TRY(hipMemcpy(tr.data(), cx.trace.p, (size_t)trace_n * 8, hipMemcpyDeviceToHost));
+      std::lock_guard<std::mutex> lock(g_brr_trace_mu);
+      g_brr_trace_host.swap(tr);
+    }
   }
-  g_brr_last_path.store(la2mode ? 4 : lamode ? 3 : sbmode ? 2 : sweep ? 1 : 0);
-  if (la2mode)
+  g_brr_last_path.store(sweep ? 4 : 0);
+  if (sweep)
     g_brr_shape.store((int64_t)la2C | ((int64_t)la2O << 12) | ((int64_t)la2R << 24) | ((int64_t)la2Ko << 32) |
                       ((int64_t)la2Kn << 44));
-  else if (sbmode)
-    g_brr_shape.store((int64_t)sbC | ((int64_t)((SBK + sbR - 1) / sbR) << 12) | ((int64_t)sbR << 24) |
-                      ((int64_t)sbK << 32) | ((int64_t)sbK << 44));
   BrrState fin{};
   GBM_HIP_TRY(hipMemcpyAsync(&fin, cx.stm.p, sizeof(BrrState), hipMemcpyDeviceToHost, s));
   GBM_HIP_TRY(hipMemcpyAsync(b_hat_out + 1, cx.bbar.p, p * 8, hipMemcpyDeviceToHost, s));
@@ -3005,6 +2073,7 @@ extern "C" int gbm_brr_fit(const double* X, int64_t n, int64_t p, int64_t ldx, c
                            double* b_hat_out, double* y_pred_out, double* var_out) {
   using namespace gbm;
   RoctxRange r_("gbm_brr_fit");
+  set_error("");  // rc 0 with a non-empty gbm_last_error() reports a fall-back (below)
   if (!X || !y || !b_hat_out || n < 3 || p < 1 || ldx < n || n_iter < 1 || n_burnin < 0 || thin < 1 ||
       !(r2 > 0.0 && r2 < 1.0) || !(df0 > 0.0))
     return fail(GBM_E_ARG, "gbm_brr_fit: bad arguments (n >= 3, p >= 1, ldx >= n, n_iter >= 1, n_burnin >= 0, "
@@ -3019,11 +2088,16 @@ extern "C" int gbm_brr_fit(const double* X, int64_t n, int64_t p, int64_t ldx, c
                         var_out, &timeout);
   // a sweep whose workgroups could not all be resident (another process or library filling the
   // device) times out loudly on the device; the fit is then run again, from the start, on the
-  // per-launch path (same chain; the two paths agree to rounding)
+  // per-launch path (same chain; the two paths agree to rounding). The call still returns GBM_OK —
+  // the results are valid — but says so: gbm_last_error() holds the warning (the Python mirror
+  // raises a RuntimeWarning, the Julia binding an @warn) and gbm_debug_brr_stats counts it.
   if (rc != GBM_OK && timeout) {
     g_brr_fallbacks.fetch_add(1);
     rc = brr_fit_impl(X, n, p, ldx, y, n_iter, n_burnin, thin, r2, df0, seed, devs[0], 0, b_hat_out, y_pred_out,
                       var_out, &timeout);
+    if (rc == GBM_OK)
+      set_error("warning: gbm_brr_fit: the persistent super-block sweep timed out (were all its workgroups resident? "
+                "another process may share the device); the fit was re-run on the per-launch path");
   }
   return rc;
 }

@@ -4,6 +4,7 @@
 #include <atomic>
 #include <cmath>
 #include <cstdlib>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -49,11 +50,25 @@ inline std::atomic<int64_t>& alloc_counter() {
   return c;
 }
 
-// Called when a device allocation runs out of memory: frees what the pooled (idle) fit contexts
-// of that device hold, then the allocation is retried once. Set by capi.cpp's context pool.
-inline std::atomic<void (*)(int)>& oom_trim_hook() {
-  static std::atomic<void (*)(int)> h{nullptr};
-  return h;
+// When a device allocation runs out of memory, every registered trim callback frees the idle pooled
+// contexts of that device (capi.cpp: GBLUP fit contexts; gibbs.hip: BRR contexts, which also hold
+// their captured graphs) and returns how many it freed; the allocation is then retried once.
+using TrimFn = int64_t (*)(int dev);
+struct OomTrim {
+  std::mutex mu;
+  std::vector<TrimFn> hooks;
+  std::atomic<int64_t> retries{0}, freed{0};  // gbm_debug_oom_retries
+};
+inline OomTrim& oom_trim() {
+  static OomTrim* t = new OomTrim;  // never destroyed (pools outlive static destruction)
+  return *t;
+}
+inline void register_trim_hook(TrimFn f) {
+  OomTrim& t = oom_trim();
+  std::lock_guard<std::mutex> lock(t.mu);
+  for (TrimFn g : t.hooks)
+    if (g == f) return;
+  t.hooks.push_back(f);
 }
 
 inline int dalloc(DevMem& m, int dev, int64_t bytes) {
@@ -61,14 +76,24 @@ inline int dalloc(DevMem& m, int dev, int64_t bytes) {
   m.dev = dev;
   if (bytes <= 0) bytes = 16;
   alloc_counter().fetch_add(1, std::memory_order_relaxed);
-  hipError_t e = hipMalloc(&m.p, (size_t)bytes);
+  // GBM_TEST_OOM_ONCE=1 (tests): every allocation's first attempt reports out-of-memory, so the
+  // trim-and-retry path below runs
+  const char* t1 = getenv("GBM_TEST_OOM_ONCE");
+  hipError_t e = (t1 && t1[0] == '1') ? hipErrorOutOfMemory : hipMalloc(&m.p, (size_t)bytes);
   if (e == hipErrorOutOfMemory) {
     (void)hipGetLastError();
-    if (void (*trim)(int) = oom_trim_hook().load()) {
-      trim(dev);
-      (void)hipSetDevice(dev);
-      e = hipMalloc(&m.p, (size_t)bytes);
+    OomTrim& t = oom_trim();
+    std::vector<TrimFn> hooks;
+    {
+      std::lock_guard<std::mutex> lock(t.mu);
+      hooks = t.hooks;
     }
+    int64_t freed = 0;
+    for (TrimFn f : hooks) freed += f(dev);
+    t.retries.fetch_add(1, std::memory_order_relaxed);
+    t.freed.fetch_add(freed, std::memory_order_relaxed);
+    (void)hipSetDevice(dev);
+    e = hipMalloc(&m.p, (size_t)bytes);
   }
   if (e != hipSuccess) {
     m.p = nullptr;

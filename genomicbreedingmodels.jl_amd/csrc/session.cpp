@@ -221,7 +221,7 @@ int solve_cached(gbm_session* s, int64_t nrhs, double lambda, double inv_q) {
   int32_t info = 0;
   GBM_HIP_TRY(hipMemcpyAsync(&info, s->info.p, 4, hipMemcpyDeviceToHost, st));
   GBM_HIP_TRY(hipStreamSynchronize(st));
-  if (info < 0) return fail(GBM_E_HIP, "back substitution: block synchronisation timed out");
+  if (info < 0) return fail(GBM_E_HIP, "solve: a wait between workgroups timed out (dataflow Cholesky or back substitution; the result is invalid)");
   if (info != 0)
     return fail(GBM_E_NOTPD, "G/q + lambda*I is not positive definite (pivot " + std::to_string(info) + ")");
   return GBM_OK;

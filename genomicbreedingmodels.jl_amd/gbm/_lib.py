@@ -40,6 +40,7 @@ EXPORTS = (
     "gbm_dev_grm_packed_size", "gbm_dev_grm_pack", "gbm_dev_grm_unpack",
     "gbm_debug_brr_stats", "gbm_debug_brr_shape", "gbm_debug_brr_trace", "gbm_debug_chol_flow_trace",
     "gbm_dev_synth_dosage_i8", "gbm_dev_standardize_i8", "gbm_dev_grm_accumulate", "gbm_dev_marker_effects_i8",
+    "gbm_debug_oom_retries",
 )
 
 
@@ -165,6 +166,8 @@ def _declare(lib):
     lib.gbm_dev_grm_unpack.argtypes = [P, I64, P, I64, P]
     lib.gbm_brr_fit.restype = I32
     lib.gbm_brr_fit.argtypes = [P, I64, I64, I64, P, I64, I64, I64, D, D, U64, I32, P, P, P]
+    lib.gbm_debug_oom_retries.restype = I32
+    lib.gbm_debug_oom_retries.argtypes = [P, P]
     lib.gbm_session_stats.restype = I32
     lib.gbm_session_stats.argtypes = [P, P, P]
     return lib

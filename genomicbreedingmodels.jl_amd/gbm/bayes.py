@@ -3,6 +3,8 @@ ridge regression), with the Gibbs sampler on the GPU (libgbm ``gbm_brr_fit``) in
 Rscript/BGLR round trip (src/bayes.jl:28-105). SURVEY.md §8f row 3, config C4."""
 from __future__ import annotations
 
+import warnings
+
 import numpy as np
 
 from . import _lib
@@ -28,6 +30,9 @@ def brr_arrays(X: np.ndarray, y: np.ndarray, *, n_iter: int = 1500, n_burnin: in
                          float(df0), int(seed) & 0xFFFFFFFFFFFFFFFF, int(device), _lib.ptr(b_hat), _lib.ptr(y_pred),
                          _lib.ptr(var))
     _lib.check(rc, "gbm_brr_fit")
+    msg = _lib.last_error()
+    if msg.startswith("warning"):  # the sweep timed out and the fit was re-run on the per-launch path
+        warnings.warn(msg, RuntimeWarning, stacklevel=2)
     return b_hat, y_pred, var
 
 

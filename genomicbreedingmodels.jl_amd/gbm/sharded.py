@@ -319,7 +319,7 @@ class HipShardStages:
         self.h_out.copy_(self.out, non_blocking=True)
         self.torch.cuda.current_stream(self.dev).synchronize()
         if int(self.h_info[0]) < 0:
-            raise _lib.GBMError("back substitution: block synchronisation timed out")
+            raise _lib.GBMError("solve: a wait between workgroups timed out (dataflow Cholesky or back substitution; the result is invalid)")
         if int(self.h_info[0]) != 0:
             raise _lib.GBMError(f"G/q + λI not positive definite (pivot {int(self.h_info[0])})")
         return dict(B=self.h_B.numpy(), y_pred=self.h_gebv.numpy()[:, : self.n].T, mu=self.h_mu.numpy(),

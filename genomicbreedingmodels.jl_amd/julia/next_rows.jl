@@ -145,6 +145,8 @@ function bglr_brr_gpu(; G::Matrix{Float64}, y::Vector{Float64}, n_iter::Int64 = 
                    G, n, p, stride(G, 2), y, n_iter, n_burnin, thin, 0.5, 5.0, seed, device, b_hat, C_NULL, C_NULL)
     end
     gbm_check(rc, "bglr_brr_gpu")
+    msg = unsafe_string(ccall((:gbm_last_error, LIBGBM), Cstring, ()))
+    startswith(msg, "warning") && @warn msg  # sweep timed out; re-run on the per-launch path (valid results)
     b_hat
 end
 

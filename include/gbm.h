@@ -382,6 +382,12 @@ int gbm_session_stats(gbm_session* s, int64_t* grm_builds, int64_t* grm_hits);
  * b0 + X b; var_out (2, optional) = posterior means of [σ²_e, σ²_b]. X column-major n x p.
  * Counter-based random numbers from `seed` (no R RNG stream: results are reproducible but the
  * chain is not BGLR's sample path).
+ * Schedule: one persistent super-block sweep launch per iteration when its workgroups fit one per CU
+ * (byte-exact genotypes, n <= 48 x CUs), else one launch per marker block. If the sweep's
+ * inter-workgroup hand-offs time out (its workgroups could not all be resident, e.g. another process
+ * fills the device) the fit is re-run from the start on the per-launch path: the call still returns
+ * GBM_OK (the results are valid) and gbm_last_error() then holds a message starting "warning:" (it
+ * is "" after any other successful call of this function).
  */
 int gbm_brr_fit(const double* X, int64_t n, int64_t p, int64_t ldx, const double* y, int64_t n_iter,
                 int64_t n_burnin, int64_t thin, double r2, double df0, uint64_t seed, int device,
@@ -390,14 +396,17 @@ int gbm_brr_fit(const double* X, int64_t n, int64_t p, int64_t ldx, const double
 /* --------------------------------------------------------------------------------------
  * Diagnostics (tests and timing tools; no reference counterpart).
  * ------------------------------------------------------------------------------------ */
-/* Which schedule the last completed gbm_brr_fit ran (*last_path: 0 one launch per block, 1 the
- * 128-block sweep, 2 the super-block sweep, 3 its look-ahead form, 4 the look-ahead form with two
- * super-blocks of slack for the partial dots) and how many fits so far fell
- * back to the per-launch schedule after a sweep hand-off timed out (*fallbacks). */
+/* Which schedule the last completed gbm_brr_fit ran (*last_path: 0 one launch per block, 4 the
+ * super-block sweep with two super-blocks of slack for the partial dots; 1-3 were earlier sweeps, no
+ * longer built) and how many fits so far fell back to the per-launch schedule after a sweep
+ * hand-off timed out (*fallbacks). */
 int gbm_debug_brr_stats(int* last_path, int64_t* fallbacks);
 /* Chunk shape of the last super-block sweep: C workgroups, the first O own R rows of every
  * super-block and take Ko individuals each, the others Kn. */
 int gbm_debug_brr_shape(int* C, int* O, int* R, int* Ko, int* Kn);
+/* Allocations that ran out of device memory and were retried after freeing the idle pooled contexts
+ * (GBLUP and BRR) of their device, and how many contexts those retries freed. */
+int gbm_debug_oom_retries(int64_t* retries, int64_t* contexts_freed);
 /* With GBM_BRR_TRACE=1 set for a fit: copies up to cap int64 timestamps (100 MHz) of the last
  * super-block sweep into host; returns the count, 0 when no trace was taken, -1 on a HIP error. */
 int64_t gbm_debug_brr_trace(int64_t* host, int64_t cap);

@@ -71,13 +71,15 @@ def test_gpu_brr_byte_storage_matches_fp64_and_oracle(monkeypatch, n, p):
 @pytest.mark.gpu
 @pytest.mark.parametrize("n,p", [(1100, 300), (12000, 260)])
 def test_gpu_brr_sweep_matches_per_launch_path_and_oracle(monkeypatch, n, p):
-    """Byte storage: the persistent sweep (one launch per iteration, partial dots handed between
-    the ⌈n/256⌉ workgroups through write-through stores and flags) against one launch per
-    128-marker block (GBM_BRR_SWEEP=0) and the oracle's literal loop. n = 12 000: 47 workgroups,
-    more than one batch of partial loads."""
+    """Byte storage: the persistent super-block sweep (one launch per iteration, hand-offs between
+    the chunk workgroups through self-validating write-through granules) against one launch per
+    128-marker block (GBM_BRR_SWEEP=0) and the oracle's literal loop. n = 12 000: 250 chunk
+    workgroups of 48 individuals, near the sweep's limit."""
     X = oracle.synth_genotypes(97 + n, n, p)
     y = oracle.synth_phenotypes(X, 98)[:, 0]
+    _, fb0 = brr_path()
     sweep = gbm.brr_arrays(X, y, n_iter=5, n_burnin=1, thin=1, seed=17)
+    assert brr_path() == (4, fb0)
     monkeypatch.setenv("GBM_BRR_SWEEP", "0")
     launches = gbm.brr_arrays(X, y, n_iter=5, n_burnin=1, thin=1, seed=17)
     ref = oracle.brr_gibbs(X, y, n_iter=5, n_burnin=1, thin=1, seed=17)
@@ -176,19 +178,17 @@ def brr_path():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("n,p,K", [(1100, 300, None), (12000, 1300, None), (5000, 777, "64"), (3000, 1025, "32"),
+@pytest.mark.parametrize("n,p,K", [(1100, 300, None), (12000, 1300, None), (5000, 777, "48"), (3000, 1025, "32"),
                                    (10000, 1100, None), (4000, 900, None), (6000, 2600, None), (10000, 1100, "R4"),
                                    (9000, 2100, "R2")])
 def test_gpu_brr_super_block_sweep_runs_and_matches(monkeypatch, n, p, K):
-    """The super-block sweeps really run (no fall-back to the per-launch path): the look-ahead forms
-    (chunks of <= 48 individuals, two granule hand-offs per super-block) with two steps of slack
-    for the partial dots (brr_sweep_la2_kernel, path 4: C2_s δ_{s−2} + C_s δ_{s−1} on the chain) and
-    with one (brr_sweep_la_kernel, path 3, GBM_BRR_LA2=0), and brr_sweep_sb_kernel (path 2: three
-    hand-offs; also GBM_BRR_LA=0). All agree with the 128-block sweep (GBM_BRR_SB=0), the
+    """The super-block sweep really runs (no fall-back to the per-launch path): chunks of <= 48
+    individuals, two granule hand-offs per super-block, two steps of slack for the partial dots
+    (brr_sweep_la2_kernel, path 4: C2_s δ_{s−2} + C_s δ_{s−1} on the chain). It agrees with the
     per-launch path and the oracle's literal loop; ragged p (p mod 512 = 300, 276, 265, 1, 76)
-    including nsb = 1, 2, 3, 6; several chunk sizes, and the two-step form's owner/non-owner chunk
-    split (owners of R = 8, 4, 2 rows with smaller chunks)."""
-    if K and K.startswith("R"):  # owners of R rows in the two-step form's chunk split
+    including nsb = 1, 2, 3, 6; several chunk sizes, and the owner/non-owner chunk split (owners of
+    R = 4, 2 rows with smaller chunks). (The round-3 schedules 1-3 are no longer built.)"""
+    if K and K.startswith("R"):  # owners of R rows in the chunk split
         monkeypatch.setenv("GBM_BRR_OWN_R", K[1:])
     elif K:
         monkeypatch.setenv("GBM_BRR_SB_K", K)
@@ -197,24 +197,36 @@ def test_gpu_brr_super_block_sweep_runs_and_matches(monkeypatch, n, p, K):
     _, fb0 = brr_path()
     la2 = gbm.brr_arrays(X, y, n_iter=4, n_burnin=1, thin=1, seed=23)
     path, fb = brr_path()
-    assert path == (2 if K == "64" else 4) and fb == fb0
-    monkeypatch.setenv("GBM_BRR_LA2", "0")
-    la = gbm.brr_arrays(X, y, n_iter=4, n_burnin=1, thin=1, seed=23)
-    path, fb = brr_path()
-    assert path == (2 if K == "64" else 3) and fb == fb0
-    monkeypatch.setenv("GBM_BRR_LA", "0")
-    sb = gbm.brr_arrays(X, y, n_iter=4, n_burnin=1, thin=1, seed=23)
-    path, fb = brr_path()
-    assert path == 2 and fb == fb0
-    monkeypatch.setenv("GBM_BRR_SB", "0")
-    s128 = gbm.brr_arrays(X, y, n_iter=4, n_burnin=1, thin=1, seed=23)
+    assert path == 4 and fb == fb0
     monkeypatch.setenv("GBM_BRR_SWEEP", "0")
     launches = gbm.brr_arrays(X, y, n_iter=4, n_burnin=1, thin=1, seed=23)
     assert brr_path()[0] == 0
     rel = lambda a, b: np.abs(a - b).max() / np.abs(b).max()
-    for a, b, c, d, e in zip(sb, s128, launches, la, la2):
-        assert rel(a, b) < 1e-10 and rel(a, c) < 1e-10 and rel(d, c) < 1e-10 and rel(e, c) < 1e-10
+    for e, c in zip(la2, launches):
+        assert rel(e, c) < 1e-10
     if n * p <= 5000 * 1000:
         ref = oracle.brr_gibbs(X, y, n_iter=4, n_burnin=1, thin=1, seed=23)
-        for got in (sb, la, la2):
-            assert rel(got[0], ref["b_hat"]) < 1e-9 and rel(got[1], ref["y_pred"]) < 1e-9
+        assert rel(la2[0], ref["b_hat"]) < 1e-9 and rel(la2[1], ref["y_pred"]) < 1e-9
+
+
+@pytest.mark.gpu
+def test_gpu_brr_fallback_is_reported(monkeypatch):
+    """A sweep whose hand-offs time out is re-run on the per-launch path; the call succeeds (valid
+    results, equal to the per-launch fit) but says so: gbm_last_error() starts with "warning", the
+    Python mirror raises a RuntimeWarning, the fall-back counter grows. GBM_BRR_TEST_SWEEP_TIMEOUT
+    makes the host treat a completed sweep as timed out (no device-side timeout is provoked)."""
+    X = oracle.synth_genotypes(55, 1200, 700)
+    y = oracle.synth_phenotypes(X, 56)[:, 0]
+    monkeypatch.setenv("GBM_BRR_SWEEP", "0")
+    ref = gbm.brr_arrays(X, y, n_iter=4, n_burnin=1, thin=1, seed=9)
+    monkeypatch.delenv("GBM_BRR_SWEEP")
+    gbm.brr_arrays(X, y, n_iter=4, n_burnin=1, thin=1, seed=9)
+    assert gbm._lib.last_error() == ""  # a clean sweep fit leaves no message
+    _, fb0 = brr_path()
+    monkeypatch.setenv("GBM_BRR_TEST_SWEEP_TIMEOUT", "1")
+    with pytest.warns(RuntimeWarning, match="per-launch path"):
+        got = gbm.brr_arrays(X, y, n_iter=4, n_burnin=1, thin=1, seed=9)
+    assert brr_path() == (0, fb0 + 1)
+    assert gbm._lib.last_error().startswith("warning")
+    for a, b in zip(got, ref):
+        assert np.array_equal(a, b)

@@ -121,3 +121,28 @@ def test_flow_few_resident_workgroups_complete_bit_identical(monkeypatch, wgs):
     torch.cuda.synchronize()
     assert int(a.info.item()) == 0 and int(b.info.item()) == 0
     assert torch.equal(a.gebv, b.gebv) and torch.equal(a.A, b.A) and torch.equal(a.mu, b.mu)
+
+
+def test_flow_timed_out_wait_drains_and_fails_loudly(monkeypatch):
+    """A wait that times out (info = −1; a bug guard, forced here by GBM_TEST_CHOL_FLOW_ABORT) stops
+    the chain before it publishes another tile and keeps workers from taking new tasks:
+    the launch drains at once and the solve reports info = −1 instead of computing on stale tiles.
+    The next solve on the same buffers is clean."""
+    import time
+
+    import torch
+    monkeypatch.setenv("GBM_CHOL_FLOW_MAX", "1000000")
+    X, Y, a, b = _pair(3000, 700, 1, 23, 1.0)
+    monkeypatch.setenv("GBM_TEST_CHOL_FLOW_ABORT", "1")
+    t0 = time.perf_counter()
+    a.solve()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    assert int(a.info.item()) == -1
+    assert dt < 2.0, dt  # drained, not ~1 s per stuck wait
+    monkeypatch.delenv("GBM_TEST_CHOL_FLOW_ABORT")
+    b.solve()
+    torch.cuda.synchronize()
+    assert int(b.info.item()) == 0
+    ref = oracle.gblup_fit(X, Y, 1.0)
+    assert rel(b.gebv[0, :3000].cpu().numpy(), ref["y_pred"][:, 0]) < 1e-9

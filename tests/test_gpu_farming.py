@@ -261,3 +261,54 @@ def test_multi_shard_fit_concurrent_equals_serial(monkeypatch, devices, chunk, l
     assert fit[3] == ref["q"] and rel(fit[1], ref["y_pred"]) < 1e-9 and rel(fit[0], ref["b_hat"]) < 1e-6
     Gr, qr = oracle.grm(X)
     assert grm[1] == qr and rel(grm[0], Gr) < 1e-12
+
+
+def _oom_counts():
+    import ctypes
+    r, f = ctypes.c_int64(0), ctypes.c_int64(0)
+    gbm.load_library().gbm_debug_oom_retries(ctypes.byref(r), ctypes.byref(f))
+    return r.value, f.value
+
+
+def test_oom_retry_frees_idle_gblup_and_brr_contexts(monkeypatch):
+    """An allocation that runs out of device memory frees the idle pooled contexts of its device —
+    the BRR pool's as well as the GBLUP pool's — and is retried once; the fit then
+    succeeds with the same results. GBM_TEST_OOM_ONCE=1 makes every allocation's first attempt fail."""
+    lib = gbm.load_library()
+    lib.gbm_release_device_cache()
+    X = oracle.synth_genotypes(404, 300, 800)
+    Y = oracle.synth_phenotypes(X, 405)
+    ref = gbm.gblup_arrays(X, Y, devices=[0])
+    gbm.brr_arrays(X, Y[:, 0], n_iter=4, n_burnin=1, thin=1, seed=3)  # leaves an idle BRR context
+    r0, f0 = _oom_counts()
+    monkeypatch.setenv("GBM_TEST_OOM_ONCE", "1")
+    X2 = oracle.synth_genotypes(406, 420, 1300)  # a larger shape: the leased context must grow
+    Y2 = oracle.synth_phenotypes(X2, 407)
+    got = gbm.gblup_arrays(X2, Y2, devices=[0])
+    monkeypatch.delenv("GBM_TEST_OOM_ONCE")
+    r1, f1 = _oom_counts()
+    assert r1 > r0 and f1 >= f0 + 1  # the idle BRR context was freed by a retry
+    want = gbm.gblup_arrays(X2, Y2, devices=[0])
+    for a, b in zip(got, want):
+        assert np.array_equal(np.asarray(a), np.asarray(b))
+    again = gbm.gblup_arrays(X, Y, devices=[0])
+    for a, b in zip(again, ref):
+        assert np.array_equal(np.asarray(a), np.asarray(b))
+
+
+def test_reml_fit_multi_leader_rehearsal(monkeypatch):
+    """gbm_gblup_fit_reml over several device leaders at a size that takes the distributed
+    factorisation (devices=[0, 0], every shard its own leader, GBM_DIST_SOLVE_MIN_N=0):
+    λ is chosen on the first leader, the other leaders' G restored from its pristine copy, and the
+    fit equals the single-device REML fit."""
+    X = oracle.synth_genotypes(515, 700, 3000)
+    Y = oracle.synth_phenotypes(X, 516, ntraits=2)
+    ref = gbm.gblup_reml_arrays(X, Y, devices=[0])
+    monkeypatch.setenv("GBM_SHARD_LEADERS", "each")
+    monkeypatch.setenv("GBM_DIST_SOLVE_MIN_N", "0")
+    got = gbm.gblup_reml_arrays(X, Y, devices=[0, 0])
+    assert got[3] == ref[3]
+    # the two G differ by the rounding of the shard sum: the λ searches agree to their tolerance
+    assert np.abs(got[4]["lambda"] - ref[4]["lambda"]).max() < 1e-5 * np.abs(ref[4]["lambda"]).max()
+    rel = lambda a, b: np.abs(a - b).max() / np.abs(b).max()
+    assert rel(got[1], ref[1]) < 1e-6 and rel(got[0], ref[0]) < 1e-5

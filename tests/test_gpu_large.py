@@ -15,6 +15,7 @@
 
 Each test prints its timings (pytest -s / the log) for DESIGN.md.
 """
+import ctypes
 import time
 
 import numpy as np
@@ -220,9 +221,15 @@ def test_c4_bayesian_ridge_5000_iterations():
     X = synth.genotypes(seed, n, p, device=0)
     y = synth.qtl_phenotypes(seed, n, p, 1, device=0)[:, 0]
     _free()
+    lib = gbm.load_library()
+    path, fb0, fb = ctypes.c_int(-1), ctypes.c_int64(0), ctypes.c_int64(0)
+    lib.gbm_debug_brr_stats(ctypes.byref(path), ctypes.byref(fb0))
     t0 = time.perf_counter()
     b_hat, y_pred, var = gbm.brr_arrays(X, y, n_iter=5000, n_burnin=1000, thin=5, seed=7)
     t1 = time.perf_counter()
+    # the fast path really ran: the super-block sweep (path 4), no fall-back to the per-launch path
+    lib.gbm_debug_brr_stats(ctypes.byref(path), ctypes.byref(fb))
+    assert path.value == 4 and fb.value == fb0.value
     print(f"\nC4 BRR 10000 x 100000, 5000 iterations: {t1 - t0:.1f} s "
           f"(posterior means: varE {var[0]:.4g}, varB {var[1]:.4g})")
     assert np.isfinite(b_hat).all() and np.isfinite(y_pred).all()

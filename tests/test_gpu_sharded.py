@@ -35,8 +35,22 @@ def _worker(rank, world, port, n, p_total, seed, Y, out_dir, env=None):
     st = HipShardStages(n, p_local, nrhs=Y.shape[1], lambda_=1.0, device=0)
     st.generate(seed, j0)
     st.load_phenotypes(Y)
-    out = sharded_gblup_step(st, TorchComm())
-    np.savez(os.path.join(out_dir, f"rank{rank}.npz"), **out, j0=j0)
+    saved = {}
+
+    def mark(label):  # the summed GRM, as the solve receives it
+        if label == "allreduce":
+            saved["G"], saved["q"] = st.G.clone(), st.q.clone()
+
+    out = sharded_gblup_step(st, TorchComm(), events=mark)
+    # the redundant launch-per-panel solve of the same summed G (the distributed factorisation computes
+    # every tile with the same kernel and operands: the same bits)
+    st.G.copy_(saved["G"])
+    st.q.copy_(saved["q"])
+    os.environ["GBM_CHOL_FLOW_MAX"] = "0"
+    st.solve()
+    torch.cuda.synchronize()
+    y_red = st.gebv[:, :n].T.cpu().numpy()
+    np.savez(os.path.join(out_dir, f"rank{rank}.npz"), **out, j0=j0, y_redundant=y_red)
     dist.barrier()
     dist.destroy_process_group()
 
@@ -59,11 +73,13 @@ def test_two_ranks_one_gpu_match_oracle(tmp_path):
     assert np.abs(b_hat - ref["b_hat"]).max() < 1e-6 * np.abs(ref["b_hat"]).max()
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 8])
 def test_ranks_one_gpu_distributed_solve_match_oracle(tmp_path, world):
     """The distributed factorisation (chol_distributed) over torch.distributed: each rank updates
     its own tile columns, strips all-gathered over gloo; forced on at a small n with 4-panel groups
-    and a short redundant tail. Every rank's GEBVs equal the oracle's."""
+    and a short redundant tail; world 8 = the north star's rank count (8 processes on the one GPU).
+    Every rank's GEBVs equal the oracle's, and equal bit for bit the redundant solve of the same
+    summed G."""
     import torch.multiprocessing as mp
 
     import oracle
@@ -80,5 +96,6 @@ def test_ranks_one_gpu_distributed_solve_match_oracle(tmp_path, world):
     for o in outs:
         assert np.abs(o["y_pred"] - ref["y_pred"]).max() < 1e-9 * np.abs(ref["y_pred"]).max()
         assert np.array_equal(o["y_pred"], outs[0]["y_pred"])
+        assert np.array_equal(o["y_pred"], o["y_redundant"])
     b_hat = assemble_b_hat(outs[0]["mu"], outs[0]["msum"], [o["B"] for o in outs], p)
     assert np.abs(b_hat - ref["b_hat"]).max() < 1e-6 * np.abs(ref["b_hat"]).max()

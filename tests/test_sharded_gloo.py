@@ -1,17 +1,40 @@
-"""The N > 1 loci-sharded path on CPU: world_size 2 over gloo drives the same
-``sharded_gblup_step`` (and the same all-reduce wiring) that bench.py runs over RCCL, with a
-numpy stage backend standing in for the HIP stages (test infrastructure, not the product)."""
+"""The N > 1 loci-sharded path on CPU: world sizes 2, 3 and 8 (the north star's rank count) over
+gloo drive the same ``sharded_gblup_step`` / ``chol_distributed`` (and the same collective wiring)
+that bench.py runs over RCCL, with a numpy stage backend standing in for the HIP stages (test
+infrastructure, not the product). The backend restates the stage semantics of gbm.sharded.
+HipShardStages at tile level: the packed partial-GRM all-reduce (upper 128-tiles + q in the last
+slot) and the distributed factorisation protocol of gbm_dev_chol_* (include/gbm.h): per panel group
+every rank factors the group's panels over the full width, updates only its own 128-column tiles
+(J ≡ rank mod R; the bordered right-hand sides on every rank), the next strip is all-gathered and
+its diagonal block factored; the tail runs redundantly. Every tile update is the same numpy op
+whichever rank computes it, so the distributed solve equals the redundant one bit for bit."""
 import os
 import socket
 
 import numpy as np
 import pytest
+import scipy.linalg as sla
 import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
 import oracle
 from gbm.sharded import TorchComm, assemble_b_hat, sharded_gblup_step
+
+NB, TB = 64, 128  # panel rows, ownership tile columns (csrc: kCholNB, the GRM tile)
+
+
+class _NumpyChol:
+    """gbm_dev_chol_group_size for the numpy backend: 4-panel groups while more than 6 blocks remain,
+    then 2-panel groups, then single panels (groups of >= 2 panels starting on a 128-row boundary
+    are distributable, as in csrc/chol.hip)."""
+
+    def __init__(self, npad):
+        self.nb = npad // NB
+
+    def gbm_dev_chol_group_size(self, n, kb):
+        rem = self.nb - kb
+        return 0 if rem <= 0 else 4 if rem > 6 else 2 if rem > 2 else 1
 
 
 class NumpyShardStages:
@@ -22,9 +45,14 @@ class NumpyShardStages:
         self.Y = Y
         self.lam = lam
         n = X_local.shape[0]
-        self.G = torch.zeros((n, n), dtype=torch.float64)
+        self.n = n
+        self.npad = -(-n // TB) * TB
+        self.gdim = self.npad + NB
+        self.lib = _NumpyChol(self.npad)
+        self.G = torch.zeros((self.gdim, self.gdim), dtype=torch.float64)
         self.q = torch.zeros(1, dtype=torch.int64)
         self.msum = torch.zeros(Y.shape[1], dtype=torch.float64)
+        self.packs = 0
 
     def standardize(self):
         self.m, self.s, self.keep = oracle.colstats(self.X)
@@ -32,25 +60,112 @@ class NumpyShardStages:
         self.q.fill_(int(self.keep.sum()))
 
     def grm_syrk(self):
-        self.G.copy_(torch.from_numpy(self.Z @ self.Z.T))
+        self.G[: self.n, : self.n] = torch.from_numpy(self.Z @ self.Z.T)
 
     def grm_reduce(self):
         pass
 
     def grm_rows(self):
-        return self.G
+        return self.G[: self.npad]
+
+    # ---- the packed all-reduce operand: upper 128-tiles of G, then q (gbm_dev_grm_pack) ----------
+    def _tiles(self):
+        nt = self.npad // TB
+        return [(i, j) for i in range(nt) for j in range(i, nt)]
+
+    def grm_pack(self):
+        self.packs += 1
+        parts = [self.G[i * TB:(i + 1) * TB, j * TB:(j + 1) * TB].reshape(-1) for i, j in self._tiles()]
+        self.Gp = torch.cat(parts + [self.q.to(torch.float64)])
+        return self.Gp
+
+    def grm_unpack(self):
+        for k, (i, j) in enumerate(self._tiles()):
+            self.G[i * TB:(i + 1) * TB, j * TB:(j + 1) * TB] = self.Gp[k * TB * TB:(k + 1) * TB * TB].view(TB, TB)
+        self.q.fill_(int(self.Gp[-1].item()))
+
+    # ---- the solve in phases (gbm_dev_chol_prepare / group / strip_pack / strip_unpack / factor_diag /
+    # finish): V = G/q + λI bordered by R = [1, y...], upper factor U, W = U⁻ᵀR in the border ---------
+    def chol_prepare(self):
+        n, npad, t = self.n, self.npad, self.Y.shape[1]
+        V = np.zeros((self.gdim, self.gdim))
+        V[:n, :n] = np.triu(self.G[:n, :n].numpy()) / int(self.q.item())
+        V[np.arange(n), np.arange(n)] += self.lam
+        V[np.arange(n, npad), np.arange(n, npad)] = 1.0
+        V[:n, npad] = 1.0
+        V[:n, npad + 1:npad + 1 + t] = self.Y
+        self.V = V
+        self.chol_factor_diag(0)
+
+    def chol_factor_diag(self, kb):
+        r = slice(NB * kb, NB * kb + NB)
+        A = np.triu(self.V[r, r])
+        self.V[r, r] = np.linalg.cholesky(A + np.triu(A, 1).T).T
+
+    def chol_group(self, kb, rank, nranks):
+        V, npad = self.V, self.npad
+        g = self.lib.gbm_dev_chol_group_size(self.n, kb)
+        k0, k1 = NB * kb, NB * (kb + g)
+        for k in range(kb, kb + g):
+            r = slice(NB * k, NB * k + NB)
+            if k > kb:  # this group's earlier panels, over the full width
+                for pj in range(kb, k):
+                    rp = slice(NB * pj, NB * pj + NB)
+                    V[r, NB * k:] -= V[rp, r].T @ V[rp, NB * k:]
+                self.chol_factor_diag(k)
+            V[r, NB * (k + 1):] = sla.solve_triangular(V[r, r], V[r, NB * (k + 1):], trans="T", lower=False)
+        # trailing update: this rank's 128-column tiles, the bordered right-hand sides on every rank
+        for c0 in range(k1, npad, TB):
+            c1 = min(c0 + TB, npad)
+            if (c0 // TB) % nranks == rank:
+                V[k1:c1, c0:c1] -= V[k0:k1, k1:c1].T @ V[k0:k1, c0:c1]
+        V[k1:npad, npad:] -= V[k0:k1, k1:npad].T @ V[k0:k1, npad:]
+        if nranks == 1 and kb + g < npad // NB:
+            self.chol_factor_diag(kb + g)  # the redundant path factors the next diagonal block itself
+
+    def _owned_cols(self, kb, rank, nranks):
+        c = np.arange(NB * kb, self.npad)
+        return c[(c // TB) % nranks == rank]
+
+    def _strip_doubles(self, kb, rows64, nranks):
+        """Per-rank pack size, padded to the largest rank's (gbm_dev_chol_strip_doubles): the
+        all-gather moves equal pieces."""
+        return NB * rows64 * max(self._owned_cols(kb, r, nranks).size for r in range(nranks))
+
+    def strip_pack(self, kb, rows64, rank, nranks):
+        rows = slice(NB * kb, NB * (kb + rows64))
+        buf = np.zeros(self._strip_doubles(kb, rows64, nranks))
+        own = np.ascontiguousarray(self.V[rows][:, self._owned_cols(kb, rank, nranks)]).ravel()
+        buf[:own.size] = own
+        return torch.from_numpy(buf)
+
+    def strip_unpack(self, kb, rows64, nranks, gathered):
+        rows = slice(NB * kb, NB * (kb + rows64))
+        g = gathered.numpy()
+        per = self._strip_doubles(kb, rows64, nranks)
+        for r in range(nranks):
+            cols = self._owned_cols(kb, r, nranks)
+            self.V[rows, cols] = g[r * per:r * per + NB * rows64 * cols.size].reshape(NB * rows64, cols.size)
+
+    def chol_finish(self):
+        n, npad, t = self.n, self.npad, self.Y.shape[1]
+        U = np.triu(self.V[:npad, :npad])
+        W = self.V[:npad, npad:npad + 1 + t]
+        w1, wy = W[:, 0], W[:, 1:]
+        mu = (w1 @ wy) / (w1 @ w1)
+        self.mu = mu
+        self.A = sla.solve_triangular(U, wy - np.outer(w1, mu), lower=False)[:n]
+        self.y_pred = mu + (self.Y - mu) - self.lam * self.A
 
     def solve(self):
-        import scipy.linalg as sla
-        n = self.X.shape[0]
-        q = int(self.q.item())
-        V = self.G.numpy() / q + self.lam * np.eye(n)
-        c = sla.cho_factor(V, lower=True)
-        one = np.ones(n)
-        mu = (one @ sla.cho_solve(c, self.Y)) / (one @ sla.cho_solve(c, one))
-        self.mu = mu
-        self.A = sla.cho_solve(c, self.Y - mu)
-        self.y_pred = mu + (self.Y - mu) - self.lam * self.A
+        """The redundant solve: the same phases on one rank (every tile owned)."""
+        self.chol_prepare()
+        kb, nb = 0, self.npad // NB
+        while kb < nb:
+            g = self.lib.gbm_dev_chol_group_size(self.n, kb)
+            self.chol_group(kb, 0, 1)
+            kb += g
+        self.chol_finish()
 
     def effects(self):
         q = int(self.q.item())
@@ -63,14 +178,25 @@ class NumpyShardStages:
         return dict(B=self.B, y_pred=self.y_pred, mu=self.mu, msum=self.msum.numpy().copy())
 
 
-def _worker(rank, world, port, X, Y, lam, out_dir):
+def _worker(rank, world, port, X, Y, lam, out_dir, env=None):
+    os.environ.update(env or {})
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
     p = X.shape[1]
     per = (p + world - 1) // world
     j0, j1 = rank * per, min(p, (rank + 1) * per)
     st = NumpyShardStages(X[:, j0:j1], Y, lam)
-    out = sharded_gblup_step(st, TorchComm())
-    np.savez(os.path.join(out_dir, f"rank{rank}.npz"), **out, j0=j0)
+    saved = {}
+
+    def mark(label):  # the summed GRM, as the solve receives it
+        if label == "allreduce":
+            saved["G"], saved["q"] = st.G.clone(), st.q.clone()
+
+    out = sharded_gblup_step(st, TorchComm(), events=mark)
+    # the redundant solve on the same summed G (what one rank alone computes from it)
+    st.G.copy_(saved["G"])
+    st.q.copy_(saved["q"])
+    st.solve()
+    np.savez(os.path.join(out_dir, f"rank{rank}.npz"), **out, j0=j0, y_redundant=st.y_pred, packs=st.packs)
     dist.barrier()
     dist.destroy_process_group()
 
@@ -99,3 +225,28 @@ def test_sharded_step_gloo_matches_full_problem(tmp_path, world):
     b_hat = assemble_b_hat(outs[0]["mu"], outs[0]["msum"], [o["B"] for o in outs], p)
     assert np.abs(b_hat - ref["b_hat"]).max() < 1e-9 * np.abs(ref["b_hat"]).max()
     assert b_hat[1 + 7, 0] == 0.0
+
+
+@pytest.mark.parametrize("world", [2, 8])
+def test_sharded_step_gloo_distributed_solve_bit_identical(tmp_path, world):
+    """World size 8 as on the north star's 8-GPU node (and 2): packed partial-GRM all-reduce, then the
+    distributed factorisation forced on at a small n (GBM_DIST_SOLVE_MIN_N = 0, a 128-row redundant
+    tail): 4- and 2-panel groups distributed over the ranks' tile columns (with 8 ranks and 5 tile
+    columns, three ranks own none), strips all-gathered over gloo, the tail redundant. Each rank's
+    distributed solve equals the redundant solve of the same summed G bit for bit, every rank holds
+    the same GEBVs, and the assembled fit matches the oracle on the full problem."""
+    n, p = 600, 1500
+    X = oracle.synth_genotypes(77, n, p)
+    Y = oracle.synth_phenotypes(X, 8, ntraits=2)
+    lam = 0.9
+    env = {"GBM_DIST_SOLVE_MIN_N": "0", "GBM_DIST_TAIL_ROWS": "128"}
+    mp.spawn(_worker, args=(world, _free_port(), X, Y, lam, str(tmp_path), env), nprocs=world, join=True)
+    outs = [dict(np.load(tmp_path / f"rank{r}.npz")) for r in range(world)]
+    ref = oracle.gblup_fit(X, Y, lam)
+    for o in outs:
+        assert int(o["packs"]) == 1  # the packed all-reduce ran
+        assert np.array_equal(o["y_pred"], o["y_redundant"])
+        assert np.array_equal(o["y_pred"], outs[0]["y_pred"])
+    assert np.abs(outs[0]["y_pred"] - ref["y_pred"]).max() < 1e-10 * np.abs(ref["y_pred"]).max()
+    b_hat = assemble_b_hat(outs[0]["mu"], outs[0]["msum"], [o["B"] for o in outs], p)
+    assert np.abs(b_hat - ref["b_hat"]).max() < 1e-9 * np.abs(ref["b_hat"]).max()

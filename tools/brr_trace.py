@@ -1,10 +1,7 @@
-"""Phase timeline of the BRR super-block sweep (GBM_BRR_TRACE=1): runs a C4-shape fit for a few
-iterations and prints, for workgroups 0 and C − 1 of the last sweep, the mean time per super-block
-of each phase (dots + publish, hand-off 1 wait, r̃ + publish, hand-off 2 wait, δ + b + publish,
-hand-off 3 wait, e update); for the look-ahead form (path 3) the steps (A) δ + partial gathers,
-(B) C δ + r̃ publish, (C) e update + dots, (D) r̃ gather + δ publish (path 4, the two-step-slack
-form, has the same marks: its dots are those of s + 2). GBM_BRR_LA2=0 traces path 3, GBM_BRR_LA=0 the
-three-hand-off sweep. Timing tool only; one JSON line."""
+"""Phase timeline of the BRR super-block sweep (GBM_BRR_TRACE=1, path 4): runs a C4-shape fit for a
+few iterations and prints per-workgroup mean times per super-block of the steps (A) δ + partial
+gathers, (B) C δ + r̃ publish, (C) e update + dots (of super-block s + 2), (D) r̃ gather + δ publish.
+Timing tool only; one JSON line."""
 import ctypes
 import json
 import os
