@@ -751,13 +751,16 @@ int allgather_strips(std::vector<std::unique_ptr<Shard>>& shards, const std::vec
 }
 
 // GBLUP solve of V = G/q + λI factored across the device leaders (each holding the summed G): the
-// C-ABI counterpart of gbm.sharded.chol_distributed. Every leader runs each panel
-// group over the full width but the group's trailing update only on its own 128-column tiles; the
-// next group's rows are all-gathered and its diagonal block factored on every leader; once the
+// C-ABI counterpart of gbm.sharded.chol_distributed. Per panel group, the leaders
+// all-gather the group's diagonal area (after an earlier distributed group: its columns were updated
+// by their owners) and factor its first block, every leader runs the group's panels and row updates
+// on its own 128-column tiles (plus the area and the right-hand sides), the group's solved rows are
+// all-gathered (each leader then holds them at every column, with their lower copy), and the
+// trailing update runs on the leader's own tiles and the right-hand sides. Once the
 // trailing matrix is small (GBM_DIST_TAIL_ROWS, default 8192) every remaining row is gathered once
 // and the tail and the back substitution run on every leader. Bit-identical to the redundant
-// launch-per-panel solve (the same kernel computes every tile). Replaces the per-device pinv/
-// Cholesky of V (reference src/gwas.jl:472,595) at multi-GPU scale.
+// launch-per-panel solve (the same kernels compute every tile from the same operands). Replaces the
+// per-device pinv/Cholesky of V (reference src/gwas.jl:472,595) at multi-GPU scale.
 int solve_distributed(std::vector<std::unique_ptr<Shard>>& shards, const std::vector<int>& leaders,
                       const std::vector<int>& ldevs, int64_t n, double inv_q, double lambda, int64_t nrhs) {
   const int64_t npad = npad_of(n), gdim = gdim_of(n), nb = npad / kCholNB;
@@ -780,33 +783,62 @@ int solve_distributed(std::vector<std::unique_ptr<Shard>>& shards, const std::ve
   auto distributable = [&](int64_t kb) {
     return gdim - kCholNB * kb > tail_rows && gbm_dev_chol_group_size(n, kb) >= 2 && (kCholNB * kb) % 128 == 0;
   };
+  // rows [64 kb, 64 (kb + rows64)) of every leader's own tiles, all-gathered. kRows: final U rows
+  // (their lower copy completed too); kRest: the trailing matrix's remaining rows (the tail switch);
+  // kArea: the square diagonal area of a group only
+  enum { kRows, kRest, kArea };
+  auto exchange = [&](int64_t kb, int64_t rows64, int what) -> int {
+    const int64_t cnt = what == kArea ? gbm_dev_chol_area_doubles(n, kb, rows64, R)
+                                      : gbm_dev_chol_strip_doubles(n, kb, rows64, R);
+    GBM_TRY(each([&](int r, FitCtx& c) {
+      GBM_TRY(ensure(c.strip, c.dev, cnt * 8));
+      GBM_TRY(ensure(c.gathered, c.dev, R * cnt * 8));
+      if (what == kArea)
+        return gbm_dev_chol_area_pack((const double*)c.G.p, gdim, n, kb, rows64, r, R, (double*)c.strip.p, c.stream.s);
+      return gbm_dev_chol_strip_pack((const double*)c.G.p, gdim, n, kb, rows64, r, R, (double*)c.strip.p, c.stream.s);
+    }));
+    GBM_TRY(allgather_strips(shards, leaders, cs, cnt));
+    return each([&](int r, FitCtx& c) {
+      const double* gathered = (const double*)c.gathered.p;
+      if (what == kRows)
+        return gbm_dev_chol_strip_unpack_rows((double*)c.G.p, gdim, n, kb, rows64, r, R, gathered, c.stream.s);
+      if (what == kArea) {
+        GBM_TRY(gbm_dev_chol_area_unpack((double*)c.G.p, gdim, n, kb, rows64, R, gathered, c.stream.s));
+      } else {
+        GBM_TRY(gbm_dev_chol_strip_unpack((double*)c.G.p, gdim, n, kb, rows64, R, gathered, c.stream.s));
+      }
+      return gbm_dev_chol_factor_diag((double*)c.G.p, gdim, n, kb, (int32_t*)c.info.p, c.wss.p, c.wss.cap, c.stream.s);
+    });
+  };
   GBM_TRY(each([&](int, FitCtx& c) {
     return gbm_dev_chol_prepare((double*)c.G.p, gdim, n, inv_q, nullptr, lambda, (const double*)c.Y.p, npad, nrhs,
                                 (int32_t*)c.info.p, c.wss.p, c.wss.cap, c.stream.s);
   }));
-  bool dist = distributable(0);
+  bool dist = distributable(0), stale = false;  // stale: a distributed update skipped other ranks' tiles
   for (int64_t kb = 0; kb < nb;) {
     const int64_t g = gbm_dev_chol_group_size(n, kb);
-    const int nr = dist ? R : 1;
+    if (!dist) {
+      GBM_TRY(each([&](int, FitCtx& c) {
+        return gbm_dev_chol_group((double*)c.G.p, gdim, n, kb, 0, 1, (int32_t*)c.info.p, c.wss.p, c.wss.cap, c.stream.s);
+      }));
+      kb += g;
+      continue;
+    }
+    if (stale) GBM_TRY(exchange(kb, g, kArea));
     GBM_TRY(each([&](int r, FitCtx& c) {
-      return gbm_dev_chol_group((double*)c.G.p, gdim, n, kb, dist ? r : 0, nr, (int32_t*)c.info.p, c.wss.p, c.wss.cap,
-                                c.stream.s);
+      return gbm_dev_chol_group_panels((double*)c.G.p, gdim, n, kb, r, R, (int32_t*)c.info.p, c.wss.p, c.wss.cap,
+                                       c.stream.s);
     }));
+    GBM_TRY(exchange(kb, g, kRows));
+    GBM_TRY(each([&](int r, FitCtx& c) {
+      return gbm_dev_chol_group_update((double*)c.G.p, gdim, n, kb, r, R, (int32_t*)c.info.p, c.wss.p, c.wss.cap,
+                                       c.stream.s);
+    }));
+    stale = true;
     kb += g;
-    if (!dist || kb >= nb) continue;
+    if (kb >= nb) break;
     dist = distributable(kb);
-    const int64_t rows64 = dist ? gbm_dev_chol_group_size(n, kb) : nb - kb;
-    const int64_t cnt = gbm_dev_chol_strip_doubles(n, kb, rows64, R);
-    GBM_TRY(each([&](int r, FitCtx& c) {
-      GBM_TRY(ensure(c.strip, c.dev, cnt * 8));
-      GBM_TRY(ensure(c.gathered, c.dev, R * cnt * 8));
-      return gbm_dev_chol_strip_pack((const double*)c.G.p, gdim, n, kb, rows64, r, R, (double*)c.strip.p, c.stream.s);
-    }));
-    GBM_TRY(allgather_strips(shards, leaders, cs, cnt));
-    GBM_TRY(each([&](int, FitCtx& c) {
-      GBM_TRY(gbm_dev_chol_strip_unpack((double*)c.G.p, gdim, n, kb, rows64, R, (const double*)c.gathered.p, c.stream.s));
-      return gbm_dev_chol_factor_diag((double*)c.G.p, gdim, n, kb, (int32_t*)c.info.p, c.wss.p, c.wss.cap, c.stream.s);
-    }));
+    if (!dist) GBM_TRY(exchange(kb, nb - kb, kRest));  // the tail: every remaining row, once
   }
   GBM_TRY(each([&](int, FitCtx& c) {
     return gbm_dev_chol_finish((double*)c.G.p, gdim, n, (const double*)c.Y.p, npad, nrhs, lambda, (double*)c.A.p,

@@ -27,7 +27,7 @@ constexpr int MAXRHS = 63;
 int launch_chol_update(double* G, int64_t ldg, int64_t k0, int64_t nb, int64_t gdim, double* Ld, double* Dinv,
                        int32_t* info, int64_t next_k0, int rank, int nranks, hipStream_t s);
 int launch_chol_row_update(double* G, int64_t ldg, int64_t k0, int kch, int64_t gdim, double* Ld, double* Dinv,
-                           int32_t* info, hipStream_t s);
+                           int32_t* info, hipStream_t s, ColKeep keep = ColKeep{});
 int64_t chol_small_lim();
 void chol_refresh_tuning();
 int64_t chol_flow_flag_bytes(int64_t gdim);
@@ -61,7 +61,7 @@ __global__ void __launch_bounds__(256) prepare_v_kernel(double* __restrict__ G, 
 }
 
 // ---- a diagonal block on its own: the first one, and in a distributed factorisation the first of
-// each panel group after the strip exchange (otherwise the previous trailing update factors it) --
+// each panel group after the area exchange (otherwise the previous trailing update factors it) ---
 __global__ void __launch_bounds__(256) factor_diag_kernel(const double* __restrict__ G, int64_t ld, int64_t k,
                                                           double* __restrict__ Ld, double* __restrict__ Dinv,
                                                           int32_t* __restrict__ info) {
@@ -118,14 +118,17 @@ __global__ void __launch_bounds__(256) chol_strip_kernel(double* __restrict__ G,
 // The solved chunk is also written transposed into the (otherwise unused) lower triangle: L = Uᵀ
 // row-major, so the back substitution and the μ̂ kernel read coalesced rows. Those entries are
 // never overwritten later: every later trailing update covers only rows/cols >= its own origin.
+// keep: in a distributed factorisation's panel phase, only the chunks of this rank's columns (the
+// others arrive through the group's row exchange, chol_lower_copy_kernel adds their lower copy).
 __global__ void __launch_bounds__(256) chol_panel_kernel(double* __restrict__ G, int64_t ld, int64_t k0,
                                                          const double* __restrict__ Ld,
-                                                         const double* __restrict__ Dinv) {
+                                                         const double* __restrict__ Dinv, ColKeep keep) {
   __shared__ __attribute__((aligned(16))) double Us[CNB * PS];
   __shared__ __attribute__((aligned(16))) double X[CNB * PS];
   __shared__ __attribute__((aligned(16))) double Di[4 * 256];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int64_t jx = k0 + ((int64_t)blockIdx.x + 1) * CNB;
+  if (!col_kept(keep, jx)) return;  // (workgroup-uniform)
   {
     const int row = tid >> 2, quarter = tid & 3;
     const double* sl = Ld + (k0 + row) * CNB + quarter * 16;
@@ -155,6 +158,27 @@ __global__ void __launch_bounds__(256) chol_panel_kernel(double* __restrict__ G,
       *reinterpret_cast<double2*>(dl + e) =
           make_double2(X[(quarter * 16 + e) * PS + row], X[(quarter * 16 + e + 1) * PS + row]);
   }
+}
+
+// ---- the transposed lower copy L = Uᵀ of a panel group's rows [r0, r0 + 64 g) for the column chunks
+// another rank solved (received by the group's row exchange): one 64x64 block per workgroup, through
+// LDS, so both the reads of U and the writes of L are coalesced rows. Chunks this rank kept (keep:
+// its own, the group's area, the right-hand sides) were written by its chol_panel_kernel.
+__global__ void __launch_bounds__(256) chol_lower_copy_kernel(double* __restrict__ G, int64_t ld, int64_t r0,
+                                                              int64_t npad, ColKeep keep) {
+  __shared__ double T[CNB][CNB + 1];
+  const int64_t rb = blockIdx.y;                               // panel of the group
+  const int64_t prow = r0 + rb * CNB;                          // its first row
+  const int64_t jx = prow + ((int64_t)blockIdx.x + 1) * CNB;  // chunk right of its diagonal block
+  if (jx >= npad || col_kept(keep, jx)) return;
+  const int tid = threadIdx.x, row = tid >> 2, quarter = tid & 3;
+  const double* su = G + (prow + row) * ld + jx + quarter * 16;
+#pragma unroll
+  for (int e = 0; e < 16; e++) T[row][quarter * 16 + e] = su[e];
+  __syncthreads();
+  double* dl = G + (jx + row) * ld + prow + quarter * 16;
+#pragma unroll
+  for (int e = 0; e < 16; e++) dl[e] = T[quarter * 16 + e][row];
 }
 
 // ---- inverses of all diagonal blocks U_bb (one workgroup per block, all in parallel) --------
@@ -404,39 +428,58 @@ int solve_prepare(double* G, int64_t ldg, int64_t n, double inv_q, const int64_t
 
 // One panel group at 64-block kb (its diagonal block already factored): the group's first panel,
 // the rows of its later panels brought up to date with the earlier ones (row updates, K = 64 j,
-// each factoring its diagonal block), their panels, then one K = 64 g trailing update, whose first
-// workgroup factors the next diagonal block. Distributed (nranks > 1): everything but the trailing
-// update is done by every rank over the full width; the trailing update covers this rank's tile
-// columns only, and the next diagonal block is left to gbm_dev_chol_factor_diag after the strip
-// exchange.
-int solve_group(double* G, int64_t ldg, int64_t n, int64_t kb, int rank, int nranks, int32_t* info, void* workspace,
-                hipStream_t s, int64_t* g_out) {
+// each factoring its diagonal block), their panels (panels_only: stop here), then one K = 64 g
+// trailing update, whose first workgroup factors the next diagonal block.
+// keep (distributed panel phase, nranks > 1): the panels and row updates cover this rank's columns,
+// the group's diagonal area and the right-hand sides only.
+int solve_group_panels(double* G, int64_t ldg, int64_t n, int64_t kb, ColKeep keep, int32_t* info, void* workspace,
+                       hipStream_t s, int64_t* g_out) {
   const int64_t npad = npad_of(n), gdim = gdim_of(n), nb = npad / NB;
   const SolveWs w = solve_ws(workspace, npad);
   const int64_t k0 = kb * NB;
   const int g = group_size(kb, nb, gdim);
-  if (nranks > 1 && (g < 2 || (k0 % 128) != 0))
-    return fail(GBM_E_ARG, "gbm_dev_chol_group: a distributed step needs a panel group of >= 2 panels on a 128-row "
-                           "boundary (finish the tail with nranks = 1)");
+  if (keep.nranks > 1) {
+    if (g < 2 || (k0 % 128) != 0)
+      return fail(GBM_E_ARG, "gbm_dev_chol_group_panels: a distributed step needs a panel group of >= 2 panels on a "
+                             "128-row boundary (finish the tail with gbm_dev_chol_group, nranks = 1)");
+    keep.keep_hi = k0 + g * NB;
+    keep.rhs0 = npad;
+  }
   auto panel = [&](int64_t k) {
     const int64_t chunks = (gdim - k) / NB - 1;  // column chunks right of the diagonal block
-    chol_panel_kernel<<<(unsigned)chunks, 256, 0, s>>>(G, ldg, k, w.Ld, w.Dinv);
+    chol_panel_kernel<<<(unsigned)chunks, 256, 0, s>>>(G, ldg, k, w.Ld, w.Dinv, keep);
     return hipGetLastError() == hipSuccess;
   };
   if (!panel(k0)) return fail(GBM_E_HIP, "chol_panel_kernel launch failed");
-  int rc;
-  if (g > 1) {
-    for (int j = 1; j < g; j++) {
-      rc = launch_chol_row_update(G, ldg, k0, j, gdim, w.Ld, w.Dinv, info, s);
-      if (rc != GBM_OK) return rc;
-      if (!panel(k0 + j * NB)) return fail(GBM_E_HIP, "chol_panel_kernel launch failed");
-    }
-    rc = launch_chol_update(G, ldg, k0, g * NB, gdim, w.Ld, w.Dinv, info, k0 + g * NB, rank, nranks, s);
-  } else {
-    rc = launch_chol_update(G, ldg, k0, NB, gdim, w.Ld, w.Dinv, info, kb + 1 < nb ? k0 + NB : -1, 0, 1, s);
+  for (int j = 1; j < g; j++) {
+    GBM_TRY(launch_chol_row_update(G, ldg, k0, j, gdim, w.Ld, w.Dinv, info, s, keep));
+    if (!panel(k0 + j * NB)) return fail(GBM_E_HIP, "chol_panel_kernel launch failed");
   }
   if (g_out) *g_out = g;
-  return rc;
+  return GBM_OK;
+}
+
+// The group's trailing update (its first workgroup factors the next diagonal block). nranks > 1:
+// this rank's tile columns and the right-hand sides, once the group's rows are complete on every
+// rank (row exchange + gbm_dev_chol_strip_unpack_rows); the next diagonal block is factored after
+// the next group's area exchange (gbm_dev_chol_area_* + gbm_dev_chol_factor_diag).
+int solve_group_update(double* G, int64_t ldg, int64_t n, int64_t kb, int rank, int nranks, int32_t* info,
+                       void* workspace, hipStream_t s) {
+  const int64_t npad = npad_of(n), gdim = gdim_of(n), nb = npad / NB;
+  const SolveWs w = solve_ws(workspace, npad);
+  const int64_t k0 = kb * NB;
+  const int g = group_size(kb, nb, gdim);
+  const int64_t next = kb + g < nb ? k0 + g * NB : -1;
+  if (g > 1) return launch_chol_update(G, ldg, k0, g * NB, gdim, w.Ld, w.Dinv, info, next, rank, nranks, s);
+  if (nranks > 1) return fail(GBM_E_ARG, "gbm_dev_chol_group_update: single-panel steps are not distributed");
+  return launch_chol_update(G, ldg, k0, NB, gdim, w.Ld, w.Dinv, info, next, 0, 1, s);
+}
+
+// One whole panel group on one rank (the redundant factorisation and the distributed one's tail).
+int solve_group(double* G, int64_t ldg, int64_t n, int64_t kb, int32_t* info, void* workspace, hipStream_t s,
+                int64_t* g_out) {
+  GBM_TRY(solve_group_panels(G, ldg, n, kb, ColKeep{}, info, workspace, s, g_out));
+  return solve_group_update(G, ldg, n, kb, 0, 1, info, workspace, s);
 }
 
 // After the last panel: inverses of the diagonal blocks, μ̂ and the back-substitution right-hand
@@ -458,12 +501,13 @@ int solve_finish(double* G, int64_t ldg, int64_t n, const double* Y, int64_t ldy
   return GBM_OK;
 }
 
+// area: the square [r0, r0 + rows) x [r0, r0 + rows) only (a panel group's diagonal area)
 void strip_geometry(int64_t n, int64_t kb, int64_t rows64, int nranks, int64_t& r0, int64_t& rows, int64_t& J0,
-                    int64_t& Jend, int64_t& cnt) {
+                    int64_t& Jend, int64_t& cnt, bool area = false) {
   r0 = kb * NB;
   rows = rows64 * NB;
   J0 = r0 / 128;
-  Jend = npad_of(n) / 128;
+  Jend = area ? (r0 + rows + 127) / 128 : npad_of(n) / 128;
   cnt = Jend > J0 ? (Jend - J0 + nranks - 1) / nranks : 0;
 }
 
@@ -491,7 +535,7 @@ extern "C" int gbm_dev_gblup_solve(double* G, int64_t ldg, int64_t n, double inv
   const int64_t nb = npad / NB;
   for (int64_t kb = 0; kb < nb;) {
     int64_t g = 1;
-    GBM_TRY(solve_group(G, ldg, n, kb, 0, 1, info, workspace, s, &g));
+    GBM_TRY(solve_group(G, ldg, n, kb, info, workspace, s, &g));
     kb += g;
   }
   return solve_finish(G, ldg, n, Y, ldy, nrhs, lambda, A_out, gebv, lda, mu, info, workspace, s);
@@ -516,9 +560,29 @@ extern "C" int64_t gbm_dev_chol_group_size(int64_t n, int64_t kb) {
 extern "C" int gbm_dev_chol_group(double* G, int64_t ldg, int64_t n, int64_t kb, int rank, int nranks, int32_t* info,
                                   void* workspace, int64_t ws_bytes, void* stream) {
   GBM_TRY(check_solve_args(G, ldg, n, info, workspace, ws_bytes, "gbm_dev_chol_group"));
+  if (kb < 0 || kb >= npad_of(n) / NB || nranks != 1 || rank != 0)
+    return fail(GBM_E_ARG, "gbm_dev_chol_group: one rank only (rank 0 of 1); a distributed step is "
+                           "gbm_dev_chol_group_panels + row exchange + gbm_dev_chol_group_update");
+  return solve_group(G, ldg, n, kb, info, workspace, (hipStream_t)stream, nullptr);
+}
+
+extern "C" int gbm_dev_chol_group_panels(double* G, int64_t ldg, int64_t n, int64_t kb, int rank, int nranks,
+                                         int32_t* info, void* workspace, int64_t ws_bytes, void* stream) {
+  GBM_TRY(check_solve_args(G, ldg, n, info, workspace, ws_bytes, "gbm_dev_chol_group_panels"));
   if (kb < 0 || kb >= npad_of(n) / NB || nranks < 1 || rank < 0 || rank >= nranks)
-    return fail(GBM_E_ARG, "gbm_dev_chol_group: bad step or rank");
-  return solve_group(G, ldg, n, kb, rank, nranks, info, workspace, (hipStream_t)stream, nullptr);
+    return fail(GBM_E_ARG, "gbm_dev_chol_group_panels: bad step or rank");
+  ColKeep keep;
+  keep.rank = rank;
+  keep.nranks = nranks;
+  return solve_group_panels(G, ldg, n, kb, keep, info, workspace, (hipStream_t)stream, nullptr);
+}
+
+extern "C" int gbm_dev_chol_group_update(double* G, int64_t ldg, int64_t n, int64_t kb, int rank, int nranks,
+                                         int32_t* info, void* workspace, int64_t ws_bytes, void* stream) {
+  GBM_TRY(check_solve_args(G, ldg, n, info, workspace, ws_bytes, "gbm_dev_chol_group_update"));
+  if (kb < 0 || kb >= npad_of(n) / NB || nranks < 1 || rank < 0 || rank >= nranks)
+    return fail(GBM_E_ARG, "gbm_dev_chol_group_update: bad step or rank");
+  return solve_group_update(G, ldg, n, kb, rank, nranks, info, workspace, (hipStream_t)stream);
 }
 
 extern "C" int gbm_dev_chol_factor_diag(double* G, int64_t ldg, int64_t n, int64_t kb, int32_t* info, void* workspace,
@@ -539,13 +603,15 @@ extern "C" int64_t gbm_dev_chol_strip_doubles(int64_t n, int64_t kb, int64_t row
 }
 
 static int strip_launch(double* G, int64_t ldg, int64_t n, int64_t kb, int64_t rows64, int rank, int nranks,
-                        double* buf, int unpack, hipStream_t s) {
+                        double* buf, int unpack, hipStream_t s, bool area = false) {
   if (!G || !buf || n < 1 || ldg < gdim_of(n) || kb < 0 || rows64 < 1 || (kb * NB) % 128 != 0 || nranks < 1 ||
       rank < 0 || rank >= nranks || (kb + rows64) * NB > npad_of(n))
     return fail(GBM_E_ARG, "gbm_dev_chol_strip_pack/unpack: bad arguments (strip rows inside [0, npad), "
                            "starting on a 128-row boundary)");
+  if (area && (rows64 & 1))
+    return fail(GBM_E_ARG, "gbm_dev_chol_area_pack/unpack: the area must end on a 128-row boundary");
   int64_t r0, rows, J0, Jend, cnt;
-  strip_geometry(n, kb, rows64, nranks, r0, rows, J0, Jend, cnt);
+  strip_geometry(n, kb, rows64, nranks, r0, rows, J0, Jend, cnt, area);
   if (cnt == 0) return GBM_OK;
   const int64_t total = cnt * rows * 64 * (unpack ? nranks : 1);
   const int64_t want = (total + 255) / 256;
@@ -563,6 +629,43 @@ extern "C" int gbm_dev_chol_strip_pack(const double* G, int64_t ldg, int64_t n, 
 extern "C" int gbm_dev_chol_strip_unpack(double* G, int64_t ldg, int64_t n, int64_t kb, int64_t rows64, int nranks,
                                          const double* gathered, void* stream) {
   return strip_launch(G, ldg, n, kb, rows64, 0, nranks, const_cast<double*>(gathered), 1, (hipStream_t)stream);
+}
+
+extern "C" int64_t gbm_dev_chol_area_doubles(int64_t n, int64_t kb, int64_t rows64, int nranks) {
+  if (nranks < 1 || kb < 0 || rows64 < 1) return 0;
+  int64_t r0, rows, J0, Jend, cnt;
+  strip_geometry(n, kb, rows64, nranks, r0, rows, J0, Jend, cnt, true);
+  return cnt * rows * 128;
+}
+
+extern "C" int gbm_dev_chol_area_pack(const double* G, int64_t ldg, int64_t n, int64_t kb, int64_t rows64, int rank,
+                                      int nranks, double* buf, void* stream) {
+  return strip_launch(const_cast<double*>(G), ldg, n, kb, rows64, rank, nranks, buf, 0, (hipStream_t)stream, true);
+}
+
+extern "C" int gbm_dev_chol_area_unpack(double* G, int64_t ldg, int64_t n, int64_t kb, int64_t rows64, int nranks,
+                                        const double* gathered, void* stream) {
+  return strip_launch(G, ldg, n, kb, rows64, 0, nranks, const_cast<double*>(gathered), 1, (hipStream_t)stream, true);
+}
+
+extern "C" int gbm_dev_chol_strip_unpack_rows(double* G, int64_t ldg, int64_t n, int64_t kb, int64_t rows64, int rank,
+                                              int nranks, const double* gathered, void* stream) {
+  if (rank < 0 || rank >= nranks) return fail(GBM_E_ARG, "gbm_dev_chol_strip_unpack_rows: bad rank");
+  hipStream_t s = (hipStream_t)stream;
+  GBM_TRY(strip_launch(G, ldg, n, kb, rows64, 0, nranks, const_cast<double*>(gathered), 1, s));
+  // the lower copy of the chunks other ranks solved (this rank's panel kernels wrote its own)
+  const int64_t npad = npad_of(n), r0 = kb * NB;
+  ColKeep keep;
+  keep.rank = rank;
+  keep.nranks = nranks;
+  keep.keep_hi = r0 + rows64 * NB;
+  keep.rhs0 = npad;
+  const int64_t chunks = (npad - r0) / NB - 1;
+  if (chunks > 0 && nranks > 1) {
+    chol_lower_copy_kernel<<<dim3((unsigned)chunks, (unsigned)rows64), 256, 0, s>>>(G, ldg, r0, npad, keep);
+    GBM_LAUNCH_CHECK();
+  }
+  return GBM_OK;
 }
 
 extern "C" int gbm_dev_chol_finish(double* G, int64_t ldg, int64_t n, const double* Y, int64_t ldy, int64_t nrhs,

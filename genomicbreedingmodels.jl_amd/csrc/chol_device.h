@@ -10,6 +10,18 @@ typedef double d4 __attribute__((ext_vector_type(4)));
 constexpr int CNB = 64;        // Cholesky block (== kCholNB)
 constexpr int PS = CNB + 16;   // LDS pitch of 64x64 images: fragment reads conflict-free
 
+// Columns a rank computes in the panel phase of a distributed factorisation (chol.hip): its own
+// 128-column tiles (J ≡ rank mod nranks), plus, on every rank, the columns left of keep_hi (the
+// panel group's own diagonal area, which the group's later panels read) and the bordered
+// right-hand sides from rhs0 on. nranks = 1: every column.
+struct ColKeep {
+  int32_t rank = 0, nranks = 1;
+  int64_t keep_hi = 0, rhs0 = INT64_MAX;
+};
+__device__ __forceinline__ bool col_kept(const ColKeep& k, int64_t col) {
+  return k.nranks == 1 || col < k.keep_hi || col >= k.rhs0 || (col / 128) % k.nranks == k.rank;
+}
+
 __device__ __forceinline__ double rsqrt_nr(double a) {  // v_rsq_f64 + one Newton step
   double y = __builtin_amdgcn_rsq(a);
   const double h = 0.5 * a * y;

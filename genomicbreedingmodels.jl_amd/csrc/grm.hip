@@ -694,13 +694,15 @@ constexpr int P64 = 80;  // LDS pitch: the two 16-lane halves of a fragment read
 __global__ void __launch_bounds__(256, 2)
 syrk64_sub_kernel(const double* __restrict__ U, int64_t ldu, int64_t c0, int64_t lim, double* __restrict__ C,
                   int64_t ldc, double* Ld, double* Dinv, int32_t* __restrict__ info,
-                  int64_t fk0, int rowonly, int kchunks) {
+                  int64_t fk0, int rowonly, int kchunks, ColKeep keep) {
   __shared__ __attribute__((aligned(16))) double As[64 * P64];
   __shared__ __attribute__((aligned(16))) double Bs[64 * P64];
   int64_t ti = 0, tj = blockIdx.x;  // rowonly: the first tile row only (the next panel's rows)
   if (!rowonly) tile_of(blockIdx.x, ti, tj);
   const bool diag = ti == tj;
   const int64_t i0 = c0 + ti * 64, j0 = c0 + tj * 64;
+  // a distributed panel phase: only this rank's columns (and the group's area, the right-hand sides)
+  if (rowonly && !col_kept(keep, j0)) return;  // (workgroup-uniform; block 0 is the group's area)
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
   const int fr = lane >> 4, fc = lane & 15;
@@ -803,11 +805,11 @@ int64_t chol_small_lim() { return g_small_lim.load(std::memory_order_relaxed); }
 // that the whole group shares one K = 64 g trailing update); the first workgroup factors the
 // diagonal block at k1 afterwards.
 int launch_chol_row_update(double* G, int64_t ldg, int64_t k0, int kch, int64_t gdim, double* Ld, double* Dinv,
-                           int32_t* info, hipStream_t s) {
+                           int32_t* info, hipStream_t s, ColKeep keep) {
   const int64_t k1 = k0 + 64 * (int64_t)kch;
   const int64_t lim = gdim - k1;
   syrk64_sub_kernel<<<(unsigned)(lim / 64), 256, 0, s>>>(G + k0 * ldg, ldg, k1, lim, G, ldg, Ld, Dinv, info, k1, 1,
-                                                         kch);
+                                                         kch, keep);
   GBM_LAUNCH_CHECK();
   return GBM_OK;
 }
@@ -816,6 +818,8 @@ int launch_chol_row_update(double* G, int64_t ldg, int64_t k0, int kch, int64_t 
 // with k1 = k0 + nb; the first workgroup then factors the diagonal block at next_k0 (if >= 0).
 // 64x64 tiles (syrk64_sub_kernel) for single panels below chol_small_lim() trailing rows (more
 // workgroups for the small trailing matrices of late panels), else the 128x128 tile kernel.
+// Distributed (nranks > 1): this rank's tile columns and the right-hand sides only; the next
+// diagonal block is factored after the ranks exchange its area (gbm_dev_chol_area_*).
 int launch_chol_update(double* G, int64_t ldg, int64_t k0, int64_t nb, int64_t gdim, double* Ld, double* Dinv,
                        int32_t* info, int64_t next_k0, int rank, int nranks, hipStream_t s) {
   const int64_t k1 = k0 + nb;
@@ -828,12 +832,12 @@ int launch_chol_update(double* G, int64_t ldg, int64_t k0, int64_t nb, int64_t g
     own.rank = rank;
     own.nranks = nranks;
     own.rhs_tile = (gdim - kRhsRows) / BT;
-    next_k0 = -1;  // the next diagonal block is factored after the strip exchange
+    next_k0 = -1;  // the next diagonal block is factored after the area exchange
   }
   if (nb == 64 && lim <= chol_small_lim()) {
     const int64_t m = (lim + 63) / 64;
     syrk64_sub_kernel<<<(unsigned)(m * (m + 1) / 2), 256, 0, s>>>(G + k0 * ldg, ldg, k1, lim, G, ldg, Ld, Dinv, info,
-                                                                  next_k0, 0, (int)(nb / 64));
+                                                                  next_k0, 0, (int)(nb / 64), ColKeep{});
     GBM_LAUNCH_CHECK();
     return GBM_OK;
   }

@@ -171,6 +171,63 @@ __global__ void __launch_bounds__(BS) standardize_kernel(const T* Xt, int64_t ld
   if (threadIdx.x == 0 && kept_local) atomicAdd(q_dev, kept_local);
 }
 
+// One locus row per wave: NPL values per lane in registers (lane l holds individuals 64k + l), mean
+// and variance by xor butterflies over the wave (every lane ends with the same bits: each level adds
+// the same two partial sums), no LDS and no workgroup barrier; four rows at a time per workgroup.
+// Same per-row semantics as standardize_kernel (two-pass ddof = 1 variance, eps filter).
+template <int NPL, bool GATHER, typename T>
+__global__ void __launch_bounds__(256) standardize_wave_kernel(const T* Xt, int64_t ldx, int64_t p,
+                                                               const int32_t* __restrict__ idx, int64_t n,
+                                                               double* Zt, int64_t ldz, double* __restrict__ mean,
+                                                               double* __restrict__ sd, int32_t* __restrict__ keep,
+                                                               unsigned long long* __restrict__ q_dev,
+                                                               int center_only, double xs) {
+  const int lane = threadIdx.x & 63;
+  const int64_t w0 = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6), nw = (int64_t)gridDim.x * 4;
+  unsigned long long kept_local = 0;
+  for (int64_t j = w0; j < p; j += nw) {
+    const T* row = Xt + j * ldx;
+    double* zrow = Zt + j * ldz;  // may alias row (in place, T = double)
+    double x[NPL];
+    double s = 0.0;
+#pragma unroll
+    for (int k = 0; k < NPL; k++) {
+      const int64_t i = (int64_t)k * 64 + lane;
+      x[k] = i < n ? load_x(row, GATHER ? idx[i] : i, xs) : 0.0;
+      s += x[k];
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) s += __shfl_xor(s, off, 64);
+    const double m = s / (double)n;
+    double ss = 0.0;
+#pragma unroll
+    for (int k = 0; k < NPL; k++) {
+      const int64_t i = (int64_t)k * 64 + lane;
+      const double d = x[k] - m;
+      ss += i < n ? d * d : 0.0;
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) ss += __shfl_xor(ss, off, 64);
+    double v = n > 1 ? sqrt(ss / (double)(n - 1)) : __builtin_nan("");
+    if (center_only) v = 1.0;  // glmnet standardize=false: centre only, keep every column
+    const bool kp = (v > 2.220446049250313e-16) && isfinite(v);
+    const double r = kp ? 1.0 / v : 0.0;
+#pragma unroll
+    for (int k = 0; k < NPL; k++) {
+      const int64_t i = (int64_t)k * 64 + lane;
+      if (i < ldz) zrow[i] = (kp && i < n) ? (x[k] - m) * r : 0.0;
+    }
+    for (int64_t i = (int64_t)NPL * 64 + lane; i < ldz; i += 64) zrow[i] = 0.0;
+    if (lane == 0) {
+      mean[j] = m;
+      sd[j] = v;
+      keep[j] = kp ? 1 : 0;
+      kept_local += kp ? 1 : 0;
+    }
+  }
+  if (lane == 0 && kept_local) atomicAdd(q_dev, kept_local);
+}
+
 static dim3 row_grid(int64_t ldx, int64_t p) {
   const int64_t gx = (ldx + 1023) / 1024;
   const int64_t gy = p < 65535 ? p : 65535;
@@ -215,6 +272,25 @@ static int launch_standardize(const T* Xt, int64_t ldx, int64_t p, const int32_t
                               hipStream_t s, double xs = 1.0) {
   const unsigned grid = (unsigned)(p < 256 * 16 ? p : 256 * 16);
   auto q = reinterpret_cast<unsigned long long*>(q_dev);
+#ifndef GBM_STD_WAVE
+#define GBM_STD_WAVE 0
+#endif
+  if (GBM_STD_WAVE && n <= 64 * 128) {
+    const int64_t wg = (p + 3) / 4;
+    const unsigned g4 = (unsigned)(wg < 4096 ? wg : 4096);
+#define GBM_STD_W(NPL)                                                                                              \
+  standardize_wave_kernel<NPL, GATHER, T><<<g4, 256, 0, s>>>(Xt, ldx, p, idx, n, Zt, ldz, mean, sd, keep, q, center_only, xs)
+    if (n <= 64 * 16) GBM_STD_W(16);
+    else if (n <= 64 * 32) GBM_STD_W(32);
+    else if (n <= 64 * 48) GBM_STD_W(48);
+    else if (n <= 64 * 64) GBM_STD_W(64);
+    else if (n <= 64 * 80) GBM_STD_W(80);
+    else if (n <= 64 * 96) GBM_STD_W(96);
+    else GBM_STD_W(128);
+#undef GBM_STD_W
+    GBM_LAUNCH_CHECK();
+    return GBM_OK;
+  }
   if (n <= 256 * 4)
     standardize_kernel<256, 4, GATHER, T><<<grid, 256, 0, s>>>(Xt, ldx, p, idx, n, Zt, ldz, mean, sd, keep, q, center_only, xs);
   else if (n <= 256 * 8)

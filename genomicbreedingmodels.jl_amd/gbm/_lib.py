@@ -40,7 +40,8 @@ EXPORTS = (
     "gbm_dev_grm_packed_size", "gbm_dev_grm_pack", "gbm_dev_grm_unpack",
     "gbm_debug_brr_stats", "gbm_debug_brr_shape", "gbm_debug_brr_trace", "gbm_debug_chol_flow_trace",
     "gbm_dev_synth_dosage_i8", "gbm_dev_standardize_i8", "gbm_dev_grm_accumulate", "gbm_dev_marker_effects_i8",
-    "gbm_debug_oom_retries",
+    "gbm_debug_oom_retries", "gbm_dev_chol_group_panels", "gbm_dev_chol_group_update", "gbm_dev_chol_strip_unpack_rows",
+    "gbm_dev_chol_area_doubles", "gbm_dev_chol_area_pack", "gbm_dev_chol_area_unpack",
 )
 
 
@@ -79,6 +80,17 @@ def _declare(lib):
     lib.gbm_dev_chol_group_size.argtypes = [I64, I64]
     lib.gbm_dev_chol_group.restype = I32
     lib.gbm_dev_chol_group.argtypes = [P, I64, I64, I64, I32, I32, P, P, I64, P]
+    for f in ("gbm_dev_chol_group_panels", "gbm_dev_chol_group_update"):
+        getattr(lib, f).restype = I32
+        getattr(lib, f).argtypes = [P, I64, I64, I64, I32, I32, P, P, I64, P]
+    lib.gbm_dev_chol_area_doubles.restype = I64
+    lib.gbm_dev_chol_area_doubles.argtypes = [I64, I64, I64, I32]
+    lib.gbm_dev_chol_area_pack.restype = I32
+    lib.gbm_dev_chol_area_pack.argtypes = [P, I64, I64, I64, I64, I32, I32, P, P]
+    lib.gbm_dev_chol_area_unpack.restype = I32
+    lib.gbm_dev_chol_area_unpack.argtypes = [P, I64, I64, I64, I64, I32, P, P]
+    lib.gbm_dev_chol_strip_unpack_rows.restype = I32
+    lib.gbm_dev_chol_strip_unpack_rows.argtypes = [P, I64, I64, I64, I64, I32, I32, P, P]
     lib.gbm_dev_chol_factor_diag.restype = I32
     lib.gbm_dev_chol_factor_diag.argtypes = [P, I64, I64, I64, P, P, I64, P]
     lib.gbm_dev_chol_strip_doubles.restype = I64

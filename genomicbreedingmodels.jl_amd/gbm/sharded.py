@@ -107,12 +107,15 @@ def chol_distributed(stages, ranks, nranks, allgather, tail_rows=None):
     ``stages``: the ranks this process drives (HipShardStages, each holding the full summed G) —
     one in the one-process-per-GPU run, all of them in a single-process rehearsal; ``ranks``: their
     rank ids; ``allgather(packs)``: one packed strip per local rank -> per local rank the flat
-    concatenation of all ranks' packs. Panel groups run on every rank over the full width, each
-    group's trailing update only on the rank's own 128-column tiles (gbm_dev_chol_group); the next
-    group's rows are then all-gathered and its diagonal block factored. Once the trailing matrix is
-    small (``tail_rows``, GBM_DIST_TAIL_ROWS, default 8192) or the groups shrink to single panels,
-    every remaining row is gathered once and the tail runs redundantly. The result is bit-identical
-    to the redundant solve (the same kernel computes every tile)."""
+    concatenation of all ranks' packs. Per panel group: after an earlier distributed group the
+    group's diagonal area is all-gathered (its columns were updated by their owners) and its first
+    block factored; every rank runs the group's panels and row updates on its own 128-column tiles
+    (plus the area and the right-hand sides; gbm_dev_chol_group_panels), the group's solved rows are
+    all-gathered (strip_unpack_rows also writes their lower copy), then the trailing update runs on
+    the rank's own tiles and the right-hand sides (gbm_dev_chol_group_update).
+    Once the trailing matrix is small (``tail_rows``, GBM_DIST_TAIL_ROWS, default 8192) or the groups
+    shrink to single panels, every remaining row is gathered once and the tail runs redundantly. The
+    result is bit-identical to the redundant solve (the same kernels compute every tile)."""
     import os
     st0 = stages[0]
     lib, n = st0.lib, st0.n
@@ -124,10 +127,24 @@ def chol_distributed(stages, ranks, nranks, allgather, tail_rows=None):
     def distributable(kb):
         return (gdim - 64 * kb > tail_rows and lib.gbm_dev_chol_group_size(n, kb) >= 2 and (64 * kb) % 128 == 0)
 
+    def exchange(kb, rows64, what):  # "rows": a group's final rows; "rest": the tail; "area": a group's area
+        pack = "area_pack" if what == "area" else "strip_pack"
+        packs = [getattr(st, pack)(kb, rows64, r, nranks) for st, r in zip(stages, ranks)]
+        for st, r, gathered in zip(stages, ranks, allgather(packs)):
+            if what == "rows":
+                st.strip_unpack_rows(kb, rows64, r, nranks, gathered)
+                continue
+            if what == "area":
+                st.area_unpack(kb, rows64, nranks, gathered)
+            else:
+                st.strip_unpack(kb, rows64, nranks, gathered)
+            st.chol_factor_diag(kb)
+
     for st in stages:
         st.chol_prepare()
     kb = 0
     dist = nranks > 1 and distributable(0)
+    stale = False  # a distributed update skipped other ranks' tiles
     while kb < nb:
         g = int(lib.gbm_dev_chol_group_size(n, kb))
         if not dist:
@@ -135,17 +152,20 @@ def chol_distributed(stages, ranks, nranks, allgather, tail_rows=None):
                 st.chol_group(kb, 0, 1)
             kb += g
             continue
+        if stale:
+            exchange(kb, g, "area")
         for st, r in zip(stages, ranks):
-            st.chol_group(kb, r, nranks)
+            st.chol_group_panels(kb, r, nranks)
+        exchange(kb, g, "rows")
+        for st, r in zip(stages, ranks):
+            st.chol_group_update(kb, r, nranks)
+        stale = True
         kb += g
         if kb >= nb:
             break
         dist = distributable(kb)
-        rows64 = int(lib.gbm_dev_chol_group_size(n, kb)) if dist else nb - kb
-        packs = [st.strip_pack(kb, rows64, r, nranks) for st, r in zip(stages, ranks)]
-        for st, gathered in zip(stages, allgather(packs)):
-            st.strip_unpack(kb, rows64, nranks, gathered)
-            st.chol_factor_diag(kb)
+        if not dist:  # the tail: every remaining row, once
+            exchange(kb, nb - kb, "rest")
     for st in stages:
         st.chol_finish()
 
@@ -286,6 +306,31 @@ class HipShardStages:
         _lib.check(self.lib.gbm_dev_chol_group(self._p(self.G), self.gdim, self.n, kb, rank, nranks, self._p(self.info),
                                                self._p(self.ws_solve), self.ws_solve_bytes, self._stream()),
                    "chol_group")
+
+    def chol_group_panels(self, kb: int, rank: int, nranks: int):
+        _lib.check(self.lib.gbm_dev_chol_group_panels(self._p(self.G), self.gdim, self.n, kb, rank, nranks,
+                                                      self._p(self.info), self._p(self.ws_solve), self.ws_solve_bytes,
+                                                      self._stream()), "chol_group_panels")
+
+    def chol_group_update(self, kb: int, rank: int, nranks: int):
+        _lib.check(self.lib.gbm_dev_chol_group_update(self._p(self.G), self.gdim, self.n, kb, rank, nranks,
+                                                      self._p(self.info), self._p(self.ws_solve), self.ws_solve_bytes,
+                                                      self._stream()), "chol_group_update")
+
+    def area_pack(self, kb: int, rows64: int, rank: int, nranks: int):
+        cnt = int(self.lib.gbm_dev_chol_area_doubles(self.n, kb, rows64, nranks))
+        buf = self.torch.empty(max(cnt, 1), dtype=self.torch.float64, device=self.dev)[:cnt]
+        _lib.check(self.lib.gbm_dev_chol_area_pack(self._p(self.G), self.gdim, self.n, kb, rows64, rank, nranks,
+                                                   self._p(buf), self._stream()), "area_pack")
+        return buf
+
+    def area_unpack(self, kb: int, rows64: int, nranks: int, gathered):
+        _lib.check(self.lib.gbm_dev_chol_area_unpack(self._p(self.G), self.gdim, self.n, kb, rows64, nranks,
+                                                     self._p(gathered), self._stream()), "area_unpack")
+
+    def strip_unpack_rows(self, kb: int, rows64: int, rank: int, nranks: int, gathered):
+        _lib.check(self.lib.gbm_dev_chol_strip_unpack_rows(self._p(self.G), self.gdim, self.n, kb, rows64, rank, nranks,
+                                                           self._p(gathered), self._stream()), "strip_unpack_rows")
 
     def chol_factor_diag(self, kb: int):
         _lib.check(self.lib.gbm_dev_chol_factor_diag(self._p(self.G), self.gdim, self.n, kb, self._p(self.info),

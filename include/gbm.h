@@ -269,13 +269,22 @@ int gbm_dev_gblup_solve(double* G, int64_t ldg, int64_t n, double inv_q, const i
  * The same solve in phases, for a factorisation distributed over ranks (one process or device per
  * rank, each holding the full summed G): gbm_dev_gblup_solve == prepare; for kb = 0 .. npad/64 − 1
  * step gbm_dev_chol_group_size(n, kb): group(kb, rank = 0, nranks = 1); finish.
- * Distributed (nranks > 1, steps whose group has >= 2 panels and starts on a 128-row boundary):
- * every rank runs each group's panels over the full width, but the group's trailing update only on
- * its own 128-column tiles (J ≡ rank mod nranks; the bordered right-hand-side tile on every rank) —
- * 1/nranks of the O(n³) work. Before the next group, the ranks exchange that group's rows of their
- * tiles (strip_pack → all-gather of gbm_dev_chol_strip_doubles per rank → strip_unpack) and factor
- * its diagonal block (factor_diag); before switching back to nranks = 1 for the tail, they exchange
- * all remaining rows the same way. Replaces the redundant per-rank pinv/Cholesky of V at
+ * Distributed (nranks > 1, groups of >= 2 panels starting on a 128-row boundary), per group:
+ *   [after an earlier distributed group] area_pack(kb, g) → all-gather of gbm_dev_chol_area_doubles
+ *                                   per rank → area_unpack; factor_diag(kb): the group's diagonal
+ *                                   area (64g x 64g), whose columns other ranks updated;
+ *   group_panels(kb, rank, nranks)  the group's panels and row updates on the rank's own 128-column
+ *                                   tiles (J ≡ rank mod nranks), the group's diagonal area and the
+ *                                   right-hand sides;
+ *   strip_pack(kb, g) → all-gather of gbm_dev_chol_strip_doubles per rank → strip_unpack_rows: every
+ *                                   rank then holds the group's final rows at every column (and their
+ *                                   lower copy, which the back substitution reads);
+ *   group_update(kb, rank, nranks)  the trailing update on the rank's own tiles and the right-hand
+ *                                   sides — 1/nranks of the O(n³) work per rank.
+ * Before switching back to nranks = 1 for the tail, the ranks exchange every remaining row once
+ * (strip_pack → all-gather → strip_unpack) and factor its first diagonal block (factor_diag).
+ * gbm_dev_chol_group itself takes rank 0 of 1 only (the arguments stay for ABI stability).
+ * Bit-identical to gbm_dev_gblup_solve. Replaces the redundant per-rank pinv/Cholesky of V at
  * reference src/gwas.jl:472,595 at multi-GPU scale.
  */
 int gbm_dev_chol_prepare(double* G, int64_t ldg, int64_t n, double inv_q, const int64_t* q_dev, double lambda,
@@ -285,6 +294,10 @@ int gbm_dev_chol_prepare(double* G, int64_t ldg, int64_t n, double inv_q, const 
 int64_t gbm_dev_chol_group_size(int64_t n, int64_t kb);
 int gbm_dev_chol_group(double* G, int64_t ldg, int64_t n, int64_t kb, int rank, int nranks, int32_t* info,
                        void* workspace, int64_t ws_bytes, void* stream);
+int gbm_dev_chol_group_panels(double* G, int64_t ldg, int64_t n, int64_t kb, int rank, int nranks, int32_t* info,
+                              void* workspace, int64_t ws_bytes, void* stream);
+int gbm_dev_chol_group_update(double* G, int64_t ldg, int64_t n, int64_t kb, int rank, int nranks, int32_t* info,
+                              void* workspace, int64_t ws_bytes, void* stream);
 int gbm_dev_chol_factor_diag(double* G, int64_t ldg, int64_t n, int64_t kb, int32_t* info, void* workspace,
                              int64_t ws_bytes, void* stream);
 /* Doubles per rank of the strip of rows [64 kb, 64 (kb + rows64)) over the tiles from column 64 kb. */
@@ -294,6 +307,16 @@ int gbm_dev_chol_strip_pack(const double* G, int64_t ldg, int64_t n, int64_t kb,
 /* gathered: nranks consecutive packs (rank order), e.g. the output of an all-gather. */
 int gbm_dev_chol_strip_unpack(double* G, int64_t ldg, int64_t n, int64_t kb, int64_t rows64, int nranks,
                               const double* gathered, void* stream);
+/* The same over the square [64 kb, 64 (kb + rows64)) only (rows64 even): a group's diagonal area. */
+int64_t gbm_dev_chol_area_doubles(int64_t n, int64_t kb, int64_t rows64, int nranks);
+int gbm_dev_chol_area_pack(const double* G, int64_t ldg, int64_t n, int64_t kb, int64_t rows64, int rank,
+                           int nranks, double* buf, void* stream);
+int gbm_dev_chol_area_unpack(double* G, int64_t ldg, int64_t n, int64_t kb, int64_t rows64, int nranks,
+                             const double* gathered, void* stream);
+/* strip_unpack of final factor rows (after group_panels) plus their lower copy for the columns this
+ * rank did not compute. */
+int gbm_dev_chol_strip_unpack_rows(double* G, int64_t ldg, int64_t n, int64_t kb, int64_t rows64, int rank,
+                                   int nranks, const double* gathered, void* stream);
 int gbm_dev_chol_finish(double* G, int64_t ldg, int64_t n, const double* Y, int64_t ldy, int64_t nrhs,
                         double lambda, double* A_out, double* gebv, int64_t lda, double* mu, int32_t* info,
                         void* workspace, int64_t ws_bytes, void* stream);

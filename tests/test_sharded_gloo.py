@@ -4,9 +4,10 @@ that bench.py runs over RCCL, with a numpy stage backend standing in for the HIP
 infrastructure, not the product). The backend restates the stage semantics of gbm.sharded.
 HipShardStages at tile level: the packed partial-GRM all-reduce (upper 128-tiles + q in the last
 slot) and the distributed factorisation protocol of gbm_dev_chol_* (include/gbm.h): per panel group
-every rank factors the group's panels over the full width, updates only its own 128-column tiles
-(J ≡ rank mod R; the bordered right-hand sides on every rank), the next strip is all-gathered and
-its diagonal block factored; the tail runs redundantly. Every tile update is the same numpy op
+the group's diagonal area is all-gathered (its columns' owners updated them) and its first block
+factored, every rank runs the group's panels and row updates on its own 128-column tiles (J ≡ rank
+mod R), the area and the bordered right-hand sides, the group's rows are all-gathered, and the
+trailing update runs on the rank's own tiles and the right-hand sides; the tail runs redundantly. Every tile update is the same numpy op
 whichever rank computes it, so the distributed solve equals the redundant one bit for bit."""
 import os
 import socket
@@ -84,7 +85,8 @@ class NumpyShardStages:
             self.G[i * TB:(i + 1) * TB, j * TB:(j + 1) * TB] = self.Gp[k * TB * TB:(k + 1) * TB * TB].view(TB, TB)
         self.q.fill_(int(self.Gp[-1].item()))
 
-    # ---- the solve in phases (gbm_dev_chol_prepare / group / strip_pack / strip_unpack / factor_diag /
+    # ---- the solve in phases (gbm_dev_chol_prepare / group_panels / strip_pack / strip_unpack_rows /
+    # group_update / area_pack / area_unpack / strip_unpack / factor_diag / group /
     # finish): V = G/q + λI bordered by R = [1, y...], upper factor U, W = U⁻ᵀR in the border ---------
     def chol_prepare(self):
         n, npad, t = self.n, self.npad, self.Y.shape[1]
@@ -102,50 +104,85 @@ class NumpyShardStages:
         A = np.triu(self.V[r, r])
         self.V[r, r] = np.linalg.cholesky(A + np.triu(A, 1).T).T
 
-    def chol_group(self, kb, rank, nranks):
-        V, npad = self.V, self.npad
+    def _chunks(self, c_lo, keep):
+        """The 128-tile column chunks of [c_lo, npad) that ``keep`` selects, then the right-hand sides
+        (every rank's). Both the redundant and the distributed solve apply each op chunk by chunk, so
+        a chunk's bits do not depend on which rank computes it."""
+        out, c = [], c_lo
+        while c < self.npad:
+            c1 = min((c // TB + 1) * TB, self.npad)
+            if keep(c):
+                out.append(slice(c, c1))
+            c = c1
+        return out + [slice(self.npad, self.gdim)]
+
+    def chol_group_panels(self, kb, rank, nranks):
+        """The group's panels and row updates on the kept columns: the rank's own tiles, the group's
+        diagonal area (< keep_hi) and the right-hand sides (gbm_dev_chol_group_panels)."""
+        V = self.V
         g = self.lib.gbm_dev_chol_group_size(self.n, kb)
-        k0, k1 = NB * kb, NB * (kb + g)
+        keep_hi = NB * (kb + g)
+        chunks = lambda lo: self._chunks(lo, lambda c: nranks == 1 or c < keep_hi or (c // TB) % nranks == rank)
         for k in range(kb, kb + g):
             r = slice(NB * k, NB * k + NB)
-            if k > kb:  # this group's earlier panels, over the full width
-                for pj in range(kb, k):
-                    rp = slice(NB * pj, NB * pj + NB)
-                    V[r, NB * k:] -= V[rp, r].T @ V[rp, NB * k:]
+            if k > kb:  # this group's earlier panels
+                for ch in chunks(NB * k):
+                    for pj in range(kb, k):
+                        rp = slice(NB * pj, NB * pj + NB)
+                        V[r, ch] -= V[rp, r].T @ V[rp, ch]
                 self.chol_factor_diag(k)
-            V[r, NB * (k + 1):] = sla.solve_triangular(V[r, r], V[r, NB * (k + 1):], trans="T", lower=False)
-        # trailing update: this rank's 128-column tiles, the bordered right-hand sides on every rank
-        for c0 in range(k1, npad, TB):
-            c1 = min(c0 + TB, npad)
-            if (c0 // TB) % nranks == rank:
-                V[k1:c1, c0:c1] -= V[k0:k1, k1:c1].T @ V[k0:k1, c0:c1]
-        V[k1:npad, npad:] -= V[k0:k1, k1:npad].T @ V[k0:k1, npad:]
-        if nranks == 1 and kb + g < npad // NB:
-            self.chol_factor_diag(kb + g)  # the redundant path factors the next diagonal block itself
+            for ch in chunks(NB * (k + 1)):
+                V[r, ch] = sla.solve_triangular(V[r, r], V[r, ch], trans="T", lower=False)
 
-    def _owned_cols(self, kb, rank, nranks):
-        c = np.arange(NB * kb, self.npad)
+    def chol_group_update(self, kb, rank, nranks):
+        """The trailing update on the rank's own tiles and the right-hand sides; on one rank the next
+        diagonal block is factored too (gbm_dev_chol_group_update)."""
+        V, npad, nb = self.V, self.npad, self.npad // NB
+        g = self.lib.gbm_dev_chol_group_size(self.n, kb)
+        k0, k1 = NB * kb, NB * (kb + g)
+        for ch in self._chunks(k1, lambda c: nranks == 1 or (c // TB) % nranks == rank):
+            rend = min(ch.stop, npad)
+            V[k1:rend, ch] -= V[k0:k1, k1:rend].T @ V[k0:k1, ch]
+        if nranks == 1 and kb + g < nb:
+            self.chol_factor_diag(kb + g)
+
+    def chol_group(self, kb, rank, nranks):
+        assert (rank, nranks) == (0, 1)  # gbm_dev_chol_group: the redundant path only
+        self.chol_group_panels(kb, 0, 1)
+        self.chol_group_update(kb, 0, 1)
+
+    def _owned_cols(self, kb, rank, nranks, end=None):
+        c = np.arange(NB * kb, self.npad if end is None else end)
         return c[(c // TB) % nranks == rank]
 
-    def _strip_doubles(self, kb, rows64, nranks):
+    def _strip_doubles(self, kb, rows64, nranks, end=None):
         """Per-rank pack size, padded to the largest rank's (gbm_dev_chol_strip_doubles): the
         all-gather moves equal pieces."""
-        return NB * rows64 * max(self._owned_cols(kb, r, nranks).size for r in range(nranks))
+        return NB * rows64 * max(self._owned_cols(kb, r, nranks, end).size for r in range(nranks))
 
-    def strip_pack(self, kb, rows64, rank, nranks):
+    def strip_pack(self, kb, rows64, rank, nranks, end=None):
         rows = slice(NB * kb, NB * (kb + rows64))
-        buf = np.zeros(self._strip_doubles(kb, rows64, nranks))
-        own = np.ascontiguousarray(self.V[rows][:, self._owned_cols(kb, rank, nranks)]).ravel()
+        buf = np.zeros(self._strip_doubles(kb, rows64, nranks, end))
+        own = np.ascontiguousarray(self.V[rows][:, self._owned_cols(kb, rank, nranks, end)]).ravel()
         buf[:own.size] = own
         return torch.from_numpy(buf)
 
-    def strip_unpack(self, kb, rows64, nranks, gathered):
+    def strip_unpack(self, kb, rows64, nranks, gathered, end=None):
         rows = slice(NB * kb, NB * (kb + rows64))
         g = gathered.numpy()
-        per = self._strip_doubles(kb, rows64, nranks)
+        per = self._strip_doubles(kb, rows64, nranks, end)
         for r in range(nranks):
-            cols = self._owned_cols(kb, r, nranks)
+            cols = self._owned_cols(kb, r, nranks, end)
             self.V[rows, cols] = g[r * per:r * per + NB * rows64 * cols.size].reshape(NB * rows64, cols.size)
+
+    def area_pack(self, kb, rows64, rank, nranks):  # the square diagonal area (gbm_dev_chol_area_pack)
+        return self.strip_pack(kb, rows64, rank, nranks, end=NB * (kb + rows64))
+
+    def area_unpack(self, kb, rows64, nranks, gathered):
+        self.strip_unpack(kb, rows64, nranks, gathered, end=NB * (kb + rows64))
+
+    def strip_unpack_rows(self, kb, rows64, rank, nranks, gathered):
+        self.strip_unpack(kb, rows64, nranks, gathered)  # (the lower copy is not modelled: finish reads triu)
 
     def chol_finish(self):
         n, npad, t = self.n, self.npad, self.Y.shape[1]
@@ -232,7 +269,7 @@ def test_sharded_step_gloo_distributed_solve_bit_identical(tmp_path, world):
     """World size 8 as on the north star's 8-GPU node (and 2): packed partial-GRM all-reduce, then the
     distributed factorisation forced on at a small n (GBM_DIST_SOLVE_MIN_N = 0, a 128-row redundant
     tail): 4- and 2-panel groups distributed over the ranks' tile columns (with 8 ranks and 5 tile
-    columns, three ranks own none), strips all-gathered over gloo, the tail redundant. Each rank's
+    columns, three ranks own none), each group's rows all-gathered over gloo, the tail redundant. Each rank's
     distributed solve equals the redundant solve of the same summed G bit for bit, every rank holds
     the same GEBVs, and the assembled fit matches the oracle on the full problem."""
     n, p = 600, 1500

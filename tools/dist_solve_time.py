@@ -1,5 +1,6 @@
 """Per-rank cost of the distributed GBLUP factorisation at a C3-like n, on one GPU: rank 0 of R
-runs every panel group (full width) and the trailing updates of its own tiles; the all-gather is
+runs every panel group's panels and trailing update on its own tiles (plus the group's diagonal
+area and the right-hand sides) and both per-group exchanges' pack/unpack; the all-gather is
 replaced by R copies of its own pack (wrong values for the other ranks' columns, so only the timing
 is meaningful). Prints the redundant single-rank solve, the per-rank solve for each R, and the bytes
 each rank would receive per solve. Timing tool only.
