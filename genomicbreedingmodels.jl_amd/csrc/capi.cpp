@@ -43,9 +43,13 @@ struct FitCtx {
   DevBuf Xt, D8, mean, sd, keep, q, G, Gc, wsg, Y, A, gebv, mu, info, wss, B, msum, packed, out, part;
   DevBuf tmp, strip, gathered;   // copy exchanges; the distributed factorisation's strip all-gather
   DevBuf errs, q2;               // streamed fit: per-chunk carry error cells; scratch kept count
+  DevBuf astrip, agathered;      // the distributed factorisation's area all-gather (on the copy stream)
+  hipEvent_t ev_area = nullptr, ev_upd = nullptr;  // area exchange done / next area updated
   ~FitCtx() {
     (void)hipSetDevice(dev);
     for (hipEvent_t e : ev) (void)hipEventDestroy(e);
+    if (ev_area) (void)hipEventDestroy(ev_area);
+    if (ev_upd) (void)hipEventDestroy(ev_upd);
   }
 };
 
@@ -628,20 +632,22 @@ int comm_set(const std::vector<int>& devs, CommSet** out) {
 }
 
 // Copy bytes from one context's buffer to another's on dst's stream (same device or peer).
-int copy_dd(FitCtx& dst, void* d, const FitCtx& src, const void* s, int64_t bytes) {
+int copy_dd(FitCtx& dst, void* d, const FitCtx& src, const void* s, int64_t bytes, hipStream_t on = nullptr) {
   GBM_HIP_TRY(hipSetDevice(dst.dev));
+  if (!on) on = dst.stream.s;
   if (dst.dev == src.dev)
-    GBM_HIP_TRY(hipMemcpyAsync(d, s, (size_t)bytes, hipMemcpyDeviceToDevice, dst.stream.s));
+    GBM_HIP_TRY(hipMemcpyAsync(d, s, (size_t)bytes, hipMemcpyDeviceToDevice, on));
   else
-    GBM_HIP_TRY(hipMemcpyPeerAsync(d, dst.dev, s, src.dev, (size_t)bytes, dst.stream.s));
+    GBM_HIP_TRY(hipMemcpyPeerAsync(d, dst.dev, s, src.dev, (size_t)bytes, on));
   return GBM_OK;
 }
 
-int sync_all(std::vector<std::unique_ptr<Shard>>& shards, const std::vector<int>& which) {
+// copy = true: the contexts' copy streams (the distributed factorisation's area exchange)
+int sync_all(std::vector<std::unique_ptr<Shard>>& shards, const std::vector<int>& which, bool copy = false) {
   for (int k : which) {
     FitCtx& c = shards[k]->x();
     GBM_HIP_TRY(hipSetDevice(c.dev));
-    GBM_HIP_TRY(hipStreamSynchronize(c.stream.s));
+    GBM_HIP_TRY(hipStreamSynchronize(copy ? c.copy.s : c.stream.s));
   }
   return GBM_OK;
 }
@@ -726,28 +732,31 @@ int allreduce_grm(std::vector<std::unique_ptr<Shard>>& shards, int64_t n) {
 
 // All-gather of the leaders' strip packs (cnt doubles each) into every leader's `gathered`, in
 // leader (= rank) order: RCCL across distinct devices, device copies when leaders share one.
+// area = true: the area buffers (astrip -> agathered) on the copy streams.
 int allgather_strips(std::vector<std::unique_ptr<Shard>>& shards, const std::vector<int>& leaders, CommSet* cs,
-                     int64_t cnt) {
+                     int64_t cnt, bool area = false) {
+  auto src = [&](FitCtx& c) { return area ? c.astrip.p : c.strip.p; };
+  auto dst = [&](FitCtx& c) { return (double*)(area ? c.agathered.p : c.gathered.p); };
   if (cs) {
     ncclResult_t r = ncclGroupStart();
     for (size_t k = 0; k < leaders.size() && r == ncclSuccess; k++) {
       FitCtx& c = shards[leaders[k]]->x();
-      r = ncclAllGather(c.strip.p, c.gathered.p, (size_t)cnt, ncclDouble, cs->comms[k], c.stream.s);
+      r = ncclAllGather(src(c), dst(c), (size_t)cnt, ncclDouble, cs->comms[k], area ? c.copy.s : c.stream.s);
     }
     ncclResult_t r2 = ncclGroupEnd();
     if (r != ncclSuccess || r2 != ncclSuccess)
       return fail(GBM_E_RCCL, std::string("ncclAllGather(Cholesky strip): ") + ncclGetErrorString(r != ncclSuccess ? r : r2));
     return GBM_OK;
   }
-  GBM_TRY(sync_all(shards, leaders));  // every pack is complete
+  GBM_TRY(sync_all(shards, leaders, area));  // every pack is complete
   for (int d : leaders) {
     FitCtx& cd = shards[d]->x();
     for (size_t r = 0; r < leaders.size(); r++) {
       FitCtx& cr = shards[leaders[r]]->x();
-      GBM_TRY(copy_dd(cd, (double*)cd.gathered.p + r * cnt, cr, cr.strip.p, cnt * 8));
+      GBM_TRY(copy_dd(cd, dst(cd) + r * cnt, cr, src(cr), cnt * 8, area ? cd.copy.s : cd.stream.s));
     }
   }
-  return sync_all(shards, leaders);  // no copy still reads a pack the next step overwrites
+  return sync_all(shards, leaders, area);  // no copy still reads a pack the next step overwrites
 }
 
 // GBLUP solve of V = G/q + λI factored across the device leaders (each holding the summed G): the
@@ -814,7 +823,42 @@ int solve_distributed(std::vector<std::unique_ptr<Shard>>& shards, const std::ve
     return gbm_dev_chol_prepare((double*)c.G.p, gdim, n, inv_q, nullptr, lambda, (const double*)c.Y.p, npad, nrhs,
                                 (int32_t*)c.info.p, c.wss.p, c.wss.cap, c.stream.s);
   }));
-  bool dist = distributable(0), stale = false;  // stale: a distributed update skipped other ranks' tiles
+  // GBM_DIST_OVERLAP (default 1): the next group's area is updated first and all-gathered on the copy
+  // streams while the rest of the trailing update runs (same kernels, same tiles: same bits)
+  const bool overlap = env_i64("GBM_DIST_OVERLAP", 1) != 0;
+  if (overlap)
+    GBM_TRY(each([&](int, FitCtx& c) -> int {
+      GBM_TRY(ensure_copy_stream(c));
+      if (!c.ev_area) GBM_HIP_TRY(hipEventCreateWithFlags(&c.ev_area, hipEventDisableTiming));
+      if (!c.ev_upd) GBM_HIP_TRY(hipEventCreateWithFlags(&c.ev_upd, hipEventDisableTiming));
+      return GBM_OK;
+    }));
+  auto update = [&](int64_t kb, int64_t lo, int64_t hi) {
+    return each([&](int r, FitCtx& c) {
+      return gbm_dev_chol_group_update_cols((double*)c.G.p, gdim, n, kb, r, R, lo, hi, (int32_t*)c.info.p, c.wss.p,
+                                            c.wss.cap, c.stream.s);
+    });
+  };
+  // the area exchange of the group at kb on the copy streams, after ev_upd (its tiles updated); ends
+  // with ev_area, which the group's panels wait for
+  auto area_async = [&](int64_t kb, int64_t g) -> int {
+    const int64_t cnt = gbm_dev_chol_area_doubles(n, kb, g, R);  // non-increasing over the groups
+    GBM_TRY(each([&](int r, FitCtx& c) -> int {
+      GBM_TRY(ensure(c.astrip, c.dev, cnt * 8));
+      GBM_TRY(ensure(c.agathered, c.dev, R * cnt * 8));
+      GBM_HIP_TRY(hipStreamWaitEvent(c.copy.s, c.ev_upd, 0));
+      return gbm_dev_chol_area_pack((const double*)c.G.p, gdim, n, kb, g, r, R, (double*)c.astrip.p, c.copy.s);
+    }));
+    GBM_TRY(allgather_strips(shards, leaders, cs, cnt, true));
+    return each([&](int, FitCtx& c) -> int {
+      GBM_TRY(gbm_dev_chol_area_unpack((double*)c.G.p, gdim, n, kb, g, R, (const double*)c.agathered.p, c.copy.s));
+      GBM_TRY(gbm_dev_chol_factor_diag((double*)c.G.p, gdim, n, kb, (int32_t*)c.info.p, c.wss.p, c.wss.cap, c.copy.s));
+      GBM_HIP_TRY(hipEventRecord(c.ev_area, c.copy.s));
+      return GBM_OK;
+    });
+  };
+  bool dist = R > 1 && distributable(0), stale = false;  // stale: a distributed update skipped other ranks' tiles
+  bool area_pending = false;                    // the current group's area is being exchanged (overlap)
   for (int64_t kb = 0; kb < nb;) {
     const int64_t g = gbm_dev_chol_group_size(n, kb);
     if (!dist) {
@@ -824,20 +868,39 @@ int solve_distributed(std::vector<std::unique_ptr<Shard>>& shards, const std::ve
       kb += g;
       continue;
     }
-    if (stale) GBM_TRY(exchange(kb, g, kArea));
+    if (area_pending) {
+      GBM_TRY(each([&](int, FitCtx& c) -> int {
+        GBM_HIP_TRY(hipStreamWaitEvent(c.stream.s, c.ev_area, 0));
+        return GBM_OK;
+      }));
+      area_pending = false;
+    } else if (stale) {
+      GBM_TRY(exchange(kb, g, kArea));
+    }
     GBM_TRY(each([&](int r, FitCtx& c) {
       return gbm_dev_chol_group_panels((double*)c.G.p, gdim, n, kb, r, R, (int32_t*)c.info.p, c.wss.p, c.wss.cap,
                                        c.stream.s);
     }));
     GBM_TRY(exchange(kb, g, kRows));
-    GBM_TRY(each([&](int r, FitCtx& c) {
-      return gbm_dev_chol_group_update((double*)c.G.p, gdim, n, kb, r, R, (int32_t*)c.info.p, c.wss.p, c.wss.cap,
-                                       c.stream.s);
-    }));
+    const int64_t k1 = kb + g;
+    const bool next_dist = k1 < nb && distributable(k1);
+    if (overlap && next_dist) {
+      const int64_t area_hi = kCholNB * (k1 + gbm_dev_chol_group_size(n, k1));
+      GBM_TRY(update(kb, kCholNB * k1, area_hi));  // the next group's area first
+      GBM_TRY(each([&](int, FitCtx& c) -> int {
+        GBM_HIP_TRY(hipEventRecord(c.ev_upd, c.stream.s));
+        return GBM_OK;
+      }));
+      GBM_TRY(update(kb, area_hi, gdim));  // the rest (and the right-hand sides) beside the exchange
+      GBM_TRY(area_async(k1, gbm_dev_chol_group_size(n, k1)));
+      area_pending = true;
+    } else {
+      GBM_TRY(update(kb, kCholNB * k1, gdim));
+    }
     stale = true;
-    kb += g;
+    kb = k1;
     if (kb >= nb) break;
-    dist = distributable(kb);
+    dist = next_dist;
     if (!dist) GBM_TRY(exchange(kb, nb - kb, kRest));  // the tail: every remaining row, once
   }
   GBM_TRY(each([&](int, FitCtx& c) {

@@ -25,7 +25,8 @@ constexpr int NB = kCholNB;  // 64
 constexpr int MAXRHS = 63;
 
 int launch_chol_update(double* G, int64_t ldg, int64_t k0, int64_t nb, int64_t gdim, double* Ld, double* Dinv,
-                       int32_t* info, int64_t next_k0, int rank, int nranks, hipStream_t s);
+                       int32_t* info, int64_t next_k0, int rank, int nranks, hipStream_t s, int64_t col_lo = 0,
+                       int64_t col_hi = INT64_MAX);
 int launch_chol_row_update(double* G, int64_t ldg, int64_t k0, int kch, int64_t gdim, double* Ld, double* Dinv,
                            int32_t* info, hipStream_t s, ColKeep keep = ColKeep{});
 int64_t chol_small_lim();
@@ -464,13 +465,14 @@ int solve_group_panels(double* G, int64_t ldg, int64_t n, int64_t kb, ColKeep ke
 // rank (row exchange + gbm_dev_chol_strip_unpack_rows); the next diagonal block is factored after
 // the next group's area exchange (gbm_dev_chol_area_* + gbm_dev_chol_factor_diag).
 int solve_group_update(double* G, int64_t ldg, int64_t n, int64_t kb, int rank, int nranks, int32_t* info,
-                       void* workspace, hipStream_t s) {
+                       void* workspace, hipStream_t s, int64_t col_lo = 0, int64_t col_hi = INT64_MAX) {
   const int64_t npad = npad_of(n), gdim = gdim_of(n), nb = npad / NB;
   const SolveWs w = solve_ws(workspace, npad);
   const int64_t k0 = kb * NB;
   const int g = group_size(kb, nb, gdim);
   const int64_t next = kb + g < nb ? k0 + g * NB : -1;
-  if (g > 1) return launch_chol_update(G, ldg, k0, g * NB, gdim, w.Ld, w.Dinv, info, next, rank, nranks, s);
+  if (g > 1)
+    return launch_chol_update(G, ldg, k0, g * NB, gdim, w.Ld, w.Dinv, info, next, rank, nranks, s, col_lo, col_hi);
   if (nranks > 1) return fail(GBM_E_ARG, "gbm_dev_chol_group_update: single-panel steps are not distributed");
   return launch_chol_update(G, ldg, k0, NB, gdim, w.Ld, w.Dinv, info, next, 0, 1, s);
 }
@@ -583,6 +585,15 @@ extern "C" int gbm_dev_chol_group_update(double* G, int64_t ldg, int64_t n, int6
   if (kb < 0 || kb >= npad_of(n) / NB || nranks < 1 || rank < 0 || rank >= nranks)
     return fail(GBM_E_ARG, "gbm_dev_chol_group_update: bad step or rank");
   return solve_group_update(G, ldg, n, kb, rank, nranks, info, workspace, (hipStream_t)stream);
+}
+
+extern "C" int gbm_dev_chol_group_update_cols(double* G, int64_t ldg, int64_t n, int64_t kb, int rank, int nranks,
+                                              int64_t col_lo, int64_t col_hi, int32_t* info, void* workspace,
+                                              int64_t ws_bytes, void* stream) {
+  GBM_TRY(check_solve_args(G, ldg, n, info, workspace, ws_bytes, "gbm_dev_chol_group_update_cols"));
+  if (kb < 0 || kb >= npad_of(n) / NB || nranks < 2 || rank < 0 || rank >= nranks || col_lo < 0 || col_hi < col_lo)
+    return fail(GBM_E_ARG, "gbm_dev_chol_group_update_cols: bad step, rank (nranks >= 2) or column range");
+  return solve_group_update(G, ldg, n, kb, rank, nranks, info, workspace, (hipStream_t)stream, col_lo, col_hi);
 }
 
 extern "C" int gbm_dev_chol_factor_diag(double* G, int64_t ldg, int64_t n, int64_t kb, int32_t* info, void* workspace,

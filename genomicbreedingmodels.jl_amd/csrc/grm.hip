@@ -54,10 +54,14 @@ enum SyrkMode { kSub = 0, kSplit = 1, kPersist = 2 };
 
 // Column ownership of a distributed Cholesky trailing update (kSub): with nranks > 1 this rank
 // updates only the 128-column tiles J (absolute, column J·128) with J mod nranks == rank, plus the
-// bordered right-hand-side tile column rhs_tile, which every rank keeps current.
+// bordered right-hand-side tile column rhs_tile, which every rank keeps current. The launch grid
+// then covers only those columns: blockIdx.y = c picks the c-th own column J = j_first + c·nranks
+// (c = ncols: the right-hand-side column, when rhs), blockIdx.x the tile row.
 struct TileOwner {
   int32_t rank = 0, nranks = 1;
   int64_t rhs_tile = -1;
+  int64_t j_first = 0, ncols = 0;
+  int32_t rhs = 0;
 };
 
 // acc[m][q] += (NEG ? −1 : 1) Σ_k U[k][i0 + ·] U[k][j0 + ·] over the stages [kstep0, kstep0 + nsteps)
@@ -390,10 +394,14 @@ syrk_kernel(const double* __restrict__ U, int64_t ldu, int64_t K, int64_t c0, in
     return;
   } else {
     int64_t ti, tj;
-    tile_of(wg, ti, tj);
-    if (own.nranks > 1) {  // (workgroup-uniform) another rank's column
-      const int64_t J = c0 / BT + tj;
-      if (J != own.rhs_tile && J % own.nranks != own.rank) return;
+    if (own.nranks > 1) {  // the compact grid over this rank's tile columns
+      const int64_t c = blockIdx.y;
+      const int64_t J = c < own.ncols ? own.j_first + c * own.nranks : own.rhs_tile;
+      tj = J - c0 / BT;
+      ti = blockIdx.x;
+      if (ti > tj) return;  // (workgroup-uniform) below the diagonal
+    } else {
+      tile_of(wg, ti, tj);
     }
     const bool diag = (ti == tj);
     const int64_t i0 = c0 + ti * BT, j0 = c0 + tj * BT;
@@ -818,21 +826,33 @@ int launch_chol_row_update(double* G, int64_t ldg, int64_t k0, int kch, int64_t 
 // with k1 = k0 + nb; the first workgroup then factors the diagonal block at next_k0 (if >= 0).
 // 64x64 tiles (syrk64_sub_kernel) for single panels below chol_small_lim() trailing rows (more
 // workgroups for the small trailing matrices of late panels), else the 128x128 tile kernel.
-// Distributed (nranks > 1): this rank's tile columns and the right-hand sides only; the next
-// diagonal block is factored after the ranks exchange its area (gbm_dev_chol_area_*).
+// Distributed (nranks > 1): this rank's tile columns in [col_lo, col_hi) and, when col_hi >= gdim,
+// the right-hand sides (a launch grid over those columns only); the next diagonal block is factored
+// after the ranks exchange its area (gbm_dev_chol_area_*).
 int launch_chol_update(double* G, int64_t ldg, int64_t k0, int64_t nb, int64_t gdim, double* Ld, double* Dinv,
-                       int32_t* info, int64_t next_k0, int rank, int nranks, hipStream_t s) {
+                       int32_t* info, int64_t next_k0, int rank, int nranks, hipStream_t s, int64_t col_lo,
+                       int64_t col_hi) {
   const int64_t k1 = k0 + nb;
   const int64_t lim = gdim - k1;
   if (lim <= 0) return GBM_OK;
   TileOwner own;
   if (nranks > 1) {
-    if ((k1 % BT) != 0 || nb == 64)
-      return fail(GBM_E_ARG, "distributed Cholesky update: panel groups must start on 128-column tiles");
+    if ((k1 % BT) != 0 || nb == 64 || (col_lo % BT) != 0)
+      return fail(GBM_E_ARG, "distributed Cholesky update: panel groups and column ranges on 128-column tiles");
     own.rank = rank;
     own.nranks = nranks;
     own.rhs_tile = (gdim - kRhsRows) / BT;
-    next_k0 = -1;  // the next diagonal block is factored after the area exchange
+    const int64_t jlo = std::max(k1, col_lo) / BT;
+    const int64_t jhi = std::min((col_hi + BT - 1) / BT, own.rhs_tile);  // regular columns only
+    own.j_first = jlo + ((rank - jlo) % nranks + nranks) % nranks;
+    own.ncols = own.j_first < jhi ? (jhi - own.j_first + nranks - 1) / nranks : 0;
+    own.rhs = col_hi >= gdim ? 1 : 0;
+    if (own.ncols + own.rhs == 0) return GBM_OK;
+    const int64_t m = (lim + BT - 1) / BT;
+    syrk_kernel<kSub><<<dim3((unsigned)m, (unsigned)(own.ncols + own.rhs)), 256, 0, s>>>(
+        G + k0 * ldg, ldg, nb, k1, lim, G, ldg, nullptr, 0, SliceBounds{}, Ld, Dinv, info, -1, own);
+    GBM_LAUNCH_CHECK();
+    return GBM_OK;
   }
   if (nb == 64 && lim <= chol_small_lim()) {
     const int64_t m = (lim + 63) / 64;

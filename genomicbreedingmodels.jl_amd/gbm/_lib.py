@@ -42,6 +42,7 @@ EXPORTS = (
     "gbm_dev_synth_dosage_i8", "gbm_dev_standardize_i8", "gbm_dev_grm_accumulate", "gbm_dev_marker_effects_i8",
     "gbm_debug_oom_retries", "gbm_dev_chol_group_panels", "gbm_dev_chol_group_update", "gbm_dev_chol_strip_unpack_rows",
     "gbm_dev_chol_area_doubles", "gbm_dev_chol_area_pack", "gbm_dev_chol_area_unpack",
+    "gbm_dev_chol_group_update_cols",
 )
 
 
@@ -83,6 +84,8 @@ def _declare(lib):
     for f in ("gbm_dev_chol_group_panels", "gbm_dev_chol_group_update"):
         getattr(lib, f).restype = I32
         getattr(lib, f).argtypes = [P, I64, I64, I64, I32, I32, P, P, I64, P]
+    lib.gbm_dev_chol_group_update_cols.restype = I32
+    lib.gbm_dev_chol_group_update_cols.argtypes = [P, I64, I64, I64, I32, I32, I64, I64, P, P, I64, P]
     lib.gbm_dev_chol_area_doubles.restype = I64
     lib.gbm_dev_chol_area_doubles.argtypes = [I64, I64, I64, I32]
     lib.gbm_dev_chol_area_pack.restype = I32

@@ -93,6 +93,9 @@ def sharded_gblup_step(stages, comm, events=None):
     return out
 
 
+_SIDE_STREAMS = {}  # device -> the distributed solve's side stream
+
+
 def dist_solve_min_n() -> int:
     """Individuals from which a multi-rank step factors V distributed (below, the latency-bound
     solve is cheaper redundantly). GBM_DIST_SOLVE_MIN_N overrides (tests)."""
@@ -112,7 +115,9 @@ def chol_distributed(stages, ranks, nranks, allgather, tail_rows=None):
     block factored; every rank runs the group's panels and row updates on its own 128-column tiles
     (plus the area and the right-hand sides; gbm_dev_chol_group_panels), the group's solved rows are
     all-gathered (strip_unpack_rows also writes their lower copy), then the trailing update runs on
-    the rank's own tiles and the right-hand sides (gbm_dev_chol_group_update).
+    the rank's own tiles and the right-hand sides (gbm_dev_chol_group_update). With overlap
+    (GBM_DIST_OVERLAP, default 1; stages with fork/side/join), the next group's area is updated first
+    and exchanged on a side stream while the rest of the update runs (gbm_dev_chol_group_update_cols).
     Once the trailing matrix is small (``tail_rows``, GBM_DIST_TAIL_ROWS, default 8192) or the groups
     shrink to single panels, every remaining row is gathered once and the tail runs redundantly. The
     result is bit-identical to the redundant solve (the same kernels compute every tile)."""
@@ -126,6 +131,8 @@ def chol_distributed(stages, ranks, nranks, allgather, tail_rows=None):
 
     def distributable(kb):
         return (gdim - 64 * kb > tail_rows and lib.gbm_dev_chol_group_size(n, kb) >= 2 and (64 * kb) % 128 == 0)
+
+    overlap = int(os.environ.get("GBM_DIST_OVERLAP", "1")) != 0 and all(hasattr(st, "fork") for st in stages)
 
     def exchange(kb, rows64, what):  # "rows": a group's final rows; "rest": the tail; "area": a group's area
         pack = "area_pack" if what == "area" else "strip_pack"
@@ -145,6 +152,7 @@ def chol_distributed(stages, ranks, nranks, allgather, tail_rows=None):
     kb = 0
     dist = nranks > 1 and distributable(0)
     stale = False  # a distributed update skipped other ranks' tiles
+    pending = False  # this group's area is being exchanged on the side stream
     while kb < nb:
         g = int(lib.gbm_dev_chol_group_size(n, kb))
         if not dist:
@@ -152,18 +160,36 @@ def chol_distributed(stages, ranks, nranks, allgather, tail_rows=None):
                 st.chol_group(kb, 0, 1)
             kb += g
             continue
-        if stale:
+        if pending:
+            for st in stages:
+                st.join()
+            pending = False
+        elif stale:
             exchange(kb, g, "area")
         for st, r in zip(stages, ranks):
             st.chol_group_panels(kb, r, nranks)
         exchange(kb, g, "rows")
-        for st, r in zip(stages, ranks):
-            st.chol_group_update(kb, r, nranks)
+        k1 = kb + g
+        next_dist = k1 < nb and distributable(k1)
+        if overlap and next_dist:
+            area_hi = 64 * (k1 + int(lib.gbm_dev_chol_group_size(n, k1)))
+            for st, r in zip(stages, ranks):  # the next group's area first
+                st.chol_group_update_cols(kb, r, nranks, 64 * k1, area_hi)
+            for st in stages:
+                st.fork()
+            for st, r in zip(stages, ranks):
+                st.chol_group_update_cols(kb, r, nranks, area_hi, gdim)
+            with stages[0].side():  # (one side stream per device)
+                exchange(k1, int(lib.gbm_dev_chol_group_size(n, k1)), "area")
+            pending = True
+        else:
+            for st, r in zip(stages, ranks):
+                st.chol_group_update(kb, r, nranks)
         stale = True
-        kb += g
+        kb = k1
         if kb >= nb:
             break
-        dist = distributable(kb)
+        dist = next_dist
         if not dist:  # the tail: every remaining row, once
             exchange(kb, nb - kb, "rest")
     for st in stages:
@@ -311,6 +337,29 @@ class HipShardStages:
         _lib.check(self.lib.gbm_dev_chol_group_panels(self._p(self.G), self.gdim, self.n, kb, rank, nranks,
                                                       self._p(self.info), self._p(self.ws_solve), self.ws_solve_bytes,
                                                       self._stream()), "chol_group_panels")
+
+    def chol_group_update_cols(self, kb: int, rank: int, nranks: int, col_lo: int, col_hi: int):
+        _lib.check(self.lib.gbm_dev_chol_group_update_cols(self._p(self.G), self.gdim, self.n, kb, rank, nranks, col_lo,
+                                                           col_hi, self._p(self.info), self._p(self.ws_solve),
+                                                           self.ws_solve_bytes, self._stream()), "chol_group_update_cols")
+
+    # the distributed solve's side stream (one per device, shared by the stages of a rehearsal):
+    # fork = the side stream waits for this device's current stream; side() = a context in which
+    # the stage methods (and a torch collective) run on it; join = the current stream waits for it
+    def _side_stream(self):
+        s = _SIDE_STREAMS.get(self.dev)
+        if s is None:
+            s = _SIDE_STREAMS[self.dev] = self.torch.cuda.Stream(self.dev)
+        return s
+
+    def fork(self):
+        self._side_stream().wait_stream(self.torch.cuda.current_stream(self.dev))
+
+    def side(self):
+        return self.torch.cuda.stream(self._side_stream())
+
+    def join(self):
+        self.torch.cuda.current_stream(self.dev).wait_stream(self._side_stream())
 
     def chol_group_update(self, kb: int, rank: int, nranks: int):
         _lib.check(self.lib.gbm_dev_chol_group_update(self._p(self.G), self.gdim, self.n, kb, rank, nranks,

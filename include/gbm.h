@@ -298,6 +298,13 @@ int gbm_dev_chol_group_panels(double* G, int64_t ldg, int64_t n, int64_t kb, int
                               void* workspace, int64_t ws_bytes, void* stream);
 int gbm_dev_chol_group_update(double* G, int64_t ldg, int64_t n, int64_t kb, int rank, int nranks, int32_t* info,
                               void* workspace, int64_t ws_bytes, void* stream);
+/* group_update restricted to the rank's tiles with columns in [col_lo, col_hi) (col_lo on a 128-column
+ * tile; the right-hand sides when col_hi >= gdim(n)); nranks >= 2. Two calls covering [64 (kb + g),
+ * gdim) equal one group_update: the first (the next group's area) lets the area exchange run beside
+ * the second. */
+int gbm_dev_chol_group_update_cols(double* G, int64_t ldg, int64_t n, int64_t kb, int rank, int nranks,
+                                   int64_t col_lo, int64_t col_hi, int32_t* info, void* workspace, int64_t ws_bytes,
+                                   void* stream);
 int gbm_dev_chol_factor_diag(double* G, int64_t ldg, int64_t n, int64_t kb, int32_t* info, void* workspace,
                              int64_t ws_bytes, void* stream);
 /* Doubles per rank of the strip of rows [64 kb, 64 (kb + rows64)) over the tiles from column 64 kb. */

@@ -1,6 +1,7 @@
 """The distributed GBLUP factorisation (gbm.sharded.chol_distributed over the gbm_dev_chol_* ABI)
 rehearsed in one process: R ranks, each a full copy of the summed G on the one GPU, each updating
-only its own 128-column tiles; the strip all-gather is a concatenation. The factorisation must be
+only its own 128-column tiles; the all-gathers are concatenations (the area exchange on the side
+stream unless GBM_DIST_OVERLAP = 0). The factorisation must be
 bit-identical to the redundant single-rank solve (the same kernel computes every tile) and match
 the oracle. Panel-group thresholds are forced so that 16/8/4/2-panel groups and the single-panel
 tail all occur at test size."""
@@ -40,6 +41,7 @@ def _stages(R, X, Y, lam):
     (3, 1500, ("0", "-1", "-1"), 0),       # 4-panel groups down to the 2-panel / single-panel tail
     (8, 3000, ("0", "0", "0"), 0),         # 16, 8, 4, 2-panel groups, then single panels
     (4, 1030, ("0", "0", "0"), 512),       # ragged n, early switch to the redundant tail
+    (8, 3000, ("0", "0", "0"), "0-seq"),   # as above without the side-stream area exchange
 ])
 def test_distributed_factorisation_bit_identical(monkeypatch, R, n, lims, tail):
     import torch
@@ -50,6 +52,9 @@ def test_distributed_factorisation_bit_identical(monkeypatch, R, n, lims, tail):
     monkeypatch.setenv("GBM_CHOL_G16_LIM", lims[2])
     monkeypatch.setenv("GBM_UPD64_LIM", "128")
     monkeypatch.setenv("GBM_CHOL_FLOW_MAX", "0")  # reference: the redundant launch-per-panel solve
+    if isinstance(tail, str):  # "<rows>-seq": GBM_DIST_OVERLAP = 0
+        monkeypatch.setenv("GBM_DIST_OVERLAP", "0")
+        tail = int(tail.split("-")[0])
     X = oracle.synth_genotypes(n + R, n, 1200)
     Y = oracle.synth_phenotypes(X, 3, ntraits=2)
     ref_st, ranks = _stages(R, X, Y, 0.8)

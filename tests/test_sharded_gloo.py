@@ -9,6 +9,7 @@ factored, every rank runs the group's panels and row updates on its own 128-colu
 mod R), the area and the bordered right-hand sides, the group's rows are all-gathered, and the
 trailing update runs on the rank's own tiles and the right-hand sides; the tail runs redundantly. Every tile update is the same numpy op
 whichever rank computes it, so the distributed solve equals the redundant one bit for bit."""
+import contextlib
 import os
 import socket
 
@@ -134,17 +135,36 @@ class NumpyShardStages:
             for ch in chunks(NB * (k + 1)):
                 V[r, ch] = sla.solve_triangular(V[r, r], V[r, ch], trans="T", lower=False)
 
-    def chol_group_update(self, kb, rank, nranks):
+    def chol_group_update(self, kb, rank, nranks, col_lo=0, col_hi=None):
         """The trailing update on the rank's own tiles and the right-hand sides; on one rank the next
-        diagonal block is factored too (gbm_dev_chol_group_update)."""
+        diagonal block is factored too (gbm_dev_chol_group_update). col_lo/col_hi: the rank's tiles
+        with columns in [col_lo, col_hi), the right-hand sides when col_hi >= gdim
+        (gbm_dev_chol_group_update_cols)."""
         V, npad, nb = self.V, self.npad, self.npad // NB
         g = self.lib.gbm_dev_chol_group_size(self.n, kb)
         k0, k1 = NB * kb, NB * (kb + g)
-        for ch in self._chunks(k1, lambda c: nranks == 1 or (c // TB) % nranks == rank):
+        col_hi = self.gdim if col_hi is None else col_hi
+        keep = lambda c: (nranks == 1 or (c // TB) % nranks == rank) and col_lo <= c < col_hi
+        for ch in self._chunks(k1, keep):
+            if ch.start >= npad and col_hi < self.gdim:
+                continue  # the right-hand sides belong to the call that reaches gdim
             rend = min(ch.stop, npad)
             V[k1:rend, ch] -= V[k0:k1, k1:rend].T @ V[k0:k1, ch]
         if nranks == 1 and kb + g < nb:
             self.chol_factor_diag(kb + g)
+
+    def chol_group_update_cols(self, kb, rank, nranks, col_lo, col_hi):
+        self.chol_group_update(kb, rank, nranks, col_lo, col_hi)
+
+    # the overlap hooks of chol_distributed (streams on the GPU; here the calls run in order)
+    def fork(self):
+        pass
+
+    def side(self):
+        return contextlib.nullcontext()
+
+    def join(self):
+        pass
 
     def chol_group(self, kb, rank, nranks):
         assert (rank, nranks) == (0, 1)  # gbm_dev_chol_group: the redundant path only
