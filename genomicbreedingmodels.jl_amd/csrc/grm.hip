@@ -843,7 +843,7 @@ int launch_chol_update(double* G, int64_t ldg, int64_t k0, int64_t nb, int64_t g
     own.nranks = nranks;
     own.rhs_tile = (gdim - kRhsRows) / BT;
     const int64_t jlo = std::max(k1, col_lo) / BT;
-    const int64_t jhi = std::min((col_hi + BT - 1) / BT, own.rhs_tile);  // regular columns only
+    const int64_t jhi = col_hi >= gdim ? own.rhs_tile : std::min((col_hi + BT - 1) / BT, own.rhs_tile);  // regular only
     own.j_first = jlo + ((rank - jlo) % nranks + nranks) % nranks;
     own.ncols = own.j_first < jhi ? (jhi - own.j_first + nranks - 1) / nranks : 0;
     own.rhs = col_hi >= gdim ? 1 : 0;
