@@ -73,3 +73,33 @@ def test_argument_errors_before_device_use():
         gbm.gblup_arrays(X, np.ones(20))
     with pytest.raises(gbm.GBMError, match="less than 2"):
         gbm.gblup_arrays(X[:1], np.ones(1))
+
+
+def test_distributed_phase_entry_points_check_their_arguments():
+    """The distributed-factorisation phases (include/gbm.h) refuse a bad step, rank or range before
+    any device work (fake, aligned pointers: nothing is dereferenced on the host)."""
+    import ctypes
+    lib = gbm.load_library()
+    n = 3000
+    G = ctypes.c_void_p(1 << 20)  # 16-byte aligned, never touched
+    ws_bytes = lib.gbm_dev_solve_workspace(n, 1)
+    ws, info = ctypes.c_void_p(1 << 21), ctypes.c_void_p(1 << 22)
+    gdim = lib.gbm_dev_gdim(n)
+    E = _lib.GBM_E_ARG
+    # gbm_dev_chol_group is the one-rank step only
+    assert lib.gbm_dev_chol_group(G, gdim, n, 0, 1, 2, info, ws, ws_bytes, None) == E
+    assert "one rank only" in _lib.last_error()
+    # the column-range update needs nranks >= 2 and an ordered range
+    assert lib.gbm_dev_chol_group_update_cols(G, gdim, n, 0, 0, 1, 0, gdim, info, ws, ws_bytes, None) == E
+    assert lib.gbm_dev_chol_group_update_cols(G, gdim, n, 0, 0, 2, 512, 256, info, ws, ws_bytes, None) == E
+    # a rank outside [0, nranks)
+    assert lib.gbm_dev_chol_group_panels(G, gdim, n, 0, 2, 2, info, ws, ws_bytes, None) == E
+    assert lib.gbm_dev_chol_group_update(G, gdim, n, 0, -1, 2, info, ws, ws_bytes, None) == E
+    # a distributed panel phase on a single-panel step (the last block)
+    nb = lib.gbm_dev_npad(n) // 64
+    assert lib.gbm_dev_chol_group_size(n, nb - 1) == 1
+    assert lib.gbm_dev_chol_group_panels(G, gdim, n, nb - 1, 0, 2, info, ws, ws_bytes, None) == E
+    # the area exchange covers a square ending on a 128-row boundary
+    assert lib.gbm_dev_chol_area_pack(G, gdim, n, 0, 3, 0, 2, ctypes.c_void_p(1 << 23), None) == E
+    assert lib.gbm_dev_chol_area_doubles(n, 0, 4, 2) == 1 * 256 * 128  # ⌈2 tiles / 2 ranks⌉ x 256 rows x 128
+    assert lib.gbm_dev_chol_strip_unpack_rows(G, gdim, n, 0, 2, 3, 2, ctypes.c_void_p(1 << 23), None) == E

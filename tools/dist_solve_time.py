@@ -4,7 +4,7 @@ area and the right-hand sides) and both per-group exchanges' pack/unpack; the al
 replaced by R copies of its own pack (wrong values for the other ranks' columns, so only the timing
 is meaningful). Prints the redundant single-rank solve, the per-rank solve for each R, and the bytes
 each rank would receive per solve. Timing tool only.
-Usage: python tools/dist_solve_time.py [n] [R ...]"""
+Usage: python tools/dist_solve_time.py [n] [R ...]   (SKIP_REDUNDANT=1: the distributed solves only)"""
 import json
 import os
 import sys
@@ -42,7 +42,9 @@ def timed(fn, reps=2):
     return min(ts[1:])
 
 
-res = {"n": n, "redundant_solve_s": timed(st.solve)}
+res = {"n": n}
+if not os.environ.get("SKIP_REDUNDANT"):  # (a kernel trace of the distributed solve alone)
+    res["redundant_solve_s"] = timed(st.solve)
 for R in Rs:
     recv = [0]
 
