@@ -23,7 +23,9 @@
 // A worker waits only for tiles of earlier rows or for the chain's step of its row; the chain's
 // step i waits only for the partials of (i, i + 1) and (i + 1, i + 1), which wait only for rows < i
 // and are dequeued first in row i: the launch completes with the chain and one resident worker. Waits are bounded (~1 s,
-// info = −1, as in chol_device.h).
+// info = −1, as in chol_device.h). Round 4: workgroup 1 is the ASSISTANT — it applies each right
+// neighbour's last k-step (k = i − 1) to the worker's partial, so the chain's input no longer waits
+// for a worker's whole epilogue after the chain's own previous step.
 //
 // Hand-off between workgroups (MI355X: per-XCD L2s are not coherent): every byte another
 // workgroup of this launch reads — U tiles in G, Ld, Dinv — is stored write-through (`sc1`
@@ -78,9 +80,11 @@ __device__ __forceinline__ void st1(__amdgpu_buffer_rsrc_t r, uint32_t voff, dou
 // and store of the calling wave: the write-through stores of a hand-off would sit on the chain)
 __device__ __forceinline__ void lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
-// tile flags: kPartial = the accumulated (not yet solved) right neighbour of a diagonal tile,
-// handed to the diagonal task; kFinal = the tile's U (or, on the diagonal, Ld + Dinv) is stored
-constexpr int32_t kPartial = 1, kFinal = 2;
+// tile flags (monotonic): kPartial = the accumulated (not yet solved) partial of a right neighbour or
+// a diagonal tile, handed on; kAssisted = a right neighbour's partial with its last k-step applied
+// by the assistant workgroup (the chain's input); kFinal = the tile's U (or, on the diagonal, Ld +
+// Dinv) is stored
+constexpr int32_t kPartial = 1, kAssisted = 2, kFinal = 3;
 __device__ __forceinline__ bool flag_at_least(const int32_t* f, int32_t v) {
   return __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= v;
 }
@@ -147,7 +151,7 @@ struct ChainSync {
   int dl;      // 4 * step + leaves whose inverse is in Dl
   int64_t tt[4];  // trace: leaf ends
   int64_t ts[4];  // trace: own-leaf starts (after following the earlier leaves)
-  int64_t th[4];  // trace: X2 fetched, Xn fetched, helper waves 0 and 1 done
+  int64_t th[5];  // trace: X2 fetched, Xn fetched, helper waves 0, 1 and 2 done
 };
 __device__ __forceinline__ int lds_poll(int* p) {
   return __builtin_amdgcn_readfirstlane(__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
@@ -404,20 +408,17 @@ __device__ __forceinline__ int factor_block_pipe(double* X, const double* X2, bo
   return bm ? (int)__builtin_ctzll(bm) : -1;
 }
 
-// task t -> tile (i, j): row-major over the upper tile triangle, except that row i's first two
-// slots hold its right neighbour (i, i + 1) and the NEXT row's diagonal tile (i + 1, i + 1), the two
-// partials the chain's step i waits for; so both are dequeued before any tile of row i that waits
-// for that step. (i, j) = (−1, −1): nothing to do (slot (nb − 1, nb)); A_00 needs no task.
-__device__ __forceinline__ void task_tile(int t, int nbc, int& i, int& j) {
-  auto start = [nbc](int r) { return r * nbc - r * (r - 1) / 2; };
-  const double b = 2.0 * nbc + 1.0;
-  int r = (int)((b - sqrt(b * b - 8.0 * (double)t)) * 0.5);
-  if (r < 0) r = 0;
-  while (r > 0 && start(r) > t) r--;
-  while (r + 1 < nbc && start(r + 1) <= t) r++;
+// task t -> tile (i, j): row-major over the upper tile triangle, except that
+//  - row r's first two slots hold its right neighbour (r, r + 1) and the NEXT row's diagonal tile
+//    (r + 1, r + 1), the partials the chain's step r waits for (dequeued before any tile of row r
+//    that waits for that step); (−1, −1) = nothing to do (slot (nb − 1, nb)); A_00 needs no task;
+//  - round 4: the right neighbour of row r ≥ 2 is dequeued two rows early, in row r − 2 right after
+//    (r − 2, r + 1). Its k-loop stops at k = r − 2 (the assistant adds k = r − 1), so everything it
+//    waits for is dequeued before it; the extra head start lets its ≈ r steps (latency-bound, one
+//    workgroup) finish before the assistant needs them.
+__device__ __forceinline__ void orig_slot_tile(int r, int slot, int nb, int& i, int& j) {
   i = r;
-  j = r + (t - start(r));
-  const int nb = nbc - 1;
+  j = r + slot;
   if (j == i) {
     if (i < nb) j = i + 1;  // the right neighbour; slot (nb, nb) stays the Schur block
   } else if (j == i + 1) {
@@ -428,6 +429,29 @@ __device__ __forceinline__ void task_tile(int t, int nbc, int& i, int& j) {
       i = j = -1;
     }
   }
+}
+__device__ __forceinline__ void task_tile(int t, int nbc, int& i, int& j) {
+  const int nb = nbc - 1;
+  auto start0 = [nbc](int r) { return r * nbc - r * (r - 1) / 2; };
+  auto start = [&](int r) {
+    const int lost = (r < nb ? r : nb) - 2, got = r < nb - 2 ? r : nb - 2;
+    return start0(r) - (lost > 0 ? lost : 0) + (got > 0 ? got : 0);
+  };
+  const double b = 2.0 * nbc + 1.0;
+  int r = (int)((b - sqrt(b * b - 8.0 * (double)t)) * 0.5);
+  if (r < 0) r = 0;
+  if (r > nb) r = nb;
+  while (r > 0 && start(r) > t) r--;
+  while (r + 1 <= nb && start(r + 1) <= t) r++;
+  const int s = t - start(r);
+  const int ins = r + 2 <= nb - 1 ? (r <= 1 ? 4 : 3) : 1 << 30;  // row r + 2's neighbour, after (r, r + 3)
+  if (s == ins) {
+    i = r + 2;
+    j = r + 3;
+    return;
+  }
+  const int moved = (r >= 2 && r <= nb - 1) ? 1 : 0;  // this row's own neighbour went two rows up
+  orig_slot_tile(r, s - (s > ins ? 1 : 0) + moved, nb, i, j);
 }
 
 // kTrace: per-task timestamps (s_memrealtime, 100 MHz) into trace[t * 24 ...] for the timeline tool;
@@ -441,13 +465,16 @@ __device__ __forceinline__ void task_tile(int t, int nbc, int& i, int& j) {
 // from LDS — so the chain never waits for its own hand-off. The other workgroups take tasks from
 // the queue (row-major; row i's right neighbour and row i + 1's diagonal tile first, task_tile):
 //   diagonal (i == j < nb, i >= 1): k-loop over k < i − 1, stored as a partial for the chain;
-//   right neighbour (j == i + 1): k-loop over k < i, stored as a partial for the chain;
+//   right neighbour (j == i + 1): k-loop over k < i − 1 (k < i for i = 0), stored as a partial for
+//   the assistant (workgroup 1), which adds the last k-step and hands it to the chain;
 //   other (j > i + 1): k-loop; once (i, i) is final, U_ij = U_ii⁻ᵀ A_ij;
 //   Schur (i == j == nb): k-loop; −WᵀW for the later kernels.
-// Deadlock freedom: the chain's step i waits only for the partials of (i, i + 1) and (i + 1, i + 1),
-// which wait only for tiles of rows < i and are dequeued before every other tile of row i; every
-// worker wait targets the chain's earlier steps or a task dequeued earlier. So the launch completes
-// with the chain and ONE resident worker.
+// Deadlock freedom: the chain's step i waits only for the assisted partial of (i, i + 1) and the
+// partial of (i + 1, i + 1). The assistant's step i waits for the partial of (i, i + 1), the tile
+// (i − 1, i + 1) of the previous row and the chain's step i − 1; the partials wait only for tiles of
+// rows < i and are dequeued before every other tile of row i; every worker wait targets the chain's
+// earlier steps or a task dequeued earlier. So the launch completes with the chain, the assistant
+// and ONE resident worker.
 template <bool kTrace>
 __global__ void __launch_bounds__(256, 1)
 chol_flow_kernel(double* __restrict__ G, int64_t ld, int nbc, double* __restrict__ Ld, double* __restrict__ Dinv,
@@ -508,9 +535,9 @@ chol_flow_kernel(double* __restrict__ G, int64_t ld, int nbc, double* __restrict
       // one wave: a partial tile of G (rows r0.., columns j0..; another workgroup's sc1 stores, seen
       // through its flag) -> dst in LDS, all 32 pieces of 16 bytes per lane in flight at once; the LDS
       // writes only after `gate` (the previous contents are no longer read)
-      auto fetch_tile = [&](double* dst, int64_t r0, const int32_t* f, auto&& gate) {
+      auto fetch_tile = [&](double* dst, int64_t r0, const int32_t* f, int32_t ready, auto&& gate) {
         const __amdgpu_buffer_rsrc_t rG = rsrc(G + r0 * ld, gbytes_rowblk);
-        wave_wait2(f, f, info, lane, kPartial);
+        wave_wait2(f, f, info, lane, ready);
         dbl2 v[32];
 #pragma unroll
         for (int q = 0; q < 32; q++) {
@@ -556,18 +583,20 @@ chol_flow_kernel(double* __restrict__ G, int64_t ld, int nbc, double* __restrict
               }
             }
           }
-          fetch_tile(X2, i0, flags + (int64_t)i * nbc + i + 1,
+          fetch_tile(X2, i0, flags + (int64_t)i * nbc + i + 1, i > 0 ? kAssisted : kPartial,
                      [&]() { lds_wait(&sy.pro, 3 * (i + 1), info, lane); });
           lds_post(&sy.x2, i + 1, lane);
           if (kTrace && lane == 0) sy.th[0] = (int64_t)__builtin_amdgcn_s_memrealtime();
         }
         if (w == 1 && next_diag) {
-          fetch_tile(Xn, j0, flags + (int64_t)(i + 1) * nbc + i + 1, []() {});
+          fetch_tile(Xn, j0, flags + (int64_t)(i + 1) * nbc + i + 1, kPartial, []() {});
           if (kTrace && lane == 0) sy.th[1] = (int64_t)__builtin_amdgcn_s_memrealtime();
         }
         if (w <= 2) {
           // column blocks: wave 0 takes 0 and 3, waves 1 and 2 their own; a column's block rows run in
-          // order on one wave, so only the leaf (sy.dl) and X2 (sy.x2) are waited for
+          // order on one wave, so only the leaf (sy.dl) and X2 (sy.x2) are waited for. (Round 4: moving
+          // column block 3's rows to the wave of the same index balanced the items but was not faster:
+          // wave 2, whose own leaf ends last, then finished last.)
 #pragma unroll 1
           for (int rb = 0; rb < 3; rb++) {
             lds_wait(&sy.x2, i + 1, info, lane);
@@ -575,7 +604,7 @@ chol_flow_kernel(double* __restrict__ G, int64_t ld, int nbc, double* __restrict
             nbr_item(rb, w);
             if (w == 0) nbr_item(rb, 3);
           }
-          if (kTrace && lane == 0) sy.th[2 + (w & 1)] = (int64_t)__builtin_amdgcn_s_memrealtime();
+          if (kTrace && lane == 0) sy.th[2 + w] = (int64_t)__builtin_amdgcn_s_memrealtime();
         }
       };
       // ---- U_ii = chol(A_ii) -> Ld, its 16x16 diagonal inverses -> Dinv (and Dl)
@@ -591,6 +620,7 @@ chol_flow_kernel(double* __restrict__ G, int64_t ld, int nbc, double* __restrict
         ct[9] = sy.th[0];
         ct[14] = sy.th[1];
         ct[15] = sy.th[2] > sy.th[3] ? sy.th[2] : sy.th[3];
+        ct[15] = ct[15] > sy.th[4] ? ct[15] : sy.th[4];
       }
       if (kTrace) ct[8] = (int64_t)__builtin_amdgcn_s_memrealtime();
       // ---- the neighbour's last block row (wave w: column block w); its earlier rows were solved
@@ -625,10 +655,93 @@ chol_flow_kernel(double* __restrict__ G, int64_t ld, int nbc, double* __restrict
         o[2] = -1;
 #pragma unroll
         for (int e = 0; e < 16; e++) o[3 + e] = ct[e];
+        o[22] = sy.th[2];  // helper wave 0 (column blocks 0 and 3) done
+        o[23] = sy.th[4];  // helper wave 2 done
       }
       double* t = Xa;
       Xa = Xn;
       Xn = t;
+    }
+    return;
+  }
+
+  if (blockIdx.x == 1) {
+    // ================================ the assistant ================================
+    // The right neighbour's last k-step, A_i,i+1 −= U_i−1,iᵀ U_i−1,i+1, off the chain's workers: the
+    // worker's partial (k < i − 1) and U_i−1,i+1 are final about a step ahead, so only U_i−1,i (the
+    // chain's previous step) is waited for at the step's start; the chain's input then arrives
+    // ≈ 5 µs earlier than from a worker that first waits for U_i−1,i and then runs its whole
+    // epilogue. Waits: a partial and tiles of row i − 1 (dequeued earlier) and the chain's step i − 1.
+    const int64_t kstep = 4 * ld * 8;
+    for (int i = 1; i < nb; i++) {
+      const int64_t i0 = (int64_t)i * FT, j0 = i0 + FT, k0 = i0 - FT;
+      const __amdgpu_buffer_rsrc_t rT = rsrc(G + i0 * ld, gbytes_rowblk);
+      const __amdgpu_buffer_rsrc_t rK = rsrc(G + k0 * ld, gbytes_rowblk);
+      const int32_t* fP = flags + (int64_t)i * nbc + i + 1;        // the worker's partial
+      const int32_t* fB = flags + (int64_t)(i - 1) * nbc + i + 1;  // U_i−1,i+1
+      const int32_t* fA = flags + (int64_t)(i - 1) * nbc + i;      // U_i−1,i (the chain)
+      wave_wait2(fP, fB, info, lane, kPartial);
+      wave_wait2(fB, fB, info, lane, kFinal);
+      int64_t at[3] = {};
+      if (kTrace) at[0] = (int64_t)__builtin_amdgcn_s_memrealtime();
+      // the chain's U_i−1,i: its flag is loaded BEFORE the operands below, so (vmcnt being in order)
+      // checking it leaves those loads in flight; a poll (a call, which drains loads in flight) only
+      // if it is not set yet
+      int a_ready = 0;
+      if (lane == 0) a_ready = flag_at_least(fA, kFinal) ? 1 : 0;
+      asm volatile("" ::: "memory");  // (the flag load stays ahead of the operand loads)
+      d4 acc[2][2];
+#pragma unroll
+      for (int m = 0; m < 2; m++)
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+          const int64_t row = 32 * wr + 2 * (fr + 4 * r) + m;
+          const dbl2 v = ld2(rT, (uint32_t)((row * ld + j0 + 32 * wc + 2 * fc) * 8), 0);
+          acc[m][0][r] = v.x;
+          acc[m][1][r] = v.y;
+        }
+      const uint32_t offA = (uint32_t)(((int64_t)fr * ld + i0 + 32 * wr + 2 * fc) * 8);
+      const uint32_t offB = (uint32_t)(((int64_t)fr * ld + j0 + 32 * wc + 2 * fc) * 8);
+      dbl2 a[16], b[16];
+#pragma unroll
+      for (int ks = 0; ks < 16; ks++) b[ks] = ld2(rK, offB, (uint32_t)(ks * kstep));
+      if (!__builtin_amdgcn_readfirstlane(a_ready)) wave_wait2(fA, fA, info, lane, kFinal);
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      if (kTrace) at[1] = (int64_t)__builtin_amdgcn_s_memrealtime();
+#pragma unroll
+      for (int ks = 0; ks < 16; ks++) a[ks] = ld2(rK, offA, (uint32_t)(ks * kstep));
+#pragma unroll
+      for (int ks = 0; ks < 16; ks++) {
+        const double na0 = -a[ks].x, na1 = -a[ks].y;
+        acc[0][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(na0, b[ks].x, acc[0][0], 0, 0, 0);
+        acc[0][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(na0, b[ks].y, acc[0][1], 0, 0, 0);
+        acc[1][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(na1, b[ks].x, acc[1][0], 0, 0, 0);
+        acc[1][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(na1, b[ks].y, acc[1][1], 0, 0, 0);
+      }
+#pragma unroll
+      for (int m = 0; m < 2; m++)
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+          const int64_t row = 32 * wr + 2 * (fr + 4 * r) + m;
+          dbl2 v;
+          v.x = acc[m][0][r];
+          v.y = acc[m][1][r];
+          st2(rT, (uint32_t)((row * ld + j0 + 32 * wc + 2 * fc) * 8), v);
+        }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      // a wait timed out somewhere (info = −1): stop before handing on a partial built from stale
+      // operands (the chain then stops at its next publish)
+      if (tid == 0) s_task = __hip_atomic_load(info, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < 0 ? 1 : 0;
+      __syncthreads();
+      if (s_task) return;
+      if (tid == 0) __hip_atomic_store(flags + (int64_t)i * nbc + i + 1, kAssisted, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (kTrace && tid == 0) {  // slots 19-21 of the chain's record of step i
+        int64_t* o = trace + (int64_t)(ntasks + i) * 24;
+        o[19] = at[0];
+        o[20] = at[1];
+        o[21] = (int64_t)__builtin_amdgcn_s_memrealtime();
+      }
+      __syncthreads();  // s_task is rewritten next step
     }
     return;
   }
@@ -655,8 +768,8 @@ chol_flow_kernel(double* __restrict__ G, int64_t ld, int nbc, double* __restrict
     // the chain waits for the diagonal tiles and right neighbours, which wait for the (i, i + 2) tiles
     if ((diag && i < nb) || nbr || j == i + 2) __builtin_amdgcn_s_setprio(2);
     const int64_t i0 = (int64_t)i * FT, j0 = (int64_t)j * FT;
-    // a diagonal tile's last update (k = i − 1) is the chain's
-    const int kend = (diag && i < nb) ? i - 1 : i;
+    // a diagonal tile's last update (k = i − 1) is the chain's, a right neighbour's the assistant's
+    const int kend = ((diag && i < nb) || (nbr && i >= 1)) ? i - 1 : i;
     int64_t tr[16] = {};
     if (kTrace) tr[0] = (int64_t)__builtin_amdgcn_s_memrealtime();
 
@@ -702,14 +815,42 @@ chol_flow_kernel(double* __restrict__ G, int64_t ld, int nbc, double* __restrict
       };
       auto fa = [&](int k) { return flags + (int64_t)k * nbc + i; };
       auto fb = [&](int k) { return flags + (int64_t)k * nbc + j; };
-      wave_wait2(fa(0), fb(0), info, lane);
+      // k-steps known to be final: U_ki and U_kj for k < kr. One vector load checks the flags of the
+      // next 32 steps (lanes 0-31: (k, i), lanes 32-63: (k, j)), so a worker catching up to the
+      // chain polls once per 32 steps: a poll per step (two dependent flag loads in a call, which
+      // drains the step's operand loads in flight) made the k-loop ≈ 2.8 µs per step, and the
+      // chain's neighbour partial (i − 1 steps) late. Bounded like poll2.
+      int kr = 0;
+      bool gave_up = false;  // a wait timed out or another waiter gave up (info = −1): drain, no more waits
+      auto ready_upto = [&](int k) {
+        for (int64_t it = 0; k >= kr && !gave_up; it++) {
+          const int kk = kr + (lane & 31);
+          int ok = 1;
+          if (kk < kend) ok = flag_at_least(lane < 32 ? fa(kk) : fb(kk), kFinal) ? 1 : 0;
+          const unsigned long long bm = __ballot(ok);
+          const unsigned both = (unsigned)bm & (unsigned)(bm >> 32);
+          kr += both == 0xffffffffu ? 32 : __builtin_ctz(~both);
+          if (k < kr) break;
+          if ((it & 255) == 255) {
+            gave_up = __hip_atomic_load(info, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < 0;
+            if (!gave_up && it > ((int64_t)1 << 22)) {
+              if (lane == 0) __hip_atomic_store(info, -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+              gave_up = true;
+            }
+            gave_up = __builtin_amdgcn_readfirstlane((int)gave_up) != 0;
+          }
+          __builtin_amdgcn_s_sleep(1);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      };
+      ready_upto(0);
       issue(a0, b0, 0, 0);
       issue(a1, b1, 0, 1);
       for (int k = 0; k < kend; k++) {
         mfma(a0, b0);
         const bool more = k + 1 < kend;
         if (more) {
-          wave_wait2(fa(k + 1), fb(k + 1), info, lane);
+          ready_upto(k + 1);
           issue(a0, b0, k + 1, 0);
         }
         mfma(a1, b1);
@@ -871,8 +1012,9 @@ int launch_chol_flow(double* G, int64_t ldg, int64_t gdim, double* Ld, double* D
   // runs every tile task in dequeue order beside the chain, which checks that no wait targets a later
   // task
   const char* ew = getenv("GBM_CHOL_FLOW_WGS");
-  const int64_t workers = ew && atoll(ew) > 0 ? atoll(ew) : flow_cus() - 1;
-  const unsigned grid = (unsigned)(1 + (ntasks < workers ? ntasks : (workers < 1 ? 1 : workers)));  // + the chain
+  const int64_t workers = ew && atoll(ew) > 0 ? atoll(ew) : flow_cus() - 2;
+  // + the chain and the assistant
+  const unsigned grid = (unsigned)(2 + (ntasks < workers ? ntasks : (workers < 1 ? 1 : workers)));
   int32_t* q = (int32_t*)flag_block;
   if (getenv("GBM_CHOL_FLOW_TRACE")) {
     // timing tool only: one record of 16 int64 per task, read back by gbm_debug_chol_flow_trace

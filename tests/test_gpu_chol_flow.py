@@ -107,11 +107,13 @@ def test_flow_reports_first_failing_pivot(monkeypatch, bad):
 
 @pytest.mark.parametrize("wgs", ["1", "2", "7"])
 def test_flow_few_resident_workgroups_complete_bit_identical(monkeypatch, wgs):
-    """Deadlock freedom: the chain workgroup waits only for its row's diagonal and
-    neighbour partials, and every worker wait targets the chain's earlier steps or a task dequeued
-    earlier (the right neighbour precedes its diagonal tile), so the launch completes with any
-    number of resident workers — GBM_CHOL_FLOW_WGS caps them, down to one worker running every tile
-    task in dequeue order beside the chain — and gives the bits of the full-grid launch."""
+    """Deadlock freedom: the chain workgroup waits only for its row's diagonal partial
+    and the assistant's neighbour partial, the assistant only for a partial, a tile of the previous
+    row and the chain's previous step, and every worker wait targets the chain's earlier steps or a
+    task dequeued earlier (the right neighbour precedes its diagonal tile), so the launch completes
+    with any number of resident workers — GBM_CHOL_FLOW_WGS caps them, down to one worker running
+    every tile task in dequeue order beside the chain and the assistant — and gives the bits of the
+    full-grid launch."""
     import torch
     monkeypatch.setenv("GBM_CHOL_FLOW_MAX", "1000000")
     X, Y, a, b = _pair(1030, 700, 2, 13, 0.9)

@@ -57,11 +57,33 @@ print("    last leaf end -> factored (sync)     ", f(us(ct[:, 8] - ct[:, 4])))
 print("    X2 (neighbour partial) in LDS, from start", f(us(ct[:, 9] - ct[:, 0])))
 print("    Xn (next diag partial) in LDS, from start", f(us(ct[:, 14] - ct[:, 0])))
 print("    helper block rows done, from start   ", f(us(ct[:, 15] - ct[:, 0])))
+if (Ch[:, 22] > 0).all():
+    print("      wave 0 (column blocks 0, 3), from start", f(us(Ch[:, 22] - ct[:, 0])))
+    print("      wave 2 (column block 2), from start  ", f(us(Ch[:, 23] - ct[:, 0])))
 print("  neighbour solve + Ld stores            ", f(us(ct[:, 10] - ct[:, 8])))
 print("  next tile update (k = i)               ", f(us(ct[:, 11] - ct[:, 10])))
 print("  drain + flags                          ", f(us(ct[:, 12] - ct[:, 11])))
 print("  published -> next step start           ", f(us(ct[1:, 0] - ct[:-1, 12])))
+A = Ch[1:, 19:22]  # the assistant's step i >= 1: partial + U_i-1,i+1 ready, U_i-1,i seen, published
+if (A > 0).all():
+    st1 = ct[1:, 0]
+    print("assistant: partial and U(i-1,i+1) ready, from start", f(us(A[:, 0] - st1)))
+    print("assistant: U(i-1,i) (chain) seen, from start       ", f(us(A[:, 1] - st1)))
+    print("assistant: published, from start                   ", f(us(A[:, 2] - st1)))
 rec = {(int(r[0]), int(r[1])): r for r in W if r[8] > 0}
+if (A > 0).all():  # the assistant's input U(i-1,i+1): when its worker dequeued, finished k, saw the leaves, published
+    T2 = np.array([rec[(i - 1, i + 1)] for i in range(1, nb) if (i - 1, i + 1) in rec])
+    if len(T2) == nb - 1:
+        st1 = ct[1:, 0]
+        for name, col in (("dequeued", 3), ("k-loop done", 4), ("last leaf seen", 6), ("published", 8)):
+            print(f"U(i-1,i+1) worker {name:15s}, from step i start", f(us(T2[:, col] - st1)))
+    T3 = np.array([rec[(i, i + 1)] for i in range(1, nb)])
+    for name, col in (("dequeued", 3), ("k-loop done", 4), ("published", 8)):
+        print(f"partial (i,i+1) worker {name:11s}, from step i start", f(us(T3[:, col] - st1)))
+    T4 = np.array([rec[(i - 2, i + 1)] for i in range(2, nb)])
+    print("U(i-2,i+1) published, from step i start     ", f(us(T4[:, 8] - st1[1:])))
+    T5 = np.array([rec[(i - 2, i)] for i in range(2, nb)])
+    print("U(i-2,i) published, from step i start       ", f(us(T5[:, 8] - st1[1:])))
 # partial readiness: neighbour (i, i+1) and diagonal (i+1, i+1) published vs the chain's need
 nbp = np.array([rec[(i, i + 1)][8] for i in range(nb)])
 dgp = np.array([rec[(i, i)][8] for i in range(1, nb)])

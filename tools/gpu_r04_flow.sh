@@ -1,0 +1,14 @@
+#!/bin/bash
+# Dataflow Cholesky with the assistant workgroup: its tests, the timeline at C2's n, the C2 bench.
+set -o pipefail
+export PYTHONUNBUFFERED=1
+cd /tmp && export TMPDIR=/tmp && cd "${GRAFT_REPO_ROOT:-/root/repo}"
+OUT=gpurun_out/flow4; mkdir -p $OUT
+timeout -k 10 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_gpu_chol_flow.py tests/test_gpu_parity.py > $OUT/tests.log 2>&1 || { tail -30 $OUT/tests.log; exit 1; }
+tail -2 $OUT/tests.log
+timeout -k 10 200 python3 tools/flow_timeline.py > $OUT/flow.txt 2> $OUT/flow.err || { tail $OUT/flow.err; exit 1; }
+cat $OUT/flow.txt
+for r in 1 2; do
+timeout -k 10 300 python bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-host-path > $OUT/b$r.json 2> $OUT/b$r.err || { tail $OUT/b$r.err; exit 1; }
+python3 -c "import json; d=json.load(open('$OUT/b$r.json')); s=d['stage_ms']; print('%.3f'%d['ms_per_step'], ' '.join('%s=%.3f'%(k,v) for k,v in s.items()))"
+done
