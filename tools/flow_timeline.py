@@ -35,6 +35,8 @@ buf = np.zeros((cap, 24), dtype=np.int64)
 got = lib.gbm_debug_chol_flow_trace(buf.ctypes.data, cap)
 assert got == cap, got
 T = buf.astype(np.float64)
+if os.environ.get("FLOW_DUMP"):  # raw records for offline analysis
+    np.save(os.environ["FLOW_DUMP"], buf)
 W = T[:ntasks]
 Ch = T[ntasks:ntasks + nb]  # chain step i: o[3 + e] = ct[e]
 ct = Ch[:, 3:19]

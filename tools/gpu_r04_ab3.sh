@@ -1,5 +1,5 @@
 #!/bin/bash
-# Dataflow Cholesky A/B: in-tree (assistant + 2-step batched worker k-loop) vs variants/libgbm_prebal.so
+# Dataflow Cholesky A/B: in-tree (candidate) vs variants/libgbm_prebal.so
 # (assistant, 1-step batches) vs variants/libgbm_flowhead.so (round-3 kernel); chol_flow tests on the
 # in-tree and kb1 builds, C2 bench stage times, then the in-tree timeline.
 set -o pipefail
