@@ -1,0 +1,531 @@
+// Exact-integer GRM of dosage genotypes on the CDNA4 int8 matrix cores.
+//
+// The GRM of SURVEY.md §8a a3 (reference src/gwas.jl:112-126: Z = standardised X, G = Z Zᵀ/q) when
+// X holds diploid dosages x = d/2, d ∈ {0, 1, 2}. With t_j = Σ_i d_ij and w_j = 1/var(d_·j) (ddof 1;
+// the ploidy cancels: z_ij = (d_ij − t_j/n)·√w_j),
+//
+//   G_ik = Σ_j w_j (d_ij − t_j/n)(d_kj − t_j/n)
+//        = 2^−F/n² · [ n² A_ik − n U_i − n U_k + C ],   A_ik = Σ_j W_j d_ij d_kj,
+//                                                       U_i  = Σ_j W_j t_j d_ij,  C = Σ_j W_j t_j²,
+//
+// with W_j = w_j·2^F an integer: F is chosen so that every locus' fp64 weight w_j is an integer
+// multiple of 2^−F (exact: its 53-bit significand lands on the integer grid) as long as the weights
+// span ≤ 2^16 (xg_choose; beyond that the smallest are rounded to the grid, error ≤ 2^−(69−Δe) each).
+// W_j is cut into S balanced base-128 digits W_j = Σ_s 128^s ω_sj, ω ∈ [−64, 63], so
+// A_ik = Σ_s 128^s Σ_j d_ij (d_kj ω_sj) is S int8 GEMMs whose products d·ω ∈ [−128, 126] fit int8 and
+// whose int32 sums are exact. The bracket is combined in 128-bit integers and rounded to fp64 once
+// (plus the division by n²): the only approximation left is the fp64 rounding of w_j itself — the
+// reference's own fp64 SYRK rounds every product and partial sum instead.
+//
+// Kernels (all stream-ordered, one host sync to size S):
+//   xg_stats_kernel   per locus: t, Σd², mean, sd, keep, q (the standardisation's outputs), w_j, the
+//                     exponent range of the kept weights, a flag for dosages outside {0, 1, 2}
+//   xg_digits_kernel  per locus: the S digits (and doubled digits) in the GEMM's per-stage layout,
+//                     V_j = W_j t_j, block partials of C
+//   xg_transpose_kernel  locus-major dosages → individual-major Dt (the A operand) and St (B: each byte
+//                     a v_perm selector picking 2ω, ω or 0 from the digit dwords)
+//   xg_u_kernel / xg_u_reduce_kernel   n·U_i and C in int128
+//   xg_gemm_kernel<S> 128 x 64 output tiles of the upper triangle; 8 waves of 64 x 16, each holding S x 4
+//                     v_mfma_i32_16x16x64_i8 accumulators; operands staged global → LDS by LDS-DMA into a
+//                     4-deep ring (counted vmcnt, raw barriers); B scaled per slice in registers by one
+//                     v_perm per dword (each scaled fragment feeds 4 MFMAs); the epilogue rebuilds the bracket in int128 and stores fp64 G.
+#include <algorithm>
+#include <climits>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+
+#include "gbm_internal.h"
+
+namespace gbm {
+
+typedef __int128 i128;
+typedef unsigned __int128 u128;
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int XG_BM = 128;       // tile rows (individuals i)
+constexpr int XG_BN = 64;        // tile columns (individuals k)
+constexpr int XG_BK = 128;       // loci per LDS stage (bytes per operand row)
+constexpr int XG_SMIN = 8, XG_SMAX = 10;
+constexpr int XG_WWSTAGE = 4096;  // digit bytes per stage in LDS (S·256 used, one 1-KB DMA piece per wave)
+constexpr int XG_STAGE = XG_BM * XG_BK + XG_BN * XG_BK + XG_WWSTAGE;  // 28 KB
+constexpr int XG_NS = 4;          // ring depth (3 stages in flight)
+constexpr int XG_UBLK = 256;      // threads per block of the U / digits kernels
+
+struct XgInfo {  // device scratch written by the stats kernel, read by the host once
+  unsigned long long wmax_bits;  // the largest kept weight (positive doubles order as their bits)
+  int32_t emin, emax, bad, pad;
+};
+
+__device__ __forceinline__ double i128_to_double(i128 x) {
+  const bool neg = x < 0;
+  const u128 m = neg ? (u128)0 - (u128)x : (u128)x;
+  const uint64_t hi = (uint64_t)(m >> 64), lo = (uint64_t)m;
+  const double r = (double)hi * 18446744073709551616.0 + (double)lo;
+  return neg ? -r : r;
+}
+
+// ---- per-locus statistics (one workgroup per locus row, grid-strided) --------------------------
+__global__ void __launch_bounds__(256) xg_stats_kernel(const int8_t* __restrict__ D, int64_t ldd, int64_t p, int64_t n,
+                                                       double xs, double* __restrict__ mean, double* __restrict__ sd,
+                                                       int32_t* __restrict__ keep, unsigned long long* __restrict__ q_dev,
+                                                       double* __restrict__ w, int64_t* __restrict__ tcol,
+                                                       XgInfo* __restrict__ info) {
+  __shared__ long long red[2][4];
+  __shared__ int badsh;
+  unsigned long long kept_local = 0;
+  for (int64_t j = blockIdx.x; j < p; j += gridDim.x) {
+    const int8_t* row = D + j * ldd;
+    long long t = 0, s2 = 0;
+    int bad = 0;
+    for (int64_t i = threadIdx.x; i < n; i += 256) {
+      const int d = row[i];
+      t += d;
+      s2 += d * d;
+      bad |= (d < 0 || d > 2);
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+      t += __shfl_xor(t, off, 64);
+      s2 += __shfl_xor(s2, off, 64);
+    }
+    bad = __any(bad) ? 1 : 0;
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    __syncthreads();
+    if (threadIdx.x == 0) badsh = 0;
+    __syncthreads();
+    if (lane == 0) {
+      red[0][wv] = t;
+      red[1][wv] = s2;
+      if (bad) badsh = 1;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      t = red[0][0] + red[0][1] + red[0][2] + red[0][3];
+      s2 = red[1][0] + red[1][1] + red[1][2] + red[1][3];
+      // var(d) = (n Σd² − t²)/(n(n − 1)), exact integers up to the division
+      const long long num = (long long)n * s2 - t * t;
+      const bool kp = n > 1 && num > 0;
+      const double dn = (double)n;
+      mean[j] = (double)t * xs / dn;
+      sd[j] = kp ? sqrt((double)num / (dn * (dn - 1.0))) * xs : 0.0;
+      keep[j] = kp ? 1 : 0;
+      kept_local += kp ? 1 : 0;
+      const double wj = kp ? (dn * (dn - 1.0)) / (double)num : 0.0;
+      w[j] = wj;
+      tcol[j] = t;
+      if (kp) {
+        const int e = ilogb(wj);
+        atomicMin(&info->emin, e);
+        atomicMax(&info->emax, e);
+        atomicMax(&info->wmax_bits, (unsigned long long)__double_as_longlong(wj));
+      }
+      if (badsh) atomicOr(&info->bad, 1);
+    }
+  }
+  if (threadIdx.x == 0 && kept_local) atomicAdd(q_dev, kept_local);
+}
+
+__global__ void xg_info_init_kernel(XgInfo* info) {
+  info->wmax_bits = 0;
+  info->emin = INT_MAX;
+  info->emax = INT_MIN;
+  info->bad = 0;
+  info->pad = 0;
+}
+
+// ---- digits: W_j = w_j 2^F → S balanced base-128 digits in the GEMM's stage layout -----------------
+// Stage layout (per 128-locus stage, S·256 bytes): [s][chunk c = 0..7][32 B: ω of loci 16c..16c+15,
+// then 2ω of the same loci].
+__global__ void __launch_bounds__(XG_UBLK) xg_digits_kernel(const double* __restrict__ w, const int64_t* __restrict__ tcol,
+                                                            int64_t p, int64_t kp, int S, int F,
+                                                            int8_t* __restrict__ WW, i128* __restrict__ V,
+                                                            i128* __restrict__ Cpart, XgInfo* __restrict__ info) {
+  __shared__ i128 red[XG_UBLK];
+  const int64_t j = (int64_t)blockIdx.x * XG_UBLK + threadIdx.x;
+  i128 W = 0, c = 0;
+  if (j < p && w[j] > 0.0) {
+    int e;
+    const double mant = frexp(w[j], &e);  // w = mant 2^e, mant ∈ [0.5, 1)
+    const long long M = (long long)ldexp(mant, 53);
+    const int sh = e - 53 + F;
+    if (sh >= 0) {
+      W = (i128)M << sh;
+    } else {  // weights spanning > 2^16 (xg_choose): round the smallest to the grid
+      const int r = -sh;
+      W = r >= 63 ? (i128)0 : (i128)((M + (1LL << (r - 1))) >> r);
+    }
+    const i128 t = (i128)tcol[j];
+    V[j] = W * t;
+    c = W * t * t;
+  } else if (j < kp) {
+    V[j] = 0;
+  }
+  if (j < kp) {
+    i128 x = W;
+    const int64_t stage = j / XG_BK, c8 = (j / 16) % 8, pos = j % 16;
+    for (int s = 0; s < S; s++) {
+      int r = (int)(x & 127);
+      if (r >= 64) r -= 128;
+      x = (x - r) >> 7;
+      const int64_t b = ((stage * S + s) * 8 + c8) * 32 + pos;
+      WW[b] = (int8_t)r;
+      WW[b + 16] = (int8_t)(2 * r);
+    }
+    if (x != 0) atomicOr(&info->bad, 2);  // W out of the digits' range (cannot happen with xg_choose's S)
+  }
+  red[threadIdx.x] = c;
+  __syncthreads();
+  for (int off = XG_UBLK / 2; off >= 1; off >>= 1) {
+    if (threadIdx.x < off) red[threadIdx.x] += red[threadIdx.x + off];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) Cpart[blockIdx.x] = red[0];
+}
+
+// ---- transpose: locus-major D (p rows of ldd bytes) → individual-major Dt, St ([npad][kp]) ----------
+// St byte at locus k (b = k mod 4, its byte in the dword): d = 2 → b (the 2ω dword, v_perm src1),
+// d = 1 → 4 + b (the ω dword, src0), d = 0 → 12 (v_perm's constant zero).
+__global__ void __launch_bounds__(256) xg_transpose_kernel(const int8_t* __restrict__ D, int64_t ldd, int64_t p, int64_t n,
+                                                           int64_t kp, int8_t* __restrict__ Dt, int8_t* __restrict__ St) {
+  __shared__ int8_t tile[64][65];
+  const int64_t k0 = (int64_t)blockIdx.x * 64, i0 = (int64_t)blockIdx.y * 64;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  for (int r = ty; r < 64; r += 4) {
+    const int64_t k = k0 + r, i = i0 + tx;
+    tile[r][tx] = (k < p && i < n) ? D[k * ldd + i] : (int8_t)0;
+  }
+  __syncthreads();
+  const int row = threadIdx.x >> 2, seg = threadIdx.x & 3;  // 64 rows x 4 segments of 16 loci
+  uint32_t dw[4], sw[4];
+#pragma unroll
+  for (int q = 0; q < 4; q++) {
+    uint32_t a = 0, s = 0;
+#pragma unroll
+    for (int b = 0; b < 4; b++) {
+      const uint32_t d = (uint32_t)(uint8_t)tile[seg * 16 + q * 4 + b][row];
+      const uint32_t sel = d == 2 ? (uint32_t)b : (d == 1 ? 4u + b : 12u);
+      a |= d << (8 * b);
+      s |= sel << (8 * b);
+    }
+    dw[q] = a;
+    sw[q] = s;
+  }
+  const int64_t off = (i0 + row) * kp + k0 + seg * 16;
+  *reinterpret_cast<uint4*>(Dt + off) = make_uint4(dw[0], dw[1], dw[2], dw[3]);
+  *reinterpret_cast<uint4*>(St + off) = make_uint4(sw[0], sw[1], sw[2], sw[3]);
+}
+
+// ---- U_i = Σ_j V_j d_ij over loci ranges, then n·U_i and C ------------------------------------------
+__global__ void __launch_bounds__(XG_UBLK) xg_u_kernel(const int8_t* __restrict__ D, int64_t ldd, int64_t p, int64_t n,
+                                                       const i128* __restrict__ V, int64_t jr, int64_t npad,
+                                                       i128* __restrict__ Upart) {
+  const int64_t i = (int64_t)blockIdx.x * XG_UBLK + threadIdx.x;
+  const int64_t j0 = (int64_t)blockIdx.y * jr;
+  const int64_t j1 = j0 + jr < p ? j0 + jr : p;
+  i128 u = 0;
+  if (i < n) {
+    for (int64_t j = j0; j < j1; j++) {
+      const int d = D[j * ldd + i];
+      const i128 v = V[j];
+      if (d & 1) u += v;
+      if (d & 2) u += v + v;
+    }
+  }
+  if (i < npad) Upart[blockIdx.y * npad + i] = u;
+}
+
+__global__ void __launch_bounds__(XG_UBLK) xg_u_reduce_kernel(const i128* __restrict__ Upart, int64_t nr, int64_t npad,
+                                                              int64_t n, const i128* __restrict__ Cpart, int64_t ncp,
+                                                              i128* __restrict__ NU, i128* __restrict__ C) {
+  const int64_t i = (int64_t)blockIdx.x * XG_UBLK + threadIdx.x;
+  if (i < npad) {
+    i128 u = 0;
+    for (int64_t r = 0; r < nr; r++) u += Upart[r * npad + i];
+    NU[i] = u * (i128)n;
+  }
+  if (i == 0) {
+    i128 c = 0;
+    for (int64_t b = 0; b < ncp; b++) c += Cpart[b];
+    *C = c;
+  }
+}
+
+// ---- the int8 GEMM -----------------------------------------------------------------------------------
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  // s_waitcnt vmcnt(N) with expcnt / lgkmcnt left alone (gfx9 encoding: vmcnt[3:0] | [15:14])
+  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
+}
+
+// unit u → (row block I, column block J) over the upper-triangle units J >= 2I (nI row blocks, nJ = 2 nI)
+__device__ __forceinline__ void xg_unit(int64_t u, int64_t nI, int64_t& I, int64_t& J) {
+  int64_t base = 0, r = 0;
+  const int64_t nJ = 2 * nI;
+  while (r < nI && base + (nJ - 2 * r) <= u) {
+    base += nJ - 2 * r;
+    r++;
+  }
+  I = r;
+  J = 2 * r + (u - base);
+}
+
+template <int S>
+__global__ void __launch_bounds__(512, 1)
+xg_gemm_kernel(const int8_t* __restrict__ Dt, const int8_t* __restrict__ St, int64_t kp, const int8_t* __restrict__ WW,
+               const i128* __restrict__ NU, const i128* __restrict__ Cp, int64_t n, int F, int64_t nI, int64_t nunits,
+               double* __restrict__ G, int64_t ldg, int accum) {
+  __shared__ __attribute__((aligned(16))) int8_t lds[XG_NS * XG_STAGE];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wm = wave >> 2, wn = wave & 3;  // 2 x 4 waves of 64 x 16
+
+  // XCD-aware bijective remap: the blocks the hardware deals to one XCD take a contiguous unit range
+  const int64_t nb = gridDim.x, b = blockIdx.x;
+  const int64_t xq = nb / 8, xr = nb % 8, x = b % 8;
+  const int64_t u = (x < xr ? x * (xq + 1) : xr * (xq + 1) + (x - xr) * xq) + b / 8;
+  if (u >= nunits) return;
+  int64_t I, J;
+  xg_unit(u, nI, I, J);
+  const int64_t i0 = I * XG_BM, j0 = J * XG_BN;
+  const int64_t wr0 = i0 + wm * 64, wc0 = j0 + wn * 16;
+  const bool active = !(wc0 + 15 < wr0) && wr0 < n && wc0 < n;
+  const int64_t nst = kp / XG_BK;
+
+  // LDS-DMA pieces of one stage (1 KB = 8 rows of 128 B each): wave w takes A pieces w and w + 8, B
+  // piece w, and waves 0-2 one digit piece each (S·256 <= 3 KB). Source chunk swizzled: LDS slot
+  // (lane & 7) of row (lane >> 3) holds chunk (lane & 7) ^ (row & 7).
+  const int prow = lane >> 3, pchunk = (lane & 7) ^ (lane >> 3);
+  const bool wdig = wave < 3;
+  auto issue = [&](int64_t st) {
+    int8_t* base = lds + (int)(st % XG_NS) * XG_STAGE;
+    const int64_t koff = st * XG_BK + pchunk * 16;
+    __builtin_amdgcn_global_load_lds((const void*)(Dt + (i0 + wave * 8 + prow) * kp + koff), (void*)(base + wave * 1024), 16, 0, 0);
+    __builtin_amdgcn_global_load_lds((const void*)(Dt + (i0 + (wave + 8) * 8 + prow) * kp + koff),
+                                     (void*)(base + (wave + 8) * 1024), 16, 0, 0);
+    __builtin_amdgcn_global_load_lds((const void*)(St + (j0 + wave * 8 + prow) * kp + koff),
+                                     (void*)(base + XG_BM * XG_BK + wave * 1024), 16, 0, 0);
+    if (wdig)
+      __builtin_amdgcn_global_load_lds((const void*)(WW + st * (int64_t)(S * 256) + wave * 1024 + lane * 16),
+                                       (void*)(base + XG_BM * XG_BK + XG_BN * XG_BK + wave * 1024), 16, 0, 0);
+  };
+  // stage st's pieces have landed (this wave's, by a counted wait — 4 pieces per stage on waves 0-2,
+  // 3 on the rest; the others', by the barrier) and every wave has finished reading the buffer the
+  // next issue overwrites (read one stage earlier)
+  auto arrive = [&](int64_t st) {
+    if (wdig) {
+      if (st + 2 < nst)
+        wait_vm<8>();
+      else if (st + 1 < nst)
+        wait_vm<4>();
+      else
+        wait_vm<0>();
+    } else {
+      if (st + 2 < nst)
+        wait_vm<6>();
+      else if (st + 1 < nst)
+        wait_vm<3>();
+      else
+        wait_vm<0>();
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    if (st + 3 < nst) issue(st + 3);
+  };
+
+  i32x4 acc[S][4];
+#pragma unroll
+  for (int s = 0; s < S; s++)
+#pragma unroll
+    for (int m = 0; m < 4; m++) acc[s][m] = (i32x4){0, 0, 0, 0};
+
+  const int fr = lane & 15, g = lane >> 4;
+  for (int64_t st = 0; st < 3 && st < nst; st++) issue(st);
+  if (!active) {  // a wave wholly below the diagonal or in the padding: stages and barriers only
+    for (int64_t st = 0; st < nst; st++) arrive(st);
+    return;
+  }
+  for (int64_t st = 0; st < nst; st++) {
+    arrive(st);
+    const int8_t* A = lds + (int)(st % XG_NS) * XG_STAGE;
+    const int8_t* B = A + XG_BM * XG_BK;
+    const int8_t* Wd = B + XG_BN * XG_BK;
+#pragma unroll
+    for (int ks = 0; ks < XG_BK / 64; ks++) {
+      const int c = ks * 4 + g;  // this lane group's 16-locus chunk
+      i32x4 af[4];
+#pragma unroll
+      for (int m = 0; m < 4; m++) {
+        const int r = wm * 64 + m * 16 + fr;
+        af[m] = *reinterpret_cast<const i32x4*>(A + r * XG_BK + ((c ^ (r & 7)) << 4));
+      }
+      const int rb = wn * 16 + fr;
+      const i32x4 bf = *reinterpret_cast<const i32x4*>(B + rb * XG_BK + ((c ^ (rb & 7)) << 4));
+      // slice digits one slice ahead in registers (the scheduler would otherwise hoist all S pairs)
+      const int8_t* wp = Wd + c * 32;
+      i32x4 w1 = *reinterpret_cast<const i32x4*>(wp);
+      i32x4 w2 = *reinterpret_cast<const i32x4*>(wp + 16);
+#pragma unroll
+      for (int s = 0; s < S; s++) {
+        i32x4 bs;
+#pragma unroll
+        for (int e = 0; e < 4; e++) bs[e] = (int)__builtin_amdgcn_perm((uint32_t)w1[e], (uint32_t)w2[e], (uint32_t)bf[e]);
+        if (s + 1 < S) {
+          w1 = *reinterpret_cast<const i32x4*>(wp + (s + 1) * 256);
+          w2 = *reinterpret_cast<const i32x4*>(wp + (s + 1) * 256 + 16);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int m = 0; m < 4; m++) acc[s][m] = __builtin_amdgcn_mfma_i32_16x16x64_i8(af[m], bs, acc[s][m], 0, 0, 0);
+        __builtin_amdgcn_s_setprio(0);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+  }
+
+  // epilogue: T = n² Σ_s 128^s acc_s − NU_i − NU_k + C in int128 → G = T 2^−F / n²
+  const i128 C = *Cp;
+  const i128 n2 = (i128)n * (i128)n;
+  const double dn2 = (double)n * (double)n;
+  const int64_t col = wc0 + fr;
+  const i128 nuk = NU[col];
+#pragma unroll
+  for (int m = 0; m < 4; m++) {
+#pragma unroll
+    for (int r = 0; r < 4; r++) {
+      const int64_t row = wr0 + m * 16 + g * 4 + r;
+      i128 a = 0;
+#pragma unroll
+      for (int s = S - 1; s >= 0; s--) a = a * 128 + (i128)acc[s][m][r];
+      const i128 T = n2 * a - NU[row] - nuk + C;
+      const double v = (row < n && col < n) ? ldexp(i128_to_double(T) / dn2, -F) : 0.0;
+      double* o = G + row * ldg + col;
+      *o = accum ? *o + v : v;
+    }
+  }
+}
+
+// ---- host side ---------------------------------------------------------------------------------
+struct XgLayout {
+  int64_t npad, kp, nst, jr, nr, ncp;
+  int64_t off_dt, off_st, off_ww, off_w, off_t, off_v, off_cp, off_up, off_nu, off_c, off_info, total;
+};
+
+static XgLayout xg_layout(int64_t n, int64_t p) {
+  XgLayout L{};
+  L.npad = npad_of(n);
+  L.kp = round_up(p < 1 ? 1 : p, XG_BK);
+  L.nst = L.kp / XG_BK;
+  L.jr = std::max<int64_t>(256, (p + 255) / 256);
+  L.nr = (p + L.jr - 1) / L.jr;
+  if (L.nr < 1) L.nr = 1;
+  L.ncp = (L.kp + XG_UBLK - 1) / XG_UBLK;
+  int64_t o = 0;
+  auto take = [&](int64_t bytes) {
+    const int64_t at = o;
+    o = round_up(o + bytes, 256);
+    return at;
+  };
+  L.off_dt = take(L.npad * L.kp);
+  L.off_st = take(L.npad * L.kp);
+  L.off_ww = take(L.nst * XG_SMAX * 256 + XG_WWSTAGE);
+  L.off_w = take(8 * L.kp);
+  L.off_t = take(8 * L.kp);
+  L.off_v = take(16 * L.kp);
+  L.off_cp = take(16 * L.ncp);
+  L.off_up = take(16 * L.nr * L.npad);
+  L.off_nu = take(16 * L.npad);
+  L.off_c = take(16);
+  L.off_info = take(sizeof(XgInfo));
+  L.total = o;
+  return L;
+}
+
+// S digits and the scale 2^F for the kept weights (exponents [emin, emax] by ilogb, largest wmax): F puts
+// the smallest weight's significand on the integer grid (every weight exact), and S is the fewest
+// balanced base-128 digits whose range (max 63·(128^S − 1)/127) holds W_max = wmax·2^F. With no such
+// S ≤ XG_SMAX (weights spanning more than ~2^16), S = XG_SMAX and F shrinks: the smallest weights are
+// rounded to the grid (relative error ≤ 2^−(69 − Δe) each). Returns 1 when exact.
+static int xg_choose(int emin, int emax, double wmax, int& S, int& F) {
+  (void)emax;
+  F = 52 - emin;
+  const double W = std::ldexp(wmax, F);
+  for (S = XG_SMIN; S <= XG_SMAX; S++)
+    if (W <= 63.0 * (std::ldexp(1.0, 7 * S) - 1.0) / 127.0 * (1.0 - 1e-12)) return 1;
+  S = XG_SMAX;
+  F = 7 * S - 3 - std::ilogb(wmax);  // W_max < 2^(7S−2) < 63·(128^S − 1)/127
+  return 0;
+}
+
+int64_t grm_exact_workspace_bytes(int64_t n, int64_t p) { return xg_layout(n, p).total; }
+
+int launch_grm_exact(const int8_t* D, int64_t ldd, int64_t p, int64_t n, int ploidy, double* G, int64_t ldg,
+                     double* mean, double* sd, int32_t* keep, int64_t* q_dev, int accum, void* ws, int64_t ws_bytes,
+                     int32_t* slices_out, hipStream_t s) {
+  if (!D || !G || !mean || !sd || !keep || !q_dev || !ws || p < 1 || n < 2 || ldd < n || ldg < npad_of(n) || ploidy != 2)
+    return fail(GBM_E_ARG, "gbm_dev_grm_exact_i8: bad arguments (diploid dosages {0,1,2}, p >= 1, n >= 2, ldg >= npad)");
+  const XgLayout L = xg_layout(n, p);
+  if (ws_bytes < L.total) return fail(GBM_E_ARG, "gbm_dev_grm_exact_i8: workspace too small (gbm_dev_grm_exact_workspace)");
+  int8_t* w8 = static_cast<int8_t*>(ws);
+  int8_t* Dt = w8 + L.off_dt;
+  int8_t* St = w8 + L.off_st;
+  int8_t* WW = w8 + L.off_ww;
+  double* w = reinterpret_cast<double*>(w8 + L.off_w);
+  int64_t* tcol = reinterpret_cast<int64_t*>(w8 + L.off_t);
+  i128* V = reinterpret_cast<i128*>(w8 + L.off_v);
+  i128* Cpart = reinterpret_cast<i128*>(w8 + L.off_cp);
+  i128* Upart = reinterpret_cast<i128*>(w8 + L.off_up);
+  i128* NU = reinterpret_cast<i128*>(w8 + L.off_nu);
+  i128* C = reinterpret_cast<i128*>(w8 + L.off_c);
+  XgInfo* info = reinterpret_cast<XgInfo*>(w8 + L.off_info);
+
+  xg_info_init_kernel<<<1, 1, 0, s>>>(info);
+  const int sgrid = (int)std::min<int64_t>(p, 256 * 32);
+  xg_stats_kernel<<<sgrid, 256, 0, s>>>(D, ldd, p, n, 1.0 / ploidy, mean, sd, keep,
+                                        reinterpret_cast<unsigned long long*>(q_dev), w, tcol, info);
+  GBM_LAUNCH_CHECK();
+  xg_transpose_kernel<<<dim3((unsigned)(L.kp / 64), (unsigned)(L.npad / 64)), 256, 0, s>>>(D, ldd, p, n, L.kp, Dt, St);
+  GBM_LAUNCH_CHECK();
+  XgInfo h{};
+  GBM_HIP_TRY(hipMemcpyAsync(&h, info, sizeof(h), hipMemcpyDeviceToHost, s));
+  GBM_HIP_TRY(hipStreamSynchronize(s));
+  if (h.bad & 1) return fail(GBM_E_ARG, "gbm_dev_grm_exact_i8: a dosage outside {0, 1, 2}");
+  int S = XG_SMIN, F = 0;
+  if (h.emax >= h.emin) {  // else no kept locus: W = 0, G = 0
+    double wmax;
+    memcpy(&wmax, &h.wmax_bits, sizeof(wmax));
+    xg_choose(h.emin, h.emax, wmax, S, F);
+  }
+  if (slices_out) *slices_out = S;
+  xg_digits_kernel<<<(unsigned)L.ncp, XG_UBLK, 0, s>>>(w, tcol, p, L.kp, S, F, WW, V, Cpart, info);
+  GBM_LAUNCH_CHECK();
+  xg_u_kernel<<<dim3((unsigned)(L.npad / XG_UBLK + (L.npad % XG_UBLK ? 1 : 0)), (unsigned)L.nr), XG_UBLK, 0, s>>>(
+      D, ldd, p, n, V, L.jr, L.npad, Upart);
+  GBM_LAUNCH_CHECK();
+  xg_u_reduce_kernel<<<(unsigned)((L.npad + XG_UBLK - 1) / XG_UBLK), XG_UBLK, 0, s>>>(Upart, L.nr, L.npad, n, Cpart,
+                                                                                      L.ncp, NU, C);
+  GBM_LAUNCH_CHECK();
+  const int64_t nI = L.npad / XG_BM;
+  const int64_t nunits = nI * (nI + 1);
+  const unsigned grid = (unsigned)nunits;
+  switch (S) {
+    case 8: xg_gemm_kernel<8><<<grid, 512, 0, s>>>(Dt, St, L.kp, WW, NU, C, n, F, nI, nunits, G, ldg, accum); break;
+    case 9: xg_gemm_kernel<9><<<grid, 512, 0, s>>>(Dt, St, L.kp, WW, NU, C, n, F, nI, nunits, G, ldg, accum); break;
+    default: xg_gemm_kernel<10><<<grid, 512, 0, s>>>(Dt, St, L.kp, WW, NU, C, n, F, nI, nunits, G, ldg, accum); break;
+  }
+  GBM_LAUNCH_CHECK();
+  return GBM_OK;
+}
+
+}  // namespace gbm
+
+extern "C" int64_t gbm_dev_grm_exact_workspace(int64_t n, int64_t p) { return gbm::grm_exact_workspace_bytes(n, p); }
+
+extern "C" int gbm_dev_grm_exact_i8(const int8_t* D, int64_t ldd, int64_t p, int64_t n, int ploidy, double* G,
+                                    int64_t ldg, double* mean, double* sd, int32_t* keep, int64_t* q_dev, int accum,
+                                    void* workspace, int64_t ws_bytes, int32_t* slices_out, void* stream) {
+  return gbm::launch_grm_exact(D, ldd, p, n, ploidy, G, ldg, mean, sd, keep, q_dev, accum, workspace, ws_bytes,
+                               slices_out, (hipStream_t)stream);
+}

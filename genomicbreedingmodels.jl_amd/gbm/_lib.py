@@ -42,7 +42,7 @@ EXPORTS = (
     "gbm_dev_synth_dosage_i8", "gbm_dev_standardize_i8", "gbm_dev_grm_accumulate", "gbm_dev_marker_effects_i8",
     "gbm_debug_oom_retries", "gbm_dev_chol_group_panels", "gbm_dev_chol_group_update", "gbm_dev_chol_strip_unpack_rows",
     "gbm_dev_chol_area_doubles", "gbm_dev_chol_area_pack", "gbm_dev_chol_area_unpack",
-    "gbm_dev_chol_group_update_cols",
+    "gbm_dev_chol_group_update_cols", "gbm_dev_grm_exact_workspace", "gbm_dev_grm_exact_i8",
 )
 
 
@@ -137,6 +137,10 @@ def _declare(lib):
     lib.gbm_dev_standardize_i8.restype = I32
     lib.gbm_dev_standardize_i8.argtypes = [P, I64, I64, I64, I32, P, I64, P, P, P, P, P]
     lib.gbm_dev_marker_effects_i8.restype = I32
+    lib.gbm_dev_grm_exact_workspace.restype = I64
+    lib.gbm_dev_grm_exact_workspace.argtypes = [I64, I64]
+    lib.gbm_dev_grm_exact_i8.restype = I32
+    lib.gbm_dev_grm_exact_i8.argtypes = [P, I64, I64, I64, I32, P, I64, P, P, P, P, I32, P, I64, P, P]
     lib.gbm_dev_marker_effects_i8.argtypes = [P, I64, I64, I64, I32, P, I64, I64, D, P, P, P, P, P, I64, P, P]
     for f in ("gbm_dev_grm", "gbm_dev_grm_syrk", "gbm_dev_grm_accumulate"):
         getattr(lib, f).restype = I32

@@ -516,3 +516,29 @@ class HipStreamedShardStages(HipShardStages):
         """(j, X[:, j:j+pc] as (pc, n) float64 on the device) over the schedule: the streamed X for checks."""
         for j, pc in self.sched:
             yield j, self.D[j:j + pc].to(self.torch.float64) / self.ploidy
+
+
+class HipExactShardStages(HipStreamedShardStages):
+    """A shard of diploid dosages (int8, 1 B per cell, resident) whose GRM is computed EXACTLY by the int8
+    matrix cores (csrc/grm_exact.hip): G = Σ_j w_j (d_j − t_j/n)(d_j − t_j/n)ᵀ with each
+    locus weight w_j = 1/var_j held as an exact fixed-point integer in base-128 digits, the digit GEMMs summed
+    in int32 and the centring in int128, one rounding to fp64 at the end. No fp64 Z is ever formed; the
+    marker effects re-read the bytes (as the loci-streamed shard does)."""
+
+    def __init__(self, n: int, p_local: int, nrhs: int = 1, lambda_: float = 1.0, device: int = 0):
+        self.slices = ctypes.c_int32(0)
+        super().__init__(n, p_local, p_local, nrhs=nrhs, lambda_=lambda_, device=device, ploidy=2)
+
+    def _alloc_rows(self, f64):
+        self.X = None
+        self.Z = None
+        self.D = self.torch.empty((self.p, self.n), dtype=self.torch.int8, device=self.dev)  # Julia (n, p) layout
+
+    def _grm_workspace(self):
+        return self.lib.gbm_dev_grm_exact_workspace(self.n, self.p)
+
+    def grm_syrk(self):
+        _lib.check(self.lib.gbm_dev_grm_exact_i8(self._p(self.D), self.n, self.p, self.n, self.ploidy, self._p(self.G),
+                                                 self.gdim, self._p(self.mean), self._p(self.sd), self._p(self.keep),
+                                                 self._p(self.q), 0, self._p(self.ws_grm), self.ws_grm_bytes,
+                                                 ctypes.byref(self.slices), self._stream()), "grm_exact_i8")

@@ -345,6 +345,21 @@ int gbm_dev_marker_effects(const double* Zt, int64_t ldz, int64_t p, int64_t n,
                            const double* mean, const double* sd, const int32_t* keep,
                            double* B, int64_t ldb, double* msum, void* stream);
 
+/* Bytes of device workspace gbm_dev_grm_exact_i8 needs for (n, p): the individual-major operand copies
+ * (2 x npad x p bytes), the per-locus digits and the 128-bit centring terms. */
+int64_t gbm_dev_grm_exact_workspace(int64_t n, int64_t p);
+/* The GRM of diploid dosages (column-major D, n x p, ldd >= n, d in {0, 1, 2}, x = d/2) computed EXACTLY up to
+ * the fp64 rounding of each locus weight 1/var_j: G = Σ_j w_j (d_j − t_j/n)(d_j − t_j/n)ᵀ, the GRM of the
+ * standardised genotypes (reference src/gwas.jl:112-126 before the 1/q), as int8 MFMA GEMMs over the base-128
+ * digits of the fixed-point weights with 128-bit centring. Also writes what
+ * gbm_dev_standardize_i8 writes except Z: mean, sd, keep (per locus) and adds the kept count to *q_dev.
+ * accum != 0: G += this GRM. *slices_out (optional): the digit count S (8-10) the weights needed.
+ * Upper tiles of G are written (ldg >= gbm_dev_npad(n)); one host synchronisation per call (sizes S).
+ * GBM_E_ARG on a dosage outside {0, 1, 2} or ploidy != 2. */
+int gbm_dev_grm_exact_i8(const int8_t* D, int64_t ldd, int64_t p, int64_t n, int ploidy, double* G, int64_t ldg,
+                         double* mean, double* sd, int32_t* keep, int64_t* q_dev, int accum, void* workspace,
+                         int64_t ws_bytes, int32_t* slices_out, void* stream);
+
 /* gbm_dev_marker_effects on int8 dosage rows (column-major D, n x p, ldd >= n, x = d/ploidy) instead of the
  * standardised fp64 rows: z = (x − mean_j)/sd_j is rebuilt in registers exactly as gbm_dev_standardize_i8
  * wrote it, so B and msum are bit-identical, at 1 byte read per cell (the loci-streamed fit's back-solve,

@@ -6,7 +6,7 @@ NAME=$1; SRC=$2
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
 OUT=$ROOT/variants/build_$NAME; mkdir -p $OUT
 pids=()
-for f in stats.hip grm.hip chol.hip chol_flow.hip effects.hip gibbs.hip capi.cpp session.cpp; do
+for f in stats.hip grm.hip grm_exact.hip chol.hip chol_flow.hip effects.hip gibbs.hip capi.cpp session.cpp; do
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 -I$ROOT/genomicbreedingmodels.jl_amd/csrc -c $SRC/$f -o $OUT/$f.o ${VARIANT_FLAGS} &
   pids+=($!)
 done
