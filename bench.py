@@ -36,6 +36,7 @@ sys.path.insert(0, os.path.join(ROOT, "genomicbreedingmodels.jl_amd"))
 
 PEAK_F64_TFLOPS = 78.6  # MI355X fp64 matrix peak (AMD datasheet)
 PEAK_HBM_GBS = 8000.0
+PEAK_I8_TOPS = 5000.0  # MI355X dense int8 MFMA (2x bf16 per clock: MI355X_MICROARCH.md, Matrix cores)
 MEASURED_MFMA_F64_TFLOPS = 74.1  # back-to-back v_mfma_f64_16x16x4_f64 loop, tools/mfma_f64_probe.hip
 
 
@@ -57,6 +58,9 @@ def parse():
     ap.add_argument("--same-device", action="store_true", help="all ranks on cuda:0 (rehearsal on a 1-GPU box)")
     ap.add_argument("--stream-chunk", type=int, default=0,
                     help="loci per chunk of the loci-streamed mode (int8 dosages resident); 0 = resident fp64 X")
+    ap.add_argument("--grm", choices=("fp64", "exact"), default="fp64",
+                    help="fp64: the fp64-MFMA SYRK on standardised rows; exact: int8 dosages resident, the GRM "
+                         "computed exactly by int8-MFMA digit GEMMs with int128 centring (csrc/grm_exact.hip)")
     return ap.parse_args()
 
 
@@ -66,14 +70,14 @@ CONFIGS = {(5000, 50000): "C2 GBLUP 5 000 x 50 000 (BASELINE.json configs[1])",
            (50000, 75000): "C3's per-GPU shard 50 000 x 75 000 (1/8 of BASELINE.json configs[2])"}
 
 
-def workload_label(n, p_local, world, stream_chunk):
+def workload_label(n, p_local, world, stream_chunk, exact=False):
     """config.workload from (n, p, N): weak scaling keeps p_local loci per GPU, so the per-GPU shape
     names the config (C2: 5 000 x 50 000 per GPU), and a one-GPU run over all loci of C3 names C3."""
     p_total = p_local * world
     name = CONFIGS.get((n, p_local)) if world > 1 else CONFIGS.get((n, p_total))
     name = name or f"custom GBLUP n={n} x p={p_total} (no BASELINE.json config)"
     mode = (f"loci-streamed ({stream_chunk}-locus fp64 chunks, int8 dosages resident)" if stream_chunk
-            else "fp64 X resident")
+            else "int8 dosages resident, exact-integer GRM" if exact else "fp64 X resident")
     return (f"{name}: n={n} x p={p_local} loci per GPU, p_total={p_total} over {world} GPU(s), {mode}"
             + (", loci-sharded, partial GRMs all-reduced" if world > 1 else ""))
 
@@ -336,14 +340,17 @@ def main():
 
     import gbm
     from gbm import synth
-    from gbm.sharded import (HipShardStages, HipStreamedShardStages, LocalComm, TorchComm, assemble_b_hat,
-                             sharded_gblup_step)
+    from gbm.sharded import (HipExactShardStages, HipShardStages, HipStreamedShardStages, LocalComm, TorchComm,
+                             assemble_b_hat, sharded_gblup_step)
 
     comm = TorchComm() if world > 1 else LocalComm()
     n, p_local = args.individuals, args.loci
     p_total = p_local * world
     j0 = rank * p_local
-    if args.stream_chunk:
+    exact = args.grm == "exact"
+    if exact:
+        st = HipExactShardStages(n, p_local, nrhs=args.nrhs, lambda_=args.lam, device=dev)
+    elif args.stream_chunk:
         st = HipStreamedShardStages(n, p_local, args.stream_chunk, nrhs=args.nrhs, lambda_=args.lam, device=dev)
     else:
         st = HipShardStages(n, p_local, nrhs=args.nrhs, lambda_=args.lam, device=dev)
@@ -407,7 +414,7 @@ def main():
     chol_flops = float(n) ** 3 / 3.0
     solve_flops = 8.0 * float(n) ** 2 * args.nrhs + 2.0 * n * p_local * args.nrhs
     achieved = grm_flops / (syrk_ms / 1000.0) / 1e12
-    traffic, traffic_stale = load_pmc(n, p_local) if not args.stream_chunk else (None, None)
+    traffic, traffic_stale = load_pmc(n, p_local) if not (args.stream_chunk or exact) else (None, None)
     e2e_frac = (grm_flops + chol_flops + solve_flops) / (ms_per_step / 1000.0) / (PEAK_F64_TFLOPS * 1e12)
 
     rec = {
@@ -421,13 +428,14 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "f64",
+        "dtype": ("i8 digit GEMMs (exact int32 sums) + int128 centring -> f64 G; f64 solve" if exact else "f64"),
         "data": "synthetic: counter-hash genotypes (MAF U(0.05,0.5), dosage Binomial(2,f), X=d/2) generated in HBM"
-                + (" as int8 dosages" if args.stream_chunk else " as fp64") + "; 1% QTL phenotype, h2=0.5",
+                + (" as int8 dosages" if (args.stream_chunk or exact) else " as fp64") + "; 1% QTL phenotype, h2=0.5",
         "config": {
-            "workload": workload_label(n, p_local, world, args.stream_chunk),
+            "workload": workload_label(n, p_local, world, args.stream_chunk, exact),
             "n": n, "p_per_gpu": p_local, "p_total": p_total, "traits": args.nrhs, "lambda": args.lam,
-            "grm_slices": int(st.lib.gbm_dev_grm_slices(n, args.stream_chunk or p_local)),
+            "grm_slices": int(st.lib.gbm_dev_grm_slices(n, args.stream_chunk or p_local)) if not exact else None,
+            "grm_digit_slices": int(st.slices.value) if exact else None,
             "stream_chunk": args.stream_chunk or None,
             "parallelism": f"loci-shard x{world}",
         },
@@ -454,6 +462,21 @@ def main():
         "stage_ms": stage_ms,
         "e2e_fp64_frac_of_peak": e2e_frac,
     }
+    if exact:
+        S = int(st.slices.value)
+        ops = S * grm_flops  # S digit GEMMs of n(n+1)/2 x p int8 multiply-adds (2 ops each)
+        tops = ops / (syrk_ms / 1000.0) / 1e12
+        rec["roofline"] = {
+            "bound": "mfma",
+            "kernel": f"GRM stage: xg_gemm_kernel<{S}> (v_mfma_i32_16x16x64_i8, {S} base-128 digit GEMMs of the fixed-"
+                      "point locus weights, 128x64 upper tiles) + its per-locus prep kernels (stats, digits, transpose, "
+                      "int128 centring terms); achieved = S n(n+1)p int8 ops / stage time",
+            "achieved": tops, "peak": PEAK_I8_TOPS, "unit": "TOPS (int8)", "frac": tops / PEAK_I8_TOPS,
+            "traffic": None, "ops_per_launch": ops, "ms_per_launch": syrk_ms,
+            "fp64_equivalent_tflops": achieved,
+        }
+        rec["e2e_fp64_frac_of_peak"] = None
+        rec["fp64_equivalent_e2e_tflops"] = (grm_flops + chol_flops + solve_flops) / (ms_per_step / 1000.0) / 1e12
     if world == 1 and not args.no_host_path and not args.stream_chunk and float(n) * p_local <= 2e9:
         rec["host_path"] = host_path(args, torch)
         rec["stage_ms"]["h2d_x_pinned"] = rec["host_path"]["h2d_x_ms_pinned"]
