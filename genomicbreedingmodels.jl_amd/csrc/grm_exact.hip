@@ -22,9 +22,9 @@
 //                     exponent range of the kept weights, a flag for dosages outside {0, 1, 2}
 //   xg_digits_kernel  per locus: the S digits (and doubled digits) in the GEMM's per-stage layout,
 //                     V_j = W_j t_j, block partials of C
-//   xg_transpose_kernel  locus-major dosages → individual-major Dt (the A operand) and St (B: each byte
-//                     a v_perm selector picking 2ω, ω or 0 from the digit dwords)
-//   xg_u_kernel / xg_u_reduce_kernel   n·U_i and C in int128
+//   xg_transpose_u_kernel  locus-major dosages → individual-major Dt (the A operand) and St (B: each byte
+//                     a v_perm selector picking 2ω, ω or 0 from the digit dwords), and partial U_i
+//   xg_u_reduce_kernel   n·U_i and C in int128
 //   xg_gemm_kernel<S> 128 x 64 output tiles of the upper triangle; 8 waves of 64 x 16, each holding S x 4
 //                     v_mfma_i32_16x16x64_i8 accumulators; operands staged global → LDS by LDS-DMA into a
 //                     4-deep ring (counted vmcnt, raw barriers); B scaled per slice in registers by one
@@ -49,7 +49,7 @@ constexpr int XG_BM = 128;       // tile rows (individuals i)
 constexpr int XG_BN = 64;        // tile columns (individuals k)
 constexpr int XG_BK = 128;       // loci per LDS stage (bytes per operand row)
 constexpr int XG_SMIN = 8, XG_SMAX = 10;
-constexpr int XG_WWSTAGE = 4096;  // digit bytes per stage in LDS (S·256 used, one 1-KB DMA piece per wave)
+constexpr int XG_WWSTAGE = 3072;  // digit bytes per stage in LDS (S·256 used: three 1-KB DMA pieces)
 constexpr int XG_STAGE = XG_BM * XG_BK + XG_BN * XG_BK + XG_WWSTAGE;  // 28 KB
 constexpr int XG_NS = 4;          // ring depth (3 stages in flight)
 constexpr int XG_UBLK = 256;      // threads per block of the U / digits kernels
@@ -67,20 +67,37 @@ __device__ __forceinline__ double i128_to_double(i128 x) {
   return neg ? -r : r;
 }
 
-// ---- per-locus statistics (one workgroup per locus row, grid-strided) --------------------------
+// ---- per-locus statistics (one wave per locus row, grid-strided over waves) ----------------------------
+// t = Σd and Σd² by v_dot4 over 4 dosages per lane per load when the rows are 4-byte aligned (ldd % 4 == 0),
+// else byte loads. The exponent range and the largest weight are kept per wave, one atomic each at the end.
 __global__ void __launch_bounds__(256) xg_stats_kernel(const int8_t* __restrict__ D, int64_t ldd, int64_t p, int64_t n,
                                                        double xs, double* __restrict__ mean, double* __restrict__ sd,
                                                        int32_t* __restrict__ keep, unsigned long long* __restrict__ q_dev,
                                                        double* __restrict__ w, int64_t* __restrict__ tcol,
                                                        XgInfo* __restrict__ info) {
-  __shared__ long long red[2][4];
-  __shared__ int badsh;
-  unsigned long long kept_local = 0;
-  for (int64_t j = blockIdx.x; j < p; j += gridDim.x) {
+  const int lane = threadIdx.x & 63;
+  const int64_t wid = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 6, nw = ((int64_t)gridDim.x * 256) >> 6;
+  const bool al4 = (ldd % 4) == 0 && ((uintptr_t)D % 4) == 0;
+  unsigned long long kept = 0, wmaxb = 0;
+  int emin = INT_MAX, emax = INT_MIN, bad = 0;
+  for (int64_t j = wid; j < p; j += nw) {
     const int8_t* row = D + j * ldd;
-    long long t = 0, s2 = 0;
-    int bad = 0;
-    for (int64_t i = threadIdx.x; i < n; i += 256) {
+    int t = 0, s2 = 0;
+    int64_t tail = 0;
+    if (al4) {
+      const int64_t n4 = n / 4;
+      const int* r4 = reinterpret_cast<const int*>(row);
+#pragma unroll 8
+      for (int64_t i = lane; i < n4; i += 64) {
+        const int v = r4[i];
+        t = __builtin_amdgcn_sdot4(v, 0x01010101, t, false);
+        s2 = __builtin_amdgcn_sdot4(v, v, s2, false);
+        // a byte outside {0, 1, 2}: any of bits 2-7 set, or both bits 0 and 1 (3)
+        bad |= (v & 0xFCFCFCFC) | ((v & 0x02020202) & ((v & 0x01010101) << 1));
+      }
+      tail = 4 * n4;
+    }
+    for (int64_t i = tail + lane; i < n; i += 64) {
       const int d = row[i];
       t += d;
       s2 += d * d;
@@ -91,41 +108,37 @@ __global__ void __launch_bounds__(256) xg_stats_kernel(const int8_t* __restrict_
       t += __shfl_xor(t, off, 64);
       s2 += __shfl_xor(s2, off, 64);
     }
-    bad = __any(bad) ? 1 : 0;
-    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    __syncthreads();
-    if (threadIdx.x == 0) badsh = 0;
-    __syncthreads();
+    // var(d) = (n Σd² − t²)/(n(n − 1)), exact integers up to the division
+    const long long num = (long long)n * s2 - (long long)t * t;
+    const bool kp = n > 1 && num > 0;
+    const double dn = (double)n;
+    const double wj = kp ? (dn * (dn - 1.0)) / (double)num : 0.0;
     if (lane == 0) {
-      red[0][wv] = t;
-      red[1][wv] = s2;
-      if (bad) badsh = 1;
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      t = red[0][0] + red[0][1] + red[0][2] + red[0][3];
-      s2 = red[1][0] + red[1][1] + red[1][2] + red[1][3];
-      // var(d) = (n Σd² − t²)/(n(n − 1)), exact integers up to the division
-      const long long num = (long long)n * s2 - t * t;
-      const bool kp = n > 1 && num > 0;
-      const double dn = (double)n;
       mean[j] = (double)t * xs / dn;
       sd[j] = kp ? sqrt((double)num / (dn * (dn - 1.0))) * xs : 0.0;
       keep[j] = kp ? 1 : 0;
-      kept_local += kp ? 1 : 0;
-      const double wj = kp ? (dn * (dn - 1.0)) / (double)num : 0.0;
       w[j] = wj;
       tcol[j] = t;
-      if (kp) {
-        const int e = ilogb(wj);
-        atomicMin(&info->emin, e);
-        atomicMax(&info->emax, e);
-        atomicMax(&info->wmax_bits, (unsigned long long)__double_as_longlong(wj));
-      }
-      if (badsh) atomicOr(&info->bad, 1);
+    }
+    if (kp) {
+      kept++;
+      const int e = ilogb(wj);
+      emin = e < emin ? e : emin;
+      emax = e > emax ? e : emax;
+      const unsigned long long bits = (unsigned long long)__double_as_longlong(wj);
+      wmaxb = bits > wmaxb ? bits : wmaxb;
     }
   }
-  if (threadIdx.x == 0 && kept_local) atomicAdd(q_dev, kept_local);
+  bad = __any(bad != 0) ? 1 : 0;
+  if (lane == 0) {
+    if (kept) {
+      atomicAdd(q_dev, kept);
+      atomicMin(&info->emin, emin);
+      atomicMax(&info->emax, emax);
+      atomicMax(&info->wmax_bits, wmaxb);
+    }
+    if (bad) atomicOr(&info->bad, 1);
+  }
 }
 
 __global__ void xg_info_init_kernel(XgInfo* info) {
@@ -138,7 +151,8 @@ __global__ void xg_info_init_kernel(XgInfo* info) {
 
 // ---- digits: W_j = w_j 2^F → S balanced base-128 digits in the GEMM's stage layout -----------------
 // Stage layout (per 128-locus stage, S·256 bytes): [s][chunk c = 0..7][32 B: ω of loci 16c..16c+15,
-// then 2ω of the same loci].
+// then 2ω of the same loci] (2ω from memory: computing it per dword costs two VALU ops per v_perm, and the
+// kernel is VALU-issue-sensitive: measured slower).
 __global__ void __launch_bounds__(XG_UBLK) xg_digits_kernel(const double* __restrict__ w, const int64_t* __restrict__ tcol,
                                                             int64_t p, int64_t kp, int S, int F,
                                                             int8_t* __restrict__ WW, i128* __restrict__ V,
@@ -185,58 +199,80 @@ __global__ void __launch_bounds__(XG_UBLK) xg_digits_kernel(const double* __rest
   if (threadIdx.x == 0) Cpart[blockIdx.x] = red[0];
 }
 
-// ---- transpose: locus-major D (p rows of ldd bytes) → individual-major Dt, St ([npad][kp]) ----------
+// ---- transpose + U: locus-major D (p rows of ldd bytes) → individual-major Dt, St ([npad][kp]) and the
+// partial U_i = Σ_j V_j d_ij over this block's loci tiles --------------------------------------------------
 // St byte at locus k (b = k mod 4, its byte in the dword): d = 2 → b (the 2ω dword, v_perm src1),
 // d = 1 → 4 + b (the ω dword, src0), d = 0 → 12 (v_perm's constant zero).
-__global__ void __launch_bounds__(256) xg_transpose_kernel(const int8_t* __restrict__ D, int64_t ldd, int64_t p, int64_t n,
-                                                           int64_t kp, int8_t* __restrict__ Dt, int8_t* __restrict__ St) {
-  __shared__ int8_t tile[64][65];
-  const int64_t k0 = (int64_t)blockIdx.x * 64, i0 = (int64_t)blockIdx.y * 64;
-  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
-  for (int r = ty; r < 64; r += 4) {
-    const int64_t k = k0 + r, i = i0 + tx;
-    tile[r][tx] = (k < p && i < n) ? D[k * ldd + i] : (int8_t)0;
-  }
-  __syncthreads();
-  const int row = threadIdx.x >> 2, seg = threadIdx.x & 3;  // 64 rows x 4 segments of 16 loci
-  uint32_t dw[4], sw[4];
-#pragma unroll
-  for (int q = 0; q < 4; q++) {
-    uint32_t a = 0, s = 0;
-#pragma unroll
-    for (int b = 0; b < 4; b++) {
-      const uint32_t d = (uint32_t)(uint8_t)tile[seg * 16 + q * 4 + b][row];
-      const uint32_t sel = d == 2 ? (uint32_t)b : (d == 1 ? 4u + b : 12u);
-      a |= d << (8 * b);
-      s |= sel << (8 * b);
-    }
-    dw[q] = a;
-    sw[q] = s;
-  }
-  const int64_t off = (i0 + row) * kp + k0 + seg * 16;
-  *reinterpret_cast<uint4*>(Dt + off) = make_uint4(dw[0], dw[1], dw[2], dw[3]);
-  *reinterpret_cast<uint4*>(St + off) = make_uint4(sw[0], sw[1], sw[2], sw[3]);
-}
-
-// ---- U_i = Σ_j V_j d_ij over loci ranges, then n·U_i and C ------------------------------------------
-__global__ void __launch_bounds__(XG_UBLK) xg_u_kernel(const int8_t* __restrict__ D, int64_t ldd, int64_t p, int64_t n,
-                                                       const i128* __restrict__ V, int64_t jr, int64_t npad,
-                                                       i128* __restrict__ Upart) {
-  const int64_t i = (int64_t)blockIdx.x * XG_UBLK + threadIdx.x;
-  const int64_t j0 = (int64_t)blockIdx.y * jr;
-  const int64_t j1 = j0 + jr < p ? j0 + jr : p;
+// Block (x, y): individuals [256x, 256x + 256), the 64-locus tiles y, y + gridDim.y, ...: each tile read
+// row by row (4 dosages per lane) into LDS, then one thread per individual assembles its 64 bytes of Dt and
+// St and adds its V_j d_ij (V_j wave-uniform).
+constexpr int XG_TP = 256 + 16;  // LDS row pitch of the 64-locus x 256-individual tile
+__global__ void __launch_bounds__(256) xg_transpose_u_kernel(const int8_t* __restrict__ D, int64_t ldd, int64_t p,
+                                                             int64_t n, int64_t kp, int64_t npad,
+                                                             const i128* __restrict__ V, int8_t* __restrict__ Dt,
+                                                             int8_t* __restrict__ St, i128* __restrict__ Upart) {
+  __shared__ __attribute__((aligned(16))) int8_t tile[64 * XG_TP];
+  const int64_t i0 = (int64_t)blockIdx.x * 256;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const bool al4 = (ldd % 4) == 0 && ((uintptr_t)D % 4) == 0;
+  const int64_t i = i0 + threadIdx.x;
+  const int64_t nkt = kp / 64;
   i128 u = 0;
-  if (i < n) {
-    for (int64_t j = j0; j < j1; j++) {
-      const int d = D[j * ldd + i];
-      const i128 v = V[j];
-      if (d & 1) u += v;
-      if (d & 2) u += v + v;
+  for (int64_t kt = blockIdx.y; kt < nkt; kt += gridDim.y) {
+    const int64_t k0 = kt * 64;
+    __syncthreads();  // the previous tile's reads are done
+    uint32_t vr[16];
+#pragma unroll
+    for (int rr = 0; rr < 16; rr++) {  // all 16 row loads of this wave in flight together
+      const int64_t k = k0 + wv + 4 * rr;
+      const int64_t ii = i0 + 4 * lane;
+      uint32_t v = 0;
+      if (k < p) {
+        const int8_t* row = D + k * ldd;
+        if (al4 && ii + 3 < n) {
+          v = *reinterpret_cast<const uint32_t*>(row + ii);
+        } else {
+#pragma unroll
+          for (int b = 0; b < 4; b++)
+            if (ii + b < n) v |= (uint32_t)(uint8_t)row[ii + b] << (8 * b);
+        }
+      }
+      vr[rr] = v;
+    }
+#pragma unroll
+    for (int rr = 0; rr < 16; rr++) *reinterpret_cast<uint32_t*>(tile + (wv + 4 * rr) * XG_TP + 4 * lane) = vr[rr];
+    __syncthreads();
+    if (i < npad) {
+      uint32_t dw[16], sw[16];
+#pragma unroll
+      for (int q = 0; q < 16; q++) {
+        uint32_t a = 0, sl = 0;
+#pragma unroll
+        for (int b = 0; b < 4; b++) {
+          const int kk = q * 4 + b;
+          const uint32_t d = (uint32_t)(uint8_t)tile[kk * XG_TP + threadIdx.x];
+          const uint32_t sel = d == 2 ? (uint32_t)b : (d == 1 ? 4u + b : 12u);
+          a |= d << (8 * b);
+          sl |= sel << (8 * b);
+          const i128 vv = V[k0 + kk];  // 0 beyond p
+          if (d & 1) u += vv;
+          if (d & 2) u += vv + vv;
+        }
+        dw[q] = a;
+        sw[q] = sl;
+      }
+      const int64_t off = i * kp + k0;
+#pragma unroll
+      for (int q = 0; q < 4; q++) {
+        *reinterpret_cast<uint4*>(Dt + off + 16 * q) = make_uint4(dw[4 * q], dw[4 * q + 1], dw[4 * q + 2], dw[4 * q + 3]);
+        *reinterpret_cast<uint4*>(St + off + 16 * q) = make_uint4(sw[4 * q], sw[4 * q + 1], sw[4 * q + 2], sw[4 * q + 3]);
+      }
     }
   }
   if (i < npad) Upart[blockIdx.y * npad + i] = u;
 }
 
+// ---- n·U_i and C from the partials ----------------------------------------------------------------------
 __global__ void __launch_bounds__(XG_UBLK) xg_u_reduce_kernel(const i128* __restrict__ Upart, int64_t nr, int64_t npad,
                                                               int64_t n, const i128* __restrict__ Cpart, int64_t ncp,
                                                               i128* __restrict__ NU, i128* __restrict__ C) {
@@ -260,10 +296,10 @@ __device__ __forceinline__ void wait_vm() {
   __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
 }
 
-// unit u → (row block I, column block J) over the upper-triangle units J >= 2I (nI row blocks, nJ = 2 nI)
-__device__ __forceinline__ void xg_unit(int64_t u, int64_t nI, int64_t& I, int64_t& J) {
+// unit u → (row block I, column block J) over the upper-triangle units J >= 2I with columns below n
+// (nI = ⌈n/128⌉ row blocks, nJ = ⌈n/64⌉ column blocks; every row block has at least one unit)
+__device__ __forceinline__ void xg_unit(int64_t u, int64_t nI, int64_t nJ, int64_t& I, int64_t& J) {
   int64_t base = 0, r = 0;
-  const int64_t nJ = 2 * nI;
   while (r < nI && base + (nJ - 2 * r) <= u) {
     base += nJ - 2 * r;
     r++;
@@ -275,7 +311,7 @@ __device__ __forceinline__ void xg_unit(int64_t u, int64_t nI, int64_t& I, int64
 template <int S>
 __global__ void __launch_bounds__(512, 1)
 xg_gemm_kernel(const int8_t* __restrict__ Dt, const int8_t* __restrict__ St, int64_t kp, const int8_t* __restrict__ WW,
-               const i128* __restrict__ NU, const i128* __restrict__ Cp, int64_t n, int F, int64_t nI, int64_t nunits,
+               const i128* __restrict__ NU, const i128* __restrict__ Cp, int64_t n, int F, int64_t nI, int64_t nJ, int64_t nunits,
                double* __restrict__ G, int64_t ldg, int accum) {
   __shared__ __attribute__((aligned(16))) int8_t lds[XG_NS * XG_STAGE];
   const int lane = threadIdx.x & 63;
@@ -288,7 +324,7 @@ xg_gemm_kernel(const int8_t* __restrict__ Dt, const int8_t* __restrict__ St, int
   const int64_t u = (x < xr ? x * (xq + 1) : xr * (xq + 1) + (x - xr) * xq) + b / 8;
   if (u >= nunits) return;
   int64_t I, J;
-  xg_unit(u, nI, I, J);
+  xg_unit(u, nI, nJ, I, J);
   const int64_t i0 = I * XG_BM, j0 = J * XG_BN;
   const int64_t wr0 = i0 + wm * 64, wc0 = j0 + wn * 16;
   const bool active = !(wc0 + 15 < wr0) && wr0 < n && wc0 < n;
@@ -351,37 +387,61 @@ xg_gemm_kernel(const int8_t* __restrict__ Dt, const int8_t* __restrict__ St, int
     const int8_t* A = lds + (int)(st % XG_NS) * XG_STAGE;
     const int8_t* B = A + XG_BM * XG_BK;
     const int8_t* Wd = B + XG_BN * XG_BK;
+    // the stage's 2S (k-step, slice) pairs in one unrolled sequence: digits two pairs ahead in a ring of
+    // three register sets, the second k-step's fragments loaded during the first k-step
+    constexpr int NKS = XG_BK / 64;
+    const int8_t* wb[NKS];
 #pragma unroll
-    for (int ks = 0; ks < XG_BK / 64; ks++) {
+    for (int ks = 0; ks < NKS; ks++) wb[ks] = Wd + (ks * 4 + g) * 32;
+    i32x4 af[NKS][4], bf[NKS], w1[3], w2[3];
+    auto load_frags = [&](int ks) {
       const int c = ks * 4 + g;  // this lane group's 16-locus chunk
-      i32x4 af[4];
 #pragma unroll
       for (int m = 0; m < 4; m++) {
         const int r = wm * 64 + m * 16 + fr;
-        af[m] = *reinterpret_cast<const i32x4*>(A + r * XG_BK + ((c ^ (r & 7)) << 4));
+        af[ks][m] = *reinterpret_cast<const i32x4*>(A + r * XG_BK + ((c ^ (r & 7)) << 4));
       }
       const int rb = wn * 16 + fr;
-      const i32x4 bf = *reinterpret_cast<const i32x4*>(B + rb * XG_BK + ((c ^ (rb & 7)) << 4));
-      // slice digits one slice ahead in registers (the scheduler would otherwise hoist all S pairs)
-      const int8_t* wp = Wd + c * 32;
-      i32x4 w1 = *reinterpret_cast<const i32x4*>(wp);
-      i32x4 w2 = *reinterpret_cast<const i32x4*>(wp + 16);
+      bf[ks] = *reinterpret_cast<const i32x4*>(B + rb * XG_BK + ((c ^ (rb & 7)) << 4));
+    };
+    auto load_digits = [&](int t) {
+      const int8_t* wp = wb[t / S] + (t % S) * 256;
+      w1[t % 3] = *reinterpret_cast<const i32x4*>(wp);
+      w2[t % 3] = *reinterpret_cast<const i32x4*>(wp + 16);
+    };
+    auto perm = [&](int t) {
+      i32x4 r;
 #pragma unroll
-      for (int s = 0; s < S; s++) {
-        i32x4 bs;
+      for (int e = 0; e < 4; e++)
+        r[e] = (int)__builtin_amdgcn_perm((uint32_t)w1[t % 3][e], (uint32_t)w2[t % 3][e], (uint32_t)bf[t / S][e]);
+      return r;
+    };
+    // software pipeline over the 2S (k-step, slice) pairs t: the MFMAs of t issue beside the v_perms of
+    // t + 1 (digits loaded at t − 2) and the digit loads of t + 3
+    load_frags(0);
+    load_digits(0);
+    load_digits(1);
+    load_digits(2);
+    i32x4 bs = perm(0);
 #pragma unroll
-        for (int e = 0; e < 4; e++) bs[e] = (int)__builtin_amdgcn_perm((uint32_t)w1[e], (uint32_t)w2[e], (uint32_t)bf[e]);
-        if (s + 1 < S) {
-          w1 = *reinterpret_cast<const i32x4*>(wp + (s + 1) * 256);
-          w2 = *reinterpret_cast<const i32x4*>(wp + (s + 1) * 256 + 16);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-        __builtin_amdgcn_s_setprio(1);
+    for (int t = 0; t < NKS * S; t++) {
+      const int ks = t / S, s = t % S;
+      if (s == 1 && ks + 1 < NKS) load_frags(ks + 1);
+      i32x4 bn = bs;
+      if (t + 1 < NKS * S) bn = perm(t + 1);
+      if (t + 3 < NKS * S) load_digits(t + 3);
+      __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-        for (int m = 0; m < 4; m++) acc[s][m] = __builtin_amdgcn_mfma_i32_16x16x64_i8(af[m], bs, acc[s][m], 0, 0, 0);
-        __builtin_amdgcn_s_setprio(0);
-        __builtin_amdgcn_sched_barrier(0);
+      for (int m = 0; m < 4; m++) acc[s][m] = __builtin_amdgcn_mfma_i32_16x16x64_i8(af[ks][m], bs, acc[s][m], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+#pragma unroll
+      for (int m = 0; m < 4; m++) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // one MFMA
+        __builtin_amdgcn_sched_group_barrier(0x002, 1, 0);  // one VALU (a v_perm of t + 1)
       }
+      __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);    // the digit loads of t + 3
+      __builtin_amdgcn_sched_barrier(0);
+      bs = bn;
     }
   }
 
@@ -409,7 +469,7 @@ xg_gemm_kernel(const int8_t* __restrict__ Dt, const int8_t* __restrict__ St, int
 
 // ---- host side ---------------------------------------------------------------------------------
 struct XgLayout {
-  int64_t npad, kp, nst, jr, nr, ncp;
+  int64_t npad, kp, nst, nr, ncp;
   int64_t off_dt, off_st, off_ww, off_w, off_t, off_v, off_cp, off_up, off_nu, off_c, off_info, total;
 };
 
@@ -418,9 +478,7 @@ static XgLayout xg_layout(int64_t n, int64_t p) {
   L.npad = npad_of(n);
   L.kp = round_up(p < 1 ? 1 : p, XG_BK);
   L.nst = L.kp / XG_BK;
-  L.jr = std::max<int64_t>(256, (p + 255) / 256);
-  L.nr = (p + L.jr - 1) / L.jr;
-  if (L.nr < 1) L.nr = 1;
+  L.nr = std::min<int64_t>(L.kp / 64, 64);  // loci-tile groups of the transpose + U kernel
   L.ncp = (L.kp + XG_UBLK - 1) / XG_UBLK;
   int64_t o = 0;
   auto take = [&](int64_t bytes) {
@@ -430,7 +488,7 @@ static XgLayout xg_layout(int64_t n, int64_t p) {
   };
   L.off_dt = take(L.npad * L.kp);
   L.off_st = take(L.npad * L.kp);
-  L.off_ww = take(L.nst * XG_SMAX * 256 + XG_WWSTAGE);
+  L.off_ww = take(L.nst * XG_SMAX * 256 + 4096);
   L.off_w = take(8 * L.kp);
   L.off_t = take(8 * L.kp);
   L.off_v = take(16 * L.kp);
@@ -482,11 +540,9 @@ int launch_grm_exact(const int8_t* D, int64_t ldd, int64_t p, int64_t n, int plo
   XgInfo* info = reinterpret_cast<XgInfo*>(w8 + L.off_info);
 
   xg_info_init_kernel<<<1, 1, 0, s>>>(info);
-  const int sgrid = (int)std::min<int64_t>(p, 256 * 32);
+  const int sgrid = (int)std::min<int64_t>((p + 3) / 4, 1024);  // one wave per locus
   xg_stats_kernel<<<sgrid, 256, 0, s>>>(D, ldd, p, n, 1.0 / ploidy, mean, sd, keep,
                                         reinterpret_cast<unsigned long long*>(q_dev), w, tcol, info);
-  GBM_LAUNCH_CHECK();
-  xg_transpose_kernel<<<dim3((unsigned)(L.kp / 64), (unsigned)(L.npad / 64)), 256, 0, s>>>(D, ldd, p, n, L.kp, Dt, St);
   GBM_LAUNCH_CHECK();
   XgInfo h{};
   GBM_HIP_TRY(hipMemcpyAsync(&h, info, sizeof(h), hipMemcpyDeviceToHost, s));
@@ -501,19 +557,19 @@ int launch_grm_exact(const int8_t* D, int64_t ldd, int64_t p, int64_t n, int plo
   if (slices_out) *slices_out = S;
   xg_digits_kernel<<<(unsigned)L.ncp, XG_UBLK, 0, s>>>(w, tcol, p, L.kp, S, F, WW, V, Cpart, info);
   GBM_LAUNCH_CHECK();
-  xg_u_kernel<<<dim3((unsigned)(L.npad / XG_UBLK + (L.npad % XG_UBLK ? 1 : 0)), (unsigned)L.nr), XG_UBLK, 0, s>>>(
-      D, ldd, p, n, V, L.jr, L.npad, Upart);
+  xg_transpose_u_kernel<<<dim3((unsigned)((L.npad + 255) / 256), (unsigned)L.nr), 256, 0, s>>>(D, ldd, p, n, L.kp, L.npad,
+                                                                                              V, Dt, St, Upart);
   GBM_LAUNCH_CHECK();
   xg_u_reduce_kernel<<<(unsigned)((L.npad + XG_UBLK - 1) / XG_UBLK), XG_UBLK, 0, s>>>(Upart, L.nr, L.npad, n, Cpart,
                                                                                       L.ncp, NU, C);
   GBM_LAUNCH_CHECK();
-  const int64_t nI = L.npad / XG_BM;
-  const int64_t nunits = nI * (nI + 1);
+  const int64_t nI = (n + XG_BM - 1) / XG_BM, nJ = (n + XG_BN - 1) / XG_BN;
+  const int64_t nunits = nI * nJ - nI * (nI - 1);
   const unsigned grid = (unsigned)nunits;
   switch (S) {
-    case 8: xg_gemm_kernel<8><<<grid, 512, 0, s>>>(Dt, St, L.kp, WW, NU, C, n, F, nI, nunits, G, ldg, accum); break;
-    case 9: xg_gemm_kernel<9><<<grid, 512, 0, s>>>(Dt, St, L.kp, WW, NU, C, n, F, nI, nunits, G, ldg, accum); break;
-    default: xg_gemm_kernel<10><<<grid, 512, 0, s>>>(Dt, St, L.kp, WW, NU, C, n, F, nI, nunits, G, ldg, accum); break;
+    case 8: xg_gemm_kernel<8><<<grid, 512, 0, s>>>(Dt, St, L.kp, WW, NU, C, n, F, nI, nJ, nunits, G, ldg, accum); break;
+    case 9: xg_gemm_kernel<9><<<grid, 512, 0, s>>>(Dt, St, L.kp, WW, NU, C, n, F, nI, nJ, nunits, G, ldg, accum); break;
+    default: xg_gemm_kernel<10><<<grid, 512, 0, s>>>(Dt, St, L.kp, WW, NU, C, n, F, nI, nJ, nunits, G, ldg, accum); break;
   }
   GBM_LAUNCH_CHECK();
   return GBM_OK;
