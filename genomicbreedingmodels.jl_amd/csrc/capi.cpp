@@ -124,6 +124,7 @@ struct Shard {
   int64_t j0 = 0, p = 0;
   int64_t q_host = 0;
   int64_t stream = 0;  // loci per chunk of the loci-streamed mode (plan_streaming); 0: resident
+  bool exact = false;  // the exact-integer GRM of the resident dosages (grm_exact.hip, GBM_GRM=exact)
   int leader = -1;  // index of the shard that holds this device's summed GRM (itself if first)
   ~Shard() {
     if (c) pool().release(std::move(c));
@@ -527,6 +528,40 @@ int stream_grm_shard(const Problem& pr, Shard& sh) {
     if (errs[k] < 0)
       return fail(GBM_E_HIP, "GRM in-order carry accumulation (streamed chunk " + std::to_string(k) +
                                  "): an inter-workgroup wait timed out (G is invalid)");
+  return GBM_OK;
+}
+
+// The exact-integer GRM (grm_exact.hip) of a dosage shard: the dosages stay resident as
+// bytes (uploaded, or generated on the device), their GRM is computed exactly by int8 digit GEMMs, and
+// the marker effects re-read them (stream_effects_shard). Chosen per call by GBM_GRM=exact for int8 and
+// synthetic sources of diploid dosages; no fp64 genotype rows are formed.
+bool exact_grm_wanted(const Problem& pr) {
+  const char* e = getenv("GBM_GRM");
+  return e && strcmp(e, "exact") == 0 && (pr.src == Source::SYNTH || (pr.src == Source::I8 && pr.ploidy == 2));
+}
+
+int exact_grm_shard(const Problem& pr, Shard& sh) {
+  FitCtx& c = sh.x();
+  const int64_t n = pr.n, gdim = gdim_of(n), pl = sh.p;
+  GBM_HIP_TRY(hipSetDevice(c.dev));
+  hipStream_t s = c.stream.s;
+  GBM_TRY(ensure(c.D8, c.dev, pl * n));
+  GBM_TRY(ensure(c.mean, c.dev, pl * 8));
+  GBM_TRY(ensure(c.sd, c.dev, pl * 8));
+  GBM_TRY(ensure(c.keep, c.dev, pl * 4));
+  GBM_TRY(ensure(c.q, c.dev, 8));
+  GBM_TRY(ensure(c.G, c.dev, gdim * gdim * 8));
+  const int64_t wsb = gbm_dev_grm_exact_workspace(n, pl);
+  GBM_TRY(ensure(c.wsg, c.dev, wsb));
+  if (pr.src == Source::SYNTH)
+    GBM_TRY(gbm_dev_synth_dosage_i8((int8_t*)c.D8.p, n, pl, n, pr.seed, sh.j0, s));
+  else
+    GBM_HIP_TRY(hipMemcpy2DAsync(c.D8.p, n, pr.D + sh.j0 * pr.ld, pr.ld, n, pl, hipMemcpyHostToDevice, s));
+  GBM_HIP_TRY(hipMemsetAsync(c.q.p, 0, 8, s));
+  GBM_TRY(launch_grm_exact((const int8_t*)c.D8.p, n, pl, n, 2, (double*)c.G.p, gdim, (double*)c.mean.p,
+                           (double*)c.sd.p, (int32_t*)c.keep.p, (int64_t*)c.q.p, 0, c.wsg.p, wsb, nullptr, s));
+  GBM_HIP_TRY(hipMemcpyAsync(&sh.q_host, c.q.p, 8, hipMemcpyDeviceToHost, s));
+  GBM_HIP_TRY(hipStreamSynchronize(s));
   return GBM_OK;
 }
 
@@ -977,7 +1012,7 @@ int solve_effects(const Problem& pr, std::vector<std::unique_ptr<Shard>>& shards
     hipStream_t s = c.stream.s;
     if (sh.leader != (int)k)
       GBM_HIP_TRY(hipMemcpyAsync(c.A.p, shards[sh.leader]->x().A.p, nt * npad * 8, hipMemcpyDeviceToDevice, s));
-    if (sh.stream)
+    if (sh.stream || sh.exact)
       GBM_TRY(stream_effects_shard(pr, sh, nt, inv_q));
     else
       GBM_TRY(gbm_dev_marker_effects((const double*)c.Xt.p, npad, sh.p, n, (const double*)c.A.p, npad, nt, inv_q,
@@ -1066,13 +1101,17 @@ int run_fit(const Problem& pr, const double* Y, int64_t ldy, int64_t nrhs, doubl
   int64_t pmax = 0;
   for (auto& sh : shards) pmax = std::max(pmax, sh->p);
   const int64_t chunk = pr.src == Source::SYNTH ? 0 : host_chunk(pmax);
-  GBM_TRY(plan_streaming(pr, shards, reml != nullptr));
+  if (exact_grm_wanted(pr))
+    for (auto& sh : shards) sh->exact = true;  // resident bytes: nothing to stream
+  else
+    GBM_TRY(plan_streaming(pr, shards, reml != nullptr));
   {
     // each shard's GRM is launched behind its own standardisation (a shard without polymorphic
     // loci contributes a zero partial; q == 0 over all shards fails below): streamed when its
     // rows do not fit, else resident (host chunks pipelined with the GRM, or in one piece)
     RoctxRange r("gbm: upload + standardise + GRM");
     GBM_TRY(parallel_shards(shards, [&](size_t, Shard& sh) {
+      if (sh.exact) return exact_grm_shard(pr, sh);
       if (sh.stream) return stream_grm_shard(pr, sh);
       if (chunk > 0) return upload_grm_pipelined(pr, sh, chunk);
       return prepare_grm_shard(pr, sh);

@@ -63,6 +63,10 @@ int launch_marker_rows(const double* Zt, int64_t ldz, int64_t p, int64_t n, cons
 int launch_marker_rows_i8(const int8_t* D, int64_t ldd, int64_t p, int64_t n, int ploidy, const double* A, int64_t lda,
                           int64_t nrhs, double inv_q, const int64_t* q_dev, const double* mean, const double* sd,
                           const int32_t* keep, double* B, int64_t ldb, hipStream_t s);
+// the exact-integer GRM of diploid dosage rows (grm_exact.hip)
+int launch_grm_exact(const int8_t* D, int64_t ldd, int64_t p, int64_t n, int ploidy, double* G, int64_t ldg,
+                     double* mean, double* sd, int32_t* keep, int64_t* q_dev, int accum, void* ws, int64_t ws_bytes,
+                     int32_t* slices_out, hipStream_t s);
 int launch_weighted_sum(const double* mean, const double* B, int64_t ldb, int64_t p, int64_t nrhs, double* msum,
                         hipStream_t s);
 int launch_center_columns(const double* Xt, int64_t ldx, int64_t p, int64_t n, double* Zt, int64_t ldz, double* mean,

@@ -200,3 +200,32 @@ def test_exact_full_size_c2_against_fp64_grm():
     assert err < 1e-12, err
     q = int(ex.q.item())
     assert abs(float(torch.diagonal(ex.G[:n, :n]).mean()) / q - (n - 1) / n) < 1e-12
+
+
+@pytest.mark.parametrize("devices", [(0,), (0, 0)])
+def test_c_abi_exact_synthetic_matches_oracle(monkeypatch, devices):
+    """gbm_gblup_fit_synthetic with GBM_GRM=exact (the C-ABI entry a Julia ccall binds): one shard, and two
+    shards on one device (their exact partial GRMs summed), against the oracle and the fp64 path."""
+    n, p, seed = 700, 5000, 77
+    X = oracle.synth_genotypes(seed, n, p)
+    Y = oracle.synth_phenotypes(X, seed + 1, ntraits=2)
+    monkeypatch.setenv("GBM_GRM", "exact")
+    b, y, mu, q = gbm.gblup_synthetic(seed, n, p, Y, lambda_=1.0, devices=list(devices))
+    ref = oracle.gblup_fit(X, Y, 1.0)
+    assert q == ref["q"]
+    assert rel(y, ref["y_pred"]) < 1e-9 and rel(mu, ref["mu"]) < 1e-9 and rel(b, ref["b_hat"]) < 1e-6
+    monkeypatch.delenv("GBM_GRM")
+    b0, y0, mu0, q0 = gbm.gblup_synthetic(seed, n, p, Y, lambda_=1.0, devices=list(devices))
+    assert q0 == q and rel(y, y0) < 1e-11 and rel(b, b0) < 1e-9
+
+
+def test_c_abi_exact_dosage_matches_oracle(monkeypatch):
+    n, p = 600, 3000
+    D = random_dosages(21, n, p)
+    X = D.astype(np.float64) / 2.0
+    Y = oracle.synth_phenotypes(X, 5, ntraits=1)
+    monkeypatch.setenv("GBM_GRM", "exact")
+    b, y, mu, q = gbm.gblup_dosage(np.asfortranarray(D), 2, Y)
+    ref = oracle.gblup_fit(X, Y, 1.0)
+    assert q == ref["q"]
+    assert rel(y, ref["y_pred"]) < 1e-9 and rel(b, ref["b_hat"]) < 1e-6
