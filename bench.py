@@ -58,6 +58,7 @@ def parse():
     ap.add_argument("--same-device", action="store_true", help="all ranks on cuda:0 (rehearsal on a 1-GPU box)")
     ap.add_argument("--stream-chunk", type=int, default=0,
                     help="loci per chunk of the loci-streamed mode (int8 dosages resident); 0 = resident fp64 X")
+    ap.add_argument("--no-exact", action="store_true", help="skip the exact-integer GRM measurement beside the fp64 line")
     ap.add_argument("--grm", choices=("fp64", "exact"), default="fp64",
                     help="fp64: the fp64-MFMA SYRK on standardised rows; exact: int8 dosages resident, the GRM "
                          "computed exactly by int8-MFMA digit GEMMs with int128 centring (csrc/grm_exact.hip)")
@@ -135,16 +136,11 @@ def cpu_baseline(args, Y, gpu):
                      f"{args.nrhs} trait(s), one full fit in {dt:.2f} s (standardise + GRM + Cholesky + solves + "
                      f"marker effects; generation untimed)"}
     if p == args.loci:
-        def rel(a, b):
-            return float(np.abs(np.asarray(a) - np.asarray(b)).max() / max(np.abs(np.asarray(b)).max(), 1e-300))
-        parity = {"oracle": "oracle/oracle.py gblup_fit (numpy/LAPACK fp64) on the same X and Y as the GPU step",
-                  "n": n, "p": p, "q_equal": int(ref["q"]) == int(gpu["q"]),
-                  "rel_err_y_pred": rel(gpu["y_pred"], ref["y_pred"]), "rel_err_mu": rel(gpu["mu"], ref["mu"]),
-                  "rel_err_b_hat": rel(gpu["b_hat"], ref["b_hat"]), "tolerance_y_pred": 1e-9}
-        parity["pass"] = bool(parity["q_equal"] and parity["rel_err_y_pred"] < 1e-9 and parity["rel_err_mu"] < 1e-9
-                              and parity["rel_err_b_hat"] < 1e-6)
+        parity = parity_of(gpu, ref)
+        parity.update({"n": n, "p": p})
     else:
         parity = {"skipped": f"CPU sample p={p} differs from the GPU step's p={args.loci}"}
+        ref = None
     if lib is not None:
         t = args.nrhs
         b = np.zeros((p + 1, t), order="F")
@@ -161,7 +157,20 @@ def cpu_baseline(args, Y, gpu):
                            "sample": f"plain C/OpenMP restatement (oracle/gbm_oracle.c gbm_ref_gblup_fit, gcc -O3 "
                                      f"-fopenmp) on the same n={n} x p={p} fit: {dtc:.2f} s; GEBVs equal the numpy "
                                      f"fit's to 1e-8"}
-    return out, parity
+    return out, parity, ref
+
+
+def parity_of(gpu, ref):
+    """rel. errors of y_pred, μ̂, b_hat of a GPU fit against the oracle's fit of the same X and Y."""
+    def rel(a, b):
+        return float(np.abs(np.asarray(a) - np.asarray(b)).max() / max(np.abs(np.asarray(b)).max(), 1e-300))
+    parity = {"oracle": "oracle/oracle.py gblup_fit (numpy/LAPACK fp64) on the same X and Y as the GPU step",
+              "q_equal": int(ref["q"]) == int(gpu["q"]),
+              "rel_err_y_pred": rel(gpu["y_pred"], ref["y_pred"]), "rel_err_mu": rel(gpu["mu"], ref["mu"]),
+              "rel_err_b_hat": rel(gpu["b_hat"], ref["b_hat"]), "tolerance_y_pred": 1e-9}
+    parity["pass"] = bool(parity["q_equal"] and parity["rel_err_y_pred"] < 1e-9 and parity["rel_err_mu"] < 1e-9
+                          and parity["rel_err_b_hat"] < 1e-6)
+    return parity
 
 
 def cpu_baseline_c3(args):
@@ -360,45 +369,76 @@ def main():
     torch.cuda.synchronize()
 
     labels = ["begin", "standardize", "grm_syrk", "grm_reduce", "allreduce", "solve", "effects", "download"]
-    recs = []
 
-    def make_marks():
-        evs = {}
+    def run_steps(st):
+        """W untimed steps, then K steps timed between barrier + synchronize pairs (max over ranks);
+        returns (ms per step, mean per-stage event times, the last step's results)."""
+        recs = []
 
-        def mark(label):
-            e = torch.cuda.Event(enable_timing=True)
-            e.record()
-            evs[label] = e
-        return evs, mark
+        def make_marks():
+            evs = {}
 
-    for _ in range(args.warmup):
-        sharded_gblup_step(st, comm)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    out = None
-    for _ in range(args.steps):
-        evs, mark = make_marks()
-        out = sharded_gblup_step(st, comm, events=mark)
-        recs.append(evs)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+            def mark(label):
+                e = torch.cuda.Event(enable_timing=True)
+                e.record()
+                evs[label] = e
+            return evs, mark
 
-    stage_ms = {}
-    for a, b in zip(labels[:-1], labels[1:]):
-        stage_ms[b] = float(np.mean([r[a].elapsed_time(r[b]) for r in recs]))
+        for _ in range(args.warmup):
+            sharded_gblup_step(st, comm)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        out = None
+        for _ in range(args.steps):
+            evs, mark = make_marks()
+            out = sharded_gblup_step(st, comm, events=mark)
+            recs.append(evs)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        elapsed = time.perf_counter() - t0
+        if world > 1:
+            t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            elapsed = float(t.item())
+        stage = {}
+        for a, b in zip(labels[:-1], labels[1:]):
+            stage[b] = float(np.mean([r[a].elapsed_time(r[b]) for r in recs]))
+        return elapsed * 1000.0 / args.steps, stage, out
+
+    ms_per_step, stage_ms, out = run_steps(st)
     syrk_ms = stage_ms["grm_syrk"]
-    ms_per_step = elapsed * 1000.0 / args.steps
     value = n * p_total / (ms_per_step / 1000.0)
+
+    # the exact-integer GRM path (§4.8) on the same genotypes and phenotypes, measured beside the fp64
+    # headline at N = 1: int8 dosages resident, the GRM exact up to each locus weight's fp64 rounding
+    alt = None
+    if world == 1 and not exact and not args.stream_chunk and not args.no_exact:
+        q_fp64 = int(st.q.item())
+        ex = HipExactShardStages(n, p_local, nrhs=args.nrhs, lambda_=args.lam, device=dev)
+        ex.generate(args.seed, j0)
+        ex.load_phenotypes(Y)
+        torch.cuda.synchronize()
+        ems, estage, eout = run_steps(ex)
+        S = int(ex.slices.value)
+        grm_ops = S * float(n) * (n + 1) * p_local
+        tops = grm_ops / (estage["grm_syrk"] / 1000.0) / 1e12
+        alt = {"path": "exact-integer GRM (bench.py --grm exact; csrc/grm_exact.hip, DESIGN.md §4.8): int8 dosages "
+                       "resident, G = exact int8-MFMA digit GEMMs + int128 centring, one fp64 rounding; f64 solve",
+               "value": n * p_total / (ems / 1000.0), "unit": "genotype-cells/s", "ms_per_step": ems,
+               "speedup_vs_fp64_path": ms_per_step / ems, "stage_ms": estage, "digit_slices": S,
+               "q_equal_fp64_path": int(ex.q.item()) == q_fp64,
+               "roofline": {"bound": "mfma", "kernel": f"xg_gemm_kernel<{S}> + prep kernels (GRM stage)",
+                            "achieved": tops, "peak": PEAK_I8_TOPS, "unit": "TOPS (int8)", "frac": tops / PEAK_I8_TOPS,
+                            "ops_per_launch": grm_ops},
+               "gpu": {"y_pred": eout["y_pred"], "mu": eout["mu"], "q": int(ex.q.item()),
+                       "b_hat": assemble_b_hat(eout["mu"], eout["msum"], [eout["B"]], p_local)}}
+        del ex
+        torch.cuda.empty_cache()
 
     # sanity: finite GEBVs, b0 assembled
     assert np.all(np.isfinite(out["y_pred"])) and np.all(np.isfinite(out["B"]))
@@ -484,7 +524,9 @@ def main():
     if world == 1 and not args.no_cpu_baseline and oracle_fits:
         gpu = {"y_pred": out["y_pred"], "mu": out["mu"], "q": int(st.q.item()),
                "b_hat": assemble_b_hat(out["mu"], out["msum"], [out["B"]], p_local)}
-        rec["cpu_baseline"], rec["parity"] = cpu_baseline(args, Y, gpu)
+        rec["cpu_baseline"], rec["parity"], ref = cpu_baseline(args, Y, gpu)
+        if alt is not None and ref is not None:
+            alt["parity"] = parity_of(alt["gpu"], ref)
         if not args.no_cpu_c3:
             rec["cpu_baseline_c3_extrapolated"] = cpu_baseline_c3(args)
     elif world == 1 and not args.no_cpu_baseline and (n, p_local) == (50000, 600000):
@@ -495,6 +537,9 @@ def main():
     else:
         rec["cpu_baseline"] = None
         rec["parity"] = {"skipped": "multi-rank run, or --no-cpu-baseline, or a size the oracle cannot fit in seconds"}
+    if alt is not None:
+        alt.pop("gpu", None)
+        rec["exact_grm_path"] = alt
     print(json.dumps(rec), flush=True)
     if world > 1:
         dist.destroy_process_group()
