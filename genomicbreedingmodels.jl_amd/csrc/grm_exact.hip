@@ -308,11 +308,35 @@ __device__ __forceinline__ void xg_unit(int64_t u, int64_t nI, int64_t nJ, int64
   J = 2 * r + (u - base);
 }
 
+// Blocked order (GBM_XG_ORDER unset or 1): the units grouped in blocks of XG_OBI row blocks x XG_OBJ column
+// blocks (32 = the CUs of an XCD), blocks row-major, units row-major inside a block; with the XCD remap an
+// XCD's concurrently running units then share 4 A and 8 B operand strips (per stage 4·16 + 8·8 KB of distinct
+// L2 lines instead of 16 + 32·8 KB in plain row-major order).
+constexpr int XG_OBI = 4, XG_OBJ = 8;
+__device__ __forceinline__ void xg_unit_blocked(int64_t u, int64_t nI, int64_t nJ, int64_t& I, int64_t& J) {
+  for (int64_t bi = 0; bi * XG_OBI < nI; bi++) {
+    for (int64_t bj = 0; bj * XG_OBJ < nJ; bj++) {
+      const int64_t i1 = min(nI, (bi + 1) * XG_OBI), j0 = bj * XG_OBJ, j1 = min(nJ, (bj + 1) * XG_OBJ);
+      for (int64_t ii = bi * XG_OBI; ii < i1; ii++) {
+        const int64_t lo = max(2 * ii, j0), cnt = j1 > lo ? j1 - lo : 0;
+        if (u < cnt) {
+          I = ii;
+          J = lo + u;
+          return;
+        }
+        u -= cnt;
+      }
+    }
+  }
+  I = nI;  // not reached for u < nunits
+  J = nJ;
+}
+
 template <int S>
 __global__ void __launch_bounds__(512, 1)
 xg_gemm_kernel(const int8_t* __restrict__ Dt, const int8_t* __restrict__ St, int64_t kp, const int8_t* __restrict__ WW,
                const i128* __restrict__ NU, const i128* __restrict__ Cp, int64_t n, int F, int64_t nI, int64_t nJ, int64_t nunits,
-               double* __restrict__ G, int64_t ldg, int accum) {
+               double* __restrict__ G, int64_t ldg, int accum, int order) {
   __shared__ __attribute__((aligned(16))) int8_t lds[XG_NS * XG_STAGE];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -324,7 +348,10 @@ xg_gemm_kernel(const int8_t* __restrict__ Dt, const int8_t* __restrict__ St, int
   const int64_t u = (x < xr ? x * (xq + 1) : xr * (xq + 1) + (x - xr) * xq) + b / 8;
   if (u >= nunits) return;
   int64_t I, J;
-  xg_unit(u, nI, nJ, I, J);
+  if (order)
+    xg_unit_blocked(u, nI, nJ, I, J);
+  else
+    xg_unit(u, nI, nJ, I, J);
   const int64_t i0 = I * XG_BM, j0 = J * XG_BN;
   const int64_t wr0 = i0 + wm * 64, wc0 = j0 + wn * 16;
   const bool active = !(wc0 + 15 < wr0) && wr0 < n && wc0 < n;
@@ -566,10 +593,12 @@ int launch_grm_exact(const int8_t* D, int64_t ldd, int64_t p, int64_t n, int plo
   const int64_t nI = (n + XG_BM - 1) / XG_BM, nJ = (n + XG_BN - 1) / XG_BN;
   const int64_t nunits = nI * nJ - nI * (nI - 1);
   const unsigned grid = (unsigned)nunits;
+  const char* oe = getenv("GBM_XG_ORDER");
+  const int order = (oe && *oe) ? atoi(oe) : 1;
   switch (S) {
-    case 8: xg_gemm_kernel<8><<<grid, 512, 0, s>>>(Dt, St, L.kp, WW, NU, C, n, F, nI, nJ, nunits, G, ldg, accum); break;
-    case 9: xg_gemm_kernel<9><<<grid, 512, 0, s>>>(Dt, St, L.kp, WW, NU, C, n, F, nI, nJ, nunits, G, ldg, accum); break;
-    default: xg_gemm_kernel<10><<<grid, 512, 0, s>>>(Dt, St, L.kp, WW, NU, C, n, F, nI, nJ, nunits, G, ldg, accum); break;
+    case 8: xg_gemm_kernel<8><<<grid, 512, 0, s>>>(Dt, St, L.kp, WW, NU, C, n, F, nI, nJ, nunits, G, ldg, accum, order); break;
+    case 9: xg_gemm_kernel<9><<<grid, 512, 0, s>>>(Dt, St, L.kp, WW, NU, C, n, F, nI, nJ, nunits, G, ldg, accum, order); break;
+    default: xg_gemm_kernel<10><<<grid, 512, 0, s>>>(Dt, St, L.kp, WW, NU, C, n, F, nI, nJ, nunits, G, ldg, accum, order); break;
   }
   GBM_LAUNCH_CHECK();
   return GBM_OK;
