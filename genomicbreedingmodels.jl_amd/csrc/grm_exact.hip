@@ -203,7 +203,7 @@ __global__ void __launch_bounds__(XG_UBLK) xg_digits_kernel(const double* __rest
 // partial U_i = Σ_j V_j d_ij over this block's loci tiles --------------------------------------------------
 // St byte at locus k (b = k mod 4, its byte in the dword): d = 2 → b (the 2ω dword, v_perm src1),
 // d = 1 → 4 + b (the ω dword, src0), d = 0 → 12 (v_perm's constant zero).
-// Block (x, y): individuals [256x, 256x + 256), the 64-locus tiles y, y + gridDim.y, ...: each tile read
+// Block (x, y): individuals [256x, 256x + 256), the y-th contiguous range of 64-locus tiles: each tile read
 // row by row (4 dosages per lane) into LDS, then one thread per individual assembles its 64 bytes of Dt and
 // St and adds its V_j d_ij (V_j wave-uniform).
 constexpr int XG_TP = 256 + 16;  // LDS row pitch of the 64-locus x 256-individual tile
@@ -216,9 +216,12 @@ __global__ void __launch_bounds__(256) xg_transpose_u_kernel(const int8_t* __res
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const bool al4 = (ldd % 4) == 0 && ((uintptr_t)D % 4) == 0;
   const int64_t i = i0 + threadIdx.x;
-  const int64_t nkt = kp / 64;
+  // a contiguous range of tiles per block: a thread's 64-byte row pieces of consecutive tiles complete
+  // the same 128-byte lines back to back (strided tiles left half-written lines to other CUs)
+  const int64_t nkt = kp / 64, per = (nkt + gridDim.y - 1) / gridDim.y;
+  const int64_t kt0 = (int64_t)blockIdx.y * per, kt1 = min(nkt, kt0 + per);
   i128 u = 0;
-  for (int64_t kt = blockIdx.y; kt < nkt; kt += gridDim.y) {
+  for (int64_t kt = kt0; kt < kt1; kt++) {
     const int64_t k0 = kt * 64;
     __syncthreads();  // the previous tile's reads are done
     uint32_t vr[16];
