@@ -47,11 +47,9 @@ typedef int i32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int XG_BM = 128;       // tile rows (individuals i)
 constexpr int XG_BN = 64;        // tile columns (individuals k)
-constexpr int XG_BK = 128;       // loci per LDS stage (bytes per operand row)
+constexpr int XG_BK = 128;       // loci per digit group (the GEMM stages 128 or 256 loci: XgStage)
+constexpr int XG_KALIGN = 256;   // kp (padded loci) multiple: whole stages for either BK
 constexpr int XG_SMIN = 8, XG_SMAX = 10;
-constexpr int XG_WWSTAGE = 3072;  // digit bytes per stage in LDS (S·256 used: three 1-KB DMA pieces)
-constexpr int XG_STAGE = XG_BM * XG_BK + XG_BN * XG_BK + XG_WWSTAGE;  // 28 KB
-constexpr int XG_NS = 4;          // ring depth (3 stages in flight)
 constexpr int XG_UBLK = 256;      // threads per block of the U / digits kernels
 
 struct XgInfo {  // device scratch written by the stats kernel, read by the host once
@@ -335,12 +333,35 @@ __device__ __forceinline__ void xg_unit_blocked(int64_t u, int64_t nI, int64_t n
   J = nJ;
 }
 
-template <int S>
+// Stage geometry per BK (loci per LDS stage): operand rows of BK bytes, the stage's digits (BK/128 groups of
+// S·256 bytes; up to 10 slices) in whole 1-KB DMA pieces, the ring depth that fits 160 KB of LDS.
+template <int BK>
+struct XgStage {
+  static constexpr int kWW = BK == 128 ? 3072 : 5120;  // digit bytes in LDS (>= (BK/128)·XG_SMAX·256... at S <= 10)
+  static constexpr int kBytes = XG_BM * BK + XG_BN * BK + kWW;
+  static constexpr int kNS = BK == 128 ? 4 : 3;        // ring depth: kNS − 1 stages in flight
+  static constexpr int kA = XG_BM * BK / 1024 / 8;     // A pieces per wave
+  static constexpr int kB = XG_BN * BK / 1024 / 8;     // B pieces per wave
+  static constexpr int kWWp = kWW / 1024;              // digit pieces (waves 0 .. kWWp − 1, one each)
+  static constexpr int kRows = 1024 / BK;               // operand rows per piece
+  __device__ static int swz(int r) { return BK == 128 ? (r & 7) : (r & 15); }  // conflict-free ds_read_b128
+};
+
+template <int N>
+__device__ __forceinline__ void wait_vm_n(int pieces) {  // s_waitcnt vmcnt(N · pieces), pieces ∈ {kL, kL + 1}
+  if (pieces == 3) wait_vm<3 * N>();
+  else if (pieces == 4) wait_vm<4 * N>();
+  else if (pieces == 6) wait_vm<6 * N>();
+  else wait_vm<7 * N>();
+}
+
+template <int S, int BK>
 __global__ void __launch_bounds__(512, 1)
 xg_gemm_kernel(const int8_t* __restrict__ Dt, const int8_t* __restrict__ St, int64_t kp, const int8_t* __restrict__ WW,
                const i128* __restrict__ NU, const i128* __restrict__ Cp, int64_t n, int F, int64_t nI, int64_t nJ, int64_t nunits,
                double* __restrict__ G, int64_t ldg, int accum, int order) {
-  __shared__ __attribute__((aligned(16))) int8_t lds[XG_NS * XG_STAGE];
+  using SG = XgStage<BK>;
+  __shared__ __attribute__((aligned(16))) int8_t lds[SG::kNS * SG::kBytes];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wm = wave >> 2, wn = wave & 3;  // 2 x 4 waves of 64 x 16
@@ -358,46 +379,45 @@ xg_gemm_kernel(const int8_t* __restrict__ Dt, const int8_t* __restrict__ St, int
   const int64_t i0 = I * XG_BM, j0 = J * XG_BN;
   const int64_t wr0 = i0 + wm * 64, wc0 = j0 + wn * 16;
   const bool active = !(wc0 + 15 < wr0) && wr0 < n && wc0 < n;
-  const int64_t nst = kp / XG_BK;
+  const int64_t nst = kp / BK;
 
-  // LDS-DMA pieces of one stage (1 KB = 8 rows of 128 B each): wave w takes A pieces w and w + 8, B
-  // piece w, and waves 0-2 one digit piece each (S·256 <= 3 KB). Source chunk swizzled: LDS slot
-  // (lane & 7) of row (lane >> 3) holds chunk (lane & 7) ^ (row & 7).
-  const int prow = lane >> 3, pchunk = (lane & 7) ^ (lane >> 3);
-  const bool wdig = wave < 3;
+  // LDS-DMA pieces of one stage (1 KB = kRows operand rows): wave w takes A pieces w, w + 8, ..., B pieces
+  // w, w + 8, ..., and waves 0 .. kWWp − 1 one digit piece each. Source chunk swizzled: LDS slot s of row r
+  // holds chunk s ^ swz(r).
+  const int prow = lane / (BK / 16), pslot = lane % (BK / 16);
+  const bool wdig = wave < SG::kWWp;
+  const int pieces = SG::kA + SG::kB + (wdig ? 1 : 0);
   auto issue = [&](int64_t st) {
-    int8_t* base = lds + (int)(st % XG_NS) * XG_STAGE;
-    const int64_t koff = st * XG_BK + pchunk * 16;
-    __builtin_amdgcn_global_load_lds((const void*)(Dt + (i0 + wave * 8 + prow) * kp + koff), (void*)(base + wave * 1024), 16, 0, 0);
-    __builtin_amdgcn_global_load_lds((const void*)(Dt + (i0 + (wave + 8) * 8 + prow) * kp + koff),
-                                     (void*)(base + (wave + 8) * 1024), 16, 0, 0);
-    __builtin_amdgcn_global_load_lds((const void*)(St + (j0 + wave * 8 + prow) * kp + koff),
-                                     (void*)(base + XG_BM * XG_BK + wave * 1024), 16, 0, 0);
-    if (wdig)
-      __builtin_amdgcn_global_load_lds((const void*)(WW + st * (int64_t)(S * 256) + wave * 1024 + lane * 16),
-                                       (void*)(base + XG_BM * XG_BK + XG_BN * XG_BK + wave * 1024), 16, 0, 0);
-  };
-  // stage st's pieces have landed (this wave's, by a counted wait — 4 pieces per stage on waves 0-2,
-  // 3 on the rest; the others', by the barrier) and every wave has finished reading the buffer the
-  // next issue overwrites (read one stage earlier)
-  auto arrive = [&](int64_t st) {
-    if (wdig) {
-      if (st + 2 < nst)
-        wait_vm<8>();
-      else if (st + 1 < nst)
-        wait_vm<4>();
-      else
-        wait_vm<0>();
-    } else {
-      if (st + 2 < nst)
-        wait_vm<6>();
-      else if (st + 1 < nst)
-        wait_vm<3>();
-      else
-        wait_vm<0>();
+    int8_t* base = lds + (int)(st % SG::kNS) * SG::kBytes;
+#pragma unroll
+    for (int a = 0; a < SG::kA; a++) {
+      const int xx = wave + 8 * a, r = xx * SG::kRows + prow;
+      __builtin_amdgcn_global_load_lds((const void*)(Dt + (i0 + r) * kp + st * BK + ((pslot ^ SG::swz(r)) << 4)),
+                                       (void*)(base + xx * 1024), 16, 0, 0);
     }
+#pragma unroll
+    for (int a = 0; a < SG::kB; a++) {
+      const int xx = wave + 8 * a, r = xx * SG::kRows + prow;
+      __builtin_amdgcn_global_load_lds((const void*)(St + (j0 + r) * kp + st * BK + ((pslot ^ SG::swz(r)) << 4)),
+                                       (void*)(base + XG_BM * BK + xx * 1024), 16, 0, 0);
+    }
+    if (wdig)
+      __builtin_amdgcn_global_load_lds((const void*)(WW + st * (int64_t)((BK / 128) * S * 256) + wave * 1024 + lane * 16),
+                                       (void*)(base + XG_BM * BK + XG_BN * BK + wave * 1024), 16, 0, 0);
+  };
+  // stage st's pieces have landed (this wave's, by a counted wait; the others', by the barrier) and every
+  // wave has finished reading the buffer the next issue overwrites (read one stage earlier)
+  constexpr int PD = SG::kNS - 1;
+  auto arrive = [&](int64_t st) {
+    const int64_t ahead = (nst - 1 - st) < (PD - 1) ? (nst - 1 - st) : (PD - 1);
+    if (ahead >= 2)
+      wait_vm_n<2>(pieces);
+    else if (ahead == 1)
+      wait_vm_n<1>(pieces);
+    else
+      wait_vm<0>();
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    if (st + 3 < nst) issue(st + 3);
+    if (st + PD < nst) issue(st + PD);
   };
 
   i32x4 acc[S][4];
@@ -407,35 +427,33 @@ xg_gemm_kernel(const int8_t* __restrict__ Dt, const int8_t* __restrict__ St, int
     for (int m = 0; m < 4; m++) acc[s][m] = (i32x4){0, 0, 0, 0};
 
   const int fr = lane & 15, g = lane >> 4;
-  for (int64_t st = 0; st < 3 && st < nst; st++) issue(st);
+  for (int64_t st = 0; st < PD && st < nst; st++) issue(st);
   if (!active) {  // a wave wholly below the diagonal or in the padding: stages and barriers only
     for (int64_t st = 0; st < nst; st++) arrive(st);
     return;
   }
   for (int64_t st = 0; st < nst; st++) {
     arrive(st);
-    const int8_t* A = lds + (int)(st % XG_NS) * XG_STAGE;
-    const int8_t* B = A + XG_BM * XG_BK;
-    const int8_t* Wd = B + XG_BN * XG_BK;
-    // the stage's 2S (k-step, slice) pairs in one unrolled sequence: digits two pairs ahead in a ring of
-    // three register sets, the second k-step's fragments loaded during the first k-step
-    constexpr int NKS = XG_BK / 64;
-    const int8_t* wb[NKS];
-#pragma unroll
-    for (int ks = 0; ks < NKS; ks++) wb[ks] = Wd + (ks * 4 + g) * 32;
-    i32x4 af[NKS][4], bf[NKS], w1[3], w2[3];
+    const int8_t* A = lds + (int)(st % SG::kNS) * SG::kBytes;
+    const int8_t* B = A + XG_BM * BK;
+    const int8_t* Wd = B + XG_BN * BK;
+    // the stage's NKS·S (k-step, slice) pairs in one unrolled sequence: digits two pairs ahead in a ring of
+    // three register sets, the next k-step's fragments loaded during the current k-step (ring of two)
+    constexpr int NKS = BK / 64;
+    i32x4 af[2][4], bf[2], w1[3], w2[3];
     auto load_frags = [&](int ks) {
       const int c = ks * 4 + g;  // this lane group's 16-locus chunk
 #pragma unroll
       for (int m = 0; m < 4; m++) {
         const int r = wm * 64 + m * 16 + fr;
-        af[ks][m] = *reinterpret_cast<const i32x4*>(A + r * XG_BK + ((c ^ (r & 7)) << 4));
+        af[ks & 1][m] = *reinterpret_cast<const i32x4*>(A + r * BK + ((c ^ SG::swz(r)) << 4));
       }
       const int rb = wn * 16 + fr;
-      bf[ks] = *reinterpret_cast<const i32x4*>(B + rb * XG_BK + ((c ^ (rb & 7)) << 4));
+      bf[ks & 1] = *reinterpret_cast<const i32x4*>(B + rb * BK + ((c ^ SG::swz(rb)) << 4));
     };
     auto load_digits = [&](int t) {
-      const int8_t* wp = wb[t / S] + (t % S) * 256;
+      const int ks = t / S;  // digit group ks/2 (128 loci), chunk (ks % 2)·4 + g inside it
+      const int8_t* wp = Wd + (ks >> 1) * (S * 256) + (t % S) * 256 + ((ks & 1) * 4 + g) * 32;
       w1[t % 3] = *reinterpret_cast<const i32x4*>(wp);
       w2[t % 3] = *reinterpret_cast<const i32x4*>(wp + 16);
     };
@@ -443,11 +461,11 @@ xg_gemm_kernel(const int8_t* __restrict__ Dt, const int8_t* __restrict__ St, int
       i32x4 r;
 #pragma unroll
       for (int e = 0; e < 4; e++)
-        r[e] = (int)__builtin_amdgcn_perm((uint32_t)w1[t % 3][e], (uint32_t)w2[t % 3][e], (uint32_t)bf[t / S][e]);
+        r[e] = (int)__builtin_amdgcn_perm((uint32_t)w1[t % 3][e], (uint32_t)w2[t % 3][e], (uint32_t)bf[(t / S) & 1][e]);
       return r;
     };
-    // software pipeline over the 2S (k-step, slice) pairs t: the MFMAs of t issue beside the v_perms of
-    // t + 1 (digits loaded at t − 2) and the digit loads of t + 3
+    // software pipeline over the pairs t: the MFMAs of t issue beside the v_perms of t + 1 (digits loaded at
+    // t − 2) and the digit loads of t + 3
     load_frags(0);
     load_digits(0);
     load_digits(1);
@@ -462,7 +480,7 @@ xg_gemm_kernel(const int8_t* __restrict__ Dt, const int8_t* __restrict__ St, int
       if (t + 3 < NKS * S) load_digits(t + 3);
       __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-      for (int m = 0; m < 4; m++) acc[s][m] = __builtin_amdgcn_mfma_i32_16x16x64_i8(af[ks][m], bs, acc[s][m], 0, 0, 0);
+      for (int m = 0; m < 4; m++) acc[s][m] = __builtin_amdgcn_mfma_i32_16x16x64_i8(af[ks & 1][m], bs, acc[s][m], 0, 0, 0);
       __builtin_amdgcn_s_setprio(0);
 #pragma unroll
       for (int m = 0; m < 4; m++) {
@@ -506,7 +524,7 @@ struct XgLayout {
 static XgLayout xg_layout(int64_t n, int64_t p) {
   XgLayout L{};
   L.npad = npad_of(n);
-  L.kp = round_up(p < 1 ? 1 : p, XG_BK);
+  L.kp = round_up(p < 1 ? 1 : p, XG_KALIGN);
   L.nst = L.kp / XG_BK;
   L.nr = std::min<int64_t>(L.kp / 64, 64);  // loci-tile groups of the transpose + U kernel
   L.ncp = (L.kp + XG_UBLK - 1) / XG_UBLK;
@@ -598,11 +616,16 @@ int launch_grm_exact(const int8_t* D, int64_t ldd, int64_t p, int64_t n, int plo
   const unsigned grid = (unsigned)nunits;
   const char* oe = getenv("GBM_XG_ORDER");
   const int order = (oe && *oe) ? atoi(oe) : 1;
-  switch (S) {
-    case 8: xg_gemm_kernel<8><<<grid, 512, 0, s>>>(Dt, St, L.kp, WW, NU, C, n, F, nI, nJ, nunits, G, ldg, accum, order); break;
-    case 9: xg_gemm_kernel<9><<<grid, 512, 0, s>>>(Dt, St, L.kp, WW, NU, C, n, F, nI, nJ, nunits, G, ldg, accum, order); break;
-    default: xg_gemm_kernel<10><<<grid, 512, 0, s>>>(Dt, St, L.kp, WW, NU, C, n, F, nI, nJ, nunits, G, ldg, accum, order); break;
+  const char* be = getenv("GBM_XG_BK");
+  const int bk = (be && atoi(be) == 256) ? 256 : 128;
+#define XG_LAUNCH(SS, BKK) \
+  xg_gemm_kernel<SS, BKK><<<grid, 512, 0, s>>>(Dt, St, L.kp, WW, NU, C, n, F, nI, nJ, nunits, G, ldg, accum, order)
+  if (bk == 256) {
+    if (S == 8) XG_LAUNCH(8, 256); else if (S == 9) XG_LAUNCH(9, 256); else XG_LAUNCH(10, 256);
+  } else {
+    if (S == 8) XG_LAUNCH(8, 128); else if (S == 9) XG_LAUNCH(9, 128); else XG_LAUNCH(10, 128);
   }
+#undef XG_LAUNCH
   GBM_LAUNCH_CHECK();
   return GBM_OK;
 }

@@ -9,9 +9,10 @@ timeout -k 10 400 python -u -m pytest tests/test_gpu_exact.py -x -q --timeout 18
 tail -2 gpurun_out/exact_tests.log
 if [ -z "$SKIP_AB" ]; then
 for r in 1 2; do
-  for o in 0 1; do
-    GBM_XG_ORDER=$o timeout -k 10 120 python3 tools/exact_grm_time.py 5000 50000 exact > gpurun_out/order_$o.json 2>&1 || { tail gpurun_out/order_$o.json; exit 1; }
-    python3 -c "import json; d=json.loads(open('gpurun_out/order_$o.json').read().strip().splitlines()[-1]); print('order $o', round(d['ms_per_step'],3), round(d['stage_ms']['grm_syrk'],3))"
+  for cfg in "1 128" "0 128" "1 256"; do
+    set -- $cfg
+    GBM_XG_ORDER=$1 GBM_XG_BK=$2 timeout -k 10 120 python3 tools/exact_grm_time.py 5000 50000 exact > gpurun_out/ab_$1_$2.json 2>&1 || { tail gpurun_out/ab_$1_$2.json; exit 1; }
+    python3 -c "import json; d=json.loads(open('gpurun_out/ab_$1_$2.json').read().strip().splitlines()[-1]); print('order $1 bk $2', round(d['ms_per_step'],3), round(d['stage_ms']['grm_syrk'],3))"
   done
 done
 fi
