@@ -1,0 +1,127 @@
+"""CPU checks of the exact-integer GRM's algebra (csrc/grm_exact.hip), in Python integers:
+
+* the weight grid: F = 52 − emin puts every kept weight's fp64 significand on the integers (W_j = w_j 2^F
+  exactly), and the digit count S of xg_choose holds the largest W_j in S balanced base-128 digits,
+* the digits: W = Σ_s 128^s ω_s with ω_s ∈ [−64, 63], so d·ω and d·2ω (d ∈ {0, 1, 2}) fit int8,
+* the centring identity G_ik = 2^−F/n² [n² A_ik − n U_i − n U_k + C] against the standardised-genotype
+  GRM of the reference (src/gwas.jl:112-126 before the 1/q; Z from oracle/oracle.py) — exactly, with
+  fractions, on a small case,
+* the v_perm selector encoding of the B operand (d = 2 → the 2ω byte, 1 → the ω byte, 0 → zero).
+"""
+import math
+from fractions import Fraction
+
+import numpy as np
+
+import oracle
+
+
+def weights(D):
+    n = D.shape[0]
+    Di = D.astype(np.int64)
+    t = Di.sum(0)
+    s2 = (Di * Di).sum(0)
+    num = n * s2 - t * t
+    keep = num > 0
+    w = np.where(keep, (float(n) * (n - 1.0)) / np.where(keep, num, 1).astype(np.float64), 0.0)
+    return t, w, keep
+
+
+def choose(w):
+    """xg_choose: (S, F, exact)."""
+    kept = w[w > 0]
+    emin = min(math.frexp(x)[1] - 1 for x in kept)  # ilogb
+    wmax = float(kept.max())
+    F = 52 - emin
+    W = math.ldexp(wmax, F)
+    for S in (8, 9, 10):
+        if W <= 63.0 * (2.0 ** (7 * S) - 1.0) / 127.0 * (1.0 - 1e-12):
+            return S, F, True
+    S = 10
+    return S, 7 * S - 3 - (math.frexp(wmax)[1] - 1), False
+
+
+def to_int(x, F):
+    m, e = math.frexp(x)
+    M = int(math.ldexp(m, 53))
+    sh = e - 53 + F
+    return M << sh if sh >= 0 else (M + (1 << (-sh - 1))) >> (-sh)
+
+
+def digits(W, S):
+    out = []
+    x = W
+    for _ in range(S):
+        r = x & 127
+        if r >= 64:
+            r -= 128
+        out.append(r)
+        x = (x - r) >> 7
+    assert x == 0
+    return out
+
+
+def random_dosages(seed, n, p, lo=0.05, hi=0.5):
+    rng = np.random.default_rng(seed)
+    return rng.binomial(2, rng.uniform(lo, hi, p), size=(n, p)).astype(np.int8)
+
+
+def test_grid_and_digits_are_exact():
+    for seed, (n, p) in enumerate([(300, 500), (2000, 200), (50, 1000)]):
+        D = random_dosages(seed, n, p)
+        D[:, 0] = 0
+        D[3, 0] = 1  # a single carrier: the widest weight range
+        t, w, keep = weights(D)
+        S, F, exact = choose(w)
+        assert exact and 8 <= S <= 10
+        for x in w[keep]:
+            W = to_int(float(x), F)
+            assert Fraction(W, 2 ** F) == Fraction(float(x))  # the weight itself, no rounding
+            ds = digits(W, S)
+            assert sum(d * 128 ** s for s, d in enumerate(ds)) == W
+            assert all(-64 <= d <= 63 for d in ds)
+            assert all(-128 <= k * d <= 127 for d in ds for k in (1, 2))
+
+
+def test_centring_identity_equals_standardised_grm():
+    n, p = 40, 60
+    D = random_dosages(7, n, p)
+    t, w, keep = weights(D)
+    S, F, _ = choose(w)
+    Wint = [to_int(float(x), F) if k else 0 for x, k in zip(w, keep)]
+    Di = D.astype(object)
+    A = [[sum(Wint[j] * int(Di[i, j]) * int(Di[k, j]) for j in range(p)) for k in range(n)] for i in range(n)]
+    U = [sum(Wint[j] * int(t[j]) * int(Di[i, j]) for j in range(p)) for i in range(n)]
+    C = sum(Wint[j] * int(t[j]) ** 2 for j in range(p))
+    G_exact = [[Fraction(n * n * A[i][k] - n * U[i] - n * U[k] + C, n * n * 2 ** F) for k in range(n)] for i in range(n)]
+    # the same sum with rational centring and the fp64 weights
+    for i in range(0, n, 7):
+        for k in range(0, n, 5):
+            ref = sum(Fraction(float(w[j])) * (int(Di[i, j]) - Fraction(int(t[j]), n)) * (int(Di[k, j]) - Fraction(int(t[j]), n))
+                      for j in range(p) if keep[j])
+            assert G_exact[i][k] == ref
+    # and the reference's standardised genotypes (fp64 oracle) to rounding
+    X = D.astype(np.float64) / 2.0
+    m, s, kp = oracle.colstats(X)
+    Z = oracle.standardize(X, m, s, kp)
+    Gz = Z @ Z.T
+    Gf = np.array([[float(v) for v in row] for row in G_exact])
+    assert np.abs(Gf - Gz).max() < 1e-12 * np.abs(Gz).max()
+
+
+def test_perm_selector_encoding():
+    """The St byte at locus k (b = k mod 4) selects, in v_perm(src0 = ω dword, src1 = 2ω dword, sel): bytes
+    0-3 come from src1, 4-7 from src0, 12 is the constant zero."""
+    rng = np.random.default_rng(3)
+    for _ in range(200):
+        om = rng.integers(-64, 64, 4)
+        d = rng.integers(0, 3, 4)
+        src0 = bytes((int(x) & 0xFF) for x in om)
+        src1 = bytes(((2 * int(x)) & 0xFF) for x in om)
+        pool = src1 + src0  # byte index 0..7
+        out = []
+        for b in range(4):
+            sel = b if d[b] == 2 else (4 + b if d[b] == 1 else 12)
+            out.append(0 if sel == 12 else pool[sel])
+        got = [x - 256 if x > 127 else x for x in out]
+        assert got == [int(d[b]) * int(om[b]) for b in range(4)]
