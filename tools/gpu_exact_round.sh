@@ -5,7 +5,7 @@ set -o pipefail
 export PYTHONUNBUFFERED=1
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out
-timeout -k 10 400 python -u -m pytest tests/test_gpu_exact.py -x -q --timeout 180 --timeout-method thread > gpurun_out/exact_tests.log 2>&1 || { tail -30 gpurun_out/exact_tests.log; exit 1; }
+timeout -k 10 600 python -u -m pytest tests/test_gpu_exact.py tests/test_gpu_streamed.py tests/test_gpu_parity.py -x -q --timeout 180 --timeout-method thread > gpurun_out/exact_tests.log 2>&1 || { tail -30 gpurun_out/exact_tests.log; exit 1; }
 tail -2 gpurun_out/exact_tests.log
 if [ -z "$SKIP_AB" ]; then
 for r in 1 2; do
