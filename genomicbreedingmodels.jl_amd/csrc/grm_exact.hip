@@ -359,17 +359,33 @@ template <int S, int BK>
 __global__ void __launch_bounds__(512, 1)
 xg_gemm_kernel(const int8_t* __restrict__ Dt, const int8_t* __restrict__ St, int64_t kp, const int8_t* __restrict__ WW,
                const i128* __restrict__ NU, const i128* __restrict__ Cp, int64_t n, int F, int64_t nI, int64_t nJ, int64_t nunits,
-               double* __restrict__ G, int64_t ldg, int accum, int order) {
+               double* __restrict__ G, int64_t ldg, int accum, int order, int64_t nfull, int ks_split,
+               i32x4* __restrict__ part, int32_t* __restrict__ cnt) {
   using SG = XgStage<BK>;
   __shared__ __attribute__((aligned(16))) int8_t lds[SG::kNS * SG::kBytes];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wm = wave >> 2, wn = wave & 3;  // 2 x 4 waves of 64 x 16
 
-  // XCD-aware bijective remap: the blocks the hardware deals to one XCD take a contiguous unit range
-  const int64_t nb = gridDim.x, b = blockIdx.x;
-  const int64_t xq = nb / 8, xr = nb % 8, x = b % 8;
-  const int64_t u = (x < xr ? x * (xq + 1) : xr * (xq + 1) + (x - xr) * xq) + b / 8;
+  // Blocks [0, nfull): whole units, XCD-aware bijective remap (the blocks the hardware deals to one XCD take
+  // a contiguous unit range). Blocks [nfull, ...): the last nunits − nfull units (the partial last round of a
+  // grid of one unit per CU) in ks_split loci ranges each, dispatched last and spread over every XCD; the
+  // last range of a unit to finish (per wave: a counter per unit and wave) sums the others' int32 partials.
+  const int64_t b = blockIdx.x;
+  int64_t u, st0 = 0, st1 = kp / BK, slot = -1;
+  int kpart = 0;
+  if (b < nfull) {
+    const int64_t xq = nfull / 8, xr = nfull % 8, x = b % 8;
+    u = (x < xr ? x * (xq + 1) : xr * (xq + 1) + (x - xr) * xq) + b / 8;
+  } else {
+    const int64_t pc = b - nfull;
+    slot = pc / ks_split;
+    kpart = (int)(pc % ks_split);
+    u = nfull + slot;
+    const int64_t per = (st1 + ks_split - 1) / ks_split;
+    st0 = kpart * per;
+    st1 = st0 + per < st1 ? st0 + per : st1;
+  }
   if (u >= nunits) return;
   int64_t I, J;
   if (order)
@@ -379,7 +395,6 @@ xg_gemm_kernel(const int8_t* __restrict__ Dt, const int8_t* __restrict__ St, int
   const int64_t i0 = I * XG_BM, j0 = J * XG_BN;
   const int64_t wr0 = i0 + wm * 64, wc0 = j0 + wn * 16;
   const bool active = !(wc0 + 15 < wr0) && wr0 < n && wc0 < n;
-  const int64_t nst = kp / BK;
 
   // LDS-DMA pieces of one stage (1 KB = kRows operand rows): wave w takes A pieces w, w + 8, ..., B pieces
   // w, w + 8, ..., and waves 0 .. kWWp − 1 one digit piece each. Source chunk swizzled: LDS slot s of row r
@@ -409,7 +424,7 @@ xg_gemm_kernel(const int8_t* __restrict__ Dt, const int8_t* __restrict__ St, int
   // wave has finished reading the buffer the next issue overwrites (read one stage earlier)
   constexpr int PD = SG::kNS - 1;
   auto arrive = [&](int64_t st) {
-    const int64_t ahead = (nst - 1 - st) < (PD - 1) ? (nst - 1 - st) : (PD - 1);
+    const int64_t ahead = (st1 - 1 - st) < (PD - 1) ? (st1 - 1 - st) : (PD - 1);
     if (ahead >= 2)
       wait_vm_n<2>(pieces);
     else if (ahead == 1)
@@ -417,7 +432,7 @@ xg_gemm_kernel(const int8_t* __restrict__ Dt, const int8_t* __restrict__ St, int
     else
       wait_vm<0>();
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    if (st + PD < nst) issue(st + PD);
+    if (st + PD < st1) issue(st + PD);
   };
 
   i32x4 acc[S][4];
@@ -427,12 +442,12 @@ xg_gemm_kernel(const int8_t* __restrict__ Dt, const int8_t* __restrict__ St, int
     for (int m = 0; m < 4; m++) acc[s][m] = (i32x4){0, 0, 0, 0};
 
   const int fr = lane & 15, g = lane >> 4;
-  for (int64_t st = 0; st < PD && st < nst; st++) issue(st);
+  for (int64_t st = st0; st < st0 + PD && st < st1; st++) issue(st);
   if (!active) {  // a wave wholly below the diagonal or in the padding: stages and barriers only
-    for (int64_t st = 0; st < nst; st++) arrive(st);
+    for (int64_t st = st0; st < st1; st++) arrive(st);
     return;
   }
-  for (int64_t st = 0; st < nst; st++) {
+  for (int64_t st = st0; st < st1; st++) {
     arrive(st);
     const int8_t* A = lds + (int)(st % SG::kNS) * SG::kBytes;
     const int8_t* B = A + XG_BM * BK;
@@ -493,6 +508,36 @@ xg_gemm_kernel(const int8_t* __restrict__ Dt, const int8_t* __restrict__ St, int
     }
   }
 
+  if (slot >= 0) {
+    // split unit: publish this range's partials (write-back + agent release before the counter, the guide's
+    // split-K hand-off per wave); the range that draws the last ticket acquires and adds the others'
+    i32x4* mine = part + (((slot * ks_split + kpart) * 8 + wave) * S * 4) * 64 + lane;
+#pragma unroll
+    for (int s = 0; s < S; s++)
+#pragma unroll
+      for (int m = 0; m < 4; m++) mine[(s * 4 + m) * 64] = acc[s][m];
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    int last = 0;
+    if (lane == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      last = __hip_atomic_fetch_add(&cnt[slot * 8 + wave], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ks_split - 1;
+    }
+    last = __builtin_amdgcn_readfirstlane(last);
+    if (!last) return;
+    if (lane == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    for (int kk = 0; kk < ks_split; kk++) {
+      if (kk == kpart) continue;
+      const i32x4* other = part + (((slot * ks_split + kk) * 8 + wave) * S * 4) * 64 + lane;
+#pragma unroll
+      for (int s = 0; s < S; s++)
+#pragma unroll
+        for (int m = 0; m < 4; m++) acc[s][m] += other[(s * 4 + m) * 64];
+    }
+  }
+
   // epilogue: T = n² Σ_s 128^s acc_s − NU_i − NU_k + C in int128 → G = T 2^−F / n²
   const i128 C = *Cp;
   const i128 n2 = (i128)n * (i128)n;
@@ -516,9 +561,10 @@ xg_gemm_kernel(const int8_t* __restrict__ Dt, const int8_t* __restrict__ St, int
 }
 
 // ---- host side ---------------------------------------------------------------------------------
+constexpr int64_t kXgSplitPieces = 256;  // the most (unit, loci range) pieces of the split tail (one round of 256 CUs)
 struct XgLayout {
   int64_t npad, kp, nst, nr, ncp;
-  int64_t off_dt, off_st, off_ww, off_w, off_t, off_v, off_cp, off_up, off_nu, off_c, off_info, total;
+  int64_t off_dt, off_st, off_ww, off_w, off_t, off_v, off_cp, off_up, off_nu, off_c, off_info, off_part, off_cnt, total;
 };
 
 static XgLayout xg_layout(int64_t n, int64_t p) {
@@ -545,6 +591,9 @@ static XgLayout xg_layout(int64_t n, int64_t p) {
   L.off_nu = take(16 * L.npad);
   L.off_c = take(16);
   L.off_info = take(sizeof(XgInfo));
+  // split-unit partials: at most kXgSplitPieces (unit, range) pieces x 8 waves x XG_SMAX x 4 i32x4 per lane
+  L.off_part = take((int64_t)kXgSplitPieces * 8 * XG_SMAX * 4 * 64 * 16);
+  L.off_cnt = take((int64_t)kXgSplitPieces * 8 * 4);
   L.total = o;
   return L;
 }
@@ -613,13 +662,33 @@ int launch_grm_exact(const int8_t* D, int64_t ldd, int64_t p, int64_t n, int plo
   GBM_LAUNCH_CHECK();
   const int64_t nI = (n + XG_BM - 1) / XG_BM, nJ = (n + XG_BN - 1) / XG_BN;
   const int64_t nunits = nI * nJ - nI * (nI - 1);
-  const unsigned grid = (unsigned)nunits;
+  // the partial last round of a grid with one unit per CU is split in loci ranges (GBM_XG_SPLIT=0: off)
+  int cus = 256;
+  {
+    int dev = 0;
+    if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (cus < 1) cus = 256;
+  }
+  const char* se = getenv("GBM_XG_SPLIT");
+  int64_t nfull = nunits, ks = 1;
+  if (!(se && *se && atoi(se) == 0)) {
+    const int64_t tail = nunits % cus;
+    if (nunits > cus && tail > 0) {
+      ks = std::min<int64_t>(std::min<int64_t>(8, cus / tail), kXgSplitPieces / tail);
+      if (ks >= 2) nfull = nunits - tail;
+      else ks = 1;
+    }
+  }
+  i32x4* part = reinterpret_cast<i32x4*>(w8 + L.off_part);
+  int32_t* cnt = reinterpret_cast<int32_t*>(w8 + L.off_cnt);
+  if (nfull < nunits) GBM_HIP_TRY(hipMemsetAsync(cnt, 0, (size_t)(nunits - nfull) * 8 * 4, s));
+  const unsigned grid = (unsigned)(nfull + (nunits - nfull) * ks);
   const char* oe = getenv("GBM_XG_ORDER");
   const int order = (oe && *oe) ? atoi(oe) : 1;
   const char* be = getenv("GBM_XG_BK");
   const int bk = (be && atoi(be) == 256) ? 256 : 128;
 #define XG_LAUNCH(SS, BKK) \
-  xg_gemm_kernel<SS, BKK><<<grid, 512, 0, s>>>(Dt, St, L.kp, WW, NU, C, n, F, nI, nJ, nunits, G, ldg, accum, order)
+  xg_gemm_kernel<SS, BKK><<<grid, 512, 0, s>>>(Dt, St, L.kp, WW, NU, C, n, F, nI, nJ, nunits, G, ldg, accum, order, nfull, (int)ks, part, cnt)
   if (bk == 256) {
     if (S == 8) XG_LAUNCH(8, 256); else if (S == 9) XG_LAUNCH(9, 256); else XG_LAUNCH(10, 256);
   } else {
