@@ -668,6 +668,8 @@ int launch_grm_exact(const int8_t* D, int64_t ldd, int64_t p, int64_t n, int plo
     int dev = 0;
     if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     if (cus < 1) cus = 256;
+    const char* ce = getenv("GBM_XG_CUS");  // tests: pretend a chip of this many CUs (forces the split tail)
+    if (ce && atoi(ce) > 0) cus = atoi(ce);
   }
   const char* se = getenv("GBM_XG_SPLIT");
   int64_t nfull = nunits, ks = 1;

@@ -229,3 +229,16 @@ def test_c_abi_exact_dosage_matches_oracle(monkeypatch):
     ref = oracle.gblup_fit(X, Y, 1.0)
     assert q == ref["q"]
     assert rel(y, ref["y_pred"]) < 1e-9 and rel(b, ref["b_hat"]) < 1e-6
+
+
+@pytest.mark.parametrize("cus", ["16", "7"])
+def test_exact_grm_split_tail(monkeypatch, cus):
+    """The partial last round of units split into loci ranges (forced on a small shape by pretending a chip
+    of 16 or 7 CUs): the ranges' int32 partials summed by the last range to finish, still exact."""
+    monkeypatch.setenv("GBM_XG_CUS", cus)
+    n, p = 700, 1500
+    D = random_dosages(31, n, p)
+    G, q, S, *_ = device_grm(D)
+    Gl, ql = exact_grm_ld(D)
+    assert q == ql
+    assert ulps_off(G, Gl) < 8
