@@ -2,7 +2,6 @@
 //   B[t, j] = (z_j · a_t) / (q s_j)  — Fit.b_hat (pattern of reference src/linear.jl:218-221)
 //   msum[t] = Σ_j m_j B[t, j]        — b0 = μ̂ − msum makes `predict` exact
 //   out[t, i] = b0_t + Σ_j X[i, j] b_t[j]   — reference src/prediction.jl:228
-#include <algorithm>
 #include <type_traits>
 
 #include "gbm_internal.h"
@@ -17,12 +16,9 @@ __device__ __forceinline__ double dosage_z(int8_t d, double xs, double m, double
   return (x - m) * r;
 }
 
-// One wave per LPW locus rows; each lane reads 16-byte pairs of a along individuals (T = double: the
-// standardised rows; T = int8_t: the dosage rows, z rebuilt in registers) and uses them for all LPW rows,
-// so a (n doubles per trait, the larger stream next to an int8 row) is read once per LPW loci instead of
-// once per locus. Up to 4 traits per pass over the rows. Each row's sum runs in the same order as with one
-// row per wave (per lane along i, then the xor butterfly): the same bits.
-constexpr int kLPW = 4;
+// One wave per locus row; each lane reads 16-byte pairs along individuals (T = double: the
+// standardised row; T = int8_t: the dosage row, z rebuilt in registers); up to 4 traits per pass
+// over the row (the row stays in L1/L2 for later passes).
 template <typename T>
 __global__ void __launch_bounds__(256) marker_effects_kernel(const T* __restrict__ Zt, int64_t ldz, int64_t p,
                                                              int64_t n, const double* __restrict__ A, int64_t lda,
@@ -37,60 +33,39 @@ __global__ void __launch_bounds__(256) marker_effects_kernel(const T* __restrict
   const int64_t nwaves = (int64_t)gridDim.x * 4;
   const int64_t n2 = (n + 1) & ~(int64_t)1;  // ldz is even and the padding is zero
   if (q_dev) inv_q = 1.0 / (double)(*q_dev);
-  for (int64_t jb = wave_g * kLPW; jb < p; jb += nwaves * kLPW) {
-    const T* z[kLPW];
-    bool kp[kLPW];
-    double m[kLPW], r[kLPW];
-#pragma unroll
-    for (int l = 0; l < kLPW; l++) {
-      const int64_t j = jb + l;
-      kp[l] = j < p && keep[j] != 0;
-      z[l] = Zt + (j < p ? j : jb) * ldz;
-      m[l] = 0.0;
-      r[l] = 0.0;
-      if constexpr (std::is_same<T, int8_t>::value) {
-        if (j < p) {
-          m[l] = mean[j];
-          r[l] = kp[l] ? 1.0 / sd[j] : 0.0;
-        }
-      }
+  for (int64_t j = wave_g; j < p; j += nwaves) {
+    const T* z = Zt + j * ldz;
+    const bool kp = keep[j] != 0;
+    double m = 0.0, r = 0.0;
+    if constexpr (std::is_same<T, int8_t>::value) {
+      m = mean[j];
+      r = kp ? 1.0 / sd[j] : 0.0;
     }
     for (int64_t t0 = 0; t0 < nrhs; t0 += 4) {
-      double acc[kLPW][4];
-#pragma unroll
-      for (int l = 0; l < kLPW; l++)
-#pragma unroll
-        for (int u = 0; u < 4; u++) acc[l][u] = 0.0;
-      for (int64_t i = (int64_t)lane * 2; i < n2; i += 128) {
-        double2 av[4];
-#pragma unroll
-        for (int u = 0; u < 4; u++)
-          av[u] = t0 + u < nrhs ? *reinterpret_cast<const double2*>(A + (t0 + u) * lda + i) : make_double2(0.0, 0.0);
-#pragma unroll
-        for (int l = 0; l < kLPW; l++) {
-          if (!kp[l]) continue;
+      double acc[4] = {0.0, 0.0, 0.0, 0.0};
+      if (kp) {
+        for (int64_t i = (int64_t)lane * 2; i < n2; i += 128) {
           double2 zv;
           if constexpr (std::is_same<T, int8_t>::value) {
-            zv.x = dosage_z(z[l][i], xs, m[l], r[l]);
-            zv.y = i + 1 < n ? dosage_z(z[l][i + 1], xs, m[l], r[l]) : 0.0;
+            zv.x = dosage_z(z[i], xs, m, r);
+            zv.y = i + 1 < n ? dosage_z(z[i + 1], xs, m, r) : 0.0;
           } else {
-            zv = *reinterpret_cast<const double2*>(z[l] + i);
+            zv = *reinterpret_cast<const double2*>(z + i);
           }
 #pragma unroll
           for (int u = 0; u < 4; u++)
-            if (t0 + u < nrhs) acc[l][u] += zv.x * av[u].x + zv.y * av[u].y;
+            if (t0 + u < nrhs) {
+              const double2 av = *reinterpret_cast<const double2*>(A + (t0 + u) * lda + i);
+              acc[u] += zv.x * av.x + zv.y * av.y;
+            }
         }
       }
 #pragma unroll
-      for (int l = 0; l < kLPW; l++) {
-        const int64_t j = jb + l;
+      for (int u = 0; u < 4; u++) {
+        double v = acc[u];
 #pragma unroll
-        for (int u = 0; u < 4; u++) {
-          double v = acc[l][u];
-#pragma unroll
-          for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
-          if (lane == 0 && j < p && t0 + u < nrhs) B[(t0 + u) * ldb + j] = kp[l] ? v * inv_q / sd[j] : 0.0;
-        }
+        for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
+        if (lane == 0 && t0 + u < nrhs) B[(t0 + u) * ldb + j] = kp ? v * inv_q / sd[j] : 0.0;
       }
     }
   }
@@ -168,7 +143,7 @@ int launch_marker_rows(const double* Zt, int64_t ldz, int64_t p, int64_t n, cons
                        double inv_q, const int64_t* q_dev, const double* sd, const int32_t* keep, double* B,
                        int64_t ldb, hipStream_t s) {
   if (p < 1) return GBM_OK;
-  const int64_t blocks = std::min<int64_t>((p + 4 * kLPW - 1) / (4 * kLPW), 8192);
+  const int64_t blocks = (p + 3) / 4 < 8192 ? (p + 3) / 4 : 8192;
   marker_effects_kernel<double><<<(unsigned)blocks, 256, 0, s>>>(Zt, ldz, p, n, A, lda, nrhs, inv_q, q_dev, nullptr, sd,
                                                                   keep, B, ldb, 1.0);
   GBM_LAUNCH_CHECK();
@@ -179,7 +154,7 @@ int launch_marker_rows_i8(const int8_t* D, int64_t ldd, int64_t p, int64_t n, in
                           int64_t nrhs, double inv_q, const int64_t* q_dev, const double* mean, const double* sd,
                           const int32_t* keep, double* B, int64_t ldb, hipStream_t s) {
   if (p < 1) return GBM_OK;
-  const int64_t blocks = std::min<int64_t>((p + 4 * kLPW - 1) / (4 * kLPW), 8192);
+  const int64_t blocks = (p + 3) / 4 < 8192 ? (p + 3) / 4 : 8192;
   marker_effects_kernel<int8_t><<<(unsigned)blocks, 256, 0, s>>>(D, ldd, p, n, A, lda, nrhs, inv_q, q_dev, mean, sd,
                                                                   keep, B, ldb, 1.0 / ploidy);
   GBM_LAUNCH_CHECK();

@@ -201,7 +201,7 @@ __global__ void __launch_bounds__(XG_UBLK) xg_digits_kernel(const double* __rest
 // partial U_i = Σ_j V_j d_ij over this block's loci tiles --------------------------------------------------
 // St byte at locus k (b = k mod 4, its byte in the dword): d = 2 → b (the 2ω dword, v_perm src1),
 // d = 1 → 4 + b (the ω dword, src0), d = 0 → 12 (v_perm's constant zero).
-// Block (x, y): individuals [256x, 256x + 256), the y-th contiguous range of 64-locus tiles: each tile read
+// Block (x, y): individuals [256x, 256x + 256), the 64-locus tiles y, y + gridDim.y, ...: each tile read
 // row by row (4 dosages per lane) into LDS, then one thread per individual assembles its 64 bytes of Dt and
 // St and adds its V_j d_ij (V_j wave-uniform).
 constexpr int XG_TP = 256 + 16;  // LDS row pitch of the 64-locus x 256-individual tile
@@ -214,12 +214,10 @@ __global__ void __launch_bounds__(256) xg_transpose_u_kernel(const int8_t* __res
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const bool al4 = (ldd % 4) == 0 && ((uintptr_t)D % 4) == 0;
   const int64_t i = i0 + threadIdx.x;
-  // a contiguous range of tiles per block: a thread's 64-byte row pieces of consecutive tiles complete
-  // the same 128-byte lines back to back (strided tiles left half-written lines to other CUs)
-  const int64_t nkt = kp / 64, per = (nkt + gridDim.y - 1) / gridDim.y;
-  const int64_t kt0 = (int64_t)blockIdx.y * per, kt1 = min(nkt, kt0 + per);
+  // tiles strided over the blocks (a contiguous range per block measured slower: 0.60 vs 0.45 ms at C2)
+  const int64_t nkt = kp / 64;
   i128 u = 0;
-  for (int64_t kt = kt0; kt < kt1; kt++) {
+  for (int64_t kt = blockIdx.y; kt < nkt; kt += gridDim.y) {
     const int64_t k0 = kt * 64;
     __syncthreads();  // the previous tile's reads are done
     uint32_t vr[16];
@@ -309,7 +307,7 @@ __device__ __forceinline__ void xg_unit(int64_t u, int64_t nI, int64_t nJ, int64
   J = 2 * r + (u - base);
 }
 
-// Blocked order (GBM_XG_ORDER unset or 1): the units grouped in blocks of XG_OBI row blocks x XG_OBJ column
+// Blocked order (GBM_XG_ORDER=1; measured slower than the default row-major order): the units grouped in blocks of XG_OBI row blocks x XG_OBJ column
 // blocks (32 = the CUs of an XCD), blocks row-major, units row-major inside a block; with the XCD remap an
 // XCD's concurrently running units then share 4 A and 8 B operand strips (per stage 4·16 + 8·8 KB of distinct
 // L2 lines instead of 16 + 32·8 KB in plain row-major order).
@@ -686,7 +684,7 @@ int launch_grm_exact(const int8_t* D, int64_t ldd, int64_t p, int64_t n, int plo
   if (nfull < nunits) GBM_HIP_TRY(hipMemsetAsync(cnt, 0, (size_t)(nunits - nfull) * 8 * 4, s));
   const unsigned grid = (unsigned)(nfull + (nunits - nfull) * ks);
   const char* oe = getenv("GBM_XG_ORDER");
-  const int order = (oe && *oe) ? atoi(oe) : 1;
+  const int order = (oe && *oe) ? atoi(oe) : 0;  // row-major measured faster than blocked (5.28 vs 5.52 ms)
   const char* be = getenv("GBM_XG_BK");
   const int bk = (be && atoi(be) == 256) ? 256 : 128;
 #define XG_LAUNCH(SS, BKK) \
