@@ -297,14 +297,15 @@ __device__ __forceinline__ void wait_vm() {
 
 // unit u → (row block I, column block J) over the upper-triangle units J >= 2I with columns below n
 // (nI = ⌈n/128⌉ row blocks, nJ = ⌈n/64⌉ column blocks; every row block has at least one unit)
+template <int RT>  // RT = row-block / column-block height ratio (2: 128 x 64 tiles, 1: 64 x 64)
 __device__ __forceinline__ void xg_unit(int64_t u, int64_t nI, int64_t nJ, int64_t& I, int64_t& J) {
   int64_t base = 0, r = 0;
-  while (r < nI && base + (nJ - 2 * r) <= u) {
-    base += nJ - 2 * r;
+  while (r < nI && base + (nJ - RT * r) <= u) {
+    base += nJ - RT * r;
     r++;
   }
   I = r;
-  J = 2 * r + (u - base);
+  J = RT * r + (u - base);
 }
 
 // Blocked order (GBM_XG_ORDER=1; measured slower than the default row-major order): the units grouped in blocks of XG_OBI row blocks x XG_OBJ column
@@ -312,12 +313,13 @@ __device__ __forceinline__ void xg_unit(int64_t u, int64_t nI, int64_t nJ, int64
 // XCD's concurrently running units then share 4 A and 8 B operand strips (per stage 4·16 + 8·8 KB of distinct
 // L2 lines instead of 16 + 32·8 KB in plain row-major order).
 constexpr int XG_OBI = 4, XG_OBJ = 8;
+template <int RT>
 __device__ __forceinline__ void xg_unit_blocked(int64_t u, int64_t nI, int64_t nJ, int64_t& I, int64_t& J) {
   for (int64_t bi = 0; bi * XG_OBI < nI; bi++) {
     for (int64_t bj = 0; bj * XG_OBJ < nJ; bj++) {
       const int64_t i1 = min(nI, (bi + 1) * XG_OBI), j0 = bj * XG_OBJ, j1 = min(nJ, (bj + 1) * XG_OBJ);
       for (int64_t ii = bi * XG_OBI; ii < i1; ii++) {
-        const int64_t lo = max(2 * ii, j0), cnt = j1 > lo ? j1 - lo : 0;
+        const int64_t lo = max(RT * ii, j0), cnt = j1 > lo ? j1 - lo : 0;
         if (u < cnt) {
           I = ii;
           J = lo + u;
@@ -333,37 +335,40 @@ __device__ __forceinline__ void xg_unit_blocked(int64_t u, int64_t nI, int64_t n
 
 // Stage geometry per BK (loci per LDS stage): operand rows of BK bytes, the stage's digits (BK/128 groups of
 // S·256 bytes; up to 10 slices) in whole 1-KB DMA pieces, the ring depth that fits 160 KB of LDS.
-template <int BK>
+template <int BK, int BM>
 struct XgStage {
+  static constexpr int kNW = BM / 16;                  // waves: 64 x 16 wave tiles over BM x 64
   static constexpr int kWW = BK == 128 ? 3072 : 5120;  // digit bytes in LDS (>= (BK/128)·XG_SMAX·256... at S <= 10)
-  static constexpr int kBytes = XG_BM * BK + XG_BN * BK + kWW;
+  static constexpr int kBytes = BM * BK + XG_BN * BK + kWW;
   static constexpr int kNS = BK == 128 ? 4 : 3;        // ring depth: kNS − 1 stages in flight
-  static constexpr int kA = XG_BM * BK / 1024 / 8;     // A pieces per wave
-  static constexpr int kB = XG_BN * BK / 1024 / 8;     // B pieces per wave
+  static constexpr int kA = BM * BK / 1024 / kNW;      // A pieces per wave
+  static constexpr int kB = XG_BN * BK / 1024 / kNW;   // B pieces per wave
   static constexpr int kWWp = kWW / 1024;              // digit pieces (waves 0 .. kWWp − 1, one each)
   static constexpr int kRows = 1024 / BK;               // operand rows per piece
   __device__ static int swz(int r) { return BK == 128 ? (r & 7) : (r & 15); }  // conflict-free ds_read_b128
 };
 
 template <int N>
-__device__ __forceinline__ void wait_vm_n(int pieces) {  // s_waitcnt vmcnt(N · pieces), pieces ∈ {kL, kL + 1}
+__device__ __forceinline__ void wait_vm_n(int pieces) {  // s_waitcnt vmcnt(N · pieces), pieces ∈ 3..7
   if (pieces == 3) wait_vm<3 * N>();
   else if (pieces == 4) wait_vm<4 * N>();
+  else if (pieces == 5) wait_vm<5 * N>();
   else if (pieces == 6) wait_vm<6 * N>();
   else wait_vm<7 * N>();
 }
 
-template <int S, int BK>
-__global__ void __launch_bounds__(512, 1)
+template <int S, int BK, int BM>
+__global__ void __launch_bounds__(BM * 4, BM == 128 ? 1 : 2)
 xg_gemm_kernel(const int8_t* __restrict__ Dt, const int8_t* __restrict__ St, int64_t kp, const int8_t* __restrict__ WW,
                const i128* __restrict__ NU, const i128* __restrict__ Cp, int64_t n, int F, int64_t nI, int64_t nJ, int64_t nunits,
                double* __restrict__ G, int64_t ldg, int accum, int order, int64_t nfull, int ks_split,
                i32x4* __restrict__ part, int32_t* __restrict__ cnt) {
-  using SG = XgStage<BK>;
+  using SG = XgStage<BK, BM>;
+  constexpr int RT = BM / XG_BN;
   __shared__ __attribute__((aligned(16))) int8_t lds[SG::kNS * SG::kBytes];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int wm = wave >> 2, wn = wave & 3;  // 2 x 4 waves of 64 x 16
+  const int wm = wave >> 2, wn = wave & 3;  // (BM/64) x 4 waves of 64 x 16
 
   // Blocks [0, nfull): whole units, XCD-aware bijective remap (the blocks the hardware deals to one XCD take
   // a contiguous unit range). Blocks [nfull, ...): the last nunits − nfull units (the partial last round of a
@@ -387,10 +392,10 @@ xg_gemm_kernel(const int8_t* __restrict__ Dt, const int8_t* __restrict__ St, int
   if (u >= nunits) return;
   int64_t I, J;
   if (order)
-    xg_unit_blocked(u, nI, nJ, I, J);
+    xg_unit_blocked<RT>(u, nI, nJ, I, J);
   else
-    xg_unit(u, nI, nJ, I, J);
-  const int64_t i0 = I * XG_BM, j0 = J * XG_BN;
+    xg_unit<RT>(u, nI, nJ, I, J);
+  const int64_t i0 = I * BM, j0 = J * XG_BN;
   const int64_t wr0 = i0 + wm * 64, wc0 = j0 + wn * 16;
   const bool active = !(wc0 + 15 < wr0) && wr0 < n && wc0 < n;
 
@@ -404,19 +409,19 @@ xg_gemm_kernel(const int8_t* __restrict__ Dt, const int8_t* __restrict__ St, int
     int8_t* base = lds + (int)(st % SG::kNS) * SG::kBytes;
 #pragma unroll
     for (int a = 0; a < SG::kA; a++) {
-      const int xx = wave + 8 * a, r = xx * SG::kRows + prow;
+      const int xx = wave + SG::kNW * a, r = xx * SG::kRows + prow;
       __builtin_amdgcn_global_load_lds((const void*)(Dt + (i0 + r) * kp + st * BK + ((pslot ^ SG::swz(r)) << 4)),
                                        (void*)(base + xx * 1024), 16, 0, 0);
     }
 #pragma unroll
     for (int a = 0; a < SG::kB; a++) {
-      const int xx = wave + 8 * a, r = xx * SG::kRows + prow;
+      const int xx = wave + SG::kNW * a, r = xx * SG::kRows + prow;
       __builtin_amdgcn_global_load_lds((const void*)(St + (j0 + r) * kp + st * BK + ((pslot ^ SG::swz(r)) << 4)),
-                                       (void*)(base + XG_BM * BK + xx * 1024), 16, 0, 0);
+                                       (void*)(base + BM * BK + xx * 1024), 16, 0, 0);
     }
     if (wdig)
       __builtin_amdgcn_global_load_lds((const void*)(WW + st * (int64_t)((BK / 128) * S * 256) + wave * 1024 + lane * 16),
-                                       (void*)(base + XG_BM * BK + XG_BN * BK + wave * 1024), 16, 0, 0);
+                                       (void*)(base + BM * BK + XG_BN * BK + wave * 1024), 16, 0, 0);
   };
   // stage st's pieces have landed (this wave's, by a counted wait; the others', by the barrier) and every
   // wave has finished reading the buffer the next issue overwrites (read one stage earlier)
@@ -448,7 +453,7 @@ xg_gemm_kernel(const int8_t* __restrict__ Dt, const int8_t* __restrict__ St, int
   for (int64_t st = st0; st < st1; st++) {
     arrive(st);
     const int8_t* A = lds + (int)(st % SG::kNS) * SG::kBytes;
-    const int8_t* B = A + XG_BM * BK;
+    const int8_t* B = A + BM * BK;
     const int8_t* Wd = B + XG_BN * BK;
     // the stage's NKS·S (k-step, slice) pairs in one unrolled sequence: digits two pairs ahead in a ring of
     // three register sets, the next k-step's fragments loaded during the current k-step (ring of two)
@@ -658,14 +663,20 @@ int launch_grm_exact(const int8_t* D, int64_t ldd, int64_t p, int64_t n, int plo
   xg_u_reduce_kernel<<<(unsigned)((L.npad + XG_UBLK - 1) / XG_UBLK), XG_UBLK, 0, s>>>(Upart, L.nr, L.npad, n, Cpart,
                                                                                       L.ncp, NU, C);
   GBM_LAUNCH_CHECK();
-  const int64_t nI = (n + XG_BM - 1) / XG_BM, nJ = (n + XG_BN - 1) / XG_BN;
-  const int64_t nunits = nI * nJ - nI * (nI - 1);
+  const char* be = getenv("GBM_XG_BK");
+  const int bk = (be && atoi(be) == 256) ? 256 : 128;
+  const char* me = getenv("GBM_XG_BM");  // 128: 128 x 64 tiles, one 8-wave workgroup per CU; 64: 64 x 64, two
+  const int bm = (me && atoi(me) == 64 && bk == 128) ? 64 : 128;
+  const int64_t rt = bm / XG_BN;
+  const int64_t nI = (n + bm - 1) / bm, nJ = (n + XG_BN - 1) / XG_BN;
+  const int64_t nunits = nI * nJ - rt * nI * (nI - 1) / 2;
   // the partial last round of a grid with one unit per CU is split in loci ranges (GBM_XG_SPLIT=0: off)
   int cus = 256;
   {
     int dev = 0;
     if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     if (cus < 1) cus = 256;
+    if (bm == 64) cus *= 2;  // two workgroups per CU
     const char* ce = getenv("GBM_XG_CUS");  // tests: pretend a chip of this many CUs (forces the split tail)
     if (ce && atoi(ce) > 0) cus = atoi(ce);
   }
@@ -685,14 +696,14 @@ int launch_grm_exact(const int8_t* D, int64_t ldd, int64_t p, int64_t n, int plo
   const unsigned grid = (unsigned)(nfull + (nunits - nfull) * ks);
   const char* oe = getenv("GBM_XG_ORDER");
   const int order = (oe && *oe) ? atoi(oe) : 0;  // row-major measured faster than blocked (5.28 vs 5.52 ms)
-  const char* be = getenv("GBM_XG_BK");
-  const int bk = (be && atoi(be) == 256) ? 256 : 128;
-#define XG_LAUNCH(SS, BKK) \
-  xg_gemm_kernel<SS, BKK><<<grid, 512, 0, s>>>(Dt, St, L.kp, WW, NU, C, n, F, nI, nJ, nunits, G, ldg, accum, order, nfull, (int)ks, part, cnt)
+#define XG_LAUNCH(SS, BKK, BMM) \
+  xg_gemm_kernel<SS, BKK, BMM><<<grid, BMM * 4, 0, s>>>(Dt, St, L.kp, WW, NU, C, n, F, nI, nJ, nunits, G, ldg, accum, order, nfull, (int)ks, part, cnt)
   if (bk == 256) {
-    if (S == 8) XG_LAUNCH(8, 256); else if (S == 9) XG_LAUNCH(9, 256); else XG_LAUNCH(10, 256);
+    if (S == 8) XG_LAUNCH(8, 256, 128); else if (S == 9) XG_LAUNCH(9, 256, 128); else XG_LAUNCH(10, 256, 128);
+  } else if (bm == 64) {
+    if (S == 8) XG_LAUNCH(8, 128, 64); else if (S == 9) XG_LAUNCH(9, 128, 64); else XG_LAUNCH(10, 128, 64);
   } else {
-    if (S == 8) XG_LAUNCH(8, 128); else if (S == 9) XG_LAUNCH(9, 128); else XG_LAUNCH(10, 128);
+    if (S == 8) XG_LAUNCH(8, 128, 128); else if (S == 9) XG_LAUNCH(9, 128, 128); else XG_LAUNCH(10, 128, 128);
   }
 #undef XG_LAUNCH
   GBM_LAUNCH_CHECK();

@@ -242,3 +242,18 @@ def test_exact_grm_split_tail(monkeypatch, cus):
     Gl, ql = exact_grm_ld(D)
     assert q == ql
     assert ulps_off(G, Gl) < 8
+
+
+@pytest.mark.parametrize("env", [{"GBM_XG_BM": "64"}, {"GBM_XG_BK": "256"}, {"GBM_XG_ORDER": "1"},
+                                 {"GBM_XG_BM": "64", "GBM_XG_CUS": "8"}])
+def test_exact_grm_kernel_variants(monkeypatch, env):
+    """The GEMM's tile (64 x 64, two workgroups per CU), stage (256 loci) and unit-order variants, and the
+    split tail of the 64 x 64 grid: the same exact GRM."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    n, p = 700, 1500
+    D = random_dosages(41, n, p)
+    G, q, S, *_ = device_grm(D)
+    Gl, ql = exact_grm_ld(D)
+    assert q == ql
+    assert ulps_off(G, Gl) < 8
