@@ -127,8 +127,27 @@ __global__ void __launch_bounds__(256) xg_stats_kernel(const int8_t* __restrict_
       wmaxb = bits > wmaxb ? bits : wmaxb;
     }
   }
+  // the block's four waves combine through LDS; one set of atomics per block
+  __shared__ unsigned long long sk[4], sw[4];
+  __shared__ int se0[4], se1[4], sb[4];
   bad = __any(bad != 0) ? 1 : 0;
+  const int wv = threadIdx.x >> 6;
   if (lane == 0) {
+    sk[wv] = kept;
+    sw[wv] = wmaxb;
+    se0[wv] = emin;
+    se1[wv] = emax;
+    sb[wv] = bad;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int k = 1; k < 4; k++) {
+      kept += sk[k];
+      wmaxb = sw[k] > wmaxb ? sw[k] : wmaxb;
+      emin = se0[k] < emin ? se0[k] : emin;
+      emax = se1[k] > emax ? se1[k] : emax;
+      bad |= sb[k];
+    }
     if (kept) {
       atomicAdd(q_dev, kept);
       atomicMin(&info->emin, emin);
@@ -217,13 +236,11 @@ __global__ void __launch_bounds__(256) xg_transpose_u_kernel(const int8_t* __res
   // tiles strided over the blocks (a contiguous range per block measured slower: 0.60 vs 0.45 ms at C2)
   const int64_t nkt = kp / 64;
   i128 u = 0;
-  for (int64_t kt = blockIdx.y; kt < nkt; kt += gridDim.y) {
-    const int64_t k0 = kt * 64;
-    __syncthreads();  // the previous tile's reads are done
-    uint32_t vr[16];
+  uint32_t vr[16];
+  auto load_rows = [&](int64_t kt) {  // this wave's 16 rows of tile kt, 4 dosages per lane, all in flight
 #pragma unroll
-    for (int rr = 0; rr < 16; rr++) {  // all 16 row loads of this wave in flight together
-      const int64_t k = k0 + wv + 4 * rr;
+    for (int rr = 0; rr < 16; rr++) {
+      const int64_t k = kt * 64 + wv + 4 * rr;
       const int64_t ii = i0 + 4 * lane;
       uint32_t v = 0;
       if (k < p) {
@@ -238,8 +255,14 @@ __global__ void __launch_bounds__(256) xg_transpose_u_kernel(const int8_t* __res
       }
       vr[rr] = v;
     }
+  };
+  if ((int64_t)blockIdx.y < nkt) load_rows(blockIdx.y);
+  for (int64_t kt = blockIdx.y; kt < nkt; kt += gridDim.y) {
+    const int64_t k0 = kt * 64;
+    __syncthreads();  // the previous tile's reads are done
 #pragma unroll
     for (int rr = 0; rr < 16; rr++) *reinterpret_cast<uint32_t*>(tile + (wv + 4 * rr) * XG_TP + 4 * lane) = vr[rr];
+    if (kt + gridDim.y < nkt) load_rows(kt + gridDim.y);  // the next tile's rows in flight during this one
     __syncthreads();
     if (i < npad) {
       uint32_t dw[16], sw[16];
@@ -640,7 +663,7 @@ int launch_grm_exact(const int8_t* D, int64_t ldd, int64_t p, int64_t n, int plo
   XgInfo* info = reinterpret_cast<XgInfo*>(w8 + L.off_info);
 
   xg_info_init_kernel<<<1, 1, 0, s>>>(info);
-  const int sgrid = (int)std::min<int64_t>((p + 3) / 4, 1024);  // one wave per locus
+  const int sgrid = (int)std::min<int64_t>((p + 3) / 4, 4096);  // one wave per locus (grid-strided)
   xg_stats_kernel<<<sgrid, 256, 0, s>>>(D, ldd, p, n, 1.0 / ploidy, mean, sd, keep,
                                         reinterpret_cast<unsigned long long*>(q_dev), w, tcol, info);
   GBM_LAUNCH_CHECK();
@@ -665,8 +688,8 @@ int launch_grm_exact(const int8_t* D, int64_t ldd, int64_t p, int64_t n, int plo
   GBM_LAUNCH_CHECK();
   const char* be = getenv("GBM_XG_BK");
   const int bk = (be && atoi(be) == 256) ? 256 : 128;
-  const char* me = getenv("GBM_XG_BM");  // 128: 128 x 64 tiles, one 8-wave workgroup per CU; 64: 64 x 64, two
-  const int bm = (me && atoi(me) == 64 && bk == 128) ? 64 : 128;
+  const char* me = getenv("GBM_XG_BM");  // 128: 128 x 64 tiles, one 8-wave workgroup per CU; 64 (default): 64 x 64, two
+  const int bm = (bk == 128 && !(me && atoi(me) == 128)) ? 64 : 128;  // 64 x 64 measured fastest at C2
   const int64_t rt = bm / XG_BN;
   const int64_t nI = (n + bm - 1) / bm, nJ = (n + XG_BN - 1) / XG_BN;
   const int64_t nunits = nI * nJ - rt * nI * (nI - 1) / 2;

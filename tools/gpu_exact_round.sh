@@ -9,7 +9,7 @@ timeout -k 10 600 python -u -m pytest tests/test_gpu_exact.py tests/test_gpu_str
 tail -2 gpurun_out/exact_tests.log
 if [ -z "$SKIP_AB" ]; then
 for r in 1 2; do
-  for cfg in "0 128 1" "0 256 1" "0 128 1 64"; do
+  for cfg in "0 128 1 64" "0 128 1 128"; do
     set -- $cfg
     GBM_XG_BM=${4:-128} GBM_XG_SPLIT=$3 GBM_XG_ORDER=$1 GBM_XG_BK=$2 timeout -k 10 120 python3 tools/exact_grm_time.py 5000 50000 exact > gpurun_out/ab_$1_$2_$3_${4:-128}.json 2>&1 || { tail gpurun_out/ab_$1_$2_$3_${4:-128}.json; exit 1; }
     python3 -c "import json; d=json.loads(open('gpurun_out/ab_$1_$2_$3_${4:-128}.json').read().strip().splitlines()[-1]); print('order $1 bk $2 split $3 bm ${4:-128}', round(d['ms_per_step'],3), round(d['stage_ms']['grm_syrk'],3))"
