@@ -473,79 +473,56 @@ xg_gemm_kernel(const int8_t* __restrict__ Dt, const int8_t* __restrict__ St, int
     for (int64_t st = st0; st < st1; st++) arrive(st);
     return;
   }
-  constexpr int NKS = BK / 64, T = NKS * S;
-  i32x4 af[2][4], bf[2], w1[3], w2[3];
-  auto load_frags = [&](const int8_t* A, int ks) {  // k-step ks's fragments into register set ks & 1
-    const int8_t* B = A + BM * BK;
-    const int c = ks * 4 + g;  // this lane group's 16-locus chunk
-#pragma unroll
-    for (int m = 0; m < 4; m++) {
-      const int r = wm * 64 + m * 16 + fr;
-      af[ks & 1][m] = *reinterpret_cast<const i32x4*>(A + r * BK + ((c ^ SG::swz(r)) << 4));
-    }
-    const int rb = wn * 16 + fr;
-    bf[ks & 1] = *reinterpret_cast<const i32x4*>(B + rb * BK + ((c ^ SG::swz(rb)) << 4));
-  };
-  auto load_digits = [&](const int8_t* A, int t) {  // pair t's digits into register set t % 3
-    const int8_t* Wd = A + BM * BK + XG_BN * BK;
-    const int ks = t / S;  // digit group ks/2 (128 loci), chunk (ks % 2)·4 + g inside it
-    const int8_t* wp = Wd + (ks >> 1) * (S * 256) + (t % S) * 256 + ((ks & 1) * 4 + g) * 32;
-    w1[t % 3] = *reinterpret_cast<const i32x4*>(wp);
-    w2[t % 3] = *reinterpret_cast<const i32x4*>(wp + 16);
-  };
-  auto perm = [&](int t) {
-    i32x4 r;
-#pragma unroll
-    for (int e = 0; e < 4; e++)
-      r[e] = (int)__builtin_amdgcn_perm((uint32_t)w1[t % 3][e], (uint32_t)w2[t % 3][e], (uint32_t)bf[(t / S) & 1][e]);
-    return r;
-  };
-  auto stage_base = [&](int64_t st) { return lds + (int)(st % SG::kNS) * SG::kBytes; };
-  auto mfma4 = [&](int t, const i32x4& bs) {
-    const int ks = t / S, s = t % S;
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int m = 0; m < 4; m++) acc[s][m] = __builtin_amdgcn_mfma_i32_16x16x64_i8(af[ks & 1][m], bs, acc[s][m], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
-  };
-  // Software pipeline over the stage's T = NKS·S (k-step, slice) pairs: the MFMAs of pair t issue beside the
-  // v_perms of t + 1 (its digits loaded at t − 2) and the digit loads of t + 3; the next k-step's fragments
-  // load during the current one. When T is a multiple of 3 the pipeline also runs ACROSS stages: at pair
-  // T − 3 the wave arrives at stage st + 1 (its counted vmcnt and barrier: every wave has issued and drained
-  // all its reads of stage st by then, so the same arrive may restage st's buffer) and starts loading st + 1's
-  // first fragments and digits, which the last three pairs of st then hide.
-  constexpr bool kCross = (T % 3) == 0;
-  arrive(st0);
-  const int8_t* A = stage_base(st0);
-  load_frags(A, 0);
-  load_digits(A, 0);
-  load_digits(A, 1);
-  load_digits(A, 2);
-  i32x4 bs = perm(0);
   for (int64_t st = st0; st < st1; st++) {
-    const bool more = st + 1 < st1;
-    const int8_t* An = A;
+    arrive(st);
+    const int8_t* A = lds + (int)(st % SG::kNS) * SG::kBytes;
+    const int8_t* B = A + BM * BK;
+    const int8_t* Wd = B + XG_BN * BK;
+    // the stage's NKS·S (k-step, slice) pairs in one unrolled sequence: digits two pairs ahead in a ring of
+    // three register sets, the next k-step's fragments loaded during the current k-step (ring of two)
+    constexpr int NKS = BK / 64;
+    i32x4 af[2][4], bf[2], w1[3], w2[3];
+    auto load_frags = [&](int ks) {
+      const int c = ks * 4 + g;  // this lane group's 16-locus chunk
 #pragma unroll
-    for (int t = 0; t < T; t++) {
+      for (int m = 0; m < 4; m++) {
+        const int r = wm * 64 + m * 16 + fr;
+        af[ks & 1][m] = *reinterpret_cast<const i32x4*>(A + r * BK + ((c ^ SG::swz(r)) << 4));
+      }
+      const int rb = wn * 16 + fr;
+      bf[ks & 1] = *reinterpret_cast<const i32x4*>(B + rb * BK + ((c ^ SG::swz(rb)) << 4));
+    };
+    auto load_digits = [&](int t) {
+      const int ks = t / S;  // digit group ks/2 (128 loci), chunk (ks % 2)·4 + g inside it
+      const int8_t* wp = Wd + (ks >> 1) * (S * 256) + (t % S) * 256 + ((ks & 1) * 4 + g) * 32;
+      w1[t % 3] = *reinterpret_cast<const i32x4*>(wp);
+      w2[t % 3] = *reinterpret_cast<const i32x4*>(wp + 16);
+    };
+    auto perm = [&](int t) {
+      i32x4 r;
+#pragma unroll
+      for (int e = 0; e < 4; e++)
+        r[e] = (int)__builtin_amdgcn_perm((uint32_t)w1[t % 3][e], (uint32_t)w2[t % 3][e], (uint32_t)bf[(t / S) & 1][e]);
+      return r;
+    };
+    // software pipeline over the pairs t: the MFMAs of t issue beside the v_perms of t + 1 (digits loaded at
+    // t − 2) and the digit loads of t + 3
+    load_frags(0);
+    load_digits(0);
+    load_digits(1);
+    load_digits(2);
+    i32x4 bs = perm(0);
+#pragma unroll
+    for (int t = 0; t < NKS * S; t++) {
       const int ks = t / S, s = t % S;
-      if (s == 1 && ks + 1 < NKS) load_frags(A, ks + 1);
+      if (s == 1 && ks + 1 < NKS) load_frags(ks + 1);
       i32x4 bn = bs;
-      if (t + 1 < T) {
-        bn = perm(t + 1);
-      } else if (kCross && more) {
-        bn = perm(0);  // the next stage's first pair (register sets 0, as t + 1 − T = 0 and T % 3 == 0)
-      }
-      if (t + 3 < T) {
-        load_digits(A, t + 3);
-      } else if (kCross && more) {
-        if (t + 3 == T) {
-          arrive(st + 1);
-          An = stage_base(st + 1);
-          load_frags(An, 0);
-        }
-        load_digits(An, t + 3 - T);
-      }
-      mfma4(t, bs);
+      if (t + 1 < NKS * S) bn = perm(t + 1);
+      if (t + 3 < NKS * S) load_digits(t + 3);
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int m = 0; m < 4; m++) acc[s][m] = __builtin_amdgcn_mfma_i32_16x16x64_i8(af[ks & 1][m], bs, acc[s][m], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
 #pragma unroll
       for (int m = 0; m < 4; m++) {
         __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // one MFMA
@@ -554,19 +531,6 @@ xg_gemm_kernel(const int8_t* __restrict__ Dt, const int8_t* __restrict__ St, int
       __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);    // the digit loads of t + 3
       __builtin_amdgcn_sched_barrier(0);
       bs = bn;
-    }
-    if (more) {
-      if constexpr (kCross) {
-        A = An;
-      } else {  // the next stage's start: arrive, then its first fragments and digits
-        arrive(st + 1);
-        A = stage_base(st + 1);
-        load_frags(A, 0);
-        load_digits(A, 0);
-        load_digits(A, 1);
-        load_digits(A, 2);
-        bs = perm(0);
-      }
     }
   }
 
