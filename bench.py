@@ -37,6 +37,9 @@ sys.path.insert(0, os.path.join(ROOT, "genomicbreedingmodels.jl_amd"))
 PEAK_F64_TFLOPS = 78.6  # MI355X fp64 matrix peak (AMD datasheet)
 PEAK_HBM_GBS = 8000.0
 PEAK_I8_TOPS = 5000.0  # MI355X dense int8 MFMA (2x bf16 per clock: MI355X_MICROARCH.md, Matrix cores)
+# back-to-back v_mfma_i32_16x16x64_i8 with the exact GEMM's 36 accumulators and one v_perm per MFMA, all CUs,
+# random operands (tools/mfma_i8_rate.hip, profiles/r04_mfma_i8_rate.jsonl; 3.8-4.7 POPS without the perms)
+MEASURED_I8_LOOP_TOPS = 3620.0
 MEASURED_MFMA_F64_TFLOPS = 74.1  # back-to-back v_mfma_f64_16x16x4_f64 loop, tools/mfma_f64_probe.hip
 
 
@@ -434,7 +437,8 @@ def main():
                "q_equal_fp64_path": int(ex.q.item()) == q_fp64,
                "roofline": {"bound": "mfma", "kernel": f"xg_gemm_kernel<{S}> + prep kernels (GRM stage)",
                             "achieved": tops, "peak": PEAK_I8_TOPS, "unit": "TOPS (int8)", "frac": tops / PEAK_I8_TOPS,
-                            "ops_per_launch": grm_ops},
+                            "frac_of_measured_i8_loop": tops / MEASURED_I8_LOOP_TOPS,
+                            "measured_i8_loop": MEASURED_I8_LOOP_TOPS, "ops_per_launch": grm_ops},
                "gpu": {"y_pred": eout["y_pred"], "mu": eout["mu"], "q": int(ex.q.item()),
                        "b_hat": assemble_b_hat(eout["mu"], eout["msum"], [eout["B"]], p_local)}}
         del ex
@@ -512,6 +516,7 @@ def main():
                       "point locus weights, 128x64 upper tiles) + its per-locus prep kernels (stats, digits, transpose, "
                       "int128 centring terms); achieved = S n(n+1)p int8 ops / stage time",
             "achieved": tops, "peak": PEAK_I8_TOPS, "unit": "TOPS (int8)", "frac": tops / PEAK_I8_TOPS,
+            "frac_of_measured_i8_loop": tops / MEASURED_I8_LOOP_TOPS, "measured_i8_loop": MEASURED_I8_LOOP_TOPS,
             "traffic": None, "ops_per_launch": ops, "ms_per_launch": syrk_ms,
             "fp64_equivalent_tflops": achieved,
         }
