@@ -337,11 +337,12 @@ __device__ __forceinline__ void xg_unit(int64_t u, int64_t nI, int64_t nJ, int64
 // L2 lines instead of 16 + 32·8 KB in plain row-major order).
 constexpr int XG_OBI = 4, XG_OBJ = 8;
 template <int RT>
-__device__ __forceinline__ void xg_unit_blocked(int64_t u, int64_t nI, int64_t nJ, int64_t& I, int64_t& J) {
-  for (int64_t bi = 0; bi * XG_OBI < nI; bi++) {
-    for (int64_t bj = 0; bj * XG_OBJ < nJ; bj++) {
-      const int64_t i1 = min(nI, (bi + 1) * XG_OBI), j0 = bj * XG_OBJ, j1 = min(nJ, (bj + 1) * XG_OBJ);
-      for (int64_t ii = bi * XG_OBI; ii < i1; ii++) {
+__device__ __forceinline__ void xg_unit_blocked(int64_t u, int64_t nI, int64_t nJ, int obi, int obj, int64_t& I,
+                                                int64_t& J) {
+  for (int64_t bi = 0; bi * obi < nI; bi++) {
+    for (int64_t bj = 0; bj * obj < nJ; bj++) {
+      const int64_t i1 = min(nI, (bi + 1) * obi), j0 = bj * obj, j1 = min(nJ, (bj + 1) * obj);
+      for (int64_t ii = bi * obi; ii < i1; ii++) {
         const int64_t lo = max(RT * ii, j0), cnt = j1 > lo ? j1 - lo : 0;
         if (u < cnt) {
           I = ii;
@@ -415,7 +416,7 @@ xg_gemm_kernel(const int8_t* __restrict__ Dt, const int8_t* __restrict__ St, int
   if (u >= nunits) return;
   int64_t I, J;
   if (order)
-    xg_unit_blocked<RT>(u, nI, nJ, I, J);
+    xg_unit_blocked<RT>(u, nI, nJ, order >> 8, order & 255, I, J);
   else
     xg_unit<RT>(u, nI, nJ, I, J);
   const int64_t i0 = I * BM, j0 = J * XG_BN;
@@ -718,7 +719,13 @@ int launch_grm_exact(const int8_t* D, int64_t ldd, int64_t p, int64_t n, int plo
   if (nfull < nunits) GBM_HIP_TRY(hipMemsetAsync(cnt, 0, (size_t)(nunits - nfull) * 8 * 4, s));
   const unsigned grid = (unsigned)(nfull + (nunits - nfull) * ks);
   const char* oe = getenv("GBM_XG_ORDER");
-  const int order = (oe && *oe) ? atoi(oe) : 0;  // row-major measured faster than blocked (5.28 vs 5.52 ms)
+  // 0: row-major units (default); "AxB": blocks of A row blocks x B column blocks (row-major blocks)
+  int order = 0;
+  if (oe && *oe) {
+    int a = 0, b = 0;
+    if (sscanf(oe, "%dx%d", &a, &b) == 2 && a > 0 && b > 0 && a < 256 && b < 256) order = (a << 8) | b;
+    else if (atoi(oe) == 1) order = (XG_OBI << 8) | XG_OBJ;
+  }
 #define XG_LAUNCH(SS, BKK, BMM) \
   xg_gemm_kernel<SS, BKK, BMM><<<grid, BMM * 4, 0, s>>>(Dt, St, L.kp, WW, NU, C, n, F, nI, nJ, nunits, G, ldg, accum, order, nfull, (int)ks, part, cnt)
   if (bk == 256) {
