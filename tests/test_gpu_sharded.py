@@ -25,14 +25,17 @@ def _worker(rank, world, port, n, p_total, seed, Y, out_dir, env=None):
     sys.path.insert(0, os.path.join(root, "genomicbreedingmodels.jl_amd"))
     import torch
     import torch.distributed as dist
-    from gbm.sharded import HipShardStages, TorchComm, sharded_gblup_step
+    from gbm.sharded import HipExactShardStages, HipShardStages, TorchComm, sharded_gblup_step
 
     torch.cuda.set_device(0)
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
     per = (p_total + world - 1) // world
     j0 = rank * per
     p_local = min(per, p_total - j0)
-    st = HipShardStages(n, p_local, nrhs=Y.shape[1], lambda_=1.0, device=0)
+    if os.environ.get("GBM_TEST_STAGES") == "exact":  # the exact-integer GRM shard (dosages resident)
+        st = HipExactShardStages(n, p_local, nrhs=Y.shape[1], lambda_=1.0, device=0)
+    else:
+        st = HipShardStages(n, p_local, nrhs=Y.shape[1], lambda_=1.0, device=0)
     st.generate(seed, j0)
     st.load_phenotypes(Y)
     saved = {}
@@ -97,5 +100,29 @@ def test_ranks_one_gpu_distributed_solve_match_oracle(tmp_path, world):
         assert np.abs(o["y_pred"] - ref["y_pred"]).max() < 1e-9 * np.abs(ref["y_pred"]).max()
         assert np.array_equal(o["y_pred"], outs[0]["y_pred"])
         assert np.array_equal(o["y_pred"], o["y_redundant"])
+    b_hat = assemble_b_hat(outs[0]["mu"], outs[0]["msum"], [o["B"] for o in outs], p)
+    assert np.abs(b_hat - ref["b_hat"]).max() < 1e-6 * np.abs(ref["b_hat"]).max()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_ranks_one_gpu_exact_grm_match_oracle(tmp_path, world):
+    """Loci-sharded exact-integer GRMs (csrc/grm_exact.hip, each rank its own weights' fixed point) summed by
+    the packed all-reduce, over gloo on the one GPU; the distributed factorisation forced on: the GEBVs and
+    b_hat equal the oracle's fit of the whole problem."""
+    import torch.multiprocessing as mp
+
+    import oracle
+    from gbm.sharded import assemble_b_hat
+
+    n, p, seed = 700, 3001, 23
+    X = oracle.synth_genotypes(seed, n, p)
+    Y = oracle.synth_phenotypes(X, 4, ntraits=2)
+    env = {"GBM_TEST_STAGES": "exact", "GBM_DIST_SOLVE_MIN_N": "0", "GBM_DIST_TAIL_ROWS": "256",
+           "GBM_CHOL_G4_LIM": "0", "GBM_CHOL_G8_LIM": "-1", "GBM_CHOL_G16_LIM": "-1", "GBM_UPD64_LIM": "128"}
+    mp.spawn(_worker, args=(world, _free_port(), n, p, seed, Y, str(tmp_path), env), nprocs=world, join=True)
+    outs = [dict(np.load(tmp_path / f"rank{r}.npz")) for r in range(world)]
+    ref = oracle.gblup_fit(X, Y, 1.0)
+    for o in outs:
+        assert np.abs(o["y_pred"] - ref["y_pred"]).max() < 1e-9 * np.abs(ref["y_pred"]).max()
     b_hat = assemble_b_hat(outs[0]["mu"], outs[0]["msum"], [o["B"] for o in outs], p)
     assert np.abs(b_hat - ref["b_hat"]).max() < 1e-6 * np.abs(ref["b_hat"]).max()
