@@ -67,6 +67,9 @@ int launch_marker_rows_i8(const int8_t* D, int64_t ldd, int64_t p, int64_t n, in
 int launch_grm_exact(const int8_t* D, int64_t ldd, int64_t p, int64_t n, int ploidy, double* G, int64_t ldg,
                      double* mean, double* sd, int32_t* keep, int64_t* q_dev, int accum, void* ws, int64_t ws_bytes,
                      int32_t* slices_out, hipStream_t s);
+// training-set dosages 2·Xt[j, idx[i]] (resident genotypes that are dosages/2) for the exact GRM
+int launch_gather_dosage(const double* Xt, int64_t ldx, int64_t p, const int32_t* idx, int64_t nT, int8_t* D,
+                         hipStream_t s);
 int launch_weighted_sum(const double* mean, const double* B, int64_t ldb, int64_t p, int64_t nrhs, double* msum,
                         hipStream_t s);
 int launch_center_columns(const double* Xt, int64_t ldx, int64_t p, int64_t n, double* Zt, int64_t ldz, double* mean,

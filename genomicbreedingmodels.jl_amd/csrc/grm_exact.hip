@@ -740,6 +740,28 @@ int launch_grm_exact(const int8_t* D, int64_t ldd, int64_t p, int64_t n, int plo
   return GBM_OK;
 }
 
+// Training-set dosages of a resident fp64 genotype matrix whose values are dosages/2 (a session of int8
+// or synthetic genotypes): D[j, i] = 2·Xt[j, idx[i]] as bytes (exact), the input of the exact GRM.
+__global__ void __launch_bounds__(256) xg_gather_dosage_kernel(const double* __restrict__ Xt, int64_t ldx, int64_t p,
+                                                               const int32_t* __restrict__ idx, int64_t nT,
+                                                               int8_t* __restrict__ D) {
+  const int64_t j = blockIdx.y;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < nT; i += (int64_t)gridDim.x * 256)
+    D[j * nT + i] = (int8_t)__double2int_rn(2.0 * Xt[j * ldx + idx[i]]);
+}
+
+int launch_gather_dosage(const double* Xt, int64_t ldx, int64_t p, const int32_t* idx, int64_t nT, int8_t* D,
+                         hipStream_t s) {
+  if (p < 1 || nT < 1) return GBM_OK;
+  const unsigned gx = (unsigned)std::min<int64_t>((nT + 255) / 256, 64);
+  for (int64_t j0 = 0; j0 < p; j0 += 65535) {
+    const unsigned gy = (unsigned)std::min<int64_t>(65535, p - j0);
+    xg_gather_dosage_kernel<<<dim3(gx, gy), 256, 0, s>>>(Xt + j0 * ldx, ldx, gy, idx, nT, D + j0 * nT);
+    GBM_LAUNCH_CHECK();
+  }
+  return GBM_OK;
+}
+
 }  // namespace gbm
 
 extern "C" int64_t gbm_dev_grm_exact_workspace(int64_t n, int64_t p) { return gbm::grm_exact_workspace_bytes(n, p); }

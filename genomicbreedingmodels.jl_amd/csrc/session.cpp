@@ -37,6 +37,11 @@ struct gbm_session {
   // predict buffers
   gbm::DevMem bvec, part, pout;
   int64_t builds = 0, hits = 0;
+  // genotypes known to be diploid dosages/2 (int8 or synthetic sessions): GBM_GRM=exact builds the
+  // training GRM with the exact-integer kernels (grm_exact.hip) from the gathered training dosages
+  bool dosage2 = false;
+  gbm::DevMem D8T, wsx, mean2, sd2, keep2, q2;
+  int64_t d8t_bytes = 0, wsx_bytes = 0;
 };
 
 namespace gbm {
@@ -184,7 +189,33 @@ int ensure_training(gbm_session* s, const int64_t* idx, int64_t nT, int mode = 0
   GBM_HIP_TRY(hipMemcpyAsync(&q, s->qd.p, 8, hipMemcpyDeviceToHost, st));
   GBM_HIP_TRY(hipStreamSynchronize(st));
   if (q == 0) return fail(GBM_E_DATA, "no polymorphic locus-allele in the training set (src/gwas.jl:112-115)");
-  GBM_TRY(gbm_dev_grm((const double*)s->Z.p, npadT, s->p, nT, (double*)s->Gc.p, gdimT, s->wsg.p, wsb, st));
+  const char* ge = getenv("GBM_GRM");
+  if (mode == 0 && s->dosage2 && ge && strcmp(ge, "exact") == 0) {
+    // exact-integer GRM of the training dosages; its per-locus statistics go to scratch (Z, mean and sd
+    // above are what the marker effects and predictions use; q is the same count)
+    if (s->d8t_bytes < s->p * nT) {
+      GBM_TRY(dalloc(s->D8T, s->dev, s->p * nT));
+      s->d8t_bytes = s->p * nT;
+    }
+    const int64_t wsx = gbm_dev_grm_exact_workspace(nT, s->p);
+    if (s->wsx_bytes < wsx) {
+      GBM_TRY(dalloc(s->wsx, s->dev, wsx));
+      s->wsx_bytes = wsx;
+    }
+    if (!s->mean2.p) {
+      GBM_TRY(dalloc(s->mean2, s->dev, s->p * 8));
+      GBM_TRY(dalloc(s->sd2, s->dev, s->p * 8));
+      GBM_TRY(dalloc(s->keep2, s->dev, s->p * 4));
+      GBM_TRY(dalloc(s->q2, s->dev, 8));
+    }
+    GBM_TRY(launch_gather_dosage((const double*)s->Xt.p, s->npad, s->p, (const int32_t*)s->idx32.p, nT,
+                                 (int8_t*)s->D8T.p, st));
+    GBM_HIP_TRY(hipMemsetAsync(s->q2.p, 0, 8, st));
+    GBM_TRY(launch_grm_exact((const int8_t*)s->D8T.p, nT, s->p, nT, 2, (double*)s->Gc.p, gdimT, (double*)s->mean2.p,
+                             (double*)s->sd2.p, (int32_t*)s->keep2.p, (int64_t*)s->q2.p, 0, s->wsx.p, wsx, nullptr, st));
+  } else {
+    GBM_TRY(gbm_dev_grm((const double*)s->Z.p, npadT, s->p, nT, (double*)s->Gc.p, gdimT, s->wsg.p, wsb, st));
+  }
   s->nT = nT;
   s->q = q;
   s->key.assign(idx, idx + nT);
@@ -288,6 +319,7 @@ extern "C" int gbm_session_create_synthetic(uint64_t seed, int64_t n, int64_t p,
   s->p = p;
   int rc = session_alloc_x(s);
   if (rc == GBM_OK) rc = gbm_dev_synth_genotypes((double*)s->Xt.p, s->npad, p, n, seed, 0, s->stream.s);
+  s->dosage2 = true;  // X = dosage/2 (SURVEY.md §8d generator)
   if (rc == GBM_OK && hipStreamSynchronize(s->stream.s) != hipSuccess)
     rc = fail(GBM_E_HIP, "gbm_session_create_synthetic: generation failed");
   if (rc != GBM_OK) {
@@ -316,6 +348,7 @@ extern "C" int gbm_session_create_dosage_i8(const int8_t* D, int64_t n, int64_t 
   if (rc == GBM_OK) rc = dalloc(d8, s->dev, n * p);
   if (rc == GBM_OK && (hipMemcpy2DAsync(d8.p, n, D, ldd, n, p, hipMemcpyHostToDevice, s->stream.s) != hipSuccess))
     rc = fail(GBM_E_HIP, "gbm_session_create_dosage_i8: upload failed");
+  s->dosage2 = ploidy == 2;  // and the bytes are checked to be in {0, 1, 2} by the exact kernels
   if (rc == GBM_OK) rc = gbm_dev_expand_dosage_i8((const int8_t*)d8.p, n, n, p, ploidy, (double*)s->Xt.p, s->npad,
                                                   s->stream.s);
   if (rc == GBM_OK && hipStreamSynchronize(s->stream.s) != hipSuccess) rc = fail(GBM_E_HIP, "stream sync");

@@ -257,3 +257,34 @@ def test_exact_grm_kernel_variants(monkeypatch, env):
     Gl, ql = exact_grm_ld(D)
     assert q == ql
     assert ulps_off(G, Gl) < 8
+
+
+@pytest.mark.parametrize("source", ["synthetic", "dosage"])
+def test_session_exact_training_grm_matches_oracle(monkeypatch, source):
+    """Sessions of dosage genotypes (synthetic, or int8 with ploidy 2) with GBM_GRM=exact: each training set's
+    GRM is the exact-integer one of the gathered training dosages (the CV fold fits of cross_validation.jl and
+    the REML path reuse it); fits against the oracle on the same rows, and against the fp64 session."""
+    from gbm.session import GenotypeSession
+    n, p, seed = 600, 3000, 13
+    X = oracle.synth_genotypes(seed, n, p)
+    Y = oracle.synth_phenotypes(X, 3, ntraits=2)
+    if source == "synthetic":
+        make = lambda: GenotypeSession.synthetic(seed, n, p)  # noqa: E731
+    else:
+        D = np.asfortranarray(np.rint(2.0 * X).astype(np.int8))
+        make = lambda: GenotypeSession(dosage_i8=D, ploidy=2)  # noqa: E731
+    rng = np.random.default_rng(5)
+    idx = np.sort(rng.choice(n, 450, replace=False))
+    monkeypatch.setenv("GBM_GRM", "exact")
+    with make() as s:
+        b, y, mu, q = s.gblup(idx, Y[idx])
+        va = np.setdiff1d(np.arange(n), idx)
+        yv = s.predict(va, b)
+    ref = oracle.gblup_fit(X[idx], Y[idx], 1.0)
+    assert q == ref["q"]
+    assert rel(y, ref["y_pred"]) < 1e-9 and rel(mu, ref["mu"]) < 1e-9 and rel(b, ref["b_hat"]) < 1e-6
+    assert rel(yv, oracle.predict_linear(X[va], ref["b_hat"])) < 1e-8
+    monkeypatch.delenv("GBM_GRM")
+    with make() as s:
+        b0, y0, mu0, q0 = s.gblup(idx, Y[idx])
+    assert q0 == q and rel(y, y0) < 1e-11
