@@ -61,7 +61,9 @@ def cv_sessions(args):
         s.close()
     if errs:
         raise RuntimeError(errs[0])
-    print(json.dumps({"bench": "cv fold farming on synthetic sessions", "n": args.n, "p": args.p,
+    import os
+    print(json.dumps({"bench": "cv fold farming on synthetic sessions", "grm": os.environ.get("GBM_GRM", "fp64"),
+                      "n": args.n, "p": args.p,
                       "traits": args.traits, "folds": args.folds, "devices": ndev, "jobs": len(jobs),
                       "session_setup_s": t_setup, "seconds": dt, "s_per_fold_job": dt / len(jobs) * ndev,
                       "mean_cor": float(np.mean(list(cors.values())))}), flush=True)
