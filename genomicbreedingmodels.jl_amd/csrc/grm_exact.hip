@@ -517,13 +517,19 @@ xg_gemm_kernel(const int8_t* __restrict__ Dt, const int8_t* __restrict__ St, int
     for (int t = 0; t < NKS * S; t++) {
       const int ks = t / S, s = t % S;
       if (s == 1 && ks + 1 < NKS) load_frags(ks + 1);
+      // each MFMA of t issued beside one v_perm of t + 1 (explicit pairs, no issue priority: 1.7 % faster
+      // than the MFMAs grouped under s_setprio and the v_perms before them)
       i32x4 bn = bs;
-      if (t + 1 < NKS * S) bn = perm(t + 1);
       if (t + 3 < NKS * S) load_digits(t + 3);
-      __builtin_amdgcn_s_setprio(1);
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-      for (int m = 0; m < 4; m++) acc[s][m] = __builtin_amdgcn_mfma_i32_16x16x64_i8(af[ks & 1][m], bs, acc[s][m], 0, 0, 0);
-      __builtin_amdgcn_s_setprio(0);
+      for (int m = 0; m < 4; m++) {
+        acc[s][m] = __builtin_amdgcn_mfma_i32_16x16x64_i8(af[ks & 1][m], bs, acc[s][m], 0, 0, 0);
+        if (t + 1 < NKS * S)
+          bn[m] = (int)__builtin_amdgcn_perm((uint32_t)w1[(t + 1) % 3][m], (uint32_t)w2[(t + 1) % 3][m],
+                                             (uint32_t)bf[((t + 1) / S) & 1][m]);
+        __builtin_amdgcn_sched_barrier(0);
+      }
 #pragma unroll
       for (int m = 0; m < 4; m++) {
         __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // one MFMA
