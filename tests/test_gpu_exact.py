@@ -288,3 +288,15 @@ def test_session_exact_training_grm_matches_oracle(monkeypatch, source):
     with make() as s:
         b0, y0, mu0, q0 = s.gblup(idx, Y[idx])
     assert q0 == q and rel(y, y0) < 1e-11
+
+
+@pytest.mark.parametrize("n,p", [(2, 1), (3, 7), (65, 130), (64, 256), (129, 257), (1000, 1)])
+def test_exact_grm_tiny_and_ragged_shapes(n, p):
+    """The smallest and ragged shapes (a single locus, two individuals, one past the tile edges)."""
+    D = random_dosages(n + 13 * p, n, p)
+    D[0, :] = 0
+    D[-1, :] = 2  # every locus polymorphic
+    G, q, S, *_ = device_grm(D)
+    Gl, ql = exact_grm_ld(D)
+    assert q == ql
+    assert ulps_off(G, Gl) < 8
