@@ -245,6 +245,48 @@ def cpu_baseline_c3(args):
                       f"total {t_c3:.1f} s on one host"}
 
 
+def _cpu_baseline_packed(packed):
+    """cpu_baseline(*packed) for the isolated child; the oracle fit comes back without its n x n arrays."""
+    out, parity, ref = cpu_baseline(*packed)
+    if ref is not None:
+        ref = {k: ref[k] for k in ("q", "y_pred", "mu", "b_hat")}
+    return out, parity, ref
+
+
+def _isolated_child(fn, args, conn):
+    try:
+        conn.send(("ok", fn(args)))
+    except Exception as e:  # pragma: no cover - reported by the parent
+        conn.send(("error", repr(e)))
+    conn.close()
+
+
+def run_isolated(fn, args, timeout_s=400):
+    """fn(args) in a fresh interpreter (spawn: no torch, no HIP): the C3 CPU extrapolation drives OpenBLAS
+    dsyrk/potrf over 50 000-row matrices, and a crash there must not take the GPU measurement with it.
+    Returns fn's result, or {"error": ...} when the child fails, crashes or times out."""
+    import multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    parent, child = ctx.Pipe(duplex=False)
+    p = ctx.Process(target=_isolated_child, args=(fn, args, child))
+    p.start()
+    child.close()
+    out = {"error": f"the isolated CPU leg did not answer within {timeout_s} s"}
+    if parent.poll(timeout_s):
+        try:
+            status, val = parent.recv()
+            out = val if status == "ok" else {"error": val}
+        except EOFError:
+            pass
+    p.join(10)
+    if p.is_alive():
+        p.kill()
+        p.join()
+    if p.exitcode not in (0, None) and "error" in out:
+        out["error"] += f" (child exit code {p.exitcode})"
+    return out
+
+
 def host_path(args, torch):
     """The product entry a Julia ccall binds (gbm_gblup_fit, X handed over in host memory), on the
     same workload (rank 0, N = 1): pageable and pinned X, the int8-dosage entry, and the H2D copy
@@ -529,13 +571,17 @@ def main():
     if world == 1 and not args.no_cpu_baseline and oracle_fits:
         gpu = {"y_pred": out["y_pred"], "mu": out["mu"], "q": int(st.q.item()),
                "b_hat": assemble_b_hat(out["mu"], out["msum"], [out["B"]], p_local)}
-        rec["cpu_baseline"], rec["parity"], ref = cpu_baseline(args, Y, gpu)
+        res = run_isolated(_cpu_baseline_packed, (args, np.asarray(Y), gpu))
+        if isinstance(res, dict):  # the child failed: no baseline, no parity from this run
+            rec["cpu_baseline"], rec["parity"], ref = res, {"skipped": "CPU leg failed: " + res["error"]}, None
+        else:
+            rec["cpu_baseline"], rec["parity"], ref = res
         if alt is not None and ref is not None:
             alt["parity"] = parity_of(alt["gpu"], ref)
         if not args.no_cpu_c3:
-            rec["cpu_baseline_c3_extrapolated"] = cpu_baseline_c3(args)
+            rec["cpu_baseline_c3_extrapolated"] = run_isolated(cpu_baseline_c3, args)
     elif world == 1 and not args.no_cpu_baseline and (n, p_local) == (50000, 600000):
-        rec["cpu_baseline"] = cpu_baseline_c3(args)  # C3: the full fit cannot run on the host
+        rec["cpu_baseline"] = run_isolated(cpu_baseline_c3, args)  # C3: the full fit cannot run on the host
         rec["parity"] = {"skipped": "the oracle cannot fit 50 000 x 600 000 on the host; C3 is checked by "
                                     "tests/test_gpu_large.py::test_c3_full_size_one_gpu_streamed (exact-solution "
                                     "properties, C ABI vs stage path)"}
