@@ -654,6 +654,10 @@ int launch_grm_exact(const int8_t* D, int64_t ldd, int64_t p, int64_t n, int plo
                      int32_t* slices_out, hipStream_t s) {
   if (!D || !G || !mean || !sd || !keep || !q_dev || !ws || p < 1 || n < 2 || ldd < n || ldg < npad_of(n) || ploidy != 2)
     return fail(GBM_E_ARG, "gbm_dev_grm_exact_i8: bad arguments (diploid dosages {0,1,2}, p >= 1, n >= 2, ldg >= npad)");
+  // int32 digit sums: |Σ_j d·ω| <= 252 p < 2^31; the int128 bracket: n² · 2^69 · 4p < 2^126 up to n = 2^19
+  if (p > ((int64_t)1 << 23) || n > ((int64_t)1 << 19))
+    return fail(GBM_E_ARG, "gbm_dev_grm_exact_i8: p <= 2^23 loci and n <= 2^19 individuals per call (integer ranges of the "
+                           "exact sums); split the loci into shards (accum = 1) beyond that");
   const XgLayout L = xg_layout(n, p);
   if (ws_bytes < L.total) return fail(GBM_E_ARG, "gbm_dev_grm_exact_i8: workspace too small (gbm_dev_grm_exact_workspace)");
   int8_t* w8 = static_cast<int8_t*>(ws);
