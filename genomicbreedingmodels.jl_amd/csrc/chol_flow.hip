@@ -160,12 +160,17 @@ __device__ __forceinline__ void lds_post(int* p, int v, int lane) {
   if (lane == 0) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 // every lane of the calling wave: spin on an LDS word of this workgroup until it reaches v (bounded: the
-// writers never wait on anything outside the workgroup, so the bound only guards a bug)
+// writers never wait on anything outside the workgroup, so the bound only guards a bug). Once any wait of
+// the factorisation has given up (info < 0) every later wait returns at once: the run then ends quickly
+// over stale tiles and the host reports info < 0, instead of each wait spinning out its own bound.
 __device__ __forceinline__ int lds_wait(int* p, int v, int32_t* info, int lane) {
   int s = lds_poll(p);
   for (int it = 0; s < v; it++) {
     __builtin_amdgcn_s_sleep(GBM_FLOW_POLL_SLEEP);  // the spin shares the LDS pipe with the leaf owner
     s = lds_poll(p);
+    if ((it & 255) == 255 &&
+        __builtin_amdgcn_readfirstlane(__hip_atomic_load(info, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) < 0)
+      return v;
     if (it > (1 << 22)) {
       if (lane == 0) atomicCAS(info, 0, -1);
       return v;
