@@ -19,9 +19,10 @@
 //
 // Kernels (all stream-ordered, one host sync to size S):
 //   xg_stats_kernel   per locus: t, Σd², mean, sd, keep, q (the standardisation's outputs), w_j, the
-//                     exponent range of the kept weights, a flag for dosages outside {0, 1, 2}
+//                     exponent range of the kept weights, a flag for dosages outside {0, 1, 2} (block partials;
+//                     xg_stats_reduce_kernel combines them)
 //   xg_digits_kernel  per locus: the S digits (and doubled digits) in the GEMM's per-stage layout,
-//                     V_j = W_j t_j, block partials of C
+//                     V_j = W_j t_j (four 24-bit limbs), block partials of C
 //   xg_transpose_u_kernel  locus-major dosages → individual-major Dt (the A operand) and St (B: each byte
 //                     a v_perm selector picking 2ω, ω or 0 from the digit dwords), and partial U_i
 //   xg_u_reduce_kernel   n·U_i and C in int128
@@ -56,6 +57,11 @@ struct XgInfo {  // device scratch written by the stats kernel, read by the host
   unsigned long long wmax_bits;  // the largest kept weight (positive doubles order as their bits)
   int32_t emin, emax, bad, pad;
 };
+struct XgStatsPart {  // one stats block's partial (reduced by xg_stats_reduce_kernel: no same-address atomics
+  unsigned long long kept, wmax_bits;  // from thousands of blocks, which serialise: measured 163 µs at C2)
+  int32_t emin, emax, bad, pad;
+};
+constexpr int XG_SGRID = 4096;  // the most stats blocks
 
 __device__ __forceinline__ double i128_to_double(i128 x) {
   const bool neg = x < 0;
@@ -72,7 +78,7 @@ __global__ void __launch_bounds__(256) xg_stats_kernel(const int8_t* __restrict_
                                                        double xs, double* __restrict__ mean, double* __restrict__ sd,
                                                        int32_t* __restrict__ keep, unsigned long long* __restrict__ q_dev,
                                                        double* __restrict__ w, int64_t* __restrict__ tcol,
-                                                       XgInfo* __restrict__ info) {
+                                                       XgStatsPart* __restrict__ part) {
   const int lane = threadIdx.x & 63;
   const int64_t wid = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 6, nw = ((int64_t)gridDim.x * 256) >> 6;
   const bool al4 = (ldd % 4) == 0 && ((uintptr_t)D % 4) == 0;
@@ -148,22 +154,47 @@ __global__ void __launch_bounds__(256) xg_stats_kernel(const int8_t* __restrict_
       emax = se1[k] > emax ? se1[k] : emax;
       bad |= sb[k];
     }
-    if (kept) {
-      atomicAdd(q_dev, kept);
-      atomicMin(&info->emin, emin);
-      atomicMax(&info->emax, emax);
-      atomicMax(&info->wmax_bits, wmaxb);
-    }
-    if (bad) atomicOr(&info->bad, 1);
+    part[blockIdx.x] = XgStatsPart{kept, wmaxb, emin, emax, bad, 0};
   }
 }
 
-__global__ void xg_info_init_kernel(XgInfo* info) {
-  info->wmax_bits = 0;
-  info->emin = INT_MAX;
-  info->emax = INT_MIN;
-  info->bad = 0;
-  info->pad = 0;
+// one block: the stats blocks' partials → XgInfo (read by the host) and q (one atomic: q accumulates over calls)
+__global__ void __launch_bounds__(256) xg_stats_reduce_kernel(const XgStatsPart* __restrict__ part, int nb,
+                                                              unsigned long long* __restrict__ q_dev,
+                                                              XgInfo* __restrict__ info) {
+  __shared__ XgStatsPart red[256];
+  XgStatsPart a{0, 0, INT_MAX, INT_MIN, 0, 0};
+  for (int b = threadIdx.x; b < nb; b += 256) {
+    const XgStatsPart x = part[b];
+    a.kept += x.kept;
+    a.wmax_bits = x.wmax_bits > a.wmax_bits ? x.wmax_bits : a.wmax_bits;
+    a.emin = x.emin < a.emin ? x.emin : a.emin;
+    a.emax = x.emax > a.emax ? x.emax : a.emax;
+    a.bad |= x.bad;
+  }
+  red[threadIdx.x] = a;
+  __syncthreads();
+  for (int off = 128; off >= 1; off >>= 1) {
+    if (threadIdx.x < off) {
+      XgStatsPart& x = red[threadIdx.x];
+      const XgStatsPart& y = red[threadIdx.x + off];
+      x.kept += y.kept;
+      x.wmax_bits = y.wmax_bits > x.wmax_bits ? y.wmax_bits : x.wmax_bits;
+      x.emin = y.emin < x.emin ? y.emin : x.emin;
+      x.emax = y.emax > x.emax ? y.emax : x.emax;
+      x.bad |= y.bad;
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    const XgStatsPart& r = red[0];
+    if (r.kept) atomicAdd(q_dev, r.kept);
+    info->wmax_bits = r.wmax_bits;
+    info->emin = r.emin;
+    info->emax = r.emax;
+    info->bad = r.bad;
+    info->pad = 0;
+  }
 }
 
 // ---- digits: W_j = w_j 2^F → S balanced base-128 digits in the GEMM's stage layout -----------------
@@ -172,7 +203,7 @@ __global__ void xg_info_init_kernel(XgInfo* info) {
 // kernel is VALU-issue-sensitive: measured slower).
 __global__ void __launch_bounds__(XG_UBLK) xg_digits_kernel(const double* __restrict__ w, const int64_t* __restrict__ tcol,
                                                             int64_t p, int64_t kp, int S, int F,
-                                                            int8_t* __restrict__ WW, i128* __restrict__ V,
+                                                            int8_t* __restrict__ WW, uint4* __restrict__ VL,
                                                             i128* __restrict__ Cpart, XgInfo* __restrict__ info) {
   __shared__ i128 red[XG_UBLK];
   const int64_t j = (int64_t)blockIdx.x * XG_UBLK + threadIdx.x;
@@ -189,10 +220,12 @@ __global__ void __launch_bounds__(XG_UBLK) xg_digits_kernel(const double* __rest
       W = r >= 63 ? (i128)0 : (i128)((M + (1LL << (r - 1))) >> r);
     }
     const i128 t = (i128)tcol[j];
-    V[j] = W * t;
+    const i128 v = W * t;  // >= 0, < 2^89: four 24-bit limbs
+    VL[j] = make_uint4((uint32_t)v & 0xFFFFFFu, (uint32_t)(v >> 24) & 0xFFFFFFu, (uint32_t)(v >> 48) & 0xFFFFFFu,
+                       (uint32_t)(v >> 72) & 0xFFFFFFu);
     c = W * t * t;
   } else if (j < kp) {
-    V[j] = 0;
+    VL[j] = make_uint4(0, 0, 0, 0);
   }
   if (j < kp) {
     i128 x = W;
@@ -226,7 +259,7 @@ __global__ void __launch_bounds__(XG_UBLK) xg_digits_kernel(const double* __rest
 constexpr int XG_TP = 256 + 16;  // LDS row pitch of the 64-locus x 256-individual tile
 __global__ void __launch_bounds__(256) xg_transpose_u_kernel(const int8_t* __restrict__ D, int64_t ldd, int64_t p,
                                                              int64_t n, int64_t kp, int64_t npad,
-                                                             const i128* __restrict__ V, int8_t* __restrict__ Dt,
+                                                             const uint4* __restrict__ VL, int8_t* __restrict__ Dt,
                                                              int8_t* __restrict__ St, i128* __restrict__ Upart) {
   __shared__ __attribute__((aligned(16))) int8_t tile[64 * XG_TP];
   const int64_t i0 = (int64_t)blockIdx.x * 256;
@@ -265,24 +298,32 @@ __global__ void __launch_bounds__(256) xg_transpose_u_kernel(const int8_t* __res
     if (kt + gridDim.y < nkt) load_rows(kt + gridDim.y);  // the next tile's rows in flight during this one
     __syncthreads();
     if (i < npad) {
+      // U in four 24-bit limbs of V_j: one v_mad_u32_u24 per limb and dosage, 32-bit sums exact over the
+      // tile's 64 loci (64·2·(2^24 − 1) < 2^31), carried into the int128 once per tile
       uint32_t dw[16], sw[16];
+      uint32_t l0 = 0, l1 = 0, l2 = 0, l3 = 0;
 #pragma unroll
       for (int q = 0; q < 16; q++) {
-        uint32_t a = 0, sl = 0;
+        uint32_t a = 0;
 #pragma unroll
         for (int b = 0; b < 4; b++) {
           const int kk = q * 4 + b;
           const uint32_t d = (uint32_t)(uint8_t)tile[kk * XG_TP + threadIdx.x];
-          const uint32_t sel = d == 2 ? (uint32_t)b : (d == 1 ? 4u + b : 12u);
           a |= d << (8 * b);
-          sl |= sel << (8 * b);
-          const i128 vv = V[k0 + kk];  // 0 beyond p
-          if (d & 1) u += vv;
-          if (d & 2) u += vv + vv;
+          const uint4 vl = VL[k0 + kk];  // 0 beyond p
+          l0 += __umul24(d, vl.x);
+          l1 += __umul24(d, vl.y);
+          l2 += __umul24(d, vl.z);
+          l3 += __umul24(d, vl.w);
         }
         dw[q] = a;
-        sw[q] = sl;
+        // the St selectors of the four bytes: 12 / 4 / 0 for d = 0 / 1 / 2 (a v_perm table lookup), plus the
+        // byte's position b where d > 0
+        const uint32_t h = __builtin_amdgcn_perm(0u, 0x0000040Cu, a);
+        const uint32_t m = (a | (a >> 1)) & 0x01010101u;
+        sw[q] = h + ((m * 0xFFu) & 0x03020100u);
       }
+      u += (i128)l0 + ((i128)l1 << 24) + ((i128)l2 << 48) + ((i128)l3 << 72);
       const int64_t off = i * kp + k0;
 #pragma unroll
       for (int q = 0; q < 4; q++) {
@@ -597,7 +638,7 @@ xg_gemm_kernel(const int8_t* __restrict__ Dt, const int8_t* __restrict__ St, int
 constexpr int64_t kXgSplitPieces = 256;  // the most (unit, loci range) pieces of the split tail (one round of 256 CUs)
 struct XgLayout {
   int64_t npad, kp, nst, nr, ncp;
-  int64_t off_dt, off_st, off_ww, off_w, off_t, off_v, off_cp, off_up, off_nu, off_c, off_info, off_part, off_cnt, total;
+  int64_t off_dt, off_st, off_ww, off_w, off_t, off_v, off_cp, off_up, off_nu, off_c, off_info, off_sp, off_part, off_cnt, total;
 };
 
 static XgLayout xg_layout(int64_t n, int64_t p) {
@@ -624,6 +665,7 @@ static XgLayout xg_layout(int64_t n, int64_t p) {
   L.off_nu = take(16 * L.npad);
   L.off_c = take(16);
   L.off_info = take(sizeof(XgInfo));
+  L.off_sp = take((int64_t)XG_SGRID * sizeof(XgStatsPart));
   // split-unit partials: at most kXgSplitPieces (unit, range) pieces x 8 waves x XG_SMAX x 4 i32x4 per lane
   L.off_part = take((int64_t)kXgSplitPieces * 8 * XG_SMAX * 4 * 64 * 16);
   L.off_cnt = take((int64_t)kXgSplitPieces * 8 * 4);
@@ -666,17 +708,19 @@ int launch_grm_exact(const int8_t* D, int64_t ldd, int64_t p, int64_t n, int plo
   int8_t* WW = w8 + L.off_ww;
   double* w = reinterpret_cast<double*>(w8 + L.off_w);
   int64_t* tcol = reinterpret_cast<int64_t*>(w8 + L.off_t);
-  i128* V = reinterpret_cast<i128*>(w8 + L.off_v);
+  uint4* VL = reinterpret_cast<uint4*>(w8 + L.off_v);
   i128* Cpart = reinterpret_cast<i128*>(w8 + L.off_cp);
   i128* Upart = reinterpret_cast<i128*>(w8 + L.off_up);
   i128* NU = reinterpret_cast<i128*>(w8 + L.off_nu);
   i128* C = reinterpret_cast<i128*>(w8 + L.off_c);
   XgInfo* info = reinterpret_cast<XgInfo*>(w8 + L.off_info);
 
-  xg_info_init_kernel<<<1, 1, 0, s>>>(info);
-  const int sgrid = (int)std::min<int64_t>((p + 3) / 4, 4096);  // one wave per locus (grid-strided)
+  XgStatsPart* spart = reinterpret_cast<XgStatsPart*>(w8 + L.off_sp);
+  const int sgrid = (int)std::min<int64_t>((p + 3) / 4, XG_SGRID);  // one wave per locus (grid-strided)
   xg_stats_kernel<<<sgrid, 256, 0, s>>>(D, ldd, p, n, 1.0 / ploidy, mean, sd, keep,
-                                        reinterpret_cast<unsigned long long*>(q_dev), w, tcol, info);
+                                        reinterpret_cast<unsigned long long*>(q_dev), w, tcol, spart);
+  GBM_LAUNCH_CHECK();
+  xg_stats_reduce_kernel<<<1, 256, 0, s>>>(spart, sgrid, reinterpret_cast<unsigned long long*>(q_dev), info);
   GBM_LAUNCH_CHECK();
   XgInfo h{};
   GBM_HIP_TRY(hipMemcpyAsync(&h, info, sizeof(h), hipMemcpyDeviceToHost, s));
@@ -689,10 +733,10 @@ int launch_grm_exact(const int8_t* D, int64_t ldd, int64_t p, int64_t n, int plo
     xg_choose(h.emin, h.emax, wmax, S, F);
   }
   if (slices_out) *slices_out = S;
-  xg_digits_kernel<<<(unsigned)L.ncp, XG_UBLK, 0, s>>>(w, tcol, p, L.kp, S, F, WW, V, Cpart, info);
+  xg_digits_kernel<<<(unsigned)L.ncp, XG_UBLK, 0, s>>>(w, tcol, p, L.kp, S, F, WW, VL, Cpart, info);
   GBM_LAUNCH_CHECK();
   xg_transpose_u_kernel<<<dim3((unsigned)((L.npad + 255) / 256), (unsigned)L.nr), 256, 0, s>>>(D, ldd, p, n, L.kp, L.npad,
-                                                                                              V, Dt, St, Upart);
+                                                                                              VL, Dt, St, Upart);
   GBM_LAUNCH_CHECK();
   xg_u_reduce_kernel<<<(unsigned)((L.npad + XG_UBLK - 1) / XG_UBLK), XG_UBLK, 0, s>>>(Upart, L.nr, L.npad, n, Cpart,
                                                                                       L.ncp, NU, C);

@@ -125,3 +125,41 @@ def test_perm_selector_encoding():
             out.append(0 if sel == 12 else pool[sel])
         got = [x - 256 if x > 127 else x for x in out]
         assert got == [int(d[b]) * int(om[b]) for b in range(4)]
+
+
+def _perm(src0, src1, sel):
+    """v_perm_b32 for selector bytes 0-7 and 12 (the only ones the exact GRM uses)."""
+    pool = [(src1 >> (8 * k)) & 0xFF for k in range(4)] + [(src0 >> (8 * k)) & 0xFF for k in range(4)]
+    out = 0
+    for b in range(4):
+        s = (sel >> (8 * b)) & 0xFF
+        v = 0 if s == 12 else pool[s]
+        out |= v << (8 * b)
+    return out
+
+
+def test_selector_dword_formula():
+    """xg_transpose_u_kernel builds the four St selectors of a dword of dosages at once:
+    h = v_perm(0, 0x0000040C, a) (12 / 4 / 0 for d = 0 / 1 / 2) plus b where d > 0."""
+    for a_b in np.ndindex(3, 3, 3, 3):
+        a = sum(d << (8 * b) for b, d in enumerate(a_b))
+        h = _perm(0, 0x0000040C, a)
+        m = (a | (a >> 1)) & 0x01010101
+        sw = (h + ((m * 0xFF) & 0x03020100)) & 0xFFFFFFFF
+        want = sum(((b if d == 2 else (4 + b if d == 1 else 12)) << (8 * b)) for b, d in enumerate(a_b))
+        assert sw == want
+
+
+def test_u_limbs():
+    """U_i = Σ_j V_j d_ij in four 24-bit limbs of V_j (V_j < 2^89), 32-bit limb sums over 64 loci."""
+    rng = np.random.default_rng(5)
+    for _ in range(20):
+        V = [int(x) for x in rng.integers(0, 2 ** 62, 64)]
+        V = [v * int(rng.integers(1, 2 ** 26)) for v in V]  # up to ~2^88
+        d = [int(x) for x in rng.integers(0, 3, 64)]
+        limbs = [0, 0, 0, 0]
+        for v, dd in zip(V, d):
+            for l in range(4):
+                limbs[l] += dd * ((v >> (24 * l)) & 0xFFFFFF)
+        assert max(limbs) < 2 ** 31
+        assert sum(x << (24 * l) for l, x in enumerate(limbs)) == sum(v * dd for v, dd in zip(V, d))
