@@ -336,19 +336,32 @@ __global__ void __launch_bounds__(256) xg_transpose_u_kernel(const int8_t* __res
 }
 
 // ---- n·U_i and C from the partials ----------------------------------------------------------------------
-__global__ void __launch_bounds__(XG_UBLK) xg_u_reduce_kernel(const i128* __restrict__ Upart, int64_t nr, int64_t npad,
-                                                              int64_t n, const i128* __restrict__ Cpart, int64_t ncp,
-                                                              i128* __restrict__ NU, i128* __restrict__ C) {
-  const int64_t i = (int64_t)blockIdx.x * XG_UBLK + threadIdx.x;
-  if (i < npad) {
-    i128 u = 0;
-    for (int64_t r = 0; r < nr; r++) u += Upart[r * npad + i];
-    NU[i] = u * (i128)n;
-  }
-  if (i == 0) {
+// Block: 64 individuals, its four waves over the loci-tile partials r = wave, wave + 4, ... (the loads of a
+// thread independent), combined through LDS; block 0 also sums the C partials with all its threads.
+__global__ void __launch_bounds__(256) xg_u_reduce_kernel(const i128* __restrict__ Upart, int64_t nr, int64_t npad,
+                                                          int64_t n, const i128* __restrict__ Cpart, int64_t ncp,
+                                                          i128* __restrict__ NU, i128* __restrict__ C) {
+  __shared__ i128 red[256];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int64_t i = (int64_t)blockIdx.x * 64 + lane;
+  i128 u = 0;
+  if (i < npad)
+#pragma unroll 4
+    for (int64_t r = wv; r < nr; r += 4) u += Upart[r * npad + i];
+  red[threadIdx.x] = u;
+  __syncthreads();
+  if (wv == 0 && i < npad) NU[i] = (red[lane] + red[64 + lane] + red[128 + lane] + red[192 + lane]) * (i128)n;
+  if (blockIdx.x == 0) {
+    __syncthreads();
     i128 c = 0;
-    for (int64_t b = 0; b < ncp; b++) c += Cpart[b];
-    *C = c;
+    for (int64_t b = threadIdx.x; b < ncp; b += 256) c += Cpart[b];
+    red[threadIdx.x] = c;
+    __syncthreads();
+    for (int off = 128; off >= 1; off >>= 1) {
+      if (threadIdx.x < off) red[threadIdx.x] += red[threadIdx.x + off];
+      __syncthreads();
+    }
+    if (threadIdx.x == 0) *C = red[0];
   }
 }
 
@@ -646,7 +659,13 @@ static XgLayout xg_layout(int64_t n, int64_t p) {
   L.npad = npad_of(n);
   L.kp = round_up(p < 1 ? 1 : p, XG_KALIGN);
   L.nst = L.kp / XG_BK;
-  L.nr = std::min<int64_t>(L.kp / 64, 64);  // loci-tile groups of the transpose + U kernel
+  // loci-tile groups of the transpose + U kernel (GBM_XG_TNR: A/B knob, read at sizing and launch alike)
+  // about 8192 blocks in all (more loci groups measured faster at C2: 64 → 312 µs, 512 → 215 µs), at
+  // least 64 groups
+  const int64_t xblocks = (L.npad + 255) / 256;  // the transpose grid's x
+  int64_t tnr = std::max<int64_t>(64, (8192 + xblocks - 1) / xblocks);
+  if (const char* te = getenv("GBM_XG_TNR")) tnr = std::max<int64_t>(1, std::min<int64_t>(atoll(te), 1024));
+  L.nr = std::min<int64_t>(L.kp / 64, tnr);
   L.ncp = (L.kp + XG_UBLK - 1) / XG_UBLK;
   int64_t o = 0;
   auto take = [&](int64_t bytes) {
@@ -738,7 +757,7 @@ int launch_grm_exact(const int8_t* D, int64_t ldd, int64_t p, int64_t n, int plo
   xg_transpose_u_kernel<<<dim3((unsigned)((L.npad + 255) / 256), (unsigned)L.nr), 256, 0, s>>>(D, ldd, p, n, L.kp, L.npad,
                                                                                               VL, Dt, St, Upart);
   GBM_LAUNCH_CHECK();
-  xg_u_reduce_kernel<<<(unsigned)((L.npad + XG_UBLK - 1) / XG_UBLK), XG_UBLK, 0, s>>>(Upart, L.nr, L.npad, n, Cpart,
+  xg_u_reduce_kernel<<<(unsigned)((L.npad + 63) / 64), 256, 0, s>>>(Upart, L.nr, L.npad, n, Cpart,
                                                                                       L.ncp, NU, C);
   GBM_LAUNCH_CHECK();
   const char* be = getenv("GBM_XG_BK");
