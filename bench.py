@@ -45,7 +45,16 @@ MEASURED_MFMA_F64_TFLOPS = 74.1  # back-to-back v_mfma_f64_16x16x4_f64 loop, too
 
 def parse():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="ranks (one process per GPU). N > 1 without torchrun's WORLD_SIZE: this process starts "
+                         "torch.distributed.run with N ranks as a child and relays its line")
+    ap.add_argument("--collectives", choices=("auto", "always"), default="auto",
+                    help="always: run the step's collectives (packed partial-GRM all-reduce, Cholesky strip "
+                         "all-gathers from n >= GBM_DIST_SOLVE_MIN_N) even at world size 1, over a 1-rank "
+                         "process group of --dist-backend (RCCL by default)")
+    ap.add_argument("--launch-check", action="store_true",
+                    help="harness check without GPU work: rendezvous, barriers, max-over-ranks timing and the "
+                         "rank-0 line around an empty step (value null); for CPU tests of the N-rank launcher")
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--individuals", type=int, default=5000)
@@ -254,6 +263,8 @@ def _cpu_baseline_packed(packed):
 
 
 def _isolated_child(fn, args, conn):
+    import faulthandler
+    faulthandler.enable()  # a fatal signal in the leg prints every thread's Python stack to stderr
     try:
         conn.send(("ok", fn(args)))
     except Exception as e:  # pragma: no cover - reported by the parent
@@ -282,9 +293,19 @@ def run_isolated(fn, args, timeout_s=400):
     if p.is_alive():
         p.kill()
         p.join()
-    if p.exitcode not in (0, None) and "error" in out:
-        out["error"] += f" (child exit code {p.exitcode})"
+    if p.exitcode not in (0, None):
+        import signal
+        crash = {"exit_code": p.exitcode,
+                 "signal": signal.Signals(-p.exitcode).name if p.exitcode < 0 else None,
+                 "leg": getattr(fn, "__name__", str(fn))}
+        if isinstance(out, dict) and "error" in out:
+            out["error"] += f" (child exit code {p.exitcode})"
+            out["crash"] = crash
+        _CRASHES.append(crash)
     return out
+
+
+_CRASHES = []  # isolated CPU legs that died (exit code / signal): reported in the line, the run marked failed
 
 
 def host_path(args, torch):
@@ -373,23 +394,106 @@ def load_pmc(n, p):
     return d.get("hbm_bytes_per_launch"), d.get("grm_hip_sha256") != sha
 
 
-def main():
-    args = parse()
-    import torch
-    import torch.distributed as dist
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
 
+
+def launch_ranks(args, argv):
+    """`bench.py --gpus N` (N > 1) run without torchrun: start `python -m torch.distributed.run
+    --nproc-per-node N ... bench.py <same arguments>` as a CHILD process (one rank per GPU; this parent
+    never touches the GPU: torch.cuda.device_count() does not initialise HIP) and exit with its code. The
+    ranks' rank-0 line goes straight to this process's stdout. Refuses (exit 3) when fewer than N devices
+    are visible, unless --same-device (all ranks on cuda:0: a rehearsal) or --launch-check."""
+    import subprocess
+    n = args.gpus
+    if not (args.same_device or args.launch_check):
+        import torch
+        have = torch.cuda.device_count()
+        if have < n:
+            print(f"bench.py: --gpus {n} needs {n} visible GPUs, found {have}; refusing to time fewer ranks "
+                  f"than asked (use --same-device to rehearse {n} ranks on one GPU)", file=sys.stderr, flush=True)
+            return 3
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + list(argv)
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # RCCL over dmabuf IPC only on this pool
+    return subprocess.call(cmd, env=env)
+
+
+def init_ranks(args, torch, dist):
+    """(world, rank, device index) of this process; initialises the process group for N > 1 ranks (and for
+    --collectives always at one rank, a 1-rank group)."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        dev_idx = 0 if args.same_device else local_rank
+    if args.gpus is not None and args.gpus != world:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world} ranks were launched")
+    dev_idx = 0 if (args.same_device or world == 1) else local_rank
+    if not args.launch_check:
         torch.cuda.set_device(dev_idx)
-        if args.dist_backend == "nccl":
+    if world > 1 or args.collectives == "always":
+        if world == 1:
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", str(_free_port()))
+            os.environ.setdefault("RANK", "0")
+            os.environ.setdefault("WORLD_SIZE", "1")
+        if args.dist_backend == "nccl" and not args.launch_check:
             dist.init_process_group("nccl", device_id=torch.device("cuda", dev_idx))
         else:
-            dist.init_process_group(args.dist_backend)
+            dist.init_process_group("gloo" if args.launch_check else args.dist_backend)
+        world = dist.get_world_size()
+        rank = dist.get_rank()
+    return world, rank, dev_idx
+
+
+def launch_check(args, torch, dist, world, rank):
+    """The N-rank harness around an empty step (no GPU): barrier, K timed steps, max over ranks, one line."""
+    def sync():
+        if world > 1 or dist.is_initialized():
+            dist.barrier()
+    for _ in range(args.warmup):
+        pass
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        pass
+    sync()
+    el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
+    if dist.is_initialized():
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+        ranks = [None] * world
+        dist.all_gather_object(ranks, {"rank": rank, "pid": os.getpid()})
     else:
-        torch.cuda.set_device(0)
+        ranks = [{"rank": 0, "pid": os.getpid()}]
+    if rank == 0:
+        print(json.dumps({"metric": "GRM+GBLUP genotype-cells/s (n x p)", "value": None, "unit": "genotype-cells/s",
+                          "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+                          "ms_per_step": float(el.item()) * 1000.0 / max(args.steps, 1), "higher_is_better": True,
+                          "scaling": "weak", "launch_check": True,
+                          "note": "harness check only (--launch-check): empty step, no GPU work, not a measurement",
+                          "world_size": world, "backend": dist.get_backend() if dist.is_initialized() else None,
+                          "ranks": ranks}), flush=True)
+    if dist.is_initialized():
+        dist.destroy_process_group()
+
+
+def main():
+    import faulthandler
+    faulthandler.enable()
+    args = parse()
+    if args.gpus is not None and args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args, sys.argv[1:]))
+    import torch
+    import torch.distributed as dist
+
+    world, rank, dev_idx = init_ranks(args, torch, dist)
+    if args.launch_check:
+        return launch_check(args, torch, dist, world, rank)
     dev = torch.cuda.current_device()
 
     import gbm
@@ -397,7 +501,7 @@ def main():
     from gbm.sharded import (HipExactShardStages, HipShardStages, HipStreamedShardStages, LocalComm, TorchComm,
                              assemble_b_hat, sharded_gblup_step)
 
-    comm = TorchComm() if world > 1 else LocalComm()
+    comm = TorchComm(force=args.collectives == "always") if dist.is_initialized() else LocalComm()
     n, p_local = args.individuals, args.loci
     p_total = p_local * world
     j0 = rank * p_local
@@ -432,7 +536,7 @@ def main():
         for _ in range(args.warmup):
             sharded_gblup_step(st, comm)
         torch.cuda.synchronize()
-        if world > 1:
+        if dist.is_initialized():
             dist.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
@@ -442,11 +546,11 @@ def main():
             out = sharded_gblup_step(st, comm, events=mark)
             recs.append(evs)
         torch.cuda.synchronize()
-        if world > 1:
+        if dist.is_initialized():
             dist.barrier()
         torch.cuda.synchronize()
         elapsed = time.perf_counter() - t0
-        if world > 1:
+        if dist.is_initialized():
             t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             elapsed = float(t.item())
@@ -457,6 +561,10 @@ def main():
 
     ms_per_step, stage_ms, out = run_steps(st)
     syrk_ms = stage_ms["grm_syrk"]
+    per_rank = [stage_ms]
+    if dist.is_initialized():  # every rank's own stage times (GRM, all-reduce, solve ...), on rank 0
+        per_rank = [None] * world
+        dist.all_gather_object(per_rank, stage_ms)
     value = n * p_total / (ms_per_step / 1000.0)
 
     # the exact-integer GRM path (§4.8) on the same genotypes and phenotypes, measured beside the fp64
@@ -490,8 +598,7 @@ def main():
     assert np.all(np.isfinite(out["y_pred"])) and np.all(np.isfinite(out["B"]))
 
     if rank != 0:
-        if world > 1:
-            dist.destroy_process_group()
+        dist.destroy_process_group()
         return
 
     # algorithmic work of SURVEY.md §8d: GRM n(n+1)p (unique triangle of the rank-p update),
@@ -547,6 +654,12 @@ def main():
         },
         "stage_ms": stage_ms,
         "e2e_fp64_frac_of_peak": e2e_frac,
+        "world_size": world,
+        "backend": dist.get_backend() if dist.is_initialized() else None,
+        "collectives": ("RCCL" if dist.is_initialized() and dist.get_backend() == "nccl" else
+                        dist.get_backend() if dist.is_initialized() else "none (one rank)")
+                       + (" (forced at one rank: --collectives always)" if world == 1 and dist.is_initialized() else ""),
+        "per_rank_stage_ms": per_rank if world > 1 or dist.is_initialized() else None,
     }
     if exact:
         S = int(st.slices.value)
@@ -591,8 +704,11 @@ def main():
     if alt is not None:
         alt.pop("gpu", None)
         rec["exact_grm_path"] = alt
+    if _CRASHES:  # a CPU leg died: a finding, not a footnote (its stack is on stderr via faulthandler)
+        rec["run_ok"] = False
+        rec["cpu_leg_crashes"] = _CRASHES
     print(json.dumps(rec), flush=True)
-    if world > 1:
+    if dist.is_initialized():
         dist.destroy_process_group()
 
 

@@ -9,6 +9,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <cstring>
 #include <map>
@@ -124,7 +125,8 @@ struct Shard {
   int64_t j0 = 0, p = 0;
   int64_t q_host = 0;
   int64_t stream = 0;  // loci per chunk of the loci-streamed mode (plan_streaming); 0: resident
-  bool exact = false;  // the exact-integer GRM of the resident dosages (grm_exact.hip, GBM_GRM=exact)
+  bool exact = false;  // the exact-integer GRM of the resident dosages (grm_exact.hip, grm_mode exact / auto)
+  bool d8_ready = false;  // fp64 X already converted into the dosage bytes D8 (dosage_upload_shard)
   int leader = -1;  // index of the shard that holds this device's summed GRM (itself if first)
   ~Shard() {
     if (c) pool().release(std::move(c));
@@ -531,16 +533,72 @@ int stream_grm_shard(const Problem& pr, Shard& sh) {
   return GBM_OK;
 }
 
+// ---- GRM mode of a call (include/gbm.h GBM_GRM_*) -------------------------------------------------------
 // The exact-integer GRM (grm_exact.hip) of a dosage shard: the dosages stay resident as
-// bytes (uploaded, or generated on the device), their GRM is computed exactly by int8 digit GEMMs, and
-// the marker effects re-read them (stream_effects_shard). Chosen per call by GBM_GRM=exact for int8 and
-// synthetic sources of diploid dosages; no fp64 genotype rows are formed.
-bool exact_grm_wanted(const Problem& pr) {
+// bytes (uploaded, converted from fp64 X on the device, or generated there), their GRM is computed exactly by
+// int8 digit GEMMs, and the marker effects re-read them (stream_effects_shard). No fp64 genotype rows are
+// formed. grm_mode exact / auto picks it per call; GBM_GRM (fp64 | exact | auto) only supplies the mode of
+// calls that pass GBM_GRM_DEFAULT.
+constexpr int kNotDosage = 1;  // internal: the genotypes are not diploid dosages (auto falls back to fp64)
+
+}  // namespace
+
+int resolve_grm_mode(int grm_mode) {
+  if (grm_mode != GBM_GRM_DEFAULT) return grm_mode;
   const char* e = getenv("GBM_GRM");
-  return e && strcmp(e, "exact") == 0 && (pr.src == Source::SYNTH || (pr.src == Source::I8 && pr.ploidy == 2));
+  if (e && strcmp(e, "exact") == 0) return GBM_GRM_EXACT;
+  if (e && strcmp(e, "auto") == 0) return GBM_GRM_AUTO;
+  return GBM_GRM_FP64;
 }
 
-int exact_grm_shard(const Problem& pr, Shard& sh) {
+namespace {
+
+// fp64 host X of a shard → dosage bytes D8 = 2x on the device (chunks of loci through two fp64 staging
+// buffers, the upload of chunk k + 1 beside the conversion of chunk k). Returns kNotDosage when some 2x is not
+// exactly 0, 1 or 2 — with early_exit (grm_mode auto) already after the first chunk, so data that is not
+// dosage-valued costs one chunk's upload before the fp64 path takes over.
+int dosage_upload_shard(const Problem& pr, Shard& sh, bool early_exit) {
+  FitCtx& c = sh.x();
+  const int64_t n = pr.n, pl = sh.p;
+  GBM_HIP_TRY(hipSetDevice(c.dev));
+  hipStream_t s = c.stream.s;
+  GBM_TRY(ensure_copy_stream(c));
+  const int64_t chunk = std::max<int64_t>(256, std::min<int64_t>((pl + 7) / 8, ((int64_t)1 << 30) / (n * 8)));
+  const auto sched = chunk_schedule(pl, std::min(chunk, pl), false);
+  const int64_t nch = (int64_t)sched.size();
+  GBM_TRY(ensure_events(c, nch + 2));
+  GBM_TRY(ensure(c.Xt, c.dev, 2 * std::min(chunk, pl) * n * 8));
+  GBM_TRY(ensure(c.D8, c.dev, pl * n));
+  GBM_TRY(ensure(c.errs, c.dev, 4));
+  GBM_HIP_TRY(hipMemsetAsync(c.errs.p, 0, 4, s));
+  int32_t bad = 0;
+  for (int64_t k = 0; k < nch; k++) {
+    const int64_t j = sched[k].first, pc = sched[k].second;
+    double* buf = (double*)c.Xt.p + (k % 2) * std::min(chunk, pl) * n;
+    if (k >= 2) GBM_HIP_TRY(hipStreamWaitEvent(c.copy.s, c.ev[nch + k % 2], 0));
+    GBM_HIP_TRY(hipMemcpy2DAsync(buf, n * 8, pr.X + (sh.j0 + j) * pr.ld, pr.ld * 8, n * 8, pc, hipMemcpyHostToDevice,
+                                 c.copy.s));
+    GBM_HIP_TRY(hipEventRecord(c.ev[k], c.copy.s));
+    GBM_HIP_TRY(hipStreamWaitEvent(s, c.ev[k], 0));
+    GBM_TRY(launch_dosage_from_f64(buf, n, n, pc, (int8_t*)c.D8.p + j * n, n, (int32_t*)c.errs.p, s));
+    GBM_HIP_TRY(hipEventRecord(c.ev[nch + k % 2], s));
+    if (k == 0 && early_exit && nch > 1) {
+      GBM_HIP_TRY(hipMemcpyAsync(&bad, c.errs.p, 4, hipMemcpyDeviceToHost, s));
+      GBM_HIP_TRY(hipStreamSynchronize(s));
+      if (bad) break;
+    }
+  }
+  GBM_HIP_TRY(hipMemcpyAsync(&bad, c.errs.p, 4, hipMemcpyDeviceToHost, s));
+  GBM_HIP_TRY(hipStreamSynchronize(s));
+  GBM_HIP_TRY(hipStreamSynchronize(c.copy.s));  // no upload still writes a staging buffer
+  if (bad) return kNotDosage;
+  sh.d8_ready = true;
+  return GBM_OK;
+}
+
+// check_bytes (grm_mode auto on int8 input): bytes outside {0, 1, 2} return kNotDosage instead of the
+// exact kernels' GBM_E_ARG, so that the call falls back to the fp64 path
+int exact_grm_shard(const Problem& pr, Shard& sh, bool check_bytes = false) {
   FitCtx& c = sh.x();
   const int64_t n = pr.n, gdim = gdim_of(n), pl = sh.p;
   GBM_HIP_TRY(hipSetDevice(c.dev));
@@ -553,10 +611,23 @@ int exact_grm_shard(const Problem& pr, Shard& sh) {
   GBM_TRY(ensure(c.G, c.dev, gdim * gdim * 8));
   const int64_t wsb = gbm_dev_grm_exact_workspace(n, pl);
   GBM_TRY(ensure(c.wsg, c.dev, wsb));
-  if (pr.src == Source::SYNTH)
-    GBM_TRY(gbm_dev_synth_dosage_i8((int8_t*)c.D8.p, n, pl, n, pr.seed, sh.j0, s));
-  else
-    GBM_HIP_TRY(hipMemcpy2DAsync(c.D8.p, n, pr.D + sh.j0 * pr.ld, pr.ld, n, pl, hipMemcpyHostToDevice, s));
+  if (!sh.d8_ready) {
+    if (pr.src == Source::SYNTH)
+      GBM_TRY(gbm_dev_synth_dosage_i8((int8_t*)c.D8.p, n, pl, n, pr.seed, sh.j0, s));
+    else if (pr.src == Source::I8)
+      GBM_HIP_TRY(hipMemcpy2DAsync(c.D8.p, n, pr.D + sh.j0 * pr.ld, pr.ld, n, pl, hipMemcpyHostToDevice, s));
+    else
+      return fail(GBM_E_ARG, "exact GRM: fp64 genotypes not converted to dosages");
+  }
+  if (check_bytes) {
+    int32_t bad = 0;
+    GBM_TRY(ensure(c.errs, c.dev, 4));
+    GBM_HIP_TRY(hipMemsetAsync(c.errs.p, 0, 4, s));
+    GBM_TRY(launch_dosage_check_i8((const int8_t*)c.D8.p, n, n, pl, (int32_t*)c.errs.p, s));
+    GBM_HIP_TRY(hipMemcpyAsync(&bad, c.errs.p, 4, hipMemcpyDeviceToHost, s));
+    GBM_HIP_TRY(hipStreamSynchronize(s));
+    if (bad) return kNotDosage;
+  }
   GBM_HIP_TRY(hipMemsetAsync(c.q.p, 0, 8, s));
   GBM_TRY(launch_grm_exact((const int8_t*)c.D8.p, n, pl, n, 2, (double*)c.G.p, gdim, (double*)c.mean.p,
                            (double*)c.sd.p, (int32_t*)c.keep.p, (int64_t*)c.q.p, 0, c.wsg.p, wsb, nullptr, s));
@@ -572,8 +643,8 @@ int stream_effects_shard(const Problem& pr, Shard& sh, int64_t nt, double inv_q)
   FitCtx& c = sh.x();
   const int64_t n = pr.n, npad = npad_of(n), pl = sh.p;
   hipStream_t s = c.stream.s;
-  if (pr.src != Source::F64) {
-    const int ploidy = pr.src == Source::SYNTH ? 2 : pr.ploidy;
+  if (pr.src != Source::F64 || sh.exact) {  // resident dosage bytes (an exact shard of fp64 X holds D8 = 2x)
+    const int ploidy = pr.src == Source::I8 ? pr.ploidy : 2;
     GBM_TRY(launch_marker_rows_i8((const int8_t*)c.D8.p, n, pl, n, ploidy, (const double*)c.A.p, npad, nt, inv_q,
                                   nullptr, (const double*)c.mean.p, (const double*)c.sd.p, (const int32_t*)c.keep.p,
                                   (double*)c.B.p, pl, s));
@@ -645,6 +716,9 @@ int parallel_shards(std::vector<std::unique_ptr<Shard>>& shards, Fn&& fn) {
 
 // ---- RCCL communicators, one set per distinct device list, created once ----------------------
 
+// successful RCCL collectives so far (gbm_debug_rccl_calls: tests check that the RCCL path ran)
+std::atomic<int64_t> g_rccl_allreduce{0}, g_rccl_allgather{0};
+
 struct CommSet {
   std::vector<ncclComm_t> comms;
   std::mutex mu;  // one collective at a time on a communicator (same op order on every device)
@@ -707,11 +781,18 @@ int copy_allreduce(std::vector<std::unique_ptr<Shard>>& shards, const std::vecto
   return GBM_OK;
 }
 
+// GBM_FORCE_RCCL=1 (re-read per call; a test hook): the collectives of a fit run even with one device
+// leader — the partial-GRM all-reduce and the Cholesky strip all-gathers (from n >= GBM_DIST_SOLVE_MIN_N)
+// execute on a 1-rank RCCL communicator (ncclCommInitAll over the one device) with the real payloads,
+// so the RCCL path runs on a one-GPU box. A sum or gather over one rank is the identity: same bits.
+bool force_rccl() { return env_i64("GBM_FORCE_RCCL", 0) != 0; }
+
 // Sum the partial GRMs of all shards into each device leader's G: the upper 128-tiles packed
 // contiguously (half the bytes of G's rows); shards on one device added there in shard order,
 // then the leaders all-reduced over RCCL (xGMI), then unpacked.
 int allreduce_grm(std::vector<std::unique_ptr<Shard>>& shards, int64_t n) {
-  if (shards.size() < 2) return GBM_OK;
+  const bool force = force_rccl();
+  if (shards.size() < 2 && !force) return GBM_OK;
   const int64_t gdim = gdim_of(n), psz = gbm_dev_grm_packed_size(n);
   for (auto& sh : shards) {
     FitCtx& c = sh->x();
@@ -737,7 +818,7 @@ int allreduce_grm(std::vector<std::unique_ptr<Shard>>& shards, int64_t n) {
   const bool shared_dev = std::adjacent_find(sorted.begin(), sorted.end()) != sorted.end();
   if (leaders.size() > 1 && shared_dev) {
     GBM_TRY(copy_allreduce(shards, leaders, psz));
-  } else if (leaders.size() > 1) {
+  } else if (leaders.size() > 1 || force) {
     CommSet* cs = nullptr;
     GBM_TRY(comm_set(devs, &cs));
     std::lock_guard<std::mutex> lock(cs->mu);
@@ -750,6 +831,8 @@ int allreduce_grm(std::vector<std::unique_ptr<Shard>>& shards, int64_t n) {
     ncclResult_t r2 = ncclGroupEnd();
     if (r != ncclSuccess || r2 != ncclSuccess)
       rc = fail(GBM_E_RCCL, std::string("ncclAllReduce(partial GRM): ") + ncclGetErrorString(r != ncclSuccess ? r : r2));
+    else
+      g_rccl_allreduce.fetch_add(1);
     for (int k : leaders) {  // complete the collective while holding the communicator
       FitCtx& c = shards[k]->x();
       (void)hipSetDevice(c.dev);
@@ -781,6 +864,7 @@ int allgather_strips(std::vector<std::unique_ptr<Shard>>& shards, const std::vec
     ncclResult_t r2 = ncclGroupEnd();
     if (r != ncclSuccess || r2 != ncclSuccess)
       return fail(GBM_E_RCCL, std::string("ncclAllGather(Cholesky strip): ") + ncclGetErrorString(r != ncclSuccess ? r : r2));
+    g_rccl_allgather.fetch_add(1);
     return GBM_OK;
   }
   GBM_TRY(sync_all(shards, leaders, area));  // every pack is complete
@@ -858,6 +942,29 @@ int solve_distributed(std::vector<std::unique_ptr<Shard>>& shards, const std::ve
     return gbm_dev_chol_prepare((double*)c.G.p, gdim, n, inv_q, nullptr, lambda, (const double*)c.Y.p, npad, nrhs,
                                 (int32_t*)c.info.p, c.wss.p, c.wss.cap, c.stream.s);
   }));
+  if (R == 1) {
+    // one leader (GBM_FORCE_RCCL): the redundant solve, each distributable group's final rows passed
+    // through the 1-rank all-gather between its panels and its trailing update (an identity exchange
+    // with the real payload; same bits as gbm_dev_gblup_solve's launch-per-panel path)
+    FitCtx& c = shards[leaders[0]]->x();
+    for (int64_t kb = 0; kb < nb;) {
+      const int64_t g = gbm_dev_chol_group_size(n, kb);
+      if (distributable(kb)) {
+        GBM_TRY(gbm_dev_chol_group_panels((double*)c.G.p, gdim, n, kb, 0, 1, (int32_t*)c.info.p, c.wss.p, c.wss.cap,
+                                          c.stream.s));
+        GBM_TRY(exchange(kb, g, kRows));
+        GBM_TRY(gbm_dev_chol_group_update((double*)c.G.p, gdim, n, kb, 0, 1, (int32_t*)c.info.p, c.wss.p, c.wss.cap,
+                                          c.stream.s));
+      } else {
+        GBM_TRY(gbm_dev_chol_group((double*)c.G.p, gdim, n, kb, 0, 1, (int32_t*)c.info.p, c.wss.p, c.wss.cap, c.stream.s));
+      }
+      kb += g;
+    }
+    GBM_TRY(gbm_dev_chol_finish((double*)c.G.p, gdim, n, (const double*)c.Y.p, npad, nrhs, lambda, (double*)c.A.p,
+                                (double*)c.gebv.p, npad, (double*)c.mu.p, (int32_t*)c.info.p, c.wss.p, c.wss.cap,
+                                c.stream.s));
+    return cs ? sync_all(shards, leaders) : GBM_OK;
+  }
   // GBM_DIST_OVERLAP (default 1): the next group's area is updated first and all-gathered on the copy
   // streams while the rest of the trailing update runs (same kernels, same tiles: same bits)
   const bool overlap = env_i64("GBM_DIST_OVERLAP", 1) != 0;
@@ -959,7 +1066,7 @@ int solve_effects(const Problem& pr, std::vector<std::unique_ptr<Shard>>& shards
   // gbm.sharded.dist_solve_min_n) each device leader solves the (identical) n x n system, all
   // devices at once; from there the leaders factor it together (solve_distributed). Either way a
   // ends up on every leader for the marker back-solve (same-device shards copy it from theirs).
-  const bool distributed = leaders.size() > 1 && n >= env_i64("GBM_DIST_SOLVE_MIN_N", 16384);
+  const bool distributed = (leaders.size() > 1 || force_rccl()) && n >= env_i64("GBM_DIST_SOLVE_MIN_N", 16384);
   std::vector<int32_t> infos(shards.size(), 0);
   {
     RoctxRange rsolve(distributed ? "gbm: distributed solve" : "gbm: solve");
@@ -1083,7 +1190,8 @@ int reml_lambda(FitCtx& c, int64_t n, int64_t q, const double* y, RemlResult& re
 }
 
 int run_fit(const Problem& pr, const double* Y, int64_t ldy, int64_t nrhs, double lambda, const int* devices, int ndev,
-            double* b_hat_out, double* y_pred_out, double* mu_out, int64_t* q_out, const RemlOut* reml = nullptr) {
+            double* b_hat_out, double* y_pred_out, double* mu_out, int64_t* q_out, const RemlOut* reml = nullptr,
+            int grm_mode = GBM_GRM_DEFAULT, int* grm_used_out = nullptr) {
   const int64_t n = pr.n, p = pr.p;
   if (n < 2) return fail(GBM_E_DATA, "there are less than 2 entries (reference src/prediction.jl:117-123)");
   if (p < 1 || pr.ld < n || !Y || ldy < n || nrhs < 1 || nrhs > 63 || !b_hat_out || !y_pred_out)
@@ -1092,6 +1200,11 @@ int run_fit(const Problem& pr, const double* Y, int64_t ldy, int64_t nrhs, doubl
     return fail(GBM_E_ARG, "gbm_gblup_fit: lambda must be finite and > 0");
   if (reml && n < 3) return fail(GBM_E_DATA, "REML needs at least 3 entries");
   GBM_TRY(check_y(Y, n, ldy, nrhs));
+  const int mode = resolve_grm_mode(grm_mode);
+  if (mode != GBM_GRM_FP64 && mode != GBM_GRM_EXACT && mode != GBM_GRM_AUTO)
+    return fail(GBM_E_ARG, "grm_mode must be GBM_GRM_DEFAULT, GBM_GRM_FP64, GBM_GRM_EXACT or GBM_GRM_AUTO (GBM_GRM: fp64 | exact | auto)");
+  if (mode == GBM_GRM_EXACT && pr.src == Source::I8 && pr.ploidy != 2)
+    return fail(GBM_E_ARG, "grm_mode exact: the exact-integer GRM needs diploid dosages (ploidy 2)");
   std::vector<int> devs;
   GBM_TRY(check_devices(devices, ndev, devs));
   const int64_t npad = npad_of(n), gdim = gdim_of(n);
@@ -1101,22 +1214,42 @@ int run_fit(const Problem& pr, const double* Y, int64_t ldy, int64_t nrhs, doubl
   int64_t pmax = 0;
   for (auto& sh : shards) pmax = std::max(pmax, sh->p);
   const int64_t chunk = pr.src == Source::SYNTH ? 0 : host_chunk(pmax);
-  if (exact_grm_wanted(pr))
-    for (auto& sh : shards) sh->exact = true;  // resident bytes: nothing to stream
-  else
+  // exact: every shard's dosages resident as bytes, nothing to stream; auto: the same unless the genotypes
+  // turn out not to be diploid dosages (2x outside {0, 1, 2}, int8 ploidy != 2), then the fp64 path
+  bool exact = mode != GBM_GRM_FP64 && !(pr.src == Source::I8 && pr.ploidy != 2);
+  auto fp64_grm = [&]() -> int {
     GBM_TRY(plan_streaming(pr, shards, reml != nullptr));
-  {
     // each shard's GRM is launched behind its own standardisation (a shard without polymorphic
     // loci contributes a zero partial; q == 0 over all shards fails below): streamed when its
     // rows do not fit, else resident (host chunks pipelined with the GRM, or in one piece)
-    RoctxRange r("gbm: upload + standardise + GRM");
-    GBM_TRY(parallel_shards(shards, [&](size_t, Shard& sh) {
-      if (sh.exact) return exact_grm_shard(pr, sh);
+    return parallel_shards(shards, [&](size_t, Shard& sh) {
       if (sh.stream) return stream_grm_shard(pr, sh);
       if (chunk > 0) return upload_grm_pipelined(pr, sh, chunk);
       return prepare_grm_shard(pr, sh);
-    }));
+    });
+  };
+  {
+    RoctxRange r("gbm: upload + standardise + GRM");
+    if (exact) {
+      for (auto& sh : shards) sh->exact = true;
+      const int rc = parallel_shards(shards, [&](size_t, Shard& sh) {
+        if (pr.src == Source::F64) GBM_TRY(dosage_upload_shard(pr, sh, mode == GBM_GRM_AUTO));
+        return exact_grm_shard(pr, sh, mode == GBM_GRM_AUTO && pr.src == Source::I8);
+      });
+      if (rc == kNotDosage && mode == GBM_GRM_EXACT)
+        return fail(GBM_E_ARG, "grm_mode exact: the genotypes are not diploid dosages (2x must be exactly 0, 1 or 2 "
+                               "in every cell; use grm_mode auto or fp64)");
+      if (rc == kNotDosage) {
+        exact = false;
+        for (auto& sh : shards) sh->exact = sh->d8_ready = false;
+        set_error("");
+      } else {
+        GBM_TRY(rc);
+      }
+    }
+    if (!exact) GBM_TRY(fp64_grm());
   }
+  if (grm_used_out) *grm_used_out = exact ? GBM_GRM_EXACT : GBM_GRM_FP64;
   for (auto& sh : shards) q += sh->q_host;
   if (q_out) *q_out = q;
   if (q == 0) return fail(GBM_E_DATA, "no polymorphic locus-allele (all standard deviations <= eps, src/gwas.jl:112-115)");
@@ -1200,43 +1333,85 @@ extern "C" int gbm_release_device_cache(void) {
   return GBM_OK;
 }
 
-extern "C" int gbm_gblup_fit(const double* X, int64_t n, int64_t p, int64_t ldx, const double* Y, int64_t ldy,
-                             int64_t nrhs, double lambda, const int* devices, int ndev, double* b_hat_out,
-                             double* y_pred_out, double* mu_out, int64_t* q_out) {
+extern "C" int gbm_gblup_fit_ex(const double* X, int64_t n, int64_t p, int64_t ldx, const double* Y, int64_t ldy,
+                                int64_t nrhs, double lambda, const int* devices, int ndev, int grm_mode,
+                                double* b_hat_out, double* y_pred_out, double* mu_out, int64_t* q_out,
+                                int* grm_used_out) {
   RoctxRange r_("gbm_gblup_fit");
   if (!X) return fail(GBM_E_ARG, "gbm_gblup_fit: X is NULL");
   Problem pr{Source::F64, X, nullptr, 1, n, p, ldx};
-  return run_fit(pr, Y, ldy, nrhs, lambda, devices, ndev, b_hat_out, y_pred_out, mu_out, q_out);
+  return run_fit(pr, Y, ldy, nrhs, lambda, devices, ndev, b_hat_out, y_pred_out, mu_out, q_out, nullptr, grm_mode,
+                 grm_used_out);
+}
+
+extern "C" int gbm_gblup_fit(const double* X, int64_t n, int64_t p, int64_t ldx, const double* Y, int64_t ldy,
+                             int64_t nrhs, double lambda, const int* devices, int ndev, double* b_hat_out,
+                             double* y_pred_out, double* mu_out, int64_t* q_out) {
+  return gbm_gblup_fit_ex(X, n, p, ldx, Y, ldy, nrhs, lambda, devices, ndev, GBM_GRM_DEFAULT, b_hat_out, y_pred_out,
+                          mu_out, q_out, nullptr);
+}
+
+extern "C" int gbm_gblup_fit_reml_ex(const double* X, int64_t n, int64_t p, int64_t ldx, const double* Y, int64_t ldy,
+                                     int64_t nrhs, const int* devices, int ndev, int grm_mode, double* b_hat_out,
+                                     double* y_pred_out, double* mu_out, int64_t* q_out, double* lambda_out,
+                                     double* sigma2_e_out, double* sigma2_u_out, int* grm_used_out) {
+  RoctxRange r_("gbm_gblup_fit_reml");
+  if (!X) return fail(GBM_E_ARG, "gbm_gblup_fit_reml: X is NULL");
+  Problem pr{Source::F64, X, nullptr, 1, n, p, ldx};
+  const RemlOut ro{lambda_out, sigma2_e_out, sigma2_u_out};
+  return run_fit(pr, Y, ldy, nrhs, 0.0, devices, ndev, b_hat_out, y_pred_out, mu_out, q_out, &ro, grm_mode,
+                 grm_used_out);
 }
 
 extern "C" int gbm_gblup_fit_reml(const double* X, int64_t n, int64_t p, int64_t ldx, const double* Y, int64_t ldy,
                                   int64_t nrhs, const int* devices, int ndev, double* b_hat_out, double* y_pred_out,
                                   double* mu_out, int64_t* q_out, double* lambda_out, double* sigma2_e_out,
                                   double* sigma2_u_out) {
-  RoctxRange r_("gbm_gblup_fit_reml");
-  if (!X) return fail(GBM_E_ARG, "gbm_gblup_fit_reml: X is NULL");
-  Problem pr{Source::F64, X, nullptr, 1, n, p, ldx};
-  const RemlOut ro{lambda_out, sigma2_e_out, sigma2_u_out};
-  return run_fit(pr, Y, ldy, nrhs, 0.0, devices, ndev, b_hat_out, y_pred_out, mu_out, q_out, &ro);
+  return gbm_gblup_fit_reml_ex(X, n, p, ldx, Y, ldy, nrhs, devices, ndev, GBM_GRM_DEFAULT, b_hat_out, y_pred_out,
+                               mu_out, q_out, lambda_out, sigma2_e_out, sigma2_u_out, nullptr);
+}
+
+extern "C" int gbm_gblup_fit_synthetic_ex(uint64_t seed, int64_t n, int64_t p, const double* Y, int64_t ldy,
+                                          int64_t nrhs, double lambda, const int* devices, int ndev, int grm_mode,
+                                          double* b_hat_out, double* y_pred_out, double* mu_out, int64_t* q_out,
+                                          int* grm_used_out) {
+  RoctxRange r_("gbm_gblup_fit_synthetic");
+  if (n < 1 || p < 1) return fail(GBM_E_ARG, "gbm_gblup_fit_synthetic: bad arguments (n, p >= 1)");
+  Problem pr{Source::SYNTH, nullptr, nullptr, 1, n, p, n};
+  pr.seed = seed;
+  return run_fit(pr, Y, ldy, nrhs, lambda, devices, ndev, b_hat_out, y_pred_out, mu_out, q_out, nullptr, grm_mode,
+                 grm_used_out);
 }
 
 extern "C" int gbm_gblup_fit_synthetic(uint64_t seed, int64_t n, int64_t p, const double* Y, int64_t ldy, int64_t nrhs,
                                        double lambda, const int* devices, int ndev, double* b_hat_out,
                                        double* y_pred_out, double* mu_out, int64_t* q_out) {
-  RoctxRange r_("gbm_gblup_fit_synthetic");
-  if (n < 1 || p < 1) return fail(GBM_E_ARG, "gbm_gblup_fit_synthetic: bad arguments (n, p >= 1)");
-  Problem pr{Source::SYNTH, nullptr, nullptr, 1, n, p, n};
-  pr.seed = seed;
-  return run_fit(pr, Y, ldy, nrhs, lambda, devices, ndev, b_hat_out, y_pred_out, mu_out, q_out);
+  return gbm_gblup_fit_synthetic_ex(seed, n, p, Y, ldy, nrhs, lambda, devices, ndev, GBM_GRM_DEFAULT, b_hat_out,
+                                    y_pred_out, mu_out, q_out, nullptr);
+}
+
+extern "C" int gbm_gblup_fit_dosage_i8_ex(const int8_t* D, int64_t n, int64_t p, int64_t ldd, int ploidy,
+                                          const double* Y, int64_t ldy, int64_t nrhs, double lambda, const int* devices,
+                                          int ndev, int grm_mode, double* b_hat_out, double* y_pred_out,
+                                          double* mu_out, int64_t* q_out, int* grm_used_out) {
+  RoctxRange r_("gbm_gblup_fit_dosage_i8");
+  if (!D || ploidy < 1) return fail(GBM_E_ARG, "gbm_gblup_fit_dosage_i8: D is NULL or ploidy < 1");
+  Problem pr{Source::I8, nullptr, D, ploidy, n, p, ldd};
+  return run_fit(pr, Y, ldy, nrhs, lambda, devices, ndev, b_hat_out, y_pred_out, mu_out, q_out, nullptr, grm_mode,
+                 grm_used_out);
 }
 
 extern "C" int gbm_gblup_fit_dosage_i8(const int8_t* D, int64_t n, int64_t p, int64_t ldd, int ploidy, const double* Y,
                                        int64_t ldy, int64_t nrhs, double lambda, const int* devices, int ndev,
                                        double* b_hat_out, double* y_pred_out, double* mu_out, int64_t* q_out) {
-  RoctxRange r_("gbm_gblup_fit_dosage_i8");
-  if (!D || ploidy < 1) return fail(GBM_E_ARG, "gbm_gblup_fit_dosage_i8: D is NULL or ploidy < 1");
-  Problem pr{Source::I8, nullptr, D, ploidy, n, p, ldd};
-  return run_fit(pr, Y, ldy, nrhs, lambda, devices, ndev, b_hat_out, y_pred_out, mu_out, q_out);
+  return gbm_gblup_fit_dosage_i8_ex(D, n, p, ldd, ploidy, Y, ldy, nrhs, lambda, devices, ndev, GBM_GRM_DEFAULT,
+                                    b_hat_out, y_pred_out, mu_out, q_out, nullptr);
+}
+
+extern "C" int gbm_debug_rccl_calls(int64_t* allreduce, int64_t* allgather) {
+  if (allreduce) *allreduce = g_rccl_allreduce.load();
+  if (allgather) *allgather = g_rccl_allgather.load();
+  return GBM_OK;
 }
 
 extern "C" int gbm_grm(const double* X, int64_t n, int64_t p, int64_t ldx, const int* devices, int ndev, double* G_out,

@@ -70,6 +70,13 @@ int launch_grm_exact(const int8_t* D, int64_t ldd, int64_t p, int64_t n, int plo
 // training-set dosages 2·Xt[j, idx[i]] (resident genotypes that are dosages/2) for the exact GRM
 int launch_gather_dosage(const double* Xt, int64_t ldx, int64_t p, const int32_t* idx, int64_t nT, int8_t* D,
                          hipStream_t s);
+// dosage detection (grm_mode exact / auto): D = 2·X as bytes (D may be NULL: check only), *bad = 1 when any
+// 2x is not 0, 1 or 2; the same check on dosage bytes
+int launch_dosage_from_f64(const double* X, int64_t ldx, int64_t n, int64_t p, int8_t* D, int64_t ldd, int32_t* bad,
+                           hipStream_t s);
+int launch_dosage_check_i8(const int8_t* D, int64_t ldd, int64_t n, int64_t p, int32_t* bad, hipStream_t s);
+// GBM_GRM_* of a call: grm_mode, or for GBM_GRM_DEFAULT the GBM_GRM environment variable, else fp64
+int resolve_grm_mode(int grm_mode);
 int launch_weighted_sum(const double* mean, const double* B, int64_t ldb, int64_t p, int64_t nrhs, double* msum,
                         hipStream_t s);
 int launch_center_columns(const double* Xt, int64_t ldx, int64_t p, int64_t n, double* Zt, int64_t ldz, double* mean,

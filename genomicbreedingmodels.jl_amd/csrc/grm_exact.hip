@@ -188,7 +188,7 @@ __global__ void __launch_bounds__(256) xg_stats_reduce_kernel(const XgStatsPart*
   }
   if (threadIdx.x == 0) {
     const XgStatsPart& r = red[0];
-    if (r.kept) atomicAdd(q_dev, r.kept);
+    if (r.kept && !(r.bad & 1)) atomicAdd(q_dev, r.kept);  // a call that fails (bad dosage) leaves q untouched
     info->wmax_bits = r.wmax_bits;
     info->emin = r.emin;
     info->emax = r.emax;
@@ -627,19 +627,20 @@ xg_gemm_kernel(const int8_t* __restrict__ Dt, const int8_t* __restrict__ St, int
 
   // epilogue: T = n² Σ_s 128^s acc_s − NU_i − NU_k + C in int128 → G = T 2^−F / n²
   const i128 C = *Cp;
-  const i128 n2 = (i128)n * (i128)n;
+  const u128 n2 = (u128)n * (u128)n;
   const double dn2 = (double)n * (double)n;
   const int64_t col = wc0 + fr;
-  const i128 nuk = NU[col];
+  const u128 nuk = (u128)NU[col];
 #pragma unroll
   for (int m = 0; m < 4; m++) {
 #pragma unroll
     for (int r = 0; r < 4; r++) {
       const int64_t row = wr0 + m * 16 + g * 4 + r;
-      i128 a = 0;
+      // unsigned 128-bit arithmetic (wrap-around defined); the final T fits 127 bits (host range check)
+      u128 a = 0;
 #pragma unroll
-      for (int s = S - 1; s >= 0; s--) a = a * 128 + (i128)acc[s][m][r];
-      const i128 T = n2 * a - NU[row] - nuk + C;
+      for (int s = S - 1; s >= 0; s--) a = a * 128u + (u128)(i128)acc[s][m][r];
+      const i128 T = (i128)(n2 * a - (u128)NU[row] - nuk + (u128)C);
       const double v = (row < n && col < n) ? ldexp(i128_to_double(T) / dn2, -F) : 0.0;
       double* o = G + row * ldg + col;
       *o = accum ? *o + v : v;
@@ -697,12 +698,33 @@ static XgLayout xg_layout(int64_t n, int64_t p) {
 // balanced base-128 digits whose range (max 63·(128^S − 1)/127) holds W_max = wmax·2^F. With no such
 // S ≤ XG_SMAX (weights spanning more than ~2^16), S = XG_SMAX and F shrinks: the smallest weights are
 // rounded to the grid (relative error ≤ 2^−(69 − Δe) each). Returns 1 when exact.
+// W = w·2^F as the digits kernel forms it (significand shifted, rounded half up below the grid)
+static i128 xg_fixed(double w, int F) {
+  if (!(w > 0.0)) return 0;
+  int e;
+  const double mant = std::frexp(w, &e);
+  const long long M = (long long)std::ldexp(mant, 53);
+  const int sh = e - 53 + F;
+  if (sh >= 0) return (i128)M << sh;
+  const int r = -sh;
+  return r >= 63 ? (i128)0 : (i128)((M + (1LL << (r - 1))) >> r);
+}
+
+// the largest W that S balanced base-128 digits in [−64, 63] represent: 63·(128^S − 1)/127
+static i128 xg_digit_max(int S) {
+  i128 m = 0;
+  for (int s = 0; s < S; s++) m = m * 128 + 63;
+  return m;
+}
+
 static int xg_choose(int emin, int emax, double wmax, int& S, int& F) {
   (void)emax;
   F = 52 - emin;
-  const double W = std::ldexp(wmax, F);
-  for (S = XG_SMIN; S <= XG_SMAX; S++)
-    if (W <= 63.0 * (std::ldexp(1.0, 7 * S) - 1.0) / 127.0 * (1.0 - 1e-12)) return 1;
+  if (F + std::ilogb(wmax) < 7 * XG_SMAX) {  // W_max < 2^70: compare in exact integers
+    const i128 W = xg_fixed(wmax, F);
+    for (S = XG_SMIN; S <= XG_SMAX; S++)
+      if (W <= xg_digit_max(S)) return 1;
+  }
   S = XG_SMAX;
   F = 7 * S - 3 - std::ilogb(wmax);  // W_max < 2^(7S−2) < 63·(128^S − 1)/127
   return 0;
@@ -715,7 +737,7 @@ int launch_grm_exact(const int8_t* D, int64_t ldd, int64_t p, int64_t n, int plo
                      int32_t* slices_out, hipStream_t s) {
   if (!D || !G || !mean || !sd || !keep || !q_dev || !ws || p < 1 || n < 2 || ldd < n || ldg < npad_of(n) || ploidy != 2)
     return fail(GBM_E_ARG, "gbm_dev_grm_exact_i8: bad arguments (diploid dosages {0,1,2}, p >= 1, n >= 2, ldg >= npad)");
-  // int32 digit sums: |Σ_j d·ω| <= 252 p < 2^31; the int128 bracket: n² · 2^69 · 4p < 2^126 up to n = 2^19
+  // int32 digit sums: |Σ_j d·ω| <= 252 p < 2^31 (p <= 2^23); the int128 bracket is checked below once W_max is known
   if (p > ((int64_t)1 << 23) || n > ((int64_t)1 << 19))
     return fail(GBM_E_ARG, "gbm_dev_grm_exact_i8: p <= 2^23 loci and n <= 2^19 individuals per call (integer ranges of the "
                            "exact sums); split the loci into shards (accum = 1) beyond that");
@@ -750,6 +772,12 @@ int launch_grm_exact(const int8_t* D, int64_t ldd, int64_t p, int64_t n, int plo
     double wmax;
     memcpy(&wmax, &h.wmax_bits, sizeof(wmax));
     xg_choose(h.emin, h.emax, wmax, S, F);
+    // every term of the bracket T = n²A − nU_i − nU_k + C is at most 4 n² p W_max in magnitude (d, t/n <= 2),
+    // so the int128 evaluation is exact when 16 n² p W_max < 2^127 (C3: 2^50.4 · W_max, W_max < 2^68: 2^122.4)
+    const double lg = 4.0 + 2.0 * std::log2((double)n) + std::log2((double)p) + std::log2(std::ldexp(wmax, F));
+    if (!(lg < 126.5))
+      return fail(GBM_E_ARG, "gbm_dev_grm_exact_i8: n^2 p W_max exceeds the 128-bit bracket range; split the loci "
+                             "into shards (accum = 1)");
   }
   if (slices_out) *slices_out = S;
   xg_digits_kernel<<<(unsigned)L.ncp, XG_UBLK, 0, s>>>(w, tcol, p, L.kp, S, F, WW, VL, Cpart, info);
@@ -835,7 +863,77 @@ int launch_gather_dosage(const double* Xt, int64_t ldx, int64_t p, const int32_t
   return GBM_OK;
 }
 
+// ---- dosage detection (grm_mode exact / auto on fp64 input, include/gbm.h) -----------------------------
+// p locus rows of n fp64 values (row j at X + j·ldx): D[j·ldd + i] = 2·x as a byte (if D != NULL), and
+// *bad = 1 when any 2x is not exactly 0, 1 or 2 (NaN and ±Inf included). HBM-bound: 8 B read + 1 B written
+// per cell; bad is only ever set to 1 (plain stores of one value, no atomics).
+template <bool kWrite>
+__global__ void __launch_bounds__(256) dosage_from_f64_kernel(const double* __restrict__ X, int64_t ldx, int64_t n,
+                                                              int64_t p, int8_t* __restrict__ D, int64_t ldd,
+                                                              int32_t* __restrict__ bad) {
+  int off = 0;
+  for (int64_t j = blockIdx.y; j < p; j += gridDim.y) {
+    const double* row = X + j * ldx;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+      const double v = 2.0 * row[i];
+      off |= !(v == 0.0 || v == 1.0 || v == 2.0);
+      if (kWrite) D[j * ldd + i] = (int8_t)(v == 1.0 ? 1 : v == 2.0 ? 2 : 0);
+    }
+  }
+  if (__any(off) && (threadIdx.x & 63) == 0) *bad = 1;
+}
+
+// the same check on dosage bytes: *bad = 1 when any byte is outside {0, 1, 2}
+__global__ void __launch_bounds__(256) dosage_check_i8_kernel(const int8_t* __restrict__ D, int64_t ldd, int64_t n,
+                                                              int64_t p, int32_t* __restrict__ bad) {
+  int off = 0;
+  for (int64_t j = blockIdx.y; j < p; j += gridDim.y) {
+    const int8_t* row = D + j * ldd;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+      const int d = row[i];
+      off |= (d < 0 || d > 2);
+    }
+  }
+  if (__any(off) && (threadIdx.x & 63) == 0) *bad = 1;
+}
+
+static dim3 dosage_grid(int64_t n, int64_t p) {
+  return dim3((unsigned)std::min<int64_t>((n + 255) / 256, 16), (unsigned)std::min<int64_t>(p, 8192));
+}
+
+int launch_dosage_from_f64(const double* X, int64_t ldx, int64_t n, int64_t p, int8_t* D, int64_t ldd, int32_t* bad,
+                           hipStream_t s) {
+  if (p < 1 || n < 1) return GBM_OK;
+  if (D)
+    dosage_from_f64_kernel<true><<<dosage_grid(n, p), 256, 0, s>>>(X, ldx, n, p, D, ldd, bad);
+  else
+    dosage_from_f64_kernel<false><<<dosage_grid(n, p), 256, 0, s>>>(X, ldx, n, p, nullptr, 0, bad);
+  GBM_LAUNCH_CHECK();
+  return GBM_OK;
+}
+
+int launch_dosage_check_i8(const int8_t* D, int64_t ldd, int64_t n, int64_t p, int32_t* bad, hipStream_t s) {
+  if (p < 1 || n < 1) return GBM_OK;
+  dosage_check_i8_kernel<<<dosage_grid(n, p), 256, 0, s>>>(D, ldd, n, p, bad);
+  GBM_LAUNCH_CHECK();
+  return GBM_OK;
+}
+
+// host-side digit-count choice, exported for the CPU algebra tests (no device work)
+int xg_choose_host(int emin, int emax, double wmax, int* S, int* F) {
+  int s = 0, f = 0;
+  const int exact = xg_choose(emin, emax, wmax, s, f);
+  if (S) *S = s;
+  if (F) *F = f;
+  return exact;
+}
+
 }  // namespace gbm
+
+extern "C" int gbm_debug_xg_choose(double wmin, double wmax, int* slices_out, int* shift_out) {
+  if (!(wmin > 0.0) || !(wmax >= wmin)) return gbm::fail(GBM_E_ARG, "gbm_debug_xg_choose: need 0 < wmin <= wmax");
+  return gbm::xg_choose_host(std::ilogb(wmin), std::ilogb(wmax), wmax, slices_out, shift_out);
+}
 
 extern "C" int64_t gbm_dev_grm_exact_workspace(int64_t n, int64_t p) { return gbm::grm_exact_workspace_bytes(n, p); }
 

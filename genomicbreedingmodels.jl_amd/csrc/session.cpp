@@ -37,9 +37,13 @@ struct gbm_session {
   // predict buffers
   gbm::DevMem bvec, part, pout;
   int64_t builds = 0, hits = 0;
-  // genotypes known to be diploid dosages/2 (int8 or synthetic sessions): GBM_GRM=exact builds the
-  // training GRM with the exact-integer kernels (grm_exact.hip) from the gathered training dosages
-  bool dosage2 = false;
+  // genotypes that are diploid dosages/2 (2x ∈ {0, 1, 2} in every cell: synthetic sessions by construction,
+  // others checked on the device once, when a fit first asks for it): grm_mode exact / auto
+  // (gbm_session_set_grm_mode, else GBM_GRM) builds the training GRM with the exact-integer kernels
+  // (grm_exact.hip) from the gathered training dosages
+  bool dosage2 = false, dosage_checked = false;
+  int grm_mode = GBM_GRM_DEFAULT;
+  bool exact_cached = false;  // the cached training GRM is the exact one (part of the cache key)
   gbm::DevMem D8T, wsx, mean2, sd2, keep2, q2;
   int64_t d8t_bytes = 0, wsx_bytes = 0;
 };
@@ -150,11 +154,37 @@ int check_idx(const gbm_session* s, const int64_t* idx, int64_t m, const char* w
   return GBM_OK;
 }
 
+// Whether the session's genotypes are diploid dosages/2 (one device pass over X, the first time it is asked).
+int session_dosage2(gbm_session* s, bool& out) {
+  if (!s->dosage_checked) {
+    GBM_TRY(dalloc(s->q2, s->dev, 8));
+    GBM_HIP_TRY(hipMemsetAsync(s->q2.p, 0, 4, s->stream.s));
+    GBM_TRY(launch_dosage_from_f64((const double*)s->Xt.p, s->npad, s->n, s->p, nullptr, 0, (int32_t*)s->q2.p,
+                                   s->stream.s));
+    int32_t bad = 0;
+    GBM_HIP_TRY(hipMemcpyAsync(&bad, s->q2.p, 4, hipMemcpyDeviceToHost, s->stream.s));
+    GBM_HIP_TRY(hipStreamSynchronize(s->stream.s));
+    s->dosage2 = bad == 0;
+    s->dosage_checked = true;
+  }
+  out = s->dosage2;
+  return GBM_OK;
+}
+
 // Standardise (mode 0) or centre (mode 1) the training set idx and build its GRM (cached).
 int ensure_training(gbm_session* s, const int64_t* idx, int64_t nT, int mode = 0) {
   GBM_TRY(check_idx(s, idx, nT, "gbm_session"));
   if (nT < 2) return fail(GBM_E_DATA, "there are less than 2 entries (reference src/prediction.jl:117-123)");
-  if (s->mode == mode && (int64_t)s->key.size() == nT && std::memcmp(s->key.data(), idx, (size_t)nT * 8) == 0) {
+  bool exact = false;
+  const int gm = resolve_grm_mode(s->grm_mode);
+  if (mode == 0 && gm != GBM_GRM_FP64) {
+    GBM_TRY(session_dosage2(s, exact));
+    if (!exact && gm == GBM_GRM_EXACT)
+      return fail(GBM_E_ARG, "grm_mode exact: the session's genotypes are not diploid dosages (2x must be exactly 0, "
+                             "1 or 2 in every cell; use grm_mode auto or fp64)");
+  }
+  if (s->mode == mode && s->exact_cached == exact && (int64_t)s->key.size() == nT &&
+      std::memcmp(s->key.data(), idx, (size_t)nT * 8) == 0) {
     s->hits++;
     return GBM_OK;
   }
@@ -189,8 +219,7 @@ int ensure_training(gbm_session* s, const int64_t* idx, int64_t nT, int mode = 0
   GBM_HIP_TRY(hipMemcpyAsync(&q, s->qd.p, 8, hipMemcpyDeviceToHost, st));
   GBM_HIP_TRY(hipStreamSynchronize(st));
   if (q == 0) return fail(GBM_E_DATA, "no polymorphic locus-allele in the training set (src/gwas.jl:112-115)");
-  const char* ge = getenv("GBM_GRM");
-  if (mode == 0 && s->dosage2 && ge && strcmp(ge, "exact") == 0) {
+  if (exact) {
     // exact-integer GRM of the training dosages; its per-locus statistics go to scratch (Z, mean and sd
     // above are what the marker effects and predictions use; q is the same count)
     if (s->d8t_bytes < s->p * nT) {
@@ -220,6 +249,7 @@ int ensure_training(gbm_session* s, const int64_t* idx, int64_t nT, int mode = 0
   s->q = q;
   s->key.assign(idx, idx + nT);
   s->mode = mode;
+  s->exact_cached = exact;
   s->builds++;
   return GBM_OK;
 }
@@ -319,7 +349,7 @@ extern "C" int gbm_session_create_synthetic(uint64_t seed, int64_t n, int64_t p,
   s->p = p;
   int rc = session_alloc_x(s);
   if (rc == GBM_OK) rc = gbm_dev_synth_genotypes((double*)s->Xt.p, s->npad, p, n, seed, 0, s->stream.s);
-  s->dosage2 = true;  // X = dosage/2 (SURVEY.md §8d generator)
+  s->dosage2 = s->dosage_checked = true;  // X = dosage/2 (SURVEY.md §8d generator)
   if (rc == GBM_OK && hipStreamSynchronize(s->stream.s) != hipSuccess)
     rc = fail(GBM_E_HIP, "gbm_session_create_synthetic: generation failed");
   if (rc != GBM_OK) {
@@ -348,7 +378,6 @@ extern "C" int gbm_session_create_dosage_i8(const int8_t* D, int64_t n, int64_t 
   if (rc == GBM_OK) rc = dalloc(d8, s->dev, n * p);
   if (rc == GBM_OK && (hipMemcpy2DAsync(d8.p, n, D, ldd, n, p, hipMemcpyHostToDevice, s->stream.s) != hipSuccess))
     rc = fail(GBM_E_HIP, "gbm_session_create_dosage_i8: upload failed");
-  s->dosage2 = ploidy == 2;  // and the bytes are checked to be in {0, 1, 2} by the exact kernels
   if (rc == GBM_OK) rc = gbm_dev_expand_dosage_i8((const int8_t*)d8.p, n, n, p, ploidy, (double*)s->Xt.p, s->npad,
                                                   s->stream.s);
   if (rc == GBM_OK && hipStreamSynchronize(s->stream.s) != hipSuccess) rc = fail(GBM_E_HIP, "stream sync");
@@ -357,6 +386,22 @@ extern "C" int gbm_session_create_dosage_i8(const int8_t* D, int64_t n, int64_t 
     return rc;
   }
   *out = s;
+  return GBM_OK;
+}
+
+extern "C" int gbm_session_set_grm_mode(gbm_session* s, int grm_mode) {
+  if (!s) return fail(GBM_E_ARG, "gbm_session_set_grm_mode: session is NULL");
+  if (grm_mode < GBM_GRM_DEFAULT || grm_mode > GBM_GRM_AUTO)
+    return fail(GBM_E_ARG, "gbm_session_set_grm_mode: grm_mode must be GBM_GRM_DEFAULT, _FP64, _EXACT or _AUTO");
+  std::lock_guard<std::mutex> lock(s->mu);
+  s->grm_mode = grm_mode;
+  return GBM_OK;
+}
+
+extern "C" int gbm_session_grm_used(gbm_session* s, int* grm_used) {
+  if (!s || !grm_used) return fail(GBM_E_ARG, "gbm_session_grm_used: NULL argument");
+  std::lock_guard<std::mutex> lock(s->mu);
+  *grm_used = s->key.empty() ? -1 : s->exact_cached ? GBM_GRM_EXACT : GBM_GRM_FP64;
   return GBM_OK;
 }
 

@@ -11,7 +11,7 @@ import threading
 
 import numpy as np
 
-ABI_VERSION = 200  # GBM_VERSION in include/gbm.h
+ABI_VERSION = 210  # GBM_VERSION in include/gbm.h
 GBM_OK = 0
 GBM_E_ARG = -1
 GBM_E_NOTPD = -2
@@ -43,7 +43,23 @@ EXPORTS = (
     "gbm_debug_oom_retries", "gbm_dev_chol_group_panels", "gbm_dev_chol_group_update", "gbm_dev_chol_strip_unpack_rows",
     "gbm_dev_chol_area_doubles", "gbm_dev_chol_area_pack", "gbm_dev_chol_area_unpack",
     "gbm_dev_chol_group_update_cols", "gbm_dev_grm_exact_workspace", "gbm_dev_grm_exact_i8",
+    "gbm_gblup_fit_ex", "gbm_gblup_fit_reml_ex", "gbm_gblup_fit_dosage_i8_ex", "gbm_gblup_fit_synthetic_ex",
+    "gbm_session_set_grm_mode", "gbm_session_grm_used", "gbm_debug_rccl_calls", "gbm_debug_xg_choose",
 )
+
+GBM_GRM_DEFAULT, GBM_GRM_FP64, GBM_GRM_EXACT, GBM_GRM_AUTO = -1, 0, 1, 2
+GRM_MODES = {None: GBM_GRM_DEFAULT, "default": GBM_GRM_DEFAULT, "fp64": GBM_GRM_FP64, "exact": GBM_GRM_EXACT,
+             "auto": GBM_GRM_AUTO}
+
+
+def grm_mode(mode) -> int:
+    """GBM_GRM_* of a Python/Julia-style mode name (None / "default", "fp64", "exact", "auto")."""
+    if isinstance(mode, int) and mode in GRM_MODES.values():
+        return mode
+    try:
+        return GRM_MODES[mode]
+    except (KeyError, TypeError):
+        raise ArgumentError(f"grm must be one of 'auto', 'exact', 'fp64' or None, got {mode!r}") from None
 
 
 class ArgumentError(ValueError):
@@ -189,6 +205,22 @@ def _declare(lib):
     lib.gbm_debug_oom_retries.argtypes = [P, P]
     lib.gbm_session_stats.restype = I32
     lib.gbm_session_stats.argtypes = [P, P, P]
+    lib.gbm_gblup_fit_ex.restype = I32
+    lib.gbm_gblup_fit_ex.argtypes = [P, I64, I64, I64, P, I64, I64, D, P, I32, I32, P, P, P, P, P]
+    lib.gbm_gblup_fit_reml_ex.restype = I32
+    lib.gbm_gblup_fit_reml_ex.argtypes = [P, I64, I64, I64, P, I64, I64, P, I32, I32, P, P, P, P, P, P, P, P]
+    lib.gbm_gblup_fit_dosage_i8_ex.restype = I32
+    lib.gbm_gblup_fit_dosage_i8_ex.argtypes = [P, I64, I64, I64, I32, P, I64, I64, D, P, I32, I32, P, P, P, P, P]
+    lib.gbm_gblup_fit_synthetic_ex.restype = I32
+    lib.gbm_gblup_fit_synthetic_ex.argtypes = [U64, I64, I64, P, I64, I64, D, P, I32, I32, P, P, P, P, P]
+    lib.gbm_session_set_grm_mode.restype = I32
+    lib.gbm_session_set_grm_mode.argtypes = [P, I32]
+    lib.gbm_session_grm_used.restype = I32
+    lib.gbm_session_grm_used.argtypes = [P, P]
+    lib.gbm_debug_rccl_calls.restype = I32
+    lib.gbm_debug_rccl_calls.argtypes = [P, P]
+    lib.gbm_debug_xg_choose.restype = I32
+    lib.gbm_debug_xg_choose.argtypes = [D, D, P, P]
     return lib
 
 

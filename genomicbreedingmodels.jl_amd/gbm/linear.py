@@ -8,6 +8,8 @@ same Fit assembly sequence (src/linear.jl:185-191,223-238); where ``ridge`` call
 """
 from __future__ import annotations
 
+import ctypes
+
 import numpy as np
 
 from . import _lib
@@ -17,8 +19,16 @@ from .prediction import extractxyetc
 from .types import Fit, Genomes, Phenomes
 
 
-def gblup_arrays(X: np.ndarray, Y: np.ndarray, lambda_: float = 1.0, devices=None):
-    """Array-level GBLUP through the C ABI. X (n, p) any order, Y (n,) or (n, t).
+def _grm_info(info, used):
+    if info is not None:
+        info["grm_used"] = {_lib.GBM_GRM_FP64: "fp64", _lib.GBM_GRM_EXACT: "exact"}.get(int(used.value), int(used.value))
+
+
+def gblup_arrays(X: np.ndarray, Y: np.ndarray, lambda_: float = 1.0, devices=None, grm=None, info=None):
+    """Array-level GBLUP through the C ABI (gbm_gblup_fit_ex). X (n, p) any order, Y (n,) or (n, t).
+    ``grm``: the GRM arithmetic (None: the GBM_GRM variable, else fp64; "fp64"; "exact": diploid dosages/2
+    only; "auto": exact when every 2x is 0, 1 or 2, else fp64 — include/gbm.h GBM_GRM_*). ``info`` (a dict,
+    optional) receives ``grm_used``.
 
     Returns (b_hat (p+1, t), y_pred (n, t), mu (t,), q)."""
     X = np.asfortranarray(np.asarray(X, dtype=np.float64))
@@ -34,13 +44,15 @@ def gblup_arrays(X: np.ndarray, Y: np.ndarray, lambda_: float = 1.0, devices=Non
     q = np.zeros(1, dtype=np.int64)
     devs, ndev = _lib.devices_arg(devices)
     lib = _lib.load()
-    rc = lib.gbm_gblup_fit(_lib.ptr(X), n, p, n, _lib.ptr(Y), n, t, float(lambda_), devs, ndev,
-                           _lib.ptr(b_hat), _lib.ptr(y_pred), _lib.ptr(mu), _lib.ptr(q))
+    used = ctypes.c_int(-1)
+    rc = lib.gbm_gblup_fit_ex(_lib.ptr(X), n, p, n, _lib.ptr(Y), n, t, float(lambda_), devs, ndev, _lib.grm_mode(grm),
+                              _lib.ptr(b_hat), _lib.ptr(y_pred), _lib.ptr(mu), _lib.ptr(q), ctypes.byref(used))
     _lib.check(rc, "gbm_gblup_fit")
+    _grm_info(info, used)
     return b_hat, y_pred, mu, int(q[0])
 
 
-def gblup_reml_arrays(X: np.ndarray, Y: np.ndarray, devices=None):
+def gblup_reml_arrays(X: np.ndarray, Y: np.ndarray, devices=None, grm=None, info=None):
     """Array-level GBLUP with λ chosen per trait by REML through the C ABI (gbm_gblup_fit_reml: the
     reference's loglikreml objective, src/gwas.jl:450-483, on the call's own GRM). Returns
     (b_hat (p+1, t), y_pred (n, t), mu (t,), q, reml) with reml = dict(lambda, sigma2_e, sigma2_u) of
@@ -58,14 +70,16 @@ def gblup_reml_arrays(X: np.ndarray, Y: np.ndarray, devices=None):
     q = np.zeros(1, dtype=np.int64)
     lam, s2e, s2u = np.zeros(t), np.zeros(t), np.zeros(t)
     devs, ndev = _lib.devices_arg(devices)
-    rc = _lib.load().gbm_gblup_fit_reml(_lib.ptr(X), n, p, n, _lib.ptr(Y), n, t, devs, ndev, _lib.ptr(b_hat),
-                                        _lib.ptr(y_pred), _lib.ptr(mu), _lib.ptr(q), _lib.ptr(lam), _lib.ptr(s2e),
-                                        _lib.ptr(s2u))
+    used = ctypes.c_int(-1)
+    rc = _lib.load().gbm_gblup_fit_reml_ex(_lib.ptr(X), n, p, n, _lib.ptr(Y), n, t, devs, ndev, _lib.grm_mode(grm),
+                                           _lib.ptr(b_hat), _lib.ptr(y_pred), _lib.ptr(mu), _lib.ptr(q), _lib.ptr(lam),
+                                           _lib.ptr(s2e), _lib.ptr(s2u), ctypes.byref(used))
     _lib.check(rc, "gbm_gblup_fit_reml")
+    _grm_info(info, used)
     return b_hat, y_pred, mu, int(q[0]), {"lambda": lam, "sigma2_e": s2e, "sigma2_u": s2u}
 
 
-def gblup_dosage(D: np.ndarray, ploidy: int, Y: np.ndarray, lambda_: float = 1.0, devices=None):
+def gblup_dosage(D: np.ndarray, ploidy: int, Y: np.ndarray, lambda_: float = 1.0, devices=None, grm=None, info=None):
     """GBLUP on int8 dosages (gbm_gblup_fit_dosage_i8: X = D/ploidy, 1 byte per cell over PCIe).
     D (n, p) int8, any order. Returns (b_hat (p+1, t), y_pred (n, t), mu (t,), q)."""
     D = np.asfortranarray(np.asarray(D, dtype=np.int8))
@@ -80,13 +94,16 @@ def gblup_dosage(D: np.ndarray, ploidy: int, Y: np.ndarray, lambda_: float = 1.0
     mu = np.zeros(t)
     q = np.zeros(1, dtype=np.int64)
     dev, nd = _lib.devices_arg(devices)
-    _lib.check(_lib.load().gbm_gblup_fit_dosage_i8(_lib.ptr(D), n, p, n, int(ploidy), _lib.ptr(Y), n, t,
-                                                  float(lambda_), dev, nd, _lib.ptr(b_hat), _lib.ptr(y_pred),
-                                                  _lib.ptr(mu), _lib.ptr(q)), "gbm_gblup_fit_dosage_i8")
+    used = ctypes.c_int(-1)
+    _lib.check(_lib.load().gbm_gblup_fit_dosage_i8_ex(_lib.ptr(D), n, p, n, int(ploidy), _lib.ptr(Y), n, t,
+                                                     float(lambda_), dev, nd, _lib.grm_mode(grm), _lib.ptr(b_hat),
+                                                     _lib.ptr(y_pred), _lib.ptr(mu), _lib.ptr(q), ctypes.byref(used)),
+               "gbm_gblup_fit_dosage_i8")
+    _grm_info(info, used)
     return b_hat, y_pred, mu, int(q[0])
 
 
-def gblup_synthetic(seed: int, n: int, p: int, Y: np.ndarray, lambda_: float = 1.0, devices=None):
+def gblup_synthetic(seed: int, n: int, p: int, Y: np.ndarray, lambda_: float = 1.0, devices=None, grm=None, info=None):
     """GBLUP on the device-generated synthetic genotypes (gbm_gblup_fit_synthetic: loci 0..p-1 of the
     SURVEY.md §8d generator, no host X). Returns (b_hat (p+1, t), y_pred (n, t), mu (t,), q)."""
     Y = np.asarray(Y, dtype=np.float64)
@@ -102,21 +119,27 @@ def gblup_synthetic(seed: int, n: int, p: int, Y: np.ndarray, lambda_: float = 1
     q = np.zeros(1, dtype=np.int64)
     devs, ndev = _lib.devices_arg(devices)
     lib = _lib.load()
-    rc = lib.gbm_gblup_fit_synthetic(int(seed), n, p, _lib.ptr(Y), n, t, float(lambda_), devs, ndev,
-                                     _lib.ptr(b_hat), _lib.ptr(y_pred), _lib.ptr(mu), _lib.ptr(q))
+    used = ctypes.c_int(-1)
+    rc = lib.gbm_gblup_fit_synthetic_ex(int(seed), n, p, _lib.ptr(Y), n, t, float(lambda_), devs, ndev,
+                                        _lib.grm_mode(grm), _lib.ptr(b_hat), _lib.ptr(y_pred), _lib.ptr(mu),
+                                        _lib.ptr(q), ctypes.byref(used))
     _lib.check(rc, "gbm_gblup_fit_synthetic")
+    _grm_info(info, used)
     return b_hat, y_pred, mu, int(q[0])
 
 
 def gblup(*, genomes: Genomes, phenomes: Phenomes, idx_entries=None, idx_loci_alleles=None,
           idx_trait: int = 1, verbose: bool = False, lambda_: float = 1.0, devices=None,
-          model_label: str = "gblup") -> Fit:
+          model_label: str = "gblup", grm: str = "auto") -> Fit:
     """GBLUP / RR-BLUP fit returning a ``Fit`` exactly like ``ridge`` does.
 
     ``model_label="ridge"`` lets the fit flow through an unmodified reference ``predict``
     whitelist (src/prediction.jl:225): GBLUP ≡ RR-BLUP, so the linear predictor is valid.
     ``lambda_="reml"`` chooses λ = σ²_e/σ²_u by REML first (the REML result is kept in
-    ``fit.metrics_reml``)."""
+    ``fit.metrics_reml``). ``grm`` (Julia ``grm = :auto``): "auto" computes the GRM exactly on the int8
+    matrix cores when the allele frequencies are diploid dosages/2 (2x ∈ {0, 1, 2} in every cell, checked on
+    the device), else with the fp64-MFMA SYRK; "fp64" / "exact" force one (include/gbm.h GBM_GRM_*). The GRM
+    used is kept in ``fit.grm_used``."""
     X, y, entries, populations, loci_alleles = extractxyetc(
         genomes, phenomes, idx_entries=idx_entries, idx_loci_alleles=idx_loci_alleles,
         idx_trait=idx_trait, add_intercept=False)
@@ -127,21 +150,23 @@ def gblup(*, genomes: Genomes, phenomes: Phenomes, idx_entries=None, idx_loci_al
     fit.entries = entries
     fit.populations = populations
     fit.y_true = y
+    info = {}
     if isinstance(lambda_, str):
         # REML choice of λ through the drop-in entry gbm_gblup_fit_reml: one
         # GRM, REML over the reference's loglikreml objective (src/gwas.jl:450-483), then the fit
         if lambda_ != "reml":
             raise ArgumentError(f"lambda_ must be a positive number or \"reml\", got {lambda_!r}")
-        b_hat, y_pred, mu, q, r = gblup_reml_arrays(X, y, devices=devices)
+        b_hat, y_pred, mu, q, r = gblup_reml_arrays(X, y, devices=devices, grm=grm, info=info)
         lambda_ = float(r["lambda"][0])
         fit.metrics_reml = {k: float(v[0]) for k, v in r.items()}
     else:
-        b_hat, y_pred, mu, q = gblup_arrays(X, y, lambda_=lambda_, devices=devices)
+        b_hat, y_pred, mu, q = gblup_arrays(X, y, lambda_=lambda_, devices=devices, grm=grm, info=info)
+    fit.grm_used = info.get("grm_used")
     fit.b_hat = b_hat[:, 0].copy()
     fit.y_pred = y_pred[:, 0].copy()
     fit.metrics = metrics(y, fit.y_pred)
     if verbose:
-        print(f"gblup: n={X.shape[0]} p={X.shape[1]} q={q} mu={mu[0]:.6g} lambda={lambda_}")
+        print(f"gblup: n={X.shape[0]} p={X.shape[1]} q={q} mu={mu[0]:.6g} lambda={lambda_} grm={fit.grm_used}")
         print(fit.metrics)
     if not fit.checkdims():
         raise GBMError("Error fitting " + fit.model + ".")

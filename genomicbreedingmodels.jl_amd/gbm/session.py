@@ -78,6 +78,19 @@ class GenotypeSession:
         except Exception:
             pass
 
+    # ---- GRM arithmetic -----------------------------------------------------------------------
+    def set_grm(self, grm):
+        """GRM arithmetic of the training GRMs: None (the GBM_GRM variable, else fp64), "fp64", "exact" or
+        "auto" (exact when the genotypes are diploid dosages/2; include/gbm.h gbm_session_set_grm_mode)."""
+        _lib.check(self.lib.gbm_session_set_grm_mode(self._h, _lib.grm_mode(grm)), "gbm_session_set_grm_mode")
+        return self
+
+    def grm_used(self):
+        """"fp64" or "exact": the GRM the cached training set was built with (None before the first fit)."""
+        v = ctypes.c_int(-1)
+        _lib.check(self.lib.gbm_session_grm_used(self._h, ctypes.byref(v)), "gbm_session_grm_used")
+        return {_lib.GBM_GRM_FP64: "fp64", _lib.GBM_GRM_EXACT: "exact"}.get(v.value)
+
     # ---- model calls ----------------------------------------------------------------------
     def gblup(self, idx, Y, lambda_: float = 1.0):
         """GBLUP on rows ``idx`` (0-based, strictly increasing); Y (n_train,) or (n_train, t).

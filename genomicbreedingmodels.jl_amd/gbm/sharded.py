@@ -26,16 +26,21 @@ from . import _lib
 
 
 class TorchComm:
-    """Sum all-reduce over torch.distributed (RCCL for cuda tensors, gloo for CPU tensors)."""
+    """Sum all-reduce over torch.distributed (RCCL for cuda tensors, gloo for CPU tensors).
 
-    def __init__(self):
+    ``force``: run every collective of the step even at world size 1 (``bench.py --collectives always``:
+    the partial-GRM all-reduce and the Cholesky strip all-gathers execute on a 1-rank RCCL communicator,
+    so the RCCL path runs on a one-GPU box; the results are the same bits as without collectives)."""
+
+    def __init__(self, force: bool = False):
         import torch.distributed as dist
         self.dist = dist
         self.world_size = dist.get_world_size() if dist.is_initialized() else 1
         self.rank = dist.get_rank() if dist.is_initialized() else 0
+        self.force = bool(force) and dist.is_initialized()
 
     def all_reduce_sum(self, t):
-        if self.world_size > 1:
+        if self.world_size > 1 or self.force:
             self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM)
 
     def all_gather(self, t):
@@ -53,6 +58,7 @@ class TorchComm:
 class LocalComm:
     world_size = 1
     rank = 0
+    force = False
 
     def all_reduce_sum(self, t):
         return None
@@ -69,7 +75,8 @@ def sharded_gblup_step(stages, comm, events=None):
     mark("grm_syrk")
     stages.grm_reduce()
     mark("grm_reduce")
-    if comm.world_size > 1:
+    collective = comm.world_size > 1 or getattr(comm, "force", False)
+    if collective:
         # the upper GRM tiles only (half of G's rows) with q in the packed buffer's last slot (one
         # collective instead of two), when the stages can pack them
         pack = getattr(stages, "grm_pack", None)
@@ -80,8 +87,9 @@ def sharded_gblup_step(stages, comm, events=None):
             comm.all_reduce_sum(stages.grm_rows())
             comm.all_reduce_sum(stages.q)
     mark("allreduce")
-    if comm.world_size > 1 and hasattr(stages, "chol_group") and stages.n >= dist_solve_min_n():
-        chol_distributed([stages], [comm.rank], comm.world_size, lambda packs: [comm.all_gather(packs[0])])
+    if collective and hasattr(stages, "chol_group") and stages.n >= dist_solve_min_n():
+        chol_distributed([stages], [comm.rank], comm.world_size, lambda packs: [comm.all_gather(packs[0])],
+                         force=getattr(comm, "force", False))
     else:
         stages.solve()
     mark("solve")
@@ -103,7 +111,7 @@ def dist_solve_min_n() -> int:
     return int(os.environ.get("GBM_DIST_SOLVE_MIN_N", "16384"))
 
 
-def chol_distributed(stages, ranks, nranks, allgather, tail_rows=None):
+def chol_distributed(stages, ranks, nranks, allgather, tail_rows=None, force=False):
     """GBLUP solve of V = G/q + λI distributed over ``nranks`` ranks, replacing the
     redundant per-rank factorisation (the reference's pinv(V), src/gwas.jl:472,595).
 
@@ -120,7 +128,12 @@ def chol_distributed(stages, ranks, nranks, allgather, tail_rows=None):
     and exchanged on a side stream while the rest of the update runs (gbm_dev_chol_group_update_cols).
     Once the trailing matrix is small (``tail_rows``, GBM_DIST_TAIL_ROWS, default 8192) or the groups
     shrink to single panels, every remaining row is gathered once and the tail runs redundantly. The
-    result is bit-identical to the redundant solve (the same kernels compute every tile)."""
+    result is bit-identical to the redundant solve (the same kernels compute every tile).
+
+    ``nranks == 1`` with ``force`` (a 1-rank communicator: ``bench.py --collectives always``, the C ABI's
+    GBM_FORCE_RCCL): the redundant solve, with each distributable group's final rows passed through the
+    all-gather between its panels and its trailing update (an identity exchange on one rank), so the
+    strip all-gather executes with real payloads; same bits as the redundant solve."""
     import os
     st0 = stages[0]
     lib, n = st0.lib, st0.n
@@ -149,6 +162,23 @@ def chol_distributed(stages, ranks, nranks, allgather, tail_rows=None):
 
     for st in stages:
         st.chol_prepare()
+    if nranks == 1 and force:
+        kb = 0
+        while kb < nb:
+            g = int(lib.gbm_dev_chol_group_size(n, kb))
+            if distributable(kb):
+                for st, r in zip(stages, ranks):
+                    st.chol_group_panels(kb, r, 1)
+                exchange(kb, g, "rows")
+                for st, r in zip(stages, ranks):
+                    st.chol_group_update(kb, r, 1)
+            else:
+                for st in stages:
+                    st.chol_group(kb, 0, 1)
+            kb += g
+        for st in stages:
+            st.chol_finish()
+        return
     kb = 0
     dist = nranks > 1 and distributable(0)
     stale = False  # a distributed update skipped other ranks' tiles

@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define GBM_VERSION 200 /* 0.2.0: pooled contexts, device farming, repeated device ordinals */
+#define GBM_VERSION 210 /* 0.2.1: per-call GRM mode (the _ex entries), 1-rank RCCL test hook */
 
 #define GBM_OK 0
 #define GBM_E_ARG (-1)    /* bad argument (ArgumentError on the Julia side, src/prediction.jl:67-127 style) */
@@ -52,6 +52,21 @@ extern "C" {
 #define GBM_E_OOM (-5)    /* device allocation failed */
 #define GBM_E_NODEV (-6)  /* no usable MI355X device */
 #define GBM_E_DATA (-7)   /* data problem: < 2 entries, zero phenotype variance, no polymorphic locus */
+
+/* GRM arithmetic of a fit (the grm_mode argument of the _ex entries and gbm_session_set_grm_mode):
+ *   GBM_GRM_FP64   the fp64-MFMA SYRK of the standardised genotypes (the north star's GRM; any X).
+ *   GBM_GRM_EXACT  the exact-integer GRM of diploid dosages (int8-MFMA digit GEMMs + int128 centring, one fp64
+ *                  rounding): X must hold dosages/2, i.e. 2x exactly 0, 1 or 2 in every cell
+ *                  (the allele frequencies extractxyetc hands a diploid gblup, src/prediction.jl:129), int8
+ *                  input needs ploidy 2; otherwise GBM_E_ARG. More accurate than fp64 and ~3x faster.
+ *   GBM_GRM_AUTO   EXACT when the genotypes are diploid dosages (checked on the device: for fp64 X while it is
+ *                  converted to bytes, one chunk of loci first), else FP64.
+ *   GBM_GRM_DEFAULT the environment variable GBM_GRM ("fp64" | "exact" | "auto", re-read per call), else FP64.
+ * The entries without _ex pass GBM_GRM_DEFAULT. */
+#define GBM_GRM_DEFAULT (-1)
+#define GBM_GRM_FP64 0
+#define GBM_GRM_EXACT 1
+#define GBM_GRM_AUTO 2
 
 /* Library version (GBM_VERSION) — used by bindings to check the ABI. */
 int gbm_version(void);
@@ -97,6 +112,13 @@ int gbm_gblup_fit(const double* X, int64_t n, int64_t p, int64_t ldx,
                   const int* devices, int ndev,
                   double* b_hat_out, double* y_pred_out, double* mu_out, int64_t* q_out);
 
+/* gbm_gblup_fit with the GRM arithmetic chosen per call (grm_mode: GBM_GRM_*); grm_used_out (may be NULL)
+ * receives GBM_GRM_FP64 or GBM_GRM_EXACT, the GRM the fit used. The same for the entries below. */
+int gbm_gblup_fit_ex(const double* X, int64_t n, int64_t p, int64_t ldx,
+                     const double* Y, int64_t ldy, int64_t nrhs, double lambda,
+                     const int* devices, int ndev, int grm_mode,
+                     double* b_hat_out, double* y_pred_out, double* mu_out, int64_t* q_out, int* grm_used_out);
+
 /*
  * gbm_gblup_fit with λ chosen per trait by REML — the drop-in `gblup(...; λ = :reml)` (Julia) /
  * `lambda_="reml"` (Python mirror). For each trait column, on the summed GRM of the call (built
@@ -112,6 +134,11 @@ int gbm_gblup_fit_reml(const double* X, int64_t n, int64_t p, int64_t ldx,
                        const int* devices, int ndev,
                        double* b_hat_out, double* y_pred_out, double* mu_out, int64_t* q_out,
                        double* lambda_out, double* sigma2_e_out, double* sigma2_u_out);
+int gbm_gblup_fit_reml_ex(const double* X, int64_t n, int64_t p, int64_t ldx,
+                          const double* Y, int64_t ldy, int64_t nrhs,
+                          const int* devices, int ndev, int grm_mode,
+                          double* b_hat_out, double* y_pred_out, double* mu_out, int64_t* q_out,
+                          double* lambda_out, double* sigma2_e_out, double* sigma2_u_out, int* grm_used_out);
 
 /*
  * Same as gbm_gblup_fit for int8 dosages: X[i, j] = D[i + j*ldd] / ploidy (exact in fp64).
@@ -121,6 +148,11 @@ int gbm_gblup_fit_dosage_i8(const int8_t* D, int64_t n, int64_t p, int64_t ldd, 
                             const double* Y, int64_t ldy, int64_t nrhs, double lambda,
                             const int* devices, int ndev,
                             double* b_hat_out, double* y_pred_out, double* mu_out, int64_t* q_out);
+int gbm_gblup_fit_dosage_i8_ex(const int8_t* D, int64_t n, int64_t p, int64_t ldd, int ploidy,
+                               const double* Y, int64_t ldy, int64_t nrhs, double lambda,
+                               const int* devices, int ndev, int grm_mode,
+                               double* b_hat_out, double* y_pred_out, double* mu_out, int64_t* q_out,
+                               int* grm_used_out);
 
 /*
  * Same as gbm_gblup_fit on the synthetic genotypes of gbm_dev_synth_genotypes (seed, loci
@@ -131,6 +163,11 @@ int gbm_gblup_fit_synthetic(uint64_t seed, int64_t n, int64_t p,
                             const double* Y, int64_t ldy, int64_t nrhs, double lambda,
                             const int* devices, int ndev,
                             double* b_hat_out, double* y_pred_out, double* mu_out, int64_t* q_out);
+int gbm_gblup_fit_synthetic_ex(uint64_t seed, int64_t n, int64_t p,
+                               const double* Y, int64_t ldy, int64_t nrhs, double lambda,
+                               const int* devices, int ndev, int grm_mode,
+                               double* b_hat_out, double* y_pred_out, double* mu_out, int64_t* q_out,
+                               int* grm_used_out);
 
 /*
  * Genomic relationship matrix only: G = Z Zᵀ / q (n x n, column-major == row-major since
@@ -385,6 +422,12 @@ int gbm_session_create_dosage_i8(const int8_t* D, int64_t n, int64_t p, int64_t 
  * on the device: benchmark-scale sessions (configs C4/C5) without a host copy of X. */
 int gbm_session_create_synthetic(uint64_t seed, int64_t n, int64_t p, int device, gbm_session** out);
 void gbm_session_destroy(gbm_session* s);
+/* GRM arithmetic of the session's training GRMs (GBM_GRM_*; default GBM_GRM_DEFAULT = the GBM_GRM variable):
+ * exact / auto build them with the exact-integer kernels when the genotypes are diploid dosages/2 (checked once
+ * on the device). The training-set cache is keyed by the GRM used as well. */
+int gbm_session_set_grm_mode(gbm_session* s, int grm_mode);
+/* The GRM the cached training set was built with: GBM_GRM_FP64, GBM_GRM_EXACT, or -1 before the first fit. */
+int gbm_session_grm_used(gbm_session* s, int* grm_used);
 /* gbm_gblup_fit on the rows idx[0..n_train) of the session's X; Y holds the training phenotypes
  * (n_train x nrhs, column-major). */
 int gbm_session_gblup_fit(gbm_session* s, const int64_t* idx, int64_t n_train, const double* Y, int64_t ldy,
@@ -458,6 +501,14 @@ int64_t gbm_debug_brr_trace(int64_t* host, int64_t cap);
 /* With GBM_CHOL_FLOW_TRACE=1 set for a solve: copies up to cap records of 24 int64 (tile, workgroup,
  * 100 MHz timestamps) of the last dataflow factorisation into host; returns the record count. */
 int64_t gbm_debug_chol_flow_trace(int64_t* host, int64_t cap);
+/* Successful RCCL collectives libgbm has issued (partial-GRM all-reduces; Cholesky strip all-gathers). With
+ * GBM_FORCE_RCCL=1 set for a call, a fit with one device leader still runs them on a 1-rank communicator
+ * (the all-gathers from n >= GBM_DIST_SOLVE_MIN_N), bit-identical to the call without: the RCCL path on a
+ * one-GPU box. */
+int gbm_debug_rccl_calls(int64_t* allreduce, int64_t* allgather);
+/* The exact GRM's digit count S and scale exponent F for kept-locus weights in [wmin, wmax] (host only, no
+ * device work; returns 1 when every weight is exact on the 2^-F grid, 0 when the smallest are rounded). */
+int gbm_debug_xg_choose(double wmin, double wmax, int* slices_out, int* shift_out);
 
 #ifdef __cplusplus
 }

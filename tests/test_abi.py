@@ -34,7 +34,7 @@ def test_library_exports_every_header_symbol():
 
 def test_library_loads_and_reports_version():
     lib = gbm.load_library()
-    assert lib.gbm_version() == 200
+    assert lib.gbm_version() == 210
     assert isinstance(_lib.last_error(), str)
     for s in _lib.EXPORTS:
         assert hasattr(lib, s)
@@ -103,3 +103,28 @@ def test_distributed_phase_entry_points_check_their_arguments():
     assert lib.gbm_dev_chol_area_pack(G, gdim, n, 0, 3, 0, 2, ctypes.c_void_p(1 << 23), None) == E
     assert lib.gbm_dev_chol_area_doubles(n, 0, 4, 2) == 1 * 256 * 128  # ⌈2 tiles / 2 ranks⌉ x 256 rows x 128
     assert lib.gbm_dev_chol_strip_unpack_rows(G, gdim, n, 0, 2, 3, 2, ctypes.c_void_p(1 << 23), None) == E
+
+
+def test_grm_mode_is_checked_before_device_use():
+    """grm_mode (include/gbm.h GBM_GRM_*) is a per-call argument: an unknown mode, or exact on int8 dosages of
+    another ploidy, is an argument error before any device work; the Python mirror maps names to modes."""
+    X = np.asfortranarray(np.random.default_rng(0).random((20, 30)))
+    y = np.arange(20.0)
+    b, yp = np.zeros(31), np.zeros(20)
+    lib = gbm.load_library()
+    assert lib.gbm_gblup_fit_ex(_lib.ptr(X), 20, 30, 20, _lib.ptr(y), 20, 1, 1.0, None, 0, 7, _lib.ptr(b),
+                                _lib.ptr(yp), None, None, None) == _lib.GBM_E_ARG
+    assert "grm_mode" in _lib.last_error()
+    with pytest.raises(gbm.ArgumentError, match="grm must be"):
+        gbm.gblup_arrays(X, np.arange(20.0), grm="int8")
+    D = np.random.default_rng(1).integers(0, 5, (20, 30)).astype(np.int8)
+    with pytest.raises(gbm.ArgumentError, match="ploidy 2"):
+        gbm.gblup_dosage(D, 4, np.arange(20.0), grm="exact")
+    assert _lib.grm_mode(None) == -1 and _lib.grm_mode("auto") == 2 and _lib.grm_mode("exact") == 1
+
+
+def test_rccl_call_counters_start_at_zero():
+    import ctypes
+    a, g = ctypes.c_int64(-1), ctypes.c_int64(-1)
+    assert gbm.load_library().gbm_debug_rccl_calls(ctypes.byref(a), ctypes.byref(g)) == 0
+    assert a.value >= 0 and g.value >= 0

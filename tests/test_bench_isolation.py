@@ -15,5 +15,9 @@ def test_isolated_leg_returns_result():
 
 
 def test_isolated_leg_survives_a_crash():
+    bench._CRASHES.clear()
     out = bench.run_isolated(ctypes.string_at, 0, timeout_s=60)  # SIGSEGV in the child
     assert "error" in out and "exit code" in out["error"]
+    assert out["crash"]["signal"] == "SIGSEGV" and out["crash"]["exit_code"] < 0
+    assert bench._CRASHES and bench._CRASHES[-1]["leg"] == "string_at"  # the line marks the run failed
+    bench._CRASHES.clear()

@@ -27,15 +27,20 @@ def weights(D):
     return t, w, keep
 
 
+def digit_max(S):
+    """The largest integer S balanced base-128 digits in [-64, 63] represent: 63 (128^S - 1) / 127."""
+    return 63 * (128 ** S - 1) // 127
+
+
 def choose(w):
     """xg_choose: (S, F, exact)."""
     kept = w[w > 0]
     emin = min(math.frexp(x)[1] - 1 for x in kept)  # ilogb
     wmax = float(kept.max())
     F = 52 - emin
-    W = math.ldexp(wmax, F)
+    W = int(Fraction(wmax) * 2 ** F)  # exact: the largest weight on the 2^-F grid
     for S in (8, 9, 10):
-        if W <= 63.0 * (2.0 ** (7 * S) - 1.0) / 127.0 * (1.0 - 1e-12):
+        if W <= digit_max(S):
             return S, F, True
     S = 10
     return S, 7 * S - 3 - (math.frexp(wmax)[1] - 1), False
@@ -163,3 +168,33 @@ def test_u_limbs():
                 limbs[l] += dd * ((v >> (24 * l)) & 0xFFFFFF)
         assert max(limbs) < 2 ** 31
         assert sum(x << (24 * l) for l, x in enumerate(limbs)) == sum(v * dd for v, dd in zip(V, d))
+
+
+def test_digit_count_at_the_range_boundary_matches_exact_integers():
+    """xg_choose (csrc/grm_exact.hip, via the host-only gbm_debug_xg_choose) picks S by an exact integer
+    comparison of W_max = w_max 2^F with 63 (128^S - 1)/127: weights at, just below and just above each boundary
+    (where the former 1e-12 double slack could round the wrong way) get the S the Python integers give, and W_max
+    then fits S balanced digits."""
+    import ctypes
+
+    import gbm
+    lib = gbm.load_library()
+    for S in (8, 9):
+        F = 52  # wmin = 1.0: emin = 0
+        for target in (digit_max(S), digit_max(S) - 1, digit_max(S) + 1, digit_max(S) - 2 ** 5):
+            w0 = float(Fraction(target, 2 ** F))
+            for wmax in (np.nextafter(w0, 0.0), w0, np.nextafter(w0, np.inf)):
+                Sc, Fc = ctypes.c_int(0), ctypes.c_int(0)
+                ex = lib.gbm_debug_xg_choose(1.0, float(wmax), ctypes.byref(Sc), ctypes.byref(Fc))
+                W = int(Fraction(float(wmax)) * 2 ** F)
+                want = next(s for s in (8, 9, 10) if W <= digit_max(s))
+                assert ex == 1 and Fc.value == F and Sc.value == want, (S, target, wmax, Sc.value, want)
+                assert W <= digit_max(Sc.value)
+                # the balanced digits of W rebuild it within S digits (the device kernel's loop)
+                x, digits = W, []
+                for _ in range(Sc.value):
+                    r = x & 127
+                    r = r - 128 if r >= 64 else r
+                    digits.append(r)
+                    x = (x - r) >> 7
+                assert x == 0 and sum(d * 128 ** k for k, d in enumerate(digits)) == W

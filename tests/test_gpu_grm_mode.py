@@ -1,0 +1,159 @@
+"""The GRM arithmetic as a per-call argument of the drop-in boundary (include/gbm.h GBM_GRM_*, the _ex entries;
+Julia `gblup(...; grm = :auto)`). The reference hands gblup the allele-frequency matrix of extractxyetc
+(src/prediction.jl:129); for diploids those are dosages/2, and `auto` must route such X to the exact-integer GRM
+(csrc/grm_exact.hip) and every other X to the fp64-MFMA SYRK — both against the oracle (src/gwas.jl:112-126,
+591-597 restated in oracle/oracle.py). GBM_GRM only supplies the mode of calls that pass GBM_GRM_DEFAULT."""
+import numpy as np
+import pytest
+
+import gbm
+import oracle
+from gbm.types import Genomes, Phenomes
+
+pytestmark = pytest.mark.gpu
+
+TOL_Y, TOL_B = 1e-9, 1e-6
+
+
+def rel(a, b):
+    return float(np.abs(np.asarray(a) - np.asarray(b)).max() / np.abs(np.asarray(b)).max())
+
+
+def check(out, ref):
+    b, y, mu, q = out
+    assert q == ref["q"] and rel(y, ref["y_pred"]) < TOL_Y and rel(mu, ref["mu"]) < TOL_Y
+    assert rel(b, ref["b_hat"]) < TOL_B
+
+
+@pytest.fixture(scope="module")
+def dosage_case():
+    n, p = 777, 2345
+    X = oracle.synth_genotypes(31, n, p)  # dosage / 2
+    Y = oracle.synth_phenotypes(X, 32, ntraits=2)
+    return X, Y, oracle.gblup_fit(X, Y, 1.0)
+
+
+def test_auto_routes_dosage_x_to_exact(dosage_case):
+    X, Y, ref = dosage_case
+    info = {}
+    out = gbm.gblup_arrays(X, Y, grm="auto", info=info)
+    assert info["grm_used"] == "exact"
+    check(out, ref)
+    info_e = {}
+    ex = gbm.gblup_arrays(X, Y, grm="exact", info=info_e)
+    assert info_e["grm_used"] == "exact"
+    for a, b in zip(ex, out):
+        assert np.array_equal(np.asarray(a), np.asarray(b))
+    info_f = {}
+    fp = gbm.gblup_arrays(X, Y, grm="fp64", info=info_f)
+    assert info_f["grm_used"] == "fp64"
+    check(fp, ref)
+
+
+def test_auto_routes_other_x_to_fp64(dosage_case):
+    X, Y, _ = dosage_case
+    n, p = X.shape
+    cases = {
+        "frequencies": np.clip(X + np.random.default_rng(5).normal(0, 0.01, X.shape), 0, 1),  # imputed values
+        "tetraploid": np.rint(X * 4 * 0.75) / 4,  # dosages/4 with odd dosages: 2x = 0.5, 1.5 occur
+        "last_locus_only": X.copy(),  # dosage-valued except one cell of the last locus (after the first chunk)
+    }
+    cases["last_locus_only"][n // 2, p - 1] = 0.3
+    for name, Xc in cases.items():
+        ref = oracle.gblup_fit(Xc, Y, 1.0)
+        info = {}
+        out = gbm.gblup_arrays(Xc, Y, grm="auto", info=info)
+        assert info["grm_used"] == "fp64", name
+        check(out, ref)
+        with pytest.raises(gbm.ArgumentError, match="not diploid dosages"):
+            gbm.gblup_arrays(Xc, Y, grm="exact")
+
+
+def test_auto_multi_shard_and_reml(dosage_case):
+    X, Y, ref = dosage_case
+    info = {}
+    out = gbm.gblup_arrays(X, Y, grm="auto", devices=[0, 0, 0], info=info)
+    assert info["grm_used"] == "exact"
+    check(out, ref)
+    info = {}
+    b, y, mu, q, r = gbm.gblup_reml_arrays(X, Y[:, 0], grm="auto", info=info)
+    b2, y2, mu2, q2, r2 = gbm.gblup_reml_arrays(X, Y[:, 0], grm="fp64")
+    assert info["grm_used"] == "exact"
+    assert abs(r["lambda"][0] - r2["lambda"][0]) < 1e-6 * r2["lambda"][0] and rel(y, y2) < 1e-8
+
+
+def test_int8_and_synthetic_sources():
+    n, p = 640, 1500
+    X = oracle.synth_genotypes(41, n, p)
+    Y = oracle.synth_phenotypes(X, 42, ntraits=1)
+    ref = oracle.gblup_fit(X, Y, 1.0)
+    D = np.rint(2 * X).astype(np.int8)
+    info = {}
+    check(gbm.gblup_dosage(D, 2, Y, grm="auto", info=info), ref)
+    assert info["grm_used"] == "exact"
+    info = {}
+    check(gbm.gblup_synthetic(41, n, p, Y, grm="auto", info=info), ref)
+    assert info["grm_used"] == "exact"
+    # tetraploid bytes: auto keeps fp64, exact refuses before any device work
+    D4 = np.rint(4 * X * 0.75).astype(np.int8)
+    ref4 = oracle.gblup_fit(D4 / 4.0, Y, 1.0)
+    info = {}
+    check(gbm.gblup_dosage(D4, 4, Y, grm="auto", info=info), ref4)
+    assert info["grm_used"] == "fp64"
+    # a byte outside {0, 1, 2} at ploidy 2: auto falls back to fp64 (x = 1.5 is a valid frequency), exact refuses
+    Db = D.copy()
+    Db[3, p - 2] = 3
+    refb = oracle.gblup_fit(Db / 2.0, Y, 1.0)
+    info = {}
+    check(gbm.gblup_dosage(Db, 2, Y, grm="auto", info=info), refb)
+    assert info["grm_used"] == "fp64"
+    with pytest.raises(gbm.ArgumentError, match="outside"):
+        gbm.gblup_dosage(Db, 2, Y, grm="exact")
+
+
+def test_environment_only_supplies_the_default(dosage_case, monkeypatch):
+    X, Y, ref = dosage_case
+    monkeypatch.setenv("GBM_GRM", "exact")
+    info = {}
+    check(gbm.gblup_arrays(X, Y, grm="fp64", info=info), ref)
+    assert info["grm_used"] == "fp64"  # the argument wins
+    info = {}
+    check(gbm.gblup_arrays(X, Y, grm=None, info=info), ref)
+    assert info["grm_used"] == "exact"  # GBM_GRM_DEFAULT: the environment
+    monkeypatch.delenv("GBM_GRM")
+    info = {}
+    gbm.gblup_arrays(X, Y, grm=None, info=info)
+    assert info["grm_used"] == "fp64"
+
+
+def test_model_function_default_auto_and_sessions(dosage_case):
+    """The drop-in gblup (grm="auto" by default, Julia grm = :auto) records the GRM it used; a session of fp64
+    X checks once whether its genotypes are dosages/2 and builds exact training GRMs under auto."""
+    X, Y, _ = dosage_case
+    n, p = X.shape
+    genomes = Genomes(entries=[f"e{i}" for i in range(n)], populations=["pop"] * n,
+                      loci_alleles=[f"chr1\t{j}\tA|T\tA" for j in range(p)], allele_frequencies=X)
+    phenomes = Phenomes(entries=genomes.entries, populations=genomes.populations, traits=["t1"],
+                        phenotypes=Y[:, :1].copy())
+    fit = gbm.gblup(genomes=genomes, phenomes=phenomes)
+    assert fit.grm_used == "exact"
+    fit64 = gbm.gblup(genomes=genomes, phenomes=phenomes, grm="fp64")
+    assert fit64.grm_used == "fp64" and rel(fit.y_pred, fit64.y_pred) < 1e-9
+    from gbm.session import GenotypeSession
+    idx = np.arange(0, n, 2)
+    ref = oracle.gblup_fit(np.asfortranarray(X[idx]), Y[idx], 1.0)
+    with GenotypeSession(X) as s:
+        s.set_grm("auto")
+        check(s.gblup(idx, Y[idx]), ref)
+        assert s.grm_used() == "exact"
+        s.set_grm("fp64")  # the cache is keyed by the GRM used: rebuilt in fp64
+        check(s.gblup(idx, Y[idx]), ref)
+        assert s.grm_used() == "fp64"
+    Xf = np.clip(X + 0.01, 0, 1)
+    with GenotypeSession(Xf) as s:
+        s.set_grm("auto")
+        s.gblup(idx, Y[idx])
+        assert s.grm_used() == "fp64"
+        s.set_grm("exact")
+        with pytest.raises(gbm.ArgumentError, match="not diploid dosages"):
+            s.gblup(idx, Y[idx])

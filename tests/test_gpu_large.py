@@ -39,6 +39,40 @@ def _free():
     gbm.load_library().gbm_release_device_cache()
 
 
+# 64 rows of C3's G, spread over the whole range (first, last, tile edges, the ragged last tile)
+C3_ROWS = np.unique(np.r_[0, 1, 127, 128, 49999, 49872, np.linspace(0, 49999, 58).astype(np.int64)])[:64]
+_C3_FP64_ROWS = {}  # the streamed fp64 G's sample rows, for the exact-GRM comparison
+
+
+def grm_rows_reference(D, n, rows, ploidy=2, step=20000):
+    """Rows `rows` of G = Z Zᵀ (unscaled, as the GRM stage leaves it) computed independently of the product's
+    kernels: each block of loci expanded from the dosage bytes, standardised by torch (mean, std with ddof = 1,
+    keep std > eps and finite: src/gwas.jl:112-115,127-130) and multiplied by torch's fp64 GEMM (rocBLAS /
+    hipBLASLt), the blocks summed in locus order."""
+    import torch
+    p = D.shape[0]
+    idx = torch.as_tensor(rows, device=D.device)
+    acc = torch.zeros((len(rows), n), dtype=torch.float64, device=D.device)
+    eps = float(np.finfo(np.float64).eps)
+    for j in range(0, p, step):
+        x = D[j:j + step, :n].to(torch.float64) / ploidy
+        m = x.mean(1, keepdim=True)
+        sd = x.std(1, keepdim=True)
+        keep = (sd > eps) & torch.isfinite(sd)
+        z = torch.where(keep, (x - m) / torch.where(keep, sd, torch.ones_like(sd)), torch.zeros_like(x))
+        acc += z[:, idx].T @ z
+        del x, z
+    return acc
+
+
+def grm_rows_of(G, rows, n):
+    """Rows of the symmetric G from a GRM buffer whose upper triangle (column >= row) is valid."""
+    import torch
+    idx = torch.as_tensor(rows, device=G.device)
+    col = torch.arange(n, device=G.device)
+    return torch.where(col[None, :] >= idx[:, None], G[idx, :n], G[:n, idx].T)
+
+
 def test_c3_per_gpu_shape():
     import torch
     from gbm.sharded import HipShardStages, assemble_b_hat
@@ -123,6 +157,14 @@ def test_c3_full_size_one_gpu_streamed():
     t2 = time.perf_counter()
     q = int(st.q.item())
     assert q == p  # MAF >= 0.05 at n = 50 000: every locus polymorphic
+    # 64 rows of the 50 000 x 50 000 G against an independent evaluation (torch standardisation + rocBLAS GEMMs)
+    ref_rows = grm_rows_reference(st.D, n, C3_ROWS)
+    got_rows = grm_rows_of(st.G, C3_ROWS, n)
+    err = float((got_rows - ref_rows).abs().max() / ref_rows.abs().max())
+    print(f"\nC3 G rows vs torch fp64 GEMMs: max rel err {err:.2e}")
+    assert err < 1e-12
+    _C3_FP64_ROWS["rows"] = got_rows.cpu().numpy()
+    del ref_rows, got_rows
     G = st.G[:n, :n]
     diag = torch.diagonal(G).clone() / q
     assert abs(float(diag.mean()) - (n - 1) / n) < 1e-12
@@ -159,6 +201,51 @@ def test_c3_full_size_one_gpu_streamed():
     print(f"gbm_gblup_fit_synthetic at 50000 x 600000 on one GPU: {t6 - t5:.2f} s")
     _free()
     assert q2 == q and rel(y2[:, 0], y_pred) < 1e-12 and rel(b2, b_hat) < 1e-10
+
+
+def test_c3_full_size_exact_grm_rows():
+    """C3 at full size through the exact-integer GRM (csrc/grm_exact.hip on the 30 GB of resident dosages, the
+    path `bench.py --individuals 50000 --loci 600000 --grm exact` times): 64 rows of G against the independent
+    torch/rocBLAS evaluation and against the fp64 streamed GRM of the test above (same rows); diag mean
+    (n − 1)/n. Then the exact fit's GEBVs against the fp64 C-ABI fit of the same problem."""
+    import torch
+    from gbm.sharded import HipExactShardStages
+
+    n, p, lam, seed = 50000, 600000, 1.0, 424242
+    _free()
+    st = HipExactShardStages(n, p, nrhs=1, lambda_=lam, device=0)
+    st.generate(seed, 0)
+    Y = synth.qtl_phenotypes(seed, n, p, 1, device=0)
+    st.load_phenotypes(Y)
+    t0 = time.perf_counter()
+    st.standardize()
+    st.grm_syrk()
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    q = int(st.q.item())
+    assert q == p
+    diag = torch.diagonal(st.G[:n, :n]) / q
+    assert abs(float(diag.mean()) - (n - 1) / n) < 1e-12
+    got = grm_rows_of(st.G, C3_ROWS, n)
+    ref = grm_rows_reference(st.D, n, C3_ROWS)
+    err = float((got - ref).abs().max() / ref.abs().max())
+    print(f"\nC3 exact GRM {t1 - t0:.2f} s ({int(st.slices.value)} digit slices); rows vs torch fp64 GEMMs: {err:.2e}")
+    assert err < 1e-12
+    if "rows" in _C3_FP64_ROWS:
+        g64 = _C3_FP64_ROWS["rows"]
+        err64 = float(np.abs(got.cpu().numpy() - g64).max() / np.abs(g64).max())
+        print(f"C3 exact vs fp64 streamed GRM rows: {err64:.2e}")
+        assert err64 < 1e-12
+    del got, ref
+    st.solve()
+    st.effects()
+    out = st.download()
+    y_exact = out["y_pred"][:, 0].copy()
+    del st
+    _free()
+    b2, y2, mu2, q2 = gbm.gblup_synthetic(seed, n, p, Y, lambda_=lam, devices=[0], grm="fp64")
+    _free()
+    assert q2 == q and rel(y_exact, y2[:, 0]) < 1e-9
 
 
 def test_c5_fold_full_size():

@@ -224,5 +224,5 @@ def test_cabi_reml_fit_matches_session_reml_and_oracle(data, devices):
     # the model function takes the same route
     g = gbm.Genomes([f"e{i}" for i in idx], ["p"] * idx.size, [f"l{j}" for j in range(X.shape[1])], Xs)
     ph = gbm.Phenomes(g.entries, g.populations, ["t1"], Ys[:, :1])
-    f1 = gbm.gblup(genomes=g, phenomes=ph, lambda_="reml", devices=devices)
+    f1 = gbm.gblup(genomes=g, phenomes=ph, lambda_="reml", devices=devices, grm=None)  # the same GRM mode as r
     assert f1.metrics_reml["lambda"] == r["lambda"][0] and np.array_equal(f1.y_pred, yp[:, 0])
