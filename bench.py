@@ -673,10 +673,8 @@ def main():
             "achieved": tops, "peak": PEAK_I8_TOPS, "unit": "TOPS (int8)", "frac": tops / PEAK_I8_TOPS,
             "frac_of_measured_i8_loop": tops / MEASURED_I8_LOOP_TOPS, "measured_i8_loop": MEASURED_I8_LOOP_TOPS,
             "traffic": None, "ops_per_launch": ops, "ms_per_launch": syrk_ms,
-            "fp64_equivalent_tflops": achieved,
         }
         rec["e2e_fp64_frac_of_peak"] = None
-        rec["fp64_equivalent_e2e_tflops"] = (grm_flops + chol_flops + solve_flops) / (ms_per_step / 1000.0) / 1e12
     if world == 1 and not args.no_host_path and not args.stream_chunk and float(n) * p_local <= 2e9:
         rec["host_path"] = host_path(args, torch)
         rec["stage_ms"]["h2d_x_pinned"] = rec["host_path"]["h2d_x_ms_pinned"]
