@@ -36,6 +36,9 @@
 // Schur block are read only by later kernels: plain stores.
 #include <atomic>
 #include <cstdlib>
+#include <map>
+#include <mutex>
+#include <vector>
 
 #include "chol_device.h"
 
@@ -413,51 +416,17 @@ __device__ __forceinline__ int factor_block_pipe(double* X, const double* X2, bo
   return bm ? (int)__builtin_ctzll(bm) : -1;
 }
 
-// task t -> tile (i, j): row-major over the upper tile triangle, except that
-//  - row r's first two slots hold its right neighbour (r, r + 1) and the NEXT row's diagonal tile
-//    (r + 1, r + 1), the partials the chain's step r waits for (dequeued before any tile of row r
-//    that waits for that step); (−1, −1) = nothing to do (slot (nb − 1, nb)); A_00 needs no task;
-//  - round 4: the right neighbour of row r ≥ 2 is dequeued two rows early, in row r − 2 right after
-//    (r − 2, r + 1). Its k-loop stops at k = r − 2 (the assistant adds k = r − 1), so everything it
-//    waits for is dequeued before it; the extra head start lets its ≈ r steps (latency-bound, one
-//    workgroup) finish before the assistant needs them.
-__device__ __forceinline__ void orig_slot_tile(int r, int slot, int nb, int& i, int& j) {
-  i = r;
-  j = r + slot;
-  if (j == i) {
-    if (i < nb) j = i + 1;  // the right neighbour; slot (nb, nb) stays the Schur block
-  } else if (j == i + 1) {
-    if (i + 1 < nb) {
-      i = i + 1;  // the next row's diagonal tile
-      j = i;
-    } else {
-      i = j = -1;
-    }
-  }
-}
-__device__ __forceinline__ void task_tile(int t, int nbc, int& i, int& j) {
-  const int nb = nbc - 1;
-  auto start0 = [nbc](int r) { return r * nbc - r * (r - 1) / 2; };
-  auto start = [&](int r) {
-    const int lost = (r < nb ? r : nb) - 2, got = r < nb - 2 ? r : nb - 2;
-    return start0(r) - (lost > 0 ? lost : 0) + (got > 0 ? got : 0);
-  };
-  const double b = 2.0 * nbc + 1.0;
-  int r = (int)((b - sqrt(b * b - 8.0 * (double)t)) * 0.5);
-  if (r < 0) r = 0;
-  if (r > nb) r = nb;
-  while (r > 0 && start(r) > t) r--;
-  while (r + 1 <= nb && start(r + 1) <= t) r++;
-  const int s = t - start(r);
-  const int ins = r + 2 <= nb - 1 ? (r <= 1 ? 4 : 3) : 1 << 30;  // row r + 2's neighbour, after (r, r + 3)
-  if (s == ins) {
-    i = r + 2;
-    j = r + 3;
-    return;
-  }
-  const int moved = (r >= 2 && r <= nb - 1) ? 1 : 0;  // this row's own neighbour went two rows up
-  orig_slot_tile(r, s - (s > ins ? 1 : 0) + moved, nb, i, j);
-}
+// The workers' dequeue order (a table t -> (i, j) built on the host, flow_order below): row-major over the
+// upper tile triangle, except that the tiles the chain's step i waits for come early —
+//  - the right neighbour (r, r + 1) of row r >= 2 is dequeued in row r − 2, right after (r − 2, r + 1) (round 4):
+//    its k-loop stops at k = r − 2 (the assistant adds k = r − 1), so everything it waits for comes before it;
+//  - the diagonal partial (d, d) of row d >= 2 is dequeued in row d − 2, right after (d − 2, d), its last
+//    operand (round 5; round 4 dequeued it in row d − 1): its k-loop (k < d − 1, d − 1 steps of ≈ 2.4 µs on
+//    one workgroup) then starts a chain step earlier — in the middle third of the C2 factorisation it used to
+//    reach the chain's LDS 5–10 µs after the step needed it (profiles/r05_chol_flow_per_step.txt);
+//  - row 0 starts with (0, 1) and (1, 1); the Schur block (nb, nb) is last. A_00 needs no task.
+// Every task follows all the tasks it waits for, and the chain's step i waits only for tasks of rows < i, so the
+// launch completes with the chain, the assistant and ONE resident worker (flow_order_check on the host).
 
 // kTrace: per-task timestamps (s_memrealtime, 100 MHz) into trace[t * 24 ...] for the timeline tool;
 // the chain workgroup's steps at trace[(ntasks + i) * 24 ...]
@@ -484,7 +453,7 @@ template <bool kTrace>
 __global__ void __launch_bounds__(256, 1)
 chol_flow_kernel(double* __restrict__ G, int64_t ld, int nbc, double* __restrict__ Ld, double* __restrict__ Dinv,
                  int32_t* __restrict__ queue, int32_t* __restrict__ flags, int32_t* __restrict__ info,
-                 int64_t* __restrict__ trace) {
+                 const int32_t* __restrict__ order, int xn_defer, int64_t* __restrict__ trace) {
   // ≈ 130 KB: one workgroup per CU (the chain's serial steps then share no SIMD with other tiles)
   __shared__ __attribute__((aligned(16))) double X[FT * PS];
   __shared__ __attribute__((aligned(16))) double X2[FT * PS];
@@ -496,7 +465,8 @@ chol_flow_kernel(double* __restrict__ G, int64_t ld, int nbc, double* __restrict
   const int wr = wave >> 1, wc = wave & 1;
   const int fr = lane >> 4, fc = lane & 15;
   const int nb = nbc - 1;  // diagonal tiles with a factor; tile (nb, nb) is the Schur block
-  const int ntasks = nbc * (nbc + 1) / 2;
+  const int ntasks = nbc * (nbc + 1) / 2;  // trace records (one more than the tasks: A_00 has none)
+  const int nwork = ntasks - 1;             // worker tasks (flow_order)
   const int64_t gbytes_rowblk = (int64_t)FT * ld * 8;
   const __amdgpu_buffer_rsrc_t rLd = rsrc(Ld, (int64_t)nb * FT * CNB * 8);
   const __amdgpu_buffer_rsrc_t rDi = rsrc(Dinv, (int64_t)nb * FT * 16 * 8);
@@ -593,9 +563,18 @@ chol_flow_kernel(double* __restrict__ G, int64_t ld, int nbc, double* __restrict
           lds_post(&sy.x2, i + 1, lane);
           if (kTrace && lane == 0) sy.th[0] = (int64_t)__builtin_amdgcn_s_memrealtime();
         }
+        // wave 1 fetches the next diagonal partial (needed at the step's end) now if it is there, else after
+        // its neighbour items, so that a late partial does not hold up the neighbour solve
+        const int32_t* fxn = flags + (int64_t)(i + 1) * nbc + i + 1;
+        bool xn_late = false;
         if (w == 1 && next_diag) {
-          fetch_tile(Xn, j0, flags + (int64_t)(i + 1) * nbc + i + 1, kPartial, []() {});
-          if (kTrace && lane == 0) sy.th[1] = (int64_t)__builtin_amdgcn_s_memrealtime();
+          int rdy = 0;
+          if (lane == 0) rdy = flag_at_least(fxn, kPartial) ? 1 : 0;
+          xn_late = xn_defer && __builtin_amdgcn_readfirstlane(rdy) == 0;
+          if (!xn_late) {
+            fetch_tile(Xn, j0, fxn, kPartial, []() {});
+            if (kTrace && lane == 0) sy.th[1] = (int64_t)__builtin_amdgcn_s_memrealtime();
+          }
         }
         if (w <= 2) {
           // column blocks: wave 0 takes 0 and 3, waves 1 and 2 their own; a column's block rows run in
@@ -610,6 +589,10 @@ chol_flow_kernel(double* __restrict__ G, int64_t ld, int nbc, double* __restrict
             if (w == 0) nbr_item(rb, 3);
           }
           if (kTrace && lane == 0) sy.th[2 + w] = (int64_t)__builtin_amdgcn_s_memrealtime();
+        }
+        if (xn_late) {
+          fetch_tile(Xn, j0, fxn, kPartial, []() {});
+          if (kTrace && lane == 0) sy.th[1] = (int64_t)__builtin_amdgcn_s_memrealtime();
         }
       };
       // ---- U_ii = chol(A_ii) -> Ld, its 16x16 diagonal inverses -> Dinv (and Dl)
@@ -756,18 +739,12 @@ chol_flow_kernel(double* __restrict__ G, int64_t ld, int nbc, double* __restrict
     // no new task once a wait has timed out (info = −1): the launch drains instead of computing on
     // tiles that will never be final
     if (tid == 0)
-      s_task = __hip_atomic_load(info, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < 0 ? ntasks : atomicAdd(queue, 1);
+      s_task = __hip_atomic_load(info, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < 0 ? nwork : atomicAdd(queue, 1);
     __syncthreads();
     const int t = __builtin_amdgcn_readfirstlane(s_task);
-    if (t >= ntasks) return;
-    int i, j;
-    task_tile(t, nbc, i, j);
-    i = __builtin_amdgcn_readfirstlane(i);
-    j = __builtin_amdgcn_readfirstlane(j);
-    if (i < 0) {
-      __syncthreads();  // every wave has read s_task before it is rewritten
-      continue;
-    }
+    if (t >= nwork) return;
+    const int32_t ij = __builtin_amdgcn_readfirstlane(order[t]);
+    const int i = ij >> 16, j = ij & 0xffff;
     const bool diag = i == j;
     const bool nbr = j == i + 1;
     // the chain waits for the diagonal tiles and right neighbours, which wait for the (i, i + 2) tiles
@@ -989,6 +966,92 @@ int64_t g_trace_cap = 0, g_trace_n = 0;
 
 }  // namespace
 
+// The workers' dequeue order (see above the kernel): (i << 16) | j per task, nbc (nbc + 1)/2 − 1 tasks.
+// variant 4 (GBM_CHOL_FLOW_ORDER=4, A/B timing only): round 4's order, the diagonal partial (d, d) in row d − 1
+std::vector<int32_t> flow_order(int nbc, int variant) {
+  const int nb = nbc - 1;
+  std::vector<int32_t> o;
+  o.reserve((size_t)nbc * (nbc + 1) / 2);
+  auto add = [&](int i, int j) { o.push_back((i << 16) | j); };
+  const bool r4 = variant == 4;
+  for (int r = 0; r <= nb; r++) {
+    if (r == 0 && nb >= 1) {
+      add(0, 1);
+      if (nb > 1) add(1, 1);
+    }
+    if (r == 1 && nb >= 2) add(1, 2);
+    if (r4 && r >= 1 && r + 1 < nb) add(r + 1, r + 1);
+    for (int j = r + 2; j < nbc; j++) {
+      add(r, j);
+      if (!r4 && j == r + 2 && r + 2 <= nb - 1) add(r + 2, r + 2);  // the diagonal partial two rows early
+      if (j == r + 3 && r + 3 <= nb) add(r + 2, r + 3);             // the right neighbour two rows early
+    }
+    if (r == nb) add(nb, nb);  // the Schur block
+  }
+  return o;
+}
+
+std::vector<int32_t> flow_order(int nbc) { return flow_order(nbc, 5); }
+
+// 0 when `order` is a valid dequeue order for nbc: every tile (i, j), i <= j <= nb, except (0, 0) exactly once, and
+// every task after the tasks it waits for (its k-loop operands (k, i), (k, j) for k < its last step, and for
+// the chain's step i (the tiles (i, j > i + 1) and every tile whose operands need it) after the chain's inputs of
+// steps <= i: (s, s + 1), (s + 1, s + 1), and the assistant's (s − 1, s + 1)); else the first failing position + 1.
+int64_t flow_order_check(int nbc, const int32_t* order, int64_t m) {
+  const int nb = nbc - 1;
+  if (m != (int64_t)nbc * (nbc + 1) / 2 - 1) return 1;
+  std::vector<int64_t> pos((size_t)nbc * nbc, -1);
+  for (int64_t t = 0; t < m; t++) {
+    const int i = order[t] >> 16, j = order[t] & 0xffff;
+    if (i < 0 || j < i || j > nb || (i == 0 && j == 0) || pos[(size_t)i * nbc + j] >= 0) return t + 1;
+    pos[(size_t)i * nbc + j] = t;
+  }
+  auto at = [&](int i, int j) { return pos[(size_t)i * nbc + j]; };
+  // the latest task the chain's step s (and the assistant's step s) needs
+  std::vector<int64_t> chain_need(nbc, -1);
+  for (int s = 0; s < nb; s++) {
+    int64_t need = s > 0 ? chain_need[s - 1] : -1;
+    need = std::max(need, at(s, s + 1));
+    if (s + 1 < nb) need = std::max(need, at(s + 1, s + 1));
+    if (s >= 1) need = std::max(need, at(s - 1, s + 1));
+    chain_need[s] = need;
+  }
+  for (int64_t t = 0; t < m; t++) {
+    const int i = order[t] >> 16, j = order[t] & 0xffff;
+    const bool diag = i == j, nbr = j == i + 1;
+    const int kend = ((diag && i < nb) || (nbr && i >= 1)) ? i - 1 : i;
+    for (int k = 0; k < kend; k++)
+      if (at(k, i) > t || at(k, j) > t || chain_need[k] > t) return t + 1;  // operands U_ki, U_kj (final after step k)
+    if (!diag && !nbr && chain_need[i] > t) return t + 1;  // the solve waits for the chain's step i
+  }
+  return 0;
+}
+
+namespace {
+
+// device copy of flow_order(nbc), built once per (device, nbc) and kept (a few KB)
+int flow_order_dev(int nbc, const int32_t** out) {
+  static std::mutex mu;
+  static auto* cache = new std::map<std::pair<int, int>, int32_t*>;  // never freed
+  int dev = 0;
+  GBM_HIP_TRY(hipGetDevice(&dev));
+  const char* ev = getenv("GBM_CHOL_FLOW_ORDER");
+  const int variant = ev && atoi(ev) == 4 ? 4 : 5;
+  std::lock_guard<std::mutex> lock(mu);
+  auto it = cache->find({dev, nbc * 8 + variant});
+  if (it == cache->end()) {
+    const std::vector<int32_t> o = flow_order(nbc, variant);
+    int32_t* d = nullptr;
+    GBM_HIP_TRY(hipMalloc((void**)&d, o.size() * sizeof(int32_t)));
+    GBM_HIP_TRY(hipMemcpy(d, o.data(), o.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+    it = cache->emplace(std::make_pair(dev, nbc * 8 + variant), d).first;
+  }
+  *out = it->second;
+  return GBM_OK;
+}
+
+}  // namespace
+
 // bytes of the flag block (queue word padded to 16 B + one int32 flag per tile), a multiple of 16
 int64_t chol_flow_flag_bytes(int64_t gdim) {
   const int64_t nbc = gdim / FT;
@@ -1007,8 +1070,10 @@ int launch_chol_flow(double* G, int64_t ldg, int64_t gdim, double* Ld, double* D
                      hipStream_t s) {
   const int64_t nbc = gdim / FT;
   const int64_t ntasks = nbc * (nbc + 1) / 2;
-  if (nbc < 2 || (int64_t)FT * ldg * 8 > 0x7fffffff || nbc * nbc > 0x3fffffff)
+  if (nbc < 2 || (int64_t)FT * ldg * 8 > 0x7fffffff || nbc * nbc > 0x3fffffff || nbc > 0x7fff)
     return fail(GBM_E_ARG, "dataflow Cholesky: matrix too large for 32-bit buffer offsets");
+  const int32_t* order = nullptr;
+  GBM_TRY(flow_order_dev((int)nbc, &order));
   GBM_HIP_TRY(hipMemsetAsync(flag_block, 0, (size_t)chol_flow_flag_bytes(gdim), s));
   // GBM_TEST_CHOL_FLOW_ABORT (tests): start as if a wait had already timed out (info = −1), so the
   // early exit of the chain and the workers runs; the solve then fails loudly, without a hang
@@ -1019,8 +1084,10 @@ int launch_chol_flow(double* G, int64_t ldg, int64_t gdim, double* Ld, double* D
   const char* ew = getenv("GBM_CHOL_FLOW_WGS");
   const int64_t workers = ew && atoll(ew) > 0 ? atoll(ew) : flow_cus() - 2;
   // + the chain and the assistant
-  const unsigned grid = (unsigned)(2 + (ntasks < workers ? ntasks : (workers < 1 ? 1 : workers)));
+  const unsigned grid = (unsigned)(2 + (ntasks - 1 < workers ? ntasks - 1 : (workers < 1 ? 1 : workers)));
   int32_t* q = (int32_t*)flag_block;
+  const char* ex = getenv("GBM_CHOL_FLOW_XN");  // 0: wave 1 always fetches the next diagonal partial first (A/B)
+  const int xn_defer = ex && atoi(ex) == 0 ? 0 : 1;
   if (getenv("GBM_CHOL_FLOW_TRACE")) {
     // timing tool only: one record of 16 int64 per task, read back by gbm_debug_chol_flow_trace
     const int64_t nrec = ntasks + nbc;  // the workers' tasks, then the chain's steps
@@ -1032,9 +1099,12 @@ int launch_chol_flow(double* G, int64_t ldg, int64_t gdim, double* Ld, double* D
     }
     GBM_HIP_TRY(hipMemsetAsync(g_trace, 0, (size_t)nrec * 192, s));
     g_trace_n = nrec;
-    chol_flow_kernel<true><<<grid, 256, 0, s>>>(G, ldg, (int)nbc, Ld, Dinv, q, q + 4, info, g_trace);
+    if (getenv("GBM_CHOL_FLOW_TRACE_PLAIN"))  // (debug) the untraced kernel with the trace buffer set up
+      chol_flow_kernel<false><<<grid, 256, 0, s>>>(G, ldg, (int)nbc, Ld, Dinv, q, q + 4, info, order, xn_defer, nullptr);
+    else
+    chol_flow_kernel<true><<<grid, 256, 0, s>>>(G, ldg, (int)nbc, Ld, Dinv, q, q + 4, info, order, xn_defer, g_trace);
   } else {
-    chol_flow_kernel<false><<<grid, 256, 0, s>>>(G, ldg, (int)nbc, Ld, Dinv, q, q + 4, info, nullptr);
+    chol_flow_kernel<false><<<grid, 256, 0, s>>>(G, ldg, (int)nbc, Ld, Dinv, q, q + 4, info, order, xn_defer, nullptr);
   }
   GBM_LAUNCH_CHECK();
   return GBM_OK;
@@ -1052,4 +1122,19 @@ extern "C" int64_t gbm_debug_chol_flow_trace(int64_t* host, int64_t cap) {
   if (hipDeviceSynchronize() != hipSuccess || hipMemcpy(host, g_trace, (size_t)n * 192, hipMemcpyDeviceToHost) != hipSuccess)
     return -1;
   return n;
+}
+
+// Host check of the dataflow factorisation's dequeue order (no device work): 0 when valid for nbc tiles per
+// side, else the first failing task position + 1; the order (nbc (nbc + 1)/2 − 1 entries of (i << 16) | j) is
+// copied to order_out when it is not NULL and cap is large enough.
+extern "C" int64_t gbm_debug_chol_flow_order(int nbc, int32_t* order_out, int64_t cap) {
+  if (nbc < 2 || nbc > 0x7fff) return -1;
+  const std::vector<int32_t> o = gbm::flow_order(nbc);
+  if (order_out && cap >= (int64_t)o.size()) std::copy(o.begin(), o.end(), order_out);
+  return gbm::flow_order_check(nbc, o.data(), (int64_t)o.size());
+}
+
+extern "C" int64_t gbm_debug_chol_flow_order_check(int nbc, const int32_t* order, int64_t m) {
+  if (nbc < 2 || nbc > 0x7fff || !order) return -1;
+  return gbm::flow_order_check(nbc, order, m);
 }

@@ -501,6 +501,13 @@ int64_t gbm_debug_brr_trace(int64_t* host, int64_t cap);
 /* With GBM_CHOL_FLOW_TRACE=1 set for a solve: copies up to cap records of 24 int64 (tile, workgroup,
  * 100 MHz timestamps) of the last dataflow factorisation into host; returns the record count. */
 int64_t gbm_debug_chol_flow_trace(int64_t* host, int64_t cap);
+/* The dataflow factorisation's worker dequeue order for nbc 64-tiles per side (host only, no device work):
+ * returns 0 when every task follows the tasks it waits for (so the launch completes with ONE worker), else the
+ * first failing position + 1 (−1 for a bad nbc); copies the nbc (nbc + 1)/2 − 1 entries (i << 16) | j to
+ * order_out when cap allows. */
+int64_t gbm_debug_chol_flow_order(int nbc, int32_t* order_out, int64_t cap);
+/* The same check of a caller's order (m entries). */
+int64_t gbm_debug_chol_flow_order_check(int nbc, const int32_t* order, int64_t m);
 /* Successful RCCL collectives libgbm has issued (partial-GRM all-reduces; Cholesky strip all-gathers). With
  * GBM_FORCE_RCCL=1 set for a call, a fit with one device leader still runs them on a 1-rank communicator
  * (the all-gathers from n >= GBM_DIST_SOLVE_MIN_N), bit-identical to the call without: the RCCL path on a

@@ -128,3 +128,52 @@ def test_rccl_call_counters_start_at_zero():
     a, g = ctypes.c_int64(-1), ctypes.c_int64(-1)
     assert gbm.load_library().gbm_debug_rccl_calls(ctypes.byref(a), ctypes.byref(g)) == 0
     assert a.value >= 0 and g.value >= 0
+
+
+def test_chol_flow_dequeue_order_is_complete_and_deadlock_free():
+    """The dataflow Cholesky's worker dequeue order (csrc/chol_flow.hip flow_order, host-built): every upper
+    64-tile except (0, 0) once, each task after everything it waits for (k-loop operands and the chain's inputs),
+    checked on the host for every tile count the dataflow path runs (npad <= 12 288: nbc <= 193); the diagonal
+    partial (d, d) follows (d − 2, d) directly (two rows early)."""
+    import ctypes
+    lib = gbm.load_library()
+    for nbc in range(2, 194):
+        m = nbc * (nbc + 1) // 2 - 1
+        buf = (ctypes.c_int32 * m)()
+        assert lib.gbm_debug_chol_flow_order(nbc, buf, m) == 0, nbc
+        order = [(v >> 16, v & 0xFFFF) for v in buf]
+        assert len(set(order)) == m
+        pos = {ij: t for t, ij in enumerate(order)}
+        for d in range(2, nbc - 2):
+            assert pos[(d, d)] == pos[(d - 2, d)] + 1
+    assert lib.gbm_debug_chol_flow_order(1, None, 0) == -1
+    # the checker itself: a diagonal partial moved in front of its last operand, a tile in front of the chain's
+    # input of its row, and a missing tile are caught; plain row-major order with the partials first is valid
+    nbc = 20
+    m = nbc * (nbc + 1) // 2 - 1
+    buf = (ctypes.c_int32 * m)()
+    lib.gbm_debug_chol_flow_order(nbc, buf, m)
+    order = list(buf)
+
+    def check(o):
+        arr = (ctypes.c_int32 * len(o))(*o)
+        return lib.gbm_debug_chol_flow_order_check(nbc, arr, len(o))
+
+    assert check(order) == 0
+    enc = lambda i, j: (i << 16) | j
+    bad = order.copy()
+    t = bad.index(enc(7, 7))
+    bad[t], bad[t - 1] = bad[t - 1], bad[t]  # (7, 7) before (5, 7)
+    assert check(bad) == t
+    bad = order.copy()
+    a, b = bad.index(enc(6, 7)), bad.index(enc(6, 9))  # the chain's step-6 input after a tile waiting for step 6
+    bad[a], bad[b] = bad[b], bad[a]
+    assert check(bad) != 0
+    assert check(order[:-1]) != 0
+    rowmajor = [enc(0, 1), enc(1, 1)]
+    for r in range(nbc):
+        if r >= 1 and r + 1 <= nbc - 1:
+            rowmajor += [enc(r, r + 1)] + ([enc(r + 1, r + 1)] if r + 1 < nbc - 1 else [])
+        rowmajor += [enc(r, j) for j in range(r + 2, nbc)]
+    rowmajor.append(enc(nbc - 1, nbc - 1))
+    assert check(rowmajor) == 0

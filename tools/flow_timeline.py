@@ -20,10 +20,13 @@ st.standardize()
 st.grm_syrk()
 st.grm_reduce()
 G0 = st.G.clone()
-for _ in range(3):
+torch.cuda.synchronize()
+print("GRM done", file=sys.stderr, flush=True)
+for r in range(3):
     st.G.copy_(G0)
     st.solve()
-torch.cuda.synchronize()
+    torch.cuda.synchronize()
+    print(f"traced solve {r} done, info={int(st.info.item())}", file=sys.stderr, flush=True)
 lib = st.lib
 lib.gbm_debug_chol_flow_trace.restype = ctypes.c_int64
 lib.gbm_debug_chol_flow_trace.argtypes = [ctypes.c_void_p, ctypes.c_int64]
