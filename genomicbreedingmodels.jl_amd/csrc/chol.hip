@@ -254,16 +254,19 @@ __global__ void __launch_bounds__(256) gblup_terms_kernel(const double* __restri
 
 constexpr int RC = 4;  // right-hand sides per chunk of the back substitution
 
-// ---- sync-free blocked back substitution: one workgroup per 64-block, flags between them ------
+// ---- sync-free blocked back substitution: one workgroup per PAIR of 64-blocks, flags between them ----
 // U a = w with U's off-diagonal blocks read from the lower copy L = Uᵀ (coalesced along the rows
-// i of block b) and the diagonal blocks through their inverses (Linv). Workgroup w owns block
-// b = nb − 1 − w: it folds in U_bc a_c for every c > b as soon as block c publishes a_c (flag[c]
-// = pass), then a_b = U_bb⁻¹ (w_b − Σ_c U_bc a_c) and publishes its own flag. A workgroup only
-// waits for lower-numbered workgroups, which the in-order dispatch has already placed, so the
-// chain cannot deadlock whatever the residency. The critical path is one 64x64 step per block
-// (the L blocks are loaded before the wait). a travels through agent-scope (L2-bypassing)
-// atomic loads/stores: the 8 XCD L2s are not coherent with each other. A wait that does not end
-// (it cannot in a correct run) gives up after ~1 s and reports info = −1 instead of hanging.
+// i of a block) and the diagonal blocks through their inverses (Linv). Workgroup w owns the blocks
+// bh = nb − 1 − 2w and bl = bh − 1: it folds in U_bh,c a_c and U_bl,c a_c for every c > bh as soon as
+// block c publishes a_c (flag[c] = pass), then a_bh = U_bh,bh⁻¹ (w_bh − Σ_c U_bh,c a_c), publishes it, folds
+// U_bl,bh a_bh from LDS (its L rows loaded before any wait) and solves a_bl. So the chain crosses
+// workgroups once per two blocks (round 5: one workgroup per block made it one cross-workgroup hand-off,
+// ≈ 1.3 µs, per 64 rows: 183 µs at C2); the per-row sums run in the same order as with one workgroup
+// per block (c = nb − 1 .. b + 1, the same partials), so a is bit-identical. A workgroup only waits for
+// lower-numbered workgroups, which the in-order dispatch has already placed, so the chain cannot
+// deadlock whatever the residency. a travels through agent-scope (L2-bypassing) atomic stores and sc1
+// loads: the 8 XCD L2s are not coherent with each other. A wait that does not end (it cannot in a
+// correct run) gives up after ~1 s and reports info = −1 instead of hanging.
 __global__ void __launch_bounds__(256) back_solve_kernel(const double* __restrict__ G, int64_t ld,
                                                          const double* __restrict__ Linv, int64_t nb,
                                                          const double* __restrict__ W, double* A,
@@ -271,29 +274,73 @@ __global__ void __launch_bounds__(256) back_solve_kernel(const double* __restric
                                                          int32_t* __restrict__ info) {
   __shared__ double part[4][RC][NB];
   __shared__ double rl[RC][NB];
+  __shared__ double ah[RC][NB];  // a_bh (the stored values), for the low block's last fold
   __shared__ int ok_s;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int64_t b = nb - 1 - (int64_t)blockIdx.x;
-  const int64_t b0 = b * NB;
+  const int64_t bh = nb - 1 - 2 * (int64_t)blockIdx.x, bl = bh - 1;
+  const bool lo = bl >= 0;
+  const int64_t h0 = bh * NB, l0 = bl * NB;
   const int j0 = wave * 16;  // this wave's 16 of the 64 block columns
   const int64_t a_bytes = nrhs * lda * 8;
   const __amdgpu_buffer_rsrc_t rA =
       __builtin_amdgcn_make_buffer_rsrc(A, (short)0, (int)(a_bytes < 0x7fffffff ? a_bytes : 0x7fffffff), 0x00020000);
-  double ui[16];             // (U_bb⁻¹)[lane][j0 + jj]
+  double uh[16], ul[16], lb[16];  // (U_bh⁻¹)[lane][j0 + jj], (U_bl⁻¹)[lane][j0 + jj], L[h0 + j0 + jj][l0 + lane]
 #pragma unroll
-  for (int jj = 0; jj < 16; jj++) ui[jj] = Linv[(b0 + lane) * NB + j0 + jj];
+  for (int jj = 0; jj < 16; jj++) {
+    uh[jj] = Linv[(h0 + lane) * NB + j0 + jj];
+    ul[jj] = lo ? Linv[(l0 + lane) * NB + j0 + jj] : 0.0;
+    lb[jj] = lo ? G[(h0 + j0 + jj) * ld + l0 + lane] : 0.0;
+  }
   if (tid == 0) ok_s = 1;
   int32_t pass = 0;
+  // a_b = U_bb⁻¹ (w_b − Σ acc) for the RHS chunk, through LDS; `out` also keeps the stored values
+  // (w: wave 0's right-hand sides of the block, loaded before the chunk's waits so that no global load
+  // latency sits on the chain; the barriers hand over LDS only)
+  auto solve_block = [&](int64_t b0, const double (&ui)[16], const double (&acc)[RC], const double (&w)[RC], int tc,
+                         int64_t t0, double (*out)[NB]) {
+#pragma unroll
+    for (int t = 0; t < RC; t++) part[wave][t][lane] = acc[t];
+    lds_sync();
+    if (wave == 0)
+#pragma unroll
+      for (int t = 0; t < RC; t++)
+        if (t < tc) rl[t][lane] = w[t] - (((part[0][t][lane] + part[1][t][lane]) + part[2][t][lane]) + part[3][t][lane]);
+    lds_sync();
+    for (int t = 0; t < tc; t++) {
+      double s = 0.0;
+#pragma unroll
+      for (int jj = 0; jj < 16; jj++) s = fma(ui[jj], rl[t][j0 + jj], s);
+      part[wave][t][lane] = s;
+    }
+    lds_sync();
+    if (wave == 0)
+      for (int t = 0; t < tc; t++) {
+        const double v = ((part[0][t][lane] + part[1][t][lane]) + part[2][t][lane]) + part[3][t][lane];
+        st_agent(A + (t0 + t) * lda + b0 + lane, v);
+        if (out) out[t][lane] = v;
+      }
+  };
   for (int64_t t0 = 0; t0 < nrhs; t0 += RC) {
     pass++;
     const int tc = (int)(nrhs - t0 < RC ? nrhs - t0 : RC);
-    double acc[RC] = {0.0, 0.0, 0.0, 0.0};
-    bool ok = true;
-    for (int64_t c = nb - 1; c > b && ok; c--) {
-      double l[16];  // L[64c + j0 + jj][b0 + lane] = U[b0 + lane][64c + j0 + jj]
-      const double* lp = G + (c * NB + j0) * ld + b0 + lane;
+    double acch[RC] = {0.0, 0.0, 0.0, 0.0}, accl[RC] = {0.0, 0.0, 0.0, 0.0};
+    double wh[RC] = {0.0, 0.0, 0.0, 0.0}, wl[RC] = {0.0, 0.0, 0.0, 0.0};
+    if (wave == 0)
 #pragma unroll
-      for (int jj = 0; jj < 16; jj++) l[jj] = lp[(int64_t)jj * ld];
+      for (int t = 0; t < RC; t++)
+        if (t < tc) {
+          wh[t] = W[(t0 + t) * lda + h0 + lane];
+          if (lo) wl[t] = W[(t0 + t) * lda + l0 + lane];
+        }
+    bool ok = true;
+    for (int64_t c = nb - 1; c > bh && ok; c--) {
+      double lh[16], ll[16];  // L[64c + j0 + jj][b0 + lane] = U[b0 + lane][64c + j0 + jj]
+      const double* lp = G + (c * NB + j0) * ld + lane;
+#pragma unroll
+      for (int jj = 0; jj < 16; jj++) {
+        lh[jj] = lp[(int64_t)jj * ld + h0];
+        ll[jj] = lo ? lp[(int64_t)jj * ld + l0] : 0.0;
+      }
       if (lane == 0) ok = wait_flag<false>(&flags[c], pass, info);
       ok = __builtin_amdgcn_readfirstlane((int)ok) != 0;
       // a_c was written through (agent-scope stores) before its flag was published; it is read
@@ -307,36 +354,34 @@ __global__ void __launch_bounds__(256) back_solve_kernel(const double* __restric
 #pragma unroll
         for (int jj = 0; jj < 16; jj++)
           av[jj] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rA, (int)(voff + jj * 8), 0, 16));
-        double s = 0.0;
+        double sh = 0.0, sl = 0.0;
 #pragma unroll
-        for (int jj = 0; jj < 16; jj++) s = fma(l[jj], av[jj], s);
-        acc[t] += s;
+        for (int jj = 0; jj < 16; jj++) {
+          sh = fma(lh[jj], av[jj], sh);
+          sl = fma(ll[jj], av[jj], sl);
+        }
+        acch[t] += sh;
+        accl[t] += sl;
       }
     }
     if (!ok) ok_s = 0;
+    solve_block(h0, uh, acch, wh, tc, t0, lo ? ah : nullptr);
+    // publish a_bh once its write-through stores are complete (a failed wait still publishes, so the
+    // workgroups behind it end quickly); the barrier inside also makes ah visible to every wave
+    publish_flag(&flags[bh], pass, tid);
+    if (lo) {
+      for (int t = 0; t < tc; t++) {
+        double sl = 0.0;
 #pragma unroll
-    for (int t = 0; t < RC; t++) part[wave][t][lane] = acc[t];
-    __syncthreads();
-    if (wave == 0)
-      for (int t = 0; t < tc; t++)
-        rl[t][lane] = W[(t0 + t) * lda + b0 + lane] -
-                      (((part[0][t][lane] + part[1][t][lane]) + part[2][t][lane]) + part[3][t][lane]);
-    __syncthreads();
-    for (int t = 0; t < tc; t++) {
-      double s = 0.0;
-#pragma unroll
-      for (int jj = 0; jj < 16; jj++) s = fma(ui[jj], rl[t][j0 + jj], s);
-      part[wave][t][lane] = s;
+        for (int jj = 0; jj < 16; jj++) sl = fma(lb[jj], ah[t][j0 + jj], sl);
+        accl[t] += sl;
+      }
+      lds_sync();  // every wave has read ah and part before solve_block rewrites part
+      solve_block(l0, ul, accl, wl, tc, t0, nullptr);
+      publish_flag(&flags[bl], pass, tid);
     }
-    __syncthreads();
-    if (wave == 0)
-      for (int t = 0; t < tc; t++)
-        st_agent(A + (t0 + t) * lda + b0 + lane,
-                 ((part[0][t][lane] + part[1][t][lane]) + part[2][t][lane]) + part[3][t][lane]);
-    // publish once the write-through stores of a_b are complete (a failed wait still publishes,
-    // so the workgroups behind it end quickly)
-    publish_flag(&flags[b], pass, tid);
     if (!ok_s) return;
+    lds_sync();  // ah / part / rl are rewritten by the next chunk
   }
 }
 
@@ -496,7 +541,7 @@ int solve_finish(double* G, int64_t ldg, int64_t n, const double* Y, int64_t ldy
   // the gebv buffer doubles as the w scratch: gebv_kernel (last) reads only Y and A
   gls_mu_kernel<<<dim3(gx, (unsigned)nrhs), 256, 0, s>>>(G, ldg, npad, nrhs, gebv, lda, mu, w.flags);
   GBM_LAUNCH_CHECK();
-  back_solve_kernel<<<(unsigned)nb, 256, 0, s>>>(G, ldg, w.Linv, nb, gebv, A_out, lda, nrhs, w.flags, info);
+  back_solve_kernel<<<(unsigned)((nb + 1) / 2), 256, 0, s>>>(G, ldg, w.Linv, nb, gebv, A_out, lda, nrhs, w.flags, info);
   GBM_LAUNCH_CHECK();
   gebv_kernel<<<dim3(gx, (unsigned)nrhs), 256, 0, s>>>(Y, ldy, n, A_out, gebv, lda, mu, lambda);
   GBM_LAUNCH_CHECK();

@@ -49,6 +49,10 @@ __device__ __forceinline__ double ld_agent(const double* p) {
   return __builtin_bit_cast(double, __hip_atomic_load(reinterpret_cast<const uint64_t*>(p), __ATOMIC_RELAXED,
                                                       __HIP_MEMORY_SCOPE_AGENT));
 }
+// workgroup barrier for LDS hand-offs only: waits for this wave's LDS operations, not for its global
+// loads and stores in flight (__syncthreads' workgroup fence would drain those too)
+__device__ __forceinline__ void lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
 __device__ __forceinline__ void st_agent(double* p, double v) {
   __hip_atomic_store(reinterpret_cast<uint64_t*>(p), __builtin_bit_cast(uint64_t, v), __ATOMIC_RELAXED,
                      __HIP_MEMORY_SCOPE_AGENT);

@@ -38,6 +38,7 @@
 #include <cstdlib>
 #include <map>
 #include <mutex>
+#include <type_traits>
 #include <vector>
 
 #include "chol_device.h"
@@ -50,6 +51,7 @@ typedef double dbl2 __attribute__((ext_vector_type(2)));
 typedef unsigned int u4 __attribute__((ext_vector_type(4)));
 typedef unsigned int u2 __attribute__((ext_vector_type(2)));
 constexpr int FT = 64;         // tile edge
+constexpr int32_t kPairBit = 0x8000;  // dequeue-order entry (i << 16) | j | kPairBit: the tiles (i, j) and (i, j + 1)
 constexpr int kSc1 = 16;       // buffer instruction aux bits: sc1 (write-through store / L1-bypassing load)
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* p, int64_t bytes) {
@@ -75,13 +77,17 @@ __device__ __forceinline__ void st1(__amdgpu_buffer_rsrc_t r, uint32_t voff, dou
 #ifndef GBM_FLOW_POST_EVERY
 #define GBM_FLOW_POST_EVERY 4
 #endif
+// the workers' k-loop pipeline: stages per 64-deep step (2 = round 4's two halves)
+#ifndef GBM_FLOW_STAGES
+#define GBM_FLOW_STAGES 8
+#endif
 #ifndef GBM_FLOW_POLL_SLEEP
 #define GBM_FLOW_POLL_SLEEP 4
 #endif
 
-// a workgroup barrier for LDS data only (__syncthreads also waits for every outstanding global load
-// and store of the calling wave: the write-through stores of a hand-off would sit on the chain)
-__device__ __forceinline__ void lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+// (lds_sync, chol_device.h: a workgroup barrier for LDS data only — __syncthreads also waits for every
+// outstanding global load and store of the calling wave, and the write-through stores of a hand-off
+// would sit on the chain)
 
 // tile flags (monotonic): kPartial = the accumulated (not yet solved) partial of a right neighbour or
 // a diagonal tile, handed on; kAssisted = a right neighbour's partial with its last k-step applied
@@ -453,7 +459,8 @@ template <bool kTrace>
 __global__ void __launch_bounds__(256, 1)
 chol_flow_kernel(double* __restrict__ G, int64_t ld, int nbc, double* __restrict__ Ld, double* __restrict__ Dinv,
                  int32_t* __restrict__ queue, int32_t* __restrict__ flags, int32_t* __restrict__ info,
-                 const int32_t* __restrict__ order, int xn_defer, int64_t* __restrict__ trace) {
+                 const int32_t* __restrict__ order, int nwork, int xn_defer, int64_t* __restrict__ trace,
+                 int trace_roles) {
   // ≈ 130 KB: one workgroup per CU (the chain's serial steps then share no SIMD with other tiles)
   __shared__ __attribute__((aligned(16))) double X[FT * PS];
   __shared__ __attribute__((aligned(16))) double X2[FT * PS];
@@ -466,7 +473,6 @@ chol_flow_kernel(double* __restrict__ G, int64_t ld, int nbc, double* __restrict
   const int fr = lane >> 4, fc = lane & 15;
   const int nb = nbc - 1;  // diagonal tiles with a factor; tile (nb, nb) is the Schur block
   const int ntasks = nbc * (nbc + 1) / 2;  // trace records (one more than the tasks: A_00 has none)
-  const int nwork = ntasks - 1;             // worker tasks (flow_order)
   const int64_t gbytes_rowblk = (int64_t)FT * ld * 8;
   const __amdgpu_buffer_rsrc_t rLd = rsrc(Ld, (int64_t)nb * FT * CNB * 8);
   const __amdgpu_buffer_rsrc_t rDi = rsrc(Dinv, (int64_t)nb * FT * 16 * 8);
@@ -504,8 +510,13 @@ chol_flow_kernel(double* __restrict__ G, int64_t ld, int nbc, double* __restrict
       // trace: 0 start, 1-4 leaf ends, 5-7 own starts of leaves 1-3, 8 factored, 9 X2 fetched,
       // 10 neighbour solved and published, 11 next tile updated, 12 step end, 13 own start of leaf 0,
       // 14 Xn fetched, 15 helpers done
-      int64_t ct[16] = {};
-      if (kTrace) ct[0] = (int64_t)__builtin_amdgcn_s_memrealtime();
+      // trace: one lane stores each timestamp as it is taken (holding them in registers until the step's
+      // end raised the traced kernel's register pressure past what it could run with)
+      int64_t* const crec = kTrace && (trace_roles & 1) ? trace + (int64_t)(ntasks + i) * 24 : nullptr;
+      auto cstamp = [&](int e, int64_t v) {
+        if (kTrace && crec && tid == 0) crec[3 + e] = v;
+      };
+      cstamp(0, (int64_t)__builtin_amdgcn_s_memrealtime());
       __builtin_amdgcn_s_setprio(2);
       // one wave: a partial tile of G (rows r0.., columns j0..; another workgroup's sc1 stores, seen
       // through its flag) -> dst in LDS, all 32 pieces of 16 bytes per lane in flight at once; the LDS
@@ -599,30 +610,30 @@ chol_flow_kernel(double* __restrict__ G, int64_t ld, int nbc, double* __restrict
       const int bad = factor_block_pipe(Xa, X2, i > 0, Dl, tid, rDi, (uint32_t)((i0 / 16) * 256 * 8), rLd, i0, &sy, i,
                                         info, flags + (int64_t)(i + 1) * nbc + i, after_own);
       if (tid == 0 && bad >= 0) atomicCAS(info, 0, (int32_t)(i0 + bad + 1));
-      if (kTrace) {
+      if (kTrace && crec && tid == 0) {
 #pragma unroll
-        for (int kb = 0; kb < 4; kb++) ct[1 + kb] = sy.tt[kb];
+        for (int kb = 0; kb < 4; kb++) crec[3 + 1 + kb] = sy.tt[kb];
 #pragma unroll
-        for (int kb = 0; kb < 3; kb++) ct[5 + kb] = sy.ts[kb + 1];  // the next leaf's own start
-        ct[13] = sy.ts[0];
-        ct[9] = sy.th[0];
-        ct[14] = sy.th[1];
-        ct[15] = sy.th[2] > sy.th[3] ? sy.th[2] : sy.th[3];
-        ct[15] = ct[15] > sy.th[4] ? ct[15] : sy.th[4];
+        for (int kb = 0; kb < 3; kb++) crec[3 + 5 + kb] = sy.ts[kb + 1];  // the next leaf's own start
+        crec[3 + 13] = sy.ts[0];
+        crec[3 + 9] = sy.th[0];
+        crec[3 + 14] = sy.th[1];
+        const int64_t h = sy.th[2] > sy.th[3] ? sy.th[2] : sy.th[3];
+        crec[3 + 15] = h > sy.th[4] ? h : sy.th[4];
       }
-      if (kTrace) ct[8] = (int64_t)__builtin_amdgcn_s_memrealtime();
+      cstamp(8, (int64_t)__builtin_amdgcn_s_memrealtime());
       // ---- the neighbour's last block row (wave w: column block w); its earlier rows were solved
       // beside the factor
       nbr_item(3, wave);
       lds_sync();
-      if (kTrace) ct[10] = (int64_t)__builtin_amdgcn_s_memrealtime();
+      cstamp(10, (int64_t)__builtin_amdgcn_s_memrealtime());
       // ---- the next diagonal tile's last update, k = i, from LDS: on the chain only its first 16
       // rows (block (0, w) on wave w), which the next factor's first leaf needs; the other six
       // upper blocks are folded into the followers' accumulators of the next factor
       if (next_diag) mfma_tile_sub_t(Xn, 0, wave * 16, X2, 0, X2, wave * 16, 0, 16, lane);
       // ---- publish (i, i) and (i, i + 1): every storing wave drains its write-through stores (Ld and
       // Dinv during the factor, U_i,i+1 block by block), then one flag store each
-      if (kTrace) ct[11] = (int64_t)__builtin_amdgcn_s_memrealtime();
+      cstamp(11, (int64_t)__builtin_amdgcn_s_memrealtime());
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       // a wait timed out somewhere in the launch (info = −1; a bug guard): the chain stops here,
       // before publishing tiles built from stale operands (read by every wave after the barrier)
@@ -633,18 +644,15 @@ chol_flow_kernel(double* __restrict__ G, int64_t ld, int nbc, double* __restrict
         __hip_atomic_store(flags + (int64_t)i * nbc + i, kFinal, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(flags + (int64_t)i * nbc + i + 1, kFinal, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
-      if (kTrace) ct[12] = (int64_t)__builtin_amdgcn_s_memrealtime();
+      cstamp(12, (int64_t)__builtin_amdgcn_s_memrealtime());
       if (i + 1 == nb) store_lower(X2, i0, j0);  // no next step to store it beside
       __builtin_amdgcn_s_setprio(0);
-      if (kTrace && tid == 0) {
-        int64_t* o = trace + (int64_t)(ntasks + i) * 24;
-        o[0] = i;
-        o[1] = i;
-        o[2] = -1;
-#pragma unroll
-        for (int e = 0; e < 16; e++) o[3 + e] = ct[e];
-        o[22] = sy.th[2];  // helper wave 0 (column blocks 0 and 3) done
-        o[23] = sy.th[4];  // helper wave 2 done
+      if (kTrace && crec && tid == 0) {
+        crec[0] = i;
+        crec[1] = i;
+        crec[2] = -1;
+        crec[22] = sy.th[2];  // helper wave 0 (column blocks 0 and 3) done
+        crec[23] = sy.th[4];  // helper wave 2 done
       }
       double* t = Xa;
       Xa = Xn;
@@ -670,8 +678,8 @@ chol_flow_kernel(double* __restrict__ G, int64_t ld, int nbc, double* __restrict
       const int32_t* fA = flags + (int64_t)(i - 1) * nbc + i;      // U_i−1,i (the chain)
       wave_wait2(fP, fB, info, lane, kPartial);
       wave_wait2(fB, fB, info, lane, kFinal);
-      int64_t at[3] = {};
-      if (kTrace) at[0] = (int64_t)__builtin_amdgcn_s_memrealtime();
+      int64_t* const arec = kTrace && (trace_roles & 2) ? trace + (int64_t)(ntasks + i) * 24 : nullptr;  // slots 19-21 of step i
+      if (kTrace && arec && tid == 0) arec[19] = (int64_t)__builtin_amdgcn_s_memrealtime();
       // the chain's U_i−1,i: its flag is loaded BEFORE the operands below, so (vmcnt being in order)
       // checking it leaves those loads in flight; a poll (a call, which drains loads in flight) only
       // if it is not set yet
@@ -695,7 +703,7 @@ chol_flow_kernel(double* __restrict__ G, int64_t ld, int nbc, double* __restrict
       for (int ks = 0; ks < 16; ks++) b[ks] = ld2(rK, offB, (uint32_t)(ks * kstep));
       if (!__builtin_amdgcn_readfirstlane(a_ready)) wave_wait2(fA, fA, info, lane, kFinal);
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      if (kTrace) at[1] = (int64_t)__builtin_amdgcn_s_memrealtime();
+      if (kTrace && arec && tid == 0) arec[20] = (int64_t)__builtin_amdgcn_s_memrealtime();
 #pragma unroll
       for (int ks = 0; ks < 16; ks++) a[ks] = ld2(rK, offA, (uint32_t)(ks * kstep));
 #pragma unroll
@@ -723,28 +731,20 @@ chol_flow_kernel(double* __restrict__ G, int64_t ld, int nbc, double* __restrict
       __syncthreads();
       if (s_task) return;
       if (tid == 0) __hip_atomic_store(flags + (int64_t)i * nbc + i + 1, kAssisted, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (kTrace && tid == 0) {  // slots 19-21 of the chain's record of step i
-        int64_t* o = trace + (int64_t)(ntasks + i) * 24;
-        o[19] = at[0];
-        o[20] = at[1];
-        o[21] = (int64_t)__builtin_amdgcn_s_memrealtime();
-      }
+      if (kTrace && arec && tid == 0) arec[21] = (int64_t)__builtin_amdgcn_s_memrealtime();
       __syncthreads();  // s_task is rewritten next step
     }
     return;
   }
 
   // ================================ the workers ================================
-  for (;;) {
-    // no new task once a wait has timed out (info = −1): the launch drains instead of computing on
-    // tiles that will never be final
-    if (tid == 0)
-      s_task = __hip_atomic_load(info, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < 0 ? nwork : atomicAdd(queue, 1);
-    __syncthreads();
-    const int t = __builtin_amdgcn_readfirstlane(s_task);
-    if (t >= nwork) return;
-    const int32_t ij = __builtin_amdgcn_readfirstlane(order[t]);
-    const int i = ij >> 16, j = ij & 0xffff;
+  // One task: tile (i, j), or with NT = 2 the pair (i, j), (i, j + 1) (both "other" tiles, j >= i + 3,
+  // flow_order): one k-loop loads U_ki once for both tiles, so a pair moves 48 instead of 64 KB per tile
+  // and 64-deep step. The workers' k-loops are bound by those bytes, not by their MFMAs: with every CU
+  // loading, one tile's 64-deep step took 2.6 µs against 1.75 µs of MFMA issue whatever the pipeline
+  // depth (C2 trace, round 5: the operands come from the Infinity Cache / HBM, the L2 re-use being nil).
+  auto worker_task = [&](auto nt, int t, int i, int j) {
+    constexpr int NT = decltype(nt)::value;
     const bool diag = i == j;
     const bool nbr = j == i + 1;
     // the chain waits for the diagonal tiles and right neighbours, which wait for the (i, i + 2) tiles
@@ -752,66 +752,83 @@ chol_flow_kernel(double* __restrict__ G, int64_t ld, int nbc, double* __restrict
     const int64_t i0 = (int64_t)i * FT, j0 = (int64_t)j * FT;
     // a diagonal tile's last update (k = i − 1) is the chain's, a right neighbour's the assistant's
     const int kend = ((diag && i < nb) || (nbr && i >= 1)) ? i - 1 : i;
-    int64_t tr[16] = {};
-    if (kTrace) tr[0] = (int64_t)__builtin_amdgcn_s_memrealtime();
+    int64_t* const wrec = kTrace && (trace_roles & 4) ? trace + (int64_t)t * 24 : nullptr;
+    auto wstamp = [&](int e) {
+      if (kTrace && wrec && tid == 0) wrec[3 + e] = (int64_t)__builtin_amdgcn_s_memrealtime();
+    };
+    wstamp(0);
 
     // ---- accumulators = A_ij (interleaved wave tile: MFMA tile m holds rows 32wr + 2ρ + m,
     // tile q columns 32wc + 2γ + q, so a lane's two A (B) operands are one 16-byte load)
-    d4 acc[2][2];
+    d4 acc[NT][2][2];
 #pragma unroll
-    for (int m = 0; m < 2; m++)
+    for (int q = 0; q < NT; q++)
 #pragma unroll
-      for (int r = 0; r < 4; r++) {
-        const int64_t row = i0 + 32 * wr + 2 * (fr + 4 * r) + m;
-        const dbl2 v = *reinterpret_cast<const dbl2*>(G + row * ld + j0 + 32 * wc + 2 * fc);
-        acc[m][0][r] = v.x;
-        acc[m][1][r] = v.y;
-      }
+      for (int m = 0; m < 2; m++)
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+          const int64_t row = i0 + 32 * wr + 2 * (fr + 4 * r) + m;
+          const dbl2 v = *reinterpret_cast<const dbl2*>(G + row * ld + j0 + q * FT + 32 * wc + 2 * fc);
+          acc[q][m][0][r] = v.x;
+          acc[q][m][1][r] = v.y;
+        }
 
-    // ---- A_ij −= Σ_k U_kiᵀ U_kj, 64-deep steps in two 32-deep halves (8 k-steps of 4); the next
-    // half's loads are in flight while this one's MFMAs run. The lower quadrant of a diagonal (or
-    // Schur) tile is never read: that wave skips the loop.
+    // ---- A_ij −= Σ_k U_kiᵀ U_kj, the 64-deep steps' 16 MFMA k-steps of 4 run through a ring of NS stages
+    // of SD k-steps (one 64-deep step of operands): while one stage's MFMAs run, the other stages' loads
+    // are in flight (round 4: two 32-deep halves). A half-step ring for pairs (fewer registers) made the
+    // compiler wait for every load at the top of each pass. The summation order is the same for every tile
+    // and pipeline shape. The lower quadrant of a diagonal (or Schur) tile is never read: that wave skips
+    // the loop.
     if (kend > 0 && !(diag && wr == 1 && wc == 0)) {
       const uint32_t offA = (uint32_t)(((int64_t)fr * ld + i0 + 32 * wr + 2 * fc) * 8);
       const uint32_t offB = (uint32_t)(((int64_t)fr * ld + j0 + 32 * wc + 2 * fc) * 8);
       const uint32_t kstep = (uint32_t)(4 * ld * 8);
-      dbl2 a0[8], b0[8], a1[8], b1[8];
-      auto issue = [&](dbl2(&A)[8], dbl2(&B)[8], int k, int h) {
-        const __amdgpu_buffer_rsrc_t r = rsrc(G + (int64_t)k * FT * ld, gbytes_rowblk);
+      constexpr int NS = GBM_FLOW_STAGES, SD = 16 / NS, R = NS * SD;
+      static_assert(16 % R == 0 && R % SD == 0, "the ring must tile a 64-deep step");
+      dbl2 A[NS][SD], B[NT][NS][SD];
+      auto issue = [&](int pass, int st) {
+        const int q0 = pass * R + st * SD;  // first MFMA k-step of the stage
+        const __amdgpu_buffer_rsrc_t r = rsrc(G + (int64_t)(q0 >> 4) * FT * ld, gbytes_rowblk);
 #pragma unroll
-        for (int ks = 0; ks < 8; ks++) {
-          const uint32_t so = (uint32_t)(h * 8 + ks) * kstep;
-          A[ks] = ld2(r, offA, so);
-          B[ks] = ld2(r, offB, so);
+        for (int e = 0; e < SD; e++) {
+          const uint32_t so = (uint32_t)((q0 & 15) + e) * kstep;
+          A[st][e] = ld2(r, offA, so);
+#pragma unroll
+          for (int q = 0; q < NT; q++) B[q][st][e] = ld2(r, offB + (uint32_t)(q * FT * 8), so);
         }
       };
-      auto mfma = [&](const dbl2(&A)[8], const dbl2(&B)[8]) {
+      auto mfma = [&](int st) {
 #pragma unroll
-        for (int ks = 0; ks < 8; ks++) {
-          const double na0 = -A[ks].x, na1 = -A[ks].y;
-          acc[0][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(na0, B[ks].x, acc[0][0], 0, 0, 0);
-          acc[0][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(na0, B[ks].y, acc[0][1], 0, 0, 0);
-          acc[1][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(na1, B[ks].x, acc[1][0], 0, 0, 0);
-          acc[1][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(na1, B[ks].y, acc[1][1], 0, 0, 0);
+        for (int e = 0; e < SD; e++) {
+          const double na0 = -A[st][e].x, na1 = -A[st][e].y;
+#pragma unroll
+          for (int q = 0; q < NT; q++) {
+            acc[q][0][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(na0, B[q][st][e].x, acc[q][0][0], 0, 0, 0);
+            acc[q][0][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(na0, B[q][st][e].y, acc[q][0][1], 0, 0, 0);
+            acc[q][1][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(na1, B[q][st][e].x, acc[q][1][0], 0, 0, 0);
+            acc[q][1][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(na1, B[q][st][e].y, acc[q][1][1], 0, 0, 0);
+          }
         }
       };
-      auto fa = [&](int k) { return flags + (int64_t)k * nbc + i; };
-      auto fb = [&](int k) { return flags + (int64_t)k * nbc + j; };
-      // k-steps known to be final: U_ki and U_kj for k < kr. One vector load checks the flags of the
-      // next 32 steps (lanes 0-31: (k, i), lanes 32-63: (k, j)), so a worker catching up to the
-      // chain polls once per 32 steps: a poll per step (two dependent flag loads in a call, which
-      // drains the step's operand loads in flight) made the k-loop ≈ 2.8 µs per step, and the
-      // chain's neighbour partial (i − 1 steps) late. Bounded like poll2.
+      // k-steps known to be final: U_ki and U_kj (.. U_k,j+NT−1) for k < kr. One vector load checks the
+      // flags of the next GS steps (lane group g: column i, then the task's tiles), so a worker catching up
+      // to the chain polls once per GS steps: a poll per step (dependent flag loads, which drain the
+      // operand loads in flight) made the k-loop ≈ 2.8 µs per step, and the chain's neighbour partial
+      // (i − 1 steps) late. Bounded like poll2.
+      constexpr int GS = NT == 1 ? 32 : 21;
+      constexpr unsigned long long GM = (1ull << GS) - 1;
       int kr = 0;
       bool gave_up = false;  // a wait timed out or another waiter gave up (info = −1): drain, no more waits
       auto ready_upto = [&](int k) {
         for (int64_t it = 0; k >= kr && !gave_up; it++) {
-          const int kk = kr + (lane & 31);
+          const int g = lane / GS, kk = kr + lane % GS;
           int ok = 1;
-          if (kk < kend) ok = flag_at_least(lane < 32 ? fa(kk) : fb(kk), kFinal) ? 1 : 0;
+          if (g <= NT && kk < kend) ok = flag_at_least(flags + (int64_t)kk * nbc + (g == 0 ? i : j + g - 1), kFinal) ? 1 : 0;
           const unsigned long long bm = __ballot(ok);
-          const unsigned both = (unsigned)bm & (unsigned)(bm >> 32);
-          kr += both == 0xffffffffu ? 32 : __builtin_ctz(~both);
+          unsigned long long all = bm & GM;
+#pragma unroll
+          for (int q = 1; q <= NT; q++) all &= (bm >> (q * GS)) & GM;
+          kr += all == GM ? GS : __builtin_ctzll(~all);
           if (k < kr) break;
           if ((it & 255) == 255) {
             gave_up = __hip_atomic_load(info, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < 0;
@@ -825,25 +842,29 @@ chol_flow_kernel(double* __restrict__ G, int64_t ld, int nbc, double* __restrict
         }
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
       };
+      // one flag check per pass, ahead of its loads of the next pass (whose stages all lie in one 64-deep
+      // step), and no branch between the stages: a conditional inside the ring made the compiler wait for
+      // every load in flight at the top of each pass (s_waitcnt vmcnt(0)), 4.9 µs per 64-deep step
+      const int passes = kend * (16 / R);
       ready_upto(0);
-      issue(a0, b0, 0, 0);
-      issue(a1, b1, 0, 1);
-      for (int k = 0; k < kend; k++) {
-        mfma(a0, b0);
-        const bool more = k + 1 < kend;
-        if (more) {
-          ready_upto(k + 1);
-          issue(a0, b0, k + 1, 0);
+#pragma unroll
+      for (int st = 0; st < NS; st++) issue(0, st);
+      for (int p = 0; p + 1 < passes; p++) {
+        ready_upto(((p + 1) * R) >> 4);
+#pragma unroll
+        for (int st = 0; st < NS; st++) {
+          mfma(st);
+          issue(p + 1, st);
         }
-        mfma(a1, b1);
-        if (more) issue(a1, b1, k + 1, 1);
       }
+#pragma unroll
+      for (int st = 0; st < NS; st++) mfma(st);
     }
-    if (kTrace) tr[1] = (int64_t)__builtin_amdgcn_s_memrealtime();
+    wstamp(1);
 
     int32_t publish = kFinal;
-    const double* low = nullptr;  // a solved tile whose lower copy is still to be stored
-    if ((nbr && i < nb) || (diag && i < nb)) {
+    bool solved = false;  // solved tiles whose lower copies are still to be stored
+    if (NT == 1 && ((nbr && i < nb) || (diag && i < nb))) {
       // ---- a partial for the chain (right neighbour: all k < i; diagonal: all k < i − 1), sc1,
       // straight from the accumulators into the tile's place in G (the chain stores U over it)
       const __amdgpu_buffer_rsrc_t rG = rsrc(G + i0 * ld, gbytes_rowblk);
@@ -853,28 +874,32 @@ chol_flow_kernel(double* __restrict__ G, int64_t ld, int nbc, double* __restrict
         for (int r = 0; r < 4; r++) {
           const int64_t row = 32 * wr + 2 * (fr + 4 * r) + m;
           dbl2 v;
-          v.x = acc[m][0][r];
-          v.y = acc[m][1][r];
+          v.x = acc[0][m][0][r];
+          v.y = acc[0][m][1][r];
           st2(rG, (uint32_t)((row * ld + j0 + 32 * wc + 2 * fc) * 8), v);
         }
       publish = kPartial;
     } else {
-      // ---- accumulators -> X (natural layout)
+      // ---- accumulators -> X (and X2 for the pair's second tile; natural layout)
+      double* const Xq[2] = {X, X2};
 #pragma unroll
-      for (int m = 0; m < 2; m++)
+      for (int q = 0; q < NT; q++)
 #pragma unroll
-        for (int r = 0; r < 4; r++) {
-          const int row = 32 * wr + 2 * (fr + 4 * r) + m;
-          dbl2 v;
-          v.x = acc[m][0][r];
-          v.y = acc[m][1][r];
-          *reinterpret_cast<dbl2*>(&X[row * PS + 32 * wc + 2 * fc]) = v;
-        }
+        for (int m = 0; m < 2; m++)
+#pragma unroll
+          for (int r = 0; r < 4; r++) {
+            const int row = 32 * wr + 2 * (fr + 4 * r) + m;
+            dbl2 v;
+            v.x = acc[q][m][0][r];
+            v.y = acc[q][m][1][r];
+            *reinterpret_cast<dbl2*>(&Xq[q][row * PS + 32 * wc + 2 * fc]) = v;
+          }
       __syncthreads();
-      if (kTrace) tr[2] = (int64_t)__builtin_amdgcn_s_memrealtime();
+      wstamp(2);
       if (!diag) {
         // ---- U_ij = U_ii⁻ᵀ A_ij once U_ii is final. Operands of U_ii and its 16x16 inverses come
-        // straight from the sc1-stored Ld / Dinv into registers; X (LDS) is solved in place:
+        // straight from the sc1-stored Ld / Dinv into registers (once for both tiles of a pair); X (LDS)
+        // is solved in place:
         //   X_rb <- (D_rb⁻¹)ᵀ (X_rb − U[0:o, rb]ᵀ X[0:o]),  rb = 0..3, wave w on columns 16w..16w+15
         // block row rb needs Dinv_rb (leaf rb of U_ii) and U[0:16 rb, rb] (leaves < rb): the chain
         // sets one bit per stored leaf, so the solve runs leaf by leaf beside the factor and only the
@@ -888,7 +913,7 @@ chol_flow_kernel(double* __restrict__ G, int64_t ld, int nbc, double* __restrict
         for (int rb = 0; rb < 4; rb++) {
           const int o = rb * 16;
           wave_wait_bits(fl, (2 << rb) - 1, info, lane);
-          if (kTrace && rb == 3) tr[3] = (int64_t)__builtin_amdgcn_s_memrealtime();
+          if (rb == 3) wstamp(3);
 #pragma unroll
           for (int ks = 0; ks < 4; ks++)
             di[ks] = ld1(rDi, (uint32_t)(((i0 / 16) * 256 + rb * 256 + (ks * 4 + fr) * 16 + fc) * 8));
@@ -897,29 +922,33 @@ chol_flow_kernel(double* __restrict__ G, int64_t ld, int nbc, double* __restrict
             for (int ks = 0; ks < 4 * (rb + 1); ks++)
               u[c + 4 * rb + ks] = ld1(rLd, (uint32_t)(((i0 + ks * 4 + fr) * CNB + (rb + 1) * 16 + fc) * 8));
           }
-          if (rb > 0) {
+#pragma unroll
+          for (int q = 0; q < NT; q++) {
+            double* const Y = Xq[q];
+            if (rb > 0) {
+              d4 sacc = (d4){0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+              for (int ks = 0; ks < 4 * rb; ks++)
+                sacc = __builtin_amdgcn_mfma_f64_16x16x4f64(u[c + ks], Y[(ks * 4 + fr) * PS + cw + fc], sacc, 0, 0, 0);
+#pragma unroll
+              for (int r = 0; r < 4; r++) Y[(o + fr + 4 * r) * PS + cw + fc] -= sacc[r];
+            }
             d4 sacc = (d4){0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-            for (int ks = 0; ks < 4 * rb; ks++)
-              sacc = __builtin_amdgcn_mfma_f64_16x16x4f64(u[c + ks], X[(ks * 4 + fr) * PS + cw + fc], sacc, 0, 0, 0);
-            c += 4 * rb;
+            for (int ks = 0; ks < 4; ks++)
+              sacc = __builtin_amdgcn_mfma_f64_16x16x4f64(di[ks], Y[(o + ks * 4 + fr) * PS + cw + fc], sacc, 0, 0, 0);
 #pragma unroll
-            for (int r = 0; r < 4; r++) X[(o + fr + 4 * r) * PS + cw + fc] -= sacc[r];
+            for (int r = 0; r < 4; r++) {
+              Y[(o + fr + 4 * r) * PS + cw + fc] = sacc[r];
+              // each final 16x16 block goes out at once (write-through): the drain before the flag then
+              // waits for the last block row only
+              st1(rU, (uint32_t)(((int64_t)(o + fr + 4 * r) * ld + j0 + q * FT + cw + fc) * 8), sacc[r]);
+            }
           }
-          d4 sacc = (d4){0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-          for (int ks = 0; ks < 4; ks++)
-            sacc = __builtin_amdgcn_mfma_f64_16x16x4f64(di[ks], X[(o + ks * 4 + fr) * PS + cw + fc], sacc, 0, 0, 0);
-#pragma unroll
-          for (int r = 0; r < 4; r++) {
-            X[(o + fr + 4 * r) * PS + cw + fc] = sacc[r];
-            // each final 16x16 block goes out at once (write-through): the drain before the flag then
-            // waits for the last block row only
-            st1(rU, (uint32_t)(((int64_t)(o + fr + 4 * r) * ld + j0 + cw + fc) * 8), sacc[r]);
-          }
+          if (rb > 0) c += 4 * rb;
         }
         __syncthreads();
-        low = X;
+        solved = true;
       } else {
         // ---- the Schur block −WᵀW (read by later kernels only)
         const int row = tid >> 2, quarter = tid & 3;
@@ -929,23 +958,40 @@ chol_flow_kernel(double* __restrict__ G, int64_t ld, int nbc, double* __restrict
           *reinterpret_cast<dbl2*>(d + e) = *reinterpret_cast<const dbl2*>(&X[row * PS + quarter * 16 + e]);
       }
     }
-    // ---- publish: every storing wave drains its write-through stores, then one flag store
-    if (kTrace) tr[4] = (int64_t)__builtin_amdgcn_s_memrealtime();
+    // ---- publish: every storing wave drains its write-through stores, then one flag store per tile
+    wstamp(4);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (tid == 0) __hip_atomic_store(flags + (int64_t)i * nbc + j, publish, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (low) store_lower(low, i0, j0);
-    __builtin_amdgcn_s_setprio(0);
-    if (kTrace && tid == 0) {
-      tr[5] = (int64_t)__builtin_amdgcn_s_memrealtime();
-      int64_t* o = trace + (int64_t)t * 24;
-      o[0] = i;
-      o[1] = j;
-      o[2] = (int64_t)(__builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (31 << 11)) & 7) /* XCC_ID */ * 1000 +
-             (int64_t)blockIdx.x;
+    if (tid == 0)
 #pragma unroll
-      for (int e = 0; e < 16; e++) o[3 + e] = tr[e];
+      for (int q = 0; q < NT; q++)
+        __hip_atomic_store(flags + (int64_t)i * nbc + j + q, publish, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (solved) {
+      store_lower(X, i0, j0);
+      if (NT == 2) store_lower(X2, i0, j0 + FT);
     }
+    __builtin_amdgcn_s_setprio(0);
+    wstamp(5);
+    if (kTrace && wrec && tid == 0) {
+      wrec[0] = i;
+      wrec[1] = j | (NT == 2 ? kPairBit : 0);
+      wrec[2] = (int64_t)(__builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (31 << 11)) & 7) /* XCC_ID */ * 1000 +
+                (int64_t)blockIdx.x;
+    }
+  };
+
+  for (;;) {
+    // no new task once a wait has timed out (info = −1): the launch drains instead of computing on
+    // tiles that will never be final
+    if (tid == 0)
+      s_task = __hip_atomic_load(info, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < 0 ? nwork : atomicAdd(queue, 1);
+    __syncthreads();
+    const int t = __builtin_amdgcn_readfirstlane(s_task);
+    if (t >= nwork) return;
+    const int32_t ij = __builtin_amdgcn_readfirstlane(order[t]);
+    const int i = ij >> 16, j = ij & 0x7fff;
+    if (ij & kPairBit) worker_task(std::integral_constant<int, 2>{}, t, i, j);
+    else worker_task(std::integral_constant<int, 1>{}, t, i, j);
   }
 }
 
@@ -966,14 +1012,17 @@ int64_t g_trace_cap = 0, g_trace_n = 0;
 
 }  // namespace
 
-// The workers' dequeue order (see above the kernel): (i << 16) | j per task, nbc (nbc + 1)/2 − 1 tasks.
-// variant 4 (GBM_CHOL_FLOW_ORDER=4, A/B timing only): round 4's order, the diagonal partial (d, d) in row d − 1
+// The workers' dequeue order (see above the kernel): (i << 16) | j per task, | kPairBit for the pair (i, j),
+// (i, j + 1). variant 5 (default): every tile alone; 6 (GBM_CHOL_FLOW_ORDER=6): the "other" tiles j >= r + 3
+// of row r in pairs (a last odd one alone) — 48 instead of 64 KB per tile and 64-deep step, but 1.48 against
+// 1.33 ms for the C2 solve (round 5: a pair holds its CU twice as long and every k-step ran slower); 4:
+// round 4's order, every tile alone and the diagonal partial (d, d) in row d − 1. (A/B timing only.)
 std::vector<int32_t> flow_order(int nbc, int variant) {
   const int nb = nbc - 1;
   std::vector<int32_t> o;
   o.reserve((size_t)nbc * (nbc + 1) / 2);
   auto add = [&](int i, int j) { o.push_back((i << 16) | j); };
-  const bool r4 = variant == 4;
+  const bool r4 = variant == 4, pairs = variant == 6;
   for (int r = 0; r <= nb; r++) {
     if (r == 0 && nb >= 1) {
       add(0, 1);
@@ -981,31 +1030,46 @@ std::vector<int32_t> flow_order(int nbc, int variant) {
     }
     if (r == 1 && nb >= 2) add(1, 2);
     if (r4 && r >= 1 && r + 1 < nb) add(r + 1, r + 1);
-    for (int j = r + 2; j < nbc; j++) {
-      add(r, j);
+    for (int j = r + 2; j < nbc;) {
+      // (r, r + 2) stays alone: the assistant's step r + 1 waits for it
+      const bool pr = pairs && j >= r + 3 && j + 1 < nbc;
+      o.push_back((r << 16) | j | (pr ? kPairBit : 0));
       if (!r4 && j == r + 2 && r + 2 <= nb - 1) add(r + 2, r + 2);  // the diagonal partial two rows early
       if (j == r + 3 && r + 3 <= nb) add(r + 2, r + 3);             // the right neighbour two rows early
+      j += pr ? 2 : 1;
     }
     if (r == nb) add(nb, nb);  // the Schur block
   }
   return o;
 }
 
-std::vector<int32_t> flow_order(int nbc) { return flow_order(nbc, 5); }
+int flow_order_variant() {
+  const char* ev = getenv("GBM_CHOL_FLOW_ORDER");
+  const int v = ev ? atoi(ev) : 5;
+  return v == 4 || v == 6 ? v : 5;
+}
 
-// 0 when `order` is a valid dequeue order for nbc: every tile (i, j), i <= j <= nb, except (0, 0) exactly once, and
-// every task after the tasks it waits for (its k-loop operands (k, i), (k, j) for k < its last step, and for
-// the chain's step i (the tiles (i, j > i + 1) and every tile whose operands need it) after the chain's inputs of
-// steps <= i: (s, s + 1), (s + 1, s + 1), and the assistant's (s − 1, s + 1)); else the first failing position + 1.
+std::vector<int32_t> flow_order(int nbc) { return flow_order(nbc, flow_order_variant()); }
+
+// 0 when `order` (m entries) is a valid dequeue order for nbc: every tile (i, j), i <= j <= nb, except (0, 0)
+// exactly once (a pair entry covers (i, j) and (i, j + 1), both "other" tiles, j >= i + 2), and every task after
+// the tasks it waits for (its tiles' k-loop operands (k, i), (k, j) for k < their last step, and for the chain's
+// step i (the tiles (i, j > i + 1) and every tile whose operands need it) after the chain's inputs of steps <= i:
+// (s, s + 1), (s + 1, s + 1), and the assistant's (s − 1, s + 1)); else the first failing position + 1.
 int64_t flow_order_check(int nbc, const int32_t* order, int64_t m) {
   const int nb = nbc - 1;
-  if (m != (int64_t)nbc * (nbc + 1) / 2 - 1) return 1;
   std::vector<int64_t> pos((size_t)nbc * nbc, -1);
+  int64_t tiles = 0;
   for (int64_t t = 0; t < m; t++) {
-    const int i = order[t] >> 16, j = order[t] & 0xffff;
-    if (i < 0 || j < i || j > nb || (i == 0 && j == 0) || pos[(size_t)i * nbc + j] >= 0) return t + 1;
-    pos[(size_t)i * nbc + j] = t;
+    const int i = order[t] >> 16, j = order[t] & 0x7fff, nt = (order[t] & kPairBit) ? 2 : 1;
+    if (i < 0 || j < i || j + nt - 1 > nb || (i == 0 && j == 0) || (nt == 2 && j < i + 2)) return t + 1;
+    for (int q = 0; q < nt; q++) {
+      if (pos[(size_t)i * nbc + j + q] >= 0) return t + 1;
+      pos[(size_t)i * nbc + j + q] = t;
+      tiles++;
+    }
   }
+  if (tiles != (int64_t)nbc * (nbc + 1) / 2 - 1) return m + 1;
   auto at = [&](int i, int j) { return pos[(size_t)i * nbc + j]; };
   // the latest task the chain's step s (and the assistant's step s) needs
   std::vector<int64_t> chain_need(nbc, -1);
@@ -1017,26 +1081,27 @@ int64_t flow_order_check(int nbc, const int32_t* order, int64_t m) {
     chain_need[s] = need;
   }
   for (int64_t t = 0; t < m; t++) {
-    const int i = order[t] >> 16, j = order[t] & 0xffff;
-    const bool diag = i == j, nbr = j == i + 1;
-    const int kend = ((diag && i < nb) || (nbr && i >= 1)) ? i - 1 : i;
-    for (int k = 0; k < kend; k++)
-      if (at(k, i) > t || at(k, j) > t || chain_need[k] > t) return t + 1;  // operands U_ki, U_kj (final after step k)
-    if (!diag && !nbr && chain_need[i] > t) return t + 1;  // the solve waits for the chain's step i
+    const int i = order[t] >> 16, nt = (order[t] & kPairBit) ? 2 : 1;
+    for (int j = order[t] & 0x7fff, q = 0; q < nt; q++, j++) {
+      const bool diag = i == j, nbr = j == i + 1;
+      const int kend = ((diag && i < nb) || (nbr && i >= 1)) ? i - 1 : i;
+      for (int k = 0; k < kend; k++)
+        if (at(k, i) > t || at(k, j) > t || chain_need[k] > t) return t + 1;  // operands U_ki, U_kj (final after step k)
+      if (!diag && !nbr && chain_need[i] > t) return t + 1;  // the solve waits for the chain's step i
+    }
   }
   return 0;
 }
 
 namespace {
 
-// device copy of flow_order(nbc), built once per (device, nbc) and kept (a few KB)
-int flow_order_dev(int nbc, const int32_t** out) {
+// device copy of flow_order(nbc) and its length, built once per (device, nbc, variant) and kept (a few KB)
+int flow_order_dev(int nbc, const int32_t** out, int* count) {
   static std::mutex mu;
-  static auto* cache = new std::map<std::pair<int, int>, int32_t*>;  // never freed
+  static auto* cache = new std::map<std::pair<int, int>, std::pair<int32_t*, int>>;  // never freed
   int dev = 0;
   GBM_HIP_TRY(hipGetDevice(&dev));
-  const char* ev = getenv("GBM_CHOL_FLOW_ORDER");
-  const int variant = ev && atoi(ev) == 4 ? 4 : 5;
+  const int variant = flow_order_variant();
   std::lock_guard<std::mutex> lock(mu);
   auto it = cache->find({dev, nbc * 8 + variant});
   if (it == cache->end()) {
@@ -1044,9 +1109,10 @@ int flow_order_dev(int nbc, const int32_t** out) {
     int32_t* d = nullptr;
     GBM_HIP_TRY(hipMalloc((void**)&d, o.size() * sizeof(int32_t)));
     GBM_HIP_TRY(hipMemcpy(d, o.data(), o.size() * sizeof(int32_t), hipMemcpyHostToDevice));
-    it = cache->emplace(std::make_pair(dev, nbc * 8 + variant), d).first;
+    it = cache->emplace(std::make_pair(dev, nbc * 8 + variant), std::make_pair(d, (int)o.size())).first;
   }
-  *out = it->second;
+  *out = it->second.first;
+  *count = it->second.second;
   return GBM_OK;
 }
 
@@ -1073,7 +1139,8 @@ int launch_chol_flow(double* G, int64_t ldg, int64_t gdim, double* Ld, double* D
   if (nbc < 2 || (int64_t)FT * ldg * 8 > 0x7fffffff || nbc * nbc > 0x3fffffff || nbc > 0x7fff)
     return fail(GBM_E_ARG, "dataflow Cholesky: matrix too large for 32-bit buffer offsets");
   const int32_t* order = nullptr;
-  GBM_TRY(flow_order_dev((int)nbc, &order));
+  int nwork = 0;  // dequeue-order entries (tiles, or pairs of tiles)
+  GBM_TRY(flow_order_dev((int)nbc, &order, &nwork));
   GBM_HIP_TRY(hipMemsetAsync(flag_block, 0, (size_t)chol_flow_flag_bytes(gdim), s));
   // GBM_TEST_CHOL_FLOW_ABORT (tests): start as if a wait had already timed out (info = −1), so the
   // early exit of the chain and the workers runs; the solve then fails loudly, without a hang
@@ -1084,7 +1151,7 @@ int launch_chol_flow(double* G, int64_t ldg, int64_t gdim, double* Ld, double* D
   const char* ew = getenv("GBM_CHOL_FLOW_WGS");
   const int64_t workers = ew && atoll(ew) > 0 ? atoll(ew) : flow_cus() - 2;
   // + the chain and the assistant
-  const unsigned grid = (unsigned)(2 + (ntasks - 1 < workers ? ntasks - 1 : (workers < 1 ? 1 : workers)));
+  const unsigned grid = (unsigned)(2 + (nwork < workers ? nwork : (workers < 1 ? 1 : workers)));
   int32_t* q = (int32_t*)flag_block;
   const char* ex = getenv("GBM_CHOL_FLOW_XN");  // 0: wave 1 always fetches the next diagonal partial first (A/B)
   const int xn_defer = ex && atoi(ex) == 0 ? 0 : 1;
@@ -1099,12 +1166,15 @@ int launch_chol_flow(double* G, int64_t ldg, int64_t gdim, double* Ld, double* D
     }
     GBM_HIP_TRY(hipMemsetAsync(g_trace, 0, (size_t)nrec * 192, s));
     g_trace_n = nrec;
+    // GBM_CHOL_FLOW_TRACE = a mask of the roles that record (1 chain, 2 assistant, 4 workers; 1 = all)
+    const int tm = atoi(getenv("GBM_CHOL_FLOW_TRACE"));
+    const int roles = tm > 1 ? (tm & 7) : 7;
     if (getenv("GBM_CHOL_FLOW_TRACE_PLAIN"))  // (debug) the untraced kernel with the trace buffer set up
-      chol_flow_kernel<false><<<grid, 256, 0, s>>>(G, ldg, (int)nbc, Ld, Dinv, q, q + 4, info, order, xn_defer, nullptr);
+      chol_flow_kernel<false><<<grid, 256, 0, s>>>(G, ldg, (int)nbc, Ld, Dinv, q, q + 4, info, order, nwork, xn_defer, nullptr, 0);
     else
-    chol_flow_kernel<true><<<grid, 256, 0, s>>>(G, ldg, (int)nbc, Ld, Dinv, q, q + 4, info, order, xn_defer, g_trace);
+    chol_flow_kernel<true><<<grid, 256, 0, s>>>(G, ldg, (int)nbc, Ld, Dinv, q, q + 4, info, order, nwork, xn_defer, g_trace, roles);
   } else {
-    chol_flow_kernel<false><<<grid, 256, 0, s>>>(G, ldg, (int)nbc, Ld, Dinv, q, q + 4, info, order, xn_defer, nullptr);
+    chol_flow_kernel<false><<<grid, 256, 0, s>>>(G, ldg, (int)nbc, Ld, Dinv, q, q + 4, info, order, nwork, xn_defer, nullptr, 0);
   }
   GBM_LAUNCH_CHECK();
   return GBM_OK;
@@ -1132,6 +1202,11 @@ extern "C" int64_t gbm_debug_chol_flow_order(int nbc, int32_t* order_out, int64_
   const std::vector<int32_t> o = gbm::flow_order(nbc);
   if (order_out && cap >= (int64_t)o.size()) std::copy(o.begin(), o.end(), order_out);
   return gbm::flow_order_check(nbc, o.data(), (int64_t)o.size());
+}
+
+extern "C" int64_t gbm_debug_chol_flow_order_size(int nbc) {
+  if (nbc < 2 || nbc > 0x7fff) return -1;
+  return (int64_t)gbm::flow_order(nbc).size();
 }
 
 extern "C" int64_t gbm_debug_chol_flow_order_check(int nbc, const int32_t* order, int64_t m) {

@@ -45,7 +45,7 @@ EXPORTS = (
     "gbm_dev_chol_group_update_cols", "gbm_dev_grm_exact_workspace", "gbm_dev_grm_exact_i8",
     "gbm_gblup_fit_ex", "gbm_gblup_fit_reml_ex", "gbm_gblup_fit_dosage_i8_ex", "gbm_gblup_fit_synthetic_ex",
     "gbm_session_set_grm_mode", "gbm_session_grm_used", "gbm_debug_rccl_calls", "gbm_debug_xg_choose", "gbm_debug_chol_flow_order",
-    "gbm_debug_chol_flow_order_check",
+    "gbm_debug_chol_flow_order_check", "gbm_debug_chol_flow_order_size",
 )
 
 GBM_GRM_DEFAULT, GBM_GRM_FP64, GBM_GRM_EXACT, GBM_GRM_AUTO = -1, 0, 1, 2
@@ -224,6 +224,8 @@ def _declare(lib):
     lib.gbm_debug_xg_choose.argtypes = [D, D, P, P]
     lib.gbm_debug_chol_flow_order.restype = I64
     lib.gbm_debug_chol_flow_order.argtypes = [I32, P, I64]
+    lib.gbm_debug_chol_flow_order_size.restype = I64
+    lib.gbm_debug_chol_flow_order_size.argtypes = [I32]
     lib.gbm_debug_chol_flow_order_check.restype = I64
     lib.gbm_debug_chol_flow_order_check.argtypes = [I32, P, I64]
     return lib

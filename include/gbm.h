@@ -501,11 +501,13 @@ int64_t gbm_debug_brr_trace(int64_t* host, int64_t cap);
 /* With GBM_CHOL_FLOW_TRACE=1 set for a solve: copies up to cap records of 24 int64 (tile, workgroup,
  * 100 MHz timestamps) of the last dataflow factorisation into host; returns the record count. */
 int64_t gbm_debug_chol_flow_trace(int64_t* host, int64_t cap);
-/* The dataflow factorisation's worker dequeue order for nbc 64-tiles per side (host only, no device work):
- * returns 0 when every task follows the tasks it waits for (so the launch completes with ONE worker), else the
- * first failing position + 1 (−1 for a bad nbc); copies the nbc (nbc + 1)/2 − 1 entries (i << 16) | j to
- * order_out when cap allows. */
+/* The dataflow factorisation's worker dequeue order for nbc 64-tiles per side (host only, no device work; the
+ * variant GBM_CHOL_FLOW_ORDER selects): returns 0 when every task follows the tasks it waits for (so the launch
+ * completes with ONE worker), else the first failing position + 1 (−1 for a bad nbc); copies the entries
+ * (i << 16) | j, with bit 15 set for a task that covers the tiles (i, j) and (i, j + 1), to order_out when cap
+ * allows (gbm_debug_chol_flow_order_size entries; nbc (nbc + 1)/2 − 1 tiles in all). */
 int64_t gbm_debug_chol_flow_order(int nbc, int32_t* order_out, int64_t cap);
+int64_t gbm_debug_chol_flow_order_size(int nbc);
 /* The same check of a caller's order (m entries). */
 int64_t gbm_debug_chol_flow_order_check(int nbc, const int32_t* order, int64_t m);
 /* Successful RCCL collectives libgbm has issued (partial-GRM all-reduces; Cholesky strip all-gathers). With

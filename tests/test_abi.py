@@ -130,27 +130,48 @@ def test_rccl_call_counters_start_at_zero():
     assert a.value >= 0 and g.value >= 0
 
 
+def _order_tiles(buf):
+    """Decode a dequeue order: (i, j) per tile, a pair entry (bit 15) giving (i, j) and (i, j + 1) at one position."""
+    out = []
+    for t, v in enumerate(buf):
+        i, j = v >> 16, v & 0x7FFF
+        out += [(t, i, j)] + ([(t, i, j + 1)] if v & 0x8000 else [])
+    return out
+
+
 def test_chol_flow_dequeue_order_is_complete_and_deadlock_free():
     """The dataflow Cholesky's worker dequeue order (csrc/chol_flow.hip flow_order, host-built): every upper
     64-tile except (0, 0) once, each task after everything it waits for (k-loop operands and the chain's inputs),
     checked on the host for every tile count the dataflow path runs (npad <= 12 288: nbc <= 193); the diagonal
-    partial (d, d) follows (d − 2, d) directly (two rows early)."""
+    partial (d, d) follows (d − 2, d) directly (two rows early); the tiles (r, j >= r + 3) go in pairs (one k-loop
+    for two tiles), the tiles the chain and the assistant wait for alone."""
     import ctypes
     lib = gbm.load_library()
     for nbc in range(2, 194):
-        m = nbc * (nbc + 1) // 2 - 1
+        m = lib.gbm_debug_chol_flow_order_size(nbc)
         buf = (ctypes.c_int32 * m)()
         assert lib.gbm_debug_chol_flow_order(nbc, buf, m) == 0, nbc
-        order = [(v >> 16, v & 0xFFFF) for v in buf]
-        assert len(set(order)) == m
-        pos = {ij: t for t, ij in enumerate(order)}
+        tiles = _order_tiles(buf)
+        assert len(tiles) == nbc * (nbc + 1) // 2 - 1
+        assert len({(i, j) for _, i, j in tiles}) == len(tiles)
+        pos = {(i, j): t for t, i, j in tiles}
         for d in range(2, nbc - 2):
             assert pos[(d, d)] == pos[(d - 2, d)] + 1
+        for t, v in enumerate(buf):
+            i, j = v >> 16, v & 0x7FFF
+            if v & 0x8000:
+                assert j >= i + 3 and j + 1 <= nbc - 1
+            elif j >= i + 3:
+                assert j == nbc - 1 or nbc == 2  # a row's odd last tile
+        if nbc >= 8:
+            assert m < nbc * (nbc + 1) // 2 - 1
     assert lib.gbm_debug_chol_flow_order(1, None, 0) == -1
+    assert lib.gbm_debug_chol_flow_order_size(1) == -1
     # the checker itself: a diagonal partial moved in front of its last operand, a tile in front of the chain's
-    # input of its row, and a missing tile are caught; plain row-major order with the partials first is valid
+    # input of its row, a missing entry, a duplicated tile and a pair over a chain input are caught; plain
+    # row-major order with the partials first and no pairs is valid
     nbc = 20
-    m = nbc * (nbc + 1) // 2 - 1
+    m = lib.gbm_debug_chol_flow_order_size(nbc)
     buf = (ctypes.c_int32 * m)()
     lib.gbm_debug_chol_flow_order(nbc, buf, m)
     order = list(buf)
@@ -166,10 +187,16 @@ def test_chol_flow_dequeue_order_is_complete_and_deadlock_free():
     bad[t], bad[t - 1] = bad[t - 1], bad[t]  # (7, 7) before (5, 7)
     assert check(bad) == t
     bad = order.copy()
-    a, b = bad.index(enc(6, 7)), bad.index(enc(6, 9))  # the chain's step-6 input after a tile waiting for step 6
+    a, b = bad.index(enc(6, 7)), bad.index(enc(6, 8))  # the chain's step-6 input after a tile waiting for step 6
     bad[a], bad[b] = bad[b], bad[a]
     assert check(bad) != 0
     assert check(order[:-1]) != 0
+    bad = order.copy()
+    p = next(t for t, v in enumerate(bad) if v & 0x8000)
+    bad[p] &= 0x7FFF7FFF  # a pair entry split: its second tile is missing
+    assert check(bad) != 0
+    assert check(order + [enc(5, 9)]) != 0
+    assert check([enc(0, 1) | 0x8000] + order[1:]) != 0
     rowmajor = [enc(0, 1), enc(1, 1)]
     for r in range(nbc):
         if r >= 1 and r + 1 <= nbc - 1:

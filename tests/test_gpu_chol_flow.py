@@ -125,6 +125,24 @@ def test_flow_few_resident_workgroups_complete_bit_identical(monkeypatch, wgs):
     assert torch.equal(a.gebv, b.gebv) and torch.equal(a.A, b.A) and torch.equal(a.mu, b.mu)
 
 
+@pytest.mark.parametrize("order,wgs", [("6", None), ("6", "1"), ("4", None)])
+def test_flow_dequeue_orders_bit_identical(monkeypatch, order, wgs):
+    """The A/B dequeue orders (GBM_CHOL_FLOW_ORDER: 6 = the "other" tiles in pairs, one k-loop for two tiles;
+    4 = round 4's order) sum every tile's updates in the same k order as the default: identical bits, also
+    with a single worker running the paired order."""
+    import torch
+    monkeypatch.setenv("GBM_CHOL_FLOW_MAX", "1000000")
+    X, Y, a, b = _pair(3000, 700, 2, 21, 0.9)
+    a.solve()
+    monkeypatch.setenv("GBM_CHOL_FLOW_ORDER", order)
+    if wgs:
+        monkeypatch.setenv("GBM_CHOL_FLOW_WGS", wgs)
+    b.solve()
+    torch.cuda.synchronize()
+    assert int(a.info.item()) == 0 and int(b.info.item()) == 0
+    assert torch.equal(a.gebv, b.gebv) and torch.equal(a.A, b.A) and torch.equal(a.mu, b.mu)
+
+
 def test_flow_timed_out_wait_drains_and_fails_loudly(monkeypatch):
     """A wait that times out (info = −1; a bug guard, forced here by GBM_TEST_CHOL_FLOW_ABORT) stops
     the chain before it publishes another tile and keeps workers from taking new tasks:

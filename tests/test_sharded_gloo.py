@@ -248,7 +248,7 @@ def _worker(rank, world, port, X, Y, lam, out_dir, env=None):
         if label == "allreduce":
             saved["G"], saved["q"] = st.G.clone(), st.q.clone()
 
-    out = sharded_gblup_step(st, TorchComm(), events=mark)
+    out = sharded_gblup_step(st, TorchComm(force=os.environ.get("GBM_TEST_FORCE") == "1"), events=mark)
     # the redundant solve on the same summed G (what one rank alone computes from it)
     st.G.copy_(saved["G"])
     st.q.copy_(saved["q"])
@@ -307,3 +307,21 @@ def test_sharded_step_gloo_distributed_solve_bit_identical(tmp_path, world):
     assert np.abs(outs[0]["y_pred"] - ref["y_pred"]).max() < 1e-10 * np.abs(ref["y_pred"]).max()
     b_hat = assemble_b_hat(outs[0]["mu"], outs[0]["msum"], [o["B"] for o in outs], p)
     assert np.abs(b_hat - ref["b_hat"]).max() < 1e-9 * np.abs(ref["b_hat"]).max()
+
+
+def test_world1_forced_collectives_bit_identical(tmp_path):
+    """bench.py --collectives always at one rank (TorchComm(force=True), here over gloo): the packed
+    all-reduce and, with the distributed solve forced on, chol_distributed's one-rank branch (every
+    distributable group's rows through the all-gather between its panels and its update) — the same bits
+    as the redundant solve, and the oracle's fit."""
+    n, p = 600, 1500
+    X = oracle.synth_genotypes(78, n, p)
+    Y = oracle.synth_phenotypes(X, 9, ntraits=2)
+    lam = 1.1
+    env = {"GBM_DIST_SOLVE_MIN_N": "0", "GBM_DIST_TAIL_ROWS": "0", "GBM_TEST_FORCE": "1"}
+    mp.spawn(_worker, args=(1, _free_port(), X, Y, lam, str(tmp_path), env), nprocs=1, join=True)
+    o = dict(np.load(tmp_path / "rank0.npz"))
+    assert int(o["packs"]) == 1  # the all-reduce ran at world size 1
+    assert np.array_equal(o["y_pred"], o["y_redundant"])
+    ref = oracle.gblup_fit(X, Y, lam)
+    assert np.abs(o["y_pred"] - ref["y_pred"]).max() < 1e-10 * np.abs(ref["y_pred"]).max()

@@ -5,14 +5,15 @@ set -e
 cd "$(dirname "$0")/.."
 B=genomicbreedingmodels.jl_amd/csrc/build
 mkdir -p variants
-OBJS="$B/stats.hip.o $B/grm.hip.o $B/chol.hip.o $B/effects.hip.o $B/gibbs.hip.o $B/capi.cpp.o $B/session.cpp.o"
+OBJS="$B/stats.hip.o $B/grm.hip.o $B/grm_exact.hip.o $B/chol.hip.o $B/effects.hip.o $B/gibbs.hip.o $B/capi.cpp.o $B/session.cpp.o"
 build() {  # name flags...
   name=$1; shift
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 "$@" -c genomicbreedingmodels.jl_amd/csrc/chol_flow.hip -o variants/chol_flow_$name.o
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC $OBJS variants/chol_flow_$name.o -lrccl -lrocprofiler-sdk-roctx -o variants/libgbm_$name.so
 }
-build v0 -DGBM_FLOW_POST_EVERY=1 -DGBM_FLOW_POLL_SLEEP=1 &
-build v1 -DGBM_FLOW_POST_EVERY=4 -DGBM_FLOW_POLL_SLEEP=1 &
-build v2 -DGBM_FLOW_POST_EVERY=4 -DGBM_FLOW_POLL_SLEEP=4 &
-build v3 -DGBM_FLOW_POST_EVERY=1 -DGBM_FLOW_POLL_SLEEP=4 &
+# worker k-loop pipeline depth (stages per 64-deep step; 2 = round 4's halves)
+build s2 -DGBM_FLOW_STAGES=2 &
+build s4 -DGBM_FLOW_STAGES=4 &
+build s8 -DGBM_FLOW_STAGES=8 &
+build s16 -DGBM_FLOW_STAGES=16 &
 wait

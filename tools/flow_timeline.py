@@ -5,7 +5,7 @@ import ctypes
 import os
 import sys
 
-os.environ["GBM_CHOL_FLOW_TRACE"] = "1"
+os.environ.setdefault("GBM_CHOL_FLOW_TRACE", "1")
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "genomicbreedingmodels.jl_amd"))
 import numpy as np  # noqa: E402
