@@ -80,11 +80,17 @@ __device__ __forceinline__ void tile_pass(const double* __restrict__ U, int64_t 
     const int64_t k = kstep * BK + r;
     double* la = base + r * LROW;
     double* lb = base + (BK + r) * LROW;
+#ifdef GBM_SYRK_TIMING_NOLOAD
+    // timing variant only (tools/build_grm_variants.sh): no operand traffic, the LDS keeps whatever it holds
+    if (k < K) {
+    } else {
+#else
     if (k < K) {
       const double* src = U + k * ldu;
       __builtin_amdgcn_global_load_lds((const void*)(src + i0 + lane * 2), (void*)la, 16, 0, 0);
       if (!diag) __builtin_amdgcn_global_load_lds((const void*)(src + j0 + lane * 2), (void*)lb, 16, 0, 0);
     } else {
+#endif
       *reinterpret_cast<double2*>(la + lane * 2) = make_double2(0.0, 0.0);
       if (!diag) *reinterpret_cast<double2*>(lb + lane * 2) = make_double2(0.0, 0.0);
     }
