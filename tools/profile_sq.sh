@@ -1,4 +1,4 @@
-# SQ counters for the GRM SYRK kernel (one PMC pass, kernel-trace only; no other trace domains)
+# SQ + GRBM counters for the GRM SYRK and dataflow Cholesky kernels (one PMC pass, no other trace domains)
 set -o pipefail
 export PYTHONUNBUFFERED=1
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
@@ -10,7 +10,7 @@ import csv, glob, collections
 f = glob.glob('gpurun_out/sq/p1/**/*counter_collection*.csv', recursive=True)[0]
 agg = collections.defaultdict(lambda: collections.defaultdict(list))
 for r in csv.DictReader(open(f)):
-    agg[r['Kernel_Name'][:40]][r['Counter_Name']].append(float(r['Counter_Value']))
+    agg[r['Kernel_Name'][:120]][r['Counter_Name']].append(float(r['Counter_Value']))
 for k, d in agg.items():
     if 'syrk' in k or 'panel' in k or 'chol_flow' in k:
         print(k, {c: '%.4g' % (sum(v) / len(v)) for c, v in d.items()})
