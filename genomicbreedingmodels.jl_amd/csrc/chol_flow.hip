@@ -77,7 +77,7 @@ __device__ __forceinline__ void st1(__amdgpu_buffer_rsrc_t r, uint32_t voff, dou
 #ifndef GBM_FLOW_POST_EVERY
 #define GBM_FLOW_POST_EVERY 4
 #endif
-// the workers' k-loop pipeline: stages per 64-deep step (2 = round 4's two halves)
+// the register k-loop's pipeline: stages per 64-deep step (2 = round 4's two halves)
 #ifndef GBM_FLOW_STAGES
 #define GBM_FLOW_STAGES 8
 #endif
@@ -779,6 +779,38 @@ chol_flow_kernel(double* __restrict__ G, int64_t ld, int nbc, double* __restrict
     // compiler wait for every load at the top of each pass. The summation order is the same for every tile
     // and pipeline shape. The lower quadrant of a diagonal (or Schur) tile is never read: that wave skips
     // the loop.
+    // k-steps known to be final: U_ki and U_kj (.. U_k,j+NT−1) for k < kr. One vector load checks the
+    // flags of the next GS steps (lane group g: column i, then the task's tiles), so a worker catching up
+    // to the chain polls once per GS steps: a poll per step (dependent flag loads, which drain the
+    // operand loads in flight) made the k-loop ≈ 2.8 µs per step, and the chain's neighbour partial
+    // (i − 1 steps) late. Bounded like poll2.
+    constexpr int GS = NT == 1 ? 32 : 21;
+    constexpr unsigned long long GM = (1ull << GS) - 1;
+    int kr = 0;
+    bool gave_up = false;  // a wait timed out or another waiter gave up (info = −1): drain, no more waits
+    auto ready_upto = [&](int k) {
+      for (int64_t it = 0; k >= kr && !gave_up; it++) {
+        const int g = lane / GS, kk = kr + lane % GS;
+        int ok = 1;
+        if (g <= NT && kk < kend) ok = flag_at_least(flags + (int64_t)kk * nbc + (g == 0 ? i : j + g - 1), kFinal) ? 1 : 0;
+        const unsigned long long bm = __ballot(ok);
+        unsigned long long all = bm & GM;
+#pragma unroll
+        for (int q = 1; q <= NT; q++) all &= (bm >> (q * GS)) & GM;
+        kr += all == GM ? GS : __builtin_ctzll(~all);
+        if (k < kr) break;
+        if ((it & 255) == 255) {
+          gave_up = __hip_atomic_load(info, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < 0;
+          if (!gave_up && it > ((int64_t)1 << 22)) {
+            if (lane == 0) __hip_atomic_store(info, -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            gave_up = true;
+          }
+          gave_up = __builtin_amdgcn_readfirstlane((int)gave_up) != 0;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    };
     if (kend > 0 && !(diag && wr == 1 && wc == 0)) {
       const uint32_t offA = (uint32_t)(((int64_t)fr * ld + i0 + 32 * wr + 2 * fc) * 8);
       const uint32_t offB = (uint32_t)(((int64_t)fr * ld + j0 + 32 * wc + 2 * fc) * 8);
@@ -786,18 +818,35 @@ chol_flow_kernel(double* __restrict__ G, int64_t ld, int nbc, double* __restrict
       constexpr int NS = GBM_FLOW_STAGES, SD = 16 / NS, R = NS * SD;
       static_assert(16 % R == 0 && R % SD == 0, "the ring must tile a 64-deep step");
       dbl2 A[NS][SD], B[NT][NS][SD];
+#ifdef GBM_FLOW_TIMING_NOLOAD
+      const dbl2 zop = acc[0][0][0][0] * 0.0 == 1.0 ? (dbl2){1.0, 1.0} : (dbl2){0.0, 0.0};
+#endif
       auto issue = [&](int pass, int st) {
         const int q0 = pass * R + st * SD;  // first MFMA k-step of the stage
         const __amdgpu_buffer_rsrc_t r = rsrc(G + (int64_t)(q0 >> 4) * FT * ld, gbytes_rowblk);
 #pragma unroll
         for (int e = 0; e < SD; e++) {
           const uint32_t so = (uint32_t)((q0 & 15) + e) * kstep;
+#ifdef GBM_FLOW_TIMING_NOLOAD
+          // timing variant only (tools/build_flow_variants.sh): zero operands, no loads
+          A[st][e] = zop;
+#pragma unroll
+          for (int q = 0; q < NT; q++) B[q][st][e] = zop;
+#else
           A[st][e] = ld2(r, offA, so);
 #pragma unroll
           for (int q = 0; q < NT; q++) B[q][st][e] = ld2(r, offB + (uint32_t)(q * FT * 8), so);
+#endif
         }
       };
       auto mfma = [&](int st) {
+#ifdef GBM_FLOW_TIMING_NOMFMA
+        // timing variant only: the operands are waited for and compared, no MFMA
+#pragma unroll
+        for (int e = 0; e < SD; e++)
+          if (A[st][e].x == 1234.5 && B[0][st][e].y == 1234.5) acc[0][0][0][0] += 1.0;
+        return;
+#endif
 #pragma unroll
         for (int e = 0; e < SD; e++) {
           const double na0 = -A[st][e].x, na1 = -A[st][e].y;
@@ -809,38 +858,6 @@ chol_flow_kernel(double* __restrict__ G, int64_t ld, int nbc, double* __restrict
             acc[q][1][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(na1, B[q][st][e].y, acc[q][1][1], 0, 0, 0);
           }
         }
-      };
-      // k-steps known to be final: U_ki and U_kj (.. U_k,j+NT−1) for k < kr. One vector load checks the
-      // flags of the next GS steps (lane group g: column i, then the task's tiles), so a worker catching up
-      // to the chain polls once per GS steps: a poll per step (dependent flag loads, which drain the
-      // operand loads in flight) made the k-loop ≈ 2.8 µs per step, and the chain's neighbour partial
-      // (i − 1 steps) late. Bounded like poll2.
-      constexpr int GS = NT == 1 ? 32 : 21;
-      constexpr unsigned long long GM = (1ull << GS) - 1;
-      int kr = 0;
-      bool gave_up = false;  // a wait timed out or another waiter gave up (info = −1): drain, no more waits
-      auto ready_upto = [&](int k) {
-        for (int64_t it = 0; k >= kr && !gave_up; it++) {
-          const int g = lane / GS, kk = kr + lane % GS;
-          int ok = 1;
-          if (g <= NT && kk < kend) ok = flag_at_least(flags + (int64_t)kk * nbc + (g == 0 ? i : j + g - 1), kFinal) ? 1 : 0;
-          const unsigned long long bm = __ballot(ok);
-          unsigned long long all = bm & GM;
-#pragma unroll
-          for (int q = 1; q <= NT; q++) all &= (bm >> (q * GS)) & GM;
-          kr += all == GM ? GS : __builtin_ctzll(~all);
-          if (k < kr) break;
-          if ((it & 255) == 255) {
-            gave_up = __hip_atomic_load(info, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < 0;
-            if (!gave_up && it > ((int64_t)1 << 22)) {
-              if (lane == 0) __hip_atomic_store(info, -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-              gave_up = true;
-            }
-            gave_up = __builtin_amdgcn_readfirstlane((int)gave_up) != 0;
-          }
-          __builtin_amdgcn_s_sleep(1);
-        }
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
       };
       // one flag check per pass, ahead of its loads of the next pass (whose stages all lie in one 64-deep
       // step), and no branch between the stages: a conditional inside the ring made the compiler wait for

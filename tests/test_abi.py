@@ -139,13 +139,17 @@ def _order_tiles(buf):
     return out
 
 
-def test_chol_flow_dequeue_order_is_complete_and_deadlock_free():
+@pytest.mark.parametrize("variant", ["default", "6", "4"])
+def test_chol_flow_dequeue_order_is_complete_and_deadlock_free(monkeypatch, variant):
     """The dataflow Cholesky's worker dequeue order (csrc/chol_flow.hip flow_order, host-built): every upper
     64-tile except (0, 0) once, each task after everything it waits for (k-loop operands and the chain's inputs),
     checked on the host for every tile count the dataflow path runs (npad <= 12 288: nbc <= 193); the diagonal
     partial (d, d) follows (d − 2, d) directly (two rows early); the tiles (r, j >= r + 3) go in pairs (one k-loop
     for two tiles), the tiles the chain and the assistant wait for alone."""
     import ctypes
+    if variant != "default":  # GBM_CHOL_FLOW_ORDER is read at every call
+        monkeypatch.setenv("GBM_CHOL_FLOW_ORDER", variant)
+    pairs = variant == "6"
     lib = gbm.load_library()
     for nbc in range(2, 194):
         m = lib.gbm_debug_chol_flow_order_size(nbc)
@@ -155,21 +159,23 @@ def test_chol_flow_dequeue_order_is_complete_and_deadlock_free():
         assert len(tiles) == nbc * (nbc + 1) // 2 - 1
         assert len({(i, j) for _, i, j in tiles}) == len(tiles)
         pos = {(i, j): t for t, i, j in tiles}
-        for d in range(2, nbc - 2):
-            assert pos[(d, d)] == pos[(d - 2, d)] + 1
+        if variant != "4":
+            for d in range(2, nbc - 2):
+                assert pos[(d, d)] == pos[(d - 2, d)] + 1
         for t, v in enumerate(buf):
             i, j = v >> 16, v & 0x7FFF
             if v & 0x8000:
-                assert j >= i + 3 and j + 1 <= nbc - 1
-            elif j >= i + 3:
-                assert j == nbc - 1 or nbc == 2  # a row's odd last tile
-        if nbc >= 8:
-            assert m < nbc * (nbc + 1) // 2 - 1
+                assert pairs and j >= i + 3 and j + 1 <= nbc - 1
+            elif j >= i + 3 and pairs:
+                assert j == nbc - 1  # a row's odd last tile
+        assert (m < nbc * (nbc + 1) // 2 - 1) == (pairs and nbc >= 5)
     assert lib.gbm_debug_chol_flow_order(1, None, 0) == -1
     assert lib.gbm_debug_chol_flow_order_size(1) == -1
     # the checker itself: a diagonal partial moved in front of its last operand, a tile in front of the chain's
     # input of its row, a missing entry, a duplicated tile and a pair over a chain input are caught; plain
     # row-major order with the partials first and no pairs is valid
+    if variant == "4":  # (the swaps below are placed for the two-rows-early diagonal partials)
+        monkeypatch.delenv("GBM_CHOL_FLOW_ORDER")
     nbc = 20
     m = lib.gbm_debug_chol_flow_order_size(nbc)
     buf = (ctypes.c_int32 * m)()
@@ -191,10 +197,11 @@ def test_chol_flow_dequeue_order_is_complete_and_deadlock_free():
     bad[a], bad[b] = bad[b], bad[a]
     assert check(bad) != 0
     assert check(order[:-1]) != 0
-    bad = order.copy()
-    p = next(t for t, v in enumerate(bad) if v & 0x8000)
-    bad[p] &= 0x7FFF7FFF  # a pair entry split: its second tile is missing
-    assert check(bad) != 0
+    if pairs:
+        bad = order.copy()
+        p = next(t for t, v in enumerate(bad) if v & 0x8000)
+        bad[p] &= 0x7FFF7FFF  # a pair entry split: its second tile is missing
+        assert check(bad) != 0
     assert check(order + [enc(5, 9)]) != 0
     assert check([enc(0, 1) | 0x8000] + order[1:]) != 0
     rowmajor = [enc(0, 1), enc(1, 1)]

@@ -11,9 +11,9 @@ build() {  # name flags...
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 "$@" -c genomicbreedingmodels.jl_amd/csrc/chol_flow.hip -o variants/chol_flow_$name.o
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC $OBJS variants/chol_flow_$name.o -lrccl -lrocprofiler-sdk-roctx -o variants/libgbm_$name.so
 }
-# worker k-loop pipeline depth (stages per 64-deep step; 2 = round 4's halves)
-build s2 -DGBM_FLOW_STAGES=2 &
-build s4 -DGBM_FLOW_STAGES=4 &
-build s8 -DGBM_FLOW_STAGES=8 &
-build s16 -DGBM_FLOW_STAGES=16 &
+# the workers' k-loop without operand loads / without MFMAs (timing only: the factorisation is of the
+# un-updated tiles)
+build base &
+build noload -DGBM_FLOW_TIMING_NOLOAD &
+build nomfma -DGBM_FLOW_TIMING_NOMFMA &
 wait
