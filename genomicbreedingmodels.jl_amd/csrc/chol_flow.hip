@@ -51,7 +51,8 @@ typedef double dbl2 __attribute__((ext_vector_type(2)));
 typedef unsigned int u4 __attribute__((ext_vector_type(4)));
 typedef unsigned int u2 __attribute__((ext_vector_type(2)));
 constexpr int FT = 64;         // tile edge
-constexpr int32_t kPairBit = 0x8000;  // dequeue-order entry (i << 16) | j | kPairBit: the tiles (i, j) and (i, j + 1)
+constexpr int32_t kPairBit = 0x8000;
+constexpr int kTraceRec = 32;  // int64 per trace record (timing tool only)  // dequeue-order entry (i << 16) | j | kPairBit: the tiles (i, j) and (i, j + 1)
 constexpr int kSc1 = 16;       // buffer instruction aux bits: sc1 (write-through store / L1-bypassing load)
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* p, int64_t bytes) {
@@ -161,6 +162,7 @@ struct ChainSync {
   int64_t tt[4];  // trace: leaf ends
   int64_t ts[4];  // trace: own-leaf starts (after following the earlier leaves)
   int64_t th[5];  // trace: X2 fetched, Xn fetched, helper waves 0, 1 and 2 done
+  int64_t tw[4];  // trace: wave 1 before its (1, 2) / (1, 3) waits, after them, last group's MFMAs issued, rows read back
 };
 __device__ __forceinline__ int lds_poll(int* p) {
   return __builtin_amdgcn_readfirstlane(__hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
@@ -198,7 +200,10 @@ __device__ __forceinline__ int lds_wait(int* p, int v, int32_t* info, int lane) 
 // instead of a broadcast read per row and element (the LDS pipe is shared with the owner).
 template <int W>
 __device__ __forceinline__ void follow_leaves(double* X, const double* X2, bool prev, ChainSync* sy, int step,
-                                              int32_t* info, int lane, double (&x)[16]) {
+                                              int32_t* info, int lane, double (&x)[16], bool tr) {
+  auto tw = [&](int e) {
+    if (W == 1 && tr && lane == 0) sy->tw[e] = (int64_t)__builtin_amdgcn_s_memrealtime();
+  };
   constexpr int NB = 4 - W;
   const int fr = lane >> 4, fc = lane & 15;
   const int base = 64 * step;
@@ -208,33 +213,52 @@ __device__ __forceinline__ void follow_leaves(double* X, const double* X2, bool 
   if (prev) {
     if (W >= 2) {
       // first, block (1, W) of wave 1's rows (wave 1, whose leaf comes first, keeps only (1, 1))
+      // every operand read first (pinned ahead of the MFMAs): read beside each MFMA, the 16 dependent MFMAs
+      // paid an LDS round trip each and wave 1 waited ≈ 1 µs for this block (round-5 trace)
       d4 t1 = (d4){0.0, 0.0, 0.0, 0.0};
+      double ta[16], tb[16];
 #pragma unroll
       for (int ks = 0; ks < 16; ks++) {
         const double* r = X2 + (ks * 4 + fr) * PS;
-        t1 = __builtin_amdgcn_mfma_f64_16x16x4f64(r[16 + fc], r[16 * W + fc], t1, 0, 0, 0);
+        ta[ks] = r[16 + fc];
+        tb[ks] = r[16 * W + fc];
       }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int ks = 0; ks < 16; ks++) t1 = __builtin_amdgcn_mfma_f64_16x16x4f64(ta[ks], tb[ks], t1, 0, 0, 0);
 #pragma unroll
       for (int r = 0; r < 4; r++) X[(16 + fr + 4 * r) * PS + 16 * W + fc] -= t1[r];
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       lds_post(W == 2 ? &sy->b12 : &sy->b13, step + 1, lane);
     }
+    // (the same for the blocks this wave keeps, eight k-steps of operands at a time)
+    constexpr int NK = W == 1 ? 1 : NB;  // blocks of the last update this wave applies
 #pragma unroll
-    for (int ks = 0; ks < 16; ks++) {
-      const double* r = X2 + (ks * 4 + fr) * PS;
-      const double a = r[16 * W + fc];
+    for (int h = 0; h < 2; h++) {
+      double pa[8], pb[8][NK];
 #pragma unroll
-      for (int b = 0; b < NB; b++)
-        if (!(W == 1 && b >= 1)) acc[b] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, r[16 * (W + b) + fc], acc[b], 0, 0, 0);
+      for (int e = 0; e < 8; e++) {
+        const double* r = X2 + ((8 * h + e) * 4 + fr) * PS;
+        pa[e] = r[16 * W + fc];
+#pragma unroll
+        for (int b = 0; b < NK; b++) pb[e][b] = r[16 * (W + b) + fc];
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int e = 0; e < 8; e++)
+#pragma unroll
+        for (int b = 0; b < NK; b++) acc[b] = __builtin_amdgcn_mfma_f64_16x16x4f64(pa[e], pb[e][b], acc[b], 0, 0, 0);
     }
   }
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // X2 read
   if (lane == 0) __hip_atomic_fetch_add(&sy->pro, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
   // the rows' current values (wave 1: with waves 2 and 3's blocks (1, 2) and (1, 3) of the last update)
+  tw(0);
   if (W == 1 && prev) {
     lds_wait(&sy->b12, step + 1, info, lane);
     lds_wait(&sy->b13, step + 1, info, lane);
   }
+  tw(1);
   const int cc = 16 * W + (lane < 64 - 16 * W ? lane : 0);
 #pragma unroll
   for (int t = 0; t < 16; t++) x[t] = X[(16 * W + t) * PS + cc];
@@ -247,6 +271,7 @@ __device__ __forceinline__ void follow_leaves(double* X, const double* X2, bool 
 #pragma unroll
     for (int b = 0; b < NB; b++) acc[b] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, r[16 * (W + b) + fc], acc[b], 0, 0, 0);
   }
+  tw(2);
   // the accumulated update, transposed to the leaf layout (lane = column) through the rows' place in X
   // (the previous leaf's last four rows applied one by one as rank-1 updates in the leaf layout
   // instead measured slower: hand-over 0.65 -> 0.9-1.4 µs)
@@ -258,6 +283,7 @@ __device__ __forceinline__ void follow_leaves(double* X, const double* X2, bool 
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
   for (int t = 0; t < 16; t++) x[t] -= X[(16 * W + t) * PS + cc];
+  tw(3);
 }
 
 // Block row RB, column block cb of the right neighbour U_i,i+1 = U_ii⁻ᵀ A_i,i+1 (in X2, pitch PS), one
@@ -317,7 +343,7 @@ template <typename AfterOwn>
 __device__ __forceinline__ int factor_block_pipe(double* X, const double* X2, bool prev, double* Dl, int tid,
                                                  __amdgpu_buffer_rsrc_t rDi, uint32_t dinv_base,
                                                  __amdgpu_buffer_rsrc_t rLd, int64_t i0, ChainSync* sy, int step,
-                                                 int32_t* info, int32_t* leaf_bits, AfterOwn&& after_own) {
+                                                 int32_t* info, int32_t* leaf_bits, AfterOwn&& after_own, bool tr = false) {
   const int lane = tid & 63, w = tid >> 6;
   const int o = 16 * w, base = 64 * step;
   const int ncols = CNB - o;
@@ -326,9 +352,9 @@ __device__ __forceinline__ int factor_block_pipe(double* X, const double* X2, bo
   // exec mask; nothing reads X below the diagonal of a factored block, so no zeros are written there
   const int cw = lane < ncols ? o + lane : CNB + (lane & 15);
   double x[16], y[16];
-  if (w == 1) follow_leaves<1>(X, X2, prev, sy, step, info, lane, x);
-  else if (w == 2) follow_leaves<2>(X, X2, prev, sy, step, info, lane, x);
-  else if (w == 3) follow_leaves<3>(X, X2, prev, sy, step, info, lane, x);
+  if (w == 1) follow_leaves<1>(X, X2, prev, sy, step, info, lane, x, tr);
+  else if (w == 2) follow_leaves<2>(X, X2, prev, sy, step, info, lane, x, tr);
+  else if (w == 3) follow_leaves<3>(X, X2, prev, sy, step, info, lane, x, tr);
   else {
 #pragma unroll
     for (int t = 0; t < 16; t++) x[t] = X[(o + t) * PS + cc];
@@ -434,8 +460,8 @@ __device__ __forceinline__ int factor_block_pipe(double* X, const double* X2, bo
 // Every task follows all the tasks it waits for, and the chain's step i waits only for tasks of rows < i, so the
 // launch completes with the chain, the assistant and ONE resident worker (flow_order_check on the host).
 
-// kTrace: per-task timestamps (s_memrealtime, 100 MHz) into trace[t * 24 ...] for the timeline tool;
-// the chain workgroup's steps at trace[(ntasks + i) * 24 ...]
+// kTrace: per-task timestamps (s_memrealtime, 100 MHz) into trace[t * kTraceRec ...] for the timeline tool;
+// the chain workgroup's steps at trace[(ntasks + i) * kTraceRec ...]
 //
 // Workgroup 0 is the CHAIN: it factors every diagonal tile in turn and keeps the chain's data in LDS.
 // Step i: U_ii = chol(A_ii) with its 16x16 inverses (Ld, Dinv); meanwhile its idle waves fetch the
@@ -512,7 +538,7 @@ chol_flow_kernel(double* __restrict__ G, int64_t ld, int nbc, double* __restrict
       // 14 Xn fetched, 15 helpers done
       // trace: one lane stores each timestamp as it is taken (holding them in registers until the step's
       // end raised the traced kernel's register pressure past what it could run with)
-      int64_t* const crec = kTrace && (trace_roles & 1) ? trace + (int64_t)(ntasks + i) * 24 : nullptr;
+      int64_t* const crec = kTrace && (trace_roles & 1) ? trace + (int64_t)(ntasks + i) * kTraceRec : nullptr;
       auto cstamp = [&](int e, int64_t v) {
         if (kTrace && crec && tid == 0) crec[3 + e] = v;
       };
@@ -608,7 +634,7 @@ chol_flow_kernel(double* __restrict__ G, int64_t ld, int nbc, double* __restrict
       };
       // ---- U_ii = chol(A_ii) -> Ld, its 16x16 diagonal inverses -> Dinv (and Dl)
       const int bad = factor_block_pipe(Xa, X2, i > 0, Dl, tid, rDi, (uint32_t)((i0 / 16) * 256 * 8), rLd, i0, &sy, i,
-                                        info, flags + (int64_t)(i + 1) * nbc + i, after_own);
+                                        info, flags + (int64_t)(i + 1) * nbc + i, after_own, kTrace && crec);
       if (tid == 0 && bad >= 0) atomicCAS(info, 0, (int32_t)(i0 + bad + 1));
       if (kTrace && crec && tid == 0) {
 #pragma unroll
@@ -653,6 +679,8 @@ chol_flow_kernel(double* __restrict__ G, int64_t ld, int nbc, double* __restrict
         crec[2] = -1;
         crec[22] = sy.th[2];  // helper wave 0 (column blocks 0 and 3) done
         crec[23] = sy.th[4];  // helper wave 2 done
+#pragma unroll
+        for (int e = 0; e < 4; e++) crec[24 + e] = sy.tw[e];  // wave 1's hand-over into leaf 1
       }
       double* t = Xa;
       Xa = Xn;
@@ -678,7 +706,7 @@ chol_flow_kernel(double* __restrict__ G, int64_t ld, int nbc, double* __restrict
       const int32_t* fA = flags + (int64_t)(i - 1) * nbc + i;      // U_i−1,i (the chain)
       wave_wait2(fP, fB, info, lane, kPartial);
       wave_wait2(fB, fB, info, lane, kFinal);
-      int64_t* const arec = kTrace && (trace_roles & 2) ? trace + (int64_t)(ntasks + i) * 24 : nullptr;  // slots 19-21 of step i
+      int64_t* const arec = kTrace && (trace_roles & 2) ? trace + (int64_t)(ntasks + i) * kTraceRec : nullptr;  // slots 19-21 of step i
       if (kTrace && arec && tid == 0) arec[19] = (int64_t)__builtin_amdgcn_s_memrealtime();
       // the chain's U_i−1,i: its flag is loaded BEFORE the operands below, so (vmcnt being in order)
       // checking it leaves those loads in flight; a poll (a call, which drains loads in flight) only
@@ -752,7 +780,7 @@ chol_flow_kernel(double* __restrict__ G, int64_t ld, int nbc, double* __restrict
     const int64_t i0 = (int64_t)i * FT, j0 = (int64_t)j * FT;
     // a diagonal tile's last update (k = i − 1) is the chain's, a right neighbour's the assistant's
     const int kend = ((diag && i < nb) || (nbr && i >= 1)) ? i - 1 : i;
-    int64_t* const wrec = kTrace && (trace_roles & 4) ? trace + (int64_t)t * 24 : nullptr;
+    int64_t* const wrec = kTrace && (trace_roles & 4) ? trace + (int64_t)t * kTraceRec : nullptr;
     auto wstamp = [&](int e) {
       if (kTrace && wrec && tid == 0) wrec[3 + e] = (int64_t)__builtin_amdgcn_s_memrealtime();
     };
@@ -1178,10 +1206,10 @@ int launch_chol_flow(double* G, int64_t ldg, int64_t gdim, double* Ld, double* D
     if (g_trace_cap < nrec) {
       if (g_trace) (void)hipFree(g_trace);
       g_trace = nullptr;
-      GBM_HIP_TRY(hipMalloc((void**)&g_trace, (size_t)nrec * 192));
+      GBM_HIP_TRY(hipMalloc((void**)&g_trace, (size_t)nrec * kTraceRec * 8));
       g_trace_cap = nrec;
     }
-    GBM_HIP_TRY(hipMemsetAsync(g_trace, 0, (size_t)nrec * 192, s));
+    GBM_HIP_TRY(hipMemsetAsync(g_trace, 0, (size_t)nrec * kTraceRec * 8, s));
     g_trace_n = nrec;
     // GBM_CHOL_FLOW_TRACE = a mask of the roles that record (1 chain, 2 assistant, 4 workers; 1 = all)
     const int tm = atoi(getenv("GBM_CHOL_FLOW_TRACE"));
@@ -1206,7 +1234,7 @@ extern "C" int64_t gbm_debug_chol_flow_trace(int64_t* host, int64_t cap) {
   using namespace gbm;
   if (!g_trace || !host) return 0;
   const int64_t n = g_trace_n < cap ? g_trace_n : cap;
-  if (hipDeviceSynchronize() != hipSuccess || hipMemcpy(host, g_trace, (size_t)n * 192, hipMemcpyDeviceToHost) != hipSuccess)
+  if (hipDeviceSynchronize() != hipSuccess || hipMemcpy(host, g_trace, (size_t)n * kTraceRec * 8, hipMemcpyDeviceToHost) != hipSuccess)
     return -1;
   return n;
 }

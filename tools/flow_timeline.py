@@ -34,7 +34,7 @@ nbc = (st.npad + 64) // 64
 ntasks = nbc * (nbc + 1) // 2
 nb = nbc - 1
 cap = ntasks + nbc
-buf = np.zeros((cap, 24), dtype=np.int64)
+buf = np.zeros((cap, 32), dtype=np.int64)  # kTraceRec
 got = lib.gbm_debug_chol_flow_trace(buf.ctypes.data, cap)
 assert got == cap, got
 T = buf.astype(np.float64)
@@ -58,6 +58,13 @@ for kb in range(4):  # wave kb owns leaf kb; the next leaf's owner goes on as so
     print(f"      leaf {kb}: hand-over (-> own start)   ", f(us(own0 - prev)))
     print(f"      leaf {kb}: own 16 steps               ", f(us(ct[:, 1 + kb] - own0)))
     prev = ct[:, 1 + kb]
+if (Ch[1:, 24:28] > 0).all():  # wave 1's hand-over into leaf 1 (steps >= 1: with the previous step's update)
+    w1 = Ch[1:, 24:28]
+    l0 = ct[1:, 1]
+    print("      wave 1: (1,2)/(1,3) waits begin, from leaf 0 end", f(us(w1[:, 0] - l0)))
+    print("      wave 1: waits end, from leaf 0 end           ", f(us(w1[:, 1] - l0)))
+    print("      wave 1: last row group's MFMAs issued, from leaf 0 end", f(us(w1[:, 2] - l0)))
+    print("      wave 1: rows read back, from leaf 0 end      ", f(us(w1[:, 3] - l0)))
 print("    last leaf end -> factored (sync)     ", f(us(ct[:, 8] - ct[:, 4])))
 print("    X2 (neighbour partial) in LDS, from start", f(us(ct[:, 9] - ct[:, 0])))
 print("    Xn (next diag partial) in LDS, from start", f(us(ct[:, 14] - ct[:, 0])))
