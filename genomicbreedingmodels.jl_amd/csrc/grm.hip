@@ -705,6 +705,11 @@ static GrmPlan plan(int64_t n, int64_t p) {
 // into the accumulators first and the A fragments are negated, so the MFMA chain itself
 // produces C − Σ_k U[k][i] U[k][j] (no separate read-modify-write).
 constexpr int P64 = 80;  // LDS pitch: the two 16-lane halves of a fragment read hit disjoint banks
+// PIPE (the multi-chunk row updates): chunk c + 1's loads are in flight in registers while chunk c's MFMAs
+// run (round 5: each chunk's loads used to wait behind the previous chunk's MFMAs — the distributed panel
+// phase's row updates, 52 of 190 ms per rank at n = 50 000, R = 8); 32 more registers, still two
+// workgroups per CU.
+template <bool PIPE>
 __global__ void __launch_bounds__(256, 2)
 syrk64_sub_kernel(const double* __restrict__ U, int64_t ldu, int64_t c0, int64_t lim, double* __restrict__ C,
                   int64_t ldc, double* Ld, double* Dinv, int32_t* __restrict__ info,
@@ -736,29 +741,37 @@ syrk64_sub_kernel(const double* __restrict__ U, int64_t ldu, int64_t c0, int64_t
         }
   }
   // K = 64 kchunks: the chunks are staged one after the other (kchunks > 1 only for the row
-  // updates that bring a later panel of a 4-panel group up to date)
+  // updates that bring a later panel of a panel group up to date)
   const double* B = Bs;
+  const int k = tid >> 2, quarter = tid & 3;
+  // all 16 loads in flight before the LDS stores (interleaving them with the diag-conditional stores
+  // made the compiler wait for each load in turn)
+  // (one 16-double vector each: as arrays carried across the chunk loop they went to scratch)
+  typedef double d16 __attribute__((ext_vector_type(16)));
+  d16 va, vb;
+  auto load_chunk = [&](int c) {
+    const double* sa = U + (c * 64 + k) * ldu + i0 + quarter * 16;
+    const double* sb = U + (c * 64 + k) * ldu + j0 + quarter * 16;
+#pragma unroll
+    for (int e = 0; e < 8; e++) {
+      const double2 x = *reinterpret_cast<const double2*>(sa + 2 * e);
+      const double2 y = *reinterpret_cast<const double2*>(sb + 2 * e);
+      va[2 * e] = x.x;
+      va[2 * e + 1] = x.y;
+      vb[2 * e] = y.x;
+      vb[2 * e + 1] = y.y;
+    }
+  };
+  load_chunk(0);
   for (int c = 0; c < kchunks; c++) {
     if (c > 0) __syncthreads();  // every wave is done with the previous chunk
-    {
-      // all 16 loads in flight before the LDS stores (interleaving them with the diag-conditional
-      // stores made the compiler wait for each load in turn)
-      const int k = tid >> 2, quarter = tid & 3;
-      const double* sa = U + (c * 64 + k) * ldu + i0 + quarter * 16;
-      const double* sb = U + (c * 64 + k) * ldu + j0 + quarter * 16;
-      double2 va[8], vb[8];
 #pragma unroll
-      for (int e = 0; e < 8; e++) {
-        va[e] = *reinterpret_cast<const double2*>(sa + 2 * e);
-        vb[e] = *reinterpret_cast<const double2*>(sb + 2 * e);
-      }
-#pragma unroll
-      for (int e = 0; e < 8; e++) {  // (on diagonal tiles vb == va: storing it anyway keeps this branch-free)
-        *reinterpret_cast<double2*>(&As[k * P64 + quarter * 16 + 2 * e]) = va[e];
-        *reinterpret_cast<double2*>(&Bs[k * P64 + quarter * 16 + 2 * e]) = vb[e];
-      }
+    for (int e = 0; e < 8; e++) {  // (on diagonal tiles vb == va: storing it anyway keeps this branch-free)
+      *reinterpret_cast<double2*>(&As[k * P64 + quarter * 16 + 2 * e]) = make_double2(va[2 * e], va[2 * e + 1]);
+      *reinterpret_cast<double2*>(&Bs[k * P64 + quarter * 16 + 2 * e]) = make_double2(vb[2 * e], vb[2 * e + 1]);
     }
     __syncthreads();
+    if (PIPE && c + 1 < kchunks) load_chunk(c + 1);  // in flight during this chunk's MFMAs
     if (active) {
 #pragma unroll
       for (int ks = 0; ks < 16; ks++) {
@@ -774,6 +787,7 @@ syrk64_sub_kernel(const double* __restrict__ U, int64_t ldu, int64_t c0, int64_t
             acc[m][q] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[m], bf[q], acc[m][q], 0, 0, 0);
       }
     }
+    if (!PIPE && c + 1 < kchunks) load_chunk(c + 1);
   }
   const bool factor_next = fk0 >= 0 && blockIdx.x == 0;
   if (!active && !factor_next) return;
@@ -822,8 +836,12 @@ int launch_chol_row_update(double* G, int64_t ldg, int64_t k0, int kch, int64_t 
                            int32_t* info, hipStream_t s, ColKeep keep) {
   const int64_t k1 = k0 + 64 * (int64_t)kch;
   const int64_t lim = gdim - k1;
-  syrk64_sub_kernel<<<(unsigned)(lim / 64), 256, 0, s>>>(G + k0 * ldg, ldg, k1, lim, G, ldg, Ld, Dinv, info, k1, 1,
-                                                         kch, keep);
+  if (kch > 1)
+    syrk64_sub_kernel<true><<<(unsigned)(lim / 64), 256, 0, s>>>(G + k0 * ldg, ldg, k1, lim, G, ldg, Ld, Dinv, info, k1,
+                                                             1, kch, keep);
+  else
+    syrk64_sub_kernel<false><<<(unsigned)(lim / 64), 256, 0, s>>>(G + k0 * ldg, ldg, k1, lim, G, ldg, Ld, Dinv, info, k1,
+                                                              1, kch, keep);
   GBM_LAUNCH_CHECK();
   return GBM_OK;
 }
@@ -862,7 +880,7 @@ int launch_chol_update(double* G, int64_t ldg, int64_t k0, int64_t nb, int64_t g
   }
   if (nb == 64 && lim <= chol_small_lim()) {
     const int64_t m = (lim + 63) / 64;
-    syrk64_sub_kernel<<<(unsigned)(m * (m + 1) / 2), 256, 0, s>>>(G + k0 * ldg, ldg, k1, lim, G, ldg, Ld, Dinv, info,
+    syrk64_sub_kernel<false><<<(unsigned)(m * (m + 1) / 2), 256, 0, s>>>(G + k0 * ldg, ldg, k1, lim, G, ldg, Ld, Dinv, info,
                                                                   next_k0, 0, (int)(nb / 64), ColKeep{});
     GBM_LAUNCH_CHECK();
     return GBM_OK;
