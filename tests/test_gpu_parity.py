@@ -39,6 +39,23 @@ def test_gblup_matches_oracle(n, p, t, seed):
     assert rel(oracle.predict_linear(X, b_hat), y_pred) < TOL_TIGHT
 
 
+@pytest.mark.parametrize("grm", ["fp64", "exact"])
+@pytest.mark.parametrize("n,p", [(2, 40), (3, 1), (65, 2), (127, 1)])
+def test_tiny_shapes_match_oracle(n, p, grm):
+    """The smallest fits the reference accepts (≥ 2 entries, prediction.jl:117-123) and single-locus GRMs:
+    one diagonal tile with mostly padding, p below one LDS stage of loci; both GRM modes."""
+    rng = np.random.default_rng(n * 1000 + p)
+    X = rng.integers(0, 3, size=(n, p)).astype(np.float64) / 2.0
+    X[0, :], X[1, :] = 0.0, 1.0  # every locus polymorphic
+    Y = rng.standard_normal((n, 2))
+    b_hat, y_pred, mu, q = gbm.gblup_arrays(X, Y, lambda_=0.7, grm=grm)
+    ref = oracle.gblup_fit(X, Y, 0.7)
+    assert q == ref["q"] == p
+    assert rel(y_pred, ref["y_pred"]) < TOL_TIGHT
+    assert rel(mu, ref["mu"]) < TOL_TIGHT
+    assert rel(b_hat, ref["b_hat"]) < TOL_CONTRACT
+
+
 def test_monomorphic_and_lambda():
     n, p = 150, 400
     X = oracle.synth_genotypes(99, n, p)
@@ -220,7 +237,7 @@ def test_cholesky_panel_groups_forced(monkeypatch, g4, g8, g16):
     n, p = 1500, 900
     X = oracle.synth_genotypes(77, n, p)
     Y = oracle.synth_phenotypes(X, 78, ntraits=2)
-    b_hat, y_pred, mu, q = gbm.gblup_arrays(X, Y, lambda_=0.7)
+    b_hat, y_pred, mu, q = gbm.gblup_arrays(X, Y, lambda_=0.7, grm=grm)
     ref = oracle.gblup_fit(X, Y, 0.7)
     assert q == ref["q"]
     assert rel(y_pred, ref["y_pred"]) < TOL_TIGHT
