@@ -130,14 +130,21 @@ __global__ void __launch_bounds__(256) chol_panel_kernel(double* __restrict__ G,
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int64_t jx = k0 + ((int64_t)blockIdx.x + 1) * CNB;
   if (!col_kept(keep, jx)) return;  // (workgroup-uniform)
+  // rows (tid >> 5) + 8 e, 16 bytes at column 2 (tid & 31): one wave instruction = two whole 512-byte rows
+  const int lrow = tid >> 5, lcol = 2 * (tid & 31);
   {
-    const int row = tid >> 2, quarter = tid & 3;
-    const double* sl = Ld + (k0 + row) * CNB + quarter * 16;
-    const double* sx = G + (k0 + row) * ld + jx + quarter * 16;
+    const double* sl = Ld + (k0 + lrow) * CNB + lcol;
+    const double* sx = G + (k0 + lrow) * ld + jx + lcol;
+    double2 vl[8], vx[8];
 #pragma unroll
-    for (int e = 0; e < 16; e += 2) {
-      *reinterpret_cast<double2*>(&Us[row * PS + quarter * 16 + e]) = *reinterpret_cast<const double2*>(sl + e);
-      *reinterpret_cast<double2*>(&X[row * PS + quarter * 16 + e]) = *reinterpret_cast<const double2*>(sx + e);
+    for (int e = 0; e < 8; e++) {
+      vl[e] = *reinterpret_cast<const double2*>(sl + 8 * e * CNB);
+      vx[e] = *reinterpret_cast<const double2*>(sx + 8 * e * ld);
+    }
+#pragma unroll
+    for (int e = 0; e < 8; e++) {
+      *reinterpret_cast<double2*>(&Us[(lrow + 8 * e) * PS + lcol]) = vl[e];
+      *reinterpret_cast<double2*>(&X[(lrow + 8 * e) * PS + lcol]) = vx[e];
     }
     const double* sd = Dinv + (k0 / 16) * 256;
     *reinterpret_cast<double2*>(&Di[tid * 2]) = *reinterpret_cast<const double2*>(sd + tid * 2);
@@ -148,11 +155,11 @@ __global__ void __launch_bounds__(256) chol_panel_kernel(double* __restrict__ G,
                     lane, wave);
   __syncthreads();
   {
-    const int row = tid >> 2, quarter = tid & 3;
-    double* dx = G + (k0 + row) * ld + jx + quarter * 16;
+    double* dx = G + (k0 + lrow) * ld + jx + lcol;
 #pragma unroll
-    for (int e = 0; e < 16; e += 2)
-      *reinterpret_cast<double2*>(dx + e) = *reinterpret_cast<const double2*>(&X[row * PS + quarter * 16 + e]);
+    for (int e = 0; e < 8; e++)
+      *reinterpret_cast<double2*>(dx + 8 * e * ld) = *reinterpret_cast<const double2*>(&X[(lrow + 8 * e) * PS + lcol]);
+    const int row = tid >> 2, quarter = tid & 3;
     double* dl = G + (jx + row) * ld + k0 + quarter * 16;
 #pragma unroll
     for (int e = 0; e < 16; e += 2)
@@ -172,14 +179,22 @@ __global__ void __launch_bounds__(256) chol_lower_copy_kernel(double* __restrict
   const int64_t prow = r0 + rb * CNB;                          // its first row
   const int64_t jx = prow + ((int64_t)blockIdx.x + 1) * CNB;  // chunk right of its diagonal block
   if (jx >= npad || col_kept(keep, jx)) return;
-  const int tid = threadIdx.x, row = tid >> 2, quarter = tid & 3;
-  const double* su = G + (prow + row) * ld + jx + quarter * 16;
+  // rows (tid >> 5) + 8 e, 16 bytes at column 2 (tid & 31): each wave instruction reads / writes two whole rows
+  const int tid = threadIdx.x, lrow = tid >> 5, lcol = 2 * (tid & 31);
+  const double* su = G + (prow + lrow) * ld + jx + lcol;
+  double2 v[8];
 #pragma unroll
-  for (int e = 0; e < 16; e++) T[row][quarter * 16 + e] = su[e];
+  for (int e = 0; e < 8; e++) v[e] = *reinterpret_cast<const double2*>(su + 8 * e * ld);
+#pragma unroll
+  for (int e = 0; e < 8; e++) {
+    T[lrow + 8 * e][lcol] = v[e].x;
+    T[lrow + 8 * e][lcol + 1] = v[e].y;
+  }
   __syncthreads();
-  double* dl = G + (jx + row) * ld + prow + quarter * 16;
+  double* dl = G + (jx + lrow) * ld + prow + lcol;
 #pragma unroll
-  for (int e = 0; e < 16; e++) dl[e] = T[quarter * 16 + e][row];
+  for (int e = 0; e < 8; e++)
+    *reinterpret_cast<double2*>(dl + 8 * e * ld) = make_double2(T[lcol][lrow + 8 * e], T[lcol + 1][lrow + 8 * e]);
 }
 
 // ---- inverses of all diagonal blocks U_bb (one workgroup per block, all in parallel) --------

@@ -743,19 +743,22 @@ syrk64_sub_kernel(const double* __restrict__ U, int64_t ldu, int64_t c0, int64_t
   // K = 64 kchunks: the chunks are staged one after the other (kchunks > 1 only for the row
   // updates that bring a later panel of a panel group up to date)
   const double* B = Bs;
-  const int k = tid >> 2, quarter = tid & 3;
+  // thread t stages 16 bytes of rows (t >> 5) + 8 e, e < 8: one load instruction of a wave covers two whole
+  // 512-byte rows (8 cache lines; 16 rows x 16 bytes per instruction left each line to 8 instructions — round
+  // 5: 12 us per K = 64 chunk of the distributed row updates), and the LDS stores of a row are contiguous
+  const int lrow = tid >> 5, lcol = 2 * (tid & 31);
   // all 16 loads in flight before the LDS stores (interleaving them with the diag-conditional stores
   // made the compiler wait for each load in turn)
   // (one 16-double vector each: as arrays carried across the chunk loop they went to scratch)
   typedef double d16 __attribute__((ext_vector_type(16)));
   d16 va, vb;
   auto load_chunk = [&](int c) {
-    const double* sa = U + (c * 64 + k) * ldu + i0 + quarter * 16;
-    const double* sb = U + (c * 64 + k) * ldu + j0 + quarter * 16;
+    const double* sa = U + (c * 64 + lrow) * ldu + i0 + lcol;
+    const double* sb = U + (c * 64 + lrow) * ldu + j0 + lcol;
 #pragma unroll
     for (int e = 0; e < 8; e++) {
-      const double2 x = *reinterpret_cast<const double2*>(sa + 2 * e);
-      const double2 y = *reinterpret_cast<const double2*>(sb + 2 * e);
+      const double2 x = *reinterpret_cast<const double2*>(sa + 8 * e * ldu);
+      const double2 y = *reinterpret_cast<const double2*>(sb + 8 * e * ldu);
       va[2 * e] = x.x;
       va[2 * e + 1] = x.y;
       vb[2 * e] = y.x;
@@ -767,8 +770,8 @@ syrk64_sub_kernel(const double* __restrict__ U, int64_t ldu, int64_t c0, int64_t
     if (c > 0) __syncthreads();  // every wave is done with the previous chunk
 #pragma unroll
     for (int e = 0; e < 8; e++) {  // (on diagonal tiles vb == va: storing it anyway keeps this branch-free)
-      *reinterpret_cast<double2*>(&As[k * P64 + quarter * 16 + 2 * e]) = make_double2(va[2 * e], va[2 * e + 1]);
-      *reinterpret_cast<double2*>(&Bs[k * P64 + quarter * 16 + 2 * e]) = make_double2(vb[2 * e], vb[2 * e + 1]);
+      *reinterpret_cast<double2*>(&As[(lrow + 8 * e) * P64 + lcol]) = make_double2(va[2 * e], va[2 * e + 1]);
+      *reinterpret_cast<double2*>(&Bs[(lrow + 8 * e) * P64 + lcol]) = make_double2(vb[2 * e], vb[2 * e + 1]);
     }
     __syncthreads();
     if (PIPE && c + 1 < kchunks) load_chunk(c + 1);  // in flight during this chunk's MFMAs
