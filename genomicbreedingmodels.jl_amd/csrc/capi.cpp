@@ -965,8 +965,8 @@ int solve_distributed(std::vector<std::unique_ptr<Shard>>& shards, const std::ve
                                 c.stream.s));
     return cs ? sync_all(shards, leaders) : GBM_OK;
   }
-  // GBM_DIST_OVERLAP (default 1): the next group's area is updated first and all-gathered on the copy
-  // streams while the rest of the trailing update runs (same kernels, same tiles: same bits)
+  // GBM_DIST_OVERLAP (default 1): the next group's area is updated and all-gathered on the copy streams
+  // while the rest of the trailing update runs (same kernels, same tiles: same bits)
   const bool overlap = env_i64("GBM_DIST_OVERLAP", 1) != 0;
   if (overlap)
     GBM_TRY(each([&](int, FitCtx& c) -> int {
@@ -981,14 +981,23 @@ int solve_distributed(std::vector<std::unique_ptr<Shard>>& shards, const std::ve
                                             c.wss.cap, c.stream.s);
     });
   };
-  // the area exchange of the group at kb on the copy streams, after ev_upd (its tiles updated); ends
-  // with ev_area, which the group's panels wait for
+  // the update of the columns [lo, hi) (the next group's area: about one tile column per rank, a few
+  // workgroups one K = 64 g tile long) on the copy streams, beside the rest of the update on the main ones
+  auto area_update_async = [&](int64_t kb, int64_t lo, int64_t hi) {
+    return each([&](int r, FitCtx& c) -> int {
+      GBM_HIP_TRY(hipEventRecord(c.ev_upd, c.stream.s));  // after the group's rows arrived
+      GBM_HIP_TRY(hipStreamWaitEvent(c.copy.s, c.ev_upd, 0));
+      return gbm_dev_chol_group_update_cols((double*)c.G.p, gdim, n, kb, r, R, lo, hi, (int32_t*)c.info.p, c.wss.p,
+                                            c.wss.cap, c.copy.s);
+    });
+  };
+  // the area exchange of the group at kb on the copy streams (after area_update_async); ends with ev_area,
+  // which the group's panels wait for
   auto area_async = [&](int64_t kb, int64_t g) -> int {
     const int64_t cnt = gbm_dev_chol_area_doubles(n, kb, g, R);  // non-increasing over the groups
     GBM_TRY(each([&](int r, FitCtx& c) -> int {
       GBM_TRY(ensure(c.astrip, c.dev, cnt * 8));
       GBM_TRY(ensure(c.agathered, c.dev, R * cnt * 8));
-      GBM_HIP_TRY(hipStreamWaitEvent(c.copy.s, c.ev_upd, 0));
       return gbm_dev_chol_area_pack((const double*)c.G.p, gdim, n, kb, g, r, R, (double*)c.astrip.p, c.copy.s);
     }));
     GBM_TRY(allgather_strips(shards, leaders, cs, cnt, true));
@@ -1028,12 +1037,8 @@ int solve_distributed(std::vector<std::unique_ptr<Shard>>& shards, const std::ve
     const bool next_dist = k1 < nb && distributable(k1);
     if (overlap && next_dist) {
       const int64_t area_hi = kCholNB * (k1 + gbm_dev_chol_group_size(n, k1));
-      GBM_TRY(update(kb, kCholNB * k1, area_hi));  // the next group's area first
-      GBM_TRY(each([&](int, FitCtx& c) -> int {
-        GBM_HIP_TRY(hipEventRecord(c.ev_upd, c.stream.s));
-        return GBM_OK;
-      }));
-      GBM_TRY(update(kb, area_hi, gdim));  // the rest (and the right-hand sides) beside the exchange
+      GBM_TRY(area_update_async(kb, kCholNB * k1, area_hi));  // the next group's area, on the copy streams
+      GBM_TRY(update(kb, area_hi, gdim));  // the rest (and the right-hand sides) beside it and its exchange
       GBM_TRY(area_async(k1, gbm_dev_chol_group_size(n, k1)));
       area_pending = true;
     } else {

@@ -124,8 +124,8 @@ def chol_distributed(stages, ranks, nranks, allgather, tail_rows=None, force=Fal
     (plus the area and the right-hand sides; gbm_dev_chol_group_panels), the group's solved rows are
     all-gathered (strip_unpack_rows also writes their lower copy), then the trailing update runs on
     the rank's own tiles and the right-hand sides (gbm_dev_chol_group_update). With overlap
-    (GBM_DIST_OVERLAP, default 1; stages with fork/side/join), the next group's area is updated first
-    and exchanged on a side stream while the rest of the update runs (gbm_dev_chol_group_update_cols).
+    (GBM_DIST_OVERLAP, default 1; stages with fork/side/join), the next group's area is updated and
+    exchanged on a side stream while the rest of the update runs (gbm_dev_chol_group_update_cols).
     Once the trailing matrix is small (``tail_rows``, GBM_DIST_TAIL_ROWS, default 8192) or the groups
     shrink to single panels, every remaining row is gathered once and the tail runs redundantly. The
     result is bit-identical to the redundant solve (the same kernels compute every tile).
@@ -202,15 +202,17 @@ def chol_distributed(stages, ranks, nranks, allgather, tail_rows=None, force=Fal
         k1 = kb + g
         next_dist = k1 < nb and distributable(k1)
         if overlap and next_dist:
+            # the next group's area (a rank owns about one of its tile columns: a few workgroups, one K = 64 g
+            # tile long) is updated and exchanged on the side stream, beside the rest of the update
             area_hi = 64 * (k1 + int(lib.gbm_dev_chol_group_size(n, k1)))
-            for st, r in zip(stages, ranks):  # the next group's area first
-                st.chol_group_update_cols(kb, r, nranks, 64 * k1, area_hi)
             for st in stages:
                 st.fork()
+            with stages[0].side():  # (one side stream per device)
+                for st, r in zip(stages, ranks):
+                    st.chol_group_update_cols(kb, r, nranks, 64 * k1, area_hi)
+                exchange(k1, int(lib.gbm_dev_chol_group_size(n, k1)), "area")
             for st, r in zip(stages, ranks):
                 st.chol_group_update_cols(kb, r, nranks, area_hi, gdim)
-            with stages[0].side():  # (one side stream per device)
-                exchange(k1, int(lib.gbm_dev_chol_group_size(n, k1)), "area")
             pending = True
         else:
             for st, r in zip(stages, ranks):
