@@ -197,6 +197,243 @@ __global__ void __launch_bounds__(256) chol_lower_copy_kernel(double* __restrict
     *reinterpret_cast<double2*>(dl + 8 * e * ld) = make_double2(T[lcol][lrow + 8 * e], T[lcol + 1][lrow + 8 * e]);
 }
 
+// ---- a panel group's panel phase in ONE launch (round 5) -----------------------------------------
+// The rows [k0, k0 + 64 g) of a panel group, for every column chunk right of the group's first
+// diagonal block that the rank keeps, are the left-looking block forward substitution
+//   A_jc −= Σ_{i<j} U_ijᵀ U_ic  (64-deep steps in i order),  then  U_jc = U_jj⁻ᵀ A_jc  (j < c)
+//   or, on the area's diagonal (j = c), U_cc = chol(A_cc) → Ld, Dinv,
+// the same arithmetic as the chain of g panel launches and g − 1 row-update launches it replaces
+// (whose per-launch latency made the panel phase ~1.35 ms per 16-panel group at n = 50 000). One
+// workgroup per column chunk walks its rows j = 0, 1, …; the area's chunks (c = 1 … g − 1: their
+// tiles U_ij and U_jj are the other chunks' operands) publish a progress flag per row, the others
+// wait for those flags only. Area chunk c keeps A_cc − Σ U_icᵀU_ic up to date after each of its
+// rows, so its diagonal step is only the factor. Workgroups take their chunk from a ticket in
+// dispatch order and wait only for smaller tickets: no deadlock whatever the residency. U tiles,
+// Ld and Dinv handed between workgroups go through write-through stores and sc1 loads (no cache
+// invalidate); flags as in chol_device.h (bounded waits, info = −1).
+struct GroupCols {
+  int32_t g = 0, nranks = 1;
+  int64_t a0 = 0;       // first chunk right of the area
+  int64_t n_own = 0;    // kept regular chunks right of the area
+  int64_t J_first = 0;  // nranks > 1: the rank's first 128-column tile at or right of chunk a0
+  int64_t rhs0 = 0, n_rhs = 0;  // the right-hand-side chunks
+};
+
+__global__ void __launch_bounds__(256, 1) chol_group_kernel(double* __restrict__ G, int64_t ld, int64_t k0, GroupCols gc,
+                                                            double* __restrict__ Ld, double* __restrict__ Dinv,
+                                                            int32_t* __restrict__ prog, int32_t* __restrict__ info) {
+  // staging of the update steps (As, Bs) | the solve (X, Us, Di, rinv): X aliases As, Us aliases Bs
+  __shared__ __attribute__((aligned(16))) double lds[2 * CNB * PS + 1024 + CNB + 16];
+  __shared__ int32_t s_tk, s_seen, s_ok;
+  double* const As = lds;
+  double* const Bs = lds + CNB * PS;
+  double* const X = lds;
+  double* const Us = lds + CNB * PS;
+  double* const Di = lds + 2 * CNB * PS;
+  double* const rinv = Di + 1024;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1, fr = lane >> 4, fc = lane & 15;
+  if (tid == 0) s_tk = atomicAdd(&prog[0], 1);
+  __syncthreads();
+  const int64_t b = s_tk;
+  const int g = gc.g;
+  const bool area = b < g - 1;
+  const int c = area ? (int)b + 1 : g;  // area column, relative to the group
+  int64_t chunk;
+  if (area) {
+    chunk = k0 / CNB + c;
+  } else if (b - (g - 1) < gc.n_own) {
+    const int64_t m = b - (g - 1);
+    chunk = gc.nranks == 1 ? gc.a0 + m : 2 * (gc.J_first + (m >> 1) * gc.nranks) + (m & 1);
+  } else {
+    chunk = gc.rhs0 + (b - (g - 1) - gc.n_own);
+  }
+  const int64_t jx = chunk * CNB;
+  const int jlast = area ? c : g - 1;
+  // 16 bytes at column lcol of rows lrow + 8 e (e < 8): a wave instruction covers two whole 512-byte rows
+  const int lrow = tid >> 5, lcol = 2 * (tid & 31);
+  const int64_t slab = (int64_t)CNB * ld * 8;  // bytes of a 64-row block of G
+  auto quad = [&](int m, int q, int r, int64_t& row, int64_t& col) {
+    row = wm * 32 + m * 16 + fr + 4 * r;
+    col = wn * 32 + q * 16 + fc;
+  };
+  d4 acc[2][2], accd[2][2];
+  if (area) {  // A_cc, brought up to date row by row
+    const double* src = G + (k0 + (int64_t)c * CNB) * ld + jx;
+#pragma unroll
+    for (int m = 0; m < 2; m++)
+#pragma unroll
+      for (int q = 0; q < 2; q++)
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+          int64_t row, col;
+          quad(m, q, r, row, col);
+          accd[m][q][r] = src[row * ld + col];
+        }
+  }
+  typedef double d16 __attribute__((ext_vector_type(16)));
+  for (int j = 0; j <= jlast; j++) {
+    const int64_t r0 = k0 + (int64_t)j * CNB;
+    const __amdgpu_buffer_rsrc_t rrow = wt_rsrc(G + r0 * ld, slab);
+    if (area && j == c) {
+      // the diagonal block: store it updated (as the row updates did), factor it, publish Ld and Dinv
+#pragma unroll
+      for (int m = 0; m < 2; m++)
+#pragma unroll
+        for (int q = 0; q < 2; q++)
+#pragma unroll
+          for (int r = 0; r < 4; r++) {
+            int64_t row, col;
+            quad(m, q, r, row, col);
+            G[(r0 + row) * ld + jx + col] = accd[m][q][r];
+            Us[row * PS + col] = accd[m][q][r];
+          }
+      __syncthreads();
+      const int bad = factor_diag_block(Us, rinv, tid);
+      if (tid == 0 && bad >= 0) atomicCAS(info, 0, (int32_t)(r0 + bad + 1));
+      const __amdgpu_buffer_rsrc_t rL = wt_rsrc(Ld + r0 * CNB, CNB * CNB * 8);
+      const __amdgpu_buffer_rsrc_t rD = wt_rsrc(Dinv + (r0 / 16) * 256, 1024 * 8);
+      store_factor_with(
+          Us, rinv, tid, [&](int e, wt_d2 v) { wt_st2(rL, (uint32_t)(e * 8), v); },
+          [&](int e, double x) { wt_st1(rD, (uint32_t)(e * 8), x); });
+      publish_flag(&prog[c], j + 1, tid);
+      break;
+    }
+    // acc = A_jc (written by earlier launches only)
+    {
+      const double* src = G + r0 * ld + jx;
+#pragma unroll
+      for (int m = 0; m < 2; m++)
+#pragma unroll
+        for (int q = 0; q < 2; q++)
+#pragma unroll
+          for (int r = 0; r < 4; r++) {
+            int64_t row, col;
+            quad(m, q, r, row, col);
+            acc[m][q][r] = src[row * ld + col];
+          }
+    }
+    // progress of area column j (row i final: prog[j] >= i + 1; its diagonal: >= j + 1). Column 0 is the
+    // group's first diagonal block, factored before the launch. Workgroup-uniform.
+    int seen = j == 0 ? 1 : 0;
+    auto need = [&](int32_t v) -> bool {
+      if (seen >= v) return true;
+      __syncthreads();  // s_seen / s_ok are rewritten below
+      if (tid == 0) {
+        s_ok = wait_flag<false>(&prog[j], v, info) ? 1 : 0;
+        s_seen = __hip_atomic_load(&prog[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      __syncthreads();
+      seen = s_seen;
+      return s_ok != 0;
+    };
+    if (j > 0) {
+      // acc −= Σ_{i<j} U_ijᵀ U_ic, staged through LDS; step i + 1's loads are in flight during step i's MFMAs
+      d16 va, vb;
+      auto load_step = [&](int i) {
+        const __amdgpu_buffer_rsrc_t rk = wt_rsrc(G + (k0 + (int64_t)i * CNB) * ld, slab);
+#pragma unroll
+        for (int e = 0; e < 8; e++) {
+          const int64_t rowoff = (int64_t)(lrow + 8 * e) * ld;
+          const wt_d2 x = wt_ld2(rk, (uint32_t)((rowoff + r0 + lcol) * 8));
+          const wt_d2 y = wt_ld2(rk, (uint32_t)((rowoff + jx + lcol) * 8));
+          va[2 * e] = x.x;
+          va[2 * e + 1] = x.y;
+          vb[2 * e] = y.x;
+          vb[2 * e + 1] = y.y;
+        }
+      };
+      if (!need(1)) return;
+      load_step(0);
+      for (int i = 0; i < j; i++) {
+        if (i > 0) __syncthreads();  // every wave is done with step i − 1
+#pragma unroll
+        for (int e = 0; e < 8; e++) {
+          *reinterpret_cast<wt_d2*>(&As[(lrow + 8 * e) * PS + lcol]) = (wt_d2){va[2 * e], va[2 * e + 1]};
+          *reinterpret_cast<wt_d2*>(&Bs[(lrow + 8 * e) * PS + lcol]) = (wt_d2){vb[2 * e], vb[2 * e + 1]};
+        }
+        __syncthreads();
+        if (i + 1 < j) {
+          if (!need(i + 2)) return;
+          load_step(i + 1);
+        }
+#pragma unroll
+        for (int ks = 0; ks < 16; ks++) {
+          double af[2], bf[2];
+#pragma unroll
+          for (int m = 0; m < 2; m++) af[m] = -As[(ks * 4 + fr) * PS + wm * 32 + m * 16 + fc];
+#pragma unroll
+          for (int q = 0; q < 2; q++) bf[q] = Bs[(ks * 4 + fr) * PS + wn * 32 + q * 16 + fc];
+#pragma unroll
+          for (int m = 0; m < 2; m++)
+#pragma unroll
+            for (int q = 0; q < 2; q++) acc[m][q] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[m], bf[q], acc[m][q], 0, 0, 0);
+        }
+      }
+      if (!need(j + 1)) return;  // U_jj factored
+    }
+    __syncthreads();  // As / Bs are free: X and Us alias them
+    // X = A_jc, Us = U_jj (Ld), Di = its 16x16 diagonal inverses (Dinv)
+#pragma unroll
+    for (int m = 0; m < 2; m++)
+#pragma unroll
+      for (int q = 0; q < 2; q++)
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+          int64_t row, col;
+          quad(m, q, r, row, col);
+          X[row * PS + col] = acc[m][q][r];
+        }
+    {
+      const __amdgpu_buffer_rsrc_t rL = wt_rsrc(Ld + r0 * CNB, CNB * CNB * 8);
+      const __amdgpu_buffer_rsrc_t rD = wt_rsrc(Dinv + (r0 / 16) * 256, 1024 * 8);
+      wt_d2 u[8];
+#pragma unroll
+      for (int k = 0; k < 8; k++) u[k] = wt_ld2(rL, (uint32_t)((2 * tid + 512 * k) * 8));
+      const wt_d2 d0 = wt_ld2(rD, (uint32_t)(2 * tid * 8)), d1 = wt_ld2(rD, (uint32_t)((512 + 2 * tid) * 8));
+#pragma unroll
+      for (int k = 0; k < 8; k++) {
+        const int e = 2 * tid + 512 * k;
+        *reinterpret_cast<wt_d2*>(&Us[(e >> 6) * PS + (e & 63)]) = u[k];
+      }
+      *reinterpret_cast<wt_d2*>(&Di[2 * tid]) = d0;
+      *reinterpret_cast<wt_d2*>(&Di[512 + 2 * tid]) = d1;
+    }
+    __syncthreads();
+    panel_chunk_solve(X, Us, [&](int rb, int ks) { return Di[rb * 256 + (ks * 4 + fr) * 16 + fc]; }, lane, wave);
+    __syncthreads();
+    // U_jc -> G (write-through: later steps of this and other workgroups read it), its transpose -> the lower copy
+#pragma unroll
+    for (int e = 0; e < 8; e++) {
+      const int row = lrow + 8 * e;
+      wt_st2(rrow, (uint32_t)(((int64_t)row * ld + jx + lcol) * 8), *reinterpret_cast<const wt_d2*>(&X[row * PS + lcol]));
+    }
+#pragma unroll
+    for (int e = 0; e < 8; e++) {
+      const int row = lrow + 8 * e;
+      *reinterpret_cast<double2*>(G + (jx + row) * ld + r0 + lcol) = make_double2(X[lcol * PS + row], X[(lcol + 1) * PS + row]);
+    }
+    if (area) {
+      // A_cc −= U_jcᵀ U_jc (from LDS), then row j of this column is published
+#pragma unroll
+      for (int ks = 0; ks < 16; ks++) {
+        double af[2], bf[2];
+#pragma unroll
+        for (int m = 0; m < 2; m++) af[m] = -X[(ks * 4 + fr) * PS + wm * 32 + m * 16 + fc];
+#pragma unroll
+        for (int q = 0; q < 2; q++) bf[q] = X[(ks * 4 + fr) * PS + wn * 32 + q * 16 + fc];
+#pragma unroll
+        for (int m = 0; m < 2; m++)
+#pragma unroll
+          for (int q = 0; q < 2; q++) accd[m][q] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[m], bf[q], accd[m][q], 0, 0, 0);
+      }
+      publish_flag(&prog[c], j + 1, tid);
+    } else {
+      __syncthreads();  // X is read before the next step's staging overwrites it
+    }
+  }
+}
+
 // ---- inverses of all diagonal blocks U_bb (one workgroup per block, all in parallel) --------
 // lane = column j: X[i][j] = (δ_ij − Σ_{k>i} U[i][k] X[k][j]) / U[i][i], the dot product split
 // over 4 partial sums so the dependent chain is a quarter of its length.
@@ -487,12 +724,19 @@ int solve_prepare(double* G, int64_t ldg, int64_t n, double inv_q, const int64_t
   return GBM_OK;
 }
 
-// One panel group at 64-block kb (its diagonal block already factored): the group's first panel,
-// the rows of its later panels brought up to date with the earlier ones (row updates, K = 64 j,
-// each factoring its diagonal block), their panels (panels_only: stop here), then one K = 64 g
-// trailing update, whose first workgroup factors the next diagonal block.
-// keep (distributed panel phase, nranks > 1): the panels and row updates cover this rank's columns,
-// the group's diagonal area and the right-hand sides only.
+// GBM_CHOL_GROUP_KERNEL (re-read per group, default 1): a panel group's panel phase as one
+// chol_group_kernel launch; 0: the chain of panel and row-update launches
+static bool group_kernel_enabled() {
+  const char* e = getenv("GBM_CHOL_GROUP_KERNEL");
+  return !e || atoi(e) != 0;
+}
+
+// The panel phase of the group at 64-block kb (its diagonal block already factored): the group's
+// rows solved for every kept column chunk — one chol_group_kernel launch for g > 1 (default), or the
+// chain of the first panel, then per later panel a row update (K = 64 j, factoring its diagonal
+// block) and its panel. The trailing update (solve_group_update) follows.
+// keep (distributed panel phase, nranks > 1): this rank's columns, the group's diagonal area and the
+// right-hand sides only.
 int solve_group_panels(double* G, int64_t ldg, int64_t n, int64_t kb, ColKeep keep, int32_t* info, void* workspace,
                        hipStream_t s, int64_t* g_out) {
   const int64_t npad = npad_of(n), gdim = gdim_of(n), nb = npad / NB;
@@ -506,6 +750,32 @@ int solve_group_panels(double* G, int64_t ldg, int64_t n, int64_t kb, ColKeep ke
     keep.keep_hi = k0 + g * NB;
     keep.rhs0 = npad;
   }
+  if (g_out) *g_out = g;
+  if (g > 1 && group_kernel_enabled()) {
+    // the whole panel phase in one launch (chol_group_kernel)
+    GroupCols gc;
+    gc.g = g;
+    gc.nranks = keep.nranks;
+    gc.a0 = kb + g;
+    gc.rhs0 = npad / NB;
+    gc.n_rhs = (gdim - npad) / NB;
+    if (keep.nranks == 1) {
+      gc.n_own = npad / NB - gc.a0;
+    } else {
+      const int64_t R = keep.nranks, J0 = gc.a0 / 2;  // (a0 even: k0 on a 128-row boundary, g even)
+      if ((gc.a0 & 1) != 0) return fail(GBM_E_ARG, "gbm_dev_chol_group_panels: odd panel group in a distributed step");
+      gc.J_first = J0 + ((keep.rank - J0) % R + R) % R;
+      for (int64_t J = gc.J_first; 2 * J < npad / NB; J += R) gc.n_own += (2 * J + 1 < npad / NB) ? 2 : 1;
+    }
+    if ((int64_t)(CNB + 1) * ldg * 8 > 0x7fffffff)
+      return fail(GBM_E_ARG, "chol_group_kernel: ldg too large for 32-bit buffer offsets");
+    int32_t* prog = reinterpret_cast<int32_t*>(w.flow);  // (the dataflow factorisation's flags: unused on this path)
+    GBM_HIP_TRY(hipMemsetAsync(prog, 0, (size_t)g * sizeof(int32_t), s));
+    const int64_t nwg = (g - 1) + gc.n_own + gc.n_rhs;
+    chol_group_kernel<<<(unsigned)nwg, 256, 0, s>>>(G, ldg, k0, gc, w.Ld, w.Dinv, prog, info);
+    GBM_LAUNCH_CHECK();
+    return GBM_OK;
+  }
   auto panel = [&](int64_t k) {
     const int64_t chunks = (gdim - k) / NB - 1;  // column chunks right of the diagonal block
     chol_panel_kernel<<<(unsigned)chunks, 256, 0, s>>>(G, ldg, k, w.Ld, w.Dinv, keep);
@@ -516,7 +786,6 @@ int solve_group_panels(double* G, int64_t ldg, int64_t n, int64_t kb, ColKeep ke
     GBM_TRY(launch_chol_row_update(G, ldg, k0, j, gdim, w.Ld, w.Dinv, info, s, keep));
     if (!panel(k0 + j * NB)) return fail(GBM_E_HIP, "chol_panel_kernel launch failed");
   }
-  if (g_out) *g_out = g;
   return GBM_OK;
 }
 

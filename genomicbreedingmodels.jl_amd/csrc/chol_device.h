@@ -169,18 +169,38 @@ __device__ __forceinline__ int factor_diag_block(double* Us, double* rinv, int t
   return m ? (int)__builtin_ctzll(m) : -1;
 }
 
+// Write-through (sc1) buffer stores and sc1 (L1-bypassing) buffer loads: data handed between workgroups of one
+// launch (chol_group_kernel; chol_flow.hip has its own copies). One resource per 64-row block of G keeps the
+// byte offsets 32-bit.
+typedef double wt_d2 __attribute__((ext_vector_type(2)));
+typedef unsigned int wt_u4 __attribute__((ext_vector_type(4)));
+typedef unsigned int wt_u2 __attribute__((ext_vector_type(2)));
+constexpr int kWtSc1 = 16;  // buffer instruction aux bits: sc1
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t wt_rsrc(const void* p, int64_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ wt_d2 wt_ld2(__amdgpu_buffer_rsrc_t r, uint32_t voff) {
+  return __builtin_bit_cast(wt_d2, __builtin_amdgcn_raw_buffer_load_b128(r, (int)voff, 0, kWtSc1));
+}
+__device__ __forceinline__ void wt_st2(__amdgpu_buffer_rsrc_t r, uint32_t voff, wt_d2 v) {
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(wt_u4, v), r, (int)voff, 0, kWtSc1);
+}
+__device__ __forceinline__ void wt_st1(__amdgpu_buffer_rsrc_t r, uint32_t voff, double v) {
+  __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(wt_u2, v), r, (int)voff, 0, kWtSc1);
+}
+
 // Store a factored block: Ld_blk (64x64 row-major, upper, zeros below) and the inverses of its
 // four 16x16 diagonal sub-blocks Dinv_blk[w][i][j] = (D_w⁻¹)[i][j] (upper). Wave w computes D_w⁻¹
 // column by column (lane j < 16), the dot products split over 2 partial sums.
-__device__ __forceinline__ void store_factor(const double* Us, const double* rinv, double* Ld_blk,
-                                             double* Dinv_blk, int tid) {
+// st_ld(e, v): Ld_blk[e..e+1] = v (e even); st_di(e, x): Dinv_blk[e] = x.
+template <typename StLd, typename StDi>
+__device__ __forceinline__ void store_factor_with(const double* Us, const double* rinv, int tid, StLd st_ld,
+                                                  StDi st_di) {
   const int lane = tid & 63, wave = tid >> 6;
-  {
-    const int row = tid >> 2, quarter = tid & 3;
-    double* dst = Ld_blk + row * CNB + quarter * 16;
 #pragma unroll
-    for (int e = 0; e < 16; e += 2)
-      *reinterpret_cast<double2*>(dst + e) = *reinterpret_cast<const double2*>(&Us[row * PS + quarter * 16 + e]);
+  for (int k = 0; k < 8; k++) {  // the block is contiguous: a wave instruction stores 1 KB
+    const int e = 2 * tid + 512 * k;
+    st_ld(e, *reinterpret_cast<const wt_d2*>(&Us[(e >> 6) * PS + (e & 63)]));
   }
   const int o = wave * 16;
   const int j = lane & 15;
@@ -197,8 +217,14 @@ __device__ __forceinline__ void store_factor(const double* Us, const double* rin
   }
   if (lane < 16) {
 #pragma unroll
-    for (int i = 0; i < 16; i++) Dinv_blk[wave * 256 + i * 16 + j] = x[i];
+    for (int i = 0; i < 16; i++) st_di(wave * 256 + i * 16 + j, x[i]);
   }
+}
+__device__ __forceinline__ void store_factor(const double* Us, const double* rinv, double* Ld_blk,
+                                             double* Dinv_blk, int tid) {
+  store_factor_with(
+      Us, rinv, tid, [&](int e, wt_d2 v) { *reinterpret_cast<wt_d2*>(Ld_blk + e) = v; },
+      [&](int e, double x) { Dinv_blk[e] = x; });
 }
 
 // Block forward substitution of one 64-column chunk X (LDS, pitch PS) of a panel row, given the
