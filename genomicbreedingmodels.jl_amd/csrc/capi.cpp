@@ -46,11 +46,13 @@ struct FitCtx {
   DevBuf errs, q2;               // streamed fit: per-chunk carry error cells; scratch kept count
   DevBuf astrip, agathered;      // the distributed factorisation's area all-gather (on the copy stream)
   hipEvent_t ev_area = nullptr, ev_upd = nullptr;  // area exchange done / next area updated
+  hipEvent_t ev_rows = nullptr;                    // (look-ahead) the next group's rows updated
   ~FitCtx() {
     (void)hipSetDevice(dev);
     for (hipEvent_t e : ev) (void)hipEventDestroy(e);
     if (ev_area) (void)hipEventDestroy(ev_area);
     if (ev_upd) (void)hipEventDestroy(ev_upd);
+    if (ev_rows) (void)hipEventDestroy(ev_rows);
   }
 };
 
@@ -281,7 +283,11 @@ int upload_grm_pipelined(const Problem& pr, Shard& sh, int64_t chunk) {
   hipStream_t s = c.stream.s;
   if (!c.copy.s) {
     c.copy.dev = c.dev;
-    GBM_HIP_TRY(hipStreamCreateWithFlags(&c.copy.s, hipStreamNonBlocking));
+    // high priority: besides the streamed uploads it carries the distributed solve's latency-bound
+    // look-ahead (area exchange, the next group's panels and row exchange) beside the trailing update
+    int lo = 0, hi = 0;
+    GBM_HIP_TRY(hipDeviceGetStreamPriorityRange(&lo, &hi));
+    GBM_HIP_TRY(hipStreamCreateWithPriority(&c.copy.s, hipStreamNonBlocking, hi));
   }
   const std::vector<std::pair<int64_t, int64_t>> sched = chunk_schedule(pl, chunk, (pr.src == Source::F64 && n <= 8192) || getenv("GBM_HOST_CHUNK") != nullptr);
   const int64_t nch = (int64_t)sched.size();
@@ -357,7 +363,11 @@ int upload_grm_pipelined(const Problem& pr, Shard& sh, int64_t chunk) {
 int ensure_copy_stream(FitCtx& c) {
   if (!c.copy.s) {
     c.copy.dev = c.dev;
-    GBM_HIP_TRY(hipStreamCreateWithFlags(&c.copy.s, hipStreamNonBlocking));
+    // high priority: besides the streamed uploads it carries the distributed solve's latency-bound
+    // look-ahead (area exchange, the next group's panels and row exchange) beside the trailing update
+    int lo = 0, hi = 0;
+    GBM_HIP_TRY(hipDeviceGetStreamPriorityRange(&lo, &hi));
+    GBM_HIP_TRY(hipStreamCreateWithPriority(&c.copy.s, hipStreamNonBlocking, hi));
   }
   return GBM_OK;
 }
@@ -851,15 +861,17 @@ int allreduce_grm(std::vector<std::unique_ptr<Shard>>& shards, int64_t n) {
 // All-gather of the leaders' strip packs (cnt doubles each) into every leader's `gathered`, in
 // leader (= rank) order: RCCL across distinct devices, device copies when leaders share one.
 // area = true: the area buffers (astrip -> agathered) on the copy streams.
+// on_copy: the strip buffers on the copy streams (the look-ahead's row exchange).
 int allgather_strips(std::vector<std::unique_ptr<Shard>>& shards, const std::vector<int>& leaders, CommSet* cs,
-                     int64_t cnt, bool area = false) {
+                     int64_t cnt, bool area = false, bool on_copy = false) {
   auto src = [&](FitCtx& c) { return area ? c.astrip.p : c.strip.p; };
   auto dst = [&](FitCtx& c) { return (double*)(area ? c.agathered.p : c.gathered.p); };
+  const bool cp = area || on_copy;
   if (cs) {
     ncclResult_t r = ncclGroupStart();
     for (size_t k = 0; k < leaders.size() && r == ncclSuccess; k++) {
       FitCtx& c = shards[leaders[k]]->x();
-      r = ncclAllGather(src(c), dst(c), (size_t)cnt, ncclDouble, cs->comms[k], area ? c.copy.s : c.stream.s);
+      r = ncclAllGather(src(c), dst(c), (size_t)cnt, ncclDouble, cs->comms[k], cp ? c.copy.s : c.stream.s);
     }
     ncclResult_t r2 = ncclGroupEnd();
     if (r != ncclSuccess || r2 != ncclSuccess)
@@ -867,15 +879,15 @@ int allgather_strips(std::vector<std::unique_ptr<Shard>>& shards, const std::vec
     g_rccl_allgather.fetch_add(1);
     return GBM_OK;
   }
-  GBM_TRY(sync_all(shards, leaders, area));  // every pack is complete
+  GBM_TRY(sync_all(shards, leaders, cp));  // every pack is complete
   for (int d : leaders) {
     FitCtx& cd = shards[d]->x();
     for (size_t r = 0; r < leaders.size(); r++) {
       FitCtx& cr = shards[leaders[r]]->x();
-      GBM_TRY(copy_dd(cd, dst(cd) + r * cnt, cr, src(cr), cnt * 8, area ? cd.copy.s : cd.stream.s));
+      GBM_TRY(copy_dd(cd, dst(cd) + r * cnt, cr, src(cr), cnt * 8, cp ? cd.copy.s : cd.stream.s));
     }
   }
-  return sync_all(shards, leaders, area);  // no copy still reads a pack the next step overwrites
+  return sync_all(shards, leaders, cp);  // no copy still reads a pack the next step overwrites
 }
 
 // GBLUP solve of V = G/q + λI factored across the device leaders (each holding the summed G): the
@@ -915,21 +927,26 @@ int solve_distributed(std::vector<std::unique_ptr<Shard>>& shards, const std::ve
   // (their lower copy completed too); kRest: the trailing matrix's remaining rows (the tail switch);
   // kArea: the square diagonal area of a group only
   enum { kRows, kRest, kArea };
-  auto exchange = [&](int64_t kb, int64_t rows64, int what) -> int {
+  // on_copy (kRows only): on the copy streams — the look-ahead's row exchange of the next group, beside the
+  // trailing update on the main streams (the strip buffers are then free of main-stream work: the sizes
+  // do not grow from group to group, and the tail's kRest exchange comes after a join)
+  auto exchange = [&](int64_t kb, int64_t rows64, int what, bool on_copy = false) -> int {
     const int64_t cnt = what == kArea ? gbm_dev_chol_area_doubles(n, kb, rows64, R)
                                       : gbm_dev_chol_strip_doubles(n, kb, rows64, R);
     GBM_TRY(each([&](int r, FitCtx& c) {
       GBM_TRY(ensure(c.strip, c.dev, cnt * 8));
       GBM_TRY(ensure(c.gathered, c.dev, R * cnt * 8));
+      const hipStream_t s = on_copy ? c.copy.s : c.stream.s;
       if (what == kArea)
-        return gbm_dev_chol_area_pack((const double*)c.G.p, gdim, n, kb, rows64, r, R, (double*)c.strip.p, c.stream.s);
-      return gbm_dev_chol_strip_pack((const double*)c.G.p, gdim, n, kb, rows64, r, R, (double*)c.strip.p, c.stream.s);
+        return gbm_dev_chol_area_pack((const double*)c.G.p, gdim, n, kb, rows64, r, R, (double*)c.strip.p, s);
+      return gbm_dev_chol_strip_pack((const double*)c.G.p, gdim, n, kb, rows64, r, R, (double*)c.strip.p, s);
     }));
-    GBM_TRY(allgather_strips(shards, leaders, cs, cnt));
+    GBM_TRY(allgather_strips(shards, leaders, cs, cnt, false, on_copy));
     return each([&](int r, FitCtx& c) {
       const double* gathered = (const double*)c.gathered.p;
       if (what == kRows)
-        return gbm_dev_chol_strip_unpack_rows((double*)c.G.p, gdim, n, kb, rows64, r, R, gathered, c.stream.s);
+        return gbm_dev_chol_strip_unpack_rows((double*)c.G.p, gdim, n, kb, rows64, r, R, gathered,
+                                              on_copy ? c.copy.s : c.stream.s);
       if (what == kArea) {
         GBM_TRY(gbm_dev_chol_area_unpack((double*)c.G.p, gdim, n, kb, rows64, R, gathered, c.stream.s));
       } else {
@@ -968,11 +985,15 @@ int solve_distributed(std::vector<std::unique_ptr<Shard>>& shards, const std::ve
   // GBM_DIST_OVERLAP (default 1): the next group's area is updated and all-gathered on the copy streams
   // while the rest of the trailing update runs (same kernels, same tiles: same bits)
   const bool overlap = env_i64("GBM_DIST_OVERLAP", 1) != 0;
+  // GBM_DIST_LOOKAHEAD (default 1, with overlap): the next group's rows are updated first, then its panels
+  // and row exchange run on the copy streams beside the rest of the trailing update
+  const bool lookahead = overlap && env_i64("GBM_DIST_LOOKAHEAD", 1) != 0;
   if (overlap)
     GBM_TRY(each([&](int, FitCtx& c) -> int {
       GBM_TRY(ensure_copy_stream(c));
       if (!c.ev_area) GBM_HIP_TRY(hipEventCreateWithFlags(&c.ev_area, hipEventDisableTiming));
       if (!c.ev_upd) GBM_HIP_TRY(hipEventCreateWithFlags(&c.ev_upd, hipEventDisableTiming));
+      if (!c.ev_rows) GBM_HIP_TRY(hipEventCreateWithFlags(&c.ev_rows, hipEventDisableTiming));
       return GBM_OK;
     }));
   auto update = [&](int64_t kb, int64_t lo, int64_t hi) {
@@ -1010,6 +1031,7 @@ int solve_distributed(std::vector<std::unique_ptr<Shard>>& shards, const std::ve
   };
   bool dist = R > 1 && distributable(0), stale = false;  // stale: a distributed update skipped other ranks' tiles
   bool area_pending = false;                    // the current group's area is being exchanged (overlap)
+  bool ahead = false;                           // (look-ahead) the current group's panels and rows: copy streams
   for (int64_t kb = 0; kb < nb;) {
     const int64_t g = gbm_dev_chol_group_size(n, kb);
     if (!dist) {
@@ -1028,18 +1050,52 @@ int solve_distributed(std::vector<std::unique_ptr<Shard>>& shards, const std::ve
     } else if (stale) {
       GBM_TRY(exchange(kb, g, kArea));
     }
-    GBM_TRY(each([&](int r, FitCtx& c) {
-      return gbm_dev_chol_group_panels((double*)c.G.p, gdim, n, kb, r, R, (int32_t*)c.info.p, c.wss.p, c.wss.cap,
-                                       c.stream.s);
-    }));
-    GBM_TRY(exchange(kb, g, kRows));
+    auto panels = [&](int64_t k, bool on_copy) {
+      return each([&](int r, FitCtx& c) {
+        return gbm_dev_chol_group_panels((double*)c.G.p, gdim, n, k, r, R, (int32_t*)c.info.p, c.wss.p, c.wss.cap,
+                                         on_copy ? c.copy.s : c.stream.s);
+      });
+    };
+    if (!ahead) {
+      GBM_TRY(panels(kb, false));
+      GBM_TRY(exchange(kb, g, kRows));
+    }
+    ahead = false;
     const int64_t k1 = kb + g;
     const bool next_dist = k1 < nb && distributable(k1);
     if (overlap && next_dist) {
-      const int64_t area_hi = kCholNB * (k1 + gbm_dev_chol_group_size(n, k1));
+      const int64_t g1 = gbm_dev_chol_group_size(n, k1);
+      const int64_t area_hi = kCholNB * (k1 + g1);
       GBM_TRY(area_update_async(kb, kCholNB * k1, area_hi));  // the next group's area, on the copy streams
-      GBM_TRY(update(kb, area_hi, gdim));  // the rest (and the right-hand sides) beside it and its exchange
-      GBM_TRY(area_async(k1, gbm_dev_chol_group_size(n, k1)));
+      if (lookahead) {
+        // the next group's rows of the rank's tiles (and the right-hand sides) first; its panels and row
+        // exchange follow the area exchange on the copy streams, beside the rest of the update (the rows
+        // from area_hi on: disjoint tiles)
+        auto tiles = [&](int64_t r_lo, int64_t r_hi) {
+          return each([&](int r, FitCtx& c) {
+            return gbm_dev_chol_group_update_tiles((double*)c.G.p, gdim, n, kb, r, R, r_lo, r_hi, area_hi, gdim,
+                                                   (int32_t*)c.info.p, c.wss.p, c.wss.cap, c.stream.s);
+          });
+        };
+        GBM_TRY(tiles(kCholNB * k1, area_hi));
+        GBM_TRY(area_async(k1, g1));
+        GBM_TRY(each([&](int, FitCtx& c) -> int {
+          GBM_HIP_TRY(hipEventRecord(c.ev_rows, c.stream.s));
+          GBM_HIP_TRY(hipStreamWaitEvent(c.copy.s, c.ev_rows, 0));
+          return GBM_OK;
+        }));
+        GBM_TRY(panels(k1, true));
+        GBM_TRY(exchange(k1, g1, kRows, true));
+        GBM_TRY(each([&](int, FitCtx& c) -> int {
+          GBM_HIP_TRY(hipEventRecord(c.ev_area, c.copy.s));  // the next group waits for all of it
+          return GBM_OK;
+        }));
+        GBM_TRY(tiles(area_hi, gdim));
+        ahead = true;
+      } else {
+        GBM_TRY(update(kb, area_hi, gdim));  // the rest (and the right-hand sides) beside it and its exchange
+        GBM_TRY(area_async(k1, g1));
+      }
       area_pending = true;
     } else {
       GBM_TRY(update(kb, kCholNB * k1, gdim));

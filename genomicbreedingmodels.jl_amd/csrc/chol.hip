@@ -26,7 +26,7 @@ constexpr int MAXRHS = 63;
 
 int launch_chol_update(double* G, int64_t ldg, int64_t k0, int64_t nb, int64_t gdim, double* Ld, double* Dinv,
                        int32_t* info, int64_t next_k0, int rank, int nranks, hipStream_t s, int64_t col_lo = 0,
-                       int64_t col_hi = INT64_MAX);
+                       int64_t col_hi = INT64_MAX, int64_t row_lo = 0, int64_t row_hi = INT64_MAX);
 int launch_chol_row_update(double* G, int64_t ldg, int64_t k0, int kch, int64_t gdim, double* Ld, double* Dinv,
                            int32_t* info, hipStream_t s, ColKeep keep = ColKeep{});
 int64_t chol_small_lim();
@@ -219,18 +219,24 @@ struct GroupCols {
   int64_t rhs0 = 0, n_rhs = 0;  // the right-hand-side chunks
 };
 
-__global__ void __launch_bounds__(256, 1) chol_group_kernel(double* __restrict__ G, int64_t ld, int64_t k0, GroupCols gc,
+// Two workgroups per CU's worth of registers and at most 88 KB of LDS: a workgroup fits beside one of the
+// trailing update's (72 KB), which the distributed solve runs concurrently (look-ahead).
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) chol_group_kernel(double* __restrict__ G, int64_t ld, int64_t k0, GroupCols gc,
                                                             double* __restrict__ Ld, double* __restrict__ Dinv,
                                                             int32_t* __restrict__ prog, int32_t* __restrict__ info) {
-  // staging of the update steps (As, Bs) | the solve (X, Us, Di, rinv): X aliases As, Us aliases Bs
-  __shared__ __attribute__((aligned(16))) double lds[2 * CNB * PS + 1024 + CNB + 16];
-  __shared__ int32_t s_tk, s_seen, s_ok;
+  // staging of the update steps (As, Bs) | the solve (X, Us) | the diagonal step (rinv, Us): X aliases As, Us
+  // aliases Bs, rinv lies in X's rows 1-2 (only used on the diagonal step); the three shared words sit in row 0's
+  // padding columns (64-79 of every pitch-PS row are never touched). 80 KB: two workgroups per CU.
+  __shared__ __attribute__((aligned(16))) double lds[2 * CNB * PS];
+  int32_t* const sw = reinterpret_cast<int32_t*>(lds + CNB);
+  int32_t& s_tk = sw[0];
+  int32_t& s_seen = sw[1];
+  int32_t& s_ok = sw[2];
   double* const As = lds;
   double* const Bs = lds + CNB * PS;
   double* const X = lds;
   double* const Us = lds + CNB * PS;
-  double* const Di = lds + 2 * CNB * PS;
-  double* const rinv = Di + 1024;
+  double* const rinv = lds + PS;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1, fr = lane >> 4, fc = lane & 15;
   if (tid == 0) s_tk = atomicAdd(&prog[0], 1);
@@ -373,7 +379,8 @@ __global__ void __launch_bounds__(256, 1) chol_group_kernel(double* __restrict__
       if (!need(j + 1)) return;  // U_jj factored
     }
     __syncthreads();  // As / Bs are free: X and Us alias them
-    // X = A_jc, Us = U_jj (Ld), Di = its 16x16 diagonal inverses (Dinv)
+    double di[16];
+    // X = A_jc, Us = U_jj (Ld); di = this lane's MFMA operands of its 16x16 diagonal inverses (Dinv)
 #pragma unroll
     for (int m = 0; m < 2; m++)
 #pragma unroll
@@ -390,17 +397,18 @@ __global__ void __launch_bounds__(256, 1) chol_group_kernel(double* __restrict__
       wt_d2 u[8];
 #pragma unroll
       for (int k = 0; k < 8; k++) u[k] = wt_ld2(rL, (uint32_t)((2 * tid + 512 * k) * 8));
-      const wt_d2 d0 = wt_ld2(rD, (uint32_t)(2 * tid * 8)), d1 = wt_ld2(rD, (uint32_t)((512 + 2 * tid) * 8));
+#pragma unroll
+      for (int rb = 0; rb < 4; rb++)
+#pragma unroll
+        for (int ks = 0; ks < 4; ks++) di[rb * 4 + ks] = wt_ld1(rD, (uint32_t)((rb * 256 + (ks * 4 + fr) * 16 + fc) * 8));
 #pragma unroll
       for (int k = 0; k < 8; k++) {
         const int e = 2 * tid + 512 * k;
         *reinterpret_cast<wt_d2*>(&Us[(e >> 6) * PS + (e & 63)]) = u[k];
       }
-      *reinterpret_cast<wt_d2*>(&Di[2 * tid]) = d0;
-      *reinterpret_cast<wt_d2*>(&Di[512 + 2 * tid]) = d1;
     }
     __syncthreads();
-    panel_chunk_solve(X, Us, [&](int rb, int ks) { return Di[rb * 256 + (ks * 4 + fr) * 16 + fc]; }, lane, wave);
+    panel_chunk_solve(X, Us, [&](int rb, int ks) { return di[rb * 4 + ks]; }, lane, wave);
     __syncthreads();
     // U_jc -> G (write-through: later steps of this and other workgroups read it), its transpose -> the lower copy
 #pragma unroll
@@ -794,14 +802,16 @@ int solve_group_panels(double* G, int64_t ldg, int64_t n, int64_t kb, ColKeep ke
 // rank (row exchange + gbm_dev_chol_strip_unpack_rows); the next diagonal block is factored after
 // the next group's area exchange (gbm_dev_chol_area_* + gbm_dev_chol_factor_diag).
 int solve_group_update(double* G, int64_t ldg, int64_t n, int64_t kb, int rank, int nranks, int32_t* info,
-                       void* workspace, hipStream_t s, int64_t col_lo = 0, int64_t col_hi = INT64_MAX) {
+                       void* workspace, hipStream_t s, int64_t col_lo = 0, int64_t col_hi = INT64_MAX,
+                       int64_t row_lo = 0, int64_t row_hi = INT64_MAX) {
   const int64_t npad = npad_of(n), gdim = gdim_of(n), nb = npad / NB;
   const SolveWs w = solve_ws(workspace, npad);
   const int64_t k0 = kb * NB;
   const int g = group_size(kb, nb, gdim);
   const int64_t next = kb + g < nb ? k0 + g * NB : -1;
   if (g > 1)
-    return launch_chol_update(G, ldg, k0, g * NB, gdim, w.Ld, w.Dinv, info, next, rank, nranks, s, col_lo, col_hi);
+    return launch_chol_update(G, ldg, k0, g * NB, gdim, w.Ld, w.Dinv, info, next, rank, nranks, s, col_lo, col_hi,
+                              row_lo, row_hi);
   if (nranks > 1) return fail(GBM_E_ARG, "gbm_dev_chol_group_update: single-panel steps are not distributed");
   return launch_chol_update(G, ldg, k0, NB, gdim, w.Ld, w.Dinv, info, next, 0, 1, s);
 }
@@ -923,6 +933,17 @@ extern "C" int gbm_dev_chol_group_update_cols(double* G, int64_t ldg, int64_t n,
   if (kb < 0 || kb >= npad_of(n) / NB || nranks < 2 || rank < 0 || rank >= nranks || col_lo < 0 || col_hi < col_lo)
     return fail(GBM_E_ARG, "gbm_dev_chol_group_update_cols: bad step, rank (nranks >= 2) or column range");
   return solve_group_update(G, ldg, n, kb, rank, nranks, info, workspace, (hipStream_t)stream, col_lo, col_hi);
+}
+
+extern "C" int gbm_dev_chol_group_update_tiles(double* G, int64_t ldg, int64_t n, int64_t kb, int rank, int nranks,
+                                               int64_t row_lo, int64_t row_hi, int64_t col_lo, int64_t col_hi,
+                                               int32_t* info, void* workspace, int64_t ws_bytes, void* stream) {
+  GBM_TRY(check_solve_args(G, ldg, n, info, workspace, ws_bytes, "gbm_dev_chol_group_update_tiles"));
+  if (kb < 0 || kb >= npad_of(n) / NB || nranks < 2 || rank < 0 || rank >= nranks || col_lo < 0 || col_hi < col_lo ||
+      row_lo < 0 || row_hi < row_lo)
+    return fail(GBM_E_ARG, "gbm_dev_chol_group_update_tiles: bad step, rank (nranks >= 2), row or column range");
+  return solve_group_update(G, ldg, n, kb, rank, nranks, info, workspace, (hipStream_t)stream, col_lo, col_hi, row_lo,
+                            row_hi);
 }
 
 extern "C" int gbm_dev_chol_factor_diag(double* G, int64_t ldg, int64_t n, int64_t kb, int32_t* info, void* workspace,

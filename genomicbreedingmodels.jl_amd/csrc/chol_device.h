@@ -182,6 +182,9 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t wt_rsrc(const void* p, int64_t
 __device__ __forceinline__ wt_d2 wt_ld2(__amdgpu_buffer_rsrc_t r, uint32_t voff) {
   return __builtin_bit_cast(wt_d2, __builtin_amdgcn_raw_buffer_load_b128(r, (int)voff, 0, kWtSc1));
 }
+__device__ __forceinline__ double wt_ld1(__amdgpu_buffer_rsrc_t r, uint32_t voff) {
+  return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, (int)voff, 0, kWtSc1));
+}
 __device__ __forceinline__ void wt_st2(__amdgpu_buffer_rsrc_t r, uint32_t voff, wt_d2 v) {
   __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(wt_u4, v), r, (int)voff, 0, kWtSc1);
 }

@@ -56,12 +56,14 @@ enum SyrkMode { kSub = 0, kSplit = 1, kPersist = 2 };
 // updates only the 128-column tiles J (absolute, column J·128) with J mod nranks == rank, plus the
 // bordered right-hand-side tile column rhs_tile, which every rank keeps current. The launch grid
 // then covers only those columns: blockIdx.y = c picks the c-th own column J = j_first + c·nranks
-// (c = ncols: the right-hand-side column, when rhs), blockIdx.x the tile row.
+// (c = ncols: the right-hand-side column, when rhs), blockIdx.x the tile row ti0 + blockIdx.x (a row
+// range of the update: the look-ahead updates the next panel group's rows first).
 struct TileOwner {
   int32_t rank = 0, nranks = 1;
   int64_t rhs_tile = -1;
   int64_t j_first = 0, ncols = 0;
   int32_t rhs = 0;
+  int64_t ti0 = 0;
 };
 
 // acc[m][q] += (NEG ? −1 : 1) Σ_k U[k][i0 + ·] U[k][j0 + ·] over the stages [kstep0, kstep0 + nsteps)
@@ -404,7 +406,7 @@ syrk_kernel(const double* __restrict__ U, int64_t ldu, int64_t K, int64_t c0, in
       const int64_t c = blockIdx.y;
       const int64_t J = c < own.ncols ? own.j_first + c * own.nranks : own.rhs_tile;
       tj = J - c0 / BT;
-      ti = blockIdx.x;
+      ti = own.ti0 + blockIdx.x;
       if (ti > tj) return;  // (workgroup-uniform) below the diagonal
     } else {
       tile_of(wg, ti, tj);
@@ -858,14 +860,14 @@ int launch_chol_row_update(double* G, int64_t ldg, int64_t k0, int kch, int64_t 
 // after the ranks exchange its area (gbm_dev_chol_area_*).
 int launch_chol_update(double* G, int64_t ldg, int64_t k0, int64_t nb, int64_t gdim, double* Ld, double* Dinv,
                        int32_t* info, int64_t next_k0, int rank, int nranks, hipStream_t s, int64_t col_lo,
-                       int64_t col_hi) {
+                       int64_t col_hi, int64_t row_lo, int64_t row_hi) {
   const int64_t k1 = k0 + nb;
   const int64_t lim = gdim - k1;
   if (lim <= 0) return GBM_OK;
   TileOwner own;
   if (nranks > 1) {
-    if ((k1 % BT) != 0 || nb == 64 || (col_lo % BT) != 0)
-      return fail(GBM_E_ARG, "distributed Cholesky update: panel groups and column ranges on 128-column tiles");
+    if ((k1 % BT) != 0 || nb == 64 || (col_lo % BT) != 0 || (row_lo % BT) != 0)
+      return fail(GBM_E_ARG, "distributed Cholesky update: panel groups, column and row ranges on 128-column tiles");
     own.rank = rank;
     own.nranks = nranks;
     own.rhs_tile = (gdim - kRhsRows) / BT;
@@ -875,7 +877,11 @@ int launch_chol_update(double* G, int64_t ldg, int64_t k0, int64_t nb, int64_t g
     own.ncols = own.j_first < jhi ? (jhi - own.j_first + nranks - 1) / nranks : 0;
     own.rhs = col_hi >= gdim ? 1 : 0;
     if (own.ncols + own.rhs == 0) return GBM_OK;
-    const int64_t m = (lim + BT - 1) / BT;
+    // row tiles [ti0, ti1) of the update (rows [row_lo, row_hi) ∩ [k1, gdim))
+    own.ti0 = (std::max(row_lo, k1) - k1) / BT;
+    const int64_t ti1 = (std::min(row_hi, gdim) - k1 + BT - 1) / BT;
+    if (ti1 <= own.ti0) return GBM_OK;
+    const int64_t m = ti1 - own.ti0;
     syrk_kernel<kSub><<<dim3((unsigned)m, (unsigned)(own.ncols + own.rhs)), 256, 0, s>>>(
         G + k0 * ldg, ldg, nb, k1, lim, G, ldg, nullptr, 0, SliceBounds{}, Ld, Dinv, info, -1, own);
     GBM_LAUNCH_CHECK();

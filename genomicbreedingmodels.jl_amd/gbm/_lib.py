@@ -11,7 +11,7 @@ import threading
 
 import numpy as np
 
-ABI_VERSION = 210  # GBM_VERSION in include/gbm.h
+ABI_VERSION = 211  # GBM_VERSION in include/gbm.h
 GBM_OK = 0
 GBM_E_ARG = -1
 GBM_E_NOTPD = -2
@@ -42,7 +42,7 @@ EXPORTS = (
     "gbm_dev_synth_dosage_i8", "gbm_dev_standardize_i8", "gbm_dev_grm_accumulate", "gbm_dev_marker_effects_i8",
     "gbm_debug_oom_retries", "gbm_dev_chol_group_panels", "gbm_dev_chol_group_update", "gbm_dev_chol_strip_unpack_rows",
     "gbm_dev_chol_area_doubles", "gbm_dev_chol_area_pack", "gbm_dev_chol_area_unpack",
-    "gbm_dev_chol_group_update_cols", "gbm_dev_grm_exact_workspace", "gbm_dev_grm_exact_i8",
+    "gbm_dev_chol_group_update_cols", "gbm_dev_chol_group_update_tiles", "gbm_dev_grm_exact_workspace", "gbm_dev_grm_exact_i8",
     "gbm_gblup_fit_ex", "gbm_gblup_fit_reml_ex", "gbm_gblup_fit_dosage_i8_ex", "gbm_gblup_fit_synthetic_ex",
     "gbm_session_set_grm_mode", "gbm_session_grm_used", "gbm_debug_rccl_calls", "gbm_debug_xg_choose", "gbm_debug_chol_flow_order",
     "gbm_debug_chol_flow_order_check", "gbm_debug_chol_flow_order_size",
@@ -103,6 +103,8 @@ def _declare(lib):
         getattr(lib, f).argtypes = [P, I64, I64, I64, I32, I32, P, P, I64, P]
     lib.gbm_dev_chol_group_update_cols.restype = I32
     lib.gbm_dev_chol_group_update_cols.argtypes = [P, I64, I64, I64, I32, I32, I64, I64, P, P, I64, P]
+    lib.gbm_dev_chol_group_update_tiles.restype = I32
+    lib.gbm_dev_chol_group_update_tiles.argtypes = [P, I64, I64, I64, I32, I32, I64, I64, I64, I64, P, P, I64, P]
     lib.gbm_dev_chol_area_doubles.restype = I64
     lib.gbm_dev_chol_area_doubles.argtypes = [I64, I64, I64, I32]
     lib.gbm_dev_chol_area_pack.restype = I32

@@ -125,7 +125,10 @@ def chol_distributed(stages, ranks, nranks, allgather, tail_rows=None, force=Fal
     all-gathered (strip_unpack_rows also writes their lower copy), then the trailing update runs on
     the rank's own tiles and the right-hand sides (gbm_dev_chol_group_update). With overlap
     (GBM_DIST_OVERLAP, default 1; stages with fork/side/join), the next group's area is updated and
-    exchanged on a side stream while the rest of the update runs (gbm_dev_chol_group_update_cols).
+    exchanged on a side stream while the rest of the update runs (gbm_dev_chol_group_update_cols); with
+    look-ahead (GBM_DIST_LOOKAHEAD, default 1) the next group's rows are updated first and its panels and
+    row exchange run on the side stream too, beside the rest of the update
+    (gbm_dev_chol_group_update_tiles).
     Once the trailing matrix is small (``tail_rows``, GBM_DIST_TAIL_ROWS, default 8192) or the groups
     shrink to single panels, every remaining row is gathered once and the tail runs redundantly. The
     result is bit-identical to the redundant solve (the same kernels compute every tile).
@@ -179,10 +182,12 @@ def chol_distributed(stages, ranks, nranks, allgather, tail_rows=None, force=Fal
         for st in stages:
             st.chol_finish()
         return
+    lookahead = overlap and int(os.environ.get("GBM_DIST_LOOKAHEAD", "1")) != 0
     kb = 0
     dist = nranks > 1 and distributable(0)
     stale = False  # a distributed update skipped other ranks' tiles
-    pending = False  # this group's area is being exchanged on the side stream
+    pending = False  # this group's area (look-ahead: also its panels and rows) is on the side stream
+    ahead = False  # (look-ahead) this group's panels and row exchange were issued on the side stream
     while kb < nb:
         g = int(lib.gbm_dev_chol_group_size(n, kb))
         if not dist:
@@ -196,23 +201,41 @@ def chol_distributed(stages, ranks, nranks, allgather, tail_rows=None, force=Fal
             pending = False
         elif stale:
             exchange(kb, g, "area")
-        for st, r in zip(stages, ranks):
-            st.chol_group_panels(kb, r, nranks)
-        exchange(kb, g, "rows")
+        if not ahead:
+            for st, r in zip(stages, ranks):
+                st.chol_group_panels(kb, r, nranks)
+            exchange(kb, g, "rows")
+        ahead = False
         k1 = kb + g
         next_dist = k1 < nb and distributable(k1)
         if overlap and next_dist:
             # the next group's area (a rank owns about one of its tile columns: a few workgroups, one K = 64 g
             # tile long) is updated and exchanged on the side stream, beside the rest of the update
-            area_hi = 64 * (k1 + int(lib.gbm_dev_chol_group_size(n, k1)))
+            g1 = int(lib.gbm_dev_chol_group_size(n, k1))
+            area_hi = 64 * (k1 + g1)
             for st in stages:
                 st.fork()
             with stages[0].side():  # (one side stream per device)
                 for st, r in zip(stages, ranks):
                     st.chol_group_update_cols(kb, r, nranks, 64 * k1, area_hi)
-                exchange(k1, int(lib.gbm_dev_chol_group_size(n, k1)), "area")
-            for st, r in zip(stages, ranks):
-                st.chol_group_update_cols(kb, r, nranks, area_hi, gdim)
+                exchange(k1, g1, "area")
+            if lookahead:
+                # look-ahead: the next group's rows first; its panels and row exchange then run on the side
+                # stream beside the rest of the update (rows from area_hi on: disjoint tiles)
+                for st, r in zip(stages, ranks):
+                    st.chol_group_update_tiles(kb, r, nranks, 64 * k1, area_hi, area_hi, gdim)
+                for st in stages:
+                    st.fork()
+                with stages[0].side():
+                    for st, r in zip(stages, ranks):
+                        st.chol_group_panels(k1, r, nranks)
+                    exchange(k1, g1, "rows")
+                for st, r in zip(stages, ranks):
+                    st.chol_group_update_tiles(kb, r, nranks, area_hi, gdim, area_hi, gdim)
+                ahead = True
+            else:
+                for st, r in zip(stages, ranks):
+                    st.chol_group_update_cols(kb, r, nranks, area_hi, gdim)
             pending = True
         else:
             for st, r in zip(stages, ranks):
@@ -375,13 +398,21 @@ class HipShardStages:
                                                            col_hi, self._p(self.info), self._p(self.ws_solve),
                                                            self.ws_solve_bytes, self._stream()), "chol_group_update_cols")
 
-    # the distributed solve's side stream (one per device, shared by the stages of a rehearsal):
+    def chol_group_update_tiles(self, kb: int, rank: int, nranks: int, row_lo: int, row_hi: int, col_lo: int,
+                                col_hi: int):
+        _lib.check(self.lib.gbm_dev_chol_group_update_tiles(self._p(self.G), self.gdim, self.n, kb, rank, nranks,
+                                                            row_lo, row_hi, col_lo, col_hi, self._p(self.info),
+                                                            self._p(self.ws_solve), self.ws_solve_bytes,
+                                                            self._stream()), "chol_group_update_tiles")
+
+    # the distributed solve's side stream (one per device, shared by the stages of a rehearsal; high
+    # priority: the look-ahead's panels are latency-bound beside the trailing update):
     # fork = the side stream waits for this device's current stream; side() = a context in which
     # the stage methods (and a torch collective) run on it; join = the current stream waits for it
     def _side_stream(self):
         s = _SIDE_STREAMS.get(self.dev)
         if s is None:
-            s = _SIDE_STREAMS[self.dev] = self.torch.cuda.Stream(self.dev)
+            s = _SIDE_STREAMS[self.dev] = self.torch.cuda.Stream(self.dev, priority=-1)
         return s
 
     def fork(self):

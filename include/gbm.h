@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define GBM_VERSION 210 /* 0.2.1: per-call GRM mode (the _ex entries), 1-rank RCCL test hook */
+#define GBM_VERSION 211 /* 0.2.1.1: row-range trailing update (distributed solve look-ahead) */
 
 #define GBM_OK 0
 #define GBM_E_ARG (-1)    /* bad argument (ArgumentError on the Julia side, src/prediction.jl:67-127 style) */
@@ -342,6 +342,12 @@ int gbm_dev_chol_group_update(double* G, int64_t ldg, int64_t n, int64_t kb, int
 int gbm_dev_chol_group_update_cols(double* G, int64_t ldg, int64_t n, int64_t kb, int rank, int nranks,
                                    int64_t col_lo, int64_t col_hi, int32_t* info, void* workspace, int64_t ws_bytes,
                                    void* stream);
+/* group_update_cols further restricted to the rows [row_lo, row_hi) (row_lo on a 128-row tile): the
+ * look-ahead updates the next group's rows first, so that group's panels (group_panels) and row exchange
+ * run beside the rest of the update (rows from the end of the next group on). */
+int gbm_dev_chol_group_update_tiles(double* G, int64_t ldg, int64_t n, int64_t kb, int rank, int nranks,
+                                    int64_t row_lo, int64_t row_hi, int64_t col_lo, int64_t col_hi, int32_t* info,
+                                    void* workspace, int64_t ws_bytes, void* stream);
 int gbm_dev_chol_factor_diag(double* G, int64_t ldg, int64_t n, int64_t kb, int32_t* info, void* workspace,
                              int64_t ws_bytes, void* stream);
 /* Doubles per rank of the strip of rows [64 kb, 64 (kb + rows64)) over the tiles from column 64 kb. */

@@ -34,7 +34,7 @@ def test_library_exports_every_header_symbol():
 
 def test_library_loads_and_reports_version():
     lib = gbm.load_library()
-    assert lib.gbm_version() == 210
+    assert lib.gbm_version() == 211
     assert isinstance(_lib.last_error(), str)
     for s in _lib.EXPORTS:
         assert hasattr(lib, s)
@@ -92,6 +92,8 @@ def test_distributed_phase_entry_points_check_their_arguments():
     # the column-range update needs nranks >= 2 and an ordered range
     assert lib.gbm_dev_chol_group_update_cols(G, gdim, n, 0, 0, 1, 0, gdim, info, ws, ws_bytes, None) == E
     assert lib.gbm_dev_chol_group_update_cols(G, gdim, n, 0, 0, 2, 512, 256, info, ws, ws_bytes, None) == E
+    assert lib.gbm_dev_chol_group_update_tiles(G, gdim, n, 0, 0, 1, 0, gdim, 0, gdim, info, ws, ws_bytes, None) == E
+    assert lib.gbm_dev_chol_group_update_tiles(G, gdim, n, 0, 0, 2, 256, 128, 0, gdim, info, ws, ws_bytes, None) == E
     # a rank outside [0, nranks)
     assert lib.gbm_dev_chol_group_panels(G, gdim, n, 0, 2, 2, info, ws, ws_bytes, None) == E
     assert lib.gbm_dev_chol_group_update(G, gdim, n, 0, -1, 2, info, ws, ws_bytes, None) == E

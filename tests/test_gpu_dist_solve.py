@@ -43,6 +43,7 @@ def _stages(R, X, Y, lam):
     (4, 1030, ("0", "0", "0"), 512),       # ragged n, early switch to the redundant tail
     (8, 3000, ("0", "0", "0"), "0-seq"),   # as above without the side-stream area exchange
     (8, 3000, ("0", "0", "0"), "0-chain"),  # the panel phase as panel / row-update launches, not one group launch
+    (8, 3000, ("0", "0", "0"), "0-nolook"),  # the next group's panels after the whole trailing update (no look-ahead)
 ])
 def test_distributed_factorisation_bit_identical(monkeypatch, R, n, lims, tail):
     import torch
@@ -53,8 +54,10 @@ def test_distributed_factorisation_bit_identical(monkeypatch, R, n, lims, tail):
     monkeypatch.setenv("GBM_CHOL_G16_LIM", lims[2])
     monkeypatch.setenv("GBM_UPD64_LIM", "128")
     monkeypatch.setenv("GBM_CHOL_FLOW_MAX", "0")  # reference: the redundant launch-per-panel solve
-    if isinstance(tail, str):  # "<rows>-seq": GBM_DIST_OVERLAP = 0; "<rows>-chain": GBM_CHOL_GROUP_KERNEL = 0
-        monkeypatch.setenv("GBM_DIST_OVERLAP" if tail.endswith("seq") else "GBM_CHOL_GROUP_KERNEL", "0")
+    if isinstance(tail, str):  # "<rows>-seq" / "-chain" / "-nolook": GBM_DIST_OVERLAP / GBM_CHOL_GROUP_KERNEL /
+        # GBM_DIST_LOOKAHEAD = 0
+        var = {"seq": "GBM_DIST_OVERLAP", "chain": "GBM_CHOL_GROUP_KERNEL", "nolook": "GBM_DIST_LOOKAHEAD"}
+        monkeypatch.setenv(var[tail.split("-")[1]], "0")
         tail = int(tail.split("-")[0])
     X = oracle.synth_genotypes(n + R, n, 1200)
     Y = oracle.synth_phenotypes(X, 3, ntraits=2)

@@ -135,26 +135,32 @@ class NumpyShardStages:
             for ch in chunks(NB * (k + 1)):
                 V[r, ch] = sla.solve_triangular(V[r, r], V[r, ch], trans="T", lower=False)
 
-    def chol_group_update(self, kb, rank, nranks, col_lo=0, col_hi=None):
+    def chol_group_update(self, kb, rank, nranks, col_lo=0, col_hi=None, row_lo=0, row_hi=None):
         """The trailing update on the rank's own tiles and the right-hand sides; on one rank the next
         diagonal block is factored too (gbm_dev_chol_group_update). col_lo/col_hi: the rank's tiles
         with columns in [col_lo, col_hi), the right-hand sides when col_hi >= gdim
-        (gbm_dev_chol_group_update_cols)."""
+        (gbm_dev_chol_group_update_cols); row_lo/row_hi: the rows [row_lo, row_hi) of those tiles
+        (gbm_dev_chol_group_update_tiles)."""
         V, npad, nb = self.V, self.npad, self.npad // NB
         g = self.lib.gbm_dev_chol_group_size(self.n, kb)
         k0, k1 = NB * kb, NB * (kb + g)
         col_hi = self.gdim if col_hi is None else col_hi
+        row_hi = self.gdim if row_hi is None else row_hi
         keep = lambda c: (nranks == 1 or (c // TB) % nranks == rank) and col_lo <= c < col_hi
         for ch in self._chunks(k1, keep):
             if ch.start >= npad and col_hi < self.gdim:
                 continue  # the right-hand sides belong to the call that reaches gdim
-            rend = min(ch.stop, npad)
-            V[k1:rend, ch] -= V[k0:k1, k1:rend].T @ V[k0:k1, ch]
+            r0, rend = max(k1, row_lo), min(ch.stop, npad, row_hi)
+            if rend > r0:
+                V[r0:rend, ch] -= V[k0:k1, r0:rend].T @ V[k0:k1, ch]
         if nranks == 1 and kb + g < nb:
             self.chol_factor_diag(kb + g)
 
     def chol_group_update_cols(self, kb, rank, nranks, col_lo, col_hi):
         self.chol_group_update(kb, rank, nranks, col_lo, col_hi)
+
+    def chol_group_update_tiles(self, kb, rank, nranks, row_lo, row_hi, col_lo, col_hi):
+        self.chol_group_update(kb, rank, nranks, col_lo, col_hi, row_lo, row_hi)
 
     # the overlap hooks of chol_distributed (streams on the GPU; here the calls run in order)
     def fork(self):
