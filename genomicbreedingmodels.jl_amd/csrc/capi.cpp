@@ -920,8 +920,9 @@ int solve_distributed(std::vector<std::unique_ptr<Shard>>& shards, const std::ve
     }
     return GBM_OK;
   };
-  auto distributable = [&](int64_t kb) {
-    return gdim - kCholNB * kb > tail_rows && gbm_dev_chol_group_size(n, kb) >= 2 && (kCholNB * kb) % 128 == 0;
+  auto distributable = [&](int64_t kb) {  // (a group reaching the end is the dataflow tail, GBM_CHOL_TAIL_FLOW)
+    const int64_t g = gbm_dev_chol_group_size(n, kb);
+    return gdim - kCholNB * kb > tail_rows && g >= 2 && g < nb - kb && (kCholNB * kb) % 128 == 0;
   };
   // rows [64 kb, 64 (kb + rows64)) of every leader's own tiles, all-gathered. kRows: final U rows
   // (their lower copy completed too); kRest: the trailing matrix's remaining rows (the tail switch);

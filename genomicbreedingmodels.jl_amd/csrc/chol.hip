@@ -698,10 +698,26 @@ int check_solve_args(const double* G, int64_t ldg, int64_t n, const int32_t* inf
   return GBM_OK;
 }
 
+// Remaining rows (64 kb .. gdim) at or below which the launch-per-panel path hands the rest of the
+// factorisation to ONE dataflow launch on the trailing sub-matrix (chol_flow.hip: the remainder is itself a
+// bordered matrix, the right-hand sides its last tile column). GBM_CHOL_TAIL_FLOW, re-read per call; by
+// default 8192 when the whole matrix was too large for the dataflow launch (npad > 12 288), else 0 (off).
+// Never the whole matrix (kb > 0).
+static int64_t tail_flow_rows(int64_t npad) {
+  const char* e = getenv("GBM_CHOL_TAIL_FLOW");
+  if (e) return (int64_t)atoll(e);
+  return npad > 12288 ? 8192 : 0;
+}
+static bool tail_flow_at(int64_t kb, int64_t npad, int64_t gdim) {
+  return kb > 0 && kb < npad / NB && gdim - kb * NB <= tail_flow_rows(npad);
+}
+
 // Panels per group of the factorisation step at 64-block kb: groups of g panels share one K = 64g
 // trailing update (HBM/MALL-bound at K = 64, balanced at K = 128, MFMA-bound at K = 256). The
 // thresholds are read at every call, so tests can force the grouped paths on small matrices.
+// At the dataflow tail (tail_flow_at): every remaining panel, one group.
 int group_size(int64_t kb, int64_t nb, int64_t gdim) {
+  if (tail_flow_at(kb, nb * NB, gdim)) return (int)(nb - kb);
   auto lim = [](const char* name, int64_t dflt) {
     const char* e = getenv(name);
     return e ? (int64_t)atoll(e) : dflt;
@@ -750,6 +766,8 @@ int solve_group_panels(double* G, int64_t ldg, int64_t n, int64_t kb, ColKeep ke
   const int64_t npad = npad_of(n), gdim = gdim_of(n), nb = npad / NB;
   const SolveWs w = solve_ws(workspace, npad);
   const int64_t k0 = kb * NB;
+  if (tail_flow_at(kb, npad, gdim))
+    return fail(GBM_E_ARG, "gbm_dev_chol_group_panels: the dataflow tail (GBM_CHOL_TAIL_FLOW) runs as gbm_dev_chol_group");
   const int g = group_size(kb, nb, gdim);
   if (keep.nranks > 1) {
     if (g < 2 || (k0 % 128) != 0)
@@ -807,6 +825,8 @@ int solve_group_update(double* G, int64_t ldg, int64_t n, int64_t kb, int rank, 
   const int64_t npad = npad_of(n), gdim = gdim_of(n), nb = npad / NB;
   const SolveWs w = solve_ws(workspace, npad);
   const int64_t k0 = kb * NB;
+  if (tail_flow_at(kb, npad, gdim))
+    return fail(GBM_E_ARG, "gbm_dev_chol_group_update: the dataflow tail (GBM_CHOL_TAIL_FLOW) runs as gbm_dev_chol_group");
   const int g = group_size(kb, nb, gdim);
   const int64_t next = kb + g < nb ? k0 + g * NB : -1;
   if (g > 1)
@@ -819,6 +839,16 @@ int solve_group_update(double* G, int64_t ldg, int64_t n, int64_t kb, int rank, 
 // One whole panel group on one rank (the redundant factorisation and the distributed one's tail).
 int solve_group(double* G, int64_t ldg, int64_t n, int64_t kb, int32_t* info, void* workspace, hipStream_t s,
                 int64_t* g_out) {
+  const int64_t npad = npad_of(n), gdim = gdim_of(n);
+  if (tail_flow_at(kb, npad, gdim)) {
+    // the rest in one dataflow launch on the trailing sub-matrix (its first diagonal block, already
+    // factored by the last trailing update or factor_diag, is factored again from the same A)
+    const SolveWs w = solve_ws(workspace, npad);
+    const int64_t k0 = kb * NB;
+    if (g_out) *g_out = npad / NB - kb;
+    return launch_chol_flow(G + k0 * ldg + k0, ldg, gdim - k0, w.Ld + k0 * CNB, w.Dinv + (k0 / 16) * 256, w.flow,
+                            info, s);
+  }
   GBM_TRY(solve_group_panels(G, ldg, n, kb, ColKeep{}, info, workspace, s, g_out));
   return solve_group_update(G, ldg, n, kb, 0, 1, info, workspace, s);
 }

@@ -145,8 +145,9 @@ def chol_distributed(stages, ranks, nranks, allgather, tail_rows=None, force=Fal
     if tail_rows is None:
         tail_rows = int(os.environ.get("GBM_DIST_TAIL_ROWS", "8192"))
 
-    def distributable(kb):
-        return (gdim - 64 * kb > tail_rows and lib.gbm_dev_chol_group_size(n, kb) >= 2 and (64 * kb) % 128 == 0)
+    def distributable(kb):  # (a group reaching the end is the dataflow tail, GBM_CHOL_TAIL_FLOW)
+        g = lib.gbm_dev_chol_group_size(n, kb)
+        return gdim - 64 * kb > tail_rows and 2 <= g < nb - kb and (64 * kb) % 128 == 0
 
     overlap = int(os.environ.get("GBM_DIST_OVERLAP", "1")) != 0 and all(hasattr(st, "fork") for st in stages)
 
