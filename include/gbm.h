@@ -317,7 +317,8 @@ int gbm_dev_gblup_solve(double* G, int64_t ldg, int64_t n, double inv_q, const i
  *                                   rank then holds the group's final rows at every column (and their
  *                                   lower copy, which the back substitution reads);
  *   group_update(kb, rank, nranks)  the trailing update on the rank's own tiles and the right-hand
- *                                   sides — 1/nranks of the O(n³) work per rank.
+ *                                   sides — 1/nranks of the O(n³) work per rank (or group_update_tiles
+ *                                   over row ranges: the look-ahead, see below).
  * Before switching back to nranks = 1 for the tail, the ranks exchange every remaining row once
  * (strip_pack → all-gather → strip_unpack) and factor its first diagonal block (factor_diag).
  * gbm_dev_chol_group itself takes rank 0 of 1 only (the arguments stay for ABI stability).
@@ -327,7 +328,9 @@ int gbm_dev_gblup_solve(double* G, int64_t ldg, int64_t n, double inv_q, const i
 int gbm_dev_chol_prepare(double* G, int64_t ldg, int64_t n, double inv_q, const int64_t* q_dev, double lambda,
                          const double* Y, int64_t ldy, int64_t nrhs, int32_t* info, void* workspace,
                          int64_t ws_bytes, void* stream);
-/* Panels in the group that starts at 64-row block kb (0 past the end). */
+/* Panels in the group that starts at 64-row block kb (0 past the end). At the dataflow tail (at most
+ * GBM_CHOL_TAIL_FLOW rows left, default 8192 when npad > 12 288; never kb = 0) every remaining panel:
+ * gbm_dev_chol_group then factors the rest in one launch, and group_panels / group_update refuse it. */
 int64_t gbm_dev_chol_group_size(int64_t n, int64_t kb);
 int gbm_dev_chol_group(double* G, int64_t ldg, int64_t n, int64_t kb, int rank, int nranks, int32_t* info,
                        void* workspace, int64_t ws_bytes, void* stream);
