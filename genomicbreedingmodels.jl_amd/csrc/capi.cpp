@@ -956,9 +956,13 @@ int solve_distributed(std::vector<std::unique_ptr<Shard>>& shards, const std::ve
       return gbm_dev_chol_factor_diag((double*)c.G.p, gdim, n, kb, (int32_t*)c.info.p, c.wss.p, c.wss.cap, c.stream.s);
     });
   };
-  GBM_TRY(each([&](int, FitCtx& c) {
-    return gbm_dev_chol_prepare((double*)c.G.p, gdim, n, inv_q, nullptr, lambda, (const double*)c.Y.p, npad, nrhs,
-                                (int32_t*)c.info.p, c.wss.p, c.wss.cap, c.stream.s);
+  // V only on the columns each leader reads before an exchange overwrites them, when the factorisation
+  // distributes from the first group on
+  const bool dist0 = R > 1 && distributable(0);
+  GBM_TRY(each([&](int r, FitCtx& c) {
+    return gbm_dev_chol_prepare_cols((double*)c.G.p, gdim, n, inv_q, nullptr, lambda, (const double*)c.Y.p, npad,
+                                     nrhs, dist0 ? r : 0, dist0 ? R : 1, (int32_t*)c.info.p, c.wss.p, c.wss.cap,
+                                     c.stream.s);
   }));
   if (R == 1) {
     // one leader (GBM_FORCE_RCCL): the redundant solve, each distributable group's final rows passed

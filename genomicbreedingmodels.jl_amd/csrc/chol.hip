@@ -37,17 +37,21 @@ int launch_chol_flow(double* G, int64_t ldg, int64_t gdim, double* Ld, double* D
                      hipStream_t s);
 
 // ---- V = G/q + λI (upper part), padding = identity, bordered R columns -----------------------
+// keep (a distributed factorisation, nranks > 1): only the columns the rank reads before an exchange
+// overwrites them — its own 128-column tiles, the first panel group's area (< keep_hi) and the
+// right-hand sides; the other columns keep G until the exchanges bring their owners' rows.
 __global__ void __launch_bounds__(256) prepare_v_kernel(double* __restrict__ G, int64_t ld, int64_t n,
                                                         int64_t npad, int64_t gdim, double inv_q,
                                                         const int64_t* __restrict__ q_dev, double lambda,
                                                         const double* __restrict__ Y, int64_t ldy, int64_t nrhs,
-                                                        int32_t* __restrict__ info) {
+                                                        int32_t* __restrict__ info, ColKeep keep) {
   const int64_t i = blockIdx.x;  // row
   if (i == 0 && threadIdx.x == 0) *info = 0;
   if (q_dev) inv_q = 1.0 / (double)(*q_dev);
   double* row = G + i * ld;
   const int64_t jbeg = (i / NB) * NB;  // from the start of the diagonal block
   for (int64_t j = jbeg + threadIdx.x; j < gdim; j += 256) {
+    if (keep.nranks > 1 && !col_kept(keep, j)) continue;
     double v = 0.0;
     if (i < npad) {
       if (j < i) v = 0.0;
@@ -736,11 +740,12 @@ int group_size(int64_t kb, int64_t nb, int64_t gdim) {
 
 int solve_prepare(double* G, int64_t ldg, int64_t n, double inv_q, const int64_t* q_dev, double lambda,
                   const double* Y, int64_t ldy, int64_t nrhs, int32_t* info, void* workspace, hipStream_t s,
-                  bool factor_first = true) {
+                  bool factor_first = true, ColKeep keep = ColKeep{}) {
   const int64_t npad = npad_of(n), gdim = gdim_of(n);
   const SolveWs w = solve_ws(workspace, npad);
   chol_refresh_tuning();
-  prepare_v_kernel<<<(unsigned)gdim, 256, 0, s>>>(G, ldg, n, npad, gdim, inv_q, q_dev, lambda, Y, ldy, nrhs, info);
+  prepare_v_kernel<<<(unsigned)gdim, 256, 0, s>>>(G, ldg, n, npad, gdim, inv_q, q_dev, lambda, Y, ldy, nrhs, info,
+                                                  keep);
   GBM_LAUNCH_CHECK();
   if (!factor_first) return GBM_OK;
   factor_diag_kernel<<<1, 256, 0, s>>>(G, ldg, 0, w.Ld, w.Dinv, info);
@@ -919,6 +924,24 @@ extern "C" int gbm_dev_chol_prepare(double* G, int64_t ldg, int64_t n, double in
     return fail(GBM_E_ARG, "gbm_dev_chol_prepare: bad arguments");
   GBM_TRY(check_solve_args(G, ldg, n, info, workspace, ws_bytes, "gbm_dev_chol_prepare"));
   return solve_prepare(G, ldg, n, inv_q, q_dev, lambda, Y, ldy, nrhs, info, workspace, (hipStream_t)stream);
+}
+
+extern "C" int gbm_dev_chol_prepare_cols(double* G, int64_t ldg, int64_t n, double inv_q, const int64_t* q_dev,
+                                         double lambda, const double* Y, int64_t ldy, int64_t nrhs, int rank,
+                                         int nranks, int32_t* info, void* workspace, int64_t ws_bytes, void* stream) {
+  if (!Y || ldy < n || nrhs < 1 || nrhs > MAXRHS || !(lambda > 0.0) || !(q_dev || inv_q > 0.0) || nranks < 1 ||
+      rank < 0 || rank >= nranks)
+    return fail(GBM_E_ARG, "gbm_dev_chol_prepare_cols: bad arguments");
+  GBM_TRY(check_solve_args(G, ldg, n, info, workspace, ws_bytes, "gbm_dev_chol_prepare_cols"));
+  ColKeep keep;
+  keep.rank = rank;
+  keep.nranks = nranks;
+  if (nranks > 1) {
+    chol_refresh_tuning();
+    keep.keep_hi = (int64_t)group_size(0, npad_of(n) / NB, gdim_of(n)) * NB;  // the first group's area
+    keep.rhs0 = npad_of(n);
+  }
+  return solve_prepare(G, ldg, n, inv_q, q_dev, lambda, Y, ldy, nrhs, info, workspace, (hipStream_t)stream, true, keep);
 }
 
 extern "C" int64_t gbm_dev_chol_group_size(int64_t n, int64_t kb) {

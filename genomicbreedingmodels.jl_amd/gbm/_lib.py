@@ -35,7 +35,7 @@ EXPORTS = (
     "gbm_session_create", "gbm_session_create_dosage_i8", "gbm_session_create_synthetic", "gbm_session_destroy", "gbm_session_gblup_fit",
     "gbm_session_predict", "gbm_session_reml_objective", "gbm_session_reml", "gbm_session_stats",
     "gbm_session_ridge_path", "gbm_session_ridge_lambda_max", "gbm_brr_fit",
-    "gbm_dev_chol_prepare", "gbm_dev_chol_group_size", "gbm_dev_chol_group", "gbm_dev_chol_factor_diag",
+    "gbm_dev_chol_prepare", "gbm_dev_chol_prepare_cols", "gbm_dev_chol_group_size", "gbm_dev_chol_group", "gbm_dev_chol_factor_diag",
     "gbm_dev_chol_strip_doubles", "gbm_dev_chol_strip_pack", "gbm_dev_chol_strip_unpack", "gbm_dev_chol_finish",
     "gbm_dev_grm_packed_size", "gbm_dev_grm_pack", "gbm_dev_grm_unpack",
     "gbm_debug_brr_stats", "gbm_debug_brr_shape", "gbm_debug_brr_trace", "gbm_debug_chol_flow_trace",
@@ -94,6 +94,8 @@ def _declare(lib):
     lib.gbm_release_device_cache.argtypes = []
     lib.gbm_dev_chol_prepare.restype = I32
     lib.gbm_dev_chol_prepare.argtypes = [P, I64, I64, D, P, D, P, I64, I64, P, P, I64, P]
+    lib.gbm_dev_chol_prepare_cols.restype = I32
+    lib.gbm_dev_chol_prepare_cols.argtypes = [P, I64, I64, D, P, D, P, I64, I64, I32, I32, P, P, I64, P]
     lib.gbm_dev_chol_group_size.restype = I64
     lib.gbm_dev_chol_group_size.argtypes = [I64, I64]
     lib.gbm_dev_chol_group.restype = I32

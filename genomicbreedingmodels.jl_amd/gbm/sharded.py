@@ -164,8 +164,12 @@ def chol_distributed(stages, ranks, nranks, allgather, tail_rows=None, force=Fal
                 st.strip_unpack(kb, rows64, nranks, gathered)
             st.chol_factor_diag(kb)
 
-    for st in stages:
-        st.chol_prepare()
+    if nranks > 1 and distributable(0):
+        for st, r in zip(stages, ranks):  # V on the columns this rank reads before an exchange only
+            st.chol_prepare_cols(r, nranks)
+    else:
+        for st in stages:
+            st.chol_prepare()
     if nranks == 1 and force:
         kb = 0
         while kb < nb:
@@ -383,6 +387,12 @@ class HipShardStages:
                                                  self._p(self.Y), self.npad, self.nrhs, self._p(self.info),
                                                  self._p(self.ws_solve), self.ws_solve_bytes, self._stream()),
                    "chol_prepare")
+
+    def chol_prepare_cols(self, rank: int, nranks: int):
+        _lib.check(self.lib.gbm_dev_chol_prepare_cols(self._p(self.G), self.gdim, self.n, 0.0, self._p(self.q),
+                                                      self.lam, self._p(self.Y), self.npad, self.nrhs, rank, nranks,
+                                                      self._p(self.info), self._p(self.ws_solve), self.ws_solve_bytes,
+                                                      self._stream()), "chol_prepare_cols")
 
     def chol_group(self, kb: int, rank: int, nranks: int):
         _lib.check(self.lib.gbm_dev_chol_group(self._p(self.G), self.gdim, self.n, kb, rank, nranks, self._p(self.info),

@@ -328,6 +328,12 @@ int gbm_dev_gblup_solve(double* G, int64_t ldg, int64_t n, double inv_q, const i
 int gbm_dev_chol_prepare(double* G, int64_t ldg, int64_t n, double inv_q, const int64_t* q_dev, double lambda,
                          const double* Y, int64_t ldy, int64_t nrhs, int32_t* info, void* workspace,
                          int64_t ws_bytes, void* stream);
+/* gbm_dev_chol_prepare for rank `rank` of a distributed factorisation (nranks > 1): V only on the columns
+ * the rank reads before an exchange overwrites them (its own 128-column tiles, the first panel group's
+ * area, the right-hand sides); nranks = 1 is gbm_dev_chol_prepare. */
+int gbm_dev_chol_prepare_cols(double* G, int64_t ldg, int64_t n, double inv_q, const int64_t* q_dev, double lambda,
+                              const double* Y, int64_t ldy, int64_t nrhs, int rank, int nranks, int32_t* info,
+                              void* workspace, int64_t ws_bytes, void* stream);
 /* Panels in the group that starts at 64-row block kb (0 past the end). At the dataflow tail (at most
  * GBM_CHOL_TAIL_FLOW rows left, default 8192 when npad > 12 288; never kb = 0) every remaining panel:
  * gbm_dev_chol_group then factors the rest in one launch, and group_panels / group_update refuse it. */

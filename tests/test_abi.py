@@ -93,6 +93,7 @@ def test_distributed_phase_entry_points_check_their_arguments():
     assert lib.gbm_dev_chol_group_update_cols(G, gdim, n, 0, 0, 1, 0, gdim, info, ws, ws_bytes, None) == E
     assert lib.gbm_dev_chol_group_update_cols(G, gdim, n, 0, 0, 2, 512, 256, info, ws, ws_bytes, None) == E
     assert lib.gbm_dev_chol_group_update_tiles(G, gdim, n, 0, 0, 1, 0, gdim, 0, gdim, info, ws, ws_bytes, None) == E
+    assert lib.gbm_dev_chol_prepare_cols(G, gdim, n, 1.0, None, 1.0, G, n, 1, 2, 2, info, ws, ws_bytes, None) == E
     assert lib.gbm_dev_chol_group_update_tiles(G, gdim, n, 0, 0, 2, 256, 128, 0, gdim, info, ws, ws_bytes, None) == E
     # a rank outside [0, nranks)
     assert lib.gbm_dev_chol_group_panels(G, gdim, n, 0, 2, 2, info, ws, ws_bytes, None) == E

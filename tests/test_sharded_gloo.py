@@ -100,6 +100,17 @@ class NumpyShardStages:
         self.V = V
         self.chol_factor_diag(0)
 
+    def chol_prepare_cols(self, rank, nranks):
+        """gbm_dev_chol_prepare_cols: V on the rank's own tiles, the first group's area and the right-hand
+        sides only; every other column keeps G (its rows arrive by exchanges before they are read)."""
+        self.chol_prepare()
+        g0 = self.lib.gbm_dev_chol_group_size(self.n, 0)
+        raw = np.zeros_like(self.V)
+        raw[:self.n, :self.n] = np.triu(self.G[:self.n, :self.n].numpy())
+        for c in range(self.npad):
+            if not (c < NB * g0 or (c // TB) % nranks == rank):
+                self.V[:, c] = raw[:, c]
+
     def chol_factor_diag(self, kb):
         r = slice(NB * kb, NB * kb + NB)
         A = np.triu(self.V[r, r])
