@@ -46,13 +46,11 @@ struct FitCtx {
   DevBuf errs, q2;               // streamed fit: per-chunk carry error cells; scratch kept count
   DevBuf astrip, agathered;      // the distributed factorisation's area all-gather (on the copy stream)
   hipEvent_t ev_area = nullptr, ev_upd = nullptr;  // area exchange done / next area updated
-  hipEvent_t ev_rows = nullptr;                    // (look-ahead) the next group's rows updated
   ~FitCtx() {
     (void)hipSetDevice(dev);
     for (hipEvent_t e : ev) (void)hipEventDestroy(e);
     if (ev_area) (void)hipEventDestroy(ev_area);
     if (ev_upd) (void)hipEventDestroy(ev_upd);
-    if (ev_rows) (void)hipEventDestroy(ev_rows);
   }
 };
 
@@ -998,7 +996,6 @@ int solve_distributed(std::vector<std::unique_ptr<Shard>>& shards, const std::ve
       GBM_TRY(ensure_copy_stream(c));
       if (!c.ev_area) GBM_HIP_TRY(hipEventCreateWithFlags(&c.ev_area, hipEventDisableTiming));
       if (!c.ev_upd) GBM_HIP_TRY(hipEventCreateWithFlags(&c.ev_upd, hipEventDisableTiming));
-      if (!c.ev_rows) GBM_HIP_TRY(hipEventCreateWithFlags(&c.ev_rows, hipEventDisableTiming));
       return GBM_OK;
     }));
   auto update = [&](int64_t kb, int64_t lo, int64_t hi) {
@@ -1073,29 +1070,25 @@ int solve_distributed(std::vector<std::unique_ptr<Shard>>& shards, const std::ve
       const int64_t area_hi = kCholNB * (k1 + g1);
       GBM_TRY(area_update_async(kb, kCholNB * k1, area_hi));  // the next group's area, on the copy streams
       if (lookahead) {
-        // the next group's rows of the rank's tiles (and the right-hand sides) first; its panels and row
-        // exchange follow the area exchange on the copy streams, beside the rest of the update (the rows
-        // from area_hi on: disjoint tiles)
-        auto tiles = [&](int64_t r_lo, int64_t r_hi) {
+        // on the copy streams (after the area update): the next group's rows of the rank's tiles (and the
+        // right-hand sides), the area exchange, the next group's panels and row exchange — beside the rest
+        // of the update on the main streams (the rows from area_hi on: disjoint tiles)
+        auto tiles = [&](int64_t r_lo, int64_t r_hi, bool on_copy) {
           return each([&](int r, FitCtx& c) {
             return gbm_dev_chol_group_update_tiles((double*)c.G.p, gdim, n, kb, r, R, r_lo, r_hi, area_hi, gdim,
-                                                   (int32_t*)c.info.p, c.wss.p, c.wss.cap, c.stream.s);
+                                                   (int32_t*)c.info.p, c.wss.p, c.wss.cap,
+                                                   on_copy ? c.copy.s : c.stream.s);
           });
         };
-        GBM_TRY(tiles(kCholNB * k1, area_hi));
+        GBM_TRY(tiles(kCholNB * k1, area_hi, true));
         GBM_TRY(area_async(k1, g1));
-        GBM_TRY(each([&](int, FitCtx& c) -> int {
-          GBM_HIP_TRY(hipEventRecord(c.ev_rows, c.stream.s));
-          GBM_HIP_TRY(hipStreamWaitEvent(c.copy.s, c.ev_rows, 0));
-          return GBM_OK;
-        }));
         GBM_TRY(panels(k1, true));
         GBM_TRY(exchange(k1, g1, kRows, true));
         GBM_TRY(each([&](int, FitCtx& c) -> int {
           GBM_HIP_TRY(hipEventRecord(c.ev_area, c.copy.s));  // the next group waits for all of it
           return GBM_OK;
         }));
-        GBM_TRY(tiles(area_hi, gdim));
+        GBM_TRY(tiles(area_hi, gdim, false));
         ahead = true;
       } else {
         GBM_TRY(update(kb, area_hi, gdim));  // the rest (and the right-hand sides) beside it and its exchange

@@ -225,13 +225,11 @@ def chol_distributed(stages, ranks, nranks, allgather, tail_rows=None, force=Fal
                     st.chol_group_update_cols(kb, r, nranks, 64 * k1, area_hi)
                 exchange(k1, g1, "area")
             if lookahead:
-                # look-ahead: the next group's rows first; its panels and row exchange then run on the side
-                # stream beside the rest of the update (rows from area_hi on: disjoint tiles)
-                for st, r in zip(stages, ranks):
-                    st.chol_group_update_tiles(kb, r, nranks, 64 * k1, area_hi, area_hi, gdim)
-                for st in stages:
-                    st.fork()
+                # look-ahead: on the side stream the next group's rows, its panels and its row exchange, beside
+                # the rest of the update on this one (rows from area_hi on: disjoint tiles)
                 with stages[0].side():
+                    for st, r in zip(stages, ranks):
+                        st.chol_group_update_tiles(kb, r, nranks, 64 * k1, area_hi, area_hi, gdim)
                     for st, r in zip(stages, ranks):
                         st.chol_group_panels(k1, r, nranks)
                     exchange(k1, g1, "rows")
