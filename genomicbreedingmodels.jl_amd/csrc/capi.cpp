@@ -1068,19 +1068,22 @@ int solve_distributed(std::vector<std::unique_ptr<Shard>>& shards, const std::ve
     if (overlap && next_dist) {
       const int64_t g1 = gbm_dev_chol_group_size(n, k1);
       const int64_t area_hi = kCholNB * (k1 + g1);
-      GBM_TRY(area_update_async(kb, kCholNB * k1, area_hi));  // the next group's area, on the copy streams
       if (lookahead) {
-        // on the copy streams (after the area update): the next group's rows of the rank's tiles (and the
-        // right-hand sides), the area exchange, the next group's panels and row exchange — beside the rest
-        // of the update on the main streams (the rows from area_hi on: disjoint tiles)
-        auto tiles = [&](int64_t r_lo, int64_t r_hi, bool on_copy) {
-          return each([&](int r, FitCtx& c) {
-            return gbm_dev_chol_group_update_tiles((double*)c.G.p, gdim, n, kb, r, R, r_lo, r_hi, area_hi, gdim,
+        // on the copy streams: the next group's rows of every kept column (its area among them: one launch),
+        // the area exchange, the next group's panels and row exchange — beside the rest of the update on
+        // the main streams (the rows from area_hi on: disjoint tiles)
+        auto tiles = [&](int64_t r_lo, int64_t r_hi, int64_t c_lo, bool on_copy) {
+          return each([&](int r, FitCtx& c) -> int {
+            if (on_copy) {
+              GBM_HIP_TRY(hipEventRecord(c.ev_upd, c.stream.s));  // after the group's rows arrived
+              GBM_HIP_TRY(hipStreamWaitEvent(c.copy.s, c.ev_upd, 0));
+            }
+            return gbm_dev_chol_group_update_tiles((double*)c.G.p, gdim, n, kb, r, R, r_lo, r_hi, c_lo, gdim,
                                                    (int32_t*)c.info.p, c.wss.p, c.wss.cap,
                                                    on_copy ? c.copy.s : c.stream.s);
           });
         };
-        GBM_TRY(tiles(kCholNB * k1, area_hi, true));
+        GBM_TRY(tiles(kCholNB * k1, area_hi, kCholNB * k1, true));
         GBM_TRY(area_async(k1, g1));
         GBM_TRY(panels(k1, true));
         GBM_TRY(exchange(k1, g1, kRows, true));
@@ -1088,9 +1091,10 @@ int solve_distributed(std::vector<std::unique_ptr<Shard>>& shards, const std::ve
           GBM_HIP_TRY(hipEventRecord(c.ev_area, c.copy.s));  // the next group waits for all of it
           return GBM_OK;
         }));
-        GBM_TRY(tiles(area_hi, gdim, false));
+        GBM_TRY(tiles(area_hi, gdim, area_hi, false));
         ahead = true;
       } else {
+        GBM_TRY(area_update_async(kb, kCholNB * k1, area_hi));  // the next group's area, on the copy streams
         GBM_TRY(update(kb, area_hi, gdim));  // the rest (and the right-hand sides) beside it and its exchange
         GBM_TRY(area_async(k1, g1));
       }

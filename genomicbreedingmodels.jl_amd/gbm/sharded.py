@@ -214,22 +214,18 @@ def chol_distributed(stages, ranks, nranks, allgather, tail_rows=None, force=Fal
         k1 = kb + g
         next_dist = k1 < nb and distributable(k1)
         if overlap and next_dist:
-            # the next group's area (a rank owns about one of its tile columns: a few workgroups, one K = 64 g
-            # tile long) is updated and exchanged on the side stream, beside the rest of the update
             g1 = int(lib.gbm_dev_chol_group_size(n, k1))
             area_hi = 64 * (k1 + g1)
             for st in stages:
                 st.fork()
-            with stages[0].side():  # (one side stream per device)
-                for st, r in zip(stages, ranks):
-                    st.chol_group_update_cols(kb, r, nranks, 64 * k1, area_hi)
-                exchange(k1, g1, "area")
             if lookahead:
-                # look-ahead: on the side stream the next group's rows, its panels and its row exchange, beside
-                # the rest of the update on this one (rows from area_hi on: disjoint tiles)
+                # look-ahead: on the side stream the next group's rows of every kept column (its area among
+                # them: one launch), the area exchange, its panels and its row exchange, beside the rest of
+                # the update on this one (rows from area_hi on: disjoint tiles)
                 with stages[0].side():
                     for st, r in zip(stages, ranks):
-                        st.chol_group_update_tiles(kb, r, nranks, 64 * k1, area_hi, area_hi, gdim)
+                        st.chol_group_update_tiles(kb, r, nranks, 64 * k1, area_hi, 64 * k1, gdim)
+                    exchange(k1, g1, "area")
                     for st, r in zip(stages, ranks):
                         st.chol_group_panels(k1, r, nranks)
                     exchange(k1, g1, "rows")
@@ -237,6 +233,12 @@ def chol_distributed(stages, ranks, nranks, allgather, tail_rows=None, force=Fal
                     st.chol_group_update_tiles(kb, r, nranks, area_hi, gdim, area_hi, gdim)
                 ahead = True
             else:
+                # the next group's area (a rank owns about one of its tile columns: a few workgroups, one
+                # K = 64 g tile long) is updated and exchanged on the side stream, beside the rest
+                with stages[0].side():  # (one side stream per device)
+                    for st, r in zip(stages, ranks):
+                        st.chol_group_update_cols(kb, r, nranks, 64 * k1, area_hi)
+                    exchange(k1, g1, "area")
                 for st, r in zip(stages, ranks):
                     st.chol_group_update_cols(kb, r, nranks, area_hi, gdim)
             pending = True
