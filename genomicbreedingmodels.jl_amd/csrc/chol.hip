@@ -1064,11 +1064,12 @@ extern "C" int gbm_dev_chol_area_unpack(double* G, int64_t ldg, int64_t n, int64
   return strip_launch(G, ldg, n, kb, rows64, 0, nranks, const_cast<double*>(gathered), 1, (hipStream_t)stream, true);
 }
 
-extern "C" int gbm_dev_chol_strip_unpack_rows(double* G, int64_t ldg, int64_t n, int64_t kb, int64_t rows64, int rank,
-                                              int nranks, const double* gathered, void* stream) {
-  if (rank < 0 || rank >= nranks) return fail(GBM_E_ARG, "gbm_dev_chol_strip_unpack_rows: bad rank");
+extern "C" int gbm_dev_chol_lower_copy(double* G, int64_t ldg, int64_t n, int64_t kb, int64_t rows64, int rank,
+                                       int nranks, void* stream) {
+  if (!G || n < 1 || ldg < gdim_of(n) || kb < 0 || rows64 < 1 || rank < 0 || rank >= nranks ||
+      (kb + rows64) * NB > npad_of(n))
+    return fail(GBM_E_ARG, "gbm_dev_chol_lower_copy: bad arguments");
   hipStream_t s = (hipStream_t)stream;
-  GBM_TRY(strip_launch(G, ldg, n, kb, rows64, 0, nranks, const_cast<double*>(gathered), 1, s));
   // the lower copy of the chunks other ranks solved (this rank's panel kernels wrote its own)
   const int64_t npad = npad_of(n), r0 = kb * NB;
   ColKeep keep;
@@ -1082,6 +1083,13 @@ extern "C" int gbm_dev_chol_strip_unpack_rows(double* G, int64_t ldg, int64_t n,
     GBM_LAUNCH_CHECK();
   }
   return GBM_OK;
+}
+
+extern "C" int gbm_dev_chol_strip_unpack_rows(double* G, int64_t ldg, int64_t n, int64_t kb, int64_t rows64, int rank,
+                                              int nranks, const double* gathered, void* stream) {
+  if (rank < 0 || rank >= nranks) return fail(GBM_E_ARG, "gbm_dev_chol_strip_unpack_rows: bad rank");
+  GBM_TRY(strip_launch(G, ldg, n, kb, rows64, 0, nranks, const_cast<double*>(gathered), 1, (hipStream_t)stream));
+  return gbm_dev_chol_lower_copy(G, ldg, n, kb, rows64, rank, nranks, stream);
 }
 
 extern "C" int gbm_dev_chol_finish(double* G, int64_t ldg, int64_t n, const double* Y, int64_t ldy, int64_t nrhs,

@@ -40,7 +40,7 @@ EXPORTS = (
     "gbm_dev_grm_packed_size", "gbm_dev_grm_pack", "gbm_dev_grm_unpack",
     "gbm_debug_brr_stats", "gbm_debug_brr_shape", "gbm_debug_brr_trace", "gbm_debug_chol_flow_trace",
     "gbm_dev_synth_dosage_i8", "gbm_dev_standardize_i8", "gbm_dev_grm_accumulate", "gbm_dev_marker_effects_i8",
-    "gbm_debug_oom_retries", "gbm_dev_chol_group_panels", "gbm_dev_chol_group_update", "gbm_dev_chol_strip_unpack_rows",
+    "gbm_debug_oom_retries", "gbm_dev_chol_group_panels", "gbm_dev_chol_group_update", "gbm_dev_chol_strip_unpack_rows", "gbm_dev_chol_lower_copy",
     "gbm_dev_chol_area_doubles", "gbm_dev_chol_area_pack", "gbm_dev_chol_area_unpack",
     "gbm_dev_chol_group_update_cols", "gbm_dev_chol_group_update_tiles", "gbm_dev_grm_exact_workspace", "gbm_dev_grm_exact_i8",
     "gbm_gblup_fit_ex", "gbm_gblup_fit_reml_ex", "gbm_gblup_fit_dosage_i8_ex", "gbm_gblup_fit_synthetic_ex",
@@ -115,6 +115,8 @@ def _declare(lib):
     lib.gbm_dev_chol_area_unpack.argtypes = [P, I64, I64, I64, I64, I32, P, P]
     lib.gbm_dev_chol_strip_unpack_rows.restype = I32
     lib.gbm_dev_chol_strip_unpack_rows.argtypes = [P, I64, I64, I64, I64, I32, I32, P, P]
+    lib.gbm_dev_chol_lower_copy.restype = I32
+    lib.gbm_dev_chol_lower_copy.argtypes = [P, I64, I64, I64, I64, I32, I32, P]
     lib.gbm_dev_chol_factor_diag.restype = I32
     lib.gbm_dev_chol_factor_diag.argtypes = [P, I64, I64, I64, P, P, I64, P]
     lib.gbm_dev_chol_strip_doubles.restype = I64

@@ -102,6 +102,7 @@ def sharded_gblup_step(stages, comm, events=None):
 
 
 _SIDE_STREAMS = {}  # device -> the distributed solve's side stream
+_LOWER_STREAMS = {}  # device -> the stream of its deferred lower copies
 
 
 def dist_solve_min_n() -> int:
@@ -151,12 +152,18 @@ def chol_distributed(stages, ranks, nranks, allgather, tail_rows=None, force=Fal
 
     overlap = int(os.environ.get("GBM_DIST_OVERLAP", "1")) != 0 and all(hasattr(st, "fork") for st in stages)
 
+    defer_lower = all(hasattr(st, "lower_fork") for st in stages)
+
     def exchange(kb, rows64, what):  # "rows": a group's final rows; "rest": the tail; "area": a group's area
+        # "rows_deferred": the final rows without their lower copy (the caller queues it on the lower stream)
         pack = "area_pack" if what == "area" else "strip_pack"
         packs = [getattr(st, pack)(kb, rows64, r, nranks) for st, r in zip(stages, ranks)]
         for st, r, gathered in zip(stages, ranks, allgather(packs)):
             if what == "rows":
                 st.strip_unpack_rows(kb, rows64, r, nranks, gathered)
+                continue
+            if what == "rows_deferred":
+                st.strip_unpack(kb, rows64, nranks, gathered)
                 continue
             if what == "area":
                 st.area_unpack(kb, rows64, nranks, gathered)
@@ -228,7 +235,15 @@ def chol_distributed(stages, ranks, nranks, allgather, tail_rows=None, force=Fal
                     exchange(k1, g1, "area")
                     for st, r in zip(stages, ranks):
                         st.chol_group_panels(k1, r, nranks)
-                    exchange(k1, g1, "rows")
+                    exchange(k1, g1, "rows_deferred" if defer_lower else "rows")
+                    if defer_lower:
+                        # the rows' lower copy (read only by chol_finish) off the side stream: the next join
+                        # does not wait for it
+                        for st in stages:
+                            st.lower_fork()
+                        with stages[0].lower():
+                            for st, r in zip(stages, ranks):
+                                st.chol_lower_copy(k1, g1, r, nranks)
                 for st, r in zip(stages, ranks):
                     st.chol_group_update_tiles(kb, r, nranks, area_hi, gdim, area_hi, gdim)
                 ahead = True
@@ -253,6 +268,8 @@ def chol_distributed(stages, ranks, nranks, allgather, tail_rows=None, force=Fal
         if not dist:  # the tail: every remaining row, once
             exchange(kb, nb - kb, "rest")
     for st in stages:
+        if defer_lower:
+            st.lower_join()  # the deferred lower copies, which the back substitution reads
         st.chol_finish()
 
 
@@ -434,6 +451,28 @@ class HipShardStages:
 
     def join(self):
         self.torch.cuda.current_stream(self.dev).wait_stream(self._side_stream())
+
+    # a third stream for the deferred lower copies of the look-ahead's rows (read only by chol_finish):
+    # lower_fork = it waits for the current stream; lower() = a context on it; lower_join = the current
+    # stream waits for it (before chol_finish)
+    def _lower_stream(self):
+        s = _LOWER_STREAMS.get(self.dev)
+        if s is None:
+            s = _LOWER_STREAMS[self.dev] = self.torch.cuda.Stream(self.dev)
+        return s
+
+    def lower_fork(self):
+        self._lower_stream().wait_stream(self.torch.cuda.current_stream(self.dev))
+
+    def lower(self):
+        return self.torch.cuda.stream(self._lower_stream())
+
+    def lower_join(self):
+        self.torch.cuda.current_stream(self.dev).wait_stream(self._lower_stream())
+
+    def chol_lower_copy(self, kb: int, rows64: int, rank: int, nranks: int):
+        _lib.check(self.lib.gbm_dev_chol_lower_copy(self._p(self.G), self.gdim, self.n, kb, rows64, rank, nranks,
+                                                    self._stream()), "chol_lower_copy")
 
     def chol_group_update(self, kb: int, rank: int, nranks: int):
         _lib.check(self.lib.gbm_dev_chol_group_update(self._p(self.G), self.gdim, self.n, kb, rank, nranks,

@@ -372,8 +372,13 @@ int gbm_dev_chol_area_pack(const double* G, int64_t ldg, int64_t n, int64_t kb, 
                            int nranks, double* buf, void* stream);
 int gbm_dev_chol_area_unpack(double* G, int64_t ldg, int64_t n, int64_t kb, int64_t rows64, int nranks,
                              const double* gathered, void* stream);
+/* The transposed lower copy (read only by gbm_dev_chol_finish) of the rows [64 kb, 64 (kb + rows64)) for the
+ * chunks other ranks solved. A driver may defer it to a stream of its own (the rows are final; nothing before
+ * finish reads or writes those entries). */
+int gbm_dev_chol_lower_copy(double* G, int64_t ldg, int64_t n, int64_t kb, int64_t rows64, int rank, int nranks,
+                            void* stream);
 /* strip_unpack of final factor rows (after group_panels) plus their lower copy for the columns this
- * rank did not compute. */
+ * rank did not compute (= strip_unpack + lower_copy). */
 int gbm_dev_chol_strip_unpack_rows(double* G, int64_t ldg, int64_t n, int64_t kb, int64_t rows64, int rank,
                                    int nranks, const double* gathered, void* stream);
 int gbm_dev_chol_finish(double* G, int64_t ldg, int64_t n, const double* Y, int64_t ldy, int64_t nrhs,

@@ -183,6 +183,18 @@ class NumpyShardStages:
     def join(self):
         pass
 
+    def lower_fork(self):
+        pass
+
+    def lower(self):
+        return contextlib.nullcontext()
+
+    def lower_join(self):
+        pass
+
+    def chol_lower_copy(self, kb, rows64, rank, nranks):
+        pass  # (V holds the upper factor only: strip_unpack and strip_unpack_rows are the same here)
+
     def chol_group(self, kb, rank, nranks):
         assert (rank, nranks) == (0, 1)  # gbm_dev_chol_group: the redundant path only
         self.chol_group_panels(kb, 0, 1)
