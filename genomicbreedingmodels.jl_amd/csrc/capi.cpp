@@ -145,17 +145,12 @@ struct Problem {
   uint64_t seed = 0;  // Source::SYNTH: genotypes generated on each device
 };
 
-int64_t env_i64(const char* name, int64_t def) {
-  const char* e = getenv(name);
-  return e && *e ? (int64_t)atoll(e) : def;
-}
-
 // GBM_SHARD_LEADERS=each (re-read per call): every shard keeps its own full G and is a rank of its
 // own in the GRM sum and the distributed factorisation, its exchanges done by device copies. That
 // is the one-GPU rehearsal of the multi-device path (devices = [0, 0, ...]; RCCL cannot put two
 // ranks on one device). Default: one leader per device, RCCL between the leaders.
 bool each_shard_leads() {
-  const char* e = getenv("GBM_SHARD_LEADERS");
+  const char* e = ::gbm::knob("GBM_SHARD_LEADERS");
   return e && strcmp(e, "each") == 0;
 }
 
@@ -231,7 +226,7 @@ int prepare_grm_shard(const Problem& pr, Shard& sh) {
 // GBM_HOST_CHUNK = loci per chunk, 0 to disable; by default p/8 (>= 4096 loci) once p >= 16384
 // (C2 host path, pageable X: 58.5 ms in one piece, 43.3 ms in 4 chunks, 40.9 ms in 8).
 int64_t host_chunk(int64_t p) {
-  const char* e = getenv("GBM_HOST_CHUNK");
+  const char* e = ::gbm::knob("GBM_HOST_CHUNK");
   int64_t c = e ? (int64_t)atoll(e) : -1;
   if (c == 0) return 0;
   if (c < 0) {
@@ -287,7 +282,7 @@ int upload_grm_pipelined(const Problem& pr, Shard& sh, int64_t chunk) {
     GBM_HIP_TRY(hipDeviceGetStreamPriorityRange(&lo, &hi));
     GBM_HIP_TRY(hipStreamCreateWithPriority(&c.copy.s, hipStreamNonBlocking, hi));
   }
-  const std::vector<std::pair<int64_t, int64_t>> sched = chunk_schedule(pl, chunk, (pr.src == Source::F64 && n <= 8192) || getenv("GBM_HOST_CHUNK") != nullptr);
+  const std::vector<std::pair<int64_t, int64_t>> sched = chunk_schedule(pl, chunk, (pr.src == Source::F64 && n <= 8192) || ::gbm::knob("GBM_HOST_CHUNK") != nullptr);
   const int64_t nch = (int64_t)sched.size();
   while ((int64_t)c.ev.size() < nch) {
     hipEvent_t e;
@@ -383,7 +378,7 @@ int ensure_events(FitCtx& c, int64_t k) {
 // fp64 at n <= 8192 or when GBM_HOST_CHUNK is set), so a streamed fit and a pipelined one over the
 // same chunk size sum the same chunk GRMs in the same order.
 std::vector<std::pair<int64_t, int64_t>> stream_schedule(const Problem& pr, const Shard& sh) {
-  return chunk_schedule(sh.p, sh.stream, (pr.src == Source::F64 && pr.n <= 8192) || getenv("GBM_HOST_CHUNK") != nullptr);
+  return chunk_schedule(sh.p, sh.stream, (pr.src == Source::F64 && pr.n <= 8192) || ::gbm::knob("GBM_HOST_CHUNK") != nullptr);
 }
 
 // Decide, per device, whether its shards' fp64 rows fit (resident, the default) or are streamed,
@@ -392,7 +387,7 @@ std::vector<std::pair<int64_t, int64_t>> stream_schedule(const Problem& pr, cons
 // memory (plus what their pooled contexts already hold, minus a margin) even after its idle pooled
 // contexts are freed; the chunk is then the largest equal split of the shard whose buffers fit.
 int plan_streaming(const Problem& pr, std::vector<std::unique_ptr<Shard>>& shards, bool reml) {
-  const int64_t forced = env_i64("GBM_STREAM_CHUNK", -1);
+  const int64_t forced = knob_i64("GBM_STREAM_CHUNK", -1);
   const int64_t n = pr.n, npad = npad_of(n), gdim = gdim_of(n);
   const bool bytes = pr.src != Source::F64;
   if (forced >= 0) {
@@ -408,7 +403,8 @@ int plan_streaming(const Problem& pr, std::vector<std::unique_ptr<Shard>>& shard
     int64_t held = 0, fixed = 0, resident = 0, dosage = 0, pmax = 0;
     for (Shard* sh : v) {
       FitCtx& c = sh->x();
-      held += c.Xt.cap + c.D8.cap + c.G.cap + c.Gc.cap + c.wsg.cap;
+      // D8 counts only where this call's path refills it (int8 or synthetic dosages); an fp64 source never reuses it
+      held += c.Xt.cap + (pr.src != Source::F64 ? c.D8.cap : 0) + c.G.cap + c.Gc.cap + c.wsg.cap;
       fixed += gdim * gdim * 8 * (reml ? 2 : 1) + gbm_dev_solve_workspace(n, 63) + sh->p * 40;
       resident += sh->p * npad * 8 + (pr.src == Source::I8 ? sh->p * n : 0) + gbm_dev_grm_workspace(n, sh->p);
       dosage += bytes ? sh->p * n : 0;
@@ -552,11 +548,12 @@ constexpr int kNotDosage = 1;  // internal: the genotypes are not diploid dosage
 }  // namespace
 
 int resolve_grm_mode(int grm_mode) {
-  if (grm_mode != GBM_GRM_DEFAULT) return grm_mode;
-  const char* e = getenv("GBM_GRM");
+  if (grm_mode != GBM_GRM_DEFAULT && grm_mode != GBM_GRM_DROPIN) return grm_mode;
+  const char* e = ::gbm::knob("GBM_GRM");
   if (e && strcmp(e, "exact") == 0) return GBM_GRM_EXACT;
   if (e && strcmp(e, "auto") == 0) return GBM_GRM_AUTO;
-  return GBM_GRM_FP64;
+  if (e && strcmp(e, "fp64") == 0) return GBM_GRM_FP64;
+  return grm_mode == GBM_GRM_DROPIN ? GBM_GRM_AUTO : GBM_GRM_FP64;
 }
 
 namespace {
@@ -640,8 +637,7 @@ int exact_grm_shard(const Problem& pr, Shard& sh, bool check_bytes = false) {
   GBM_TRY(launch_grm_exact((const int8_t*)c.D8.p, n, pl, n, 2, (double*)c.G.p, gdim, (double*)c.mean.p,
                            (double*)c.sd.p, (int32_t*)c.keep.p, (int64_t*)c.q.p, 0, c.wsg.p, wsb, nullptr, s));
   GBM_HIP_TRY(hipMemcpyAsync(&sh.q_host, c.q.p, 8, hipMemcpyDeviceToHost, s));
-  GBM_HIP_TRY(hipStreamSynchronize(s));
-  return GBM_OK;
+  return grm_exact_status(c.wsg.p, n, pl, s);  // syncs the stream
 }
 
 // Marker effects of a streamed shard into B (nt x p) and msum: from the resident dosages in one
@@ -695,7 +691,7 @@ int grm_shard(const Problem& pr, Shard& sh) {
 template <class Fn>
 int parallel_shards(std::vector<std::unique_ptr<Shard>>& shards, Fn&& fn) {
   const size_t m = shards.size();
-  const char* e = getenv("GBM_SHARD_THREADS");  // "0": one shard after the other (A/B, tests)
+  const char* e = ::gbm::knob("GBM_SHARD_THREADS");  // "0": one shard after the other (A/B, tests)
   if (m == 1 || (e && strcmp(e, "0") == 0)) {
     for (size_t k = 0; k < m; k++) GBM_TRY(fn(k, *shards[k]));
     return GBM_OK;
@@ -717,6 +713,10 @@ int parallel_shards(std::vector<std::unique_ptr<Shard>>& shards, Fn&& fn) {
   }
   run(0);
   for (auto& t : th) t.join();
+  // a real error (negative code) of any shard takes priority over an internal status (kNotDosage > 0) of a
+  // lower-numbered one: a fall-back must never hide a HIP/RCCL/OOM failure
+  for (size_t k = 0; k < m; k++)
+    if (rc[k] < 0) return fail(rc[k], msg[k]);
   for (size_t k = 0; k < m; k++)
     if (rc[k] != GBM_OK) return fail(rc[k], msg[k]);
   return GBM_OK;
@@ -793,7 +793,7 @@ int copy_allreduce(std::vector<std::unique_ptr<Shard>>& shards, const std::vecto
 // leader — the partial-GRM all-reduce and the Cholesky strip all-gathers (from n >= GBM_DIST_SOLVE_MIN_N)
 // execute on a 1-rank RCCL communicator (ncclCommInitAll over the one device) with the real payloads,
 // so the RCCL path runs on a one-GPU box. A sum or gather over one rank is the identity: same bits.
-bool force_rccl() { return env_i64("GBM_FORCE_RCCL", 0) != 0; }
+bool force_rccl() { return knob_i64("GBM_FORCE_RCCL", 0) != 0; }
 
 // Sum the partial GRMs of all shards into each device leader's G: the upper 128-tiles packed
 // contiguously (half the bytes of G's rows); shards on one device added there in shard order,
@@ -903,7 +903,7 @@ int solve_distributed(std::vector<std::unique_ptr<Shard>>& shards, const std::ve
                       const std::vector<int>& ldevs, int64_t n, double inv_q, double lambda, int64_t nrhs) {
   const int64_t npad = npad_of(n), gdim = gdim_of(n), nb = npad / kCholNB;
   const int R = (int)leaders.size();
-  const int64_t tail_rows = env_i64("GBM_DIST_TAIL_ROWS", 8192);
+  const int64_t tail_rows = knob_i64("GBM_DIST_TAIL_ROWS", 8192);
   std::vector<int> sorted = ldevs;
   std::sort(sorted.begin(), sorted.end());
   CommSet* cs = nullptr;
@@ -987,10 +987,12 @@ int solve_distributed(std::vector<std::unique_ptr<Shard>>& shards, const std::ve
   }
   // GBM_DIST_OVERLAP (default 1): the next group's area is updated and all-gathered on the copy streams
   // while the rest of the trailing update runs (same kernels, same tiles: same bits)
-  const bool overlap = env_i64("GBM_DIST_OVERLAP", 1) != 0;
-  // GBM_DIST_LOOKAHEAD (default 1, with overlap): the next group's rows are updated first, then its panels
-  // and row exchange run on the copy streams beside the rest of the trailing update
-  const bool lookahead = overlap && env_i64("GBM_DIST_LOOKAHEAD", 1) != 0;
+  const bool overlap = knob_i64("GBM_DIST_OVERLAP", 1) != 0;
+  // GBM_DIST_LOOKAHEAD (with overlap): the next group's rows are updated first, then its panels and row
+  // exchange run on the copy streams beside the rest of the trailing update. Default 1 for the device-copy
+  // exchanges (the one-GPU rehearsal, tested bit-identical); default 0 over real RCCL (cs != nullptr) until a
+  // multi-GPU run has shown the look-ahead's stream/communicator interleaving bit-identical there
+  const bool lookahead = overlap && knob_i64("GBM_DIST_LOOKAHEAD", cs ? 0 : 1) != 0;
   if (overlap)
     GBM_TRY(each([&](int, FitCtx& c) -> int {
       GBM_TRY(ensure_copy_stream(c));
@@ -1129,7 +1131,7 @@ int solve_effects(const Problem& pr, std::vector<std::unique_ptr<Shard>>& shards
   // gbm.sharded.dist_solve_min_n) each device leader solves the (identical) n x n system, all
   // devices at once; from there the leaders factor it together (solve_distributed). Either way a
   // ends up on every leader for the marker back-solve (same-device shards copy it from theirs).
-  const bool distributed = (leaders.size() > 1 || force_rccl()) && n >= env_i64("GBM_DIST_SOLVE_MIN_N", 16384);
+  const bool distributed = (leaders.size() > 1 || force_rccl()) && n >= knob_i64("GBM_DIST_SOLVE_MIN_N", 16384);
   std::vector<int32_t> infos(shards.size(), 0);
   {
     RoctxRange rsolve(distributed ? "gbm: distributed solve" : "gbm: solve");
@@ -1302,9 +1304,22 @@ int run_fit(const Problem& pr, const double* Y, int64_t ldy, int64_t nrhs, doubl
       if (rc == kNotDosage && mode == GBM_GRM_EXACT)
         return fail(GBM_E_ARG, "grm_mode exact: the genotypes are not diploid dosages (2x must be exactly 0, 1 or 2 "
                                "in every cell; use grm_mode auto or fp64)");
-      if (rc == kNotDosage) {
+      // auto: data that is not dosage-valued, and the exact path's own limits (out of memory for the resident
+      // bytes and staging, the 128-bit bracket's range: GBM_E_OOM / GBM_E_ARG), fall back to the fp64 path
+      const bool fallback = mode == GBM_GRM_AUTO && (rc == kNotDosage || rc == GBM_E_OOM || rc == GBM_E_ARG);
+      if (fallback) {
         exact = false;
-        for (auto& sh : shards) sh->exact = sh->d8_ready = false;
+        for (auto& sh : shards) {
+          sh->exact = sh->d8_ready = false;
+          // the fp64 path of fp64 genotypes never reads D8: free it, so plan_streaming sees the memory (a
+          // dosage source keeps it: its fp64 path refills D8)
+          FitCtx& c = sh->x();
+          if (pr.src == Source::F64 && c.D8.p) {
+            (void)hipSetDevice(c.dev);
+            c.D8.reset();
+            c.D8.cap = 0;
+          }
+        }
         set_error("");
       } else {
         GBM_TRY(rc);

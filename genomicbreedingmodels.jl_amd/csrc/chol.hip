@@ -711,7 +711,7 @@ int check_solve_args(const double* G, int64_t ldg, int64_t n, const int32_t* inf
 // default 8192 when the whole matrix was too large for the dataflow launch (npad > 12 288), else 0 (off).
 // Never the whole matrix (kb > 0).
 static int64_t tail_flow_rows(int64_t npad) {
-  const char* e = getenv("GBM_CHOL_TAIL_FLOW");
+  const char* e = ::gbm::knob("GBM_CHOL_TAIL_FLOW");
   if (e) return (int64_t)atoll(e);
   return npad > 12288 ? 8192 : 0;
 }
@@ -726,7 +726,7 @@ static bool tail_flow_at(int64_t kb, int64_t npad, int64_t gdim) {
 int group_size(int64_t kb, int64_t nb, int64_t gdim) {
   if (tail_flow_at(kb, nb * NB, gdim)) return (int)(nb - kb);
   auto lim = [](const char* name, int64_t dflt) {
-    const char* e = getenv(name);
+    const char* e = ::gbm::knob(name);
     return e ? (int64_t)atoll(e) : dflt;
   };
   // 4-panel groups while the trailing matrix exceeds 8192 rows; 8-panel (K = 512) above 8192 and
@@ -759,7 +759,7 @@ int solve_prepare(double* G, int64_t ldg, int64_t n, double inv_q, const int64_t
 // GBM_CHOL_GROUP_KERNEL (re-read per group, default 1): a panel group's panel phase as one
 // chol_group_kernel launch; 0: the chain of panel and row-update launches
 static bool group_kernel_enabled() {
-  const char* e = getenv("GBM_CHOL_GROUP_KERNEL");
+  const char* e = ::gbm::knob("GBM_CHOL_GROUP_KERNEL");
   return !e || atoi(e) != 0;
 }
 

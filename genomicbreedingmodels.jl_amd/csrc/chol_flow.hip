@@ -1089,7 +1089,7 @@ std::vector<int32_t> flow_order(int nbc, int variant) {
 }
 
 int flow_order_variant() {
-  const char* ev = getenv("GBM_CHOL_FLOW_ORDER");
+  const char* ev = ::gbm::knob("GBM_CHOL_FLOW_ORDER");
   const int v = ev ? atoi(ev) : 5;
   return v == 4 || v == 6 ? v : 5;
 }
@@ -1172,7 +1172,7 @@ int64_t chol_flow_flag_bytes(int64_t gdim) {
 // n up to this many padded rows use the dataflow factorisation (GBM_CHOL_FLOW_MAX, re-read at
 // every solve; 0 = always the launch-per-panel path)
 bool chol_flow_enabled(int64_t npad) {
-  const char* e = getenv("GBM_CHOL_FLOW_MAX");
+  const char* e = ::gbm::knob("GBM_CHOL_FLOW_MAX");
   const int64_t lim = e ? (int64_t)atoll(e) : (int64_t)12288;  // n = 10 000: 10.1 vs 13.6 ms; n = 16 000: 37.2 vs 36.6
   return npad <= lim;
 }
@@ -1189,18 +1189,18 @@ int launch_chol_flow(double* G, int64_t ldg, int64_t gdim, double* Ld, double* D
   GBM_HIP_TRY(hipMemsetAsync(flag_block, 0, (size_t)chol_flow_flag_bytes(gdim), s));
   // GBM_TEST_CHOL_FLOW_ABORT (tests): start as if a wait had already timed out (info = −1), so the
   // early exit of the chain and the workers runs; the solve then fails loudly, without a hang
-  if (getenv("GBM_TEST_CHOL_FLOW_ABORT")) GBM_HIP_TRY(hipMemsetAsync(info, 0xFF, sizeof(int32_t), s));
+  if (::gbm::knob("GBM_TEST_CHOL_FLOW_ABORT")) GBM_HIP_TRY(hipMemsetAsync(info, 0xFF, sizeof(int32_t), s));
   // one workgroup per CU; GBM_CHOL_FLOW_WGS (re-read per solve) caps the workers: with 1, one worker
   // runs every tile task in dequeue order beside the chain, which checks that no wait targets a later
   // task
-  const char* ew = getenv("GBM_CHOL_FLOW_WGS");
+  const char* ew = ::gbm::knob("GBM_CHOL_FLOW_WGS");
   const int64_t workers = ew && atoll(ew) > 0 ? atoll(ew) : flow_cus() - 2;
   // + the chain and the assistant
   const unsigned grid = (unsigned)(2 + (nwork < workers ? nwork : (workers < 1 ? 1 : workers)));
   int32_t* q = (int32_t*)flag_block;
-  const char* ex = getenv("GBM_CHOL_FLOW_XN");  // 0: wave 1 always fetches the next diagonal partial first (A/B)
+  const char* ex = ::gbm::knob("GBM_CHOL_FLOW_XN");  // 0: wave 1 always fetches the next diagonal partial first (A/B)
   const int xn_defer = ex && atoi(ex) == 0 ? 0 : 1;
-  if (getenv("GBM_CHOL_FLOW_TRACE")) {
+  if (::gbm::knob("GBM_CHOL_FLOW_TRACE")) {
     // timing tool only: one record of 16 int64 per task, read back by gbm_debug_chol_flow_trace
     const int64_t nrec = ntasks + nbc;  // the workers' tasks, then the chain's steps
     if (g_trace_cap < nrec) {
@@ -1212,9 +1212,9 @@ int launch_chol_flow(double* G, int64_t ldg, int64_t gdim, double* Ld, double* D
     GBM_HIP_TRY(hipMemsetAsync(g_trace, 0, (size_t)nrec * kTraceRec * 8, s));
     g_trace_n = nrec;
     // GBM_CHOL_FLOW_TRACE = a mask of the roles that record (1 chain, 2 assistant, 4 workers; 1 = all)
-    const int tm = atoi(getenv("GBM_CHOL_FLOW_TRACE"));
+    const int tm = atoi(::gbm::knob("GBM_CHOL_FLOW_TRACE"));
     const int roles = tm > 1 ? (tm & 7) : 7;
-    if (getenv("GBM_CHOL_FLOW_TRACE_PLAIN"))  // (debug) the untraced kernel with the trace buffer set up
+    if (::gbm::knob("GBM_CHOL_FLOW_TRACE_PLAIN"))  // (debug) the untraced kernel with the trace buffer set up
       chol_flow_kernel<false><<<grid, 256, 0, s>>>(G, ldg, (int)nbc, Ld, Dinv, q, q + 4, info, order, nwork, xn_defer, nullptr, 0);
     else
     chol_flow_kernel<true><<<grid, 256, 0, s>>>(G, ldg, (int)nbc, Ld, Dinv, q, q + 4, info, order, nwork, xn_defer, g_trace, roles);

@@ -22,6 +22,12 @@ inline int64_t gdim_of(int64_t n) { return npad_of(n) + kRhsRows; }
 void set_error(const std::string& msg);
 int fail(int code, const std::string& msg);
 
+// GBM_* tuning/test knobs (knobs.cpp): the environment is read once, at the first lookup; afterwards
+// values change only through gbm_debug_set. knob() returns the value (a pointer valid for the life of
+// the process) or nullptr when unset; knob_i64 parses it (def when unset or empty).
+const char* knob(const char* name);
+int64_t knob_i64(const char* name, int64_t def);
+
 #define GBM_HIP_TRY(expr)                                                                      \
   do {                                                                                         \
     hipError_t e_ = (expr);                                                                    \
@@ -67,6 +73,8 @@ int launch_marker_rows_i8(const int8_t* D, int64_t ldd, int64_t p, int64_t n, in
 int launch_grm_exact(const int8_t* D, int64_t ldd, int64_t p, int64_t n, int ploidy, double* G, int64_t ldg,
                      double* mean, double* sd, int32_t* keep, int64_t* q_dev, int accum, void* ws, int64_t ws_bytes,
                      int32_t* slices_out, hipStream_t s);
+// after launch_grm_exact (syncs the stream): GBM_E_HIP when a weight overflowed its digits (XgInfo bit 2)
+int grm_exact_status(const void* ws, int64_t n, int64_t p, hipStream_t s);
 // training-set dosages 2·Xt[j, idx[i]] (resident genotypes that are dosages/2) for the exact GRM
 int launch_gather_dosage(const double* Xt, int64_t ldx, int64_t p, const int32_t* idx, int64_t nT, int8_t* D,
                          hipStream_t s);

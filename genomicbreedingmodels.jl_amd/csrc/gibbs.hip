@@ -1780,7 +1780,7 @@ static int brr_fit_impl(const double* X, int64_t n, int64_t p, int64_t ldx, cons
   // GBM_BRR_I8=0 keeps fp64 storage (read per call).
   double xs = 0.0;  // 0: fp64 storage
   {
-    const char* ev = std::getenv("GBM_BRR_I8");
+    const char* ev = ::gbm::knob("GBM_BRR_I8");
     if (!(ev && ev[0] == '0')) {
       GBM_TRY(ensure(cx.D, dev, p * npad + 4096));  // + slack: the super-block sweep's last chunk reads past n
       GBM_TRY(ensure(cx.badm, dev, sizeof(int)));
@@ -1808,11 +1808,11 @@ static int brr_fit_impl(const double* X, int64_t n, int64_t p, int64_t ldx, cons
   int sbK = 0, sbC = 0, sbR = 0;
   int la2Ko = 0, la2Kn = 0, la2R = 0, la2O = 0, la2C = 0;
   if (xs > 0.0 && sweep_mode != 0) {
-    const char* ev = std::getenv("GBM_BRR_SWEEP");
+    const char* ev = ::gbm::knob("GBM_BRR_SWEEP");
     int per_cu = 0;
     GBM_HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, brr_sweep_la2_kernel<false>, 256, 0));
     sbK = (int)round_up(std::max<int64_t>(16, (n + cus - 1) / cus), 16);
-    if (const char* ek = std::getenv("GBM_BRR_SB_K"))  // (timing experiments) a larger chunk
+    if (const char* ek = ::gbm::knob("GBM_BRR_SB_K"))  // (timing experiments) a larger chunk
       sbK = std::max<int>(sbK, (int)round_up(std::max<int64_t>(16, atoll(ek)), 16));
     sbC = (int)((n + sbK - 1) / sbK);
     sbR = (int)round_up((SBK + sbC - 1) / sbC, 2);
@@ -1829,7 +1829,7 @@ static int brr_fit_impl(const double* X, int64_t n, int64_t p, int64_t ldx, cons
     la2C = sbC;
     if (sweep) {
       int R2 = 0;
-      if (const char* er = std::getenv("GBM_BRR_OWN_R")) R2 = std::max(2, std::min<int>(SB_RMAX, atoi(er) & ~1));
+      if (const char* er = ::gbm::knob("GBM_BRR_OWN_R")) R2 = std::max(2, std::min<int>(SB_RMAX, atoi(er) & ~1));
       const int O2 = R2 > 0 ? (SBK + R2 - 1) / R2 : 0;
       const int ncu = std::min(cus, 256);
       for (int Ko = 16; R2 > 0 && Ko <= LA_KMAX && O2 < ncu; Ko += 16) {
@@ -1861,7 +1861,7 @@ static int brr_fit_impl(const double* X, int64_t n, int64_t p, int64_t ldx, cons
   GBM_TRY(ensure(cx.gamm, dev, nblk * bk * 8));
   brr_gram_kernel<<<(unsigned)(nblk * nw), 256, 0, s>>>((const double*)cx.Xt.p, npad, p, n, nw, (double*)cx.W.p);
   GBM_LAUNCH_CHECK();
-  const bool traced = sweep && std::getenv("GBM_BRR_TRACE") != nullptr;
+  const bool traced = sweep && ::gbm::knob("GBM_BRR_TRACE") != nullptr;
   const int64_t trace_n = traced ? (int64_t)la2C * nsb * 8 : 0;
   if (sweep) {
     GBM_TRY(ensure(cx.Wsb, dev, nsb * SB_PAIRS * BK2 * BK2 * 8));
@@ -2029,7 +2029,7 @@ static int brr_fit_impl(const double* X, int64_t n, int64_t p, int64_t ldx, cons
     int32_t inf = 0;
     GBM_HIP_TRY(hipMemcpyAsync(&inf, (int32_t*)cx.sbcnt.p + 24, sizeof(int32_t), hipMemcpyDeviceToHost, s));
     GBM_HIP_TRY(hipStreamSynchronize(s));
-    if (std::getenv("GBM_BRR_TEST_SWEEP_TIMEOUT")) inf = -1;  // tests: the fall-back's reporting, no device timeout
+    if (::gbm::knob("GBM_BRR_TEST_SWEEP_TIMEOUT")) inf = -1;  // tests: the fall-back's reporting, no device timeout
     if (inf < 0) {
       *sweep_timeout = true;
       return fail(GBM_E_HIP, "gbm_brr_fit: a sweep hand-off between workgroups timed out");

@@ -504,8 +504,8 @@ static int resident_wgs() {
   return cus * WPS;  // WPS workgroups per CU (LDS 2 x 2 x BK x 1152 B each)
 }
 
-// Environment tuning of the GRM launch, read at every plan (cheap: a few getenv calls), so the
-// modes can be forced per call (tests) without a process restart.
+// Tuning of the GRM launch (GBM_* knobs, knobs.cpp), read at every plan (a few table lookups), so the
+// modes can be forced per call (tests, through gbm_debug_set) without a process restart.
 struct GrmTuning {
   int carry = -1;              // GBM_GRM_CARRY: 0 slabs, 1 in-order carry, -1 automatic
   bool edge = true;            // GBM_GRM_EDGE: ragged-edge kernel for a last tile column of <= 64
@@ -517,14 +517,14 @@ struct GrmTuning {
 static GrmTuning grm_tuning() {
   GrmTuning t;
   auto flag = [](const char* name, bool dflt) {
-    const char* e = getenv(name);
+    const char* e = ::gbm::knob(name);
     return e ? atoi(e) != 0 : dflt;
   };
-  if (const char* e = getenv("GBM_GRM_CARRY")) t.carry = atoi(e) != 0 ? 1 : 0;
+  if (const char* e = ::gbm::knob("GBM_GRM_CARRY")) t.carry = atoi(e) != 0 ? 1 : 0;
   t.edge = flag("GBM_GRM_EDGE", true);
   t.persist = flag("GBM_GRM_PERSIST", true);
   t.edge_concurrent = flag("GBM_GRM_EDGE_CONCURRENT", true);
-  if (const char* ov = getenv("GBM_GRM_SPLIT")) {
+  if (const char* ov = ::gbm::knob("GBM_GRM_SPLIT")) {
     for (const char* q = ov; *q;) {
       char* end = nullptr;
       const double x = strtod(q, &end);
@@ -828,7 +828,7 @@ syrk64_sub_kernel(const double* __restrict__ U, int64_t ldu, int64_t c0, int64_t
 // re-read at every solve so tests can force the grouped paths on small matrices)
 static std::atomic<int64_t> g_small_lim{2048};
 void chol_refresh_tuning() {
-  const char* e = getenv("GBM_UPD64_LIM");
+  const char* e = ::gbm::knob("GBM_UPD64_LIM");
   g_small_lim.store(e ? (int64_t)atoll(e) : (int64_t)2048, std::memory_order_relaxed);
 }
 int64_t chol_small_lim() { return g_small_lim.load(std::memory_order_relaxed); }

@@ -665,7 +665,7 @@ static XgLayout xg_layout(int64_t n, int64_t p) {
   // least 64 groups
   const int64_t xblocks = (L.npad + 255) / 256;  // the transpose grid's x
   int64_t tnr = std::max<int64_t>(64, (8192 + xblocks - 1) / xblocks);
-  if (const char* te = getenv("GBM_XG_TNR")) tnr = std::max<int64_t>(1, std::min<int64_t>(atoll(te), 1024));
+  if (const char* te = ::gbm::knob("GBM_XG_TNR")) tnr = std::max<int64_t>(1, std::min<int64_t>(atoll(te), 1024));
   L.nr = std::min<int64_t>(L.kp / 64, tnr);
   L.ncp = (L.kp + XG_UBLK - 1) / XG_UBLK;
   int64_t o = 0;
@@ -732,6 +732,22 @@ static int xg_choose(int emin, int emax, double wmax, int& S, int& F) {
 
 int64_t grm_exact_workspace_bytes(int64_t n, int64_t p) { return xg_layout(n, p).total; }
 
+// The status launch_grm_exact leaves in its workspace, read after the stream has drained: bit 1 (a byte outside
+// {0, 1, 2}; launch_grm_exact already failed with GBM_E_ARG) and bit 2 (a weight did not fit its S digits: the
+// digit GEMMs summed a wrong W, so G is invalid — xg_choose's bound makes that impossible, this check makes a
+// violation loud). Synchronises the stream.
+int grm_exact_status(const void* ws, int64_t n, int64_t p, hipStream_t s) {
+  if (!ws || n < 2 || p < 1) return fail(GBM_E_ARG, "gbm_dev_grm_exact_status: bad arguments");
+  const XgLayout L = xg_layout(n, p);
+  XgInfo h{};
+  GBM_HIP_TRY(hipMemcpyAsync(&h, static_cast<const int8_t*>(ws) + L.off_info, sizeof(h), hipMemcpyDeviceToHost, s));
+  GBM_HIP_TRY(hipStreamSynchronize(s));
+  if (h.bad & 2)
+    return fail(GBM_E_HIP, "exact GRM: a locus weight did not fit its base-128 digits (XgInfo bit 2); G is invalid");
+  if (h.bad & 1) return fail(GBM_E_ARG, "exact GRM: a dosage outside {0, 1, 2}");
+  return GBM_OK;
+}
+
 int launch_grm_exact(const int8_t* D, int64_t ldd, int64_t p, int64_t n, int ploidy, double* G, int64_t ldg,
                      double* mean, double* sd, int32_t* keep, int64_t* q_dev, int accum, void* ws, int64_t ws_bytes,
                      int32_t* slices_out, hipStream_t s) {
@@ -779,6 +795,9 @@ int launch_grm_exact(const int8_t* D, int64_t ldd, int64_t p, int64_t n, int plo
       return fail(GBM_E_ARG, "gbm_dev_grm_exact_i8: n^2 p W_max exceeds the 128-bit bracket range; split the loci "
                              "into shards (accum = 1)");
   }
+  // (tests) GBM_XG_TEST_S: force fewer digits than xg_choose's S, so the digits kernel flags W out of range
+  // (XgInfo.bad bit 2) and grm_exact_status reports it instead of the caller using a wrong G
+  if (const int64_t ts = knob_i64("GBM_XG_TEST_S", 0); ts >= 1 && ts < S) S = (int)std::max<int64_t>(XG_SMIN, ts);
   if (slices_out) *slices_out = S;
   xg_digits_kernel<<<(unsigned)L.ncp, XG_UBLK, 0, s>>>(w, tcol, p, L.kp, S, F, WW, VL, Cpart, info);
   GBM_LAUNCH_CHECK();
@@ -788,9 +807,9 @@ int launch_grm_exact(const int8_t* D, int64_t ldd, int64_t p, int64_t n, int plo
   xg_u_reduce_kernel<<<(unsigned)((L.npad + 63) / 64), 256, 0, s>>>(Upart, L.nr, L.npad, n, Cpart,
                                                                                       L.ncp, NU, C);
   GBM_LAUNCH_CHECK();
-  const char* be = getenv("GBM_XG_BK");
+  const char* be = ::gbm::knob("GBM_XG_BK");
   const int bk = (be && atoi(be) == 256) ? 256 : 128;
-  const char* me = getenv("GBM_XG_BM");  // 128: 128 x 64 tiles, one 8-wave workgroup per CU; 64 (default): 64 x 64, two
+  const char* me = ::gbm::knob("GBM_XG_BM");  // 128: 128 x 64 tiles, one 8-wave workgroup per CU; 64 (default): 64 x 64, two
   const int bm = (bk == 128 && !(me && atoi(me) == 128)) ? 64 : 128;  // 64 x 64 measured fastest at C2
   const int64_t rt = bm / XG_BN;
   const int64_t nI = (n + bm - 1) / bm, nJ = (n + XG_BN - 1) / XG_BN;
@@ -802,10 +821,10 @@ int launch_grm_exact(const int8_t* D, int64_t ldd, int64_t p, int64_t n, int plo
     if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     if (cus < 1) cus = 256;
     if (bm == 64) cus *= 2;  // two workgroups per CU
-    const char* ce = getenv("GBM_XG_CUS");  // tests: pretend a chip of this many CUs (forces the split tail)
+    const char* ce = ::gbm::knob("GBM_XG_CUS");  // tests: pretend a chip of this many CUs (forces the split tail)
     if (ce && atoi(ce) > 0) cus = atoi(ce);
   }
-  const char* se = getenv("GBM_XG_SPLIT");
+  const char* se = ::gbm::knob("GBM_XG_SPLIT");
   int64_t nfull = nunits, ks = 1;
   if (!(se && *se && atoi(se) == 0)) {
     const int64_t tail = nunits % cus;
@@ -819,7 +838,7 @@ int launch_grm_exact(const int8_t* D, int64_t ldd, int64_t p, int64_t n, int plo
   int32_t* cnt = reinterpret_cast<int32_t*>(w8 + L.off_cnt);
   if (nfull < nunits) GBM_HIP_TRY(hipMemsetAsync(cnt, 0, (size_t)(nunits - nfull) * 8 * 4, s));
   const unsigned grid = (unsigned)(nfull + (nunits - nfull) * ks);
-  const char* oe = getenv("GBM_XG_ORDER");
+  const char* oe = ::gbm::knob("GBM_XG_ORDER");
   // 0: row-major units (default); "AxB": blocks of A row blocks x B column blocks (row-major blocks)
   int order = 0;
   if (oe && *oe) {
@@ -936,6 +955,10 @@ extern "C" int gbm_debug_xg_choose(double wmin, double wmax, int* slices_out, in
 }
 
 extern "C" int64_t gbm_dev_grm_exact_workspace(int64_t n, int64_t p) { return gbm::grm_exact_workspace_bytes(n, p); }
+
+extern "C" int gbm_dev_grm_exact_status(const void* workspace, int64_t n, int64_t p, void* stream) {
+  return gbm::grm_exact_status(workspace, n, p, (hipStream_t)stream);
+}
 
 extern "C" int gbm_dev_grm_exact_i8(const int8_t* D, int64_t ldd, int64_t p, int64_t n, int ploidy, double* G,
                                     int64_t ldg, double* mean, double* sd, int32_t* keep, int64_t* q_dev, int accum,

@@ -78,7 +78,7 @@ inline int dalloc(DevMem& m, int dev, int64_t bytes) {
   alloc_counter().fetch_add(1, std::memory_order_relaxed);
   // GBM_TEST_OOM_ONCE=1 (tests): every allocation's first attempt reports out-of-memory, so the
   // trim-and-retry path below runs
-  const char* t1 = getenv("GBM_TEST_OOM_ONCE");
+  const char* t1 = ::gbm::knob("GBM_TEST_OOM_ONCE");
   hipError_t e = (t1 && t1[0] == '1') ? hipErrorOutOfMemory : hipMalloc(&m.p, (size_t)bytes);
   if (e == hipErrorOutOfMemory) {
     (void)hipGetLastError();
@@ -147,7 +147,7 @@ inline int check_devices(const int* devices, int ndev, std::vector<int>& out) {
   out.clear();
   if (!devices || ndev <= 0) {
     std::vector<int> pool;
-    if (const char* env = getenv("GBM_DEVICES")) {
+    if (const char* env = ::gbm::knob("GBM_DEVICES")) {
       for (const char* q = env; *q;) {
         char* end = nullptr;
         const long v = strtol(q, &end, 10);

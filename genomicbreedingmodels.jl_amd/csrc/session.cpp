@@ -242,6 +242,7 @@ int ensure_training(gbm_session* s, const int64_t* idx, int64_t nT, int mode = 0
     GBM_HIP_TRY(hipMemsetAsync(s->q2.p, 0, 8, st));
     GBM_TRY(launch_grm_exact((const int8_t*)s->D8T.p, nT, s->p, nT, 2, (double*)s->Gc.p, gdimT, (double*)s->mean2.p,
                              (double*)s->sd2.p, (int32_t*)s->keep2.p, (int64_t*)s->q2.p, 0, s->wsx.p, wsx, nullptr, st));
+    GBM_TRY(grm_exact_status(s->wsx.p, nT, s->p, st));
   } else {
     GBM_TRY(gbm_dev_grm((const double*)s->Z.p, npadT, s->p, nT, (double*)s->Gc.p, gdimT, s->wsg.p, wsb, st));
   }
@@ -391,8 +392,8 @@ extern "C" int gbm_session_create_dosage_i8(const int8_t* D, int64_t n, int64_t 
 
 extern "C" int gbm_session_set_grm_mode(gbm_session* s, int grm_mode) {
   if (!s) return fail(GBM_E_ARG, "gbm_session_set_grm_mode: session is NULL");
-  if (grm_mode < GBM_GRM_DEFAULT || grm_mode > GBM_GRM_AUTO)
-    return fail(GBM_E_ARG, "gbm_session_set_grm_mode: grm_mode must be GBM_GRM_DEFAULT, _FP64, _EXACT or _AUTO");
+  if (grm_mode < GBM_GRM_DEFAULT || grm_mode > GBM_GRM_DROPIN)
+    return fail(GBM_E_ARG, "gbm_session_set_grm_mode: grm_mode must be GBM_GRM_DEFAULT, _FP64, _EXACT, _AUTO or _DROPIN");
   std::lock_guard<std::mutex> lock(s->mu);
   s->grm_mode = grm_mode;
   return GBM_OK;

@@ -11,7 +11,7 @@ import threading
 
 import numpy as np
 
-ABI_VERSION = 211  # GBM_VERSION in include/gbm.h
+ABI_VERSION = 212  # GBM_VERSION in include/gbm.h
 GBM_OK = 0
 GBM_E_ARG = -1
 GBM_E_NOTPD = -2
@@ -45,12 +45,12 @@ EXPORTS = (
     "gbm_dev_chol_group_update_cols", "gbm_dev_chol_group_update_tiles", "gbm_dev_grm_exact_workspace", "gbm_dev_grm_exact_i8",
     "gbm_gblup_fit_ex", "gbm_gblup_fit_reml_ex", "gbm_gblup_fit_dosage_i8_ex", "gbm_gblup_fit_synthetic_ex",
     "gbm_session_set_grm_mode", "gbm_session_grm_used", "gbm_debug_rccl_calls", "gbm_debug_xg_choose", "gbm_debug_chol_flow_order",
-    "gbm_debug_chol_flow_order_check", "gbm_debug_chol_flow_order_size",
+    "gbm_debug_chol_flow_order_check", "gbm_debug_chol_flow_order_size", "gbm_dev_grm_exact_status", "gbm_debug_set",
 )
 
-GBM_GRM_DEFAULT, GBM_GRM_FP64, GBM_GRM_EXACT, GBM_GRM_AUTO = -1, 0, 1, 2
+GBM_GRM_DEFAULT, GBM_GRM_FP64, GBM_GRM_EXACT, GBM_GRM_AUTO, GBM_GRM_DROPIN = -1, 0, 1, 2, 3
 GRM_MODES = {None: GBM_GRM_DEFAULT, "default": GBM_GRM_DEFAULT, "fp64": GBM_GRM_FP64, "exact": GBM_GRM_EXACT,
-             "auto": GBM_GRM_AUTO}
+             "auto": GBM_GRM_AUTO, "dropin": GBM_GRM_DROPIN}
 
 
 def grm_mode(mode) -> int:
@@ -60,7 +60,7 @@ def grm_mode(mode) -> int:
     try:
         return GRM_MODES[mode]
     except (KeyError, TypeError):
-        raise ArgumentError(f"grm must be one of 'auto', 'exact', 'fp64' or None, got {mode!r}") from None
+        raise ArgumentError(f"grm must be one of 'auto', 'exact', 'fp64', 'dropin' or None, got {mode!r}") from None
 
 
 class ArgumentError(ValueError):
@@ -234,6 +234,10 @@ def _declare(lib):
     lib.gbm_debug_chol_flow_order_size.argtypes = [I32]
     lib.gbm_debug_chol_flow_order_check.restype = I64
     lib.gbm_debug_chol_flow_order_check.argtypes = [I32, P, I64]
+    lib.gbm_dev_grm_exact_status.restype = I32
+    lib.gbm_dev_grm_exact_status.argtypes = [P, I64, I64, P]
+    lib.gbm_debug_set.restype = I32
+    lib.gbm_debug_set.argtypes = [ctypes.c_char_p, ctypes.c_char_p]
     return lib
 
 
@@ -266,6 +270,17 @@ def load():
             if v != ABI_VERSION:
                 raise ImportError(f"libgbm.so ABI version {v} != {ABI_VERSION}")
         return _lib
+
+
+def debug_set(name: str, value=None):
+    """Set (or with None clear) a GBM_* knob in libgbm and in os.environ alike. libgbm reads the environment
+    once, at its first knob lookup, so a knob changed after the library has run goes through here (tests,
+    timing tools); the os.environ copy serves the Python-level knobs (gbm.sharded) and child processes."""
+    if value is None:
+        os.environ.pop(name, None)
+    else:
+        os.environ[name] = str(value)
+    check(load().gbm_debug_set(name.encode(), None if value is None else str(value).encode()), "gbm_debug_set")
 
 
 def last_error() -> str:

@@ -130,16 +130,16 @@ def gblup_synthetic(seed: int, n: int, p: int, Y: np.ndarray, lambda_: float = 1
 
 def gblup(*, genomes: Genomes, phenomes: Phenomes, idx_entries=None, idx_loci_alleles=None,
           idx_trait: int = 1, verbose: bool = False, lambda_: float = 1.0, devices=None,
-          model_label: str = "gblup", grm: str = "auto") -> Fit:
+          model_label: str = "gblup", grm: str = "dropin") -> Fit:
     """GBLUP / RR-BLUP fit returning a ``Fit`` exactly like ``ridge`` does.
 
     ``model_label="ridge"`` lets the fit flow through an unmodified reference ``predict``
     whitelist (src/prediction.jl:225): GBLUP ≡ RR-BLUP, so the linear predictor is valid.
     ``lambda_="reml"`` chooses λ = σ²_e/σ²_u by REML first (the REML result is kept in
-    ``fit.metrics_reml``). ``grm`` (Julia ``grm = :auto``): "auto" computes the GRM exactly on the int8
+    ``fit.metrics_reml``). ``grm`` (Julia ``grm = :dropin``): "auto" computes the GRM exactly on the int8
     matrix cores when the allele frequencies are diploid dosages/2 (2x ∈ {0, 1, 2} in every cell, checked on
-    the device), else with the fp64-MFMA SYRK; "fp64" / "exact" force one (include/gbm.h GBM_GRM_*). The GRM
-    used is kept in ``fit.grm_used``."""
+    the device), else with the fp64-MFMA SYRK; "fp64" / "exact" force one; the default "dropin" is the GBM_GRM
+    variable when it is set, else "auto" (include/gbm.h GBM_GRM_*). The GRM used is kept in ``fit.grm_used``."""
     X, y, entries, populations, loci_alleles = extractxyetc(
         genomes, phenomes, idx_entries=idx_entries, idx_loci_alleles=idx_loci_alleles,
         idx_trait=idx_trait, add_intercept=False)

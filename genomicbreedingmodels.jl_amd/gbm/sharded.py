@@ -655,3 +655,10 @@ class HipExactShardStages(HipStreamedShardStages):
                                                  self.gdim, self._p(self.mean), self._p(self.sd), self._p(self.keep),
                                                  self._p(self.q), 0, self._p(self.ws_grm), self.ws_grm_bytes,
                                                  ctypes.byref(self.slices), self._stream()), "grm_exact_i8")
+
+    def download(self):
+        # the exact GRM's own status (a weight outside its digits' range: G invalid) before the results are used;
+        # the stream is drained here anyway
+        _lib.check(self.lib.gbm_dev_grm_exact_status(self._p(self.ws_grm), self.n, self.p, self._stream()),
+                   "grm_exact_status")
+        return super().download()

@@ -14,10 +14,12 @@ end
 
 # GRM arithmetic (include/gbm.h GBM_GRM_*): :auto = exact int8-MFMA GRM when the allele frequencies are
 # diploid dosages/2 (2x ∈ {0, 1, 2} in every cell, checked on the device), else the fp64-MFMA SYRK
-const GBM_GRM_MODES = Dict(:default => Cint(-1), :fp64 => Cint(0), :exact => Cint(1), :auto => Cint(2))
+# :dropin (gblup's default) = the GBM_GRM variable when it is set, else :auto
+const GBM_GRM_MODES = Dict(:default => Cint(-1), :fp64 => Cint(0), :exact => Cint(1), :auto => Cint(2),
+                           :dropin => Cint(3))
 
 function gbm_grm_mode(grm::Symbol)::Cint
-    haskey(GBM_GRM_MODES, grm) || throw(ArgumentError("grm must be :auto, :exact, :fp64 or :default, got :$grm"))
+    haskey(GBM_GRM_MODES, grm) || throw(ArgumentError("grm must be :dropin, :auto, :exact, :fp64 or :default, got :$grm"))
     GBM_GRM_MODES[grm]
 end
 
@@ -29,7 +31,7 @@ end
 
 """
     gblup(; genomes, phenomes, idx_entries=nothing, idx_loci_alleles=nothing, idx_trait=1,
-          verbose=false, λ=1.0, devices=Int32[], model_label="gblup", grm=:auto)::Fit
+          verbose=false, λ=1.0, devices=Int32[], model_label="gblup", grm=:dropin)::Fit
 
 GBLUP / RR-BLUP on V = G + λI with G = ZZᵀ/q, fitted on MI355X GPUs through libgbm.so.
 Same keywords and Fit assembly as `ridge` (src/linear.jl:162-239), so it runs unchanged under
@@ -38,9 +40,10 @@ Same keywords and Fit assembly as `ridge` (src/linear.jl:162-239), so it runs un
 reference's loglikreml objective, src/gwas.jl:450-483, over gwasreml's box, :577-590); a partial
 of `gblup` with `λ = :reml` (e.g. `gblup_reml(; kw...) = gblup(; kw..., λ = :reml)`) then goes into
 `cvbulk(models = [...])` unchanged.
-`grm = :auto` (default) computes the GRM exactly on the int8 matrix cores when the allele frequencies
+`grm = :auto` computes the GRM exactly on the int8 matrix cores when the allele frequencies
 are diploid dosages/2 (the usual `Genomes` of a diploid population; ≈3× faster at n = 5 000 and exact up to
-each locus weight's fp64 rounding), else with the fp64-MFMA SYRK; `:fp64` / `:exact` force one.
+each locus weight's fp64 rounding), else with the fp64-MFMA SYRK; `:fp64` / `:exact` force one. The default
+`grm = :dropin` is `:auto` unless the environment sets GBM_GRM (fp64 | exact | auto), which then decides.
 """
 function gblup(;
     genomes::Genomes,
@@ -52,7 +55,7 @@ function gblup(;
     λ::Union{Float64,Symbol} = 1.0,
     devices::Vector{Int32} = Int32[],
     model_label::String = "gblup",
-    grm::Symbol = :auto,
+    grm::Symbol = :dropin,
 )::Fit
     X, y, entries, populations, loci_alleles = extractxyetc(
         genomes,

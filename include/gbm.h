@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define GBM_VERSION 211 /* 0.2.1.1: row-range trailing update (distributed solve look-ahead) */
+#define GBM_VERSION 212 /* 0.2.1.2: knobs read once (gbm_debug_set), gbm_dev_grm_exact_status */
 
 #define GBM_OK 0
 #define GBM_E_ARG (-1)    /* bad argument (ArgumentError on the Julia side, src/prediction.jl:67-127 style) */
@@ -61,12 +61,15 @@ extern "C" {
  *                  input needs ploidy 2; otherwise GBM_E_ARG. More accurate than fp64 and ~3x faster.
  *   GBM_GRM_AUTO   EXACT when the genotypes are diploid dosages (checked on the device: for fp64 X while it is
  *                  converted to bytes, one chunk of loci first), else FP64.
- *   GBM_GRM_DEFAULT the environment variable GBM_GRM ("fp64" | "exact" | "auto", re-read per call), else FP64.
+ *   GBM_GRM_DEFAULT the environment variable GBM_GRM ("fp64" | "exact" | "auto"; read once, gbm_debug_set), else FP64.
+ *   GBM_GRM_DROPIN  GBM_GRM when it is set, else AUTO: the default of the drop-in gblup (Julia and Python), so a
+ *                   GBM_GRM=fp64 set by a user or CI pins the fp64 SYRK there as everywhere else.
  * The entries without _ex pass GBM_GRM_DEFAULT. */
 #define GBM_GRM_DEFAULT (-1)
 #define GBM_GRM_FP64 0
 #define GBM_GRM_EXACT 1
 #define GBM_GRM_AUTO 2
+#define GBM_GRM_DROPIN 3
 
 /* Library version (GBM_VERSION) — used by bindings to check the ABI. */
 int gbm_version(void);
@@ -416,6 +419,11 @@ int64_t gbm_dev_grm_exact_workspace(int64_t n, int64_t p);
 int gbm_dev_grm_exact_i8(const int8_t* D, int64_t ldd, int64_t p, int64_t n, int ploidy, double* G, int64_t ldg,
                          double* mean, double* sd, int32_t* keep, int64_t* q_dev, int accum, void* workspace,
                          int64_t ws_bytes, int32_t* slices_out, void* stream);
+/* The status a gbm_dev_grm_exact_i8 launch left in its workspace (same n, p, workspace; synchronises the
+ * stream): GBM_E_HIP when a locus weight did not fit its S base-128 digits (G invalid; xg_choose's bound rules it
+ * out, this makes a violation loud), GBM_E_ARG for a dosage outside {0, 1, 2}, else GBM_OK. The C-ABI fits and
+ * sessions call it after every exact GRM. */
+int gbm_dev_grm_exact_status(const void* workspace, int64_t n, int64_t p, void* stream);
 
 /* gbm_dev_marker_effects on int8 dosage rows (column-major D, n x p, ldd >= n, x = d/ploidy) instead of the
  * standardised fp64 rows: z = (x − mean_j)/sd_j is rebuilt in registers exactly as gbm_dev_standardize_i8
@@ -538,6 +546,11 @@ int gbm_debug_rccl_calls(int64_t* allreduce, int64_t* allgather);
 /* The exact GRM's digit count S and scale exponent F for kept-locus weights in [wmin, wmax] (host only, no
  * device work; returns 1 when every weight is exact on the 2^-F grid, 0 when the smallest are rounded). */
 int gbm_debug_xg_choose(double wmin, double wmax, int* slices_out, int* shift_out);
+/* Sets (value != NULL) or clears (NULL) a GBM_* tuning/test knob. libgbm reads the environment's GBM_*
+ * variables ONCE, at its first knob lookup, and never calls getenv on a fit path afterwards (no race with a
+ * setenv in another thread under Threads.@threads); later changes go through this entry only. Thread-safe.
+ * GBM_E_ARG unless name starts with "GBM_". */
+int gbm_debug_set(const char* name, const char* value);
 
 #ifdef __cplusplus
 }

@@ -35,3 +35,41 @@ def oracle_c():
     lib.gbm_ref_gblup_fit.restype = I
     lib.gbm_ref_gblup_fit.argtypes = [P, I, I, I, P, I, I, D, P, P, P, P]
     return lib
+
+
+class _GbmEnv:
+    """monkeypatch.setenv / delenv for GBM_* knobs: libgbm reads its environment once (csrc/knobs.cpp), so a
+    knob a test changes goes through gbm_debug_set (gbm._lib.debug_set, which also updates os.environ for the
+    Python-level knobs); every knob touched is restored when the test ends."""
+
+    def __init__(self):
+        self._saved = {}
+
+    def _save(self, name):
+        if name not in self._saved:
+            self._saved[name] = os.environ.get(name)
+
+    def setenv(self, name, value):
+        from gbm import _lib
+        self._save(name)
+        _lib.debug_set(name, str(value))
+
+    def delenv(self, name, raising=True):
+        from gbm import _lib
+        if raising and name not in os.environ:
+            raise KeyError(name)
+        self._save(name)
+        _lib.debug_set(name, None)
+
+    def undo(self):
+        from gbm import _lib
+        for name, value in self._saved.items():
+            _lib.debug_set(name, value)
+        self._saved.clear()
+
+
+@pytest.fixture
+def gbm_env():
+    env = _GbmEnv()
+    yield env
+    env.undo()

@@ -107,6 +107,26 @@ int main() {
     });
   for (auto& x : th) x.join();
   for (int t = 0; t < 8; t++) CHECK(ok[t] == 20);
+  // knobs (csrc/knobs.cpp): four threads change GBM_CHOL_FLOW_ORDER through gbm_debug_set while four others
+  // read it on every host-side dequeue-order build; no getenv, no torn or freed value (ASan)
+  CHECK(gbm_debug_set("PATH", "x") == GBM_E_ARG);
+  std::vector<std::thread> kt;
+  std::vector<int> kbad(8, 0);
+  for (int t = 0; t < 8; t++)
+    kt.emplace_back([t, &kbad] {
+      static const char* vals[3] = {"4", "6", nullptr};
+      for (int r = 0; r < 200; r++) {
+        if (t < 4) {
+          if (gbm_debug_set("GBM_CHOL_FLOW_ORDER", vals[(r + t) % 3]) != GBM_OK) kbad[t]++;
+        } else {
+          // one knob read per call: every variant's order is complete and deadlock-free (return 0)
+          if (gbm_debug_chol_flow_order(24, nullptr, 0) != 0) kbad[t]++;
+        }
+      }
+    });
+  for (auto& x : kt) x.join();
+  for (int t = 0; t < 8; t++) CHECK(kbad[t] == 0);
+  CHECK(gbm_debug_set("GBM_CHOL_FLOW_ORDER", nullptr) == GBM_OK);
   std::printf("asan driver: %d failures\n", failures);
   return failures ? 1 : 0;
 }

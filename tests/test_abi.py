@@ -34,7 +34,7 @@ def test_library_exports_every_header_symbol():
 
 def test_library_loads_and_reports_version():
     lib = gbm.load_library()
-    assert lib.gbm_version() == 211
+    assert lib.gbm_version() == 212
     assert isinstance(_lib.last_error(), str)
     for s in _lib.EXPORTS:
         assert hasattr(lib, s)
@@ -143,7 +143,7 @@ def _order_tiles(buf):
 
 
 @pytest.mark.parametrize("variant", ["default", "6", "4"])
-def test_chol_flow_dequeue_order_is_complete_and_deadlock_free(monkeypatch, variant):
+def test_chol_flow_dequeue_order_is_complete_and_deadlock_free(gbm_env, variant):
     """The dataflow Cholesky's worker dequeue order (csrc/chol_flow.hip flow_order, host-built): every upper
     64-tile except (0, 0) once, each task after everything it waits for (k-loop operands and the chain's inputs),
     checked on the host for every tile count the dataflow path runs (npad <= 12 288: nbc <= 193); the diagonal
@@ -151,7 +151,7 @@ def test_chol_flow_dequeue_order_is_complete_and_deadlock_free(monkeypatch, vari
     for two tiles), the tiles the chain and the assistant wait for alone."""
     import ctypes
     if variant != "default":  # GBM_CHOL_FLOW_ORDER is read at every call
-        monkeypatch.setenv("GBM_CHOL_FLOW_ORDER", variant)
+        gbm_env.setenv("GBM_CHOL_FLOW_ORDER", variant)
     pairs = variant == "6"
     lib = gbm.load_library()
     for nbc in range(2, 194):
@@ -178,7 +178,7 @@ def test_chol_flow_dequeue_order_is_complete_and_deadlock_free(monkeypatch, vari
     # input of its row, a missing entry, a duplicated tile and a pair over a chain input are caught; plain
     # row-major order with the partials first and no pairs is valid
     if variant == "4":  # (the swaps below are placed for the two-rows-early diagonal partials)
-        monkeypatch.delenv("GBM_CHOL_FLOW_ORDER")
+        gbm_env.delenv("GBM_CHOL_FLOW_ORDER")
     nbc = 20
     m = lib.gbm_debug_chol_flow_order_size(nbc)
     buf = (ctypes.c_int32 * m)()

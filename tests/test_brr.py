@@ -50,7 +50,7 @@ def test_gpu_brr_multi_chunk_matches_oracle():
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("n,p", [(700, 450), (1100, 129), (300, 128), (513, 1000)])
-def test_gpu_brr_byte_storage_matches_fp64_and_oracle(monkeypatch, n, p):
+def test_gpu_brr_byte_storage_matches_fp64_and_oracle(gbm_env, n, p):
     """Allele frequencies k/2 are stored as bytes for the sweeps (x = d/2 exactly) and run in
     128-marker blocks (two 64-marker halves: δ_A = M_A r̃_A, δ_B = M_B r̃_B + O r̃_A) inside one
     persistent sweep launch; the fp64 storage (GBM_BRR_I8=0) runs one launch per 64-marker block. Same sample path: both agree with each
@@ -59,7 +59,7 @@ def test_gpu_brr_byte_storage_matches_fp64_and_oracle(monkeypatch, n, p):
     X = oracle.synth_genotypes(93 + p, n, p)
     y = oracle.synth_phenotypes(X, 94)[:, 0]
     got = gbm.brr_arrays(X, y, n_iter=8, n_burnin=2, thin=1, seed=11)
-    monkeypatch.setenv("GBM_BRR_I8", "0")
+    gbm_env.setenv("GBM_BRR_I8", "0")
     f64 = gbm.brr_arrays(X, y, n_iter=8, n_burnin=2, thin=1, seed=11)
     ref = oracle.brr_gibbs(X, y, n_iter=8, n_burnin=2, thin=1, seed=11)
     rel = lambda a, b: np.abs(a - b).max() / np.abs(b).max()
@@ -70,7 +70,7 @@ def test_gpu_brr_byte_storage_matches_fp64_and_oracle(monkeypatch, n, p):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("n,p", [(1100, 300), (12000, 260)])
-def test_gpu_brr_sweep_matches_per_launch_path_and_oracle(monkeypatch, n, p):
+def test_gpu_brr_sweep_matches_per_launch_path_and_oracle(gbm_env, n, p):
     """Byte storage: the persistent super-block sweep (one launch per iteration, hand-offs between
     the chunk workgroups through self-validating write-through granules) against one launch per
     128-marker block (GBM_BRR_SWEEP=0) and the oracle's literal loop. n = 12 000: 250 chunk
@@ -80,7 +80,7 @@ def test_gpu_brr_sweep_matches_per_launch_path_and_oracle(monkeypatch, n, p):
     _, fb0 = brr_path()
     sweep = gbm.brr_arrays(X, y, n_iter=5, n_burnin=1, thin=1, seed=17)
     assert brr_path() == (4, fb0)
-    monkeypatch.setenv("GBM_BRR_SWEEP", "0")
+    gbm_env.setenv("GBM_BRR_SWEEP", "0")
     launches = gbm.brr_arrays(X, y, n_iter=5, n_burnin=1, thin=1, seed=17)
     ref = oracle.brr_gibbs(X, y, n_iter=5, n_burnin=1, thin=1, seed=17)
     rel = lambda a, b: np.abs(a - b).max() / np.abs(b).max()
@@ -132,14 +132,14 @@ def test_gpu_bayesian_model_function():
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("sweep", ["1", "0"])
-def test_gpu_brr_pooled_no_allocation_after_warmup_and_threads(monkeypatch, sweep):
+def test_gpu_brr_pooled_no_allocation_after_warmup_and_threads(gbm_env, sweep):
     """gbm_brr_fit leases a pooled per-device context (VERDICT r02 Weak #9): after a warm-up fit, a
     fit of the same shape makes no device allocation and reuses its captured iteration graph
     (bit-identical results). Four threads fitting at once on one device (cvmultithread! with
     bayesian("BRR")) give the serial results bit for bit: their persistent sweeps take turns
     (a per-device lock), so none can be partly resident and spin on another."""
     import threading
-    monkeypatch.setenv("GBM_BRR_SWEEP", sweep)
+    gbm_env.setenv("GBM_BRR_SWEEP", sweep)
     lib = gbm.load_library()
     X = oracle.synth_genotypes(301, 700, 900)
     ys = [oracle.synth_phenotypes(X, 302 + k)[:, 0] for k in range(4)]
@@ -181,7 +181,7 @@ def brr_path():
 @pytest.mark.parametrize("n,p,K", [(1100, 300, None), (12000, 1300, None), (5000, 777, "48"), (3000, 1025, "32"),
                                    (10000, 1100, None), (4000, 900, None), (6000, 2600, None), (10000, 1100, "R4"),
                                    (9000, 2100, "R2")])
-def test_gpu_brr_super_block_sweep_runs_and_matches(monkeypatch, n, p, K):
+def test_gpu_brr_super_block_sweep_runs_and_matches(gbm_env, n, p, K):
     """The super-block sweep really runs (no fall-back to the per-launch path): chunks of <= 48
     individuals, two granule hand-offs per super-block, two steps of slack for the partial dots
     (brr_sweep_la2_kernel, path 4: C2_s δ_{s−2} + C_s δ_{s−1} on the chain). It agrees with the
@@ -189,16 +189,16 @@ def test_gpu_brr_super_block_sweep_runs_and_matches(monkeypatch, n, p, K):
     including nsb = 1, 2, 3, 6; several chunk sizes, and the owner/non-owner chunk split (owners of
     R = 4, 2 rows with smaller chunks). (The round-3 schedules 1-3 are no longer built.)"""
     if K and K.startswith("R"):  # owners of R rows in the chunk split
-        monkeypatch.setenv("GBM_BRR_OWN_R", K[1:])
+        gbm_env.setenv("GBM_BRR_OWN_R", K[1:])
     elif K:
-        monkeypatch.setenv("GBM_BRR_SB_K", K)
+        gbm_env.setenv("GBM_BRR_SB_K", K)
     X = oracle.synth_genotypes(n + p, n, p)
     y = oracle.synth_phenotypes(X, 17)[:, 0]
     _, fb0 = brr_path()
     la2 = gbm.brr_arrays(X, y, n_iter=4, n_burnin=1, thin=1, seed=23)
     path, fb = brr_path()
     assert path == 4 and fb == fb0
-    monkeypatch.setenv("GBM_BRR_SWEEP", "0")
+    gbm_env.setenv("GBM_BRR_SWEEP", "0")
     launches = gbm.brr_arrays(X, y, n_iter=4, n_burnin=1, thin=1, seed=23)
     assert brr_path()[0] == 0
     rel = lambda a, b: np.abs(a - b).max() / np.abs(b).max()
@@ -210,20 +210,20 @@ def test_gpu_brr_super_block_sweep_runs_and_matches(monkeypatch, n, p, K):
 
 
 @pytest.mark.gpu
-def test_gpu_brr_fallback_is_reported(monkeypatch):
+def test_gpu_brr_fallback_is_reported(gbm_env):
     """A sweep whose hand-offs time out is re-run on the per-launch path; the call succeeds (valid
     results, equal to the per-launch fit) but says so: gbm_last_error() starts with "warning", the
     Python mirror raises a RuntimeWarning, the fall-back counter grows. GBM_BRR_TEST_SWEEP_TIMEOUT
     makes the host treat a completed sweep as timed out (no device-side timeout is provoked)."""
     X = oracle.synth_genotypes(55, 1200, 700)
     y = oracle.synth_phenotypes(X, 56)[:, 0]
-    monkeypatch.setenv("GBM_BRR_SWEEP", "0")
+    gbm_env.setenv("GBM_BRR_SWEEP", "0")
     ref = gbm.brr_arrays(X, y, n_iter=4, n_burnin=1, thin=1, seed=9)
-    monkeypatch.delenv("GBM_BRR_SWEEP")
+    gbm_env.delenv("GBM_BRR_SWEEP")
     gbm.brr_arrays(X, y, n_iter=4, n_burnin=1, thin=1, seed=9)
     assert gbm._lib.last_error() == ""  # a clean sweep fit leaves no message
     _, fb0 = brr_path()
-    monkeypatch.setenv("GBM_BRR_TEST_SWEEP_TIMEOUT", "1")
+    gbm_env.setenv("GBM_BRR_TEST_SWEEP_TIMEOUT", "1")
     with pytest.warns(RuntimeWarning, match="per-launch path"):
         got = gbm.brr_arrays(X, y, n_iter=4, n_burnin=1, thin=1, seed=9)
     assert brr_path() == (0, fb0 + 1)

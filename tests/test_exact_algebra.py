@@ -198,3 +198,25 @@ def test_digit_count_at_the_range_boundary_matches_exact_integers():
                     digits.append(r)
                     x = (x - r) >> 7
                 assert x == 0 and sum(d * 128 ** k for k, d in enumerate(digits)) == W
+
+
+def test_digit_overflow_is_flagged_exactly_past_the_boundary():
+    """xg_digits_kernel's range check (csrc/grm_exact.hip: after S balanced base-128 digits the remainder x must be
+    0, else XgInfo bit 2 and gbm_dev_grm_exact_status fails the call): W = 63 (128^S - 1)/127 is the largest W that
+    S digits hold (remainder 0, digits rebuild W), W + 1 is the first that leaves a remainder; for S = 8, 9, 10."""
+    def remainder(W, S):
+        x = W
+        for _ in range(S):
+            r = x & 127
+            r = r - 128 if r >= 64 else r
+            x = (x - r) >> 7
+        return x
+
+    for S in (8, 9, 10):
+        top = digit_max(S)
+        assert top == 63 * (128 ** S - 1) // 127
+        assert remainder(top, S) == 0 and digits(top, S) == [63] * S
+        assert remainder(top + 1, S) != 0
+        assert remainder(top - 1, S) == 0
+        # forcing S - 1 digits on a weight that needs S (GBM_XG_TEST_S, the GPU test's fault injection) is flagged
+        assert remainder(digit_max(S - 1) + 1, S - 1) != 0

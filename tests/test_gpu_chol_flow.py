@@ -43,12 +43,12 @@ def _pair(n, p, t, seed, lam):
     (3000, 2000, 2, 11, 0.8),    # 48 tile rows
     (5000, 1500, 1, 19, 1.0),    # the C2 individual count (80 tile rows)
 ])
-def test_flow_matches_oracle_and_panel_path(monkeypatch, n, p, t, seed, lam):
+def test_flow_matches_oracle_and_panel_path(gbm_env, n, p, t, seed, lam):
     import torch
     X, Y, flow, panel = _pair(n, p, t, seed, lam)
-    monkeypatch.setenv("GBM_CHOL_FLOW_MAX", "1000000")
+    gbm_env.setenv("GBM_CHOL_FLOW_MAX", "1000000")
     flow.solve()
-    monkeypatch.setenv("GBM_CHOL_FLOW_MAX", "0")
+    gbm_env.setenv("GBM_CHOL_FLOW_MAX", "0")
     panel.solve()
     torch.cuda.synchronize()
     assert int(flow.info.item()) == 0 and int(panel.info.item()) == 0
@@ -65,11 +65,11 @@ def test_flow_matches_oracle_and_panel_path(monkeypatch, n, p, t, seed, lam):
     assert rel(flow.mu.cpu().numpy(), ref["mu"]) < 1e-9
 
 
-def test_flow_repeated_solves_bit_identical(monkeypatch):
+def test_flow_repeated_solves_bit_identical(gbm_env):
     """Each tile's updates are summed in k order in its own accumulators, whatever the schedule:
     repeated solves (different workgroup placement and timing) give identical bits."""
     import torch
-    monkeypatch.setenv("GBM_CHOL_FLOW_MAX", "1000000")
+    gbm_env.setenv("GBM_CHOL_FLOW_MAX", "1000000")
     X, Y, a, b = _pair(2100, 900, 2, 5, 1.0)
     G0 = a.G.clone()
     first = None
@@ -86,7 +86,7 @@ def test_flow_repeated_solves_bit_identical(monkeypatch):
 
 
 @pytest.mark.parametrize("bad", [0, 700, 1029])
-def test_flow_reports_first_failing_pivot(monkeypatch, bad):
+def test_flow_reports_first_failing_pivot(gbm_env, bad):
     """A matrix that is not positive definite: the factorisation ends (no hang) and info is the
     first failing column + 1, as in the launch-per-panel path."""
     import torch
@@ -96,9 +96,9 @@ def test_flow_reports_first_failing_pivot(monkeypatch, bad):
         st.G[:st.npad, :st.npad].fill_diagonal_(1.0)
         st.G[bad, bad] = -5.0
         st.q.fill_(1)
-    monkeypatch.setenv("GBM_CHOL_FLOW_MAX", "1000000")
+    gbm_env.setenv("GBM_CHOL_FLOW_MAX", "1000000")
     a.solve()
-    monkeypatch.setenv("GBM_CHOL_FLOW_MAX", "0")
+    gbm_env.setenv("GBM_CHOL_FLOW_MAX", "0")
     b.solve()
     torch.cuda.synchronize()
     assert int(a.info.item()) == bad + 1
@@ -106,7 +106,7 @@ def test_flow_reports_first_failing_pivot(monkeypatch, bad):
 
 
 @pytest.mark.parametrize("wgs", ["1", "2", "7"])
-def test_flow_few_resident_workgroups_complete_bit_identical(monkeypatch, wgs):
+def test_flow_few_resident_workgroups_complete_bit_identical(gbm_env, wgs):
     """Deadlock freedom: the chain workgroup waits only for its row's diagonal partial
     and the assistant's neighbour partial, the assistant only for a partial, a tile of the previous
     row and the chain's previous step, and every worker wait targets the chain's earlier steps or a
@@ -115,10 +115,10 @@ def test_flow_few_resident_workgroups_complete_bit_identical(monkeypatch, wgs):
     every tile task in dequeue order beside the chain and the assistant — and gives the bits of the
     full-grid launch."""
     import torch
-    monkeypatch.setenv("GBM_CHOL_FLOW_MAX", "1000000")
+    gbm_env.setenv("GBM_CHOL_FLOW_MAX", "1000000")
     X, Y, a, b = _pair(1030, 700, 2, 13, 0.9)
     a.solve()
-    monkeypatch.setenv("GBM_CHOL_FLOW_WGS", wgs)
+    gbm_env.setenv("GBM_CHOL_FLOW_WGS", wgs)
     b.solve()
     torch.cuda.synchronize()
     assert int(a.info.item()) == 0 and int(b.info.item()) == 0
@@ -126,24 +126,24 @@ def test_flow_few_resident_workgroups_complete_bit_identical(monkeypatch, wgs):
 
 
 @pytest.mark.parametrize("order,wgs", [("6", None), ("6", "1"), ("4", None)])
-def test_flow_dequeue_orders_bit_identical(monkeypatch, order, wgs):
+def test_flow_dequeue_orders_bit_identical(gbm_env, order, wgs):
     """The A/B dequeue orders (GBM_CHOL_FLOW_ORDER: 6 = the "other" tiles in pairs, one k-loop for two tiles;
     4 = round 4's order) sum every tile's updates in the same k order as the default: identical bits, also
     with a single worker running the paired order."""
     import torch
-    monkeypatch.setenv("GBM_CHOL_FLOW_MAX", "1000000")
+    gbm_env.setenv("GBM_CHOL_FLOW_MAX", "1000000")
     X, Y, a, b = _pair(3000, 700, 2, 21, 0.9)
     a.solve()
-    monkeypatch.setenv("GBM_CHOL_FLOW_ORDER", order)
+    gbm_env.setenv("GBM_CHOL_FLOW_ORDER", order)
     if wgs:
-        monkeypatch.setenv("GBM_CHOL_FLOW_WGS", wgs)
+        gbm_env.setenv("GBM_CHOL_FLOW_WGS", wgs)
     b.solve()
     torch.cuda.synchronize()
     assert int(a.info.item()) == 0 and int(b.info.item()) == 0
     assert torch.equal(a.gebv, b.gebv) and torch.equal(a.A, b.A) and torch.equal(a.mu, b.mu)
 
 
-def test_flow_timed_out_wait_drains_and_fails_loudly(monkeypatch):
+def test_flow_timed_out_wait_drains_and_fails_loudly(gbm_env):
     """A wait that times out (info = −1; a bug guard, forced here by GBM_TEST_CHOL_FLOW_ABORT) stops
     the chain before it publishes another tile and keeps workers from taking new tasks:
     the launch drains at once and the solve reports info = −1 instead of computing on stale tiles.
@@ -151,16 +151,16 @@ def test_flow_timed_out_wait_drains_and_fails_loudly(monkeypatch):
     import time
 
     import torch
-    monkeypatch.setenv("GBM_CHOL_FLOW_MAX", "1000000")
+    gbm_env.setenv("GBM_CHOL_FLOW_MAX", "1000000")
     X, Y, a, b = _pair(3000, 700, 1, 23, 1.0)
-    monkeypatch.setenv("GBM_TEST_CHOL_FLOW_ABORT", "1")
+    gbm_env.setenv("GBM_TEST_CHOL_FLOW_ABORT", "1")
     t0 = time.perf_counter()
     a.solve()
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     assert int(a.info.item()) == -1
     assert dt < 2.0, dt  # drained, not ~1 s per stuck wait
-    monkeypatch.delenv("GBM_TEST_CHOL_FLOW_ABORT")
+    gbm_env.delenv("GBM_TEST_CHOL_FLOW_ABORT")
     b.solve()
     torch.cuda.synchronize()
     assert int(b.info.item()) == 0

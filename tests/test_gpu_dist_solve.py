@@ -46,20 +46,20 @@ def _stages(R, X, Y, lam):
     (8, 3000, ("0", "0", "0"), "0-nolook"),  # the next group's panels after the whole trailing update (no look-ahead)
     (8, 3000, ("0", "0", "0"), "0-tailflow"),  # the last 1024 rows in one dataflow launch (GBM_CHOL_TAIL_FLOW)
 ])
-def test_distributed_factorisation_bit_identical(monkeypatch, R, n, lims, tail):
+def test_distributed_factorisation_bit_identical(gbm_env, R, n, lims, tail):
     import torch
 
     from gbm.sharded import chol_distributed
-    monkeypatch.setenv("GBM_CHOL_G4_LIM", lims[0])
-    monkeypatch.setenv("GBM_CHOL_G8_LIM", lims[1])
-    monkeypatch.setenv("GBM_CHOL_G16_LIM", lims[2])
-    monkeypatch.setenv("GBM_UPD64_LIM", "128")
-    monkeypatch.setenv("GBM_CHOL_FLOW_MAX", "0")  # reference: the redundant launch-per-panel solve
+    gbm_env.setenv("GBM_CHOL_G4_LIM", lims[0])
+    gbm_env.setenv("GBM_CHOL_G8_LIM", lims[1])
+    gbm_env.setenv("GBM_CHOL_G16_LIM", lims[2])
+    gbm_env.setenv("GBM_UPD64_LIM", "128")
+    gbm_env.setenv("GBM_CHOL_FLOW_MAX", "0")  # reference: the redundant launch-per-panel solve
     if isinstance(tail, str):  # "<rows>-seq" / "-chain" / "-nolook": GBM_DIST_OVERLAP / GBM_CHOL_GROUP_KERNEL /
         # GBM_DIST_LOOKAHEAD = 0; "-tailflow": GBM_CHOL_TAIL_FLOW = 1024
         var = {"seq": "GBM_DIST_OVERLAP", "chain": "GBM_CHOL_GROUP_KERNEL", "nolook": "GBM_DIST_LOOKAHEAD",
                "tailflow": "GBM_CHOL_TAIL_FLOW"}
-        monkeypatch.setenv(var[tail.split("-")[1]], "1024" if tail.endswith("tailflow") else "0")
+        gbm_env.setenv(var[tail.split("-")[1]], "1024" if tail.endswith("tailflow") else "0")
         tail = int(tail.split("-")[0])
     X = oracle.synth_genotypes(n + R, n, 1200)
     Y = oracle.synth_phenotypes(X, 3, ntraits=2)

@@ -203,28 +203,28 @@ def test_exact_full_size_c2_against_fp64_grm():
 
 
 @pytest.mark.parametrize("devices", [(0,), (0, 0)])
-def test_c_abi_exact_synthetic_matches_oracle(monkeypatch, devices):
+def test_c_abi_exact_synthetic_matches_oracle(gbm_env, devices):
     """gbm_gblup_fit_synthetic with GBM_GRM=exact (the C-ABI entry a Julia ccall binds): one shard, and two
     shards on one device (their exact partial GRMs summed), against the oracle and the fp64 path."""
     n, p, seed = 700, 5000, 77
     X = oracle.synth_genotypes(seed, n, p)
     Y = oracle.synth_phenotypes(X, seed + 1, ntraits=2)
-    monkeypatch.setenv("GBM_GRM", "exact")
+    gbm_env.setenv("GBM_GRM", "exact")
     b, y, mu, q = gbm.gblup_synthetic(seed, n, p, Y, lambda_=1.0, devices=list(devices))
     ref = oracle.gblup_fit(X, Y, 1.0)
     assert q == ref["q"]
     assert rel(y, ref["y_pred"]) < 1e-9 and rel(mu, ref["mu"]) < 1e-9 and rel(b, ref["b_hat"]) < 1e-6
-    monkeypatch.delenv("GBM_GRM")
+    gbm_env.delenv("GBM_GRM")
     b0, y0, mu0, q0 = gbm.gblup_synthetic(seed, n, p, Y, lambda_=1.0, devices=list(devices))
     assert q0 == q and rel(y, y0) < 1e-11 and rel(b, b0) < 1e-9
 
 
-def test_c_abi_exact_dosage_matches_oracle(monkeypatch):
+def test_c_abi_exact_dosage_matches_oracle(gbm_env):
     n, p = 600, 3000
     D = random_dosages(21, n, p)
     X = D.astype(np.float64) / 2.0
     Y = oracle.synth_phenotypes(X, 5, ntraits=1)
-    monkeypatch.setenv("GBM_GRM", "exact")
+    gbm_env.setenv("GBM_GRM", "exact")
     b, y, mu, q = gbm.gblup_dosage(np.asfortranarray(D), 2, Y)
     ref = oracle.gblup_fit(X, Y, 1.0)
     assert q == ref["q"]
@@ -232,10 +232,10 @@ def test_c_abi_exact_dosage_matches_oracle(monkeypatch):
 
 
 @pytest.mark.parametrize("cus", ["16", "7"])
-def test_exact_grm_split_tail(monkeypatch, cus):
+def test_exact_grm_split_tail(gbm_env, cus):
     """The partial last round of units split into loci ranges (forced on a small shape by pretending a chip
     of 16 or 7 CUs): the ranges' int32 partials summed by the last range to finish, still exact."""
-    monkeypatch.setenv("GBM_XG_CUS", cus)
+    gbm_env.setenv("GBM_XG_CUS", cus)
     n, p = 700, 1500
     D = random_dosages(31, n, p)
     G, q, S, *_ = device_grm(D)
@@ -246,11 +246,11 @@ def test_exact_grm_split_tail(monkeypatch, cus):
 
 @pytest.mark.parametrize("env", [{"GBM_XG_BM": "64"}, {"GBM_XG_BK": "256"}, {"GBM_XG_ORDER": "1"},
                                  {"GBM_XG_BM": "64", "GBM_XG_CUS": "8"}])
-def test_exact_grm_kernel_variants(monkeypatch, env):
+def test_exact_grm_kernel_variants(gbm_env, env):
     """The GEMM's tile (64 x 64, two workgroups per CU), stage (256 loci) and unit-order variants, and the
     split tail of the 64 x 64 grid: the same exact GRM."""
     for k, v in env.items():
-        monkeypatch.setenv(k, v)
+        gbm_env.setenv(k, v)
     n, p = 700, 1500
     D = random_dosages(41, n, p)
     G, q, S, *_ = device_grm(D)
@@ -260,7 +260,7 @@ def test_exact_grm_kernel_variants(monkeypatch, env):
 
 
 @pytest.mark.parametrize("source", ["synthetic", "dosage"])
-def test_session_exact_training_grm_matches_oracle(monkeypatch, source):
+def test_session_exact_training_grm_matches_oracle(gbm_env, source):
     """Sessions of dosage genotypes (synthetic, or int8 with ploidy 2) with GBM_GRM=exact: each training set's
     GRM is the exact-integer one of the gathered training dosages (the CV fold fits of cross_validation.jl and
     the REML path reuse it); fits against the oracle on the same rows, and against the fp64 session."""
@@ -275,7 +275,7 @@ def test_session_exact_training_grm_matches_oracle(monkeypatch, source):
         make = lambda: GenotypeSession(dosage_i8=D, ploidy=2)  # noqa: E731
     rng = np.random.default_rng(5)
     idx = np.sort(rng.choice(n, 450, replace=False))
-    monkeypatch.setenv("GBM_GRM", "exact")
+    gbm_env.setenv("GBM_GRM", "exact")
     with make() as s:
         b, y, mu, q = s.gblup(idx, Y[idx])
         va = np.setdiff1d(np.arange(n), idx)
@@ -284,7 +284,7 @@ def test_session_exact_training_grm_matches_oracle(monkeypatch, source):
     assert q == ref["q"]
     assert rel(y, ref["y_pred"]) < 1e-9 and rel(mu, ref["mu"]) < 1e-9 and rel(b, ref["b_hat"]) < 1e-6
     assert rel(yv, oracle.predict_linear(X[va], ref["b_hat"])) < 1e-8
-    monkeypatch.delenv("GBM_GRM")
+    gbm_env.delenv("GBM_GRM")
     with make() as s:
         b0, y0, mu0, q0 = s.gblup(idx, Y[idx])
     assert q0 == q and rel(y, y0) < 1e-11
@@ -300,3 +300,34 @@ def test_exact_grm_tiny_and_ragged_shapes(n, p):
     Gl, ql = exact_grm_ld(D)
     assert q == ql
     assert ulps_off(G, Gl) < 8
+
+
+def test_digit_overflow_fails_loudly(gbm_env):
+    """Round-4 ADVICE item 2: a locus weight that does not fit its S base-128 digits (fault-injected with
+    GBM_XG_TEST_S, one digit fewer than xg_choose's S) makes the exact GRM's status GBM_E_HIP — through the C ABI
+    fit (exact and auto alike: it is not a data property, so auto must not hide it), the stage path's download and
+    gbm_dev_grm_exact_status — instead of returning a G built from wrong weights."""
+    import torch
+    n, p = 500, 900
+    D = random_dosages(77, n, p)
+    D[:, 0] = 0
+    D[5, 0] = 1  # a single carrier: the widest weight range (S >= 9)
+    _, _, S, *_ = device_grm(D)
+    assert S >= 9
+    X = D.astype(np.float64) / 2.0
+    Y = oracle.synth_phenotypes(X, 3, ntraits=1)
+    ref = oracle.gblup_fit(X, Y, 1.0)
+    gbm_env.setenv("GBM_XG_TEST_S", str(S - 1))
+    for mode in ("exact", "auto"):
+        with pytest.raises(gbm.GBMError, match="digits"):
+            gbm.gblup_arrays(X, Y, grm=mode)
+    st = HipExactShardStages(n, p, nrhs=1, lambda_=1.0, device=0)
+    st.D.copy_(torch.from_numpy(np.ascontiguousarray(D.T)).to(st.D.device))
+    st.load_phenotypes(Y)
+    with pytest.raises(gbm.GBMError, match="digits"):
+        sharded_gblup_step(st, LocalComm())
+    gbm_env.delenv("GBM_XG_TEST_S")
+    out = sharded_gblup_step(st, LocalComm())  # the same shard, the right S: a valid fit
+    assert rel(out["y_pred"], ref["y_pred"]) < 1e-9
+    b, y, mu, q = gbm.gblup_arrays(X, Y, grm="exact")
+    assert rel(y, ref["y_pred"]) < 1e-9

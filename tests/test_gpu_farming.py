@@ -48,23 +48,23 @@ def test_same_device_shards_match_oracle(devices, n, p, t):
     ([0, 0, 0, 0], 3000, ("0", "0", "0"), "0"),     # 16, 8, 4, 2-panel groups, then single panels
     ([0, 0], 1030, ("0", "0", "0"), "512"),         # ragged n
 ])
-def test_cabi_distributed_factorisation_bit_identical(monkeypatch, devices, n, lims, tail):
+def test_cabi_distributed_factorisation_bit_identical(gbm_env, devices, n, lims, tail):
     """gbm_gblup_fit with several device leaders factors V across them (solve_distributed in
     capi.cpp: own-tile trailing updates, strip all-gathers, redundant tail). Rehearsed on one GPU
     with every shard its own leader (GBM_SHARD_LEADERS=each: copy all-reduce and copy all-gather
     in place of RCCL); bit-identical to the default path, where the shards' partial GRMs are summed
     on the device and one leader solves redundantly."""
-    monkeypatch.setenv("GBM_CHOL_G4_LIM", lims[0])
-    monkeypatch.setenv("GBM_CHOL_G8_LIM", lims[1])
-    monkeypatch.setenv("GBM_CHOL_G16_LIM", lims[2])
-    monkeypatch.setenv("GBM_UPD64_LIM", "128")
-    monkeypatch.setenv("GBM_CHOL_FLOW_MAX", "0")  # both sides on the launch-per-panel solve
+    gbm_env.setenv("GBM_CHOL_G4_LIM", lims[0])
+    gbm_env.setenv("GBM_CHOL_G8_LIM", lims[1])
+    gbm_env.setenv("GBM_CHOL_G16_LIM", lims[2])
+    gbm_env.setenv("GBM_UPD64_LIM", "128")
+    gbm_env.setenv("GBM_CHOL_FLOW_MAX", "0")  # both sides on the launch-per-panel solve
     X = oracle.synth_genotypes(n + len(devices), n, 1900)
     Y = oracle.synth_phenotypes(X, 3, ntraits=2)
     ref = gbm.gblup_arrays(X, Y, lambda_=0.8, devices=devices)
-    monkeypatch.setenv("GBM_SHARD_LEADERS", "each")
-    monkeypatch.setenv("GBM_DIST_SOLVE_MIN_N", "0")
-    monkeypatch.setenv("GBM_DIST_TAIL_ROWS", tail)
+    gbm_env.setenv("GBM_SHARD_LEADERS", "each")
+    gbm_env.setenv("GBM_DIST_SOLVE_MIN_N", "0")
+    gbm_env.setenv("GBM_DIST_TAIL_ROWS", tail)
     got = gbm.gblup_arrays(X, Y, lambda_=0.8, devices=devices)
     for a, b in zip(got, ref):
         assert np.array_equal(np.asarray(a), np.asarray(b))
@@ -87,11 +87,12 @@ def test_cabi_distributed_factorisation_default_thresholds():
     Y = np.asfortranarray(rng.standard_normal((n, 2)))
     assert "GBM_DIST_SOLVE_MIN_N" not in os.environ
     ref = gbm.gblup_synthetic(99, n, p, Y, lambda_=0.5, devices=[0, 0])
-    os.environ["GBM_SHARD_LEADERS"] = "each"
+    from gbm import _lib
+    _lib.debug_set("GBM_SHARD_LEADERS", "each")
     try:
         got = gbm.gblup_synthetic(99, n, p, Y, lambda_=0.5, devices=[0, 0])
     finally:
-        del os.environ["GBM_SHARD_LEADERS"]
+        _lib.debug_set("GBM_SHARD_LEADERS", None)
         gbm.load_library().gbm_release_device_cache()
     for a, b in zip(got, ref):
         assert np.array_equal(np.asarray(a), np.asarray(b))
@@ -128,12 +129,12 @@ def test_no_device_allocation_after_warmup():
     assert lib.gbm_device_allocations() > a1  # the cache was really dropped
 
 
-def test_gbm_devices_farming_eight_threads(monkeypatch):
+def test_gbm_devices_farming_eight_threads(gbm_env):
     """cvmultithread! calls the model from Threads.@threads with no devices argument: every
     thread takes its own slot of GBM_DEVICES. Eight threads on a one-GPU box (GBM_DEVICES lists
     device 0 eight times) give the serial results bit for bit, and once the pool holds a context
     per concurrent call, a round allocates nothing (each call leases a pooled context)."""
-    monkeypatch.setenv("GBM_DEVICES", ",".join(["0"] * 8))
+    gbm_env.setenv("GBM_DEVICES", ",".join(["0"] * 8))
     lib = gbm.load_library()
     lib.gbm_release_device_cache()
     X = oracle.synth_genotypes(5, 1030, 1400)
@@ -170,28 +171,28 @@ def test_gbm_devices_farming_eight_threads(monkeypatch):
     assert quiet
 
 
-def test_gbm_devices_bad_ordinal_is_an_argument_error(monkeypatch):
-    monkeypatch.setenv("GBM_DEVICES", "0,4096")
+def test_gbm_devices_bad_ordinal_is_an_argument_error(gbm_env):
+    gbm_env.setenv("GBM_DEVICES", "0,4096")
     X = oracle.synth_genotypes(1, 50, 100)
     with pytest.raises(gbm.ArgumentError):
         gbm.gblup_arrays(X, np.arange(50.0))
 
 
 @pytest.mark.parametrize("chunk,carry", [(500, None), (1024, None), (1200, None), (1200, "1")])
-def test_pipelined_host_upload_matches_oracle(monkeypatch, chunk, carry):
+def test_pipelined_host_upload_matches_oracle(gbm_env, chunk, carry):
     """gbm_gblup_fit with the host genotypes uploaded in loci chunks overlapped with the device
     work (GBM_HOST_CHUNK, re-read per call): chunk GRMs summed in order into G. Matches the oracle
     and the one-piece upload to rounding; the int8 entry (same chunks) stays bit-identical. Chunks
     after the first are added into G by the GRM itself (slab reduce, or range 0 of the in-order
     carry when GBM_GRM_CARRY=1); 1200 = 1200 + the halving tail 550 + 550."""
     if carry is None:
-        monkeypatch.delenv("GBM_GRM_CARRY", raising=False)  # the planner's choice (slabs here)
+        gbm_env.delenv("GBM_GRM_CARRY", raising=False)  # the planner's choice (slabs here)
     else:
-        monkeypatch.setenv("GBM_GRM_CARRY", carry)
+        gbm_env.setenv("GBM_GRM_CARRY", carry)
     n, p = 700, 2300
     X = oracle.synth_genotypes(31, n, p)
     Y = oracle.synth_phenotypes(X, 32, ntraits=2)
-    monkeypatch.setenv("GBM_HOST_CHUNK", str(chunk))
+    gbm_env.setenv("GBM_HOST_CHUNK", str(chunk))
     b_hat, y_pred, mu, q = gbm.gblup_arrays(X, Y, lambda_=0.8)
     ref = oracle.gblup_fit(X, Y, 0.8)
     assert q == ref["q"]
@@ -210,22 +211,22 @@ def test_pipelined_host_upload_matches_oracle(monkeypatch, chunk, carry):
                                      b2.ctypes.data, y2.ctypes.data, mu2.ctypes.data, q2.ctypes.data)
     assert rc == 0, lib.gbm_last_error()
     assert np.array_equal(y2, y_pred) and np.array_equal(b2, b_hat)
-    monkeypatch.setenv("GBM_HOST_CHUNK", "0")
+    gbm_env.setenv("GBM_HOST_CHUNK", "0")
     b3, y3, mu3, q3 = gbm.gblup_arrays(X, Y, lambda_=0.8)
     assert q3 == q and np.abs(y3 - y_pred).max() < 1e-11 * np.abs(y3).max()
 
 
 @pytest.mark.parametrize("devices,chunk,leaders", [
     ([0, 0], "500", None), ([0, 0, 0], "700", None), ([0, 0], "500", "each"), ([0, 0], "0", None)])
-def test_multi_shard_fit_concurrent_equals_serial(monkeypatch, devices, chunk, leaders):
+def test_multi_shard_fit_concurrent_equals_serial(gbm_env, devices, chunk, leaders):
     """The in-process multi-device fit drives every shard's upload, standardisation and partial GRM
     from its own host thread (capi.cpp parallel_shards; VERDICT r02 Missing #1): shard k+1's upload
     no longer waits for shard k's GRM. Same-device shards rehearse it on one GPU. Bit-identical to
     the one-after-the-other schedule (GBM_SHARD_THREADS=0) for the chunked host upload, the
     one-piece upload, both leader modes, the int8 entry and the GRM entries; matches the oracle."""
-    monkeypatch.setenv("GBM_HOST_CHUNK", chunk)
+    gbm_env.setenv("GBM_HOST_CHUNK", chunk)
     if leaders:
-        monkeypatch.setenv("GBM_SHARD_LEADERS", leaders)
+        gbm_env.setenv("GBM_SHARD_LEADERS", leaders)
     n, p = 700, 2900
     X = oracle.synth_genotypes(77, n, p)
     X[:, 3] = 0.5
@@ -247,7 +248,7 @@ def test_multi_shard_fit_concurrent_equals_serial(monkeypatch, devices, chunk, l
 
     runs = {}
     for mode in ("1", "0"):
-        monkeypatch.setenv("GBM_SHARD_THREADS", mode)
+        gbm_env.setenv("GBM_SHARD_THREADS", mode)
         runs[mode] = (gbm.gblup_arrays(X, Y, lambda_=0.8, devices=devices), i8_fit(),
                       gbm.grm(X, devices=devices), gbm.grm_ploidy_aware(X, ploidy=2, devices=devices))
     (fit, i8, grm, gpa), (fit0, i80, grm0, gpa0) = runs["1"], runs["0"]
@@ -270,7 +271,7 @@ def _oom_counts():
     return r.value, f.value
 
 
-def test_oom_retry_frees_idle_gblup_and_brr_contexts(monkeypatch):
+def test_oom_retry_frees_idle_gblup_and_brr_contexts(gbm_env):
     """An allocation that runs out of device memory frees the idle pooled contexts of its device —
     the BRR pool's as well as the GBLUP pool's — and is retried once; the fit then
     succeeds with the same results. GBM_TEST_OOM_ONCE=1 makes every allocation's first attempt fail."""
@@ -281,11 +282,11 @@ def test_oom_retry_frees_idle_gblup_and_brr_contexts(monkeypatch):
     ref = gbm.gblup_arrays(X, Y, devices=[0])
     gbm.brr_arrays(X, Y[:, 0], n_iter=4, n_burnin=1, thin=1, seed=3)  # leaves an idle BRR context
     r0, f0 = _oom_counts()
-    monkeypatch.setenv("GBM_TEST_OOM_ONCE", "1")
+    gbm_env.setenv("GBM_TEST_OOM_ONCE", "1")
     X2 = oracle.synth_genotypes(406, 420, 1300)  # a larger shape: the leased context must grow
     Y2 = oracle.synth_phenotypes(X2, 407)
     got = gbm.gblup_arrays(X2, Y2, devices=[0])
-    monkeypatch.delenv("GBM_TEST_OOM_ONCE")
+    gbm_env.delenv("GBM_TEST_OOM_ONCE")
     r1, f1 = _oom_counts()
     assert r1 > r0 and f1 >= f0 + 1  # the idle BRR context was freed by a retry
     want = gbm.gblup_arrays(X2, Y2, devices=[0])
@@ -296,7 +297,7 @@ def test_oom_retry_frees_idle_gblup_and_brr_contexts(monkeypatch):
         assert np.array_equal(np.asarray(a), np.asarray(b))
 
 
-def test_reml_fit_multi_leader_rehearsal(monkeypatch):
+def test_reml_fit_multi_leader_rehearsal(gbm_env):
     """gbm_gblup_fit_reml over several device leaders at a size that takes the distributed
     factorisation (devices=[0, 0], every shard its own leader, GBM_DIST_SOLVE_MIN_N=0):
     λ is chosen on the first leader, the other leaders' G restored from its pristine copy, and the
@@ -304,8 +305,8 @@ def test_reml_fit_multi_leader_rehearsal(monkeypatch):
     X = oracle.synth_genotypes(515, 700, 3000)
     Y = oracle.synth_phenotypes(X, 516, ntraits=2)
     ref = gbm.gblup_reml_arrays(X, Y, devices=[0])
-    monkeypatch.setenv("GBM_SHARD_LEADERS", "each")
-    monkeypatch.setenv("GBM_DIST_SOLVE_MIN_N", "0")
+    gbm_env.setenv("GBM_SHARD_LEADERS", "each")
+    gbm_env.setenv("GBM_DIST_SOLVE_MIN_N", "0")
     got = gbm.gblup_reml_arrays(X, Y, devices=[0, 0])
     assert got[3] == ref[3]
     # the two G differ by the rounding of the shard sum: the λ searches agree to their tolerance

@@ -160,19 +160,19 @@ def _ws_bytes(n, p):
 
 @pytest.mark.parametrize("n,p", [(1030, 1234), (4999, 600), (1100, 2049), (700, 5000)])
 @pytest.mark.parametrize("persist", ["1", "0"])
-def test_grm_carry_mode_matches_oracle(monkeypatch, n, p, persist):
+def test_grm_carry_mode_matches_oracle(gbm_env, n, p, persist):
     """In-order carry accumulation (unit (s, t) waits for (s−1, t)'s flag, adds its partial to
     the running tile in G): used automatically when the slabs would exceed 4 GiB (n ≳ 13 000);
     forced here with four loci ranges on ragged shapes. Also the slab mode with hardware
     dispatch (GBM_GRM_PERSIST=0)."""
     X = oracle.synth_genotypes(n * 7 + p, n, p)
     Gr, qr = oracle.grm(X)
-    monkeypatch.setenv("GBM_GRM_SPLIT", "4,2,1,1")
-    monkeypatch.setenv("GBM_GRM_PERSIST", persist)
-    monkeypatch.setenv("GBM_GRM_CARRY", "0")
+    gbm_env.setenv("GBM_GRM_SPLIT", "4,2,1,1")
+    gbm_env.setenv("GBM_GRM_PERSIST", persist)
+    gbm_env.setenv("GBM_GRM_CARRY", "0")
     slab_ws = _ws_bytes(n, p)
     G0, q0 = gbm.grm(X)
-    monkeypatch.setenv("GBM_GRM_CARRY", "1")
+    gbm_env.setenv("GBM_GRM_CARRY", "1")
     carry_ws = _ws_bytes(n, p)
     assert carry_ws < slab_ws  # carry mode: tile flags instead of the loci-range slabs
     assert gbm.load_library().gbm_dev_grm_slices(n, p) == 4
@@ -184,9 +184,9 @@ def test_grm_carry_mode_matches_oracle(monkeypatch, n, p, persist):
     assert np.array_equal(G0, G1)
 
 
-def test_gblup_carry_mode_matches_oracle(monkeypatch):
-    monkeypatch.setenv("GBM_GRM_CARRY", "1")
-    monkeypatch.setenv("GBM_GRM_SPLIT", "5,3,1")
+def test_gblup_carry_mode_matches_oracle(gbm_env):
+    gbm_env.setenv("GBM_GRM_CARRY", "1")
+    gbm_env.setenv("GBM_GRM_SPLIT", "5,3,1")
     n, p = 1030, 3000
     X = oracle.synth_genotypes(5, n, p)
     Y = oracle.synth_phenotypes(X, 6, ntraits=2)
@@ -195,14 +195,14 @@ def test_gblup_carry_mode_matches_oracle(monkeypatch):
     assert q == ref["q"] and rel(y_pred, ref["y_pred"]) < TOL_TIGHT and rel(b_hat, ref["b_hat"]) < TOL_CONTRACT
 
 
-def test_grm_carry_timeout_is_reported(monkeypatch):
+def test_grm_carry_timeout_is_reported(gbm_env):
     """A timed-out inter-workgroup wait sets the carry error cell (int32 after the ntiles tile
     flags) to −1; gbm_dev_grm_reduce reads it back and fails instead of returning a wrong G.
     The cell is poisoned between the two stages to exercise that check."""
     import torch
-    monkeypatch.setenv("GBM_GRM_CARRY", "1")
-    monkeypatch.setenv("GBM_GRM_SPLIT", "1,1")
-    monkeypatch.setenv("GBM_GRM_EDGE", "0")
+    gbm_env.setenv("GBM_GRM_CARRY", "1")
+    gbm_env.setenv("GBM_GRM_SPLIT", "1,1")
+    gbm_env.setenv("GBM_GRM_EDGE", "0")
     lib = gbm.load_library()
     n, p = 640, 512
     npad, gdim = lib.gbm_dev_npad(n), lib.gbm_dev_gdim(n)

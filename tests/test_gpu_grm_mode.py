@@ -111,24 +111,44 @@ def test_int8_and_synthetic_sources():
         gbm.gblup_dosage(Db, 2, Y, grm="exact")
 
 
-def test_environment_only_supplies_the_default(dosage_case, monkeypatch):
+def test_environment_only_supplies_the_default(dosage_case, gbm_env):
     X, Y, ref = dosage_case
-    monkeypatch.setenv("GBM_GRM", "exact")
+    gbm_env.setenv("GBM_GRM", "exact")
     info = {}
     check(gbm.gblup_arrays(X, Y, grm="fp64", info=info), ref)
     assert info["grm_used"] == "fp64"  # the argument wins
     info = {}
     check(gbm.gblup_arrays(X, Y, grm=None, info=info), ref)
     assert info["grm_used"] == "exact"  # GBM_GRM_DEFAULT: the environment
-    monkeypatch.delenv("GBM_GRM")
+    gbm_env.delenv("GBM_GRM")
     info = {}
     gbm.gblup_arrays(X, Y, grm=None, info=info)
     assert info["grm_used"] == "fp64"
 
 
+def test_dropin_default_follows_a_set_grm_variable(dosage_case, gbm_env):
+    """The drop-in's default (grm="dropin", Julia grm = :dropin): GBM_GRM=fp64 set by a user or CI
+    pins the fp64 SYRK for gblup as for every other entry; unset, the drop-in is auto (exact on dosages)."""
+    X, Y, ref = dosage_case
+    n, p = X.shape
+    genomes = Genomes(entries=[f"e{i}" for i in range(n)], populations=["pop"] * n,
+                      loci_alleles=[f"chr1\t{j}\tA|T\tA" for j in range(p)], allele_frequencies=X)
+    phenomes = Phenomes(entries=genomes.entries, populations=genomes.populations, traits=["t1"],
+                        phenotypes=Y[:, :1].copy())
+    gbm_env.setenv("GBM_GRM", "fp64")
+    assert gbm.gblup(genomes=genomes, phenomes=phenomes).grm_used == "fp64"
+    assert gbm.gblup(genomes=genomes, phenomes=phenomes, grm="auto").grm_used == "exact"  # an argument wins
+    gbm_env.setenv("GBM_GRM", "exact")
+    assert gbm.gblup(genomes=genomes, phenomes=phenomes).grm_used == "exact"
+    gbm_env.delenv("GBM_GRM")
+    fit = gbm.gblup(genomes=genomes, phenomes=phenomes)
+    assert fit.grm_used == "exact"
+    assert rel(fit.y_pred, ref["y_pred"][:, 0]) < 1e-9
+
+
 def test_model_function_default_auto_and_sessions(dosage_case):
-    """The drop-in gblup (grm="auto" by default, Julia grm = :auto) records the GRM it used; a session of fp64
-    X checks once whether its genotypes are dosages/2 and builds exact training GRMs under auto."""
+    """The drop-in gblup (grm="dropin" by default: auto with GBM_GRM unset) records the GRM it used; a session of
+    fp64 X checks once whether its genotypes are dosages/2 and builds exact training GRMs under auto."""
     X, Y, _ = dosage_case
     n, p = X.shape
     genomes = Genomes(entries=[f"e{i}" for i in range(n)], populations=["pop"] * n,

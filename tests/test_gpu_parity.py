@@ -226,19 +226,19 @@ def test_repeated_solves_are_bit_identical():
 
 @pytest.mark.parametrize("g4,g8,g16,group,tail", [(0, -1, -1, 1, 0), (-1, 0, -1, 1, 0), (-1, -1, 0, 1, 0),
                                                  (0, 0, 0, 1, 0), (0, 0, 0, 0, 0), (0, 0, 0, 1, 704)])
-def test_cholesky_panel_groups_forced(monkeypatch, g4, g8, g16, group, tail):
+def test_cholesky_panel_groups_forced(gbm_env, g4, g8, g16, group, tail):
     """The 4/8/16-panel groups (K = 256/512/1024 trailing updates; the panel phase as one
     chol_group_kernel launch, or with group = 0 as panel / row-update launches of K = 64 j) run
     only on large trailing matrices by default; force them on a small one (the thresholds are
     read at every solve) and compare with the oracle. tail > 0: the last rows (≤ tail) in one dataflow
     launch on the trailing sub-matrix (GBM_CHOL_TAIL_FLOW)."""
-    monkeypatch.setenv("GBM_CHOL_GROUP_KERNEL", str(group))
-    monkeypatch.setenv("GBM_CHOL_TAIL_FLOW", str(tail))
-    monkeypatch.setenv("GBM_CHOL_G4_LIM", str(g4))
-    monkeypatch.setenv("GBM_CHOL_G8_LIM", str(g8))
-    monkeypatch.setenv("GBM_CHOL_G16_LIM", str(g16))
-    monkeypatch.setenv("GBM_UPD64_LIM", "128")
-    monkeypatch.setenv("GBM_CHOL_FLOW_MAX", "0")  # the launch-per-panel path (not the dataflow one)
+    gbm_env.setenv("GBM_CHOL_GROUP_KERNEL", str(group))
+    gbm_env.setenv("GBM_CHOL_TAIL_FLOW", str(tail))
+    gbm_env.setenv("GBM_CHOL_G4_LIM", str(g4))
+    gbm_env.setenv("GBM_CHOL_G8_LIM", str(g8))
+    gbm_env.setenv("GBM_CHOL_G16_LIM", str(g16))
+    gbm_env.setenv("GBM_UPD64_LIM", "128")
+    gbm_env.setenv("GBM_CHOL_FLOW_MAX", "0")  # the launch-per-panel path (not the dataflow one)
     n, p = 1500, 900
     X = oracle.synth_genotypes(77, n, p)
     Y = oracle.synth_phenotypes(X, 78, ntraits=2)

@@ -33,7 +33,7 @@ def _rccl_calls():
 
 
 @pytest.mark.parametrize("devices", [[0], [0, 0]])
-def test_c_abi_forced_rccl_one_rank_bit_identical(monkeypatch, devices):
+def test_c_abi_forced_rccl_one_rank_bit_identical(gbm_env, devices):
     """gbm_gblup_fit with GBM_FORCE_RCCL=1: the packed partial GRM goes through ncclAllReduce and every
     distributable panel group's final rows through ncclAllGather (GBM_DIST_SOLVE_MIN_N / GBM_DIST_TAIL_ROWS = 0
     so that a 3 000-row fit has them) — bit-identical to the same fit without collectives (both on the
@@ -41,12 +41,12 @@ def test_c_abi_forced_rccl_one_rank_bit_identical(monkeypatch, devices):
     n, p = 3000, 4000
     X = oracle.synth_genotypes(515, n, p)
     Y = oracle.synth_phenotypes(X, 16, ntraits=2)
-    monkeypatch.setenv("GBM_CHOL_FLOW_MAX", "0")
-    monkeypatch.setenv("GBM_DIST_SOLVE_MIN_N", "0")
-    monkeypatch.setenv("GBM_DIST_TAIL_ROWS", "0")
+    gbm_env.setenv("GBM_CHOL_FLOW_MAX", "0")
+    gbm_env.setenv("GBM_DIST_SOLVE_MIN_N", "0")
+    gbm_env.setenv("GBM_DIST_TAIL_ROWS", "0")
     ref_gpu = gbm.gblup_arrays(X, Y, lambda_=1.0, devices=devices, grm="fp64")
     a0, g0 = _rccl_calls()
-    monkeypatch.setenv("GBM_FORCE_RCCL", "1")
+    gbm_env.setenv("GBM_FORCE_RCCL", "1")
     forced = gbm.gblup_arrays(X, Y, lambda_=1.0, devices=devices, grm="fp64")
     a1, g1 = _rccl_calls()
     assert a1 - a0 == 1, (a0, a1)  # one partial-GRM all-reduce
@@ -76,15 +76,16 @@ def _world1_worker(rank, port, n, p, seed, out_dir):
     torch.cuda.set_device(0)
     dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1,
                             device_id=torch.device("cuda", 0))
-    os.environ["GBM_CHOL_FLOW_MAX"] = "0"
+    from gbm import _lib
+    _lib.debug_set("GBM_CHOL_FLOW_MAX", "0")
     st = HipShardStages(n, p, nrhs=1, lambda_=1.0, device=0)
     st.generate(seed, 0)
     Y = synth.qtl_phenotypes(seed, n, p, 1, device=0)
     st.load_phenotypes(Y)
     base = sharded_gblup_step(st, LocalComm())
     base = {k: np.array(v) for k, v in base.items()}
-    os.environ["GBM_DIST_SOLVE_MIN_N"] = "0"
-    os.environ["GBM_DIST_TAIL_ROWS"] = "0"
+    _lib.debug_set("GBM_DIST_SOLVE_MIN_N", "0")
+    _lib.debug_set("GBM_DIST_TAIL_ROWS", "0")
     comm = TorchComm(force=True)
     calls = {"all_reduce": 0, "all_gather": 0}
     ar, ag = comm.all_reduce_sum, comm.all_gather

@@ -49,7 +49,8 @@ def _worker(rank, world, port, n, p_total, seed, Y, out_dir, env=None):
     # every tile with the same kernel and operands: the same bits)
     st.G.copy_(saved["G"])
     st.q.copy_(saved["q"])
-    os.environ["GBM_CHOL_FLOW_MAX"] = "0"
+    from gbm import _lib
+    _lib.debug_set("GBM_CHOL_FLOW_MAX", "0")  # (libgbm read the environment at its first call)
     st.solve()
     torch.cuda.synchronize()
     y_red = st.gebv[:, :n].T.cpu().numpy()

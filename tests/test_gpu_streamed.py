@@ -35,92 +35,92 @@ def data():
     return X, Y
 
 
-def _fit_synth(monkeypatch, stream, Y, devices=(0,), host_chunk=None):
-    monkeypatch.setenv("GBM_STREAM_CHUNK", str(stream))
+def _fit_synth(gbm_env, stream, Y, devices=(0,), host_chunk=None):
+    gbm_env.setenv("GBM_STREAM_CHUNK", str(stream))
     if host_chunk:
-        monkeypatch.setenv("GBM_HOST_CHUNK", str(host_chunk))
+        gbm_env.setenv("GBM_HOST_CHUNK", str(host_chunk))
     else:
-        monkeypatch.delenv("GBM_HOST_CHUNK", raising=False)
+        gbm_env.delenv("GBM_HOST_CHUNK", raising=False)
     return gbm.gblup_synthetic(SEED, N, P, Y, lambda_=1.0, devices=list(devices))
 
 
-def test_streamed_synthetic_matches_oracle_and_resident(monkeypatch, data):
+def test_streamed_synthetic_matches_oracle_and_resident(gbm_env, data):
     X, Y = data
-    b, y, mu, q = _fit_synth(monkeypatch, CHUNK, Y)
+    b, y, mu, q = _fit_synth(gbm_env, CHUNK, Y)
     ref = oracle.gblup_fit(X, Y, 1.0)
     assert q == ref["q"]
     assert rel(y, ref["y_pred"]) < 1e-9 and rel(mu, ref["mu"]) < 1e-9 and rel(b, ref["b_hat"]) < 1e-6
-    b0, y0, mu0, q0 = _fit_synth(monkeypatch, 0, Y)
+    b0, y0, mu0, q0 = _fit_synth(gbm_env, 0, Y)
     assert q0 == q and rel(y, y0) < 1e-12 and rel(b, b0) < 1e-10
     # the predict identity of reference src/prediction.jl:228 on the streamed fit
     assert rel(b[0] + X @ b[1:], y) < 1e-9
 
 
 @pytest.mark.parametrize("host_chunk", [CHUNK, 1024])
-def test_streamed_int8_same_bits_as_pipelined_upload(monkeypatch, data, host_chunk):
+def test_streamed_int8_same_bits_as_pipelined_upload(gbm_env, data, host_chunk):
     X, Y = data
     D = np.asfortranarray(np.rint(2.0 * X).astype(np.int8))
-    monkeypatch.setenv("GBM_HOST_CHUNK", str(host_chunk))
-    monkeypatch.setenv("GBM_STREAM_CHUNK", str(host_chunk))
+    gbm_env.setenv("GBM_HOST_CHUNK", str(host_chunk))
+    gbm_env.setenv("GBM_STREAM_CHUNK", str(host_chunk))
     s = gbm.gblup_dosage(D, 2, Y)
-    monkeypatch.setenv("GBM_STREAM_CHUNK", "0")
+    gbm_env.setenv("GBM_STREAM_CHUNK", "0")
     r = gbm.gblup_dosage(D, 2, Y)
     for a, b in zip(s, r):
         assert np.array_equal(np.asarray(a), np.asarray(b))
 
 
-def test_streamed_fp64_same_bits_as_pipelined_and_int8(monkeypatch, data):
+def test_streamed_fp64_same_bits_as_pipelined_and_int8(gbm_env, data):
     X, Y = data
     D = np.asfortranarray(np.rint(2.0 * X).astype(np.int8))
-    monkeypatch.setenv("GBM_HOST_CHUNK", str(CHUNK))
-    monkeypatch.setenv("GBM_STREAM_CHUNK", str(CHUNK))
+    gbm_env.setenv("GBM_HOST_CHUNK", str(CHUNK))
+    gbm_env.setenv("GBM_STREAM_CHUNK", str(CHUNK))
     s = gbm.gblup_arrays(X, Y)
     s8 = gbm.gblup_dosage(D, 2, Y)
-    monkeypatch.setenv("GBM_STREAM_CHUNK", "0")
+    gbm_env.setenv("GBM_STREAM_CHUNK", "0")
     r = gbm.gblup_arrays(X, Y)
     for a, b, c in zip(s, r, s8):
         assert np.array_equal(np.asarray(a), np.asarray(b))
         assert np.array_equal(np.asarray(a), np.asarray(c))
 
 
-def test_streamed_synthetic_same_bits_as_streamed_int8(monkeypatch, data):
+def test_streamed_synthetic_same_bits_as_streamed_int8(gbm_env, data):
     """On-device dosage generation == the same bytes uploaded from the host."""
     X, Y = data
     D = np.asfortranarray(np.rint(2.0 * X).astype(np.int8))
-    s = _fit_synth(monkeypatch, CHUNK, Y)
+    s = _fit_synth(gbm_env, CHUNK, Y)
     r = gbm.gblup_dosage(D, 2, Y)  # GBM_STREAM_CHUNK still set by _fit_synth
     for a, b in zip(s, r):
         assert np.array_equal(np.asarray(a), np.asarray(b))
 
 
-def test_streamed_single_range_tail_chunk(monkeypatch, data):
+def test_streamed_single_range_tail_chunk(gbm_env, data):
     """A last chunk too small for a multi-range GRM plan goes through its own G and an add (Gc)."""
     X, Y = data
     lib = gbm.load_library()
     chunk = P - 16  # tail of 16 loci
     assert lib.gbm_dev_grm_slices(N, 16) == 1 and lib.gbm_dev_grm_slices(N, chunk) > 1
-    b, y, mu, q = _fit_synth(monkeypatch, chunk, Y)
-    b0, y0, mu0, q0 = _fit_synth(monkeypatch, 0, Y)
+    b, y, mu, q = _fit_synth(gbm_env, chunk, Y)
+    b0, y0, mu0, q0 = _fit_synth(gbm_env, 0, Y)
     assert q == q0 and rel(y, y0) < 1e-12 and rel(b, b0) < 1e-10
 
 
-def test_streamed_two_shards_one_device(monkeypatch, data):
+def test_streamed_two_shards_one_device(gbm_env, data):
     X, Y = data
-    b, y, mu, q = _fit_synth(monkeypatch, 1000, Y, devices=(0, 0))
-    b0, y0, mu0, q0 = _fit_synth(monkeypatch, 0, Y, devices=(0, 0))
+    b, y, mu, q = _fit_synth(gbm_env, 1000, Y, devices=(0, 0))
+    b0, y0, mu0, q0 = _fit_synth(gbm_env, 0, Y, devices=(0, 0))
     assert q == q0 and rel(y, y0) < 1e-12 and rel(b, b0) < 1e-10
 
 
-def test_streamed_reml(monkeypatch, data):
+def test_streamed_reml(gbm_env, data):
     X, Y = data
-    monkeypatch.setenv("GBM_STREAM_CHUNK", str(CHUNK))
+    gbm_env.setenv("GBM_STREAM_CHUNK", str(CHUNK))
     s = gbm.gblup_reml_arrays(X, Y)
-    monkeypatch.setenv("GBM_STREAM_CHUNK", "0")
+    gbm_env.setenv("GBM_STREAM_CHUNK", "0")
     r = gbm.gblup_reml_arrays(X, Y)
     assert rel(s[1], r[1]) < 1e-9 and rel(s[4]["lambda"], r[4]["lambda"]) < 1e-8
 
 
-def test_streamed_stage_path_matches_c_abi(monkeypatch, data):
+def test_streamed_stage_path_matches_c_abi(gbm_env, data):
     import torch
     from gbm.sharded import HipStreamedShardStages, assemble_b_hat
 
@@ -138,7 +138,7 @@ def test_streamed_stage_path_matches_c_abi(monkeypatch, data):
     b_st = assemble_b_hat(out["mu"], out["msum"], [out["B"]], P)
     del st
     torch.cuda.empty_cache()
-    b, y, mu, q2 = _fit_synth(monkeypatch, CHUNK, Y)
+    b, y, mu, q2 = _fit_synth(gbm_env, CHUNK, Y)
     assert q == q2
     assert rel(out["y_pred"], y) < 1e-13 and rel(b_st, b) < 1e-12
 
