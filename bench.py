@@ -15,6 +15,13 @@ results (b, GEBVs, μ̂) copied to pinned host memory.
 --loci 600000 --stream-chunk 75000`): the genotypes resident as int8 dosages (1 B per cell), each
 chunk of C loci standardised and added into G in place, the marker effects from the bytes.
 
+The C3 leg (`--c3-leg`, on by default whenever N > 1): after the headline, every rank
+runs BASELINE.json configs[2] — n = 50 000, 600 000 loci SPLIT over the N ranks (75 000 per rank at N = 8, int8
+dosages resident, 75 000-locus fp64 chunks), the packed RCCL all-reduce of the partial GRMs, the distributed
+Cholesky (strip all-gathers) — 1 warm-up + 2 timed steps, reported under the line's "c3" key with the GRM and
+end-to-end fractions of N x the fp64 peak and every rank's GRM / all-reduce / solve / all-gather-wait times. The
+N = 1 headline is unchanged.
+
 Parity (rank 0, N = 1, when the oracle can run the same problem): the numpy restatement fits the
 SAME genotypes and phenotypes the GPU step fitted; the line carries rel_err of y_pred, μ̂, b_hat and
 q equality.
@@ -71,6 +78,16 @@ def parse():
     ap.add_argument("--stream-chunk", type=int, default=0,
                     help="loci per chunk of the loci-streamed mode (int8 dosages resident); 0 = resident fp64 X")
     ap.add_argument("--no-exact", action="store_true", help="skip the exact-integer GRM measurement beside the fp64 line")
+    ap.add_argument("--c3-leg", choices=("auto", "on", "off"), default="auto",
+                    help="the C3 leg (BASELINE.json configs[2], the north star): after the headline, n = --c3-individuals "
+                         "x --c3-loci loci SPLIT over the launched ranks (strong scaling), loci-streamed fp64 GRM, "
+                         "packed RCCL all-reduce, distributed Cholesky; auto = on when more than one rank runs")
+    ap.add_argument("--c3-individuals", type=int, default=50000)
+    ap.add_argument("--c3-loci", type=int, default=600000, help="loci in total (split over the ranks)")
+    ap.add_argument("--c3-chunk", type=int, default=75000, help="loci per fp64 chunk of a rank's streamed shard")
+    ap.add_argument("--c3-steps", type=int, default=2)
+    ap.add_argument("--c3-warmup", type=int, default=1)
+    ap.add_argument("--c3-seed", type=int, default=424242)
     ap.add_argument("--grm", choices=("fp64", "exact"), default="fp64",
                     help="fp64: the fp64-MFMA SYRK on standardised rows; exact: int8 dosages resident, the GRM "
                          "computed exactly by int8-MFMA digit GEMMs with int128 centring (csrc/grm_exact.hip)")
@@ -337,6 +354,13 @@ def host_path(args, torch):
         _lib.check(lib.gbm_gblup_fit(_lib.ptr(X), n, p, n, _lib.ptr(Y), n, t, args.lam, None, 0, _lib.ptr(b),
                                      _lib.ptr(yp), _lib.ptr(mu), _lib.ptr(q)), "gbm_gblup_fit")
 
+    def fit_auto(X):  # the drop-in's mode on dosage-valued X: the device dosage check + the exact GRM
+        used = ctypes.c_int(-1)
+        _lib.check(lib.gbm_gblup_fit_ex(_lib.ptr(X), n, p, n, _lib.ptr(Y), n, t, args.lam, None, 0, _lib.GBM_GRM_AUTO,
+                                        _lib.ptr(b), _lib.ptr(yp), _lib.ptr(mu), _lib.ptr(q), ctypes.byref(used)),
+                   "gbm_gblup_fit_ex(auto)")
+        assert used.value == _lib.GBM_GRM_EXACT
+
     def fit_i8():
         _lib.check(lib.gbm_gblup_fit_dosage_i8(_lib.ptr(D_page), n, p, n, 2, _lib.ptr(Y), n, t, args.lam, None, 0,
                                                _lib.ptr(b), _lib.ptr(yp), _lib.ptr(mu), _lib.ptr(q)),
@@ -355,6 +379,8 @@ def host_path(args, torch):
     ms_page = timed(lambda: fit_f64(X_page))
     ms_pin = timed(lambda: fit_f64(X_pin))
     ms_i8 = timed(fit_i8)
+    ms_auto = timed(lambda: fit_auto(X_page))
+    ms_auto_pin = timed(lambda: fit_auto(X_pin))
     dev_buf = torch.empty((p, n), dtype=torch.float64, device="cuda")
 
     def h2d(src):
@@ -371,6 +397,10 @@ def host_path(args, torch):
     return {
         "entry": "gbm_gblup_fit (C ABI, host X column-major n x p; Julia ccall path) on the same workload",
         "ms_per_call_pageable_x": ms_page, "ms_per_call_pinned_x": ms_pin, "ms_per_call_dosage_i8": ms_i8,
+        "ms_per_call_auto_f64_x": ms_auto, "ms_per_call_auto_f64_x_pinned": ms_auto_pin,
+        "auto_note": "gbm_gblup_fit_ex(GBM_GRM_AUTO) on the same pageable (and pinned) fp64 X: the drop-in gblup's "
+                     "default on diploid data (julia/gblup.jl grm = :dropin with GBM_GRM unset) — fp64 X over PCIe in "
+                     "chunks, 2x checked and packed to int8 on the device, then the exact-integer GRM",
         "h2d_x_ms_pinned": h2d_pin, "h2d_x_ms_pageable": h2d_page, "x_bytes": 8 * n * p,
         "cells_per_s_pinned_x": n * p / (ms_pin / 1000.0), "device_allocations_per_call_after_warmup": 0,
     }
@@ -392,6 +422,161 @@ def load_pmc(n, p):
     with open(os.path.join(ROOT, "genomicbreedingmodels.jl_amd", "csrc", "grm.hip"), "rb") as f:
         sha = hashlib.sha256(f.read()).hexdigest()
     return d.get("hbm_bytes_per_launch"), d.get("grm_hip_sha256") != sha
+
+
+class TimedComm:
+    """A comm (TorchComm) whose collectives are bracketed by timing events on the stream that issues them (the
+    compute stream, or the distributed solve's side stream): per collective kind, the time that stream spent from
+    issuing the collective to its completion (waiting for the slowest rank included)."""
+
+    def __init__(self, comm, torch):
+        self.comm, self.torch = comm, torch
+        self.world_size, self.rank = comm.world_size, comm.rank
+        self.force = getattr(comm, "force", False)
+        self.spans = []  # (kind, bytes, event before, event after)
+
+    def _timed(self, kind, fn, t):
+        e0 = self.torch.cuda.Event(enable_timing=True)
+        e1 = self.torch.cuda.Event(enable_timing=True)
+        e0.record()
+        out = fn(t)
+        e1.record()
+        self.spans.append((kind, int(t.numel() * t.element_size()), e0, e1))
+        return out
+
+    def all_reduce_sum(self, t):
+        return self._timed("all_reduce", self.comm.all_reduce_sum, t)
+
+    def all_gather(self, t):
+        return self._timed("all_gather", self.comm.all_gather, t)
+
+    def take(self):
+        """{kind: [ms, calls, bytes]} of the spans recorded since the last take (events complete: call after a
+        synchronize)."""
+        out = {}
+        for kind, nb, e0, e1 in self.spans:
+            acc = out.setdefault(kind, [0.0, 0, 0])
+            acc[0] += e0.elapsed_time(e1)
+            acc[1] += 1
+            acc[2] += nb
+        self.spans = []
+        return out
+
+
+def c3_split(p_total, world, rank):
+    """(j0, p_local) of rank's contiguous block of loci: ceil(p/world) per rank."""
+    per = (p_total + world - 1) // world
+    j0 = min(rank * per, p_total)
+    return j0, max(0, min(per, p_total - j0))
+
+
+def c3_record(n, p_total, world, steps, warmup, ms_per_step, per_rank, chunk, backend):
+    """rank 0's `c3` object from the leg's timings: per_rank = one dict per rank with its mean per-step stage
+    times (grm = standardise + GRM of its loci, allreduce, solve, effects) and collective spans. The fractions
+    count the algorithmic flops of SURVEY.md §8d (GRM n(n+1)p, Cholesky n³/3, solves 8n², back-solve 2np) against
+    N x the fp64 MFMA peak."""
+    grm_flops = float(n) * (n + 1) * p_total
+    chol_flops = float(n) ** 3 / 3.0
+    other = 8.0 * float(n) ** 2 + 2.0 * n * p_total
+    grm_ms = max((r.get("grm_ms") or 0.0) for r in per_rank) if per_rank else 0.0
+    peak = world * PEAK_F64_TFLOPS * 1e12
+    ok = ms_per_step is not None and ms_per_step > 0
+    return {
+        "workload": f"C3 GBLUP {n} x {p_total} (BASELINE.json configs[2] at n=50000, p=600000): the loci split over "
+                    f"{world} rank(s) ({-(-p_total // world)} per rank, int8 dosages resident, {chunk}-locus fp64 "
+                    f"chunks), packed partial-GRM all-reduce ({backend}), distributed Cholesky; strong scaling",
+        "n": n, "p_total": p_total, "ranks": world, "steps": steps, "warmup": warmup,
+        "ms_per_step": ms_per_step,
+        "value": n * p_total / (ms_per_step / 1000.0) if ok else None, "unit": "genotype-cells/s",
+        "grm_frac_of_peak": grm_flops / (grm_ms / 1000.0) / peak if grm_ms > 0 else None,
+        "grm_ms_max_over_ranks": grm_ms,
+        "e2e_fp64_frac_of_peak": (grm_flops + chol_flops + other) / (ms_per_step / 1000.0) / peak if ok else None,
+        "peak_tflops_per_gpu": PEAK_F64_TFLOPS, "backend": backend,
+        "per_rank": per_rank,
+    }
+
+
+def run_c3_leg(args, torch, dist, base_comm, world, rank, dev):
+    """The C3 leg: n x p_total over the launched ranks, each rank a contiguous block of loci
+    (int8 dosages generated in HBM, standardised per fp64 chunk into the partial GRM), the packed all-reduce of the
+    upper tiles + q, the distributed Cholesky from n >= GBM_DIST_SOLVE_MIN_N (each rank its own tile columns,
+    strip all-gathers), marker effects; W untimed + K timed steps between barrier + synchronize pairs, max over
+    ranks. Every rank returns its record; rank 0's carries every rank's stage times."""
+    import gbm
+    from gbm import synth
+    from gbm.sharded import HipStreamedShardStages, sharded_gblup_step
+
+    n, p_total = args.c3_individuals, args.c3_loci
+    j0, p_local = c3_split(p_total, world, rank)
+    chunk = min(args.c3_chunk, p_local)
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    gbm.load_library().gbm_release_device_cache()
+    st = HipStreamedShardStages(n, p_local, chunk, nrhs=1, lambda_=args.lam, device=dev)
+    st.generate(args.c3_seed, j0)
+    Y = synth.qtl_phenotypes(args.c3_seed, n, p_total, 1, device=dev)
+    st.load_phenotypes(Y)
+    comm = TimedComm(base_comm, torch)
+    labels = ["begin", "standardize", "grm_syrk", "grm_reduce", "allreduce", "solve", "effects", "download"]
+    for _ in range(args.c3_warmup):
+        sharded_gblup_step(st, comm)
+    torch.cuda.synchronize()
+    comm.take()
+    if dist.is_initialized():
+        dist.barrier()
+    torch.cuda.synchronize()
+    recs, out = [], None
+    t0 = time.perf_counter()
+    for _ in range(args.c3_steps):
+        evs = {}
+
+        def mark(label, evs=evs):
+            e = torch.cuda.Event(enable_timing=True)
+            e.record()
+            evs[label] = e
+        out = sharded_gblup_step(st, comm, events=mark)
+        recs.append(evs)
+    torch.cuda.synchronize()
+    if dist.is_initialized():
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if dist.is_initialized():
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    K = max(args.c3_steps, 1)
+    stage = {}
+    for a, b in zip(labels[:-1], labels[1:]):
+        stage[b] = float(np.mean([r[a].elapsed_time(r[b]) for r in recs]))
+    coll = comm.take()
+    y = np.asarray(out["y_pred"])
+    mine = {"rank": rank, "loci": p_local, "j0": j0,
+            "grm_ms": stage["standardize"] + stage["grm_syrk"] + stage["grm_reduce"],
+            "allreduce_ms": stage["allreduce"], "solve_ms": stage["solve"], "effects_ms": stage["effects"],
+            "download_ms": stage["download"],
+            "allgather_blocked_ms": coll.get("all_gather", [0.0])[0] / K,
+            "allgather_calls": coll.get("all_gather", [0, 0])[1] // K,
+            "allgather_bytes_received": coll.get("all_gather", [0, 0, 0])[2] * world // K,
+            "allreduce_span_ms": coll.get("all_reduce", [0.0])[0] / K,
+            "allreduce_bytes": coll.get("all_reduce", [0, 0, 0])[2] // K,
+            "q": int(st.q.item()), "y_pred_finite": bool(np.all(np.isfinite(y))),
+            "y_pred_sum": float(y.sum()), "mu": float(out["mu"][0])}
+    per_rank = [mine]
+    if dist.is_initialized():
+        per_rank = [None] * world
+        dist.all_gather_object(per_rank, mine)
+    del st
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    backend = dist.get_backend() if dist.is_initialized() else "none"
+    rec = c3_record(n, p_total, world, args.c3_steps, args.c3_warmup, elapsed * 1000.0 / K, per_rank, chunk,
+                    "RCCL" if backend == "nccl" else backend)
+    # every rank solved the same summed system: identical GEBVs (the distributed factorisation is bit-identical to
+    # the redundant one); q = p_total (MAF >= 0.05: every locus polymorphic at this n)
+    rec["ranks_agree"] = len({(r["y_pred_sum"], r["mu"]) for r in per_rank}) == 1
+    rec["q"] = per_rank[0]["q"]
+    return rec
 
 
 def _free_port():
@@ -470,8 +655,16 @@ def launch_check(args, torch, dist, world, rank):
         dist.all_gather_object(ranks, {"rank": rank, "pid": os.getpid()})
     else:
         ranks = [{"rank": 0, "pid": os.getpid()}]
+    c3 = None
+    if args.c3_leg == "on" or (args.c3_leg == "auto" and world > 1):  # the record's shape around empty timings
+        pr = [{"rank": r, "loci": c3_split(args.c3_loci, world, r)[1], "j0": c3_split(args.c3_loci, world, r)[0],
+               "grm_ms": 0.0, "allreduce_ms": 0.0, "solve_ms": 0.0, "effects_ms": 0.0, "download_ms": 0.0,
+               "allgather_blocked_ms": 0.0, "allgather_calls": 0, "allgather_bytes_received": 0,
+               "allreduce_span_ms": 0.0, "allreduce_bytes": 0} for r in range(world)]
+        c3 = c3_record(args.c3_individuals, args.c3_loci, world, args.c3_steps, args.c3_warmup, None, pr,
+                       min(args.c3_chunk, pr[0]["loci"]), dist.get_backend() if dist.is_initialized() else "none")
     if rank == 0:
-        print(json.dumps({"metric": "GRM+GBLUP genotype-cells/s (n x p)", "value": None, "unit": "genotype-cells/s",
+        print(json.dumps({"metric": "GRM+GBLUP genotype-cells/s (n x p)", "value": None, "unit": "genotype-cells/s", "c3": c3,
                           "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
                           "ms_per_step": float(el.item()) * 1000.0 / max(args.steps, 1), "higher_is_better": True,
                           "scaling": "weak", "launch_check": True,
@@ -597,6 +790,15 @@ def main():
     # sanity: finite GEBVs, b0 assembled
     assert np.all(np.isfinite(out["y_pred"])) and np.all(np.isfinite(out["B"]))
 
+    # the C3 leg (north star, BASELINE.json configs[2]): on by default whenever more than one rank runs
+    head_q = int(st.q.item())
+    grm_slices = int(st.lib.gbm_dev_grm_slices(n, args.stream_chunk or p_local)) if not exact else None
+    digit_slices = int(st.slices.value) if exact else None
+    c3 = None
+    if args.c3_leg == "on" or (args.c3_leg == "auto" and world > 1):
+        del st  # the headline shard's HBM back before the C3 shard is allocated
+        c3 = run_c3_leg(args, torch, dist, comm, world, rank, dev)
+
     if rank != 0:
         dist.destroy_process_group()
         return
@@ -627,8 +829,8 @@ def main():
         "config": {
             "workload": workload_label(n, p_local, world, args.stream_chunk, exact),
             "n": n, "p_per_gpu": p_local, "p_total": p_total, "traits": args.nrhs, "lambda": args.lam,
-            "grm_slices": int(st.lib.gbm_dev_grm_slices(n, args.stream_chunk or p_local)) if not exact else None,
-            "grm_digit_slices": int(st.slices.value) if exact else None,
+            "grm_slices": grm_slices,
+            "grm_digit_slices": digit_slices,
             "stream_chunk": args.stream_chunk or None,
             "parallelism": f"loci-shard x{world}",
         },
@@ -662,7 +864,7 @@ def main():
         "per_rank_stage_ms": per_rank if world > 1 or dist.is_initialized() else None,
     }
     if exact:
-        S = int(st.slices.value)
+        S = digit_slices
         ops = S * grm_flops  # S digit GEMMs of n(n+1)/2 x p int8 multiply-adds (2 ops each)
         tops = ops / (syrk_ms / 1000.0) / 1e12
         rec["roofline"] = {
@@ -675,12 +877,14 @@ def main():
             "traffic": None, "ops_per_launch": ops, "ms_per_launch": syrk_ms,
         }
         rec["e2e_fp64_frac_of_peak"] = None
+    if c3 is not None:
+        rec["c3"] = c3
     if world == 1 and not args.no_host_path and not args.stream_chunk and float(n) * p_local <= 2e9:
         rec["host_path"] = host_path(args, torch)
         rec["stage_ms"]["h2d_x_pinned"] = rec["host_path"]["h2d_x_ms_pinned"]
     oracle_fits = float(n) * p_local <= 5e8 and args.cpu_sample_p in (0, p_local)  # ~seconds on the host
     if world == 1 and not args.no_cpu_baseline and oracle_fits:
-        gpu = {"y_pred": out["y_pred"], "mu": out["mu"], "q": int(st.q.item()),
+        gpu = {"y_pred": out["y_pred"], "mu": out["mu"], "q": head_q,
                "b_hat": assemble_b_hat(out["mu"], out["msum"], [out["B"]], p_local)}
         res = run_isolated(_cpu_baseline_packed, (args, np.asarray(Y), gpu))
         if isinstance(res, dict):  # the child failed: no baseline, no parity from this run

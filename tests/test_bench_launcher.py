@@ -54,3 +54,43 @@ def test_gpus_must_match_launched_world_size():
     env = {"WORLD_SIZE": "1", "RANK": "0", "LOCAL_RANK": "0"}
     out = _run(["--gpus", "2", "--launch-check"], env=env)
     assert out.returncode != 0 and "WORLD_SIZE=1" in out.stderr
+
+
+def test_c3_leg_record_at_two_ranks():
+    """--gpus 2 turns the C3 leg on (auto): the line carries the "c3" record with the loci split over the two
+    ranks, the fractions' fields and one stage-time entry per rank (timings empty under --launch-check)."""
+    out = _run(["--gpus", "2", "--same-device", "--launch-check", "--steps", "1", "--warmup", "0"])
+    assert out.returncode == 0, out.stderr[-2000:]
+    rec = json.loads([ln for ln in out.stdout.splitlines() if ln.startswith("{")][0])
+    c3 = rec["c3"]
+    assert c3["n"] == 50000 and c3["p_total"] == 600000 and c3["ranks"] == 2
+    assert [r["loci"] for r in c3["per_rank"]] == [300000, 300000]
+    assert [r["j0"] for r in c3["per_rank"]] == [0, 300000]
+    for key in ("ms_per_step", "value", "grm_frac_of_peak", "e2e_fp64_frac_of_peak", "steps", "warmup", "workload"):
+        assert key in c3
+    for key in ("grm_ms", "allreduce_ms", "solve_ms", "allgather_blocked_ms", "allgather_calls"):
+        assert all(key in r for r in c3["per_rank"])
+    assert "strong scaling" in c3["workload"]
+
+
+def test_c3_leg_off_at_one_rank_by_default():
+    out = _run(["--launch-check", "--steps", "1", "--warmup", "0"])
+    assert out.returncode == 0, out.stderr[-2000:]
+    rec = json.loads([ln for ln in out.stdout.splitlines() if ln.startswith("{")][0])
+    assert rec["c3"] is None
+
+
+def test_c3_record_arithmetic():
+    """bench.c3_record: value = n p / time; GRM fraction from the slowest rank's GRM stage over N x peak; e2e from
+    all algorithmic flops."""
+    sys.path.insert(0, ROOT)
+    import bench
+    pr = [{"grm_ms": 2000.0}, {"grm_ms": 2500.0}]
+    r = bench.c3_record(50000, 600000, 8, 2, 1, 3000.0, pr, 75000, "RCCL")
+    assert abs(r["value"] - 50000 * 600000 / 3.0) < 1e-3
+    grm = 50000.0 * 50001 * 600000
+    assert abs(r["grm_frac_of_peak"] - grm / 2.5 / (8 * 78.6e12)) < 1e-12
+    tot = grm + 50000.0 ** 3 / 3 + 8 * 50000.0 ** 2 + 2 * 50000.0 * 600000
+    assert abs(r["e2e_fp64_frac_of_peak"] - tot / 3.0 / (8 * 78.6e12)) < 1e-12
+    assert bench.c3_split(600000, 8, 7) == (525000, 75000)
+    assert bench.c3_split(10, 3, 2) == (8, 2)

@@ -127,3 +127,32 @@ def test_ranks_one_gpu_exact_grm_match_oracle(tmp_path, world):
         assert np.abs(o["y_pred"] - ref["y_pred"]).max() < 1e-9 * np.abs(ref["y_pred"]).max()
     b_hat = assemble_b_hat(outs[0]["mu"], outs[0]["msum"], [o["B"] for o in outs], p)
     assert np.abs(b_hat - ref["b_hat"]).max() < 1e-6 * np.abs(ref["b_hat"]).max()
+
+
+def test_bench_c3_leg_two_ranks_same_device():
+    """bench.py's C3 leg at N = 2 on the one GPU of the test box (--same-device, gloo: RCCL
+    needs one device per rank), on a reduced C3 (n = 20 000, 60 000 loci split 2 x 30 000, 15 000-locus chunks):
+    the packed all-reduce and — n >= GBM_DIST_SOLVE_MIN_N = 16 384 — the distributed Cholesky run through the leg,
+    both ranks end with the same GEBVs, q = p, and the record carries every rank's stage and collective times."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cmd = [sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--same-device", "--dist-backend", "gloo",
+           "--individuals", "2000", "--loci", "5000", "--steps", "1", "--warmup", "0", "--no-cpu-baseline",
+           "--no-exact", "--no-host-path", "--c3-leg", "on", "--c3-individuals", "20000", "--c3-loci", "60000",
+           "--c3-chunk", "15000", "--c3-steps", "1", "--c3-warmup", "1"]
+    env = dict(os.environ)
+    env.pop("WORLD_SIZE", None)
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=400, env=env, cwd=root)
+    assert out.returncode == 0, out.stderr[-3000:]
+    rec = json.loads([ln for ln in out.stdout.splitlines() if ln.startswith("{")][0])
+    c3 = rec["c3"]
+    print("\nC3 leg (reduced, 2 ranks on one GPU, gloo):", json.dumps(c3))
+    assert c3["ranks"] == 2 and c3["n"] == 20000 and c3["p_total"] == 60000
+    assert c3["ranks_agree"] and c3["q"] == 60000
+    assert c3["value"] > 0 and 0 < c3["grm_frac_of_peak"] and 0 < c3["e2e_fp64_frac_of_peak"]
+    for r in c3["per_rank"]:
+        assert r["loci"] == 30000 and r["y_pred_finite"]
+        assert r["allgather_calls"] > 0 and r["allgather_blocked_ms"] > 0  # the distributed solve engaged
+        assert r["allreduce_bytes"] > 8 * 20000 * 20000 // 2  # the packed upper tiles (+ q) were all-reduced
