@@ -88,6 +88,7 @@ def parse():
     ap.add_argument("--c3-steps", type=int, default=2)
     ap.add_argument("--c3-warmup", type=int, default=1)
     ap.add_argument("--c3-seed", type=int, default=424242)
+    ap.add_argument("--c3-timeout", type=float, default=300.0, help="watchdog of the C3 leg (seconds)")
     ap.add_argument("--grm", choices=("fp64", "exact"), default="fp64",
                     help="fp64: the fp64-MFMA SYRK on standardised rows; exact: int8 dosages resident, the GRM "
                          "computed exactly by int8-MFMA digit GEMMs with int128 centring (csrc/grm_exact.hip)")
@@ -675,6 +676,105 @@ def launch_check(args, torch, dist, world, rank):
         dist.destroy_process_group()
 
 
+def headline_record(args, n, p_local, p_total, world, value, ms_per_step, syrk_ms, stage_ms, per_rank, exact,
+                    grm_slices, digit_slices, dist):
+    """rank 0's line (the headline step) before the C3 leg and the host/CPU legs add to it."""
+    # algorithmic work of SURVEY.md §8d: GRM n(n+1)p (unique triangle of the rank-p update),
+    # Cholesky n³/3, solves 8n² per right-hand side (four triangular solves), back-solve 2np
+    grm_flops = float(n) * (n + 1) * p_local
+    chol_flops = float(n) ** 3 / 3.0
+    solve_flops = 8.0 * float(n) ** 2 * args.nrhs + 2.0 * n * p_local * args.nrhs
+    achieved = grm_flops / (syrk_ms / 1000.0) / 1e12
+    traffic, traffic_stale = load_pmc(n, p_local) if not (args.stream_chunk or exact) else (None, None)
+    e2e_frac = (grm_flops + chol_flops + solve_flops) / (ms_per_step / 1000.0) / (PEAK_F64_TFLOPS * 1e12)
+
+    rec = {
+        "metric": "GRM+GBLUP genotype-cells/s (n x p)",
+        "value": value,
+        "unit": "genotype-cells/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": ms_per_step,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": ("i8 digit GEMMs (exact int32 sums) + int128 centring -> f64 G; f64 solve" if exact else "f64"),
+        "data": "synthetic: counter-hash genotypes (MAF U(0.05,0.5), dosage Binomial(2,f), X=d/2) generated in HBM"
+                + (" as int8 dosages" if (args.stream_chunk or exact) else " as fp64") + "; 1% QTL phenotype, h2=0.5",
+        "config": {
+            "workload": workload_label(n, p_local, world, args.stream_chunk, exact),
+            "n": n, "p_per_gpu": p_local, "p_total": p_total, "traits": args.nrhs, "lambda": args.lam,
+            "grm_slices": grm_slices,
+            "grm_digit_slices": digit_slices,
+            "stream_chunk": args.stream_chunk or None,
+            "parallelism": f"loci-shard x{world}",
+        },
+        "roofline": {
+            "bound": "mfma",
+            "kernel": "GRM stage: syrk_kernel<kPersist> (fp64 v_mfma_f64_16x16x4_f64 128x128 tiles) + "
+                      "grm_edge_kernel (ragged last column); achieved = all n(n+1)p flops / stage time"
+                      + ("; streamed: the stage also standardises each chunk from the int8 dosages"
+                         if args.stream_chunk else ""),
+            "achieved": achieved,
+            "peak": PEAK_F64_TFLOPS,
+            "unit": "TFLOP/s",
+            "frac": achieved / PEAK_F64_TFLOPS,
+            "frac_of_measured_mfma": achieved / MEASURED_MFMA_F64_TFLOPS,
+            "measured_mfma_peak": MEASURED_MFMA_F64_TFLOPS,
+            "traffic": traffic,
+            "traffic_source": "profiles/pmc_grm.json: rocprofv3 --pmc FETCH_SIZE (x2, gfx950 16 B/lane "
+                              "under-count) + WRITE_SIZE per GRM launch, separate passes of this command"
+                              if traffic is not None else None,
+            "traffic_stale": traffic_stale,
+            "flops_per_launch": grm_flops,
+            "ms_per_launch": syrk_ms,
+        },
+        "stage_ms": stage_ms,
+        "e2e_fp64_frac_of_peak": e2e_frac,
+        "world_size": world,
+        "backend": dist.get_backend() if dist.is_initialized() else None,
+        "collectives": ("RCCL" if dist.is_initialized() and dist.get_backend() == "nccl" else
+                        dist.get_backend() if dist.is_initialized() else "none (one rank)")
+                       + (" (forced at one rank: --collectives always)" if world == 1 and dist.is_initialized() else ""),
+        "per_rank_stage_ms": per_rank if world > 1 or dist.is_initialized() else None,
+    }
+    if exact:
+        S = digit_slices
+        ops = S * grm_flops  # S digit GEMMs of n(n+1)/2 x p int8 multiply-adds (2 ops each)
+        tops = ops / (syrk_ms / 1000.0) / 1e12
+        rec["roofline"] = {
+            "bound": "mfma",
+            "kernel": f"GRM stage: xg_gemm_kernel<{S}> (v_mfma_i32_16x16x64_i8, {S} base-128 digit GEMMs of the fixed-"
+                      "point locus weights, 128x64 upper tiles) + its per-locus prep kernels (stats, digits, transpose, "
+                      "int128 centring terms); achieved = S n(n+1)p int8 ops / stage time",
+            "achieved": tops, "peak": PEAK_I8_TOPS, "unit": "TOPS (int8)", "frac": tops / PEAK_I8_TOPS,
+            "frac_of_measured_i8_loop": tops / MEASURED_I8_LOOP_TOPS, "measured_i8_loop": MEASURED_I8_LOOP_TOPS,
+            "traffic": None, "ops_per_launch": ops, "ms_per_launch": syrk_ms,
+        }
+        rec["e2e_fp64_frac_of_peak"] = None
+    return rec
+
+
+def c3_watchdog(args, rank, rec):
+    """A daemon timer: after --c3-timeout seconds rank 0 prints its line with "c3" = an error (the headline is
+    complete) and every rank leaves with os._exit(0), so a hung collective cannot cost the whole run's line."""
+    import threading
+
+    def fire():
+        if rank == 0:
+            rec["c3"] = {"error": f"the C3 leg did not finish within {args.c3_timeout} s (watchdog); the headline "
+                                  f"fields of this line are complete"}
+            print(json.dumps(rec), flush=True)
+        sys.stderr.write(f"bench.py rank {rank}: C3 leg watchdog fired after {args.c3_timeout} s\n")
+        sys.stderr.flush()
+        os._exit(0)
+    t = threading.Timer(args.c3_timeout, fire)
+    t.daemon = True
+    t.start()
+    return t
+
+
 def main():
     import faulthandler
     faulthandler.enable()
@@ -790,95 +890,35 @@ def main():
     # sanity: finite GEBVs, b0 assembled
     assert np.all(np.isfinite(out["y_pred"])) and np.all(np.isfinite(out["B"]))
 
-    # the C3 leg (north star, BASELINE.json configs[2]): on by default whenever more than one rank runs
     head_q = int(st.q.item())
     grm_slices = int(st.lib.gbm_dev_grm_slices(n, args.stream_chunk or p_local)) if not exact else None
     digit_slices = int(st.slices.value) if exact else None
-    c3 = None
+    rec = headline_record(args, n, p_local, p_total, world, value, ms_per_step, syrk_ms, stage_ms, per_rank, exact,
+                          grm_slices, digit_slices, dist) if rank == 0 else None
+
+    # the C3 leg (north star, BASELINE.json configs[2]): on by default whenever more than one rank runs. A watchdog
+    # bounds it: should a collective hang, rank 0 prints the headline line (its "c3" an error) and every rank exits
     if args.c3_leg == "on" or (args.c3_leg == "auto" and world > 1):
         del st  # the headline shard's HBM back before the C3 shard is allocated
-        c3 = run_c3_leg(args, torch, dist, comm, world, rank, dev)
+        dog = c3_watchdog(args, rank, rec)
+        try:
+            c3 = run_c3_leg(args, torch, dist, comm, world, rank, dev)
+        except Exception as e:  # a failed leg is reported in the line; the headline stands
+            import traceback
+            traceback.print_exc()
+            c3 = {"error": f"the C3 leg failed: {e!r}"}
+            if world > 1:  # the other ranks may be inside a collective: end the run after the line
+                if rank == 0:
+                    rec["c3"] = c3
+                    print(json.dumps(rec), flush=True)
+                os._exit(0)
+        dog.cancel()
+        if rank == 0:
+            rec["c3"] = c3
 
     if rank != 0:
         dist.destroy_process_group()
         return
-
-    # algorithmic work of SURVEY.md §8d: GRM n(n+1)p (unique triangle of the rank-p update),
-    # Cholesky n³/3, solves 8n² per right-hand side (four triangular solves), back-solve 2np
-    grm_flops = float(n) * (n + 1) * p_local
-    chol_flops = float(n) ** 3 / 3.0
-    solve_flops = 8.0 * float(n) ** 2 * args.nrhs + 2.0 * n * p_local * args.nrhs
-    achieved = grm_flops / (syrk_ms / 1000.0) / 1e12
-    traffic, traffic_stale = load_pmc(n, p_local) if not (args.stream_chunk or exact) else (None, None)
-    e2e_frac = (grm_flops + chol_flops + solve_flops) / (ms_per_step / 1000.0) / (PEAK_F64_TFLOPS * 1e12)
-
-    rec = {
-        "metric": "GRM+GBLUP genotype-cells/s (n x p)",
-        "value": value,
-        "unit": "genotype-cells/s",
-        "n_gpus": world,
-        "steps": args.steps,
-        "warmup": args.warmup,
-        "ms_per_step": ms_per_step,
-        "higher_is_better": True,
-        "scaling": "weak",
-        "vs_baseline": None,
-        "dtype": ("i8 digit GEMMs (exact int32 sums) + int128 centring -> f64 G; f64 solve" if exact else "f64"),
-        "data": "synthetic: counter-hash genotypes (MAF U(0.05,0.5), dosage Binomial(2,f), X=d/2) generated in HBM"
-                + (" as int8 dosages" if (args.stream_chunk or exact) else " as fp64") + "; 1% QTL phenotype, h2=0.5",
-        "config": {
-            "workload": workload_label(n, p_local, world, args.stream_chunk, exact),
-            "n": n, "p_per_gpu": p_local, "p_total": p_total, "traits": args.nrhs, "lambda": args.lam,
-            "grm_slices": grm_slices,
-            "grm_digit_slices": digit_slices,
-            "stream_chunk": args.stream_chunk or None,
-            "parallelism": f"loci-shard x{world}",
-        },
-        "roofline": {
-            "bound": "mfma",
-            "kernel": "GRM stage: syrk_kernel<kPersist> (fp64 v_mfma_f64_16x16x4_f64 128x128 tiles) + "
-                      "grm_edge_kernel (ragged last column); achieved = all n(n+1)p flops / stage time"
-                      + ("; streamed: the stage also standardises each chunk from the int8 dosages"
-                         if args.stream_chunk else ""),
-            "achieved": achieved,
-            "peak": PEAK_F64_TFLOPS,
-            "unit": "TFLOP/s",
-            "frac": achieved / PEAK_F64_TFLOPS,
-            "frac_of_measured_mfma": achieved / MEASURED_MFMA_F64_TFLOPS,
-            "measured_mfma_peak": MEASURED_MFMA_F64_TFLOPS,
-            "traffic": traffic,
-            "traffic_source": "profiles/pmc_grm.json: rocprofv3 --pmc FETCH_SIZE (x2, gfx950 16 B/lane "
-                              "under-count) + WRITE_SIZE per GRM launch, separate passes of this command"
-                              if traffic is not None else None,
-            "traffic_stale": traffic_stale,
-            "flops_per_launch": grm_flops,
-            "ms_per_launch": syrk_ms,
-        },
-        "stage_ms": stage_ms,
-        "e2e_fp64_frac_of_peak": e2e_frac,
-        "world_size": world,
-        "backend": dist.get_backend() if dist.is_initialized() else None,
-        "collectives": ("RCCL" if dist.is_initialized() and dist.get_backend() == "nccl" else
-                        dist.get_backend() if dist.is_initialized() else "none (one rank)")
-                       + (" (forced at one rank: --collectives always)" if world == 1 and dist.is_initialized() else ""),
-        "per_rank_stage_ms": per_rank if world > 1 or dist.is_initialized() else None,
-    }
-    if exact:
-        S = digit_slices
-        ops = S * grm_flops  # S digit GEMMs of n(n+1)/2 x p int8 multiply-adds (2 ops each)
-        tops = ops / (syrk_ms / 1000.0) / 1e12
-        rec["roofline"] = {
-            "bound": "mfma",
-            "kernel": f"GRM stage: xg_gemm_kernel<{S}> (v_mfma_i32_16x16x64_i8, {S} base-128 digit GEMMs of the fixed-"
-                      "point locus weights, 128x64 upper tiles) + its per-locus prep kernels (stats, digits, transpose, "
-                      "int128 centring terms); achieved = S n(n+1)p int8 ops / stage time",
-            "achieved": tops, "peak": PEAK_I8_TOPS, "unit": "TOPS (int8)", "frac": tops / PEAK_I8_TOPS,
-            "frac_of_measured_i8_loop": tops / MEASURED_I8_LOOP_TOPS, "measured_i8_loop": MEASURED_I8_LOOP_TOPS,
-            "traffic": None, "ops_per_launch": ops, "ms_per_launch": syrk_ms,
-        }
-        rec["e2e_fp64_frac_of_peak"] = None
-    if c3 is not None:
-        rec["c3"] = c3
     if world == 1 and not args.no_host_path and not args.stream_chunk and float(n) * p_local <= 2e9:
         rec["host_path"] = host_path(args, torch)
         rec["stage_ms"]["h2d_x_pinned"] = rec["host_path"]["h2d_x_ms_pinned"]
