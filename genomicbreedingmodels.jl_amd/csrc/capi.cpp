@@ -11,6 +11,7 @@
 #include <algorithm>
 #include <atomic>
 #include <cmath>
+#include <condition_variable>
 #include <cstring>
 #include <map>
 #include <memory>
@@ -46,6 +47,7 @@ struct FitCtx {
   DevBuf errs, q2;               // streamed fit: per-chunk carry error cells; scratch kept count
   DevBuf astrip, agathered;      // the distributed factorisation's area all-gather (on the copy stream)
   hipEvent_t ev_area = nullptr, ev_upd = nullptr;  // area exchange done / next area updated
+  HostPinned pack;               // host-pack staging ring (fp64 host X packed to dosage bytes)
   ~FitCtx() {
     (void)hipSetDevice(dev);
     for (hipEvent_t e : ev) (void)hipEventDestroy(e);
@@ -596,6 +598,98 @@ int dosage_upload_shard(const Problem& pr, Shard& sh, bool early_exit) {
   GBM_HIP_TRY(hipMemcpyAsync(&bad, c.errs.p, 4, hipMemcpyDeviceToHost, s));
   GBM_HIP_TRY(hipStreamSynchronize(s));
   GBM_HIP_TRY(hipStreamSynchronize(c.copy.s));  // no upload still writes a staging buffer
+  if (bad) return kNotDosage;
+  sh.d8_ready = true;
+  return GBM_OK;
+}
+
+// fp64 host X of a shard → dosage bytes D8 = 2x, packed on the HOST (GBM_HOST_PACK, default 1): `threads` workers
+// check and pack chunks of loci (≈ 4 MB of bytes each) into a ring of pinned staging slots, and this thread
+// uploads each chunk as soon as it is packed (the copy stream), keeping two copies in flight; a slot is reused
+// only after its previous chunk's copy has completed. Only n·p bytes cross PCIe (C2: 250 MB instead of 2 GB of
+// fp64). Returns kNotDosage as soon as any worker meets a 2x that is not exactly 0, 1 or 2 (every worker stops).
+int host_pack_upload_shard(const Problem& pr, Shard& sh, int threads) {
+  FitCtx& c = sh.x();
+  const int64_t n = pr.n, pl = sh.p;
+  GBM_HIP_TRY(hipSetDevice(c.dev));
+  GBM_TRY(ensure_copy_stream(c));
+  const int T = std::max(1, threads);
+  // loci per chunk: ≈ 4 MB of bytes (GBM_PACK_CHUNK: tests, many chunks through a small ring)
+  const int64_t pc = std::max<int64_t>(1, std::min<int64_t>(pl, knob_i64("GBM_PACK_CHUNK", ((int64_t)4 << 20) / n)));
+  const int64_t nch = (pl + pc - 1) / pc;
+  const int64_t R = std::max<int64_t>(4, 2 * (int64_t)T);
+  GBM_TRY(ensure(c.D8, c.dev, pl * n));
+  GBM_TRY(ensure_pinned(c.pack, R * pc * n));
+  GBM_TRY(ensure_events(c, R));
+  int8_t* ring = static_cast<int8_t*>(c.pack.p);
+  std::mutex mu;
+  std::condition_variable cv;
+  std::vector<char> ready(nch, 0);
+  int64_t copies_done = 0;  // chunks [0, copies_done) have landed on the device: their slots are free
+  bool bad = false, stop = false;
+  auto worker = [&](int t) {
+    for (int64_t m = t; m < nch; m += T) {
+      {
+        std::unique_lock<std::mutex> lk(mu);
+        cv.wait(lk, [&] { return bad || stop || m < copies_done + R; });
+        if (bad || stop) return;
+      }
+      const int64_t j = m * pc, cnt = std::min(pc, pl - j);
+      const bool ok = pack_dosage_columns(pr.X + (sh.j0 + j) * pr.ld, pr.ld, n, cnt, ring + (m % R) * pc * n);
+      std::lock_guard<std::mutex> lk(mu);
+      if (!ok) bad = true;
+      else ready[m] = 1;
+      cv.notify_all();
+      if (!ok) return;
+    }
+  };
+  std::vector<std::thread> th;
+  th.reserve(T);
+  for (int t = 0; t < T; t++) {
+    try {
+      th.emplace_back(worker, t);
+    } catch (...) {  // no thread available: this thread packs (and uploads) the rest alone
+      break;
+    }
+  }
+  const int started = (int)th.size();
+  int rc = GBM_OK;
+  int64_t issued = 0;
+  for (int64_t k = 0; k < nch && rc == GBM_OK; k++) {
+    if (started == 0) {  // no worker threads: pack here (slot reuse is safe: copies are synchronised below)
+      const int64_t j = k * pc, cnt = std::min(pc, pl - j);
+      if (!pack_dosage_columns(pr.X + (sh.j0 + j) * pr.ld, pr.ld, n, cnt, ring + (k % R) * pc * n)) {
+        bad = true;
+        break;
+      }
+    } else {
+      std::unique_lock<std::mutex> lk(mu);
+      cv.wait(lk, [&] { return bad || ready[k]; });
+      if (bad) break;
+    }
+    const int64_t j = k * pc, cnt = std::min(pc, pl - j);
+    hipError_t e = hipMemcpyAsync((int8_t*)c.D8.p + j * n, ring + (k % R) * pc * n, cnt * n, hipMemcpyHostToDevice,
+                                  c.copy.s);
+    if (e == hipSuccess) e = hipEventRecord(c.ev[k % R], c.copy.s);
+    issued = k + 1;
+    // two copies in flight at most; the chunks before them have landed: their slots go back to the workers
+    while (e == hipSuccess && copies_done < k - 1) {
+      e = hipEventSynchronize(c.ev[copies_done % R]);
+      std::lock_guard<std::mutex> lk(mu);
+      copies_done++;
+      cv.notify_all();
+    }
+    if (e != hipSuccess) rc = fail(GBM_E_HIP, std::string("host-pack upload: HIP error '") + hipGetErrorString(e) + "'");
+  }
+  {
+    std::lock_guard<std::mutex> lk(mu);
+    stop = true;
+    cv.notify_all();
+  }
+  for (auto& x : th) x.join();
+  (void)issued;
+  GBM_HIP_TRY(hipStreamSynchronize(c.copy.s));  // no copy still reads a staging slot
+  GBM_TRY(rc);
   if (bad) return kNotDosage;
   sh.d8_ready = true;
   return GBM_OK;
@@ -1297,8 +1391,17 @@ int run_fit(const Problem& pr, const double* Y, int64_t ldy, int64_t nrhs, doubl
     RoctxRange r("gbm: upload + standardise + GRM");
     if (exact) {
       for (auto& sh : shards) sh->exact = true;
+      // fp64 host X: packed to dosage bytes on the host (GBM_HOST_PACK=1, default) or converted on the device from
+      // uploaded fp64 chunks (0); the host threads are shared among the call's shards
+      const bool host_pack = knob_i64("GBM_HOST_PACK", 1) != 0;
+      const int pack_threads = std::max(1, host_pack_threads() / (int)shards.size());
       const int rc = parallel_shards(shards, [&](size_t, Shard& sh) {
-        if (pr.src == Source::F64) GBM_TRY(dosage_upload_shard(pr, sh, mode == GBM_GRM_AUTO));
+        if (pr.src == Source::F64) {
+          if (host_pack)
+            GBM_TRY(host_pack_upload_shard(pr, sh, pack_threads));
+          else
+            GBM_TRY(dosage_upload_shard(pr, sh, mode == GBM_GRM_AUTO));
+        }
         return exact_grm_shard(pr, sh, mode == GBM_GRM_AUTO && pr.src == Source::I8);
       });
       if (rc == kNotDosage && mode == GBM_GRM_EXACT)

@@ -83,6 +83,10 @@ int launch_gather_dosage(const double* Xt, int64_t ldx, int64_t p, const int32_t
 int launch_dosage_from_f64(const double* X, int64_t ldx, int64_t n, int64_t p, int8_t* D, int64_t ldd, int32_t* bad,
                            hipStream_t s);
 int launch_dosage_check_i8(const int8_t* D, int64_t ldd, int64_t n, int64_t p, int32_t* bad, hipStream_t s);
+// host packing (hostpack.cpp): fp64 columns (column j at X + j·ld) → dosage bytes 2x (n per column); false when
+// some 2x is not exactly 0, 1 or 2. host_pack_threads: the packing workers of one call (GBM_PACK_THREADS)
+bool pack_dosage_columns(const double* X, int64_t ld, int64_t n, int64_t p, int8_t* dst);
+int host_pack_threads();
 // GBM_GRM_* of a call: grm_mode, or for GBM_GRM_DEFAULT the GBM_GRM environment variable, else fp64
 int resolve_grm_mode(int grm_mode);
 int launch_weighted_sum(const double* mean, const double* B, int64_t ldb, int64_t p, int64_t nrhs, double* msum,

@@ -119,6 +119,33 @@ inline int ensure(DevBuf& b, int dev, int64_t bytes) {
   return rc;
 }
 
+// A pinned (page-locked) host buffer that only grows (the host-pack staging ring of a pooled context).
+struct HostPinned {
+  void* p = nullptr;
+  int64_t cap = 0;
+  HostPinned() = default;
+  HostPinned(const HostPinned&) = delete;
+  HostPinned& operator=(const HostPinned&) = delete;
+  ~HostPinned() {
+    if (p) (void)hipHostFree(p);
+  }
+};
+inline int ensure_pinned(HostPinned& b, int64_t bytes) {
+  if (b.p && b.cap >= bytes) return GBM_OK;
+  if (b.p) (void)hipHostFree(b.p);
+  b.p = nullptr;
+  b.cap = 0;
+  const hipError_t e = hipHostMalloc(&b.p, (size_t)bytes, hipHostMallocDefault);
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    b.p = nullptr;
+    return fail(GBM_E_OOM, std::string("pinned host allocation of ") + std::to_string(bytes) + " bytes failed: " +
+                               hipGetErrorString(e));
+  }
+  b.cap = bytes;
+  return GBM_OK;
+}
+
 struct Stream {
   hipStream_t s = nullptr;
   int dev = 0;

@@ -14,6 +14,10 @@
 
 #include "../../include/gbm.h"
 
+namespace gbm {  // internal host helper (csrc/hostpack.cpp), linked in with the shim's objects
+bool pack_dosage_columns(const double* X, int64_t ld, int64_t n, int64_t p, int8_t* dst);
+}
+
 static int failures = 0;
 #define CHECK(cond)                                                     \
   do {                                                                  \
@@ -87,8 +91,31 @@ static void entry_points(int seed) {
   CHECK(gbm_dev_grm_syrk(nullptr, 0, 0, 0, nullptr, 0, nullptr, 0, nullptr) == GBM_E_ARG);
 }
 
+// the host packer (grm_mode exact / auto on fp64 host X): 2x in {0, 1, 2} packed, anything else flagged —
+// 0.25, 1.5, NaN, ±Inf, a negative dosage — in any column of a strided (ld > n) block
+static void host_pack() {
+  const int64_t n = 37, ld = 41, p = 5;
+  std::vector<double> X(ld * p, 7.0);
+  for (int64_t j = 0; j < p; j++)
+    for (int64_t i = 0; i < n; i++) X[j * ld + i] = 0.5 * (double)((i * 7 + j) % 3);
+  X[2 * ld + 3] = -0.0;
+  std::vector<int8_t> D(n * p, -1);
+  CHECK(gbm::pack_dosage_columns(X.data(), ld, n, p, D.data()));
+  bool same = true;
+  for (int64_t j = 0; j < p; j++)
+    for (int64_t i = 0; i < n; i++) same &= D[j * n + i] == (int8_t)(2.0 * X[j * ld + i]);
+  CHECK(same);
+  const double bad_vals[] = {0.25, 1.5, NAN, INFINITY, -INFINITY, -0.5, 1.0000000000000002};
+  for (double v : bad_vals) {
+    std::vector<double> Y(X);
+    Y[(p - 1) * ld + n - 1] = v;  // the last cell of the last column
+    CHECK(!gbm::pack_dosage_columns(Y.data(), ld, n, p, D.data()));
+  }
+}
+
 int main() {
   CHECK(gbm_version() == GBM_VERSION);
+  host_pack();
   entry_points(0);
   // eight threads at once: every error message stays in its own thread
   std::vector<std::thread> th;

@@ -177,3 +177,43 @@ def test_model_function_default_auto_and_sessions(dosage_case):
         s.set_grm("exact")
         with pytest.raises(gbm.ArgumentError, match="not diploid dosages"):
             s.gblup(idx, Y[idx])
+
+
+@pytest.mark.parametrize("threads,chunk", [("1", "64"), ("3", "100"), ("16", "64"), ("4", "0")])
+def test_host_packed_auto_bit_identical_to_device_checked(dosage_case, gbm_env, threads, chunk):
+    """fp64 host X under auto / exact is checked and packed to dosage bytes on the HOST
+    (GBM_HOST_PACK=1, the default: worker threads, a ring of pinned slots, each chunk uploaded as it is packed)
+    instead of uploaded as fp64 and converted on the device (GBM_HOST_PACK=0). Both give the same bits, against the
+    oracle; many small chunks (GBM_PACK_CHUNK) reuse every ring slot; one non-dosage cell in the last locus falls
+    back to fp64 both ways (auto) or fails (exact); two shards on one device split the threads."""
+    X, Y, ref = dosage_case
+    n, p = X.shape
+    gbm_env.setenv("GBM_PACK_THREADS", threads)
+    if chunk != "0":
+        gbm_env.setenv("GBM_PACK_CHUNK", chunk)
+    out = {}
+    for hp in ("1", "0"):
+        gbm_env.setenv("GBM_HOST_PACK", hp)
+        info = {}
+        out[hp] = gbm.gblup_arrays(X, Y, grm="auto", info=info)
+        assert info["grm_used"] == "exact"
+        check(out[hp], ref)
+    for a, b in zip(out["1"], out["0"]):
+        assert np.array_equal(np.asarray(a), np.asarray(b))
+    Xb = X.copy()
+    Xb[n - 1, p - 1] = 0.25  # not a dosage/2, in the last chunk
+    refb = oracle.gblup_fit(Xb, Y, 1.0)
+    got = {}
+    for hp in ("1", "0"):
+        gbm_env.setenv("GBM_HOST_PACK", hp)
+        info = {}
+        got[hp] = gbm.gblup_arrays(Xb, Y, grm="auto", info=info)
+        assert info["grm_used"] == "fp64"
+        check(got[hp], refb)
+        with pytest.raises(gbm.ArgumentError, match="not diploid dosages"):
+            gbm.gblup_arrays(Xb, Y, grm="exact")
+    for a, b in zip(got["1"], got["0"]):
+        assert np.array_equal(np.asarray(a), np.asarray(b))
+    gbm_env.setenv("GBM_HOST_PACK", "1")
+    two = gbm.gblup_arrays(X, Y, grm="auto", devices=[0, 0])
+    check(two, ref)

@@ -11,10 +11,12 @@ HIPCC=${HIPCC:-/opt/rocm/bin/hipcc}
 SAN="-Xarch_host -fsanitize=address -Xarch_host -fsanitize=undefined -Xarch_host -fno-sanitize-recover=all"
 objs=()
 pids=()
-for f in stats.hip grm.hip grm_exact.hip chol.hip chol_flow.hip effects.hip gibbs.hip capi.cpp session.cpp knobs.cpp; do
+for f in stats.hip grm.hip grm_exact.hip chol.hip chol_flow.hip effects.hip gibbs.hip capi.cpp session.cpp knobs.cpp hostpack.cpp; do
   o="$OUT/$f.o"
   objs+=("$o")
-  $HIPCC --offload-arch=gfx950 -O1 -g -fno-omit-frame-pointer -fPIC -std=c++17 $SAN -c "$CSRC/$f" -o "$o" &
+  HO=""
+  [ "$f" = hostpack.cpp ] && HO="--offload-host-only"
+  $HIPCC --offload-arch=gfx950 $HO -O1 -g -fno-omit-frame-pointer -fPIC -std=c++17 $SAN -c "$CSRC/$f" -o "$o" &
   pids+=($!)
 done
 for p in "${pids[@]}"; do wait "$p"; done
