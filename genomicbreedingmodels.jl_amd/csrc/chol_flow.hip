@@ -505,8 +505,10 @@ chol_flow_kernel(double* __restrict__ G, int64_t ld, int nbc, double* __restrict
 
   // a solved tile's transposed copy -> G lower (rows j0.., columns i0..; read only by the back
   // substitution / μ̂ kernels after this launch, so stored after the tile's flag)
+  // (wave = quarter, lane = row: a wave's LDS reads walk one source row, conflict-free; with four lanes per row and
+  // the quarters in the same 32-lane half, the four quarters' rows 16 apart hit the same banks: 4-way)
   auto store_lower = [&](const double* Xs, int64_t i0, int64_t j0) {
-    const int row = tid >> 2, quarter = tid & 3;
+    const int row = tid & 63, quarter = tid >> 6;
     double* dl = G + (j0 + row) * ld + i0 + quarter * 16;
 #pragma unroll
     for (int e = 0; e < 16; e += 2) {
@@ -583,8 +585,10 @@ chol_flow_kernel(double* __restrict__ G, int64_t ld, int nbc, double* __restrict
       auto after_own = [&](int w) {
         if (w == 0) {
           if (i > 0) {
-            for (int e = lane; e < FT * 8; e += 64) {  // 64 rows x 8 pieces of 8 doubles
-              const int row = e >> 3, piece = e & 7;
+            // 64 rows x 8 pieces of 8 doubles, lane = row (conflict-free LDS reads: the former 8 pieces per row in
+            // one 32-lane half read rows 8 apart, the same banks: 8-way)
+            for (int piece = 0; piece < 8; piece++) {
+              const int row = lane;
               double* dl = G + (i0 + row) * ld + (i0 - FT) + piece * 8;
 #pragma unroll
               for (int u = 0; u < 8; u += 2) {
