@@ -400,8 +400,11 @@ def host_path(args, torch):
         "ms_per_call_pageable_x": ms_page, "ms_per_call_pinned_x": ms_pin, "ms_per_call_dosage_i8": ms_i8,
         "ms_per_call_auto_f64_x": ms_auto, "ms_per_call_auto_f64_x_pinned": ms_auto_pin,
         "auto_note": "gbm_gblup_fit_ex(GBM_GRM_AUTO) on the same pageable (and pinned) fp64 X: the drop-in gblup's "
-                     "default on diploid data (julia/gblup.jl grm = :dropin with GBM_GRM unset) — fp64 X over PCIe in "
-                     "chunks, 2x checked and packed to int8 on the device, then the exact-integer GRM",
+                     "default on diploid data (julia/gblup.jl grm = :dropin with GBM_GRM unset) — 2x checked and packed "
+                     "to dosage bytes on the host by up to 16 threads (GBM_HOST_PACK=1, the default), 1 B per cell over "
+                     "PCIe chunk by chunk, then the exact-integer GRM (DESIGN.md §4.8)",
+        "host_pack": {"enabled": os.environ.get("GBM_HOST_PACK", "1") != "0",
+                      "threads": int(os.environ.get("GBM_PACK_THREADS", "0") or 0) or min(16, len(os.sched_getaffinity(0)))},
         "h2d_x_ms_pinned": h2d_pin, "h2d_x_ms_pageable": h2d_page, "x_bytes": 8 * n * p,
         "cells_per_s_pinned_x": n * p / (ms_pin / 1000.0), "device_allocations_per_call_after_warmup": 0,
     }
