@@ -89,6 +89,9 @@ def parse():
     ap.add_argument("--c3-warmup", type=int, default=1)
     ap.add_argument("--c3-seed", type=int, default=424242)
     ap.add_argument("--c3-timeout", type=float, default=300.0, help="watchdog of the C3 leg (seconds)")
+    ap.add_argument("--c3-exact", choices=("auto", "on", "off"), default="auto",
+                    help="also time C3 with the exact-integer GRM (the drop-in default on diploid data) after the fp64 "
+                         "leg; auto = whenever the C3 leg runs")
     ap.add_argument("--grm", choices=("fp64", "exact"), default="fp64",
                     help="fp64: the fp64-MFMA SYRK on standardised rows; exact: int8 dosages resident, the GRM "
                          "computed exactly by int8-MFMA digit GEMMs with int128 centring (csrc/grm_exact.hip)")
@@ -474,7 +477,7 @@ def c3_split(p_total, world, rank):
     return j0, max(0, min(per, p_total - j0))
 
 
-def c3_record(n, p_total, world, steps, warmup, ms_per_step, per_rank, chunk, backend):
+def c3_record(n, p_total, world, steps, warmup, ms_per_step, per_rank, chunk, backend, slices=None):
     """rank 0's `c3` object from the leg's timings: per_rank = one dict per rank with its mean per-step stage
     times (grm = standardise + GRM of its loci, allreduce, solve, effects) and collective spans. The fractions
     count the algorithmic flops of SURVEY.md §8d (GRM n(n+1)p, Cholesky n³/3, solves 8n², back-solve 2np) against
@@ -485,6 +488,20 @@ def c3_record(n, p_total, world, steps, warmup, ms_per_step, per_rank, chunk, ba
     grm_ms = max((r.get("grm_ms") or 0.0) for r in per_rank) if per_rank else 0.0
     peak = world * PEAK_F64_TFLOPS * 1e12
     ok = ms_per_step is not None and ms_per_step > 0
+    if slices:  # the exact-integer GRM: S int8 digit GEMMs of n(n+1)p ops against N x the int8 peak
+        ops = slices * grm_flops
+        return {
+            "workload": f"C3 GBLUP {n} x {p_total} with the exact-integer GRM (the drop-in default on diploid data): "
+                        f"the loci split over {world} rank(s), int8 dosages resident, {slices} int8-MFMA digit GEMMs + "
+                        f"int128 centring per rank, packed partial-GRM all-reduce ({backend}), distributed Cholesky; "
+                        f"strong scaling",
+            "n": n, "p_total": p_total, "ranks": world, "steps": steps, "warmup": warmup, "ms_per_step": ms_per_step,
+            "value": n * p_total / (ms_per_step / 1000.0) if ok else None, "unit": "genotype-cells/s",
+            "digit_slices": slices,
+            "grm_int8_frac_of_peak": ops / (grm_ms / 1000.0) / (world * PEAK_I8_TOPS * 1e12) if grm_ms > 0 else None,
+            "grm_ms_max_over_ranks": grm_ms, "peak_tops_per_gpu": PEAK_I8_TOPS, "backend": backend,
+            "per_rank": per_rank,
+        }
     return {
         "workload": f"C3 GBLUP {n} x {p_total} (BASELINE.json configs[2] at n=50000, p=600000): the loci split over "
                     f"{world} rank(s) ({-(-p_total // world)} per rank, int8 dosages resident, {chunk}-locus fp64 "
@@ -500,7 +517,7 @@ def c3_record(n, p_total, world, steps, warmup, ms_per_step, per_rank, chunk, ba
     }
 
 
-def run_c3_leg(args, torch, dist, base_comm, world, rank, dev):
+def run_c3_leg(args, torch, dist, base_comm, world, rank, dev, exact=False):
     """The C3 leg: n x p_total over the launched ranks, each rank a contiguous block of loci
     (int8 dosages generated in HBM, standardised per fp64 chunk into the partial GRM), the packed all-reduce of the
     upper tiles + q, the distributed Cholesky from n >= GBM_DIST_SOLVE_MIN_N (each rank its own tile columns,
@@ -508,7 +525,7 @@ def run_c3_leg(args, torch, dist, base_comm, world, rank, dev):
     ranks. Every rank returns its record; rank 0's carries every rank's stage times."""
     import gbm
     from gbm import synth
-    from gbm.sharded import HipStreamedShardStages, sharded_gblup_step
+    from gbm.sharded import HipExactShardStages, HipStreamedShardStages, sharded_gblup_step
 
     n, p_total = args.c3_individuals, args.c3_loci
     j0, p_local = c3_split(p_total, world, rank)
@@ -516,7 +533,10 @@ def run_c3_leg(args, torch, dist, base_comm, world, rank, dev):
     torch.cuda.synchronize()
     torch.cuda.empty_cache()
     gbm.load_library().gbm_release_device_cache()
-    st = HipStreamedShardStages(n, p_local, chunk, nrhs=1, lambda_=args.lam, device=dev)
+    if exact:
+        st = HipExactShardStages(n, p_local, nrhs=1, lambda_=args.lam, device=dev)
+    else:
+        st = HipStreamedShardStages(n, p_local, chunk, nrhs=1, lambda_=args.lam, device=dev)
     st.generate(args.c3_seed, j0)
     Y = synth.qtl_phenotypes(args.c3_seed, n, p_total, 1, device=dev)
     st.load_phenotypes(Y)
@@ -570,12 +590,13 @@ def run_c3_leg(args, torch, dist, base_comm, world, rank, dev):
     if dist.is_initialized():
         per_rank = [None] * world
         dist.all_gather_object(per_rank, mine)
+    slices = int(st.slices.value) if exact else None
     del st
     torch.cuda.synchronize()
     torch.cuda.empty_cache()
     backend = dist.get_backend() if dist.is_initialized() else "none"
     rec = c3_record(n, p_total, world, args.c3_steps, args.c3_warmup, elapsed * 1000.0 / K, per_rank, chunk,
-                    "RCCL" if backend == "nccl" else backend)
+                    "RCCL" if backend == "nccl" else backend, slices=slices)
     # every rank solved the same summed system: identical GEBVs (the distributed factorisation is bit-identical to
     # the redundant one); q = p_total (MAF >= 0.05: every locus polymorphic at this n)
     rec["ranks_agree"] = len({(r["y_pred_sum"], r["mu"]) for r in per_rank}) == 1
@@ -667,6 +688,9 @@ def launch_check(args, torch, dist, world, rank):
                "allreduce_span_ms": 0.0, "allreduce_bytes": 0} for r in range(world)]
         c3 = c3_record(args.c3_individuals, args.c3_loci, world, args.c3_steps, args.c3_warmup, None, pr,
                        min(args.c3_chunk, pr[0]["loci"]), dist.get_backend() if dist.is_initialized() else "none")
+        if args.c3_exact != "off":
+            c3["exact_grm_leg"] = sorted(c3_record(args.c3_individuals, args.c3_loci, world, args.c3_steps,
+                                                   args.c3_warmup, None, pr, 0, "none", slices=9))
     if rank == 0:
         print(json.dumps({"metric": "GRM+GBLUP genotype-cells/s (n x p)", "value": None, "unit": "genotype-cells/s", "c3": c3,
                           "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
@@ -766,8 +790,9 @@ def c3_watchdog(args, rank, rec):
 
     def fire():
         if rank == 0:
-            rec["c3"] = {"error": f"the C3 leg did not finish within {args.c3_timeout} s (watchdog); the headline "
-                                  f"fields of this line are complete"}
+            key = "c3_exact_grm" if "c3" in rec else "c3"  # (a finished fp64 leg keeps its record)
+            rec[key] = {"error": f"the C3 leg did not finish within {args.c3_timeout} s (watchdog); the headline "
+                                 f"fields of this line are complete"}
             print(json.dumps(rec), flush=True)
         sys.stderr.write(f"bench.py rank {rank}: C3 leg watchdog fired after {args.c3_timeout} s\n")
         sys.stderr.flush()
@@ -904,20 +929,28 @@ def main():
     if args.c3_leg == "on" or (args.c3_leg == "auto" and world > 1):
         del st  # the headline shard's HBM back before the C3 shard is allocated
         dog = c3_watchdog(args, rank, rec)
-        try:
-            c3 = run_c3_leg(args, torch, dist, comm, world, rank, dev)
-        except Exception as e:  # a failed leg is reported in the line; the headline stands
-            import traceback
-            traceback.print_exc()
-            c3 = {"error": f"the C3 leg failed: {e!r}"}
-            if world > 1:  # the other ranks may be inside a collective: end the run after the line
-                if rank == 0:
-                    rec["c3"] = c3
-                    print(json.dumps(rec), flush=True)
-                os._exit(0)
-        dog.cancel()
+
+        def leg(exact):
+            try:
+                return run_c3_leg(args, torch, dist, comm, world, rank, dev, exact=exact)
+            except Exception as e:  # a failed leg is reported in the line; the headline stands
+                import traceback
+                traceback.print_exc()
+                err = {"error": f"the C3 leg ({'exact' if exact else 'fp64'} GRM) failed: {e!r}"}
+                if world > 1:  # the other ranks may be inside a collective: end the run after the line
+                    if rank == 0:
+                        rec["c3_exact_grm" if exact else "c3"] = err
+                        print(json.dumps(rec), flush=True)
+                    os._exit(0)
+                return err
+        c3 = leg(False)
         if rank == 0:
             rec["c3"] = c3
+        if args.c3_exact != "off":
+            c3x = leg(True)
+            if rank == 0:
+                rec["c3_exact_grm"] = c3x
+        dog.cancel()
 
     if rank != 0:
         dist.destroy_process_group()

@@ -71,6 +71,8 @@ def test_c3_leg_record_at_two_ranks():
     for key in ("grm_ms", "allreduce_ms", "solve_ms", "allgather_blocked_ms", "allgather_calls"):
         assert all(key in r for r in c3["per_rank"])
     assert "strong scaling" in c3["workload"]
+    # the exact-integer GRM leg that follows (its record's keys; launch-check has no timings)
+    assert {"digit_slices", "grm_int8_frac_of_peak", "per_rank", "value"} <= set(c3["exact_grm_leg"])
 
 
 def test_c3_leg_off_at_one_rank_by_default():
@@ -87,6 +89,8 @@ def test_c3_record_arithmetic():
     import bench
     pr = [{"grm_ms": 2000.0}, {"grm_ms": 2500.0}]
     r = bench.c3_record(50000, 600000, 8, 2, 1, 3000.0, pr, 75000, "RCCL")
+    rx = bench.c3_record(50000, 600000, 8, 2, 1, 800.0, pr, 0, "RCCL", slices=9)
+    assert abs(rx["grm_int8_frac_of_peak"] - 9 * 50000.0 * 50001 * 600000 / 2.5 / (8 * 5000e12)) < 1e-12
     assert abs(r["value"] - 50000 * 600000 / 3.0) < 1e-3
     grm = 50000.0 * 50001 * 600000
     assert abs(r["grm_frac_of_peak"] - grm / 2.5 / (8 * 78.6e12)) < 1e-12

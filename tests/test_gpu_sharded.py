@@ -156,3 +156,9 @@ def test_bench_c3_leg_two_ranks_same_device():
         assert r["loci"] == 30000 and r["y_pred_finite"]
         assert r["allgather_calls"] > 0 and r["allgather_blocked_ms"] > 0  # the distributed solve engaged
         assert r["allreduce_bytes"] > 8 * 20000 * 20000 // 2  # the packed upper tiles (+ q) were all-reduced
+    cx = rec["c3_exact_grm"]  # the same C3 with the exact-integer GRM: the same q, both ranks agree
+    print("C3 leg, exact GRM:", json.dumps({k: v for k, v in cx.items() if k != "per_rank"}))
+    assert cx["ranks"] == 2 and cx["digit_slices"] >= 8 and cx["value"] > 0
+    assert {r["q"] for r in cx["per_rank"]} == {60000} and len({(r["y_pred_sum"], r["mu"]) for r in cx["per_rank"]}) == 1
+    # the exact and fp64 GRMs give the same fit to rounding
+    assert abs(cx["per_rank"][0]["mu"] - c3["per_rank"][0]["mu"]) < 1e-9 * abs(c3["per_rank"][0]["mu"])
