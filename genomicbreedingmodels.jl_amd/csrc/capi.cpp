@@ -604,94 +604,130 @@ int dosage_upload_shard(const Problem& pr, Shard& sh, bool early_exit) {
 }
 
 // fp64 host X of a shard → dosage bytes D8 = 2x, packed on the HOST (GBM_HOST_PACK, default 1): `threads` workers
-// check and pack chunks of loci (≈ 4 MB of bytes each) into a ring of pinned staging slots, and this thread
-// uploads each chunk as soon as it is packed (the copy stream), keeping two copies in flight; a slot is reused
-// only after its previous chunk's copy has completed. Only n·p bytes cross PCIe (C2: 250 MB instead of 2 GB of
-// fp64). Returns kNotDosage as soon as any worker meets a 2x that is not exactly 0, 1 or 2 (every worker stops).
+// check and pack chunks of loci (≈ 4 MB of bytes each, GBM_PACK_CHUNK loci for tests) into a ring of pinned
+// staging slots (ChunkPacker, hostpack.cpp), and this thread uploads each chunk as soon as it is packed (the copy
+// stream); a slot is reused only after its previous chunk's copy has landed. Only n·p bytes cross PCIe (C2: 250 MB
+// instead of 2 GB of fp64). Returns kNotDosage as soon as any worker meets a 2x that is not exactly 0, 1 or 2.
 int host_pack_upload_shard(const Problem& pr, Shard& sh, int threads) {
   FitCtx& c = sh.x();
   const int64_t n = pr.n, pl = sh.p;
   GBM_HIP_TRY(hipSetDevice(c.dev));
   GBM_TRY(ensure_copy_stream(c));
-  const int T = std::max(1, threads);
-  // loci per chunk: ≈ 4 MB of bytes (GBM_PACK_CHUNK: tests, many chunks through a small ring)
   const int64_t pc = std::max<int64_t>(1, std::min<int64_t>(pl, knob_i64("GBM_PACK_CHUNK", ((int64_t)4 << 20) / n)));
-  const int64_t nch = (pl + pc - 1) / pc;
-  const int64_t R = std::max<int64_t>(4, 2 * (int64_t)T);
+  const auto sched = chunk_schedule(pl, pc, false);
+  constexpr int R = 4;
   GBM_TRY(ensure(c.D8, c.dev, pl * n));
   GBM_TRY(ensure_pinned(c.pack, R * pc * n));
   GBM_TRY(ensure_events(c, R));
-  int8_t* ring = static_cast<int8_t*>(c.pack.p);
-  std::mutex mu;
-  std::condition_variable cv;
-  std::vector<char> ready(nch, 0);
-  int64_t copies_done = 0;  // chunks [0, copies_done) have landed on the device: their slots are free
-  bool bad = false, stop = false;
-  auto worker = [&](int t) {
-    for (int64_t m = t; m < nch; m += T) {
-      {
-        std::unique_lock<std::mutex> lk(mu);
-        cv.wait(lk, [&] { return bad || stop || m < copies_done + R; });
-        if (bad || stop) return;
-      }
-      const int64_t j = m * pc, cnt = std::min(pc, pl - j);
-      const bool ok = pack_dosage_columns(pr.X + (sh.j0 + j) * pr.ld, pr.ld, n, cnt, ring + (m % R) * pc * n);
-      std::lock_guard<std::mutex> lk(mu);
-      if (!ok) bad = true;
-      else ready[m] = 1;
-      cv.notify_all();
-      if (!ok) return;
-    }
-  };
-  std::vector<std::thread> th;
-  th.reserve(T);
-  for (int t = 0; t < T; t++) {
-    try {
-      th.emplace_back(worker, t);
-    } catch (...) {  // no thread available: this thread packs (and uploads) the rest alone
-      break;
-    }
-  }
-  const int started = (int)th.size();
   int rc = GBM_OK;
-  int64_t issued = 0;
-  for (int64_t k = 0; k < nch && rc == GBM_OK; k++) {
-    if (started == 0) {  // no worker threads: pack here (slot reuse is safe: copies are synchronised below)
-      const int64_t j = k * pc, cnt = std::min(pc, pl - j);
-      if (!pack_dosage_columns(pr.X + (sh.j0 + j) * pr.ld, pr.ld, n, cnt, ring + (k % R) * pc * n)) {
+  bool bad = false;
+  {
+    ChunkPacker packer(pr.X + sh.j0 * pr.ld, pr.ld, n, sched, static_cast<int8_t*>(c.pack.p), pc * n, R, threads);
+    for (int64_t k = 0; k < (int64_t)sched.size(); k++) {
+      const int8_t* src = packer.wait(k);
+      if (!src) {
         bad = true;
         break;
       }
-    } else {
-      std::unique_lock<std::mutex> lk(mu);
-      cv.wait(lk, [&] { return bad || ready[k]; });
-      if (bad) break;
+      const int64_t j = sched[k].first, cnt = sched[k].second;
+      hipError_t e = hipMemcpyAsync((int8_t*)c.D8.p + j * n, src, cnt * n, hipMemcpyHostToDevice, c.copy.s);
+      if (e == hipSuccess) e = hipEventRecord(c.ev[k % R], c.copy.s);
+      // the previous chunk has landed: its slot (and every earlier one) goes back to the packer
+      if (e == hipSuccess && k >= 1) e = hipEventSynchronize(c.ev[(k - 1) % R]);
+      if (e != hipSuccess) {
+        rc = fail(GBM_E_HIP, std::string("host-pack upload: HIP error '") + hipGetErrorString(e) + "'");
+        break;
+      }
+      packer.release_upto(k);
     }
-    const int64_t j = k * pc, cnt = std::min(pc, pl - j);
-    hipError_t e = hipMemcpyAsync((int8_t*)c.D8.p + j * n, ring + (k % R) * pc * n, cnt * n, hipMemcpyHostToDevice,
-                                  c.copy.s);
-    if (e == hipSuccess) e = hipEventRecord(c.ev[k % R], c.copy.s);
-    issued = k + 1;
-    // two copies in flight at most; the chunks before them have landed: their slots go back to the workers
-    while (e == hipSuccess && copies_done < k - 1) {
-      e = hipEventSynchronize(c.ev[copies_done % R]);
-      std::lock_guard<std::mutex> lk(mu);
-      copies_done++;
-      cv.notify_all();
-    }
-    if (e != hipSuccess) rc = fail(GBM_E_HIP, std::string("host-pack upload: HIP error '") + hipGetErrorString(e) + "'");
-  }
-  {
-    std::lock_guard<std::mutex> lk(mu);
-    stop = true;
-    cv.notify_all();
-  }
-  for (auto& x : th) x.join();
-  (void)issued;
+  }  // (the packer's workers have stopped)
   GBM_HIP_TRY(hipStreamSynchronize(c.copy.s));  // no copy still reads a staging slot
   GBM_TRY(rc);
   if (bad) return kNotDosage;
   sh.d8_ready = true;
+  return GBM_OK;
+}
+
+// The pipelined fp64 upload + GRM (upload_grm_pipelined) of fp64 host X whose values are dosages/2, through the
+// host packer (grm_mode fp64, GBM_HOST_PACK): each pipeline chunk (the fp64 schedule, so the chunk GRMs are summed
+// exactly as there) is packed to bytes by the host workers into a pinned slot, uploaded at 1 B per cell and
+// standardised straight from the bytes (launch_standardize_i8: the same Z bits as the fp64 standardisation of
+// d/2), then its GRM added into G as in the fp64 path. Returns kNotDosage (G untouched by later chunks) when a
+// chunk is not dosage-valued: the caller then runs the plain fp64 upload for the shard.
+int upload_grm_pipelined_packed(const Problem& pr, Shard& sh, int64_t chunk, int threads) {
+  FitCtx& c = sh.x();
+  const int64_t n = pr.n, npad = npad_of(n), gdim = gdim_of(n), pl = sh.p;
+  GBM_HIP_TRY(hipSetDevice(c.dev));
+  hipStream_t s = c.stream.s;
+  GBM_TRY(ensure_copy_stream(c));
+  const auto sched = chunk_schedule(pl, chunk, n <= 8192 || ::gbm::knob("GBM_HOST_CHUNK") != nullptr);
+  const int64_t nch = (int64_t)sched.size();
+  int64_t pmax = 0;
+  for (const auto& jc : sched) pmax = std::max(pmax, jc.second);
+  constexpr int R = 3;
+  GBM_TRY(ensure_events(c, nch));
+  GBM_TRY(ensure(c.Xt, c.dev, pl * npad * 8));
+  GBM_TRY(ensure(c.D8, c.dev, pl * n));
+  GBM_TRY(ensure(c.mean, c.dev, pl * 8));
+  GBM_TRY(ensure(c.sd, c.dev, pl * 8));
+  GBM_TRY(ensure(c.keep, c.dev, pl * 4));
+  GBM_TRY(ensure(c.q, c.dev, 8));
+  GBM_TRY(ensure(c.G, c.dev, gdim * gdim * 8));
+  GBM_TRY(ensure_pinned(c.pack, R * pmax * n));
+  int64_t wsb = 0;
+  for (const auto& jc : sched) wsb = std::max(wsb, gbm_dev_grm_workspace(n, jc.second));
+  GBM_TRY(ensure(c.wsg, c.dev, wsb));
+  for (int64_t k = 1; k < nch; k++)
+    if (!grm_can_accumulate(n, sched[k].second)) {
+      GBM_TRY(ensure(c.Gc, c.dev, gdim * gdim * 8));
+      break;
+    }
+  GBM_HIP_TRY(hipMemsetAsync(c.q.p, 0, 8, s));
+  double* Xt = (double*)c.Xt.p;
+  int rc = GBM_OK;
+  bool bad = false;
+  {
+    ChunkPacker packer(pr.X + sh.j0 * pr.ld, pr.ld, n, sched, static_cast<int8_t*>(c.pack.p), pmax * n, R, threads);
+    for (int64_t k = 0; k < nch && rc == GBM_OK; k++) {
+      const int8_t* src = packer.wait(k);
+      if (!src) {
+        bad = true;
+        break;
+      }
+      const int64_t j = sched[k].first, pc = sched[k].second;
+      hipError_t e = hipMemcpyAsync((int8_t*)c.D8.p + j * n, src, pc * n, hipMemcpyHostToDevice, c.copy.s);
+      if (e == hipSuccess) e = hipEventRecord(c.ev[k], c.copy.s);
+      if (e == hipSuccess) e = hipStreamWaitEvent(s, c.ev[k], 0);
+      if (e != hipSuccess) {
+        rc = fail(GBM_E_HIP, std::string("host-pack upload: HIP error '") + hipGetErrorString(e) + "'");
+        break;
+      }
+      rc = launch_standardize_i8((const int8_t*)c.D8.p + j * n, n, pc, n, 2, Xt + j * npad, npad, (double*)c.mean.p + j,
+                                 (double*)c.sd.p + j, (int32_t*)c.keep.p + j, (int64_t*)c.q.p, s);
+      if (rc == GBM_OK) {
+        if (k > 0 && grm_can_accumulate(n, pc)) {
+          rc = launch_grm(Xt + j * npad, npad, pc, n, (double*)c.G.p, gdim, c.wsg.p, wsb, s, 1);
+        } else {
+          rc = gbm_dev_grm(Xt + j * npad, npad, pc, n, k == 0 ? (double*)c.G.p : (double*)c.Gc.p, gdim, c.wsg.p, wsb, s);
+          if (rc == GBM_OK && k > 0) rc = launch_add_inplace((double*)c.G.p, (const double*)c.Gc.p, gdim * gdim, s);
+        }
+      }
+      // the previous chunk's copy has landed: its slot goes back to the packer
+      if (rc == GBM_OK && k >= 1) {
+        e = hipEventSynchronize(c.ev[k - 1]);
+        if (e != hipSuccess) rc = fail(GBM_E_HIP, std::string("host-pack upload: HIP error '") + hipGetErrorString(e) + "'");
+      }
+      packer.release_upto(k);
+    }
+  }
+  GBM_HIP_TRY(hipStreamSynchronize(c.copy.s));
+  GBM_TRY(rc);
+  if (bad) {
+    GBM_HIP_TRY(hipStreamSynchronize(s));  // the chunks already queued are done before the fp64 path reuses G
+    return kNotDosage;
+  }
+  GBM_HIP_TRY(hipMemcpyAsync(&sh.q_host, c.q.p, 8, hipMemcpyDeviceToHost, s));
+  GBM_HIP_TRY(hipStreamSynchronize(s));
   return GBM_OK;
 }
 
@@ -1381,9 +1417,19 @@ int run_fit(const Problem& pr, const double* Y, int64_t ldy, int64_t nrhs, doubl
     // each shard's GRM is launched behind its own standardisation (a shard without polymorphic
     // loci contributes a zero partial; q == 0 over all shards fails below): streamed when its
     // rows do not fit, else resident (host chunks pipelined with the GRM, or in one piece)
+    // fp64 host X with grm_mode fp64: tried as dosages packed on the host first (GBM_HOST_PACK), 1 B per cell over
+    // PCIe; X that is not dosage-valued falls back to the fp64 upload at its first non-dosage chunk
+    const bool pack = mode == GBM_GRM_FP64 && pr.src == Source::F64 && knob_i64("GBM_HOST_PACK", 1) != 0;
+    const int pthreads = std::max(1, host_pack_threads() / (int)shards.size());
     return parallel_shards(shards, [&](size_t, Shard& sh) {
       if (sh.stream) return stream_grm_shard(pr, sh);
-      if (chunk > 0) return upload_grm_pipelined(pr, sh, chunk);
+      if (chunk > 0) {
+        if (pack) {
+          const int rc = upload_grm_pipelined_packed(pr, sh, chunk, pthreads);
+          if (rc != kNotDosage) return rc;
+        }
+        return upload_grm_pipelined(pr, sh, chunk);
+      }
       return prepare_grm_shard(pr, sh);
     });
   };

@@ -87,6 +87,24 @@ int launch_dosage_check_i8(const int8_t* D, int64_t ldd, int64_t n, int64_t p, i
 // some 2x is not exactly 0, 1 or 2. host_pack_threads: the packing workers of one call (GBM_PACK_THREADS)
 bool pack_dosage_columns(const double* X, int64_t ld, int64_t n, int64_t p, int8_t* dst);
 int host_pack_threads();
+// Packs the loci chunks sched[k] = (first locus, count) of fp64 columns (column j at X + j·ld) into dosage bytes,
+// chunk k into ring slot k mod slots (slot_bytes each, n bytes per locus), by `threads` workers that split each
+// chunk in order. wait(k): chunk k's packed bytes, or nullptr once any chunk was not dosage-valued (the workers then
+// stop); release_upto(k): the slots of chunks < k may be overwritten. The destructor stops and joins the workers.
+class ChunkPacker {
+ public:
+  ChunkPacker(const double* X, int64_t ld, int64_t n, const std::vector<std::pair<int64_t, int64_t>>& sched,
+              int8_t* ring, int64_t slot_bytes, int slots, int threads);
+  ~ChunkPacker();
+  ChunkPacker(const ChunkPacker&) = delete;
+  ChunkPacker& operator=(const ChunkPacker&) = delete;
+  const int8_t* wait(int64_t k);
+  void release_upto(int64_t k);
+
+ private:
+  struct Impl;
+  Impl* d_;
+};
 // GBM_GRM_* of a call: grm_mode, or for GBM_GRM_DEFAULT the GBM_GRM environment variable, else fp64
 int resolve_grm_mode(int grm_mode);
 int launch_weighted_sum(const double* mean, const double* B, int64_t ldb, int64_t p, int64_t nrhs, double* msum,

@@ -6,7 +6,11 @@
 #include <sched.h>
 
 #include <algorithm>
+#include <condition_variable>
 #include <cstdint>
+#include <mutex>
+#include <thread>
+#include <vector>
 
 #include "gbm_internal.h"
 
@@ -35,6 +39,100 @@ bool pack_dosage_columns(const double* X, int64_t ld, int64_t n, int64_t p, int8
   int bad = 0;
   for (int64_t j = 0; j < p; j++) bad |= pack_column(X + j * ld, n, dst + j * n);
   return bad == 0;
+}
+
+// ---- ChunkPacker ------------------------------------------------------------------------------------------
+struct ChunkPacker::Impl {
+  const double* X;
+  int64_t ld, n;
+  std::vector<std::pair<int64_t, int64_t>> sched;
+  int8_t* ring;
+  int64_t slot_bytes;
+  int R, T;
+  std::mutex mu;
+  std::condition_variable cv;
+  std::vector<int> done;     // parts packed per chunk
+  int64_t released = 0;      // chunks [0, released) have left their slots
+  int64_t next_item = 0;     // (chunk, part) items handed out, chunk-major
+  bool bad = false, stop = false;
+  std::vector<std::thread> th;
+
+  void work() {
+    for (;;) {
+      int64_t item, k;
+      {
+        std::unique_lock<std::mutex> lk(mu);
+        if (bad || stop || next_item >= (int64_t)sched.size() * T) return;
+        item = next_item++;
+        k = item / T;
+        cv.wait(lk, [&] { return bad || stop || k < released + R; });
+        if (bad || stop) return;
+      }
+      const int part = (int)(item % T);
+      const int64_t j = sched[k].first, pc = sched[k].second;
+      const int64_t a = pc * part / T, b = pc * (part + 1) / T;  // this part's loci of the chunk
+      const bool ok = b <= a || pack_dosage_columns(X + (j + a) * ld, ld, n, b - a, ring + (k % R) * slot_bytes + a * n);
+      std::lock_guard<std::mutex> lk(mu);
+      if (!ok) bad = true;
+      else done[k]++;
+      cv.notify_all();
+      if (!ok) return;
+    }
+  }
+};
+
+ChunkPacker::ChunkPacker(const double* X, int64_t ld, int64_t n, const std::vector<std::pair<int64_t, int64_t>>& sched,
+                         int8_t* ring, int64_t slot_bytes, int slots, int threads)
+    : d_(new Impl) {
+  d_->X = X;
+  d_->ld = ld;
+  d_->n = n;
+  d_->sched = sched;
+  d_->ring = ring;
+  d_->slot_bytes = slot_bytes;
+  d_->R = std::max(1, slots);
+  d_->T = std::max(1, threads);
+  d_->done.assign(sched.size(), 0);
+  for (int t = 0; t < d_->T; t++) {
+    try {
+      d_->th.emplace_back([this] { d_->work(); });
+    } catch (...) {  // no thread available: wait() packs on the calling thread
+      break;
+    }
+  }
+}
+
+ChunkPacker::~ChunkPacker() {
+  {
+    std::lock_guard<std::mutex> lk(d_->mu);
+    d_->stop = true;
+    d_->cv.notify_all();
+  }
+  for (auto& t : d_->th) t.join();
+  delete d_;
+}
+
+const int8_t* ChunkPacker::wait(int64_t k) {
+  Impl& d = *d_;
+  if (d.th.empty()) {  // no workers: pack the whole chunk here (its slot is free: the caller released k − R)
+    const int64_t j = d.sched[k].first, pc = d.sched[k].second;
+    if (d.bad || !pack_dosage_columns(d.X + j * d.ld, d.ld, d.n, pc, d.ring + (k % d.R) * d.slot_bytes)) {
+      d.bad = true;
+      return nullptr;
+    }
+    return d.ring + (k % d.R) * d.slot_bytes;
+  }
+  std::unique_lock<std::mutex> lk(d.mu);
+  d.cv.wait(lk, [&] { return d.bad || d.done[k] == d.T; });
+  return d.bad ? nullptr : d.ring + (k % d.R) * d.slot_bytes;
+}
+
+void ChunkPacker::release_upto(int64_t k) {
+  std::lock_guard<std::mutex> lk(d_->mu);
+  if (k > d_->released) {
+    d_->released = k;
+    d_->cv.notify_all();
+  }
 }
 
 int host_pack_threads() {

@@ -217,3 +217,38 @@ def test_host_packed_auto_bit_identical_to_device_checked(dosage_case, gbm_env, 
     gbm_env.setenv("GBM_HOST_PACK", "1")
     two = gbm.gblup_arrays(X, Y, grm="auto", devices=[0, 0])
     check(two, ref)
+
+
+@pytest.mark.parametrize("threads", ["16", "3"])
+def test_fp64_mode_host_packed_pipeline_bit_identical(gbm_env, threads):
+    """grm_mode fp64 on dosage-valued fp64 host X (the C-ABI default): every pipeline chunk is packed to bytes on the
+    host (GBM_HOST_PACK=1), uploaded at 1 B per cell and standardised from the bytes, the chunk GRMs summed in the
+    fp64 path's order — the same bits as the fp64 upload (GBM_HOST_PACK=0), against the oracle; a non-dosage cell
+    in a late chunk falls back to the fp64 upload (same bits again); two shards on one device split the threads."""
+    n, p = 777, 20000  # p >= 16 384: the pipelined upload (8 chunks + the halving tail at n <= 8192)
+    X = oracle.synth_genotypes(61, n, p)
+    Y = oracle.synth_phenotypes(X, 62, ntraits=2)
+    ref = oracle.gblup_fit(X, Y, 1.0)
+    gbm_env.setenv("GBM_PACK_THREADS", threads)
+    got = {}
+    for hp in ("1", "0"):
+        gbm_env.setenv("GBM_HOST_PACK", hp)
+        info = {}
+        got[hp] = gbm.gblup_arrays(X, Y, grm="fp64", info=info)
+        assert info["grm_used"] == "fp64"
+        check(got[hp], ref)
+    for a, b in zip(got["1"], got["0"]):
+        assert np.array_equal(np.asarray(a), np.asarray(b))
+    Xb = X.copy()
+    Xb[5, p - 3] = 0.3
+    refb = oracle.gblup_fit(Xb, Y, 1.0)
+    gotb = {}
+    for hp in ("1", "0"):
+        gbm_env.setenv("GBM_HOST_PACK", hp)
+        gotb[hp] = gbm.gblup_arrays(Xb, Y, grm="fp64")
+        check(gotb[hp], refb)
+    for a, b in zip(gotb["1"], gotb["0"]):
+        assert np.array_equal(np.asarray(a), np.asarray(b))
+    gbm_env.setenv("GBM_HOST_PACK", "1")
+    two = gbm.gblup_arrays(X, Y, grm="fp64", devices=[0, 0])
+    check(two, ref)
