@@ -14,9 +14,7 @@
 
 #include "../../include/gbm.h"
 
-namespace gbm {  // internal host helper (csrc/hostpack.cpp), linked in with the shim's objects
-bool pack_dosage_columns(const double* X, int64_t ld, int64_t n, int64_t p, int8_t* dst);
-}
+#include "../../genomicbreedingmodels.jl_amd/csrc/gbm_internal.h"  // internal host helpers (csrc/hostpack.cpp)
 
 static int failures = 0;
 #define CHECK(cond)                                                     \
@@ -113,9 +111,42 @@ static void host_pack() {
   }
 }
 
+// the chunked packer: 13 chunks of a strided block through a 3-slot ring by 5 workers, each slot released after
+// its chunk is consumed; then a non-dosage value in chunk 9 stops it there
+static void chunk_packer() {
+  const int64_t n = 53, ld = 60, p = 397, pc = 31, R = 3;
+  std::vector<double> X(ld * p, 9.0);
+  for (int64_t j = 0; j < p; j++)
+    for (int64_t i = 0; i < n; i++) X[j * ld + i] = 0.5 * (double)((i * 5 + j * 3) % 3);
+  std::vector<std::pair<int64_t, int64_t>> sched;
+  for (int64_t j = 0; j < p; j += pc) sched.emplace_back(j, std::min(pc, p - j));
+  std::vector<int8_t> ring(R * pc * n), out(n * p, -1);
+  for (int round = 0; round < 2; round++) {
+    if (round == 1) X[(9 * pc + 4) * ld + 7] = 0.75;
+    gbm::ChunkPacker pk(X.data(), ld, n, sched, ring.data(), pc * n, (int)R, 5);
+    int64_t k = 0;
+    for (; k < (int64_t)sched.size(); k++) {
+      const int8_t* src = pk.wait(k);
+      if (!src) break;
+      std::memcpy(out.data() + sched[k].first * n, src, sched[k].second * n);
+      pk.release_upto(k + 1);
+    }
+    if (round == 0) {
+      CHECK(k == (int64_t)sched.size());
+      bool same = true;
+      for (int64_t j = 0; j < p; j++)
+        for (int64_t i = 0; i < n; i++) same &= out[j * n + i] == (int8_t)(2.0 * X[j * ld + i]);
+      CHECK(same);
+    } else {
+      CHECK(k <= 9);
+    }
+  }
+}
+
 int main() {
   CHECK(gbm_version() == GBM_VERSION);
   host_pack();
+  chunk_packer();
   entry_points(0);
   // eight threads at once: every error message stays in its own thread
   std::vector<std::thread> th;
