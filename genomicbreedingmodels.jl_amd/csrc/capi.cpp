@@ -604,7 +604,7 @@ int dosage_upload_shard(const Problem& pr, Shard& sh, bool early_exit) {
 }
 
 // fp64 host X of a shard → dosage bytes D8 = 2x, packed on the HOST (GBM_HOST_PACK, default 1): `threads` workers
-// check and pack chunks of loci (≈ 4 MB of bytes each, GBM_PACK_CHUNK loci for tests) into a ring of pinned
+// check and pack chunks of loci (≈ 16 MB of bytes each, GBM_PACK_CHUNK loci for tests) into a ring of pinned
 // staging slots (ChunkPacker, hostpack.cpp), and this thread uploads each chunk as soon as it is packed (the copy
 // stream); a slot is reused only after its previous chunk's copy has landed. Only n·p bytes cross PCIe (C2: 250 MB
 // instead of 2 GB of fp64). Returns kNotDosage as soon as any worker meets a 2x that is not exactly 0, 1 or 2.
@@ -613,7 +613,7 @@ int host_pack_upload_shard(const Problem& pr, Shard& sh, int threads) {
   const int64_t n = pr.n, pl = sh.p;
   GBM_HIP_TRY(hipSetDevice(c.dev));
   GBM_TRY(ensure_copy_stream(c));
-  const int64_t pc = std::max<int64_t>(1, std::min<int64_t>(pl, knob_i64("GBM_PACK_CHUNK", ((int64_t)4 << 20) / n)));
+  const int64_t pc = std::max<int64_t>(1, std::min<int64_t>(pl, knob_i64("GBM_PACK_CHUNK", ((int64_t)16 << 20) / n)));
   const auto sched = chunk_schedule(pl, pc, false);
   constexpr int R = 4;
   GBM_TRY(ensure(c.D8, c.dev, pl * n));

@@ -75,7 +75,9 @@ struct ChunkPacker::Impl {
       std::lock_guard<std::mutex> lk(mu);
       if (!ok) bad = true;
       else done[k]++;
-      cv.notify_all();
+      // wake the waiters only when it matters: a finished chunk (the uploader) or a stop (everyone); a worker
+      // waiting for a slot is woken by release_upto
+      if (!ok || done[k] == T) cv.notify_all();
       if (!ok) return;
     }
   }
