@@ -16,10 +16,14 @@ __device__ __forceinline__ double dosage_z(int8_t d, double xs, double m, double
   return (x - m) * r;
 }
 
-// One wave per locus row; each lane reads 16-byte pairs along individuals (T = double: the
-// standardised row; T = int8_t: the dosage row, z rebuilt in registers); up to 4 traits per pass
-// over the row (the row stays in L1/L2 for later passes).
-template <typename T>
+// R locus rows per wave (round 6); each lane takes four consecutive individuals per pass, i = 4·lane + 256·k
+// (T = double: the standardised row, two 16-byte loads; T = int8_t: the dosage row, one 4-byte load, z rebuilt in
+// registers), and the trait vectors' values for them are loaded once for the wave's R rows. Every row is summed in
+// the same order whatever R and T — per lane fma(z_i, a_i, ·) over its individuals in order, then an xor-shuffle
+// tree — so B is bit-identical between the fp64 rows and the dosage bytes. Up to 4 traits per pass over the rows.
+// (Round 5 ran one row per wave with 2 individuals per lane: the int8 variant issued two byte loads per lane per
+// 128 individuals and re-read the trait vector from L2 for every locus, 0.29 ms at C2 for 250 MB of bytes.)
+template <typename T, int R>
 __global__ void __launch_bounds__(256) marker_effects_kernel(const T* __restrict__ Zt, int64_t ldz, int64_t p,
                                                              int64_t n, const double* __restrict__ A, int64_t lda,
                                                              int64_t nrhs, double inv_q,
@@ -28,45 +32,96 @@ __global__ void __launch_bounds__(256) marker_effects_kernel(const T* __restrict
                                                              const double* __restrict__ sd,
                                                              const int32_t* __restrict__ keep,
                                                              double* __restrict__ B, int64_t ldb, double xs) {
+  constexpr bool kI8 = std::is_same<T, int8_t>::value;
   const int lane = threadIdx.x & 63;
   const int64_t wave_g = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   const int64_t nwaves = (int64_t)gridDim.x * 4;
-  const int64_t n2 = (n + 1) & ~(int64_t)1;  // ldz is even and the padding is zero
   if (q_dev) inv_q = 1.0 / (double)(*q_dev);
-  for (int64_t j = wave_g; j < p; j += nwaves) {
-    const T* z = Zt + j * ldz;
-    const bool kp = keep[j] != 0;
-    double m = 0.0, r = 0.0;
-    if constexpr (std::is_same<T, int8_t>::value) {
-      m = mean[j];
-      r = kp ? 1.0 / sd[j] : 0.0;
+  for (int64_t j0 = wave_g * R; j0 < p; j0 += nwaves * R) {
+    const T* z[R];
+    bool kp[R], any = false;
+    double m[R], r[R];
+#pragma unroll
+    for (int q = 0; q < R; q++) {
+      const int64_t j = j0 + q < p ? j0 + q : p - 1;  // (a row past p repeats the last one; never stored)
+      z[q] = Zt + j * ldz;
+      kp[q] = j0 + q < p && keep[j] != 0;
+      any |= kp[q];
+      m[q] = kI8 ? mean[j] : 0.0;
+      r[q] = kI8 && kp[q] ? 1.0 / sd[j] : 0.0;
     }
     for (int64_t t0 = 0; t0 < nrhs; t0 += 4) {
-      double acc[4] = {0.0, 0.0, 0.0, 0.0};
-      if (kp) {
-        for (int64_t i = (int64_t)lane * 2; i < n2; i += 128) {
-          double2 zv;
-          if constexpr (std::is_same<T, int8_t>::value) {
-            zv.x = dosage_z(z[i], xs, m, r);
-            zv.y = i + 1 < n ? dosage_z(z[i + 1], xs, m, r) : 0.0;
-          } else {
-            zv = *reinterpret_cast<const double2*>(z + i);
+      double acc[R][4];
+#pragma unroll
+      for (int q = 0; q < R; q++)
+#pragma unroll
+        for (int u = 0; u < 4; u++) acc[q][u] = 0.0;
+      if (any) {
+        for (int64_t i = (int64_t)lane * 4; i < n; i += 256) {
+          const bool whole = i + 4 <= n;
+          double zv[R][4];
+#pragma unroll
+          for (int q = 0; q < R; q++) {
+            if constexpr (kI8) {
+              const int8_t* zr = z[q] + i;
+              int8_t d[4];
+              if (whole && ((uintptr_t)zr & 3) == 0) {
+                const uint32_t w = *reinterpret_cast<const uint32_t*>(zr);
+#pragma unroll
+                for (int e = 0; e < 4; e++) d[e] = (int8_t)(w >> (8 * e));
+              } else {
+#pragma unroll
+                for (int e = 0; e < 4; e++) d[e] = i + e < n ? zr[e] : 0;
+              }
+#pragma unroll
+              for (int e = 0; e < 4; e++) zv[q][e] = i + e < n ? dosage_z(d[e], xs, m[q], r[q]) : 0.0;
+            } else {
+              const double* zr = z[q] + i;
+              if (whole) {
+                const double2 v0 = *reinterpret_cast<const double2*>(zr);
+                const double2 v1 = *reinterpret_cast<const double2*>(zr + 2);
+                zv[q][0] = v0.x;
+                zv[q][1] = v0.y;
+                zv[q][2] = v1.x;
+                zv[q][3] = v1.y;
+              } else {
+#pragma unroll
+                for (int e = 0; e < 4; e++) zv[q][e] = i + e < n ? zr[e] : 0.0;
+              }
+            }
           }
 #pragma unroll
           for (int u = 0; u < 4; u++)
             if (t0 + u < nrhs) {
-              const double2 av = *reinterpret_cast<const double2*>(A + (t0 + u) * lda + i);
-              acc[u] += zv.x * av.x + zv.y * av.y;
+              const double* ar = A + (t0 + u) * lda + i;
+              double av[4];
+              if (whole) {
+                const double2 a0 = *reinterpret_cast<const double2*>(ar);
+                const double2 a1 = *reinterpret_cast<const double2*>(ar + 2);
+                av[0] = a0.x;
+                av[1] = a0.y;
+                av[2] = a1.x;
+                av[3] = a1.y;
+              } else {
+#pragma unroll
+                for (int e = 0; e < 4; e++) av[e] = i + e < n ? ar[e] : 0.0;
+              }
+#pragma unroll
+              for (int q = 0; q < R; q++)
+#pragma unroll
+                for (int e = 0; e < 4; e++) acc[q][u] = __builtin_fma(zv[q][e], av[e], acc[q][u]);
             }
         }
       }
 #pragma unroll
-      for (int u = 0; u < 4; u++) {
-        double v = acc[u];
+      for (int q = 0; q < R; q++)
 #pragma unroll
-        for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
-        if (lane == 0 && t0 + u < nrhs) B[(t0 + u) * ldb + j] = kp ? v * inv_q / sd[j] : 0.0;
-      }
+        for (int u = 0; u < 4; u++) {
+          double v = acc[q][u];
+#pragma unroll
+          for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
+          if (lane == 0 && t0 + u < nrhs && j0 + q < p) B[(t0 + u) * ldb + j0 + q] = kp[q] ? v * inv_q / sd[j0 + q] : 0.0;
+        }
     }
   }
 }
@@ -143,8 +198,9 @@ int launch_marker_rows(const double* Zt, int64_t ldz, int64_t p, int64_t n, cons
                        double inv_q, const int64_t* q_dev, const double* sd, const int32_t* keep, double* B,
                        int64_t ldb, hipStream_t s) {
   if (p < 1) return GBM_OK;
-  const int64_t blocks = (p + 3) / 4 < 8192 ? (p + 3) / 4 : 8192;
-  marker_effects_kernel<double><<<(unsigned)blocks, 256, 0, s>>>(Zt, ldz, p, n, A, lda, nrhs, inv_q, q_dev, nullptr, sd,
+  constexpr int R = 2;  // rows per wave (the trait vector's loads shared by them)
+  const int64_t groups = (p + R - 1) / R, blocks = (groups + 3) / 4 < 8192 ? (groups + 3) / 4 : 8192;
+  marker_effects_kernel<double, R><<<(unsigned)blocks, 256, 0, s>>>(Zt, ldz, p, n, A, lda, nrhs, inv_q, q_dev, nullptr, sd,
                                                                   keep, B, ldb, 1.0);
   GBM_LAUNCH_CHECK();
   return GBM_OK;
@@ -154,8 +210,9 @@ int launch_marker_rows_i8(const int8_t* D, int64_t ldd, int64_t p, int64_t n, in
                           int64_t nrhs, double inv_q, const int64_t* q_dev, const double* mean, const double* sd,
                           const int32_t* keep, double* B, int64_t ldb, hipStream_t s) {
   if (p < 1) return GBM_OK;
-  const int64_t blocks = (p + 3) / 4 < 8192 ? (p + 3) / 4 : 8192;
-  marker_effects_kernel<int8_t><<<(unsigned)blocks, 256, 0, s>>>(D, ldd, p, n, A, lda, nrhs, inv_q, q_dev, mean, sd,
+  constexpr int R = 4;
+  const int64_t groups = (p + R - 1) / R, blocks = (groups + 3) / 4 < 8192 ? (groups + 3) / 4 : 8192;
+  marker_effects_kernel<int8_t, R><<<(unsigned)blocks, 256, 0, s>>>(D, ldd, p, n, A, lda, nrhs, inv_q, q_dev, mean, sd,
                                                                   keep, B, ldb, 1.0 / ploidy);
   GBM_LAUNCH_CHECK();
   return GBM_OK;
