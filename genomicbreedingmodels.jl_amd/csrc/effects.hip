@@ -23,7 +23,16 @@ __device__ __forceinline__ double dosage_z(int8_t d, double xs, double m, double
 // tree — so B is bit-identical between the fp64 rows and the dosage bytes. Up to 4 traits per pass over the rows.
 // (Round 5 ran one row per wave with 2 individuals per lane: the int8 variant issued two byte loads per lane per
 // 128 individuals and re-read the trait vector from L2 for every locus, 0.29 ms at C2 for 250 MB of bytes.)
-template <typename T, int R>
+#ifndef GBM_EFF_R_I8
+#define GBM_EFF_R_I8 4  // rows per wave of the dosage-byte variant (timing variants: tools/build_effects_variants.sh)
+#endif
+#ifndef GBM_EFF_R_F64
+#define GBM_EFF_R_F64 2
+#endif
+#ifndef GBM_EFF_UNROLL
+#define GBM_EFF_UNROLL 1  // passes of the individuals loop unrolled (loads of the next pass in flight)
+#endif
+template <typename T, int R, int TU>  // TU: traits per pass over the rows (1: the single-trait fit, fewer registers)
 __global__ void __launch_bounds__(256) marker_effects_kernel(const T* __restrict__ Zt, int64_t ldz, int64_t p,
                                                              int64_t n, const double* __restrict__ A, int64_t lda,
                                                              int64_t nrhs, double inv_q,
@@ -50,13 +59,14 @@ __global__ void __launch_bounds__(256) marker_effects_kernel(const T* __restrict
       m[q] = kI8 ? mean[j] : 0.0;
       r[q] = kI8 && kp[q] ? 1.0 / sd[j] : 0.0;
     }
-    for (int64_t t0 = 0; t0 < nrhs; t0 += 4) {
-      double acc[R][4];
+    for (int64_t t0 = 0; t0 < nrhs; t0 += TU) {
+      double acc[R][TU];
 #pragma unroll
       for (int q = 0; q < R; q++)
 #pragma unroll
-        for (int u = 0; u < 4; u++) acc[q][u] = 0.0;
+        for (int u = 0; u < TU; u++) acc[q][u] = 0.0;
       if (any) {
+#pragma unroll GBM_EFF_UNROLL
         for (int64_t i = (int64_t)lane * 4; i < n; i += 256) {
           const bool whole = i + 4 <= n;
           double zv[R][4];
@@ -91,7 +101,7 @@ __global__ void __launch_bounds__(256) marker_effects_kernel(const T* __restrict
             }
           }
 #pragma unroll
-          for (int u = 0; u < 4; u++)
+          for (int u = 0; u < TU; u++)
             if (t0 + u < nrhs) {
               const double* ar = A + (t0 + u) * lda + i;
               double av[4];
@@ -116,7 +126,7 @@ __global__ void __launch_bounds__(256) marker_effects_kernel(const T* __restrict
 #pragma unroll
       for (int q = 0; q < R; q++)
 #pragma unroll
-        for (int u = 0; u < 4; u++) {
+        for (int u = 0; u < TU; u++) {
           double v = acc[q][u];
 #pragma unroll
           for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
@@ -198,10 +208,14 @@ int launch_marker_rows(const double* Zt, int64_t ldz, int64_t p, int64_t n, cons
                        double inv_q, const int64_t* q_dev, const double* sd, const int32_t* keep, double* B,
                        int64_t ldb, hipStream_t s) {
   if (p < 1) return GBM_OK;
-  constexpr int R = 2;  // rows per wave (the trait vector's loads shared by them)
+  constexpr int R = GBM_EFF_R_F64;  // rows per wave (the trait vector's loads shared by them)
   const int64_t groups = (p + R - 1) / R, blocks = (groups + 3) / 4 < 8192 ? (groups + 3) / 4 : 8192;
-  marker_effects_kernel<double, R><<<(unsigned)blocks, 256, 0, s>>>(Zt, ldz, p, n, A, lda, nrhs, inv_q, q_dev, nullptr, sd,
-                                                                  keep, B, ldb, 1.0);
+  if (nrhs == 1)
+    marker_effects_kernel<double, R, 1><<<(unsigned)blocks, 256, 0, s>>>(Zt, ldz, p, n, A, lda, nrhs, inv_q, q_dev,
+                                                                         nullptr, sd, keep, B, ldb, 1.0);
+  else
+    marker_effects_kernel<double, R, 4><<<(unsigned)blocks, 256, 0, s>>>(Zt, ldz, p, n, A, lda, nrhs, inv_q, q_dev,
+                                                                         nullptr, sd, keep, B, ldb, 1.0);
   GBM_LAUNCH_CHECK();
   return GBM_OK;
 }
@@ -210,10 +224,14 @@ int launch_marker_rows_i8(const int8_t* D, int64_t ldd, int64_t p, int64_t n, in
                           int64_t nrhs, double inv_q, const int64_t* q_dev, const double* mean, const double* sd,
                           const int32_t* keep, double* B, int64_t ldb, hipStream_t s) {
   if (p < 1) return GBM_OK;
-  constexpr int R = 4;
+  constexpr int R = GBM_EFF_R_I8;
   const int64_t groups = (p + R - 1) / R, blocks = (groups + 3) / 4 < 8192 ? (groups + 3) / 4 : 8192;
-  marker_effects_kernel<int8_t, R><<<(unsigned)blocks, 256, 0, s>>>(D, ldd, p, n, A, lda, nrhs, inv_q, q_dev, mean, sd,
-                                                                  keep, B, ldb, 1.0 / ploidy);
+  if (nrhs == 1)
+    marker_effects_kernel<int8_t, R, 1><<<(unsigned)blocks, 256, 0, s>>>(D, ldd, p, n, A, lda, nrhs, inv_q, q_dev, mean,
+                                                                         sd, keep, B, ldb, 1.0 / ploidy);
+  else
+    marker_effects_kernel<int8_t, R, 4><<<(unsigned)blocks, 256, 0, s>>>(D, ldd, p, n, A, lda, nrhs, inv_q, q_dev, mean,
+                                                                         sd, keep, B, ldb, 1.0 / ploidy);
   GBM_LAUNCH_CHECK();
   return GBM_OK;
 }
