@@ -23,11 +23,14 @@ __device__ __forceinline__ double dosage_z(int8_t d, double xs, double m, double
 // tree — so B is bit-identical between the fp64 rows and the dosage bytes. Up to 4 traits per pass over the rows.
 // (Round 5 ran one row per wave with 2 individuals per lane: the int8 variant issued two byte loads per lane per
 // 128 individuals and re-read the trait vector from L2 for every locus, 0.29 ms at C2 for 250 MB of bytes.)
+// rows per wave of the dosage-byte and fp64 variants (timing variants: tools/build_effects_variants.sh; C2 exact
+// path, single trait: 0.31 ms in round 5, R = 4 0.26, R = 2 0.19, R = 1 0.19 ms; the fp64 rows are HBM-bound at
+// ≈ 5.5 TB/s, 0.365 ms, whatever R)
 #ifndef GBM_EFF_R_I8
-#define GBM_EFF_R_I8 4  // rows per wave of the dosage-byte variant (timing variants: tools/build_effects_variants.sh)
+#define GBM_EFF_R_I8 2
 #endif
 #ifndef GBM_EFF_R_F64
-#define GBM_EFF_R_F64 2
+#define GBM_EFF_R_F64 1
 #endif
 #ifndef GBM_EFF_UNROLL
 #define GBM_EFF_UNROLL 1  // passes of the individuals loop unrolled (loads of the next pass in flight)
