@@ -717,7 +717,7 @@ int upload_grm_pipelined_packed(const Problem& pr, Shard& sh, int64_t chunk, int
         e = hipEventSynchronize(c.ev[k - 1]);
         if (e != hipSuccess) rc = fail(GBM_E_HIP, std::string("host-pack upload: HIP error '") + hipGetErrorString(e) + "'");
       }
-      packer.release_upto(k);
+      if (rc == GBM_OK) packer.release_upto(k);  // (after a failure no slot is handed back: a copy may still read it)
     }
   }
   GBM_HIP_TRY(hipStreamSynchronize(c.copy.s));
