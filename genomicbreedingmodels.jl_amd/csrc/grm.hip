@@ -19,7 +19,8 @@
 // a mode per call: GBM_GRM_CARRY (0/1: slabs / in-order carry; unset: automatic),
 // GBM_GRM_PERSIST=0 (hardware-dispatched workgroups), GBM_GRM_EDGE=0 (no ragged-edge kernel),
 // GBM_GRM_EDGE_CONCURRENT=0 (edge kernel after the tiles), GBM_GRM_SPLIT=w0,w1,... (relative
-// loci-range sizes instead of the planner's).
+// loci-range sizes instead of the planner's), GBM_GRM_FUSED=1 (the slab reduce inside the persistent tile
+// kernel; same bits, opt-in: DESIGN.md §7, round 6).
 #include <algorithm>
 #include <atomic>
 #include <cmath>
@@ -168,6 +169,11 @@ struct SliceBounds {
   int64_t e0, eslab_off;
   // carry mode with accumulation (G += this GRM): range 0 adds G's existing tile as well
   int32_t accum = 0;
+  // fuse = 1 (persistent slabs mode, GBM_GRM_FUSED): the reduce runs inside the tile kernel — each unit stores
+  // its slab, releases it (agent scope) and takes a ticket on its tile's counter; the unit that draws the last
+  // ticket sums the tile's slabs into G in range order (the reduce kernel's order), so grm_slab_reduce_kernel
+  // is not launched
+  int32_t fuse = 0;
 };
 
 // Ragged last tile column of the GRM: when n = 128 (nt − 1) + r with small r, the last tile
@@ -343,6 +349,66 @@ syrk_kernel(const double* __restrict__ U, int64_t ldu, int64_t K, int64_t c0, in
           }
       }
       publish_flag(&tflags[t], sl + 1, threadIdx.x);
+    } else if (MODE == kPersist && sb.fuse && sb.n > 1) {
+      // the fused reduce (SliceBounds::fuse), the guide's split-K hand-off in its plain-store form: the unit's
+      // slab with plain stores, every wave drains them, barrier, ONE agent-scope release (L2 write-back) and
+      // the relaxed agent-scope ticket; the unit that draws the tile's last ticket acquires (agent scope) and
+      // reads every range's slab (its own too) with plain loads, adding them from 0.0 in range order exactly
+      // as grm_slab_reduce_kernel does
+      const int64_t per = (int64_t)BT * BT;
+      const int64_t eoff = (wm * 64 + 4 * frag_row) * BT + wn * 64 + 4 * frag_col;
+      if (active) {
+        double* out = slab + ((int64_t)sl * ntiles + t) * per + eoff;
+#pragma unroll
+        for (int m = 0; m < 4; m++)
+#pragma unroll
+          for (int r = 0; r < 4; r++) {
+            double* o = out + (16 * r + m) * BT;
+            *reinterpret_cast<double2*>(o) = make_double2(acc[m][0][r], acc[m][1][r]);
+            *reinterpret_cast<double2*>(o + 2) = make_double2(acc[m][2][r], acc[m][3][r]);
+          }
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      int* s_last = reinterpret_cast<int*>(lds);  // (the staging buffers are free: tile_pass ended in a barrier)
+      if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const bool lt = __hip_atomic_fetch_add(&info[8 + t], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == sb.n - 1;
+        if (lt) {
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        *s_last = lt;
+      }
+      __syncthreads();
+      const bool last = *s_last != 0;
+      __syncthreads();  // every wave has read s_last before the next unit stages into lds
+      if (last && active) {
+        double* gout = C + (i0 + wm * 64 + 4 * frag_row) * ldc + j0 + wn * 64 + 4 * frag_col;
+        const double* tbase = slab + t * per + eoff;
+#pragma unroll 1
+        for (int mr = 0; mr < 16; mr++) {
+          const int m = mr & 3, r = mr >> 2;
+          double2 v01 = make_double2(0.0, 0.0), v23 = make_double2(0.0, 0.0);
+          for (int s2 = 0; s2 < sb.n; s2++) {
+            const double* src = tbase + (int64_t)s2 * ntiles * per + (16 * r + m) * BT;
+            const double2 x01 = *reinterpret_cast<const double2*>(src), x23 = *reinterpret_cast<const double2*>(src + 2);
+            v01.x += x01.x;
+            v01.y += x01.y;
+            v23.x += x23.x;
+            v23.y += x23.y;
+          }
+          double* g = gout + (16 * r + m) * ldc;
+          if (sb.accum) {
+            const double2 a01 = *reinterpret_cast<const double2*>(g), a23 = *reinterpret_cast<const double2*>(g + 2);
+            v01 = make_double2(a01.x + v01.x, a01.y + v01.y);
+            v23 = make_double2(a23.x + v23.x, a23.y + v23.y);
+          }
+          *reinterpret_cast<double2*>(g) = v01;
+          *reinterpret_cast<double2*>(g + 2) = v23;
+        }
+      }
     } else if (active) {
       // a single slice stores straight into G (no workspace, the reduce is a no-op)
       const int64_t ld = sb.n == 1 ? ldc : BT;
@@ -511,6 +577,7 @@ struct GrmTuning {
   bool edge = true;            // GBM_GRM_EDGE: ragged-edge kernel for a last tile column of <= 64
   bool persist = true;         // GBM_GRM_PERSIST: persistent workgroups with per-XCD queues
   bool edge_concurrent = true; // GBM_GRM_EDGE_CONCURRENT: edge kernel on the helper stream
+  bool fuse = false;           // GBM_GRM_FUSED: the slab reduce inside the persistent tile kernel
   std::vector<double> split;   // GBM_GRM_SPLIT: relative loci-range sizes (tuning experiments)
 };
 
@@ -524,6 +591,7 @@ static GrmTuning grm_tuning() {
   t.edge = flag("GBM_GRM_EDGE", true);
   t.persist = flag("GBM_GRM_PERSIST", true);
   t.edge_concurrent = flag("GBM_GRM_EDGE_CONCURRENT", true);
+  t.fuse = flag("GBM_GRM_FUSED", false);
   if (const char* ov = ::gbm::knob("GBM_GRM_SPLIT")) {
     for (const char* q = ov; *q;) {
       char* end = nullptr;
@@ -614,6 +682,7 @@ static GrmPlan plan(int64_t n, int64_t p) {
       gp.edge_doubles = (int64_t)gp.sb.es * gp.sb.erb * 256 * 16 * gp.sb.et;
     }
     gp.persist = tune.persist && !gp.sb.carry;
+    gp.sb.fuse = (gp.persist && gp.sb.n > 1 && tune.fuse) ? 1 : 0;
     // the ragged-column kernel and its reduce run on the helper stream, beside the persistent tiles
     gp.edge_concurrent = gp.sb.er > 0 && gp.persist && tune.edge_concurrent;
   };
@@ -940,10 +1009,12 @@ static int aux_stream(hipStream_t caller, AuxStream& a, bool* usable) {
   return GBM_OK;
 }
 
-// workspace: [slabs or carry flags][edge partials][8 queue counters of the persistent launch]
+// workspace: [slabs or carry flags][edge partials][8 queue counters of the persistent launch, then (fused
+// reduce) one ticket counter per tile]
+static int64_t grm_counter_doubles(const GrmPlan& g) { return 4 + (g.sb.fuse ? (g.ntiles + 1) / 2 : 0); }
 int64_t grm_workspace_bytes(int64_t n, int64_t p) {
   const GrmPlan g = plan(n, p);
-  return (g.main_doubles + g.edge_doubles + 4) * (int64_t)sizeof(double);
+  return (g.main_doubles + g.edge_doubles + grm_counter_doubles(g)) * (int64_t)sizeof(double);
 }
 
 static int check_grm_args(const double* Zt, int64_t ldz, int64_t p, int64_t n, double* G, int64_t ldg) {
@@ -964,7 +1035,7 @@ int launch_grm_syrk(const double* Zt, int64_t ldz, int64_t p, int64_t n, double*
   const GrmPlan g = plan(n, p);
   SliceBounds sb = g.sb;
   sb.accum = accum;
-  const int64_t need = (g.main_doubles + g.edge_doubles + 4) * (int64_t)sizeof(double);
+  const int64_t need = (g.main_doubles + g.edge_doubles + grm_counter_doubles(g)) * (int64_t)sizeof(double);
   if (need > 0 && (!ws || ws_bytes < need))
     return fail(GBM_E_ARG, "gbm_dev_grm: workspace too small (" + std::to_string(ws_bytes) + " < " +
                                std::to_string(need) + ")");
@@ -988,10 +1059,10 @@ int launch_grm_syrk(const double* Zt, int64_t ldz, int64_t p, int64_t n, double*
     }
   }
   if (g.persist) {
-    GBM_HIP_TRY(hipMemsetAsync(ctr, 0, 8 * sizeof(int32_t), s));
+    GBM_HIP_TRY(hipMemsetAsync(ctr, 0, (size_t)(8 + (g.sb.fuse ? g.ntiles : 0)) * sizeof(int32_t), s));
     const int64_t units = (int64_t)g.sb.n * g.ntiles;
     const unsigned pgrid = (unsigned)(units < resident_wgs() ? units : resident_wgs());
-    syrk_kernel<kPersist><<<pgrid, 256, 0, s>>>(Zt, ldz, p, 0, lim, G, ldg, (double*)ws, g.ntiles, g.sb, nullptr,
+    syrk_kernel<kPersist><<<pgrid, 256, 0, s>>>(Zt, ldz, p, 0, lim, G, ldg, (double*)ws, g.ntiles, sb, nullptr,
                                                 nullptr, ctr, -1, TileOwner{});
   } else {
     syrk_kernel<kSplit><<<grid, 256, 0, s>>>(Zt, ldz, p, 0, lim, G, ldg, (double*)ws, g.ntiles, sb, nullptr, nullptr,
@@ -1038,7 +1109,7 @@ int launch_grm_reduce(int64_t n, int64_t p, double* G, int64_t ldg, const void* 
                                                                                  g.sb, G, ldg, accum);
     GBM_LAUNCH_CHECK();
   }
-  if (g.sb.n == 1) return GBM_OK;
+  if (g.sb.n == 1 || g.sb.fuse) return GBM_OK;  // (fused: the tile kernel has summed the slabs)
   if (g.sb.carry && err_out) {
     GBM_HIP_TRY(hipMemcpyAsync(err_out, (const int32_t*)ws + g.ntiles, sizeof(int32_t), hipMemcpyDeviceToDevice, s));
     return GBM_OK;

@@ -5,7 +5,7 @@ set -e
 cd "$(dirname "$0")/.."
 B=genomicbreedingmodels.jl_amd/csrc/build
 mkdir -p variants
-OBJS="$B/stats.hip.o $B/grm_exact.hip.o $B/chol.hip.o $B/chol_flow.hip.o $B/effects.hip.o $B/gibbs.hip.o $B/capi.cpp.o $B/session.cpp.o"
+OBJS="$B/stats.hip.o $B/grm_exact.hip.o $B/chol.hip.o $B/chol_flow.hip.o $B/effects.hip.o $B/gibbs.hip.o $B/capi.cpp.o $B/session.cpp.o $B/knobs.cpp.o $B/hostpack.cpp.o"
 build() {  # name flags...
   name=$1; shift
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 "$@" -c genomicbreedingmodels.jl_amd/csrc/grm.hip -o variants/grm_$name.o
