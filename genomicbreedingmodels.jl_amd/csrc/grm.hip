@@ -51,7 +51,9 @@ __device__ __forceinline__ void tile_of(int64_t t, int64_t& ti, int64_t& tj) {
   ti = t - r * (r + 1) / 2;
 }
 
-enum SyrkMode { kSub = 0, kSplit = 1, kPersist = 2 };
+// kPersistFused: kPersist with the slab reduce inside (SliceBounds::fuse; its own instantiation, so the default
+// persistent kernel keeps its registers)
+enum SyrkMode { kSub = 0, kSplit = 1, kPersist = 2, kPersistFused = 3 };
 
 // Column ownership of a distributed Cholesky trailing update (kSub): with nranks > 1 this rank
 // updates only the 128-column tiles J (absolute, column J·128) with J mod nranks == rank, plus the
@@ -287,7 +289,7 @@ syrk_kernel(const double* __restrict__ U, int64_t ldu, int64_t K, int64_t c0, in
   const int64_t nst = (K + BK - 1) / BK;
   const int64_t rlim = c0 + lim;
 
-  if constexpr (MODE == kSplit || MODE == kPersist) {
+  if constexpr (MODE == kSplit || MODE == kPersist || MODE == kPersistFused) {
     // one (loci range sl, tile t) unit: the tile's partial sum over the range, then the slab /
     // carry / direct epilogue
     auto run_unit = [&](int sl, int64_t t) {
@@ -349,7 +351,7 @@ syrk_kernel(const double* __restrict__ U, int64_t ldu, int64_t K, int64_t c0, in
           }
       }
       publish_flag(&tflags[t], sl + 1, threadIdx.x);
-    } else if (MODE == kPersist && sb.fuse && sb.n > 1) {
+    } else if (MODE == kPersistFused && sb.n > 1) {
       // the fused reduce (SliceBounds::fuse), the guide's split-K hand-off in its plain-store form: the unit's
       // slab with plain stores, every wave drains them, barrier, ONE agent-scope release (L2 write-back) and
       // the relaxed agent-scope ticket; the unit that draws the tile's last ticket acquires (agent scope) and
@@ -428,7 +430,7 @@ syrk_kernel(const double* __restrict__ U, int64_t ldu, int64_t K, int64_t c0, in
     // range (T8 = round_up(ntiles, 8)), so neighbouring tiles share A/B strips in that XCD's L2
     // and later ranges revisit the same tiles
     const int64_t T8 = (ntiles + 7) & ~(int64_t)7;
-    if constexpr (MODE == kPersist) {
+    if constexpr (MODE == kPersist || MODE == kPersistFused) {
       // persistent workgroups (one per resident slot): each takes units from its own XCD's queue
       // (XCC_ID hardware register; units in range-major order over the XCD's tiles) through an
       // atomic counter, then steals from the other XCDs' queues once its own is empty. Dynamic
@@ -1062,8 +1064,12 @@ int launch_grm_syrk(const double* Zt, int64_t ldz, int64_t p, int64_t n, double*
     GBM_HIP_TRY(hipMemsetAsync(ctr, 0, (size_t)(8 + (g.sb.fuse ? g.ntiles : 0)) * sizeof(int32_t), s));
     const int64_t units = (int64_t)g.sb.n * g.ntiles;
     const unsigned pgrid = (unsigned)(units < resident_wgs() ? units : resident_wgs());
-    syrk_kernel<kPersist><<<pgrid, 256, 0, s>>>(Zt, ldz, p, 0, lim, G, ldg, (double*)ws, g.ntiles, sb, nullptr,
-                                                nullptr, ctr, -1, TileOwner{});
+    if (g.sb.fuse)
+      syrk_kernel<kPersistFused><<<pgrid, 256, 0, s>>>(Zt, ldz, p, 0, lim, G, ldg, (double*)ws, g.ntiles, sb, nullptr,
+                                                       nullptr, ctr, -1, TileOwner{});
+    else
+      syrk_kernel<kPersist><<<pgrid, 256, 0, s>>>(Zt, ldz, p, 0, lim, G, ldg, (double*)ws, g.ntiles, sb, nullptr,
+                                                  nullptr, ctr, -1, TileOwner{});
   } else {
     syrk_kernel<kSplit><<<grid, 256, 0, s>>>(Zt, ldz, p, 0, lim, G, ldg, (double*)ws, g.ntiles, sb, nullptr, nullptr,
                                              nullptr, -1, TileOwner{});
