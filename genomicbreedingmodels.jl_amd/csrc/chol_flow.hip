@@ -381,7 +381,9 @@ __device__ __forceinline__ int factor_block_pipe(double* X, const double* X2, bo
       if (c + d < 16) {
         const double u = readlane_d(lc, c + d);  // U[o + c][o + c + d]
         x[c + d] = fma(-lc, u, x[c + d]);
+#ifndef GBM_FLOW_TIMING_NOY
         y[c + d] = fma(-yc, u, y[c + d]);
+#endif
       }
     __builtin_amdgcn_sched_barrier(0);
     // row c − 1 (written last step) is in X: publish it to the followers, read U[c − 1][·] -> b1;
@@ -398,7 +400,9 @@ __device__ __forceinline__ int factor_block_pipe(double* X, const double* X2, bo
 #pragma unroll
       for (int t = c + 1; t < 16; t++) {
         x[t] = fma(-l2, b2[t], x[t]);
+#ifndef GBM_FLOW_TIMING_NOY  // (timing variant: the identity columns' eliminations left out; Dinv wrong)
         y[t] = fma(-m2, b2[t], y[t]);
+#endif
       }
     }
     // y[c] is final here: pinned, so that LLVM cannot sink the identity columns' eliminations out of

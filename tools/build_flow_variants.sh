@@ -16,4 +16,5 @@ build() {  # name flags...
 build base &
 build noload -DGBM_FLOW_TIMING_NOLOAD &
 build nomfma -DGBM_FLOW_TIMING_NOMFMA &
+build noy -DGBM_FLOW_TIMING_NOY &
 wait
