@@ -257,6 +257,11 @@ __global__ void __launch_bounds__(XG_UBLK) xg_digits_kernel(const double* __rest
 // row by row (4 dosages per lane) into LDS, then one thread per individual assembles its 64 bytes of Dt and
 // St and adds its V_j d_ij (V_j wave-uniform).
 constexpr int XG_TP = 256 + 16;  // LDS row pitch of the 64-locus x 256-individual tile
+// the dosage rows read with the nontemporal hint (read once here): C2 transpose 211 → 204 µs, same G digests
+// (profiles/r06_nt_reduce_transpose_ab.txt; GBM_XG_TP_NT=0 builds the plain loads)
+#ifndef GBM_XG_TP_NT
+#define GBM_XG_TP_NT 1
+#endif
 __global__ void __launch_bounds__(256) xg_transpose_u_kernel(const int8_t* __restrict__ D, int64_t ldd, int64_t p,
                                                              int64_t n, int64_t kp, int64_t npad,
                                                              const uint4* __restrict__ VL, int8_t* __restrict__ Dt,
@@ -279,7 +284,11 @@ __global__ void __launch_bounds__(256) xg_transpose_u_kernel(const int8_t* __res
       if (k < p) {
         const int8_t* row = D + k * ldd;
         if (al4 && ii + 3 < n) {
+#if GBM_XG_TP_NT
+          v = __builtin_nontemporal_load(reinterpret_cast<const uint32_t*>(row + ii));
+#else
           v = *reinterpret_cast<const uint32_t*>(row + ii);
+#endif
         } else {
 #pragma unroll
           for (int b = 0; b < 4; b++)
